@@ -1,0 +1,1030 @@
+/*
+ * yjs_oracle.c -- TEST INFRASTRUCTURE ONLY (the parity checker, never the product).
+ *
+ * A literal, sequential, CPU restatement of the three yjs update-level functions
+ * that sit on Hocuspocus's persistence / sync hot path:
+ *
+ *   mergeUpdates(us)               yjs mergeUpdatesV2 with V1 coders   (Y@39011-40710)
+ *   diffUpdate(u, sv)              yjs diffUpdateV2   with V1 coders   (Y@40711-41209)
+ *   encodeStateVectorFromUpdate(u) yjs encodeStateVectorFromUpdateV2   (Y@37728-38303)
+ *
+ * `Y@N` = byte offset N on line 1 of the yjs 13.5.16 bundle named in SURVEY.md
+ * ("Citation conventions").  The reference (Hocuspocus 3.2.4) reaches these
+ * functions through packages/extension-database/src/Database.ts:44-60 and
+ * packages/server/src/MessageReceiver.ts:137-213; the arithmetic itself lives in
+ * the un-vendored npm dependency yjs@13.6.26 / lib0@0.2.104
+ * (package-lock.json:20726-20732, :13716-13719), whose published algorithm this
+ * file restates.  Parity is pinned against tests/golden/yjs13516_vectors.jsonl.gz
+ * (outputs of yjs 13.5.16 run in the build container) and
+ * tests/golden/v8_timsort_vectors.json.gz (V8's Array.prototype.sort).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this library.  It is deliberately written as a different program from the
+ * HIP engine (hocuspocus_amd/csrc): object-per-struct, re-encode-everything,
+ * exactly the loop structure of yjs.
+ *
+ * Flags: YO_COMPAT_135 emulates yjs 13.5.16 / lib0 0.2.42 where they differ from
+ * the 13.6.26 default: delete-set clients written in
+ * first-seen order instead of client-descending, and a lone surrogate produced
+ * by diffUpdate's string slicing throws instead of being written as U+FFFD.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+#include <math.h>
+
+#define YO_OK 0
+#define YO_EMALFORMED 1
+#define YO_ERANGE 2
+#define YO_ENONCANON 3
+#define YO_ESURROGATE 4
+#define YO_EDEPTH 5
+#define YO_ENOMEM 6
+
+#define YO_COMPAT_135 1
+
+#define MAX_SAFE 9007199254740991ULL
+#define ANY_MAX_DEPTH 64
+
+static __thread int g_flags; /* flags of the current top-level call */
+
+/* ------------------------------------------------------------------ buffers */
+typedef struct { uint8_t *b; size_t n, cap; int oom; } Buf;
+static void bput(Buf *o, const void *p, size_t n) {
+  if (o->oom) return;
+  if (o->n + n > o->cap) {
+    size_t c = o->cap ? o->cap : 64;
+    while (c < o->n + n) c *= 2;
+    uint8_t *nb = (uint8_t *)realloc(o->b, c);
+    if (!nb) { o->oom = 1; return; }
+    o->b = nb; o->cap = c;
+  }
+  memcpy(o->b + o->n, p, n); o->n += n;
+}
+static void bbyte(Buf *o, uint8_t v) { bput(o, &v, 1); }
+/* lib0 writeVarUint (L0@7250) */
+static void bvu(Buf *o, uint64_t v) {
+  while (v > 127) { bbyte(o, (uint8_t)(0x80 | (v & 127))); v >>= 7; }
+  bbyte(o, (uint8_t)v);
+}
+static void bstr(Buf *o, const uint8_t *s, size_t n) { bvu(o, n); bput(o, s, n); }
+
+/* ------------------------------------------------------------------ decoder */
+typedef struct { const uint8_t *a; size_t n, p; int err; int nm; } Dec; /* nm: saw a non-minimal varuint */
+static void seterr(Dec *d, int e) { if (!d->err) d->err = e; }
+static uint8_t rd8(Dec *d) {
+  if (d->p >= d->n) { seterr(d, YO_EMALFORMED); return 0; }
+  return d->a[d->p++];
+}
+/* lib0 readVarUint (0.2.104 semantics; L0@2955 is the 0.2.42 variant) */
+static uint64_t rdu(Dec *d) {
+  uint64_t num = 0; int shift = 0;
+  for (;;) {
+    if (d->p >= d->n) { seterr(d, YO_EMALFORMED); return 0; }
+    uint8_t r = d->a[d->p++];
+    if (shift < 63) num += (uint64_t)(r & 127) << shift; else if (r & 127) { seterr(d, YO_ERANGE); return 0; }
+    shift += 7;
+    if (r < 128) { if (num > MAX_SAFE) { seterr(d, YO_ERANGE); return 0; } if (r == 0 && shift > 7) d->nm = 1; return num; }
+    if (num > MAX_SAFE) { seterr(d, YO_ERANGE); return 0; }
+  }
+}
+/* lib0 readVarUint8Array: returns pointer into input */
+static const uint8_t *rdbuf(Dec *d, size_t *len) {
+  *len = 0;
+  uint64_t n = rdu(d);
+  if (d->err) return NULL;
+  if (n > d->n - d->p) { seterr(d, YO_EMALFORMED); return NULL; }
+  const uint8_t *s = d->a + d->p; d->p += (size_t)n; *len = (size_t)n; return s;
+}
+
+/* Strict UTF-8 check (lib0 0.2.104 decodes with TextDecoder{fatal:true});
+ * returns UTF-16 length or -1. */
+static long utf8_check(const uint8_t *s, size_t n) {
+  long u16 = 0; size_t i = 0;
+  while (i < n) {
+    uint8_t c = s[i];
+    if (c < 0x80) { i++; u16++; continue; }
+    int k; uint32_t cp, min;
+    if ((c & 0xE0) == 0xC0) { k = 1; cp = c & 0x1F; min = 0x80; }
+    else if ((c & 0xF0) == 0xE0) { k = 2; cp = c & 0x0F; min = 0x800; }
+    else if ((c & 0xF8) == 0xF0) { k = 3; cp = c & 0x07; min = 0x10000; }
+    else return -1;
+    for (int j = 1; j <= k; j++) {
+      if (i + j >= n) return -1;
+      uint8_t cc = s[i + j]; if ((cc & 0xC0) != 0x80) return -1;
+      cp = (cp << 6) | (cc & 0x3F);
+    }
+    if (cp < min || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) return -1;
+    u16 += cp >= 0x10000 ? 2 : 1; i += k + 1;
+  }
+  return u16;
+}
+static const uint8_t *rdstr(Dec *d, size_t *len) {
+  const uint8_t *s = rdbuf(d, len);
+  if (d->err) return NULL;
+  if (utf8_check(s, *len) < 0) { seterr(d, YO_EMALFORMED); return NULL; }
+  return s;
+}
+
+/* ------------------------------------------------ Any (lib0 readAny / writeAny) */
+/* Validates one Any value (L0@4074 reader) and decides whether lib0 0.2.104's
+ * writeAny (L0@8284-8700) would write back the same bytes.  Sets *nc on a value
+ * that would be re-encoded differently. */
+static int is_array_index(const uint8_t *k, size_t n) { /* canonical uint32 < 2^32-1 */
+  if (n == 0 || n > 10) return 0;
+  if (n > 1 && k[0] == '0') return 0;
+  uint64_t v = 0;
+  for (size_t i = 0; i < n; i++) { if (k[i] < '0' || k[i] > '9') return 0; v = v * 10 + (k[i] - '0'); }
+  return v < 4294967295ULL;
+}
+static uint64_t index_val(const uint8_t *k, size_t n) { uint64_t v = 0; for (size_t i = 0; i < n; i++) v = v * 10 + (k[i] - '0'); return v; }
+static double be_f64(const uint8_t *p) { uint64_t u = 0; for (int i = 0; i < 8; i++) u = (u << 8) | p[i]; double x; memcpy(&x, &u, 8); return x; }
+static float be_f32(const uint8_t *p) { uint32_t u = 0; for (int i = 0; i < 4; i++) u = (u << 8) | p[i]; float x; memcpy(&x, &u, 4); return x; }
+/* lib0 writeAny's integer test: 0.2.104 `isInteger && abs(x) <= BITS31`; 0.2.42
+ * lacks the abs (L0@8319), so any negative integer is written as a varInt. */
+static int js_small_int(double x) {
+  if (!(x == floor(x) && !isinf(x))) return 0;
+  if (g_flags & YO_COMPAT_135) return x <= 2147483647.0;
+  return fabs(x) <= 2147483647.0;
+}
+
+static void rd_any(Dec *d, int depth, int *nc) {
+  if (depth > ANY_MAX_DEPTH) { seterr(d, YO_EDEPTH); return; }
+  uint8_t tag = rd8(d);
+  if (d->err) return;
+  switch (tag) {
+    case 127: case 126: case 121: case 120: return;
+    case 125: { /* readVarInt */
+      size_t s = d->p; uint8_t r = rd8(d); uint64_t num = r & 63; int shift = 6; int nb = 1;
+      if (r & 128) {
+        for (;;) {
+          uint8_t c = rd8(d); if (d->err) return; nb++;
+          if (shift < 60) num += (uint64_t)(c & 127) << shift; else if (c & 127) { seterr(d, YO_ERANGE); return; }
+          shift += 7;
+          if (c < 128) { if (c == 0) *nc = 1; break; }
+          if (num > MAX_SAFE) { seterr(d, YO_ERANGE); return; }
+        }
+      }
+      if (num > MAX_SAFE) { seterr(d, YO_ERANGE); return; }
+      (void)s; (void)nb;
+      if (num > 2147483647ULL) *nc = 1; /* written back as float */
+      if (num <= 63 && (r & 128)) *nc = 1;
+      return;
+    }
+    case 124: {
+      if (d->n - d->p < 4) { seterr(d, YO_EMALFORMED); return; }
+      float f = be_f32(d->a + d->p); d->p += 4;
+      if (isnan(f) || js_small_int((double)f)) *nc = 1;
+      return;
+    }
+    case 123: {
+      if (d->n - d->p < 8) { seterr(d, YO_EMALFORMED); return; }
+      double x = be_f64(d->a + d->p); d->p += 8;
+      if (isnan(x)) return; /* V8 keeps the f64 NaN bits (vector 'any 7b7ff8000000000001') */
+      if (js_small_int(x) || (double)(float)x == x) *nc = 1;
+      return;
+    }
+    case 122: if (d->n - d->p < 8) { seterr(d, YO_EMALFORMED); return; } d->p += 8; return;
+    case 119: { size_t l; const uint8_t *s = rdbuf(d, &l); if (d->err) return; if (utf8_check(s, l) < 0) seterr(d, YO_EMALFORMED); return; }
+    case 116: { size_t l; rdbuf(d, &l); return; }
+    case 117: { uint64_t n = rdu(d); for (uint64_t i = 0; i < n && !d->err; i++) rd_any(d, depth + 1, nc); return; }
+    case 118: {
+      uint64_t n = rdu(d);
+      const uint8_t *pk[64]; size_t pl[64]; int seen_str = 0; uint64_t last_idx = 0; int have_idx = 0;
+      for (uint64_t i = 0; i < n && !d->err; i++) {
+        size_t kl; const uint8_t *k = rdstr(d, &kl); if (d->err) return;
+        if (kl == 9 && !memcmp(k, "__proto__", 9)) *nc = 1;
+        if (is_array_index(k, kl)) {
+          uint64_t v = index_val(k, kl);
+          if (seen_str || (have_idx && v <= last_idx)) *nc = 1;
+          have_idx = 1; last_idx = v;
+        } else seen_str = 1;
+        if (i < 64) { for (uint64_t j = 0; j < i; j++) if (pl[j] == kl && !memcmp(pk[j], k, kl)) *nc = 1; pk[i] = k; pl[i] = kl; }
+        else *nc = 1; /* duplicate check bounded; be conservative */
+        rd_any(d, depth + 1, nc);
+      }
+      return;
+    }
+    default: seterr(d, YO_EMALFORMED); return; /* lookup-table miss -> TypeError in JS */
+  }
+}
+
+/* ---------------------------------------- JSON (JSON.parse / JSON.stringify) */
+/* Strict RFC 8259 parse; *nc is set when JSON.stringify(JSON.parse(s)) !== s
+ * may hold (conservative: 16-17 significant digit numbers and \ud escapes). */
+typedef struct { const uint8_t *s; size_t n, p; int err; int nc; } J;
+static int jpeek(J *j) { return j->p < j->n ? j->s[j->p] : -1; }
+static void jws(J *j) { while (j->p < j->n && (j->s[j->p] == ' ' || j->s[j->p] == '\t' || j->s[j->p] == '\n' || j->s[j->p] == '\r')) { j->p++; j->nc = 1; } }
+static void jvalue(J *j, int depth);
+static int hexv(int c) { if (c >= '0' && c <= '9') return c - '0'; if (c >= 'a' && c <= 'f') return c - 'a' + 10; if (c >= 'A' && c <= 'F') return c - 'A' + 10; return -1; }
+/* parses a string; returns start/len of raw body for key comparisons */
+static void jstring(J *j, size_t *bs, size_t *bl) {
+  j->p++; *bs = j->p;
+  for (;;) {
+    if (j->p >= j->n) { j->err = 1; return; }
+    uint8_t c = j->s[j->p];
+    if (c == '"') { *bl = j->p - *bs; j->p++; return; }
+    if (c < 0x20) { j->err = 1; return; }
+    if (c == '\\') {
+      if (j->p + 1 >= j->n) { j->err = 1; return; }
+      uint8_t e = j->s[j->p + 1];
+      if (e == '"' || e == '\\' || e == 'b' || e == 'f' || e == 'n' || e == 'r' || e == 't') { j->p += 2; continue; }
+      if (e == '/') { j->nc = 1; j->p += 2; continue; }
+      if (e == 'u') {
+        if (j->p + 6 > j->n) { j->err = 1; return; }
+        int v = 0;
+        for (int k = 0; k < 4; k++) { int h = hexv(j->s[j->p + 2 + k]); if (h < 0) { j->err = 1; return; } v = v * 16 + h; if (j->s[j->p + 2 + k] >= 'A' && j->s[j->p + 2 + k] <= 'F') j->nc = 1; }
+        /* JSON.stringify writes \u00xx only for control chars without a short form */
+        if (!(v < 0x20 && v != 8 && v != 9 && v != 10 && v != 12 && v != 13)) j->nc = 1;
+        j->p += 6; continue;
+      }
+      j->err = 1; return;
+    }
+    j->p++;
+  }
+}
+static void jnumber(J *j) {
+  size_t s = j->p; int neg = 0;
+  if (jpeek(j) == '-') { neg = 1; j->p++; }
+  if (jpeek(j) == '0') { j->p++; }
+  else if (jpeek(j) >= '1' && jpeek(j) <= '9') { while (jpeek(j) >= '0' && jpeek(j) <= '9') j->p++; }
+  else { j->err = 1; return; }
+  size_t int_end = j->p; int has_frac = 0, has_exp = 0;
+  if (jpeek(j) == '.') { j->p++; has_frac = 1; if (!(jpeek(j) >= '0' && jpeek(j) <= '9')) { j->err = 1; return; } while (jpeek(j) >= '0' && jpeek(j) <= '9') j->p++; }
+  size_t frac_end = j->p;
+  if (jpeek(j) == 'e' || jpeek(j) == 'E') {
+    has_exp = 1; j->p++;
+    if (jpeek(j) == '+' || jpeek(j) == '-') j->p++;
+    if (!(jpeek(j) >= '0' && jpeek(j) <= '9')) { j->err = 1; return; }
+    while (jpeek(j) >= '0' && jpeek(j) <= '9') j->p++;
+  }
+  /* canonical (Number::toString) check, conservative */
+  char buf[64]; size_t L = j->p - s;
+  if (L >= sizeof buf) { j->nc = 1; return; }
+  memcpy(buf, j->s + s, L); buf[L] = 0;
+  double x = strtod(buf, NULL);
+  if (has_exp) { j->nc = 1; return; } /* only >=1e21 / <1e-6 use exponents; accept none */
+  if (x == 0) { if (neg || has_frac) j->nc = 1; return; }
+  if (fabs(x) >= 1e21 || fabs(x) < 1e-6) { j->nc = 1; return; }
+  /* significant digits */
+  int sig = 0, started = 0; size_t last_nz = 0;
+  for (size_t i = s + neg; i < frac_end; i++) {
+    uint8_t c = j->s[i]; if (c == '.') continue;
+    if (c != '0') started = 1;
+    if (started) { sig++; }
+  }
+  (void)last_nz; (void)int_end;
+  if (has_frac && j->s[frac_end - 1] == '0') j->nc = 1;
+  /* count sig digits ignoring trailing zeros of an integer */
+  if (!has_frac) { size_t e = frac_end; while (e > s + neg + 1 && j->s[e - 1] == '0') { e--; sig--; } }
+  if (sig > 15) j->nc = 1;
+}
+static void jvalue(J *j, int depth) {
+  if (depth > ANY_MAX_DEPTH) { j->err = 2; return; }
+  jws(j);
+  int c = jpeek(j);
+  if (c == '{') {
+    j->p++; jws(j);
+    size_t ks[64], kl[64]; int nk = 0, seen_str = 0, have_idx = 0; uint64_t last_idx = 0;
+    if (jpeek(j) == '}') { j->p++; return; }
+    for (;;) {
+      jws(j);
+      if (jpeek(j) != '"') { j->err = 1; return; }
+      size_t bs, bl; jstring(j, &bs, &bl); if (j->err) return;
+      const uint8_t *k = j->s + bs;
+      int has_esc = memchr(k, '\\', bl) != NULL;
+      if (has_esc) j->nc = 1;
+      if (is_array_index(k, bl)) { uint64_t v = index_val(k, bl); if (seen_str || (have_idx && v <= last_idx)) j->nc = 1; have_idx = 1; last_idx = v; }
+      else seen_str = 1;
+      if (nk < 64) { for (int q = 0; q < nk; q++) if (kl[q] == bl && !memcmp(j->s + ks[q], k, bl)) j->nc = 1; ks[nk] = bs; kl[nk] = bl; nk++; } else j->nc = 1;
+      jws(j); if (jpeek(j) != ':') { j->err = 1; return; } j->p++;
+      jvalue(j, depth + 1); if (j->err) return;
+      jws(j);
+      if (jpeek(j) == ',') { j->p++; continue; }
+      if (jpeek(j) == '}') { j->p++; return; }
+      j->err = 1; return;
+    }
+  } else if (c == '[') {
+    j->p++; jws(j);
+    if (jpeek(j) == ']') { j->p++; return; }
+    for (;;) {
+      jvalue(j, depth + 1); if (j->err) return;
+      jws(j);
+      if (jpeek(j) == ',') { j->p++; continue; }
+      if (jpeek(j) == ']') { j->p++; return; }
+      j->err = 1; return;
+    }
+  } else if (c == '"') { size_t a, b; jstring(j, &a, &b); }
+  else if (c == 't') { if (j->n - j->p >= 4 && !memcmp(j->s + j->p, "true", 4)) j->p += 4; else j->err = 1; }
+  else if (c == 'f') { if (j->n - j->p >= 5 && !memcmp(j->s + j->p, "false", 5)) j->p += 5; else j->err = 1; }
+  else if (c == 'n') { if (j->n - j->p >= 4 && !memcmp(j->s + j->p, "null", 4)) j->p += 4; else j->err = 1; }
+  else if (c == '-' || (c >= '0' && c <= '9')) jnumber(j);
+  else j->err = 1;
+}
+/* returns 0 ok, sets *nc; YO_EMALFORMED on a JSON.parse SyntaxError */
+static int json_check(const uint8_t *s, size_t n, int *nc) {
+  J j = { s, n, 0, 0, 0 };
+  jvalue(&j, 0);
+  if (!j.err) { jws(&j); if (j.p != j.n) j.err = 1; }
+  if (j.err == 2) return YO_EDEPTH;
+  if (j.err) return YO_EMALFORMED;
+  if (j.nc) *nc = 1;
+  return 0;
+}
+
+/* ------------------------------------------------------------------ structs */
+enum { K_GC = 0, K_SKIP = 1, K_ITEM = 2 };
+typedef struct {
+  int kind;
+  uint64_t client, clock, len;
+  /* Item fields (Y@80416 Item.write, Y@36564 reader) */
+  int ref;
+  int has_origin, has_right; uint64_t oc, ok, rc, rk;
+  int parent_is_key;          /* parent is a ykey string (else an ID) */
+  const uint8_t *pkey; size_t pkey_len; uint64_t pc, pk;
+  int has_sub; const uint8_t *sub; size_t sub_len;
+  const uint8_t *content; size_t content_len;  /* raw content bytes in the input */
+  uint64_t cut;               /* content.splice(cut) already applied (sliceStruct) */
+  int nc;                     /* content would be re-encoded differently by yjs */
+} St;
+
+/* readItemContent (Y@81141 table) -- validates and measures the content, leaves
+ * it referenced in place. */
+static void rd_content(Dec *d, St *s) {
+  size_t start = d->p; int nc = 0;
+  switch (s->ref) {
+    case 1: s->len = rdu(d); break;                                            /* ContentDeleted */
+    case 2: { uint64_t n = rdu(d); s->len = n;                                  /* ContentJSON */
+      for (uint64_t i = 0; i < n && !d->err; i++) {
+        size_t l; const uint8_t *t = rdstr(d, &l); if (d->err) break;
+        if (l == 9 && !memcmp(t, "undefined", 9)) continue;
+        int e = json_check(t, l, &nc); if (e) seterr(d, e);
+      }
+      break; }
+    case 3: { size_t l; rdbuf(d, &l); s->len = 1; break; }                      /* ContentBinary */
+    case 4: { size_t l; const uint8_t *t = rdbuf(d, &l); if (d->err) break;     /* ContentString */
+      long u = utf8_check(t, l); if (u < 0) { seterr(d, YO_EMALFORMED); break; } s->len = (uint64_t)u; break; }
+    case 5: { size_t l; const uint8_t *t = rdstr(d, &l); if (d->err) break;     /* ContentEmbed */
+      int e = json_check(t, l, &nc); if (e) seterr(d, e); s->len = 1; break; }
+    case 6: { size_t l; rdstr(d, &l); if (d->err) break;                        /* ContentFormat */
+      const uint8_t *t = rdstr(d, &l); if (d->err) break;
+      int e = json_check(t, l, &nc); if (e) seterr(d, e); s->len = 1; break; }
+    case 7: { uint64_t tr = rdu(d); if (d->err) break;       /* ContentType */
+      if (tr > 6) { seterr(d, YO_EMALFORMED); break; }
+      if (tr == 3 || tr == 5) { size_t l; rdstr(d, &l); }
+      s->len = 1; break; }
+    case 8: { uint64_t n = rdu(d); s->len = n;                                  /* ContentAny */
+      d->nm = 0;
+      for (uint64_t i = 0; i < n && !d->err; i++) rd_any(d, 0, &nc);
+      if (d->nm) nc = 1; /* a non-minimal varuint inside an Any is re-encoded by writeAny */
+      break; }
+    case 9: { size_t l; rdstr(d, &l); if (d->err) break;                        /* ContentDoc */
+      /* opts are re-created from new Doc({guid, ...opts}) (Y@70773): canonical only
+       * as an object whose keys are an ordered subset of gc:false, autoLoad:true, meta:<any non-null> */
+      size_t o0 = d->p; int anc = 0; d->nm = 0; rd_any(d, 0, &anc); if (d->err) break;
+      if (d->nm || anc) nc = 1;
+      Dec q = { d->a + o0, d->p - o0, 0, 0, 0 };
+      if (rd8(&q) != 118) { nc = 1; }
+      else {
+        uint64_t n = rdu(&q); int stage = 0;
+        for (uint64_t i = 0; i < n; i++) {
+          size_t kl; const uint8_t *k = rdbuf(&q, &kl);
+          size_t v0 = q.p; int vnc = 0; rd_any(&q, 0, &vnc);
+          uint8_t vt = q.a[v0];
+          if (kl == 2 && !memcmp(k, "gc", 2) && stage < 1 && vt == 121) stage = 1;
+          else if (kl == 8 && !memcmp(k, "autoLoad", 8) && stage < 2 && vt == 120) stage = 2;
+          else if (kl == 4 && !memcmp(k, "meta", 4) && stage < 3 && vt != 126 && vt != 127 && !vnc) stage = 3;
+          else nc = 1;
+        }
+      }
+      s->len = 1; break; }
+    default: seterr(d, YO_EMALFORMED); break;
+  }
+  if (d->err) return;
+  /* every varuint inside the content must be minimal to be written back unchanged */
+  s->content = d->a + start; s->content_len = d->p - start;
+  s->nc = nc;
+}
+
+/* lazyStructReaderGenerator (Y@36564) as an explicit state machine */
+typedef struct {
+  Dec d;
+  uint64_t blocks_left, structs_left, client, clock;
+  int started, filter_skips;
+  St cur; int has_cur;
+} Reader;
+
+static void reader_next(Reader *r) {
+  for (;;) {
+    r->has_cur = 0;
+    if (r->d.err) return;
+    while (r->structs_left == 0) {
+      if (r->blocks_left == 0) return;
+      r->blocks_left--;
+      r->structs_left = rdu(&r->d);
+      r->client = rdu(&r->d);
+      r->clock = rdu(&r->d);
+      if (r->d.err) return;
+    }
+    r->structs_left--;
+    St *s = &r->cur; memset(s, 0, sizeof *s);
+    s->client = r->client; s->clock = r->clock;
+    uint8_t info = rd8(&r->d);
+    if (r->d.err) return;
+    if (info == 10) { s->kind = K_SKIP; s->len = rdu(&r->d); }
+    else if (info & 31) {
+      s->kind = K_ITEM; s->ref = info & 31;
+      int cant_copy_parent = (info & (0x40 | 0x80)) == 0;
+      if (info & 0x80) { s->has_origin = 1; s->oc = rdu(&r->d); s->ok = rdu(&r->d); }
+      if (info & 0x40) { s->has_right = 1; s->rc = rdu(&r->d); s->rk = rdu(&r->d); }
+      if (cant_copy_parent) {
+        uint64_t pi = rdu(&r->d); /* readParentInfo: varUint === 1 */
+        if (pi == 1) { s->parent_is_key = 1; s->pkey = rdstr(&r->d, &s->pkey_len); }
+        else { s->parent_is_key = 0; s->pc = rdu(&r->d); s->pk = rdu(&r->d); }
+        if (info & 0x20) { s->has_sub = 1; s->sub = rdstr(&r->d, &s->sub_len); }
+      }
+      if (r->d.err) return;
+      if (s->ref == 10) { seterr(&r->d, YO_EMALFORMED); return; } /* contentRefs[10] -> unexpectedCase */
+      rd_content(&r->d, s);
+    } else { s->kind = K_GC; s->len = rdu(&r->d); }
+    if (r->d.err) return;
+    if (r->clock + s->len > MAX_SAFE) { seterr(&r->d, YO_ERANGE); return; }
+    r->clock += s->len;
+    r->has_cur = 1;
+    if (r->filter_skips && s->kind == K_SKIP) continue;
+    return;
+  }
+}
+static void reader_init(Reader *r, const uint8_t *u, size_t n, int filter_skips) {
+  memset(r, 0, sizeof *r);
+  r->d.a = u; r->d.n = n; r->filter_skips = filter_skips;
+  r->blocks_left = rdu(&r->d);
+  reader_next(r);
+}
+
+/* ------------------------------------------------ content slicing / writing */
+/* UTF-16 offset -> byte offset inside a UTF-8 string. *mid = 1 if the cut
+ * falls between the two halves of a surrogate pair. */
+static size_t u16_to_byte(const uint8_t *s, size_t n, uint64_t off, int *mid) {
+  size_t i = 0; uint64_t u = 0; *mid = 0;
+  while (i < n && u < off) {
+    uint8_t c = s[i];
+    int k = c < 0x80 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : 4;
+    if (k == 4) { if (u + 1 == off) { *mid = 1; return i + 4; } u += 2; }
+    else u += 1;
+    i += k;
+  }
+  return i;
+}
+
+/* content.write(encoder, offset) for all refs; `cut` from a prior splice is
+ * composed with `offset` (yjs never applies both to one struct). */
+static int write_content(Buf *o, const St *s, uint64_t offset, int flags) {
+  Dec d = { s->content, s->content_len, 0, 0, 0 };
+  uint64_t off = s->cut + offset;
+  switch (s->ref) {
+    case 1: { uint64_t n = rdu(&d); bvu(o, n - off); return 0; }
+    case 2: case 8: {
+      uint64_t n = rdu(&d); bvu(o, n - off);
+      for (uint64_t i = 0; i < n; i++) {
+        size_t a = d.p;
+        if (s->ref == 2) { size_t l; rdbuf(&d, &l); } else { int nc = 0; rd_any(&d, 0, &nc); }
+        if (i >= off) {
+          if (s->ref == 2) { Dec e = { d.a + a, d.p - a, 0, 0, 0 }; size_t l; const uint8_t *t = rdbuf(&e, &l); bstr(o, t, l); }
+          else bput(o, d.a + a, d.p - a);
+        }
+      }
+      return 0;
+    }
+    case 4: {
+      size_t l; const uint8_t *t = rdbuf(&d, &l);
+      if (off == 0) { bstr(o, t, l); return 0; }
+      int mid; size_t b = u16_to_byte(t, l, off, &mid);
+      if (mid) {
+        /* splice (sliceStruct): the right part starts with U+FFFD (Y@72776 splice).
+         * write(offset): str.slice(offset) starts with a lone low surrogate;
+         * lib0 0.2.104 encodes it as U+FFFD, lib0 0.2.42 throws (URI malformed). */
+        if (offset > 0 && (flags & YO_COMPAT_135)) return YO_ESURROGATE;
+        bvu(o, (l - b) + 3); bbyte(o, 0xEF); bbyte(o, 0xBF); bbyte(o, 0xBD); bput(o, t + b, l - b);
+      } else bstr(o, t + b, l - b);
+      return 0;
+    }
+    case 3: { size_t l; const uint8_t *t = rdbuf(&d, &l); bstr(o, t, l); return 0; }
+    case 5: { size_t l; const uint8_t *t = rdbuf(&d, &l); bstr(o, t, l); return 0; }
+    case 6: { size_t l; const uint8_t *t = rdbuf(&d, &l); bstr(o, t, l); t = rdbuf(&d, &l); bstr(o, t, l); return 0; }
+    case 7: { uint64_t tr = rdu(&d); bvu(o, tr); if (tr == 3 || tr == 5) { size_t l; const uint8_t *t = rdbuf(&d, &l); bstr(o, t, l); } return 0; }
+    case 9: { size_t l; const uint8_t *t = rdbuf(&d, &l); bstr(o, t, l); bput(o, d.a + d.p, d.n - d.p); return 0; }
+  }
+  return YO_EMALFORMED;
+}
+
+/* GC.write / Skip.write / Item.write (Y@68955, Y@81211, Y@80416) */
+static int write_struct(Buf *o, const St *s, uint64_t offset, int flags) {
+  if (s->kind == K_GC) { bbyte(o, 0); bvu(o, s->len - offset); return 0; }
+  if (s->kind == K_SKIP) { bbyte(o, 10); bvu(o, s->len - offset); return 0; }
+  if (s->nc) return YO_ENONCANON;
+  int ho = s->has_origin || offset > 0;
+  uint64_t oc = s->oc, ok = s->ok;
+  if (offset > 0) { oc = s->client; ok = s->clock + offset - 1; }
+  uint8_t info = (uint8_t)((s->ref & 31) | (ho ? 0x80 : 0) | (s->has_right ? 0x40 : 0) | (s->has_sub ? 0x20 : 0));
+  bbyte(o, info);
+  if (ho) { bvu(o, oc); bvu(o, ok); }
+  if (s->has_right) { bvu(o, s->rc); bvu(o, s->rk); }
+  if (!ho && !s->has_right) {
+    if (s->parent_is_key) { bvu(o, 1); bstr(o, s->pkey, s->pkey_len); }
+    else { bvu(o, 0); bvu(o, s->pc); bvu(o, s->pk); }
+    if (s->has_sub) bstr(o, s->sub, s->sub_len);
+  }
+  return write_content(o, s, offset, flags);
+}
+
+/* LazyStructWriter + writeStructToLazyStructWriter + finishLazyStructWriting (Y@41240-41806) */
+typedef struct { uint64_t written; Buf b; } Part;
+typedef struct {
+  uint64_t curr_client, written; Buf rest;
+  Part *parts; size_t nparts, cap; int err;
+} LWriter;
+static void lw_flush(LWriter *w) {
+  if (w->written > 0) {
+    if (w->nparts == w->cap) { w->cap = w->cap ? w->cap * 2 : 8; Part *np = (Part *)realloc(w->parts, w->cap * sizeof(Part)); if (!np) { w->err = YO_ENOMEM; return; } w->parts = np; }
+    w->parts[w->nparts].written = w->written; w->parts[w->nparts].b = w->rest; w->nparts++;
+    memset(&w->rest, 0, sizeof w->rest); w->written = 0;
+  }
+}
+static void lw_write(LWriter *w, const St *s, uint64_t offset, int flags) {
+  if (w->err) return;
+  if (w->written > 0 && w->curr_client != s->client) lw_flush(w);
+  if (w->written == 0) { w->curr_client = s->client; bvu(&w->rest, s->client); bvu(&w->rest, s->clock + offset); }
+  int e = write_struct(&w->rest, s, offset, flags);
+  if (e) w->err = e;
+  w->written++;
+}
+static void lw_finish(LWriter *w, Buf *out) {
+  lw_flush(w);
+  bvu(out, w->nparts);
+  for (size_t i = 0; i < w->nparts; i++) { bvu(out, w->parts[i].written); bput(out, w->parts[i].b.b, w->parts[i].b.n); }
+}
+static void lw_free(LWriter *w) {
+  for (size_t i = 0; i < w->nparts; i++) free(w->parts[i].b.b);
+  free(w->parts); free(w->rest.b);
+}
+
+/* ---------------------------------------------------------------- DeleteSet */
+typedef struct { uint64_t clock, len; } DItem;
+typedef struct { uint64_t client; DItem *it; size_t n, cap; } DClient;
+typedef struct { DClient *c; size_t n, cap; } DS;
+static DClient *ds_get(DS *ds, uint64_t client, int create) {
+  for (size_t i = 0; i < ds->n; i++) if (ds->c[i].client == client) return &ds->c[i];
+  if (!create) return NULL;
+  if (ds->n == ds->cap) { ds->cap = ds->cap ? ds->cap * 2 : 8; ds->c = (DClient *)realloc(ds->c, ds->cap * sizeof(DClient)); }
+  DClient *c = &ds->c[ds->n++]; memset(c, 0, sizeof *c); c->client = client; return c;
+}
+static void dc_push(DClient *c, uint64_t clock, uint64_t len) {
+  if (c->n == c->cap) { c->cap = c->cap ? c->cap * 2 : 8; c->it = (DItem *)realloc(c->it, c->cap * sizeof(DItem)); }
+  c->it[c->n].clock = clock; c->it[c->n].len = len; c->n++;
+}
+static void ds_free(DS *ds) { for (size_t i = 0; i < ds->n; i++) free(ds->c[i].it); free(ds->c); memset(ds, 0, sizeof *ds); }
+/* readDeleteSet (Y@11346) */
+static void ds_read(Dec *d, DS *ds) {
+  uint64_t n = rdu(d);
+  for (uint64_t i = 0; i < n && !d->err; i++) {
+    uint64_t client = rdu(d), nd = rdu(d);
+    if (d->err) return;
+    if (nd > 0) {
+      DClient *c = ds_get(ds, client, 1);
+      for (uint64_t k = 0; k < nd && !d->err; k++) { uint64_t ck = rdu(d), l = rdu(d); if (!d->err) dc_push(c, ck, l); }
+    }
+  }
+}
+static int cmp_ditem(const void *a, const void *b) {
+  const DItem *x = (const DItem *)a, *y = (const DItem *)b;
+  return x->clock < y->clock ? -1 : x->clock > y->clock ? 1 : 0;
+}
+/* sortAndMergeDeleteSet (Y@10246): stable sort by clock, then merge overlapping/adjacent */
+static void ds_sort_merge(DS *ds) {
+  for (size_t ci = 0; ci < ds->n; ci++) {
+    DClient *c = &ds->c[ci];
+    /* stable insertion sort (merge result does not depend on tie order) */
+    for (size_t i = 1; i < c->n; i++) { DItem t = c->it[i]; size_t j = i; while (j > 0 && cmp_ditem(&c->it[j - 1], &t) > 0) { c->it[j] = c->it[j - 1]; j--; } c->it[j] = t; }
+    size_t i, j;
+    for (i = 1, j = 1; i < c->n; i++) {
+      DItem *l = &c->it[j - 1], *r = &c->it[i];
+      if (l->clock + l->len >= r->clock) { uint64_t e = r->clock + r->len - l->clock; if (e > l->len) l->len = e; }
+      else { if (j < i) c->it[j] = *r; j++; }
+    }
+    if (c->n) c->n = j;
+  }
+}
+/* writeDeleteSet (Y@11105; 13.6.x sorts clients descending) */
+static void ds_write(Buf *o, DS *ds, int flags) {
+  bvu(o, ds->n);
+  size_t *ord = (size_t *)malloc((ds->n + 1) * sizeof(size_t));
+  for (size_t i = 0; i < ds->n; i++) ord[i] = i;
+  if (!(flags & YO_COMPAT_135)) {
+    for (size_t i = 1; i < ds->n; i++) { size_t t = ord[i]; size_t j = i; while (j > 0 && ds->c[ord[j - 1]].client < ds->c[t].client) { ord[j] = ord[j - 1]; j--; } ord[j] = t; }
+  }
+  for (size_t q = 0; q < ds->n; q++) {
+    DClient *c = &ds->c[ord[q]];
+    bvu(o, c->client); bvu(o, c->n);
+    for (size_t k = 0; k < c->n; k++) { bvu(o, c->it[k].clock); bvu(o, c->it[k].len); }
+  }
+  free(ord);
+}
+
+/* -------------------------------------------- V8 Array.prototype.sort (TimSort) */
+/* V8's ArrayTimSort (third_party/v8/builtins/array-sort.tq), i.e. CPython's
+ * listsort with binary insertion, run detection and galloping merges.  Only
+ * the sequence of comparator calls matters: yjs's decoder comparator is not a
+ * consistent order (Y@39011 returns -1 both ways for GC-vs-Item ties). */
+typedef int (*cmp_fn)(void *ctx, int a, int b);
+typedef struct { int *a; int *tmp; cmp_fn cmp; void *ctx; int min_gallop; int run_base[85], run_len[85]; int nruns; } TS;
+#define TS_CMP(x, y) ts->cmp(ts->ctx, (x), (y))
+static int ts_min_run(int n) { int r = 0; while (n >= 64) { r |= n & 1; n >>= 1; } return n + r; }
+static void ts_reverse(int *a, int lo, int hi) { hi--; while (lo < hi) { int t = a[lo]; a[lo] = a[hi]; a[hi] = t; lo++; hi--; } }
+static int ts_count_run(TS *ts, int lo_arg, int high) {
+  int *a = ts->a; int low = lo_arg + 1;
+  if (low == high) return 1;
+  int run = 2;
+  int order = TS_CMP(a[low], a[low - 1]);
+  int desc = order < 0;
+  int prev = a[low];
+  for (int i = low + 1; i < high; i++) {
+    int cur = a[i]; order = TS_CMP(cur, prev);
+    if (desc) { if (order >= 0) break; } else { if (order < 0) break; }
+    prev = cur; run++;
+  }
+  if (desc) ts_reverse(a, lo_arg, lo_arg + run);
+  return run;
+}
+static void ts_binary_insertion(TS *ts, int low, int start_arg, int high) {
+  int *a = ts->a; int start = low == start_arg ? start_arg + 1 : start_arg;
+  for (; start < high; start++) {
+    int left = low, right = start; int pivot = a[start];
+    while (left < right) { int mid = left + ((right - left) >> 1); int order = TS_CMP(pivot, a[mid]); if (order < 0) right = mid; else left = mid + 1; }
+    for (int p = start; p > left; p--) a[p] = a[p - 1];
+    a[left] = pivot;
+  }
+}
+static int ts_gallop_left(TS *ts, int *arr, int key, int base, int length, int hint) {
+  int last = 0, ofs = 1;
+  int order = TS_CMP(arr[base + hint], key);
+  if (order < 0) {
+    int max = length - hint;
+    while (ofs < max) { order = TS_CMP(arr[base + hint + ofs], key); if (order >= 0) break; last = ofs; ofs = (ofs << 1) + 1; if (ofs <= 0) ofs = max; }
+    if (ofs > max) ofs = max;
+    last += hint; ofs += hint;
+  } else {
+    int max = hint + 1;
+    while (ofs < max) { order = TS_CMP(arr[base + hint - ofs], key); if (order < 0) break; last = ofs; ofs = (ofs << 1) + 1; if (ofs <= 0) ofs = max; }
+    if (ofs > max) ofs = max;
+    int t = last; last = hint - ofs; ofs = hint - t;
+  }
+  last++;
+  while (last < ofs) { int m = last + ((ofs - last) >> 1); order = TS_CMP(arr[base + m], key); if (order < 0) last = m + 1; else ofs = m; }
+  return ofs;
+}
+static int ts_gallop_right(TS *ts, int *arr, int key, int base, int length, int hint) {
+  int last = 0, ofs = 1;
+  int order = TS_CMP(key, arr[base + hint]);
+  if (order < 0) {
+    int max = hint + 1;
+    while (ofs < max) { order = TS_CMP(key, arr[base + hint - ofs]); if (order >= 0) break; last = ofs; ofs = (ofs << 1) + 1; if (ofs <= 0) ofs = max; }
+    if (ofs > max) ofs = max;
+    int t = last; last = hint - ofs; ofs = hint - t;
+  } else {
+    int max = length - hint;
+    while (ofs < max) { order = TS_CMP(key, arr[base + hint + ofs]); if (order < 0) break; last = ofs; ofs = (ofs << 1) + 1; if (ofs <= 0) ofs = max; }
+    if (ofs > max) ofs = max;
+    last += hint; ofs += hint;
+  }
+  last++;
+  while (last < ofs) { int m = last + ((ofs - last) >> 1); order = TS_CMP(key, arr[base + m]); if (order < 0) ofs = m; else last = m + 1; }
+  return ofs;
+}
+#define MIN_GALLOP 7
+static void ts_merge_low(TS *ts, int baseA, int lenA, int baseB, int lenB) {
+  int *w = ts->a, *t = ts->tmp;
+  memcpy(t, w + baseA, lenA * sizeof(int));
+  int dest = baseA, ct = 0, cb = baseB;
+  w[dest++] = w[cb++];
+  if (--lenB == 0) goto succeed;
+  if (lenA == 1) goto copyB;
+  {
+    int mg = ts->min_gallop;
+    for (;;) {
+      int wa = 0, wb = 0;
+      for (;;) {
+        int order = TS_CMP(w[cb], t[ct]);
+        if (order < 0) { w[dest++] = w[cb++]; wb++; lenB--; wa = 0; if (lenB == 0) goto succeed; if (wb >= mg) break; }
+        else { w[dest++] = t[ct++]; wa++; lenA--; wb = 0; if (lenA == 1) goto copyB; if (wa >= mg) break; }
+      }
+      mg++;
+      int first = 1;
+      while (wa >= MIN_GALLOP || wb >= MIN_GALLOP || first) {
+        first = 0;
+        mg = mg - 1 > 1 ? mg - 1 : 1; ts->min_gallop = mg;
+        wa = ts_gallop_right(ts, t, w[cb], ct, lenA, 0);
+        if (wa > 0) { memcpy(w + dest, t + ct, wa * sizeof(int)); dest += wa; ct += wa; lenA -= wa; if (lenA == 1) goto copyB; if (lenA == 0) goto succeed; }
+        w[dest++] = w[cb++];
+        if (--lenB == 0) goto succeed;
+        wb = ts_gallop_left(ts, w, t[ct], cb, lenB, 0);
+        if (wb > 0) { memmove(w + dest, w + cb, wb * sizeof(int)); dest += wb; cb += wb; lenB -= wb; if (lenB == 0) goto succeed; }
+        w[dest++] = t[ct++];
+        if (--lenA == 1) goto copyB;
+      }
+      mg++; ts->min_gallop = mg;
+    }
+  }
+succeed:
+  if (lenA > 0) memcpy(w + dest, t + ct, lenA * sizeof(int));
+  return;
+copyB:
+  memmove(w + dest, w + cb, lenB * sizeof(int));
+  w[dest + lenB] = t[ct];
+}
+static void ts_merge_high(TS *ts, int baseA, int lenA, int baseB, int lenB) {
+  int *w = ts->a, *t = ts->tmp;
+  memcpy(t, w + baseB, lenB * sizeof(int));
+  int dest = baseB + lenB - 1, ct = lenB - 1, ca = baseA + lenA - 1;
+  w[dest--] = w[ca--];
+  if (--lenA == 0) goto succeed;
+  if (lenB == 1) goto copyA;
+  {
+    int mg = ts->min_gallop;
+    for (;;) {
+      int wa = 0, wb = 0;
+      for (;;) {
+        int order = TS_CMP(t[ct], w[ca]);
+        if (order < 0) { w[dest--] = w[ca--]; wa++; lenA--; wb = 0; if (lenA == 0) goto succeed; if (wa >= mg) break; }
+        else { w[dest--] = t[ct--]; wb++; lenB--; wa = 0; if (lenB == 1) goto copyA; if (wb >= mg) break; }
+      }
+      mg++;
+      int first = 1;
+      while (wa >= MIN_GALLOP || wb >= MIN_GALLOP || first) {
+        first = 0;
+        mg = mg - 1 > 1 ? mg - 1 : 1; ts->min_gallop = mg;
+        int k = ts_gallop_right(ts, w, t[ct], baseA, lenA, lenA - 1);
+        wa = lenA - k;
+        if (wa > 0) { dest -= wa; ca -= wa; memmove(w + dest + 1, w + ca + 1, wa * sizeof(int)); lenA -= wa; if (lenA == 0) goto succeed; }
+        w[dest--] = t[ct--];
+        if (--lenB == 1) goto copyA;
+        k = ts_gallop_left(ts, t, w[ca], 0, lenB, lenB - 1);
+        wb = lenB - k;
+        if (wb > 0) { dest -= wb; ct -= wb; memcpy(w + dest + 1, t + ct + 1, wb * sizeof(int)); lenB -= wb; if (lenB == 1) goto copyA; if (lenB == 0) goto succeed; }
+        w[dest--] = w[ca--];
+        if (--lenA == 0) goto succeed;
+      }
+      mg++; ts->min_gallop = mg;
+    }
+  }
+succeed:
+  if (lenB > 0) memcpy(w + dest - (lenB - 1), t, lenB * sizeof(int));
+  return;
+copyA:
+  dest -= lenA; ca -= lenA;
+  memmove(w + dest + 1, w + ca + 1, lenA * sizeof(int));
+  w[dest] = t[ct];
+}
+static void ts_merge_at(TS *ts, int i) {
+  int n = ts->nruns;
+  int baseA = ts->run_base[i], lenA = ts->run_len[i], baseB = ts->run_base[i + 1], lenB = ts->run_len[i + 1];
+  ts->run_len[i] = lenA + lenB;
+  if (i == n - 3) { ts->run_base[i + 1] = ts->run_base[i + 2]; ts->run_len[i + 1] = ts->run_len[i + 2]; }
+  ts->nruns = n - 1;
+  int k = ts_gallop_right(ts, ts->a, ts->a[baseB], baseA, lenA, 0);
+  baseA += k; lenA -= k;
+  if (lenA == 0) return;
+  lenB = ts_gallop_left(ts, ts->a, ts->a[baseA + lenA - 1], baseB, lenB, lenB - 1);
+  if (lenB == 0) return;
+  if (lenA <= lenB) ts_merge_low(ts, baseA, lenA, baseB, lenB); else ts_merge_high(ts, baseA, lenA, baseB, lenB);
+}
+static int ts_inv(TS *ts, int n) { if (n < 2) return 1; return ts->run_len[n - 2] > ts->run_len[n - 1] + ts->run_len[n]; }
+static void ts_collapse(TS *ts) {
+  while (ts->nruns > 1) {
+    int n = ts->nruns - 2;
+    if (!ts_inv(ts, n + 1) || !ts_inv(ts, n)) { if (ts->run_len[n - 1] < ts->run_len[n + 1]) n--; ts_merge_at(ts, n); }
+    else if (ts->run_len[n] <= ts->run_len[n + 1]) ts_merge_at(ts, n);
+    else break;
+  }
+}
+static void ts_force_collapse(TS *ts) {
+  while (ts->nruns > 1) {
+    int n = ts->nruns - 2;
+    if (n > 0 && ts->run_len[n - 1] < ts->run_len[n + 1]) n--;
+    ts_merge_at(ts, n);
+  }
+}
+/* sorts a[0..n) of element ids in place, exactly as V8 would */
+int yo_v8_sort(int *a, int n, cmp_fn cmp, void *ctx) {
+  if (n < 2) return 0;
+  TS ts; memset(&ts, 0, sizeof ts);
+  ts.a = a; ts.cmp = cmp; ts.ctx = ctx; ts.min_gallop = MIN_GALLOP;
+  ts.tmp = (int *)malloc(sizeof(int) * (size_t)n);
+  if (!ts.tmp) return YO_ENOMEM;
+  int remaining = n, low = 0, minrun = ts_min_run(n);
+  while (remaining) {
+    int run = ts_count_run(&ts, low, low + remaining);
+    if (run < minrun) { int forced = minrun < remaining ? minrun : remaining; ts_binary_insertion(&ts, low, low + run, low + forced); run = forced; }
+    ts.run_base[ts.nruns] = low; ts.run_len[ts.nruns] = run; ts.nruns++;
+    ts_collapse(&ts);
+    low += run; remaining -= run;
+  }
+  ts_force_collapse(&ts);
+  free(ts.tmp);
+  return 0;
+}
+
+/* test hook: comparator given as an n*n table of {-1,0,1} */
+typedef struct { const int8_t *T; int n; long calls; } TabCtx;
+static int tab_cmp(void *c, int a, int b) { TabCtx *t = (TabCtx *)c; t->calls++; return t->T[a * t->n + b]; }
+long yo_v8_sort_table(int *a, int n, const int8_t *T) { TabCtx c = { T, n, 0 }; yo_v8_sort(a, n, tab_cmp, &c); return c.calls; }
+
+/* ------------------------------------------------------------ mergeUpdates */
+typedef struct { Reader *r; } DecCtx;
+/* the comparator of Y@39011 */
+static int dec_cmp(void *ctx, int x, int y) {
+  Reader *R = (Reader *)ctx; const St *a = &R[x].cur, *b = &R[y].cur;
+  if (a->client == b->client) {
+    if (a->clock == b->clock) return a->kind == b->kind ? 0 : (a->kind == K_SKIP ? 1 : -1);
+    return a->clock < b->clock ? -1 : 1;
+  }
+  return b->client < a->client ? -1 : 1;
+}
+/* sliceStruct (Y@38665) */
+static St slice_struct(const St *s, uint64_t diff) {
+  St r = *s;
+  r.clock = s->clock + diff; r.len = s->len - diff;
+  if (s->kind == K_ITEM) { r.has_origin = 1; r.oc = s->client; r.ok = s->clock + diff - 1; r.cut = s->cut + diff; }
+  return r;
+}
+
+int yo_merge(const uint8_t *const *ups, const size_t *lens, size_t n, int flags, uint8_t **out, size_t *out_len) {
+  g_flags = flags;
+  *out = NULL; *out_len = 0;
+  if (n == 1) { /* single input returned as-is */
+    *out = (uint8_t *)malloc(lens[0] ? lens[0] : 1); if (!*out) return YO_ENOMEM;
+    memcpy(*out, ups[0], lens[0]); *out_len = lens[0]; return YO_OK;
+  }
+  Reader *R = (Reader *)calloc(n ? n : 1, sizeof(Reader));
+  int *order = (int *)malloc(sizeof(int) * (n ? n : 1));
+  int err = 0; size_t nd = 0;
+  LWriter W; memset(&W, 0, sizeof W);
+  St cw; int has_cw = 0;
+  for (size_t i = 0; i < n; i++) { reader_init(&R[i], ups[i], lens[i], 1); if (R[i].d.err && !err) err = R[i].d.err; order[i] = (int)i; }
+  nd = n;
+  if (err) goto done;
+  for (;;) {
+    /* decs = decs.filter(d => d.curr) ; decs.sort(cmp) */
+    size_t k = 0; for (size_t i = 0; i < nd; i++) if (R[order[i]].has_cur) order[k++] = order[i];
+    nd = k;
+    if (yo_v8_sort(order, (int)nd, dec_cmp, R)) { err = YO_ENOMEM; goto done; }
+    if (nd == 0) break;
+    Reader *t = &R[order[0]];
+    uint64_t first_client = t->cur.client;
+    if (has_cw) {
+      St *curr = t->has_cur ? &t->cur : NULL; int iterated = 0;
+      while (curr && curr->clock + curr->len <= cw.clock + cw.len && curr->client >= cw.client) {
+        reader_next(t); if (t->d.err) { err = t->d.err; goto done; }
+        curr = t->has_cur ? &t->cur : NULL; iterated = 1;
+      }
+      if (!curr || curr->client != first_client || (iterated && curr->clock > cw.clock + cw.len)) continue;
+      if (first_client != cw.client) {
+        lw_write(&W, &cw, 0, flags); cw = *curr; reader_next(t);
+      } else if (cw.clock + cw.len < curr->clock) {
+        if (cw.kind == K_SKIP) { cw.len = curr->clock + curr->len - cw.clock; }
+        else {
+          lw_write(&W, &cw, 0, flags);
+          uint64_t diff = curr->clock - cw.clock - cw.len;
+          St sk; memset(&sk, 0, sizeof sk); sk.kind = K_SKIP; sk.client = first_client; sk.clock = cw.clock + cw.len; sk.len = diff;
+          cw = sk;
+        }
+      } else {
+        uint64_t diff = cw.clock + cw.len - curr->clock;
+        St c2 = *curr;
+        if (diff > 0) { if (cw.kind == K_SKIP) cw.len -= diff; else c2 = slice_struct(curr, diff); }
+        /* mergeWith: GC+GC, Skip+Skip add lengths; lazy Items never merge (right !== null) */
+        if ((cw.kind == K_GC && c2.kind == K_GC) || (cw.kind == K_SKIP && c2.kind == K_SKIP)) cw.len += c2.len;
+        else { lw_write(&W, &cw, 0, flags); cw = c2; reader_next(t); }
+      }
+    } else {
+      cw = t->cur; has_cw = 1; reader_next(t);
+    }
+    if (t->d.err) { err = t->d.err; goto done; }
+    while (t->has_cur && t->cur.client == first_client && t->cur.clock == cw.clock + cw.len && t->cur.kind != K_SKIP) {
+      lw_write(&W, &cw, 0, flags); cw = t->cur;
+      reader_next(t); if (t->d.err) { err = t->d.err; goto done; }
+    }
+    if (W.err) { err = W.err; goto done; }
+  }
+  if (has_cw) lw_write(&W, &cw, 0, flags);
+  if (W.err) { err = W.err; goto done; }
+  {
+    Buf o; memset(&o, 0, sizeof o);
+    lw_finish(&W, &o);
+    /* dss = updates.map(readDeleteSet); mergeDeleteSets (Y@10486); writeDeleteSet */
+    DS *dss = (DS *)calloc(n ? n : 1, sizeof(DS)); DS m; memset(&m, 0, sizeof m);
+    for (size_t i = 0; i < n && !err; i++) { ds_read(&R[i].d, &dss[i]); if (R[i].d.err) err = R[i].d.err; }
+    if (!err) {
+      for (size_t i = 0; i < n; i++) for (size_t c = 0; c < dss[i].n; c++) {
+        DClient *src = &dss[i].c[c];
+        if (ds_get(&m, src->client, 0)) continue;
+        DClient *dst = ds_get(&m, src->client, 1);
+        for (size_t k2 = 0; k2 < src->n; k2++) dc_push(dst, src->it[k2].clock, src->it[k2].len);
+        for (size_t j = i + 1; j < n; j++) { DClient *o2 = ds_get(&dss[j], src->client, 0); if (o2) for (size_t k2 = 0; k2 < o2->n; k2++) dc_push(dst, o2->it[k2].clock, o2->it[k2].len); }
+      }
+      ds_sort_merge(&m);
+      ds_write(&o, &m, flags);
+    }
+    for (size_t i = 0; i < n; i++) ds_free(&dss[i]);
+    free(dss); ds_free(&m);
+    if (o.oom && !err) err = YO_ENOMEM;
+    if (!err) { *out = o.b; *out_len = o.n; } else free(o.b);
+  }
+done:
+  lw_free(&W); free(R); free(order);
+  return err;
+}
+
+/* -------------------------------------------------------------- diffUpdate */
+int yo_diff(const uint8_t *u, size_t ulen, const uint8_t *sv, size_t svlen, int flags, uint8_t **out, size_t *out_len) {
+  g_flags = flags;
+  *out = NULL; *out_len = 0;
+  /* decodeStateVector: Map, later entries win */
+  Dec sd = { sv, svlen, 0, 0, 0 };
+  uint64_t ns = rdu(&sd);
+  size_t cap = ns < 1024 ? (size_t)ns : 1024; uint64_t *svc = NULL, *svk = NULL; size_t nsv = 0;
+  if (!sd.err) { svc = (uint64_t *)malloc((cap + 1) * 8); svk = (uint64_t *)malloc((cap + 1) * 8); }
+  for (uint64_t i = 0; i < ns && !sd.err; i++) {
+    uint64_t c = rdu(&sd), k = rdu(&sd); if (sd.err) break;
+    size_t j; for (j = 0; j < nsv; j++) if (svc[j] == c) break;
+    if (j == nsv) { if (nsv == cap) { cap *= 2; svc = (uint64_t *)realloc(svc, (cap + 1) * 8); svk = (uint64_t *)realloc(svk, (cap + 1) * 8); } svc[nsv] = c; nsv++; }
+    svk[j] = k;
+  }
+  if (sd.err) { free(svc); free(svk); return sd.err; }
+  LWriter W; memset(&W, 0, sizeof W);
+  Reader r; reader_init(&r, u, ulen, 0);
+  int err = r.d.err;
+  while (!err && r.has_cur) {
+    uint64_t client = r.cur.client, svclock = 0;
+    for (size_t j = 0; j < nsv; j++) if (svc[j] == client) { svclock = svk[j]; break; }
+    if (r.cur.kind == K_SKIP) { reader_next(&r); err = r.d.err; continue; }
+    if (r.cur.clock + r.cur.len > svclock) {
+      uint64_t off = svclock > r.cur.clock ? svclock - r.cur.clock : 0;
+      lw_write(&W, &r.cur, off, flags);
+      reader_next(&r); err = r.d.err;
+      while (!err && r.has_cur && r.cur.client == client) { lw_write(&W, &r.cur, 0, flags); reader_next(&r); err = r.d.err; }
+    } else {
+      while (!err && r.has_cur && r.cur.client == client && r.cur.clock + r.cur.len <= svclock) { reader_next(&r); err = r.d.err; }
+    }
+    if (!err && W.err) err = W.err;
+  }
+  if (!err && W.err) err = W.err;
+  Buf o; memset(&o, 0, sizeof o);
+  if (!err) {
+    lw_finish(&W, &o);
+    DS ds; memset(&ds, 0, sizeof ds);
+    ds_read(&r.d, &ds); err = r.d.err;
+    if (!err) ds_write(&o, &ds, flags);
+    ds_free(&ds);
+  }
+  lw_free(&W); free(svc); free(svk);
+  if (o.oom && !err) err = YO_ENOMEM;
+  if (!err) { *out = o.b; *out_len = o.n; } else free(o.b);
+  return err;
+}
+
+/* ----------------------------------------------- encodeStateVectorFromUpdate */
+int yo_sv(const uint8_t *u, size_t ulen, int flags, uint8_t **out, size_t *out_len) {
+  g_flags = flags;
+  (void)flags;
+  *out = NULL; *out_len = 0;
+  Reader r; reader_init(&r, u, ulen, 0);
+  if (r.d.err) return r.d.err;
+  Buf body; memset(&body, 0, sizeof body); Buf o; memset(&o, 0, sizeof o);
+  uint64_t size = 0;
+  if (r.has_cur) {
+    uint64_t cur_client = r.cur.client;
+    int stop = r.cur.clock != 0;
+    uint64_t cur_clock = stop ? 0 : r.cur.clock + r.cur.len;
+    while (r.has_cur) {
+      if (cur_client != r.cur.client) {
+        if (cur_clock != 0) { size++; bvu(&body, cur_client); bvu(&body, cur_clock); }
+        cur_client = r.cur.client; cur_clock = 0; stop = r.cur.clock != 0;
+      }
+      if (r.cur.kind == K_SKIP) stop = 1;
+      if (!stop) cur_clock = r.cur.clock + r.cur.len;
+      reader_next(&r);
+      if (r.d.err) { free(body.b); return r.d.err; }
+    }
+    if (cur_clock != 0) { size++; bvu(&body, cur_client); bvu(&body, cur_clock); }
+  }
+  bvu(&o, size); bput(&o, body.b, body.n);
+  free(body.b);
+  if (o.oom) { free(o.b); return YO_ENOMEM; }
+  *out = o.b; *out_len = o.n;
+  return YO_OK;
+}
+
+void yo_free(void *p) { free(p); }
+const char *yo_version(void) { return "yjs_oracle 1 (yjs 13.6.26 semantics; YO_COMPAT_135 = 13.5.16)"; }

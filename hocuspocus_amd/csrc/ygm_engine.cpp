@@ -1,0 +1,341 @@
+// ygm_engine.cpp -- host runtime behind include/ygm.h.
+//
+// One context per GPU: a HIP stream, grow-only device workspaces, host result
+// buffers and HIP-event timers.  A batch call = H2D of the packed inputs, one
+// fast-path launch (look-back placed, packed output), an 8-byte-class meta
+// read, the sequential kernel only when some document needed it, D2H.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/ygm.h"
+
+extern "C" {
+size_t ygm_k_meta_bytes();
+size_t ygm_k_seq_reader_bytes();
+size_t ygm_k_drec_bytes();
+int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,
+                     uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
+                     unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
+int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
+                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta,
+                            uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
+int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list, uint32_t n_fb,
+                           uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
+                           void* readers, int* order, int* tmp, const uint8_t** ubase, uint32_t* ulen, uint64_t upd_cap,
+                           uint32_t* cnt, void* drec, uint64_t byte_cap, uint64_t out_cap, hipStream_t s);
+}
+
+namespace {
+
+// mirrors ygm::DocMeta (ygm_kernels.hip)
+struct Meta {
+  unsigned int ticket, fault, fb_count, pad;
+  unsigned long long fast_total, seq_cursor, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor;
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t n) {
+    if (n <= cap && p) return true;
+    if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+    size_t c = std::max<size_t>(n, 256);
+    c += c / 4;  // grow with headroom
+    if (hipMalloc(&p, c) != hipSuccess) { p = nullptr; return false; }
+    cap = c;
+    return true;
+  }
+  void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+  template <class T> T* as() const { return (T*)p; }
+};
+
+}  // namespace
+
+struct ygm_ctx {
+  int device = 0;
+  uint32_t flags = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
+  // device inputs (host API staging)
+  DevBuf arena, offs, docs, sv_arena, sv_offs;
+  // device outputs + state
+  DevBuf out, out_off, out_len, status, lb, meta, fb_list;
+  DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
+  // host results
+  std::vector<uint8_t> h_data;
+  std::vector<uint64_t> h_off, h_len;
+  std::vector<int32_t> h_status;
+  std::vector<uint32_t> h_doc_upd;
+  ygm_stats_t stats{};
+};
+
+static int herr(hipError_t e) { return e == hipSuccess ? YGM_OK : YGM_EDEVICE; }
+#define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return YGM_EDEVICE; } while (0)
+
+extern "C" {
+
+const char* ygm_version(void) { return "ygm 0.1 (gfx950; yjs 13.6.26 update-v1 semantics)"; }
+
+const char* ygm_strerror(int code) {
+  switch (code) {
+    case YGM_OK: return "ok";
+    case YGM_EMALFORMED: return "Unexpected end of array / malformed update";
+    case YGM_ERANGE: return "Integer out of Range";
+    case YGM_ENONCANON: return "non-canonical content (yjs would re-encode it)";
+    case YGM_ESURROGATE: return "lone surrogate in string slice (yjs 13.5 compat)";
+    case YGM_EDEPTH: return "Any/JSON nesting too deep";
+    case YGM_ENOMEM: return "out of device memory";
+    case YGM_EDEVICE: return "HIP device error";
+    case YGM_EINVAL: return "invalid argument";
+  }
+  return "unknown error";
+}
+
+int ygm_open(int device, uint32_t flags, ygm_ctx** out) {
+  if (!out) return YGM_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return YGM_EDEVICE;
+  ygm_ctx* c = new ygm_ctx();
+  c->device = device; c->flags = flags;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess || hipEventCreate(&c->e2) != hipSuccess ||
+      hipEventCreate(&c->e3) != hipSuccess) {
+    delete c;
+    return YGM_EDEVICE;
+  }
+  if (!c->meta.ensure(sizeof(Meta))) { ygm_close(c); return YGM_ENOMEM; }
+  *out = c;
+  return YGM_OK;
+}
+
+void ygm_close(ygm_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
+                    &c->lb, &c->meta, &c->fb_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
+                    &c->s_drec})
+    b->release();
+  for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int ygm_stats(ygm_ctx* c, ygm_stats_t* out) {
+  if (!c || !out) return YGM_EINVAL;
+  *out = c->stats;
+  return YGM_OK;
+}
+
+// ------------------------------------------------------------------ device API
+static int prep_outputs(ygm_ctx* c, uint32_t n_docs, uint64_t out_cap, hipStream_t s) {
+  const uint32_t tiles = n_docs + 1;
+  if (!c->out.ensure(out_cap + 64) || !c->out_off.ensure((size_t)n_docs * 8 + 8) || !c->out_len.ensure((size_t)n_docs * 8 + 8) ||
+      !c->status.ensure((size_t)n_docs * 4 + 4) || !c->lb.ensure((size_t)tiles * 8) || !c->fb_list.ensure((size_t)n_docs * 4 + 4))
+    return YGM_ENOMEM;
+  HIPCHK(hipMemsetAsync(c->lb.p, 0, (size_t)tiles * 8, s));
+  HIPCHK(hipMemsetAsync(c->meta.p, 0, sizeof(Meta), s));
+  return YGM_OK;
+}
+
+static void fill_dev_result(ygm_ctx* c, uint64_t data_bytes, ygm_device_result* out) {
+  out->data = c->out.as<uint8_t>();
+  out->off = c->out_off.as<uint64_t>();
+  out->len = c->out_len.as<uint64_t>();
+  out->status = c->status.as<int32_t>();
+  out->data_bytes = data_bytes;
+}
+
+int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_upd_off,
+                        const uint32_t* d_doc_upd, uint32_t n_upd, uint32_t n_docs, void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  (void)hipSetDevice(c->device);
+  // merge output <= 3 x input (+ per-document constants); kernels also check the cap
+  const uint64_t out_cap = 3 * arena_bytes + 16ull * n_docs + 64;
+  int e = prep_outputs(c, n_docs, out_cap, s);
+  if (e) return e;
+  HIPCHK(hipEventRecord(c->e0, s));
+  if (ygm_k_launch_merge_fast(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
+                              c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->lb.as<unsigned long long>(), c->meta.p,
+                              c->fb_list.as<uint32_t>(), out_cap, s))
+    return YGM_EDEVICE;
+  HIPCHK(hipEventRecord(c->e1, s));
+  Meta m;
+  HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (m.fault) return YGM_EDEVICE;
+  uint64_t total = m.fast_total;
+  if (m.fb_count) {
+    const uint64_t upd_cap = m.fb_upds + 1, byte_cap = m.fb_bytes + 8ull * m.fb_count + 8;
+    if (!c->s_readers.ensure(upd_cap * ygm_k_seq_reader_bytes()) || !c->s_order.ensure(upd_cap * 4) || !c->s_tmp.ensure(upd_cap * 4) ||
+        !c->s_ubase.ensure(upd_cap * 8) || !c->s_ulen.ensure(upd_cap * 4) || !c->s_cnt.ensure(byte_cap * 4) ||
+        !c->s_drec.ensure((byte_cap / 2 + 1) * ygm_k_drec_bytes()))
+      return YGM_ENOMEM;
+    if (ygm_k_launch_merge_seq(d_arena, d_upd_off, d_doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->out.as<uint8_t>(),
+                               c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->meta.p,
+                               c->s_readers.p, c->s_order.as<int>(), c->s_tmp.as<int>(), c->s_ubase.as<const uint8_t*>(),
+                               c->s_ulen.as<uint32_t>(), upd_cap, c->s_cnt.as<uint32_t>(), c->s_drec.p, byte_cap, out_cap, s))
+      return YGM_EDEVICE;
+    HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    total = m.fast_total + m.seq_cursor;
+    c->stats.docs_seq += m.fb_count;
+  }
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;
+  c->stats.calls++; c->stats.docs += n_docs; c->stats.updates += n_upd;
+  c->stats.docs_fast += n_docs - m.fb_count;
+  c->stats.bytes_in += arena_bytes; c->stats.bytes_out += total;
+  fill_dev_result(c, total, out);
+  return YGM_OK;
+}
+
+static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off,
+                          const uint8_t* d_sv, const uint64_t* d_sv_off, uint32_t n_docs, void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  (void)hipSetDevice(c->device);
+  const uint64_t out_cap = 2 * arena_bytes + 32ull * n_docs + 64;
+  int e = prep_outputs(c, n_docs, out_cap, s);
+  if (e) return e;
+  HIPCHK(hipEventRecord(c->e0, s));
+  if (ygm_k_launch_doc(mode, d_arena, d_doc_off, d_sv, d_sv_off, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
+                       c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->lb.as<unsigned long long>(), c->meta.p, out_cap, s))
+    return YGM_EDEVICE;
+  HIPCHK(hipEventRecord(c->e1, s));
+  Meta m;
+  HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (m.fault) return YGM_EDEVICE;
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;
+  c->stats.calls++; c->stats.docs += n_docs; c->stats.docs_fast += n_docs;
+  c->stats.bytes_in += arena_bytes; c->stats.bytes_out += m.fast_total;
+  fill_dev_result(c, m.fast_total, out);
+  return YGM_OK;
+}
+
+int ygm_diff_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, const uint8_t* d_sv_arena,
+                       const uint64_t* d_sv_off, uint32_t n_docs, void* stream, ygm_device_result* out) {
+  return run_doc_kernel(c, 1, d_arena, arena_bytes, d_doc_off, d_sv_arena, d_sv_off, n_docs, stream, out);
+}
+
+int ygm_sv_from_update_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
+                                 void* stream, ygm_device_result* out) {
+  return run_doc_kernel(c, 0, d_arena, arena_bytes, d_doc_off, nullptr, nullptr, n_docs, stream, out);
+}
+
+// ------------------------------------------------------------------ host API
+static int h2d(ygm_ctx* c, DevBuf& b, const void* src, size_t n, size_t pad) {
+  if (!b.ensure(n + pad)) return YGM_ENOMEM;
+  if (n) HIPCHK(hipMemcpyAsync(b.p, src, n, hipMemcpyHostToDevice, c->stream));
+  if (pad) HIPCHK(hipMemsetAsync((uint8_t*)b.p + n, 0, pad, c->stream));
+  return YGM_OK;
+}
+
+static int fetch_results(ygm_ctx* c, uint32_t n_docs, const ygm_device_result& dr, ygm_result* out) {
+  c->h_off.resize(n_docs); c->h_len.resize(n_docs); c->h_status.resize(n_docs);
+  c->h_data.resize(dr.data_bytes ? dr.data_bytes : 1);
+  HIPCHK(hipEventRecord(c->e2, c->stream));
+  if (n_docs) {
+    HIPCHK(hipMemcpyAsync(c->h_off.data(), dr.off, n_docs * 8ull, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_len.data(), dr.len, n_docs * 8ull, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_status.data(), dr.status, n_docs * 4ull, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (dr.data_bytes) HIPCHK(hipMemcpyAsync(c->h_data.data(), dr.data, dr.data_bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipEventRecord(c->e3, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->e2, c->e3) == hipSuccess) c->stats.d2h_ms += ms;
+  for (uint32_t d = 0; d < n_docs; d++)
+    if (c->h_status[d] >= 100 || c->h_status[d] < 0) c->h_status[d] = YGM_EDEVICE;  // never left internal codes
+  out->data = c->h_data.data(); out->off = c->h_off.data(); out->len = c->h_len.data(); out->status = c->h_status.data();
+  out->n_docs = n_docs; out->data_bytes = dr.data_bytes;
+  return YGM_OK;
+}
+
+int ygm_merge_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* upd_off, const uint32_t* upd_doc, uint32_t n_upd, uint32_t n_docs,
+                 ygm_result* out) {
+  if (!c || !out || (n_upd && (!arena || !upd_off || !upd_doc))) return YGM_EINVAL;
+  (void)hipSetDevice(c->device);
+  // per-document update ranges; document ids must be non-decreasing
+  c->h_doc_upd.assign((size_t)n_docs + 1, 0);
+  for (uint32_t i = 0; i < n_upd; i++) {
+    if (upd_doc[i] >= n_docs || (i && upd_doc[i] < upd_doc[i - 1])) return YGM_EINVAL;
+    if (upd_off[i + 1] < upd_off[i]) return YGM_EINVAL;
+    c->h_doc_upd[upd_doc[i] + 1]++;
+  }
+  for (uint32_t d = 0; d < n_docs; d++) c->h_doc_upd[d + 1] += c->h_doc_upd[d];
+  const uint64_t bytes = n_upd ? upd_off[n_upd] - upd_off[0] : 0;
+  // offsets are rebased to the first update
+  std::vector<uint64_t> rel(n_upd + 1);
+  for (uint32_t i = 0; i <= n_upd; i++) rel[i] = n_upd ? upd_off[i] - upd_off[0] : 0;
+  HIPCHK(hipEventRecord(c->e2, c->stream));
+  int e;
+  if ((e = h2d(c, c->arena, n_upd ? arena + upd_off[0] : nullptr, bytes, 64))) return e;
+  if ((e = h2d(c, c->offs, rel.data(), rel.size() * 8, 0))) return e;
+  if ((e = h2d(c, c->docs, c->h_doc_upd.data(), c->h_doc_upd.size() * 4, 0))) return e;
+  HIPCHK(hipEventRecord(c->e3, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->e2, c->e3) == hipSuccess) c->stats.h2d_ms += ms;
+  ygm_device_result dr;
+  if ((e = ygm_merge_v1_device(c, c->arena.as<uint8_t>(), bytes, c->offs.as<uint64_t>(), c->docs.as<uint32_t>(), n_upd, n_docs,
+                               nullptr, &dr)))
+    return e;
+  return fetch_results(c, n_docs, dr, out);
+}
+
+static int host_doc_call(ygm_ctx* c, int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena,
+                         const uint64_t* sv_off, uint32_t n_docs, ygm_result* out) {
+  if (!c || !out || (n_docs && (!arena || !doc_off))) return YGM_EINVAL;
+  if (mode == 1 && n_docs && (!sv_arena || !sv_off)) return YGM_EINVAL;
+  (void)hipSetDevice(c->device);
+  for (uint32_t d = 0; d < n_docs; d++) {
+    if (doc_off[d + 1] < doc_off[d]) return YGM_EINVAL;
+    if (mode == 1 && sv_off[d + 1] < sv_off[d]) return YGM_EINVAL;
+  }
+  const uint64_t bytes = n_docs ? doc_off[n_docs] - doc_off[0] : 0;
+  std::vector<uint64_t> rel(n_docs + 1), srel;
+  for (uint32_t d = 0; d <= n_docs; d++) rel[d] = n_docs ? doc_off[d] - doc_off[0] : 0;
+  HIPCHK(hipEventRecord(c->e2, c->stream));
+  int e;
+  if ((e = h2d(c, c->arena, n_docs ? arena + doc_off[0] : nullptr, bytes, 64))) return e;
+  if ((e = h2d(c, c->offs, rel.data(), rel.size() * 8, 0))) return e;
+  uint64_t sv_bytes = 0;
+  if (mode == 1) {
+    sv_bytes = n_docs ? sv_off[n_docs] - sv_off[0] : 0;
+    srel.resize(n_docs + 1);
+    for (uint32_t d = 0; d <= n_docs; d++) srel[d] = n_docs ? sv_off[d] - sv_off[0] : 0;
+    if ((e = h2d(c, c->sv_arena, n_docs ? sv_arena + sv_off[0] : nullptr, sv_bytes, 64))) return e;
+    if ((e = h2d(c, c->sv_offs, srel.data(), srel.size() * 8, 0))) return e;
+  }
+  HIPCHK(hipEventRecord(c->e3, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->e2, c->e3) == hipSuccess) c->stats.h2d_ms += ms;
+  ygm_device_result dr;
+  if (mode == 1)
+    e = ygm_diff_v1_device(c, c->arena.as<uint8_t>(), bytes, c->offs.as<uint64_t>(), c->sv_arena.as<uint8_t>(), c->sv_offs.as<uint64_t>(),
+                           n_docs, nullptr, &dr);
+  else
+    e = ygm_sv_from_update_v1_device(c, c->arena.as<uint8_t>(), bytes, c->offs.as<uint64_t>(), n_docs, nullptr, &dr);
+  if (e) return e;
+  return fetch_results(c, n_docs, dr, out);
+}
+
+int ygm_diff_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,
+                uint32_t n_docs, ygm_result* out) {
+  return host_doc_call(c, 1, arena, doc_off, sv_arena, sv_off, n_docs, out);
+}
+
+int ygm_sv_from_update_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, ygm_result* out) {
+  return host_doc_call(c, 0, arena, doc_off, nullptr, nullptr, n_docs, out);
+}
+
+}  // extern "C"

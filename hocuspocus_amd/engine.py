@@ -1,0 +1,257 @@
+"""ctypes binding of libygm.so (include/ygm.h) -- the MI355X batched Yjs update engine.
+
+Python mirror of the yjs update-level API that Hocuspocus's persistence and
+sync path calls, batched over documents:
+
+* ``Engine.merge_updates_batch(docs)``          per document ``Y.mergeUpdates(updates)``
+* ``Engine.diff_update_batch(updates, svs)``    per document ``Y.diffUpdate(update, sv)``
+* ``Engine.encode_state_vector_from_update_batch(updates)``
+                                                 per document ``Y.encodeStateVectorFromUpdate``
+
+Single-document helpers (``merge_updates`` ...) raise :class:`YjsError` where yjs
+throws, mirroring the reference's error behaviour.  There is no CPU fallback:
+if the HIP library is missing or no GPU is present, construction fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libygm.so")
+
+OK, EMALFORMED, ERANGE, ENONCANON, ESURROGATE, EDEPTH, ENOMEM, EDEVICE, EINVAL = range(9)
+STATUS_NAMES = {0: "OK", 1: "EMALFORMED", 2: "ERANGE", 3: "ENONCANON", 4: "ESURROGATE", 5: "EDEPTH",
+                6: "ENOMEM", 7: "EDEVICE", 8: "EINVAL"}
+F_COMPAT_135 = 1
+F_FORCE_SEQ = 2
+
+
+class YjsError(Exception):
+    """Raised where yjs would throw (or where the engine refuses a document)."""
+
+    def __init__(self, code: int):
+        self.code = code
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {strerror(code)}")
+
+
+class _Result(ctypes.Structure):
+    _fields_ = [("data", ctypes.POINTER(ctypes.c_uint8)), ("off", ctypes.POINTER(ctypes.c_uint64)),
+                ("len", ctypes.POINTER(ctypes.c_uint64)), ("status", ctypes.POINTER(ctypes.c_int32)),
+                ("n_docs", ctypes.c_uint32), ("data_bytes", ctypes.c_uint64)]
+
+
+class _DevResult(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("off", ctypes.c_void_p), ("len", ctypes.c_void_p),
+                ("status", ctypes.c_void_p), ("data_bytes", ctypes.c_uint64)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("calls", ctypes.c_uint64), ("docs", ctypes.c_uint64), ("updates", ctypes.c_uint64),
+                ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64), ("docs_fast", ctypes.c_uint64),
+                ("docs_seq", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
+                ("d2h_ms", ctypes.c_double)]
+
+
+_lib = None
+
+# every symbol include/ygm.h declares
+EXPORTS = ("ygm_open", "ygm_close", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_update_v1", "ygm_merge_v1_device",
+           "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_stats", "ygm_strerror", "ygm_version")
+
+
+def lib():
+    """Loads libygm.so (raises OSError when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        L.ygm_open.argtypes = [ctypes.c_int, u32, ctypes.POINTER(vp)]
+        L.ygm_close.argtypes = [vp]
+        L.ygm_close.restype = None
+        L.ygm_merge_v1.argtypes = [vp, vp, vp, vp, u32, u32, ctypes.POINTER(_Result)]
+        L.ygm_diff_v1.argtypes = [vp, vp, vp, vp, vp, u32, ctypes.POINTER(_Result)]
+        L.ygm_sv_from_update_v1.argtypes = [vp, vp, vp, u32, ctypes.POINTER(_Result)]
+        L.ygm_merge_v1_device.argtypes = [vp, vp, u64, vp, vp, u32, u32, vp, ctypes.POINTER(_DevResult)]
+        L.ygm_diff_v1_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, vp, ctypes.POINTER(_DevResult)]
+        L.ygm_sv_from_update_v1_device.argtypes = [vp, vp, u64, vp, u32, vp, ctypes.POINTER(_DevResult)]
+        L.ygm_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+        L.ygm_strerror.argtypes = [i32]
+        L.ygm_strerror.restype = ctypes.c_char_p
+        L.ygm_version.restype = ctypes.c_char_p
+        for f in ("ygm_open", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_update_v1", "ygm_merge_v1_device",
+                  "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_stats"):
+            getattr(L, f).restype = i32
+        _lib = L
+    return _lib
+
+
+def strerror(code: int) -> str:
+    return lib().ygm_strerror(code).decode()
+
+
+def _pack(blobs):
+    arena = b"".join(blobs)
+    off = np.zeros(len(blobs) + 1, dtype=np.uint64)
+    if blobs:
+        np.cumsum(np.fromiter((len(b) for b in blobs), dtype=np.uint64, count=len(blobs)), out=off[1:])
+    return arena, off
+
+
+def _ptr(a):
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(ctypes.c_void_p)
+    return ctypes.c_char_p(a) if a else None
+
+
+@dataclass
+class DeviceResult:
+    """Outputs left in HBM by a device-resident call (context-owned memory)."""
+    data: int
+    off: int
+    len: int
+    status: int
+    data_bytes: int
+
+
+class Engine:
+    """One engine context on one GPU (not thread-safe; one batch in flight)."""
+
+    def __init__(self, device: int = 0, compat135: bool = False, force_seq: bool = False):
+        flags = (F_COMPAT_135 if compat135 else 0) | (F_FORCE_SEQ if force_seq else 0)
+        ctx = ctypes.c_void_p()
+        st = lib().ygm_open(device, flags, ctypes.byref(ctx))
+        if st != OK:
+            raise YjsError(st)
+        self._ctx = ctx
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            lib().ygm_close(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------ results
+    @staticmethod
+    def _unpack(res: _Result):
+        n = res.n_docs
+        if n == 0:
+            return []
+        off = np.ctypeslib.as_array(res.off, shape=(n,))
+        ln = np.ctypeslib.as_array(res.len, shape=(n,))
+        status = np.ctypeslib.as_array(res.status, shape=(n,))
+        data = ctypes.string_at(res.data, res.data_bytes) if res.data_bytes else b""
+        out = []
+        for d in range(n):
+            st = int(status[d])
+            if st == OK:
+                o = int(off[d])
+                out.append((OK, data[o:o + int(ln[d])]))
+            else:
+                out.append((st, None))
+        return out
+
+    # ------------------------------------------------------------ batch API
+    def merge_updates_batch(self, docs):
+        """docs: list of lists of update bytes -> list of (status, merged bytes | None)."""
+        blobs, doc_ids = [], []
+        for d, ups in enumerate(docs):
+            for u in ups:
+                blobs.append(bytes(u))
+                doc_ids.append(d)
+        arena, off = _pack(blobs)
+        upd_doc = np.asarray(doc_ids, dtype=np.uint32)
+        res = _Result()
+        st = lib().ygm_merge_v1(self._ctx, arena or None, _ptr(off), _ptr(upd_doc), len(blobs), len(docs), ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._unpack(res)
+
+    def merge_packed(self, arena: np.ndarray, upd_off: np.ndarray, upd_doc: np.ndarray, n_docs: int):
+        """Packed host-array form of merge_updates_batch (arena uint8, upd_off uint64, upd_doc uint32)."""
+        res = _Result()
+        st = lib().ygm_merge_v1(self._ctx, _ptr(arena), _ptr(upd_off), _ptr(upd_doc), len(upd_doc), n_docs, ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._unpack(res)
+
+    def diff_update_batch(self, updates, svs):
+        arena, off = _pack([bytes(u) for u in updates])
+        sva, svo = _pack([bytes(s) for s in svs])
+        res = _Result()
+        st = lib().ygm_diff_v1(self._ctx, arena or None, _ptr(off), sva or None, _ptr(svo), len(updates), ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._unpack(res)
+
+    def encode_state_vector_from_update_batch(self, updates):
+        arena, off = _pack([bytes(u) for u in updates])
+        res = _Result()
+        st = lib().ygm_sv_from_update_v1(self._ctx, arena or None, _ptr(off), len(updates), ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._unpack(res)
+
+    # ------------------------------------------------------------ yjs-shaped single calls
+    def merge_updates(self, updates):
+        st, out = self.merge_updates_batch([list(updates)])[0]
+        if st != OK:
+            raise YjsError(st)
+        return out
+
+    def diff_update(self, update, sv):
+        st, out = self.diff_update_batch([update], [sv])[0]
+        if st != OK:
+            raise YjsError(st)
+        return out
+
+    def encode_state_vector_from_update(self, update):
+        st, out = self.encode_state_vector_from_update_batch([update])[0]
+        if st != OK:
+            raise YjsError(st)
+        return out
+
+    # ------------------------------------------------------------ device-resident API
+    def merge_device(self, d_arena: int, arena_bytes: int, d_upd_off: int, d_doc_upd: int, n_upd: int, n_docs: int,
+                     stream: int = 0) -> DeviceResult:
+        r = _DevResult()
+        st = lib().ygm_merge_v1_device(self._ctx, d_arena, arena_bytes, d_upd_off, d_doc_upd, n_upd, n_docs, stream or None,
+                                       ctypes.byref(r))
+        if st != OK:
+            raise YjsError(st)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes)
+
+    def diff_device(self, d_arena, arena_bytes, d_doc_off, d_sv, d_sv_off, n_docs, stream=0) -> DeviceResult:
+        r = _DevResult()
+        st = lib().ygm_diff_v1_device(self._ctx, d_arena, arena_bytes, d_doc_off, d_sv, d_sv_off, n_docs, stream or None,
+                                      ctypes.byref(r))
+        if st != OK:
+            raise YjsError(st)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes)
+
+    def sv_device(self, d_arena, arena_bytes, d_doc_off, n_docs, stream=0) -> DeviceResult:
+        r = _DevResult()
+        st = lib().ygm_sv_from_update_v1_device(self._ctx, d_arena, arena_bytes, d_doc_off, n_docs, stream or None,
+                                                ctypes.byref(r))
+        if st != OK:
+            raise YjsError(st)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes)
+
+    def stats(self) -> Stats:
+        s = Stats()
+        lib().ygm_stats(self._ctx, ctypes.byref(s))
+        return s

@@ -1,0 +1,127 @@
+/*
+ * ygm.h -- C ABI of the MI355X batched Yjs update engine ("ygm" = Yjs GPU Merge).
+ *
+ * The drop-in boundary for Hocuspocus's persistence / sync hot path.  Plain
+ * pointers and sizes only (no torch, no HIP types in signatures).  Each entry
+ * point replaces a per-document yjs call that the reference makes one document
+ * at a time on the Node event loop:
+ *
+ *   ygm_merge_v1           <- Y.mergeUpdates(updates)                  (yjs Y@37704; the
+ *                             store path packages/extension-database/src/Database.ts:55-60
+ *                             persists Y.encodeStateAsUpdate(doc); the GPU extension persists
+ *                             mergeUpdates([snapshot, ...onChange updates]) instead,
+ *                             packages/server/src/Hocuspocus.ts:244-277,417-447)
+ *   ygm_diff_v1            <- Y.diffUpdate(update, stateVector)        (yjs Y@41210; the Step1 ->
+ *                             Step2 reply of packages/server/src/MessageReceiver.ts:137-155)
+ *   ygm_sv_from_update_v1  <- Y.encodeStateVectorFromUpdate(update)    (yjs Y@38304; the SV a
+ *                             server sends in SyncStep1, packages/server/src/OutgoingMessage.ts:93-99)
+ *
+ * Byte-for-byte identical to yjs 13.6.26 by default; YGM_F_COMPAT_135 selects
+ * the yjs 13.5.16 / lib0 0.2.42 behaviours.  A document whose
+ * content yjs would re-encode (non-canonical Any/JSON) is
+ * refused with YGM_ENONCANON instead of being silently copied.
+ *
+ * Error behaviour mirrors the reference: yjs throws per document; here the
+ * batch call succeeds and the failing document carries a non-zero status
+ * (the extension then rejects only that document's hook, Hocuspocus.ts:431-435).
+ */
+#ifndef YGM_H
+#define YGM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- per-document status codes ------------------------------------------ */
+#define YGM_OK 0
+#define YGM_EMALFORMED 1   /* yjs throws: truncated input, bad UTF-8, unknown content/Any tag, bad JSON */
+#define YGM_ERANGE 2       /* yjs throws "Integer out of Range": varuint > 2^53 */
+#define YGM_ENONCANON 3    /* yjs would re-encode content (non-canonical Any/JSON): refused, not copied */
+#define YGM_ESURROGATE 4   /* compat 13.5 only: lib0 0.2.42 throws writing a lone surrogate */
+#define YGM_EDEPTH 5       /* Any/JSON nesting deeper than YGM_MAX_DEPTH */
+#define YGM_ENOMEM 6
+#define YGM_EDEVICE 7      /* HIP error / device fault */
+#define YGM_EINVAL 8       /* bad call arguments */
+
+#define YGM_MAX_DEPTH 32
+
+/* ---- context flags -------------------------------------------------------- */
+#define YGM_F_COMPAT_135 1u   /* delete-set clients in first-seen order; lone surrogate -> error */
+#define YGM_F_FORCE_SEQ 2u    /* route every merge through the exact sequential kernel (testing) */
+
+typedef struct ygm_ctx ygm_ctx;
+
+/* Result of one batch call.  Owned by the context; valid until the next call
+ * on the same context or ygm_close.  Document d's output is
+ * data[off[d] .. off[d]+len[d]) when status[d] == YGM_OK.  Offsets are NOT
+ * monotone in d (documents handled by the sequential kernel are appended). */
+typedef struct {
+  const uint8_t *data;
+  const uint64_t *off;
+  const uint64_t *len;
+  const int32_t *status;
+  uint32_t n_docs;
+  uint64_t data_bytes;
+} ygm_result;
+
+typedef struct {
+  uint64_t calls, docs, updates;
+  uint64_t bytes_in, bytes_out;       /* algorithmic bytes */
+  uint64_t docs_fast, docs_seq;        /* documents per kernel class */
+  double kernel_ms, h2d_ms, d2h_ms;    /* cumulative, HIP-event timed */
+} ygm_stats_t;
+
+/* Opens the engine on HIP device `device` (one context per GPU; contexts are
+ * independent, not thread-safe: one batch in flight per context). */
+int ygm_open(int device, uint32_t flags, ygm_ctx **out);
+void ygm_close(ygm_ctx *ctx);
+
+/* ---- host-memory batch API (what the N-API addon / ctypes binding call) ---
+ * arena      concatenated V1 updates
+ * upd_off    n_upd+1 byte offsets into arena
+ * upd_doc    n_upd document ids, non-decreasing; updates of a document keep
+ *            their order (the order of yjs's `updates` array) */
+int ygm_merge_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *upd_off, const uint32_t *upd_doc,
+                 uint32_t n_upd, uint32_t n_docs, ygm_result *out);
+/* doc_off: n_docs+1 offsets of one update per document; sv_off: n_docs+1
+ * offsets of one encoded state vector per document in sv_arena. */
+int ygm_diff_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, const uint8_t *sv_arena,
+                const uint64_t *sv_off, uint32_t n_docs, ygm_result *out);
+int ygm_sv_from_update_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, uint32_t n_docs,
+                          ygm_result *out);
+
+/* ---- device-resident API (inputs already in HBM; used by bench.py) --------
+ * All pointers are device pointers.  doc_upd: n_docs+1 update-index offsets
+ * (document d owns updates doc_upd[d] .. doc_upd[d+1]).  Results stay on the
+ * device: the data/off/len/status pointers of the result point into context-owned device
+ * memory.  `stream` is a hipStream_t (NULL = the context's stream); the call
+ * is asynchronous except for one 8-byte read of the output size. */
+typedef struct {
+  uint8_t *data;
+  uint64_t *off;
+  uint64_t *len;
+  int32_t *status;
+  uint64_t data_bytes;
+} ygm_device_result;
+
+int ygm_merge_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_upd_off,
+                        const uint32_t *d_doc_upd, uint32_t n_upd, uint32_t n_docs, void *stream,
+                        ygm_device_result *out);
+int ygm_diff_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
+                       const uint8_t *d_sv_arena, const uint64_t *d_sv_off, uint32_t n_docs, void *stream,
+                       ygm_device_result *out);
+int ygm_sv_from_update_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes,
+                                 const uint64_t *d_doc_off, uint32_t n_docs, void *stream,
+                                 ygm_device_result *out);
+
+int ygm_stats(ygm_ctx *ctx, ygm_stats_t *out);
+const char *ygm_strerror(int code);
+const char *ygm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YGM_H */

@@ -53,8 +53,9 @@ def check_result(c, status, out):
 
 
 def ds_to_desc(update_hex):
-    """Rewrite an update's delete set into client-descending order (13.6.x writeDeleteSet)."""
-    from hocuspocus_amd.v1 import split_update, encode_ds
+    """Rewrites an output's delete set into client-descending order (yjs 13.6.x writeDeleteSet)."""
+    from v1util import ds_offset, encode_ds, read_ds
     b = bytes.fromhex(update_hex)
-    structs, ds = split_update(b)
-    return (structs + encode_ds(sorted(ds, key=lambda e: -e[0]))).hex()
+    p = ds_offset(b)
+    ds, _ = read_ds(b, p)
+    return (b[:p] + encode_ds(sorted(ds, key=lambda e: -e[0]))).hex()

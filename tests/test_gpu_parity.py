@@ -1,0 +1,225 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle and the
+yjs golden vectors.  One process, batched calls (each call = one kernel batch)."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from golden import case_inputs, check_result, load_yjs_vectors
+
+pytestmark = pytest.mark.gpu
+
+HEADER, CASES = load_yjs_vectors()
+THROWS = {1, 2, 4, 5}
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from hocuspocus_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def eng135():
+    from hocuspocus_amd import Engine
+    e = Engine(0, compat135=True)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def eng_seq():
+    from hocuspocus_amd import Engine
+    e = Engine(0, force_seq=True)
+    yield e
+    e.close()
+
+
+def same(oracle_res, gpu_res):
+    """statuses agree (any throw == any throw) and bytes agree when OK."""
+    so, bo = oracle_res
+    sg, bg = gpu_res
+    if so in THROWS:
+        return sg in THROWS
+    return so == sg and bo == bg
+
+
+def run_batch(e, op, cases):
+    if op == "merge":
+        return e.merge_updates_batch([case_inputs(c) for c in cases])
+    if op == "diff":
+        ins = [case_inputs(c) for c in cases]
+        return e.diff_update_batch([u for u, _ in ins], [s for _, s in ins])
+    return e.encode_state_vector_from_update_batch([case_inputs(c) for c in cases])
+
+
+@pytest.mark.parametrize("op", ["merge", "diff", "sv"])
+def test_golden_vectors_compat135(eng135, op):
+    cases = [c for c in CASES if c["op"] == op]
+    res = run_batch(eng135, op, cases)
+    bad = []
+    for c, (st, out) in zip(cases, res):
+        why = check_result(c, st, out)
+        if why:
+            bad.append((c["id"], c.get("note"), why))
+    assert not bad, f"{len(bad)} of {len(cases)} differ; first {bad[:3]}"
+
+
+@pytest.mark.parametrize("op", ["merge", "diff", "sv"])
+def test_golden_inputs_default_mode_vs_oracle(eng, op):
+    cases = [c for c in CASES if c["op"] == op]
+    res = run_batch(eng, op, cases)
+    bad = []
+    for c, g in zip(cases, res):
+        if op == "merge":
+            o = oracle.merge_updates(case_inputs(c))
+        elif op == "diff":
+            o = oracle.diff_update(*case_inputs(c))
+        else:
+            o = oracle.encode_state_vector_from_update(case_inputs(c))
+        if not same(o, g):
+            bad.append((c["id"], c.get("note"), o[0], g[0]))
+    assert not bad, f"{len(bad)} of {len(cases)} differ; first {bad[:5]}"
+
+
+def test_sequential_kernel_on_golden_merges(eng_seq):
+    cases = [c for c in CASES if c["op"] == "merge"]
+    res = run_batch(eng_seq, "merge", cases)
+    bad = []
+    for c, g in zip(cases, res):
+        o = oracle.merge_updates(case_inputs(c))
+        if not same(o, g):
+            bad.append((c["id"], c.get("note"), o[0], g[0]))
+    assert not bad, f"{len(bad)} of {len(cases)} differ; first {bad[:5]}"
+
+
+def _synth_docs(n_docs, n_upd, seed, del_pct=0, shuffle=False):
+    from tools import synth
+    arena, upd_off, doc_upd = synth.text_updates(n_docs, n_upd, seed=seed, del_pct=del_pct)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(n_docs)]
+    if shuffle:
+        rng = random.Random(seed)
+        for d in docs:
+            rng.shuffle(d)
+    return docs
+
+
+@pytest.mark.parametrize("del_pct,shuffle", [(0, False), (20, False), (20, True)])
+def test_synthetic_c2_merge_vs_oracle(eng, del_pct, shuffle):
+    docs = _synth_docs(600, 200, seed=5 + del_pct, del_pct=del_pct, shuffle=shuffle)
+    res = eng.merge_updates_batch(docs)
+    for d, us in enumerate(docs):
+        assert same(oracle.merge_updates(us), res[d]), d
+    st = eng.stats()
+    assert st.docs_seq == 0 or del_pct > 0  # insert-only C2 docs never need the sequential kernel
+
+
+def test_merge_with_duplicates_and_premerged(eng):
+    # overlap class: duplicated updates and overlapping pre-merged halves -> sequential kernel
+    rng = random.Random(9)
+    docs = _synth_docs(200, 60, seed=9, del_pct=10)
+    batch = []
+    for us in docs:
+        x = list(us)
+        x += rng.sample(us, 3)
+        rng.shuffle(x)
+        a = oracle.merge_updates(us[:40])[1]
+        b = oracle.merge_updates(us[20:])[1]
+        batch += [x, [a, b], [b, a] + us[:5]]
+    res = eng.merge_updates_batch(batch)
+    for i, us in enumerate(batch):
+        assert same(oracle.merge_updates(us), res[i]), i
+
+
+def test_synthetic_c4_sv_and_diff_vs_oracle(eng):
+    from tools import synth
+    arena, doc_off, sva, sv_off = synth.text_states(800, seed=21)
+    docs = synth.split(arena, doc_off)
+    svs = synth.split(sva, sv_off)
+    res = eng.encode_state_vector_from_update_batch(docs)
+    for d, u in enumerate(docs):
+        assert same(oracle.encode_state_vector_from_update(u), res[d]), d
+    res = eng.diff_update_batch(docs, svs)
+    for d, u in enumerate(docs):
+        assert same(oracle.diff_update(u, svs[d]), res[d]), d
+
+
+def test_fuzzed_inputs_vs_oracle(eng):
+    # truncations and byte flips of real inputs: error class and bytes must agree
+    rng = random.Random(1234)
+    merges, diffs, svs = [], [], []
+    pool = [c for c in CASES if c["out"] is not None]
+    for _ in range(3000):
+        c = rng.choice(pool)
+        if c["op"] == "merge":
+            us = [bytearray(u) for u in case_inputs(c)]
+            if len(us) < 2:
+                continue
+            u = rng.choice(us)
+            if u and rng.random() < 0.5:
+                u[rng.randrange(len(u))] = rng.randrange(256)
+            elif u:
+                del u[rng.randrange(len(u)):]
+            merges.append([bytes(x) for x in us])
+        elif c["op"] == "diff":
+            u, s = case_inputs(c)
+            u = bytearray(u)
+            if u:
+                u[rng.randrange(len(u))] ^= 1 << rng.randrange(8)
+            diffs.append((bytes(u), s))
+        else:
+            u = bytearray(case_inputs(c))
+            if u:
+                del u[rng.randrange(len(u)):]
+            svs.append(bytes(u))
+    res = eng.merge_updates_batch(merges)
+    for us, g in zip(merges, res):
+        assert same(oracle.merge_updates(us), g), [u.hex() for u in us]
+    res = eng.diff_update_batch([u for u, _ in diffs], [s for _, s in diffs])
+    for (u, s), g in zip(diffs, res):
+        assert same(oracle.diff_update(u, s), g), (u.hex(), s.hex())
+    res = eng.encode_state_vector_from_update_batch(svs)
+    for u, g in zip(svs, res):
+        assert same(oracle.encode_state_vector_from_update(u), g), u.hex()
+
+
+def test_empty_and_edge_batches(eng):
+    assert eng.merge_updates_batch([]) == []
+    assert eng.merge_updates_batch([[]]) == [(0, bytes.fromhex("0000"))]
+    one = bytes.fromhex("01010500040101740568656c6c6f00")
+    assert eng.merge_updates_batch([[one]]) == [(0, one)]
+    assert eng.merge_updates_batch([[b"\x01"]]) == [(0, b"\x01")]  # single input: returned as-is
+    r = eng.merge_updates_batch([[b"\x01", b"\x00\x00"], [one, one]])
+    assert r[0][0] in THROWS and r[1] == (0, one)
+
+
+def test_full_size_c2_properties(eng):
+    # BASELINE configs[1] size (10k docs x 200 updates): size-independent properties
+    from tools import synth
+    arena, upd_off, doc_upd = synth.text_updates(10000, 200, seed=1)
+    res = eng.merge_packed(arena, upd_off, doc_upd[:-1].repeat(np.diff(doc_upd)) if False else
+                           np.repeat(np.arange(10000, dtype=np.uint32), np.diff(doc_upd).astype(np.int64)), 10000)
+    assert all(st == 0 for st, _ in res)
+    merged = [m for _, m in res]
+    # (1) diff against an empty state vector reproduces a canonical merged update
+    d = eng.diff_update_batch(merged, [b"\x00"] * len(merged))
+    assert all(x == (0, m) for x, m in zip(d, merged))
+    # (2) every insert is present: SV clocks sum to the number of updates
+    svs = eng.encode_state_vector_from_update_batch(merged)
+    from v1util import rd_vu
+    for st, sv in svs[:2000]:
+        n, p = rd_vu(sv, 0)
+        tot = 0
+        for _ in range(n):
+            _, p = rd_vu(sv, p)
+            k, p = rd_vu(sv, p)
+            tot += k
+        assert tot == 200
+    # (3) spot-check against the oracle
+    ups = synth.split(arena, upd_off)
+    for dd in range(0, 10000, 97):
+        assert (0, merged[dd]) == oracle.merge_updates(ups[doc_upd[dd]:doc_upd[dd + 1]])

@@ -1,0 +1,60 @@
+"""Seeded synthetic Yjs update-v1 corpora (ctypes over tools/libsynth.so).
+
+Bench / test infrastructure: the GPU box has no yjs, so corpora are emitted as
+V1 bytes directly.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(_HERE, "libsynth.so")
+        if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(os.path.join(_HERE, "synth.c")):
+            subprocess.check_call(["make", "-s", "-C", _HERE])
+        L = ctypes.CDLL(path)
+        P = ctypes.c_void_p
+        L.synth_text_updates.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P, P, P]
+        L.synth_text_updates.restype = ctypes.c_size_t
+        L.synth_text_states.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        P, P, P, P, ctypes.POINTER(ctypes.c_size_t)]
+        L.synth_text_states.restype = ctypes.c_size_t
+        _lib = L
+    return _lib
+
+
+def text_updates(n_docs, n_updates=200, min_clients=1, max_clients=4, del_pct=0, seed=1):
+    """Config C2: returns (arena uint8, upd_off uint64[n_upd+1], doc_upd uint32[n_docs+1])."""
+    n_upd = n_docs * n_updates
+    buf = np.empty(n_upd * 40 + 64, dtype=np.uint8)
+    upd_off = np.empty(n_upd + 1, dtype=np.uint64)
+    doc_upd = np.empty(n_docs + 1, dtype=np.uint32)
+    n = lib().synth_text_updates(seed, n_docs, n_updates, min_clients, max_clients, del_pct,
+                                 buf.ctypes.data, upd_off.ctypes.data, doc_upd.ctypes.data)
+    return buf[:n].copy(), upd_off, doc_upd
+
+
+def text_states(n_docs, min_ops=40, max_ops=400, min_clients=1, max_clients=16, seed=1):
+    """Config C4: returns (arena, doc_off[n_docs+1], sv_arena, sv_off[n_docs+1])."""
+    buf = np.empty(n_docs * max_ops * 40 + 64, dtype=np.uint8)
+    doc_off = np.empty(n_docs + 1, dtype=np.uint64)
+    sv = np.empty(n_docs * (1 + max_clients * 16) + 64, dtype=np.uint8)
+    sv_off = np.empty(n_docs + 1, dtype=np.uint64)
+    svb = ctypes.c_size_t()
+    n = lib().synth_text_states(seed, n_docs, min_ops, max_ops, min_clients, max_clients, buf.ctypes.data, doc_off.ctypes.data,
+                                sv.ctypes.data, sv_off.ctypes.data, ctypes.byref(svb))
+    return buf[:n].copy(), doc_off, sv[:svb.value].copy(), sv_off
+
+
+def split(arena, off):
+    """bytes objects of each [off[i], off[i+1]) slice."""
+    a = arena.tobytes()
+    o = [int(x) for x in off]
+    return [a[o[i]:o[i + 1]] for i in range(len(o) - 1)]

@@ -1,0 +1,218 @@
+"""Benchmark: batched Y.mergeUpdates on MI355X (BASELINE.json metric, config C2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+One step = one batched mergeUpdates over the whole per-GPU workload (10 000
+documents x 200 single-character Y.Text insert updates from 1-4 clients,
+SURVEY.md §8d config C2, BASELINE.json configs[1]) with the inputs already
+resident in HBM: ``ygm_merge_v1_device`` = the fast-path kernel launch, the
+per-document look-back placement and the 64-byte meta read-back.  For N > 1 the
+driver starts one process per GPU (torchrun); every rank merges its own shard
+of documents (documents are independent, partitioned by name hash, weak
+scaling) and the time is the max over ranks.  RCCL carries only the timing
+reduction / stats gather, never data.
+
+Algorithmic bytes: merge = sum(|inputs|) + |output| per document.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+N_DOCS, N_UPDATES = 10000, 200
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--docs", type=int, default=N_DOCS)
+    ap.add_argument("--updates", type=int, default=N_UPDATES)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(arena, upd_off, doc_upd, budget_s):
+    """The CPU oracle (oracle/yjs_oracle.c, a literal port of yjs mergeUpdates) on a bounded
+    sample of the same workload, one thread per host core."""
+    import oracle
+    from tools import synth
+    ups = synth.split(arena, upd_off)
+    n_docs = len(doc_upd) - 1
+    cores = min(16, os.cpu_count() or 1)
+    # calibrate the sample on one thread
+    t0 = time.perf_counter(); d = 0; nbytes = 0
+    while time.perf_counter() - t0 < 0.5 and d < n_docs:
+        us = ups[doc_upd[d]:doc_upd[d + 1]]
+        st, out = oracle.merge_updates(us)
+        nbytes += sum(map(len, us)) + len(out)
+        d += 1
+    per_doc = (time.perf_counter() - t0) / max(d, 1)
+    sample = int(min(n_docs, max(cores, budget_s * cores / max(per_doc, 1e-9))))
+    docs = [ups[doc_upd[i]:doc_upd[i + 1]] for i in range(sample)]
+    chunks = [docs[i::cores] for i in range(cores)]
+    algo = [0] * cores
+
+    def work(i):
+        b = 0
+        for us in chunks[i]:
+            st, out = oracle.merge_updates(us)
+            b += sum(map(len, us)) + len(out)
+        algo[i] = b
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        list(ex.map(work, range(cores)))
+    dt = time.perf_counter() - t0
+    return {"value": round(sum(algo) / dt / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port",
+            "docs_per_s": round(sample / dt, 1),
+            "sample": f"{sample} of the {n_docs} C2 documents, oracle/yjs_oracle.c mergeUpdates "
+                      f"(literal yjs restatement), {cores} threads, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from hocuspocus_amd import Engine
+    from tools import synth
+
+    # ---- this rank's shard: documents whose name hash maps to this rank (seeded per rank)
+    arena, upd_off, doc_upd = synth.text_updates(args.docs, args.updates, seed=1000 + rank)
+    n_upd = int(doc_upd[-1])
+    dev = torch.device("cuda", local)
+    d_arena = torch.from_numpy(np.concatenate([arena, np.zeros(64, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(upd_off.view(np.int64)).to(dev)
+    d_doc = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    eng = Engine(local)
+
+    def step():
+        return eng.merge_device(d_arena.data_ptr(), len(arena), d_off.data_ptr(), d_doc.data_ptr(), n_upd, args.docs,
+                                stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        r = step()
+    torch.cuda.synchronize()
+    s0 = eng.stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    s1 = eng.stats()
+
+    out_bytes = int(r.data_bytes)
+    algo_bytes = len(arena) + out_bytes              # per step, this rank
+    kernel_ms = (s1.kernel_ms - s0.kernel_ms) / args.steps
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(algo_bytes), float(args.docs), float(s1.docs_seq - s0.docs_seq)], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    dt = float(t.item())
+    all_bytes, all_docs = float(tot[0].item()), float(tot[1].item())
+
+    # ---- parity spot-check of the timed outputs (rank 0 sample vs the CPU oracle)
+    parity = None
+    if rank == 0:
+        import oracle
+        n = args.docs
+        torch.cuda.synchronize()
+        off = _d2h(r.off, n * 8).view(np.uint64)
+        ln = _d2h(r.len, n * 8).view(np.uint64)
+        st = _d2h(r.status, n * 4).view(np.int32)
+        hdata = _d2h(r.data, out_bytes).tobytes()
+        ups = synth.split(arena, upd_off)
+        checked = 0
+        for dd in range(0, n, max(1, n // 400)):
+            exp = oracle.merge_updates(ups[doc_upd[dd]:doc_upd[dd + 1]])
+            got = (int(st[dd]), hdata[int(off[dd]):int(off[dd]) + int(ln[dd])])
+            assert exp == got, f"parity failure on document {dd}"
+            checked += 1
+        assert (st == 0).all()
+        parity = f"bit-exact vs oracle on {checked} sampled docs; all {n} statuses OK"
+
+    if rank == 0:
+        value = all_bytes * args.steps / dt / 1e6
+        achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
+        line = {
+            "metric": "merged update MB/s (bit-exact vs yjs mergeUpdates)",
+            "value": round(value, 3),
+            "unit": "MB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded V1 updates, tools/synth.c; SURVEY.md §8d C2)",
+            "config": {"workload": f"C2: {args.docs} docs x {args.updates} single-char Y.Text insert updates per GPU, "
+                                   "1-4 uint32 clients, batched Y.mergeUpdates, inputs resident in HBM",
+                       "docs_per_gpu": args.docs, "updates_per_gpu": n_upd, "bytes_in_per_gpu": len(arena),
+                       "bytes_out_per_gpu": out_bytes, "parallelism": f"doc-sharded x{world}"},
+            "docs_per_s": round(all_docs * args.steps / dt, 1),
+            "roofline": {"bound": "hbm", "kernel": "k_merge_fast",
+                         "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 5) if achieved else None,
+                         "kernel_ms": round(kernel_ms, 4), "traffic": _pmc_traffic()},
+            "parity": parity,
+            "seq_kernel_docs": float(tot[2].item()),
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(arena, upd_off, doc_upd, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def _d2h(src, n):
+    """Copies n bytes of engine-owned device memory to a host numpy array."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    out = np.empty(max(n, 1), np.uint8)
+    if n:
+        assert hip.hipMemcpy(out.ctypes.data, src, n, 2) == 0  # hipMemcpyDeviceToHost
+    return out[:n]
+
+
+def _pmc_traffic():
+    """HBM bytes per k_merge_fast launch from the committed rocprofv3 PMC pass (profiles/), if any."""
+    p = os.path.join(ROOT, "profiles", "pmc_merge_fast.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p)).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+if __name__ == "__main__":
+    main()

@@ -392,7 +392,8 @@ YDEV_NI int json_check(const uint8_t* s, uint32_t n, bool& nc) {
 // One parsed struct (lazyStructReaderGenerator, Y@36564).
 struct SInfo {
   uint8_t kind, info, ref;
-  bool nc;           // content would be re-encoded by yjs
+  bool nc;           // content would be re-encoded by yjs (non-canonical Any/JSON): refused
+  bool renc;         // content holds non-minimal varuints: re-encoded on output (as yjs does)
   uint64_t len;      // clock length
   uint32_t start;    // position of the info byte
   uint32_t cstart;   // position of the content
@@ -436,9 +437,7 @@ YDEV_NI uint64_t read_content(Cur& c, uint8_t ref, bool& nc, uint32_t flags) {
       return 1;
     }
     case 7: {                                                        // ContentType
-      const uint32_t p0 = c.pos;
       const uint64_t tr = c.vu(); if (c.err) return 1;
-      if (c.pos - p0 > 1) nc = true;  // typeRef re-encoded minimal by the writer
       if (tr > 6) { c.fail(ST_MALFORMED); return 1; }
       if (tr == 3 || tr == 5) { uint32_t l; const uint32_t s = c.buf(l); if (!c.err && utf8_u16(c.p + s, l) < 0) c.fail(ST_MALFORMED); }
       return 1;
@@ -477,7 +476,7 @@ YDEV_NI uint64_t read_content(Cur& c, uint8_t ref, bool& nc, uint32_t flags) {
 // Parses the struct at c.pos.  Header varuints are re-encoded on output, so
 // only content varuints count toward `nc`.
 YDEV_NI void read_struct(Cur& c, SInfo& s, uint32_t flags) {
-  s.start = c.pos; s.nc = false; s.ref = 0;
+  s.start = c.pos; s.nc = false; s.renc = false; s.ref = 0;
   const uint8_t info = c.u8();
   s.info = info;
   if (c.err) return;
@@ -498,7 +497,7 @@ YDEV_NI void read_struct(Cur& c, SInfo& s, uint32_t flags) {
   const int nm0 = c.nm; c.nm = 0;
   bool nc = false;
   s.len = read_content(c, s.ref, nc, flags);
-  if (c.nm) nc = true;
+  if (c.nm) s.renc = true;  // Any values track their own non-minimal varuints (-> nc)
   c.nm = nm0;
   s.nc = nc;
   s.end = c.pos;
@@ -533,7 +532,7 @@ YDEV uint32_t u16_to_byte(const uint8_t* s, uint32_t n, uint64_t off, bool& mid)
 // (U+FFFD in 13.6 / throw in 13.5 compat).  Returns ST_OK or an error.
 YDEV_NI int write_content(Out& o, const uint8_t* base, const SInfo& s, uint64_t off, bool splice, uint32_t flags) {
   Cur c{base, s.cstart, s.end, 0, 0};
-  if (off == 0) { o.copy(base + s.cstart, s.end - s.cstart); return ST_OK; }
+  if (off == 0 && !s.renc) { o.copy(base + s.cstart, s.end - s.cstart); return ST_OK; }
   switch (s.ref) {
     case 1: { const uint64_t n = c.vu(); o.vu(n - off); return ST_OK; }
     case 2: case 8: {
@@ -541,14 +540,19 @@ YDEV_NI int write_content(Out& o, const uint8_t* base, const SInfo& s, uint64_t 
       o.vu(n - off);
       for (uint64_t k = 0; k < n && !c.err; k++) {
         const uint32_t a = c.pos;
-        if (s.ref == 2) { uint32_t l; c.buf(l); } else any_skip(c);
-        if (k >= off) o.copy(base + a, c.pos - a);
+        if (s.ref == 2) {
+          uint32_t l; const uint32_t st = c.buf(l);
+          if (k >= off) { o.vu(l); o.copy(base + st, l); }
+        } else {
+          any_skip(c);
+          if (k >= off) o.copy(base + a, c.pos - a);
+        }
       }
       return ST_OK;
     }
     case 4: {
       uint32_t l; const uint32_t st = c.buf(l);
-      bool mid; const uint32_t b = u16_to_byte(base + st, l, off, mid);
+      bool mid; const uint32_t b = off ? u16_to_byte(base + st, l, off, mid) : (mid = false, 0u);
       if (mid) {
         if (!splice && (flags & F_COMPAT_135)) return ST_SURROGATE;
         o.vu((uint64_t)(l - b) + 3); o.b(0xEF); o.b(0xBF); o.b(0xBD);
@@ -556,7 +560,23 @@ YDEV_NI int write_content(Out& o, const uint8_t* base, const SInfo& s, uint64_t 
       o.copy(base + st + b, l - b);
       return ST_OK;
     }
-    default: return ST_MALFORMED;  // length-1 contents are never cut
+    case 3: case 5: { uint32_t l; const uint32_t st = c.buf(l); o.vu(l); o.copy(base + st, l); return ST_OK; }
+    case 6: {
+      uint32_t l; uint32_t st = c.buf(l); o.vu(l); o.copy(base + st, l);
+      st = c.buf(l); o.vu(l); o.copy(base + st, l);
+      return ST_OK;
+    }
+    case 7: {
+      const uint64_t tr = c.vu(); o.vu(tr);
+      if (tr == 3 || tr == 5) { uint32_t l; const uint32_t st = c.buf(l); o.vu(l); o.copy(base + st, l); }
+      return ST_OK;
+    }
+    case 9: {
+      uint32_t l; const uint32_t st = c.buf(l); o.vu(l); o.copy(base + st, l);
+      o.copy(base + c.pos, s.end - c.pos);
+      return ST_OK;
+    }
+    default: return ST_MALFORMED;
   }
 }
 

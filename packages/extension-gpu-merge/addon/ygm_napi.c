@@ -1,0 +1,275 @@
+/*
+ * ygm_napi.c -- N-API addon: the thin extern "C" bridge between Node and libygm.so
+ * (include/ygm.h).  Every batch runs on a libuv worker thread (napi_async_work),
+ * so the Hocuspocus event loop never blocks on the GPU; results come back as a
+ * Promise of { status: Int32Array, outputs: (Buffer|null)[] }.
+ *
+ * JS surface (see ../index.d.ts):
+ *   open(device, flags)                                  -> handle
+ *   mergeMany(h, arena:Buffer, lens:Uint32Array, docs:Uint32Array, nDocs)  -> Promise
+ *   diffMany(h, arena, lens, svArena, svLens)           -> Promise
+ *   svMany(h, arena, lens)                              -> Promise
+ *   stats(h) -> object ; close(h) ; strerror(code) -> string
+ * Input bytes are copied into native memory before the worker runs (JS owns its
+ * typed arrays; SURVEY.md §8b "Ownership"); outputs are fresh Buffers.
+ */
+#include <node_api.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../../include/ygm.h"
+
+#define NAPI_CALL(env, call) do { if ((call) != napi_ok) { napi_throw_error((env), NULL, "N-API call failed: " #call); return NULL; } } while (0)
+
+typedef struct {
+  ygm_ctx *ctx;
+  int busy;
+} Handle;
+
+typedef struct {
+  int op; /* 0 merge, 1 diff, 2 sv */
+  Handle *h;
+  uint8_t *arena; uint64_t *off; uint32_t *docs; uint32_t n_upd, n_docs;
+  uint8_t *sv; uint64_t *sv_off;
+  int rc;
+  /* copied results */
+  uint8_t *data; uint64_t *roff, *rlen; int32_t *status; uint32_t rn;
+  napi_deferred deferred;
+  napi_async_work work;
+} Job;
+
+static void handle_finalize(napi_env env, void *data, void *hint) {
+  (void)env; (void)hint;
+  Handle *h = (Handle *)data;
+  if (h->ctx) ygm_close(h->ctx);
+  free(h);
+}
+
+static Handle *get_handle(napi_env env, napi_value v) {
+  Handle *h = NULL;
+  if (napi_get_value_external(env, v, (void **)&h) != napi_ok || !h || !h->ctx) {
+    napi_throw_error(env, NULL, "ygm: closed or invalid engine handle");
+    return NULL;
+  }
+  return h;
+}
+
+static napi_value js_open(napi_env env, napi_callback_info info) {
+  size_t argc = 2; napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int32_t device = 0; uint32_t flags = 0;
+  if (argc > 0) napi_get_value_int32(env, argv[0], &device);
+  if (argc > 1) napi_get_value_uint32(env, argv[1], &flags);
+  Handle *h = (Handle *)calloc(1, sizeof(Handle));
+  int rc = ygm_open(device, flags, &h->ctx);
+  if (rc != YGM_OK) { free(h); napi_throw_error(env, "YGM_EOPEN", ygm_strerror(rc)); return NULL; }
+  napi_value ext;
+  NAPI_CALL(env, napi_create_external(env, h, handle_finalize, NULL, &ext));
+  return ext;
+}
+
+static napi_value js_close(napi_env env, napi_callback_info info) {
+  size_t argc = 1; napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  Handle *h = NULL;
+  if (napi_get_value_external(env, argv[0], (void **)&h) == napi_ok && h && h->ctx && !h->busy) { ygm_close(h->ctx); h->ctx = NULL; }
+  return NULL;
+}
+
+static napi_value js_strerror(napi_env env, napi_callback_info info) {
+  size_t argc = 1; napi_value argv[1]; int32_t code = 0;
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  napi_get_value_int32(env, argv[0], &code);
+  napi_value s;
+  NAPI_CALL(env, napi_create_string_utf8(env, ygm_strerror(code), NAPI_AUTO_LENGTH, &s));
+  return s;
+}
+
+static napi_value js_stats(napi_env env, napi_callback_info info) {
+  size_t argc = 1; napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  Handle *h = get_handle(env, argv[0]);
+  if (!h) return NULL;
+  ygm_stats_t s; ygm_stats(h->ctx, &s);
+  napi_value o, v;
+  NAPI_CALL(env, napi_create_object(env, &o));
+#define SETN(name, val) NAPI_CALL(env, napi_create_double(env, (double)(val), &v)); NAPI_CALL(env, napi_set_named_property(env, o, name, v));
+  SETN("calls", s.calls) SETN("docs", s.docs) SETN("updates", s.updates) SETN("bytesIn", s.bytes_in) SETN("bytesOut", s.bytes_out)
+  SETN("docsFast", s.docs_fast) SETN("docsSeq", s.docs_seq) SETN("kernelMs", s.kernel_ms) SETN("h2dMs", s.h2d_ms) SETN("d2hMs", s.d2h_ms)
+#undef SETN
+  return o;
+}
+
+/* copies a Buffer / TypedArray argument into malloc'd memory */
+static int get_bytes(napi_env env, napi_value v, void **out, size_t *len) {
+  bool is_ta = false, is_buf = false; void *data = NULL; size_t n = 0;
+  napi_is_typedarray(env, v, &is_ta);
+  napi_is_buffer(env, v, &is_buf);
+  if (is_buf) { if (napi_get_buffer_info(env, v, &data, &n) != napi_ok) return -1; }
+  else if (is_ta) {
+    napi_typedarray_type t; size_t cnt; napi_value ab; size_t boff;
+    if (napi_get_typedarray_info(env, v, &t, &cnt, &data, &ab, &boff) != napi_ok) return -1;
+    size_t el = (t == napi_uint32_array || t == napi_int32_array || t == napi_float32_array) ? 4 : (t == napi_float64_array || t == napi_bigint64_array || t == napi_biguint64_array) ? 8 : (t == napi_uint16_array || t == napi_int16_array) ? 2 : 1;
+    n = cnt * el;
+  } else return -1;
+  *out = malloc(n ? n : 1);
+  if (!*out) return -1;
+  if (n) memcpy(*out, data, n);
+  *len = n;
+  return 0;
+}
+
+static uint64_t *lens_to_off(const uint32_t *lens, uint32_t n) {
+  uint64_t *off = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+  off[0] = 0;
+  for (uint32_t i = 0; i < n; i++) off[i + 1] = off[i] + lens[i];
+  return off;
+}
+
+static void job_execute(napi_env env, void *data) {
+  (void)env;
+  Job *j = (Job *)data;
+  ygm_result r; memset(&r, 0, sizeof r);
+  if (j->op == 0) j->rc = ygm_merge_v1(j->h->ctx, j->arena, j->off, j->docs, j->n_upd, j->n_docs, &r);
+  else if (j->op == 1) j->rc = ygm_diff_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
+  else j->rc = ygm_sv_from_update_v1(j->h->ctx, j->arena, j->off, j->n_docs, &r);
+  if (j->rc != YGM_OK) return;
+  /* results are context-owned: copy out before the next batch may reuse them */
+  j->rn = r.n_docs;
+  j->data = (uint8_t *)malloc(r.data_bytes ? r.data_bytes : 1);
+  j->roff = (uint64_t *)malloc(sizeof(uint64_t) * (r.n_docs + 1));
+  j->rlen = (uint64_t *)malloc(sizeof(uint64_t) * (r.n_docs + 1));
+  j->status = (int32_t *)malloc(sizeof(int32_t) * (r.n_docs + 1));
+  if (r.data_bytes) memcpy(j->data, r.data, r.data_bytes);
+  if (r.n_docs) {
+    memcpy(j->roff, r.off, sizeof(uint64_t) * r.n_docs);
+    memcpy(j->rlen, r.len, sizeof(uint64_t) * r.n_docs);
+    memcpy(j->status, r.status, sizeof(int32_t) * r.n_docs);
+  }
+}
+
+static void job_free(Job *j) {
+  free(j->arena); free(j->off); free(j->docs); free(j->sv); free(j->sv_off);
+  free(j->data); free(j->roff); free(j->rlen); free(j->status);
+  free(j);
+}
+
+static void job_complete(napi_env env, napi_status st, void *data) {
+  Job *j = (Job *)data;
+  j->h->busy = 0;
+  napi_value result = NULL, err = NULL;
+  if (st != napi_ok || j->rc != YGM_OK) {
+    napi_value msg, code;
+    napi_create_string_utf8(env, ygm_strerror(st != napi_ok ? YGM_EINVAL : j->rc), NAPI_AUTO_LENGTH, &msg);
+    napi_create_string_utf8(env, "YGM_EBATCH", NAPI_AUTO_LENGTH, &code);
+    napi_create_error(env, code, msg, &err);
+    napi_reject_deferred(env, j->deferred, err);
+  } else {
+    napi_value status_ab, status_arr, outs;
+    void *sp = NULL;
+    napi_create_arraybuffer(env, sizeof(int32_t) * j->rn, &sp, &status_ab);
+    if (j->rn) memcpy(sp, j->status, sizeof(int32_t) * j->rn);
+    napi_create_typedarray(env, napi_int32_array, j->rn, status_ab, 0, &status_arr);
+    napi_create_array_with_length(env, j->rn, &outs);
+    for (uint32_t d = 0; d < j->rn; d++) {
+      napi_value b;
+      if (j->status[d] == YGM_OK) napi_create_buffer_copy(env, j->rlen[d], j->data + j->roff[d], NULL, &b);
+      else napi_get_null(env, &b);
+      napi_set_element(env, outs, d, b);
+    }
+    napi_create_object(env, &result);
+    napi_set_named_property(env, result, "status", status_arr);
+    napi_set_named_property(env, result, "outputs", outs);
+    napi_resolve_deferred(env, j->deferred, result);
+  }
+  napi_delete_async_work(env, j->work);
+  job_free(j);
+}
+
+static napi_value submit(napi_env env, Job *j, const char *name) {
+  napi_value promise, res_name;
+  if (j->h->busy) { job_free(j); napi_throw_error(env, "YGM_EBUSY", "ygm: one batch in flight per engine handle"); return NULL; }
+  NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
+  NAPI_CALL(env, napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res_name));
+  NAPI_CALL(env, napi_create_async_work(env, NULL, res_name, job_execute, job_complete, j, &j->work));
+  j->h->busy = 1;
+  NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+/* mergeMany(h, arena, lens, docs, nDocs) */
+static napi_value js_merge(napi_env env, napi_callback_info info) {
+  size_t argc = 5; napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 5) { napi_throw_type_error(env, NULL, "mergeMany(handle, arena, lens, docs, nDocs)"); return NULL; }
+  Handle *h = get_handle(env, argv[0]);
+  if (!h) return NULL;
+  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = 0; j->h = h;
+  size_t an, ln, dn; void *lens = NULL;
+  if (get_bytes(env, argv[1], (void **)&j->arena, &an) || get_bytes(env, argv[2], &lens, &ln) || get_bytes(env, argv[3], (void **)&j->docs, &dn)) {
+    free(lens); job_free(j); napi_throw_type_error(env, NULL, "mergeMany: expected Buffer / Uint32Array arguments"); return NULL;
+  }
+  napi_get_value_uint32(env, argv[4], &j->n_docs);
+  j->n_upd = (uint32_t)(ln / 4);
+  if (dn / 4 != j->n_upd) { free(lens); job_free(j); napi_throw_range_error(env, NULL, "mergeMany: lens/docs length mismatch"); return NULL; }
+  j->off = lens_to_off((const uint32_t *)lens, j->n_upd);
+  free(lens);
+  if (j->off[j->n_upd] != an) { job_free(j); napi_throw_range_error(env, NULL, "mergeMany: sum(lens) != arena length"); return NULL; }
+  return submit(env, j, "ygm.mergeMany");
+}
+
+/* diffMany(h, arena, lens, svArena, svLens) */
+static napi_value js_diff(napi_env env, napi_callback_info info) {
+  size_t argc = 5; napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 5) { napi_throw_type_error(env, NULL, "diffMany(handle, arena, lens, svArena, svLens)"); return NULL; }
+  Handle *h = get_handle(env, argv[0]);
+  if (!h) return NULL;
+  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = 1; j->h = h;
+  size_t an, ln, sn, sln; void *lens = NULL, *slens = NULL;
+  if (get_bytes(env, argv[1], (void **)&j->arena, &an) || get_bytes(env, argv[2], &lens, &ln) || get_bytes(env, argv[3], (void **)&j->sv, &sn) ||
+      get_bytes(env, argv[4], &slens, &sln) || ln != sln) {
+    free(lens); free(slens); job_free(j); napi_throw_type_error(env, NULL, "diffMany: bad arguments"); return NULL;
+  }
+  j->n_docs = (uint32_t)(ln / 4);
+  j->off = lens_to_off((const uint32_t *)lens, j->n_docs);
+  j->sv_off = lens_to_off((const uint32_t *)slens, j->n_docs);
+  free(lens); free(slens);
+  if (j->off[j->n_docs] != an || j->sv_off[j->n_docs] != sn) { job_free(j); napi_throw_range_error(env, NULL, "diffMany: lengths do not match arenas"); return NULL; }
+  return submit(env, j, "ygm.diffMany");
+}
+
+/* svMany(h, arena, lens) */
+static napi_value js_sv(napi_env env, napi_callback_info info) {
+  size_t argc = 3; napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 3) { napi_throw_type_error(env, NULL, "svMany(handle, arena, lens)"); return NULL; }
+  Handle *h = get_handle(env, argv[0]);
+  if (!h) return NULL;
+  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = 2; j->h = h;
+  size_t an, ln; void *lens = NULL;
+  if (get_bytes(env, argv[1], (void **)&j->arena, &an) || get_bytes(env, argv[2], &lens, &ln)) {
+    free(lens); job_free(j); napi_throw_type_error(env, NULL, "svMany: bad arguments"); return NULL;
+  }
+  j->n_docs = (uint32_t)(ln / 4);
+  j->off = lens_to_off((const uint32_t *)lens, j->n_docs);
+  free(lens);
+  if (j->off[j->n_docs] != an) { job_free(j); napi_throw_range_error(env, NULL, "svMany: sum(lens) != arena length"); return NULL; }
+  return submit(env, j, "ygm.svMany");
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+  napi_property_descriptor d[] = {
+    { "open", NULL, js_open, NULL, NULL, NULL, napi_default, NULL },
+    { "close", NULL, js_close, NULL, NULL, NULL, napi_default, NULL },
+    { "mergeMany", NULL, js_merge, NULL, NULL, NULL, napi_default, NULL },
+    { "diffMany", NULL, js_diff, NULL, NULL, NULL, napi_default, NULL },
+    { "svMany", NULL, js_sv, NULL, NULL, NULL, napi_default, NULL },
+    { "stats", NULL, js_stats, NULL, NULL, NULL, napi_default, NULL },
+    { "strerror", NULL, js_strerror, NULL, NULL, NULL, napi_default, NULL },
+  };
+  napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

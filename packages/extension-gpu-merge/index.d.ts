@@ -1,0 +1,50 @@
+// Type declarations for @hocuspocus/extension-gpu-merge (see src/index.js).
+import type { Extension, fetchPayload, storePayload, onLoadDocumentPayload, afterLoadDocumentPayload,
+  onChangePayload, onStoreDocumentPayload, afterUnloadDocumentPayload } from '@hocuspocus/server'
+
+export declare class YgmError extends Error {
+  code: 'EMALFORMED' | 'ERANGE' | 'ENONCANON' | 'ESURROGATE' | 'EDEPTH' | 'ENOMEM' | 'EDEVICE' | 'EINVAL' | string
+  status: number
+}
+
+export interface GpuEngineOptions { device?: number; compat135?: boolean; batchWindowMs?: number; maxBatchDocs?: number }
+
+export declare class GpuEngine {
+  constructor (opts?: GpuEngineOptions)
+  mergeUpdates (updates: Uint8Array[]): Promise<Uint8Array>
+  diffUpdate (update: Uint8Array, stateVector: Uint8Array): Promise<Uint8Array>
+  encodeStateVectorFromUpdate (update: Uint8Array): Promise<Uint8Array>
+  mergeMany (docs: Uint8Array[][]): Promise<(Uint8Array | YgmError)[]>
+  diffMany (states: Uint8Array[], svs: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  stateVectorsMany (states: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  stats (): Record<string, number>
+  close (): void
+}
+
+export declare class DocumentStore {
+  fetchMany (payloads: fetchPayload[]): Promise<(Uint8Array | Uint8Array[] | null)[]>
+  storeMany (entries: { payload: onStoreDocumentPayload; state: Buffer }[]): Promise<void>
+  static fromDatabase (config: { fetch?: (p: fetchPayload) => Promise<Uint8Array | Uint8Array[] | null>; store?: (p: storePayload) => Promise<void> }): DocumentStore
+}
+
+export interface GpuMergeConfiguration extends GpuEngineOptions {
+  /** a batched DocumentStore, or the DatabaseConfiguration.store function (Database.ts:19) */
+  store?: DocumentStore | ((p: storePayload) => Promise<void>)
+  fetch?: (p: fetchPayload) => Promise<Uint8Array | Uint8Array[] | null>
+  priority?: number
+  engine?: GpuEngine
+  Y?: any
+}
+
+export declare class GpuMerge implements Extension {
+  extensionName: string
+  priority: number
+  constructor (configuration?: GpuMergeConfiguration)
+  onConfigure (): Promise<void>
+  onLoadDocument (data: onLoadDocumentPayload): Promise<void>
+  afterLoadDocument (data: afterLoadDocumentPayload): Promise<void>
+  onChange (data: onChangePayload): Promise<void>
+  onStoreDocument (data: onStoreDocumentPayload): Promise<void>
+  afterUnloadDocument (data: afterUnloadDocumentPayload): Promise<void>
+  onDestroy (): Promise<void>
+}

@@ -1,0 +1,140 @@
+'use strict'
+/**
+ * GpuEngine -- Promise API over the N-API addon (addon/ygm_napi.c -> libygm.so).
+ *
+ * Requests from many documents that arrive within `batchWindowMs` (or until
+ * `maxBatchDocs`) are packed into ONE GPU batch: the batch formation point is
+ * the debounced store of Hocuspocus (packages/server/src/Hocuspocus.ts:417-447,
+ * SURVEY.md §8a row a4).  One batch is in flight per engine; later requests
+ * queue for the next batch.  A document whose status is not OK rejects only its
+ * own promise, with yjs's error text (SURVEY.md §8b "Errors").
+ */
+const path = require('path')
+
+let addon = null
+function loadAddon () {
+  if (!addon) addon = require(path.join(__dirname, '..', 'build', 'ygm_napi.node'))
+  return addon
+}
+
+const STATUS = ['OK', 'EMALFORMED', 'ERANGE', 'ENONCANON', 'ESURROGATE', 'EDEPTH', 'ENOMEM', 'EDEVICE', 'EINVAL']
+
+class YgmError extends Error {
+  constructor (code, message) {
+    super(message)
+    this.name = 'YgmError'
+    this.code = STATUS[code] || String(code)
+    this.status = code
+  }
+}
+
+class Batcher {
+  constructor (engine, op) {
+    this.engine = engine
+    this.op = op
+    this.queue = []
+    this.timer = null
+    this.inflight = false
+  }
+
+  push (job) {
+    return new Promise((resolve, reject) => {
+      this.queue.push({ job, resolve, reject })
+      if (this.queue.length >= this.engine.maxBatchDocs) this.kick(0)
+      else this.kick(this.engine.batchWindowMs)
+    })
+  }
+
+  kick (delay) {
+    if (this.inflight) return
+    if (delay === 0) { if (this.timer) { clearTimeout(this.timer); this.timer = null } setImmediate(() => this.flush()); return }
+    if (!this.timer) this.timer = setTimeout(() => { this.timer = null; this.flush() }, delay)
+  }
+
+  async flush () {
+    if (this.inflight || this.queue.length === 0) return
+    const batch = this.queue.splice(0, this.engine.maxBatchDocs)
+    this.inflight = true
+    try {
+      const res = await this.engine._run(this.op, batch.map(b => b.job))
+      batch.forEach((b, i) => {
+        const st = res.status[i]
+        if (st === 0) b.resolve(res.outputs[i])
+        else b.reject(new YgmError(st, loadAddon().strerror(st)))
+      })
+    } catch (e) {
+      batch.forEach(b => b.reject(e))
+    } finally {
+      this.inflight = false
+      if (this.queue.length) this.kick(this.queue.length >= this.engine.maxBatchDocs ? 0 : this.engine.batchWindowMs)
+    }
+  }
+}
+
+function packBlobs (blobs) {
+  const lens = new Uint32Array(blobs.length)
+  let total = 0
+  for (let i = 0; i < blobs.length; i++) { lens[i] = blobs[i].length; total += blobs[i].length }
+  const arena = Buffer.allocUnsafe(total)
+  let o = 0
+  for (const b of blobs) { arena.set(b, o); o += b.length }
+  return { arena, lens }
+}
+
+class GpuEngine {
+  /**
+   * @param {{device?: number, compat135?: boolean, batchWindowMs?: number, maxBatchDocs?: number}} [opts]
+   */
+  constructor (opts = {}) {
+    this.device = opts.device || 0
+    this.flags = opts.compat135 ? 1 : 0
+    this.batchWindowMs = opts.batchWindowMs === undefined ? 2 : opts.batchWindowMs
+    this.maxBatchDocs = opts.maxBatchDocs || 65536
+    this.handle = loadAddon().open(this.device, this.flags)
+    this.batchers = { merge: new Batcher(this, 'merge'), diff: new Batcher(this, 'diff'), sv: new Batcher(this, 'sv') }
+    this.chain = Promise.resolve()
+  }
+
+  // one native batch at a time per handle (the addon enforces it; chain them here)
+  _run (op, jobs) {
+    const run = () => {
+      const a = loadAddon()
+      if (op === 'merge') {
+        const blobs = []; const docs = []
+        jobs.forEach((ups, d) => { for (const u of ups) { blobs.push(u); docs.push(d) } })
+        const { arena, lens } = packBlobs(blobs)
+        return a.mergeMany(this.handle, arena, lens, Uint32Array.from(docs), jobs.length)
+      }
+      if (op === 'diff') {
+        const u = packBlobs(jobs.map(j => j[0])); const s = packBlobs(jobs.map(j => j[1]))
+        return a.diffMany(this.handle, u.arena, u.lens, s.arena, s.lens)
+      }
+      const u = packBlobs(jobs)
+      return a.svMany(this.handle, u.arena, u.lens)
+    }
+    const p = this.chain.then(run, run)
+    this.chain = p.catch(() => {})
+    return p
+  }
+
+  /** Y.mergeUpdates(updates), batched with concurrent callers. */
+  mergeUpdates (updates) { return this.batchers.merge.push(updates.map(u => u instanceof Uint8Array ? u : Uint8Array.from(u))) }
+  /** Y.diffUpdate(update, stateVector) */
+  diffUpdate (update, sv) { return this.batchers.diff.push([update, sv]) }
+  /** Y.encodeStateVectorFromUpdate(update) */
+  encodeStateVectorFromUpdate (update) { return this.batchers.sv.push(update) }
+
+  /** explicit batches (sync responders, bulk snapshot jobs) */
+  async mergeMany (docs) { const r = await this._run('merge', docs); return unpack(r) }
+  async diffMany (states, svs) { const r = await this._run('diff', states.map((s, i) => [s, svs[i]])); return unpack(r) }
+  async stateVectorsMany (states) { const r = await this._run('sv', states); return unpack(r) }
+
+  stats () { return loadAddon().stats(this.handle) }
+  close () { if (this.handle) { loadAddon().close(this.handle); this.handle = null } }
+}
+
+function unpack (r) {
+  return Array.from(r.status, (st, i) => st === 0 ? r.outputs[i] : new YgmError(st, loadAddon().strerror(st)))
+}
+
+module.exports = { GpuEngine, YgmError, STATUS, loadAddon }

@@ -1,0 +1,123 @@
+'use strict'
+/**
+ * @hocuspocus/extension-gpu-merge -- drop-in persistence extension whose
+ * merge / diff / state-vector work runs on MI355X.
+ *
+ * Mirrors the reference's persistence contract:
+ *   interface Extension            packages/server/src/types.ts:36-63
+ *   DatabaseConfiguration{fetch,store}  packages/extension-database/src/Database.ts:10-20
+ *   storePayload.state: Buffer     packages/server/src/types.ts:329-331
+ *
+ * What changes versus extension-database: instead of Y.encodeStateAsUpdate(doc)
+ * on every debounced store (Database.ts:55-60), the stored state is
+ * Y.mergeUpdates([base, ...updates since base]) computed in a GPU batch with
+ * every other document whose store fires in the same window.  The stored bytes
+ * are a valid V1 update of the same document state (mergeUpdates semantics,
+ * byte-identical to yjs); loading applies it exactly as Database.ts:44-50 does.
+ */
+const { GpuEngine, YgmError } = require('./engine')
+
+/**
+ * A batched document store.  `fromDatabase` adapts any DatabaseConfiguration
+ * (sqlite / s3 / custom) document by document.
+ */
+class DocumentStore {
+  /** @returns {Promise<(Uint8Array|Uint8Array[]|null)[]>} */
+  async fetchMany (payloads) { return payloads.map(() => null) }
+  /** @param {{payload: any, state: Buffer}[]} entries */
+  async storeMany (entries) {}
+
+  static fromDatabase (config) {
+    const s = new DocumentStore()
+    s.fetchMany = payloads => Promise.all(payloads.map(p => config.fetch ? config.fetch(p) : null))
+    s.storeMany = entries => Promise.all(entries.map(e => config.store ? config.store({ ...e.payload, state: e.state }) : undefined))
+    return s
+  }
+}
+
+class GpuMerge {
+  /**
+   * @param {{store?: DocumentStore|Function, fetch?: Function, device?: number, Y?: any,
+   *          engine?: GpuEngine, batchWindowMs?: number, maxBatchDocs?: number, compat135?: boolean}} configuration
+   */
+  constructor (configuration = {}) {
+    this.extensionName = 'GpuMerge'
+    // after Redis (priority 1000, which takes the store lock first), before plain storage extensions (100)
+    this.priority = configuration.priority || 900
+    this.configuration = configuration
+    // drop-in for `new Database({ fetch, store })`, or a batched DocumentStore instance
+    const st = configuration.store
+    this.store = st && typeof st.storeMany === 'function'
+      ? st
+      : DocumentStore.fromDatabase({ fetch: configuration.fetch, store: typeof st === 'function' ? st : undefined })
+    this.Y = configuration.Y || null
+    this.engine = configuration.engine || null
+    /** documentName -> { base: Uint8Array|null, log: Uint8Array[] } */
+    this.docs = new Map()
+  }
+
+  _Y () { if (!this.Y) this.Y = require('yjs'); return this.Y }
+  _engine () {
+    if (!this.engine) this.engine = new GpuEngine({ device: this.configuration.device || 0, compat135: this.configuration.compat135, batchWindowMs: this.configuration.batchWindowMs, maxBatchDocs: this.configuration.maxBatchDocs })
+    return this.engine
+  }
+
+  async onConfigure () { this._engine() }
+
+  /** fetch -> (GPU merge of snapshot + log rows) -> Y.applyUpdate, as Database.onLoadDocument (Database.ts:44-50) */
+  async onLoadDocument (data) {
+    const [fetched] = await this.store.fetchMany([data])
+    let state = null
+    if (Array.isArray(fetched)) {
+      const parts = fetched.filter(Boolean)
+      state = parts.length === 0 ? null : parts.length === 1 ? parts[0] : await this._engine().mergeUpdates(parts)
+    } else if (fetched) state = fetched
+    if (state) this._Y().applyUpdate(data.document, state)
+    this.docs.set(data.documentName, { base: state, log: [] })
+  }
+
+  /**
+   * Content added while loading (other extensions' onLoadDocument, a returned Doc,
+   * Hocuspocus.ts:357-372) never reaches onChange (the listener is registered after
+   * load, :382-391): capture it once here (SURVEY.md §8b log-capture hazard 2).
+   */
+  async afterLoadDocument (data) {
+    const Y = this._Y()
+    const entry = this.docs.get(data.documentName) || { base: null, log: [] }
+    this.docs.set(data.documentName, entry)
+    const baseSV = entry.base ? Y.encodeStateVectorFromUpdate(entry.base) : new Uint8Array([0])
+    const missing = Y.encodeStateAsUpdate(data.document, baseSV)
+    if (!isEmptyUpdate(missing)) entry.log.push(missing)
+  }
+
+  /** every post-load update, whatever its origin (Hocuspocus.ts:263; hazard 1) */
+  async onChange (data) {
+    let entry = this.docs.get(data.documentName)
+    if (!entry) { entry = { base: null, log: [] }; this.docs.set(data.documentName, entry) }
+    entry.log.push(data.update)
+  }
+
+  /** store = mergeUpdates([base, ...log]) on the GPU, then the same store payload shape (Database.ts:55-60) */
+  async onStoreDocument (data) {
+    const entry = this.docs.get(data.documentName) || { base: null, log: [] }
+    this.docs.set(data.documentName, entry)
+    const taken = entry.log.length
+    const parts = (entry.base ? [entry.base] : []).concat(entry.log.slice(0, taken))
+    let state
+    if (parts.length === 0) state = this._Y().encodeStateAsUpdate(data.document) // nothing captured: same bytes as extension-database
+    else if (parts.length === 1) state = parts[0]
+    else state = await this._engine().mergeUpdates(parts)
+    await this.store.storeMany([{ payload: data, state: Buffer.from(state.buffer, state.byteOffset, state.byteLength) }])
+    // the stored merge becomes the new base (under the document's saveMutex, Hocuspocus.ts:427)
+    entry.base = state
+    entry.log.splice(0, taken)
+  }
+
+  async afterUnloadDocument (data) { this.docs.delete(data.documentName) }
+
+  async onDestroy () { if (this.engine && !this.configuration.engine) this.engine.close(); this.engine = null }
+}
+
+function isEmptyUpdate (u) { return u.length === 2 && u[0] === 0 && u[1] === 0 }
+
+module.exports = { GpuMerge, DocumentStore, GpuEngine, YgmError }

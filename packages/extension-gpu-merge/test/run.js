@@ -1,0 +1,147 @@
+'use strict'
+// Extension tests: node test/run.js --cpu|--gpu
+//  --cpu : the extension's hook logic with an injected engine double (Y.mergeUpdates of
+//          the bundled yjs) -- no GPU in the build container
+//  --gpu : the same scenarios through the real N-API addon on the MI355X, plus byte parity
+//          of the stored state with yjs and batching checks
+const path = require('path')
+const assert = require('assert')
+const { GpuMerge } = require('../src/index.js')
+const { MiniHocuspocus } = require('./harness.js')
+
+const mode = process.argv.includes('--gpu') ? 'gpu' : 'cpu'
+const Y = require(path.join(__dirname, '..', '..', '..', 'tests', 'golden', 'gen', 'yjs_loader.js')).load()
+
+class CpuDouble { // test double (never shipped): same API as GpuEngine
+  constructor () { this.calls = 0 }
+  async mergeUpdates (u) { this.calls++; return Y.mergeUpdates(u) }
+  close () {}
+}
+
+function makeEngine () {
+  if (mode === 'cpu') return new CpuDouble()
+  const { GpuEngine } = require('../src/engine.js')
+  return new GpuEngine({ device: 0, batchWindowMs: 5 })
+}
+
+const sleep = ms => new Promise(resolve => setTimeout(resolve, ms))
+const tests = []
+const test = (name, fn) => tests.push({ name, fn })
+
+function memoryDb () {
+  const rows = new Map()
+  return { rows, fetch: async ({ documentName }) => rows.get(documentName) || null, store: async ({ documentName, state }) => { rows.set(documentName, state) } }
+}
+
+// tests/extension-s3/fetch.ts:92-114 -- stored state round-trips through fetch + applyUpdate
+test('store -> fetch -> applyUpdate preserves content', async (engine) => {
+  const db = memoryDb()
+  const ext = new GpuMerge({ ...db, Y, engine })
+  const hp = new MiniHocuspocus({ extensions: [ext], Y })
+  const doc = await hp.loadDocument('hocuspocus-test')
+  doc.transact(() => doc.getMap('map').set('attribute', 'value'), 'connection')
+  await hp.flushAll(); await hp.lastStore
+  assert.ok(db.rows.get('hocuspocus-test') instanceof Buffer)
+  const hp2 = new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine })], Y })
+  const doc2 = await hp2.loadDocument('hocuspocus-test')
+  assert.strictEqual(doc2.getMap('map').get('attribute'), 'value')
+})
+
+// tests/server/onStoreDocument.ts:521-630 -- two debounced saves, a new client sees ["foo","bar"]
+test('two saves then reload sees both', async (engine) => {
+  const db = memoryDb()
+  const hp = new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine })], Y })
+  const doc = await hp.loadDocument('doc')
+  doc.transact(() => doc.getArray('foo').push(['foo']), 'c1')
+  await hp.flushAll(); await hp.lastStore
+  doc.transact(() => doc.getArray('foo').push(['bar']), 'c1')
+  await hp.flushAll(); await hp.lastStore
+  const hp2 = new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine })], Y })
+  const d2 = await hp2.loadDocument('doc')
+  assert.deepStrictEqual(d2.getArray('foo').toArray(), ['foo', 'bar'])
+})
+
+// tests/server/onStoreDocument.ts:110-145 -- five changes, one store
+test('five changes debounce into one store', async (engine) => {
+  const db = memoryDb()
+  const hp = new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine })], Y, debounce: 40 })
+  const doc = await hp.loadDocument('d5')
+  for (let i = 0; i < 5; i++) doc.transact(() => doc.getText('t').insert(0, String(i)), 'c1')
+  await sleep(120); await hp.lastStore
+  assert.strictEqual(hp.stores, 1)
+  const d2 = await new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine })], Y }).loadDocument('d5')
+  assert.strictEqual(d2.getText('t').toString(), '43210')
+})
+
+// tests/server/onChange.ts:60-80 + SURVEY.md §8b hazard 2: content added during load is persisted
+test('content added by another extension during load is captured', async (engine) => {
+  const db = memoryDb()
+  const seeder = { priority: 50, async onLoadDocument ({ document }) { document.getText('t').insert(0, 'seeded') } }
+  const hp = new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine }), seeder], Y })
+  const doc = await hp.loadDocument('seeded')
+  doc.transact(() => doc.getText('t').insert(6, '!'), 'c1')
+  await hp.flushAll(); await hp.lastStore
+  const d2 = await new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine })], Y }).loadDocument('seeded')
+  assert.strictEqual(d2.getText('t').toString(), 'seeded!')
+})
+
+// the stored state is byte-identical to Y.mergeUpdates([base, ...updates])
+test('stored bytes == yjs mergeUpdates([snapshot, ...log])', async (engine) => {
+  const db = memoryDb()
+  const ext = new GpuMerge({ ...db, Y, engine })
+  const hp = new MiniHocuspocus({ extensions: [ext], Y })
+  const doc = await hp.loadDocument('bytes')
+  const log = []
+  doc.on('update', (u, o) => { if (o) log.push(u) })
+  for (let i = 0; i < 20; i++) doc.transact(() => doc.getText('t').insert(Math.floor(Math.random() * (doc.getText('t').length + 1)), 'x' + i), 'c1')
+  await hp.flushAll(); await hp.lastStore
+  const first = db.rows.get('bytes')
+  assert.strictEqual(Buffer.from(Y.mergeUpdates(log)).toString('hex'), first.toString('hex'))
+  const log2 = []
+  doc.on('update', (u, o) => { if (o) log2.push(u) })
+  doc.transact(() => doc.getText('t').delete(0, 3), 'c1')
+  doc.transact(() => doc.getText('t').insert(0, 'héllo 😀'), 'c1')
+  await hp.flushAll(); await hp.lastStore
+  assert.strictEqual(Buffer.from(Y.mergeUpdates([first].concat(log2))).toString('hex'), db.rows.get('bytes').toString('hex'))
+})
+
+// many documents storing in the same window share one GPU batch
+test('concurrent stores of many documents', async (engine) => {
+  const db = memoryDb()
+  const hp = new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine })], Y })
+  const docs = []
+  for (let d = 0; d < 64; d++) docs.push(await hp.loadDocument('many-' + d))
+  docs.forEach((doc, d) => { for (let i = 0; i < 10; i++) doc.transact(() => doc.getText('t').insert(0, String.fromCharCode(97 + ((d + i) % 26))), 'c') })
+  const before = mode === 'gpu' ? engine.stats().calls : 0
+  await hp.flushAll(); await hp.lastStore
+  await sleep(20)
+  for (let d = 0; d < 64; d++) {
+    const d2 = await new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine })], Y }).loadDocument('many-' + d)
+    assert.strictEqual(d2.getText('t').toString(), docs[d].getText('t').toString())
+  }
+  if (mode === 'gpu') assert.ok(engine.stats().calls - before <= 3, 'stores were batched')
+})
+
+// a failing document rejects only its own store (Hocuspocus.ts:431-435)
+test('malformed update rejects only its document', async (engine) => {
+  const db = memoryDb()
+  const ext = new GpuMerge({ ...db, Y, engine })
+  ext.docs.set('bad', { base: Uint8Array.from([1, 1, 5, 0, 4, 1, 1, 0x74]), log: [Uint8Array.from([0, 0])] }) // truncated base
+  const payload = name => ({ documentName: name, document: new Y.Doc(), context: {} })
+  ext.docs.set('good', { base: null, log: [Uint8Array.from([0, 0]), Uint8Array.from([0, 0])] })
+  const r = await Promise.allSettled([ext.onStoreDocument(payload('bad')), ext.onStoreDocument(payload('good'))])
+  assert.strictEqual(r[0].status, 'rejected')
+  assert.strictEqual(r[1].status, 'fulfilled')
+})
+
+async function main () {
+  const engine = makeEngine()
+  let failed = 0
+  for (const t of tests) {
+    try { await t.fn(engine); console.log('ok   ' + t.name) } catch (e) { failed++; console.log('FAIL ' + t.name + '\n     ' + (e && e.stack)) }
+  }
+  engine.close()
+  console.log(`${tests.length - failed}/${tests.length} passed (${mode})`)
+  process.exit(failed ? 1 : 0)
+}
+main()

@@ -22,6 +22,16 @@
 #include "ygm_seqdoc.hpp"
 #include "ygm_v1.hpp"
 
+#ifdef YGM_DIAG
+// diagnostic build only (libygm_diag.so): per-phase shader-clock sums of k_merge_fast
+__device__ unsigned long long ygm_diag[16];
+#define DIAG_T0 unsigned long long _dt = __builtin_amdgcn_s_memtime();
+#define DIAG(i) do { if (threadIdx.x == 0) { unsigned long long _n = __builtin_amdgcn_s_memtime(); atomicAdd(&ygm_diag[i], _n - _dt); _dt = _n; } } while (0)
+#else
+#define DIAG_T0
+#define DIAG(i)
+#endif
+
 namespace ygm {
 
 // ======================================================================= SV / diff
@@ -196,6 +206,7 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
                                                       unsigned long long* lb, DocMeta* meta, uint32_t* fb_list, uint64_t out_cap) {
   __shared__ MergeLds L;
   const int t = threadIdx.x;
+  DIAG_T0
   if (t == 0) { L.tile = atomicAdd(&meta->ticket, 1u); L.err = 0; L.fb = 0; L.nc = 0; }
   __syncthreads();
   const uint32_t d = L.tile;
@@ -215,9 +226,11 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
     for (uint32_t i = t; i < (uint32_t)nbytes; i += M_NT) L.in[i] = arena[b0 + i];
     for (uint32_t i = t; i < k; i += M_NT) { const uint64_t a = upd_off[u0 + i], b = upd_off[u0 + i + 1]; L.ustart[i] = (uint32_t)(a - b0); L.ulen[i] = (uint32_t)(b - a); }
     __syncthreads();
+    DIAG(0);
     // ---- pass A: validate + count
     for (uint32_t i = t; i < k; i += M_NT) m_parse_update(L, i, 0, flags);
     __syncthreads();
+    DIAG(1);
     if (L.err) st = L.err;
     else if (L.fb) st = ST_FALLBACK;
     if (st == ST_OK) {
@@ -235,8 +248,10 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
     for (int j = S + t; j < NS; j += M_NT) { L.key[j] = ~0ull; L.idx[j] = 0xFFFF; }
     for (int j = D + t; j < ND; j += M_NT) { L.dkey[j] = ~0ull; L.didx[j] = 0xFFFF; }
     __syncthreads();
+    DIAG(2);
     bitonic_sort<M_NT>(L.key, L.idx, NS);
     bitonic_sort<M_NT>(L.dkey, L.didx, ND);
+    DIAG(3);
     // ---- structs: classify each sorted element against its predecessor
     for (int j = t; j < S; j += M_NT) {
       const uint64_t kj = L.key[j]; const uint32_t r = L.idx[j];
@@ -303,6 +318,7 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
     __syncthreads();
     struct_bytes = block_scan_array<M_NT>(L.eA, S, L.tmp32);
     hdr0 = vu_len(nblocks);
+    DIAG(4);
     // ---- delete set: segments (clients) and runs
     for (int j = t; j < D; j += M_NT) {
       const uint64_t kj = L.dkey[j];
@@ -352,6 +368,7 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
     size = hdr0 + struct_bytes + ds_bytes;
     if (t == 0) L.nseg = nseg;
   }
+  DIAG(5);
   // ---- look-back: this document's place in the packed output
   const uint64_t mysz = (st == ST_OK) ? size : 0;
   if (t < WAVE) {
@@ -368,6 +385,7 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
     }
   }
   __syncthreads();
+  DIAG(6);
   const uint64_t base = L.base;
   if (meta->fault && st == ST_OK) st = ST_DEVICE;
   if (st == ST_OK && base + size > out_cap) st = ST_NOMEM;
@@ -400,6 +418,7 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
     if (f & 1u) { w.vu(cl); w.vu(L.dC[L.dB[j]]); }
     if (f & 2u) { w.vu(ck); w.vu(L.dE[j] - ck); }
   }
+  DIAG(7);
 }
 
 // ======================================================================= merge sequential
@@ -436,13 +455,14 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
   if (st == ST_OK) {
     for (int i = 0; i < k; i++) { const uint64_t a = upd_off[u0 + i], b = upd_off[u0 + i + 1]; ub[i] = arena + a; ul[i] = (uint32_t)(b - a); }
     Out o{nullptr, 0};
-    LW lw{&o, false, flags, 0, 0, 0, cnt, cnt_cap, 0};
+    LW lw{&o, false, flags, 0, 0, 0, cnt, cnt_cap, 0, false};
     st = merge_pass(R, order, tmp, k, ub, ul, flags, lw);
     if (st == ST_OK) {
       nblocks = lw.bi;
       o.vu(nblocks);
       const int64_t nr = ds_collect(R, k, drec, drec_cap);
       if (nr < 0) st = (int)(-nr);
+      else if (lw.nc) st = ST_NONCANON;
       else { ds_union_write(drec, (uint64_t)nr, flags, o); size = o.n; }
     }
   }
@@ -454,7 +474,7 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
   if (st == ST_OK) {  // write pass: block count, structs, delete set
     Out o{out + at, 0};
     o.vu(nblocks);
-    LW lw{&o, true, flags, 0, 0, 0, cnt, cnt_cap, 0};
+    LW lw{&o, true, flags, 0, 0, 0, cnt, cnt_cap, 0, false};
     st = merge_pass(R, order, tmp, k, ub, ul, flags, lw);
     if (st == ST_OK) {
       const int64_t nr = ds_collect(R, k, drec, drec_cap);
@@ -471,6 +491,14 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
 extern "C" {
 
 using namespace ygm;
+
+#ifdef YGM_DIAG
+int ygm_diag_read(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ygm_diag), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) { unsigned long long z[16] = {0}; (void)hipMemcpyToSymbol(HIP_SYMBOL(ygm_diag), z, sizeof z); }
+  return 0;
+}
+#endif
 
 size_t ygm_k_meta_bytes() { return sizeof(DocMeta); }
 size_t ygm_k_seq_reader_bytes() { return sizeof(Stream); }

@@ -248,6 +248,7 @@ struct LW {
   uint64_t written, curr_client, bi;
   uint32_t* cnt; uint64_t cnt_cap;
   int err;
+  bool nc;  // NONCANON content written: reported only if nothing else throws
   YDEV void flush() {
     if (written > 0) {
       if (!write) { if (bi < cnt_cap) cnt[bi] = (uint32_t)written; else err = ST_NOMEM; o->n += vu_len(written); }
@@ -266,7 +267,8 @@ struct LW {
     if (w.s.kind == K_GC) { o->b(0); o->vu(w.len); }
     else if (w.s.kind == K_SKIP) { o->b(10); o->vu(w.len); }
     else e = write_struct(*o, w.base, w.s, w.client, w.clock0, w.cut, true, flags);
-    if (e) err = e;
+    if (e == ST_NONCANON) nc = true;
+    else if (e) err = e;
     written++;
   }
 };

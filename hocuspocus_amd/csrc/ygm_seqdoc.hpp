@@ -80,15 +80,19 @@ YDEV_NI int sv_doc(const uint8_t* p, uint32_t n, uint32_t flags, Out& o, uint64_
 // clients are merged into their first non-empty entry (Map semantics of
 // readDeleteSet).  Output order: client-descending (yjs 13.6 writeDeleteSet) or
 // first-seen (13.5 compat).  O(C^2) client scans: delete sets are small.
+YDEV_NI bool ds_seen_before(const uint8_t* p, uint32_t dstart, uint32_t dend, uint32_t upto, uint64_t client);
+// validates the DS at c and counts its distinct clients with >= 1 range
 YDEV_NI int ds_validate(Cur c, uint64_t& nclients_out) {
+  const uint32_t dstart = c.pos;
   const uint64_t n = c.vu();
-  uint64_t nonempty = 0;
+  uint64_t distinct = 0;
   for (uint64_t i = 0; i < n && !c.err; i++) {
-    c.vu(); const uint64_t nd = c.vu();
+    const uint32_t at = c.pos;
+    const uint64_t cl = c.vu(); const uint64_t nd = c.vu();
     for (uint64_t k = 0; k < nd && !c.err; k++) { c.vu(); c.vu(); }
-    if (nd > 0) nonempty++;
+    if (!c.err && nd > 0 && !ds_seen_before(c.p, dstart, c.end, at, cl)) distinct++;
   }
-  nclients_out = nonempty;
+  nclients_out = distinct;
   return c.err;
 }
 // entry i: position of its client varuint (after the count)
@@ -215,6 +219,7 @@ YDEV_NI int diff_doc(const uint8_t* p, uint32_t n, const uint8_t* sv, uint32_t s
   if (e) return e;
   DiffGen g; g.init(p, n, sv, svn, flags);
   if (g.s.c.err) return g.s.c.err;
+  bool nc = false;
   if (write) o.vu(nblocks);
   uint64_t written = 0, wclient = 0, bi = 0;
   SInfo ev; uint64_t cl, ck, off;
@@ -237,7 +242,8 @@ YDEV_NI int diff_doc(const uint8_t* p, uint32_t n, const uint8_t* sv, uint32_t s
       else { o.vu(cl); o.vu(ck + off); }  // count varuint added when the block closes
     }
     const int we = write_struct(o, p, ev, cl, ck, off, false, flags);
-    if (we) return we;
+    if (we == ST_NONCANON) nc = true;  // reported after the rest has been validated
+    else if (we) return we;
     written++;
   }
   if (g.s.c.err) return g.s.c.err;
@@ -264,6 +270,7 @@ YDEV_NI int diff_doc(const uint8_t* p, uint32_t n, const uint8_t* sv, uint32_t s
   uint64_t ncl;
   e = ds_validate(Cur{p, dstart, n, 0, 0}, ncl);
   if (e) return e;
+  if (nc) return ST_NONCANON;
   ds_copy(p, dstart, n, ncl, flags, o);
   return ST_OK;
 }

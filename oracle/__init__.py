@@ -44,6 +44,8 @@ def lib():
         L.yo_diff.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, ctypes.c_int, P(u8p), P(ctypes.c_size_t)]
         L.yo_sv.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, P(u8p), P(ctypes.c_size_t)]
         L.yo_free.argtypes = [ctypes.c_void_p]
+        L.yo_merge_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
         L.yo_v8_sort_table.argtypes = [P(ctypes.c_int), ctypes.c_int, P(ctypes.c_int8)]
         L.yo_v8_sort_table.restype = ctypes.c_long
         for f in (L.yo_merge, L.yo_diff, L.yo_sv):
@@ -109,3 +111,19 @@ def v8_sort_table(arr, table):
     t = (ctypes.c_int8 * max(len(table), 1))(*table)
     calls = L.yo_v8_sort_table(a, n, t)
     return list(a)[:n], calls
+
+
+def merge_batch(arena, upd_off, doc_upd, threads=1, compat135=False):
+    """mergeUpdates over every document of a packed corpus on `threads` pthreads
+    (CPU-baseline driver).  Returns (status int32 array, algorithmic bytes)."""
+    import numpy as np
+    L = lib()
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    upd_off = np.ascontiguousarray(upd_off, dtype=np.uint64)
+    doc_upd = np.ascontiguousarray(doc_upd, dtype=np.uint32)
+    n_docs = len(doc_upd) - 1
+    status = np.zeros(max(n_docs, 1), dtype=np.int32)
+    algo = ctypes.c_uint64()
+    L.yo_merge_batch(arena.ctypes.data, upd_off.ctypes.data, doc_upd.ctypes.data, n_docs, COMPAT_135 if compat135 else 0,
+                     threads, status.ctypes.data, ctypes.byref(algo))
+    return status[:n_docs], algo.value

@@ -544,6 +544,7 @@ typedef struct { uint64_t written; Buf b; } Part;
 typedef struct {
   uint64_t curr_client, written; Buf rest;
   Part *parts; size_t nparts, cap; int err;
+  int nc;  /* a written struct's content would be re-encoded: reported only if nothing throws */
 } LWriter;
 static void lw_flush(LWriter *w) {
   if (w->written > 0) {
@@ -557,7 +558,8 @@ static void lw_write(LWriter *w, const St *s, uint64_t offset, int flags) {
   if (w->written > 0 && w->curr_client != s->client) lw_flush(w);
   if (w->written == 0) { w->curr_client = s->client; bvu(&w->rest, s->client); bvu(&w->rest, s->clock + offset); }
   int e = write_struct(&w->rest, s, offset, flags);
-  if (e) w->err = e;
+  if (e == YO_ENONCANON) w->nc = 1;
+  else if (e) w->err = e;
   w->written++;
 }
 static void lw_finish(LWriter *w, Buf *out) {
@@ -939,6 +941,7 @@ int yo_merge(const uint8_t *const *ups, const size_t *lens, size_t n, int flags,
     for (size_t i = 0; i < n; i++) ds_free(&dss[i]);
     free(dss); ds_free(&m);
     if (o.oom && !err) err = YO_ENOMEM;
+    if (!err && W.nc) err = YO_ENONCANON;
     if (!err) { *out = o.b; *out_len = o.n; } else free(o.b);
   }
 done:
@@ -990,6 +993,7 @@ int yo_diff(const uint8_t *u, size_t ulen, const uint8_t *sv, size_t svlen, int 
   }
   lw_free(&W); free(svc); free(svk);
   if (o.oom && !err) err = YO_ENOMEM;
+  if (!err && W.nc) err = YO_ENONCANON;
   if (!err) { *out = o.b; *out_len = o.n; } else free(o.b);
   return err;
 }
@@ -1028,3 +1032,47 @@ int yo_sv(const uint8_t *u, size_t ulen, int flags, uint8_t **out, size_t *out_l
 
 void yo_free(void *p) { free(p); }
 const char *yo_version(void) { return "yjs_oracle 1 (yjs 13.6.26 semantics; YO_COMPAT_135 = 13.5.16)"; }
+
+/* ------------------------------------------------------------ batch driver */
+/* CPU baseline driver: mergeUpdates over n_docs documents on `nthreads` pthreads
+ * (documents dealt round-robin).  Outputs are discarded; returns the total
+ * algorithmic bytes (inputs + outputs) in *algo_bytes and per-doc status. */
+#include <pthread.h>
+typedef struct {
+  const uint8_t *arena; const uint64_t *upd_off; const uint32_t *doc_upd;
+  uint32_t n_docs; int flags; int tid, nthreads;
+  uint64_t algo; int32_t *status;
+} BatchJob;
+static void *batch_worker(void *arg) {
+  BatchJob *j = (BatchJob *)arg;
+  const uint8_t **ptrs = NULL; size_t *lens = NULL; size_t cap = 0;
+  for (uint32_t d = (uint32_t)j->tid; d < j->n_docs; d += (uint32_t)j->nthreads) {
+    uint32_t u0 = j->doc_upd[d], u1 = j->doc_upd[d + 1], k = u1 - u0;
+    if (k > cap) { cap = k * 2; ptrs = (const uint8_t **)realloc(ptrs, cap * sizeof *ptrs); lens = (size_t *)realloc(lens, cap * sizeof *lens); }
+    uint64_t in = 0;
+    for (uint32_t i = 0; i < k; i++) { ptrs[i] = j->arena + j->upd_off[u0 + i]; lens[i] = (size_t)(j->upd_off[u0 + i + 1] - j->upd_off[u0 + i]); in += lens[i]; }
+    uint8_t *out = NULL; size_t ol = 0;
+    int st = yo_merge(ptrs, lens, k, j->flags, &out, &ol);
+    j->status[d] = st;
+    j->algo += in + (st == YO_OK ? ol : 0);
+    free(out);
+  }
+  free(ptrs); free(lens);
+  return NULL;
+}
+int yo_merge_batch(const uint8_t *arena, const uint64_t *upd_off, const uint32_t *doc_upd, uint32_t n_docs, int flags,
+                   int nthreads, int32_t *status, uint64_t *algo_bytes) {
+  if (nthreads < 1) nthreads = 1;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  BatchJob *jobs = (BatchJob *)calloc((size_t)nthreads, sizeof(BatchJob));
+  for (int t = 0; t < nthreads; t++) {
+    BatchJob b = { arena, upd_off, doc_upd, n_docs, flags, t, nthreads, 0, status };
+    jobs[t] = b;
+    pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
+  }
+  uint64_t tot = 0;
+  for (int t = 0; t < nthreads; t++) { pthread_join(th[t], NULL); tot += jobs[t].algo; }
+  *algo_bytes = tot;
+  free(th); free(jobs);
+  return 0;
+}

@@ -19,9 +19,12 @@ size_t ygm_k_drec_bytes();
 int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,
                      uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
                      unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
-int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
+int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta,
-                            uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
+                            uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
+int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
+                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* lb,
+                            void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list, uint32_t n_fb,
                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
                            void* readers, int* order, int* tmp, const uint8_t** ubase, uint32_t* ulen, uint64_t upd_cap,
@@ -32,8 +35,8 @@ namespace {
 
 // mirrors ygm::DocMeta (ygm_kernels.hip)
 struct Meta {
-  unsigned int ticket, fault, fb_count, pad;
-  unsigned long long fast_total, seq_cursor, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor;
+  unsigned int ticket, fault, fb_count, defer_count, ticket_m, pad[3];
+  unsigned long long fast_total, m_total, seq_cursor, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor;
 };
 
 struct DevBuf {
@@ -62,7 +65,7 @@ struct ygm_ctx {
   // device inputs (host API staging)
   DevBuf arena, offs, docs, sv_arena, sv_offs;
   // device outputs + state
-  DevBuf out, out_off, out_len, status, lb, meta, fb_list;
+  DevBuf out, out_off, out_len, status, lb, meta, fb_list, defer_list;
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
   // host results
   std::vector<uint8_t> h_data;
@@ -117,7 +120,7 @@ void ygm_close(ygm_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
-                    &c->lb, &c->meta, &c->fb_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
+                    &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
                     &c->s_drec})
     b->release();
   for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
@@ -133,11 +136,12 @@ int ygm_stats(ygm_ctx* c, ygm_stats_t* out) {
 
 // ------------------------------------------------------------------ device API
 static int prep_outputs(ygm_ctx* c, uint32_t n_docs, uint64_t out_cap, hipStream_t s) {
-  const uint32_t tiles = n_docs + 1;
+  const size_t tiles = 2 * (size_t)n_docs + 2;  // two look-back regions (wave kernel, workgroup kernel)
   if (!c->out.ensure(out_cap + 64) || !c->out_off.ensure((size_t)n_docs * 8 + 8) || !c->out_len.ensure((size_t)n_docs * 8 + 8) ||
-      !c->status.ensure((size_t)n_docs * 4 + 4) || !c->lb.ensure((size_t)tiles * 8) || !c->fb_list.ensure((size_t)n_docs * 4 + 4))
+      !c->status.ensure((size_t)n_docs * 4 + 4) || !c->lb.ensure(tiles * 8) || !c->fb_list.ensure((size_t)n_docs * 4 + 4) ||
+      !c->defer_list.ensure((size_t)n_docs * 4 + 4))
     return YGM_ENOMEM;
-  HIPCHK(hipMemsetAsync(c->lb.p, 0, (size_t)tiles * 8, s));
+  HIPCHK(hipMemsetAsync(c->lb.p, 0, tiles * 8, s));
   HIPCHK(hipMemsetAsync(c->meta.p, 0, sizeof(Meta), s));
   return YGM_OK;
 }
@@ -160,16 +164,30 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
   int e = prep_outputs(c, n_docs, out_cap, s);
   if (e) return e;
   HIPCHK(hipEventRecord(c->e0, s));
-  if (ygm_k_launch_merge_fast(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
+  if (ygm_k_launch_merge_wave(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
                               c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->lb.as<unsigned long long>(), c->meta.p,
-                              c->fb_list.as<uint32_t>(), out_cap, s))
+                              c->defer_list.as<uint32_t>(), c->fb_list.as<uint32_t>(), out_cap, s))
     return YGM_EDEVICE;
   HIPCHK(hipEventRecord(c->e1, s));
   Meta m;
   HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (m.fault) return YGM_EDEVICE;
-  uint64_t total = m.fast_total;
+  float ms0 = 0;
+  if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
+  if (m.defer_count) {  // documents over the wave class: one workgroup per document
+    HIPCHK(hipEventRecord(c->e0, s));
+    if (ygm_k_launch_merge_fast(d_arena, d_upd_off, d_doc_upd, c->defer_list.as<uint32_t>(), m.defer_count, c->flags,
+                                c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
+                                c->lb.as<unsigned long long>() + n_docs + 1, c->meta.p, c->fb_list.as<uint32_t>(), out_cap, s))
+      return YGM_EDEVICE;
+    HIPCHK(hipEventRecord(c->e1, s));
+    HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (m.fault) return YGM_EDEVICE;
+    if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
+  }
+  uint64_t total = m.fast_total + m.m_total;
   if (m.fb_count) {
     const uint64_t upd_cap = m.fb_upds + 1, byte_cap = m.fb_bytes + 8ull * m.fb_count + 8;
     if (!c->s_readers.ensure(upd_cap * ygm_k_seq_reader_bytes()) || !c->s_order.ensure(upd_cap * 4) || !c->s_tmp.ensure(upd_cap * 4) ||
@@ -183,11 +201,9 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
       return YGM_EDEVICE;
     HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    total = m.fast_total + m.seq_cursor;
+    total = m.fast_total + m.m_total + m.seq_cursor;
     c->stats.docs_seq += m.fb_count;
   }
-  float ms = 0;
-  if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;
   c->stats.calls++; c->stats.docs += n_docs; c->stats.updates += n_upd;
   c->stats.docs_fast += n_docs - m.fb_count;
   c->stats.bytes_in += arena_bytes; c->stats.bytes_out += total;

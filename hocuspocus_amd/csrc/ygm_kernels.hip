@@ -19,6 +19,7 @@
 
 #include "ygm_common.hpp"
 #include "ygm_merge_seq.hpp"
+#include "ygm_merge_wave.hpp"
 #include "ygm_seqdoc.hpp"
 #include "ygm_v1.hpp"
 
@@ -27,7 +28,9 @@
 __device__ unsigned long long ygm_diag[16];
 #define DIAG_T0 unsigned long long _dt = __builtin_amdgcn_s_memtime();
 #define DIAG(i) do { if (threadIdx.x == 0) { unsigned long long _n = __builtin_amdgcn_s_memtime(); atomicAdd(&ygm_diag[i], _n - _dt); _dt = _n; } } while (0)
+#define DIAGW(i) do { if ((threadIdx.x & 63) == 0) { unsigned long long _n = __builtin_amdgcn_s_memtime(); atomicAdd(&ygm_diag[8 + (i)], _n - _dt); _dt = _n; } } while (0)
 #else
+#define DIAGW(i)
 #define DIAG_T0
 #define DIAG(i)
 #endif
@@ -42,8 +45,11 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned int ticket;
   unsigned int fault;
   unsigned int fb_count;            // documents sent to the sequential kernel
-  unsigned int pad;
-  unsigned long long fast_total;    // bytes in the look-back (fast) region
+  unsigned int defer_count;         // documents sent from the wave kernel to the workgroup kernel
+  unsigned int ticket_m;            // tickets of the workgroup kernel
+  unsigned int pad[3];
+  unsigned long long fast_total;    // bytes in the first look-back region
+  unsigned long long m_total;       // bytes in the workgroup-kernel region (after fast_total)
   unsigned long long seq_cursor;    // bytes appended by the sequential kernel
   unsigned long long fb_upds;       // updates / bytes of fallback documents (scratch sizing)
   unsigned long long fb_bytes;
@@ -199,17 +205,23 @@ YDEV_NI void m_parse_update(MergeLds& L, int i, int pass, uint32_t flags) {
 
 YDEV int pow2_ceil(int n) { int p = 1; while (p < n) p <<= 1; return p; }
 
+// Documents deferred by the wave kernel (list `docs`, n_docs entries); output
+// region starts at meta->fast_total.
 __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
-                                                      const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t flags,
-                                                      uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
+                                                      const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ docs,
+                                                      uint32_t n_docs, uint32_t flags,
+                                                      uint8_t* __restrict__ out_all, uint64_t* __restrict__ out_off,
                                                       uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
                                                       unsigned long long* lb, DocMeta* meta, uint32_t* fb_list, uint64_t out_cap) {
   __shared__ MergeLds L;
   const int t = threadIdx.x;
   DIAG_T0
-  if (t == 0) { L.tile = atomicAdd(&meta->ticket, 1u); L.err = 0; L.fb = 0; L.nc = 0; }
+  if (t == 0) { L.tile = atomicAdd(&meta->ticket_m, 1u); L.err = 0; L.fb = 0; L.nc = 0; }
   __syncthreads();
-  const uint32_t d = L.tile;
+  const uint32_t tile = L.tile;
+  const uint32_t d = docs[tile];
+  const uint64_t region = meta->fast_total;
+  uint8_t* out = out_all + region;
   const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
   const uint32_t k = u1 - u0;
   const uint64_t b0 = upd_off[u0], b1 = upd_off[u1];
@@ -372,10 +384,10 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
   // ---- look-back: this document's place in the packed output
   const uint64_t mysz = (st == ST_OK) ? size : 0;
   if (t < WAVE) {
-    const uint64_t b = lookback(lb, d, mysz, &meta->fault);
+    const uint64_t b = lookback(lb, tile, mysz, &meta->fault);
     if (t == 0) {
       L.base = b;
-      if (d == n_docs - 1) meta->fast_total = b + mysz;
+      if (tile == n_docs - 1) meta->m_total = b + mysz;
       if (st == ST_FALLBACK) {
         const uint32_t q = atomicAdd(&meta->fb_count, 1u);
         fb_list[q] = d;
@@ -388,8 +400,8 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
   DIAG(6);
   const uint64_t base = L.base;
   if (meta->fault && st == ST_OK) st = ST_DEVICE;
-  if (st == ST_OK && base + size > out_cap) st = ST_NOMEM;
-  if (t == 0) { out_off[d] = base; out_len[d] = st == ST_OK ? size : 0; status[d] = st == ST_FALLBACK ? ST_FALLBACK : st; }
+  if (st == ST_OK && region + base + size > out_cap) st = ST_NOMEM;
+  if (t == 0) { out_off[d] = region + base; out_len[d] = st == ST_OK ? size : 0; status[d] = st == ST_FALLBACK ? ST_FALLBACK : st; }
   if (st != ST_OK) return;
   uint8_t* o = out + base;
   if (mode == 1) { if (t == 0) { o[0] = 0; o[1] = 0; } return; }
@@ -419,6 +431,342 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
     if (f & 2u) { w.vu(ck); w.vu(L.dE[j] - ck); }
   }
   DIAG(7);
+}
+
+
+// ======================================================================= merge: one wave per document
+__global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+                                                               const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t flags,
+                                                               uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
+                                                               uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+                                                               unsigned long long* lb, DocMeta* meta, uint32_t* defer_list,
+                                                               uint32_t* fb_list, uint64_t out_cap) {
+  __shared__ WaveLds LS[W_WAVES];
+  DIAG_T0
+  const uint32_t l = threadIdx.x % WAVE;
+  WaveLds& L = LS[threadIdx.x / WAVE];
+  uint32_t tk = 0;
+  if (l == 0) tk = atomicAdd(&meta->ticket, 1u);
+  const uint32_t d = (uint32_t)__shfl((int)tk, 0, WAVE);
+  if (d >= n_docs) return;
+  const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
+  const uint32_t k = u1 - u0;
+  const uint64_t b0 = upd_off[u0], b1 = upd_off[u1];
+  const uint64_t nbytes = b1 - b0;
+  constexpr int ST_DEFER = 101;
+  int st = ST_OK, mode = 0;
+  uint64_t size = 0;
+  uint32_t S = 0, D = 0, nblocks = 0, nseg = 0, hdr0 = 0, sbytes = 0, dsbytes = 0;
+  uint32_t F[W_E], nb[W_E], epos[W_E];
+  uint32_t DF[W_DE], sid[W_DE], dpos[W_DE];
+#pragma unroll
+  for (int q = 0; q < W_E; q++) { F[q] = 0; nb[q] = 0; epos[q] = 0; }
+#pragma unroll
+  for (int q = 0; q < W_DE; q++) { DF[q] = 0; sid[q] = 0; dpos[q] = 0; }
+  if (k == 0) { mode = 1; size = 2; }
+  else if (k == 1) { mode = 2; size = nbytes; }
+  else if (k > (uint32_t)W_K || nbytes + 16 > (uint64_t)W_IN || (flags & 2u)) st = ST_DEFER;
+  if (mode == 0 && st == ST_OK) {
+    // ---- stage: 16-byte loads of [b0 & ~15, b1) (arenas carry >= 16 readable bytes of tail padding)
+    const uint64_t a0 = b0 & ~15ull;
+    const uint32_t shift = (uint32_t)(b0 - a0);
+    const uint32_t nch = (uint32_t)((shift + nbytes + 15) / 16);
+    for (uint32_t c = l; c < nch; c += WAVE) *(uint4*)(L.in + c * 16) = *(const uint4*)(arena + a0 + (uint64_t)c * 16);
+    for (uint32_t i = l; i < k; i += WAVE) {
+      const uint64_t a = upd_off[u0 + i], b = upd_off[u0 + i + 1];
+      L.ustart[i] = (uint16_t)(a - b0 + shift); L.ulen[i] = (uint16_t)(b - a);
+    }
+    wave_sync();
+    DIAGW(0);
+    // ---- pass A: validate + count; lane l parses updates l*R .. l*R+R-1
+    const uint32_t R = (k + WAVE - 1) / WAVE;
+    uint32_t ns[W_R], nd[W_R];
+    int err = 0; bool fb = false, nc = false;
+#pragma unroll
+    for (int r = 0; r < W_R; r++) {
+      ns[r] = 0; nd[r] = 0;
+      const uint32_t i = l * R + r;
+      if ((uint32_t)r < R && i < k) { const UpdCount c = w_parse_update(L, (int)i, false, 0, 0, flags, err, fb, nc); ns[r] = c.ns; nd[r] = c.nd; }
+    }
+    DIAGW(1);
+    const unsigned long long eb = __ballot(err != 0);
+    if (eb) st = __shfl(err, __ffsll((long long)eb) - 1, WAVE);
+    else if (__ballot(fb)) st = ST_DEFER;
+    else {
+      uint32_t sl = 0, dl = 0;
+#pragma unroll
+      for (int r = 0; r < W_R; r++) { sl += ns[r]; dl += nd[r]; }
+      uint32_t sb = wave_exscan(sl, S), db = wave_exscan(dl, D);
+      if (S > (uint32_t)W_S || D > (uint32_t)W_D || ((flags & F_COMPAT_135) && D > 0)) st = ST_DEFER;
+      else if (__ballot(nc)) st = ST_NONCANON;
+      else {
+        // ---- pass B: records
+#pragma unroll
+        for (int r = 0; r < W_R; r++) {
+          const uint32_t i = l * R + r;
+          if ((uint32_t)r < R && i < k && (ns[r] | nd[r])) { int e2 = 0; bool f2 = false, n2 = false; w_parse_update(L, (int)i, true, sb, db, flags, e2, f2, n2); }
+          sb += ns[r]; db += nd[r];
+        }
+        wave_sync();
+        DIAGW(2);
+        // ---- rank sort of struct keys (ties by record id; equal keys are caught as overlap)
+        {
+          uint64_t mk[W_E]; uint32_t rk[W_E];
+#pragma unroll
+          for (int q = 0; q < W_E; q++) { const uint32_t j = l + WAVE * q; mk[q] = j < S ? L.key[j] : ~0ull; rk[q] = 0; }
+          for (uint32_t i = 0; i < S; i++) {
+            const uint64_t ki = L.key[i];
+#pragma unroll
+            for (int q = 0; q < W_E; q++) rk[q] += (ki < mk[q]) || (ki == mk[q] && i < l + WAVE * q);
+          }
+          wave_sync();
+#pragma unroll
+          for (int q = 0; q < W_E; q++) { const uint32_t j = l + WAVE * q; if (j < S) { L.key[rk[q]] = mk[q]; L.sidx[rk[q]] = (uint16_t)j; } }
+        }
+        {
+          uint64_t mk[W_DE]; uint32_t ml[W_DE], rk[W_DE];
+#pragma unroll
+          for (int q = 0; q < W_DE; q++) { const uint32_t j = l + WAVE * q; mk[q] = j < D ? L.dkey[j] : ~0ull; ml[q] = j < D ? L.dlen[j] : 0; rk[q] = 0; }
+          for (uint32_t i = 0; i < D; i++) {
+            const uint64_t ki = L.dkey[i];
+#pragma unroll
+            for (int q = 0; q < W_DE; q++) rk[q] += (ki < mk[q]) || (ki == mk[q] && i < l + WAVE * q);
+          }
+          wave_sync();
+#pragma unroll
+          for (int q = 0; q < W_DE; q++) { const uint32_t j = l + WAVE * q; if (j < D) { L.dkey[rk[q]] = mk[q]; L.dlen[rk[q]] = ml[q]; } }
+        }
+        DIAGW(3);
+        for (uint32_t j = l; j < S; j += WAVE) L.runend[j] = 0;
+        for (uint32_t j = l; j < D; j += WAVE) L.drunend[j] = 0;
+        for (uint32_t j = l; j < W_BLK; j += WAVE) { L.blkcnt[j] = 0; L.segcnt[j] = 0; }
+        wave_sync();
+        // ---- classify sorted structs (blocked: lane l owns l*W_E .. l*W_E+W_E-1)
+        uint32_t v[W_E];
+        bool ovl = false;
+#pragma unroll
+        for (int q = 0; q < W_E; q++) {
+          const uint32_t j = l * W_E + q;
+          v[q] = 0;
+          if (j < S) {
+            const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
+            uint32_t f = (L.r_flag[r] & 3) == K_GC ? EF_GC : 0;
+            if (j == 0) f |= EF_NEWC;
+            else {
+              const uint64_t kp = L.key[j - 1]; const uint32_t rp = L.sidx[j - 1];
+              const uint32_t pend = (uint32_t)kp + L.r_len[rp];
+              if ((uint32_t)(kp >> 32) != (uint32_t)(kj >> 32)) f |= EF_NEWC;
+              else if ((uint32_t)kj < pend) ovl = true;
+              else if ((uint32_t)kj > pend) f |= EF_GAP;
+              else {
+                const uint32_t ss = L.r_ss[r], sp = L.r_ss[rp];
+                if ((ss >> 8) == (sp >> 8) && (ss & 0xFF) == (sp & 0xFF) + 1) f |= EF_SDN;
+                if ((f & EF_GC) && (L.r_flag[rp] & 3) == K_GC) f |= EF_CGG;
+              }
+            }
+            if (!(f & EF_CGG)) f |= EF_NONID | EF_T;
+            else if (!(f & EF_SDN)) f |= EF_NONID;
+            F[q] = f;
+            v[q] = (f & EF_NONID) ? j + 1 : 0;
+            nb[q] = (f & EF_NEWC) ? 1 : 0;
+            L.eflag[j] = (uint8_t)f;
+          }
+        }
+        if (__ballot(ovl)) st = ST_FALLBACK;  // overlapping structs: exact sequential replay
+        else {
+          // client blocks and delete-set clients must fit the W_BLK counters
+          uint32_t nbk = 0, nsg = 0;
+#pragma unroll
+          for (int q = 0; q < W_E; q++) nbk += nb[q];
+          for (uint32_t j = l; j < D; j += WAVE) nsg += (j == 0 || (L.dkey[j - 1] >> 32) != (L.dkey[j] >> 32)) ? 1u : 0u;
+          if (wave_sum(nbk) > (uint32_t)W_BLK || wave_sum(nsg) > (uint32_t)W_BLK) st = ST_DEFER;
+        }
+      }
+    }
+  }
+  if (mode == 0 && st == ST_OK) {
+    wave_sync();
+    // last non-identity element <= j (max-scan) and block index (count of NEWC <= j, minus 1)
+    uint32_t v[W_E];
+    uint32_t m = 0, c = 0;
+#pragma unroll
+    for (int q = 0; q < W_E; q++) {
+      const uint32_t j = l * W_E + q;
+      v[q] = (j < S && (F[q] & EF_NONID)) ? j + 1 : 0;
+      m = v[q] > m ? v[q] : m; v[q] = m;
+      c += nb[q]; nb[q] = c;
+    }
+    uint32_t mex = wave_incl_scan_max(m); mex = __shfl_up(mex, 1, WAVE); if (l == 0) mex = 0;
+    const uint32_t cex = wave_exscan(c, nblocks);
+    uint32_t hm = 0, head[W_E];
+#pragma unroll
+    for (int q = 0; q < W_E; q++) {
+      const uint32_t j = l * W_E + q;
+      head[q] = 0;
+      if (j < S) {
+        const uint32_t lnid = (v[q] > mex ? v[q] : mex) - 1;
+        if (L.eflag[lnid] & EF_T) F[q] |= EF_EMIT;        // otherwise merged into the previous GC
+        nb[q] = nb[q] + cex - 1;
+        head[q] = (F[q] & EF_EMIT) ? j + 1 : 0;
+      }
+      hm = head[q] > hm ? head[q] : hm; head[q] = hm;
+    }
+    uint32_t hex = wave_incl_scan_max(hm); hex = __shfl_up(hex, 1, WAVE); if (l == 0) hex = 0;
+    // per-block struct counts, GC run ends
+#pragma unroll
+    for (int q = 0; q < W_E; q++) {
+      const uint32_t j = l * W_E + q;
+      if (j < S) {
+        const uint32_t cnt = ((F[q] & EF_GAP) ? 1u : 0u) + ((F[q] & EF_EMIT) ? 1u : 0u);
+        if (cnt) atomicAdd(&L.blkcnt[nb[q]], cnt);
+        const uint32_t end = (uint32_t)L.key[j] + L.r_len[L.sidx[j]];
+        const uint32_t h = (head[q] > hex ? head[q] : hex) - 1;   // this element's run head
+        atomicMax(&L.runend[h], end);
+      }
+    }
+    wave_sync();
+    // element sizes -> positions
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < W_E; q++) {
+      const uint32_t j = l * W_E + q;
+      uint32_t sz = 0;
+      if (j < S) {
+        const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
+        const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(kj >> 32), ck = (uint32_t)kj;
+        if (F[q] & EF_NEWC) sz += vu_len(L.blkcnt[nb[q]]) + vu_len(cl) + vu_len(ck);
+        if (F[q] & EF_GAP) { const uint64_t kp = L.key[j - 1]; sz += 1 + vu_len(ck - ((uint32_t)kp + L.r_len[L.sidx[j - 1]])); }
+        if (F[q] & EF_EMIT) sz += (F[q] & EF_GC) ? 1 + vu_len(L.runend[j] - ck) : L.r_out[r];
+      }
+      epos[q] = acc; acc += sz;
+    }
+    const uint32_t lb0 = wave_exscan(acc, sbytes);
+#pragma unroll
+    for (int q = 0; q < W_E; q++) epos[q] += lb0;
+    hdr0 = vu_len(nblocks);
+    DIAGW(4);
+    // ---- delete set: segments (clients, descending) and runs (rule R-DS)
+    uint64_t dv[W_DE]; uint32_t sn = 0;
+#pragma unroll
+    for (int q = 0; q < W_DE; q++) {
+      const uint32_t j = l * W_DE + q;
+      DF[q] = 0;
+      if (j < D) { if (j == 0 || (L.dkey[j - 1] >> 32) != (L.dkey[j] >> 32)) DF[q] = 1; }
+      sn += DF[q]; sid[q] = sn;
+    }
+    const uint32_t sex = wave_exscan(sn, nseg);
+    uint64_t mm = 0;
+#pragma unroll
+    for (int q = 0; q < W_DE; q++) {
+      const uint32_t j = l * W_DE + q;
+      sid[q] = sid[q] + sex - 1;
+      dv[q] = 0;
+      if (j < D) dv[q] = ((uint64_t)sid[q] << 32) | ((uint32_t)L.dkey[j] + L.dlen[j]);
+      mm = dv[q] > mm ? dv[q] : mm; dv[q] = mm;                 // inclusive running max
+    }
+    uint64_t dmex = wave_incl_scan_max(mm); dmex = __shfl_up(dmex, 1, WAVE); if (l == 0) dmex = 0;
+    uint32_t rh = 0, rhead[W_DE];
+#pragma unroll
+    for (int q = 0; q < W_DE; q++) {
+      const uint32_t j = l * W_DE + q;
+      rhead[q] = 0;
+      if (j < D) {
+        const uint64_t prev = q == 0 ? dmex : (dv[q - 1] > dmex ? dv[q - 1] : dmex);
+        const bool rs = (DF[q] & 1) || (uint32_t)L.dkey[j] > (uint32_t)prev;
+        if (rs) { DF[q] |= 2; atomicAdd(&L.segcnt[sid[q]], 1u); }
+        rhead[q] = rs ? j + 1 : 0;
+      }
+      rh = rhead[q] > rh ? rhead[q] : rh; rhead[q] = rh;
+    }
+    uint32_t rhex = wave_incl_scan_max(rh); rhex = __shfl_up(rhex, 1, WAVE); if (l == 0) rhex = 0;
+#pragma unroll
+    for (int q = 0; q < W_DE; q++) {
+      const uint32_t j = l * W_DE + q;
+      if (j < D) atomicMax(&L.drunend[(rhead[q] > rhex ? rhead[q] : rhex) - 1], (uint32_t)L.dkey[j] + L.dlen[j]);
+    }
+    wave_sync();
+    uint32_t dacc = 0;
+#pragma unroll
+    for (int q = 0; q < W_DE; q++) {
+      const uint32_t j = l * W_DE + q;
+      uint32_t sz = 0;
+      if (j < D) {
+        const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.dkey[j] >> 32), ck = (uint32_t)L.dkey[j];
+        if (DF[q] & 1) sz += vu_len(cl) + vu_len(L.segcnt[sid[q]]);
+        if (DF[q] & 2) sz += vu_len(ck) + vu_len(L.drunend[j] - ck);
+      }
+      dpos[q] = dacc; dacc += sz;
+    }
+    const uint32_t dl0 = wave_exscan(dacc, dsbytes);
+#pragma unroll
+    for (int q = 0; q < W_DE; q++) dpos[q] += dl0;
+    size = (uint64_t)hdr0 + sbytes + vu_len(nseg) + dsbytes;
+  }
+  DIAGW(5);
+  // ---- look-back (whole wave) -> this document's offset in the packed output
+  const uint64_t mysz = st == ST_OK ? size : 0;
+  const uint64_t base = lookback(lb, d, mysz, &meta->fault);
+  DIAGW(6);
+  if (d == n_docs - 1 && l == 0) meta->fast_total = base + mysz;
+  if (st == ST_OK && meta->fault) st = ST_DEVICE;
+  if (st == ST_OK && base + size > out_cap) st = ST_NOMEM;
+  if (l == 0) {
+    out_off[d] = base; out_len[d] = st == ST_OK ? size : 0;
+    status[d] = st == ST_DEFER ? ST_FALLBACK : st;
+    if (st == ST_DEFER) defer_list[atomicAdd(&meta->defer_count, 1u)] = d;
+    if (st == ST_FALLBACK) {
+      fb_list[atomicAdd(&meta->fb_count, 1u)] = d;
+      atomicAdd(&meta->fb_upds, (unsigned long long)k);
+      atomicAdd(&meta->fb_bytes, (unsigned long long)nbytes);
+    }
+  }
+  if (st != ST_OK) return;
+  uint8_t* o = out + base;
+  if (mode == 1) { if (l == 0) { o[0] = 0; o[1] = 0; } return; }
+  if (mode == 2) { for (uint64_t i = l; i < nbytes; i += WAVE) o[i] = arena[b0 + i]; return; }
+  // ---- emit: lane-contiguous segments
+  if (l == 0) { Out w{o, 0}; w.vu(nblocks); }
+  GWriter gw; gw.init(o, hdr0 + epos[0]);
+#pragma unroll
+  for (int q = 0; q < W_E; q++) {
+    const uint32_t j = l * W_E + q;
+    if (j >= S) break;
+    const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
+    const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(kj >> 32), ck = (uint32_t)kj;
+    const uint32_t f = F[q];
+    if (f & EF_NEWC) { gw.vu(L.blkcnt[nb[q]]); gw.vu(cl); gw.vu(ck); }
+    if (f & EF_GAP) { const uint64_t kp = L.key[j - 1]; gw.b(10); gw.vu(ck - ((uint32_t)kp + L.r_len[L.sidx[j - 1]])); }
+    if (f & EF_EMIT) {
+      if (f & EF_GC) { gw.b(0); gw.vu(L.runend[j] - ck); }
+      else if (!(L.r_flag[r] & 4)) {  // canonical item: input bytes, info bit 0x20 dropped when an origin is set
+        const uint32_t s0 = L.r_start[r], n = L.r_blen[r];
+        const uint8_t info = L.in[s0];
+        gw.b((info & 0xC0) ? (uint8_t)(info & ~0x20) : info);
+        for (uint32_t i = 1; i < n; i++) gw.b(L.in[s0 + i]);
+      } else {
+        gw.flush();
+        Cur c{L.in, L.r_start[r], (uint32_t)L.r_start[r] + L.r_blen[r], 0, 0};
+        SInfo si; read_struct(c, si, flags);
+        Out w{o + gw.pos, 0};
+        write_struct(w, L.in, si, cl, ck, 0, false, flags);
+        gw.jump(w.n);
+      }
+    }
+  }
+  gw.flush();
+  const uint32_t dsb = hdr0 + sbytes;
+  if (l == 0) { Out w{o + dsb, 0}; w.vu(nseg); }
+  GWriter dw; dw.init(o, dsb + vu_len(nseg) + dpos[0]);
+#pragma unroll
+  for (int q = 0; q < W_DE; q++) {
+    const uint32_t j = l * W_DE + q;
+    if (j >= D) break;
+    const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.dkey[j] >> 32), ck = (uint32_t)L.dkey[j];
+    if (DF[q] & 1) { dw.vu(cl); dw.vu(L.segcnt[sid[q]]); }
+    if (DF[q] & 2) { dw.vu(ck); dw.vu(L.drunend[j] - ck); }
+  }
+  dw.flush();
+  DIAGW(7);
 }
 
 // ======================================================================= merge sequential
@@ -468,7 +816,7 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
   }
   uint64_t at = 0;
   if (st == ST_OK) {
-    at = meta->fast_total + atomicAdd(&meta->seq_cursor, (unsigned long long)size);
+    at = meta->fast_total + meta->m_total + atomicAdd(&meta->seq_cursor, (unsigned long long)size);
     if (at + size > out_cap) st = ST_NOMEM;
   }
   if (st == ST_OK) {  // write pass: block count, structs, delete set
@@ -516,11 +864,20 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
   return (int)hipGetLastError();
 }
 
-int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
+int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta,
-                            uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
+                            uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
   if (n_docs == 0) return 0;
-  hipLaunchKernelGGL(k_merge_fast, dim3(n_docs), dim3(M_NT), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len,
+  hipLaunchKernelGGL(k_merge_wave, dim3((n_docs + W_WAVES - 1) / W_WAVES), dim3(WAVE * W_WAVES), 0, s, arena, upd_off, doc_upd, n_docs,
+                     flags, out, out_off, out_len, status, lb, (DocMeta*)meta, defer_list, fb_list, out_cap);
+  return (int)hipGetLastError();
+}
+
+int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
+                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* lb,
+                            void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
+  if (n_docs == 0) return 0;
+  hipLaunchKernelGGL(k_merge_fast, dim3(n_docs), dim3(M_NT), 0, s, arena, upd_off, doc_upd, docs, n_docs, flags, out, out_off, out_len,
                      status, lb, (DocMeta*)meta, fb_list, out_cap);
   return (int)hipGetLastError();
 }

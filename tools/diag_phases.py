@@ -23,10 +23,13 @@ for rep in range(3):
     L.ygm_diag_read(buf.ctypes.data, 1)
     e.merge_packed(arena, upd_off, upd_doc, n_docs)
     L.ygm_diag_read(buf.ctypes.data, 0)
-names = ["stage", "passA", "scan+passB", "sort", "classify", "deleteset", "lookback", "emit"]
-tot = buf[:8].sum()
-print("per-document shader cycles (mean over docs, last rep):")
-for i, nm in enumerate(names):
-    print(f"  {nm:16s} {buf[i] / n_docs:12.0f}  {100.0 * buf[i] / max(tot, 1):5.1f}%")
+for title, names, lo in (("k_merge_wave (wave per document)", ["stage", "passA", "passB", "sort", "classify+scan", "deleteset", "lookback", "emit"], 8),
+                         ("k_merge_fast (workgroup per document)", ["stage", "passA", "scan+passB", "sort", "classify", "deleteset", "lookback", "emit"], 0)):
+    tot = buf[lo:lo + 8].sum()
+    if tot == 0:
+        continue
+    print(title, "- shader cycles per document (mean, last rep):")
+    for i, nm in enumerate(names):
+        print(f"  {nm:16s} {buf[lo + i] / n_docs:12.0f}  {100.0 * buf[lo + i] / max(tot, 1):5.1f}%")
 s = e.stats()
 print("kernel_ms (3 reps)", s.kernel_ms)

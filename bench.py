@@ -117,12 +117,14 @@ def main():
     algo_bytes = len(arena) + out_bytes              # per step, this rank
     kernel_ms = (s1.kernel_ms - s0.kernel_ms) / args.steps
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    tot = torch.tensor([float(algo_bytes), float(args.docs), float(s1.docs_seq - s0.docs_seq)], dtype=torch.float64, device=dev)
     if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)   # the job's time = the slowest rank
     dt = float(t.item())
-    all_bytes, all_docs = float(tot[0].item()), float(tot[1].item())
+    # node-wide stats all-gather (the only other collective; no update data crosses GPUs)
+    from hocuspocus_amd.shard import gather_stats
+    node = gather_stats({"docs": args.docs, "updates": n_upd, "bytes_in": len(arena), "bytes_out": out_bytes,
+                         "docs_seq": s1.docs_seq - s0.docs_seq, "kernel_ms": kernel_ms}, dist, dev)
+    all_bytes, all_docs = node["bytes_in"] + node["bytes_out"], node["docs"]
 
     # ---- parity spot-check of the timed outputs (rank 0 sample vs the CPU oracle)
     parity = None
@@ -165,12 +167,12 @@ def main():
                        "docs_per_gpu": args.docs, "updates_per_gpu": n_upd, "bytes_in_per_gpu": len(arena),
                        "bytes_out_per_gpu": out_bytes, "parallelism": f"doc-sharded x{world}"},
             "docs_per_s": round(all_docs * args.steps / dt, 1),
-            "roofline": {"bound": "hbm", "kernel": "k_merge_fast",
+            "roofline": {"bound": "hbm", "kernel": "k_merge_wave (+k_merge_fast for deferred docs)",
                          "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5) if achieved else None,
                          "kernel_ms": round(kernel_ms, 4), "traffic": _pmc_traffic()},
             "parity": parity,
-            "seq_kernel_docs": float(tot[2].item()),
+            "seq_kernel_docs": node["docs_seq"],
         }
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(arena, upd_off, doc_upd, args.cpu_seconds)

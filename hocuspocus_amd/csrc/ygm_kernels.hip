@@ -435,6 +435,8 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
 
 
 // ======================================================================= merge: one wave per document
+// Per-element state lives in LDS (eflag/eblk/epos, dflag/dsid/dposs) and every
+// per-element loop is rolled: the kernel stays small enough for the I-cache.
 __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                                const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t flags,
                                                                uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
@@ -457,12 +459,6 @@ __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __
   int st = ST_OK, mode = 0;
   uint64_t size = 0;
   uint32_t S = 0, D = 0, nblocks = 0, nseg = 0, hdr0 = 0, sbytes = 0, dsbytes = 0;
-  uint32_t F[W_E], nb[W_E], epos[W_E];
-  uint32_t DF[W_DE], sid[W_DE], dpos[W_DE];
-#pragma unroll
-  for (int q = 0; q < W_E; q++) { F[q] = 0; nb[q] = 0; epos[q] = 0; }
-#pragma unroll
-  for (int q = 0; q < W_DE; q++) { DF[q] = 0; sid[q] = 0; dpos[q] = 0; }
   if (k == 0) { mode = 1; size = 2; }
   else if (k == 1) { mode = 2; size = nbytes; }
   else if (k > (uint32_t)W_K || nbytes + 16 > (uint64_t)W_IN || (flags & 2u)) st = ST_DEFER;
@@ -479,228 +475,186 @@ __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __
     wave_sync();
     DIAGW(0);
     // ---- pass A: validate + count; lane l parses updates l*R .. l*R+R-1
+    LWave* LW = (LWave*)&L;
     const uint32_t R = (k + WAVE - 1) / WAVE;
-    uint32_t ns[W_R], nd[W_R];
     int err = 0; bool fb = false, nc = false;
-#pragma unroll
-    for (int r = 0; r < W_R; r++) {
-      ns[r] = 0; nd[r] = 0;
+    uint32_t sl = 0, dl = 0;
+    for (uint32_t r = 0; r < R; r++) {
       const uint32_t i = l * R + r;
-      if ((uint32_t)r < R && i < k) { const UpdCount c = w_parse_update(L, (int)i, false, 0, 0, flags, err, fb, nc); ns[r] = c.ns; nd[r] = c.nd; }
+      if (i < k) {
+        const UpdCount c = w_parse_update(LW, (int)i, false, 0, 0, flags);
+        L.uns[i] = (uint16_t)(c.ns > 0xFFFF ? 0xFFFF : c.ns); L.und[i] = (uint16_t)(c.nd > 0xFFFF ? 0xFFFF : c.nd);
+        sl += c.ns; dl += c.nd;
+        if (c.err && !err) err = c.err;
+        fb |= c.fb != 0; nc |= c.nc != 0;
+      }
     }
     DIAGW(1);
     const unsigned long long eb = __ballot(err != 0);
     if (eb) st = __shfl(err, __ffsll((long long)eb) - 1, WAVE);
     else if (__ballot(fb)) st = ST_DEFER;
     else {
-      uint32_t sl = 0, dl = 0;
-#pragma unroll
-      for (int r = 0; r < W_R; r++) { sl += ns[r]; dl += nd[r]; }
-      uint32_t sb = wave_exscan(sl, S), db = wave_exscan(dl, D);
+      (void)wave_exscan(sl, S); (void)wave_exscan(dl, D);
       if (S > (uint32_t)W_S || D > (uint32_t)W_D || ((flags & F_COMPAT_135) && D > 0)) st = ST_DEFER;
       else if (__ballot(nc)) st = ST_NONCANON;
-      else {
-        // ---- pass B: records
-#pragma unroll
-        for (int r = 0; r < W_R; r++) {
-          const uint32_t i = l * R + r;
-          if ((uint32_t)r < R && i < k && (ns[r] | nd[r])) { int e2 = 0; bool f2 = false, n2 = false; w_parse_update(L, (int)i, true, sb, db, flags, e2, f2, n2); }
-          sb += ns[r]; db += nd[r];
+    }
+    if (st == ST_OK) {
+      // ---- pass B: records
+      uint32_t sb, db, tS, tD;
+      sb = wave_exscan(sl, tS); db = wave_exscan(dl, tD);
+      for (uint32_t r = 0; r < R; r++) {
+        const uint32_t i = l * R + r;
+        if (i < k) {
+          const uint32_t ns = L.uns[i], nd = L.und[i];
+          if (ns | nd) w_parse_update(LW, (int)i, true, sb, db, flags);
+          sb += ns; db += nd;
         }
-        wave_sync();
-        DIAGW(2);
-        // ---- rank sort of struct keys (ties by record id; equal keys are caught as overlap)
-        {
-          uint64_t mk[W_E]; uint32_t rk[W_E];
-#pragma unroll
-          for (int q = 0; q < W_E; q++) { const uint32_t j = l + WAVE * q; mk[q] = j < S ? L.key[j] : ~0ull; rk[q] = 0; }
-          for (uint32_t i = 0; i < S; i++) {
-            const uint64_t ki = L.key[i];
-#pragma unroll
-            for (int q = 0; q < W_E; q++) rk[q] += (ki < mk[q]) || (ki == mk[q] && i < l + WAVE * q);
-          }
-          wave_sync();
-#pragma unroll
-          for (int q = 0; q < W_E; q++) { const uint32_t j = l + WAVE * q; if (j < S) { L.key[rk[q]] = mk[q]; L.sidx[rk[q]] = (uint16_t)j; } }
-        }
-        {
-          uint64_t mk[W_DE]; uint32_t ml[W_DE], rk[W_DE];
-#pragma unroll
-          for (int q = 0; q < W_DE; q++) { const uint32_t j = l + WAVE * q; mk[q] = j < D ? L.dkey[j] : ~0ull; ml[q] = j < D ? L.dlen[j] : 0; rk[q] = 0; }
-          for (uint32_t i = 0; i < D; i++) {
-            const uint64_t ki = L.dkey[i];
-#pragma unroll
-            for (int q = 0; q < W_DE; q++) rk[q] += (ki < mk[q]) || (ki == mk[q] && i < l + WAVE * q);
-          }
-          wave_sync();
-#pragma unroll
-          for (int q = 0; q < W_DE; q++) { const uint32_t j = l + WAVE * q; if (j < D) { L.dkey[rk[q]] = mk[q]; L.dlen[rk[q]] = ml[q]; } }
-        }
-        DIAGW(3);
-        for (uint32_t j = l; j < S; j += WAVE) L.runend[j] = 0;
-        for (uint32_t j = l; j < D; j += WAVE) L.drunend[j] = 0;
-        for (uint32_t j = l; j < W_BLK; j += WAVE) { L.blkcnt[j] = 0; L.segcnt[j] = 0; }
-        wave_sync();
-        // ---- classify sorted structs (blocked: lane l owns l*W_E .. l*W_E+W_E-1)
-        uint32_t v[W_E];
-        bool ovl = false;
+      }
+      wave_sync();
+      DIAGW(2);
+      // ---- rank sort (ties by record id; equal struct keys are caught below as overlap)
+      for (int pass = 0; pass < 2; pass++) {
+        const uint32_t n = pass ? D : S;
+        uint64_t mk[W_E]; uint32_t ml[W_E], rk[W_E];
 #pragma unroll
         for (int q = 0; q < W_E; q++) {
-          const uint32_t j = l * W_E + q;
-          v[q] = 0;
-          if (j < S) {
-            const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
-            uint32_t f = (L.r_flag[r] & 3) == K_GC ? EF_GC : 0;
-            if (j == 0) f |= EF_NEWC;
-            else {
-              const uint64_t kp = L.key[j - 1]; const uint32_t rp = L.sidx[j - 1];
-              const uint32_t pend = (uint32_t)kp + L.r_len[rp];
-              if ((uint32_t)(kp >> 32) != (uint32_t)(kj >> 32)) f |= EF_NEWC;
-              else if ((uint32_t)kj < pend) ovl = true;
-              else if ((uint32_t)kj > pend) f |= EF_GAP;
-              else {
-                const uint32_t ss = L.r_ss[r], sp = L.r_ss[rp];
-                if ((ss >> 8) == (sp >> 8) && (ss & 0xFF) == (sp & 0xFF) + 1) f |= EF_SDN;
-                if ((f & EF_GC) && (L.r_flag[rp] & 3) == K_GC) f |= EF_CGG;
-              }
-            }
-            if (!(f & EF_CGG)) f |= EF_NONID | EF_T;
-            else if (!(f & EF_SDN)) f |= EF_NONID;
-            F[q] = f;
-            v[q] = (f & EF_NONID) ? j + 1 : 0;
-            nb[q] = (f & EF_NEWC) ? 1 : 0;
-            L.eflag[j] = (uint8_t)f;
+          const uint32_t j = l + WAVE * q;
+          mk[q] = j < n ? (pass ? L.dkey[j] : L.key[j]) : ~0ull; ml[q] = (pass && j < n) ? L.dlen[j] : 0; rk[q] = 0;
+        }
+        for (uint32_t i = 0; i < n; i++) {
+          const uint64_t ki = pass ? L.dkey[i] : L.key[i];
+#pragma unroll
+          for (int q = 0; q < W_E; q++) rk[q] += (ki < mk[q]) || (ki == mk[q] && i < l + WAVE * q);
+        }
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < W_E; q++) {
+          const uint32_t j = l + WAVE * q;
+          if (j < n) { if (pass) { L.dkey[rk[q]] = mk[q]; L.dlen[rk[q]] = ml[q]; } else { L.key[rk[q]] = mk[q]; L.sidx[rk[q]] = (uint16_t)j; } }
+        }
+      }
+      for (uint32_t j = l; j < S; j += WAVE) L.runend[j] = 0;
+      for (uint32_t j = l; j < D; j += WAVE) L.drunend[j] = 0;
+      for (uint32_t j = l; j < W_BLK; j += WAVE) { L.blkcnt[j] = 0; L.segcnt[j] = 0; }
+      wave_sync();
+      DIAGW(3);
+      // ---- classify sorted structs (blocked: lane l owns elements l*W_E .. l*W_E+W_E-1)
+      const uint32_t e0 = l * W_E, e1 = min(e0 + W_E, S);
+      bool ovl = false;
+      uint32_t vmax = 0, nnew = 0;
+      for (uint32_t j = e0; j < e1; j++) {
+        const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
+        uint32_t f = (L.r_flag[r] & 3) == K_GC ? EF_GC : 0;
+        if (j == 0) f |= EF_NEWC;
+        else {
+          const uint64_t kp = L.key[j - 1]; const uint32_t rp = L.sidx[j - 1];
+          const uint32_t pend = (uint32_t)kp + L.r_len[rp];
+          if ((uint32_t)(kp >> 32) != (uint32_t)(kj >> 32)) f |= EF_NEWC;
+          else if ((uint32_t)kj < pend) ovl = true;
+          else if ((uint32_t)kj > pend) f |= EF_GAP;
+          else {
+            const uint32_t ss = L.r_ss[r], sp = L.r_ss[rp];
+            if ((ss >> 8) == (sp >> 8) && (ss & 0xFF) == (sp & 0xFF) + 1) f |= EF_SDN;
+            if ((f & EF_GC) && (L.r_flag[rp] & 3) == K_GC) f |= EF_CGG;
           }
         }
-        if (__ballot(ovl)) st = ST_FALLBACK;  // overlapping structs: exact sequential replay
-        else {
-          // client blocks and delete-set clients must fit the W_BLK counters
-          uint32_t nbk = 0, nsg = 0;
-#pragma unroll
-          for (int q = 0; q < W_E; q++) nbk += nb[q];
-          for (uint32_t j = l; j < D; j += WAVE) nsg += (j == 0 || (L.dkey[j - 1] >> 32) != (L.dkey[j] >> 32)) ? 1u : 0u;
-          if (wave_sum(nbk) > (uint32_t)W_BLK || wave_sum(nsg) > (uint32_t)W_BLK) st = ST_DEFER;
+        if (!(f & EF_CGG)) f |= EF_NONID | EF_T;
+        else if (!(f & EF_SDN)) f |= EF_NONID;
+        L.eflag[j] = (uint8_t)f;
+        if (f & EF_NONID) vmax = j + 1;
+        nnew += (f & EF_NEWC) ? 1 : 0;
+      }
+      uint32_t nsg = 0;
+      for (uint32_t j = l; j < D; j += WAVE) nsg += (j == 0 || (L.dkey[j - 1] >> 32) != (L.dkey[j] >> 32)) ? 1u : 0u;
+      if (__ballot(ovl)) st = ST_FALLBACK;  // overlapping structs: exact sequential replay
+      else if (wave_sum(nnew) > (uint32_t)W_BLK || wave_sum(nsg) > (uint32_t)W_BLK) st = ST_DEFER;
+      else {
+        wave_sync();
+        // last non-identity element <= j (max-scan) and block index (count of NEWC <= j, minus 1)
+        uint32_t mex = wave_incl_scan_max(vmax); mex = __shfl_up(mex, 1, WAVE); if (l == 0) mex = 0;
+        uint32_t cex = wave_exscan(nnew, nblocks);
+        uint32_t hmax = 0, lastnid = mex, blk = cex;
+        for (uint32_t j = e0; j < e1; j++) {
+          uint32_t f = L.eflag[j];
+          if (f & EF_NONID) lastnid = j + 1;
+          if (L.eflag[lastnid - 1] & EF_T) f |= EF_EMIT;   // otherwise merged into the previous GC
+          L.eflag[j] = (uint8_t)f;
+          blk += (f & EF_NEWC) ? 1 : 0;
+          L.eblk[j] = (uint8_t)(blk - 1);
+          if (f & EF_EMIT) hmax = j + 1;
         }
+        uint32_t hex = wave_incl_scan_max(hmax); hex = __shfl_up(hex, 1, WAVE); if (l == 0) hex = 0;
+        // per-block struct counts, GC run ends (LDS atomics)
+        uint32_t head = hex;
+        for (uint32_t j = e0; j < e1; j++) {
+          const uint32_t f = L.eflag[j];
+          if (f & EF_EMIT) head = j + 1;
+          const uint32_t cnt = ((f & EF_GAP) ? 1u : 0u) + ((f & EF_EMIT) ? 1u : 0u);
+          if (cnt) atomicAdd(&L.blkcnt[L.eblk[j]], cnt);
+          atomicMax(&L.runend[head - 1], (uint32_t)L.key[j] + L.r_len[L.sidx[j]]);
+        }
+        wave_sync();
+        // element sizes -> positions (epos, relative to the struct section)
+        uint32_t acc = 0;
+        for (uint32_t j = e0; j < e1; j++) {
+          const uint32_t f = L.eflag[j];
+          const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
+          const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(kj >> 32), ck = (uint32_t)kj;
+          uint32_t sz = 0;
+          if (f & EF_NEWC) sz += vu_len(L.blkcnt[L.eblk[j]]) + vu_len(cl) + vu_len(ck);
+          if (f & EF_GAP) { const uint64_t kp = L.key[j - 1]; sz += 1 + vu_len(ck - ((uint32_t)kp + L.r_len[L.sidx[j - 1]])); }
+          if (f & EF_EMIT) sz += (f & EF_GC) ? 1 + vu_len(L.runend[j] - ck) : L.r_out[r];
+          L.epos[j] = (uint16_t)acc; acc += sz;
+        }
+        const uint32_t lb0 = wave_exscan(acc, sbytes);
+        for (uint32_t j = e0; j < e1; j++) L.epos[j] = (uint16_t)(L.epos[j] + lb0);
+        hdr0 = vu_len(nblocks);
+        DIAGW(4);
+        // ---- delete set: segments (clients, descending) and runs (rule R-DS); lane owns d0 .. d1-1
+        const uint32_t d0 = l * W_DE, d1 = min(d0 + W_DE, D);
+        uint32_t sn = 0; uint64_t mm = 0;
+        for (uint32_t j = d0; j < d1; j++) {
+          const bool sg = j == 0 || (L.dkey[j - 1] >> 32) != (L.dkey[j] >> 32);
+          L.dflag[j] = sg ? 1 : 0;
+          sn += sg ? 1 : 0;
+        }
+        const uint32_t sex = wave_exscan(sn, nseg);
+        uint32_t sidr = sex;
+        for (uint32_t j = d0; j < d1; j++) {
+          sidr += L.dflag[j] & 1;
+          L.dsid[j] = (uint8_t)(sidr - 1);
+          const uint64_t v = ((uint64_t)(sidr - 1) << 32) | ((uint32_t)L.dkey[j] + L.dlen[j]);
+          mm = v > mm ? v : mm;
+        }
+        uint64_t dmex = wave_incl_scan_max(mm); dmex = __shfl_up(dmex, 1, WAVE); if (l == 0) dmex = 0;
+        uint64_t runmax = dmex; uint32_t rh = 0;
+        for (uint32_t j = d0; j < d1; j++) {
+          const uint32_t sidj = L.dsid[j];
+          const bool rs = (L.dflag[j] & 1) || (uint32_t)L.dkey[j] > (uint32_t)runmax;
+          if (rs) { L.dflag[j] |= 2; atomicAdd(&L.segcnt[sidj], 1u); rh = j + 1; }
+          const uint64_t v = ((uint64_t)sidj << 32) | ((uint32_t)L.dkey[j] + L.dlen[j]);
+          runmax = v > runmax ? v : runmax;
+        }
+        uint32_t rhex = wave_incl_scan_max(rh); rhex = __shfl_up(rhex, 1, WAVE); if (l == 0) rhex = 0;
+        uint32_t rhead = rhex;
+        for (uint32_t j = d0; j < d1; j++) {
+          if (L.dflag[j] & 2) rhead = j + 1;
+          atomicMax(&L.drunend[rhead - 1], (uint32_t)L.dkey[j] + L.dlen[j]);
+        }
+        wave_sync();
+        uint32_t dacc = 0;
+        for (uint32_t j = d0; j < d1; j++) {
+          const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.dkey[j] >> 32), ck = (uint32_t)L.dkey[j];
+          uint32_t sz = 0;
+          if (L.dflag[j] & 1) sz += vu_len(cl) + vu_len(L.segcnt[L.dsid[j]]);
+          if (L.dflag[j] & 2) sz += vu_len(ck) + vu_len(L.drunend[j] - ck);
+          L.dposs[j] = (uint16_t)dacc; dacc += sz;
+        }
+        const uint32_t dl0 = wave_exscan(dacc, dsbytes);
+        for (uint32_t j = d0; j < d1; j++) L.dposs[j] = (uint16_t)(L.dposs[j] + dl0);
+        size = (uint64_t)hdr0 + sbytes + vu_len(nseg) + dsbytes;
       }
     }
-  }
-  if (mode == 0 && st == ST_OK) {
-    wave_sync();
-    // last non-identity element <= j (max-scan) and block index (count of NEWC <= j, minus 1)
-    uint32_t v[W_E];
-    uint32_t m = 0, c = 0;
-#pragma unroll
-    for (int q = 0; q < W_E; q++) {
-      const uint32_t j = l * W_E + q;
-      v[q] = (j < S && (F[q] & EF_NONID)) ? j + 1 : 0;
-      m = v[q] > m ? v[q] : m; v[q] = m;
-      c += nb[q]; nb[q] = c;
-    }
-    uint32_t mex = wave_incl_scan_max(m); mex = __shfl_up(mex, 1, WAVE); if (l == 0) mex = 0;
-    const uint32_t cex = wave_exscan(c, nblocks);
-    uint32_t hm = 0, head[W_E];
-#pragma unroll
-    for (int q = 0; q < W_E; q++) {
-      const uint32_t j = l * W_E + q;
-      head[q] = 0;
-      if (j < S) {
-        const uint32_t lnid = (v[q] > mex ? v[q] : mex) - 1;
-        if (L.eflag[lnid] & EF_T) F[q] |= EF_EMIT;        // otherwise merged into the previous GC
-        nb[q] = nb[q] + cex - 1;
-        head[q] = (F[q] & EF_EMIT) ? j + 1 : 0;
-      }
-      hm = head[q] > hm ? head[q] : hm; head[q] = hm;
-    }
-    uint32_t hex = wave_incl_scan_max(hm); hex = __shfl_up(hex, 1, WAVE); if (l == 0) hex = 0;
-    // per-block struct counts, GC run ends
-#pragma unroll
-    for (int q = 0; q < W_E; q++) {
-      const uint32_t j = l * W_E + q;
-      if (j < S) {
-        const uint32_t cnt = ((F[q] & EF_GAP) ? 1u : 0u) + ((F[q] & EF_EMIT) ? 1u : 0u);
-        if (cnt) atomicAdd(&L.blkcnt[nb[q]], cnt);
-        const uint32_t end = (uint32_t)L.key[j] + L.r_len[L.sidx[j]];
-        const uint32_t h = (head[q] > hex ? head[q] : hex) - 1;   // this element's run head
-        atomicMax(&L.runend[h], end);
-      }
-    }
-    wave_sync();
-    // element sizes -> positions
-    uint32_t acc = 0;
-#pragma unroll
-    for (int q = 0; q < W_E; q++) {
-      const uint32_t j = l * W_E + q;
-      uint32_t sz = 0;
-      if (j < S) {
-        const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
-        const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(kj >> 32), ck = (uint32_t)kj;
-        if (F[q] & EF_NEWC) sz += vu_len(L.blkcnt[nb[q]]) + vu_len(cl) + vu_len(ck);
-        if (F[q] & EF_GAP) { const uint64_t kp = L.key[j - 1]; sz += 1 + vu_len(ck - ((uint32_t)kp + L.r_len[L.sidx[j - 1]])); }
-        if (F[q] & EF_EMIT) sz += (F[q] & EF_GC) ? 1 + vu_len(L.runend[j] - ck) : L.r_out[r];
-      }
-      epos[q] = acc; acc += sz;
-    }
-    const uint32_t lb0 = wave_exscan(acc, sbytes);
-#pragma unroll
-    for (int q = 0; q < W_E; q++) epos[q] += lb0;
-    hdr0 = vu_len(nblocks);
-    DIAGW(4);
-    // ---- delete set: segments (clients, descending) and runs (rule R-DS)
-    uint64_t dv[W_DE]; uint32_t sn = 0;
-#pragma unroll
-    for (int q = 0; q < W_DE; q++) {
-      const uint32_t j = l * W_DE + q;
-      DF[q] = 0;
-      if (j < D) { if (j == 0 || (L.dkey[j - 1] >> 32) != (L.dkey[j] >> 32)) DF[q] = 1; }
-      sn += DF[q]; sid[q] = sn;
-    }
-    const uint32_t sex = wave_exscan(sn, nseg);
-    uint64_t mm = 0;
-#pragma unroll
-    for (int q = 0; q < W_DE; q++) {
-      const uint32_t j = l * W_DE + q;
-      sid[q] = sid[q] + sex - 1;
-      dv[q] = 0;
-      if (j < D) dv[q] = ((uint64_t)sid[q] << 32) | ((uint32_t)L.dkey[j] + L.dlen[j]);
-      mm = dv[q] > mm ? dv[q] : mm; dv[q] = mm;                 // inclusive running max
-    }
-    uint64_t dmex = wave_incl_scan_max(mm); dmex = __shfl_up(dmex, 1, WAVE); if (l == 0) dmex = 0;
-    uint32_t rh = 0, rhead[W_DE];
-#pragma unroll
-    for (int q = 0; q < W_DE; q++) {
-      const uint32_t j = l * W_DE + q;
-      rhead[q] = 0;
-      if (j < D) {
-        const uint64_t prev = q == 0 ? dmex : (dv[q - 1] > dmex ? dv[q - 1] : dmex);
-        const bool rs = (DF[q] & 1) || (uint32_t)L.dkey[j] > (uint32_t)prev;
-        if (rs) { DF[q] |= 2; atomicAdd(&L.segcnt[sid[q]], 1u); }
-        rhead[q] = rs ? j + 1 : 0;
-      }
-      rh = rhead[q] > rh ? rhead[q] : rh; rhead[q] = rh;
-    }
-    uint32_t rhex = wave_incl_scan_max(rh); rhex = __shfl_up(rhex, 1, WAVE); if (l == 0) rhex = 0;
-#pragma unroll
-    for (int q = 0; q < W_DE; q++) {
-      const uint32_t j = l * W_DE + q;
-      if (j < D) atomicMax(&L.drunend[(rhead[q] > rhex ? rhead[q] : rhex) - 1], (uint32_t)L.dkey[j] + L.dlen[j]);
-    }
-    wave_sync();
-    uint32_t dacc = 0;
-#pragma unroll
-    for (int q = 0; q < W_DE; q++) {
-      const uint32_t j = l * W_DE + q;
-      uint32_t sz = 0;
-      if (j < D) {
-        const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.dkey[j] >> 32), ck = (uint32_t)L.dkey[j];
-        if (DF[q] & 1) sz += vu_len(cl) + vu_len(L.segcnt[sid[q]]);
-        if (DF[q] & 2) sz += vu_len(ck) + vu_len(L.drunend[j] - ck);
-      }
-      dpos[q] = dacc; dacc += sz;
-    }
-    const uint32_t dl0 = wave_exscan(dacc, dsbytes);
-#pragma unroll
-    for (int q = 0; q < W_DE; q++) dpos[q] += dl0;
-    size = (uint64_t)hdr0 + sbytes + vu_len(nseg) + dsbytes;
   }
   DIAGW(5);
   // ---- look-back (whole wave) -> this document's offset in the packed output
@@ -726,15 +680,13 @@ __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __
   if (mode == 2) { for (uint64_t i = l; i < nbytes; i += WAVE) o[i] = arena[b0 + i]; return; }
   // ---- emit: lane-contiguous segments
   if (l == 0) { Out w{o, 0}; w.vu(nblocks); }
-  GWriter gw; gw.init(o, hdr0 + epos[0]);
-#pragma unroll
-  for (int q = 0; q < W_E; q++) {
-    const uint32_t j = l * W_E + q;
-    if (j >= S) break;
+  const uint32_t e0 = l * W_E, e1 = min(e0 + W_E, S);
+  GWriter gw; gw.init(o, hdr0 + (e0 < S ? L.epos[e0] : sbytes));
+  for (uint32_t j = e0; j < e1; j++) {
+    const uint32_t f = L.eflag[j];
     const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
     const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(kj >> 32), ck = (uint32_t)kj;
-    const uint32_t f = F[q];
-    if (f & EF_NEWC) { gw.vu(L.blkcnt[nb[q]]); gw.vu(cl); gw.vu(ck); }
+    if (f & EF_NEWC) { gw.vu(L.blkcnt[L.eblk[j]]); gw.vu(cl); gw.vu(ck); }
     if (f & EF_GAP) { const uint64_t kp = L.key[j - 1]; gw.b(10); gw.vu(ck - ((uint32_t)kp + L.r_len[L.sidx[j - 1]])); }
     if (f & EF_EMIT) {
       if (f & EF_GC) { gw.b(0); gw.vu(L.runend[j] - ck); }
@@ -756,14 +708,12 @@ __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __
   gw.flush();
   const uint32_t dsb = hdr0 + sbytes;
   if (l == 0) { Out w{o + dsb, 0}; w.vu(nseg); }
-  GWriter dw; dw.init(o, dsb + vu_len(nseg) + dpos[0]);
-#pragma unroll
-  for (int q = 0; q < W_DE; q++) {
-    const uint32_t j = l * W_DE + q;
-    if (j >= D) break;
+  const uint32_t d0 = l * W_DE, d1 = min(d0 + W_DE, D);
+  GWriter dw; dw.init(o, dsb + vu_len(nseg) + (d0 < D ? L.dposs[d0] : dsbytes));
+  for (uint32_t j = d0; j < d1; j++) {
     const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.dkey[j] >> 32), ck = (uint32_t)L.dkey[j];
-    if (DF[q] & 1) { dw.vu(cl); dw.vu(L.segcnt[sid[q]]); }
-    if (DF[q] & 2) { dw.vu(ck); dw.vu(L.drunend[j] - ck); }
+    if (L.dflag[j] & 1) { dw.vu(cl); dw.vu(L.segcnt[L.dsid[j]]); }
+    if (L.dflag[j] & 2) { dw.vu(ck); dw.vu(L.drunend[j] - ck); }
   }
   dw.flush();
   DIAGW(7);

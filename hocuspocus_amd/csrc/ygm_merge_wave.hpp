@@ -30,6 +30,7 @@ constexpr int W_BLK = 64;      // client blocks (struct section) and delete-set 
 struct WaveLds {
   uint8_t in[W_IN + 32];
   uint16_t ustart[W_K], ulen[W_K];
+  uint16_t uns[W_K], und[W_K];   // per-update struct / delete-range counts (pass A)
   uint64_t key[W_S];         // by record id; permuted in place into rank order by the sort
   uint16_t sidx[W_S];        // rank -> record id
   uint16_t r_start[W_S], r_blen[W_S], r_ss[W_S];
@@ -37,6 +38,10 @@ struct WaveLds {
   uint8_t r_flag[W_S];       // bits 0-1 kind, bit 2 slow-emit
   uint16_t r_out[W_S];       // re-encoded byte length of an item
   uint8_t eflag[W_S];        // per sorted element: EF_* bits
+  uint8_t eblk[W_S];         // per sorted element: client-block index (< W_BLK)
+  uint16_t epos[W_S];        // per sorted element: output offset inside the struct section
+  uint8_t dflag[W_D], dsid[W_D];
+  uint16_t dposs[W_D];
   uint32_t blkcnt[W_BLK];
   uint32_t runend[W_S];
   uint64_t dkey[W_D];        // permuted in place into rank order
@@ -44,6 +49,10 @@ struct WaveLds {
   uint32_t segcnt[W_BLK];
   uint32_t drunend[W_D];
 };
+
+// LDS-typed views: keep ds_* addressing across non-inlined helpers
+typedef __attribute__((address_space(3))) WaveLds LWave;
+typedef __attribute__((address_space(3))) const uint8_t LU8;
 
 YDEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -53,16 +62,17 @@ YDEV void wave_sync() {
 
 // Byte reader over an 8-byte-aligned LDS buffer: one ds_read_b64 per 8 bytes.
 struct WinRd {
-  const uint8_t* base;
+  LU8* base;
   uint32_t pos, end, wat;
   uint64_t win;
   int err, nm;
-  YDEV void init(const uint8_t* b, uint32_t p, uint32_t e) { base = b; pos = p; end = e; wat = 0xFFFFFFFFu; win = 0; err = 0; nm = 0; }
+  YDEV void init(LU8* b, uint32_t p, uint32_t e) { base = b; pos = p; end = e; wat = 0xFFFFFFFFu; win = 0; err = 0; nm = 0; }
   YDEV void fail(int e) { if (!err) err = e; pos = end; }
+  YDEV const uint8_t* generic() const { return (const uint8_t*)base; }
   YDEV uint8_t u8() {
     if (pos >= end) { fail(ST_MALFORMED); return 0; }
     const uint32_t a = pos & ~7u;
-    if (a != wat) { wat = a; win = *(const uint64_t*)(base + a); }
+    if (a != wat) { wat = a; win = *(__attribute__((address_space(3))) const uint64_t*)(base + a); }
     const uint8_t v = (uint8_t)(win >> ((pos & 7u) * 8u));
     pos++;
     return v;
@@ -125,12 +135,12 @@ YDEV void w_struct(WinRd& r, uint32_t flags, uint8_t& kind, uint64_t& len, uint3
   if (fast) {
     out_len = r.pos - start;
     slow = r.nm != 0;  // a non-minimal varuint: the writer re-encodes (different length)
-    if (slow) { Out o{nullptr, 0}; Cur c{r.base, start, r.end, 0, 0}; SInfo si; read_struct(c, si, flags); write_struct(o, r.base, si, 0, 0, 0, false, flags); out_len = o.n; }
+    if (slow) { Out o{nullptr, 0}; Cur c{r.generic(), start, r.end, 0, 0}; SInfo si; read_struct(c, si, flags); write_struct(o, r.generic(), si, 0, 0, 0, false, flags); out_len = o.n; }
     r.nm = nm0;
     return;
   }
   // general path (noinline validator over a generic pointer)
-  Cur c{r.base, start, r.end, 0, 0};
+  Cur c{r.generic(), start, r.end, 0, 0};
   SInfo si; read_struct(c, si, flags);
   if (c.err) { r.fail(c.err); return; }
   r.pos = c.pos; r.wat = 0xFFFFFFFFu;
@@ -138,7 +148,7 @@ YDEV void w_struct(WinRd& r, uint32_t flags, uint8_t& kind, uint64_t& len, uint3
   Out o{nullptr, 0};
   const bool hdr_nm = c.nm != 0;
   slow = si.renc || hdr_nm || true;  // general-path items are always written by write_struct
-  if (!si.nc) write_struct(o, r.base, si, 0, 0, 0, false, flags);
+  if (!si.nc) write_struct(o, r.generic(), si, 0, 0, 0, false, flags);
   out_len = o.n;
   r.nm = nm0;
 }
@@ -167,7 +177,8 @@ struct GWriter {
     }
     acc = 0;
   }
-  YDEV void jump(uint64_t n) { flush(); pos += n; seg_start = pos; }  // bytes written elsewhere
+  // n bytes were written at pos by someone else (after a flush()): skip them
+  YDEV void jump(uint64_t n) { pos += n; seg_start = pos; acc = 0; }
 };
 
 YDEV uint32_t wave_exscan(uint32_t v, uint32_t& total) {
@@ -176,12 +187,13 @@ YDEV uint32_t wave_exscan(uint32_t v, uint32_t& total) {
   return inc - v;
 }
 
-// parse pass over update i: counts (pass 0) or record writes (pass 1)
-struct UpdCount { uint32_t ns, nd; };
-YDEV UpdCount w_parse_update(WaveLds& L, int i, bool write, uint32_t sbase, uint32_t dbase, uint32_t flags, int& err,
-                             bool& fb, bool& nc) {
-  WinRd r; r.init(L.in, L.ustart[i], (uint32_t)L.ustart[i] + L.ulen[i]);
-  UpdCount uc{0, 0};
+// parse pass over update i: counts (pass A) or record writes (pass B).  One
+// non-inlined instance (LDS-typed pointer, results by value in registers).
+struct UpdCount { uint32_t ns, nd; int err; uint32_t fb, nc; };
+YDEV_NI UpdCount w_parse_update(LWave* L, int i, bool write, uint32_t sbase, uint32_t dbase, uint32_t flags) {
+  WinRd r; r.init(L->in, L->ustart[i], (uint32_t)L->ustart[i] + L->ulen[i]);
+  UpdCount uc{0, 0, 0, 0, 0};
+  bool fb = false, nc = false;
   uint64_t prev_client = 0, prev_end = 0; bool have_prev = false;
   const uint64_t nb = r.vu();
   for (uint64_t b = 0; b < nb && !r.err; b++) {
@@ -203,11 +215,11 @@ YDEV UpdCount w_parse_update(WaveLds& L, int i, bool write, uint32_t sbase, uint
         if (write && !fb) {
           const uint32_t j = sbase + uc.ns;
           if (j < (uint32_t)W_S) {
-            L.key[j] = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | (uint32_t)clock;
-            L.r_start[j] = (uint16_t)start; L.r_blen[j] = (uint16_t)(r.pos - start);
-            L.r_len[j] = (uint32_t)len; L.r_ss[j] = (uint16_t)((i << 8) | (uc.ns & 0xFF));
-            L.r_flag[j] = (uint8_t)(kind | (slow ? 4 : 0));
-            L.r_out[j] = (uint16_t)olen;
+            L->key[j] = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | (uint32_t)clock;
+            L->r_start[j] = (uint16_t)start; L->r_blen[j] = (uint16_t)(r.pos - start);
+            L->r_len[j] = (uint32_t)len; L->r_ss[j] = (uint16_t)((i << 8) | (uc.ns & 0xFF));
+            L->r_flag[j] = (uint8_t)(kind | (slow ? 4 : 0));
+            L->r_out[j] = (uint16_t)olen;
           }
         }
         uc.ns++;
@@ -225,12 +237,12 @@ YDEV UpdCount w_parse_update(WaveLds& L, int i, bool write, uint32_t sbase, uint
       if (cl > 0xFFFFFFFFull || ck + ln > 0xFFFFFFFFull) fb = true;
       if (write && !fb) {
         const uint32_t j = dbase + uc.nd;
-        if (j < (uint32_t)W_D) { L.dkey[j] = ((uint64_t)(0xFFFFFFFFu - (uint32_t)cl) << 32) | (uint32_t)ck; L.dlen[j] = (uint32_t)ln; }
+        if (j < (uint32_t)W_D) { L->dkey[j] = ((uint64_t)(0xFFFFFFFFu - (uint32_t)cl) << 32) | (uint32_t)ck; L->dlen[j] = (uint32_t)ln; }
       }
       uc.nd++;
     }
   }
-  if (r.err && !err) err = r.err;
+  uc.err = r.err; uc.fb = fb; uc.nc = nc;
   return uc;
 }
 

@@ -122,6 +122,7 @@ YDEV void w_struct(WinRd& r, uint32_t flags, uint8_t& kind, uint64_t& len, uint3
     if (info & 0x40) { r.vu(); r.vu(); }
     if ((info & 0xC0) == 0) {
       const uint64_t pi = r.vu();
+      if (pi > 1) r.nm = 1;  // parentInfo is written back as 0 (non-key): re-encode
       if (pi == 1) { const uint64_t l = r.vu(); if (!r.err && !r.ascii(l)) fast = false; }
       else { r.vu(); r.vu(); }
       if (fast && (info & 0x20)) { const uint64_t l = r.vu(); if (!r.err && !r.ascii(l)) fast = false; }

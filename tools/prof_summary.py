@@ -1,0 +1,75 @@
+"""Summaries of rocprofv3 runs for profiles/ (test/measurement tooling, not product).
+
+    python tools/prof_summary.py stats  <rocprof out dir>            -> kernel stats table (markdown)
+    python tools/prof_summary.py pmc    <fetch dir> <write dir> <out.json>
+
+``stats`` reads ``*kernel_stats.csv`` (``rocprofv3 --kernel-trace --stats
+--output-format csv``).  ``pmc`` reads the ``counter_collection.csv`` of two
+separate ``--pmc FETCH_SIZE`` / ``--pmc WRITE_SIZE`` passes and writes the HBM
+bytes per launch of each merge kernel, with the gfx950 correction of
+MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts half the bytes of wide
+(16 B/lane) streaming reads, so it is doubled; WRITE_SIZE is taken as is.
+Both counters are reported by rocprofv3 in KiB.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def _find(d, pat):
+    hits = sorted(glob.glob(os.path.join(d, "**", pat), recursive=True))
+    if not hits:
+        raise SystemExit(f"no {pat} under {d}")
+    return hits
+
+
+def stats(d):
+    rows = []
+    for p in _find(d, "*kernel_stats.csv"):
+        rows += list(csv.DictReader(open(p)))
+    print("| kernel | calls | total ms | avg us | min us | max us | % |")
+    print("|---|---|---|---|---|---|---|")
+    for r in rows:
+        name = r["Name"]
+        short = name.split("(")[0].replace("void ", "")
+        print(f"| `{short}` | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.3f} | {float(r['AverageNs'])/1e3:.2f} | "
+              f"{float(r['MinNs'])/1e3:.2f} | {float(r['MaxNs'])/1e3:.2f} | {float(r['Percentage']):.2f} |")
+
+
+def _per_kernel(d, counter):
+    acc = {}
+    for p in _find(d, "*counter_collection.csv"):
+        for r in csv.DictReader(open(p)):
+            if r.get("Counter_Name") != counter:
+                continue
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            acc.setdefault(k, {})
+            disp = r.get("Dispatch_Id")
+            acc[k][disp] = acc[k].get(disp, 0.0) + float(r["Counter_Value"])
+    return {k: sum(v.values()) / len(v) for k, v in acc.items()}
+
+
+def pmc(fetch_dir, write_dir, out):
+    f = _per_kernel(fetch_dir, "FETCH_SIZE")
+    w = _per_kernel(write_dir, "WRITE_SIZE")
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB per dispatch",
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount, MI355X_MICROARCH.md HBM section)",
+           "kernels": {}}
+    for k in sorted(set(f) | set(w)):
+        rd = f.get(k, 0.0) * 1024 * 2
+        wr = w.get(k, 0.0) * 1024
+        res["kernels"][k] = {"fetch_bytes": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr}
+    main = [k for k in res["kernels"] if "k_merge_wave" in k]
+    if main:
+        res["hbm_bytes_per_launch"] = res["kernels"][main[0]]["hbm_bytes_per_launch"]
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2])
+    else:
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4])

@@ -5,8 +5,8 @@
 One step = one batched mergeUpdates over the whole per-GPU workload (10 000
 documents x 200 single-character Y.Text insert updates from 1-4 clients,
 SURVEY.md §8d config C2, BASELINE.json configs[1]) with the inputs already
-resident in HBM: ``ygm_merge_v1_device`` = the fast-path kernel launch, the
-per-document look-back placement and the 64-byte meta read-back.  For N > 1 the
+resident in HBM: ``ygm_merge_v1_device`` = the wave-per-document kernel launch (each
+document written into its own output slot) and the 64-byte meta read-back.  For N > 1 the
 driver starts one process per GPU (torchrun); every rank merges its own shard
 of documents (documents are independent, partitioned by name hash, weak
 scaling) and the time is the max over ranks.  RCCL carries only the timing
@@ -113,7 +113,7 @@ def main():
     dt = time.perf_counter() - t0
     s1 = eng.stats()
 
-    out_bytes = int(r.data_bytes)
+    out_bytes = int(r.payload_bytes)                 # sum of the merged outputs' lengths
     algo_bytes = len(arena) + out_bytes              # per step, this rank
     kernel_ms = (s1.kernel_ms - s0.kernel_ms) / args.steps
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -135,7 +135,7 @@ def main():
         off = _d2h(r.off, n * 8).view(np.uint64)
         ln = _d2h(r.len, n * 8).view(np.uint64)
         st = _d2h(r.status, n * 4).view(np.int32)
-        hdata = _d2h(r.data, out_bytes).tobytes()
+        hdata = _d2h(r.data, int(r.data_bytes)).tobytes()
         ups = synth.split(arena, upd_off)
         checked = 0
         for dd in range(0, n, max(1, n // 400)):

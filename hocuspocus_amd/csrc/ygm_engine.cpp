@@ -20,15 +20,15 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
                      uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
                      unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
-                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta,
+                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
                             uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
-                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* lb,
+                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, uint64_t slot_total,
                             void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list, uint32_t n_fb,
                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
                            void* readers, int* order, int* tmp, const uint8_t** ubase, uint32_t* ulen, uint64_t upd_cap,
-                           uint32_t* cnt, void* drec, uint64_t byte_cap, uint64_t out_cap, hipStream_t s);
+                           uint32_t* cnt, void* drec, uint64_t byte_cap, uint64_t slot_total, uint64_t out_cap, hipStream_t s);
 }
 
 namespace {
@@ -36,7 +36,7 @@ namespace {
 // mirrors ygm::DocMeta (ygm_kernels.hip)
 struct Meta {
   unsigned int ticket, fault, fb_count, defer_count, ticket_m, pad[3];
-  unsigned long long fast_total, m_total, seq_cursor, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor;
+  unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor;
 };
 
 struct DevBuf {
@@ -152,6 +152,7 @@ static void fill_dev_result(ygm_ctx* c, uint64_t data_bytes, ygm_device_result* 
   out->len = c->out_len.as<uint64_t>();
   out->status = c->status.as<int32_t>();
   out->data_bytes = data_bytes;
+  out->payload_bytes = data_bytes;
 }
 
 int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_upd_off,
@@ -159,14 +160,16 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
   if (!c || !out) return YGM_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   (void)hipSetDevice(c->device);
-  // merge output <= 3 x input (+ per-document constants); kernels also check the cap
-  const uint64_t out_cap = 3 * arena_bytes + 16ull * n_docs + 64;
+  // output arena: one slot per document (2|in| + 64 B, no cross-document dependency),
+  // then the overflow region for outputs that outgrow their slot (<= 3|in| + 16/doc)
+  const uint64_t slot_total = 2 * arena_bytes + 64ull * n_docs;
+  const uint64_t out_cap = slot_total + 3 * arena_bytes + 16ull * n_docs + 64;
   int e = prep_outputs(c, n_docs, out_cap, s);
   if (e) return e;
   HIPCHK(hipEventRecord(c->e0, s));
   if (ygm_k_launch_merge_wave(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
-                              c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->lb.as<unsigned long long>(), c->meta.p,
-                              c->defer_list.as<uint32_t>(), c->fb_list.as<uint32_t>(), out_cap, s))
+                              c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->meta.p, c->defer_list.as<uint32_t>(),
+                              c->fb_list.as<uint32_t>(), out_cap, s))
     return YGM_EDEVICE;
   HIPCHK(hipEventRecord(c->e1, s));
   Meta m;
@@ -179,7 +182,7 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
     HIPCHK(hipEventRecord(c->e0, s));
     if (ygm_k_launch_merge_fast(d_arena, d_upd_off, d_doc_upd, c->defer_list.as<uint32_t>(), m.defer_count, c->flags,
                                 c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
-                                c->lb.as<unsigned long long>() + n_docs + 1, c->meta.p, c->fb_list.as<uint32_t>(), out_cap, s))
+                                slot_total, c->meta.p, c->fb_list.as<uint32_t>(), out_cap, s))
       return YGM_EDEVICE;
     HIPCHK(hipEventRecord(c->e1, s));
     HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
@@ -187,7 +190,6 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
     if (m.fault) return YGM_EDEVICE;
     if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
   }
-  uint64_t total = m.fast_total + m.m_total;
   if (m.fb_count) {
     const uint64_t upd_cap = m.fb_upds + 1, byte_cap = m.fb_bytes + 8ull * m.fb_count + 8;
     if (!c->s_readers.ensure(upd_cap * ygm_k_seq_reader_bytes()) || !c->s_order.ensure(upd_cap * 4) || !c->s_tmp.ensure(upd_cap * 4) ||
@@ -197,17 +199,18 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
     if (ygm_k_launch_merge_seq(d_arena, d_upd_off, d_doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->out.as<uint8_t>(),
                                c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->meta.p,
                                c->s_readers.p, c->s_order.as<int>(), c->s_tmp.as<int>(), c->s_ubase.as<const uint8_t*>(),
-                               c->s_ulen.as<uint32_t>(), upd_cap, c->s_cnt.as<uint32_t>(), c->s_drec.p, byte_cap, out_cap, s))
+                               c->s_ulen.as<uint32_t>(), upd_cap, c->s_cnt.as<uint32_t>(), c->s_drec.p, byte_cap, slot_total, out_cap, s))
       return YGM_EDEVICE;
     HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    total = m.fast_total + m.m_total + m.seq_cursor;
     c->stats.docs_seq += m.fb_count;
   }
+  const uint64_t extent = slot_total + m.cursor;
   c->stats.calls++; c->stats.docs += n_docs; c->stats.updates += n_upd;
   c->stats.docs_fast += n_docs - m.fb_count;
-  c->stats.bytes_in += arena_bytes; c->stats.bytes_out += total;
-  fill_dev_result(c, total, out);
+  c->stats.bytes_in += arena_bytes; c->stats.bytes_out += m.payload;
+  fill_dev_result(c, extent, out);
+  out->payload_bytes = m.payload;
   return YGM_OK;
 }
 

@@ -48,14 +48,28 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned int defer_count;         // documents sent from the wave kernel to the workgroup kernel
   unsigned int ticket_m;            // tickets of the workgroup kernel
   unsigned int pad[3];
-  unsigned long long fast_total;    // bytes in the first look-back region
-  unsigned long long m_total;       // bytes in the workgroup-kernel region (after fast_total)
-  unsigned long long seq_cursor;    // bytes appended by the sequential kernel
+  unsigned long long fast_total;    // SV/diff: bytes of the packed (look-back placed) output
+  unsigned long long cursor;        // merge: bytes in the overflow region (after the per-document slots)
+  unsigned long long payload;       // merge: sum of output lengths (algorithmic output bytes)
   unsigned long long fb_upds;       // updates / bytes of fallback documents (scratch sizing)
   unsigned long long fb_bytes;
   unsigned long long scr_upd_cursor;
   unsigned long long scr_byte_cursor;
 };
+
+// Merge output placement.  Document d owns the 16-byte aligned slot starting at
+// align16(2*b0 + 64d) with capacity 2*(b1-b0) + 48 (b0, b1 = its input byte
+// range), inside [2*b0 + 64d, 2*b1 + 64(d+1)): slots never overlap and need no
+// cross-document scan (slot_total = 2*arena + 64*n_docs).  An output that does
+// not fit its slot goes to the overflow region after slot_total (atomic cursor).
+YDEV uint64_t merge_slot(uint64_t b0, uint32_t d) { return (2 * b0 + 64ull * d + 15) & ~15ull; }
+YDEV uint64_t merge_slot_cap(uint64_t nbytes) { return 2 * nbytes + 48; }
+YDEV uint64_t merge_place(const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t d, uint64_t size, uint64_t slot_total,
+                          DocMeta* meta) {
+  const uint64_t b0 = upd_off[doc_upd[d]], b1 = upd_off[doc_upd[d + 1]];
+  if (size <= merge_slot_cap(b1 - b0)) return merge_slot(b0, d);
+  return slot_total + atomicAdd(&meta->cursor, (unsigned long long)size);
+}
 
 template <int MODE>  // 0 = sv, 1 = diff
 __global__ __launch_bounds__(DOC_NT) void k_doc(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off,
@@ -205,23 +219,20 @@ YDEV_NI void m_parse_update(MergeLds& L, int i, int pass, uint32_t flags) {
 
 YDEV int pow2_ceil(int n) { int p = 1; while (p < n) p <<= 1; return p; }
 
-// Documents deferred by the wave kernel (list `docs`, n_docs entries); output
-// region starts at meta->fast_total.
+// Documents deferred by the wave kernel (list `docs`, n_docs entries), one
+// workgroup each; outputs placed by merge_place.
 __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                       const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ docs,
                                                       uint32_t n_docs, uint32_t flags,
                                                       uint8_t* __restrict__ out_all, uint64_t* __restrict__ out_off,
                                                       uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
-                                                      unsigned long long* lb, DocMeta* meta, uint32_t* fb_list, uint64_t out_cap) {
+                                                      uint64_t slot_total, DocMeta* meta, uint32_t* fb_list, uint64_t out_cap) {
   __shared__ MergeLds L;
   const int t = threadIdx.x;
   DIAG_T0
-  if (t == 0) { L.tile = atomicAdd(&meta->ticket_m, 1u); L.err = 0; L.fb = 0; L.nc = 0; }
+  if (t == 0) { L.err = 0; L.fb = 0; L.nc = 0; }
   __syncthreads();
-  const uint32_t tile = L.tile;
-  const uint32_t d = docs[tile];
-  const uint64_t region = meta->fast_total;
-  uint8_t* out = out_all + region;
+  const uint32_t d = docs[blockIdx.x];
   const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
   const uint32_t k = u1 - u0;
   const uint64_t b0 = upd_off[u0], b1 = upd_off[u1];
@@ -381,29 +392,26 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
     if (t == 0) L.nseg = nseg;
   }
   DIAG(5);
-  // ---- look-back: this document's place in the packed output
-  const uint64_t mysz = (st == ST_OK) ? size : 0;
-  if (t < WAVE) {
-    const uint64_t b = lookback(lb, tile, mysz, &meta->fault);
-    if (t == 0) {
-      L.base = b;
-      if (tile == n_docs - 1) meta->m_total = b + mysz;
-      if (st == ST_FALLBACK) {
-        const uint32_t q = atomicAdd(&meta->fb_count, 1u);
-        fb_list[q] = d;
-        atomicAdd(&meta->fb_upds, (unsigned long long)k);
-        atomicAdd(&meta->fb_bytes, (unsigned long long)nbytes);
-      }
+  // ---- placement: the document's own slot (or the overflow region)
+  if (t == 0) {
+    L.base = st == ST_OK ? merge_place(upd_off, doc_upd, d, size, slot_total, meta) : 0;
+    if (st == ST_FALLBACK) {
+      const uint32_t q = atomicAdd(&meta->fb_count, 1u);
+      fb_list[q] = d;
+      atomicAdd(&meta->fb_upds, (unsigned long long)k);
+      atomicAdd(&meta->fb_bytes, (unsigned long long)nbytes);
     }
   }
   __syncthreads();
   DIAG(6);
   const uint64_t base = L.base;
-  if (meta->fault && st == ST_OK) st = ST_DEVICE;
-  if (st == ST_OK && region + base + size > out_cap) st = ST_NOMEM;
-  if (t == 0) { out_off[d] = region + base; out_len[d] = st == ST_OK ? size : 0; status[d] = st == ST_FALLBACK ? ST_FALLBACK : st; }
+  if (st == ST_OK && base + size > out_cap) st = ST_NOMEM;
+  if (t == 0) {
+    if (st == ST_OK) atomicAdd(&meta->payload, (unsigned long long)size);
+    out_off[d] = base; out_len[d] = st == ST_OK ? size : 0; status[d] = st;
+  }
   if (st != ST_OK) return;
-  uint8_t* o = out + base;
+  uint8_t* o = out_all + base;
   if (mode == 1) { if (t == 0) { o[0] = 0; o[1] = 0; } return; }
   if (mode == 2) { for (uint64_t i = t; i < nbytes; i += M_NT) o[i] = arena[b0 + i]; return; }
   // ---- emit structs
@@ -435,30 +443,35 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
 
 
 // ======================================================================= merge: one wave per document
-// Per-element state lives in LDS (eflag/eblk/epos, dflag/dsid/dposs) and every
-// per-element loop is rolled: the kernel stays small enough for the I-cache.
+// See ygm_merge_wave.hpp for the phase plan.  Per-element state lives in LDS
+// and every per-element loop is rolled (the kernel stays I-cache sized).
+YDEV uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) { const uint32_t o = (uint32_t)__shfl_xor((int)v, d, WAVE); v = o < v ? o : v; }
+  return v;
+}
+
 __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                                const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t flags,
                                                                uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                                uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
-                                                               unsigned long long* lb, DocMeta* meta, uint32_t* defer_list,
-                                                               uint32_t* fb_list, uint64_t out_cap) {
+                                                               DocMeta* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap) {
   __shared__ WaveLds LS[W_WAVES];
   DIAG_T0
   const uint32_t l = threadIdx.x % WAVE;
   WaveLds& L = LS[threadIdx.x / WAVE];
-  uint32_t tk = 0;
-  if (l == 0) tk = atomicAdd(&meta->ticket, 1u);
-  const uint32_t d = (uint32_t)__shfl((int)tk, 0, WAVE);
+  LWave* LW = (LWave*)&L;
+  const uint32_t d = blockIdx.x * W_WAVES + threadIdx.x / WAVE;
   if (d >= n_docs) return;
   const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
   const uint32_t k = u1 - u0;
   const uint64_t b0 = upd_off[u0], b1 = upd_off[u1];
   const uint64_t nbytes = b1 - b0;
+  const uint64_t slot = merge_slot(b0, d), cap = merge_slot_cap(nbytes);
   constexpr int ST_DEFER = 101;
   int st = ST_OK, mode = 0;
   uint64_t size = 0;
-  uint32_t S = 0, D = 0, nblocks = 0, nseg = 0, hdr0 = 0, sbytes = 0, dsbytes = 0;
+  uint32_t S = 0, D = 0, nC = 0, nseg = 0, hdr0 = 0, sbytes = 0, dsbytes = 0;
   if (k == 0) { mode = 1; size = 2; }
   else if (k == 1) { mode = 2; size = nbytes; }
   else if (k > (uint32_t)W_K || nbytes + 16 > (uint64_t)W_IN || (flags & 2u)) st = ST_DEFER;
@@ -472,200 +485,232 @@ __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __
       const uint64_t a = upd_off[u0 + i], b = upd_off[u0 + i + 1];
       L.ustart[i] = (uint16_t)(a - b0 + shift); L.ulen[i] = (uint16_t)(b - a);
     }
+    if (l == 0) { L.nrec = 0; L.ndel = 0; }
     wave_sync();
     DIAGW(0);
-    // ---- pass A: validate + count; lane l parses updates l*R .. l*R+R-1
-    LWave* LW = (LWave*)&L;
-    const uint32_t R = (k + WAVE - 1) / WAVE;
-    int err = 0; bool fb = false, nc = false;
-    uint32_t sl = 0, dl = 0;
-    for (uint32_t r = 0; r < R; r++) {
-      const uint32_t i = l * R + r;
-      if (i < k) {
-        const UpdCount c = w_parse_update(LW, (int)i, false, 0, 0, flags);
-        L.uns[i] = (uint16_t)(c.ns > 0xFFFF ? 0xFFFF : c.ns); L.und[i] = (uint16_t)(c.nd > 0xFFFF ? 0xFFFF : c.nd);
-        sl += c.ns; dl += c.nd;
-        if (c.err && !err) err = c.err;
-        fb |= c.fb != 0; nc |= c.nc != 0;
-      }
+    // ---- parse: one pass, lane l takes updates l, l+64, ...; first error by update index wins
+    uint32_t ekey = 0xFFFFFFFFu; bool fb = false, nc = false;
+    for (uint32_t i = l; i < k; i += WAVE) {
+      const UpdCount c = w_parse_update(LW, (int)i, flags);
+      fb |= c.fb != 0; nc |= c.nc != 0;
+      if (c.err) { ekey = (i << 8) | (uint32_t)c.err; break; }
     }
+    wave_sync();
     DIAGW(1);
-    const unsigned long long eb = __ballot(err != 0);
-    if (eb) st = __shfl(err, __ffsll((long long)eb) - 1, WAVE);
-    else if (__ballot(fb)) st = ST_DEFER;
-    else {
-      (void)wave_exscan(sl, S); (void)wave_exscan(dl, D);
-      if (S > (uint32_t)W_S || D > (uint32_t)W_D || ((flags & F_COMPAT_135) && D > 0)) st = ST_DEFER;
-      else if (__ballot(nc)) st = ST_NONCANON;
-    }
+    ekey = wave_min_u32(ekey);
+    S = L.nrec; D = L.ndel;
+    if (ekey != 0xFFFFFFFFu) st = (int)(ekey & 0xFF);
+    else if (__ballot(fb) || S > (uint32_t)W_S || D > (uint32_t)W_D || ((flags & F_COMPAT_135) && D > 0)) st = ST_DEFER;
+    else if (__ballot(nc)) st = ST_NONCANON;
     if (st == ST_OK) {
-      // ---- pass B: records
-      uint32_t sb, db, tS, tD;
-      sb = wave_exscan(sl, tS); db = wave_exscan(dl, tD);
-      for (uint32_t r = 0; r < R; r++) {
-        const uint32_t i = l * R + r;
-        if (i < k) {
-          const uint32_t ns = L.uns[i], nd = L.und[i];
-          if (ns | nd) w_parse_update(LW, (int)i, true, sb, db, flags);
-          sb += ns; db += nd;
-        }
+      // ---- clients: distinct values by wave vote, ranked descending
+      uint32_t rc[W_E]; uint8_t cid[W_E];
+#pragma unroll
+      for (int q = 0; q < W_E; q++) { const uint32_t e = l + WAVE * q; rc[q] = e < S ? L.rcl[e] : 0; cid[q] = e < S ? 0xFF : 0xFE; }
+      uint32_t myc = 0;
+      for (;;) {
+        bool has = false; uint32_t cand = 0;
+#pragma unroll
+        for (int q = 0; q < W_E; q++) if (cid[q] == 0xFF && !has) { has = true; cand = rc[q]; }
+        const uint64_t m = __ballot(has);
+        if (!m) break;
+        if (nC == (uint32_t)W_C) { st = ST_DEFER; break; }
+        const uint32_t c = (uint32_t)__shfl((int)cand, __ffsll((long long)m) - 1, WAVE);
+#pragma unroll
+        for (int q = 0; q < W_E; q++) if (cid[q] == 0xFF && rc[q] == c) cid[q] = (uint8_t)nC;
+        if (l == nC) myc = c;
+        nC++;
       }
-      wave_sync();
-      DIAGW(2);
-      // ---- rank sort (ties by record id; equal struct keys are caught below as overlap)
-      for (int pass = 0; pass < 2; pass++) {
-        const uint32_t n = pass ? D : S;
-        uint64_t mk[W_E]; uint32_t ml[W_E], rk[W_E];
+      if (st == ST_OK) {
+        uint32_t rank = 0;
+        for (uint32_t t = 0; t < nC; t++) rank += (uint32_t)__shfl((int)myc, (int)t, WAVE) > myc ? 1u : 0u;
+        if (l < nC) { L.ctab[rank] = myc; L.blkcnt[rank] = 0; }
+        // ---- sort keys (client rank << 40 | clock << 8 | record) in registers
+        uint64_t kr[4];
 #pragma unroll
-        for (int q = 0; q < W_E; q++) {
-          const uint32_t j = l + WAVE * q;
-          mk[q] = j < n ? (pass ? L.dkey[j] : L.key[j]) : ~0ull; ml[q] = (pass && j < n) ? L.dlen[j] : 0; rk[q] = 0;
+        for (int q = 0; q < 4; q++) {
+          const uint32_t e = l + WAVE * q;
+          const uint32_t cr = (uint32_t)__shfl((int)rank, q < W_E ? (int)(cid[q] & 63) : 0, WAVE);
+          kr[q] = (q < W_E && e < S) ? (L.key[e] | ((uint64_t)cr << 40)) : ~0ull;
         }
-        for (uint32_t i = 0; i < n; i++) {
-          const uint64_t ki = pass ? L.dkey[i] : L.key[i];
+        // stable split by client rank (records were allocated in update order, so a
+        // log whose updates arrive in clock order per client is sorted after it);
+        // anything else: bitonic sort
+        bool sorted = false;
+        if (nC <= 8) {
+          uint32_t pos[W_E], base = 0;
+          for (uint32_t b = 0; b < nC; b++) {
 #pragma unroll
-          for (int q = 0; q < W_E; q++) rk[q] += (ki < mk[q]) || (ki == mk[q] && i < l + WAVE * q);
+            for (int q = 0; q < W_E; q++) {
+              const bool in_b = (kr[q] >> 40) == b;   // padding keys (~0) never match
+              const uint64_t m = __ballot(in_b);
+              if (in_b) pos[q] = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+              base += (uint32_t)__popcll(m);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < W_E; q++) if (l + WAVE * q < S) L.key[pos[q]] = kr[q];
+          wave_sync();
+          bool bad = false;
+          for (uint32_t j = l + 1; j < S; j += WAVE) bad |= L.key[j - 1] > L.key[j];
+          sorted = __ballot(bad) == 0;
+          wave_sync();
         }
+        if (!sorted) {
+          if (S <= 64) wave_bitonic<1>(kr);
+          else if (S <= 128) wave_bitonic<2>(kr);
+          else wave_bitonic<4>(kr);
+          const uint32_t E = S <= 64 ? 1u : S <= 128 ? 2u : 4u;
+#pragma unroll
+          for (int q = 0; q < 4; q++) { const uint32_t i = E * l + q; if ((uint32_t)q < E && i < S) L.key[i] = kr[q]; }
+        }
+        for (uint32_t j = l; j < S; j += WAVE) L.rcl[j] = 0;   // becomes the GC run end by sorted element
         wave_sync();
-#pragma unroll
-        for (int q = 0; q < W_E; q++) {
-          const uint32_t j = l + WAVE * q;
-          if (j < n) { if (pass) { L.dkey[rk[q]] = mk[q]; L.dlen[rk[q]] = ml[q]; } else { L.key[rk[q]] = mk[q]; L.sidx[rk[q]] = (uint16_t)j; } }
-        }
-      }
-      for (uint32_t j = l; j < S; j += WAVE) L.runend[j] = 0;
-      for (uint32_t j = l; j < D; j += WAVE) L.drunend[j] = 0;
-      for (uint32_t j = l; j < W_BLK; j += WAVE) { L.blkcnt[j] = 0; L.segcnt[j] = 0; }
-      wave_sync();
-      DIAGW(3);
-      // ---- classify sorted structs (blocked: lane l owns elements l*W_E .. l*W_E+W_E-1)
-      const uint32_t e0 = l * W_E, e1 = min(e0 + W_E, S);
-      bool ovl = false;
-      uint32_t vmax = 0, nnew = 0;
-      for (uint32_t j = e0; j < e1; j++) {
-        const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
-        uint32_t f = (L.r_flag[r] & 3) == K_GC ? EF_GC : 0;
-        if (j == 0) f |= EF_NEWC;
-        else {
-          const uint64_t kp = L.key[j - 1]; const uint32_t rp = L.sidx[j - 1];
-          const uint32_t pend = (uint32_t)kp + L.r_len[rp];
-          if ((uint32_t)(kp >> 32) != (uint32_t)(kj >> 32)) f |= EF_NEWC;
-          else if ((uint32_t)kj < pend) ovl = true;
-          else if ((uint32_t)kj > pend) f |= EF_GAP;
+        DIAGW(2);
+        // ---- classify sorted structs (blocked: lane l owns elements l*W_E .. l*W_E+W_E-1)
+        const uint32_t e0 = l * W_E, e1 = min(e0 + W_E, S);
+        bool ovl = false;
+        uint32_t vmax = 0;
+        for (uint32_t j = e0; j < e1; j++) {
+          const uint64_t kj = L.key[j]; const uint32_t r = (uint32_t)kj & 0xFF;
+          const uint32_t rbj = L.rb[r];
+          uint32_t f = ((rbj >> 13) & 3) == K_GC ? EF_GC : 0;
+          if (j == 0 || (L.key[j - 1] >> 40) != (kj >> 40)) f |= EF_NEWC;
           else {
-            const uint32_t ss = L.r_ss[r], sp = L.r_ss[rp];
-            if ((ss >> 8) == (sp >> 8) && (ss & 0xFF) == (sp & 0xFF) + 1) f |= EF_SDN;
-            if ((f & EF_GC) && (L.r_flag[rp] & 3) == K_GC) f |= EF_CGG;
+            const uint64_t kp = L.key[j - 1]; const uint32_t rp = (uint32_t)kp & 0xFF;
+            const uint32_t pend = (uint32_t)(kp >> 8) + (uint32_t)L.ra[rp];
+            const uint32_t ck = (uint32_t)(kj >> 8);
+            const uint32_t rbp = L.rb[rp];
+            if (ck < pend) ovl = true;
+            else if (ck > pend) f |= EF_GAP;
+            else {
+              const uint32_t ss = rbj >> 16, sp = rbp >> 16;
+              if ((ss >> 8) == (sp >> 8) && (ss & 0xFF) == (sp & 0xFF) + 1) f |= EF_SDN;
+              if ((f & EF_GC) && ((rbp >> 13) & 3) == K_GC) f |= EF_CGG;
+            }
+          }
+          if (!(f & EF_CGG)) f |= EF_NONID | EF_T;
+          else if (!(f & EF_SDN)) f |= EF_NONID;
+          L.eflag[j] = (uint8_t)f;
+          if (f & EF_NONID) vmax = j + 1;
+        }
+        if (__ballot(ovl)) st = ST_FALLBACK;  // overlapping structs: exact sequential replay
+        else {
+          wave_sync();
+          // GC provenance: last non-identity element <= j (max-scan); emitted heads
+          uint32_t mex = wave_incl_scan_max(vmax); mex = __shfl_up(mex, 1, WAVE); if (l == 0) mex = 0;
+          uint32_t hmax = 0, lastnid = mex;
+          for (uint32_t j = e0; j < e1; j++) {
+            uint32_t f = L.eflag[j];
+            if (f & EF_NONID) lastnid = j + 1;
+            if (L.eflag[lastnid - 1] & EF_T) f |= EF_EMIT;   // otherwise merged into the previous GC
+            L.eflag[j] = (uint8_t)f;
+            if (f & EF_EMIT) hmax = j + 1;
+          }
+          uint32_t hex = wave_incl_scan_max(hmax); hex = __shfl_up(hex, 1, WAVE); if (l == 0) hex = 0;
+          // per-client struct counts, GC run ends (LDS atomics)
+          uint32_t head = hex;
+          for (uint32_t j = e0; j < e1; j++) {
+            const uint32_t f = L.eflag[j];
+            const uint64_t kj = L.key[j];
+            if (f & EF_EMIT) head = j + 1;
+            const uint32_t cnt = ((f & EF_GAP) ? 1u : 0u) + ((f & EF_EMIT) ? 1u : 0u);
+            if (cnt) atomicAdd(&L.blkcnt[kj >> 40], cnt);
+            atomicMax(&L.rcl[head - 1], (uint32_t)(kj >> 8) + (uint32_t)L.ra[kj & 0xFF]);
+          }
+          wave_sync();
+          // element sizes -> positions (epos, relative to the struct section)
+          uint32_t acc = 0;
+          for (uint32_t j = e0; j < e1; j++) {
+            const uint32_t f = L.eflag[j];
+            const uint64_t kj = L.key[j]; const uint32_t r = (uint32_t)kj & 0xFF;
+            const uint32_t crk = (uint32_t)(kj >> 40), ck = (uint32_t)(kj >> 8);
+            uint32_t sz = 0;
+            if (f & EF_NEWC) sz += vu_len(L.blkcnt[crk]) + vu_len(L.ctab[crk]) + vu_len(ck);
+            if (f & EF_GAP) { const uint64_t kp = L.key[j - 1]; sz += 1 + vu_len(ck - ((uint32_t)(kp >> 8) + (uint32_t)L.ra[kp & 0xFF])); }
+            if (f & EF_EMIT) sz += (f & EF_GC) ? 1 + vu_len(L.rcl[j] - ck) : (L.rb[r] & 0x1FFF);
+            L.epos[j] = (uint16_t)acc; acc += sz;
+          }
+          const uint32_t lb0 = wave_exscan(acc, sbytes);
+          for (uint32_t j = e0; j < e1; j++) L.epos[j] = (uint16_t)(L.epos[j] + lb0);
+          hdr0 = vu_len(nC);
+          DIAGW(3);
+          // ---- delete set: rank sort, segments (clients, descending) and runs (rule R-DS)
+          if (D) {
+            uint64_t mk[W_DE]; uint32_t ml[W_DE], rk[W_DE];
+#pragma unroll
+            for (int q = 0; q < W_DE; q++) {
+              const uint32_t j = l + WAVE * q;
+              mk[q] = j < D ? L.dkey[j] : ~0ull; ml[q] = j < D ? L.dlen[j] : 0; rk[q] = 0;
+            }
+            for (uint32_t i = 0; i < D; i++) {
+              const uint64_t ki = L.dkey[i];
+#pragma unroll
+              for (int q = 0; q < W_DE; q++) rk[q] += (ki < mk[q]) || (ki == mk[q] && i < l + WAVE * q);
+            }
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < W_DE; q++) if (l + WAVE * q < D) { L.dkey[rk[q]] = mk[q]; L.dlen[rk[q]] = ml[q]; }
+            for (uint32_t j = l; j < D; j += WAVE) L.drunend[j] = 0;
+            for (uint32_t j = l; j < W_BLK; j += WAVE) L.segcnt[j] = 0;
+            wave_sync();
+          }
+          const uint32_t d0 = l * W_DE, d1 = min(d0 + W_DE, D);
+          uint32_t sn = 0; uint64_t mm = 0;
+          for (uint32_t j = d0; j < d1; j++) {
+            const bool sg = j == 0 || (L.dkey[j - 1] >> 32) != (L.dkey[j] >> 32);
+            L.dflag[j] = sg ? 1 : 0;
+            sn += sg ? 1 : 0;
+          }
+          const uint32_t sex = wave_exscan(sn, nseg);
+          if (nseg > (uint32_t)W_BLK) st = ST_DEFER;   // segment ids index segcnt[W_BLK]
+          else {
+          uint32_t sidr = sex;
+          for (uint32_t j = d0; j < d1; j++) {
+            sidr += L.dflag[j] & 1;
+            L.dflag[j] = (uint8_t)((L.dflag[j] & 3) | ((sidr - 1) << 2));
+            const uint64_t v = ((uint64_t)(sidr - 1) << 32) | ((uint32_t)L.dkey[j] + L.dlen[j]);
+            mm = v > mm ? v : mm;
+          }
+          uint64_t dmex = wave_incl_scan_max(mm); dmex = __shfl_up(dmex, 1, WAVE); if (l == 0) dmex = 0;
+          uint64_t runmax = dmex; uint32_t rh = 0;
+          for (uint32_t j = d0; j < d1; j++) {
+            const uint32_t sidj = L.dflag[j] >> 2;
+            const bool rs = (L.dflag[j] & 1) || (uint32_t)L.dkey[j] > (uint32_t)runmax;
+            if (rs) { L.dflag[j] |= 2; atomicAdd(&L.segcnt[sidj], 1u); rh = j + 1; }
+            const uint64_t v = ((uint64_t)sidj << 32) | ((uint32_t)L.dkey[j] + L.dlen[j]);
+            runmax = v > runmax ? v : runmax;
+          }
+          uint32_t rhex = wave_incl_scan_max(rh); rhex = __shfl_up(rhex, 1, WAVE); if (l == 0) rhex = 0;
+          uint32_t rhead = rhex;
+          for (uint32_t j = d0; j < d1; j++) {
+            if (L.dflag[j] & 2) rhead = j + 1;
+            atomicMax(&L.drunend[rhead - 1], (uint32_t)L.dkey[j] + L.dlen[j]);
+          }
+          wave_sync();
+          uint32_t dacc = 0;
+          for (uint32_t j = d0; j < d1; j++) {
+            const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.dkey[j] >> 32), ck = (uint32_t)L.dkey[j];
+            uint32_t sz = 0;
+            if (L.dflag[j] & 1) sz += vu_len(cl) + vu_len(L.segcnt[L.dflag[j] >> 2]);
+            if (L.dflag[j] & 2) sz += vu_len(ck) + vu_len(L.drunend[j] - ck);
+            L.dposs[j] = (uint16_t)dacc; dacc += sz;
+          }
+          const uint32_t dl0 = wave_exscan(dacc, dsbytes);
+          for (uint32_t j = d0; j < d1; j++) L.dposs[j] = (uint16_t)(L.dposs[j] + dl0);
+          size = (uint64_t)hdr0 + sbytes + vu_len(nseg) + dsbytes;
+          // the copy-out writes align16(size) bytes of the LDS buffer into the slot
+          if (((size + 15) & ~15ull) > cap || size > (uint64_t)W_OUT) st = ST_DEFER;   // the workgroup kernel places it
           }
         }
-        if (!(f & EF_CGG)) f |= EF_NONID | EF_T;
-        else if (!(f & EF_SDN)) f |= EF_NONID;
-        L.eflag[j] = (uint8_t)f;
-        if (f & EF_NONID) vmax = j + 1;
-        nnew += (f & EF_NEWC) ? 1 : 0;
-      }
-      uint32_t nsg = 0;
-      for (uint32_t j = l; j < D; j += WAVE) nsg += (j == 0 || (L.dkey[j - 1] >> 32) != (L.dkey[j] >> 32)) ? 1u : 0u;
-      if (__ballot(ovl)) st = ST_FALLBACK;  // overlapping structs: exact sequential replay
-      else if (wave_sum(nnew) > (uint32_t)W_BLK || wave_sum(nsg) > (uint32_t)W_BLK) st = ST_DEFER;
-      else {
-        wave_sync();
-        // last non-identity element <= j (max-scan) and block index (count of NEWC <= j, minus 1)
-        uint32_t mex = wave_incl_scan_max(vmax); mex = __shfl_up(mex, 1, WAVE); if (l == 0) mex = 0;
-        uint32_t cex = wave_exscan(nnew, nblocks);
-        uint32_t hmax = 0, lastnid = mex, blk = cex;
-        for (uint32_t j = e0; j < e1; j++) {
-          uint32_t f = L.eflag[j];
-          if (f & EF_NONID) lastnid = j + 1;
-          if (L.eflag[lastnid - 1] & EF_T) f |= EF_EMIT;   // otherwise merged into the previous GC
-          L.eflag[j] = (uint8_t)f;
-          blk += (f & EF_NEWC) ? 1 : 0;
-          L.eblk[j] = (uint8_t)(blk - 1);
-          if (f & EF_EMIT) hmax = j + 1;
-        }
-        uint32_t hex = wave_incl_scan_max(hmax); hex = __shfl_up(hex, 1, WAVE); if (l == 0) hex = 0;
-        // per-block struct counts, GC run ends (LDS atomics)
-        uint32_t head = hex;
-        for (uint32_t j = e0; j < e1; j++) {
-          const uint32_t f = L.eflag[j];
-          if (f & EF_EMIT) head = j + 1;
-          const uint32_t cnt = ((f & EF_GAP) ? 1u : 0u) + ((f & EF_EMIT) ? 1u : 0u);
-          if (cnt) atomicAdd(&L.blkcnt[L.eblk[j]], cnt);
-          atomicMax(&L.runend[head - 1], (uint32_t)L.key[j] + L.r_len[L.sidx[j]]);
-        }
-        wave_sync();
-        // element sizes -> positions (epos, relative to the struct section)
-        uint32_t acc = 0;
-        for (uint32_t j = e0; j < e1; j++) {
-          const uint32_t f = L.eflag[j];
-          const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
-          const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(kj >> 32), ck = (uint32_t)kj;
-          uint32_t sz = 0;
-          if (f & EF_NEWC) sz += vu_len(L.blkcnt[L.eblk[j]]) + vu_len(cl) + vu_len(ck);
-          if (f & EF_GAP) { const uint64_t kp = L.key[j - 1]; sz += 1 + vu_len(ck - ((uint32_t)kp + L.r_len[L.sidx[j - 1]])); }
-          if (f & EF_EMIT) sz += (f & EF_GC) ? 1 + vu_len(L.runend[j] - ck) : L.r_out[r];
-          L.epos[j] = (uint16_t)acc; acc += sz;
-        }
-        const uint32_t lb0 = wave_exscan(acc, sbytes);
-        for (uint32_t j = e0; j < e1; j++) L.epos[j] = (uint16_t)(L.epos[j] + lb0);
-        hdr0 = vu_len(nblocks);
-        DIAGW(4);
-        // ---- delete set: segments (clients, descending) and runs (rule R-DS); lane owns d0 .. d1-1
-        const uint32_t d0 = l * W_DE, d1 = min(d0 + W_DE, D);
-        uint32_t sn = 0; uint64_t mm = 0;
-        for (uint32_t j = d0; j < d1; j++) {
-          const bool sg = j == 0 || (L.dkey[j - 1] >> 32) != (L.dkey[j] >> 32);
-          L.dflag[j] = sg ? 1 : 0;
-          sn += sg ? 1 : 0;
-        }
-        const uint32_t sex = wave_exscan(sn, nseg);
-        uint32_t sidr = sex;
-        for (uint32_t j = d0; j < d1; j++) {
-          sidr += L.dflag[j] & 1;
-          L.dsid[j] = (uint8_t)(sidr - 1);
-          const uint64_t v = ((uint64_t)(sidr - 1) << 32) | ((uint32_t)L.dkey[j] + L.dlen[j]);
-          mm = v > mm ? v : mm;
-        }
-        uint64_t dmex = wave_incl_scan_max(mm); dmex = __shfl_up(dmex, 1, WAVE); if (l == 0) dmex = 0;
-        uint64_t runmax = dmex; uint32_t rh = 0;
-        for (uint32_t j = d0; j < d1; j++) {
-          const uint32_t sidj = L.dsid[j];
-          const bool rs = (L.dflag[j] & 1) || (uint32_t)L.dkey[j] > (uint32_t)runmax;
-          if (rs) { L.dflag[j] |= 2; atomicAdd(&L.segcnt[sidj], 1u); rh = j + 1; }
-          const uint64_t v = ((uint64_t)sidj << 32) | ((uint32_t)L.dkey[j] + L.dlen[j]);
-          runmax = v > runmax ? v : runmax;
-        }
-        uint32_t rhex = wave_incl_scan_max(rh); rhex = __shfl_up(rhex, 1, WAVE); if (l == 0) rhex = 0;
-        uint32_t rhead = rhex;
-        for (uint32_t j = d0; j < d1; j++) {
-          if (L.dflag[j] & 2) rhead = j + 1;
-          atomicMax(&L.drunend[rhead - 1], (uint32_t)L.dkey[j] + L.dlen[j]);
-        }
-        wave_sync();
-        uint32_t dacc = 0;
-        for (uint32_t j = d0; j < d1; j++) {
-          const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.dkey[j] >> 32), ck = (uint32_t)L.dkey[j];
-          uint32_t sz = 0;
-          if (L.dflag[j] & 1) sz += vu_len(cl) + vu_len(L.segcnt[L.dsid[j]]);
-          if (L.dflag[j] & 2) sz += vu_len(ck) + vu_len(L.drunend[j] - ck);
-          L.dposs[j] = (uint16_t)dacc; dacc += sz;
-        }
-        const uint32_t dl0 = wave_exscan(dacc, dsbytes);
-        for (uint32_t j = d0; j < d1; j++) L.dposs[j] = (uint16_t)(L.dposs[j] + dl0);
-        size = (uint64_t)hdr0 + sbytes + vu_len(nseg) + dsbytes;
       }
     }
   }
   DIAGW(5);
-  // ---- look-back (whole wave) -> this document's offset in the packed output
-  const uint64_t mysz = st == ST_OK ? size : 0;
-  const uint64_t base = lookback(lb, d, mysz, &meta->fault);
-  DIAGW(6);
-  if (d == n_docs - 1 && l == 0) meta->fast_total = base + mysz;
-  if (st == ST_OK && meta->fault) st = ST_DEVICE;
-  if (st == ST_OK && base + size > out_cap) st = ST_NOMEM;
+  if (st == ST_OK && slot + size > out_cap) st = ST_NOMEM;
   if (l == 0) {
-    out_off[d] = base; out_len[d] = st == ST_OK ? size : 0;
+    if (st == ST_OK) atomicAdd(&meta->payload, (unsigned long long)size);
+    out_off[d] = slot; out_len[d] = st == ST_OK ? size : 0;
     status[d] = st == ST_DEFER ? ST_FALLBACK : st;
     if (st == ST_DEFER) defer_list[atomicAdd(&meta->defer_count, 1u)] = d;
     if (st == ST_FALLBACK) {
@@ -675,47 +720,51 @@ __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __
     }
   }
   if (st != ST_OK) return;
-  uint8_t* o = out + base;
+  uint8_t* o = out + slot;
   if (mode == 1) { if (l == 0) { o[0] = 0; o[1] = 0; } return; }
   if (mode == 2) { for (uint64_t i = l; i < nbytes; i += WAVE) o[i] = arena[b0 + i]; return; }
-  // ---- emit: lane-contiguous segments
-  if (l == 0) { Out w{o, 0}; w.vu(nblocks); }
+  // ---- emit: lane-contiguous segments into the LDS output buffer
+  LO8* lo = (LO8*)L.out;
+  if (l == 0) { LWriter w{lo, 0}; w.vu(nC); }
   const uint32_t e0 = l * W_E, e1 = min(e0 + W_E, S);
-  GWriter gw; gw.init(o, hdr0 + (e0 < S ? L.epos[e0] : sbytes));
+  LWriter gw{lo, hdr0 + (e0 < S ? L.epos[e0] : sbytes)};
   for (uint32_t j = e0; j < e1; j++) {
     const uint32_t f = L.eflag[j];
-    const uint64_t kj = L.key[j]; const uint32_t r = L.sidx[j];
-    const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(kj >> 32), ck = (uint32_t)kj;
-    if (f & EF_NEWC) { gw.vu(L.blkcnt[L.eblk[j]]); gw.vu(cl); gw.vu(ck); }
-    if (f & EF_GAP) { const uint64_t kp = L.key[j - 1]; gw.b(10); gw.vu(ck - ((uint32_t)kp + L.r_len[L.sidx[j - 1]])); }
+    const uint64_t kj = L.key[j]; const uint32_t r = (uint32_t)kj & 0xFF;
+    const uint32_t crk = (uint32_t)(kj >> 40), ck = (uint32_t)(kj >> 8);
+    const uint32_t cl = L.ctab[crk];
+    if (f & EF_NEWC) { gw.vu(L.blkcnt[crk]); gw.vu(cl); gw.vu(ck); }
+    if (f & EF_GAP) { const uint64_t kp = L.key[j - 1]; gw.b(10); gw.vu(ck - ((uint32_t)(kp >> 8) + (uint32_t)L.ra[kp & 0xFF])); }
     if (f & EF_EMIT) {
-      if (f & EF_GC) { gw.b(0); gw.vu(L.runend[j] - ck); }
-      else if (!(L.r_flag[r] & 4)) {  // canonical item: input bytes, info bit 0x20 dropped when an origin is set
-        const uint32_t s0 = L.r_start[r], n = L.r_blen[r];
+      const uint64_t ra = L.ra[r];
+      const uint32_t s0 = (uint32_t)(ra >> 48), n = (uint32_t)(ra >> 32) & 0xFFFF;
+      if (f & EF_GC) { gw.b(0); gw.vu(L.rcl[j] - ck); }
+      else if (!((L.rb[r] >> 13) & 4)) {  // canonical item: input bytes, info bit 0x20 dropped when an origin is set
         const uint8_t info = L.in[s0];
         gw.b((info & 0xC0) ? (uint8_t)(info & ~0x20) : info);
-        for (uint32_t i = 1; i < n; i++) gw.b(L.in[s0 + i]);
+        gw.copy((LU8*)L.in, s0 + 1, n - 1);
       } else {
-        gw.flush();
-        Cur c{L.in, L.r_start[r], (uint32_t)L.r_start[r] + L.r_blen[r], 0, 0};
+        Cur c{L.in, s0, s0 + n, 0, 0};
         SInfo si; read_struct(c, si, flags);
-        Out w{o + gw.pos, 0};
+        Out w{(uint8_t*)(lo + gw.pos), 0};
         write_struct(w, L.in, si, cl, ck, 0, false, flags);
-        gw.jump(w.n);
+        gw.pos += (uint32_t)w.n;
       }
     }
   }
-  gw.flush();
   const uint32_t dsb = hdr0 + sbytes;
-  if (l == 0) { Out w{o + dsb, 0}; w.vu(nseg); }
+  if (l == 0) { LWriter w{lo, dsb}; w.vu(nseg); }
   const uint32_t d0 = l * W_DE, d1 = min(d0 + W_DE, D);
-  GWriter dw; dw.init(o, dsb + vu_len(nseg) + (d0 < D ? L.dposs[d0] : dsbytes));
+  LWriter dw{lo, dsb + vu_len(nseg) + (d0 < D ? L.dposs[d0] : dsbytes)};
   for (uint32_t j = d0; j < d1; j++) {
     const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.dkey[j] >> 32), ck = (uint32_t)L.dkey[j];
-    if (L.dflag[j] & 1) { dw.vu(cl); dw.vu(L.segcnt[L.dsid[j]]); }
+    if (L.dflag[j] & 1) { dw.vu(cl); dw.vu(L.segcnt[L.dflag[j] >> 2]); }
     if (L.dflag[j] & 2) { dw.vu(ck); dw.vu(L.drunend[j] - ck); }
   }
-  dw.flush();
+  wave_sync();
+  // ---- coalesced copy-out (the slot is 16-byte aligned and holds align16(size) bytes)
+  const uint32_t nch = (uint32_t)((size + 15) / 16);
+  for (uint32_t c = l; c < nch; c += WAVE) *(uint4*)(o + 16 * c) = *(const uint4*)(L.out + 16 * c);
   DIAGW(7);
 }
 
@@ -732,7 +781,8 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
                                                   const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
                                                   uint32_t n_fb, uint32_t flags, uint8_t* __restrict__ out,
                                                   uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len,
-                                                  int32_t* __restrict__ status, DocMeta* meta, SeqScratch scr, uint64_t out_cap) {
+                                                  int32_t* __restrict__ status, DocMeta* meta, SeqScratch scr, uint64_t slot_total,
+                                                  uint64_t out_cap) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= n_fb) return;
   const uint32_t d = fb_list[q];
@@ -766,7 +816,7 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
   }
   uint64_t at = 0;
   if (st == ST_OK) {
-    at = meta->fast_total + meta->m_total + atomicAdd(&meta->seq_cursor, (unsigned long long)size);
+    at = merge_place(upd_off, doc_upd, d, size, slot_total, meta);
     if (at + size > out_cap) st = ST_NOMEM;
   }
   if (st == ST_OK) {  // write pass: block count, structs, delete set
@@ -780,6 +830,7 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
       else ds_union_write(drec, (uint64_t)nr, flags, o);
     }
   }
+  if (st == ST_OK) atomicAdd(&meta->payload, (unsigned long long)size);
   out_off[d] = at; out_len[d] = st == ST_OK ? size : 0; status[d] = st;
 }
 
@@ -815,31 +866,31 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
 }
 
 int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
-                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta,
+                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
                             uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
   if (n_docs == 0) return 0;
   hipLaunchKernelGGL(k_merge_wave, dim3((n_docs + W_WAVES - 1) / W_WAVES), dim3(WAVE * W_WAVES), 0, s, arena, upd_off, doc_upd, n_docs,
-                     flags, out, out_off, out_len, status, lb, (DocMeta*)meta, defer_list, fb_list, out_cap);
+                     flags, out, out_off, out_len, status, (DocMeta*)meta, defer_list, fb_list, out_cap);
   return (int)hipGetLastError();
 }
 
 int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
-                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* lb,
+                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, uint64_t slot_total,
                             void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
   if (n_docs == 0) return 0;
   hipLaunchKernelGGL(k_merge_fast, dim3(n_docs), dim3(M_NT), 0, s, arena, upd_off, doc_upd, docs, n_docs, flags, out, out_off, out_len,
-                     status, lb, (DocMeta*)meta, fb_list, out_cap);
+                     status, slot_total, (DocMeta*)meta, fb_list, out_cap);
   return (int)hipGetLastError();
 }
 
 int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list, uint32_t n_fb,
                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
                            void* readers, int* order, int* tmp, const uint8_t** ubase, uint32_t* ulen, uint64_t upd_cap,
-                           uint32_t* cnt, void* drec, uint64_t byte_cap, uint64_t out_cap, hipStream_t s) {
+                           uint32_t* cnt, void* drec, uint64_t byte_cap, uint64_t slot_total, uint64_t out_cap, hipStream_t s) {
   if (n_fb == 0) return 0;
   SeqScratch scr{(Stream*)readers, order, tmp, ubase, ulen, cnt, (DRec*)drec, upd_cap, byte_cap};
   hipLaunchKernelGGL(k_merge_seq, dim3((n_fb + 63) / 64), dim3(64), 0, s, arena, upd_off, doc_upd, fb_list, n_fb, flags, out, out_off,
-                     out_len, status, (DocMeta*)meta, scr, out_cap);
+                     out_len, status, (DocMeta*)meta, scr, slot_total, out_cap);
   return (int)hipGetLastError();
 }
 

@@ -46,7 +46,7 @@ class _Result(ctypes.Structure):
 
 class _DevResult(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("off", ctypes.c_void_p), ("len", ctypes.c_void_p),
-                ("status", ctypes.c_void_p), ("data_bytes", ctypes.c_uint64)]
+                ("status", ctypes.c_void_p), ("data_bytes", ctypes.c_uint64), ("payload_bytes", ctypes.c_uint64)]
 
 
 class Stats(ctypes.Structure):
@@ -116,7 +116,8 @@ class DeviceResult:
     off: int
     len: int
     status: int
-    data_bytes: int
+    data_bytes: int      # used extent of `data` (merge outputs sit in per-document slots)
+    payload_bytes: int   # sum of the per-document output lengths
 
 
 class Engine:
@@ -233,7 +234,7 @@ class Engine:
                                        ctypes.byref(r))
         if st != OK:
             raise YjsError(st)
-        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)
 
     def diff_device(self, d_arena, arena_bytes, d_doc_off, d_sv, d_sv_off, n_docs, stream=0) -> DeviceResult:
         r = _DevResult()
@@ -241,7 +242,7 @@ class Engine:
                                       ctypes.byref(r))
         if st != OK:
             raise YjsError(st)
-        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)
 
     def sv_device(self, d_arena, arena_bytes, d_doc_off, n_docs, stream=0) -> DeviceResult:
         r = _DevResult()
@@ -249,7 +250,7 @@ class Engine:
                                                 ctypes.byref(r))
         if st != OK:
             raise YjsError(st)
-        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)
 
     def stats(self) -> Stats:
         s = Stats()

@@ -95,16 +95,23 @@ int ygm_sv_from_update_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *do
 
 /* ---- device-resident API (inputs already in HBM; used by bench.py) --------
  * All pointers are device pointers.  doc_upd: n_docs+1 update-index offsets
- * (document d owns updates doc_upd[d] .. doc_upd[d+1]).  Results stay on the
- * device: the data/off/len/status pointers of the result point into context-owned device
- * memory.  `stream` is a hipStream_t (NULL = the context's stream); the call
- * is asynchronous except for one 8-byte read of the output size. */
+ * (document d owns updates doc_upd[d] .. doc_upd[d+1]); upd_off must be
+ * non-decreasing.  Results stay on the device: the data/off/len/status
+ * pointers of the result point into context-owned device memory.  Merge
+ * outputs are NOT packed: document d's bytes are data[off[d] .. off[d]+len[d])
+ * inside its own slot (2*in_off + 64*d, capacity 2*|in| + 64) or, when they
+ * outgrow it, in an overflow region after the slots; data_bytes is the used
+ * extent of `data`, payload_bytes the sum of len[].  SV/diff outputs are
+ * packed in document order (payload_bytes == data_bytes).  `stream` is a
+ * hipStream_t (NULL = the context's stream); the call returns after one
+ * 64-byte read of the launch counters. */
 typedef struct {
   uint8_t *data;
   uint64_t *off;
   uint64_t *len;
   int32_t *status;
   uint64_t data_bytes;
+  uint64_t payload_bytes;
 } ygm_device_result;
 
 int ygm_merge_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_upd_off,

@@ -1,4 +1,4 @@
-"""Phase breakdown of k_merge_fast on the C2 workload (diagnostic build libygm_diag.so)."""
+"""Phase breakdown of the merge kernels on the C2 workload (diagnostic build libygm_diag.so; tooling, not product)."""
 import ctypes
 import os
 import sys
@@ -23,8 +23,8 @@ for rep in range(3):
     L.ygm_diag_read(buf.ctypes.data, 1)
     e.merge_packed(arena, upd_off, upd_doc, n_docs)
     L.ygm_diag_read(buf.ctypes.data, 0)
-for title, names, lo in (("k_merge_wave (wave per document)", ["stage", "passA", "passB", "sort", "classify+scan", "deleteset", "lookback", "emit"], 8),
-                         ("k_merge_fast (workgroup per document)", ["stage", "passA", "scan+passB", "sort", "classify", "deleteset", "lookback", "emit"], 0)):
+for title, names, lo in (("k_merge_wave (wave per document)", ["stage", "parse", "clients+sort", "classify+scan", "-", "deleteset", "-", "emit"], 8),
+                         ("k_merge_fast (workgroup per document)", ["stage", "passA", "scan+passB", "sort", "classify", "deleteset", "place", "emit"], 0)):
     tot = buf[lo:lo + 8].sum()
     if tot == 0:
         continue

@@ -19,8 +19,11 @@ size_t ygm_k_drec_bytes();
 int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,
                      uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
                      unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
-int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
-                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
+int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
+                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list,
+                            uint64_t out_cap, hipStream_t s);
+int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
+                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
                             uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
                             uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, uint64_t slot_total,
@@ -35,8 +38,14 @@ namespace {
 
 // mirrors ygm::DocMeta (ygm_kernels.hip)
 struct Meta {
-  unsigned int ticket, fault, fb_count, defer_count, ticket_m, pad[3];
+  unsigned int ticket, fault, fb_count, defer_count, lean_defer, pad[3];
   unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor;
+  unsigned long long payload_sh[16 * 16];
+  unsigned long long payload_total() const {
+    unsigned long long t = payload;
+    for (unsigned long long x : payload_sh) t += x;
+    return t;
+  }
 };
 
 struct DevBuf {
@@ -65,7 +74,8 @@ struct ygm_ctx {
   // device inputs (host API staging)
   DevBuf arena, offs, docs, sv_arena, sv_offs;
   // device outputs + state
-  DevBuf out, out_off, out_len, status, lb, meta, fb_list, defer_list;
+  DevBuf out, out_off, out_len, status, lb, meta, fb_list, defer_list, defer2_list;
+  Meta* h_meta = nullptr;  // pinned read-back of the per-launch counters
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
   // host results
   std::vector<uint8_t> h_data;
@@ -111,6 +121,7 @@ int ygm_open(int device, uint32_t flags, ygm_ctx** out) {
     return YGM_EDEVICE;
   }
   if (!c->meta.ensure(sizeof(Meta))) { ygm_close(c); return YGM_ENOMEM; }
+  if (hipHostMalloc((void**)&c->h_meta, sizeof(Meta), hipHostMallocDefault) != hipSuccess) { c->h_meta = nullptr; ygm_close(c); return YGM_ENOMEM; }
   *out = c;
   return YGM_OK;
 }
@@ -120,10 +131,11 @@ void ygm_close(ygm_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
-                    &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
+                    &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
                     &c->s_drec})
     b->release();
   for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
+  if (c->h_meta) (void)hipHostFree(c->h_meta);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -135,14 +147,21 @@ int ygm_stats(ygm_ctx* c, ygm_stats_t* out) {
 }
 
 // ------------------------------------------------------------------ device API
-static int prep_outputs(ygm_ctx* c, uint32_t n_docs, uint64_t out_cap, hipStream_t s) {
-  const size_t tiles = 2 * (size_t)n_docs + 2;  // two look-back regions (wave kernel, workgroup kernel)
+static int prep_outputs(ygm_ctx* c, uint32_t n_docs, uint64_t out_cap, hipStream_t s, bool lookback) {
+  const size_t tiles = (size_t)n_docs / 256 + 2;  // look-back tiles of the SV/diff kernels (256 documents each)
   if (!c->out.ensure(out_cap + 64) || !c->out_off.ensure((size_t)n_docs * 8 + 8) || !c->out_len.ensure((size_t)n_docs * 8 + 8) ||
       !c->status.ensure((size_t)n_docs * 4 + 4) || !c->lb.ensure(tiles * 8) || !c->fb_list.ensure((size_t)n_docs * 4 + 4) ||
-      !c->defer_list.ensure((size_t)n_docs * 4 + 4))
+      !c->defer_list.ensure((size_t)n_docs * 4 + 4) || !c->defer2_list.ensure((size_t)n_docs * 4 + 4))
     return YGM_ENOMEM;
-  HIPCHK(hipMemsetAsync(c->lb.p, 0, tiles * 8, s));
+  if (lookback) HIPCHK(hipMemsetAsync(c->lb.p, 0, tiles * 8, s));
   HIPCHK(hipMemsetAsync(c->meta.p, 0, sizeof(Meta), s));
+  return YGM_OK;
+}
+
+static int read_meta(ygm_ctx* c, hipStream_t s, Meta& m) {
+  HIPCHK(hipMemcpyAsync(c->h_meta, c->meta.p, sizeof(Meta), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  m = *c->h_meta;
   return YGM_OK;
 }
 
@@ -164,29 +183,38 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
   // then the overflow region for outputs that outgrow their slot (<= 3|in| + 16/doc)
   const uint64_t slot_total = 2 * arena_bytes + 64ull * n_docs;
   const uint64_t out_cap = slot_total + 3 * arena_bytes + 16ull * n_docs + 64;
-  int e = prep_outputs(c, n_docs, out_cap, s);
+  int e = prep_outputs(c, n_docs, out_cap, s, false);
   if (e) return e;
+  Meta m;
+  float ms0 = 0;
+  // tier 1: lean wave-per-document kernel (debounce-log shape); everything else is deferred
   HIPCHK(hipEventRecord(c->e0, s));
-  if (ygm_k_launch_merge_wave(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
-                              c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->meta.p, c->defer_list.as<uint32_t>(),
-                              c->fb_list.as<uint32_t>(), out_cap, s))
+  if (ygm_k_launch_merge_lean(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
+                              c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->meta.p, c->defer_list.as<uint32_t>(), out_cap, s))
     return YGM_EDEVICE;
   HIPCHK(hipEventRecord(c->e1, s));
-  Meta m;
-  HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  if ((e = read_meta(c, s, m))) return e;
   if (m.fault) return YGM_EDEVICE;
-  float ms0 = 0;
-  if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
-  if (m.defer_count) {  // documents over the wave class: one workgroup per document
+  if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) { c->stats.kernel_ms += ms0; c->stats.lean_ms += ms0; }
+  if (m.lean_defer) {  // tier 2: general wave-per-document kernel over the deferred list
     HIPCHK(hipEventRecord(c->e0, s));
-    if (ygm_k_launch_merge_fast(d_arena, d_upd_off, d_doc_upd, c->defer_list.as<uint32_t>(), m.defer_count, c->flags,
+    if (ygm_k_launch_merge_wave(d_arena, d_upd_off, d_doc_upd, c->defer_list.as<uint32_t>(), m.lean_defer, c->flags, c->out.as<uint8_t>(),
+                                c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->meta.p,
+                                c->defer2_list.as<uint32_t>(), c->fb_list.as<uint32_t>(), out_cap, s))
+      return YGM_EDEVICE;
+    HIPCHK(hipEventRecord(c->e1, s));
+    if ((e = read_meta(c, s, m))) return e;
+    if (m.fault) return YGM_EDEVICE;
+    if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
+  }
+  if (m.defer_count) {  // tier 3: documents over the wave class, one workgroup per document
+    HIPCHK(hipEventRecord(c->e0, s));
+    if (ygm_k_launch_merge_fast(d_arena, d_upd_off, d_doc_upd, c->defer2_list.as<uint32_t>(), m.defer_count, c->flags,
                                 c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
                                 slot_total, c->meta.p, c->fb_list.as<uint32_t>(), out_cap, s))
       return YGM_EDEVICE;
     HIPCHK(hipEventRecord(c->e1, s));
-    HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if ((e = read_meta(c, s, m))) return e;
     if (m.fault) return YGM_EDEVICE;
     if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
   }
@@ -201,16 +229,16 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
                                c->s_readers.p, c->s_order.as<int>(), c->s_tmp.as<int>(), c->s_ubase.as<const uint8_t*>(),
                                c->s_ulen.as<uint32_t>(), upd_cap, c->s_cnt.as<uint32_t>(), c->s_drec.p, byte_cap, slot_total, out_cap, s))
       return YGM_EDEVICE;
-    HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if ((e = read_meta(c, s, m))) return e;
     c->stats.docs_seq += m.fb_count;
   }
   const uint64_t extent = slot_total + m.cursor;
   c->stats.calls++; c->stats.docs += n_docs; c->stats.updates += n_upd;
   c->stats.docs_fast += n_docs - m.fb_count;
-  c->stats.bytes_in += arena_bytes; c->stats.bytes_out += m.payload;
+  c->stats.docs_lean += n_docs - m.lean_defer;
+  c->stats.bytes_in += arena_bytes; c->stats.bytes_out += m.payload_total();
   fill_dev_result(c, extent, out);
-  out->payload_bytes = m.payload;
+  out->payload_bytes = m.payload_total();
   return YGM_OK;
 }
 
@@ -220,7 +248,7 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   (void)hipSetDevice(c->device);
   const uint64_t out_cap = 2 * arena_bytes + 32ull * n_docs + 64;
-  int e = prep_outputs(c, n_docs, out_cap, s);
+  int e = prep_outputs(c, n_docs, out_cap, s, true);
   if (e) return e;
   HIPCHK(hipEventRecord(c->e0, s));
   if (ygm_k_launch_doc(mode, d_arena, d_doc_off, d_sv, d_sv_off, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
@@ -228,8 +256,7 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
     return YGM_EDEVICE;
   HIPCHK(hipEventRecord(c->e1, s));
   Meta m;
-  HIPCHK(hipMemcpyAsync(&m, c->meta.p, sizeof m, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  if ((e = read_meta(c, s, m))) return e;
   if (m.fault) return YGM_EDEVICE;
   float ms = 0;
   if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;

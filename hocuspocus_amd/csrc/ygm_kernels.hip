@@ -16,20 +16,29 @@
 // fast region through an atomic cursor (offsets are reported per document).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ygm_common.hpp"
 #include "ygm_merge_seq.hpp"
 #include "ygm_merge_wave.hpp"
+#include "ygm_merge_lean.hpp"
 #include "ygm_seqdoc.hpp"
 #include "ygm_v1.hpp"
 
 #ifdef YGM_DIAG
 // diagnostic build only (libygm_diag.so): per-phase shader-clock sums of k_merge_fast
-__device__ unsigned long long ygm_diag[16];
+__device__ unsigned long long ygm_diag[24];
 #define DIAG_T0 unsigned long long _dt = __builtin_amdgcn_s_memtime();
 #define DIAG(i) do { if (threadIdx.x == 0) { unsigned long long _n = __builtin_amdgcn_s_memtime(); atomicAdd(&ygm_diag[i], _n - _dt); _dt = _n; } } while (0)
 #define DIAGW(i) do { if ((threadIdx.x & 63) == 0) { unsigned long long _n = __builtin_amdgcn_s_memtime(); atomicAdd(&ygm_diag[8 + (i)], _n - _dt); _dt = _n; } } while (0)
+// lean kernel: absolute shader-clock stamps per document (no atomics): ygm_diag_ts[(d % 16384) * 8 + slot]
+__device__ unsigned long long ygm_diag_ts[16384 * 8];
+// (s_memrealtime: the chip-wide 100 MHz clock, comparable across waves and XCDs)
+#define DIAGL_T0 if (threadIdx.x == 0) ygm_diag_ts[(blockIdx.x & 16383u) * 8] = __builtin_amdgcn_s_memrealtime();
+#define DIAGL(i) do { if (threadIdx.x == 0) ygm_diag_ts[(blockIdx.x & 16383u) * 8 + 1 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define DIAGL_T0
+#define DIAGL(i)
 #define DIAGW(i)
 #define DIAG_T0
 #define DIAG(i)
@@ -46,7 +55,7 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned int fault;
   unsigned int fb_count;            // documents sent to the sequential kernel
   unsigned int defer_count;         // documents sent from the wave kernel to the workgroup kernel
-  unsigned int ticket_m;            // tickets of the workgroup kernel
+  unsigned int lean_defer;          // documents sent from the lean kernel to the wave kernel
   unsigned int pad[3];
   unsigned long long fast_total;    // SV/diff: bytes of the packed (look-back placed) output
   unsigned long long cursor;        // merge: bytes in the overflow region (after the per-document slots)
@@ -55,7 +64,9 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned long long fb_bytes;
   unsigned long long scr_upd_cursor;
   unsigned long long scr_byte_cursor;
+  unsigned long long payload_sh[16 * 16]; // merge: output lengths summed in 16 shards, one 128-B line each (no hot atomic line)
 };
+YDEV void add_payload(DocMeta* m, uint32_t d, uint64_t n) { atomicAdd(&m->payload_sh[(d & 15u) * 16u], (unsigned long long)n); }
 
 // Merge output placement.  Document d owns the 16-byte aligned slot starting at
 // align16(2*b0 + 64d) with capacity 2*(b1-b0) + 48 (b0, b1 = its input byte
@@ -407,7 +418,7 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
   const uint64_t base = L.base;
   if (st == ST_OK && base + size > out_cap) st = ST_NOMEM;
   if (t == 0) {
-    if (st == ST_OK) atomicAdd(&meta->payload, (unsigned long long)size);
+    if (st == ST_OK) add_payload(meta, d, size);
     out_off[d] = base; out_len[d] = st == ST_OK ? size : 0; status[d] = st;
   }
   if (st != ST_OK) return;
@@ -452,7 +463,8 @@ YDEV uint32_t wave_min_u32(uint32_t v) {
 }
 
 __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
-                                                               const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t flags,
+                                                               const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ docs,
+                                                               uint32_t n_docs, uint32_t flags,
                                                                uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                                uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
                                                                DocMeta* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap) {
@@ -461,8 +473,9 @@ __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __
   const uint32_t l = threadIdx.x % WAVE;
   WaveLds& L = LS[threadIdx.x / WAVE];
   LWave* LW = (LWave*)&L;
-  const uint32_t d = blockIdx.x * W_WAVES + threadIdx.x / WAVE;
-  if (d >= n_docs) return;
+  const uint32_t di = blockIdx.x * W_WAVES + threadIdx.x / WAVE;
+  if (di >= n_docs) return;
+  const uint32_t d = docs ? docs[di] : di;
   const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
   const uint32_t k = u1 - u0;
   const uint64_t b0 = upd_off[u0], b1 = upd_off[u1];
@@ -709,7 +722,7 @@ __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __
   DIAGW(5);
   if (st == ST_OK && slot + size > out_cap) st = ST_NOMEM;
   if (l == 0) {
-    if (st == ST_OK) atomicAdd(&meta->payload, (unsigned long long)size);
+    if (st == ST_OK) add_payload(meta, d, size);
     out_off[d] = slot; out_len[d] = st == ST_OK ? size : 0;
     status[d] = st == ST_DEFER ? ST_FALLBACK : st;
     if (st == ST_DEFER) defer_list[atomicAdd(&meta->defer_count, 1u)] = d;
@@ -766,6 +779,291 @@ __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __
   const uint32_t nch = (uint32_t)((size + 15) / 16);
   for (uint32_t c = l; c < nch; c += WAVE) *(uint4*)(o + 16 * c) = *(const uint4*)(L.out + 16 * c);
   DIAGW(7);
+}
+
+
+// ======================================================================= merge: lean fast path
+// Persistent waves (ygm_merge_lean.hpp): wave w takes documents w, w + G, w + 2G, ...
+// While document i is parsed, the chunk loads of document i + 1 are in flight (register
+// prefetch) and the scalar header loads of documents i + 1 / i + 2 run ahead of them.
+// Documents outside the lean shape are appended to `defer_list` for k_merge_wave.
+struct LeanHdr { uint32_t u0, k; uint64_t b0, nbytes; };
+
+// Document headers come through VECTOR loads (lane-dependent addresses, then readlane): a
+// scalar load would share lgkmcnt with the LDS traffic of the document being parsed, and
+// every LDS wait would then also wait for the header's trip to memory.
+YDEV uint32_t lean_du_load(const uint32_t* __restrict__ doc_upd, uint32_t d, uint32_t n_docs) {
+  const uint32_t l = threadIdx.x;
+  return d < n_docs ? doc_upd[d + (l & 1u)] : 0u;          // lanes 0 / 1: doc_upd[d], doc_upd[d + 1]
+}
+YDEV uint64_t lean_bo_load(const uint64_t* __restrict__ upd_off, uint32_t du, uint32_t d, uint32_t n_docs) {
+  const uint32_t u0 = rdlane(du, 0), u1 = rdlane(du, 1);
+  return d < n_docs ? upd_off[(threadIdx.x & 1u) ? u1 : u0] : 0ull;
+}
+YDEV LeanHdr lean_hdr_of(uint32_t du, uint64_t bo) {
+  LeanHdr h;
+  h.u0 = rdlane(du, 0); h.k = rdlane(du, 1) - h.u0;
+  const uint64_t b0 = ((uint64_t)rdlane((uint32_t)(bo >> 32), 0) << 32) | rdlane((uint32_t)bo, 0);
+  const uint64_t b1 = ((uint64_t)rdlane((uint32_t)(bo >> 32), 1) << 32) | rdlane((uint32_t)bo, 1);
+  h.b0 = b0; h.nbytes = b1 - b0;
+  return h;
+}
+YDEV bool lean_stageable(const LeanHdr& h) {
+  return h.k >= 2 && h.k <= (uint32_t)(WAVE * LN_ROWS) && (h.b0 & 15u) + h.nbytes <= (uint64_t)LN_IN;
+}
+// issues the loads of one document: staged chunks and the per-row update offsets.  Every
+// load is unconditional (clamped addresses) so the prefetch registers are dead between the
+// staging of one document and the prefetch of the next (no loop-carried live ranges).
+YDEV void lean_prefetch(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off, const LeanHdr& h, bool go,
+                        u32x4 (&v)[LN_IN / 16 / WAVE], uint32_t (&rx)[LN_ROWS], uint32_t (&ry)[LN_ROWS]) {
+  const uint32_t l = threadIdx.x;
+  const uint64_t a0 = go ? (h.b0 & ~15ull) : 0ull;
+  const uint32_t last = go ? (uint32_t)(((h.b0 & 15u) + h.nbytes + 15) / 16) - 1u : 0u;
+#pragma unroll
+  for (int j = 0; j < LN_IN / 16 / WAVE; j++) {
+    const uint32_t c = l + WAVE * j;
+    v[j] = *(const u32x4*)(arena + a0 + 16ull * (c < last ? c : last));
+  }
+  // low dwords only (offsets inside one document differ by < 2^32; whole-register loads keep
+  // the allocator from reusing a dead high half while the load is in flight -- a forced wait)
+  const uint32_t* off32 = (const uint32_t*)upd_off;
+  const uint32_t kk = go ? h.k : 0u;
+#pragma unroll
+  for (int q = 0; q < LN_ROWS; q++) {
+    const uint32_t i = l + WAVE * q;
+    const uint32_t ix = h.u0 + (i < kk ? i : 0u);
+    rx[q] = off32[2ull * ix]; ry[q] = off32[2ull * ix + 2];
+  }
+}
+
+__global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+                                                     const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t flags,
+                                                     uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
+                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
+                                                     uint32_t* __restrict__ defer_list, uint64_t out_cap) {
+  __shared__ LeanLds LS;
+  LB8* lin = (LB8*)LS.in;
+  LB8* lout = (LB8*)LS.out;
+  const uint32_t l = threadIdx.x;
+  const uint32_t G = gridDim.x;
+  const bool force_seq = (flags & 2u) != 0;
+  uint32_t d = blockIdx.x;
+  uint32_t du = lean_du_load(doc_upd, d, n_docs);
+  LeanHdr hn = lean_hdr_of(du, lean_bo_load(upd_off, du, d, n_docs));
+  du = lean_du_load(doc_upd, d + G, n_docs);                  // header pipeline: doc_upd one document ahead
+  u32x4 v[LN_IN / 16 / WAVE];
+  uint32_t rx[LN_ROWS], ry[LN_ROWS];
+#pragma unroll
+  for (int q = 0; q < LN_ROWS; q++) { rx[q] = 0; ry[q] = 0; }
+  bool gn = !force_seq && lean_stageable(hn);
+  lean_prefetch(arena, upd_off, hn, gn, v, rx, ry);
+  uint64_t payload = 0;   // this wave's output bytes: one atomic per wave, not per document
+  for (; d < n_docs; d += G) {
+    DIAGL_T0
+    const LeanHdr h = hn;
+    const bool go = gn;
+    const uint32_t k = h.k;
+    const uint64_t b0 = h.b0, nbytes = h.nbytes;
+    const uint64_t slot = merge_slot(b0, d), cap = merge_slot_cap(nbytes);
+    const uint32_t shift = (uint32_t)(b0 & 15u);
+    // ---- stage the prefetched document into LDS
+    uint32_t us[LN_ROWS], un[LN_ROWS];
+    if (go) {
+      const uint32_t nch = (uint32_t)((shift + nbytes + 15) / 16);
+#pragma unroll
+      for (int j = 0; j < LN_IN / 16 / WAVE; j++) {
+        const uint32_t c = l + WAVE * j;
+        if (c < nch) *(LB128*)(lin + 16 * c) = v[j];
+      }
+#pragma unroll
+      for (int q = 0; q < LN_ROWS; q++) { us[q] = shift + (rx[q] - (uint32_t)b0); un[q] = ry[q] - rx[q]; }
+      // the output buffer is assembled by OR: zero it
+      const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < (LN_OUT + 48) / 16 / WAVE; j++) *(LB128*)(lout + 16 * (l + WAVE * j)) = z;
+      if (l < (uint32_t)(((LN_OUT + 48) / 16) % WAVE)) *(LB128*)(lout + 16 * (l + WAVE * ((LN_OUT + 48) / 16 / WAVE))) = z;
+    }
+    wave_sync();
+    DIAGL(0);
+#if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 1   // timing experiment: stage only
+    { hn = lean_hdr_of(du, lean_bo_load(upd_off, du, d + G, n_docs)); du = lean_du_load(doc_upd, d + 2 * G, n_docs);
+      gn = !force_seq && lean_stageable(hn); lean_prefetch(arena, upd_off, hn, gn, v, rx, ry); wave_sync(); continue; }
+#endif
+    // ---- header of the next document (its prefetch is issued after the parse) and doc_upd of the one after
+    const uint64_t bo_next = lean_bo_load(upd_off, du, d + G, n_docs);
+    const uint32_t du_next = lean_du_load(doc_upd, d + 2 * G, n_docs);
+    bool defer = !go && !(k < 2 && !force_seq);
+    uint32_t size = 0;
+    if (k < 2 && !force_seq) {   // mergeUpdates([]) = 0000; a single input is returned as is (Y@39011)
+      size = k == 0 ? 2u : (uint32_t)nbytes;
+      if (k == 1 && nbytes > 0xFFFFFFFFull) size = 0;
+      uint8_t* o = out + slot;
+      if (slot + (k == 0 ? 2 : nbytes) > out_cap) { size = 0; if (l == 0) { out_off[d] = slot; out_len[d] = 0; status[d] = ST_NOMEM; } }
+      else {
+        if (k == 0) { if (l == 0) { o[0] = 0; o[1] = 0; } }
+        else for (uint64_t c = l; c * 16 < nbytes; c += WAVE) {   // unaligned 16-byte loads (arena tail padding >= 16), aligned stores
+          uint4 x; __builtin_memcpy(&x, arena + b0 + 16 * c, 16);
+          *(uint4*)(o + 16 * c) = x;
+        }
+        if (l == 0) { out_off[d] = slot; out_len[d] = k == 0 ? 2 : nbytes; status[d] = ST_OK; }
+        payload += k == 0 ? 2 : nbytes;
+      }
+      hn = lean_hdr_of(du, bo_next); du = du_next;
+      gn = !force_seq && lean_stageable(hn);
+      lean_prefetch(arena, upd_off, hn, gn, v, rx, ry);
+      continue;
+    }
+    // ---- parse, lane per update
+    LRec rec[LN_ROWS];
+    bool bad = false;
+    if (go) {
+#pragma unroll
+      for (int q = 0; q < LN_ROWS; q++) {
+        const bool valid = l + WAVE * q < k;
+        if (valid) { rec[q] = lean_parse(lin, us[q], un[q]); bad |= !rec[q].ok; }
+        else { rec[q].ok = true; rec[q].client = 0; rec[q].clock = 0; rec[q].clen = 0; rec[q].span = 0; }
+      }
+    }
+    DIAGL(1);
+    // ---- prefetch the next document while this one is scanned and emitted
+    hn = lean_hdr_of(du, bo_next); du = du_next;
+    gn = !force_seq && lean_stageable(hn);
+    lean_prefetch(arena, upd_off, hn, gn, v, rx, ry);
+    defer = defer || __ballot(bad) != 0;
+#if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 2   // timing experiment: stage + parse
+    if (l == 0) status[d] = (int)bad; wave_sync(); continue;
+#endif
+    if (!defer) {
+      // ---- clients: distinct values by wave vote (<= 4), ranked descending
+      uint32_t bid[LN_ROWS];
+#pragma unroll
+      for (int q = 0; q < LN_ROWS; q++) bid[q] = (l + WAVE * q < k) ? 0xFFu : 0xFEu;
+      uint32_t cl0 = 0, cl1 = 0, cl2 = 0, cl3 = 0, nC = 0;
+      for (int it = 0; it < 5; it++) {
+        uint32_t cand = 0; bool found = false;
+#pragma unroll
+        for (int q = 0; q < LN_ROWS; q++) {
+          const uint64_t m = __ballot(bid[q] == 0xFFu);
+          if (!found && m) { cand = rdlane(rec[q].client, (uint32_t)__builtin_ctzll(m)); found = true; }
+        }
+        if (!found) break;
+        if (nC == 4) { defer = true; break; }
+#pragma unroll
+        for (int q = 0; q < LN_ROWS; q++) if (bid[q] == 0xFFu && rec[q].client == cand) bid[q] = nC;
+        if (nC == 0) cl0 = cand; else if (nC == 1) cl1 = cand; else if (nC == 2) cl2 = cand; else cl3 = cand;
+        nC++;
+      }
+      if (!defer) {
+        // rank (descending client) of each discovery id; ctab = clients by rank
+        const uint32_t cls[4] = {cl0, cl1, cl2, cl3};
+        uint32_t rk[4], ctab[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+          uint32_t r = 0;
+#pragma unroll
+          for (int b = 0; b < 4; b++) r += ((uint32_t)b < nC && cls[b] > cls[a]) ? 1u : 0u;
+          rk[a] = r;
+        }
+#pragma unroll
+        for (int a = 0; a < 4; a++) if ((uint32_t)a < nC) { if (rk[a] == 0) ctab[0] = cls[a]; else if (rk[a] == 1) ctab[1] = cls[a]; else if (rk[a] == 2) ctab[2] = cls[a]; else ctab[3] = cls[a]; }
+        // ---- per-row scans: in-block byte offsets (packed 16-bit fields), predecessor clock checks
+        uint32_t run0 = 0, run1 = 0, nst0 = 0, nst1 = 0;
+        uint32_t last_end[4] = {0, 0, 0, 0}, first_clock[4] = {0, 0, 0, 0};
+        bool have[4] = {false, false, false, false};
+        uint32_t blk[LN_ROWS], inb[LN_ROWS];
+#pragma unroll
+        for (int q = 0; q < LN_ROWS; q++) {
+          const bool valid = l + WAVE * q < k;
+          const uint32_t id = bid[q] & 3u;
+          const uint32_t b = valid ? (id == 0 ? rk[0] : id == 1 ? rk[1] : id == 2 ? rk[2] : rk[3]) : 7u;
+          blk[q] = b;
+          const uint32_t sb = valid ? (rec[q].span & 0xFFu) : 0u, ns = valid ? ((rec[q].span >> 8) & 0xFFu) : 0u;
+          const uint32_t fs = (b & 1u) ? 16u : 0u;
+          const uint32_t p0 = b < 2u ? sb << fs : 0u, p1 = (b >= 2u && b < 4u) ? sb << fs : 0u;
+          nst0 += b < 2u ? ns << fs : 0u; nst1 += (b >= 2u && b < 4u) ? ns << fs : 0u;
+          const uint32_t i0 = dpp_incl_add(p0), i1 = dpp_incl_add(p1);
+          const uint32_t w = b < 2u ? run0 + i0 - p0 : run1 + i1 - p1;
+          inb[q] = (w >> fs) & 0xFFFFu;
+          run0 += lane63(i0); run1 += lane63(i1);
+          // predecessor in the same block: nearest lower lane of this row, else the last record of earlier rows
+          const uint32_t end = rec[q].clock + rec[q].clen;
+          uint64_t mb[4];
+#pragma unroll
+          for (int bb = 0; bb < 4; bb++) mb[bb] = __ballot(b == (uint32_t)bb);
+          const uint64_t mine = b == 0 ? mb[0] : b == 1 ? mb[1] : b == 2 ? mb[2] : mb[3];
+          const uint64_t below = mine & ((1ull << l) - 1ull);
+          const int pl = below ? 63 - __builtin_clzll(below) : 0;
+          const uint32_t pend = (uint32_t)__shfl((int)end, pl, WAVE);
+          const uint32_t lend = b == 0 ? last_end[0] : b == 1 ? last_end[1] : b == 2 ? last_end[2] : last_end[3];
+          const bool hv = b == 0 ? have[0] : b == 1 ? have[1] : b == 2 ? have[2] : have[3];
+          if (valid && (below ? pend != rec[q].clock : (hv && lend != rec[q].clock))) bad = true;
+#pragma unroll
+          for (int bb = 0; bb < 4; bb++) {
+            if (mb[bb]) {
+              last_end[bb] = rdlane(end, 63u - (uint32_t)__builtin_clzll(mb[bb]));
+              if (!have[bb]) { first_clock[bb] = rdlane(rec[q].clock, (uint32_t)__builtin_ctzll(mb[bb])); have[bb] = true; }
+            }
+          }
+        }
+        DIAGL(2);
+        defer = __ballot(bad) != 0;
+#if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 3   // timing experiment: stage + parse + scan
+        if (l == 0) status[d] = (int)bad + (int)(inb[0] & 1) + (int)(inb[1] & 1) + (int)(inb[2] & 1) + (int)(inb[3] & 1); wave_sync(); continue;
+#endif
+        if (!defer) {
+          const uint32_t t0 = lane63(dpp_incl_add(nst0)), t1 = lane63(dpp_incl_add(nst1));
+          const uint32_t cnt[4] = {t0 & 0xFFFFu, t0 >> 16, t1 & 0xFFFFu, t1 >> 16};
+          const uint32_t byt[4] = {run0 & 0xFFFFu, run0 >> 16, run1 & 0xFFFFu, run1 >> 16};
+          uint32_t base[4], hdr[4];
+          uint32_t at = vu_len(nC);
+#pragma unroll
+          for (int b = 0; b < 4; b++) {
+            hdr[b] = vu_len(cnt[b]) + vu_len(ctab[b]) + vu_len(first_clock[b]);
+            base[b] = at;
+            if ((uint32_t)b < nC) at += hdr[b] + byt[b];
+          }
+          size = at + 1;   // + the empty delete set
+          if (size > (uint32_t)LN_OUT || ((size + 15u) & ~15u) > cap || slot + size > out_cap) defer = true;
+          else {
+            // ---- emit into the LDS output buffer: structs (funnel copies), block headers, document header, delete set
+#pragma unroll
+            for (int q = 0; q < LN_ROWS; q++) {
+              if (l + WAVE * q < k) {
+                const uint32_t b = blk[q];
+                const uint32_t t = (b == 0 ? base[0] + hdr[0] : b == 1 ? base[1] + hdr[1] : b == 2 ? base[2] + hdr[2] : base[3] + hdr[3]) + inb[q];
+                lds_or_copy(lout, lin, t, rec[q].span >> 16, rec[q].span & 0xFFu);
+              }
+            }
+            if (l < nC) {
+              const uint32_t bb = l;
+              uint32_t t = bb == 0 ? base[0] : bb == 1 ? base[1] : bb == 2 ? base[2] : base[3];
+              t = lds_vu(lout, t, bb == 0 ? cnt[0] : bb == 1 ? cnt[1] : bb == 2 ? cnt[2] : cnt[3]);
+              t = lds_vu(lout, t, bb == 0 ? ctab[0] : bb == 1 ? ctab[1] : bb == 2 ? ctab[2] : ctab[3]);
+              lds_vu(lout, t, bb == 0 ? first_clock[0] : bb == 1 ? first_clock[1] : bb == 2 ? first_clock[2] : first_clock[3]);
+            }
+            if (l == 0) lds_vu(lout, 0, nC);   // (the final delete-set byte 0 is already zero)
+            wave_sync();
+            DIAGL(3);
+            uint8_t* o = out + slot;
+            const uint32_t nco = (size + 15u) / 16u;
+            for (uint32_t c = l; c < nco; c += WAVE) *(u32x4*)(o + 16 * c) = *(const LB128*)(lout + 16 * c);
+          }
+        }
+      }
+    }
+    if (!defer) payload += size;
+    if (l == 0) {
+      if (defer) {
+        status[d] = ST_FALLBACK;
+        defer_list[atomicAdd(&meta->lean_defer, 1u)] = d;
+      } else {
+        out_off[d] = slot; out_len[d] = size; status[d] = ST_OK;
+      }
+    }
+    DIAGL(4);
+    wave_sync();   // the next document's staging overwrites lin / lout
+  }
+  if (l == 0 && payload) add_payload(meta, blockIdx.x, payload);
 }
 
 // ======================================================================= merge sequential
@@ -830,7 +1128,7 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
       else ds_union_write(drec, (uint64_t)nr, flags, o);
     }
   }
-  if (st == ST_OK) atomicAdd(&meta->payload, (unsigned long long)size);
+  if (st == ST_OK) add_payload(meta, d, size);
   out_off[d] = at; out_len[d] = st == ST_OK ? size : 0; status[d] = st;
 }
 
@@ -842,9 +1140,14 @@ extern "C" {
 using namespace ygm;
 
 #ifdef YGM_DIAG
+int ygm_diag_ts_read(unsigned long long* out, int reset) {  // 16384 x 8 stamps of the lean kernel
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ygm_diag_ts), sizeof(unsigned long long) * 16384 * 8) != hipSuccess) return -1;
+  (void)reset;
+  return 0;
+}
 int ygm_diag_read(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ygm_diag), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-  if (reset) { unsigned long long z[16] = {0}; (void)hipMemcpyToSymbol(HIP_SYMBOL(ygm_diag), z, sizeof z); }
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ygm_diag), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
+  if (reset) { unsigned long long z[24] = {0}; (void)hipMemcpyToSymbol(HIP_SYMBOL(ygm_diag), z, sizeof z); }
   return 0;
 }
 #endif
@@ -865,11 +1168,26 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
   return (int)hipGetLastError();
 }
 
-int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
-                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
+int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
+                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list,
+                            uint64_t out_cap, hipStream_t s) {
+  if (n_docs == 0) return 0;
+  // persistent waves: enough for full occupancy, each looping over documents d, d + G, ...
+  static int n_cu = 0;
+  if (!n_cu) { int dev = 0; (void)hipGetDevice(&dev); if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256; }
+  const char* env = getenv("YGM_LEAN_WAVES_PER_CU");
+  const uint32_t wpc = env ? (uint32_t)atoi(env) : 16u;
+  const uint32_t grid = n_docs < (uint32_t)n_cu * wpc ? n_docs : (uint32_t)n_cu * wpc;
+  hipLaunchKernelGGL(k_merge_lean, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len, status,
+                     (DocMeta*)meta, defer_list, out_cap);
+  return (int)hipGetLastError();
+}
+
+int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
+                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
                             uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
   if (n_docs == 0) return 0;
-  hipLaunchKernelGGL(k_merge_wave, dim3((n_docs + W_WAVES - 1) / W_WAVES), dim3(WAVE * W_WAVES), 0, s, arena, upd_off, doc_upd, n_docs,
+  hipLaunchKernelGGL(k_merge_wave, dim3((n_docs + W_WAVES - 1) / W_WAVES), dim3(WAVE * W_WAVES), 0, s, arena, upd_off, doc_upd, docs, n_docs,
                      flags, out, out_off, out_len, status, (DocMeta*)meta, defer_list, fb_list, out_cap);
   return (int)hipGetLastError();
 }

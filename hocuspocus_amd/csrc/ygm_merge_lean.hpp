@@ -1,0 +1,236 @@
+// ygm_merge_lean.hpp -- mergeUpdates fast path for Hocuspocus debounce logs: ONE WAVE PER
+// DOCUMENT, no calls, no scratch, no per-struct LDS records.
+//
+// Shape it takes (the onChange stream of row a4/a5): k >= 2 updates of
+// <= 32 bytes, each ONE client block of Items (ContentString ASCII / ContentDeleted)
+// and an empty delete set, at most 4 distinct clients, and every client's updates
+// clock-contiguous in log order.  For such a document rule R-M
+// degenerates to: blocks by client descending, each block = the clients' structs in
+// log order, copied byte for byte (Items never merge, Y@79424; no gaps, so no Skips;
+// no GC, so no coalescing), then an empty delete set.  Anything else -- or anything
+// this kernel cannot prove -- is deferred to the general kernels (k_merge_wave ->
+// k_merge_fast -> k_merge_seq), which also produce every error status.
+//
+// Phases (all in registers except the two LDS byte buffers):
+//   stage   every 16-byte chunk load of the document issued before the first wait
+//   parse   lane per update (rows q = 0..3 hold updates l + 64q); the update's bytes are
+//           read as three aligned ds_read_b128 and normalised to a 32-byte register
+//           window; varuint ends come from a terminator bit mask (no byte loop)
+//   clients distinct clients by wave vote, ranked descending (scalar)
+//   scan    per-row DPP scans of packed 16-bit per-client byte counts; predecessor
+//           clock checks by one bpermute per row
+//   emit    ds_or_b32 of funnel-shifted source dwords into a zeroed LDS output buffer
+//           (branch-free, order-free), then 16-byte coalesced stores
+#pragma once
+#include "ygm_common.hpp"
+
+namespace ygm {
+
+constexpr int LN_IN = 5120;     // staged input bytes (including the 0..15 byte alignment shift)
+constexpr int LN_ROWS = 4;      // updates per lane: k <= 256
+constexpr int LN_UMAX = 32;     // bytes per update
+
+constexpr int LN_OUT = 4096;    // staged output bytes
+
+struct alignas(16) LeanLds {
+  uint8_t in[LN_IN + 64];       // + slack: an update's window reads reach 47 bytes past its start
+  uint8_t out[LN_OUT + 48];      // + slack: lds_or_copy ORs zero into up to 36 bytes past a range
+};
+
+typedef __attribute__((address_space(3))) uint8_t LB8;
+typedef __attribute__((address_space(3))) uint32_t LB32;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 LB128;
+
+// ---- DPP wave scans (row_shr within 16-lane rows, then row_bcast:15 / row_bcast:31)
+YDEV uint32_t dpp_incl_add(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);   // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+YDEV uint32_t lane63(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
+YDEV uint32_t rdlane(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
+YDEV uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// ---- register window: bytes 0..39 of one update (U[0] = bytes 0..7)
+// 8 bytes starting at byte p (p <= 31)
+YDEV uint64_t win8(const uint64_t (&U)[5], uint32_t p) {
+  const uint32_t q = p >> 3, sh = (p & 7u) * 8u;
+  const uint64_t a01 = (q & 1) ? U[1] : U[0], a23 = (q & 1) ? U[3] : U[2];
+  const uint64_t b12 = (q & 1) ? U[2] : U[1], b34 = (q & 1) ? U[4] : U[3];
+  const uint64_t lo = (q & 2) ? a23 : a01, hi = (q & 2) ? b34 : b12;
+  return sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+}
+YDEV uint32_t byte_at(const uint64_t (&U)[5], uint32_t p) { return (uint32_t)win8(U, p) & 0xFFu; }
+// value of an n-byte varuint (1 <= n <= 8) whose bytes start the word w
+YDEV uint64_t pext7(uint64_t w, uint32_t n) {
+  uint64_t x = (n >= 8 ? w : (w & ((1ull << (8u * n)) - 1ull))) & 0x7f7f7f7f7f7f7f7full;
+  x = ((x >> 1) & 0x3f803f803f803f80ull) | (x & 0x007f007f007f007full);
+  x = ((x >> 2) & 0x0fffc0000fffc000ull) | (x & 0x00003fff00003fffull);
+  x = ((x >> 4) & 0x00fffffff0000000ull) | (x & 0x000000000fffffffull);
+  return x;
+}
+// 8 bits: bit i = top bit of byte i of the 8 bytes (lo, hi) -- two v_dot4_u32_u8, no multiplies
+YDEV uint32_t hibits8(uint32_t lo, uint32_t hi) {
+  const uint32_t a = __builtin_amdgcn_udot4((lo >> 7) & 0x01010101u, 0x08040201u, 0u, false);
+  return __builtin_amdgcn_udot4((hi >> 7) & 0x01010101u, 0x80402010u, a, false);
+}
+
+// One parsed update (row record).
+struct LRec {
+  uint32_t client, clock, clen;
+  uint32_t span;   // sstart (doc-relative staged position of the first struct) << 16 | nst << 8 | sbytes
+  bool ok;
+};
+
+// Parses the update at staged position s (n bytes).  ok == false: the document is deferred.
+YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
+  LRec R; R.ok = false; R.client = 0; R.clock = 0; R.clen = 0; R.span = 0;
+  if (n < 4 || n > (uint32_t)LN_UMAX) return R;
+  const uint32_t a = s & ~15u, r = s & 15u;
+  const u32x4 c0 = *(const LB128*)(in + a), c1 = *(const LB128*)(in + a + 16), c2 = *(const LB128*)(in + a + 32);
+  const uint32_t w[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+  // normalise: d[j] = bytes 4j..4j+3 of the update = (w[j + r/4 + 1] : w[j + r/4]) >> 8(r & 3)
+  // (mask selects, not ?: -- the compiler turns a ?: of array elements into a scratch-indexed load)
+  const uint32_t m1 = 0u - ((r >> 2) & 1u), m2 = 0u - ((r >> 3) & 1u);
+  uint32_t L[11];
+#pragma unroll
+  for (int j = 0; j < 11; j++) {
+    const uint32_t s0 = (w[j + 1] & m1) | (w[j] & ~m1);
+    const uint32_t s1 = (w[j + 3 > 11 ? 11 : j + 3] & m1) | (w[j + 2 > 11 ? 11 : j + 2] & ~m1);
+    L[j] = (s1 & m2) | (s0 & ~m2);
+  }
+  uint32_t d[10];
+#pragma unroll
+  for (int j = 0; j < 10; j++) d[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], r & 3u);
+  uint64_t U[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++) U[j] = ((uint64_t)d[2 * j + 1] << 32) | d[2 * j];
+  // masks over the n valid bytes: H = top bit set, Z = zero byte
+  // (Z may flag a non-zero byte right above a zero byte -- "haszero" borrow -- which only defers)
+  uint32_t H = 0, Z = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    H |= hibits8(d[2 * j], d[2 * j + 1]) << (8 * j);
+    const uint32_t z0 = (d[2 * j] - 0x01010101u) & ~d[2 * j], z1 = (d[2 * j + 1] - 0x01010101u) & ~d[2 * j + 1];
+    Z |= hibits8(z0, z1) << (8 * j);
+  }
+  const uint32_t V = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+  const uint64_t T = (uint64_t)(~H & V);   // varuint terminators among the valid bytes
+  const uint64_t H64 = (uint64_t)(H & V);
+  bool fail = false, nm = false;
+  // end (index of the terminator) of the varuint at p; fails past the valid bytes or beyond 7 bytes
+#define LN_VEND(p, e)                                                         \
+  do {                                                                        \
+    const uint64_t _t = (p) < 40u ? (T >> (p)) : 0ull;                         \
+    const uint32_t _k = _t ? (uint32_t)__builtin_ctzll(_t) : 40u;              \
+    (e) = (p) + _k;                                                           \
+    fail |= _k > 6u || (e) >= n;                                              \
+    nm |= _k > 0u && (e) < 32u && ((Z >> (e)) & 1u);                          \
+  } while (0)
+  const uint32_t b0 = d[0] & 0xFFu, b1 = (d[0] >> 8) & 0xFFu;
+  fail |= b0 != 1u || b1 == 0u || b1 >= 128u;   // one client block of 1..127 structs
+  uint32_t e;
+  LN_VEND(2u, e);
+  const uint64_t client = pext7(U[0] >> 16 | U[1] << 48, e - 1u);
+  uint32_t p = e + 1u;
+  LN_VEND(p, e);
+  const uint64_t clock = pext7(win8(U, p < 31u ? p : 31u), e - p + 1u);
+  p = e + 1u;
+  fail |= client > 0xFFFFFFFFull || clock > 0xFFFFFFFFull;
+  const uint32_t sstart = p;
+  uint64_t clen = 0;
+  // predicated form: the varuint is consumed only when `on` (branch-free origin / right skips)
+#define LN_VEND_IF(on, p, e)                                                  \
+  do {                                                                        \
+    const uint64_t _t = (p) < 40u ? (T >> (p)) : 0ull;                         \
+    const uint32_t _k = _t ? (uint32_t)__builtin_ctzll(_t) : 40u;              \
+    (e) = (p) + _k;                                                           \
+    fail |= (on) && (_k > 6u || (e) >= n);                                    \
+    nm |= (on) && _k > 0u && (e) < 32u && ((Z >> (e)) & 1u);                  \
+  } while (0)
+  for (uint32_t st = 0; st < b1 && !fail; st++) {
+    fail |= p >= n;
+    const uint32_t info = byte_at(U, p < 31u ? p : 31u); p++;
+    const uint32_t ref = info & 31u;
+    // Skip/GC/other content go to the general path; bit 0x20 is dropped on re-encode when an origin is set
+    fail |= info == 10u || (ref != 1u && ref != 4u) || ((info & 0xC0u) && (info & 0x20u));
+    const uint32_t nsk = ((info >> 6) & 1u) * 2u + ((info >> 7) & 1u) * 2u;   // origin and/or right origin ids
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) { LN_VEND_IF(j < nsk, p, e); p = j < nsk ? e + 1u : p; }
+    if ((info & 0xC0u) == 0u) {   // parent (rare: inserts at the start of a type, map keys)
+      fail |= p >= n;
+      const uint32_t pi = byte_at(U, p < 31u ? p : 31u); p++;
+      if (pi == 1u) {
+        const uint32_t L = p < 32u ? byte_at(U, p) : 255u; p++;
+        fail |= L >= 32u || p + L > n || ((H64 >> p) & ((1ull << L) - 1ull)) != 0;   // ASCII key
+        p += L < 32u ? L : 0u;
+      } else if (pi == 0u) {
+        LN_VEND(p, e); p = e + 1u; LN_VEND(p, e); p = e + 1u;
+      } else fail = true;   // parentInfo is re-encoded as 0/1
+      if (info & 0x20u) {
+        const uint32_t L = p < 32u ? byte_at(U, p) : 255u; p++;
+        fail |= L >= 32u || p + L > n || ((H64 >> p) & ((1ull << L) - 1ull)) != 0;
+        p += L < 32u ? L : 0u;
+      }
+    }
+    fail |= p >= n;
+    if (ref == 1u) {   // ContentDeleted: varuint length
+      LN_VEND(p, e);
+      const uint64_t v = pext7(win8(U, p < 31u ? p : 31u), e - p + 1u);
+      fail |= v == 0 || v > 0xFFFFFFull;
+      clen += v;
+      p = e + 1u;
+    } else {           // ContentString: single-byte length, ASCII bytes (UTF-16 length == byte length)
+      const uint32_t L = byte_at(U, p < 31u ? p : 31u); p++;
+      fail |= L == 0u || L >= 32u || p + L > n || ((H64 >> (p < 40u ? p : 40u)) & ((1ull << (L < 32u ? L : 0u)) - 1ull)) != 0;
+      p += L < 32u ? L : 0u;
+      clen += L;
+    }
+  }
+#undef LN_VEND_IF
+#undef LN_VEND
+  fail |= nm || p >= n || (p < 32u && byte_at(U, p < 31u ? p : 31u) != 0u) || clock + clen > 0xFFFFFFFFull;
+  R.ok = !fail;
+  R.client = (uint32_t)client; R.clock = (uint32_t)clock; R.clen = (uint32_t)clen;
+  R.span = ((s + sstart) << 16) | (b1 << 8) | ((p - sstart) & 0xFFu);
+  return R;
+}
+
+// Copies n (<= 31) bytes from staged input position s to output position t (both LDS) into a
+// ZEROED output buffer: every destination dword the range touches gets ds_or_b32 of the
+// funnel-shifted source bytes masked to the range.  Byte ranges of different lanes are
+// disjoint, so the ORs commute: no edge cases, no branches, no ordering between lanes.
+// Dwords past the range are OR-ed with 0 (the output buffer has slack for them).
+YDEV void lds_or_copy(LB8* out, LB8* in, uint32_t t, uint32_t s, uint32_t n) {
+  const uint32_t head = t & 3u;
+  const uint32_t src0 = s - head;                 // source byte that maps to destination byte t & ~3
+  const uint32_t sb = src0 & 3u;
+  LB32* sw = (LB32*)(in + (src0 & ~3u));
+  uint32_t w[10];
+#pragma unroll
+  for (int j = 0; j < 10; j++) w[j] = sw[j];      // may read past the update: the staged buffer has slack
+  LB32* od = (LB32*)(out + (t & ~3u));
+  const uint32_t last = head + n;                 // destination bytes [head, last) of the dword run are ours
+#pragma unroll
+  for (int j = 0; j < 9; j++) {                   // last <= 34: at most 9 dwords
+    const uint32_t v = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sb);
+    const int a = (int)head - 4 * j, b = (int)last - 4 * j;
+    const uint32_t ca = a < 0 ? 0u : a > 4 ? 4u : (uint32_t)a, cb = b < 0 ? 0u : b > 4 ? 4u : (uint32_t)b;
+    const uint32_t m = (uint32_t)(((1ull << (8u * cb)) - 1ull) ^ ((1ull << (8u * ca)) - 1ull));
+    __hip_atomic_fetch_or(od + j, v & m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+YDEV uint32_t lds_vu(LB8* out, uint32_t t, uint32_t v) {
+  while (v > 127u) { out[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; }
+  out[t++] = (uint8_t)v;
+  return t;
+}
+
+}  // namespace ygm

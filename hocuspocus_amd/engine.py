@@ -21,7 +21,7 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libygm.so")
+LIB_PATH = os.environ.get("YGM_LIB") or os.path.join(_HERE, "libygm.so")  # YGM_LIB: experiment builds (tooling)
 
 OK, EMALFORMED, ERANGE, ENONCANON, ESURROGATE, EDEPTH, ENOMEM, EDEVICE, EINVAL = range(9)
 STATUS_NAMES = {0: "OK", 1: "EMALFORMED", 2: "ERANGE", 3: "ENONCANON", 4: "ESURROGATE", 5: "EDEPTH",
@@ -53,7 +53,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("docs", ctypes.c_uint64), ("updates", ctypes.c_uint64),
                 ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64), ("docs_fast", ctypes.c_uint64),
                 ("docs_seq", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
-                ("d2h_ms", ctypes.c_double)]
+                ("d2h_ms", ctypes.c_double),
+                ("docs_lean", ctypes.c_uint64), ("lean_ms", ctypes.c_double)]
 
 
 _lib = None

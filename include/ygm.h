@@ -72,6 +72,8 @@ typedef struct {
   uint64_t bytes_in, bytes_out;       /* algorithmic bytes */
   uint64_t docs_fast, docs_seq;        /* documents per kernel class */
   double kernel_ms, h2d_ms, d2h_ms;    /* cumulative, HIP-event timed */
+  uint64_t docs_lean;                  /* merges finished by the lean (debounce-log) kernel */
+  double lean_ms;                      /* HIP-event time of the lean kernel launches (part of kernel_ms) */
 } ygm_stats_t;
 
 /* Opens the engine on HIP device `device` (one context per GPU; contexts are

@@ -224,3 +224,30 @@ def test_full_size_c2_properties(eng):
     ups = synth.split(arena, upd_off)
     for dd in range(0, 10000, 97):
         assert (0, merged[dd]) == oracle.merge_updates(ups[doc_upd[dd]:doc_upd[dd + 1]])
+
+
+def test_lean_kernel_takes_debounce_logs(eng):
+    # C2-shaped logs (1-4 clients, per-client clock order) are finished by the lean kernel;
+    # 5-8 clients, shuffled logs and delete-carrying logs are deferred -- all bit-exact.
+    from tools import synth
+    cases = [(dict(min_clients=1, max_clients=4), 0, False, True),
+             (dict(min_clients=5, max_clients=8), 0, False, False),
+             (dict(min_clients=1, max_clients=4), 0, True, None),
+             (dict(min_clients=1, max_clients=3), 15, False, None)]
+    for kw, del_pct, shuffle, all_lean in cases:
+        arena, upd_off, doc_upd = synth.text_updates(300, 120, del_pct=del_pct, seed=77, **kw)
+        ups = synth.split(arena, upd_off)
+        docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(300)]
+        if shuffle:
+            rng = random.Random(3)
+            for dd in docs:
+                rng.shuffle(dd)
+        lean0 = eng.stats().docs_lean
+        res = eng.merge_updates_batch(docs)
+        for d, us in enumerate(docs):
+            assert same(oracle.merge_updates(us), res[d]), (kw, del_pct, shuffle, d)
+        took = eng.stats().docs_lean - lean0
+        if all_lean is True:
+            assert took == 300
+        elif all_lean is False:
+            assert took == 0

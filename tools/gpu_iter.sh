@@ -1,11 +1,9 @@
 #!/bin/bash
 # GPU-box iteration run (gpurun): parity tests, phase diagnostics, bench line, SQ counter pass.
-# Every GPU step has its own time limit; the chain stops at the first failure (pytest: only on a test
-# failure, exit 1, does it go on -- never after a crash or timeout).
+# Every GPU step has its own time limit; the chain stops at the first failure.
 mkdir -p gpurun_out && R=$PWD
-timeout -k 10 600 python -m pytest tests -q -m gpu -x > gpurun_out/gpu_tests.log 2>&1; rc=$?; echo "pytest rc=$rc"
-[ $rc -le 1 ] || exit $rc
-timeout -k 10 120 python tools/diag_phases.py > gpurun_out/diag.log 2>&1 && \
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1 && \
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 120 python -u tools/diag_phases.py > gpurun_out/diag.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1 && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d $R/gpurun_out/prof_sq -o sq -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/prof_sq.log 2>&1

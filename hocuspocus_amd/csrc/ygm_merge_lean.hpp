@@ -89,7 +89,19 @@ struct LRec {
   bool ok;
 };
 
+// value of the <= 5-byte varuint whose first 4 bytes are x and 5th byte is y (n = length)
+YDEV uint32_t pext32(uint32_t x, uint32_t y, uint32_t n) {
+  x &= n >= 4u ? 0xFFFFFFFFu : ((1u << (8u * n)) - 1u);
+  x &= 0x7f7f7f7fu;
+  x = ((x >> 1) & 0x3f803f80u) | (x & 0x007f007fu);
+  x = ((x >> 2) & 0x0fffc000u) | (x & 0x00003fffu);
+  return x | (n >= 5u ? (y & 0x7Fu) << 28 : 0u);
+}
+
 // Parses the update at staged position s (n bytes).  ok == false: the document is deferred.
+// Failure conditions are OR-ed into one integer (no per-condition lane masks); bytes the
+// walk branches on (info, parentInfo, string lengths) are single ds_read_u8 of the staged
+// copy; varuint ends come from the terminator mask T.
 YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
   LRec R; R.ok = false; R.client = 0; R.clock = 0; R.clen = 0; R.span = 0;
   if (n < 4 || n > (uint32_t)LN_UMAX) return R;
@@ -99,21 +111,18 @@ YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
   // normalise: d[j] = bytes 4j..4j+3 of the update = (w[j + r/4 + 1] : w[j + r/4]) >> 8(r & 3)
   // (mask selects, not ?: -- the compiler turns a ?: of array elements into a scratch-indexed load)
   const uint32_t m1 = 0u - ((r >> 2) & 1u), m2 = 0u - ((r >> 3) & 1u);
-  uint32_t L[11];
+  uint32_t L[9];
 #pragma unroll
-  for (int j = 0; j < 11; j++) {
+  for (int j = 0; j < 9; j++) {
     const uint32_t s0 = (w[j + 1] & m1) | (w[j] & ~m1);
-    const uint32_t s1 = (w[j + 3 > 11 ? 11 : j + 3] & m1) | (w[j + 2 > 11 ? 11 : j + 2] & ~m1);
+    const uint32_t s1 = (w[j + 3] & m1) | (w[j + 2] & ~m1);
     L[j] = (s1 & m2) | (s0 & ~m2);
   }
-  uint32_t d[10];
+  uint32_t d[8];
 #pragma unroll
-  for (int j = 0; j < 10; j++) d[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], r & 3u);
-  uint64_t U[5];
-#pragma unroll
-  for (int j = 0; j < 5; j++) U[j] = ((uint64_t)d[2 * j + 1] << 32) | d[2 * j];
-  // masks over the n valid bytes: H = top bit set, Z = zero byte
-  // (Z may flag a non-zero byte right above a zero byte -- "haszero" borrow -- which only defers)
+  for (int j = 0; j < 8; j++) d[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], r & 3u);
+  // masks over the 32 window bytes: H = top bit set, Z = zero byte ("haszero": may also flag a
+  // 0x01 right above a zero byte, which only defers)
   uint32_t H = 0, Z = 0;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
@@ -121,84 +130,96 @@ YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
     const uint32_t z0 = (d[2 * j] - 0x01010101u) & ~d[2 * j], z1 = (d[2 * j + 1] - 0x01010101u) & ~d[2 * j + 1];
     Z |= hibits8(z0, z1) << (8 * j);
   }
-  const uint32_t V = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
-  const uint64_t T = (uint64_t)(~H & V);   // varuint terminators among the valid bytes
-  const uint64_t H64 = (uint64_t)(H & V);
-  bool fail = false, nm = false;
-  // end (index of the terminator) of the varuint at p; fails past the valid bytes or beyond 7 bytes
+  const uint32_t V = n >= 32u ? 0xFFFFFFFFu : ((1u << n) - 1u);
+  const uint32_t T = ~H & V;                 // varuint terminators among the valid bytes
+  const uint32_t HV = H & V;
+  LB8* u = in + s;
+  uint32_t bad = 0, nm = 0;
+  // e = index of the terminator of the varuint at p (<= 7 bytes, inside the update)
 #define LN_VEND(p, e)                                                         \
   do {                                                                        \
-    const uint64_t _t = (p) < 40u ? (T >> (p)) : 0ull;                         \
-    const uint32_t _k = _t ? (uint32_t)__builtin_ctzll(_t) : 40u;              \
-    (e) = (p) + _k;                                                           \
-    fail |= _k > 6u || (e) >= n;                                              \
-    nm |= _k > 0u && (e) < 32u && ((Z >> (e)) & 1u);                          \
+    const uint32_t _p = (p) < 31u ? (p) : 31u;                                \
+    const uint32_t _k = (uint32_t)__builtin_ctz((T >> _p) | 0x80000000u);    \
+    (e) = _p + _k;                                                            \
+    bad |= ((6u - _k) | (n - 1u - (e))) & 0x80000000u;                       \
+    nm |= (Z >> ((e) & 31u)) & ((0u - _k) >> 31);                            \
   } while (0)
+  // ASCII run of L bytes at p inside the update (L <= 31)
+#define LN_ASCII(p, L) (bad |= ((n - (p) - (L)) & 0x80000000u) | ((L) & ~31u) | ((HV >> ((p) < 31u ? (p) : 31u)) & ((1u << ((L) & 31u)) - 1u)))
   const uint32_t b0 = d[0] & 0xFFu, b1 = (d[0] >> 8) & 0xFFu;
-  fail |= b0 != 1u || b1 == 0u || b1 >= 128u;   // one client block of 1..127 structs
-  uint32_t e;
+  bad |= (b0 ^ 1u) | ((b1 - 1u) & ~127u);    // one client block of 1..127 structs
+  uint32_t e, p;
   LN_VEND(2u, e);
-  const uint64_t client = pext7(U[0] >> 16 | U[1] << 48, e - 1u);
-  uint32_t p = e + 1u;
+  const uint32_t cl_n = e - 1u;              // client bytes 2..e
+  const uint32_t client = pext32(__builtin_amdgcn_alignbyte(d[1], d[0], 2u), (d[1] >> 16) & 0xFFu, cl_n);
+  bad |= (cl_n > 5u ? 1u : 0u) | (cl_n == 5u ? ((d[1] >> 16) & 0x70u) : 0u);   // clients are uint32
+  p = e + 1u;                                 // 3..7
   LN_VEND(p, e);
-  const uint64_t clock = pext7(win8(U, p < 31u ? p : 31u), e - p + 1u);
+  const uint32_t ck_n = e - p + 1u;
+  const uint64_t U01 = ((uint64_t)d[1] << 32) | d[0], U23 = ((uint64_t)d[3] << 32) | d[2];
+  const uint64_t cw = (U01 >> (8u * (p & 7u))) | (p & 7u ? (U23 << (64u - 8u * (p & 7u))) : 0ull);   // bytes p..p+7, 3 <= p <= 7
+  const uint32_t clock = pext32((uint32_t)cw, (uint32_t)(cw >> 32) & 0xFFu, ck_n);
+  bad |= (ck_n > 5u ? 1u : 0u) | (ck_n == 5u ? ((uint32_t)(cw >> 32) & 0x70u) : 0u);
   p = e + 1u;
-  fail |= client > 0xFFFFFFFFull || clock > 0xFFFFFFFFull;
   const uint32_t sstart = p;
-  uint64_t clen = 0;
-  // predicated form: the varuint is consumed only when `on` (branch-free origin / right skips)
-#define LN_VEND_IF(on, p, e)                                                  \
-  do {                                                                        \
-    const uint64_t _t = (p) < 40u ? (T >> (p)) : 0ull;                         \
-    const uint32_t _k = _t ? (uint32_t)__builtin_ctzll(_t) : 40u;              \
-    (e) = (p) + _k;                                                           \
-    fail |= (on) && (_k > 6u || (e) >= n);                                    \
-    nm |= (on) && _k > 0u && (e) < 32u && ((Z >> (e)) & 1u);                  \
-  } while (0)
-  for (uint32_t st = 0; st < b1 && !fail; st++) {
-    fail |= p >= n;
-    const uint32_t info = byte_at(U, p < 31u ? p : 31u); p++;
+  uint32_t clen = 0;
+  // structs: the first always, the rest (multi-struct transactions) by the back edge
+  uint32_t st = 0;
+  do {
+    const uint32_t pc = p < 40u ? p : 40u;
+    const uint32_t info = u[pc];
+    p = pc + 1u;
     const uint32_t ref = info & 31u;
     // Skip/GC/other content go to the general path; bit 0x20 is dropped on re-encode when an origin is set
-    fail |= info == 10u || (ref != 1u && ref != 4u) || ((info & 0xC0u) && (info & 0x20u));
+    bad |= (info == 10u ? 1u : 0u) | ((ref != 1u && ref != 4u) ? 1u : 0u) | ((info & 0xC0u) && (info & 0x20u) ? 1u : 0u);
     const uint32_t nsk = ((info >> 6) & 1u) * 2u + ((info >> 7) & 1u) * 2u;   // origin and/or right origin ids
 #pragma unroll
-    for (uint32_t j = 0; j < 4; j++) { LN_VEND_IF(j < nsk, p, e); p = j < nsk ? e + 1u : p; }
+    for (uint32_t j = 0; j < 4; j++) {
+      uint32_t ee;
+      const uint32_t _p = p < 31u ? p : 31u;
+      const uint32_t _k = (uint32_t)__builtin_ctz((T >> _p) | 0x80000000u);
+      ee = _p + _k;
+      const uint32_t on = 0u - (j < nsk ? 1u : 0u);
+      bad |= ((6u - _k) | (n - 1u - ee)) & 0x80000000u & on;
+      nm |= (Z >> (ee & 31u)) & ((0u - _k) >> 31) & on;
+      p = j < nsk ? ee + 1u : p;
+    }
     if ((info & 0xC0u) == 0u) {   // parent (rare: inserts at the start of a type, map keys)
-      fail |= p >= n;
-      const uint32_t pi = byte_at(U, p < 31u ? p : 31u); p++;
+      const uint32_t pi = u[p < 40u ? p : 40u]; p++;
       if (pi == 1u) {
-        const uint32_t L = p < 32u ? byte_at(U, p) : 255u; p++;
-        fail |= L >= 32u || p + L > n || ((H64 >> p) & ((1ull << L) - 1ull)) != 0;   // ASCII key
-        p += L < 32u ? L : 0u;
-      } else if (pi == 0u) {
+        const uint32_t Lk = u[p < 40u ? p : 40u]; p++;
+        LN_ASCII(p, Lk); p += Lk & 31u;
+      } else {
+        bad |= pi;                  // parentInfo is re-encoded as 0/1
         LN_VEND(p, e); p = e + 1u; LN_VEND(p, e); p = e + 1u;
-      } else fail = true;   // parentInfo is re-encoded as 0/1
+      }
       if (info & 0x20u) {
-        const uint32_t L = p < 32u ? byte_at(U, p) : 255u; p++;
-        fail |= L >= 32u || p + L > n || ((H64 >> p) & ((1ull << L) - 1ull)) != 0;
-        p += L < 32u ? L : 0u;
+        const uint32_t Ls = u[p < 40u ? p : 40u]; p++;
+        LN_ASCII(p, Ls); p += Ls & 31u;
       }
     }
-    fail |= p >= n;
     if (ref == 1u) {   // ContentDeleted: varuint length
       LN_VEND(p, e);
-      const uint64_t v = pext7(win8(U, p < 31u ? p : 31u), e - p + 1u);
-      fail |= v == 0 || v > 0xFFFFFFull;
+      const uint32_t pp = p < 31u ? p : 31u;
+      const uint32_t x = u[pp] | ((uint32_t)u[pp + 1] << 8) | ((uint32_t)u[pp + 2] << 16) | ((uint32_t)u[pp + 3] << 24);
+      const uint32_t v = pext32(x, 0u, e - p + 1u);
+      bad |= (v == 0u ? 1u : 0u) | ((e - p) > 2u ? 1u : 0u);   // 1..3 bytes: < 2^21
       clen += v;
       p = e + 1u;
     } else {           // ContentString: single-byte length, ASCII bytes (UTF-16 length == byte length)
-      const uint32_t L = byte_at(U, p < 31u ? p : 31u); p++;
-      fail |= L == 0u || L >= 32u || p + L > n || ((H64 >> (p < 40u ? p : 40u)) & ((1ull << (L < 32u ? L : 0u)) - 1ull)) != 0;
-      p += L < 32u ? L : 0u;
-      clen += L;
+      const uint32_t Lc = u[p < 40u ? p : 40u]; p++;
+      bad |= Lc == 0u ? 1u : 0u;
+      LN_ASCII(p, Lc);
+      p += Lc & 31u;
+      clen += Lc;
     }
-  }
-#undef LN_VEND_IF
+  } while (++st < b1 && (bad | (p >= n ? 1u : 0u)) == 0u);
 #undef LN_VEND
-  fail |= nm || p >= n || (p < 32u && byte_at(U, p < 31u ? p : 31u) != 0u) || clock + clen > 0xFFFFFFFFull;
-  R.ok = !fail;
-  R.client = (uint32_t)client; R.clock = (uint32_t)clock; R.clen = (uint32_t)clen;
+#undef LN_ASCII
+  bad |= nm | ((n - 1u - p) & 0x80000000u) | u[p < 40u ? p : 40u];   // then the empty delete set (count 0)
+  bad |= (uint32_t)(((uint64_t)clock + clen) >> 32);
+  R.ok = bad == 0u;
+  R.client = client; R.clock = clock; R.clen = clen;
   R.span = ((s + sstart) << 16) | (b1 << 8) | ((p - sstart) & 0xFFu);
   return R;
 }

@@ -251,3 +251,87 @@ def test_lean_kernel_takes_debounce_logs(eng):
             assert took == 300
         elif all_lean is False:
             assert took == 0
+
+
+def _lean_edge_docs(n_docs, seed):
+    """Debounce-log-like documents whose updates probe every branch of the lean kernel's
+    parser: string lengths around the 32-byte window, non-ASCII, ContentDeleted, parent
+    keys / ids, parentSub with and without origins, non-minimal varuints, 5-byte clients
+    (some >= 2^32), large clocks, multi-struct updates, trailing bytes, gaps and overlaps."""
+    from v1util import vu
+    rng = random.Random(seed)
+    docs = []
+    for _ in range(n_docs):
+        ncl = rng.choice([1, 1, 2, 3, 4, 5])
+        clients = [rng.choice([rng.randrange(1, 2 ** 32), rng.randrange(1, 200), 2 ** 32 + rng.randrange(5)])
+                   if rng.random() < 0.1 else rng.randrange(1, 2 ** 32) for _ in range(ncl)]
+        clocks = [rng.choice([0, 0, 0, rng.randrange(2 ** 28, 2 ** 31)]) for _ in range(ncl)]
+        ups = []
+        for _ in range(rng.randrange(2, 60)):
+            c = rng.randrange(ncl)
+            nst = 1 if rng.random() < 0.85 else rng.randrange(2, 4)
+            body = bytearray()
+            clen_total = 0
+            for _s in range(nst):
+                kind = rng.random()
+                nm = rng.random() < 0.03
+                def id_(cl, ck):
+                    b = vu(cl) + vu(ck)
+                    return b[:-1] + bytes([b[-1] | 0x80, 0]) if nm else b
+                info, extra = 0, b""
+                shape = rng.random()
+                if shape < 0.6:
+                    info |= 0x80 | 0x40
+                    extra = id_(rng.choice(clients), rng.randrange(300)) + id_(rng.choice(clients), rng.randrange(300))
+                elif shape < 0.7:
+                    info |= 0x80
+                    extra = id_(rng.choice(clients), rng.randrange(300))
+                elif shape < 0.8:
+                    info |= 0x40
+                    extra = id_(rng.choice(clients), rng.randrange(300))
+                elif shape < 0.9:
+                    extra = b"\x01" + vu(1) + b"t"                    # parent ykey
+                    if rng.random() < 0.5:
+                        info |= 0x20
+                        extra += vu(3) + b"key"                      # parentSub
+                else:
+                    extra = b"\x00" + id_(rng.choice(clients), rng.randrange(50))   # parent id
+                if shape < 0.8 and rng.random() < 0.05:
+                    info |= 0x20                                     # dropped on re-encode (origin present)
+                if kind < 0.8:
+                    ln = rng.choice([1, 1, 1, 2, 5, 20, 31, 32, 40])
+                    txt = "".join(rng.choice("abcdefgh") for _ in range(ln))
+                    if rng.random() < 0.05:
+                        txt = txt[:-1] + "é"
+                    raw = txt.encode()
+                    info |= 4
+                    content = vu(len(raw)) + raw
+                    clen = len(txt.encode("utf-16-le")) // 2
+                else:
+                    clen = rng.choice([1, 3, 200, 70000])
+                    info |= 1
+                    content = vu(clen)
+                body += bytes([info]) + extra + content
+                clen_total += clen
+            ck = clocks[c]
+            if rng.random() < 0.02:
+                ck += 1                                              # gap
+            elif rng.random() < 0.02 and ck > 0:
+                ck -= 1                                              # overlap
+            u = vu(1) + vu(nst) + vu(clients[c]) + vu(ck) + bytes(body) + b"\x00"
+            if rng.random() < 0.02:
+                u += b"\x07\x07"                                     # trailing bytes: ignored by yjs
+            ups.append(u)
+            clocks[c] = ck + clen_total
+        docs.append(ups)
+    return docs
+
+
+def test_lean_kernel_edge_shapes_vs_oracle(eng):
+    docs = _lean_edge_docs(1500, seed=4242)
+    lean0 = eng.stats().docs_lean
+    res = eng.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+    assert not bad, (len(bad), [u.hex() for u in docs[bad[0]]])
+    took = eng.stats().docs_lean - lean0
+    assert 0 < took < len(docs)   # both the lean path and the deferral path are exercised

@@ -134,16 +134,14 @@ YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
   const uint32_t T = ~H & V;                 // varuint terminators among the valid bytes
   const uint32_t HV = H & V;
   LB8* u = in + s;
-  uint32_t bad = 0, nm = 0;
-  // e = index of the terminator of the varuint at p (<= 7 bytes, inside the update)
-#define LN_VEND(p, e)                                                         \
-  do {                                                                        \
-    const uint32_t _p = (p) < 31u ? (p) : 31u;                                \
-    const uint32_t _k = (uint32_t)__builtin_ctz((T >> _p) | 0x80000000u);    \
-    (e) = _p + _k;                                                            \
-    bad |= ((6u - _k) | (n - 1u - (e))) & 0x80000000u;                       \
-    nm |= (Z >> ((e) & 31u)) & ((0u - _k) >> 31);                            \
-  } while (0)
+  // Whole-window checks instead of per-varuint ones:
+  //  * a run of >= 7 bytes with the top bit set (a varuint of >= 8 bytes: possibly >= 2^53) defers;
+  //  * a zero byte right after a top-bit byte is a non-minimal varuint terminator (or a client
+  //    id 0 right after an info byte) -- yjs re-encodes those, so the document defers.
+  const uint32_t h2 = HV & (HV >> 1), h4 = h2 & (h2 >> 2), h7 = h4 & (h4 >> 3);
+  uint32_t bad = h7 | (Z & (HV << 1) & V);
+  // position of the terminator of the varuint at p; past the window: >= 31 (then p >= n fails below)
+#define LN_VEND(p, e) ((e) = ((p) < 31u ? (p) : 31u) + (uint32_t)__builtin_ctz((T >> ((p) < 31u ? (p) : 31u)) | 0x80000000u))
   // ASCII run of L bytes at p inside the update (L <= 31)
 #define LN_ASCII(p, L) (bad |= ((n - (p) - (L)) & 0x80000000u) | ((L) & ~31u) | ((HV >> ((p) < 31u ? (p) : 31u)) & ((1u << ((L) & 31u)) - 1u)))
   const uint32_t b0 = d[0] & 0xFFu, b1 = (d[0] >> 8) & 0xFFu;
@@ -172,17 +170,14 @@ YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
     const uint32_t ref = info & 31u;
     // Skip/GC/other content go to the general path; bit 0x20 is dropped on re-encode when an origin is set
     bad |= (info == 10u ? 1u : 0u) | ((ref != 1u && ref != 4u) ? 1u : 0u) | ((info & 0xC0u) && (info & 0x20u) ? 1u : 0u);
-    const uint32_t nsk = ((info >> 6) & 1u) * 2u + ((info >> 7) & 1u) * 2u;   // origin and/or right origin ids
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-      uint32_t ee;
-      const uint32_t _p = p < 31u ? p : 31u;
-      const uint32_t _k = (uint32_t)__builtin_ctz((T >> _p) | 0x80000000u);
-      ee = _p + _k;
-      const uint32_t on = 0u - (j < nsk ? 1u : 0u);
-      bad |= ((6u - _k) | (n - 1u - ee)) & 0x80000000u & on;
-      nm |= (Z >> (ee & 31u)) & ((0u - _k) >> 31) & on;
-      p = j < nsk ? ee + 1u : p;
+    // origin and/or right origin: 2 or 4 varuints -- the 2nd / 4th terminator from p
+    {
+      const uint32_t pp = p < 31u ? p : 31u;
+      const uint32_t t0 = (T >> pp) | 0x80000000u, t1 = t0 & (t0 - 1u), t2 = t1 & (t1 - 1u), t3 = t2 & (t2 - 1u);
+      const uint32_t nsk = ((info >> 6) & 1u) + ((info >> 7) & 1u);   // id pairs
+      const uint32_t e2 = pp + (uint32_t)__builtin_ctz(t1 | 0x80000000u) + 1u;
+      const uint32_t e4 = pp + (uint32_t)__builtin_ctz(t3 | 0x80000000u) + 1u;
+      p = nsk == 2u ? e4 : nsk == 1u ? e2 : p;
     }
     if ((info & 0xC0u) == 0u) {   // parent (rare: inserts at the start of a type, map keys)
       const uint32_t pi = u[p < 40u ? p : 40u]; p++;
@@ -216,6 +211,7 @@ YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
   } while (++st < b1 && (bad | (p >= n ? 1u : 0u)) == 0u);
 #undef LN_VEND
 #undef LN_ASCII
+  const uint32_t nm = 0;
   bad |= nm | ((n - 1u - p) & 0x80000000u) | u[p < 40u ? p : 40u];   // then the empty delete set (count 0)
   bad |= (uint32_t)(((uint64_t)clock + clen) >> 32);
   R.ok = bad == 0u;

@@ -809,7 +809,7 @@ YDEV LeanHdr lean_hdr_of(uint32_t du, uint64_t bo) {
   return h;
 }
 YDEV bool lean_stageable(const LeanHdr& h) {
-  return h.k >= 2 && h.k <= (uint32_t)(WAVE * LN_ROWS) && (h.b0 & 15u) + h.nbytes <= (uint64_t)LN_IN;
+  return h.k >= 2 && h.k < (uint32_t)(WAVE * LN_ROWS) && (h.b0 & 15u) + h.nbytes <= (uint64_t)LN_IN;
 }
 // issues the loads of one document: staged chunks and the per-row update offsets.  Every
 // load is unconditional (clamped addresses) so the prefetch registers are dead between the
@@ -877,11 +877,6 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
       }
 #pragma unroll
       for (int q = 0; q < LN_ROWS; q++) { us[q] = shift + (rx[q] - (uint32_t)b0); un[q] = ry[q] - rx[q]; }
-      // the output buffer is assembled by OR: zero it
-      const u32x4 z = {0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int j = 0; j < (LN_OUT + 48) / 16 / WAVE; j++) *(LB128*)(lout + 16 * (l + WAVE * j)) = z;
-      if (l < (uint32_t)(((LN_OUT + 48) / 16) % WAVE)) *(LB128*)(lout + 16 * (l + WAVE * ((LN_OUT + 48) / 16 / WAVE))) = z;
     }
     wave_sync();
     DIAGL(0);
@@ -966,11 +961,10 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
         }
 #pragma unroll
         for (int a = 0; a < 4; a++) if ((uint32_t)a < nC) { if (rk[a] == 0) ctab[0] = cls[a]; else if (rk[a] == 1) ctab[1] = cls[a]; else if (rk[a] == 2) ctab[2] = cls[a]; else ctab[3] = cls[a]; }
-        // ---- per-row scans: in-block byte offsets (packed 16-bit fields), predecessor clock checks
-        uint32_t run0 = 0, run1 = 0, nst0 = 0, nst1 = 0;
-        uint32_t last_end[4] = {0, 0, 0, 0}, first_clock[4] = {0, 0, 0, 0};
-        bool have[4] = {false, false, false, false};
-        uint32_t blk[LN_ROWS], inb[LN_ROWS];
+        // ---- per-row DPP scans of packed per-block fields: record index in its block (8-bit
+        //      fields, k <= 255) and byte offset in its block (16-bit fields)
+        uint32_t runc = 0, run0 = 0, run1 = 0, nst0 = 0, nst1 = 0;
+        uint32_t blk[LN_ROWS], inb[LN_ROWS], idx[LN_ROWS];
 #pragma unroll
         for (int q = 0; q < LN_ROWS; q++) {
           const bool valid = l + WAVE * q < k;
@@ -978,6 +972,10 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
           const uint32_t b = valid ? (id == 0 ? rk[0] : id == 1 ? rk[1] : id == 2 ? rk[2] : rk[3]) : 7u;
           blk[q] = b;
           const uint32_t sb = valid ? (rec[q].span & 0xFFu) : 0u, ns = valid ? ((rec[q].span >> 8) & 0xFFu) : 0u;
+          const uint32_t pc = valid ? 1u << (8u * b) : 0u;
+          const uint32_t ic = dpp_incl_add(pc);
+          idx[q] = ((runc + ic - pc) >> (8u * (b & 3u))) & 0xFFu;
+          runc += lane63(ic);
           const uint32_t fs = (b & 1u) ? 16u : 0u;
           const uint32_t p0 = b < 2u ? sb << fs : 0u, p1 = (b >= 2u && b < 4u) ? sb << fs : 0u;
           nst0 += b < 2u ? ns << fs : 0u; nst1 += (b >= 2u && b < 4u) ? ns << fs : 0u;
@@ -985,25 +983,40 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
           const uint32_t w = b < 2u ? run0 + i0 - p0 : run1 + i1 - p1;
           inb[q] = (w >> fs) & 0xFFFFu;
           run0 += lane63(i0); run1 += lane63(i1);
-          // predecessor in the same block: nearest lower lane of this row, else the last record of earlier rows
-          const uint32_t end = rec[q].clock + rec[q].clen;
-          uint64_t mb[4];
+        }
+        // ---- contiguity (rule R-M without gaps/overlaps): every record's clock is the end of the
+        //      previous record of its block.  (clock, end) pairs are scattered to their sorted slot in
+        //      the output buffer (free until the emit) and each record reads its predecessor.
+        const uint32_t rcnt[4] = {runc & 0xFFu, (runc >> 8) & 0xFFu, (runc >> 16) & 0xFFu, runc >> 24};
+        const uint32_t rbase[4] = {0u, rcnt[0], rcnt[0] + rcnt[1], rcnt[0] + rcnt[1] + rcnt[2]};
+        LB32* scr = (LB32*)lout;
 #pragma unroll
-          for (int bb = 0; bb < 4; bb++) mb[bb] = __ballot(b == (uint32_t)bb);
-          const uint64_t mine = b == 0 ? mb[0] : b == 1 ? mb[1] : b == 2 ? mb[2] : mb[3];
-          const uint64_t below = mine & ((1ull << l) - 1ull);
-          const int pl = below ? 63 - __builtin_clzll(below) : 0;
-          const uint32_t pend = (uint32_t)__shfl((int)end, pl, WAVE);
-          const uint32_t lend = b == 0 ? last_end[0] : b == 1 ? last_end[1] : b == 2 ? last_end[2] : last_end[3];
-          const bool hv = b == 0 ? have[0] : b == 1 ? have[1] : b == 2 ? have[2] : have[3];
-          if (valid && (below ? pend != rec[q].clock : (hv && lend != rec[q].clock))) bad = true;
-#pragma unroll
-          for (int bb = 0; bb < 4; bb++) {
-            if (mb[bb]) {
-              last_end[bb] = rdlane(end, 63u - (uint32_t)__builtin_clzll(mb[bb]));
-              if (!have[bb]) { first_clock[bb] = rdlane(rec[q].clock, (uint32_t)__builtin_ctzll(mb[bb])); have[bb] = true; }
-            }
+        for (int q = 0; q < LN_ROWS; q++) {
+          if (l + WAVE * q < k) {
+            const uint32_t b = blk[q];
+            const uint32_t j = (b == 0 ? rbase[0] : b == 1 ? rbase[1] : b == 2 ? rbase[2] : rbase[3]) + idx[q];
+            scr[2 * j] = rec[q].clock; scr[2 * j + 1] = rec[q].clock + rec[q].clen;
           }
+        }
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < LN_ROWS; q++) {
+          if (l + WAVE * q < k && idx[q] > 0u) {
+            const uint32_t b = blk[q];
+            const uint32_t j = (b == 0 ? rbase[0] : b == 1 ? rbase[1] : b == 2 ? rbase[2] : rbase[3]) + idx[q];
+            bad |= scr[2 * j - 1] != rec[q].clock;
+          }
+        }
+        uint32_t first_clock[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) first_clock[b] = (uint32_t)__builtin_amdgcn_readfirstlane((int)scr[2 * (rbase[b] < 255u ? rbase[b] : 0u)]);
+        wave_sync();
+        // the output buffer is assembled by OR: zero it
+        {
+          const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int j = 0; j < (LN_OUT + 48) / 16 / WAVE; j++) *(LB128*)(lout + 16 * (l + WAVE * j)) = z;
+          if (l < (uint32_t)(((LN_OUT + 48) / 16) % WAVE)) *(LB128*)(lout + 16 * (l + WAVE * ((LN_OUT + 48) / 16 / WAVE))) = z;
         }
         DIAGL(2);
         defer = __ballot(bad) != 0;
@@ -1025,6 +1038,37 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
           size = at + 1;   // + the empty delete set
           if (size > (uint32_t)LN_OUT || ((size + 15u) & ~15u) > cap || slot + size > out_cap) defer = true;
           else {
+#ifdef YGM_LEAN_GEMIT   // experiment: structs straight to global memory as unaligned dword pieces
+            {
+              uint8_t* o = out + slot;
+#pragma unroll
+              for (int q = 0; q < LN_ROWS; q++) {
+                if (l + WAVE * q < k) {
+                  const uint32_t b = blk[q];
+                  const uint32_t t = (b == 0 ? base[0] + hdr[0] : b == 1 ? base[1] + hdr[1] : b == 2 ? base[2] + hdr[2] : base[3] + hdr[3]) + inb[q];
+                  const uint32_t s0 = rec[q].span >> 16, n = rec[q].span & 0xFFu;   // n >= 4 for every struct the parser accepts
+                  for (uint32_t off = 0; off < n; off += 4) {
+                    const uint32_t oo = off + 4u <= n ? off : n - 4u;           // the last piece overlaps its predecessor
+                    uint32_t v; __builtin_memcpy(&v, (const uint8_t*)(lin + s0 + oo), 4);
+                    __builtin_memcpy(o + t + oo, &v, 4);
+                  }
+                }
+              }
+              if (l < nC) {
+                const uint32_t bb = l;
+                uint64_t t = bb == 0 ? base[0] : bb == 1 ? base[1] : bb == 2 ? base[2] : base[3];
+                uint32_t v = bb == 0 ? cnt[0] : bb == 1 ? cnt[1] : bb == 2 ? cnt[2] : cnt[3];
+                while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; } o[t++] = (uint8_t)v;
+                v = bb == 0 ? ctab[0] : bb == 1 ? ctab[1] : bb == 2 ? ctab[2] : ctab[3];
+                while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; } o[t++] = (uint8_t)v;
+                v = bb == 0 ? first_clock[0] : bb == 1 ? first_clock[1] : bb == 2 ? first_clock[2] : first_clock[3];
+                while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; } o[t++] = (uint8_t)v;
+              }
+              if (l == 0) { uint32_t v = nC; uint64_t t = 0; while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; } o[t++] = (uint8_t)v; o[size - 1] = 0; }
+            }
+            if (false)
+#endif
+            {
             // ---- emit into the LDS output buffer: structs (funnel copies), block headers, document header, delete set
 #pragma unroll
             for (int q = 0; q < LN_ROWS; q++) {
@@ -1047,6 +1091,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
             uint8_t* o = out + slot;
             const uint32_t nco = (size + 15u) / 16u;
             for (uint32_t c = l; c < nco; c += WAVE) *(u32x4*)(o + 16 * c) = *(const LB128*)(lout + 16 * c);
+            }
           }
         }
       }

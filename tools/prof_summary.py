@@ -61,7 +61,7 @@ def pmc(fetch_dir, write_dir, out):
         rd = f.get(k, 0.0) * 1024 * 2
         wr = w.get(k, 0.0) * 1024
         res["kernels"][k] = {"fetch_bytes": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr}
-    main = [k for k in res["kernels"] if "k_merge_wave" in k]
+    main = [k for k in res["kernels"] if "k_merge_lean" in k] or [k for k in res["kernels"] if "k_merge_wave" in k]
     if main:
         res["hbm_bytes_per_launch"] = res["kernels"][main[0]]["hbm_bytes_per_launch"]
     json.dump(res, open(out, "w"), indent=1)

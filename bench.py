@@ -5,8 +5,12 @@
 One step = one batched mergeUpdates over the whole per-GPU workload (10 000
 documents x 200 single-character Y.Text insert updates from 1-4 clients,
 SURVEY.md §8d config C2, BASELINE.json configs[1]) with the inputs already
-resident in HBM: ``ygm_merge_v1_device`` = the wave-per-document kernel launch (each
-document written into its own output slot) and the 64-byte meta read-back.  For N > 1 the
+resident in HBM: ``ygm_merge_v1_device_async`` = the counter reset and the lean
+kernel launch, each document written into its own output slot.  Steps are enqueued
+back to back on one stream; the last one is completed by ``ygm_merge_v1_device_finish``
+(fault check, payload).  Every C2 document is finished by the lean kernel -- asserted
+on the warmup (identical inputs every step) and on the timed run -- so no step needs
+the host-driven wave / workgroup / sequential tiers.  For N > 1 the
 driver starts one process per GPU (torchrun); every rank merges its own shard
 of documents (documents are independent, partitioned by name hash, weak
 scaling) and the time is the max over ranks.  RCCL carries only the timing
@@ -27,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 N_DOCS, N_UPDATES = 10000, 200
-PMC_PROFILE = "r01_lean_v1/pmc_hbm.json"  # latest committed PMC summary of the bench kernel
+PMC_PROFILE = "r01_lean_v2/pmc_hbm.json"  # latest committed PMC summary of the bench kernel
 
 
 def parse():
@@ -99,28 +103,39 @@ def main():
     eng = Engine(local)
 
     def step():
-        return eng.merge_device(d_arena.data_ptr(), len(arena), d_off.data_ptr(), d_doc.data_ptr(), n_upd, args.docs,
-                                stream.cuda_stream)
+        # one batched merge of the shard, enqueued on the stream (counter reset + lean kernel);
+        # back-to-back steps pipeline.  Every document of this workload is finished by the lean
+        # kernel (asserted on the warmup below: the inputs are identical in every step), so each
+        # enqueued step is a complete merge without the host-driven tiers of finish().
+        eng.merge_device_async(d_arena.data_ptr(), len(arena), d_off.data_ptr(), d_doc.data_ptr(), n_upd, args.docs,
+                               stream.cuda_stream)
 
-    for _ in range(args.warmup):
-        r = step()
+    w0 = eng.stats()
+    for _ in range(max(args.warmup, 1)):
+        step()
+        eng.merge_device_finish()
     torch.cuda.synchronize()
     s0 = eng.stats()
+    assert s0.docs_lean - w0.docs_lean == args.docs * max(args.warmup, 1), "not every document takes the lean kernel"
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        r = step()
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    # finish the last step: fault check, payload (and no deferred document, as on the warmup)
+    r = eng.merge_device_finish()
     s1 = eng.stats()
+    assert s1.docs_lean - s0.docs_lean == args.docs, "a timed step deferred documents to the host-driven tiers"
 
     out_bytes = int(r.payload_bytes)                 # sum of the merged outputs' lengths
     algo_bytes = len(arena) + out_bytes              # per step, this rank
-    kernel_ms = (s1.kernel_ms - s0.kernel_ms) / args.steps
+    # HIP events on the launch stream: one span over the timed back-to-back lean launches
+    kernel_ms = (s1.lean_ms - s0.lean_ms) / max(s1.lean_launches - s0.lean_launches, 1)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)   # the job's time = the slowest rank

@@ -5,6 +5,8 @@
 // fast-path launch (look-back placed, packed output), an 8-byte-class meta
 // read, the sequential kernel only when some document needed it, D2H.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -20,14 +22,14 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
                      uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
                      unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
-                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list,
-                            uint64_t out_cap, hipStream_t s);
-int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
-                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
-                            uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
-int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
-                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, uint64_t slot_total,
-                            void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
+                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
+                            uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
+int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
+                            const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
+                            int32_t* status, void* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
+int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
+                            const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
+                            int32_t* status, uint64_t slot_total, void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list, uint32_t n_fb,
                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
                            void* readers, int* order, int* tmp, const uint8_t** ubase, uint32_t* ulen, uint64_t upd_cap,
@@ -36,10 +38,10 @@ int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const 
 
 namespace {
 
-// mirrors ygm::DocMeta (ygm_kernels.hip)
+// mirrors ygm::DocMeta (ygm_kernels.hip); sizeof is a multiple of 16
 struct Meta {
   unsigned int ticket, fault, fb_count, defer_count, lean_defer, pad[3];
-  unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor;
+  unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor, pad2;
   unsigned long long payload_sh[16 * 16];
   unsigned long long payload_total() const {
     unsigned long long t = payload;
@@ -76,6 +78,8 @@ struct ygm_ctx {
   // device outputs + state
   DevBuf out, out_off, out_len, status, lb, meta, fb_list, defer_list, defer2_list;
   Meta* h_meta = nullptr;  // pinned read-back of the per-launch counters
+  int mslot = 0;           // counter slot of the next merge launch
+  void* meta_slot(int i) const { return (uint8_t*)meta.p + (size_t)i * sizeof(Meta); }
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
   // host results
   std::vector<uint8_t> h_data;
@@ -83,6 +87,16 @@ struct ygm_ctx {
   std::vector<int32_t> h_status;
   std::vector<uint32_t> h_doc_upd;
   ygm_stats_t stats{};
+  // the batch enqueued by ygm_merge_v1_device_async, completed by ygm_merge_v1_device_finish
+  struct Pending {
+    bool live = false;
+    hipStream_t s = nullptr;
+    const uint8_t* arena = nullptr; const uint64_t* upd_off = nullptr; const uint32_t* doc_upd = nullptr;
+    uint64_t arena_bytes = 0, slot_total = 0, out_cap = 0;
+    uint32_t n_upd = 0, n_docs = 0;
+    void* meta = nullptr;   // counter slot of the launch
+  } pend;
+  uint32_t lean_span_n = 0;   // lean launches enqueued since the last finish (timed as one span, e0 .. e1)
 };
 
 static int herr(hipError_t e) { return e == hipSuccess ? YGM_OK : YGM_EDEVICE; }
@@ -120,7 +134,9 @@ int ygm_open(int device, uint32_t flags, ygm_ctx** out) {
     delete c;
     return YGM_EDEVICE;
   }
-  if (!c->meta.ensure(sizeof(Meta))) { ygm_close(c); return YGM_ENOMEM; }
+  // counter slots: 0 / 1 alternate between merge launches (each lean launch zeroes the other
+  // slot for the next one: no reset kernel per batch), 2 = SV / diff (reset per call)
+  if (!c->meta.ensure(3 * sizeof(Meta)) || hipMemset(c->meta.p, 0, 3 * sizeof(Meta)) != hipSuccess) { ygm_close(c); return YGM_ENOMEM; }
   if (hipHostMalloc((void**)&c->h_meta, sizeof(Meta), hipHostMallocDefault) != hipSuccess) { c->h_meta = nullptr; ygm_close(c); return YGM_ENOMEM; }
   *out = c;
   return YGM_OK;
@@ -153,13 +169,15 @@ static int prep_outputs(ygm_ctx* c, uint32_t n_docs, uint64_t out_cap, hipStream
       !c->status.ensure((size_t)n_docs * 4 + 4) || !c->lb.ensure(tiles * 8) || !c->fb_list.ensure((size_t)n_docs * 4 + 4) ||
       !c->defer_list.ensure((size_t)n_docs * 4 + 4) || !c->defer2_list.ensure((size_t)n_docs * 4 + 4))
     return YGM_ENOMEM;
-  if (lookback) HIPCHK(hipMemsetAsync(c->lb.p, 0, tiles * 8, s));
-  HIPCHK(hipMemsetAsync(c->meta.p, 0, sizeof(Meta), s));
+  if (lookback) {   // SV / diff: look-back tiles and counter slot 2 reset per call
+    HIPCHK(hipMemsetAsync(c->lb.p, 0, tiles * 8, s));
+    HIPCHK(hipMemsetAsync(c->meta_slot(2), 0, sizeof(Meta), s));
+  }
   return YGM_OK;
 }
 
-static int read_meta(ygm_ctx* c, hipStream_t s, Meta& m) {
-  HIPCHK(hipMemcpyAsync(c->h_meta, c->meta.p, sizeof(Meta), hipMemcpyDeviceToHost, s));
+static int read_meta(ygm_ctx* c, hipStream_t s, Meta& m, const void* slot) {
+  HIPCHK(hipMemcpyAsync(c->h_meta, slot, sizeof(Meta), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   m = *c->h_meta;
   return YGM_OK;
@@ -174,9 +192,10 @@ static void fill_dev_result(ygm_ctx* c, uint64_t data_bytes, ygm_device_result* 
   out->payload_bytes = data_bytes;
 }
 
-int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_upd_off,
-                        const uint32_t* d_doc_upd, uint32_t n_upd, uint32_t n_docs, void* stream, ygm_device_result* out) {
-  if (!c || !out) return YGM_EINVAL;
+// offsets of the DocMeta counters the tier kernels read as device-side counts
+int ygm_merge_v1_device_async(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_upd_off,
+                              const uint32_t* d_doc_upd, uint32_t n_upd, uint32_t n_docs, void* stream) {
+  if (!c) return YGM_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   (void)hipSetDevice(c->device);
   // output arena: one slot per document (2|in| + 64 B, no cross-document dependency),
@@ -185,61 +204,91 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
   const uint64_t out_cap = slot_total + 3 * arena_bytes + 16ull * n_docs + 64;
   int e = prep_outputs(c, n_docs, out_cap, s, false);
   if (e) return e;
-  Meta m;
-  float ms0 = 0;
-  // tier 1: lean wave-per-document kernel (debounce-log shape); everything else is deferred
-  HIPCHK(hipEventRecord(c->e0, s));
+  // tier 1: lean wave-per-document kernel (debounce-log shape); everything else is deferred.
+  // Timing: one event before the first launch since the last finish, one in finish after the
+  // last -- per-launch event pairs between back-to-back launches cost ~8 us of stream time each.
+  if (c->lean_span_n == 0) HIPCHK(hipEventRecord(c->e0, s));
+  c->lean_span_n++;
+  void* meta = c->meta_slot(c->mslot);
+  void* meta_next = c->meta_slot(1 - c->mslot);   // zeroed by this launch for the next one
   if (ygm_k_launch_merge_lean(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
-                              c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->meta.p, c->defer_list.as<uint32_t>(), out_cap, s))
+                              c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta, meta_next, c->defer_list.as<uint32_t>(), out_cap, s))
     return YGM_EDEVICE;
+  if (n_docs) c->mslot = 1 - c->mslot;   // (an empty batch launches nothing: the slot stays current)
+  c->pend.live = true; c->pend.s = s;
+  c->pend.arena = d_arena; c->pend.upd_off = d_upd_off; c->pend.doc_upd = d_doc_upd;
+  c->pend.arena_bytes = arena_bytes; c->pend.slot_total = slot_total; c->pend.out_cap = out_cap;
+  c->pend.n_upd = n_upd; c->pend.n_docs = n_docs; c->pend.meta = meta;
+  return YGM_OK;
+}
+
+int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
+  if (!c || !out || !c->pend.live) return YGM_EINVAL;
+  ygm_ctx::Pending& P = c->pend;
+  P.live = false;
+  hipStream_t s = P.s;
+  (void)hipSetDevice(c->device);
   HIPCHK(hipEventRecord(c->e1, s));
-  if ((e = read_meta(c, s, m))) return e;
+  Meta m;
+  int e = read_meta(c, s, m, P.meta);
+  if (e) return e;
   if (m.fault) return YGM_EDEVICE;
-  if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) { c->stats.kernel_ms += ms0; c->stats.lean_ms += ms0; }
-  if (m.lean_defer) {  // tier 2: general wave-per-document kernel over the deferred list
+  float ms0 = 0;
+  if (c->lean_span_n && hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) { c->stats.kernel_ms += ms0; c->stats.lean_ms += ms0; }
+  c->stats.lean_launches += c->lean_span_n;
+  c->lean_span_n = 0;
+  if (m.lean_defer) {  // tier 2: general wave-per-document kernel over the lean kernel's deferred list
     HIPCHK(hipEventRecord(c->e0, s));
-    if (ygm_k_launch_merge_wave(d_arena, d_upd_off, d_doc_upd, c->defer_list.as<uint32_t>(), m.lean_defer, c->flags, c->out.as<uint8_t>(),
-                                c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->meta.p,
-                                c->defer2_list.as<uint32_t>(), c->fb_list.as<uint32_t>(), out_cap, s))
+    if (ygm_k_launch_merge_wave(P.arena, P.upd_off, P.doc_upd, c->defer_list.as<uint32_t>(), nullptr, m.lean_defer, c->flags,
+                                c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
+                                P.meta, c->defer2_list.as<uint32_t>(), c->fb_list.as<uint32_t>(), P.out_cap, s))
       return YGM_EDEVICE;
     HIPCHK(hipEventRecord(c->e1, s));
-    if ((e = read_meta(c, s, m))) return e;
+    if ((e = read_meta(c, s, m, P.meta))) return e;
     if (m.fault) return YGM_EDEVICE;
     if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
   }
   if (m.defer_count) {  // tier 3: documents over the wave class, one workgroup per document
     HIPCHK(hipEventRecord(c->e0, s));
-    if (ygm_k_launch_merge_fast(d_arena, d_upd_off, d_doc_upd, c->defer2_list.as<uint32_t>(), m.defer_count, c->flags,
+    if (ygm_k_launch_merge_fast(P.arena, P.upd_off, P.doc_upd, c->defer2_list.as<uint32_t>(), nullptr, m.defer_count, c->flags,
                                 c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
-                                slot_total, c->meta.p, c->fb_list.as<uint32_t>(), out_cap, s))
+                                P.slot_total, P.meta, c->fb_list.as<uint32_t>(), P.out_cap, s))
       return YGM_EDEVICE;
     HIPCHK(hipEventRecord(c->e1, s));
-    if ((e = read_meta(c, s, m))) return e;
+    if ((e = read_meta(c, s, m, P.meta))) return e;
     if (m.fault) return YGM_EDEVICE;
     if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
   }
-  if (m.fb_count) {
+  if (m.fb_count) {  // tier 4: the exact sequential replay (scratch sized from the counters)
     const uint64_t upd_cap = m.fb_upds + 1, byte_cap = m.fb_bytes + 8ull * m.fb_count + 8;
     if (!c->s_readers.ensure(upd_cap * ygm_k_seq_reader_bytes()) || !c->s_order.ensure(upd_cap * 4) || !c->s_tmp.ensure(upd_cap * 4) ||
         !c->s_ubase.ensure(upd_cap * 8) || !c->s_ulen.ensure(upd_cap * 4) || !c->s_cnt.ensure(byte_cap * 4) ||
         !c->s_drec.ensure((byte_cap / 2 + 1) * ygm_k_drec_bytes()))
       return YGM_ENOMEM;
-    if (ygm_k_launch_merge_seq(d_arena, d_upd_off, d_doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->out.as<uint8_t>(),
-                               c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->meta.p,
+    if (ygm_k_launch_merge_seq(P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->out.as<uint8_t>(),
+                               c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), P.meta,
                                c->s_readers.p, c->s_order.as<int>(), c->s_tmp.as<int>(), c->s_ubase.as<const uint8_t*>(),
-                               c->s_ulen.as<uint32_t>(), upd_cap, c->s_cnt.as<uint32_t>(), c->s_drec.p, byte_cap, slot_total, out_cap, s))
+                               c->s_ulen.as<uint32_t>(), upd_cap, c->s_cnt.as<uint32_t>(), c->s_drec.p, byte_cap, P.slot_total, P.out_cap, s))
       return YGM_EDEVICE;
-    if ((e = read_meta(c, s, m))) return e;
+    if ((e = read_meta(c, s, m, P.meta))) return e;
     c->stats.docs_seq += m.fb_count;
   }
-  const uint64_t extent = slot_total + m.cursor;
-  c->stats.calls++; c->stats.docs += n_docs; c->stats.updates += n_upd;
-  c->stats.docs_fast += n_docs - m.fb_count;
-  c->stats.docs_lean += n_docs - m.lean_defer;
-  c->stats.bytes_in += arena_bytes; c->stats.bytes_out += m.payload_total();
+  const uint64_t extent = P.slot_total + m.cursor;
+  c->stats.calls++; c->stats.docs += P.n_docs; c->stats.updates += P.n_upd;
+  c->stats.docs_fast += P.n_docs - m.fb_count;
+  c->stats.docs_lean += P.n_docs - m.lean_defer;
+  c->stats.bytes_in += P.arena_bytes; c->stats.bytes_out += m.payload_total();
   fill_dev_result(c, extent, out);
   out->payload_bytes = m.payload_total();
   return YGM_OK;
+}
+
+int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_upd_off,
+                        const uint32_t* d_doc_upd, uint32_t n_upd, uint32_t n_docs, void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  const int e = ygm_merge_v1_device_async(c, d_arena, arena_bytes, d_upd_off, d_doc_upd, n_upd, n_docs, stream);
+  if (e) return e;
+  return ygm_merge_v1_device_finish(c, out);
 }
 
 static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off,
@@ -252,11 +301,11 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
   if (e) return e;
   HIPCHK(hipEventRecord(c->e0, s));
   if (ygm_k_launch_doc(mode, d_arena, d_doc_off, d_sv, d_sv_off, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
-                       c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->lb.as<unsigned long long>(), c->meta.p, out_cap, s))
+                       c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->lb.as<unsigned long long>(), c->meta_slot(2), out_cap, s))
     return YGM_EDEVICE;
   HIPCHK(hipEventRecord(c->e1, s));
   Meta m;
-  if ((e = read_meta(c, s, m))) return e;
+  if ((e = read_meta(c, s, m, c->meta_slot(2)))) return e;
   if (m.fault) return YGM_EDEVICE;
   float ms = 0;
   if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;

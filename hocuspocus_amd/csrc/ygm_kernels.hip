@@ -64,6 +64,7 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned long long fb_bytes;
   unsigned long long scr_upd_cursor;
   unsigned long long scr_byte_cursor;
+  unsigned long long pad2;            // (16-byte multiple: the lean kernel zeroes slots in 16-byte pieces)
   unsigned long long payload_sh[16 * 16]; // merge: output lengths summed in 16 shards, one 128-B line each (no hot atomic line)
 };
 YDEV void add_payload(DocMeta* m, uint32_t d, uint64_t n) { atomicAdd(&m->payload_sh[(d & 15u) * 16u], (unsigned long long)n); }
@@ -232,18 +233,15 @@ YDEV int pow2_ceil(int n) { int p = 1; while (p < n) p <<= 1; return p; }
 
 // Documents deferred by the wave kernel (list `docs`, n_docs entries), one
 // workgroup each; outputs placed by merge_place.
-__global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
-                                                      const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ docs,
-                                                      uint32_t n_docs, uint32_t flags,
-                                                      uint8_t* __restrict__ out_all, uint64_t* __restrict__ out_off,
-                                                      uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
-                                                      uint64_t slot_total, DocMeta* meta, uint32_t* fb_list, uint64_t out_cap) {
-  __shared__ MergeLds L;
+YDEV void merge_fast_doc(MergeLds& L, uint32_t d, const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+                         const uint32_t* __restrict__ doc_upd, uint32_t flags,
+                         uint8_t* __restrict__ out_all, uint64_t* __restrict__ out_off,
+                         uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+                         uint64_t slot_total, DocMeta* meta, uint32_t* fb_list, uint64_t out_cap) {
   const int t = threadIdx.x;
   DIAG_T0
   if (t == 0) { L.err = 0; L.fb = 0; L.nc = 0; }
   __syncthreads();
-  const uint32_t d = docs[blockIdx.x];
   const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
   const uint32_t k = u1 - u0;
   const uint64_t b0 = upd_off[u0], b1 = upd_off[u1];
@@ -452,6 +450,22 @@ __global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__
   DIAG(7);
 }
 
+// Documents deferred by the wave kernel, one workgroup at a time (persistent grid).  The count is
+// read from device memory (`n_dev`, written by the previous kernel in stream order) when given.
+__global__ __launch_bounds__(M_NT) void k_merge_fast(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+                                                      const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ docs,
+                                                      const unsigned int* n_dev, uint32_t n_docs, uint32_t flags,
+                                                      uint8_t* __restrict__ out_all, uint64_t* __restrict__ out_off,
+                                                      uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+                                                      uint64_t slot_total, DocMeta* meta, uint32_t* fb_list, uint64_t out_cap) {
+  __shared__ MergeLds L;
+  const uint32_t N = n_dev ? *n_dev : n_docs;
+  for (uint32_t i = blockIdx.x; i < N; i += gridDim.x) {
+    merge_fast_doc(L, docs[i], arena, upd_off, doc_upd, flags, out_all, out_off, out_len, status, slot_total, meta, fb_list, out_cap);
+    __syncthreads();
+  }
+}
+
 
 // ======================================================================= merge: one wave per document
 // See ygm_merge_wave.hpp for the phase plan.  Per-element state lives in LDS
@@ -462,20 +476,14 @@ YDEV uint32_t wave_min_u32(uint32_t v) {
   return v;
 }
 
-__global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
-                                                               const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ docs,
-                                                               uint32_t n_docs, uint32_t flags,
-                                                               uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
-                                                               uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
-                                                               DocMeta* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap) {
-  __shared__ WaveLds LS[W_WAVES];
+YDEV void merge_wave_doc(WaveLds& L, uint32_t d, const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+                         const uint32_t* __restrict__ doc_upd, uint32_t flags,
+                         uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
+                         uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+                         DocMeta* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap) {
   DIAG_T0
   const uint32_t l = threadIdx.x % WAVE;
-  WaveLds& L = LS[threadIdx.x / WAVE];
   LWave* LW = (LWave*)&L;
-  const uint32_t di = blockIdx.x * W_WAVES + threadIdx.x / WAVE;
-  if (di >= n_docs) return;
-  const uint32_t d = docs ? docs[di] : di;
   const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
   const uint32_t k = u1 - u0;
   const uint64_t b0 = upd_off[u0], b1 = upd_off[u1];
@@ -781,6 +789,21 @@ __global__ __launch_bounds__(WAVE * W_WAVES) void k_merge_wave(const uint8_t* __
   DIAGW(7);
 }
 
+// Documents deferred by the lean kernel, one wave each (persistent grid; count from device memory).
+__global__ __launch_bounds__(WAVE) void k_merge_wave(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+                                                     const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ docs,
+                                                     const unsigned int* n_dev, uint32_t n_docs, uint32_t flags,
+                                                     uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
+                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status,
+                                                     DocMeta* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap) {
+  __shared__ WaveLds L;
+  const uint32_t N = n_dev ? *n_dev : n_docs;
+  for (uint32_t i = blockIdx.x; i < N; i += gridDim.x) {
+    merge_wave_doc(L, docs ? docs[i] : i, arena, upd_off, doc_upd, flags, out, out_off, out_len, status, meta, defer_list, fb_list, out_cap);
+    wave_sync();
+  }
+}
+
 
 // ======================================================================= merge: lean fast path
 // Persistent waves (ygm_merge_lean.hpp): wave w takes documents w, w + G, w + 2G, ...
@@ -840,8 +863,13 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
                                                      const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t flags,
                                                      uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                      uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
-                                                     uint32_t* __restrict__ defer_list, uint64_t out_cap) {
+                                                     DocMeta* __restrict__ meta_next, uint32_t* __restrict__ defer_list, uint64_t out_cap) {
   __shared__ LeanLds LS;
+  if (blockIdx.x == 0) {   // the next launch's counter slot (nothing reads it during this launch)
+    static_assert(sizeof(DocMeta) % 16 == 0, "DocMeta is zeroed in 16-byte pieces");
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (uint32_t i = threadIdx.x; i < sizeof(DocMeta) / 16; i += WAVE) ((u32x4*)meta_next)[i] = z;
+  }
   LB8* lin = (LB8*)LS.in;
   LB8* lout = (LB8*)LS.out;
   const uint32_t l = threadIdx.x;
@@ -1214,8 +1242,8 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
 }
 
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
-                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list,
-                            uint64_t out_cap, hipStream_t s) {
+                            uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
+                            uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
   if (n_docs == 0) return 0;
   // persistent waves: enough for full occupancy, each looping over documents d, d + G, ...
   static int n_cu = 0;
@@ -1224,24 +1252,26 @@ int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const
   const uint32_t wpc = env ? (uint32_t)atoi(env) : 16u;
   const uint32_t grid = n_docs < (uint32_t)n_cu * wpc ? n_docs : (uint32_t)n_cu * wpc;
   hipLaunchKernelGGL(k_merge_lean, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len, status,
-                     (DocMeta*)meta, defer_list, out_cap);
+                     (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap);
   return (int)hipGetLastError();
 }
 
-int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
-                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
-                            uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
+int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
+                            const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
+                            int32_t* status, void* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
   if (n_docs == 0) return 0;
-  hipLaunchKernelGGL(k_merge_wave, dim3((n_docs + W_WAVES - 1) / W_WAVES), dim3(WAVE * W_WAVES), 0, s, arena, upd_off, doc_upd, docs, n_docs,
+  const uint32_t grid = n_docs < 2048u ? n_docs : 2048u;   // persistent: n_docs is the upper bound of the device count
+  hipLaunchKernelGGL(k_merge_wave, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, docs, n_dev, n_docs,
                      flags, out, out_off, out_len, status, (DocMeta*)meta, defer_list, fb_list, out_cap);
   return (int)hipGetLastError();
 }
 
-int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, uint32_t n_docs,
-                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, uint64_t slot_total,
-                            void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
+int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
+                            const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
+                            int32_t* status, uint64_t slot_total, void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
   if (n_docs == 0) return 0;
-  hipLaunchKernelGGL(k_merge_fast, dim3(n_docs), dim3(M_NT), 0, s, arena, upd_off, doc_upd, docs, n_docs, flags, out, out_off, out_len,
+  const uint32_t grid = n_docs < 512u ? n_docs : 512u;
+  hipLaunchKernelGGL(k_merge_fast, dim3(grid), dim3(M_NT), 0, s, arena, upd_off, doc_upd, docs, n_dev, n_docs, flags, out, out_off, out_len,
                      status, slot_total, (DocMeta*)meta, fb_list, out_cap);
   return (int)hipGetLastError();
 }

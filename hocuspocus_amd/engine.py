@@ -54,13 +54,15 @@ class Stats(ctypes.Structure):
                 ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64), ("docs_fast", ctypes.c_uint64),
                 ("docs_seq", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
                 ("d2h_ms", ctypes.c_double),
-                ("docs_lean", ctypes.c_uint64), ("lean_ms", ctypes.c_double)]
+                ("docs_lean", ctypes.c_uint64), ("lean_ms", ctypes.c_double),
+                ("lean_launches", ctypes.c_uint64)]
 
 
 _lib = None
 
 # every symbol include/ygm.h declares
 EXPORTS = ("ygm_open", "ygm_close", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_update_v1", "ygm_merge_v1_device",
+           "ygm_merge_v1_device_async", "ygm_merge_v1_device_finish",
            "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_stats", "ygm_strerror", "ygm_version")
 
 
@@ -79,6 +81,8 @@ def lib():
         L.ygm_diff_v1.argtypes = [vp, vp, vp, vp, vp, u32, ctypes.POINTER(_Result)]
         L.ygm_sv_from_update_v1.argtypes = [vp, vp, vp, u32, ctypes.POINTER(_Result)]
         L.ygm_merge_v1_device.argtypes = [vp, vp, u64, vp, vp, u32, u32, vp, ctypes.POINTER(_DevResult)]
+        L.ygm_merge_v1_device_async.argtypes = [vp, vp, u64, vp, vp, u32, u32, vp]
+        L.ygm_merge_v1_device_finish.argtypes = [vp, ctypes.POINTER(_DevResult)]
         L.ygm_diff_v1_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_sv_from_update_v1_device.argtypes = [vp, vp, u64, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_stats.argtypes = [vp, ctypes.POINTER(Stats)]
@@ -86,6 +90,7 @@ def lib():
         L.ygm_strerror.restype = ctypes.c_char_p
         L.ygm_version.restype = ctypes.c_char_p
         for f in ("ygm_open", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_update_v1", "ygm_merge_v1_device",
+                  "ygm_merge_v1_device_async", "ygm_merge_v1_device_finish",
                   "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_stats"):
             getattr(L, f).restype = i32
         _lib = L
@@ -233,6 +238,21 @@ class Engine:
         r = _DevResult()
         st = lib().ygm_merge_v1_device(self._ctx, d_arena, arena_bytes, d_upd_off, d_doc_upd, n_upd, n_docs, stream or None,
                                        ctypes.byref(r))
+        if st != OK:
+            raise YjsError(st)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)
+
+    def merge_device_async(self, d_arena: int, arena_bytes: int, d_upd_off: int, d_doc_upd: int, n_upd: int, n_docs: int,
+                           stream: int = 0) -> None:
+        """Enqueues a device-resident batch merge without waiting (ygm_merge_v1_device_async)."""
+        st = lib().ygm_merge_v1_device_async(self._ctx, d_arena, arena_bytes, d_upd_off, d_doc_upd, n_upd, n_docs, stream or None)
+        if st != OK:
+            raise YjsError(st)
+
+    def merge_device_finish(self) -> DeviceResult:
+        """Completes the last enqueued batch (sequential tier, fault check, payload) -- ygm_merge_v1_device_finish."""
+        r = _DevResult()
+        st = lib().ygm_merge_v1_device_finish(self._ctx, ctypes.byref(r))
         if st != OK:
             raise YjsError(st)
         return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)

@@ -73,7 +73,9 @@ typedef struct {
   uint64_t docs_fast, docs_seq;        /* documents per kernel class */
   double kernel_ms, h2d_ms, d2h_ms;    /* cumulative, HIP-event timed */
   uint64_t docs_lean;                  /* merges finished by the lean (debounce-log) kernel */
-  double lean_ms;                      /* HIP-event time of the lean kernel launches (part of kernel_ms) */
+  double lean_ms;                      /* HIP-event time of the lean kernel launches (part of kernel_ms): one span
+                                          from the first launch after a finish to that finish */
+  uint64_t lean_launches;              /* lean kernel launches timed in lean_ms */
 } ygm_stats_t;
 
 /* Opens the engine on HIP device `device` (one context per GPU; contexts are
@@ -106,7 +108,7 @@ int ygm_sv_from_update_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *do
  * extent of `data`, payload_bytes the sum of len[].  SV/diff outputs are
  * packed in document order (payload_bytes == data_bytes).  `stream` is a
  * hipStream_t (NULL = the context's stream); the call returns after one
- * 64-byte read of the launch counters. */
+ * read of the launch counters. */
 typedef struct {
   uint8_t *data;
   uint64_t *off;
@@ -119,6 +121,19 @@ typedef struct {
 int ygm_merge_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_upd_off,
                         const uint32_t *d_doc_upd, uint32_t n_upd, uint32_t n_docs, void *stream,
                         ygm_device_result *out);
+/* Asynchronous form of ygm_merge_v1_device for GPU-resident pipelines: enqueues
+ * the counter reset and the lean kernel on `stream` and returns without waiting.
+ * Documents the lean kernel finishes are complete when the stream reaches this
+ * point; every other document (deferred to the wave / workgroup / sequential
+ * tiers) is completed by ygm_merge_v1_device_finish, which waits for the stream,
+ * runs the tiers the device counters ask for, checks the fault flag and fills
+ * out->data_bytes / payload_bytes.  A context holds one batch: the next enqueue
+ * on it reuses the result buffers.
+ * (Replaces no single reference interface: the batched form of Y.mergeUpdates,
+ * yjs Y@37704, for GPU-resident pipelines.) */
+int ygm_merge_v1_device_async(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_upd_off,
+                              const uint32_t *d_doc_upd, uint32_t n_upd, uint32_t n_docs, void *stream);
+int ygm_merge_v1_device_finish(ygm_ctx *ctx, ygm_device_result *out);
 int ygm_diff_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
                        const uint8_t *d_sv_arena, const uint64_t *d_sv_off, uint32_t n_docs, void *stream,
                        ygm_device_result *out);

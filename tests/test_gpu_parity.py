@@ -335,3 +335,39 @@ def test_lean_kernel_edge_shapes_vs_oracle(eng):
     assert not bad, (len(bad), [u.hex() for u in docs[bad[0]]])
     took = eng.stats().docs_lean - lean0
     assert 0 < took < len(docs)   # both the lean path and the deferral path are exercised
+
+
+def test_async_device_api_matches_host_api(eng):
+    # ygm_merge_v1_device_async + finish (what bench.py times) == the host API, including a batch
+    # whose documents need every tier (lean, wave, workgroup, sequential)
+    import torch
+    from tools import synth
+    from v1util import vu  # noqa: F401
+    arena, upd_off, doc_upd = synth.text_updates(400, 120, seed=31, del_pct=10)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(400)]
+    rng = random.Random(5)
+    for d in range(0, 400, 7):
+        docs[d] = docs[d] + rng.sample(docs[d], 2)          # duplicates: the sequential tier
+    docs += _lean_edge_docs(100, seed=77)
+    blobs = [u for us in docs for u in us]
+    a = np.frombuffer(b"".join(blobs) + bytes(64), np.uint8)
+    off = np.cumsum([0] + [len(b) for b in blobs]).astype(np.uint64)
+    du = np.cumsum([0] + [len(us) for us in docs]).astype(np.uint32)
+    dev = torch.device("cuda", 0)
+    ta, to, td = (torch.from_numpy(x.copy()).to(dev) for x in (a, off.view(np.int64), du.view(np.int32)))
+    for _ in range(2):   # the second enqueue reuses the context's buffers
+        eng.merge_device_async(ta.data_ptr(), len(a) - 64, to.data_ptr(), td.data_ptr(), len(blobs), len(docs))
+    r = eng.merge_device_finish()
+    torch.cuda.synchronize()
+    import bench
+    n = len(docs)
+    offs = bench._d2h(r.off, n * 8).view(np.uint64)
+    lens = bench._d2h(r.len, n * 8).view(np.uint64)
+    sts = bench._d2h(r.status, n * 4).view(np.int32)
+    data = bench._d2h(r.data, int(r.data_bytes)).tobytes()
+    host = eng.merge_updates_batch(docs)
+    for d in range(n):
+        got = (int(sts[d]), data[int(offs[d]):int(offs[d]) + int(lens[d])] if sts[d] == 0 else None)
+        assert got[0] == host[d][0] and (got[0] != 0 or got[1] == host[d][1]), d
+    assert r.payload_bytes == sum(len(h[1]) for h in host if h[0] == 0)

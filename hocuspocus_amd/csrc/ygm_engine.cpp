@@ -19,8 +19,11 @@ size_t ygm_k_meta_bytes();
 size_t ygm_k_seq_reader_bytes();
 size_t ygm_k_drec_bytes();
 int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,
-                     uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
-                     unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
+                     const uint32_t* docs, uint64_t out_base, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
+                     uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
+int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
+                          uint64_t sv_bytes, const uint64_t* sv_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
+                          uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
                             uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
@@ -292,37 +295,58 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
 }
 
 static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off,
-                          const uint8_t* d_sv, const uint64_t* d_sv_off, uint32_t n_docs, void* stream, ygm_device_result* out) {
+                          const uint8_t* d_sv, uint64_t sv_bytes, const uint64_t* d_sv_off, uint32_t n_docs, void* stream,
+                          ygm_device_result* out) {
   if (!c || !out) return YGM_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   (void)hipSetDevice(c->device);
-  const uint64_t out_cap = 2 * arena_bytes + 32ull * n_docs + 64;
+  // per-document slots (lean kernel), then the packed region of the exact kernel's deferred documents
+  const uint64_t slot_total = 2 * arena_bytes + 64ull * n_docs;
+  const uint64_t out_cap = slot_total + 2 * arena_bytes + 32ull * n_docs + 64;
   int e = prep_outputs(c, n_docs, out_cap, s, true);
   if (e) return e;
+  void* meta = c->meta_slot(2);
   HIPCHK(hipEventRecord(c->e0, s));
-  if (ygm_k_launch_doc(mode, d_arena, d_doc_off, d_sv, d_sv_off, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
-                       c->out_len.as<uint64_t>(), c->status.as<int32_t>(), c->lb.as<unsigned long long>(), c->meta_slot(2), out_cap, s))
+  if (ygm_k_launch_doc_lean(mode, d_arena, arena_bytes, d_doc_off, d_sv, sv_bytes, d_sv_off, n_docs, c->flags, c->out.as<uint8_t>(),
+                            c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta,
+                            c->defer_list.as<uint32_t>(), out_cap, s))
     return YGM_EDEVICE;
   HIPCHK(hipEventRecord(c->e1, s));
   Meta m;
-  if ((e = read_meta(c, s, m, c->meta_slot(2)))) return e;
+  if ((e = read_meta(c, s, m, meta))) return e;
   if (m.fault) return YGM_EDEVICE;
   float ms = 0;
-  if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;
-  c->stats.calls++; c->stats.docs += n_docs; c->stats.docs_fast += n_docs;
-  c->stats.bytes_in += arena_bytes; c->stats.bytes_out += m.fast_total;
-  fill_dev_result(c, m.fast_total, out);
+  if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) { c->stats.kernel_ms += ms; c->stats.lean_ms += ms; c->stats.lean_launches++; }
+  if (m.lean_defer) {   // the exact per-document kernel over the deferred list, packed after the slots
+    HIPCHK(hipEventRecord(c->e0, s));
+    if (ygm_k_launch_doc(mode, d_arena, d_doc_off, d_sv, d_sv_off, c->defer_list.as<uint32_t>(), slot_total, m.lean_defer, c->flags,
+                         c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
+                         c->lb.as<unsigned long long>(), meta, out_cap, s))
+      return YGM_EDEVICE;
+    HIPCHK(hipEventRecord(c->e1, s));
+    if ((e = read_meta(c, s, m, meta))) return e;
+    if (m.fault) return YGM_EDEVICE;
+    if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;
+  }
+  const uint64_t payload = m.payload_total() + m.fast_total;
+  c->stats.calls++; c->stats.docs += n_docs; c->stats.docs_fast += n_docs; c->stats.docs_lean += n_docs - m.lean_defer;
+  c->stats.bytes_in += arena_bytes; c->stats.bytes_out += payload;
+  fill_dev_result(c, slot_total + m.fast_total, out);
+  out->payload_bytes = payload;
   return YGM_OK;
 }
 
 int ygm_diff_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, const uint8_t* d_sv_arena,
                        const uint64_t* d_sv_off, uint32_t n_docs, void* stream, ygm_device_result* out) {
-  return run_doc_kernel(c, 1, d_arena, arena_bytes, d_doc_off, d_sv_arena, d_sv_off, n_docs, stream, out);
+  // (the state-vector arena's extent is the last offset; its 16-byte window reads stay inside its padding)
+  uint64_t sv_end = 0;
+  if (n_docs && hipMemcpy(&sv_end, d_sv_off + n_docs, 8, hipMemcpyDeviceToHost) != hipSuccess) return YGM_EDEVICE;
+  return run_doc_kernel(c, 1, d_arena, arena_bytes, d_doc_off, d_sv_arena, sv_end, d_sv_off, n_docs, stream, out);
 }
 
 int ygm_sv_from_update_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
                                  void* stream, ygm_device_result* out) {
-  return run_doc_kernel(c, 0, d_arena, arena_bytes, d_doc_off, nullptr, nullptr, n_docs, stream, out);
+  return run_doc_kernel(c, 0, d_arena, arena_bytes, d_doc_off, nullptr, 0, nullptr, n_docs, stream, out);
 }
 
 // ------------------------------------------------------------------ host API

@@ -22,6 +22,7 @@
 #include "ygm_merge_seq.hpp"
 #include "ygm_merge_wave.hpp"
 #include "ygm_merge_lean.hpp"
+#include "ygm_doc_lean.hpp"
 #include "ygm_seqdoc.hpp"
 #include "ygm_v1.hpp"
 
@@ -86,6 +87,7 @@ YDEV uint64_t merge_place(const uint64_t* upd_off, const uint32_t* doc_upd, uint
 template <int MODE>  // 0 = sv, 1 = diff
 __global__ __launch_bounds__(DOC_NT) void k_doc(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off,
                                                  const uint8_t* __restrict__ sv_arena, const uint64_t* __restrict__ sv_off,
+                                                 const uint32_t* __restrict__ docs, uint64_t out_base,
                                                  uint32_t n_docs, uint32_t flags, uint8_t* __restrict__ out,
                                                  uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len,
                                                  int32_t* __restrict__ status, unsigned long long* lb, DocMeta* meta,
@@ -97,8 +99,9 @@ __global__ __launch_bounds__(DOC_NT) void k_doc(const uint8_t* __restrict__ aren
   if (threadIdx.x == 0) s_tile = atomicAdd(&meta->ticket, 1u);
   __syncthreads();
   const uint32_t tile = s_tile;
-  const uint32_t d = tile * DOC_NT + threadIdx.x;
-  const bool live = d < n_docs;
+  const uint32_t di = tile * DOC_NT + threadIdx.x;   // index into `docs` (the lean kernel's deferred list) or the document
+  const bool live = di < n_docs;
+  const uint32_t d = live ? (docs ? docs[di] : di) : 0u;
   const uint8_t* p = nullptr; uint32_t n = 0;
   const uint8_t* sv = nullptr; uint32_t svn = 0;
   if (live) {
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(DOC_NT) void k_doc(const uint8_t* __restrict__ aren
   }
   __syncthreads();
   if (!live) return;
-  const uint64_t at = s_base + pre;
+  const uint64_t at = out_base + s_base + pre;
   if (st == ST_OK && at + mysz > out_cap) st = ST_NOMEM;
   if (st == ST_OK) {
     Out w{out + at, 0};
@@ -134,6 +137,180 @@ __global__ __launch_bounds__(DOC_NT) void k_doc(const uint8_t* __restrict__ aren
   }
   if (meta->fault) st = ST_DEVICE;
   out_off[d] = at; out_len[d] = st == ST_OK ? mysz : 0; status[d] = st;
+}
+
+
+// ======================================================================= SV / diff: lean lane-per-document path
+// ygm_doc_lean.hpp.  MODE 0 = encodeStateVectorFromUpdate (rule R-SV), 1 = diffUpdate (rule R-D).
+// Each lane loops over documents d = global lane, + total lanes; outputs go to the document's
+// slot (merge_slot); documents outside the lean shape are appended to `defer_list` for k_doc.
+template <int MODE>
+__global__ __launch_bounds__(WAVE) void k_doc_lean(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                  const uint64_t* __restrict__ doc_off, const uint8_t* __restrict__ sv_arena,
+                                                  uint64_t sv_bytes, const uint64_t* __restrict__ sv_off, uint32_t n_docs, uint32_t flags,
+                                                  uint8_t* __restrict__ out, uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len,
+                                                  int32_t* __restrict__ status, DocMeta* meta, uint32_t* __restrict__ defer_list,
+                                                  uint64_t out_cap) {
+  __shared__ uint32_t svt[MODE == 1 ? WAVE * DL_SV_MAX * 2 : 1];   // per-lane state-vector table (client, clock)
+  const uint32_t l = threadIdx.x;
+  const uint64_t lastc = arena_bytes & ~15ull, sv_lastc = sv_bytes & ~15ull;
+  uint64_t payload = 0;
+  for (uint32_t d = blockIdx.x * WAVE + l; d < n_docs; d += gridDim.x * WAVE) {
+    const uint64_t a = doc_off[d], b = doc_off[d + 1];
+    const uint64_t slot = merge_slot(a, d), cap = merge_slot_cap(b - a);
+    const uint64_t body0 = slot + 16;        // the header is written right-aligned in front of the body
+    const uint64_t tend = slot + cap < out_cap ? slot + cap : out_cap;
+    uint32_t bad = (b - a) >> 31 ? 1u : 0u;
+    SWin w;
+    uint32_t nsv = 0;
+    if (MODE == 1) {   // decodeStateVector: last entry per client wins (Map.set)
+      const uint64_t sa = sv_off[d], sb = sv_off[d + 1];
+      w.init(sv_arena, sa, sv_lastc);
+      uint32_t dd[8]; w.view(sa, dd);
+      VMask m = vmask(dd, sb - sa);
+      uint32_t e = vend(m.T, 0);
+      const uint32_t n = vval(dd, 0, e, bad);
+      uint64_t q = sa + e + 1u;
+      bad |= n > (uint32_t)DL_SV_MAX ? 1u : 0u;
+      for (uint32_t i = 0; i < n && !bad; i++) {
+        w.advance(q); w.view(q, dd); m = vmask(dd, sb - q);
+        bad |= m.Z & ((m.H & m.V) << 1) & m.V;   // non-minimal varuints are fine for an SV, but rare: defer
+        const uint32_t e1 = vend(m.T, 0); const uint32_t cl = vval(dd, 0, e1, bad);
+        const uint32_t e2 = vend(m.T, e1 + 1u); const uint32_t ck = vval(dd, e1 + 1u, e2, bad);
+        q += e2 + 1u;
+        bad |= q > sb ? 1u : 0u;
+        uint32_t at = nsv;
+        for (uint32_t j = 0; j < nsv; j++) if (svt[(l * DL_SV_MAX + j) * 2] == cl) at = j;
+        svt[(l * DL_SV_MAX + at) * 2] = cl; svt[(l * DL_SV_MAX + at) * 2 + 1] = ck;
+        if (at == nsv) nsv++;
+      }
+      bad |= q != sb ? 1u : 0u;   // trailing bytes in a state vector: exact kernel decides
+    }
+    w.init(arena, a, lastc);
+    uint32_t dd[8]; w.view(a, dd);
+    VMask m = vmask(dd, b - a);
+    uint32_t e = vend(m.T, 0);
+    const uint32_t nb = vval(dd, 0, e, bad);
+    uint64_t pos = a + e + 1u;
+    uint64_t t = body0;
+    uint32_t count = 0;                       // SV entries / written blocks
+    // SV state (sv_doc): current client, its contiguous clock, whether it stopped
+    uint32_t cc = 0, clk = 0; bool first = true, stop = false;
+    uint32_t prev_client = 0xFFFFFFFFu; bool have_prev = false;
+    for (uint32_t blk = 0; blk < nb && !bad; blk++) {
+      w.advance(pos); w.view(pos, dd); m = vmask(dd, b - pos);
+      bad |= m.Z & ((m.H & m.V) << 1) & m.V;
+      const uint32_t e1 = vend(m.T, 0); const uint32_t nst = vval(dd, 0, e1, bad);
+      const uint32_t e2 = vend(m.T, e1 + 1u); const uint32_t client = vval(dd, e1 + 1u, e2, bad);
+      const uint32_t e3 = vend(m.T, e2 + 1u); uint32_t clock = vval(dd, e2 + 1u, e3, bad);
+      pos += e3 + 1u;
+      if (MODE == 1) {   // canonical (client-descending, distinct) block order; anything else: exact kernel
+        bad |= (have_prev && client >= prev_client) ? 1u : 0u;
+        prev_client = client; have_prev = true;
+      }
+      uint32_t svc = 0;
+      if (MODE == 1) for (uint32_t j = 0; j < nsv; j++) if (svt[(l * DL_SV_MAX + j) * 2] == client) svc = svt[(l * DL_SV_MAX + j) * 2 + 1];
+      bool emitted = false;
+      uint64_t run0 = 0;                      // diff: start of the verbatim run after the first written struct
+      for (uint32_t st = 0; st < nst && !bad; st++) {
+        const LStruct sx = lean_doc_struct(w, pos, b);
+        bad |= sx.sbad;
+        if (bad) break;
+        const uint64_t end = (uint64_t)clock + sx.len;
+        bad |= end >> 32 ? 1u : 0u;
+        if (MODE == 0) {
+          if (first) { cc = client; stop = clock != 0; clk = stop ? 0u : (uint32_t)end; first = false; }
+          if (cc != client) {
+            if (clk) { if (t + 10 > tend) bad = 1; else { t = gw_vu(out, t, cc); t = gw_vu(out, t, clk); count++; } }
+            cc = client; clk = 0; stop = clock != 0;
+          }
+          if (sx.kind == K_SKIP) stop = true;
+          if (!stop) clk = (uint32_t)end;
+        } else if (!emitted && sx.kind != K_SKIP && end > svc) {
+          // the first written struct of this client: header, then the struct with offset svc - clock
+          const uint32_t off = svc > clock ? svc - clock : 0u;
+          if (t + 64 + (sx.end - pos) > tend) bad = 1;
+          else {
+            t = gw_vu(out, t, nst - st); t = gw_vu(out, t, client); t = gw_vu(out, t, (uint64_t)clock + off);
+            if (off == 0) { gw_copy(out + t, arena + pos, sx.end - pos); t += sx.end - pos; }
+            else t = lean_write_sliced(out, t, arena, pos, sx, client, clock, off);
+            emitted = true; count++;
+            run0 = sx.end;
+          }
+        }
+        clock = (uint32_t)end;
+        pos = sx.end;
+      }
+      if (MODE == 1 && emitted && !bad) {   // the rest of the client's block, verbatim (Skips included)
+        if (t + (pos - run0) > tend) bad = 1;
+        else { gw_copy(out + t, arena + run0, pos - run0); t += pos - run0; }
+      }
+    }
+    if (MODE == 0 && !bad && !first && clk) {
+      if (t + 10 > tend) bad = 1; else { t = gw_vu(out, t, cc); t = gw_vu(out, t, clk); count++; }
+    }
+    if (MODE == 1 && !bad) {
+      // delete set: copied verbatim when readDeleteSet + writeDeleteSet reproduce it -- distinct clients
+      // with >= 1 range each, client-descending (13.6) / any order (13.5 first-seen), minimal varuints
+      const uint64_t ds0 = pos;
+      w.advance(pos); w.view(pos, dd); m = vmask(dd, b - pos);
+      bad |= m.Z & ((m.H & m.V) << 1) & m.V;
+      e = vend(m.T, 0);
+      const uint32_t ncl = vval(dd, 0, e, bad);
+      pos += e + 1u;
+      uint32_t pc = 0xFFFFFFFFu; bool hp = false;
+      for (uint32_t i = 0; i < ncl && !bad; i++) {
+        w.advance(pos); w.view(pos, dd); m = vmask(dd, b - pos);
+        bad |= m.Z & ((m.H & m.V) << 1) & m.V;
+        const uint32_t e1 = vend(m.T, 0); const uint32_t cl = vval(dd, 0, e1, bad);
+        const uint32_t e2 = vend(m.T, e1 + 1u); const uint32_t nr = vval(dd, e1 + 1u, e2, bad);
+        pos += e2 + 1u;
+        bad |= nr == 0u ? 1u : 0u;
+        if (flags & F_COMPAT_135) {   // first-seen order: distinct clients (checked against every earlier entry)
+          bad |= (hp && cl == pc) ? 1u : 0u;
+          if (i > 0) {   // earlier entries are re-read from the document (rare: multi-client delete sets)
+            Cur c{arena + ds0, 0, (uint32_t)(b - ds0), 0, 0};
+            const uint64_t n0 = c.vu();
+            for (uint64_t k = 0; k < n0 && k < i && !c.err; k++) {
+              const uint64_t c2 = c.vu(), r2 = c.vu();
+              for (uint64_t r = 0; r < r2 && !c.err; r++) { c.vu(); c.vu(); }
+              if (c2 == cl) bad = 1;
+            }
+          }
+        } else bad |= (hp && cl >= pc) ? 1u : 0u;
+        pc = cl; hp = true;
+        for (uint32_t r = 0; r < nr && !bad; r++) {
+          w.advance(pos); w.view(pos, dd); m = vmask(dd, b - pos);
+          bad |= m.Z & ((m.H & m.V) << 1) & m.V;
+          const uint32_t f1 = vend(m.T, 0); (void)vval(dd, 0, f1, bad);
+          const uint32_t f2 = vend(m.T, f1 + 1u); (void)vval(dd, f1 + 1u, f2, bad);
+          pos += f2 + 1u;
+        }
+      }
+      bad |= pos > b ? 1u : 0u;
+      if (!bad) {
+        if (t + (pos - ds0) > tend) bad = 1;
+        else { gw_copy(out + t, arena + ds0, pos - ds0); t += pos - ds0; }
+      }
+    }
+    bad |= pos > b ? 1u : 0u;
+#ifdef YGM_DEBUG_LEAN
+    if (d < 4) printf("doc_lean<%d> d=%u bad=%u nb=%u pos=%lu a=%lu b=%lu count=%u t-body=%lu nsv=%u\n", MODE, d, bad, nb,
+                      (unsigned long)pos, (unsigned long)a, (unsigned long)b, count, (unsigned long)(t - body0), nsv);
+#endif
+    if (bad) {
+      status[d] = ST_FALLBACK;
+      defer_list[atomicAdd(&meta->lean_defer, 1u)] = d;
+    } else {
+      uint32_t hl = 1; for (uint32_t v = count; v > 127u; v >>= 7) hl++;
+      gw_vu(out, body0 - hl, count);
+      out_off[d] = body0 - hl; out_len[d] = hl + (t - body0); status[d] = ST_OK;
+      payload += hl + (t - body0);
+    }
+  }
+  // one atomic per wave for the output bytes (lanes reduced through the first lane)
+  payload = wave_sum(payload);
+  if (l == 0 && payload) add_payload(meta, blockIdx.x, payload);
 }
 
 // ======================================================================= merge fast path
@@ -1230,14 +1407,31 @@ size_t ygm_k_seq_reader_bytes() { return sizeof(Stream); }
 size_t ygm_k_drec_bytes() { return sizeof(DRec); }
 
 int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,
-                     uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
-                     unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s) {
+                     const uint32_t* docs, uint64_t out_base, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
+                     uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s) {
   const uint32_t tiles = (n_docs + DOC_NT - 1) / DOC_NT;
   if (tiles == 0) return 0;
   if (mode == 0)
-    hipLaunchKernelGGL(k_doc<0>, dim3(tiles), dim3(DOC_NT), 0, s, arena, doc_off, sv_arena, sv_off, n_docs, flags, out, out_off, out_len, status, lb, (DocMeta*)meta, out_cap);
+    hipLaunchKernelGGL(k_doc<0>, dim3(tiles), dim3(DOC_NT), 0, s, arena, doc_off, sv_arena, sv_off, docs, out_base, n_docs, flags, out, out_off, out_len, status, lb, (DocMeta*)meta, out_cap);
   else
-    hipLaunchKernelGGL(k_doc<1>, dim3(tiles), dim3(DOC_NT), 0, s, arena, doc_off, sv_arena, sv_off, n_docs, flags, out, out_off, out_len, status, lb, (DocMeta*)meta, out_cap);
+    hipLaunchKernelGGL(k_doc<1>, dim3(tiles), dim3(DOC_NT), 0, s, arena, doc_off, sv_arena, sv_off, docs, out_base, n_docs, flags, out, out_off, out_len, status, lb, (DocMeta*)meta, out_cap);
+  return (int)hipGetLastError();
+}
+
+int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
+                          uint64_t sv_bytes, const uint64_t* sv_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
+                          uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
+  if (n_docs == 0) return 0;
+  static int n_cu = 0;
+  if (!n_cu) { int dev = 0; (void)hipGetDevice(&dev); if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256; }
+  const uint32_t waves = (n_docs + WAVE - 1) / WAVE, cap = (uint32_t)n_cu * 16u;   // lane per document, persistent lanes
+  const uint32_t grid = waves < cap ? waves : cap;
+  if (mode == 0)
+    hipLaunchKernelGGL(k_doc_lean<0>, dim3(grid), dim3(WAVE), 0, s, arena, arena_bytes, doc_off, sv_arena, sv_bytes, sv_off, n_docs, flags, out,
+                       out_off, out_len, status, (DocMeta*)meta, defer_list, out_cap);
+  else
+    hipLaunchKernelGGL(k_doc_lean<1>, dim3(grid), dim3(WAVE), 0, s, arena, arena_bytes, doc_off, sv_arena, sv_bytes, sv_off, n_docs, flags, out,
+                       out_off, out_len, status, (DocMeta*)meta, defer_list, out_cap);
   return (int)hipGetLastError();
 }
 

@@ -371,3 +371,42 @@ def test_async_device_api_matches_host_api(eng):
         got = (int(sts[d]), data[int(offs[d]):int(offs[d]) + int(lens[d])] if sts[d] == 0 else None)
         assert got[0] == host[d][0] and (got[0] != 0 or got[1] == host[d][1]), d
     assert r.payload_bytes == sum(len(h[1]) for h in host if h[0] == 0)
+
+
+def test_lean_sv_diff_edge_states_vs_oracle(eng):
+    # merged states with every struct shape of the lean-edge corpus (long strings, non-ASCII, deleted
+    # content, parents, 5-byte clients, large clocks, multi-struct blocks), diffed against random state
+    # vectors (missing clients, clocks inside / at / past each client's range, repeated entries)
+    from v1util import vu
+    rng = random.Random(99)
+    states, svs = [], []
+    for us in _lean_edge_docs(600, seed=2024):
+        st, m = oracle.merge_updates(us)
+        if st != 0:
+            continue
+        states.append(m)
+        svst, sv = oracle.encode_state_vector_from_update(m)
+        ents = []
+        if svst == 0 and sv:
+            n, p = 0, 0
+            from v1util import rd_vu
+            n, p = rd_vu(sv, 0)
+            for _ in range(n):
+                c, p = rd_vu(sv, p)
+                k, p = rd_vu(sv, p)
+                ents.append((c, rng.choice([0, k, max(k - 1, 0), rng.randrange(k + 1), k + 5])))
+        rng.shuffle(ents)
+        if ents and rng.random() < 0.2:
+            ents.append(ents[0])                       # repeated client: the last entry wins
+        if rng.random() < 0.1:
+            ents = []
+        svs.append(vu(len(ents)) + b"".join(vu(c) + vu(k) for c, k in ents))
+    lean0 = eng.stats().docs_lean
+    res = eng.encode_state_vector_from_update_batch(states)
+    for d, u in enumerate(states):
+        assert same(oracle.encode_state_vector_from_update(u), res[d]), u.hex()
+    res = eng.diff_update_batch(states, svs)
+    for d, u in enumerate(states):
+        assert same(oracle.diff_update(u, svs[d]), res[d]), (u.hex(), svs[d].hex())
+    took = eng.stats().docs_lean - lean0
+    assert 0 < took < 2 * len(states)

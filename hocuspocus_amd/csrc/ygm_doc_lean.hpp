@@ -118,17 +118,19 @@ struct LStruct {
 
 // Decodes the struct at pos from a fresh view; long ASCII strings are verified by streaming
 // through the window (which is advanced past them).  sbad != 0: the document is deferred.
-YDEV LStruct lean_doc_struct(SWin& w, uint64_t pos, uint64_t doc_end) {
-  LStruct s; s.kind = K_ITEM; s.len = 0; s.end = pos; s.ro_p = 0; s.ro_e = 0; s.c_p = 0; s.sbad = 0;
-  w.advance(pos);
-  uint32_t d[8];
-  w.view(pos, d);
-  const VMask m = vmask(d, doc_end - pos);
+// whole-view checks: a >= 7-byte run of top-bit bytes (a varuint of >= 8 bytes), or a zero byte
+// right after a top-bit byte (a non-minimal varuint): the document defers
+YDEV uint32_t vcheck(const VMask& m) {
   const uint32_t HV = m.H & m.V;
-  // whole-view checks: a >= 7-byte run of top-bit bytes, or a zero byte after a top-bit byte
-  // (a non-minimal varuint): the document defers
   const uint32_t h2 = HV & (HV >> 1), h4 = h2 & (h2 >> 2), h7 = h4 & (h4 >> 3);
-  uint32_t bad = h7 | (m.Z & (HV << 1) & m.V);
+  return h7 | (m.Z & (HV << 1) & m.V);
+}
+
+// The struct at pos, given the view d / masks m at pos (w advanced so that pos - cb < 16).
+YDEV LStruct lean_struct_at(SWin& w, uint64_t pos, uint64_t doc_end, const uint32_t (&d)[8], const VMask& m) {
+  LStruct s; s.kind = K_ITEM; s.len = 0; s.end = pos; s.ro_p = 0; s.ro_e = 0; s.c_p = 0; s.sbad = 0;
+  const uint32_t HV = m.H & m.V;
+  uint32_t bad = 0;
   const uint32_t info = d[0] & 0xFFu;
   s.info = info;
   bad |= (m.V & 1u) ^ 1u;
@@ -219,25 +221,37 @@ YDEV LStruct lean_doc_struct(SWin& w, uint64_t pos, uint64_t doc_end) {
   return s;
 }
 
+YDEV LStruct lean_doc_struct(SWin& w, uint64_t pos, uint64_t doc_end) {
+  w.advance(pos);
+  uint32_t d[8];
+  w.view(pos, d);
+  const VMask m = vmask(d, doc_end - pos);
+  LStruct s = lean_struct_at(w, pos, doc_end, d, m);
+  s.sbad |= vcheck(m);
+  return s;
+}
+
 // ---- lane-private output writers (global memory)
 YDEV uint64_t gw_vu(uint8_t* __restrict__ o, uint64_t t, uint64_t v) {
   while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; }
   o[t++] = (uint8_t)v;
   return t;
 }
-// copies n bytes from src to dst (both global, unaligned): 16-byte pieces, the last one
-// overlapping its predecessor (all inside [dst, dst + n)); short runs byte by byte
+// copies n bytes from src to dst (both global, unaligned): batches of eight 16-byte pieces (eight
+// loads in flight before the stores), then single pieces, the last one overlapping its predecessor
+// (all inside [dst, dst + n)); short runs byte by byte
 YDEV void gw_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t n) {
-  if (n >= 16) {
-    for (uint64_t off = 0;; off += 16) {
-      const uint64_t o = off + 16 <= n ? off : n - 16;
-      u32x4 v; __builtin_memcpy(&v, src + o, 16);
-      __builtin_memcpy(dst + o, &v, 16);
-      if (o == n - 16) break;
-    }
-  } else {
-    for (uint64_t i = 0; i < n; i++) dst[i] = src[i];
+  if (n < 16) { for (uint64_t i = 0; i < n; i++) dst[i] = src[i]; return; }
+  uint64_t o = 0;
+  for (; o + 128 <= n; o += 128) {
+    u32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) __builtin_memcpy(&v[k], src + o + 16 * k, 16);
+#pragma unroll
+    for (int k = 0; k < 8; k++) __builtin_memcpy(dst + o + 16 * k, &v[k], 16);
   }
+  for (; o + 16 <= n; o += 16) { u32x4 v; __builtin_memcpy(&v, src + o, 16); __builtin_memcpy(dst + o, &v, 16); }
+  if (o < n) { u32x4 v; __builtin_memcpy(&v, src + n - 16, 16); __builtin_memcpy(dst + n - 16, &v, 16); }
 }
 
 // Re-encodes the struct at pos with `off` leading clock units removed (Item.write(encoder,

@@ -144,6 +144,10 @@ __global__ __launch_bounds__(DOC_NT) void k_doc(const uint8_t* __restrict__ aren
 // ygm_doc_lean.hpp.  MODE 0 = encodeStateVectorFromUpdate (rule R-SV), 1 = diffUpdate (rule R-D).
 // Each lane loops over documents d = global lane, + total lanes; outputs go to the document's
 // slot (merge_slot); documents outside the lean shape are appended to `defer_list` for k_doc.
+enum : uint32_t {   // lean SV / diff walker phases: one unit (header, struct, delete-set entry) per iteration
+  PH_NEXT = 0, PH_SV, PH_UPD, PH_BLOCK, PH_STRUCT, PH_DS, PH_DSC, PH_DSR, PH_FIN
+};
+
 template <int MODE>
 __global__ __launch_bounds__(WAVE) void k_doc_lean(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                   const uint64_t* __restrict__ doc_off, const uint8_t* __restrict__ sv_arena,
@@ -151,164 +155,171 @@ __global__ __launch_bounds__(WAVE) void k_doc_lean(const uint8_t* __restrict__ a
                                                   uint8_t* __restrict__ out, uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len,
                                                   int32_t* __restrict__ status, DocMeta* meta, uint32_t* __restrict__ defer_list,
                                                   uint64_t out_cap) {
+  // The walk is ONE flat loop per lane: every iteration slides the window to `pos`, builds the view and
+  // masks once and decodes one unit -- a state-vector entry, the update header, a block header, a
+  // struct or a delete-set entry -- so lanes stay in lockstep whatever the block structure of their
+  // documents, and a lane that finishes a document starts its next one in the same loop.
   __shared__ uint32_t svt[MODE == 1 ? WAVE * DL_SV_MAX * 2 : 1];   // per-lane state-vector table (client, clock)
   const uint32_t l = threadIdx.x;
   const uint64_t lastc = arena_bytes & ~15ull, sv_lastc = sv_bytes & ~15ull;
+  const uint32_t stride = gridDim.x * WAVE;
   uint64_t payload = 0;
-  for (uint32_t d = blockIdx.x * WAVE + l; d < n_docs; d += gridDim.x * WAVE) {
-    const uint64_t a = doc_off[d], b = doc_off[d + 1];
-    const uint64_t slot = merge_slot(a, d), cap = merge_slot_cap(b - a);
-    const uint64_t body0 = slot + 16;        // the header is written right-aligned in front of the body
-    const uint64_t tend = slot + cap < out_cap ? slot + cap : out_cap;
-    uint32_t bad = (b - a) >> 31 ? 1u : 0u;
-    SWin w;
-    uint32_t nsv = 0;
-    if (MODE == 1) {   // decodeStateVector: last entry per client wins (Map.set)
-      const uint64_t sa = sv_off[d], sb = sv_off[d + 1];
-      w.init(sv_arena, sa, sv_lastc);
-      uint32_t dd[8]; w.view(sa, dd);
-      VMask m = vmask(dd, sb - sa);
-      uint32_t e = vend(m.T, 0);
-      const uint32_t n = vval(dd, 0, e, bad);
-      uint64_t q = sa + e + 1u;
-      bad |= n > (uint32_t)DL_SV_MAX ? 1u : 0u;
-      for (uint32_t i = 0; i < n && !bad; i++) {
-        w.advance(q); w.view(q, dd); m = vmask(dd, sb - q);
-        bad |= m.Z & ((m.H & m.V) << 1) & m.V;   // non-minimal varuints are fine for an SV, but rare: defer
+  uint32_t d = blockIdx.x * WAVE + l - stride;   // PH_NEXT advances it
+  uint32_t phase = PH_NEXT, bad = 0;
+  uint64_t a = 0, b = 0, slot = 0, body0 = 0, tend = 0, t = 0, pos = 0, sb = 0, run0 = 0, ds0 = 0;
+  uint32_t nsv = 0, n_left = 0, nst = 0, st = 0, client = 0, clock = 0, svc = 0, count = 0;
+  uint32_t cc = 0, clk = 0, prev = 0;
+  bool first = true, stop = false, emitted = false, have_prev = false;
+  SWin w;
+  for (;;) {
+    if (phase == PH_NEXT || phase == PH_FIN) {
+      if (phase == PH_FIN) {   // finish the document
+        bad |= pos > b ? 1u : 0u;
+        if (bad) {
+          status[d] = ST_FALLBACK;
+          defer_list[atomicAdd(&meta->lean_defer, 1u)] = d;
+        } else {
+          uint32_t hl = 1; for (uint32_t v = count; v > 127u; v >>= 7) hl++;
+          gw_vu(out, body0 - hl, count);
+          out_off[d] = body0 - hl; out_len[d] = hl + (t - body0); status[d] = ST_OK;
+          payload += hl + (t - body0);
+        }
+      }
+      d += stride;
+      if (d >= n_docs) break;
+      a = doc_off[d]; b = doc_off[d + 1];
+      slot = merge_slot(a, d);
+      const uint64_t cap = merge_slot_cap(b - a);
+      body0 = slot + 16;   // the header (a count known at the end) goes right-aligned in front of the body
+      tend = slot + cap < out_cap ? slot + cap : out_cap;
+      t = body0; bad = (b - a) >> 31 ? 1u : 0u; count = 0; nsv = 0;
+      cc = 0; clk = 0; first = true; stop = false; have_prev = false; prev = 0;
+      if (MODE == 1) { pos = sv_off[d]; sb = sv_off[d + 1]; w.init(sv_arena, pos, sv_lastc); phase = PH_SV; n_left = 0xFFFFFFFFu; }
+      else { pos = a; w.init(arena, a, lastc); phase = PH_UPD; }
+      continue;
+    }
+    const uint64_t lim = phase == PH_SV ? sb : b;
+    w.advance(pos);
+    uint32_t dd[8];
+    w.view(pos, dd);
+    const VMask m = vmask(dd, lim - pos);
+    if (phase != PH_STRUCT) bad |= vcheck(m);
+    if (phase == PH_STRUCT) {
+      const LStruct sx = lean_struct_at(w, pos, b, dd, m);
+      bad |= sx.sbad | vcheck(m);
+      const uint64_t end = (uint64_t)clock + sx.len;
+      bad |= end >> 32 ? 1u : 0u;
+      if (MODE == 0) {   // sv_doc's state machine (rule R-SV)
+        if (first) { cc = client; stop = clock != 0; clk = stop ? 0u : (uint32_t)end; first = false; }
+        if (cc != client) {
+          if (clk) { if (t + 10 > tend) bad = 1; else { t = gw_vu(out, t, cc); t = gw_vu(out, t, clk); count++; } }
+          cc = client; clk = 0; stop = clock != 0;
+        }
+        if (sx.kind == K_SKIP) stop = true;
+        if (!stop) clk = (uint32_t)end;
+      } else if (!emitted && sx.kind != K_SKIP && end > svc && !bad) {
+        // the first written struct of the client (rule R-D): block header, then the struct with offset svc - clock
+        const uint32_t off = svc > clock ? svc - clock : 0u;
+        if (t + 64 + (sx.end - pos) > tend) bad = 1;
+        else {
+          t = gw_vu(out, t, nst - st); t = gw_vu(out, t, client); t = gw_vu(out, t, (uint64_t)clock + off);
+          if (off == 0) { gw_copy(out + t, arena + pos, sx.end - pos); t += sx.end - pos; }
+          else t = lean_write_sliced(out, t, arena, pos, sx, client, clock, off);
+          emitted = true; count++;
+          run0 = sx.end;
+        }
+      }
+      clock = (uint32_t)end;
+      pos = sx.end;
+      if (++st == nst) {   // end of the client block
+        if (MODE == 1 && emitted && !bad) {   // the rest of the block, verbatim (Skips included)
+          if (t + (pos - run0) > tend) bad = 1;
+          else { gw_copy(out + t, arena + run0, pos - run0); t += pos - run0; }
+        }
+        phase = --n_left ? PH_BLOCK : (MODE == 1 ? PH_DS : PH_FIN);
+      }
+    } else if (phase == PH_BLOCK) {
+      const uint32_t e1 = vend(m.T, 0); nst = vval(dd, 0, e1, bad);
+      const uint32_t e2 = vend(m.T, e1 + 1u); client = vval(dd, e1 + 1u, e2, bad);
+      const uint32_t e3 = vend(m.T, e2 + 1u); clock = vval(dd, e2 + 1u, e3, bad);
+      pos += e3 + 1u;
+      if (MODE == 1) {   // canonical (client-descending, distinct) block order; anything else: the exact kernel
+        bad |= (have_prev && client >= prev) ? 1u : 0u;
+        prev = client; have_prev = true;
+        svc = 0;
+        for (uint32_t j = 0; j < nsv; j++) if (svt[(l * DL_SV_MAX + j) * 2] == client) svc = svt[(l * DL_SV_MAX + j) * 2 + 1];
+        emitted = false;
+      }
+      st = 0;
+      if (nst == 0) phase = --n_left ? PH_BLOCK : (MODE == 1 ? PH_DS : PH_FIN);
+      else phase = PH_STRUCT;
+    } else if (phase == PH_UPD) {
+      const uint32_t e = vend(m.T, 0);
+      n_left = vval(dd, 0, e, bad);
+      pos += e + 1u;
+      phase = n_left ? PH_BLOCK : (MODE == 1 ? PH_DS : PH_FIN);
+    } else if (phase == PH_SV) {   // decodeStateVector: the count, then (client, clock) entries; last one per client wins
+      if (n_left == 0xFFFFFFFFu) {
+        const uint32_t e = vend(m.T, 0);
+        n_left = vval(dd, 0, e, bad);
+        pos += e + 1u;
+        bad |= n_left > (uint32_t)DL_SV_MAX ? 1u : 0u;
+      } else {
         const uint32_t e1 = vend(m.T, 0); const uint32_t cl = vval(dd, 0, e1, bad);
         const uint32_t e2 = vend(m.T, e1 + 1u); const uint32_t ck = vval(dd, e1 + 1u, e2, bad);
-        q += e2 + 1u;
-        bad |= q > sb ? 1u : 0u;
+        pos += e2 + 1u;
         uint32_t at = nsv;
         for (uint32_t j = 0; j < nsv; j++) if (svt[(l * DL_SV_MAX + j) * 2] == cl) at = j;
-        svt[(l * DL_SV_MAX + at) * 2] = cl; svt[(l * DL_SV_MAX + at) * 2 + 1] = ck;
+        if (at < (uint32_t)DL_SV_MAX) { svt[(l * DL_SV_MAX + at) * 2] = cl; svt[(l * DL_SV_MAX + at) * 2 + 1] = ck; }
         if (at == nsv) nsv++;
+        n_left--;
       }
-      bad |= q != sb ? 1u : 0u;   // trailing bytes in a state vector: exact kernel decides
-    }
-    w.init(arena, a, lastc);
-    uint32_t dd[8]; w.view(a, dd);
-    VMask m = vmask(dd, b - a);
-    uint32_t e = vend(m.T, 0);
-    const uint32_t nb = vval(dd, 0, e, bad);
-    uint64_t pos = a + e + 1u;
-    uint64_t t = body0;
-    uint32_t count = 0;                       // SV entries / written blocks
-    // SV state (sv_doc): current client, its contiguous clock, whether it stopped
-    uint32_t cc = 0, clk = 0; bool first = true, stop = false;
-    uint32_t prev_client = 0xFFFFFFFFu; bool have_prev = false;
-    for (uint32_t blk = 0; blk < nb && !bad; blk++) {
-      w.advance(pos); w.view(pos, dd); m = vmask(dd, b - pos);
-      bad |= m.Z & ((m.H & m.V) << 1) & m.V;
-      const uint32_t e1 = vend(m.T, 0); const uint32_t nst = vval(dd, 0, e1, bad);
-      const uint32_t e2 = vend(m.T, e1 + 1u); const uint32_t client = vval(dd, e1 + 1u, e2, bad);
-      const uint32_t e3 = vend(m.T, e2 + 1u); uint32_t clock = vval(dd, e2 + 1u, e3, bad);
-      pos += e3 + 1u;
-      if (MODE == 1) {   // canonical (client-descending, distinct) block order; anything else: exact kernel
-        bad |= (have_prev && client >= prev_client) ? 1u : 0u;
-        prev_client = client; have_prev = true;
+      if (n_left == 0 && !bad) {   // the document itself
+        bad |= pos != sb ? 1u : 0u;   // trailing bytes in a state vector: the exact kernel decides
+        pos = a; w.init(arena, a, lastc); phase = PH_UPD;
       }
-      uint32_t svc = 0;
-      if (MODE == 1) for (uint32_t j = 0; j < nsv; j++) if (svt[(l * DL_SV_MAX + j) * 2] == client) svc = svt[(l * DL_SV_MAX + j) * 2 + 1];
-      bool emitted = false;
-      uint64_t run0 = 0;                      // diff: start of the verbatim run after the first written struct
-      for (uint32_t st = 0; st < nst && !bad; st++) {
-        const LStruct sx = lean_doc_struct(w, pos, b);
-        bad |= sx.sbad;
-        if (bad) break;
-        const uint64_t end = (uint64_t)clock + sx.len;
-        bad |= end >> 32 ? 1u : 0u;
-        if (MODE == 0) {
-          if (first) { cc = client; stop = clock != 0; clk = stop ? 0u : (uint32_t)end; first = false; }
-          if (cc != client) {
-            if (clk) { if (t + 10 > tend) bad = 1; else { t = gw_vu(out, t, cc); t = gw_vu(out, t, clk); count++; } }
-            cc = client; clk = 0; stop = clock != 0;
-          }
-          if (sx.kind == K_SKIP) stop = true;
-          if (!stop) clk = (uint32_t)end;
-        } else if (!emitted && sx.kind != K_SKIP && end > svc) {
-          // the first written struct of this client: header, then the struct with offset svc - clock
-          const uint32_t off = svc > clock ? svc - clock : 0u;
-          if (t + 64 + (sx.end - pos) > tend) bad = 1;
-          else {
-            t = gw_vu(out, t, nst - st); t = gw_vu(out, t, client); t = gw_vu(out, t, (uint64_t)clock + off);
-            if (off == 0) { gw_copy(out + t, arena + pos, sx.end - pos); t += sx.end - pos; }
-            else t = lean_write_sliced(out, t, arena, pos, sx, client, clock, off);
-            emitted = true; count++;
-            run0 = sx.end;
-          }
-        }
-        clock = (uint32_t)end;
-        pos = sx.end;
-      }
-      if (MODE == 1 && emitted && !bad) {   // the rest of the client's block, verbatim (Skips included)
-        if (t + (pos - run0) > tend) bad = 1;
-        else { gw_copy(out + t, arena + run0, pos - run0); t += pos - run0; }
-      }
-    }
-    if (MODE == 0 && !bad && !first && clk) {
-      if (t + 10 > tend) bad = 1; else { t = gw_vu(out, t, cc); t = gw_vu(out, t, clk); count++; }
-    }
-    if (MODE == 1 && !bad) {
-      // delete set: copied verbatim when readDeleteSet + writeDeleteSet reproduce it -- distinct clients
-      // with >= 1 range each, client-descending (13.6) / any order (13.5 first-seen), minimal varuints
-      const uint64_t ds0 = pos;
-      w.advance(pos); w.view(pos, dd); m = vmask(dd, b - pos);
-      bad |= m.Z & ((m.H & m.V) << 1) & m.V;
-      e = vend(m.T, 0);
-      const uint32_t ncl = vval(dd, 0, e, bad);
+    } else if (phase == PH_DS) {   // delete set: copied verbatim when readDeleteSet + writeDeleteSet reproduce it
+      ds0 = pos;
+      const uint32_t e = vend(m.T, 0);
+      n_left = vval(dd, 0, e, bad);
       pos += e + 1u;
-      uint32_t pc = 0xFFFFFFFFu; bool hp = false;
-      for (uint32_t i = 0; i < ncl && !bad; i++) {
-        w.advance(pos); w.view(pos, dd); m = vmask(dd, b - pos);
-        bad |= m.Z & ((m.H & m.V) << 1) & m.V;
-        const uint32_t e1 = vend(m.T, 0); const uint32_t cl = vval(dd, 0, e1, bad);
-        const uint32_t e2 = vend(m.T, e1 + 1u); const uint32_t nr = vval(dd, e1 + 1u, e2, bad);
-        pos += e2 + 1u;
-        bad |= nr == 0u ? 1u : 0u;
-        if (flags & F_COMPAT_135) {   // first-seen order: distinct clients (checked against every earlier entry)
-          bad |= (hp && cl == pc) ? 1u : 0u;
-          if (i > 0) {   // earlier entries are re-read from the document (rare: multi-client delete sets)
-            Cur c{arena + ds0, 0, (uint32_t)(b - ds0), 0, 0};
-            const uint64_t n0 = c.vu();
-            for (uint64_t k = 0; k < n0 && k < i && !c.err; k++) {
-              const uint64_t c2 = c.vu(), r2 = c.vu();
-              for (uint64_t r = 0; r < r2 && !c.err; r++) { c.vu(); c.vu(); }
-              if (c2 == cl) bad = 1;
-            }
-          }
-        } else bad |= (hp && cl >= pc) ? 1u : 0u;
-        pc = cl; hp = true;
-        for (uint32_t r = 0; r < nr && !bad; r++) {
-          w.advance(pos); w.view(pos, dd); m = vmask(dd, b - pos);
-          bad |= m.Z & ((m.H & m.V) << 1) & m.V;
-          const uint32_t f1 = vend(m.T, 0); (void)vval(dd, 0, f1, bad);
-          const uint32_t f2 = vend(m.T, f1 + 1u); (void)vval(dd, f1 + 1u, f2, bad);
-          pos += f2 + 1u;
-        }
-      }
-      bad |= pos > b ? 1u : 0u;
-      if (!bad) {
+      have_prev = false;
+      if (n_left) phase = PH_DSC;
+      else {   // an empty delete set: its single count byte
         if (t + (pos - ds0) > tend) bad = 1;
         else { gw_copy(out + t, arena + ds0, pos - ds0); t += pos - ds0; }
+        phase = PH_FIN;
+      }
+    } else if (phase == PH_DSC) {   // a client entry: distinct clients with >= 1 range, client-descending (13.6)
+      const uint32_t e1 = vend(m.T, 0); const uint32_t cl = vval(dd, 0, e1, bad);
+      const uint32_t e2 = vend(m.T, e1 + 1u); nst = vval(dd, e1 + 1u, e2, bad);   // (nst: ranges left)
+      pos += e2 + 1u;
+      bad |= nst == 0u ? 1u : 0u;
+      if (flags & F_COMPAT_135) bad |= have_prev ? 1u : 0u;   // first-seen order: one client entry only (else exact kernel)
+      else bad |= (have_prev && cl >= prev) ? 1u : 0u;
+      prev = cl; have_prev = true;
+      phase = PH_DSR;
+    } else if (phase == PH_DSR) {   // a (clock, len) range
+      const uint32_t f1 = vend(m.T, 0); (void)vval(dd, 0, f1, bad);
+      const uint32_t f2 = vend(m.T, f1 + 1u); (void)vval(dd, f1 + 1u, f2, bad);
+      pos += f2 + 1u;
+      if (--nst == 0) {
+        if (--n_left == 0) {   // the whole delete set parsed: copy it
+          bad |= pos > b ? 1u : 0u;
+          if (!bad) {
+            if (t + (pos - ds0) > tend) bad = 1;
+            else { gw_copy(out + t, arena + ds0, pos - ds0); t += pos - ds0; }
+          }
+          phase = PH_FIN;
+        } else phase = PH_DSC;
       }
     }
-    bad |= pos > b ? 1u : 0u;
-#ifdef YGM_DEBUG_LEAN
-    if (d < 4) printf("doc_lean<%d> d=%u bad=%u nb=%u pos=%lu a=%lu b=%lu count=%u t-body=%lu nsv=%u\n", MODE, d, bad, nb,
-                      (unsigned long)pos, (unsigned long)a, (unsigned long)b, count, (unsigned long)(t - body0), nsv);
-#endif
-    if (bad) {
-      status[d] = ST_FALLBACK;
-      defer_list[atomicAdd(&meta->lean_defer, 1u)] = d;
-    } else {
-      uint32_t hl = 1; for (uint32_t v = count; v > 127u; v >>= 7) hl++;
-      gw_vu(out, body0 - hl, count);
-      out_off[d] = body0 - hl; out_len[d] = hl + (t - body0); status[d] = ST_OK;
-      payload += hl + (t - body0);
+    if (bad) phase = PH_FIN;
+    if (MODE == 0 && phase == PH_FIN && !bad && !first && clk) {   // the last state-vector entry
+      if (t + 10 > tend) bad = 1; else { t = gw_vu(out, t, cc); t = gw_vu(out, t, clk); count++; }
     }
   }
-  // one atomic per wave for the output bytes (lanes reduced through the first lane)
+  // one atomic per wave for the output bytes
   payload = wave_sum(payload);
   if (l == 0 && payload) add_payload(meta, blockIdx.x, payload);
 }

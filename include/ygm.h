@@ -101,12 +101,12 @@ int ygm_sv_from_update_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *do
  * All pointers are device pointers.  doc_upd: n_docs+1 update-index offsets
  * (document d owns updates doc_upd[d] .. doc_upd[d+1]); upd_off must be
  * non-decreasing.  Results stay on the device: the data/off/len/status
- * pointers of the result point into context-owned device memory.  Merge
- * outputs are NOT packed: document d's bytes are data[off[d] .. off[d]+len[d])
- * inside its own slot (2*in_off + 64*d, capacity 2*|in| + 64) or, when they
- * outgrow it, in an overflow region after the slots; data_bytes is the used
- * extent of `data`, payload_bytes the sum of len[].  SV/diff outputs are
- * packed in document order (payload_bytes == data_bytes).  `stream` is a
+ * pointers of the result point into context-owned device memory.  Outputs
+ * are NOT packed: document d's bytes are data[off[d] .. off[d]+len[d]) inside
+ * its own slot (2*in_off + 64*d, capacity 2*|in| + 64) or, for documents the
+ * lean kernels defer, in a region after the slots (merge: overflow cursor;
+ * SV / diff: packed by the exact per-document kernel); data_bytes is the used
+ * extent of `data`, payload_bytes the sum of len[].  `stream` is a
  * hipStream_t (NULL = the context's stream); the call returns after one
  * read of the launch counters. */
 typedef struct {

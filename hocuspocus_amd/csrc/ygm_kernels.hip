@@ -1126,13 +1126,18 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
     }
     // ---- parse, lane per update
     LRec rec[LN_ROWS];
+    bool hs[LN_ROWS], hasd[LN_ROWS];   // row holds an update with structs / with a non-empty delete set
     bool bad = false;
+#pragma unroll
+    for (int q = 0; q < LN_ROWS; q++) { hs[q] = false; hasd[q] = false; }
     if (go) {
 #pragma unroll
       for (int q = 0; q < LN_ROWS; q++) {
         const bool valid = l + WAVE * q < k;
         if (valid) { rec[q] = lean_parse(lin, us[q], un[q]); bad |= !rec[q].ok; }
         else { rec[q].ok = true; rec[q].client = 0; rec[q].clock = 0; rec[q].clen = 0; rec[q].span = 0; }
+        hs[q] = valid && (rec[q].span & 0xFF00u) != 0u;
+        hasd[q] = valid && rec[q].ok && lin[lean_ds_pos(us[q], rec[q].span)] != 0;
       }
     }
     DIAGL(1);
@@ -1148,7 +1153,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
       // ---- clients: distinct values by wave vote (<= 4), ranked descending
       uint32_t bid[LN_ROWS];
 #pragma unroll
-      for (int q = 0; q < LN_ROWS; q++) bid[q] = (l + WAVE * q < k) ? 0xFFu : 0xFEu;
+      for (int q = 0; q < LN_ROWS; q++) bid[q] = hs[q] ? 0xFFu : 0xFEu;
       uint32_t cl0 = 0, cl1 = 0, cl2 = 0, cl3 = 0, nC = 0;
       for (int it = 0; it < 5; it++) {
         uint32_t cand = 0; bool found = false;
@@ -1183,7 +1188,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
         uint32_t blk[LN_ROWS], inb[LN_ROWS], idx[LN_ROWS];
 #pragma unroll
         for (int q = 0; q < LN_ROWS; q++) {
-          const bool valid = l + WAVE * q < k;
+          const bool valid = hs[q];
           const uint32_t id = bid[q] & 3u;
           const uint32_t b = valid ? (id == 0 ? rk[0] : id == 1 ? rk[1] : id == 2 ? rk[2] : rk[3]) : 7u;
           blk[q] = b;
@@ -1208,7 +1213,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
         LB32* scr = (LB32*)lout;
 #pragma unroll
         for (int q = 0; q < LN_ROWS; q++) {
-          if (l + WAVE * q < k) {
+          if (hs[q]) {
             const uint32_t b = blk[q];
             const uint32_t j = (b == 0 ? rbase[0] : b == 1 ? rbase[1] : b == 2 ? rbase[2] : rbase[3]) + idx[q];
             scr[2 * j] = rec[q].clock; scr[2 * j + 1] = rec[q].clock + rec[q].clen;
@@ -1217,7 +1222,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
         wave_sync();
 #pragma unroll
         for (int q = 0; q < LN_ROWS; q++) {
-          if (l + WAVE * q < k && idx[q] > 0u) {
+          if (hs[q] && idx[q] > 0u) {
             const uint32_t b = blk[q];
             const uint32_t j = (b == 0 ? rbase[0] : b == 1 ? rbase[1] : b == 2 ? rbase[2] : rbase[3]) + idx[q];
             bad |= scr[2 * j - 1] != rec[q].clock;
@@ -1227,6 +1232,19 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
 #pragma unroll
         for (int b = 0; b < 4; b++) first_clock[b] = (uint32_t)__builtin_amdgcn_readfirstlane((int)scr[2 * (rbase[b] < 255u ? rbase[b] : 0u)]);
         wave_sync();
+        // ---- delete sets: union of every update's ranges (scratch after the contiguity pairs)
+        LDsUnion dsu; dsu.bytes = 1u; dsu.bad = false; dsu.nsegs = 0;
+        bool anyds = false;
+#pragma unroll
+        for (int q = 0; q < LN_ROWS; q++) anyds |= hasd[q];
+        if (__ballot(anyds) != 0) {
+          uint32_t dpos[LN_ROWS], uend[LN_ROWS];
+#pragma unroll
+          for (int q = 0; q < LN_ROWS; q++) { dpos[q] = lean_ds_pos(us[q], rec[q].span); uend[q] = us[q] + un[q]; }
+          dsu = lean_ds_union(lin, (LB32*)(lout + 2048), dpos, uend, hasd, flags);
+          bad |= dsu.bad;
+          wave_sync();
+        }
         // the output buffer is assembled by OR: zero it
         {
           const u32x4 z = {0u, 0u, 0u, 0u};
@@ -1251,44 +1269,14 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
             base[b] = at;
             if ((uint32_t)b < nC) at += hdr[b] + byt[b];
           }
-          size = at + 1;   // + the empty delete set
+          size = at + dsu.bytes;   // + the delete set
           if (size > (uint32_t)LN_OUT || ((size + 15u) & ~15u) > cap || slot + size > out_cap) defer = true;
           else {
-#ifdef YGM_LEAN_GEMIT   // experiment: structs straight to global memory as unaligned dword pieces
-            {
-              uint8_t* o = out + slot;
-#pragma unroll
-              for (int q = 0; q < LN_ROWS; q++) {
-                if (l + WAVE * q < k) {
-                  const uint32_t b = blk[q];
-                  const uint32_t t = (b == 0 ? base[0] + hdr[0] : b == 1 ? base[1] + hdr[1] : b == 2 ? base[2] + hdr[2] : base[3] + hdr[3]) + inb[q];
-                  const uint32_t s0 = rec[q].span >> 16, n = rec[q].span & 0xFFu;   // n >= 4 for every struct the parser accepts
-                  for (uint32_t off = 0; off < n; off += 4) {
-                    const uint32_t oo = off + 4u <= n ? off : n - 4u;           // the last piece overlaps its predecessor
-                    uint32_t v; __builtin_memcpy(&v, (const uint8_t*)(lin + s0 + oo), 4);
-                    __builtin_memcpy(o + t + oo, &v, 4);
-                  }
-                }
-              }
-              if (l < nC) {
-                const uint32_t bb = l;
-                uint64_t t = bb == 0 ? base[0] : bb == 1 ? base[1] : bb == 2 ? base[2] : base[3];
-                uint32_t v = bb == 0 ? cnt[0] : bb == 1 ? cnt[1] : bb == 2 ? cnt[2] : cnt[3];
-                while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; } o[t++] = (uint8_t)v;
-                v = bb == 0 ? ctab[0] : bb == 1 ? ctab[1] : bb == 2 ? ctab[2] : ctab[3];
-                while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; } o[t++] = (uint8_t)v;
-                v = bb == 0 ? first_clock[0] : bb == 1 ? first_clock[1] : bb == 2 ? first_clock[2] : first_clock[3];
-                while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; } o[t++] = (uint8_t)v;
-              }
-              if (l == 0) { uint32_t v = nC; uint64_t t = 0; while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; } o[t++] = (uint8_t)v; o[size - 1] = 0; }
-            }
-            if (false)
-#endif
             {
             // ---- emit into the LDS output buffer: structs (funnel copies), block headers, document header, delete set
 #pragma unroll
             for (int q = 0; q < LN_ROWS; q++) {
-              if (l + WAVE * q < k) {
+              if (hs[q]) {
                 const uint32_t b = blk[q];
                 const uint32_t t = (b == 0 ? base[0] + hdr[0] : b == 1 ? base[1] + hdr[1] : b == 2 ? base[2] + hdr[2] : base[3] + hdr[3]) + inb[q];
                 lds_or_copy(lout, lin, t, rec[q].span >> 16, rec[q].span & 0xFFu);
@@ -1301,7 +1289,8 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
               t = lds_vu(lout, t, bb == 0 ? ctab[0] : bb == 1 ? ctab[1] : bb == 2 ? ctab[2] : ctab[3]);
               lds_vu(lout, t, bb == 0 ? first_clock[0] : bb == 1 ? first_clock[1] : bb == 2 ? first_clock[2] : first_clock[3]);
             }
-            if (l == 0) lds_vu(lout, 0, nC);   // (the final delete-set byte 0 is already zero)
+            if (l == 0) lds_vu(lout, 0, nC);
+            if (dsu.bytes > 1u) lean_ds_emit(lout, at, dsu);   // (an empty delete set is the zero byte already there)
             wave_sync();
             DIAGL(3);
             uint8_t* o = out + slot;

@@ -2,12 +2,14 @@
 // DOCUMENT, no calls, no scratch, no per-struct LDS records.
 //
 // Shape it takes (the onChange stream of row a4/a5): k >= 2 updates of
-// <= 32 bytes, each ONE client block of Items (ContentString ASCII / ContentDeleted)
-// and an empty delete set, at most 4 distinct clients, and every client's updates
-// clock-contiguous in log order.  For such a document rule R-M
-// degenerates to: blocks by client descending, each block = the clients' structs in
-// log order, copied byte for byte (Items never merge, Y@79424; no gaps, so no Skips;
-// no GC, so no coalescing), then an empty delete set.  Anything else -- or anything
+// <= 32 bytes, each either ONE client block of Items (ContentString ASCII / ContentDeleted)
+// or no structs at all (a deletion: delete set only), at most 4 distinct struct clients,
+// every client's updates clock-contiguous in log order, and at most 64 delete-set ranges
+// in the document.  For such a document rule R-M degenerates to:
+// blocks by client descending, each block = the clients' structs in log order, copied
+// byte for byte (Items never merge, Y@79424; no gaps, so no Skips; no GC, so no
+// coalescing); the delete sets are unioned by rule R-DS (one range per lane: rank sort,
+// segmented max scan, run encoding).  Anything else -- or anything
 // this kernel cannot prove -- is deferred to the general kernels (k_merge_wave ->
 // k_merge_fast -> k_merge_seq), which also produce every error status.
 //
@@ -23,6 +25,7 @@
 //           (branch-free, order-free), then 16-byte coalesced stores
 #pragma once
 #include "ygm_common.hpp"
+#include "ygm_merge_wave.hpp"
 
 namespace ygm {
 
@@ -83,6 +86,10 @@ YDEV uint32_t hibits8(uint32_t lo, uint32_t hi) {
 }
 
 // One parsed update (row record).
+// staged position of an update's delete set: right after its structs (update at us, span of
+// its parse), or after the 0 block count of an update without structs
+YDEV uint32_t lean_ds_pos(uint32_t us, uint32_t span) { return span ? (span >> 16) + (span & 0xFFu) : us + 1u; }
+
 struct LRec {
   uint32_t client, clock, clen;
   uint32_t span;   // sstart (doc-relative staged position of the first struct) << 16 | nst << 8 | sbytes
@@ -102,31 +109,44 @@ YDEV uint32_t pext32(uint32_t x, uint32_t y, uint32_t n) {
 // Failure conditions are OR-ed into one integer (no per-condition lane masks); bytes the
 // walk branches on (info, parentInfo, string lengths) are single ds_read_u8 of the staged
 // copy; varuint ends come from the terminator mask T.
-YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
-  LRec R; R.ok = false; R.client = 0; R.clock = 0; R.clen = 0; R.span = 0;
-  if (n < 4 || n > (uint32_t)LN_UMAX) return R;
+// bitwise select: x where m is set, y elsewhere (no ?: on array elements -- the compiler turns
+// a ?: of array elements into a scratch-indexed load)
+YDEV uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); }
+
+// 32 bytes of staged input from position s as d[0..7] (d[j] = bytes 4j..4j+3): three aligned
+// ds_read_b128 normalised by selects and v_alignbyte (an unaligned b128 read replays)
+YDEV void lean_window(LB8* in, uint32_t s, uint32_t (&d)[8]) {
   const uint32_t a = s & ~15u, r = s & 15u;
   const u32x4 c0 = *(const LB128*)(in + a), c1 = *(const LB128*)(in + a + 16), c2 = *(const LB128*)(in + a + 32);
   const uint32_t w[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
-  // normalise: d[j] = bytes 4j..4j+3 of the update = (w[j + r/4 + 1] : w[j + r/4]) >> 8(r & 3)
-  // (mask selects, not ?: -- the compiler turns a ?: of array elements into a scratch-indexed load)
+  // d[j] = (w[j + r/4 + 1] : w[j + r/4]) >> 8(r & 3)
   const uint32_t m1 = 0u - ((r >> 2) & 1u), m2 = 0u - ((r >> 3) & 1u);
   uint32_t L[9];
 #pragma unroll
-  for (int j = 0; j < 9; j++) {
-    const uint32_t s0 = (w[j + 1] & m1) | (w[j] & ~m1);
-    const uint32_t s1 = (w[j + 3] & m1) | (w[j + 2] & ~m1);
-    L[j] = (s1 & m2) | (s0 & ~m2);
-  }
-  uint32_t d[8];
+  for (int j = 0; j < 9; j++) L[j] = bsel(m2, bsel(m1, w[j + 3], w[j + 2]), bsel(m1, w[j + 1], w[j]));
 #pragma unroll
   for (int j = 0; j < 8; j++) d[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], r & 3u);
+}
+// H = top-bit mask of the 32 window bytes
+YDEV uint32_t lean_hmask(const uint32_t (&d)[8]) {
+  uint32_t H = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) H |= hibits8(d[2 * j], d[2 * j + 1]) << (8 * j);
+  return H;
+}
+
+YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
+  LRec R; R.ok = false; R.client = 0; R.clock = 0; R.clen = 0; R.span = 0;
+  if (n < 2 || n > (uint32_t)LN_UMAX) return R;
+  uint32_t d[8];
+  lean_window(in, s, d);
+  if ((d[0] & 0xFFu) == 0u) { R.ok = true; return R; }   // no structs: a delete set only (at s + 1)
   // masks over the 32 window bytes: H = top bit set, Z = zero byte ("haszero": may also flag a
   // 0x01 right above a zero byte, which only defers)
-  uint32_t H = 0, Z = 0;
+  const uint32_t H = lean_hmask(d);
+  uint32_t Z = 0;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    H |= hibits8(d[2 * j], d[2 * j + 1]) << (8 * j);
     const uint32_t z0 = (d[2 * j] - 0x01010101u) & ~d[2 * j], z1 = (d[2 * j + 1] - 0x01010101u) & ~d[2 * j + 1];
     Z |= hibits8(z0, z1) << (8 * j);
   }
@@ -145,7 +165,7 @@ YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
   // ASCII run of L bytes at p inside the update (L <= 31)
 #define LN_ASCII(p, L) (bad |= ((n - (p) - (L)) & 0x80000000u) | ((L) & ~31u) | ((HV >> ((p) < 31u ? (p) : 31u)) & ((1u << ((L) & 31u)) - 1u)))
   const uint32_t b0 = d[0] & 0xFFu, b1 = (d[0] >> 8) & 0xFFu;
-  bad |= (b0 ^ 1u) | ((b1 - 1u) & ~127u);    // one client block of 1..127 structs
+  bad |= (b0 ^ 1u) | ((b1 - 1u) & ~127u) | (n < 4u ? 1u : 0u);    // one client block of 1..127 structs
   uint32_t e, p;
   LN_VEND(2u, e);
   const uint32_t cl_n = e - 1u;              // client bytes 2..e
@@ -211,13 +231,58 @@ YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
   } while (++st < b1 && (bad | (p >= n ? 1u : 0u)) == 0u);
 #undef LN_VEND
 #undef LN_ASCII
-  const uint32_t nm = 0;
-  bad |= nm | ((n - 1u - p) & 0x80000000u) | u[p < 40u ? p : 40u];   // then the empty delete set (count 0)
+  bad |= (n - 1u - p) & 0x80000000u;          // then the delete set (at least its count byte)
   bad |= (uint32_t)(((uint64_t)clock + clen) >> 32);
   R.ok = bad == 0u;
   R.client = client; R.clock = clock; R.clen = clen;
-  R.span = ((s + sstart) << 16) | (b1 << 8) | ((p - sstart) & 0xFFu);
+  R.span = ((s + sstart) << 16) | (b1 << 8) | ((p - sstart) & 0xFFu);   // the delete set follows the structs
   return R;
+}
+
+// ---- delete sets (rule R-DS): a DS is varuints only, so one update's DS is
+// walked in a 32-byte register window by its terminator mask, one range per call.
+constexpr int LN_DSMAX = 64;    // delete-set ranges per document (one per lane in the union)
+struct LDsCur {
+  LB8* u;                       // the DS bytes (staged)
+  uint32_t T, lim;              // terminator mask over the valid window bytes; window bytes of the update
+  uint32_t p, cl_left, r_left, client, bad;
+};
+// next varuint of the DS (at most maxb bytes; 5 = any uint32): its end from the terminator
+// mask, its bytes by independent ds_read_u8
+YDEV uint32_t lean_ds_vu(LDsCur& c, uint32_t maxb) {
+  const uint32_t pp = c.p < 31u ? c.p : 31u;
+  const uint32_t e = pp + (uint32_t)__builtin_ctz((c.T >> pp) | 0x80000000u);
+  const uint32_t nb = e - c.p + 1u;
+  LB8* b = c.u + pp;
+  const uint32_t x = b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24), y = b[4];
+  c.bad |= (c.p >= c.lim ? 1u : 0u) | (e >= c.lim ? 1u : 0u) | (nb > maxb ? 1u : 0u) | (nb == 5u ? (y & 0x70u) : 0u);
+  c.p = e + 1u;
+  return pext32(x, y, nb);
+}
+// opens the DS at staged position a, n bytes to the end of its update
+YDEV void lean_ds_open(LB8* in, uint32_t a, uint32_t n, LDsCur& c) {
+  uint32_t d[8];
+  lean_window(in, a, d);
+  c.u = in + a;
+  c.lim = n < 32u ? n : 32u;
+  c.T = ~lean_hmask(d) & (c.lim >= 32u ? 0xFFFFFFFFu : ((1u << c.lim) - 1u));
+  c.p = 0; c.bad = 0; c.r_left = 0; c.client = 0;
+  c.cl_left = lean_ds_vu(c, 4u);
+}
+YDEV bool lean_ds_more(const LDsCur& c) { return c.bad == 0u && (c.r_left | c.cl_left) != 0u; }
+// next range (client, clock, len); clients with no ranges defer (they add no records, but
+// need a loop here); clocks and lengths below 2^28
+YDEV void lean_ds_next(LDsCur& c, uint32_t& client, uint32_t& clock, uint32_t& len) {
+  if (c.r_left == 0u) {
+    c.client = lean_ds_vu(c, 5u);
+    c.r_left = lean_ds_vu(c, 4u);
+    c.bad |= c.r_left == 0u ? 1u : 0u;
+    c.cl_left--;
+  }
+  client = c.client;
+  clock = lean_ds_vu(c, 4u);
+  len = lean_ds_vu(c, 4u);
+  c.r_left -= c.r_left ? 1u : 0u;
 }
 
 // Copies n (<= 31) bytes from staged input position s to output position t (both LDS) into a
@@ -248,6 +313,112 @@ YDEV uint32_t lds_vu(LB8* out, uint32_t t, uint32_t v) {
   while (v > 127u) { out[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; }
   out[t++] = (uint8_t)v;
   return t;
+}
+
+YDEV uint32_t vlen32(uint32_t v) {   // bytes of the varuint encoding of v
+  return 1u + (v > 0x7Fu ? 1u : 0u) + (v > 0x3FFFu ? 1u : 0u) + (v > 0x1FFFFFu ? 1u : 0u) + (v > 0xFFFFFFFu ? 1u : 0u);
+}
+YDEV uint64_t lean_max_scan64(uint64_t v) {   // inclusive prefix max over the wave
+  const uint32_t l = threadIdx.x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t t = __shfl_up(v, (unsigned)o, 64);
+    v = (l >= (uint32_t)o && t > v) ? t : v;
+  }
+  return v;
+}
+
+// The merged delete set of one document (mergeDeleteSets Y@10486 + sortAndMergeDeleteSet
+// Y@10246 + writeDeleteSet): lane i holds the i-th range of the union, sorted by (client
+// descending, clock); the caller emits it with lean_ds_emit after zeroing the output buffer.
+struct LDsUnion {
+  uint32_t client, nruns, sclock, rend;   // per lane: its client / runs of its client / its run
+  bool segstart, runend;
+  uint32_t pos;                           // lane's first byte, relative to the DS start
+  uint32_t nsegs, bytes;                  // uniform: clients, encoded DS bytes
+  bool bad;
+};
+// scratch: 16 * LN_DSMAX bytes of LDS (records, then the sorted records)
+YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS], const uint32_t (&uend)[LN_ROWS],
+                            const bool (&hasd)[LN_ROWS], uint32_t flags) {
+  const uint32_t l = threadIdx.x;
+  LDsUnion U; U.bad = false; U.nsegs = 0; U.bytes = 1; U.segstart = false; U.runend = false; U.pos = 0;
+  U.client = 0; U.nruns = 0; U.sclock = 0; U.rend = 0;
+  LB32* rc = scr; LB32* rk = scr + LN_DSMAX; LB32* re = scr + 2 * LN_DSMAX;
+  uint32_t nrec = 0, bad = 0;
+  // ---- records of every update's DS, in update order (the order only matters for ties, which
+  //      the union does not see)
+#pragma unroll
+  for (int q = 0; q < LN_ROWS; q++) {
+    if (__ballot(hasd[q]) == 0) continue;
+    LDsCur c;
+    if (hasd[q]) lean_ds_open(lin, dpos[q], uend[q] - dpos[q], c);
+    else { c.bad = 0; c.cl_left = 0; c.r_left = 0; }
+    for (int it = 0; it < LN_DSMAX; it++) {
+      bool has = lean_ds_more(c);
+      if (__ballot(has) == 0) break;
+      uint32_t cl = 0, ck = 0, ln = 0;
+      if (has) lean_ds_next(c, cl, ck, ln);
+      has = has && c.bad == 0u;
+      const uint64_t m = __ballot(has);
+      const uint32_t slot = nrec + lanes_below(m);
+      if (has && slot < (uint32_t)LN_DSMAX) { rc[slot] = cl; rk[slot] = ck; re[slot] = ck + ln; }
+      nrec += (uint32_t)__builtin_popcountll(m);
+    }
+    bad |= c.bad | (lean_ds_more(c) ? 1u : 0u);   // malformed, or more ranges than the loop takes
+  }
+  U.bad = __ballot(bad != 0u) != 0 || nrec > (uint32_t)LN_DSMAX || nrec == 0u;
+  if (U.bad) return U;
+  wave_sync();
+  // ---- rank sort by (client descending, clock ascending, record order)
+  const bool v = l < nrec;
+  const uint32_t cl = v ? rc[l] : 0u, ck = v ? rk[l] : 0u, en = v ? re[l] : 0u;
+  uint32_t rank = 0;
+  for (uint32_t j = 0; j < nrec; j++) {
+    const uint32_t cj = rdlane(cl, j), kj = rdlane(ck, j);
+    rank += (cj > cl || (cj == cl && (kj < ck || (kj == ck && j < l)))) ? 1u : 0u;
+  }
+  LB32* sc = scr + 3 * LN_DSMAX;   // sorted clients; clocks / ends reuse rk / re after the reads above
+  wave_sync();
+  if (v) { sc[rank] = cl; rk[rank] = ck; re[rank] = en; }
+  wave_sync();
+  const uint32_t c = v ? sc[l] : 0u, k = v ? rk[l] : 0u, e = v ? re[l] : 0u;
+  const uint32_t cprev = (v && l > 0u) ? sc[l - 1u] : 0u;
+  // ---- runs: a range starts a run when it is its client's first or starts past every end so far
+  const bool segstart = v && (l == 0u || cprev != c);
+  const uint32_t segidx = dpp_incl_add(segstart ? 1u : 0u);
+  const uint32_t nsegs = lane63(segidx);
+  const uint64_t incl = lean_max_scan64(v ? (((uint64_t)segidx << 32) | e) : 0ull);
+  const uint32_t prevmax = (uint32_t)__shfl_up(incl, 1u, 64);
+  const bool runstart = v && (segstart || k > prevmax);
+  const bool nxt_rs = __shfl_down(runstart ? 1 : 0, 1u, 64) != 0;
+  const bool runend = v && (l + 1u == nrec || nxt_rs);
+  const uint32_t sidx = (uint32_t)lean_max_scan64(runstart ? l : 0u);
+  const uint32_t sclock = (uint32_t)__shfl(k, (int)sidx, 64);
+  // runs per client: the inclusive run count at the client's last range, minus the count before its first
+  const uint32_t rsc = dpp_incl_add(runstart ? 1u : 0u);
+  // (shuffles run with every lane active: a bpermute from an inactive lane reads 0)
+  const bool nxt_ss = __shfl_down(segstart ? 1 : 0, 1u, 64) != 0;
+  const bool segend = v && (l + 1u == nrec || nxt_ss);
+  LB32* cnt = scr;                 // rc is free again
+  wave_sync();
+  if (segend) cnt[segidx - 1u] = rsc;
+  wave_sync();
+  const uint32_t nruns = segstart ? cnt[segidx - 1u] - rsc + 1u : 0u;
+  const uint32_t tb = (segstart ? vlen32(c) + vlen32(nruns) : 0u) + (runend ? vlen32(sclock) + vlen32((uint32_t)incl - sclock) : 0u);
+  const uint32_t ib = dpp_incl_add(tb);
+  U.client = c; U.nruns = nruns; U.sclock = sclock; U.rend = (uint32_t)incl;
+  U.segstart = segstart; U.runend = runend; U.pos = ib - tb;
+  U.nsegs = nsegs; U.bytes = vlen32(nsegs) + lane63(ib);
+  U.bad = (flags & 1u) && nsegs > 1u;   // yjs 13.5 writes clients in first-seen order: general path
+  return U;
+}
+// writes the delete set at t (the output buffer is zeroed)
+YDEV void lean_ds_emit(LB8* out, uint32_t t, const LDsUnion& U) {
+  if (threadIdx.x == 0) lds_vu(out, t, U.nsegs);
+  uint32_t o = t + vlen32(U.nsegs) + U.pos;
+  if (U.segstart) { o = lds_vu(out, o, U.client); o = lds_vu(out, o, U.nruns); }
+  if (U.runend) { o = lds_vu(out, o, U.sclock); lds_vu(out, o, U.rend - U.sclock); }
 }
 
 }  // namespace ygm

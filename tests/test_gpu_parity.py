@@ -227,13 +227,14 @@ def test_full_size_c2_properties(eng):
 
 
 def test_lean_kernel_takes_debounce_logs(eng):
-    # C2-shaped logs (1-4 clients, per-client clock order) are finished by the lean kernel;
-    # 5-8 clients, shuffled logs and delete-carrying logs are deferred -- all bit-exact.
+    # C2-shaped logs (1-4 clients, per-client clock order, with or without deletions) are
+    # finished by the lean kernel; 5-8 clients and shuffled logs are deferred -- all bit-exact.
     from tools import synth
     cases = [(dict(min_clients=1, max_clients=4), 0, False, True),
              (dict(min_clients=5, max_clients=8), 0, False, False),
              (dict(min_clients=1, max_clients=4), 0, True, None),
-             (dict(min_clients=1, max_clients=3), 15, False, None)]
+             (dict(min_clients=1, max_clients=3), 15, False, True),
+             (dict(min_clients=1, max_clients=4), 20, False, True)]
     for kw, del_pct, shuffle, all_lean in cases:
         arena, upd_off, doc_upd = synth.text_updates(300, 120, del_pct=del_pct, seed=77, **kw)
         ups = synth.split(arena, upd_off)
@@ -410,3 +411,74 @@ def test_lean_sv_diff_edge_states_vs_oracle(eng):
         assert same(oracle.diff_update(u, svs[d]), res[d]), (u.hex(), svs[d].hex())
     took = eng.stats().docs_lean - lean0
     assert 0 < took < 2 * len(states)
+
+
+def _lean_ds_docs(n_docs, seed):
+    """Debounce logs with deletions: struct updates (1-4 clients, clock-contiguous) mixed with
+    delete-set-only updates and struct updates carrying a delete set.  The delete sets probe
+    rule R-DS: several clients (in and outside the struct blocks), overlapping, adjacent,
+    duplicate and zero-length ranges, clients without ranges, > 64 ranges per document,
+    5-byte clients, clocks past 2^28, non-minimal varuints and truncated delete sets."""
+    from v1util import vu, encode_ds
+    rng = random.Random(seed)
+    docs = []
+    for _ in range(n_docs):
+        ncl = rng.choice([1, 1, 2, 3, 4])
+        clients = [rng.randrange(1, 2 ** 32) if rng.random() < 0.9 else rng.randrange(1, 100) for _ in range(ncl)]
+        others = [rng.randrange(1, 2 ** 32) for _ in range(rng.choice([0, 1, 2, 5]))]
+        clocks = [0] * ncl
+        big = rng.random() < 0.04
+        many = rng.random() < 0.04
+        ups = []
+        for _ in range(rng.randrange(2, 80)):
+            r = rng.random()
+            if r < 0.6 or not ups:
+                c = rng.randrange(ncl)
+                txt = "".join(rng.choice("xyz") for _ in range(rng.choice([1, 1, 2, 4])))
+                body = bytes([0x84]) + vu(clients[c]) + vu(max(clocks[c], 1) - 1) + vu(len(txt)) + txt.encode()
+                if clocks[c] == 0:
+                    body = bytes([4]) + b"\x01" + vu(1) + b"t" + vu(len(txt)) + txt.encode()
+                u = vu(1) + vu(1) + vu(clients[c]) + vu(clocks[c]) + body
+                clocks[c] += len(txt)
+                ds = [] if rng.random() < 0.85 else None
+            else:
+                u = b"\x00"
+                ds = None
+            if ds is None:   # a delete set
+                pool = clients + others
+                ds = []
+                for cl in rng.sample(pool, min(len(pool), rng.choice([1, 1, 1, 2, 3]))):
+                    rs = []
+                    for _r in range(rng.choice([1, 1, 2, 3] + ([12] if many else []))):
+                        ck = rng.randrange(2 ** 29, 2 ** 30) if big and rng.random() < 0.3 else rng.randrange(0, 60)
+                        ln = rng.choice([1, 1, 2, 5]) if rng.random() < 0.97 else 0
+                        rs.append((ck, ln))
+                    if rng.random() < 0.02:
+                        rs = []                                   # a client without ranges
+                    ds.append((cl, rs))
+            e = encode_ds(ds)
+            if rng.random() < 0.02 and len(e) > 2:
+                e = e[:-1] + bytes([e[-1] | 0x80, 0])              # non-minimal last varuint
+            if rng.random() < 0.001:
+                e = e[:-1]                                         # truncated: yjs throws
+            ups.append(u + e)
+        docs.append(ups)
+    return docs
+
+
+def test_lean_kernel_delete_sets_vs_oracle(eng):
+    docs = _lean_ds_docs(1500, seed=606)
+    lean0 = eng.stats().docs_lean
+    res = eng.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+    assert not bad, (len(bad), [u.hex() for u in docs[bad[0]]])
+    took = eng.stats().docs_lean - lean0
+    assert len(docs) // 10 < took < len(docs)   # both paths (updates > 32 bytes defer)
+
+
+def test_lean_kernel_delete_sets_compat135_vs_oracle(eng135):
+    # yjs 13.5 writes delete-set clients in first-seen order: single-client unions stay lean
+    docs = _lean_ds_docs(600, seed=607)
+    res = eng135.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us, compat135=True), res[d])]
+    assert not bad, (len(bad), [u.hex() for u in docs[bad[0]]])

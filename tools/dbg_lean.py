@@ -1,16 +1,17 @@
-import sys; sys.path.insert(0,'tests'); sys.path.insert(0,'.')
+"""Ad-hoc GPU check: a few merge inputs through the engine vs the oracle (hex dump)."""
+import sys; sys.path.insert(0, 'tests'); sys.path.insert(0, '.')
 from hocuspocus_amd import Engine
 import oracle
-u=bytes.fromhex('02038080010000020a038480800104010001858080800800000200'); sv=bytes.fromhex('028080010a858080800801')
-for compat in (False, True):
-    e=Engine(0, compat135=compat)
-    print('diff', compat, e.diff_update_batch([u],[sv]), oracle.diff_update(u, sv))
-    print('sv', e.encode_state_vector_from_update_batch([u]), oracle.encode_state_vector_from_update(u))
-    e.close()
-from tools import synth
-a,o,s,so=synth.text_states(4, seed=3)
-docs=synth.split(a,o); svs=synth.split(s,so)
-e=Engine(0)
-print(e.encode_state_vector_from_update_batch(docs)[:2])
-print(e.diff_update_batch(docs, svs)[0][0])
-print(docs[0][:60].hex())
+cases = [['000102010001', '000109010001'],
+         ['0001c8010219041604', '0000', '0000', '0002020216000b0401011601'],
+         ['0000', '0003020404030d030f021d05c801020b01090402011804', '000101010602'],
+         ['000102010001', '000102010101'],
+         ['01010500040101740568656c6c6f00', '000105010001'],
+         ['01010500040101740568656c6c6f00', '01010505840500016100', '000105010001']]
+e = Engine(0)
+for c in cases:
+    us = [bytes.fromhex(x) for x in c]
+    l0 = e.stats().docs_lean
+    g = e.merge_updates_batch([us])[0]
+    o = oracle.merge_updates(us)
+    print('OK ' if g == o else 'BAD', e.stats().docs_lean - l0, g[0], g[1].hex(), '| oracle', o[0], o[1].hex())

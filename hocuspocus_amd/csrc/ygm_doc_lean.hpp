@@ -66,9 +66,9 @@ YDEV VMask vmask(const uint32_t (&d)[8], uint64_t rem) {
   VMask m; m.H = 0; m.Z = 0;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    m.H |= hibits8(d[2 * j], d[2 * j + 1]) << (8 * j);
+    m.H |= top8(d[2 * j], d[2 * j + 1]) << (8 * j);
     const uint32_t z0 = (d[2 * j] - 0x01010101u) & ~d[2 * j], z1 = (d[2 * j + 1] - 0x01010101u) & ~d[2 * j + 1];
-    m.Z |= hibits8(z0, z1) << (8 * j);
+    m.Z |= top8(z0, z1) << (8 * j);
   }
   m.V = rem >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)rem) - 1u);
   m.T = ~m.H & m.V & 0x7FFFFFFFu;   // (byte 31 is never taken as a terminator: vend() == 31 means "not in the view")

@@ -1276,11 +1276,9 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
             // ---- emit into the LDS output buffer: structs (funnel copies), block headers, document header, delete set
 #pragma unroll
             for (int q = 0; q < LN_ROWS; q++) {
-              if (hs[q]) {
-                const uint32_t b = blk[q];
-                const uint32_t t = (b == 0 ? base[0] + hdr[0] : b == 1 ? base[1] + hdr[1] : b == 2 ? base[2] + hdr[2] : base[3] + hdr[3]) + inb[q];
-                lds_or_copy(lout, lin, t, rec[q].span >> 16, rec[q].span & 0xFFu);
-              }
+              const uint32_t b = blk[q];
+              const uint32_t t = (b == 0 ? base[0] + hdr[0] : b == 1 ? base[1] + hdr[1] : b == 2 ? base[2] + hdr[2] : base[3] + hdr[3]) + inb[q];
+              lean_copy(lout, lin, hs[q], t, rec[q].span >> 16, rec[q].span & 0xFFu);
             }
             if (l < nC) {
               const uint32_t bb = l;

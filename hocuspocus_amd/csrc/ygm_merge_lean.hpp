@@ -113,25 +113,26 @@ YDEV uint32_t pext32(uint32_t x, uint32_t y, uint32_t n) {
 // a ?: of array elements into a scratch-indexed load)
 YDEV uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); }
 
-// 32 bytes of staged input from position s as d[0..7] (d[j] = bytes 4j..4j+3): three aligned
-// ds_read_b128 normalised by selects and v_alignbyte (an unaligned b128 read replays)
+// 32 bytes of staged input from position s as d[0..7] (d[j] = bytes 4j..4j+3): nine
+// dword-aligned ds_read_b32 funnelled by v_alignbyte (no selects; an unaligned b128 read replays)
 YDEV void lean_window(LB8* in, uint32_t s, uint32_t (&d)[8]) {
-  const uint32_t a = s & ~15u, r = s & 15u;
-  const u32x4 c0 = *(const LB128*)(in + a), c1 = *(const LB128*)(in + a + 16), c2 = *(const LB128*)(in + a + 32);
-  const uint32_t w[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
-  // d[j] = (w[j + r/4 + 1] : w[j + r/4]) >> 8(r & 3)
-  const uint32_t m1 = 0u - ((r >> 2) & 1u), m2 = 0u - ((r >> 3) & 1u);
+  const LB32* w = (const LB32*)(in + (s & ~3u));
   uint32_t L[9];
 #pragma unroll
-  for (int j = 0; j < 9; j++) L[j] = bsel(m2, bsel(m1, w[j + 3], w[j + 2]), bsel(m1, w[j + 1], w[j]));
+  for (int j = 0; j < 9; j++) L[j] = w[j];
 #pragma unroll
-  for (int j = 0; j < 8; j++) d[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], r & 3u);
+  for (int j = 0; j < 8; j++) d[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], s & 3u);
+}
+// top bits of the 8 bytes (lo, hi) as bits 0..7: bytes masked to 0x00 / 0x80 times u8 weights
+YDEV uint32_t top8(uint32_t lo, uint32_t hi) {
+  const uint32_t a = __builtin_amdgcn_udot4(lo & 0x80808080u, 0x08040201u, 0u, false);
+  return __builtin_amdgcn_udot4(hi & 0x80808080u, 0x80402010u, a, false) >> 7;
 }
 // H = top-bit mask of the 32 window bytes
 YDEV uint32_t lean_hmask(const uint32_t (&d)[8]) {
   uint32_t H = 0;
 #pragma unroll
-  for (int j = 0; j < 4; j++) H |= hibits8(d[2 * j], d[2 * j + 1]) << (8 * j);
+  for (int j = 0; j < 4; j++) H |= top8(d[2 * j], d[2 * j + 1]) << (8 * j);
   return H;
 }
 
@@ -146,10 +147,7 @@ YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
   const uint32_t H = lean_hmask(d);
   uint32_t Z = 0;
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const uint32_t z0 = (d[2 * j] - 0x01010101u) & ~d[2 * j], z1 = (d[2 * j + 1] - 0x01010101u) & ~d[2 * j + 1];
-    Z |= hibits8(z0, z1) << (8 * j);
-  }
+  for (int j = 0; j < 4; j++) Z |= top8((d[2 * j] - 0x01010101u) & ~d[2 * j], (d[2 * j + 1] - 0x01010101u) & ~d[2 * j + 1]) << (8 * j);
   const uint32_t V = n >= 32u ? 0xFFFFFFFFu : ((1u << n) - 1u);
   const uint32_t T = ~H & V;                 // varuint terminators among the valid bytes
   const uint32_t HV = H & V;
@@ -285,29 +283,37 @@ YDEV void lean_ds_next(LDsCur& c, uint32_t& client, uint32_t& clock, uint32_t& l
   c.r_left -= c.r_left ? 1u : 0u;
 }
 
-// Copies n (<= 31) bytes from staged input position s to output position t (both LDS) into a
+// Copies n (4..31) bytes from staged input position s to output position t (both LDS) into a
 // ZEROED output buffer: every destination dword the range touches gets ds_or_b32 of the
 // funnel-shifted source bytes masked to the range.  Byte ranges of different lanes are
-// disjoint, so the ORs commute: no edge cases, no branches, no ordering between lanes.
-// Dwords past the range are OR-ed with 0 (the output buffer has slack for them).
+// disjoint, so the ORs commute: no edge cases, no ordering between lanes.  ND (wave-uniform)
+// bounds the destination dwords: head + n <= 4 ND (lean_copy picks 6 or 9).
+template <int ND>
 YDEV void lds_or_copy(LB8* out, LB8* in, uint32_t t, uint32_t s, uint32_t n) {
   const uint32_t head = t & 3u;
   const uint32_t src0 = s - head;                 // source byte that maps to destination byte t & ~3
   const uint32_t sb = src0 & 3u;
   LB32* sw = (LB32*)(in + (src0 & ~3u));
-  uint32_t w[10];
+  uint32_t w[ND + 1];
 #pragma unroll
-  for (int j = 0; j < 10; j++) w[j] = sw[j];      // may read past the update: the staged buffer has slack
+  for (int j = 0; j <= ND; j++) w[j] = sw[j];     // may read past the update: the staged buffer has slack
   LB32* od = (LB32*)(out + (t & ~3u));
   const uint32_t last = head + n;                 // destination bytes [head, last) of the dword run are ours
+  const uint32_t jl = (last - 1u) >> 2;           // last dword touched
+  const uint32_t mtail = 0xFFFFFFFFu >> (8u * (4u * jl + 4u - last));
 #pragma unroll
-  for (int j = 0; j < 9; j++) {                   // last <= 34: at most 9 dwords
+  for (int j = 0; j < ND; j++) {
     const uint32_t v = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sb);
-    const int a = (int)head - 4 * j, b = (int)last - 4 * j;
-    const uint32_t ca = a < 0 ? 0u : a > 4 ? 4u : (uint32_t)a, cb = b < 0 ? 0u : b > 4 ? 4u : (uint32_t)b;
-    const uint32_t m = (uint32_t)(((1ull << (8u * cb)) - 1ull) ^ ((1ull << (8u * ca)) - 1ull));
+    uint32_t m = (uint32_t)j < jl ? 0xFFFFFFFFu : (uint32_t)j == jl ? mtail : 0u;
+    if (j == 0) m &= 0xFFFFFFFFu << (8u * head);
     __hip_atomic_fetch_or(od + j, v & m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+}
+// one row of struct copies: 6 destination dwords when every lane's run fits (C2 structs are
+// <= 19 bytes), else 9
+YDEV void lean_copy(LB8* out, LB8* in, bool go, uint32_t t, uint32_t s, uint32_t n) {
+  if (__ballot(go && (t & 3u) + n > 24u) == 0) { if (go) lds_or_copy<6>(out, in, t, s, n); }
+  else if (go) lds_or_copy<9>(out, in, t, s, n);
 }
 YDEV uint32_t lds_vu(LB8* out, uint32_t t, uint32_t v) {
   while (v > 127u) { out[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; }

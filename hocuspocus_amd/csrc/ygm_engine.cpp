@@ -268,17 +268,20 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
         !c->s_ubase.ensure(upd_cap * 8) || !c->s_ulen.ensure(upd_cap * 4) || !c->s_cnt.ensure(byte_cap * 4) ||
         !c->s_drec.ensure((byte_cap / 2 + 1) * ygm_k_drec_bytes()))
       return YGM_ENOMEM;
+    HIPCHK(hipEventRecord(c->e0, s));
     if (ygm_k_launch_merge_seq(P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->out.as<uint8_t>(),
                                c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), P.meta,
                                c->s_readers.p, c->s_order.as<int>(), c->s_tmp.as<int>(), c->s_ubase.as<const uint8_t*>(),
                                c->s_ulen.as<uint32_t>(), upd_cap, c->s_cnt.as<uint32_t>(), c->s_drec.p, byte_cap, P.slot_total, P.out_cap, s))
       return YGM_EDEVICE;
+    HIPCHK(hipEventRecord(c->e1, s));
     if ((e = read_meta(c, s, m, P.meta))) return e;
+    if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
     c->stats.docs_seq += m.fb_count;
   }
   const uint64_t extent = P.slot_total + m.cursor;
   c->stats.calls++; c->stats.docs += P.n_docs; c->stats.updates += P.n_upd;
-  c->stats.docs_fast += P.n_docs - m.fb_count;
+  c->stats.docs_fast += m.lean_defer - m.fb_count;   // finished by the wave / workgroup tiers
   c->stats.docs_lean += P.n_docs - m.lean_defer;
   c->stats.bytes_in += P.arena_bytes; c->stats.bytes_out += m.payload_total();
   fill_dev_result(c, extent, out);
@@ -329,7 +332,7 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
     if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;
   }
   const uint64_t payload = m.payload_total() + m.fast_total;
-  c->stats.calls++; c->stats.docs += n_docs; c->stats.docs_fast += n_docs; c->stats.docs_lean += n_docs - m.lean_defer;
+  c->stats.calls++; c->stats.docs += n_docs; c->stats.docs_fast += m.lean_defer; c->stats.docs_lean += n_docs - m.lean_defer;
   c->stats.bytes_in += arena_bytes; c->stats.bytes_out += payload;
   fill_dev_result(c, slot_total + m.fast_total, out);
   out->payload_bytes = payload;

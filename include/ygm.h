@@ -70,9 +70,11 @@ typedef struct {
 typedef struct {
   uint64_t calls, docs, updates;
   uint64_t bytes_in, bytes_out;       /* algorithmic bytes */
-  uint64_t docs_fast, docs_seq;        /* documents per kernel class */
+  uint64_t docs_fast, docs_seq;        /* documents finished by the general tiers (merge: wave / workgroup kernels;
+                                          SV / diff: the exact per-document kernel) / by the sequential merge kernel */
   double kernel_ms, h2d_ms, d2h_ms;    /* cumulative, HIP-event timed */
-  uint64_t docs_lean;                  /* merges finished by the lean (debounce-log) kernel */
+  uint64_t docs_lean;                  /* documents finished by the lean kernels (merge: debounce-log kernel; SV / diff:
+                                          lane-per-document walker) */
   double lean_ms;                      /* HIP-event time of the lean kernel launches (part of kernel_ms): one span
                                           from the first launch after a finish to that finish */
   uint64_t lean_launches;              /* lean kernel launches timed in lean_ms */

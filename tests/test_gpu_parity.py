@@ -482,3 +482,21 @@ def test_lean_kernel_delete_sets_compat135_vs_oracle(eng135):
     res = eng135.merge_updates_batch(docs)
     bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us, compat135=True), res[d])]
     assert not bad, (len(bad), [u.hex() for u in docs[bad[0]]])
+
+
+@pytest.mark.parametrize("xml", [False, True])
+def test_large_documents_c3_c5_vs_oracle(eng, xml):
+    # SURVEY.md §8d C3 / C5 shapes at test size: Zipf-sized [snapshot, ...log] documents (GC,
+    # deleted content, merged delete sets, 40 % deletions in the log) and XmlFragment snapshots
+    # over thousands of client blocks -- the workgroup and sequential tiers, bit-exact
+    from tools import synth
+    if xml:
+        arena, upd_off, doc_upd = synth.big_docs(4, 400000, 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=4)
+    else:
+        arena, upd_off, doc_upd = synth.big_docs(60, 300000, 1024, max_clients=64, max_k=200, seed=3)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(len(doc_upd) - 1)]
+    res = eng.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+    assert not bad, (len(bad), bad[:5])
+    assert all(st == 0 for st, _ in res)

@@ -17,6 +17,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 
 typedef struct { uint64_t s; } Rng;
 static uint64_t rnext(Rng *r) { uint64_t x = r->s; x ^= x >> 12; x ^= x << 25; x ^= x >> 27; r->s = x; return x * 2685821657736338717ULL; }
@@ -152,5 +153,126 @@ size_t synth_text_states(uint64_t seed, uint32_t n_docs, uint32_t min_ops, uint3
   }
   doc_off[n_docs] = b; sv_off[n_docs] = s; *sv_bytes = s;
   free(doc); free(tmp); free(toff);
+  return b;
+}
+
+/* ---- configs C3 / C5: [snapshot, ...log] documents of a target size --------------------------
+ * The snapshot is one merged update: client blocks in descending client order, each a run of
+ * structs with contiguous clocks -- Item ContentString (ASCII and 2-byte UTF-8), ContentDeleted,
+ * GC, and with `xml` ContentType (XmlElement "paragraph" / XmlText), ContentFormat and
+ * ContentEmbed -- every Item after a block's first carrying an origin (and sometimes a right
+ * origin) on a random earlier id; then a sorted, merged delete set over the deleted runs.  The
+ * log holds k-1 updates: inserts continuing a client's clock (1-3 string structs) and
+ * delete-set-only updates over random existing ids.  Sizes follow size(r) = max_bytes * r^-0.8
+ * for the document of rank r = d + 1 (floored at min_bytes).
+ * buf capacity: sum of the sizes + n_docs * 64 KiB; upd_off: n_docs * 200 + 1; doc_upd: n_docs + 1. */
+typedef struct { uint32_t client, clock; } Id;
+static size_t w_str(uint8_t *o, const char *s, size_t n) { size_t b = vu(o, n); memcpy(o + b, s, n); return b + n; }
+size_t synth_big_docs(uint64_t seed, uint32_t n_docs, uint64_t max_bytes, uint64_t min_bytes, uint32_t max_clients,
+                      uint32_t max_k, int xml, uint8_t *buf, uint64_t *upd_off, uint32_t *doc_upd) {
+  Rng r = { seed * 0x9E3779B97F4A7C15ULL + 11 };
+  size_t b = 0; uint32_t nu = 0;
+  uint32_t *clients = (uint32_t *)malloc(sizeof(uint32_t) * max_clients);
+  uint32_t *ends = (uint32_t *)malloc(sizeof(uint32_t) * max_clients);
+  /* deleted runs of the snapshot, per client in clock order: (client index, clock, len) */
+  size_t dcap = 1 << 16, nd = 0;
+  uint32_t *dcl = (uint32_t *)malloc(sizeof(uint32_t) * dcap), *dck = (uint32_t *)malloc(sizeof(uint32_t) * dcap), *dln = (uint32_t *)malloc(sizeof(uint32_t) * dcap);
+  static const char *words[] = {"lorem", "ipsum", "dolor", "sit", "amet", "caf\xc3\xa9", "na\xc3\xafve", "x"};
+  for (uint32_t d = 0; d < n_docs; d++) {
+    doc_upd[d] = nu;
+    const double sz = (double)max_bytes * pow((double)(d + 1), -0.8);   /* size(r) = max * r^-0.8 */
+    uint64_t target = (uint64_t)sz; if (target < min_bytes) target = min_bytes;
+    uint32_t nc = 1 + (uint32_t)rbelow(&r, max_clients);
+    if (xml && max_clients > 64) nc = max_clients / 2 + (uint32_t)rbelow(&r, max_clients / 2 + 1);
+    pick_clients(&r, (int)nc, clients);
+    /* descending client order */
+    for (uint32_t i = 1; i < nc; i++) { uint32_t t = clients[i], j = i; while (j > 0 && clients[j - 1] < t) { clients[j] = clients[j - 1]; j--; } clients[j] = t; }
+    /* per-client struct budget */
+    uint64_t per = target / nc + 1;
+    upd_off[nu++] = b;
+    b += vu(buf + b, nc);
+    nd = 0;
+    for (uint32_t c = 0; c < nc; c++) {
+      /* count structs first into a temp region: write block body after a header placeholder */
+      const size_t bstart = b; b += 16;         /* header slot: the body is moved up behind the real header */
+      const size_t body0 = b;
+      uint32_t clock = 0, nst = 0; int last_gc = 0;
+      while ((uint64_t)(b - body0) < per || nst == 0) {
+        const uint32_t kind = (uint32_t)rbelow(&r, 100);
+        if (nst > 0 && kind < 6 && !last_gc) {           /* GC run (never two in a row) */
+          const uint32_t ln = 1 + (uint32_t)rbelow(&r, 20);
+          buf[b++] = 0; b += vu(buf + b, ln); clock += ln; nst++; last_gc = 1; continue;
+        }
+        last_gc = 0;
+        uint8_t info; int has_o = nst > 0, has_r = nst > 0 && rbelow(&r, 3) == 0;
+        uint32_t ref;
+        if (kind < 26) ref = 1;                          /* ContentDeleted */
+        else if (xml && kind < 34) ref = 7;              /* ContentType */
+        else if (xml && kind < 44) ref = 6;              /* ContentFormat */
+        else if (xml && kind < 47) ref = 5;              /* ContentEmbed */
+        else ref = 4;                                    /* ContentString */
+        info = (uint8_t)(ref | (has_o ? 0x80 : 0) | (has_r ? 0x40 : 0));
+        buf[b++] = info;
+        if (has_o) { const uint32_t oc = (uint32_t)rbelow(&r, c + 1); b += vu(buf + b, clients[oc]); b += vu(buf + b, oc == c ? clock - 1 : (uint32_t)rbelow(&r, 50)); }
+        if (has_r) { const uint32_t oc = (uint32_t)rbelow(&r, nc); b += vu(buf + b, clients[oc]); b += vu(buf + b, (uint32_t)rbelow(&r, 50)); }
+        if (!has_o && !has_r) { buf[b++] = 1; b += w_str(buf + b, xml ? "prosemirror" : "t", xml ? 11 : 1); }
+        uint32_t len = 1;
+        if (ref == 1) { len = 1 + (uint32_t)rbelow(&r, 30); b += vu(buf + b, len);
+          if (nd == dcap) { dcap *= 2; dcl = realloc(dcl, 4 * dcap); dck = realloc(dck, 4 * dcap); dln = realloc(dln, 4 * dcap); }
+          dcl[nd] = c; dck[nd] = clock; dln[nd] = len; nd++; }
+        else if (ref == 7) { const int el = rbelow(&r, 2) == 0; b += vu(buf + b, el ? 3 : 6); if (el) b += w_str(buf + b, "paragraph", 9); }
+        else if (ref == 6) { const uint32_t f = (uint32_t)rbelow(&r, 3);
+          if (f == 0) { b += w_str(buf + b, "bold", 4); b += w_str(buf + b, "true", 4); }
+          else if (f == 1) { b += w_str(buf + b, "italic", 6); b += w_str(buf + b, "1.5", 3); }
+          else { b += w_str(buf + b, "link", 4); b += w_str(buf + b, "{\"href\":\"https://x.y/z\"}", 24); } }
+        else if (ref == 5) { b += w_str(buf + b, "{\"image\":\"a.png\"}", 17); }
+        else { char s[256]; size_t sl = 0; uint32_t units = 0; const uint32_t nw = 1 + (uint32_t)rbelow(&r, 8);
+          for (uint32_t w = 0; w < nw; w++) { const char *t = words[rbelow(&r, 8)]; size_t tl = strlen(t);
+            memcpy(s + sl, t, tl); sl += tl; s[sl++] = ' ';
+            for (size_t q = 0; q < tl; q++) units += (t[q] & 0xC0) != 0x80;   /* UTF-16 units (all BMP) */
+            units++; }
+          len = units; b += w_str(buf + b, s, sl); }
+        clock += len; nst++;
+      }
+      ends[c] = clock;
+      /* header: nst, client, clock 0 -- written in front of the body (shift the body left) */
+      uint8_t h[16]; size_t hl = 0; hl += vu(h + hl, nst); hl += vu(h + hl, clients[c]); h[hl++] = 0;
+      memmove(buf + bstart + hl, buf + body0, b - body0);
+      memcpy(buf + bstart, h, hl);
+      b = bstart + hl + (b - body0);
+    }
+    /* delete set of the snapshot: clients descending (the block order), runs merged */
+    { uint32_t ncl = 0; for (size_t i = 0; i < nd; i++) if (i == 0 || dcl[i] != dcl[i - 1]) ncl++;
+      b += vu(buf + b, ncl);
+      size_t i = 0;
+      while (i < nd) { size_t j = i; while (j < nd && dcl[j] == dcl[i]) j++;
+        /* runs: merge adjacent */
+        uint32_t nr = 0; for (size_t q = i; q < j; q++) if (q == i || dck[q] != dck[q - 1] + dln[q - 1]) nr++;
+        b += vu(buf + b, clients[dcl[i]]); b += vu(buf + b, nr);
+        size_t q = i; while (q < j) { uint32_t s0 = dck[q], e0 = dck[q] + dln[q]; q++; while (q < j && dck[q] == e0) { e0 += dln[q]; q++; } b += vu(buf + b, s0); b += vu(buf + b, e0 - s0); }
+        i = j; } }
+    /* the log */
+    const uint32_t k = 2 + (uint32_t)rbelow(&r, max_k - 1);
+    for (uint32_t u = 1; u < k; u++) {
+      upd_off[nu++] = b;
+      if (rbelow(&r, 100) < 40) {                         /* deletion: DS only */
+        buf[b++] = 0;
+        const uint32_t c = (uint32_t)rbelow(&r, nc);
+        const uint32_t nr = 1 + (uint32_t)rbelow(&r, 3);
+        buf[b++] = 1; b += vu(buf + b, clients[c]); b += vu(buf + b, nr);
+        for (uint32_t q = 0; q < nr; q++) { b += vu(buf + b, (uint32_t)rbelow(&r, ends[c] + 1)); b += vu(buf + b, 1 + (uint32_t)rbelow(&r, 4)); }
+      } else {                                            /* insert: 1-3 strings continuing a client */
+        const uint32_t c = (uint32_t)rbelow(&r, nc), ns = 1 + (uint32_t)rbelow(&r, 3);
+        buf[b++] = 1; b += vu(buf + b, ns); b += vu(buf + b, clients[c]); b += vu(buf + b, ends[c]);
+        for (uint32_t s = 0; s < ns; s++) {
+          buf[b++] = 0x84; b += vu(buf + b, clients[c]); b += vu(buf + b, ends[c] > 0 ? ends[c] - 1 : 0);
+          const char ch = (char)('a' + rbelow(&r, 26)); b += w_str(buf + b, &ch, 1); ends[c]++;
+        }
+        buf[b++] = 0;
+      }
+    }
+  }
+  doc_upd[n_docs] = nu; upd_off[nu] = b;
+  free(clients); free(ends); free(dcl); free(dck); free(dln);
   return b;
 }

@@ -26,6 +26,9 @@ def lib():
         L.synth_text_states.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                         P, P, P, P, ctypes.POINTER(ctypes.c_size_t)]
         L.synth_text_states.restype = ctypes.c_size_t
+        L.synth_big_docs.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                     ctypes.c_uint32, ctypes.c_int, P, P, P]
+        L.synth_big_docs.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -51,6 +54,23 @@ def text_states(n_docs, min_ops=40, max_ops=400, min_clients=1, max_clients=16, 
     n = lib().synth_text_states(seed, n_docs, min_ops, max_ops, min_clients, max_clients, buf.ctypes.data, doc_off.ctypes.data,
                                 sv.ctypes.data, sv_off.ctypes.data, ctypes.byref(svb))
     return buf[:n].copy(), doc_off, sv[:svb.value].copy(), sv_off
+
+
+def big_docs(n_docs, max_bytes, min_bytes=1024, max_clients=64, max_k=200, xml=False, seed=1):
+    """Configs C3 / C5: [snapshot, ...log] per document, snapshot of max_bytes * rank^-0.8 bytes
+    (C3: GC / deleted content / strings, a merged delete set, 40 % deletions in the log; C5 with
+    xml=True and max_clients=10000: XmlElement / XmlText / ContentFormat / ContentEmbed runs over
+    thousands of client blocks).  Returns (arena, upd_off[n_upd+1], doc_upd[n_docs+1])."""
+    sizes = np.maximum(max_bytes * np.arange(1, n_docs + 1, dtype=np.float64) ** -0.8, min_bytes)
+    cap = int(sizes.sum() * 1.6) + n_docs * (max_clients * 512 + max_k * 64 + 4096)
+    buf = np.empty(cap, dtype=np.uint8)
+    upd_off = np.empty(n_docs * max_k + 1, dtype=np.uint64)
+    doc_upd = np.empty(n_docs + 1, dtype=np.uint32)
+    n = lib().synth_big_docs(seed, n_docs, int(max_bytes), int(min_bytes), max_clients, max_k, 1 if xml else 0,
+                             buf.ctypes.data, upd_off.ctypes.data, doc_upd.ctypes.data)
+    assert n <= cap
+    nu = int(doc_upd[n_docs])
+    return buf[:n].copy(), upd_off[:nu + 1].copy(), doc_upd
 
 
 def split(arena, off):

@@ -37,14 +37,19 @@ int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const 
                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
                            void* readers, int* order, int* tmp, const uint8_t** ubase, uint32_t* ulen, uint64_t upd_cap,
                            uint32_t* cnt, void* drec, uint64_t byte_cap, uint64_t slot_total, uint64_t out_cap, hipStream_t s);
+size_t ygm_k_big_blk_bytes();
+int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
+                           uint32_t n_fb, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
+                           void* meta, uint32_t* fb2_list, void* blk, uint64_t blk_cap, uint64_t slot_total, uint64_t out_cap,
+                           hipStream_t s);
 }
 
 namespace {
 
 // mirrors ygm::DocMeta (ygm_kernels.hip); sizeof is a multiple of 16
 struct Meta {
-  unsigned int ticket, fault, fb_count, defer_count, lean_defer, pad[3];
-  unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor, pad2;
+  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer, pad[2];
+  unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor, big_cursor;
   unsigned long long payload_sh[16 * 16];
   unsigned long long payload_total() const {
     unsigned long long t = payload;
@@ -84,6 +89,7 @@ struct ygm_ctx {
   int mslot = 0;           // counter slot of the next merge launch
   void* meta_slot(int i) const { return (uint8_t*)meta.p + (size_t)i * sizeof(Meta); }
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
+  DevBuf big_blk, big_list;   // large-document tier: U0 block tables, documents sent on to the sequential kernel
   // host results
   std::vector<uint8_t> h_data;
   std::vector<uint64_t> h_off, h_len;
@@ -151,7 +157,7 @@ void ygm_close(ygm_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
-                    &c->s_drec})
+                    &c->s_drec, &c->big_blk, &c->big_list})
     b->release();
   for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
   if (c->h_meta) (void)hipHostFree(c->h_meta);
@@ -262,14 +268,30 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
     if (m.fault) return YGM_EDEVICE;
     if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
   }
-  if (m.fb_count) {  // tier 4: the exact sequential replay (scratch sized from the counters)
+  uint32_t n_seq = 0;
+  if (m.fb_count) {  // tier 4: large [snapshot, ...log] documents, one wave each; the rest go on to tier 5
+    const uint64_t blk_cap = m.fb_bytes / 4 + 2ull * m.fb_count + 16;
+    if (!c->big_blk.ensure(blk_cap * ygm_k_big_blk_bytes()) || !c->big_list.ensure((size_t)m.fb_count * 4 + 4)) return YGM_ENOMEM;
+    HIPCHK(hipEventRecord(c->e0, s));
+    if (ygm_k_launch_merge_big(P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->out.as<uint8_t>(),
+                               c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), P.meta,
+                               c->big_list.as<uint32_t>(), c->big_blk.p, blk_cap, P.slot_total, P.out_cap, s))
+      return YGM_EDEVICE;
+    HIPCHK(hipEventRecord(c->e1, s));
+    if ((e = read_meta(c, s, m, P.meta))) return e;
+    if (m.fault) return YGM_EDEVICE;
+    if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
+    c->stats.docs_big += m.fb_count - m.big_defer;
+    n_seq = m.big_defer;
+  }
+  if (n_seq) {  // tier 5: the exact sequential replay (scratch sized from the tier-4 counters: an upper bound)
     const uint64_t upd_cap = m.fb_upds + 1, byte_cap = m.fb_bytes + 8ull * m.fb_count + 8;
     if (!c->s_readers.ensure(upd_cap * ygm_k_seq_reader_bytes()) || !c->s_order.ensure(upd_cap * 4) || !c->s_tmp.ensure(upd_cap * 4) ||
         !c->s_ubase.ensure(upd_cap * 8) || !c->s_ulen.ensure(upd_cap * 4) || !c->s_cnt.ensure(byte_cap * 4) ||
         !c->s_drec.ensure((byte_cap / 2 + 1) * ygm_k_drec_bytes()))
       return YGM_ENOMEM;
     HIPCHK(hipEventRecord(c->e0, s));
-    if (ygm_k_launch_merge_seq(P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->out.as<uint8_t>(),
+    if (ygm_k_launch_merge_seq(P.arena, P.upd_off, P.doc_upd, c->big_list.as<uint32_t>(), n_seq, c->flags, c->out.as<uint8_t>(),
                                c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), P.meta,
                                c->s_readers.p, c->s_order.as<int>(), c->s_tmp.as<int>(), c->s_ubase.as<const uint8_t*>(),
                                c->s_ulen.as<uint32_t>(), upd_cap, c->s_cnt.as<uint32_t>(), c->s_drec.p, byte_cap, P.slot_total, P.out_cap, s))
@@ -277,11 +299,11 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
     HIPCHK(hipEventRecord(c->e1, s));
     if ((e = read_meta(c, s, m, P.meta))) return e;
     if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
-    c->stats.docs_seq += m.fb_count;
+    c->stats.docs_seq += n_seq;
   }
   const uint64_t extent = P.slot_total + m.cursor;
   c->stats.calls++; c->stats.docs += P.n_docs; c->stats.updates += P.n_upd;
-  c->stats.docs_fast += m.lean_defer - m.fb_count;   // finished by the wave / workgroup tiers
+  c->stats.docs_fast += m.lean_defer - m.fb_count;   // finished by the wave / workgroup tiers (tier 4 counted above)
   c->stats.docs_lean += P.n_docs - m.lean_defer;
   c->stats.bytes_in += P.arena_bytes; c->stats.bytes_out += m.payload_total();
   fill_dev_result(c, extent, out);

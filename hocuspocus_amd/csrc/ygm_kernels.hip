@@ -23,6 +23,7 @@
 #include "ygm_merge_wave.hpp"
 #include "ygm_merge_lean.hpp"
 #include "ygm_doc_lean.hpp"
+#include "ygm_merge_big.hpp"
 #include "ygm_seqdoc.hpp"
 #include "ygm_v1.hpp"
 
@@ -57,7 +58,8 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned int fb_count;            // documents sent to the sequential kernel
   unsigned int defer_count;         // documents sent from the wave kernel to the workgroup kernel
   unsigned int lean_defer;          // documents sent from the lean kernel to the wave kernel
-  unsigned int pad[3];
+  unsigned int big_defer;           // documents sent from the large-document kernel to the sequential kernel
+  unsigned int pad[2];
   unsigned long long fast_total;    // SV/diff: bytes of the packed (look-back placed) output
   unsigned long long cursor;        // merge: bytes in the overflow region (after the per-document slots)
   unsigned long long payload;       // merge: sum of output lengths (algorithmic output bytes)
@@ -65,7 +67,8 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned long long fb_bytes;
   unsigned long long scr_upd_cursor;
   unsigned long long scr_byte_cursor;
-  unsigned long long pad2;            // (16-byte multiple: the lean kernel zeroes slots in 16-byte pieces)
+  unsigned long long big_cursor;      // large-document kernel: block-table entries carved (16-byte multiple:
+                                      // the lean kernel zeroes slots in 16-byte pieces)
   unsigned long long payload_sh[16 * 16]; // merge: output lengths summed in 16 shards, one 128-B line each (no hot atomic line)
 };
 YDEV void add_payload(DocMeta* m, uint32_t d, uint64_t n) { atomicAdd(&m->payload_sh[(d & 15u) * 16u], (unsigned long long)n); }
@@ -1314,6 +1317,250 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
   if (l == 0 && payload) add_payload(meta, blockIdx.x, payload);
 }
 
+// ======================================================================= merge: large documents
+// One wave per document the workgroup tier sent on (ygm_merge_big.hpp); documents outside its class
+// go on to the sequential kernel through fb2_list.
+template <class T>
+YDEV void big_bitonic(T* a, uint32_t n) {   // ascending by key; n <= 1024 (entries [n, pow2) padded)
+  uint32_t P = 1;
+  while (P < n) P <<= 1;
+  for (uint32_t i = n + threadIdx.x; i < P; i += WAVE) a[i].key = ~0ull;
+  wave_sync();
+  for (uint32_t k = 2; k <= P; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < P; i += WAVE) {
+        const uint32_t x = i ^ j;
+        if (x > i) {
+          const T A = a[i], B = a[x];
+          if ((A.key > B.key) == ((i & k) == 0)) { a[i] = B; a[x] = A; }
+        }
+      }
+      wave_sync();
+    }
+}
+YDEV void big_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {   // the wave copies n bytes, 16 per lane-step
+  for (uint64_t c = 16ull * threadIdx.x; c < n; c += 16ull * WAVE) {
+    if (c + 16 <= n) { uint4 v; __builtin_memcpy(&v, src + c, 16); __builtin_memcpy(dst + c, &v, 16); }
+    else for (uint64_t q = c; q < n; q++) dst[q] = src[q];
+  }
+}
+// output sink: pass 0 counts, pass 1 stores (lane 0 writes literals; copies are wave-wide)
+struct BigOut {
+  uint8_t* o; uint64_t n; bool w;
+  YDEV void b(uint32_t v) { if (w && threadIdx.x == 0) o[n] = (uint8_t)v; n++; }
+  YDEV void vu(uint64_t v) { while (v > 127) { b(0x80u | (uint32_t)(v & 127)); v >>= 7; } b((uint32_t)v); }
+  YDEV void copy(const uint8_t* s, uint64_t len) { if (w) big_copy(o + n, s, len); n += len; }
+};
+// U0's delete set as a stream of ranges (every lane walks it redundantly: same bytes, same state)
+struct BigDs {
+  GCur c; uint64_t cl_left, r_left, client; bool has; uint64_t key, len;
+  YDEV void next() {
+    has = false;
+    while (r_left == 0 && cl_left > 0 && !c.err) { client = c.vu(); r_left = c.vu(); cl_left--; }
+    if (r_left == 0 || c.err) return;
+    const uint64_t ck = c.vu(); len = c.vu(); r_left--;
+    key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | ck;
+    has = !c.err;
+  }
+};
+
+__global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+                                                    const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
+                                                    uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
+                                                    uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
+                                                    uint32_t* __restrict__ fb2_list, BigBlk* __restrict__ blk, uint64_t blk_cap,
+                                                    uint64_t slot_total, uint64_t out_cap) {
+  __shared__ BigLds L;
+  __shared__ unsigned long long s_pick;
+  __shared__ uint64_t s_base, s_nb, s_ds0, s_at;
+  const uint32_t l = threadIdx.x;
+  const uint32_t d = fb_list[blockIdx.x];
+  const uint32_t ua = doc_upd[d], k = doc_upd[d + 1] - ua;
+  if (l == 0) { L.npc = 0; L.nrg = 0; L.bad = (flags & 2u) ? 1u : 0u; s_pick = 0; }   // YGM_F_FORCE_SEQ: all to the sequential kernel
+  wave_sync();
+  // ---- the snapshot U0: the largest update (the first of equal ones)
+  for (uint32_t i = l; i < k; i += WAVE) {
+    const uint64_t n = upd_off[ua + i + 1] - upd_off[ua + i];
+    if (n >= 0xFFFFFFFFull) L.bad = 1;
+    atomicMax(&s_pick, ((unsigned long long)(n < 0xFFFFFFFFull ? n : 0xFFFFFFFFull) << 32) | (0xFFFFFFFFu - i));
+  }
+  wave_sync();
+  const uint32_t U0 = 0xFFFFFFFFu - (uint32_t)s_pick;
+  // ---- log updates, lanes in parallel: every struct a piece, every delete range a record
+  for (uint32_t i = l; i < k; i += WAVE) {
+    if (i == U0) continue;
+    const uint64_t a = upd_off[ua + i];
+    GCur c; c.init(arena + a, (uint32_t)(upd_off[ua + i + 1] - a));
+    bool bad = false;
+    const uint64_t nb = c.vu();
+    uint64_t prevc = ~0ull;
+    for (uint64_t b = 0; b < nb && !c.err && !bad; b++) {
+      const uint64_t nst = c.vu(), client = c.vu();
+      uint64_t clock = c.vu();
+      // blocks in descending client order in every input (otherwise yjs's writer can revisit a client)
+      bad |= client > 0xFFFFFFFFull || client >= prevc;
+      prevc = client;
+      for (uint64_t q = 0; q < nst && !c.err && !bad; q++) {
+        const uint32_t b0 = c.pos;
+        const GStruct g = big_struct(c, flags);
+        bad |= !g.ok || g.len == 0 || clock + g.len > 0xFFFFFFFFull;
+        if (bad) break;
+        const uint32_t slot = atomicAdd(&L.npc, 1u);
+        if (slot < (uint32_t)LB_MAXS) {
+          BigPiece& P = L.pc[slot];
+          P.key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | clock;
+          P.len = (uint32_t)g.len; P.upd = i; P.b0 = b0; P.b1 = c.pos; P.gc = g.kind == 0;
+        }
+        clock += g.len;
+      }
+    }
+    const uint64_t nc = c.vu();
+    for (uint64_t q = 0; q < nc && !c.err && !bad; q++) {
+      const uint64_t client = c.vu(), nr = c.vu();
+      for (uint64_t r = 0; r < nr && !c.err && !bad; r++) {
+        const uint64_t ck = c.vu(), ln = c.vu();
+        bad |= client > 0xFFFFFFFFull || ck + ln > 0xFFFFFFFFull;
+        if (bad) break;
+        const uint32_t slot = atomicAdd(&L.nrg, 1u);
+        if (slot < (uint32_t)LB_MAXD) { L.rg[slot].key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | ck; L.rg[slot].len = (uint32_t)ln; }
+      }
+    }
+    if (bad || c.err) L.bad = 1;
+  }
+  // ---- U0 (lane 0): block table + delete-set order check
+  const uint8_t* u0p = arena + upd_off[ua + U0];
+  const uint32_t n0 = (uint32_t)(upd_off[ua + U0 + 1] - upd_off[ua + U0]);
+  if (l == 0 && !L.bad) {
+    GCur c; c.init(u0p, n0);
+    bool bad = false;
+    const uint64_t nb = c.vu();
+    const uint64_t base = atomicAdd(&meta->big_cursor, (unsigned long long)nb);
+    bad |= c.err || nb > n0 / 4u + 1u || base + nb > blk_cap;
+    uint64_t prevc = ~0ull;
+    for (uint64_t b = 0; b < nb && !bad; b++) {
+      BigBlk B;
+      B.nst = (uint32_t)c.vu(); B.client = c.vu(); B.clock0 = c.vu();
+      bad |= c.err || B.nst == 0 || B.client >= prevc || B.client > 0xFFFFFFFFull;
+      prevc = B.client;
+      B.b0 = c.pos;
+      uint64_t clk = B.clock0;
+      B.first_gc = 0; B.last_gc = 0;
+      for (uint32_t q = 0; q < B.nst && !bad; q++) {
+        const GStruct g = big_struct(c, flags);
+        bad |= !g.ok || g.len == 0;
+        if (q == 0) B.first_gc = g.kind == 0;
+        B.last_gc = g.kind == 0;
+        clk += g.len;
+      }
+      bad |= clk > 0xFFFFFFFFull;
+      B.clock1 = clk; B.b1 = c.pos;
+      if (!bad) blk[base + b] = B;
+    }
+    s_ds0 = c.pos;
+    // U0's delete set must already be in union order (client descending, clock ascending)
+    BigDs D; D.c = c; D.cl_left = D.c.vu(); D.r_left = 0; D.client = 0;
+    uint64_t prev = 0;
+    for (D.next(); D.has && !bad; D.next()) { bad |= D.key < prev || D.client > 0xFFFFFFFFull || D.key + D.len > ((D.key >> 32) << 32) + 0xFFFFFFFFull; prev = D.key; }
+    bad |= D.c.err != 0;
+    s_base = base; s_nb = nb;
+    if (bad) L.bad = 1;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // lane 0's block table (global) before every lane reads it
+  wave_sync();
+  const uint32_t npc = L.npc, nrg = L.nrg;
+  bool bad = L.bad || npc > (uint32_t)LB_MAXS || nrg > (uint32_t)LB_MAXD;
+  if (!bad) { big_bitonic(L.pc, npc); big_bitonic(L.rg, nrg); }
+  const BigBlk* T = blk + s_base;
+  const uint64_t nb = bad ? 0 : s_nb;
+  // ---- emit: pass 0 sizes (and proves the class), pass 1 bytes.  Every lane runs the same plan.
+  uint64_t nblocks = 0, ndsc = 0, size = 0;
+  for (int pass = 0; pass < 2 && !bad; pass++) {
+    BigOut o; o.o = out + (pass ? s_at : 0); o.n = 0; o.w = pass == 1;
+    o.vu(nblocks);
+    uint64_t i = 0, nbo = 0;
+    uint32_t j = 0;
+    while ((i < nb || j < npc) && !bad) {
+      const uint64_t cu = i < nb ? T[i].client : 0, cp = j < npc ? 0xFFFFFFFFull - (L.pc[j].key >> 32) : 0;
+      const bool hu = i < nb && (j >= npc || cu >= cp);
+      const uint64_t X = hu ? cu : cp;
+      BigBlk B; if (hu) B = T[i];
+      uint32_t j1 = j;
+      while (j1 < npc && 0xFFFFFFFFull - (L.pc[j1].key >> 32) == X) j1++;
+      // items in clock order: the U0 block slots in before the first piece at or after its clock
+      for (int sweep = 0; sweep < 2 && !bad; sweep++) {
+        uint64_t cnt = 0, first = 0, pend = 0; bool any = false, pgc = false, upend = hu;
+        uint32_t q = j;
+        while (upend || q < j1) {
+          const bool takeu = upend && (q >= j1 || B.clock0 <= (uint32_t)L.pc[q].key);
+          const uint64_t c0 = takeu ? B.clock0 : (uint32_t)L.pc[q].key;
+          const uint64_t c1 = takeu ? B.clock1 : c0 + L.pc[q].len;
+          const bool fgc = takeu ? B.first_gc : L.pc[q].gc, lgc = takeu ? B.last_gc : L.pc[q].gc;
+          if (any) {
+            if (c0 < pend || (c0 == pend && pgc && fgc)) { bad = true; break; }   // overlap / GC junction
+            if (c0 > pend) { cnt++; if (sweep) { o.b(10); o.vu(c0 - pend); } }   // Skip over the gap
+          } else first = c0;
+          if (sweep) {
+            if (takeu) o.copy(u0p + B.b0, B.b1 - B.b0);
+            else o.copy(arena + upd_off[ua + L.pc[q].upd] + L.pc[q].b0, L.pc[q].b1 - L.pc[q].b0);
+          }
+          cnt += takeu ? B.nst : 1u;
+          any = true; pend = c1; pgc = lgc;
+          if (takeu) upend = false; else q++;
+        }
+        if (sweep == 0 && !bad) { o.vu(cnt); o.vu(X); o.vu(first); }
+      }
+      nbo++;
+      if (hu) i++;
+      j = j1;
+    }
+    // delete set: U0's sorted stream merged with the sorted log ranges, runs merged per client
+    BigDs D; D.c.init(u0p, n0); D.c.pos = (uint32_t)s_ds0; D.cl_left = D.c.vu(); D.r_left = 0; D.client = 0; D.next();
+    uint32_t r = 0;
+    uint64_t nc = 0;
+    o.vu(ndsc);
+    while ((D.has || r < nrg) && !bad) {
+      const uint64_t kx = (D.has && (r >= nrg || D.key <= L.rg[r].key)) ? D.key : L.rg[r].key;
+      const uint64_t hi = kx >> 32;
+      const BigDs D0 = D; const uint32_t r0 = r;
+      uint64_t runs = 0;
+      for (int sweep = 0; sweep < 2; sweep++) {
+        D = D0; r = r0;
+        if (sweep) { o.vu(0xFFFFFFFFull - hi); o.vu(runs); }
+        uint64_t rs = 0, re = 0; bool open = false;
+        for (;;) {
+          const bool du = D.has && (D.key >> 32) == hi, dl = r < nrg && (L.rg[r].key >> 32) == hi;
+          if (!du && !dl) break;
+          const bool tu = du && (!dl || D.key <= L.rg[r].key);
+          const uint64_t ck = (uint32_t)(tu ? D.key : L.rg[r].key), ln = tu ? D.len : L.rg[r].len;
+          if (open && ck <= re) { if (ck + ln > re) re = ck + ln; }
+          else { if (open) { if (sweep) { o.vu(rs); o.vu(re - rs); } else runs++; } rs = ck; re = ck + ln; open = true; }
+          if (tu) D.next(); else r++;
+        }
+        if (open) { if (sweep) { o.vu(rs); o.vu(re - rs); } else runs++; }
+      }
+      nc++;
+    }
+    bad |= D.c.err != 0;
+    if (pass == 0) {
+      nblocks = nbo; ndsc = nc; size = o.n;
+      bad |= ((flags & 1u) && nc > 1) ;                       // yjs 13.5: first-seen client order -> general path
+      // the header varuints were sized with 0: resize with the real counts
+      size += vu_len(nblocks) - 1 + vu_len(ndsc) - 1;
+      if (!bad && l == 0) {
+        const uint64_t at = merge_place(upd_off, doc_upd, d, size, slot_total, meta);
+        s_at = at;
+        if (at + size > out_cap) L.bad = 1;
+      }
+      wave_sync();
+      bad |= L.bad != 0;
+    }
+  }
+  if (l == 0) {
+    if (bad) { status[d] = ST_FALLBACK; fb2_list[atomicAdd(&meta->big_defer, 1u)] = d; }
+    else { out_off[d] = s_at; out_len[d] = size; status[d] = ST_OK; add_payload(meta, d, size); }
+  }
+}
+
 // ======================================================================= merge sequential
 // One lane per fallback document.  Scratch (readers, sort arrays, block
 // counts, delete-set records) is carved with atomic cursors.
@@ -1400,6 +1647,16 @@ int ygm_diag_read(unsigned long long* out, int reset) {
 }
 #endif
 
+size_t ygm_k_big_blk_bytes() { return sizeof(BigBlk); }
+int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
+                           uint32_t n_fb, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
+                           void* meta, uint32_t* fb2_list, void* blk, uint64_t blk_cap, uint64_t slot_total, uint64_t out_cap,
+                           hipStream_t s) {
+  if (n_fb == 0) return 0;
+  hipLaunchKernelGGL(k_merge_big, dim3(n_fb), dim3(WAVE), 0, s, arena, upd_off, doc_upd, fb_list, flags, out, out_off, out_len,
+                     status, (DocMeta*)meta, fb2_list, (BigBlk*)blk, blk_cap, slot_total, out_cap);
+  return (int)hipGetLastError();
+}
 size_t ygm_k_meta_bytes() { return sizeof(DocMeta); }
 size_t ygm_k_seq_reader_bytes() { return sizeof(Stream); }
 size_t ygm_k_drec_bytes() { return sizeof(DRec); }

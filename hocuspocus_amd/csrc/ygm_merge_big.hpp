@@ -1,0 +1,201 @@
+// ygm_merge_big.hpp -- mergeUpdates for LARGE [snapshot, ...log] documents:
+// ONE WAVE PER DOCUMENT, global memory, no per-struct records for the snapshot.
+//
+// Shape it takes (what Hocuspocus stores: the engine's previous output plus the onChange updates
+// since, row a4): the largest update U0 (the snapshot) has its client blocks in strictly
+// descending client order and a delete set sorted by (client descending, clock); every other
+// update (the log) is small -- at most LB_MAXS structs and LB_MAXD delete ranges in all -- has its
+// blocks in descending client order too (else yjs's writer can revisit a client: golden vector
+// 7955), and its structs do not overlap U0's or each other's clock ranges.  For that class rule R-M (SURVEY.md
+// App. B.5) is: per client (descending), the pieces -- U0's block as one piece, every log struct
+// as one piece -- in clock order, a Skip over every gap, U0's block bytes verbatim; and the delete
+// sets are unioned by R-DS with U0's sorted list streamed.  Anything else (overlaps, input Skips,
+// GC-GC junctions between sources, re-encoded structs, ContentAny / ContentDoc in U0, 13.5
+// multi-client delete sets, malformed input) is deferred to the exact sequential kernel.
+//
+//   walk   lane 0 walks U0 with a 16-byte register-window cursor (GCur): every struct is validated
+//          as read_struct does (UTF-8 by 16-byte chunks with an ASCII fast path) and must be
+//          byte-for-byte what write_struct would emit; one table entry per block in global scratch
+//   log    lanes walk the log updates in parallel (Cur over global memory; they are small) into
+//          LDS records; bitonic sorts by (client descending, clock)
+//   emit   lane 0 merges the block table with the sorted log pieces twice (sizes, then bytes);
+//          the wave copies each U0 block range with 16-byte loads / stores
+#pragma once
+#include "ygm_seqdoc.hpp"
+
+namespace ygm {
+
+constexpr int LB_MAXS = 1024;   // log structs per document
+constexpr int LB_MAXD = 1024;   // log delete-set ranges per document
+
+// ---- global-memory cursor with a 16-byte register window
+struct GCur {
+  const uint8_t* p;
+  uint32_t pos, end;
+  int err, nm;
+  uintptr_t wa;                  // absolute address of the window (16-byte aligned); 1 = none
+  uint32_t w0, w1, w2, w3;
+  YDEV void init(const uint8_t* base, uint32_t n) { p = base; pos = 0; end = n; err = 0; nm = 0; wa = 1; }
+  YDEV void fail(int e) { if (!err) err = e; pos = end; }
+  YDEV uint32_t raw(uint32_t q) {        // byte at p + q (q < end: the aligned chunk is inside the arena)
+    const uintptr_t a = (uintptr_t)(p + q), b = a & ~(uintptr_t)15;
+    if (b != wa) { const uint4 v = *(const uint4*)b; w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w; wa = b; }
+    const uint32_t o = (uint32_t)(a & 15u);
+    const uint32_t dw = o < 8u ? (o < 4u ? w0 : w1) : (o < 12u ? w2 : w3);
+    return (dw >> (8u * (o & 3u))) & 0xFFu;
+  }
+  YDEV uint32_t u8() { if (pos >= end) { fail(ST_MALFORMED); return 0; } return raw(pos++); }
+  YDEV uint64_t vu() {   // lib0 readVarUint (Cur::vu semantics)
+    uint64_t num = 0; uint32_t shift = 0;
+    for (;;) {
+      if (pos >= end) { fail(ST_MALFORMED); return 0; }
+      const uint32_t r = raw(pos++);
+      if (shift < 63) num |= (uint64_t)(r & 127u) << shift;
+      else if (r & 127u) { fail(ST_RANGE); return 0; }
+      shift += 7;
+      if (r < 128u) {
+        if (num > MAX_SAFE) { fail(ST_RANGE); return 0; }
+        if (r == 0 && shift > 7) nm = 1;
+        return num;
+      }
+      if (num > MAX_SAFE) { fail(ST_RANGE); return 0; }
+    }
+  }
+  YDEV uint32_t buf(uint32_t& len) {
+    const uint64_t n = vu();
+    if (err) { len = 0; return pos; }
+    if (n > (uint64_t)(end - pos)) { fail(ST_MALFORMED); len = 0; return pos; }
+    const uint32_t s = pos; pos += (uint32_t)n; len = (uint32_t)n; return s;
+  }
+};
+
+// utf8_u16 (strict UTF-8, UTF-16 length or -1) over global memory by aligned 16-byte chunks: a
+// chunk of ASCII counts its bytes at once, any other chunk runs the decoder over its registers
+YDEV int64_t gutf8_u16(const uint8_t* s, uint32_t n) {
+  int64_t u16 = 0;
+  uint32_t rem = 0, cp = 0, mn = 0;
+  const uintptr_t a0 = (uintptr_t)s, a1 = a0 + n;
+  for (uintptr_t b = a0 & ~(uintptr_t)15; b < a1; b += 16) {
+    const uint4 v = *(const uint4*)b;
+    const uint32_t lo = b < a0 ? (uint32_t)(a0 - b) : 0u, hi = a1 - b < 16 ? (uint32_t)(a1 - b) : 16u;   // bytes [lo, hi) are ours
+    const uint64_t x0 = ((uint64_t)v.y << 32) | v.x, x1 = ((uint64_t)v.w << 32) | v.z;
+    uint64_t m0 = 0x8080808080808080ull, m1 = 0x8080808080808080ull;
+    if (lo) { if (lo >= 8) { m0 = 0; m1 &= ~0ull << (8u * (lo - 8)); } else m0 &= ~0ull << (8u * lo); }
+    if (hi < 16) { if (hi <= 8) { m1 = 0; m0 &= hi == 8 ? ~0ull : ((1ull << (8u * hi)) - 1ull); } else m1 &= (1ull << (8u * (hi - 8))) - 1ull; }
+    if (rem == 0 && (x0 & m0) == 0 && (x1 & m1) == 0) { u16 += hi - lo; continue; }
+    for (uint32_t i = lo; i < hi; i++) {
+      const uint32_t c = (uint32_t)((i < 8 ? x0 >> (8 * i) : x1 >> (8 * (i - 8))) & 0xFFu);
+      if (rem == 0) {
+        if (c < 0x80u) { u16++; continue; }
+        if ((c & 0xE0u) == 0xC0u) { rem = 1; cp = c & 0x1Fu; mn = 0x80; }
+        else if ((c & 0xF0u) == 0xE0u) { rem = 2; cp = c & 0x0Fu; mn = 0x800; }
+        else if ((c & 0xF8u) == 0xF0u) { rem = 3; cp = c & 0x07u; mn = 0x10000; }
+        else return -1;
+      } else {
+        if ((c & 0xC0u) != 0x80u) return -1;
+        cp = (cp << 6) | (c & 0x3Fu);
+        if (--rem == 0) {
+          if (cp < mn || cp > 0x10FFFFu || (cp >= 0xD800u && cp <= 0xDFFFu)) return -1;
+          u16 += cp >= 0x10000u ? 2 : 1;
+        }
+      }
+    }
+  }
+  return rem ? -1 : u16;
+}
+
+// One U0 struct: validated as read_struct (Y@81141 readers) and accepted only
+// if write_struct(off = 0) reproduces its bytes (canonical info byte, parentInfo 0/1, minimal
+// varuints, canonical content).  Returns the clock length; kind: 0 GC, 1 Item; ok = false defers.
+struct GStruct { uint64_t len; uint32_t kind; bool ok; };
+YDEV GStruct big_struct(GCur& c, uint32_t flags) {
+  GStruct R; R.len = 0; R.kind = 1; R.ok = false;
+  c.nm = 0;
+  const uint32_t info = c.u8();
+  if (c.err) return R;
+  if (info == 10u) return R;                                       // Skip: filtered by the reader -> general path
+  if ((info & 31u) == 0u) {                                        // GC
+    R.kind = 0; R.len = c.vu();
+    R.ok = !c.err && !c.nm && info == 0u;
+    return R;
+  }
+  const uint32_t ref = info & 31u;
+  const bool ho = (info & 0x80u) != 0, hr = (info & 0x40u) != 0;
+  if ((ho || hr) && (info & 0x20u)) return R;                      // bit 0x20 dropped on re-encode
+  if (ho) { c.vu(); c.vu(); }
+  if (hr) { c.vu(); c.vu(); }
+  if (!ho && !hr) {
+    const uint64_t pi = c.vu();
+    if (pi == 1) { uint32_t l; const uint32_t s0 = c.buf(l); if (!c.err && gutf8_u16(c.p + s0, l) < 0) return R; }
+    else if (pi == 0) { c.vu(); c.vu(); }
+    else return R;                                                 // parentInfo re-encoded as 0
+    if (info & 0x20u) { uint32_t l; const uint32_t s0 = c.buf(l); if (!c.err && gutf8_u16(c.p + s0, l) < 0) return R; }
+  }
+  if (c.err || c.nm) return R;
+  bool nc = false;
+  switch (ref) {
+    case 1: R.len = c.vu(); break;                                 // ContentDeleted
+    case 2: {                                                      // ContentJSON
+      const uint64_t n = c.vu();
+      for (uint64_t k = 0; k < n && !c.err; k++) {
+        uint32_t l; const uint32_t s = c.buf(l); if (c.err) break;
+        if (gutf8_u16(c.p + s, l) < 0) return R;
+        const uint8_t* t = c.p + s;
+        if (l == 9 && t[0] == 'u' && t[1] == 'n' && t[2] == 'd' && t[3] == 'e' && t[4] == 'f' && t[5] == 'i' && t[6] == 'n' && t[7] == 'e' && t[8] == 'd') continue;
+        if (json_check(t, l, nc)) return R;
+      }
+      R.len = n; break;
+    }
+    case 3: { uint32_t l; c.buf(l); R.len = 1; break; }            // ContentBinary
+    case 4: {                                                      // ContentString
+      uint32_t l; const uint32_t s = c.buf(l); if (c.err) return R;
+      const int64_t u = gutf8_u16(c.p + s, l);
+      if (u < 0) return R;
+      R.len = (uint64_t)u; break;
+    }
+    case 5: {                                                      // ContentEmbed
+      uint32_t l; const uint32_t s = c.buf(l); if (c.err) return R;
+      if (gutf8_u16(c.p + s, l) < 0 || json_check(c.p + s, l, nc)) return R;
+      R.len = 1; break;
+    }
+    case 6: {                                                      // ContentFormat
+      uint32_t l; uint32_t s = c.buf(l); if (c.err) return R;
+      if (gutf8_u16(c.p + s, l) < 0) return R;
+      s = c.buf(l); if (c.err) return R;
+      if (gutf8_u16(c.p + s, l) < 0 || json_check(c.p + s, l, nc)) return R;
+      R.len = 1; break;
+    }
+    case 7: {                                                      // ContentType
+      const uint64_t tr = c.vu(); if (c.err || tr > 6) return R;
+      if (tr == 3 || tr == 5) { uint32_t l; const uint32_t s = c.buf(l); if (c.err || gutf8_u16(c.p + s, l) < 0) return R; }
+      R.len = 1; break;
+    }
+    default: return R;                                             // Any / Doc (validated by the general path), bad refs
+  }
+  R.ok = !c.err && !c.nm && !nc;
+  return R;
+}
+
+// U0 block table entry (global scratch)
+struct BigBlk {
+  uint64_t client, clock0, clock1;   // clock range [clock0, clock1)
+  uint32_t b0, b1;                   // struct bytes [b0, b1) of U0
+  uint32_t nst;
+  uint8_t first_gc, last_gc, pad[2];
+};
+// log piece (LDS): one struct of a log update
+struct BigPiece {
+  uint64_t key;                      // (~client) << 32 | clock: ascending = client descending, clock ascending
+  uint32_t len, upd;                 // clock length, update index within the document
+  uint32_t b0, b1;                   // struct bytes [b0, b1) within update `upd`
+  uint32_t gc, pad;
+};
+struct BigRange { uint64_t key; uint32_t len, pad; };   // log delete range: key as BigPiece
+
+struct BigLds {
+  BigPiece pc[LB_MAXS];
+  BigRange rg[LB_MAXD];
+  uint32_t npc, nrg, bad, u0;
+};
+
+}  // namespace ygm

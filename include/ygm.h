@@ -78,6 +78,7 @@ typedef struct {
   double lean_ms;                      /* HIP-event time of the lean kernel launches (part of kernel_ms): one span
                                           from the first launch after a finish to that finish */
   uint64_t lean_launches;              /* lean kernel launches timed in lean_ms */
+  uint64_t docs_big;                   /* merges finished by the large-document ([snapshot, ...log]) kernel */
 } ygm_stats_t;
 
 /* Opens the engine on HIP device `device` (one context per GPU; contexts are

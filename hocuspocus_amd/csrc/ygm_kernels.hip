@@ -1374,6 +1374,7 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
   __shared__ unsigned long long s_pick;
   __shared__ uint64_t s_base, s_nb, s_ds0, s_at;
   const uint32_t l = threadIdx.x;
+  DIAGL_T0
   const uint32_t d = fb_list[blockIdx.x];
   const uint32_t ua = doc_upd[d], k = doc_upd[d + 1] - ua;
   if (l == 0) { L.npc = 0; L.nrg = 0; L.bad = (flags & 2u) ? 1u : 0u; s_pick = 0; }   // YGM_F_FORCE_SEQ: all to the sequential kernel
@@ -1427,6 +1428,7 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
     }
     if (bad || c.err) L.bad = 1;
   }
+  DIAGL(0);
   // ---- U0 (lane 0): block table + delete-set order check
   const uint8_t* u0p = arena + upd_off[ua + U0];
   const uint32_t n0 = (uint32_t)(upd_off[ua + U0 + 1] - upd_off[ua + U0]);
@@ -1467,11 +1469,13 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // lane 0's block table (global) before every lane reads it
   wave_sync();
+  DIAGL(1);
   const uint32_t npc = L.npc, nrg = L.nrg;
   bool bad = L.bad || npc > (uint32_t)LB_MAXS || nrg > (uint32_t)LB_MAXD;
   if (!bad) { big_bitonic(L.pc, npc); big_bitonic(L.rg, nrg); }
   const BigBlk* T = blk + s_base;
   const uint64_t nb = bad ? 0 : s_nb;
+  DIAGL(2);
   // ---- emit: pass 0 sizes (and proves the class), pass 1 bytes.  Every lane runs the same plan.
   uint64_t nblocks = 0, ndsc = 0, size = 0;
   for (int pass = 0; pass < 2 && !bad; pass++) {
@@ -1541,6 +1545,7 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
       nc++;
     }
     bad |= D.c.err != 0;
+    DIAGL(3 + pass);
     if (pass == 0) {
       nblocks = nbo; ndsc = nc; size = o.n;
       bad |= ((flags & 1u) && nc > 1) ;                       // yjs 13.5: first-seen client order -> general path

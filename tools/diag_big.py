@@ -1,0 +1,38 @@
+"""Phase breakdown of k_merge_big on C5 documents (diagnostic build libygm_diag.so; tooling).
+Stamps (s_memrealtime, 100 MHz) per document: start, log walk, U0 walk, sorts, pass 0, pass 1."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import hocuspocus_amd.engine as eng  # noqa: E402
+
+eng.LIB_PATH = os.path.join(ROOT, "hocuspocus_amd", "libygm_diag.so")
+from tools import synth  # noqa: E402
+
+xml = len(sys.argv) > 1 and sys.argv[1] == "c5"
+if xml:
+    arena, upd_off, doc_upd = synth.big_docs(20, 600000, 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=9)
+else:
+    arena, upd_off, doc_upd = synth.big_docs(200, 300000, 1024, max_clients=64, max_k=200, seed=8)
+n = len(doc_upd) - 1
+upd_doc = np.repeat(np.arange(n, dtype=np.uint32), np.diff(doc_upd).astype(np.int64))
+e = eng.Engine(0)
+L = eng.lib()
+L.ygm_diag_ts_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+ts = np.zeros(16384 * 8, np.uint64)
+e.merge_packed(arena, upd_off, upd_doc, n)
+e.merge_packed(arena, upd_off, upd_doc, n)
+L.ygm_diag_ts_read(ts.ctypes.data, 0)
+st = e.stats()
+print("docs_big", st.docs_big, "docs_seq", st.docs_seq)
+t = ts.reshape(16384, 8)[:n].astype(np.int64)
+d = np.diff(t[:, :6], axis=1) * 10 / 1000.0   # us
+names = ["log walk", "U0 walk", "sorts", "pass0", "pass1"]
+sizes = np.diff(upd_off[doc_upd].astype(np.int64))
+for q in np.argsort(-d.sum(1))[:5]:
+    print("block", q, "us", dict(zip(names, np.round(d[q], 1))))
+print("mean us", dict(zip(names, np.round(d.mean(0), 1))), "max total us", round(d.sum(1).max(), 1), "bytes max", sizes.max())

@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 N_DOCS, N_UPDATES = 10000, 200
-PMC_PROFILE = "r01_lean_v2/pmc_hbm.json"  # latest committed PMC summary of the bench kernel
+PMC_PROFILE = "r01_lean_v3/pmc_hbm.json"  # latest committed PMC summary of the bench kernel
 
 
 def parse():
@@ -187,7 +187,7 @@ def main():
                        "docs_per_gpu": args.docs, "updates_per_gpu": n_upd, "bytes_in_per_gpu": len(arena),
                        "bytes_out_per_gpu": out_bytes, "parallelism": f"doc-sharded x{world}"},
             "docs_per_s": round(all_docs * args.steps / dt, 1),
-            "roofline": {"bound": "hbm", "kernel": "k_merge_lean (+ k_merge_wave / k_merge_fast / k_merge_seq for deferred docs)",
+            "roofline": {"bound": "hbm", "kernel": "k_merge_lean (+ k_merge_wave / k_merge_fast / k_merge_big / k_merge_seq for deferred docs)",
                          "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5) if achieved else None,
                          "kernel_ms": round(kernel_ms, 4), "traffic": _pmc_traffic()},

@@ -1432,11 +1432,14 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
   // ---- U0 (lane 0): block table + delete-set order check
   const uint8_t* u0p = arena + upd_off[ua + U0];
   const uint32_t n0 = (uint32_t)(upd_off[ua + U0 + 1] - upd_off[ua + U0]);
-  if (l == 0 && !L.bad) {
+  wave_sync();
+  if (!L.bad) {   // every lane walks (uniform state: scalar registers and scalar loads); lane 0 stores
     GCur c; c.init(u0p, n0);
     bool bad = false;
     const uint64_t nb = c.vu();
-    const uint64_t base = atomicAdd(&meta->big_cursor, (unsigned long long)nb);
+    if (l == 0) s_base = atomicAdd(&meta->big_cursor, (unsigned long long)nb);
+    wave_sync();
+    const uint64_t base = __builtin_amdgcn_readfirstlane((uint32_t)s_base) | ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_base >> 32)) << 32);
     bad |= c.err || nb > n0 / 4u + 1u || base + nb > blk_cap;
     uint64_t prevc = ~0ull;
     for (uint64_t b = 0; b < nb && !bad; b++) {
@@ -1456,16 +1459,16 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
       }
       bad |= clk > 0xFFFFFFFFull;
       B.clock1 = clk; B.b1 = c.pos;
-      if (!bad) blk[base + b] = B;
+      if (!bad && l == 0) blk[base + b] = B;
     }
-    s_ds0 = c.pos;
+    const uint32_t ds0 = c.pos;
     // U0's delete set must already be in union order (client descending, clock ascending)
     BigDs D; D.c = c; D.cl_left = D.c.vu(); D.r_left = 0; D.client = 0;
     uint64_t prev = 0;
     for (D.next(); D.has && !bad; D.next()) { bad |= D.key < prev || D.client > 0xFFFFFFFFull || D.key + D.len > ((D.key >> 32) << 32) + 0xFFFFFFFFull; prev = D.key; }
     bad |= D.c.err != 0;
-    s_base = base; s_nb = nb;
-    if (bad) L.bad = 1;
+    wave_sync();
+    if (l == 0) { s_nb = nb; s_ds0 = ds0; if (bad) L.bad = 1; }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // lane 0's block table (global) before every lane reads it
   wave_sync();

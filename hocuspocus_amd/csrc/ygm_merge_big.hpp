@@ -22,6 +22,7 @@
 //          the wave copies each U0 block range with 16-byte loads / stores
 #pragma once
 #include "ygm_seqdoc.hpp"
+#include "ygm_merge_lean.hpp"
 
 namespace ygm {
 
@@ -38,14 +39,34 @@ struct GCur {
   YDEV void init(const uint8_t* base, uint32_t n) { p = base; pos = 0; end = n; err = 0; nm = 0; wa = 1; }
   YDEV void fail(int e) { if (!err) err = e; pos = end; }
   YDEV uint32_t raw(uint32_t q) {        // byte at p + q (q < end: the aligned chunk is inside the arena)
-    const uintptr_t a = (uintptr_t)(p + q), b = a & ~(uintptr_t)15;
-    if (b != wa) { const uint4 v = *(const uint4*)b; w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w; wa = b; }
+    const uint8_t* ap = p + q;
+    const uintptr_t a = (uintptr_t)ap, b = a & ~(uintptr_t)15;
+    if (b != wa) {   // pointer arithmetic keeps the global address space (an integer round trip would make it flat)
+      const uint4 v = *(const uint4*)(ap - (a & 15u));
+      w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w; wa = b;
+    }
     const uint32_t o = (uint32_t)(a & 15u);
     const uint32_t dw = o < 8u ? (o < 4u ? w0 : w1) : (o < 12u ? w2 : w3);
     return (dw >> (8u * (o & 3u))) & 0xFFu;
   }
   YDEV uint32_t u8() { if (pos >= end) { fail(ST_MALFORMED); return 0; } return raw(pos++); }
   YDEV uint64_t vu() {   // lib0 readVarUint (Cur::vu semantics)
+    // fast path: the whole varuint (<= 8 bytes) inside the current 16-byte window and the update
+    if (pos < end) {
+      raw(pos);
+      const uint32_t o = (uint32_t)(((uintptr_t)(p + pos)) & 15u);
+      const uint64_t X = ((uint64_t)w1 << 32) | w0, Y = ((uint64_t)w3 << 32) | w2;
+      const uint64_t v8 = o == 0 ? X : o < 8 ? (X >> (8 * o)) | (Y << (64 - 8 * o)) : (Y >> (8 * (o - 8)));
+      const uint64_t t = ~v8 & 0x8080808080808080ull;
+      const uint32_t k = t ? (uint32_t)__builtin_ctzll(t) >> 3 : 8u;          // terminator byte index
+      if (k < 8u && k < 16u - o && pos + k < end) {
+        const uint64_t num = pext7(v8, k + 1);
+        if (num > MAX_SAFE) { fail(ST_RANGE); return 0; }
+        if (k > 0 && ((v8 >> (8 * k)) & 0xFFu) == 0) nm = 1;
+        pos += k + 1;
+        return num;
+      }
+    }
     uint64_t num = 0; uint32_t shift = 0;
     for (;;) {
       if (pos >= end) { fail(ST_MALFORMED); return 0; }

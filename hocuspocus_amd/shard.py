@@ -36,6 +36,47 @@ def partition(document_names, n_shards: int):
     return parts
 
 
+class ShardedEngine:
+    """One process driving several GPUs of a node: one Engine (context + stream) per device,
+    documents routed by ``shard_of(name, N)``; a batch is split by shard, the shards run
+    concurrently (the C ABI releases the GIL for the whole call) and results come back in
+    caller order.  Same batch API as :class:`hocuspocus_amd.engine.Engine` plus document names
+    (mirror of ``GpuEnginePool`` in packages/extension-gpu-merge/src/engine.js)."""
+
+    def __init__(self, devices=(0,), engines=None, **engine_kw):
+        if engines is None:
+            from .engine import Engine
+            engines = [Engine(d, **engine_kw) for d in devices]
+        self.engines = list(engines)
+        from concurrent.futures import ThreadPoolExecutor
+        self._pool = ThreadPoolExecutor(max_workers=len(self.engines))
+
+    def _run(self, names, cols, call):
+        parts = partition(names, len(self.engines))
+        futs = {k: self._pool.submit(call, self.engines[k], *[[c[i] for i in idx] for c in cols])
+                for k, idx in enumerate(parts) if idx}
+        out = [None] * len(names)
+        for k, f in futs.items():
+            for i, r in zip(parts[k], f.result()):
+                out[i] = r
+        return out
+
+    def merge_updates_batch(self, names, docs):
+        return self._run(names, [docs], lambda e, d: e.merge_updates_batch(d))
+
+    def diff_update_batch(self, names, updates, svs):
+        return self._run(names, [updates, svs], lambda e, u, s: e.diff_update_batch(u, s))
+
+    def encode_state_vector_from_update_batch(self, names, updates):
+        return self._run(names, [updates], lambda e, u: e.encode_state_vector_from_update_batch(u))
+
+    def close(self):
+        self._pool.shutdown()
+        for e in self.engines:
+            if hasattr(e, "close"):
+                e.close()
+
+
 def gather_stats(stats: dict, dist=None, device=None):
     """All-gathers one fixed-size stats vector per rank and returns the node totals.
     kernel_ms is reduced with max (ranks run concurrently), everything else summed."""

@@ -21,6 +21,31 @@ export declare class GpuEngine {
   close (): void
 }
 
+/** FNV-1a 64 of the UTF-8 document name: the device of a document is fnv1a64(name) % devices.length */
+export declare function fnv1a64 (name: string): bigint
+
+/** One GpuEngine per device; documents sharded by fnv1a64(documentName) mod N (SURVEY.md §8e). */
+export declare class GpuEnginePool {
+  constructor (opts?: GpuEngineOptions & { devices?: number[] })
+  shardOf (documentName: string): number
+  engineFor (documentName: string): GpuEngine
+  mergeUpdates (updates: Uint8Array[], documentName?: string): Promise<Uint8Array>
+  diffUpdate (update: Uint8Array, stateVector: Uint8Array, documentName?: string): Promise<Uint8Array>
+  encodeStateVectorFromUpdate (update: Uint8Array, documentName?: string): Promise<Uint8Array>
+  mergeMany (names: string[], docs: Uint8Array[][]): Promise<(Uint8Array | YgmError)[]>
+  diffMany (names: string[], states: Uint8Array[], svs: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  stateVectorsMany (names: string[], states: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  stats (): Record<string, number>[]
+  close (): void
+}
+
+/** Batched SyncStep1 -> SyncStep2 responder (SURVEY.md §8f-2; src/sync.js). */
+export declare class SyncResponder {
+  constructor (opts: { engine: GpuEngine | GpuEnginePool, getState: (documentName: string) => Promise<Uint8Array | Uint8Array[] | null> })
+  /** per message: [Step2 reply, server Step1] for SyncStep1, null for other messages, an Error if malformed */
+  answerMany (messages: Uint8Array[], opts?: { path?: 'connection' | 'reply' | 'none' }): Promise<(Uint8Array[] | Error | null)[]>
+}
+
 export declare class DocumentStore {
   fetchMany (payloads: fetchPayload[]): Promise<(Uint8Array | Uint8Array[] | null)[]>
   storeMany (entries: { payload: onStoreDocumentPayload; state: Buffer }[]): Promise<void>
@@ -28,6 +53,8 @@ export declare class DocumentStore {
 }
 
 export interface GpuMergeConfiguration extends GpuEngineOptions {
+  /** several GPUs: documents sharded by fnv1a64(documentName) mod devices.length */
+  devices?: number[]
   /** a batched DocumentStore, or the DatabaseConfiguration.store function (Database.ts:19) */
   store?: DocumentStore | ((p: storePayload) => Promise<void>)
   fetch?: (p: fetchPayload) => Promise<Uint8Array | Uint8Array[] | null>
@@ -47,4 +74,6 @@ export declare class GpuMerge implements Extension {
   onStoreDocument (data: onStoreDocumentPayload): Promise<void>
   afterUnloadDocument (data: afterUnloadDocumentPayload): Promise<void>
   onDestroy (): Promise<void>
+  /** batched SyncStep1 responder over the captured state (snapshot + updates since) */
+  syncResponder (): SyncResponder
 }

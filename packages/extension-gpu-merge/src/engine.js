@@ -137,4 +137,53 @@ function unpack (r) {
   return Array.from(r.status, (st, i) => st === 0 ? r.outputs[i] : new YgmError(st, loadAddon().strerror(st)))
 }
 
-module.exports = { GpuEngine, YgmError, STATUS, loadAddon }
+const FNV_OFFSET = BigInt('0xcbf29ce484222325')
+const FNV_PRIME = BigInt('0x100000001b3')
+const U64 = BigInt('0xffffffffffffffff')
+/** FNV-1a 64 over the UTF-8 bytes of a document name (SURVEY.md §8e: gpu = fnv1a64(name) mod N). */
+function fnv1a64 (name) {
+  let h = FNV_OFFSET
+  for (const b of Buffer.from(String(name), 'utf8')) h = ((h ^ BigInt(b)) * FNV_PRIME) & U64
+  return h
+}
+
+/**
+ * Documents sharded over several GPUs of one node: one GpuEngine (context, stream, batcher) per
+ * device, document -> device by fnv1a64(documentName) mod N, no cross-device traffic (documents
+ * are independent; the reference scales by document too, docs/guides/scalability.md:12-14).
+ * Same API as GpuEngine with a trailing document name; the *Many forms split a batch by shard,
+ * run the shards concurrently (one libuv worker each) and return results in caller order.
+ */
+class GpuEnginePool {
+  constructor (opts = {}) {
+    const devices = opts.devices && opts.devices.length ? opts.devices : [opts.device || 0]
+    const make = opts.makeEngine || (device => new GpuEngine({ ...opts, device }))
+    this.engines = devices.map(make)
+  }
+
+  shardOf (documentName) { return Number(fnv1a64(documentName) % BigInt(this.engines.length)) }
+  engineFor (documentName) { return this.engines[this.shardOf(documentName)] }
+  mergeUpdates (updates, documentName = '') { return this.engineFor(documentName).mergeUpdates(updates) }
+  diffUpdate (update, sv, documentName = '') { return this.engineFor(documentName).diffUpdate(update, sv) }
+  encodeStateVectorFromUpdate (update, documentName = '') { return this.engineFor(documentName).encodeStateVectorFromUpdate(update) }
+
+  async _many (names, cols, run) {
+    const parts = this.engines.map(() => [])
+    names.forEach((n, i) => parts[this.shardOf(n)].push(i))
+    const out = new Array(names.length)
+    await Promise.all(parts.map(async (idx, e) => {
+      if (!idx.length) return
+      const r = await run(this.engines[e], ...cols.map(c => idx.map(i => c[i])))
+      idx.forEach((i, k) => { out[i] = r[k] })
+    }))
+    return out
+  }
+
+  mergeMany (names, docs) { return this._many(names, [docs], (e, d) => e.mergeMany(d)) }
+  diffMany (names, states, svs) { return this._many(names, [states, svs], (e, a, b) => e.diffMany(a, b)) }
+  stateVectorsMany (names, states) { return this._many(names, [states], (e, a) => e.stateVectorsMany(a)) }
+  stats () { return this.engines.map(e => e.stats()) }
+  close () { this.engines.forEach(e => e.close()) }
+}
+
+module.exports = { GpuEngine, GpuEnginePool, fnv1a64, YgmError, STATUS, loadAddon }

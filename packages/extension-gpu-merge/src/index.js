@@ -15,7 +15,8 @@
  * are a valid V1 update of the same document state (mergeUpdates semantics,
  * byte-identical to yjs); loading applies it exactly as Database.ts:44-50 does.
  */
-const { GpuEngine, YgmError } = require('./engine')
+const { GpuEngine, GpuEnginePool, fnv1a64, YgmError } = require('./engine')
+const { SyncResponder } = require('./sync')
 
 /**
  * A batched document store.  `fromDatabase` adapts any DatabaseConfiguration
@@ -58,8 +59,24 @@ class GpuMerge {
 
   _Y () { if (!this.Y) this.Y = require('yjs'); return this.Y }
   _engine () {
-    if (!this.engine) this.engine = new GpuEngine({ device: this.configuration.device || 0, compat135: this.configuration.compat135, batchWindowMs: this.configuration.batchWindowMs, maxBatchDocs: this.configuration.maxBatchDocs })
+    if (!this.engine) {
+      const c = this.configuration
+      const opts = { device: c.device || 0, compat135: c.compat135, batchWindowMs: c.batchWindowMs, maxBatchDocs: c.maxBatchDocs }
+      // several GPUs of the node: documents sharded by fnv1a64(documentName) mod N (SURVEY.md §8e)
+      this.engine = c.devices && c.devices.length > 1 ? new GpuEnginePool({ ...opts, devices: c.devices }) : new GpuEngine(opts)
+    }
     return this.engine
+  }
+
+  /**
+   * A batched SyncStep1 responder over this extension's captured state (stored snapshot + the
+   * updates since): reconnect storms answered by one GPU diff batch (SURVEY.md §8f-2, src/sync.js).
+   */
+  syncResponder () {
+    return new SyncResponder({
+      engine: this._engine(),
+      getState: async name => { const e = this.docs.get(name); return e ? (e.base ? [e.base] : []).concat(e.log) : null }
+    })
   }
 
   async onConfigure () { this._engine() }
@@ -70,7 +87,7 @@ class GpuMerge {
     let state = null
     if (Array.isArray(fetched)) {
       const parts = fetched.filter(Boolean)
-      state = parts.length === 0 ? null : parts.length === 1 ? parts[0] : await this._engine().mergeUpdates(parts)
+      state = parts.length === 0 ? null : parts.length === 1 ? parts[0] : await this._engine().mergeUpdates(parts, data.documentName)
     } else if (fetched) state = fetched
     if (state) this._Y().applyUpdate(data.document, state)
     this.docs.set(data.documentName, { base: state, log: [] })
@@ -106,7 +123,7 @@ class GpuMerge {
     let state
     if (parts.length === 0) state = this._Y().encodeStateAsUpdate(data.document) // nothing captured: same bytes as extension-database
     else if (parts.length === 1) state = parts[0]
-    else state = await this._engine().mergeUpdates(parts)
+    else state = await this._engine().mergeUpdates(parts, data.documentName)
     await this.store.storeMany([{ payload: data, state: Buffer.from(state.buffer, state.byteOffset, state.byteLength) }])
     // the stored merge becomes the new base (under the document's saveMutex, Hocuspocus.ts:427)
     entry.base = state
@@ -120,4 +137,4 @@ class GpuMerge {
 
 function isEmptyUpdate (u) { return u.length === 2 && u[0] === 0 && u[1] === 0 }
 
-module.exports = { GpuMerge, DocumentStore, GpuEngine, YgmError }
+module.exports = { GpuMerge, DocumentStore, GpuEngine, GpuEnginePool, SyncResponder, fnv1a64, YgmError }

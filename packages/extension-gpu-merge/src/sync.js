@@ -1,0 +1,134 @@
+'use strict'
+// Batched sync responder (SURVEY.md §8f-2): answers many SyncStep1 messages -- a reconnect storm --
+// with one GPU diff batch instead of one encodeStateAsUpdate(doc, sv) per connection.
+//
+// Wire format (packages/server/src/types.ts:12-23 MessageType, OutgoingMessage.ts:17-50,
+// Connection.ts:180-186, MessageReceiver.ts:29-60 / 120-155, y-protocols/sync):
+//   message = varString(documentName) varUint(MessageType) payload
+//   Sync payload: varUint(step: 0 Step1 | 1 Step2 | 2 Update) varUint8Array(stateVector | update)
+// The reference replies to Step1 with [Sync, Step2, encodeStateAsUpdate(doc, sv)] and then sends its
+// own first sync step [SyncReply (or Sync), Step1, encodeStateVector(doc)] (MessageReceiver.ts:137-155).
+// Here a document's state is its stored update (snapshot + captured log, merged on the GPU) and the
+// Step2 payload is diffUpdate(state, sv) -- byte-identical to yjs diffUpdate on that update; the
+// server's Step1 carries encodeStateVectorFromUpdate(state).  (Byte parity with encodeStateAsUpdate
+// of a live Y.Doc needs YATA integration: §8f-1.)
+
+const MessageType = { Sync: 0, SyncReply: 4 }
+const SyncStep = { Step1: 0, Step2: 1, Update: 2 }
+
+// lib0 decoding (L0@2955 readVarUint, L0@3467 readVarString): a reader over one message
+class Reader {
+  constructor (buf) { this.buf = buf; this.pos = 0 }
+  varUint () {
+    let num = 0; let mult = 1
+    for (;;) {
+      if (this.pos >= this.buf.length) throw new Error('Unexpected end of array')
+      const r = this.buf[this.pos++]
+      num += (r & 127) * mult
+      mult *= 128
+      if (r < 128) return num
+      if (num > Number.MAX_SAFE_INTEGER) throw new Error('Integer out of Range')
+    }
+  }
+  varUint8Array () {
+    const n = this.varUint()
+    if (this.pos + n > this.buf.length) throw new Error('Unexpected end of array')
+    const s = this.buf.subarray(this.pos, this.pos + n); this.pos += n; return s
+  }
+  varString () { return Buffer.from(this.varUint8Array()).toString('utf8') }
+}
+
+// lib0 encoding (L0@7250 writeVarUint, L0@7454 writeVarString)
+function varUintBytes (v) {
+  const out = []
+  while (v > 127) { out.push(0x80 | (v % 128)); v = Math.floor(v / 128) }
+  out.push(v)
+  return out
+}
+function frame (documentName, type, step, payload) {
+  const name = Buffer.from(documentName, 'utf8')
+  const head = [...varUintBytes(name.length), ...name, ...varUintBytes(type), ...varUintBytes(step), ...varUintBytes(payload.length)]
+  const out = new Uint8Array(head.length + payload.length)
+  out.set(head, 0); out.set(payload, head.length)
+  return out
+}
+
+/** { documentName, messageType, step, payload } of a Sync / SyncReply message, or null for other types. */
+function decodeSyncMessage (message) {
+  const r = new Reader(message)
+  const documentName = r.varString()
+  const messageType = r.varUint()
+  if (messageType !== MessageType.Sync && messageType !== MessageType.SyncReply) return null
+  const step = r.varUint()
+  return { documentName, messageType, step, payload: r.varUint8Array() }
+}
+
+class SyncResponder {
+  /**
+   * @param {{ engine: any, getState: (documentName: string) => Promise<Uint8Array | Uint8Array[] | null> }} opts
+   *   engine: GpuEngine or GpuEnginePool; getState: the document's stored update, or [snapshot, ...log]
+   */
+  constructor ({ engine, getState }) { this.engine = engine; this.getState = getState }
+
+  _pooled () { return typeof this.engine.shardOf === 'function' }
+  _merge (names, docs) { return this._pooled() ? this.engine.mergeMany(names, docs) : this.engine.mergeMany(docs) }
+  _diff (names, states, svs) { return this._pooled() ? this.engine.diffMany(names, states, svs) : this.engine.diffMany(states, svs) }
+  _svs (names, states) { return this._pooled() ? this.engine.stateVectorsMany(names, states) : this.engine.stateVectorsMany(states) }
+
+  /**
+   * Answers a batch of incoming messages.  For each SyncStep1 message the result is [Step2 reply,
+   * server Step1]: path 'connection' (Connection.handleMessage -> MessageReceiver.apply(doc, connection),
+   * the websocket path) always sends the server Step1 as a Sync message; path 'reply' (apply with a
+   * reply callback) sends it as SyncReply, and only for Sync requests (requestFirstSync,
+   * MessageReceiver.ts:39-47 / 137-155); path 'none' omits it.  Other messages give null; a
+   * malformed message or document gives an Error for that message only.
+   */
+  async answerMany (messages, { path = 'connection' } = {}) {
+    const requestFirstSync = path !== 'none'
+    const out = new Array(messages.length).fill(null)
+    const asks = []
+    messages.forEach((m, i) => {
+      try {
+        const d = decodeSyncMessage(m)
+        if (d && d.step === SyncStep.Step1) asks.push({ i, ...d })
+      } catch (e) { out[i] = e }
+    })
+    if (!asks.length) return out
+    // one state per document: fetched in parallel, multi-part logs merged in one GPU batch
+    const names = Array.from(new Set(asks.map(a => a.documentName)))
+    const fetched = await Promise.all(names.map(n => this.getState(n)))
+    const state = new Map()
+    const toMerge = []
+    names.forEach((n, k) => {
+      const f = fetched[k]
+      const parts = Array.isArray(f) ? f.filter(Boolean) : (f ? [f] : [])
+      if (parts.length > 1) toMerge.push({ n, parts })
+      else state.set(n, parts.length ? parts[0] : new Uint8Array([0, 0]))
+    })
+    if (toMerge.length) {
+      const merged = await this._merge(toMerge.map(t => t.n), toMerge.map(t => t.parts))
+      toMerge.forEach((t, k) => state.set(t.n, merged[k]))
+    }
+    const live = asks.filter(a => !(state.get(a.documentName) instanceof Error))
+    asks.filter(a => state.get(a.documentName) instanceof Error).forEach(a => { out[a.i] = state.get(a.documentName) })
+    const diffs = await this._diff(live.map(a => a.documentName), live.map(a => state.get(a.documentName)), live.map(a => a.payload))
+    let ownSv = new Map()
+    if (requestFirstSync) {
+      const svs = await this._svs(names, names.map(n => state.get(n) instanceof Error ? new Uint8Array([0, 0]) : state.get(n)))
+      ownSv = new Map(names.map((n, k) => [n, svs[k]]))
+    }
+    live.forEach((a, k) => {
+      if (diffs[k] instanceof Error) { out[a.i] = diffs[k]; return }
+      const replies = [frame(a.documentName, MessageType.Sync, SyncStep.Step2, diffs[k])]
+      const sv = ownSv.get(a.documentName)
+      if (sv && !(sv instanceof Error)) {
+        if (path === 'connection') replies.push(frame(a.documentName, MessageType.Sync, SyncStep.Step1, sv))
+        else if (path === 'reply' && a.messageType === MessageType.Sync) replies.push(frame(a.documentName, MessageType.SyncReply, SyncStep.Step1, sv))
+      }
+      out[a.i] = replies
+    })
+    return out
+  }
+}
+
+module.exports = { SyncResponder, decodeSyncMessage, frame, MessageType, SyncStep }

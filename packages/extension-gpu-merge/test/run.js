@@ -6,15 +6,19 @@
 //          of the stored state with yjs and batching checks
 const path = require('path')
 const assert = require('assert')
-const { GpuMerge } = require('../src/index.js')
+const { GpuMerge, GpuEnginePool, fnv1a64 } = require('../src/index.js')
+const { frame, decodeSyncMessage, MessageType, SyncStep } = require('../src/sync.js')
 const { MiniHocuspocus } = require('./harness.js')
 
 const mode = process.argv.includes('--gpu') ? 'gpu' : 'cpu'
 const Y = require(path.join(__dirname, '..', '..', '..', 'tests', 'golden', 'gen', 'yjs_loader.js')).load()
 
 class CpuDouble { // test double (never shipped): same API as GpuEngine
-  constructor () { this.calls = 0 }
+  constructor (device = 0) { this.calls = 0; this.device = device }
   async mergeUpdates (u) { this.calls++; return Y.mergeUpdates(u) }
+  async mergeMany (docs) { this.calls++; return docs.map(u => Y.mergeUpdates(u)) }
+  async diffMany (states, svs) { this.calls++; return states.map((u, i) => Y.diffUpdate(u, svs[i])) }
+  async stateVectorsMany (states) { this.calls++; return states.map(u => Y.encodeStateVectorFromUpdate(u)) }
   close () {}
 }
 
@@ -132,6 +136,73 @@ test('malformed update rejects only its document', async (engine) => {
   const r = await Promise.allSettled([ext.onStoreDocument(payload('bad')), ext.onStoreDocument(payload('good'))])
   assert.strictEqual(r[0].status, 'rejected')
   assert.strictEqual(r[1].status, 'fulfilled')
+})
+
+// SURVEY.md §8e: documents sharded over the node's GPUs by fnv1a64(documentName) mod N
+test('engine pool shards by fnv1a64(name) and keeps caller order', async () => {
+  assert.strictEqual(fnv1a64('').toString(16), 'cbf29ce484222325')     // FNV-1a 64 published vectors
+  assert.strictEqual(fnv1a64('foobar').toString(16), '85944171f73967e8')
+  const pool = mode === 'cpu'
+    ? new GpuEnginePool({ devices: [0, 1, 2], makeEngine: d => new CpuDouble(d) })
+    : new GpuEnginePool({ devices: [0, 0], batchWindowMs: 1 })            // two contexts on the box's one GPU
+  const names = []; const docs = []
+  for (let d = 0; d < 24; d++) {
+    const doc = new Y.Doc(); const ups = []
+    doc.on('update', u => ups.push(u))
+    for (let i = 0; i < 5; i++) doc.getText('t').insert(0, 'p' + d + i)
+    names.push('shard-' + d); docs.push(ups)
+  }
+  const merged = await pool.mergeMany(names, docs)
+  merged.forEach((m, i) => assert.strictEqual(Buffer.from(m).toString('hex'), Buffer.from(Y.mergeUpdates(docs[i])).toString('hex')))
+  names.forEach(n => assert.strictEqual(pool.shardOf(n), Number(fnv1a64(n) % BigInt(pool.engines.length))))
+  if (mode === 'cpu') {
+    const used = new Set(names.map(n => pool.shardOf(n)))
+    pool.engines.forEach((e, k) => assert.strictEqual(e.calls, used.has(k) ? 1 : 0))
+  }
+  const one = await pool.mergeUpdates(docs[3], names[3])
+  assert.strictEqual(Buffer.from(one).toString('hex'), Buffer.from(Y.mergeUpdates(docs[3])).toString('hex'))
+  pool.close()
+})
+
+// SURVEY.md §8f-2: a reconnect storm -- SyncStep1 from many clients -- answered in one batch
+test('sync responder answers a SyncStep1 batch', async (engine) => {
+  const db = memoryDb()
+  const ext = new GpuMerge({ ...db, Y, engine })
+  const hp = new MiniHocuspocus({ extensions: [ext], Y })
+  const names = ['room-a', 'room-b', 'room-c']
+  const snaps = {}
+  for (const n of names) {
+    const doc = await hp.loadDocument(n)
+    doc.transact(() => doc.getText('t').insert(0, 'hello ' + n), 'c1')
+    await hp.flushAll(); await hp.lastStore
+    snaps[n] = Y.encodeStateVector(doc)                                   // a client that saw the first store
+    doc.transact(() => doc.getText('t').insert(0, '> '), 'c2')          // captured log, not stored yet
+    doc.transact(() => doc.getText('t').delete(2, 3), 'c2')
+  }
+  const msgs = []; const want = []
+  for (const n of names) {
+    for (const sv of [Uint8Array.from([0]), snaps[n]]) { msgs.push(frame(n, MessageType.Sync, SyncStep.Step1, sv)); want.push({ n, sv }) }
+  }
+  msgs.push(frame('room-a', 1, 0, Uint8Array.from([1, 2, 3])))          // awareness: not a sync message
+  msgs.push(Uint8Array.from([5, 0x72, 0x6f]))                           // truncated
+  const replies = await ext.syncResponder().answerMany(msgs)
+  assert.strictEqual(replies[msgs.length - 2], null)
+  assert.ok(replies[msgs.length - 1] instanceof Error)
+  want.forEach(({ n, sv }, i) => {
+    const e = ext.docs.get(n)
+    const state = Y.mergeUpdates([e.base].concat(e.log))
+    const [step2, step1] = replies[i]
+    const a = decodeSyncMessage(step2); const b = decodeSyncMessage(step1)
+    assert.strictEqual(a.documentName, n); assert.strictEqual(a.messageType, MessageType.Sync); assert.strictEqual(a.step, SyncStep.Step2)
+    assert.strictEqual(Buffer.from(a.payload).toString('hex'), Buffer.from(Y.diffUpdate(state, sv)).toString('hex'))
+    assert.strictEqual(b.step, SyncStep.Step1)
+    assert.strictEqual(Buffer.from(b.payload).toString('hex'), Buffer.from(Y.encodeStateVectorFromUpdate(state)).toString('hex'))
+    // a client at `sv` that applies the reply ends up with the server's content
+    const client = new Y.Doc()
+    if (sv.length > 1) Y.applyUpdate(client, db.rows.get(n))
+    Y.applyUpdate(client, a.payload)
+    assert.strictEqual(client.getText('t').toString(), hp.documents.get(n).getText('t').toString())
+  })
 })
 
 async function main () {

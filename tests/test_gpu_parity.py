@@ -500,3 +500,24 @@ def test_large_documents_c3_c5_vs_oracle(eng, xml):
     bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
     assert not bad, (len(bad), bad[:5])
     assert all(st == 0 for st, _ in res)
+
+
+def test_sharded_engine_two_contexts_match_single(eng):
+    # SURVEY.md §8e in one process: two engine contexts (the box has one GPU) behind fnv1a64 routing
+    from hocuspocus_amd.shard import ShardedEngine
+    from tools import synth
+    arena, upd_off, doc_upd = synth.text_updates(300, 60, seed=12, del_pct=10)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(300)]
+    names = [f"doc-{d}" for d in range(300)]
+    se = ShardedEngine(devices=(0, 0))
+    try:
+        got = se.merge_updates_batch(names, docs)
+        merged = [m for _, m in got]
+        svs = se.encode_state_vector_from_update_batch(names, merged)
+        diffs = se.diff_update_batch(names, merged, [b"\x00"] * len(merged))
+    finally:
+        se.close()
+    assert got == eng.merge_updates_batch(docs)
+    assert svs == eng.encode_state_vector_from_update_batch(merged)
+    assert all(d == (0, m) for d, m in zip(diffs, merged))

@@ -80,3 +80,31 @@ def test_shard_of_is_stable():
     assert fnv1a64(b"") == 0xCBF29CE484222325
     assert fnv1a64(b"a") == 0xAF63DC4C8601EC8C  # FNV-1a 64 test vector
     assert all(0 <= shard_of(f"d{i}", 8) < 8 for i in range(100))
+
+
+def test_sharded_engine_routes_and_reassembles():
+    # single-process multi-GPU form: documents routed by fnv1a64(name) mod N, results in caller order
+    # (the CPU oracle stands in for the per-device engine here)
+    import oracle
+    from hocuspocus_amd.shard import ShardedEngine, shard_of
+    from tools import synth
+
+    class OracleEngine:
+        def __init__(self):
+            self.docs = []
+
+        def merge_updates_batch(self, docs):
+            self.docs.append(len(docs))
+            return [oracle.merge_updates(us) for us in docs]
+
+    engines = [OracleEngine() for _ in range(3)]
+    se = ShardedEngine(engines=engines)
+    arena, upd_off, doc_upd = synth.text_updates(40, 12, seed=5)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(40)]
+    names = [f"room/{d}" for d in range(40)]
+    res = se.merge_updates_batch(names, docs)
+    assert res == [oracle.merge_updates(us) for us in docs]
+    counts = [sum(1 for n in names if shard_of(n, 3) == k) for k in range(3)]
+    assert [sum(e.docs) for e in engines] == counts and all(len(e.docs) <= 1 for e in engines)
+    se.close()

@@ -38,17 +38,19 @@ int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const 
                            void* readers, int* order, int* tmp, const uint8_t** ubase, uint32_t* ulen, uint64_t upd_cap,
                            uint32_t* cnt, void* drec, uint64_t byte_cap, uint64_t slot_total, uint64_t out_cap, hipStream_t s);
 size_t ygm_k_big_blk_bytes();
+size_t ygm_k_big_rec_bytes();
 int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
                            uint32_t n_fb, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
-                           void* meta, uint32_t* fb2_list, void* blk, uint64_t blk_cap, uint64_t slot_total, uint64_t out_cap,
-                           hipStream_t s);
+                           void* meta, uint32_t* fb2_list, void* blk, uint64_t blk_cap, void* rec, uint64_t rec_cap,
+                           uint64_t slot_total, uint64_t out_cap, hipStream_t s);
 }
 
 namespace {
 
 // mirrors ygm::DocMeta (ygm_kernels.hip); sizeof is a multiple of 16
 struct Meta {
-  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer, pad[2];
+  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer;
+  unsigned long long big_scur;
   unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor, big_cursor;
   unsigned long long payload_sh[16 * 16];
   unsigned long long payload_total() const {
@@ -89,7 +91,7 @@ struct ygm_ctx {
   int mslot = 0;           // counter slot of the next merge launch
   void* meta_slot(int i) const { return (uint8_t*)meta.p + (size_t)i * sizeof(Meta); }
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
-  DevBuf big_blk, big_list;   // large-document tier: U0 block tables, documents sent on to the sequential kernel
+  DevBuf big_blk, big_rec, big_list;   // large-document tier: block tables, struct records, documents sent on
   // host results
   std::vector<uint8_t> h_data;
   std::vector<uint64_t> h_off, h_len;
@@ -157,7 +159,7 @@ void ygm_close(ygm_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
-                    &c->s_drec, &c->big_blk, &c->big_list})
+                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list})
     b->release();
   for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
   if (c->h_meta) (void)hipHostFree(c->h_meta);
@@ -270,12 +272,14 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
   }
   uint32_t n_seq = 0;
   if (m.fb_count) {  // tier 4: large [snapshot, ...log] documents, one wave each; the rest go on to tier 5
-    const uint64_t blk_cap = m.fb_bytes / 4 + 2ull * m.fb_count + 16;
-    if (!c->big_blk.ensure(blk_cap * ygm_k_big_blk_bytes()) || !c->big_list.ensure((size_t)m.fb_count * 4 + 4)) return YGM_ENOMEM;
+    const uint64_t blk_cap = m.fb_bytes / 4 + 2ull * m.fb_count + 16, rec_cap = m.fb_bytes / 2 + 2ull * m.fb_count + 16;
+    if (!c->big_blk.ensure(blk_cap * ygm_k_big_blk_bytes()) || !c->big_rec.ensure(rec_cap * ygm_k_big_rec_bytes()) ||
+        !c->big_list.ensure((size_t)m.fb_count * 4 + 4))
+      return YGM_ENOMEM;
     HIPCHK(hipEventRecord(c->e0, s));
     if (ygm_k_launch_merge_big(P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->out.as<uint8_t>(),
                                c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), P.meta,
-                               c->big_list.as<uint32_t>(), c->big_blk.p, blk_cap, P.slot_total, P.out_cap, s))
+                               c->big_list.as<uint32_t>(), c->big_blk.p, blk_cap, c->big_rec.p, rec_cap, P.slot_total, P.out_cap, s))
       return YGM_EDEVICE;
     HIPCHK(hipEventRecord(c->e1, s));
     if ((e = read_meta(c, s, m, P.meta))) return e;

@@ -59,7 +59,7 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned int defer_count;         // documents sent from the wave kernel to the workgroup kernel
   unsigned int lean_defer;          // documents sent from the lean kernel to the wave kernel
   unsigned int big_defer;           // documents sent from the large-document kernel to the sequential kernel
-  unsigned int pad[2];
+  unsigned long long big_scur;      // large-document kernel: struct-record entries carved
   unsigned long long fast_total;    // SV/diff: bytes of the packed (look-back placed) output
   unsigned long long cursor;        // merge: bytes in the overflow region (after the per-document slots)
   unsigned long long payload;       // merge: sum of output lengths (algorithmic output bytes)
@@ -1369,10 +1369,10 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
                                                     uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
                                                     uint32_t* __restrict__ fb2_list, BigBlk* __restrict__ blk, uint64_t blk_cap,
-                                                    uint64_t slot_total, uint64_t out_cap) {
+                                                    BigRec* __restrict__ rec, uint64_t rec_cap, uint64_t slot_total, uint64_t out_cap) {
   __shared__ BigLds L;
   __shared__ unsigned long long s_pick;
-  __shared__ uint64_t s_base, s_nb, s_ds0, s_at;
+  __shared__ uint64_t s_base, s_sbase, s_ds0, s_at;
   const uint32_t l = threadIdx.x;
   DIAGL_T0
   const uint32_t d = fb_list[blockIdx.x];
@@ -1429,36 +1429,39 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
     if (bad || c.err) L.bad = 1;
   }
   DIAGL(0);
-  // ---- U0 (lane 0): block table + delete-set order check
+  // ---- U0: a skip-only walk (every lane in lockstep, lane 0 stores) records every struct's byte
+  //      range and the block table; the structs are then validated by the whole wave in parallel
   const uint8_t* u0p = arena + upd_off[ua + U0];
   const uint32_t n0 = (uint32_t)(upd_off[ua + U0 + 1] - upd_off[ua + U0]);
+  const uint64_t ncap = n0 / 2u + 1u;                       // structs take >= 2 bytes
   wave_sync();
-  if (!L.bad) {   // every lane walks (uniform state: scalar registers and scalar loads); lane 0 stores
+  uint64_t base = 0, sbase = 0, nb = 0, NS = 0;
+  if (!L.bad) {
     GCur c; c.init(u0p, n0);
     bool bad = false;
-    const uint64_t nb = c.vu();
-    if (l == 0) s_base = atomicAdd(&meta->big_cursor, (unsigned long long)nb);
+    nb = c.vu();
+    if (l == 0) { s_base = atomicAdd(&meta->big_cursor, (unsigned long long)nb); s_sbase = atomicAdd(&meta->big_scur, (unsigned long long)ncap); }
     wave_sync();
-    const uint64_t base = __builtin_amdgcn_readfirstlane((uint32_t)s_base) | ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_base >> 32)) << 32);
-    bad |= c.err || nb > n0 / 4u + 1u || base + nb > blk_cap;
+    base = s_base; sbase = s_sbase;
+    bad |= c.err || nb > n0 / 4u + 1u || base + nb > blk_cap || sbase + ncap > rec_cap;
     uint64_t prevc = ~0ull;
     for (uint64_t b = 0; b < nb && !bad; b++) {
       BigBlk B;
       B.nst = (uint32_t)c.vu(); B.client = c.vu(); B.clock0 = c.vu();
       bad |= c.err || B.nst == 0 || B.client >= prevc || B.client > 0xFFFFFFFFull;
       prevc = B.client;
-      B.b0 = c.pos;
-      uint64_t clk = B.clock0;
-      B.first_gc = 0; B.last_gc = 0;
+      B.b0 = c.pos; B.s0 = (uint32_t)NS;
+      B.first_gc = 0; B.last_gc = 0; B.clock1 = 0;
       for (uint32_t q = 0; q < B.nst && !bad; q++) {
-        const GStruct g = big_struct(c, flags);
-        bad |= !g.ok || g.len == 0;
-        if (q == 0) B.first_gc = g.kind == 0;
-        B.last_gc = g.kind == 0;
-        clk += g.len;
+        const uint32_t st = c.pos;
+        uint32_t kind;
+        bad |= !big_skip(c, kind);
+        if (l == 0) { rec[sbase + NS].start = st; rec[sbase + NS].end = c.pos; }
+        if (q == 0) B.first_gc = kind == 0;
+        B.last_gc = kind == 0;
+        NS++;
       }
-      bad |= clk > 0xFFFFFFFFull;
-      B.clock1 = clk; B.b1 = c.pos;
+      B.b1 = c.pos;
       if (!bad && l == 0) blk[base + b] = B;
     }
     const uint32_t ds0 = c.pos;
@@ -1468,16 +1471,39 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
     for (D.next(); D.has && !bad; D.next()) { bad |= D.key < prev || D.client > 0xFFFFFFFFull || D.key + D.len > ((D.key >> 32) << 32) + 0xFFFFFFFFull; prev = D.key; }
     bad |= D.c.err != 0;
     wave_sync();
-    if (l == 0) { s_nb = nb; s_ds0 = ds0; if (bad) L.bad = 1; }
+    if (l == 0) { s_ds0 = ds0; if (bad) L.bad = 1; }
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // lane 0's block table (global) before every lane reads it
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // lane 0's records (global) before every lane reads them
   wave_sync();
+  if (!L.bad) {
+    // every struct validated as read_struct does and byte-identical to what write_struct emits
+    bool bad = false;
+    for (uint64_t i = l; i < NS && !bad; i += WAVE) {
+      GCur v; v.init(u0p, n0); v.pos = rec[sbase + i].start;
+      const GStruct g = big_struct(v, flags);
+      bad |= !g.ok || g.len == 0 || v.pos != rec[sbase + i].end || g.len > 0xFFFFFFFFull;
+      rec[sbase + i].len = (uint32_t)g.len;
+    }
+    if (bad) L.bad = 1;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_sync();
+    // block clock ranges: clock0 + the lengths of the block's structs
+    for (uint64_t b = l; b < nb && !L.bad; b += WAVE) {
+      const BigBlk B = blk[base + b];
+      uint64_t clk = B.clock0;
+      for (uint32_t q = 0; q < B.nst; q++) clk += rec[sbase + B.s0 + q].len;
+      if (clk > 0xFFFFFFFFull) L.bad = 1;
+      blk[base + b].clock1 = clk;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_sync();
+  }
   DIAGL(1);
   const uint32_t npc = L.npc, nrg = L.nrg;
   bool bad = L.bad || npc > (uint32_t)LB_MAXS || nrg > (uint32_t)LB_MAXD;
   if (!bad) { big_bitonic(L.pc, npc); big_bitonic(L.rg, nrg); }
   const BigBlk* T = blk + s_base;
-  const uint64_t nb = bad ? 0 : s_nb;
+  if (bad) nb = 0;
   DIAGL(2);
   // ---- emit: pass 0 sizes (and proves the class), pass 1 bytes.  Every lane runs the same plan.
   uint64_t nblocks = 0, ndsc = 0, size = 0;
@@ -1656,13 +1682,14 @@ int ygm_diag_read(unsigned long long* out, int reset) {
 #endif
 
 size_t ygm_k_big_blk_bytes() { return sizeof(BigBlk); }
+size_t ygm_k_big_rec_bytes() { return sizeof(BigRec); }
 int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
                            uint32_t n_fb, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
-                           void* meta, uint32_t* fb2_list, void* blk, uint64_t blk_cap, uint64_t slot_total, uint64_t out_cap,
-                           hipStream_t s) {
+                           void* meta, uint32_t* fb2_list, void* blk, uint64_t blk_cap, void* rec, uint64_t rec_cap,
+                           uint64_t slot_total, uint64_t out_cap, hipStream_t s) {
   if (n_fb == 0) return 0;
   hipLaunchKernelGGL(k_merge_big, dim3(n_fb), dim3(WAVE), 0, s, arena, upd_off, doc_upd, fb_list, flags, out, out_off, out_len,
-                     status, (DocMeta*)meta, fb2_list, (BigBlk*)blk, blk_cap, slot_total, out_cap);
+                     status, (DocMeta*)meta, fb2_list, (BigBlk*)blk, blk_cap, (BigRec*)rec, rec_cap, slot_total, out_cap);
   return (int)hipGetLastError();
 }
 size_t ygm_k_meta_bytes() { return sizeof(DocMeta); }

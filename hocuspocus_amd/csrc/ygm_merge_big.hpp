@@ -197,13 +197,43 @@ YDEV GStruct big_struct(GCur& c, uint32_t flags) {
   return R;
 }
 
+// Skip-only parse of one U0 struct (the sequential part of the walk): the bytes it spans and its
+// kind (0 GC, 1 Item); validation and lengths come later, in parallel (big_struct).  false: a
+// Skip, Any / Doc content or an unknown ref -- the document goes on to the general path.
+YDEV bool big_skip(GCur& c, uint32_t& kind) {
+  const uint32_t info = c.u8();
+  kind = 1;
+  if (c.err || info == 10u) return false;
+  if ((info & 31u) == 0u) { kind = 0; c.vu(); return !c.err; }
+  uint32_t l;
+  if (info & 0x80u) { c.vu(); c.vu(); }
+  if (info & 0x40u) { c.vu(); c.vu(); }
+  if ((info & 0xC0u) == 0u) {
+    const uint64_t pi = c.vu();
+    if (pi == 1) c.buf(l); else { c.vu(); c.vu(); }
+    if (info & 0x20u) c.buf(l);
+  }
+  switch (info & 31u) {
+    case 1: c.vu(); break;
+    case 2: { const uint64_t n = c.vu(); for (uint64_t k = 0; k < n && !c.err; k++) c.buf(l); break; }
+    case 3: case 4: case 5: c.buf(l); break;
+    case 6: c.buf(l); c.buf(l); break;
+    case 7: { const uint64_t tr = c.vu(); if (tr == 3 || tr == 5) c.buf(l); break; }
+    default: return false;
+  }
+  return !c.err;
+}
+
 // U0 block table entry (global scratch)
 struct BigBlk {
   uint64_t client, clock0, clock1;   // clock range [clock0, clock1)
   uint32_t b0, b1;                   // struct bytes [b0, b1) of U0
   uint32_t nst;
-  uint8_t first_gc, last_gc, pad[2];
+  uint32_t s0;                       // index of the block's first struct record (walk scratch)
+  uint8_t first_gc, last_gc, pad[6];
 };
+// one U0 struct record (walk scratch): its bytes [start, end), then its clock length once validated
+struct BigRec { uint32_t start, end, len; };
 // log piece (LDS): one struct of a log update
 struct BigPiece {
   uint64_t key;                      // (~client) << 32 | clock: ascending = client descending, clock ascending

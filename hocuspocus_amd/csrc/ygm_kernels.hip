@@ -16,6 +16,7 @@
 // fast region through an atomic cursor (offsets are reported per document).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include "ygm_common.hpp"
@@ -38,9 +39,13 @@ __device__ unsigned long long ygm_diag_ts[16384 * 8];
 // (s_memrealtime: the chip-wide 100 MHz clock, comparable across waves and XCDs)
 #define DIAGL_T0 if (threadIdx.x == 0) ygm_diag_ts[(blockIdx.x & 16383u) * 8] = __builtin_amdgcn_s_memrealtime();
 #define DIAGL(i) do { if (threadIdx.x == 0) ygm_diag_ts[(blockIdx.x & 16383u) * 8 + 1 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define DIAG_NOW() __builtin_amdgcn_s_memrealtime()
+#define DIAG_PUT(i, v) do { if (threadIdx.x == 0) ygm_diag_ts[(blockIdx.x & 16383u) * 8 + (i)] = (v); } while (0)
 #else
 #define DIAGL_T0
 #define DIAGL(i)
+#define DIAG_NOW() 0ull
+#define DIAG_PUT(i, v)
 #define DIAGW(i)
 #define DIAG_T0
 #define DIAG(i)
@@ -1320,6 +1325,8 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
 // ======================================================================= merge: large documents
 // One wave per document the workgroup tier sent on (ygm_merge_big.hpp); documents outside its class
 // go on to the sequential kernel through fb2_list.
+constexpr uint32_t BIG_SBN = 256;   // block-table entries staged in the U0 tile's LDS during emit
+static_assert(sizeof(BigTile) >= BIG_SBN * sizeof(BigBlk) && sizeof(BigBlk) % 16 == 0, "block staging");
 template <class T>
 YDEV void big_bitonic(T* a, uint32_t n) {   // ascending by key; n <= 1024 (entries [n, pow2) padded)
   uint32_t P = 1;
@@ -1371,6 +1378,7 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ fb2_list, BigBlk* __restrict__ blk, uint64_t blk_cap,
                                                     BigRec* __restrict__ rec, uint64_t rec_cap, uint64_t slot_total, uint64_t out_cap) {
   __shared__ BigLds L;
+  __shared__ BigTile T0;
   __shared__ unsigned long long s_pick;
   __shared__ uint64_t s_base, s_sbase, s_ds0, s_at;
   const uint32_t l = threadIdx.x;
@@ -1429,13 +1437,70 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
     if (bad || c.err) L.bad = 1;
   }
   DIAGL(0);
-  // ---- U0: a skip-only walk (every lane in lockstep, lane 0 stores) records every struct's byte
-  //      range and the block table; the structs are then validated by the whole wave in parallel
+  // ---- U0, tile by tile (BigTile): the wave stages BT_CH + BT_OV bytes in LDS with aligned 16-byte
+  //      loads; every lane parses a struct speculatively (skip-only: end and kind) at each of its
+  //      positions of the first BT_CH bytes; the chain of real struct boundaries is then followed
+  //      with one LDS lookup per struct (block headers parsed from the tile), every struct's byte
+  //      range recorded; before the tile moves on, the wave validates its structs in parallel from LDS.
+  //      A struct the speculative parse could not take (leaves the tile, long JSON) is parsed from
+  //      global memory; a struct failing validation in the tile is validated again from global memory.
   const uint8_t* u0p = arena + upd_off[ua + U0];
   const uint32_t n0 = (uint32_t)(upd_off[ua + U0 + 1] - upd_off[ua + U0]);
   const uint64_t ncap = n0 / 2u + 1u;                       // structs take >= 2 bytes
   wave_sync();
   uint64_t base = 0, sbase = 0, nb = 0, NS = 0;
+  // tile origin tc0 (U0 position), tb = tc0 rounded down to a 16-byte aligned address: LDS byte j of
+  // the tile is U0 byte tb + j, so tile cursors run in tile coordinates (pointers stay inside T0)
+  uint32_t tc0 = 0, tb = 0, tn = 0;                        // tn: tile cursor end (tile coordinates)
+  uint64_t dg_spec = 0, dg_val = 0;                        // diagnostic build: time in the speculative parse / validation
+  const uint8_t* const tp = (const uint8_t*)T0.b;
+  auto load_tile = [&](uint32_t at, bool spec) {
+    const uint32_t mis = (uint32_t)((uintptr_t)(u0p + at) & 15u);
+    const uint4* g = (const uint4*)(u0p + at - mis);
+    const uint32_t nld = (n0 - at + mis + 15u) / 16u;     // aligned chunks up to the end of U0 (arena tail padding)
+    wave_sync();                                           // readers of the previous tile are done
+    for (uint32_t j = l; j < BT_TILE / 16 && j < nld; j += WAVE) T0.b[j] = g[j];
+    tc0 = at; tb = at - mis;
+    tn = n0 - tb < BT_TILE ? n0 - tb : BT_TILE;
+    wave_sync();
+    if (!spec) return;
+    const uint64_t dg0 = DIAG_NOW();
+    for (uint32_t i = l; i < BT_CH; i += WAVE) {
+      uint16_t e = 0;
+      // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item
+      // ref 1..7 without bit 0x20 next to an origin (a rejected position falls back to a global parse)
+      const uint32_t ib = ((const uint8_t*)T0.b)[mis + i];
+      const uint32_t rf = ib & 31u;
+      if (at + i < n0 && (ib == 0u || (rf >= 1u && rf <= 7u && !((ib & 0xC0u) && (ib & 0x20u))))) {
+        GCur t; t.init(tp, tn); t.pos = mis + i;
+        uint32_t kind;
+        if (big_skip(t, kind, 64) && !t.err) e = (uint16_t)((t.pos - mis) | (kind == 0 ? 0x8000u : 0u));
+      }
+      T0.nx[i] = e;
+    }
+    wave_sync();
+    dg_spec += DIAG_NOW() - dg0;
+  };
+  uint64_t vs = 0;                                         // first struct record not yet validated
+  auto validate = [&]() {                                  // records [vs, NS): all start inside the tile
+    const uint64_t dg0 = DIAG_NOW();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // lane 0's records (global) before every lane reads them
+    wave_sync();
+    bool vbad = false;
+    for (uint64_t i = vs + l; i < NS; i += WAVE) {
+      const BigRec R = rec[sbase + i];
+      GCur v; v.init(tp, tn); v.pos = R.start - tb;
+      GStruct g = big_struct(v, flags);
+      uint32_t e = v.pos + tb;
+      if (!g.ok || e != R.end) { GCur w; w.init(u0p, n0); w.pos = R.start; g = big_struct(w, flags); e = w.pos; }
+      vbad |= !g.ok || g.len == 0 || e != R.end || g.len > 0xFFFFFFFFull;
+      rec[sbase + i].len = (uint32_t)g.len;
+    }
+    if (vbad) L.bad = 1;
+    vs = NS;
+    wave_sync();
+    dg_val += DIAG_NOW() - dg0;
+  };
   if (!L.bad) {
     GCur c; c.init(u0p, n0);
     bool bad = false;
@@ -1444,49 +1509,68 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
     wave_sync();
     base = s_base; sbase = s_sbase;
     bad |= c.err || nb > n0 / 4u + 1u || base + nb > blk_cap || sbase + ncap > rec_cap;
+    uint32_t pos = c.pos;
+    bool have = false;
     uint64_t prevc = ~0ull;
     for (uint64_t b = 0; b < nb && !bad; b++) {
+      if (!have || pos >= tc0 + BT_CH) { if (have) validate(); load_tile(pos, true); have = true; }
       BigBlk B;
-      B.nst = (uint32_t)c.vu(); B.client = c.vu(); B.clock0 = c.vu();
-      bad |= c.err || B.nst == 0 || B.client >= prevc || B.client > 0xFFFFFFFFull;
+      GCur h; h.init(tp, tn); h.pos = pos - tb; h.nm = 0;
+      B.nst = (uint32_t)h.vu(); B.client = h.vu(); B.clock0 = h.vu();
+      bad |= h.err || B.nst == 0 || B.client >= prevc || B.client > 0xFFFFFFFFull;
       prevc = B.client;
-      B.b0 = c.pos; B.s0 = (uint32_t)NS;
+      B.h0 = pos; B.hcanon = h.nm == 0; B.pad = 0;
+      pos = h.pos + tb;
+      B.b0 = pos; B.s0 = (uint32_t)NS;
       B.first_gc = 0; B.last_gc = 0; B.clock1 = 0;
       for (uint32_t q = 0; q < B.nst && !bad; q++) {
-        const uint32_t st = c.pos;
-        uint32_t kind;
-        bad |= !big_skip(c, kind);
-        if (l == 0) { rec[sbase + NS].start = st; rec[sbase + NS].end = c.pos; }
+        if (pos >= tc0 + BT_CH) { validate(); load_tile(pos, true); }
+        const uint32_t e = T0.nx[pos - tc0];
+        uint32_t end, kind;
+        if (e) { end = tc0 + (e & 0x7FFFu); kind = (e & 0x8000u) ? 0u : 1u; }
+        else { GCur g; g.init(u0p, n0); g.pos = pos; bad |= !big_skip(g, kind); end = g.pos; }
+        if (l == 0) { rec[sbase + NS].start = pos; rec[sbase + NS].end = end; }
         if (q == 0) B.first_gc = kind == 0;
         B.last_gc = kind == 0;
         NS++;
+        pos = end;
       }
-      B.b1 = c.pos;
+      B.b1 = pos;
       if (!bad && l == 0) blk[base + b] = B;
     }
-    const uint32_t ds0 = c.pos;
-    // U0's delete set must already be in union order (client descending, clock ascending)
-    BigDs D; D.c = c; D.cl_left = D.c.vu(); D.r_left = 0; D.client = 0;
-    uint64_t prev = 0;
-    for (D.next(); D.has && !bad; D.next()) { bad |= D.key < prev || D.client > 0xFFFFFFFFull || D.key + D.len > ((D.key >> 32) << 32) + 0xFFFFFFFFull; prev = D.key; }
-    bad |= D.c.err != 0;
+    if (have && !bad) validate();
+    const uint32_t ds0 = pos;
+    // U0's delete set must already be in union order (client descending, clock ascending): checked
+    // from tiles (no speculative parse), and again from global memory if that fails
+    for (int from_tile = 1; from_tile >= 0 && !bad; from_tile--) {
+      BigDs D;
+      if (from_tile) { if (!have || pos < tc0 || pos >= tc0 + BT_CH) load_tile(pos, false); D.c.init(tp, tn); D.c.pos = pos - tb; }
+      else { D.c.init(u0p, n0); D.c.pos = pos; }
+      D.cl_left = D.c.vu(); D.r_left = 0; D.client = 0;
+      uint64_t prev = 0;
+      bool dbad = false;
+      for (;;) {
+        if (from_tile && D.c.pos + tb >= tc0 + BT_CH && D.c.pos + tb < n0 && !D.c.err) {
+          const uint32_t at = D.c.pos + tb;
+          load_tile(at, false);
+          D.c.init(tp, tn); D.c.pos = at - tb;
+        }
+        D.next();
+        if (!D.has || dbad) break;
+        dbad |= D.key < prev || D.client > 0xFFFFFFFFull || D.key + D.len > ((D.key >> 32) << 32) + 0xFFFFFFFFull;
+        prev = D.key;
+      }
+      dbad |= D.c.err != 0;
+      if (!dbad) break;
+      if (!from_tile) bad = true;
+    }
     wave_sync();
     if (l == 0) { s_ds0 = ds0; if (bad) L.bad = 1; }
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // lane 0's records (global) before every lane reads them
+  DIAG_PUT(6, dg_spec); DIAG_PUT(7, dg_val);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // validated lengths before the clock-range pass
   wave_sync();
   if (!L.bad) {
-    // every struct validated as read_struct does and byte-identical to what write_struct emits
-    bool bad = false;
-    for (uint64_t i = l; i < NS && !bad; i += WAVE) {
-      GCur v; v.init(u0p, n0); v.pos = rec[sbase + i].start;
-      const GStruct g = big_struct(v, flags);
-      bad |= !g.ok || g.len == 0 || v.pos != rec[sbase + i].end || g.len > 0xFFFFFFFFull;
-      rec[sbase + i].len = (uint32_t)g.len;
-    }
-    if (bad) L.bad = 1;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    wave_sync();
     // block clock ranges: clock0 + the lengths of the block's structs
     for (uint64_t b = l; b < nb && !L.bad; b += WAVE) {
       const BigBlk B = blk[base + b];
@@ -1512,13 +1596,35 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
     o.vu(nblocks);
     uint64_t i = 0, nbo = 0;
     uint32_t j = 0;
+    // U0 blocks no log piece touches (and whose headers are minimal) are U0's bytes [h0, b1) as
+    // written: consecutive ones go out as one verbatim run [r0, r1)
+    uint64_t r0 = 0, r1 = 0;
+    // the block table is read through LDS (the U0 tile is free now): BIG_SBN entries per refill
+    uint64_t sc = ~0ull;
+    const BigBlk* SB = (const BigBlk*)&T0;
     while ((i < nb || j < npc) && !bad) {
-      const uint64_t cu = i < nb ? T[i].client : 0, cp = j < npc ? 0xFFFFFFFFull - (L.pc[j].key >> 32) : 0;
+      if (i < nb && (sc == ~0ull || i >= sc + BIG_SBN)) {
+        const uint64_t m = nb - i < BIG_SBN ? nb - i : BIG_SBN;
+        const uint4* g = (const uint4*)(T + i);
+        uint4* t = (uint4*)&T0;
+        wave_sync();
+        for (uint32_t u = l; u < (uint32_t)m * (sizeof(BigBlk) / 16); u += WAVE) t[u] = g[u];
+        wave_sync();
+        sc = i;
+      }
+      const uint64_t cu = i < nb ? SB[i - sc].client : 0, cp = j < npc ? 0xFFFFFFFFull - (L.pc[j].key >> 32) : 0;
       const bool hu = i < nb && (j >= npc || cu >= cp);
       const uint64_t X = hu ? cu : cp;
-      BigBlk B; if (hu) B = T[i];
+      BigBlk B; if (hu) B = SB[i - sc];
       uint32_t j1 = j;
       while (j1 < npc && 0xFFFFFFFFull - (L.pc[j1].key >> 32) == X) j1++;
+      if (hu && j1 == j && B.hcanon) {
+        if (r1 != B.h0) { if (r1 > r0) o.copy(u0p + r0, r1 - r0); r0 = B.h0; }
+        r1 = B.b1; nbo++; i++;
+        continue;
+      }
+      if (r1 > r0) o.copy(u0p + r0, r1 - r0);
+      r0 = r1 = 0;
       // items in clock order: the U0 block slots in before the first piece at or after its clock
       for (int sweep = 0; sweep < 2 && !bad; sweep++) {
         uint64_t cnt = 0, first = 0, pend = 0; bool any = false, pgc = false, upend = hu;
@@ -1546,33 +1652,55 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
       if (hu) i++;
       j = j1;
     }
-    // delete set: U0's sorted stream merged with the sorted log ranges, runs merged per client
-    BigDs D; D.c.init(u0p, n0); D.c.pos = (uint32_t)s_ds0; D.cl_left = D.c.vu(); D.r_left = 0; D.client = 0; D.next();
+    if (r1 > r0) o.copy(u0p + r0, r1 - r0);
+    // delete set: U0's sorted stream (read through LDS tiles, forward only) merged with the sorted log
+    // ranges, runs merged per client in one sweep.  Pass 0 keeps each client's run count in the struct
+    // records' scratch (free after the clock-range pass) for pass 1's header.
+    uint32_t* runs_of = (uint32_t*)(rec + sbase);
+    const uint64_t runs_cap = ncap * (sizeof(BigRec) / 4);
+    BigDs D;
+    {
+      const uint32_t at = (uint32_t)s_ds0;
+      load_tile(at, false);
+      D.c.init(tp, tn); D.c.pos = at - tb;
+    }
+    auto dnext = [&]() __attribute__((always_inline)) {
+      if (D.c.pos + tb >= tc0 + BT_CH && D.c.pos + tb < n0 && !D.c.err) {
+        const uint32_t at = D.c.pos + tb;
+        load_tile(at, false);
+        D.c.init(tp, tn); D.c.pos = at - tb;
+      }
+      D.next();
+    };
+    D.cl_left = D.c.vu(); D.r_left = 0; D.client = 0;
+    dnext();
     uint32_t r = 0;
     uint64_t nc = 0;
     o.vu(ndsc);
     while ((D.has || r < nrg) && !bad) {
       const uint64_t kx = (D.has && (r >= nrg || D.key <= L.rg[r].key)) ? D.key : L.rg[r].key;
       const uint64_t hi = kx >> 32;
-      const BigDs D0 = D; const uint32_t r0 = r;
-      uint64_t runs = 0;
-      for (int sweep = 0; sweep < 2; sweep++) {
-        D = D0; r = r0;
-        if (sweep) { o.vu(0xFFFFFFFFull - hi); o.vu(runs); }
-        uint64_t rs = 0, re = 0; bool open = false;
-        for (;;) {
-          const bool du = D.has && (D.key >> 32) == hi, dl = r < nrg && (L.rg[r].key >> 32) == hi;
-          if (!du && !dl) break;
-          const bool tu = du && (!dl || D.key <= L.rg[r].key);
-          const uint64_t ck = (uint32_t)(tu ? D.key : L.rg[r].key), ln = tu ? D.len : L.rg[r].len;
-          if (open && ck <= re) { if (ck + ln > re) re = ck + ln; }
-          else { if (open) { if (sweep) { o.vu(rs); o.vu(re - rs); } else runs++; } rs = ck; re = ck + ln; open = true; }
-          if (tu) D.next(); else r++;
-        }
-        if (open) { if (sweep) { o.vu(rs); o.vu(re - rs); } else runs++; }
+      if (pass) { o.vu(0xFFFFFFFFull - hi); o.vu(runs_of[nc]); }
+      uint64_t runs = 0, rs = 0, re = 0;
+      bool open = false;
+      for (;;) {
+        const bool du = D.has && (D.key >> 32) == hi, dl = r < nrg && (L.rg[r].key >> 32) == hi;
+        if (!du && !dl) break;
+        const bool tu = du && (!dl || D.key <= L.rg[r].key);
+        const uint64_t ck = (uint32_t)(tu ? D.key : L.rg[r].key), ln = tu ? D.len : L.rg[r].len;
+        if (open && ck <= re) { if (ck + ln > re) re = ck + ln; }
+        else { if (open) { o.vu(rs); o.vu(re - rs); runs++; } rs = ck; re = ck + ln; open = true; }
+        if (tu) dnext(); else r++;
+      }
+      if (open) { o.vu(rs); o.vu(re - rs); runs++; }
+      if (!pass) {
+        o.n += vu_len(0xFFFFFFFFull - hi) + vu_len(runs);
+        if (nc >= runs_cap) bad = true;
+        else if (l == 0) runs_of[nc] = (uint32_t)runs;
       }
       nc++;
     }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // pass 0's run counts before pass 1 reads them
     bad |= D.c.err != 0;
     DIAGL(3 + pass);
     if (pass == 0) {
@@ -1664,6 +1792,13 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
 }  // namespace ygm
 
 // ======================================================================= launch glue
+// a failed launch names its kernel and the HIP error on stderr (the C ABI only returns YGM_EDEVICE)
+static int launch_rc(const char* fn) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fprintf(stderr, "ygm: %s: %s\n", fn, hipGetErrorString(e));
+  return (int)e;
+}
+
 extern "C" {
 
 using namespace ygm;
@@ -1690,7 +1825,7 @@ int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const 
   if (n_fb == 0) return 0;
   hipLaunchKernelGGL(k_merge_big, dim3(n_fb), dim3(WAVE), 0, s, arena, upd_off, doc_upd, fb_list, flags, out, out_off, out_len,
                      status, (DocMeta*)meta, fb2_list, (BigBlk*)blk, blk_cap, (BigRec*)rec, rec_cap, slot_total, out_cap);
-  return (int)hipGetLastError();
+  return launch_rc(__func__);
 }
 size_t ygm_k_meta_bytes() { return sizeof(DocMeta); }
 size_t ygm_k_seq_reader_bytes() { return sizeof(Stream); }
@@ -1705,7 +1840,7 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
     hipLaunchKernelGGL(k_doc<0>, dim3(tiles), dim3(DOC_NT), 0, s, arena, doc_off, sv_arena, sv_off, docs, out_base, n_docs, flags, out, out_off, out_len, status, lb, (DocMeta*)meta, out_cap);
   else
     hipLaunchKernelGGL(k_doc<1>, dim3(tiles), dim3(DOC_NT), 0, s, arena, doc_off, sv_arena, sv_off, docs, out_base, n_docs, flags, out, out_off, out_len, status, lb, (DocMeta*)meta, out_cap);
-  return (int)hipGetLastError();
+  return launch_rc(__func__);
 }
 
 int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
@@ -1722,7 +1857,7 @@ int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, 
   else
     hipLaunchKernelGGL(k_doc_lean<1>, dim3(grid), dim3(WAVE), 0, s, arena, arena_bytes, doc_off, sv_arena, sv_bytes, sv_off, n_docs, flags, out,
                        out_off, out_len, status, (DocMeta*)meta, defer_list, out_cap);
-  return (int)hipGetLastError();
+  return launch_rc(__func__);
 }
 
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
@@ -1737,7 +1872,7 @@ int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const
   const uint32_t grid = n_docs < (uint32_t)n_cu * wpc ? n_docs : (uint32_t)n_cu * wpc;
   hipLaunchKernelGGL(k_merge_lean, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len, status,
                      (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap);
-  return (int)hipGetLastError();
+  return launch_rc(__func__);
 }
 
 int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
@@ -1747,7 +1882,7 @@ int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const
   const uint32_t grid = n_docs < 2048u ? n_docs : 2048u;   // persistent: n_docs is the upper bound of the device count
   hipLaunchKernelGGL(k_merge_wave, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, docs, n_dev, n_docs,
                      flags, out, out_off, out_len, status, (DocMeta*)meta, defer_list, fb_list, out_cap);
-  return (int)hipGetLastError();
+  return launch_rc(__func__);
 }
 
 int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
@@ -1757,7 +1892,7 @@ int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const
   const uint32_t grid = n_docs < 512u ? n_docs : 512u;
   hipLaunchKernelGGL(k_merge_fast, dim3(grid), dim3(M_NT), 0, s, arena, upd_off, doc_upd, docs, n_dev, n_docs, flags, out, out_off, out_len,
                      status, slot_total, (DocMeta*)meta, fb_list, out_cap);
-  return (int)hipGetLastError();
+  return launch_rc(__func__);
 }
 
 int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list, uint32_t n_fb,
@@ -1768,7 +1903,7 @@ int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const 
   SeqScratch scr{(Stream*)readers, order, tmp, ubase, ulen, cnt, (DRec*)drec, upd_cap, byte_cap};
   hipLaunchKernelGGL(k_merge_seq, dim3((n_fb + 63) / 64), dim3(64), 0, s, arena, upd_off, doc_upd, fb_list, n_fb, flags, out, out_off,
                      out_len, status, (DocMeta*)meta, scr, slot_total, out_cap);
-  return (int)hipGetLastError();
+  return launch_rc(__func__);
 }
 
 }  // extern "C"

@@ -45,9 +45,12 @@ struct GCur {
       const uint4 v = *(const uint4*)(ap - (a & 15u));
       w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w; wa = b;
     }
+    // selects between computed halves, not between the members: a select of two member loads becomes a
+    // load through a selected pointer, and the cursor then cannot live in registers (scratch round trips)
     const uint32_t o = (uint32_t)(a & 15u);
-    const uint32_t dw = o < 8u ? (o < 4u ? w0 : w1) : (o < 12u ? w2 : w3);
-    return (dw >> (8u * (o & 3u))) & 0xFFu;
+    const uint64_t X = ((uint64_t)w1 << 32) | w0, Y = ((uint64_t)w3 << 32) | w2;
+    const uint64_t h = (o & 8u) ? Y : X;
+    return (uint32_t)(h >> (8u * (o & 7u))) & 0xFFu;
   }
   YDEV uint32_t u8() { if (pos >= end) { fail(ST_MALFORMED); return 0; } return raw(pos++); }
   YDEV uint64_t vu() {   // lib0 readVarUint (Cur::vu semantics)
@@ -200,7 +203,7 @@ YDEV GStruct big_struct(GCur& c, uint32_t flags) {
 // Skip-only parse of one U0 struct (the sequential part of the walk): the bytes it spans and its
 // kind (0 GC, 1 Item); validation and lengths come later, in parallel (big_struct).  false: a
 // Skip, Any / Doc content or an unknown ref -- the document goes on to the general path.
-YDEV bool big_skip(GCur& c, uint32_t& kind) {
+YDEV bool big_skip(GCur& c, uint32_t& kind, uint64_t jcap = ~0ull) {   // jcap: most ContentJSON entries taken
   const uint32_t info = c.u8();
   kind = 1;
   if (c.err || info == 10u) return false;
@@ -215,7 +218,7 @@ YDEV bool big_skip(GCur& c, uint32_t& kind) {
   }
   switch (info & 31u) {
     case 1: c.vu(); break;
-    case 2: { const uint64_t n = c.vu(); for (uint64_t k = 0; k < n && !c.err; k++) c.buf(l); break; }
+    case 2: { const uint64_t n = c.vu(); if (n > jcap) return false; for (uint64_t k = 0; k < n && !c.err; k++) c.buf(l); break; }
     case 3: case 4: case 5: c.buf(l); break;
     case 6: c.buf(l); c.buf(l); break;
     case 7: { const uint64_t tr = c.vu(); if (tr == 3 || tr == 5) c.buf(l); break; }
@@ -230,7 +233,10 @@ struct BigBlk {
   uint32_t b0, b1;                   // struct bytes [b0, b1) of U0
   uint32_t nst;
   uint32_t s0;                       // index of the block's first struct record (walk scratch)
-  uint8_t first_gc, last_gc, pad[6];
+  uint8_t first_gc, last_gc;
+  uint8_t hcanon;                    // block header varuints minimal: U0 bytes [h0, b1) are the block as written
+  uint8_t pad;
+  uint32_t h0;                       // block header start in U0
 };
 // one U0 struct record (walk scratch): its bytes [start, end), then its clock length once validated
 struct BigRec { uint32_t start, end, len; };
@@ -242,6 +248,15 @@ struct BigPiece {
   uint32_t gc, pad;
 };
 struct BigRange { uint64_t key; uint32_t len, pad; };   // log delete range: key as BigPiece
+
+// U0 tile (LDS): bytes staged by the whole wave; structs are parsed speculatively at every
+// position of its first BT_CH bytes; BT_OV bytes of overlap let a struct starting there end inside
+// (static LDS stays under the 64 KiB a workgroup may allocate)
+constexpr uint32_t BT_CH = 4096, BT_OV = 2048, BT_TILE = BT_CH + BT_OV + 16;
+struct BigTile {
+  uint4 b[BT_TILE / 16];
+  uint16_t nx[BT_CH];                // speculative struct end - tile origin, bit 15 = GC; 0 = no parse
+};
 
 struct BigLds {
   BigPiece pc[LB_MAXS];

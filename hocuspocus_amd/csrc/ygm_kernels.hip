@@ -1371,7 +1371,44 @@ struct BigDs {
   }
 };
 
-__global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+// The U0 tile work the whole workgroup shares (BIG_WAVES waves; wave 0 drives, helper waves join
+// through BigCmd): the speculative parse of a tile's positions, and the validation of its structs.
+constexpr uint32_t BIG_WAVES = 4, BIG_THREADS = BIG_WAVES * WAVE;
+struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; };   // cmd 0 done, 1 spec, 2 validate
+YDEV void big_spec(BigTile& T, uint32_t at, uint32_t mis, uint32_t tn, uint32_t n0, uint32_t t0) {
+  const uint8_t* tp = (const uint8_t*)T.b;
+  for (uint32_t i = t0; i < BT_CH; i += BIG_THREADS) {
+    uint16_t e = 0;
+    // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item
+    // ref 1..7 without bit 0x20 next to an origin (a rejected position falls back to a global parse)
+    const uint32_t ib = tp[mis + i];
+    const uint32_t rf = ib & 31u;
+    if (at + i < n0 && (ib == 0u || (rf >= 1u && rf <= 7u && !((ib & 0xC0u) && (ib & 0x20u))))) {
+      GCur t; t.init(tp, tn); t.pos = mis + i;
+      uint32_t kind;
+      if (big_skip(t, kind, 8) && !t.err) e = (uint16_t)((t.pos - mis) | (kind == 0 ? 0x8000u : 0u));
+    }
+    T.nx[i] = e;
+  }
+}
+// struct records [vs, ns) (all starting inside the tile): validated from LDS, again from global memory
+// when that fails; true if any is not what write_struct emits
+YDEV bool big_validate(const BigTile& T, BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0) {
+  const uint8_t* tp = (const uint8_t*)T.b;
+  bool vbad = false;
+  for (uint64_t i = C.vs + t0; i < C.ns; i += BIG_THREADS) {
+    const BigRec R = rec[C.sbase + i];
+    GCur v; v.init(tp, C.tn); v.pos = R.start - C.tb;
+    GStruct g = big_struct(v, flags);
+    uint32_t e = v.pos + C.tb;
+    if (!g.ok || e != R.end) { GCur w; w.init(C.u0p, C.n0); w.pos = R.start; g = big_struct(w, flags); e = w.pos; }
+    vbad |= !g.ok || g.len == 0 || e != R.end || g.len > 0xFFFFFFFFull;
+    rec[C.sbase + i].len = (uint32_t)g.len;
+  }
+  return vbad;
+}
+
+__global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                     const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
                                                     uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
@@ -1381,6 +1418,17 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
   __shared__ BigTile T0;
   __shared__ unsigned long long s_pick;
   __shared__ uint64_t s_base, s_sbase, s_ds0, s_at;
+  __shared__ BigCmd s_cmd;
+  if (threadIdx.x >= WAVE) {   // helper waves: wave 0's tile commands until it sends 0 (one barrier pair per command)
+    for (;;) {
+      __syncthreads();
+      const BigCmd C = s_cmd;
+      if (C.cmd == 0) return;
+      if (C.cmd == 1) big_spec(T0, C.at, C.mis, C.tn, C.n0, threadIdx.x);
+      else if (big_validate(T0, rec, C, flags, threadIdx.x)) L.bad = 1;
+      __syncthreads();
+    }
+  }
   const uint32_t l = threadIdx.x;
   DIAGL_T0
   const uint32_t d = fb_list[blockIdx.x];
@@ -1442,7 +1490,7 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
   //      positions of the first BT_CH bytes; the chain of real struct boundaries is then followed
   //      with one LDS lookup per struct (block headers parsed from the tile), every struct's byte
   //      range recorded; before the tile moves on, the wave validates its structs in parallel from LDS.
-  //      A struct the speculative parse could not take (leaves the tile, long JSON) is parsed from
+  //      A struct the speculative parse could not take (leaves the tile, JSON of > 8 entries) is parsed from
   //      global memory; a struct failing validation in the tile is validated again from global memory.
   const uint8_t* u0p = arena + upd_off[ua + U0];
   const uint32_t n0 = (uint32_t)(upd_off[ua + U0 + 1] - upd_off[ua + U0]);
@@ -1465,38 +1513,21 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
     wave_sync();
     if (!spec) return;
     const uint64_t dg0 = DIAG_NOW();
-    for (uint32_t i = l; i < BT_CH; i += WAVE) {
-      uint16_t e = 0;
-      // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item
-      // ref 1..7 without bit 0x20 next to an origin (a rejected position falls back to a global parse)
-      const uint32_t ib = ((const uint8_t*)T0.b)[mis + i];
-      const uint32_t rf = ib & 31u;
-      if (at + i < n0 && (ib == 0u || (rf >= 1u && rf <= 7u && !((ib & 0xC0u) && (ib & 0x20u))))) {
-        GCur t; t.init(tp, tn); t.pos = mis + i;
-        uint32_t kind;
-        if (big_skip(t, kind, 64) && !t.err) e = (uint16_t)((t.pos - mis) | (kind == 0 ? 0x8000u : 0u));
-      }
-      T0.nx[i] = e;
-    }
-    wave_sync();
+    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.tn = tn; s_cmd.n0 = n0; }
+    __syncthreads();
+    big_spec(T0, at, mis, tn, n0, l);
+    __syncthreads();
     dg_spec += DIAG_NOW() - dg0;
   };
   uint64_t vs = 0;                                         // first struct record not yet validated
   auto validate = [&]() {                                  // records [vs, NS): all start inside the tile
     const uint64_t dg0 = DIAG_NOW();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // lane 0's records (global) before every lane reads them
-    wave_sync();
-    bool vbad = false;
-    for (uint64_t i = vs + l; i < NS; i += WAVE) {
-      const BigRec R = rec[sbase + i];
-      GCur v; v.init(tp, tn); v.pos = R.start - tb;
-      GStruct g = big_struct(v, flags);
-      uint32_t e = v.pos + tb;
-      if (!g.ok || e != R.end) { GCur w; w.init(u0p, n0); w.pos = R.start; g = big_struct(w, flags); e = w.pos; }
-      vbad |= !g.ok || g.len == 0 || e != R.end || g.len > 0xFFFFFFFFull;
-      rec[sbase + i].len = (uint32_t)g.len;
+    if (l == 0) {
+      s_cmd.cmd = 2; s_cmd.vs = vs; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.tb = tb; s_cmd.tn = tn; s_cmd.u0p = u0p; s_cmd.n0 = n0;
     }
-    if (vbad) L.bad = 1;
+    __syncthreads();                                       // lane 0's records (global) and the command before every wave reads them
+    if (big_validate(T0, rec, s_cmd, flags, l)) L.bad = 1;
+    __syncthreads();
     vs = NS;
     wave_sync();
     dg_val += DIAG_NOW() - dg0;
@@ -1582,6 +1613,8 @@ __global__ __launch_bounds__(WAVE) void k_merge_big(const uint8_t* __restrict__ 
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     wave_sync();
   }
+  if (l == 0) s_cmd.cmd = 0;   // the helper waves are done: everything below is wave 0's
+  __syncthreads();
   DIAGL(1);
   const uint32_t npc = L.npc, nrg = L.nrg;
   bool bad = L.bad || npc > (uint32_t)LB_MAXS || nrg > (uint32_t)LB_MAXD;
@@ -1823,7 +1856,7 @@ int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const 
                            void* meta, uint32_t* fb2_list, void* blk, uint64_t blk_cap, void* rec, uint64_t rec_cap,
                            uint64_t slot_total, uint64_t out_cap, hipStream_t s) {
   if (n_fb == 0) return 0;
-  hipLaunchKernelGGL(k_merge_big, dim3(n_fb), dim3(WAVE), 0, s, arena, upd_off, doc_upd, fb_list, flags, out, out_off, out_len,
+  hipLaunchKernelGGL(k_merge_big, dim3(n_fb), dim3(BIG_THREADS), 0, s, arena, upd_off, doc_upd, fb_list, flags, out, out_off, out_len,
                      status, (DocMeta*)meta, fb2_list, (BigBlk*)blk, blk_cap, (BigRec*)rec, rec_cap, slot_total, out_cap);
   return launch_rc(__func__);
 }

@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 N_DOCS, N_UPDATES = 10000, 200
-PMC_PROFILE = "r01_lean_v3/pmc_hbm.json"  # latest committed PMC summary of the bench kernel
+PMC_PROFILE = "r01_big_v1/pmc_hbm.json"  # latest committed PMC summary of the bench kernel
 
 
 def parse():
@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--docs", type=int, default=N_DOCS)
     ap.add_argument("--updates", type=int, default=N_UPDATES)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--big", choices=["c3", "c5"], default=None,
+                    help="instead of the C2 line: one C3 / C5 large-document batch on the GPU next to the CPU oracle "
+                         "over the same documents (reported beside the headline, never as it)")
+    ap.add_argument("--big-docs", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -77,8 +81,49 @@ def cpu_baseline(arena, upd_off, doc_upd, budget_s):
                       f"loop), {cores} pthreads, {dt:.2f} s wall"}
 
 
+def big_line(args):
+    """C3 / C5 ([snapshot, ...log] large documents): the whole batch merged on cuda:0
+    (device-resident inputs, host-driven tier cascade, kernel time from the engine's HIP events) and
+    by the CPU oracle on all host threads over the same documents."""
+    import torch
+    import oracle
+    from hocuspocus_amd import Engine
+    from tools import synth
+    xml = args.big == "c5"
+    n = args.big_docs or (20 if xml else 2000)
+    if xml:
+        arena, upd_off, doc_upd = synth.big_docs(n, 1_000_000, 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=9)
+    else:
+        arena, upd_off, doc_upd = synth.big_docs(n, 1_000_000, 1024, max_clients=64, max_k=200, seed=8)
+    dev = torch.device("cuda", 0)
+    da = torch.from_numpy(np.concatenate([arena, np.zeros(64, np.uint8)])).to(dev)
+    do = torch.from_numpy(upd_off.view(np.int64)).to(dev)
+    dd = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
+    e = Engine(0)
+    for _ in range(2):   # the second run is timed (scratch already grown)
+        s0 = e.stats()
+        r = e.merge_device(da.data_ptr(), len(arena), do.data_ptr(), dd.data_ptr(), int(doc_upd[-1]), n)
+        s1 = e.stats()
+    ms = s1.kernel_ms - s0.kernel_ms
+    algo = len(arena) + r.payload_bytes
+    cores = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    st, calgo = oracle.merge_batch(arena, upd_off, doc_upd, cores)
+    cdt = time.perf_counter() - t0
+    assert (st == 0).all()
+    sizes = np.diff(upd_off[doc_upd].astype(np.int64))
+    print(json.dumps({"config": args.big.upper(), "op": "merge", "docs": n, "bytes_in": len(arena), "largest_doc": int(sizes.max()),
+                      "gpu_ms": round(ms, 3), "gpu_MBps": round(algo / ms / 1e3, 1), "gpu_docs_per_s": round(n / ms * 1e3),
+                      "docs_big_tier": s1.docs_big - s0.docs_big, "docs_seq_tier": s1.docs_seq - s0.docs_seq,
+                      "cpu_baseline": {"ms": round(cdt * 1e3, 3), "MBps": round(calgo / cdt / 1e6, 1), "cores": cores, "kind": "port",
+                                       "sample": "all documents of the batch through oracle/yjs_oracle.c yo_merge_batch, one pass"}}),
+          flush=True)
+
+
 def main():
     args = parse()
+    if args.big:
+        return big_line(args)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))

@@ -1571,6 +1571,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     }
     if (have && !bad) validate();
     const uint32_t ds0 = pos;
+    const uint64_t dgd0 = DIAG_NOW();
     // U0's delete set must already be in union order (client descending, clock ascending): checked
     // from tiles (no speculative parse), and again from global memory if that fails
     for (int from_tile = 1; from_tile >= 0 && !bad; from_tile--) {
@@ -1596,6 +1597,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       if (!from_tile) bad = true;
     }
     wave_sync();
+    dg_val += DIAG_NOW() - dgd0;   // diagnostic build: the delete-set check counts with validation
     if (l == 0) { s_ds0 = ds0; if (bad) L.bad = 1; }
   }
   DIAG_PUT(6, dg_spec); DIAG_PUT(7, dg_val);

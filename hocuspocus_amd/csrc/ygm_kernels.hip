@@ -1373,7 +1373,7 @@ struct BigDs {
 
 // The U0 tile work the whole workgroup shares (BIG_WAVES waves; wave 0 drives, helper waves join
 // through BigCmd): the speculative parse of a tile's positions, and the validation of its structs.
-constexpr uint32_t BIG_WAVES = 8, BIG_THREADS = BIG_WAVES * WAVE;
+constexpr uint32_t BIG_WAVES = 16, BIG_THREADS = BIG_WAVES * WAVE;
 struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; };   // cmd 0 done, 1 spec, 2 validate
 YDEV void big_spec(BigTile& T, uint32_t at, uint32_t mis, uint32_t tn, uint32_t n0, uint32_t t0) {
   const uint8_t* tp = (const uint8_t*)T.b;

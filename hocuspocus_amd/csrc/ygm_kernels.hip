@@ -1391,19 +1391,22 @@ YDEV void big_spec(BigTile& T, uint32_t at, uint32_t mis, uint32_t tn, uint32_t 
     T.nx[i] = e;
   }
 }
-// struct records [vs, ns) (all starting inside the tile): validated from LDS, again from global memory
-// when that fails; true if any is not what write_struct emits
-YDEV bool big_validate(const BigTile& T, BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0) {
+// struct records [vs, ns) (all starting inside the tile; byte ranges in rs / re, LDS): validated from
+// LDS, again from global memory when that fails, then stored with their clock lengths; true if any is
+// not what write_struct emits
+YDEV bool big_validate(const BigTile& T, const uint32_t* rs, const uint32_t* re, BigRec* rec, const BigCmd& C, uint32_t flags,
+                       uint32_t t0) {
   const uint8_t* tp = (const uint8_t*)T.b;
   bool vbad = false;
   for (uint64_t i = C.vs + t0; i < C.ns; i += BIG_THREADS) {
-    const BigRec R = rec[C.sbase + i];
+    BigRec R; R.start = rs[i - C.vs]; R.end = re[i - C.vs];
     GCur v; v.init(tp, C.tn); v.pos = R.start - C.tb;
     GStruct g = big_struct(v, flags);
     uint32_t e = v.pos + C.tb;
     if (!g.ok || e != R.end) { GCur w; w.init(C.u0p, C.n0); w.pos = R.start; g = big_struct(w, flags); e = w.pos; }
     vbad |= !g.ok || g.len == 0 || e != R.end || g.len > 0xFFFFFFFFull;
-    rec[C.sbase + i].len = (uint32_t)g.len;
+    R.len = (uint32_t)g.len;
+    rec[C.sbase + i] = R;
   }
   return vbad;
 }
@@ -1419,13 +1422,14 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   __shared__ unsigned long long s_pick;
   __shared__ uint64_t s_base, s_sbase, s_ds0, s_at;
   __shared__ BigCmd s_cmd;
+  __shared__ uint32_t s_rst[BT_CH / 2], s_ren[BT_CH / 2];   // byte ranges of the current tile's structs (>= 2 bytes each)
   if (threadIdx.x >= WAVE) {   // helper waves: wave 0's tile commands until it sends 0 (one barrier pair per command)
     for (;;) {
       __syncthreads();
       const BigCmd C = s_cmd;
       if (C.cmd == 0) return;
       if (C.cmd == 1) big_spec(T0, C.at, C.mis, C.tn, C.n0, threadIdx.x);
-      else if (big_validate(T0, rec, C, flags, threadIdx.x)) L.bad = 1;
+      else if (big_validate(T0, s_rst, s_ren, rec, C, flags, threadIdx.x)) L.bad = 1;
       __syncthreads();
     }
   }
@@ -1525,8 +1529,8 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     if (l == 0) {
       s_cmd.cmd = 2; s_cmd.vs = vs; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.tb = tb; s_cmd.tn = tn; s_cmd.u0p = u0p; s_cmd.n0 = n0;
     }
-    __syncthreads();                                       // lane 0's records (global) and the command before every wave reads them
-    if (big_validate(T0, rec, s_cmd, flags, l)) L.bad = 1;
+    __syncthreads();                                       // lane 0's byte ranges and the command before every wave reads them
+    if (big_validate(T0, s_rst, s_ren, rec, s_cmd, flags, l)) L.bad = 1;
     __syncthreads();
     vs = NS;
     wave_sync();
@@ -1560,7 +1564,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
         uint32_t end, kind;
         if (e) { end = tc0 + (e & 0x7FFFu); kind = (e & 0x8000u) ? 0u : 1u; }
         else { GCur g; g.init(u0p, n0); g.pos = pos; bad |= !big_skip(g, kind); end = g.pos; }
-        if (l == 0) { rec[sbase + NS].start = pos; rec[sbase + NS].end = end; }
+        if (l == 0) { s_rst[NS - vs] = pos; s_ren[NS - vs] = end; }
         if (q == 0) B.first_gc = kind == 0;
         B.last_gc = kind == 0;
         NS++;

@@ -1575,33 +1575,9 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     }
     if (have && !bad) validate();
     const uint32_t ds0 = pos;
-    const uint64_t dgd0 = DIAG_NOW();
-    // U0's delete set must already be in union order (client descending, clock ascending): checked
-    // from tiles (no speculative parse), and again from global memory if that fails
-    for (int from_tile = 1; from_tile >= 0 && !bad; from_tile--) {
-      BigDs D;
-      if (from_tile) { if (!have || pos < tc0 || pos >= tc0 + BT_CH) load_tile(pos, false); D.c.init(tp, tn); D.c.pos = pos - tb; }
-      else { D.c.init(u0p, n0); D.c.pos = pos; }
-      D.cl_left = D.c.vu(); D.r_left = 0; D.client = 0;
-      uint64_t prev = 0;
-      bool dbad = false;
-      for (;;) {
-        if (from_tile && D.c.pos + tb >= tc0 + BT_CH && D.c.pos + tb < n0 && !D.c.err) {
-          const uint32_t at = D.c.pos + tb;
-          load_tile(at, false);
-          D.c.init(tp, tn); D.c.pos = at - tb;
-        }
-        D.next();
-        if (!D.has || dbad) break;
-        dbad |= D.key < prev || D.client > 0xFFFFFFFFull || D.key + D.len > ((D.key >> 32) << 32) + 0xFFFFFFFFull;
-        prev = D.key;
-      }
-      dbad |= D.c.err != 0;
-      if (!dbad) break;
-      if (!from_tile) bad = true;
-    }
+    // U0's delete set must already be in union order (client descending, clock ascending): checked by
+    // the emit's first pass, which streams it anyway
     wave_sync();
-    dg_val += DIAG_NOW() - dgd0;   // diagnostic build: the delete-set check counts with validation
     if (l == 0) { s_ds0 = ds0; if (bad) L.bad = 1; }
   }
   DIAG_PUT(6, dg_spec); DIAG_PUT(7, dg_val);
@@ -1703,6 +1679,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       load_tile(at, false);
       D.c.init(tp, tn); D.c.pos = at - tb;
     }
+    uint64_t dprev = 0;
     auto dnext = [&]() __attribute__((always_inline)) {
       if (D.c.pos + tb >= tc0 + BT_CH && D.c.pos + tb < n0 && !D.c.err) {
         const uint32_t at = D.c.pos + tb;
@@ -1710,6 +1687,8 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
         D.c.init(tp, tn); D.c.pos = at - tb;
       }
       D.next();
+      // U0's delete set in union order, every range inside 32-bit clocks (else the general path)
+      if (D.has) { bad |= D.key < dprev || D.client > 0xFFFFFFFFull || D.key + D.len > ((D.key >> 32) << 32) + 0xFFFFFFFFull; dprev = D.key; }
     };
     D.cl_left = D.c.vu(); D.r_left = 0; D.client = 0;
     dnext();

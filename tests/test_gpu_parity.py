@@ -515,6 +515,19 @@ def test_large_document_tile_edges_vs_oracle(eng):
     assert eng.stats().docs_big - st0.docs_big == len(docs)   # the large-document tier took every one
 
 
+def test_large_document_unsorted_delete_set_goes_on(eng):
+    # a snapshot delete set outside union order: the large-document tier's first emit pass refuses it and
+    # the sequential kernel merges it, bit-exact
+    from tile_docs import tile_edge_docs
+    docs = tile_edge_docs(6, ds_ascending=True)
+    st0 = eng.stats()
+    res = eng.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+    assert not bad, bad
+    st1 = eng.stats()
+    assert st1.docs_big - st0.docs_big == 0 and st1.docs_seq - st0.docs_seq == len(docs)
+
+
 def test_sharded_engine_two_contexts_match_single(eng):
     # SURVEY.md §8e in one process: two engine contexts (the box has one GPU) behind fnv1a64 routing
     from hocuspocus_amd.shard import ShardedEngine

@@ -16,12 +16,13 @@ def _vs(b):
     return _vu(len(b)) + b
 
 
-def tile_edge_docs(seed):
+def tile_edge_docs(seed, ds_ascending=False):
     """[snapshot, ...log] documents over 16 KB (the large-document tier) whose snapshots hold what the
     tiled walk must hand to global memory: strings longer than a tile's overlap (2 KB), ContentJSON
     with more entries than the speculative parse takes (64), structs straddling tile boundaries,
     more client blocks than one LDS staging refill (256), GC runs, a delete set; log updates touch
-    clients between untouched (verbatim-run) blocks."""
+    clients between untouched (verbatim-run) blocks.  ds_ascending: the snapshot's delete set lists its
+    clients in ascending order (not yjs's union order), which the large-document tier must hand on."""
     rnd = random.Random(seed)
     docs = []
     for d in range(6):
@@ -61,7 +62,9 @@ def tile_edge_docs(seed):
         snap = bytearray(_vu(len(blocks)))
         for c, structs in blocks:
             snap += _vu(len(structs)) + _vu(c) + _vu(0) + b"".join(structs)
-        dcl = clients[: max(1, nclients // 10)]
+        dcl = clients[: max(2, nclients // 10)]
+        if ds_ascending:
+            dcl = dcl[::-1]
         snap += _vu(len(dcl))
         for c in dcl:
             snap += _vu(c) + _vu(1) + _vu(0) + _vu(1)

@@ -31,10 +31,10 @@ st = e.stats()
 print("docs_big", st.docs_big, "docs_seq", st.docs_seq)
 t = ts.reshape(16384, 8)[:n].astype(np.int64)
 # stamps: start, log walk, U0 walk, sorts, pass0, pass1; slots 6 / 7: time inside the U0 walk spent in
-# the speculative tile parse / in validation and the delete-set check
+# the speculative tile parse / in validation
 d = np.diff(t[:, :6], axis=1) * 10 / 1000.0   # us
 d = np.concatenate([d[:, :1], d[:, 1:2] - (t[:, 6:8].sum(1, keepdims=True) * 10 / 1000.0), t[:, 6:8] * 10 / 1000.0, d[:, 2:]], axis=1)
-names = ["log walk", "U0 follow", "U0 spec parse", "U0 validate + DS check", "sorts", "pass0", "pass1"]
+names = ["log walk", "U0 follow", "U0 spec parse", "U0 validate", "sorts", "pass0", "pass1"]
 sizes = np.diff(upd_off[doc_upd].astype(np.int64))
 for q in np.argsort(-d.sum(1))[:5]:
     print("block", q, "us", dict(zip(names, np.round(d[q], 1))))

@@ -1371,6 +1371,15 @@ struct BigDs {
   }
 };
 
+// A U0 struct the speculative parse could not take, parsed from global memory (rare: kept out of line so
+// the chain follow's loop stays small).  Returns end | kind << 32 | failed << 63.
+YDEV_NI uint64_t big_skip_global(const uint8_t* u0p, uint32_t n0, uint32_t pos) {
+  GCur g; g.init(u0p, n0); g.pos = pos;
+  uint32_t kind;
+  const bool ok = big_skip(g, kind);
+  return (uint64_t)g.pos | ((uint64_t)(kind & 1u) << 32) | (ok ? 0ull : 1ull << 63);
+}
+
 // The U0 tile work the whole workgroup shares (BIG_WAVES waves; wave 0 drives, helper waves join
 // through BigCmd): the speculative parse of a tile's positions, and the validation of its structs.
 constexpr uint32_t BIG_WAVES = 16, BIG_THREADS = BIG_WAVES * WAVE;
@@ -1563,7 +1572,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
         const uint32_t e = T0.nx[pos - tc0];
         uint32_t end, kind;
         if (e) { end = tc0 + (e & 0x7FFFu); kind = (e & 0x8000u) ? 0u : 1u; }
-        else { GCur g; g.init(u0p, n0); g.pos = pos; bad |= !big_skip(g, kind); end = g.pos; }
+        else { const uint64_t r = big_skip_global(u0p, n0, pos); bad |= (r >> 63) != 0; kind = (uint32_t)(r >> 32) & 1u; end = (uint32_t)r; }
         if (l == 0) { s_rst[NS - vs] = pos; s_ren[NS - vs] = end; }
         if (q == 0) B.first_gc = kind == 0;
         B.last_gc = kind == 0;

@@ -1636,6 +1636,24 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
         wave_sync();
         sc = i;
       }
+      if (i < nb) {
+        // up to 64 untouched blocks at once: lane q tests block i + q (minimal header, client above the next
+        // log piece's); the leading run of such blocks extends the verbatim run (U0 blocks are contiguous)
+        const uint64_t cpx = j < npc ? 0xFFFFFFFFull - (L.pc[j].key >> 32) : 0;
+        const uint64_t q = i + l;
+        bool ok = q < nb && q < sc + BIG_SBN;
+        uint32_t h0q = 0, b1q = 0;
+        if (ok) { const BigBlk& Q = SB[q - sc]; ok = Q.hcanon && (j >= npc || Q.client > cpx); h0q = Q.h0; b1q = Q.b1; }
+        const uint64_t m = __ballot(ok);
+        const uint32_t len = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
+        if (len) {
+          const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)h0q, 0);
+          const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)b1q, (int)len - 1);
+          if (r1 != h0) { if (r1 > r0) o.copy(u0p + r0, r1 - r0); r0 = h0; }
+          r1 = b1; nbo += len; i += len;
+          continue;
+        }
+      }
       const uint64_t cu = i < nb ? SB[i - sc].client : 0, cp = j < npc ? 0xFFFFFFFFull - (L.pc[j].key >> 32) : 0;
       const bool hu = i < nb && (j >= npc || cu >= cp);
       const uint64_t X = hu ? cu : cp;

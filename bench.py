@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 N_DOCS, N_UPDATES = 10000, 200
-PMC_PROFILE = "r01_big_v3/pmc_hbm.json"  # latest committed PMC summary of the bench kernel
+PMC_PROFILE = "r01_big_v4/pmc_hbm.json"  # latest committed PMC summary of the bench kernel
 
 
 def parse():

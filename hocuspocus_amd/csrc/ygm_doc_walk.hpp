@@ -1,0 +1,182 @@
+// ygm_doc_walk.hpp -- encodeStateVectorFromUpdate / diffUpdate fast path (the
+// reconnect-sync shape): ONE LANE PER DOCUMENT, 64 documents of a wave walked side by side, each
+// lane streaming its document through a private ring in LDS.
+//
+// Why lane-per-document: a V1 update is a chain -- every struct's start is the previous struct's
+// end, and a client block's extent is known only by counting its structs.  Splitting one 1-8 KB
+// document over a wave needs a resolution pass per client block (the speculative walks cross block
+// headers blind), which costs more wave instructions than the walk itself; 64 documents give 64
+// independent chains for free.  What made the round-1 walker slow was not the mapping but ~1000
+// VALU per struct (a 64-byte register window shifted by moves, full byte views, per-byte stores)
+// and loads that every iteration waited on.  Here:
+//   * staging: per round each lane loads its next one or two 64-byte chunks (16-byte loads) into
+//     registers; they are written to the lane's ring (4 chunk slots) at the next round start, so a
+//     load has a whole round (DW_R iterations) to land.  No other vector-memory instruction runs
+//     inside the parse iterations: output bytes, copy runs and finished documents are written at
+//     the round start, after the staged loads have been waited on and before new ones are issued
+//     (vmcnt is in order on gfx950: a store issued mid-round would be waited on by the next load
+//     use).
+//   * struct boundaries: when a chunk lands its terminator mask (bit = byte with the top bit clear,
+//     i.e. the end of a varuint) is built by v_dot4 from its 16 dwords and kept in LDS; a struct's
+//     varuint ends are the k-th set bits of the 64-bit mask window at its start (popcount-select:
+//     clear-lowest + ctz), its string bytes are checked ASCII against the same mask, and only the
+//     content-length bytes are read.  Non-minimal varuints (a top-bit byte followed by 0x00) and
+//     varuints of >= 6 bytes are found per chunk from the same masks.
+//   * diff output: the block header (and, when the state vector cuts a struct, its re-encoded
+//     prefix) is written at the round start; the verbatim rest of the client block streams from
+//     the ring to the output in 16-byte pieces as the walk passes it (no second read of the input).
+//
+// Rules: R-SV (yjs Y@37728) and R-D (App. B.2, Y@40711), restated from sv_doc /
+// DiffGen (ygm_seqdoc.hpp), which stay the exact reference for what this kernel defers: content other
+// than String (ASCII) / Deleted / Type / Binary, items with parent info other than 0 / 1, info bit
+// 0x20 beside an origin, GC info bytes other than 0, values >= 2^32, blocks not strictly
+// client-descending or empty, delete sets not strictly client-descending or with empty clients,
+// state vectors of > 16 entries or with trailing bytes, outputs over the slot, documents >= 1 GB.
+#pragma once
+#include "ygm_merge_lean.hpp"
+
+namespace ygm {
+
+constexpr int DW_S = 4;           // 64-byte chunk slots per lane ring
+constexpr int DW_P = DW_S * 4;    // 16-byte pieces per ring
+constexpr int DW_R = 6;           // parse iterations per round (<= 2 staged chunks = 128 bytes per round)
+constexpr int DW_SVN = 16;        // state-vector entries per lane (diff)
+constexpr uint32_t DW_OPEN = 0xFFFFFFFFu;
+
+struct DWLds {
+  u32x4 ring[DW_P][WAVE];         // piece p (16 bytes) of lane l's ring: ring-relative bytes r with (r >> 4) % DW_P == p
+  uint64_t mask[DW_S][WAVE];      // terminator mask of the chunk in each slot (bit i: byte i has its top bit clear)
+};
+
+enum : uint32_t { WK_IDLE = 0, WK_SVN, WK_SVE, WK_UPD, WK_BLK, WK_ST, WK_STR, WK_DS, WK_DSC, WK_DSR, WK_FIN };
+
+YDEV uint64_t dw_lowmask(uint32_t n) { return n >= 64u ? ~0ull : ((1ull << n) - 1ull); }
+YDEV uint32_t dw_ctz(uint64_t x) { return x ? (uint32_t)__builtin_ctzll(x) : 64u; }
+// bits >= p of x (p may be >= 64)
+YDEV uint64_t dw_from(uint64_t x, uint32_t p) { return p >= 64u ? 0ull : (x >> p) << p; }
+// (lo, hi) >> sh for sh in [0, 63]
+YDEV uint64_t dw_fsh(uint64_t lo, uint64_t hi, uint32_t sh) { return (lo >> sh) | ((hi << (63u - sh)) << 1); }
+// bytes of the varuint of v: 1 + floor(bits / 7) for bits = index of the top set bit ((x * 37) >> 8 == x / 7 for x < 64)
+YDEV uint32_t dw_vulen(uint32_t v) { return 1u + (((31u - (uint32_t)__builtin_clz(v | 1u)) * 37u) >> 8); }
+
+// the aligned 8 ring bytes at ring-relative x (x % 8 == 0)
+YDEV uint64_t dw_word(const DWLds& L, uint32_t l, uint32_t x) {
+  return ((const uint64_t*)&L.ring[(x >> 4) & (DW_P - 1)][l])[(x >> 3) & 1u];
+}
+YDEV uint32_t dw_byte(const DWLds& L, uint32_t l, uint32_t r) {
+  return ((const uint8_t*)&L.ring[(r >> 4) & (DW_P - 1)][l])[r & 15u];
+}
+// 16 bytes at ring-relative r as (lo, hi)
+YDEV void dw_rd16(const DWLds& L, uint32_t l, uint32_t r, uint64_t& lo, uint64_t& hi) {
+  const uint32_t A = r & ~7u, sh = (r & 7u) * 8u;
+  const uint64_t w0 = dw_word(L, l, A), w1 = dw_word(L, l, A + 8u), w2 = dw_word(L, l, A + 16u);
+  lo = dw_fsh(w0, w1, sh);
+  hi = dw_fsh(w1, w2, sh);
+}
+YDEV uint64_t dw_rd8(const DWLds& L, uint32_t l, uint32_t r) {
+  const uint32_t A = r & ~7u;
+  return dw_fsh(dw_word(L, l, A), dw_word(L, l, A + 8u), (r & 7u) * 8u);
+}
+// 8 bytes from byte p (p < 16) of the 16-byte view (lo, hi); bytes past the view read as 0
+YDEV uint64_t dw_at(uint64_t lo, uint64_t hi, uint32_t p) { return p >= 8u ? (hi >> (8u * (p - 8u))) : dw_fsh(lo, hi, 8u * p); }
+// 16 ring bytes at any alignment (for the output stream)
+YDEV u32x4 dw_ring16(const DWLds& L, uint32_t l, uint32_t r) {
+  const u32x4 a = L.ring[(r >> 4) & (DW_P - 1)][l], b = L.ring[((r >> 4) + 1u) & (DW_P - 1)][l];
+  const uint32_t s = (r >> 2) & 3u, sh = r & 3u;
+  const uint32_t D[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t E[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    const uint32_t x0 = (s & 1u) ? D[j + 1] : D[j], x1 = (s & 1u) ? D[j + 3 < 8 ? j + 3 : 7] : D[j + 2];
+    E[j] = (s & 2u) ? x1 : x0;
+  }
+  u32x4 o;
+  o.x = __builtin_amdgcn_alignbyte(E[1], E[0], sh);
+  o.y = __builtin_amdgcn_alignbyte(E[2], E[1], sh);
+  o.z = __builtin_amdgcn_alignbyte(E[3], E[2], sh);
+  o.w = __builtin_amdgcn_alignbyte(E[4], E[3], sh);
+  return o;
+}
+// 64-bit terminator window at ring-relative r: bit i = byte r + i ends a varuint.  Chunks not yet
+// landed read as "no terminator" (only used where the segment ends before them).
+YDEV uint64_t dw_win(const DWLds& L, uint32_t l, uint32_t r, uint32_t landed) {
+  const uint32_t k = r >> 6;
+  const uint64_t lo = L.mask[k & (DW_S - 1)][l];
+  const uint64_t hi = k + 1u < landed ? L.mask[(k + 1u) & (DW_S - 1)][l] : 0ull;
+  return dw_fsh(lo, hi, r & 63u);
+}
+// value of the n-byte varuint (n = 1..5) in the low bytes of w; bad when n is outside 1..5 or >= 2^32
+YDEV uint32_t dw_val(uint64_t w, uint32_t n, uint32_t& bad) {
+  bad |= (n - 1u) > 4u ? 1u : 0u;
+  const uint32_t nn = n > 5u ? 5u : (n ? n : 1u);
+  bad |= (nn == 5u && ((w >> 32) & 0x70u)) ? 1u : 0u;
+  return (uint32_t)pext7(w, nn);
+}
+// the bytes [p, p + 8) of the struct at q: from the 16-byte view when p <= 8, else from the ring
+YDEV uint64_t dw_bytes_at(const DWLds& L, uint32_t l, uint32_t q, uint64_t lo, uint64_t hi, uint32_t p) {
+  return p <= 8u ? dw_at(lo, hi, p) : dw_rd8(L, l, q + p);
+}
+// a varString at p of the unit at q (window win): returns the position after it; ASCII only, inside the window
+YDEV uint32_t dw_str(const DWLds& L, uint32_t l, uint32_t q, uint64_t win, uint64_t lo, uint64_t hi, uint32_t p, uint32_t& bad) {
+  const uint32_t e = dw_ctz(dw_from(win, p));
+  const uint32_t n = dw_val(dw_bytes_at(L, l, q, lo, hi, p < 56u ? p : 56u), e - p + 1u, bad);
+  const uint32_t s = e + 1u, f = s + n;
+  bad |= f > 64u ? 1u : 0u;
+  bad |= (s < 64u && ((~win >> s) & dw_lowmask(n))) ? 1u : 0u;
+  return f;
+}
+
+// Writes a chunk to its ring slot and builds its terminator mask; checks the segment part
+// [vlo, vhi) of it for varuints of >= 6 bytes (runs of >= 6 top-bit bytes: values past 2^35, which the
+// walker never takes) and, with BP, for non-minimal varuints (a top-bit byte followed by a zero byte:
+// yjs re-encodes them minimally, so a verbatim copy would differ -- diff only; the state vector is
+// written from values), carrying the previous chunk's last 8 top bits in prev8.
+template <bool BP>
+YDEV void dw_commit(DWLds& L, uint32_t l, uint32_t k, const u32x4& p0, const u32x4& p1, const u32x4& p2, const u32x4& p3,
+                    uint32_t vlo, uint32_t vhi, uint32_t& prev8, uint32_t& bad) {
+  const uint32_t s = k & (DW_S - 1);
+  L.ring[s * 4 + 0][l] = p0;
+  L.ring[s * 4 + 1][l] = p1;
+  L.ring[s * 4 + 2][l] = p2;
+  L.ring[s * 4 + 3][l] = p3;
+  const uint32_t D[16] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};
+  uint64_t H = 0, Z = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint32_t a = D[2 * j], b = D[2 * j + 1];
+    H |= (uint64_t)hibits8(a, b) << (8 * j);
+    if (BP) {
+      const uint32_t za = ~(((a & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | a) & 0x80808080u;
+      const uint32_t zb = ~(((b & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | b) & 0x80808080u;
+      Z |= (uint64_t)hibits8(za, zb) << (8 * j);
+    }
+  }
+  L.mask[s][l] = ~H;
+  const uint64_t vm = dw_lowmask(vhi) & ~dw_lowmask(vlo);
+  const uint64_t Hm = H & vm;
+  const uint64_t r2 = Hm & (Hm >> 1), r4 = r2 & (r2 >> 2), r6 = r4 & (r2 >> 4);
+  const uint32_t c = ((uint32_t)(Hm & 0xFFu) << 8) | prev8;
+  const uint32_t c2 = c & (c >> 1), c4 = c2 & (c2 >> 2), c6 = c4 & (c2 >> 4);
+  uint64_t bp = 0;
+  if (BP) bp = ((Hm << 1) | ((prev8 >> 7) & 1u)) & Z & vm;
+  bad |= (bp | r6 | (uint64_t)c6) ? 1u : 0u;
+  prev8 = (uint32_t)(Hm >> 56);
+}
+
+// byte stores of a varuint at o[t..]; returns the new position
+YDEV uint64_t dw_put_vu(uint8_t* __restrict__ o, uint64_t t, uint32_t v) {
+  while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; }
+  o[t++] = (uint8_t)v;
+  return t;
+}
+// ring bytes [r, r + n) to o[t..]: 16-byte pieces (any alignment on both sides), then single bytes
+YDEV void dw_put_ring(const DWLds& L, uint32_t l, uint8_t* __restrict__ o, uint64_t t, uint32_t r, uint32_t n) {
+  uint32_t k = 0;
+  for (; k + 16u <= n; k += 16u) {
+    const u32x4 v = dw_ring16(L, l, r + k);
+    __builtin_memcpy(o + t + k, &v, 16);
+  }
+  for (; k < n; k++) o[t + k] = (uint8_t)dw_byte(L, l, r + k);
+}
+
+}  // namespace ygm

@@ -23,7 +23,7 @@
 #include "ygm_merge_seq.hpp"
 #include "ygm_merge_wave.hpp"
 #include "ygm_merge_lean.hpp"
-#include "ygm_doc_lean.hpp"
+#include "ygm_doc_walk.hpp"
 #include "ygm_merge_big.hpp"
 #include "ygm_seqdoc.hpp"
 #include "ygm_v1.hpp"
@@ -148,188 +148,547 @@ __global__ __launch_bounds__(DOC_NT) void k_doc(const uint8_t* __restrict__ aren
 }
 
 
-// ======================================================================= SV / diff: lean lane-per-document path
-// ygm_doc_lean.hpp.  MODE 0 = encodeStateVectorFromUpdate (rule R-SV), 1 = diffUpdate (rule R-D).
-// Each lane loops over documents d = global lane, + total lanes; outputs go to the document's
-// slot (merge_slot); documents outside the lean shape are appended to `defer_list` for k_doc.
-enum : uint32_t {   // lean SV / diff walker phases: one unit (header, struct, delete-set entry) per iteration
-  PH_NEXT = 0, PH_SV, PH_UPD, PH_BLOCK, PH_STRUCT, PH_DS, PH_DSC, PH_DSR, PH_FIN
+// ======================================================================= SV / diff: lane-per-document ring walker
+// ygm_doc_walk.hpp.  MODE 0 = encodeStateVectorFromUpdate (rule R-SV), 1 = diffUpdate (rule R-D).
+// Wave w owns documents [n*w/G, n*(w+1)/G); a lane that finishes one takes the wave's next document
+// at the following round start (offsets prefetched one round ahead, handed over by bpermute).
+// Outputs go to the document's slot (merge_slot): the header (a count known only at the end) is
+// written right-aligned in front of the body at slot + 16.  Documents outside the walker's shape are
+// appended to `defer_list` for k_doc.
+YDEV uint64_t dw_shfl64(uint64_t v, uint32_t src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// MODE 1: per-lane state-vector tables, sorted by client descending (the block order), and the
+// scratch of the cooperative parse
+template <int MODE>
+struct DWSvt {
+  uint32_t c[MODE == 1 ? DW_SVN : 1][WAVE], k[MODE == 1 ? DW_SVN : 1][WAVE];
+  uint32_t tc[DW_SVN + 1], tk[DW_SVN + 1];
 };
 
 template <int MODE>
-__global__ __launch_bounds__(WAVE) void k_doc_lean(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                                  const uint64_t* __restrict__ doc_off, const uint8_t* __restrict__ sv_arena,
-                                                  uint64_t sv_bytes, const uint64_t* __restrict__ sv_off, uint32_t n_docs, uint32_t flags,
-                                                  uint8_t* __restrict__ out, uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len,
-                                                  int32_t* __restrict__ status, DocMeta* meta, uint32_t* __restrict__ defer_list,
-                                                  uint64_t out_cap) {
-  // The walk is ONE flat loop per lane: every iteration slides the window to `pos`, builds the view and
-  // masks once and decodes one unit -- a state-vector entry, the update header, a block header, a
-  // struct or a delete-set entry -- so lanes stay in lockstep whatever the block structure of their
-  // documents, and a lane that finishes a document starts its next one in the same loop.
-  __shared__ uint32_t svt[MODE == 1 ? WAVE * DL_SV_MAX * 2 : 1];   // per-lane state-vector table (client, clock)
+__global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off,
+                                                  const uint8_t* __restrict__ sv_arena, const uint64_t* __restrict__ sv_off,
+                                                  uint32_t n_docs, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
+                                                  uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
+                                                  uint32_t* __restrict__ defer_list, uint64_t out_cap) {
+  __shared__ DWLds L;
+  __shared__ DWSvt<MODE> S;
   const uint32_t l = threadIdx.x;
-  const uint64_t lastc = arena_bytes & ~15ull, sv_lastc = sv_bytes & ~15ull;
-  const uint32_t stride = gridDim.x * WAVE;
-  uint64_t payload = 0;
-  uint32_t d = blockIdx.x * WAVE + l - stride;   // PH_NEXT advances it
-  uint32_t phase = PH_NEXT, bad = 0;
-  uint64_t a = 0, b = 0, slot = 0, body0 = 0, tend = 0, t = 0, pos = 0, sb = 0, run0 = 0, ds0 = 0;
-  uint32_t nsv = 0, n_left = 0, nst = 0, st = 0, client = 0, clock = 0, svc = 0, count = 0;
-  uint32_t cc = 0, clk = 0, prev = 0;
-  bool first = true, stop = false, emitted = false, have_prev = false;
-  SWin w;
-  for (;;) {
-    if (phase == PH_NEXT || phase == PH_FIN) {
-      if (phase == PH_FIN) {   // finish the document
-        bad |= pos > b ? 1u : 0u;
-        if (bad) {
-          status[d] = ST_FALLBACK;
-          defer_list[atomicAdd(&meta->lean_defer, 1u)] = d;
-        } else {
-          uint32_t hl = 1; for (uint32_t v = count; v > 127u; v >>= 7) hl++;
-          gw_vu(out, body0 - hl, count);
-          out_off[d] = body0 - hl; out_len[d] = hl + (t - body0); status[d] = ST_OK;
-          payload += hl + (t - body0);
-        }
-      }
-      d += stride;
-      if (d >= n_docs) break;
-      a = doc_off[d]; b = doc_off[d + 1];
-      slot = merge_slot(a, d);
-      const uint64_t cap = merge_slot_cap(b - a);
-      body0 = slot + 16;   // the header (a count known at the end) goes right-aligned in front of the body
-      tend = slot + cap < out_cap ? slot + cap : out_cap;
-      t = body0; bad = (b - a) >> 31 ? 1u : 0u; count = 0; nsv = 0;
-      cc = 0; clk = 0; first = true; stop = false; have_prev = false; prev = 0;
-      if (MODE == 1) { pos = sv_off[d]; sb = sv_off[d + 1]; w.init(sv_arena, pos, sv_lastc); phase = PH_SV; n_left = 0xFFFFFFFFu; }
-      else { pos = a; w.init(arena, a, lastc); phase = PH_UPD; }
-      continue;
-    }
-    const uint64_t lim = phase == PH_SV ? sb : b;
-    w.advance(pos);
-    uint32_t dd[8];
-    w.view(pos, dd);
-    const VMask m = vmask(dd, lim - pos);
-    if (phase != PH_STRUCT) bad |= vcheck(m);
-    if (phase == PH_STRUCT) {
-      const LStruct sx = lean_struct_at(w, pos, b, dd, m);
-      bad |= sx.sbad | vcheck(m);
-      const uint64_t end = (uint64_t)clock + sx.len;
-      bad |= end >> 32 ? 1u : 0u;
-      if (MODE == 0) {   // sv_doc's state machine (rule R-SV)
-        if (first) { cc = client; stop = clock != 0; clk = stop ? 0u : (uint32_t)end; first = false; }
-        if (cc != client) {
-          if (clk) { if (t + 10 > tend) bad = 1; else { t = gw_vu(out, t, cc); t = gw_vu(out, t, clk); count++; } }
-          cc = client; clk = 0; stop = clock != 0;
-        }
-        if (sx.kind == K_SKIP) stop = true;
-        if (!stop) clk = (uint32_t)end;
-      } else if (!emitted && sx.kind != K_SKIP && end > svc && !bad) {
-        // the first written struct of the client (rule R-D): block header, then the struct with offset svc - clock
-        const uint32_t off = svc > clock ? svc - clock : 0u;
-        if (t + 64 + (sx.end - pos) > tend) bad = 1;
-        else {
-          t = gw_vu(out, t, nst - st); t = gw_vu(out, t, client); t = gw_vu(out, t, (uint64_t)clock + off);
-          if (off == 0) { gw_copy(out + t, arena + pos, sx.end - pos); t += sx.end - pos; }
-          else t = lean_write_sliced(out, t, arena, pos, sx, client, clock, off);
-          emitted = true; count++;
-          run0 = sx.end;
-        }
-      }
-      clock = (uint32_t)end;
-      pos = sx.end;
-      if (++st == nst) {   // end of the client block
-        if (MODE == 1 && emitted && !bad) {   // the rest of the block, verbatim (Skips included)
-          if (t + (pos - run0) > tend) bad = 1;
-          else { gw_copy(out + t, arena + run0, pos - run0); t += pos - run0; }
-        }
-        phase = --n_left ? PH_BLOCK : (MODE == 1 ? PH_DS : PH_FIN);
-      }
-    } else if (phase == PH_BLOCK) {
-      const uint32_t e1 = vend(m.T, 0); nst = vval(dd, 0, e1, bad);
-      const uint32_t e2 = vend(m.T, e1 + 1u); client = vval(dd, e1 + 1u, e2, bad);
-      const uint32_t e3 = vend(m.T, e2 + 1u); clock = vval(dd, e2 + 1u, e3, bad);
-      pos += e3 + 1u;
-      if (MODE == 1) {   // canonical (client-descending, distinct) block order; anything else: the exact kernel
-        bad |= (have_prev && client >= prev) ? 1u : 0u;
-        prev = client; have_prev = true;
-        svc = 0;
-        for (uint32_t j = 0; j < nsv; j++) if (svt[(l * DL_SV_MAX + j) * 2] == client) svc = svt[(l * DL_SV_MAX + j) * 2 + 1];
-        emitted = false;
-      }
-      st = 0;
-      if (nst == 0) phase = --n_left ? PH_BLOCK : (MODE == 1 ? PH_DS : PH_FIN);
-      else phase = PH_STRUCT;
-    } else if (phase == PH_UPD) {
-      const uint32_t e = vend(m.T, 0);
-      n_left = vval(dd, 0, e, bad);
-      pos += e + 1u;
-      phase = n_left ? PH_BLOCK : (MODE == 1 ? PH_DS : PH_FIN);
-    } else if (phase == PH_SV) {   // decodeStateVector: the count, then (client, clock) entries; last one per client wins
-      if (n_left == 0xFFFFFFFFu) {
-        const uint32_t e = vend(m.T, 0);
-        n_left = vval(dd, 0, e, bad);
-        pos += e + 1u;
-        bad |= n_left > (uint32_t)DL_SV_MAX ? 1u : 0u;
-      } else {
-        const uint32_t e1 = vend(m.T, 0); const uint32_t cl = vval(dd, 0, e1, bad);
-        const uint32_t e2 = vend(m.T, e1 + 1u); const uint32_t ck = vval(dd, e1 + 1u, e2, bad);
-        pos += e2 + 1u;
-        uint32_t at = nsv;
-        for (uint32_t j = 0; j < nsv; j++) if (svt[(l * DL_SV_MAX + j) * 2] == cl) at = j;
-        if (at < (uint32_t)DL_SV_MAX) { svt[(l * DL_SV_MAX + at) * 2] = cl; svt[(l * DL_SV_MAX + at) * 2 + 1] = ck; }
-        if (at == nsv) nsv++;
-        n_left--;
-      }
-      if (n_left == 0 && !bad) {   // the document itself
-        bad |= pos != sb ? 1u : 0u;   // trailing bytes in a state vector: the exact kernel decides
-        pos = a; w.init(arena, a, lastc); phase = PH_UPD;
-      }
-    } else if (phase == PH_DS) {   // delete set: copied verbatim when readDeleteSet + writeDeleteSet reproduce it
-      ds0 = pos;
-      const uint32_t e = vend(m.T, 0);
-      n_left = vval(dd, 0, e, bad);
-      pos += e + 1u;
-      have_prev = false;
-      if (n_left) phase = PH_DSC;
-      else {   // an empty delete set: its single count byte
-        if (t + (pos - ds0) > tend) bad = 1;
-        else { gw_copy(out + t, arena + ds0, pos - ds0); t += pos - ds0; }
-        phase = PH_FIN;
-      }
-    } else if (phase == PH_DSC) {   // a client entry: distinct clients with >= 1 range, client-descending (13.6)
-      const uint32_t e1 = vend(m.T, 0); const uint32_t cl = vval(dd, 0, e1, bad);
-      const uint32_t e2 = vend(m.T, e1 + 1u); nst = vval(dd, e1 + 1u, e2, bad);   // (nst: ranges left)
-      pos += e2 + 1u;
-      bad |= nst == 0u ? 1u : 0u;
-      if (flags & F_COMPAT_135) bad |= have_prev ? 1u : 0u;   // first-seen order: one client entry only (else exact kernel)
-      else bad |= (have_prev && cl >= prev) ? 1u : 0u;
-      prev = cl; have_prev = true;
-      phase = PH_DSR;
-    } else if (phase == PH_DSR) {   // a (clock, len) range
-      const uint32_t f1 = vend(m.T, 0); (void)vval(dd, 0, f1, bad);
-      const uint32_t f2 = vend(m.T, f1 + 1u); (void)vval(dd, f1 + 1u, f2, bad);
-      pos += f2 + 1u;
-      if (--nst == 0) {
-        if (--n_left == 0) {   // the whole delete set parsed: copy it
-          bad |= pos > b ? 1u : 0u;
-          if (!bad) {
-            if (t + (pos - ds0) > tend) bad = 1;
-            else { gw_copy(out + t, arena + ds0, pos - ds0); t += pos - ds0; }
-          }
-          phase = PH_FIN;
-        } else phase = PH_DSC;
-      }
-    }
-    if (bad) phase = PH_FIN;
-    if (MODE == 0 && phase == PH_FIN && !bad && !first && clk) {   // the last state-vector entry
-      if (t + 10 > tend) bad = 1; else { t = gw_vu(out, t, cc); t = gw_vu(out, t, clk); count++; }
-    }
+  const uint32_t D1 = (uint32_t)((uint64_t)n_docs * (blockIdx.x + 1) / gridDim.x);
+  uint32_t next = (uint32_t)((uint64_t)n_docs * blockIdx.x / gridDim.x);   // wave-uniform: first document not taken
+
+  // offsets of the next 64 documents (lane i: document next + i), loaded one round ahead
+  uint64_t pa = 0, pb = 0, psa = 0, psb = 0;
+  if (next + l < D1) {
+    pa = doc_off[next + l]; pb = doc_off[next + l + 1];
+    if (MODE == 1) { psa = sv_off[next + l]; psb = sv_off[next + l + 1]; }
   }
-  // one atomic per wave for the output bytes
+
+  // ---- lane state
+  uint32_t ph = WK_IDLE, d = 0, bad = 0;
+  uint64_t da = 0, db = 0;                 // the document's bytes in `arena`
+  bool seg_sv = false;                     // segment walked: the state vector (diff) or the document
+  uint64_t cbase = 0;                      // 16-byte aligned segment-arena offset of ring-relative byte 0
+  uint32_t srel = 0, q = 0, rb = 0;        // segment start / parse position / segment end, ring-relative
+  uint32_t landed = 0, stg_n = 0, stg_k = 0, prev8 = 0;
+  u32x4 g0 = {0u, 0u, 0u, 0u}, g1 = g0, g2 = g0, g3 = g0, g4 = g0, g5 = g0, g6 = g0, g7 = g0;   // staged chunks
+  uint32_t n_left = 0, st_left = 0, client = 0, clock = 0, prevc = 0;
+  bool have_prev = false;
+  uint64_t slot = 0;                       // the document's output slot; t / tend / e_dst / cdst relative to it
+  uint8_t* ob = out;                       // out + slot
+  uint32_t tend = 0, t = 0;
+  uint32_t count = 0;
+  uint32_t sp = 0, str_end = 0, ph_after = 0;   // WK_STR: bytes [sp, str_end) of a long string still to check
+  bool str_ascii = false;
+  uint32_t clk = 0, cc = 0;                // MODE 0: the current block's state-vector clock
+  bool stop = false, fst = false;          // fst: the document's first struct (its end counts even for a Skip)
+  // pending output, written at the next round start.  MODE 0: entry (e_a, e_b); MODE 1: block header
+  // (e_a, e_b, e_c) = (structs, client, clock) and, when e_pl > 0, the re-encoded prefix of a cut struct.
+  bool e_on = false;
+  uint32_t e_dst = 0;
+  uint32_t e_a = 0, e_b = 0, e_c = 0, e_pl = 0, e_info = 0, e_oclk = 0, e_q = 0, e_ro_p = 0, e_ro_e = 0, e_clen = 0;
+  // MODE 1: state vector (S.c / S.k [0, nsv), svp = first entry not above the current block's client);
+  // copy run (ring bytes [cp, run_end) -> output at cdst)
+  uint32_t nsv = 0, svp = 0, svc = 0;
+  bool emitted = false, run_on = false;
+  uint32_t cp = 0, run_end = 0, rs0 = 0;
+  uint32_t cdst = 0, cd0 = 0;
+  uint64_t payload = 0;
+  uint32_t rounds = 0;
+#ifdef YGM_DIAG
+  unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // lane-iterations: fast, general, not ready, idle, string; rounds, general iterations
+#define WDG(i, v) dg[i] += (v)
+#else
+#define WDG(i, v)
+#endif
+
+  // end of a client block (after its last struct): MODE 0 queues the block's state-vector entry,
+  // MODE 1 closes the block's copy run
+  auto block_end = [&]() {
+    if (MODE == 0) {
+      if (clk) {
+        const uint32_t el = dw_vulen(cc) + dw_vulen(clk);
+        if (t + el > tend) bad = 1;
+        else { e_on = true; e_dst = t; e_a = cc; e_b = clk; t += el; count++; }
+      }
+      ph = --n_left ? WK_BLK : WK_FIN;
+    } else {
+      if (emitted) {   // the rest of the block, verbatim (Skips included)
+        run_end = q;
+        t = cd0 + (run_end - rs0);
+        bad |= t > tend ? 1u : 0u;
+      }
+      ph = --n_left ? WK_BLK : WK_DS;
+    }
+  };
+  // a block header: canonical blocks are strictly client-descending
+  auto block_begin = [&](uint32_t nst, uint32_t cl, uint32_t ck) {
+    bad |= (nst == 0u || (have_prev && cl >= prevc)) ? 1u : 0u;
+    fst = !have_prev;
+    prevc = cl; have_prev = true;
+    st_left = nst; client = cl; clock = ck;
+    if (MODE == 0) { cc = cl; stop = ck != 0u; clk = 0u; }
+    else {   // the state-vector clock of the client: walk the descending table
+      uint32_t s = 0;
+      while (svp < nsv) {
+        const uint32_t c = S.c[svp][l];
+        if (c > cl) { svp++; continue; }
+        if (c == cl) s = S.k[svp][l];
+        break;
+      }
+      svc = s; emitted = false;
+    }
+    ph = WK_ST;
+  };
+
+  for (;;) {
+    // ---- (1) the chunks staged last round land in the ring (the compiler waits for their loads here)
+    if (stg_n) {
+      dw_commit<MODE == 1>(L, l, stg_k, g0, g1, g2, g3, stg_k == 0u ? srel : 0u, rb - 64u * stg_k < 64u ? rb - 64u * stg_k : 64u, prev8, bad);
+      if (stg_n > 1u) {
+        const uint32_t k1 = stg_k + 1u;
+        dw_commit<MODE == 1>(L, l, k1, g4, g5, g6, g7, 0u, rb - 64u * k1 < 64u ? rb - 64u * k1 : 64u, prev8, bad);
+      }
+      landed = stg_k + stg_n;
+      stg_n = 0;
+    }
+    // ---- (1b) diff: state vectors that have landed are parsed by the whole wave, one after the other
+    //      (byte per lane, terminator ballot, value per varuint end), then sorted by client descending
+    //      into the owner's table, the last entry of a repeated client winning (decodeStateVector's Map)
+    if (MODE == 1) {
+      uint64_t fm = __ballot(ph == WK_SVN && (landed << 6) >= rb);
+      while (fm) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(fm);
+        fm &= fm - 1ull;
+        const uint32_t js = rdlane(srel, j), jn = rdlane(rb, j) - js;
+        uint32_t jb = (jn == 0u || jn > 128u) ? 1u : 0u;
+        const uint32_t blo = l < jn ? dw_byte(L, j, js + l) : 0x80u;
+        const uint32_t bhi = l + 64u < jn ? dw_byte(L, j, js + 64u + l) : 0x80u;
+        const uint64_t T0 = __ballot(blo < 0x80u), T1 = __ballot(bhi < 0x80u);
+        const uint32_t n_ent = rdlane(blo, 0);
+        jb |= (!(T0 & 1ull) || n_ent > (uint32_t)DW_SVN) ? 1u : 0u;
+        jb |= (uint32_t)(__popcll(T0) + __popcll(T1)) != 1u + 2u * n_ent ? 1u : 0u;
+        const uint32_t lastp = T1 ? 127u - (uint32_t)__builtin_clzll(T1) : (T0 ? 63u - (uint32_t)__builtin_clzll(T0) : 0u);
+        jb |= lastp + 1u != jn ? 1u : 0u;   // trailing bytes: the exact kernel decides
+        uint32_t lb = 0;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {   // bytes l and l + 64: a varuint ends here -> its value
+          const uint32_t pos = (uint32_t)h * 64u + l;
+          const bool term = h ? bhi < 0x80u : blo < 0x80u;
+          if (term && pos < jn) {
+            const uint64_t below = h ? (T1 & dw_lowmask(l)) : (T0 & dw_lowmask(l));
+            const uint32_t kk = h ? (uint32_t)__popcll(T0) + (uint32_t)__popcll(below) : (uint32_t)__popcll(below);
+            const uint32_t prevp = h ? (below ? 64u + 63u - (uint32_t)__builtin_clzll(below) : (T0 ? 63u - (uint32_t)__builtin_clzll(T0) : DW_OPEN))
+                                     : (below ? 63u - (uint32_t)__builtin_clzll(below) : DW_OPEN);
+            const uint32_t st0 = prevp + 1u, nb = pos - prevp;
+            const uint32_t v = dw_val(dw_rd8(L, j, js + st0), nb, lb);
+            if (kk >= 1u && kk <= 2u * (uint32_t)DW_SVN) { if (kk & 1u) S.tc[(kk - 1u) >> 1] = v; else S.tk[(kk - 1u) >> 1] = v; }
+          }
+        }
+        jb |= __ballot(lb != 0u) ? 1u : 0u;
+        __syncthreads();
+        const bool ent = l < n_ent && !jb;
+        const uint32_t ec = ent ? S.tc[l] : 0u, ek = ent ? S.tk[l] : 0u;
+        bool drop = false;
+        for (uint32_t e2 = 0; e2 < (jb ? 0u : n_ent); e2++) drop |= e2 > l && rdlane(ec, e2) == ec;
+        const uint64_t keep = __ballot(ent && !drop);
+        uint32_t rank = 0;
+        for (uint32_t e2 = 0; e2 < (jb ? 0u : n_ent); e2++) rank += ((keep >> e2) & 1ull) && rdlane(ec, e2) > ec ? 1u : 0u;
+        if (ent && !drop) { S.c[rank][j] = ec; S.k[rank][j] = ek; }
+        __syncthreads();
+        if (l == j) {   // the document itself next
+          bad |= jb;
+          nsv = (uint32_t)__popcll(keep); svp = 0;
+          seg_sv = false;
+          cbase = da & ~15ull; srel = (uint32_t)(da - cbase); q = srel; rb = (uint32_t)(db - cbase);
+          landed = 0; stg_n = 0; prev8 = 0;
+          ph = WK_UPD;
+        }
+      }
+    }
+    // ---- (2) lanes that are idle or finishing take the wave's next documents
+    const bool want = ph == WK_IDLE || ph == WK_FIN;
+    const uint64_t wm = __ballot(want);
+    const uint32_t rank = lanes_below(wm) & 63u;
+    const uint64_t na = dw_shfl64(pa, rank), nb = dw_shfl64(pb, rank);
+    uint64_t nsa = 0, nsb = 0;
+    if (MODE == 1) { nsa = dw_shfl64(psa, rank); nsb = dw_shfl64(psb, rank); }
+    const uint32_t avail = D1 - next;
+    const bool got = want && rank < avail;
+    const uint32_t nd = next + rank;
+    const uint32_t npop = (uint32_t)__popcll(wm);
+    next += npop < avail ? npop : avail;
+    // ---- (3) output of the last round: pending header / entry, the copy run, finished documents
+    if (e_on) {
+      e_on = false;
+      if (!bad) {
+        uint64_t o = dw_put_vu(ob, e_dst, e_a);
+        o = dw_put_vu(ob, o, e_b);
+        if (MODE == 1) {
+          o = dw_put_vu(ob, o, e_c);
+          if (e_pl) {
+            ob[o++] = (uint8_t)e_info;
+            if (e_info) {   // an item: origin (client, clock + off - 1), right origin verbatim
+              o = dw_put_vu(ob, o, e_b);
+              o = dw_put_vu(ob, o, e_oclk);
+              dw_put_ring(L, l, ob, o, e_q + e_ro_p, e_ro_e - e_ro_p);
+              o += e_ro_e - e_ro_p;
+            }
+            dw_put_vu(ob, o, e_clen);
+          }
+        }
+      }
+    }
+    if (MODE == 1 && run_on) {
+      if (bad) run_on = false;
+      else {
+        const uint32_t done = ph == WK_STR ? sp : q;
+        uint32_t ce = run_end < done ? run_end : done;
+        if (ce < cp) ce = cp;
+        const bool fin = ce == run_end;
+        uint32_t n = ce - cp;
+        if (!fin) n &= ~15u;
+        if (cdst + n > tend) bad = 1;
+        else {
+          dw_put_ring(L, l, ob, cdst, cp, n);
+          cp += n; cdst += n;
+          if (fin) run_on = false;
+        }
+      }
+    }
+    if (ph == WK_FIN) {
+      const uint64_t bm = __ballot(bad != 0u);   // (only finishing lanes reach here)
+      if (bm) {
+        uint32_t base = 0;
+        if (l == (uint32_t)__builtin_ctzll(bm)) base = atomicAdd(&meta->lean_defer, (uint32_t)__popcll(bm));
+        base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(bm));
+        if (bad) { defer_list[base + lanes_below(bm)] = d; status[d] = ST_FALLBACK; }
+      }
+      if (!bad) {
+        const uint32_t hl = dw_vulen(count);
+        dw_put_vu(ob, 16u - hl, count);
+        out_off[d] = slot + 16u - hl; out_len[d] = hl + (t - 16u); status[d] = ST_OK;
+        payload += hl + (t - 16u);
+      }
+      ph = WK_IDLE; run_on = false; e_on = false;
+    }
+    // ---- (4) new documents
+    if (got) {
+      d = nd; bad = 0; da = na; db = nb; count = 0; emitted = false; have_prev = false; nsv = 0; svp = 0;
+      slot = merge_slot(da, d);
+      ob = out + slot;
+      const uint64_t cap = merge_slot_cap(db - da), room = out_cap > slot ? out_cap - slot : 0ull;
+      tend = (uint32_t)(cap < room ? cap : room);
+      t = 16u;   // the header (a count known only at the end) goes right-aligned in front of the body
+      const uint64_t sa = MODE == 1 ? nsa : da, sb = MODE == 1 ? nsb : db;
+      seg_sv = MODE == 1;
+      cbase = sa & ~15ull; srel = (uint32_t)(sa - cbase); q = srel; rb = (uint32_t)(sb - cbase);
+      landed = 0; stg_n = 0; prev8 = 0;
+      bad |= (sb < sa || db < da || ((sb - sa) >> 30) || ((db - da) >> 30)) ? 1u : 0u;
+      ph = MODE == 1 ? WK_SVN : WK_UPD;
+    }
+    if (__ballot(ph != WK_IDLE) == 0 && next >= D1) break;
+    // ---- (5) stage the next chunks of the segment (one or two; the ring keeps DW_S)
+    if (ph != WK_IDLE && ph != WK_FIN) {
+      uint32_t need = ph == WK_STR ? sp : q;
+      if (run_on && cp < need) need = cp;
+      const uint32_t nch = (rb + 63u) >> 6;
+      const uint32_t wk = (need >> 6) + DW_S < nch ? (need >> 6) + DW_S : nch;
+      const uint32_t n = wk > landed ? (wk - landed < 2u ? wk - landed : 2u) : 0u;
+      stg_k = landed; stg_n = n;
+      const u32x4* src = (const u32x4*)((seg_sv ? sv_arena : arena) + cbase + 64ull * landed);
+      if (n >= 1u) { g0 = src[0]; g1 = src[1]; g2 = src[2]; g3 = src[3]; }
+      if (n >= 2u) { g4 = src[4]; g5 = src[5]; g6 = src[6]; g7 = src[7]; }
+    }
+    // ---- (6) offsets of the documents the next round hands out
+    pa = 0; pb = 0; psa = 0; psb = 0;
+    if (next + l < D1) {
+      pa = doc_off[next + l]; pb = doc_off[next + l + 1];
+      if (MODE == 1) { psa = sv_off[next + l]; psb = sv_off[next + l + 1]; }
+    }
+    // ---- (7) parse: per lane and iteration one unit, by the fast decoder when it has the common shape
+    //      (an Item with origin(s) and a one-byte String / Deleted length inside 32 bytes, a block header
+    //      of a <= 2-byte count and a one-byte clock, a one-byte update header, an empty delete set),
+    //      else by the general decoder -- which then runs for the lanes that need it only
+#pragma unroll 1
+    for (int it = 0; it < DW_R; it++) {
+      if (bad && ph != WK_IDLE) ph = WK_FIN;
+      const uint32_t lend = landed << 6;
+      const bool rdy = (q + 64u <= lend) || (lend >= rb);
+      bool done = false;
+      if (rdy && (ph == WK_ST || ph == WK_BLK || ph == WK_UPD || (MODE == 1 && ph == WK_DS))) {
+        const uint32_t kq = q >> 6, sq = q & 63u;
+        const uint64_t m0 = L.mask[kq & (DW_S - 1)][l], m1 = L.mask[(kq + 1u) & (DW_S - 1)][l];
+        // bytes q .. q + 31 (chunks past the segment may hold stale masks: every unit is checked against rb)
+        const uint32_t w32 = (uint32_t)((m0 >> sq) | ((m1 << (63u - sq)) << 1));
+        const uint32_t b0 = dw_byte(L, l, q);
+        if (ph == WK_ST) {   // Item with origin(s), one-byte String (ASCII) / Deleted length, inside 32 bytes
+          const uint32_t hoh = b0 >> 6, ref = b0 & 0x3Fu;
+          const uint32_t tt = w32 >> 1, x2 = tt & (tt - 1u), x3 = x2 & (x2 - 1u), x4 = x3 & (x3 - 1u);
+          const uint32_t cpos = (uint32_t)__builtin_ctz((hoh == 3u ? x4 : x2) | 0x80000000u) + 2u;   // after the origins
+          const uint32_t cq = cpos & 31u;
+          const uint32_t lv = dw_byte(L, l, q + cq);
+          const uint32_t isS = ref == 4u ? 1u : 0u;
+          const uint32_t end = cq + 1u + (isS ? lv : 0u);
+          const uint32_t mk = isS ? (((1u << (lv & 31u)) - 1u) << ((cq + 1u) & 31u)) : 0u;   // the string's bytes: ASCII
+          const uint32_t ce = clock + lv;
+          uint32_t ok = (hoh != 0u) & (isS | (ref == 1u)) & (cpos < 31u) & (w32 >> cq) & (lv != 0u) & (end <= 32u) &
+                        ((w32 & mk) == mk) & (ce >= clock);
+          uint32_t emit = 0;
+          if (MODE == 0) ok &= (st_left != 1u) | !e_on;
+          else {
+            emit = (!emitted) & (ce > svc);
+            ok &= (!emit) | ((svc <= clock) & !e_on & !run_on);   // a cut struct: the general decoder
+          }
+          if (ok) {
+            done = true;
+            if (MODE == 0) {
+              clk = stop ? clk : ce;   // (no Skips here: the first-struct seeding is the same)
+              fst = false;
+            } else if (emit) {
+              const uint32_t hl = dw_vulen(st_left) + dw_vulen(client) + dw_vulen(clock);
+              if (t + hl > tend) bad = 1;
+              else {
+                e_on = true; e_dst = t; e_a = st_left; e_b = client; e_c = clock; e_pl = 0; e_q = q;
+                t += hl;
+                run_on = true; cp = q; rs0 = q; cdst = t; cd0 = t; run_end = DW_OPEN;
+                emitted = true; count++;
+              }
+            }
+            clock = ce;
+            q += end;
+            if (--st_left == 0u) block_end();
+          }
+        } else if (ph == WK_BLK) {   // block header: <= 2-byte count, <= 5-byte client, one-byte clock
+          const uint32_t y = w32 & (w32 - 1u), z = y & (y - 1u);
+          const uint32_t e1 = (uint32_t)__builtin_ctz(w32 | 0x80000000u), e2 = (uint32_t)__builtin_ctz(y | 0x80000000u);
+          const uint32_t e3 = (uint32_t)__builtin_ctz(z | 0x80000000u);
+          const uint32_t b1 = dw_byte(L, l, q + 1u);
+          const uint32_t cn = e2 - e1;   // client bytes
+          const uint64_t cw = dw_rd8(L, l, q + (e1 & 1u) + 1u);
+          const uint32_t nst = e1 == 0u ? b0 : ((b0 & 0x7Fu) | (b1 << 7));
+          const uint32_t ok = (z != 0u) & (e1 <= 1u) & (e3 == e2 + 1u) & (cn - 1u <= 4u) & !((cn == 5u) & (((uint32_t)(cw >> 32) & 0x70u) != 0u));
+          if (ok) {
+            done = true;
+            const uint32_t cl = (uint32_t)pext7(cw, cn);
+            const uint32_t ck = (uint32_t)(cw >> (8u * (cn & 7u))) & 0x7Fu;
+            q += e3 + 1u;
+            block_begin(nst, cl, ck);
+          }
+        } else if (ph == WK_UPD) {
+          if (w32 & 1u) {
+            done = true;
+            q += 1u;
+            if (b0) { n_left = b0; have_prev = false; ph = WK_BLK; }
+            else ph = MODE == 1 ? WK_DS : WK_FIN;
+          }
+        } else if ((w32 & 1u) && b0 == 0u && !run_on) {   // MODE 1 WK_DS: the empty delete set ("00")
+          done = true;
+          run_on = true; cp = q; rs0 = q; cdst = t; cd0 = t;
+          q += 1u; run_end = q; t += 1u;
+          bad |= t > tend ? 1u : 0u;
+          ph = WK_FIN;
+        }
+        if (q > rb) bad = 1;
+      }
+      WDG(0, done ? 1 : 0);
+      WDG(2, (!rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN && ph != WK_STR) ? 1 : 0);
+      WDG(3, (ph == WK_IDLE || ph == WK_FIN || ph == WK_SVN) ? 1 : 0);
+      WDG(4, ph == WK_STR ? 1 : 0);
+      WDG(1, (!done && rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN && ph != WK_STR) ? 1 : 0);
+#ifdef YGM_DIAG
+      if (l == 0) dg[6] += __ballot(!done && rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN && ph != WK_STR) ? 1 : 0;
+#endif
+      if (!done && ph == WK_STR) {   // the rest of a long string (or binary): checked against the chunk masks
+        if (sp < lend) {
+          const uint64_t wn = dw_win(L, l, sp, landed);
+          uint32_t n = str_end - sp;
+          if (n > lend - sp) n = lend - sp;
+          if (n > 64u) n = 64u;
+          if (str_ascii && ((~wn) & dw_lowmask(n))) bad = 1;
+          sp += n;
+          if (sp == str_end) ph = ph_after;
+        }
+      } else if (!done && rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN) {   // ---- the general decoder
+        const uint64_t win = dw_win(L, l, q, landed);
+        uint64_t lo, hi;
+        dw_rd16(L, l, q, lo, hi);
+        if (ph == WK_ST) {
+          const uint32_t info = (uint32_t)lo & 0xFFu;
+          const uint64_t w1 = win & ~1ull;   // terminators after the info byte
+          uint32_t len = 0, end = 0, kind = K_ITEM, ro_p = 0, ro_e = 0, cdata = 0, ref = 0, ho = 0, hr = 0;
+          bool spill = false, sasc = true;
+          if ((info & 31u) == 0u || info == 10u) {   // GC / Skip: varuint length
+            kind = info == 10u ? K_SKIP : K_GC;
+            bad |= (info != 0u && info != 10u) ? 1u : 0u;   // GC written back as info 0 by yjs
+            const uint32_t e = dw_ctz(w1);
+            len = dw_val(dw_at(lo, hi, 1u), e, bad);
+            bad |= len == 0u ? 1u : 0u;
+            end = e + 1u;
+          } else {
+            ref = info & 31u; ho = (info >> 7) & 1u; hr = (info >> 6) & 1u;
+            bad |= ((info & 0xC0u) && (info & 0x20u)) ? 1u : 0u;   // yjs drops the bit on re-encode
+            uint32_t cs;
+            if (ho | hr) {   // origin and/or right origin: two varuints each
+              uint64_t x = w1;
+              const uint32_t t2 = dw_ctz(x & (x - 1ull));
+              x &= x - 1ull; x &= x - 1ull; x &= x - 1ull;
+              const uint32_t t4 = dw_ctz(x);
+              cs = ((ho & hr) ? t4 : t2) + 1u;
+              ro_p = ho ? t2 + 1u : 1u; ro_e = cs;
+            } else {   // parent: parentInfo 1 -> y-key string, 0 -> parent id; parentSub string when bit 0x20
+              const uint32_t pe = dw_ctz(w1);
+              const uint32_t pi = dw_val(dw_at(lo, hi, 1u), pe, bad);
+              bad |= pi > 1u ? 1u : 0u;
+              uint32_t p = pe + 1u;
+              if (pi == 1u) p = dw_str(L, l, q, win, lo, hi, p < 63u ? p : 63u, bad);
+              else { uint64_t x = dw_from(win, p); x &= x - 1ull; p = dw_ctz(x) + 1u; }
+              if (info & 0x20u) p = dw_str(L, l, q, win, lo, hi, p < 63u ? p : 63u, bad);
+              cs = p;
+            }
+            bad |= cs >= 60u ? 1u : 0u;
+            const uint32_t csx = cs < 56u ? cs : 56u;
+            const uint32_t ce = dw_ctz(dw_from(win, csx));
+            const uint32_t v = dw_val(dw_bytes_at(L, l, q, lo, hi, csx), ce - csx + 1u, bad);
+            const uint32_t cend = ce + 1u;
+            if (ref == 1u) {   // ContentDeleted
+              len = v; end = cend;
+              bad |= v == 0u ? 1u : 0u;
+            } else if (ref == 4u || ref == 3u) {   // ContentString (ASCII: UTF-16 length = bytes) / ContentBinary
+              sasc = ref == 4u;
+              len = sasc ? v : 1u; cdata = cend; end = cend + v;
+              bad |= (sasc && v == 0u) ? 1u : 0u;
+              if (end <= 64u) { if (sasc && cdata < 64u && ((~win >> cdata) & dw_lowmask(v))) bad = 1; }
+              else { spill = true; if (sasc && cdata < 64u && (~win >> cdata)) bad = 1; }
+            } else if (ref == 7u) {   // ContentType: typeRef, key for XmlElement / XmlHook
+              len = 1u; end = cend;
+              bad |= v > 6u ? 1u : 0u;
+              if (v == 3u || v == 5u) end = dw_str(L, l, q, win, lo, hi, cend < 63u ? cend : 63u, bad);
+            } else bad = 1;   // JSON / Embed / Format / Any / Doc: the exact kernel
+          }
+          if (!bad) {
+            const uint64_t ce64 = (uint64_t)clock + len;
+            bad |= (ce64 >> 32) ? 1u : 0u;
+            bool emit = false, stall;
+            if (MODE == 0) stall = st_left == 1u && e_on;   // this block's entry needs the entry slot
+            else {
+              emit = !emitted && kind != K_SKIP && ce64 > svc;
+              stall = emit && (e_on || run_on);   // one block header / copy run in flight per lane
+            }
+            if (!stall && !bad) {
+              const uint32_t q0 = q;
+              if (MODE == 0) {
+                if (fst && !stop) clk = (uint32_t)ce64;   // yjs seeds the count with the first struct, Skip or not
+                fst = false;
+                if (kind == K_SKIP) stop = true;
+                if (!stop) clk = (uint32_t)ce64;
+              } else if (emit) {   // the first struct of the client past the state vector (rule R-D)
+                const uint32_t off = svc > clock ? svc - clock : 0u;
+                const uint32_t hck = clock + off;
+                const uint32_t hl = dw_vulen(st_left) + dw_vulen(client) + dw_vulen(hck);
+                uint32_t pl = 0, rstart = q;
+                if (off) {   // cut: GC -> GC(len - off); Deleted / String -> origin (client, clock + off - 1)
+                  if (kind == K_GC) { e_info = 0; e_clen = len - off; pl = 1u + dw_vulen(e_clen); rstart = q + end; }
+                  else {
+                    e_info = ref | 0x80u | (hr ? 0x40u : 0u) | ((!ho && !hr && (info & 0x20u)) ? 0x20u : 0u);
+                    e_oclk = clock + off - 1u;
+                    e_ro_p = hr ? ro_p : 0u; e_ro_e = hr ? ro_e : 0u;
+                    e_clen = len - off;
+                    pl = 1u + dw_vulen(client) + dw_vulen(e_oclk) + (e_ro_e - e_ro_p) + dw_vulen(e_clen);
+                    rstart = ref == 4u ? q + cdata + off : q + end;
+                  }
+                }
+                if (t + hl + pl > tend) bad = 1;
+                else {
+                  e_on = true; e_dst = t; e_a = st_left; e_b = client; e_c = hck; e_pl = pl; e_q = q;
+                  t += hl + pl;
+                  run_on = true; cp = rstart; rs0 = rstart; cdst = t; cd0 = t; run_end = DW_OPEN;
+                  emitted = true; count++;
+                }
+              }
+              clock = (uint32_t)ce64;
+              q += end;
+              if (--st_left == 0u) block_end();
+              if (spill) { sp = q0 + 64u; str_end = q0 + end; str_ascii = sasc; ph_after = ph; ph = WK_STR; }
+            }
+          }
+        } else {   // headers and delete-set entries: up to three varuints
+          uint64_t x = win;
+          const uint32_t e1 = dw_ctz(x); x &= x - 1ull;
+          const uint32_t e2 = dw_ctz(x); x &= x - 1ull;
+          const uint32_t e3 = dw_ctz(x);
+          uint32_t b1 = 0, b2 = e2 >= 16u ? 1u : 0u, b3 = e3 >= 16u ? 1u : 0u;
+          const uint32_t v1 = dw_val(lo, e1 + 1u, b1);
+          const uint32_t v2 = dw_val(dw_at(lo, hi, e1 + 1u < 15u ? e1 + 1u : 15u), e2 - e1, b2);
+          const uint32_t v3 = dw_val(dw_at(lo, hi, e2 + 1u < 15u ? e2 + 1u : 15u), e3 - e2, b3);
+          if (ph == WK_UPD) {
+            bad |= b1;
+            q += e1 + 1u;
+            if (v1) { n_left = v1; have_prev = false; ph = WK_BLK; }
+            else ph = MODE == 1 ? WK_DS : WK_FIN;
+          } else if (ph == WK_DS) {   // the delete set is copied verbatim (readDeleteSet + writeDeleteSet)
+            if (!run_on) {
+              bad |= b1;
+              const uint32_t q0 = q;
+              q += e1 + 1u;
+              run_on = true; cp = q0; rs0 = q0; cdst = t; cd0 = t; run_end = DW_OPEN;
+              if (v1) { n_left = v1; have_prev = false; ph = WK_DSC; }
+              else { run_end = q; t = cd0 + (q - q0); bad |= t > tend ? 1u : 0u; ph = WK_FIN; }
+            }
+          } else if (ph == WK_BLK) {   // client block header: structs, client, first clock
+            bad |= b1 | b2 | b3;
+            q += e3 + 1u;
+            if (!bad) block_begin(v1, v2, v3);
+          } else if (ph == WK_DSC) {   // delete-set client: >= 1 range, clients strictly descending
+            bad |= b1 | b2;
+            q += e2 + 1u;
+            bad |= (v2 == 0u || (have_prev && v1 >= prevc)) ? 1u : 0u;
+            prevc = v1; have_prev = true;
+            st_left = v2; ph = WK_DSR;
+          } else {   // WK_DSR: one (clock, len) range, copied verbatim
+            bad |= e2 >= 64u ? 1u : 0u;
+            q += e2 + 1u;
+            if (--st_left == 0u) {
+              if (--n_left == 0u) { run_end = q; t = cd0 + (q - rs0); bad |= t > tend ? 1u : 0u; ph = WK_FIN; }
+              else ph = WK_DSC;
+            }
+          }
+        }
+        if (q > rb) bad = 1;
+      }
+    }
+    if (++rounds > (1u << 26)) { if (l == 0) atomicOr(&meta->fault, 1u); break; }
+  }
   payload = wave_sum(payload);
   if (l == 0 && payload) add_payload(meta, blockIdx.x, payload);
+#ifdef YGM_DIAG
+  dg[5] = l == 0 ? rounds : 0;
+  for (int i = 0; i < 8; i++) { const unsigned long long v = wave_sum(dg[i]); if (l == 0) atomicAdd(&ygm_diag[16 + i], v); }
+#endif
+#undef WDG
 }
 
 // ======================================================================= merge fast path
@@ -1891,17 +2250,22 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
 int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
                           uint64_t sv_bytes, const uint64_t* sv_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
                           uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
+  (void)arena_bytes; (void)sv_bytes; (void)flags;   // segments are read in 64-byte chunks: 64 bytes of tail padding (ygm.h)
   if (n_docs == 0) return 0;
   static int n_cu = 0;
   if (!n_cu) { int dev = 0; (void)hipGetDevice(&dev); if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256; }
-  const uint32_t waves = (n_docs + WAVE - 1) / WAVE, cap = (uint32_t)n_cu * 16u;   // lane per document, persistent lanes
-  const uint32_t grid = waves < cap ? waves : cap;
+  const char* env = getenv("YGM_WALK_WAVES_PER_CU");
+  const uint32_t wpc = env ? (uint32_t)atoi(env) : (mode == 0 ? 8u : 5u);   // resident waves per CU (LDS 18 / 26 KB per wave)
+  const uint32_t waves = (n_docs + WAVE - 1) / WAVE, cap = (uint32_t)n_cu * (wpc ? wpc : 1u);
+  uint32_t grid = waves < cap ? waves : cap;
+  const char* genv = getenv("YGM_WALK_GRID");   // testing: a small grid gives every lane many documents
+  if (genv && atoi(genv) > 0 && (uint32_t)atoi(genv) < grid) grid = (uint32_t)atoi(genv);
   if (mode == 0)
-    hipLaunchKernelGGL(k_doc_lean<0>, dim3(grid), dim3(WAVE), 0, s, arena, arena_bytes, doc_off, sv_arena, sv_bytes, sv_off, n_docs, flags, out,
-                       out_off, out_len, status, (DocMeta*)meta, defer_list, out_cap);
+    hipLaunchKernelGGL(k_doc_walk<0>, dim3(grid), dim3(WAVE), 0, s, arena, doc_off, sv_arena, sv_off, n_docs, out, out_off, out_len,
+                       status, (DocMeta*)meta, defer_list, out_cap);
   else
-    hipLaunchKernelGGL(k_doc_lean<1>, dim3(grid), dim3(WAVE), 0, s, arena, arena_bytes, doc_off, sv_arena, sv_bytes, sv_off, n_docs, flags, out,
-                       out_off, out_len, status, (DocMeta*)meta, defer_list, out_cap);
+    hipLaunchKernelGGL(k_doc_walk<1>, dim3(grid), dim3(WAVE), 0, s, arena, doc_off, sv_arena, sv_off, n_docs, out, out_off, out_len,
+                       status, (DocMeta*)meta, defer_list, out_cap);
   return launch_rc(__func__);
 }
 

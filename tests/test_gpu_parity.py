@@ -413,6 +413,133 @@ def test_lean_sv_diff_edge_states_vs_oracle(eng):
     assert 0 < took < 2 * len(states)
 
 
+def _walker_states(n_docs, seed):
+    """Merged-state-shaped updates for the SV / diff ring walker: 0-20 client blocks (mostly strictly
+    descending, 5-byte and small clients, first clocks 0 or large), strings of 1-300 bytes (past the
+    64-byte mask window and the 256-byte ring), non-ASCII strings, ContentDeleted, GC (canonical and
+    not), Skips, ContentType with keys, ContentBinary, parent ids / y-keys / parentSub, delete sets
+    (descending or not, empty clients), truncations and trailing bytes."""
+    from v1util import vu
+    rng = random.Random(seed)
+    docs, ends = [], []
+    for _ in range(n_docs):
+        nb = rng.choice([0, 1, 1, 2, 3, 5, 8, 12, 16, 20])
+        cl = set()
+        while len(cl) < nb:
+            cl.add(rng.choice([rng.randrange(1, 2 ** 32), rng.randrange(1, 300), rng.randrange(2 ** 28, 2 ** 32)]))
+        clients = sorted(cl, reverse=True)
+        if nb > 1 and rng.random() < 0.05:
+            rng.shuffle(clients)
+        body = bytearray(vu(nb))
+        end = {}
+        for c in clients:
+            clock = 0 if rng.random() < 0.8 else rng.randrange(1, 2 ** 20)
+            ns = rng.choice([1, 1, 2, 3, 5, 10, 25, 40])
+            b = bytearray()
+            ck = clock
+            for _s in range(ns):
+                r = rng.random()
+                if r < 0.55:
+                    ln = rng.choice([1, 1, 1, 2, 3, 7, 20, 50, 63, 64, 65, 100, 200, 300])
+                    txt = bytes(rng.choice(b"abcdefghij ") for _ in range(ln))
+                    if rng.random() < 0.03:
+                        txt = txt[:-1] + "\u00e9".encode()
+                    shape = rng.random()
+                    if shape < 0.5:
+                        hdr = bytes([0xC4]) + vu(rng.choice(clients)) + vu(rng.randrange(400)) + vu(rng.choice(clients)) + vu(rng.randrange(400))
+                    elif shape < 0.75:
+                        hdr = bytes([0x84]) + vu(rng.choice(clients)) + vu(rng.randrange(400))
+                    elif shape < 0.85:
+                        hdr = bytes([0x44]) + vu(rng.choice(clients)) + vu(rng.randrange(400))
+                    elif shape < 0.93:
+                        sub = rng.random() < 0.4
+                        hdr = bytes([0x24 if sub else 0x04]) + b"\x01" + vu(7) + b"default" + ((vu(3) + b"key") if sub else b"")
+                    else:
+                        hdr = bytes([0x04]) + b"\x00" + vu(rng.choice(clients)) + vu(rng.randrange(50))
+                    b += hdr + vu(len(txt)) + txt
+                    ck += len(txt.decode().encode("utf-16-le")) // 2
+                elif r < 0.7:
+                    n = rng.choice([1, 2, 9, 300, 70000])
+                    b += bytes([0x81]) + vu(rng.choice(clients)) + vu(rng.randrange(400)) + vu(n)
+                    ck += n
+                elif r < 0.78:
+                    n = rng.choice([1, 3, 40])
+                    b += bytes([0x20 if rng.random() < 0.03 else 0x00]) + vu(n)
+                    ck += n
+                elif r < 0.84:
+                    n = rng.choice([1, 5, 200])
+                    b += bytes([10]) + vu(n)
+                    ck += n
+                elif r < 0.92:
+                    if rng.random() < 0.5:
+                        b += bytes([0x87]) + vu(rng.choice(clients)) + vu(rng.randrange(400)) + vu(3) + vu(9) + b"paragraph"
+                    else:
+                        b += bytes([0x87]) + vu(rng.choice(clients)) + vu(rng.randrange(400)) + vu(6)
+                    ck += 1
+                else:
+                    raw = bytes(rng.randrange(256) for _ in range(rng.choice([0, 3, 80])))
+                    b += bytes([0x83]) + vu(rng.choice(clients)) + vu(rng.randrange(400)) + vu(len(raw)) + raw
+                    ck += 1
+            body += vu(ns) + vu(c) + vu(clock) + b
+            end[c] = ck
+        nds = rng.choice([0, 0, 1, 2, 4])
+        dcl = sorted({rng.randrange(1, 2 ** 32) for _ in range(nds)} | set(rng.sample(clients, min(len(clients), 1))) if nds else set(),
+                     reverse=True)
+        if len(dcl) > 1 and rng.random() < 0.1:
+            rng.shuffle(dcl)
+        body += vu(len(dcl))
+        for c in dcl:
+            nr = 0 if rng.random() < 0.03 else rng.choice([1, 1, 2, 5])
+            body += vu(c) + vu(nr)
+            for _r in range(nr):
+                body += vu(rng.randrange(500)) + vu(rng.choice([1, 2, 30]))
+        u = bytes(body)
+        if rng.random() < 0.04 and len(u) > 1:
+            u = u[:rng.randrange(1, len(u))]
+        elif rng.random() < 0.03:
+            u = u + b"\x07"
+        docs.append(u)
+        ends.append(end)
+    return docs, ends
+
+
+def _walker_svs(ends, seed):
+    from v1util import vu
+    rng = random.Random(seed)
+    svs = []
+    for end in ends:
+        ents = [(c, rng.choice([0, e, max(e - 1, 0), rng.randrange(e + 1), e + 3])) for c, e in end.items() if rng.random() < 0.8]
+        if rng.random() < 0.1:
+            ents.append((rng.randrange(1, 2 ** 32), rng.randrange(100)))
+        rng.shuffle(ents)
+        if ents and rng.random() < 0.1:
+            ents.append(ents[0])
+        sv = vu(len(ents)) + b"".join(vu(c) + vu(k) for c, k in ents)
+        if rng.random() < 0.02:
+            sv += b"\x01"
+        svs.append(sv)
+    return svs
+
+
+@pytest.mark.parametrize("grid", [None, "3"])
+def test_walker_states_vs_oracle(eng, grid, monkeypatch):
+    # the SV / diff ring walker on rich merged-state shapes; grid=3 gives every lane ~10 documents
+    # (the per-round hand-over of documents, ring reuse across documents)
+    if grid:
+        monkeypatch.setenv("YGM_WALK_GRID", grid)
+    docs, ends = _walker_states(2000, seed=77)
+    svs = _walker_svs(ends, seed=78)
+    lean0 = eng.stats().docs_lean
+    res = eng.encode_state_vector_from_update_batch(docs)
+    bad = [d for d, u in enumerate(docs) if not same(oracle.encode_state_vector_from_update(u), res[d])]
+    assert not bad, (len(bad), docs[bad[0]].hex())
+    res = eng.diff_update_batch(docs, svs)
+    bad = [d for d, u in enumerate(docs) if not same(oracle.diff_update(u, svs[d]), res[d])]
+    assert not bad, (len(bad), docs[bad[0]].hex(), svs[bad[0]].hex())
+    took = eng.stats().docs_lean - lean0
+    assert len(docs) // 2 < took < 2 * len(docs)   # most documents stay on the walker, some defer
+
+
 def _lean_ds_docs(n_docs, seed):
     """Debounce logs with deletions: struct updates (1-4 clients, clock-contiguous) mixed with
     delete-set-only updates and struct updates carrying a delete set.  The delete sets probe

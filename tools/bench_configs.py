@@ -43,6 +43,8 @@ def c4(n):
         ms = s1.kernel_ms - s0.kernel_ms
         algo = len(arena) + r.payload_bytes + (len(sva) if op == "diff" else 0)
         print(json.dumps({"config": "C4", "op": op, "docs": n, "bytes_in": len(arena), "kernel_ms": round(ms, 3),
+                          "walker_ms": round(s1.lean_ms - s0.lean_ms, 3), "walker_docs": s1.docs_lean - s0.docs_lean,
+                          "exact_docs": s1.docs_fast - s0.docs_fast,
                           "docs_per_s": round(n / ms * 1e3), "algo_GBps": round(algo / ms / 1e6, 1), "gen_s": round(gen, 1)}))
 
 

@@ -9,8 +9,9 @@
  *    characters' ids (exactly what Y.Text.insert records); `del_pct` percent of
  *    the operations are single-character deletes (delete-set-only updates).
  *  text_states: config C4 -- the merged state of such a session written as one
- *    update (client blocks descending, clocks ascending) plus a per-document
- *    state vector with a uniform clock per client (10 % empty).
+ *    update (client blocks descending, clocks ascending; 1-16 clients, log-uniform
+ *    1-8 KB) plus a per-document state vector with a uniform clock per client
+ *    (10 % empty); documents generated in parallel from per-document streams.
  *
  * xorshift64* PRNG; identical bytes for identical (seed, parameters).
  */
@@ -18,6 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <math.h>
+#include <pthread.h>
 
 typedef struct { uint64_t s; } Rng;
 static uint64_t rnext(Rng *r) { uint64_t x = r->s; x ^= x >> 12; x ^= x << 25; x ^= x >> 27; r->s = x; return x * 2685821657736338717ULL; }
@@ -28,19 +30,19 @@ static size_t vu(uint8_t *o, uint64_t v) { size_t n = 0; while (v > 127) { o[n++
 typedef struct { uint32_t client, clock; uint8_t ch; uint8_t deleted; } Ch;
 typedef struct { uint32_t client, clock; uint8_t ch; int32_t oi, ri; uint32_t oc, ok, rc, rk; } Rec;  /* one insert */
 
-/* Runs one document's editing session; returns number of chars, fills recs/ops. */
+/* Runs one document's editing session; returns number of chars, fills recs/ops.
+ * `vis` tracks the visible characters (no scan when nothing was deleted). */
 static int session(Rng *r, int n_ops, int nclients, uint32_t *clients, uint32_t *clocks, Ch *doc, int *ndoc,
                    uint8_t *buf, size_t *blen, uint64_t *upd_off, uint32_t *nupd, int del_pct) {
-  int len = 0; size_t b = *blen;
+  int len = 0, visible = 0, ndel = 0; size_t b = *blen;
   for (int op = 0; op < n_ops; op++) {
     const int ci = (int)rbelow(r, nclients);
     const uint32_t client = clients[ci];
-    int visible = 0; for (int i = 0; i < len; i++) visible += !doc[i].deleted;
     if (visible > 0 && (int)rbelow(r, 100) < del_pct) {
       /* delete one visible char: DS-only update */
       int k = (int)rbelow(r, visible), i = 0;
       for (;; i++) if (!doc[i].deleted && k-- == 0) break;
-      doc[i].deleted = 1;
+      doc[i].deleted = 1; visible--; ndel++;
       upd_off[(*nupd)++] = b;
       buf[b++] = 0;                       /* no structs */
       buf[b++] = 1;                       /* 1 DS client */
@@ -50,12 +52,13 @@ static int session(Rng *r, int n_ops, int nclients, uint32_t *clients, uint32_t 
     }
     /* insert at a uniform visible position; neighbours = adjacent chars in the list */
     int pos = (int)rbelow(r, (uint64_t)visible + 1), at = 0, seen = 0;
-    for (at = 0; at < len; at++) { if (seen == pos) break; if (!doc[at].deleted) seen++; }
+    if (ndel == 0) at = pos;
+    else for (at = 0; at < len; at++) { if (seen == pos) break; if (!doc[at].deleted) seen++; }
     const char ch = "abcdefghijklmnopqrstuvwxyz"[rbelow(r, 26)];
     const int has_o = at > 0, has_r = at < len;
     memmove(doc + at + 1, doc + at, (size_t)(len - at) * sizeof(Ch));
     doc[at].client = client; doc[at].clock = clocks[ci]; doc[at].ch = (uint8_t)ch; doc[at].deleted = 0;
-    len++;
+    len++; visible++;
     upd_off[(*nupd)++] = b;
     buf[b++] = 1; buf[b++] = 1;
     b += vu(buf + b, client); b += vu(buf + b, clocks[ci]);
@@ -99,61 +102,131 @@ size_t synth_text_updates(uint64_t seed, uint32_t n_docs, uint32_t n_updates, ui
 }
 
 /* Config C4: one merged state update per document + a state vector.
- * ops per doc uniform in [min_ops, max_ops].  buf: n_docs*max_ops*40; sv: n_docs*(1+max_clients*16). */
-size_t synth_text_states(uint64_t seed, uint32_t n_docs, uint32_t min_ops, uint32_t max_ops, uint32_t min_clients, uint32_t max_clients,
-                         uint8_t *buf, uint64_t *doc_off, uint8_t *sv, uint64_t *sv_off, size_t *sv_bytes) {
-  Rng r = { seed * 0x9E3779B97F4A7C15ULL + 7 };
+ * Document d is generated from its own PRNG stream (seed, d), so documents are built in parallel
+ * (pthreads) and the bytes do not depend on the thread count.  The op count is log-uniform so that
+ * the state is log-uniform in [min_bytes, max_bytes] (about 16 bytes per one-character Item with both origins).
+ * Two calls: synth_text_states_gen builds the corpus into a handle and returns its sizes;
+ * synth_text_states_take copies it into caller arrays and frees the handle. */
+typedef struct { uint8_t *buf, *sv; uint64_t *doff, *soff; size_t nb, ns; } C4Part;
+typedef struct { uint64_t seed; uint32_t d0, d1, min_cl, max_cl; double lo, hi; C4Part *p; } C4Job;
+
+static void c4_doc(uint64_t seed, uint32_t d, uint32_t ops, uint32_t min_cl, uint32_t max_cl, Rng *r,
+                   Ch *doc, uint8_t *tmp, uint64_t *toff, uint32_t *uidx, C4Part *P) {
+  uint32_t clients[64], clocks[64] = {0};
+  int nc = (int)(min_cl + rbelow(r, max_cl - min_cl + 1));
+  if (nc > 64) nc = 64;
+  pick_clients(r, nc, clients);
+  int nd; size_t tl = 0; uint32_t nu = 0;
+  session(r, (int)ops, nc, clients, clocks, doc, &nd, tmp, &tl, toff, &nu, 0);
+  toff[nu] = tl;
+  /* update index of each (client, clock): inserts of a client arrive in clock order */
+  uint32_t base[65]; base[0] = 0; for (int i = 0; i < nc; i++) base[i + 1] = base[i] + clocks[i];
+  uint32_t fill[64] = {0};
+  for (uint32_t u = 0; u < nu; u++) {
+    const uint8_t *p = tmp + toff[u]; size_t i = 2; uint64_t cl = 0; int sh = 0;
+    do { cl |= (uint64_t)(p[i] & 127) << sh; sh += 7; } while (p[i++] & 128);
+    int ci = 0; while (clients[ci] != (uint32_t)cl) ci++;
+    uidx[base[ci] + fill[ci]++] = u;
+  }
+  /* merged state: client blocks in descending client order; a client's inserts in clock order
+   * (each insert's struct re-emitted from its update: structs start at 2 + vu(client) + vu(clock)) */
+  int ord[64]; for (int i = 0; i < nc; i++) ord[i] = i;
+  for (int i = 1; i < nc; i++) { int t = ord[i], j = i; while (j > 0 && clients[ord[j - 1]] < clients[t]) { ord[j] = ord[j - 1]; j--; } ord[j] = t; }
+  int nblocks = 0; for (int i = 0; i < nc; i++) nblocks += clocks[i] > 0;
+  uint8_t *o = P->buf; size_t b = P->nb;
+  P->doff[d] = b;
+  b += vu(o + b, (uint64_t)nblocks);
+  for (int q = 0; q < nc; q++) {
+    const int ci = ord[q];
+    if (!clocks[ci]) continue;
+    b += vu(o + b, clocks[ci]); b += vu(o + b, clients[ci]); o[b++] = 0;
+    for (uint32_t k = 0; k < clocks[ci]; k++) {
+      const uint32_t u = uidx[base[ci] + k];
+      const uint8_t *p = tmp + toff[u]; size_t i = 2;
+      while (p[i++] & 128) {}
+      while (p[i++] & 128) {}
+      const size_t end = toff[u + 1] - 1; /* drop the update's empty DS byte */
+      memcpy(o + b, p + i, end - toff[u] - i); b += end - toff[u] - i;
+    }
+  }
+  o[b++] = 0; /* empty delete set */
+  P->nb = b;
+  (void)seed;
+  /* state vector: each client with probability 0.9, clock uniform in [0, end] */
+  int empty = rbelow(r, 10) == 0;
+  uint8_t *sp = P->sv + P->ns; size_t sn = 0; int ne = 0;
+  uint8_t ent[64 * 20]; size_t el = 0;
+  if (!empty) for (int i = 0; i < nc; i++) {
+    if (!clocks[i]) continue;
+    el += vu(ent + el, clients[i]); el += vu(ent + el, rbelow(r, (uint64_t)clocks[i] + 1)); ne++;
+  }
+  P->soff[d] = P->ns;
+  sn += vu(sp, (uint64_t)ne); memcpy(sp + sn, ent, el); sn += el; P->ns += sn;
+}
+
+static void *c4_run(void *arg) {
+  C4Job *J = (C4Job *)arg;
+  const uint32_t max_ops = (uint32_t)exp(J->hi) + 2;
   Ch *doc = (Ch *)malloc(sizeof(Ch) * (max_ops + 1));
   uint8_t *tmp = (uint8_t *)malloc((size_t)max_ops * 40 + 64);
   uint64_t *toff = (uint64_t *)malloc(sizeof(uint64_t) * (max_ops + 2));
-  size_t b = 0, s = 0;
-  for (uint32_t d = 0; d < n_docs; d++) {
-    doc_off[d] = b; sv_off[d] = s;
-    uint32_t clients[64], clocks[64] = {0};
-    int nc = (int)(min_clients + rbelow(&r, max_clients - min_clients + 1));
-    if (nc > 64) nc = 64;
-    pick_clients(&r, nc, clients);
-    const int ops = (int)(min_ops + rbelow(&r, max_ops - min_ops + 1));
-    int nd; size_t tl = 0; uint32_t nu = 0;
-    session(&r, ops, nc, clients, clocks, doc, &nd, tmp, &tl, toff, &nu, 0);
-    /* merged state: client blocks in descending client order; a client's inserts in clock order.
-     * Re-emit each insert's struct from the per-update bytes (structs start at offset 2+vu(client)+vu(clock)). */
-    int ord[64]; for (int i = 0; i < nc; i++) ord[i] = i;
-    for (int i = 1; i < nc; i++) { int t = ord[i], j = i; while (j > 0 && clients[ord[j - 1]] < clients[t]) { ord[j] = ord[j - 1]; j--; } ord[j] = t; }
-    int nblocks = 0; for (int i = 0; i < nc; i++) nblocks += clocks[i] > 0;
-    b += vu(buf + b, (uint64_t)nblocks);
-    for (int q = 0; q < nc; q++) {
-      const int ci = ord[q];
-      if (!clocks[ci]) continue;
-      b += vu(buf + b, clocks[ci]); b += vu(buf + b, clients[ci]); buf[b++] = 0;
-      for (uint32_t k = 0; k < clocks[ci]; k++) {
-        /* find update of (client, k): scan updates (insert-only sessions) */
-        for (uint32_t u = 0; u < nu; u++) {
-          const uint8_t *p = tmp + toff[u]; size_t i = 2; uint64_t cl = 0, ck = 0; int sh = 0;
-          do { cl |= (uint64_t)(p[i] & 127) << sh; sh += 7; } while (p[i++] & 128);
-          sh = 0; do { ck |= (uint64_t)(p[i] & 127) << sh; sh += 7; } while (p[i++] & 128);
-          if (cl == clients[ci] && ck == k) {
-            const size_t end = (u + 1 < nu ? toff[u + 1] : tl) - 1; /* drop the update's empty DS byte */
-            memcpy(buf + b, p + i, end - toff[u] - i); b += end - toff[u] - i;
-            break;
-          }
-        }
-      }
-    }
-    buf[b++] = 0; /* empty delete set */
-    /* state vector: each client with probability 0.9, clock uniform in [0, end] */
-    int empty = rbelow(&r, 10) == 0;
-    uint8_t *sp = sv + s; size_t sn = 0; int ne = 0;
-    uint8_t ent[64 * 20]; size_t el = 0;
-    if (!empty) for (int i = 0; i < nc; i++) {
-      if (!clocks[i]) continue;
-      el += vu(ent + el, clients[i]); el += vu(ent + el, rbelow(&r, (uint64_t)clocks[i] + 1)); ne++;
-    }
-    sn += vu(sp, (uint64_t)ne); memcpy(sp + sn, ent, el); sn += el; s += sn;
+  uint32_t *uidx = (uint32_t *)malloc(sizeof(uint32_t) * (max_ops + 2));
+  const size_t n = J->d1 - J->d0;
+  C4Part *P = J->p;
+  size_t cap = 1 << 20, scap = n * (1 + (size_t)J->max_cl * 16) + 64;
+  P->buf = (uint8_t *)malloc(cap); P->sv = (uint8_t *)malloc(scap); P->nb = 0; P->ns = 0;
+  for (uint32_t d = J->d0; d < J->d1; d++) {
+    Rng r = { (J->seed * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)(d + 1) * 0xD1B54A32D192ED03ULL) };
+    rnext(&r); rnext(&r);
+    const double u = (double)(rnext(&r) >> 11) * (1.0 / 9007199254740992.0);
+    const uint32_t ops = (uint32_t)exp(J->lo + u * (J->hi - J->lo));
+    if (P->nb + (size_t)ops * 40 + 64 > cap) { while (P->nb + (size_t)ops * 40 + 64 > cap) cap *= 2; P->buf = (uint8_t *)realloc(P->buf, cap); }
+    c4_doc(J->seed, d - J->d0, ops < 1 ? 1 : ops, J->min_cl, J->max_cl, &r, doc, tmp, toff, uidx, P);
   }
-  doc_off[n_docs] = b; sv_off[n_docs] = s; *sv_bytes = s;
-  free(doc); free(tmp); free(toff);
-  return b;
+  free(doc); free(tmp); free(toff); free(uidx);
+  return NULL;
+}
+
+typedef struct { uint32_t n_docs, n_parts; C4Part *parts; uint32_t *pd0; size_t nb, ns; } C4Handle;
+
+void *synth_text_states_gen(uint64_t seed, uint32_t n_docs, uint32_t min_bytes, uint32_t max_bytes, uint32_t min_clients,
+                            uint32_t max_clients, uint32_t threads, uint64_t *out_bytes, uint64_t *out_sv_bytes) {
+  if (threads < 1) threads = 1;
+  if (threads > n_docs) threads = n_docs ? n_docs : 1;
+  C4Handle *H = (C4Handle *)calloc(1, sizeof(C4Handle));
+  H->n_docs = n_docs; H->n_parts = threads;
+  H->parts = (C4Part *)calloc(threads, sizeof(C4Part));
+  H->pd0 = (uint32_t *)calloc(threads + 1, sizeof(uint32_t));
+  C4Job *jobs = (C4Job *)calloc(threads, sizeof(C4Job));
+  pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
+  const double lo = log((double)min_bytes / 16.0), hi = log((double)max_bytes / 16.0);
+  for (uint32_t t = 0; t < threads; t++) {
+    jobs[t].seed = seed; jobs[t].d0 = (uint32_t)((uint64_t)n_docs * t / threads); jobs[t].d1 = (uint32_t)((uint64_t)n_docs * (t + 1) / threads);
+    jobs[t].min_cl = min_clients; jobs[t].max_cl = max_clients; jobs[t].lo = lo; jobs[t].hi = hi; jobs[t].p = &H->parts[t];
+    H->pd0[t] = jobs[t].d0;
+    const size_t n = jobs[t].d1 - jobs[t].d0;
+    H->parts[t].doff = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1)); H->parts[t].soff = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+    pthread_create(&th[t], NULL, c4_run, &jobs[t]);
+  }
+  H->pd0[threads] = n_docs;
+  for (uint32_t t = 0; t < threads; t++) { pthread_join(th[t], NULL); H->nb += H->parts[t].nb; H->ns += H->parts[t].ns; }
+  free(jobs); free(th);
+  *out_bytes = H->nb; *out_sv_bytes = H->ns;
+  return H;
+}
+
+void synth_text_states_take(void *h, uint8_t *buf, uint64_t *doc_off, uint8_t *sv, uint64_t *sv_off) {
+  C4Handle *H = (C4Handle *)h;
+  size_t b = 0, s = 0;
+  for (uint32_t t = 0; t < H->n_parts; t++) {
+    C4Part *P = &H->parts[t];
+    memcpy(buf + b, P->buf, P->nb); memcpy(sv + s, P->sv, P->ns);
+    for (uint32_t i = 0; i < H->pd0[t + 1] - H->pd0[t]; i++) { doc_off[H->pd0[t] + i] = b + P->doff[i]; sv_off[H->pd0[t] + i] = s + P->soff[i]; }
+    b += P->nb; s += P->ns;
+    free(P->buf); free(P->sv); free(P->doff); free(P->soff);
+  }
+  doc_off[H->n_docs] = b; sv_off[H->n_docs] = s;
+  free(H->parts); free(H->pd0); free(H);
 }
 
 /* ---- configs C3 / C5: [snapshot, ...log] documents of a target size --------------------------

@@ -23,9 +23,12 @@ def lib():
         P = ctypes.c_void_p
         L.synth_text_updates.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P, P, P]
         L.synth_text_updates.restype = ctypes.c_size_t
-        L.synth_text_states.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                                        P, P, P, P, ctypes.POINTER(ctypes.c_size_t)]
-        L.synth_text_states.restype = ctypes.c_size_t
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.synth_text_states_gen.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint32, u64p, u64p]
+        L.synth_text_states_gen.restype = P
+        L.synth_text_states_take.argtypes = [P, P, P, P, P]
+        L.synth_text_states_take.restype = None
         L.synth_big_docs.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                      ctypes.c_uint32, ctypes.c_int, P, P, P]
         L.synth_big_docs.restype = ctypes.c_size_t
@@ -44,16 +47,21 @@ def text_updates(n_docs, n_updates=200, min_clients=1, max_clients=4, del_pct=0,
     return buf[:n].copy(), upd_off, doc_upd
 
 
-def text_states(n_docs, min_ops=40, max_ops=400, min_clients=1, max_clients=16, seed=1):
-    """Config C4: returns (arena, doc_off[n_docs+1], sv_arena, sv_off[n_docs+1])."""
-    buf = np.empty(n_docs * max_ops * 40 + 64, dtype=np.uint8)
+def text_states(n_docs, min_bytes=1024, max_bytes=8192, min_clients=1, max_clients=16, seed=1, threads=None):
+    """Config C4: merged Y.Text states of 1-16 clients, log-uniform 1-8 KB, plus one
+    state vector per document.  Returns (arena, doc_off[n_docs+1], sv_arena, sv_off[n_docs+1]).
+    Documents come from per-document PRNG streams, so the bytes do not depend on `threads`."""
+    if threads is None:
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    nb, ns = ctypes.c_uint64(), ctypes.c_uint64()
+    h = lib().synth_text_states_gen(seed, n_docs, min_bytes, max_bytes, min_clients, max_clients, threads,
+                                    ctypes.byref(nb), ctypes.byref(ns))
+    buf = np.empty(nb.value, dtype=np.uint8)
+    sv = np.empty(ns.value, dtype=np.uint8)
     doc_off = np.empty(n_docs + 1, dtype=np.uint64)
-    sv = np.empty(n_docs * (1 + max_clients * 16) + 64, dtype=np.uint8)
     sv_off = np.empty(n_docs + 1, dtype=np.uint64)
-    svb = ctypes.c_size_t()
-    n = lib().synth_text_states(seed, n_docs, min_ops, max_ops, min_clients, max_clients, buf.ctypes.data, doc_off.ctypes.data,
-                                sv.ctypes.data, sv_off.ctypes.data, ctypes.byref(svb))
-    return buf[:n].copy(), doc_off, sv[:svb.value].copy(), sv_off
+    lib().synth_text_states_take(h, buf.ctypes.data, doc_off.ctypes.data, sv.ctypes.data, sv_off.ctypes.data)
+    return buf, doc_off, sv, sv_off
 
 
 def big_docs(n_docs, max_bytes, min_bytes=1024, max_clients=64, max_k=200, xml=False, seed=1):

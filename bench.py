@@ -1,26 +1,39 @@
-"""Benchmark: batched Y.mergeUpdates on MI355X (BASELINE.json metric, config C2).
+"""Benchmark: batched Y.mergeUpdates / diffUpdate / encodeStateVectorFromUpdate on MI355X
+(BASELINE.json metric "merged update MB/s + docs/sec (bit-exact vs yjs) at 1/2/4/8 MI355X").
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [...]
 
-One step = one batched mergeUpdates over the whole per-GPU workload (10 000
-documents x 200 single-character Y.Text insert updates from 1-4 clients,
-SURVEY.md §8d config C2, BASELINE.json configs[1]) with the inputs already
-resident in HBM: ``ygm_merge_v1_device_async`` = the counter reset and the lean
-kernel launch, each document written into its own output slot.  Steps are enqueued
-back to back on one stream; the last one is completed by ``ygm_merge_v1_device_finish``
-(fault check, payload).  Every C2 document is finished by the lean kernel -- asserted
-on the warmup (identical inputs every step) and on the timed run -- so no step needs
-the host-driven wave / workgroup / sequential tiers.  For N > 1 the
-driver starts one process per GPU (torchrun); every rank merges its own shard
-of documents (documents are independent, partitioned by name hash, weak
-scaling) and the time is the max over ranks.  RCCL carries only the timing
-reduction / stats gather, never data.
+One JSON line (rank 0).  Its headline (`value`, `roofline`, `cpu_baseline`) is config C2
+(BASELINE.json configs[1]): 10 000 documents x 200 single-character Y.Text insert
+updates per GPU, one step = one batched mergeUpdates over all of them with the inputs resident in
+HBM (ygm_merge_v1_device_async: counter reset + the lean kernel; every C2 document is finished by
+the lean kernel -- asserted -- so no step needs the host-driven tiers).  Beside it, as extra keys:
 
-Algorithmic bytes: merge = sum(|inputs|) + |output| per document.
+  c2_100k  the same merge at 100 000 documents per GPU (0.47 GB in: past the 256 MiB Infinity Cache,
+           so the HBM fraction is not L3-served)
+  c4       config C4 (configs[3]): 1 000 000 merged Y.Text states (1-16 clients, log-uniform 1-8 KB,
+           3.2 GB) sharded over the ranks, encodeStateVectorFromUpdate and diffUpdate against per-document
+           state vectors (the mass-reconnect Step1 -> Step2 path, MessageReceiver.ts:137-155)
+  cpu_baseline  the reference yjs path on the GPU box's host cores (yjs 13.5.16 from the image's
+           JupyterLab bundle on Node worker_threads, kind "reference") with the C restatement
+           (oracle/yjs_oracle.c on pthreads, kind "port") nested beside it; c4 carries its own
+
+N > 1: one process per GPU.  Run directly as `python bench.py --gpus N` the script starts N rank
+processes through torch.distributed.run before anything touches a GPU (and exits with their code);
+under torchrun it reads RANK / LOCAL_RANK / WORLD_SIZE.  Documents are named ("c2-<i>", "c4-<i>") and
+each rank takes those with fnv1a64(name) mod N == rank (hocuspocus_amd.shard): C2 is weak-scaled
+(10 000 x N documents in all), C4 strong-scaled (1 000 000 in all).  No update data crosses GPUs: the
+collectives are the barrier, the max-reduction of the timed spans and the node stats gather.
+
+Algorithmic bytes: merge sum(|inputs|) + |output|; diff |u| + |sv| + |out|; state vector
+|u| + |out|.  `roofline.achieved` = one launch's algorithmic bytes / its HIP-event time on the stream
+it ran on; peak 8 TB/s (MI355X_MICROARCH.md).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,8 +43,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
-N_DOCS, N_UPDATES = 10000, 200
-PMC_PROFILE = "r01_big_v4/pmc_hbm.json"  # latest committed PMC summary of the bench kernel
+PMC_PROFILE = "r01_big_v4/pmc_hbm.json"   # committed rocprofv3 PMC summary of the headline kernel (k_merge_lean)
+PMC_C4 = "r02_walk/pmc.json"              # ... of the SV / diff walker at C4
 
 
 def parse():
@@ -39,52 +52,447 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--docs", type=int, default=N_DOCS)
-    ap.add_argument("--updates", type=int, default=N_UPDATES)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
-    ap.add_argument("--big", choices=["c3", "c5"], default=None,
-                    help="instead of the C2 line: one C3 / C5 large-document batch on the GPU next to the CPU oracle "
-                         "over the same documents (reported beside the headline, never as it)")
-    ap.add_argument("--big-docs", type=int, default=None)
+    ap.add_argument("--docs", type=int, default=10000, help="C2 documents per GPU")
+    ap.add_argument("--updates", type=int, default=200)
+    ap.add_argument("--c2big-docs", type=int, default=100000, help="C2 documents per GPU of the c2_100k block (0: skip)")
+    ap.add_argument("--c4-docs", type=int, default=1000000, help="C4 documents in all (0: skip)")
+    ap.add_argument("--c4-steps", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="budget of each CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads / workers (0: the cores granted, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-yjs", action="store_true", help="skip the Node / yjs leg of the CPU baseline")
+    ap.add_argument("--big", choices=["c3", "c5"], default=None,
+                    help="instead of the standard line: one C3 / C5 large-document batch on the GPU next to the CPU oracle")
+    ap.add_argument("--big-docs", type=int, default=None)
+    ap.add_argument("--dry-run", action="store_true", help="no GPU: gloo + the CPU oracle stand in (tests of the rank path)")
     return ap.parse_args()
 
 
-def cpu_baseline(arena, upd_off, doc_upd, budget_s):
-    """The CPU oracle (oracle/yjs_oracle.c: a literal C restatement of yjs mergeUpdates,
-    "port") on a bounded sample of the same workload, one pthread per host core."""
-    import oracle
-    n_docs = len(doc_upd) - 1
-    cores = min(16, os.cpu_count() or 1)
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
-    def run(n, threads):
-        sub_upd = doc_upd[:n + 1]
+
+def spawn_ranks(args):
+    """`python bench.py --gpus N` outside torchrun: N rank processes, started before any GPU call."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_cores(args):
+    if args.cpu_threads:
+        return args.cpu_threads
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+# ----------------------------------------------------------------------------- backends
+class GpuBackend:
+    """Device-resident batches on one MI355X through the C ABI (include/ygm.h)."""
+
+    def __init__(self, local):
+        import torch
+        from hocuspocus_amd import Engine
+        self.torch = torch
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        self.eng = Engine(local)
+        self.stream = torch.cuda.current_stream(self.dev)
+
+    def put(self, a, pad=0):
+        a = np.ascontiguousarray(a)
+        if pad:
+            a = np.concatenate([a.view(np.uint8).reshape(-1), np.zeros(pad, np.uint8)])
+        return self.torch.from_numpy(a).to(self.dev)
+
+    def merge_async(self, c):
+        self.eng.merge_device_async(c["da"].data_ptr(), c["bytes"], c["do"].data_ptr(), c["dd"].data_ptr(), c["n_upd"], c["n"],
+                                    self.stream.cuda_stream)
+
+    def merge_finish(self):
+        return self.eng.merge_device_finish()
+
+    def sv(self, c):
+        return self.eng.sv_device(c["da"].data_ptr(), c["bytes"], c["do"].data_ptr(), c["n"], self.stream.cuda_stream)
+
+    def diff(self, c):
+        return self.eng.diff_device(c["da"].data_ptr(), c["bytes"], c["do"].data_ptr(), c["ds"].data_ptr(), c["dso"].data_ptr(), c["n"],
+                                    self.stream.cuda_stream)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def stats(self):
+        return self.eng.stats()
+
+    def fetch(self, r, n):
+        """(status, off, len, data bytes) of a device result."""
+        self.sync()
+        return (_d2h(r.status, n * 4).view(np.int32), _d2h(r.off, n * 8).view(np.uint64), _d2h(r.len, n * 8).view(np.uint64),
+                _d2h(r.data, int(r.data_bytes)).tobytes())
+
+    def close(self):
+        self.eng.close()
+
+
+class DryBackend:
+    """--dry-run: the CPU oracle stands in for the engine (no timing meaning; tests the rank path)."""
+
+    class _S:
+        def __init__(self):
+            self.kernel_ms = self.lean_ms = 0.0
+            self.lean_launches = self.docs_lean = self.docs_seq = self.docs_fast = 0
+
+    class _R:
+        def __init__(self, payload):
+            self.payload_bytes = payload
+
+    def __init__(self):
+        import oracle
+        self.o = oracle
+        self.s = self._S()
+        self.last = None
+
+    def put(self, a, pad=0):
+        return np.ascontiguousarray(a)
+
+    def _t(self, f, launches, docs):
         t0 = time.perf_counter()
-        st, algo = oracle.merge_batch(arena, upd_off, sub_upd, threads)
+        r = f()
+        ms = (time.perf_counter() - t0) * 1e3
+        self.s.kernel_ms += ms
+        self.s.lean_ms += ms
+        self.s.lean_launches += launches
+        self.s.docs_lean += docs
+        return r
+
+    def merge_async(self, c):
+        st, algo = self._t(lambda: self.o.merge_batch(c["da"], c["do"], c["dd"], 1), 1, 0)
+        self.last = self._R(algo - c["bytes"])
+        self.last_n = c["n"]
+
+    def merge_finish(self):   # (the engine counts a span's documents once, at its finish)
+        self.s.docs_lean += self.last_n
+        return self.last
+
+    def sv(self, c):
+        st, algo = self._t(lambda: self.o.doc_batch("sv", c["da"], c["do"], threads=1), 1, c["n"])
+        return self._R(algo - c["bytes"])
+
+    def diff(self, c):
+        st, algo = self._t(lambda: self.o.doc_batch("diff", c["da"], c["do"], c["ds"], c["dso"], threads=1), 1, c["n"])
+        return self._R(algo - c["bytes"] - c["sv_bytes"])
+
+    def sync(self):
+        pass
+
+    def stats(self):
+        import copy
+        return copy.copy(self.s)
+
+    def close(self):
+        pass
+
+
+def _d2h(src, n):
+    """Copies n bytes of engine-owned device memory to a host numpy array."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    out = np.empty(max(n, 1), np.uint8)
+    if n:
+        assert hip.hipMemcpy(out.ctypes.data, src, n, 2) == 0  # hipMemcpyDeviceToHost
+    return out[:n]
+
+
+def _pmc(name, key):
+    """HBM bytes per launch of a kernel (FETCH_SIZE x2 + WRITE_SIZE from separate rocprofv3 --pmc passes,
+    MI355X_MICROARCH.md §HBM) from the committed profile summary, if any."""
+    p = os.path.join(ROOT, "profiles", name)
+    try:
+        d = json.load(open(p))
+        return d.get(key) if key else d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+# ----------------------------------------------------------------------------- workloads
+def c2_corpus(be, prefix, per_gpu, updates, rank, world):
+    from tools import synth
+    idx = synth.partition(prefix, per_gpu * world, world, rank)
+    arena, upd_off, doc_upd = synth.text_updates_docs(idx, updates)
+    c = {"arena": arena, "upd_off": upd_off, "doc_upd": doc_upd, "n": len(idx), "n_upd": int(doc_upd[-1]), "bytes": len(arena)}
+    c["da"] = be.put(arena, 64)
+    c["do"] = be.put(upd_off.view(np.int64))
+    c["dd"] = be.put(doc_upd.view(np.int32))
+    return c
+
+
+def time_merge(be, c, steps, warmup, dist):
+    """Back-to-back async merges of the whole shard; returns (wall s, kernel ms per launch, payload, stats delta)."""
+    w0 = be.stats()
+    for _ in range(max(warmup, 1)):
+        be.merge_async(c)
+        be.merge_finish()
+    be.sync()
+    s0 = be.stats()
+    assert s0.docs_lean - w0.docs_lean == c["n"] * max(warmup, 1), "not every document takes the lean kernel"
+    if dist:
+        dist.barrier()
+    be.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        be.merge_async(c)
+    be.sync()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    r = be.merge_finish()
+    s1 = be.stats()
+    assert s1.docs_lean - s0.docs_lean == c["n"], "a timed step deferred documents to the host-driven tiers"
+    kms = (s1.lean_ms - s0.lean_ms) / max(s1.lean_launches - s0.lean_launches, 1)
+    return dt, kms, int(r.payload_bytes), r
+
+
+def time_doc(be, c, op, steps, dist):
+    """SV or diff over the whole shard, `steps` times after one warmup; kernel time from the engine's HIP events."""
+    f = be.sv if op == "sv" else be.diff
+    f(c)
+    be.sync()
+    if dist:
+        dist.barrier()
+    s0 = be.stats()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = f(c)
+    be.sync()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    s1 = be.stats()
+    return dt, (s1.kernel_ms - s0.kernel_ms) / steps, r, s1.docs_lean - s0.docs_lean, s1.docs_fast - s0.docs_fast
+
+
+def allmax(x, dist, dev):
+    if not dist:
+        return x
+    import torch
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allsum(xs, dist, dev):
+    if not dist:
+        return list(xs)
+    import torch
+    t = torch.tensor([float(x) for x in xs], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
+def roof(algo_bytes, kernel_ms, kernel, traffic):
+    a = algo_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
+    return {"bound": "hbm", "kernel": kernel, "achieved": round(a, 2) if a else None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(a / HBM_PEAK_GBPS, 5) if a else None, "kernel_ms": round(kernel_ms, 4), "traffic": traffic}
+
+
+# ----------------------------------------------------------------------------- CPU baselines
+def cpu_port_merge(c, cores, budget_s):
+    """oracle/yjs_oracle.c yo_merge_batch (literal C restatement of yjs mergeUpdates incl. V8 TimSort) on a bounded sample."""
+    import oracle
+    n = c["n"]
+
+    def run(k, threads):
+        t0 = time.perf_counter()
+        st, algo = oracle.merge_batch(c["arena"], c["upd_off"], c["doc_upd"][:k + 1], threads)
         return time.perf_counter() - t0, algo, st
 
-    # calibrate on one thread, then size the sample for ~budget_s of all-core work
-    n0 = min(n_docs, 200)
+    n0 = min(n, 200)
     dt0, _, _ = run(n0, 1)
-    per_doc = dt0 / n0
-    sample = int(min(n_docs, max(n0, budget_s * cores / per_doc)))
-    # repeat passes over the sample until ~budget_s of all-core CPU work has been timed
-    dt, algo, reps = 0.0, 0, 0
+    sample = int(min(n, max(n0, budget_s * cores / max(dt0 / n0, 1e-9))))
+    dt = algo = reps = 0
     while reps == 0 or dt * cores < budget_s:
         t, a, st = run(sample, cores)
         assert (st == 0).all()
         dt += t; algo += a; reps += 1
-    return {"value": round(algo / dt / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port",
-            "docs_per_s": round(sample * reps / dt, 1),
-            "sample": f"{reps} pass(es) over {sample} of the {n_docs} C2 documents through oracle/yjs_oracle.c "
-                      f"yo_merge_batch (literal C restatement of yjs mergeUpdates incl. its V8-TimSort decoder "
-                      f"loop), {cores} pthreads, {dt:.2f} s wall"}
+    return {"value": round(algo / dt / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port", "docs_per_s": round(sample * reps / dt, 1),
+            "sample": f"{reps} pass(es) over {sample} of the {n} C2 documents through oracle/yjs_oracle.c yo_merge_batch "
+                      f"(C restatement of yjs mergeUpdates), {cores} pthreads, {dt:.2f} s wall"}
+
+
+def cpu_port_doc(c, op, cores, k):
+    """oracle/yjs_oracle.c yo_doc_batch (C restatement of encodeStateVectorFromUpdate / diffUpdate) over the first k documents."""
+    import oracle
+    t0 = time.perf_counter()
+    if op == "diff":
+        st, algo = oracle.doc_batch("diff", c["arena"], c["doc_off"][:k + 1], c["sva"], c["sv_off"][:k + 1], threads=cores)
+    else:
+        st, algo = oracle.doc_batch("sv", c["arena"], c["doc_off"][:k + 1], threads=cores)
+    dt = time.perf_counter() - t0
+    return {"value": round(algo / dt / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port", "docs_per_s": round(k / dt, 1),
+            "sample": f"the first {k} C4 documents through oracle/yjs_oracle.c yo_doc_batch, {cores} pthreads, {dt:.2f} s wall"}
+
+
+def cpu_yjs(kind, c, cores, k):
+    """yjs 13.5.16 (the image's JupyterLab bundle) on Node worker_threads = cores, over the first k documents."""
+    import shutil
+    import tempfile
+    if shutil.which("node") is None:
+        return None
+    d = tempfile.mkdtemp(prefix="ygm_yjs_")
+    try:
+        if kind == "merge":
+            u_end = int(c["doc_upd"][k])
+            c["arena"][:int(c["upd_off"][u_end])].tofile(os.path.join(d, "arena.bin"))
+            c["upd_off"][:u_end + 1].astype(np.uint64).tofile(os.path.join(d, "off.bin"))
+            c["doc_upd"][:k + 1].astype(np.uint32).tofile(os.path.join(d, "docs.bin"))
+        else:
+            c["arena"][:int(c["doc_off"][k])].tofile(os.path.join(d, "arena.bin"))
+            c["doc_off"][:k + 1].astype(np.uint64).tofile(os.path.join(d, "off.bin"))
+            if kind == "diff":
+                c["sva"][:int(c["sv_off"][k])].tofile(os.path.join(d, "sv.bin"))
+                c["sv_off"][:k + 1].astype(np.uint64).tofile(os.path.join(d, "svoff.bin"))
+        r = subprocess.run(["node", os.path.join(ROOT, "tools", "yjs_cpu_baseline.js"), d, kind, str(cores)], capture_output=True,
+                           text=True, timeout=600)
+        if r.returncode != 0:
+            return {"error": r.stderr[-300:]}
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+        ver = subprocess.run(["node", "--version"], capture_output=True, text=True).stdout.strip()
+        return {"value": round(j["algo_bytes"] / j["seconds"] / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "reference",
+                "docs_per_s": round(k / j["seconds"], 1),
+                "sample": f"yjs 13.5.16 (JupyterLab bundle in the image; the reference pins 13.6.26) Y."
+                          f"{ {'merge': 'mergeUpdates', 'sv': 'encodeStateVectorFromUpdate', 'diff': 'diffUpdate'}[kind]} over the first "
+                          f"{k} documents on Node {ver} worker_threads x {cores}, op loop only, slowest worker {j['seconds']:.2f} s"}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+# ----------------------------------------------------------------------------- the rank
+def run_rank(args, rank, world, dist, be, dev=None):
+    from hocuspocus_amd.shard import gather_stats
+    # ---- headline: C2 merge, 10 000 documents per GPU
+    c = c2_corpus(be, "c2-", args.docs, args.updates, rank, world)
+    dt, kms, out_bytes, r = time_merge(be, c, args.steps, args.warmup, dist)
+    algo = c["bytes"] + out_bytes
+    dt = allmax(dt, dist, dev)
+    node = gather_stats({"docs": c["n"], "updates": c["n_upd"], "bytes_in": c["bytes"], "bytes_out": out_bytes, "kernel_ms": kms}, dist, dev)
+    parity = None
+    if rank == 0 and not args.dry_run:
+        import oracle
+        from tools import synth
+        st, off, ln, data = be.fetch(r, c["n"])
+        ups = synth.split(c["arena"], c["upd_off"])
+        checked = 0
+        for d in range(0, c["n"], max(1, c["n"] // 400)):
+            exp = oracle.merge_updates(ups[c["doc_upd"][d]:c["doc_upd"][d + 1]])
+            assert exp == (int(st[d]), data[int(off[d]):int(off[d]) + int(ln[d])]), f"parity failure on C2 document {d}"
+            checked += 1
+        assert (st == 0).all()
+        parity = f"bit-exact vs oracle on {checked} sampled docs; all {c['n']} statuses OK"
+    line = None
+    if rank == 0:
+        value = (node["bytes_in"] + node["bytes_out"]) * args.steps / dt / 1e6
+        line = {
+            "metric": "merged update MB/s (bit-exact vs yjs mergeUpdates)",
+            "value": round(value, 3), "unit": "MB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded V1 updates from per-document PRNG streams, tools/synth.c; SURVEY.md §8d C2)",
+            "config": {"workload": f"C2: {args.docs} docs x {args.updates} single-char Y.Text insert updates per GPU (documents "
+                                   f"'c2-<i>', i < {args.docs * world}, sharded by fnv1a64(name) mod {world}), 1-4 uint32 clients, "
+                                   "batched Y.mergeUpdates, inputs resident in HBM",
+                       "docs_per_gpu": args.docs, "docs_total": int(node["docs"]), "updates_total": int(node["updates"]),
+                       "bytes_in_total": int(node["bytes_in"]), "bytes_out_total": int(node["bytes_out"]),
+                       "parallelism": f"doc-sharded x{world}"},
+            "docs_per_s": round(node["docs"] * args.steps / dt, 1),
+            "roofline": roof(algo, kms, "k_merge_lean (rank 0; every C2 document is finished by it)", _pmc(PMC_PROFILE, None)),
+            "parity": parity,
+        }
+    del c
+    # ---- C2 at 100 000 documents per GPU (past the Infinity Cache)
+    if args.c2big_docs:
+        cb = c2_corpus(be, "c2b-", args.c2big_docs, args.updates, rank, world)
+        dtb, kmsb, outb, _ = time_merge(be, cb, max(args.steps // 2, 1), 1, dist)
+        dtb = allmax(dtb, dist, dev)
+        tot = allsum([cb["n"], cb["bytes"] + outb], dist, dev)
+        if rank == 0:
+            sb = max(args.steps // 2, 1)
+            line["c2_100k"] = {"docs_per_gpu": args.c2big_docs, "docs_total": int(tot[0]), "steps": sb,
+                               "value": round(tot[1] * sb / dtb / 1e6, 3), "unit": "MB/s", "docs_per_s": round(tot[0] * sb / dtb, 1),
+                               "ms_per_step": round(dtb / sb * 1e3, 4),
+                               "roofline": roof(cb["bytes"] + outb, kmsb, "k_merge_lean (rank 0)", _pmc(PMC_C4, "k_merge_lean@100k"))}
+        del cb
+    # ---- C4: 1M merged states, state vector + diffUpdate (strong scaling over the ranks)
+    if args.c4_docs:
+        from tools import synth
+        idx = synth.partition("c4-", args.c4_docs, world, rank)
+        arena, doc_off, sva, sv_off = synth.text_states(0, seed=3, idx=idx)
+        c = {"arena": arena, "doc_off": doc_off, "sva": sva, "sv_off": sv_off, "n": len(idx), "bytes": len(arena), "sv_bytes": len(sva)}
+        c["da"] = be.put(arena, 64)
+        c["do"] = be.put(doc_off.view(np.int64))
+        c["ds"] = be.put(sva, 64)
+        c["dso"] = be.put(sv_off.view(np.int64))
+        blk = {"docs_total": args.c4_docs, "bytes_in_total": None, "steps": args.c4_steps,
+               "workload": f"C4: {args.c4_docs} merged Y.Text states 'c4-<i>' (1-16 clients, log-uniform 1-8 KB, one state "
+                           f"vector each, 10 % empty) sharded by fnv1a64(name) mod {world}, inputs resident in HBM"}
+        for op in ("sv", "diff"):
+            dto, kmo, ro, lean, exact = time_doc(be, c, op, args.c4_steps, dist)
+            algo = c["bytes"] + int(ro.payload_bytes) + (c["sv_bytes"] if op == "diff" else 0)
+            dto = allmax(dto, dist, dev)
+            tot = allsum([algo, c["n"], c["bytes"]], dist, dev)
+            if rank == 0:
+                blk["bytes_in_total"] = int(tot[2])
+                pr = None
+                if not args.dry_run:
+                    import oracle
+                    st, off, ln, data = be.fetch(ro, c["n"])
+                    checked = 0
+                    for d in range(0, c["n"], max(1, c["n"] // 300)):
+                        u = arena[doc_off[d]:doc_off[d + 1]].tobytes()
+                        exp = oracle.encode_state_vector_from_update(u) if op == "sv" else oracle.diff_update(u, sva[sv_off[d]:sv_off[d + 1]].tobytes())
+                        got = (int(st[d]), data[int(off[d]):int(off[d]) + int(ln[d])] if st[d] == 0 else None)
+                        assert exp == got, f"parity failure on C4 document {d} ({op})"
+                        checked += 1
+                    pr = f"bit-exact vs oracle on {checked} sampled docs"
+                blk[op] = {"value": round(tot[0] * args.c4_steps / dto / 1e6, 3), "unit": "MB/s",
+                           "docs_per_s": round(tot[1] * args.c4_steps / dto, 1), "ms_per_step": round(dto / args.c4_steps * 1e3, 4),
+                           "walker_docs_rank0": int(lean), "exact_kernel_docs_rank0": int(exact),
+                           "roofline": roof(algo, kmo, f"k_doc_walk<{0 if op == 'sv' else 1}> + k_doc for deferred docs (rank 0)",
+                                            _pmc(PMC_C4, f"k_doc_walk<{0 if op == 'sv' else 1}>")),
+                           "parity": pr}
+        if rank == 0:
+            line["c4"] = blk
+        c4 = c
+    # ---- CPU baselines (rank 0 at N = 1 only)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
+        cores = cpu_cores(args)
+        from tools import synth
+        idx = synth.partition("c2-", args.docs, 1, 0)
+        a2, o2, d2 = synth.text_updates_docs(idx, args.updates)
+        c2 = {"arena": a2, "upd_off": o2, "doc_upd": d2, "n": len(idx)}
+        port = cpu_port_merge(c2, cores, args.cpu_seconds)
+        y = None if args.no_yjs else cpu_yjs("merge", c2, cores, min(c2["n"], 4000))
+        if y and "value" in y:
+            line["cpu_baseline"] = dict(y, port=port, os_cpu_count=os.cpu_count())
+        else:
+            line["cpu_baseline"] = dict(port, yjs=y, os_cpu_count=os.cpu_count())
+        if args.c4_docs:
+            for op in ("sv", "diff"):
+                e = {"port": cpu_port_doc(c4, op, cores, min(c4["n"], 200000))}
+                if not args.no_yjs:
+                    e["yjs"] = cpu_yjs(op, c4, cores, min(c4["n"], 60000))
+                line["c4"][op]["cpu_baseline"] = e
+    return line
 
 
 def big_line(args):
     """C3 / C5 ([snapshot, ...log] large documents): the whole batch merged on cuda:0
     (device-resident inputs, host-driven tier cascade, kernel time from the engine's HIP events) and
-    by the CPU oracle on all host threads over the same documents."""
+    by the CPU oracle on the host threads over the same documents."""
     import torch
     import oracle
     from hocuspocus_amd import Engine
@@ -106,7 +514,7 @@ def big_line(args):
         s1 = e.stats()
     ms = s1.kernel_ms - s0.kernel_ms
     algo = len(arena) + r.payload_bytes
-    cores = min(16, os.cpu_count() or 1)
+    cores = cpu_cores(args)
     t0 = time.perf_counter()
     st, calgo = oracle.merge_batch(arena, upd_off, doc_upd, cores)
     cdt = time.perf_counter() - t0
@@ -124,150 +532,33 @@ def main():
     args = parse()
     if args.big:
         return big_line(args)
+    in_torchrun = "WORLD_SIZE" in os.environ
+    if args.gpus > 1 and not in_torchrun:
+        sys.exit(spawn_ranks(args))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    import torch
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    from hocuspocus_amd import Engine
-    from tools import synth
-
-    # ---- this rank's shard: documents whose name hash maps to this rank (seeded per rank)
-    arena, upd_off, doc_upd = synth.text_updates(args.docs, args.updates, seed=1000 + rank)
-    n_upd = int(doc_upd[-1])
-    dev = torch.device("cuda", local)
-    d_arena = torch.from_numpy(np.concatenate([arena, np.zeros(64, np.uint8)])).to(dev)
-    d_off = torch.from_numpy(upd_off.view(np.int64)).to(dev)
-    d_doc = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
-    stream = torch.cuda.current_stream(dev)
-    eng = Engine(local)
-
-    def step():
-        # one batched merge of the shard, enqueued on the stream (counter reset + lean kernel);
-        # back-to-back steps pipeline.  Every document of this workload is finished by the lean
-        # kernel (asserted on the warmup below: the inputs are identical in every step), so each
-        # enqueued step is a complete merge without the host-driven tiers of finish().
-        eng.merge_device_async(d_arena.data_ptr(), len(arena), d_off.data_ptr(), d_doc.data_ptr(), n_upd, args.docs,
-                               stream.cuda_stream)
-
-    w0 = eng.stats()
-    for _ in range(max(args.warmup, 1)):
-        step()
-        eng.merge_device_finish()
-    torch.cuda.synchronize()
-    s0 = eng.stats()
-    assert s0.docs_lean - w0.docs_lean == args.docs * max(args.warmup, 1), "not every document takes the lean kernel"
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    # finish the last step: fault check, payload (and no deferred document, as on the warmup)
-    r = eng.merge_device_finish()
-    s1 = eng.stats()
-    assert s1.docs_lean - s0.docs_lean == args.docs, "a timed step deferred documents to the host-driven tiers"
-
-    out_bytes = int(r.payload_bytes)                 # sum of the merged outputs' lengths
-    algo_bytes = len(arena) + out_bytes              # per step, this rank
-    # HIP events on the launch stream: one span over the timed back-to-back lean launches
-    kernel_ms = (s1.lean_ms - s0.lean_ms) / max(s1.lean_launches - s0.lean_launches, 1)
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)   # the job's time = the slowest rank
-    dt = float(t.item())
-    # node-wide stats all-gather (the only other collective; no update data crosses GPUs)
-    from hocuspocus_amd.shard import gather_stats
-    node = gather_stats({"docs": args.docs, "updates": n_upd, "bytes_in": len(arena), "bytes_out": out_bytes,
-                         "docs_seq": s1.docs_seq - s0.docs_seq, "kernel_ms": kernel_ms}, dist, dev)
-    all_bytes, all_docs = node["bytes_in"] + node["bytes_out"], node["docs"]
-
-    # ---- parity spot-check of the timed outputs (rank 0 sample vs the CPU oracle)
-    parity = None
+    if in_torchrun:
+        assert world == args.gpus, f"WORLD_SIZE {world} != --gpus {args.gpus}"
+    dist, dev = None, None
+    if args.dry_run:
+        be = DryBackend()
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+    else:
+        import torch
+        be = GpuBackend(local)
+        dev = be.dev
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    line = run_rank(args, rank, world, dist, be, dev)
     if rank == 0:
-        import oracle
-        n = args.docs
-        torch.cuda.synchronize()
-        off = _d2h(r.off, n * 8).view(np.uint64)
-        ln = _d2h(r.len, n * 8).view(np.uint64)
-        st = _d2h(r.status, n * 4).view(np.int32)
-        hdata = _d2h(r.data, int(r.data_bytes)).tobytes()
-        ups = synth.split(arena, upd_off)
-        checked = 0
-        for dd in range(0, n, max(1, n // 400)):
-            exp = oracle.merge_updates(ups[doc_upd[dd]:doc_upd[dd + 1]])
-            got = (int(st[dd]), hdata[int(off[dd]):int(off[dd]) + int(ln[dd])])
-            assert exp == got, f"parity failure on document {dd}"
-            checked += 1
-        assert (st == 0).all()
-        parity = f"bit-exact vs oracle on {checked} sampled docs; all {n} statuses OK"
-
-    if rank == 0:
-        value = all_bytes * args.steps / dt / 1e6
-        achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
-        line = {
-            "metric": "merged update MB/s (bit-exact vs yjs mergeUpdates)",
-            "value": round(value, 3),
-            "unit": "MB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (seeded V1 updates, tools/synth.c; SURVEY.md §8d C2)",
-            "config": {"workload": f"C2: {args.docs} docs x {args.updates} single-char Y.Text insert updates per GPU, "
-                                   "1-4 uint32 clients, batched Y.mergeUpdates, inputs resident in HBM",
-                       "docs_per_gpu": args.docs, "updates_per_gpu": n_upd, "bytes_in_per_gpu": len(arena),
-                       "bytes_out_per_gpu": out_bytes, "parallelism": f"doc-sharded x{world}"},
-            "docs_per_s": round(all_docs * args.steps / dt, 1),
-            "roofline": {"bound": "hbm", "kernel": "k_merge_lean (+ k_merge_wave / k_merge_fast / k_merge_big / k_merge_seq for deferred docs)",
-                         "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 5) if achieved else None,
-                         "kernel_ms": round(kernel_ms, 4), "traffic": _pmc_traffic()},
-            "parity": parity,
-            "seq_kernel_docs": node["docs_seq"],
-        }
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(arena, upd_off, doc_upd, args.cpu_seconds)
         print(json.dumps(line), flush=True)
-    eng.close()
+    be.close()
     if dist:
         dist.destroy_process_group()
-
-
-def _d2h(src, n):
-    """Copies n bytes of engine-owned device memory to a host numpy array."""
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    out = np.empty(max(n, 1), np.uint8)
-    if n:
-        assert hip.hipMemcpy(out.ctypes.data, src, n, 2) == 0  # hipMemcpyDeviceToHost
-    return out[:n]
-
-
-def _pmc_traffic():
-    """HBM bytes per k_merge_wave launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc passes of this
-    same command; tools/prof_summary.py) from the committed profile, if any."""
-    p = os.path.join(ROOT, "profiles", PMC_PROFILE)
-    if os.path.exists(p):
-        try:
-            return json.load(open(p)).get("hbm_bytes_per_launch")
-        except Exception:
-            return None
-    return None
 
 
 if __name__ == "__main__":

@@ -39,7 +39,8 @@ namespace ygm {
 
 constexpr int DW_S = 4;           // 64-byte chunk slots per lane ring
 constexpr int DW_P = DW_S * 4;    // 16-byte pieces per ring
-constexpr int DW_R = 6;           // parse iterations per round (<= 2 staged chunks = 128 bytes per round)
+constexpr int DW_R = 4;           // parse iterations per round (<= 3 staged chunks = 192 bytes per round)
+constexpr int DW_BATCH = 256;     // documents sorted (largest first) per batch of a wave's range
 constexpr int DW_SVN = 16;        // state-vector entries per lane (diff)
 constexpr uint32_t DW_OPEN = 0xFFFFFFFFu;
 

@@ -176,16 +176,23 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
                                                   uint32_t* __restrict__ defer_list, uint64_t out_cap) {
   __shared__ DWLds L;
   __shared__ DWSvt<MODE> S;
+  __shared__ uint64_t ordk[DW_BATCH];      // the current batch of documents, largest first: (bytes << 32 | index in batch)
   const uint32_t l = threadIdx.x;
   const uint32_t D1 = (uint32_t)((uint64_t)n_docs * (blockIdx.x + 1) / gridDim.x);
-  uint32_t next = (uint32_t)((uint64_t)n_docs * blockIdx.x / gridDim.x);   // wave-uniform: first document not taken
+  uint32_t bnext = (uint32_t)((uint64_t)n_docs * blockIdx.x / gridDim.x);   // wave-uniform: first document of the next batch
+  uint32_t bbase = bnext, bn = 0, next = 0;                                  // the batch [bbase, bbase + bn); next: its first untaken entry
 
-  // offsets of the next 64 documents (lane i: document next + i), loaded one round ahead
+  // offsets of the next 64 documents of the batch (lane i: entry next + i), loaded one round ahead
+  uint32_t pd = 0;
   uint64_t pa = 0, pb = 0, psa = 0, psb = 0;
-  if (next + l < D1) {
-    pa = doc_off[next + l]; pb = doc_off[next + l + 1];
-    if (MODE == 1) { psa = sv_off[next + l]; psb = sv_off[next + l + 1]; }
-  }
+  auto prefetch = [&]() {
+    pa = 0; pb = 0; psa = 0; psb = 0; pd = 0;
+    if (next + l < bn) {
+      pd = bbase + (uint32_t)ordk[next + l];
+      pa = doc_off[pd]; pb = doc_off[pd + 1];
+      if (MODE == 1) { psa = sv_off[pd]; psb = sv_off[pd + 1]; }
+    }
+  };
 
   // ---- lane state
   uint32_t ph = WK_IDLE, d = 0, bad = 0;
@@ -195,6 +202,7 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
   uint32_t srel = 0, q = 0, rb = 0;        // segment start / parse position / segment end, ring-relative
   uint32_t landed = 0, stg_n = 0, stg_k = 0, prev8 = 0;
   u32x4 g0 = {0u, 0u, 0u, 0u}, g1 = g0, g2 = g0, g3 = g0, g4 = g0, g5 = g0, g6 = g0, g7 = g0;   // staged chunks
+  u32x4 g8 = g0, g9 = g0, g10 = g0, g11 = g0;
   uint32_t n_left = 0, st_left = 0, client = 0, clock = 0, prevc = 0;
   bool have_prev = false;
   uint64_t slot = 0;                       // the document's output slot; t / tend / e_dst / cdst relative to it
@@ -265,12 +273,37 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
   };
 
   for (;;) {
+    // ---- (0) a new batch of documents: sorted by size, largest first (the documents left at the end of a
+    //      wave's range are its smallest: the last lanes to finish wait least)
+    if (next >= bn && bnext < D1) {
+      bbase = bnext; bn = D1 - bnext < (uint32_t)DW_BATCH ? D1 - bnext : (uint32_t)DW_BATCH; bnext = bbase + bn; next = 0;
+      for (uint32_t e = l; e < (uint32_t)DW_BATCH; e += WAVE) {
+        // key bytes + 1 (padding entries past bn: 0, sorted behind every document)
+        const uint64_t sz = e < bn ? doc_off[bbase + e + 1] - doc_off[bbase + e] + 1ull : 0ull;
+        ordk[e] = ((sz < 0xFFFFFFFFull ? sz : 0xFFFFFFFFull) << 32) | e;
+      }
+      __syncthreads();
+      for (uint32_t kk = 2; kk <= (uint32_t)DW_BATCH; kk <<= 1)
+        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+          for (uint32_t t2 = l; t2 < (uint32_t)DW_BATCH / 2; t2 += WAVE) {
+            const uint32_t lo = ((t2 / jj) * 2 * jj) + (t2 % jj), hi = lo + jj;
+            const uint64_t x = ordk[lo], y = ordk[hi];
+            if ((x < y) == ((lo & kk) == 0)) { ordk[lo] = y; ordk[hi] = x; }   // descending
+          }
+          __syncthreads();
+        }
+      prefetch();
+    }
     // ---- (1) the chunks staged last round land in the ring (the compiler waits for their loads here)
     if (stg_n) {
       dw_commit<MODE == 1>(L, l, stg_k, g0, g1, g2, g3, stg_k == 0u ? srel : 0u, rb - 64u * stg_k < 64u ? rb - 64u * stg_k : 64u, prev8, bad);
       if (stg_n > 1u) {
         const uint32_t k1 = stg_k + 1u;
         dw_commit<MODE == 1>(L, l, k1, g4, g5, g6, g7, 0u, rb - 64u * k1 < 64u ? rb - 64u * k1 : 64u, prev8, bad);
+      }
+      if (stg_n > 2u) {
+        const uint32_t k2 = stg_k + 2u;
+        dw_commit<MODE == 1>(L, l, k2, g8, g9, g10, g11, 0u, rb - 64u * k2 < 64u ? rb - 64u * k2 : 64u, prev8, bad);
       }
       landed = stg_k + stg_n;
       stg_n = 0;
@@ -334,11 +367,11 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
     const uint64_t wm = __ballot(want);
     const uint32_t rank = lanes_below(wm) & 63u;
     const uint64_t na = dw_shfl64(pa, rank), nb = dw_shfl64(pb, rank);
+    const uint32_t nd = (uint32_t)__shfl((int)pd, (int)rank);
     uint64_t nsa = 0, nsb = 0;
     if (MODE == 1) { nsa = dw_shfl64(psa, rank); nsb = dw_shfl64(psb, rank); }
-    const uint32_t avail = D1 - next;
+    const uint32_t avail = bn - next;
     const bool got = want && rank < avail;
-    const uint32_t nd = next + rank;
     const uint32_t npop = (uint32_t)__popcll(wm);
     next += npop < avail ? npop : avail;
     // ---- (3) output of the last round: pending header / entry, the copy run, finished documents
@@ -410,25 +443,22 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
       bad |= (sb < sa || db < da || ((sb - sa) >> 30) || ((db - da) >> 30)) ? 1u : 0u;
       ph = MODE == 1 ? WK_SVN : WK_UPD;
     }
-    if (__ballot(ph != WK_IDLE) == 0 && next >= D1) break;
-    // ---- (5) stage the next chunks of the segment (one or two; the ring keeps DW_S)
+    if (__ballot(ph != WK_IDLE) == 0 && next >= bn && bnext >= D1) break;
+    // ---- (5) stage the next chunks of the segment (up to three; the ring keeps DW_S)
     if (ph != WK_IDLE && ph != WK_FIN) {
       uint32_t need = ph == WK_STR ? sp : q;
       if (run_on && cp < need) need = cp;
       const uint32_t nch = (rb + 63u) >> 6;
       const uint32_t wk = (need >> 6) + DW_S < nch ? (need >> 6) + DW_S : nch;
-      const uint32_t n = wk > landed ? (wk - landed < 2u ? wk - landed : 2u) : 0u;
+      const uint32_t n = wk > landed ? (wk - landed < 3u ? wk - landed : 3u) : 0u;
       stg_k = landed; stg_n = n;
       const u32x4* src = (const u32x4*)((seg_sv ? sv_arena : arena) + cbase + 64ull * landed);
       if (n >= 1u) { g0 = src[0]; g1 = src[1]; g2 = src[2]; g3 = src[3]; }
       if (n >= 2u) { g4 = src[4]; g5 = src[5]; g6 = src[6]; g7 = src[7]; }
+      if (n >= 3u) { g8 = src[8]; g9 = src[9]; g10 = src[10]; g11 = src[11]; }
     }
     // ---- (6) offsets of the documents the next round hands out
-    pa = 0; pb = 0; psa = 0; psb = 0;
-    if (next + l < D1) {
-      pa = doc_off[next + l]; pb = doc_off[next + l + 1];
-      if (MODE == 1) { psa = sv_off[next + l]; psb = sv_off[next + l + 1]; }
-    }
+    prefetch();
     // ---- (7) parse: per lane and iteration one unit, by the fast decoder when it has the common shape
     //      (an Item with origin(s) and a one-byte String / Deleted length inside 32 bytes, a block header
     //      of a <= 2-byte count and a one-byte clock, a one-byte update header, an empty delete set),
@@ -437,50 +467,61 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
     for (int it = 0; it < DW_R; it++) {
       if (bad && ph != WK_IDLE) ph = WK_FIN;
       const uint32_t lend = landed << 6;
-      const bool rdy = (q + 64u <= lend) || (lend >= rb);
+      const bool rdy = (q + 64u <= lend) || (lend >= rb);   // the general decoder reads up to 64 bytes ahead
+      // the fast decoders take a unit whose bytes have all landed (masks past lend are stale: a unit
+      // that ends there is refused and retried)
+      const uint32_t avl = lend > q ? lend - q : 0u;
       bool done = false;
-      if (rdy && (ph == WK_ST || ph == WK_BLK || ph == WK_UPD || (MODE == 1 && ph == WK_DS))) {
+      if (avl && (ph == WK_ST || ph == WK_BLK || ph == WK_UPD || (MODE == 1 && ph == WK_DS))) {
         const uint32_t kq = q >> 6, sq = q & 63u;
         const uint64_t m0 = L.mask[kq & (DW_S - 1)][l], m1 = L.mask[(kq + 1u) & (DW_S - 1)][l];
-        // bytes q .. q + 31 (chunks past the segment may hold stale masks: every unit is checked against rb)
-        const uint32_t w32 = (uint32_t)((m0 >> sq) | ((m1 << (63u - sq)) << 1));
+        // bytes q .. q + 63 (chunks past the segment may hold stale masks: every unit is checked against rb)
+        const uint64_t w64 = (m0 >> sq) | ((m1 << (63u - sq)) << 1);
+        const uint32_t w32 = (uint32_t)w64;
         const uint32_t b0 = dw_byte(L, l, q);
-        if (ph == WK_ST) {   // Item with origin(s), one-byte String (ASCII) / Deleted length, inside 32 bytes
-          const uint32_t hoh = b0 >> 6, ref = b0 & 0x3Fu;
-          const uint32_t tt = w32 >> 1, x2 = tt & (tt - 1u), x3 = x2 & (x2 - 1u), x4 = x3 & (x3 - 1u);
-          const uint32_t cpos = (uint32_t)__builtin_ctz((hoh == 3u ? x4 : x2) | 0x80000000u) + 2u;   // after the origins
-          const uint32_t cq = cpos & 31u;
-          const uint32_t lv = dw_byte(L, l, q + cq);
-          const uint32_t isS = ref == 4u ? 1u : 0u;
-          const uint32_t end = cq + 1u + (isS ? lv : 0u);
-          const uint32_t mk = isS ? (((1u << (lv & 31u)) - 1u) << ((cq + 1u) & 31u)) : 0u;   // the string's bytes: ASCII
-          const uint32_t ce = clock + lv;
-          uint32_t ok = (hoh != 0u) & (isS | (ref == 1u)) & (cpos < 31u) & (w32 >> cq) & (lv != 0u) & (end <= 32u) &
-                        ((w32 & mk) == mk) & (ce >= clock);
-          uint32_t emit = 0;
-          if (MODE == 0) ok &= (st_left != 1u) | !e_on;
-          else {
-            emit = (!emitted) & (ce > svc);
-            ok &= (!emit) | ((svc <= clock) & !e_on & !run_on);   // a cut struct: the general decoder
-          }
-          if (ok) {
-            done = true;
-            if (MODE == 0) {
-              clk = stop ? clk : ce;   // (no Skips here: the first-struct seeding is the same)
-              fst = false;
-            } else if (emit) {
-              const uint32_t hl = dw_vulen(st_left) + dw_vulen(client) + dw_vulen(clock);
-              if (t + hl > tend) bad = 1;
-              else {
-                e_on = true; e_dst = t; e_a = st_left; e_b = client; e_c = clock; e_pl = 0; e_q = q;
-                t += hl;
-                run_on = true; cp = q; rs0 = q; cdst = t; cd0 = t; run_end = DW_OPEN;
-                emitted = true; count++;
-              }
+        if (ph == WK_ST) {   // Item with origin(s), one-byte String (ASCII) / Deleted length, inside 32 bytes;
+                             // a second one right behind it from the same 64-byte window
+          uint32_t qo = 0, bb = b0;
+#pragma unroll
+          for (int u = 0; u < 2; u++) {
+            const uint32_t wq = (uint32_t)(w64 >> qo);
+            if (u == 1) bb = dw_byte(L, l, q);
+            const uint32_t hoh = bb >> 6, ref = bb & 0x3Fu;
+            const uint32_t tt = wq >> 1, x2 = tt & (tt - 1u), x3 = x2 & (x2 - 1u), x4 = x3 & (x3 - 1u);
+            const uint32_t cpos = (uint32_t)__builtin_ctz((hoh == 3u ? x4 : x2) | 0x80000000u) + 2u;   // after the origins
+            const uint32_t cq = cpos & 31u;
+            const uint32_t lv = dw_byte(L, l, q + cq);
+            const uint32_t isS = ref == 4u ? 1u : 0u;
+            const uint32_t end = cq + 1u + (isS ? lv : 0u);
+            const uint32_t mk = isS ? (((1u << (lv & 31u)) - 1u) << ((cq + 1u) & 31u)) : 0u;   // the string's bytes: ASCII
+            const uint32_t ce = clock + lv;
+            uint32_t ok = (ph == WK_ST) & (hoh != 0u) & (isS | (ref == 1u)) & (cpos < 31u) & (wq >> cq) & (lv != 0u) &
+                          (end <= 32u) & ((wq & mk) == mk) & (ce >= clock) & (qo + end <= avl) & (u == 0 || (done && qo + end <= 32u));
+            uint32_t emit = 0;
+            if (MODE == 0) ok &= (st_left != 1u) | !e_on;
+            else {
+              emit = (!emitted) & (ce > svc);
+              ok &= (!emit) | ((svc <= clock) & !e_on & !run_on);   // a cut struct: the general decoder
             }
-            clock = ce;
-            q += end;
-            if (--st_left == 0u) block_end();
+            if (ok) {
+              done = true;
+              if (MODE == 0) {
+                clk = stop ? clk : ce;   // (no Skips here: the first-struct seeding is the same)
+                fst = false;
+              } else if (emit) {
+                const uint32_t hl = dw_vulen(st_left) + dw_vulen(client) + dw_vulen(clock);
+                if (t + hl > tend) bad = 1;
+                else {
+                  e_on = true; e_dst = t; e_a = st_left; e_b = client; e_c = clock; e_pl = 0; e_q = q;
+                  t += hl;
+                  run_on = true; cp = q; rs0 = q; cdst = t; cd0 = t; run_end = DW_OPEN;
+                  emitted = true; count++;
+                }
+              }
+              clock = ce;
+              q += end; qo += end;
+              if (--st_left == 0u) block_end();
+            }
           }
         } else if (ph == WK_BLK) {   // block header: <= 2-byte count, <= 5-byte client, one-byte clock
           const uint32_t y = w32 & (w32 - 1u), z = y & (y - 1u);
@@ -490,7 +531,8 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
           const uint32_t cn = e2 - e1;   // client bytes
           const uint64_t cw = dw_rd8(L, l, q + (e1 & 1u) + 1u);
           const uint32_t nst = e1 == 0u ? b0 : ((b0 & 0x7Fu) | (b1 << 7));
-          const uint32_t ok = (z != 0u) & (e1 <= 1u) & (e3 == e2 + 1u) & (cn - 1u <= 4u) & !((cn == 5u) & (((uint32_t)(cw >> 32) & 0x70u) != 0u));
+          const uint32_t ok = (z != 0u) & (e1 <= 1u) & (e3 == e2 + 1u) & (cn - 1u <= 4u) & !((cn == 5u) & (((uint32_t)(cw >> 32) & 0x70u) != 0u)) &
+                              (e3 < avl);
           if (ok) {
             done = true;
             const uint32_t cl = (uint32_t)pext7(cw, cn);
@@ -505,7 +547,7 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
             if (b0) { n_left = b0; have_prev = false; ph = WK_BLK; }
             else ph = MODE == 1 ? WK_DS : WK_FIN;
           }
-        } else if ((w32 & 1u) && b0 == 0u && !run_on) {   // MODE 1 WK_DS: the empty delete set ("00")
+        } else if ((w32 & 1u) && b0 == 0u && !run_on) {   // MODE 1 WK_DS: the empty delete set ("00") (avl >= 1)
           done = true;
           run_on = true; cp = q; rs0 = q; cdst = t; cd0 = t;
           q += 1u; run_end = q; t += 1u;

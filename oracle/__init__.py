@@ -46,6 +46,8 @@ def lib():
         L.yo_free.argtypes = [ctypes.c_void_p]
         L.yo_merge_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+        L.yo_doc_batch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
         L.yo_v8_sort_table.argtypes = [P(ctypes.c_int), ctypes.c_int, P(ctypes.c_int8)]
         L.yo_v8_sort_table.restype = ctypes.c_long
         for f in (L.yo_merge, L.yo_diff, L.yo_sv):
@@ -126,4 +128,23 @@ def merge_batch(arena, upd_off, doc_upd, threads=1, compat135=False):
     algo = ctypes.c_uint64()
     L.yo_merge_batch(arena.ctypes.data, upd_off.ctypes.data, doc_upd.ctypes.data, n_docs, COMPAT_135 if compat135 else 0,
                      threads, status.ctypes.data, ctypes.byref(algo))
+    return status[:n_docs], algo.value
+
+
+def doc_batch(mode, arena, doc_off, sv_arena=None, sv_off=None, threads=1, compat135=False):
+    """encodeStateVectorFromUpdate (mode "sv") or diffUpdate (mode "diff") over every document of a
+    packed corpus on `threads` pthreads (CPU-baseline driver).  Returns (status int32 array, algorithmic bytes)."""
+    import numpy as np
+    L = lib()
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+    n_docs = len(doc_off) - 1
+    if mode == "diff":
+        sv_arena = np.ascontiguousarray(sv_arena, dtype=np.uint8)
+        sv_off = np.ascontiguousarray(sv_off, dtype=np.uint64)
+    status = np.zeros(max(n_docs, 1), dtype=np.int32)
+    algo = ctypes.c_uint64()
+    L.yo_doc_batch(1 if mode == "diff" else 0, arena.ctypes.data, doc_off.ctypes.data,
+                   sv_arena.ctypes.data if mode == "diff" else None, sv_off.ctypes.data if mode == "diff" else None,
+                   n_docs, COMPAT_135 if compat135 else 0, threads, status.ctypes.data, ctypes.byref(algo))
     return status[:n_docs], algo.value

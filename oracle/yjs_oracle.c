@@ -1076,3 +1076,44 @@ int yo_merge_batch(const uint8_t *arena, const uint64_t *upd_off, const uint32_t
   free(th); free(jobs);
   return 0;
 }
+
+/* CPU baseline driver for the per-document functions: mode 0 = encodeStateVectorFromUpdate,
+ * 1 = diffUpdate(doc, sv), over n_docs documents of a packed corpus on `nthreads` pthreads.
+ * Returns the algorithmic bytes (input + state vector + output) in *algo_bytes. */
+typedef struct {
+  int mode; const uint8_t *arena; const uint64_t *doc_off; const uint8_t *sv; const uint64_t *sv_off;
+  uint32_t n_docs; int flags; int tid, nthreads; uint64_t algo; int32_t *status;
+} DocJob;
+static void *doc_worker(void *arg) {
+  DocJob *j = (DocJob *)arg;
+  for (uint32_t d = (uint32_t)j->tid; d < j->n_docs; d += (uint32_t)j->nthreads) {
+    const uint8_t *u = j->arena + j->doc_off[d];
+    const size_t ul = (size_t)(j->doc_off[d + 1] - j->doc_off[d]);
+    uint8_t *out = NULL; size_t ol = 0; int st; size_t svl = 0;
+    if (j->mode == 0) st = yo_sv(u, ul, j->flags, &out, &ol);
+    else {
+      svl = (size_t)(j->sv_off[d + 1] - j->sv_off[d]);
+      st = yo_diff(u, ul, j->sv + j->sv_off[d], svl, j->flags, &out, &ol);
+    }
+    j->status[d] = st;
+    j->algo += ul + svl + (st == YO_OK ? ol : 0);
+    free(out);
+  }
+  return NULL;
+}
+int yo_doc_batch(int mode, const uint8_t *arena, const uint64_t *doc_off, const uint8_t *sv, const uint64_t *sv_off, uint32_t n_docs,
+                 int flags, int nthreads, int32_t *status, uint64_t *algo_bytes) {
+  if (nthreads < 1) nthreads = 1;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  DocJob *jobs = (DocJob *)calloc((size_t)nthreads, sizeof(DocJob));
+  for (int t = 0; t < nthreads; t++) {
+    DocJob b = { mode, arena, doc_off, sv, sv_off, n_docs, flags, t, nthreads, 0, status };
+    jobs[t] = b;
+    pthread_create(&th[t], NULL, doc_worker, &jobs[t]);
+  }
+  uint64_t tot = 0;
+  for (int t = 0; t < nthreads; t++) { pthread_join(th[t], NULL); tot += jobs[t].algo; }
+  *algo_bytes = tot;
+  free(th); free(jobs);
+  return 0;
+}

@@ -11,7 +11,7 @@ const { frame, decodeSyncMessage, MessageType, SyncStep } = require('../src/sync
 const { MiniHocuspocus } = require('./harness.js')
 
 const mode = process.argv.includes('--gpu') ? 'gpu' : 'cpu'
-const Y = require(path.join(__dirname, '..', '..', '..', 'tests', 'golden', 'gen', 'yjs_loader.js')).load()
+const Y = require(path.join(__dirname, '..', '..', '..', 'tools', 'yjs_bundle.js')).load()   // the test oracle: yjs from the image's bundle
 
 class CpuDouble { // test double (never shipped): same API as GpuEngine
   constructor (device = 0) { this.calls = 0; this.device = device }

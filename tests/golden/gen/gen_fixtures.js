@@ -1,6 +1,6 @@
 // Golden-vector generator (test-fixture tooling; runs only in the build container).
 //
-// Drives the yjs 13.5.16 bundle (see yjs_loader.js) and records
+// Drives the yjs 13.5.16 bundle (see tools/yjs_bundle.js) and records
 //   mergeUpdates(us)                 -> out   (yjs Y@37704 / Y@39011)
 //   diffUpdate(u, sv)                -> out   (Y@41210 -> Y@40711)
 //   encodeStateVectorFromUpdate(u)   -> out   (Y@38304 -> Y@37728)
@@ -14,7 +14,7 @@
 const zlib = require('zlib')
 const fs = require('fs')
 const path = require('path')
-const { load } = require('./yjs_loader')
+const { load } = require('../../../tools/yjs_bundle')
 const Y = load()
 
 // ---------------------------------------------------------------- utilities

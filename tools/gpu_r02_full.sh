@@ -1,0 +1,5 @@
+#!/bin/bash
+# Full GPU check: every -m gpu test, then the default bench line.
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 600 python -u bench.py > gpurun_out/bench.log 2>&1

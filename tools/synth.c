@@ -8,6 +8,8 @@
  *    each insert one V1 update whose origin/rightOrigin are the neighbouring
  *    characters' ids (exactly what Y.Text.insert records); `del_pct` percent of
  *    the operations are single-character deletes (delete-set-only updates).
+ *  text_updates_gen: config C2 with one PRNG stream per document (global index), so any subset of
+ *    a document set (a rank's shard) is generated alone, in parallel.
  *  text_states: config C4 -- the merged state of such a session written as one
  *    update (client blocks descending, clocks ascending; 1-16 clients, log-uniform
  *    1-8 KB) plus a per-document state vector with a uniform clock per client
@@ -108,7 +110,7 @@ size_t synth_text_updates(uint64_t seed, uint32_t n_docs, uint32_t n_updates, ui
  * Two calls: synth_text_states_gen builds the corpus into a handle and returns its sizes;
  * synth_text_states_take copies it into caller arrays and frees the handle. */
 typedef struct { uint8_t *buf, *sv; uint64_t *doff, *soff; size_t nb, ns; } C4Part;
-typedef struct { uint64_t seed; uint32_t d0, d1, min_cl, max_cl; double lo, hi; C4Part *p; } C4Job;
+typedef struct { uint64_t seed; uint32_t d0, d1, min_cl, max_cl; double lo, hi; C4Part *p; const uint32_t *idx; } C4Job;
 
 static void c4_doc(uint64_t seed, uint32_t d, uint32_t ops, uint32_t min_cl, uint32_t max_cl, Rng *r,
                    Ch *doc, uint8_t *tmp, uint64_t *toff, uint32_t *uidx, C4Part *P) {
@@ -176,7 +178,8 @@ static void *c4_run(void *arg) {
   size_t cap = 1 << 20, scap = n * (1 + (size_t)J->max_cl * 16) + 64;
   P->buf = (uint8_t *)malloc(cap); P->sv = (uint8_t *)malloc(scap); P->nb = 0; P->ns = 0;
   for (uint32_t d = J->d0; d < J->d1; d++) {
-    Rng r = { (J->seed * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)(d + 1) * 0xD1B54A32D192ED03ULL) };
+    const uint32_t gi = J->idx ? J->idx[d] : d;   /* the document's global index: its PRNG stream */
+    Rng r = { (J->seed * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)(gi + 1) * 0xD1B54A32D192ED03ULL) };
     rnext(&r); rnext(&r);
     const double u = (double)(rnext(&r) >> 11) * (1.0 / 9007199254740992.0);
     const uint32_t ops = (uint32_t)exp(J->lo + u * (J->hi - J->lo));
@@ -189,8 +192,8 @@ static void *c4_run(void *arg) {
 
 typedef struct { uint32_t n_docs, n_parts; C4Part *parts; uint32_t *pd0; size_t nb, ns; } C4Handle;
 
-void *synth_text_states_gen(uint64_t seed, uint32_t n_docs, uint32_t min_bytes, uint32_t max_bytes, uint32_t min_clients,
-                            uint32_t max_clients, uint32_t threads, uint64_t *out_bytes, uint64_t *out_sv_bytes) {
+void *synth_text_states_gen(uint64_t seed, const uint32_t *idx, uint32_t n_docs, uint32_t min_bytes, uint32_t max_bytes,
+                            uint32_t min_clients, uint32_t max_clients, uint32_t threads, uint64_t *out_bytes, uint64_t *out_sv_bytes) {
   if (threads < 1) threads = 1;
   if (threads > n_docs) threads = n_docs ? n_docs : 1;
   C4Handle *H = (C4Handle *)calloc(1, sizeof(C4Handle));
@@ -202,7 +205,7 @@ void *synth_text_states_gen(uint64_t seed, uint32_t n_docs, uint32_t min_bytes, 
   const double lo = log((double)min_bytes / 16.0), hi = log((double)max_bytes / 16.0);
   for (uint32_t t = 0; t < threads; t++) {
     jobs[t].seed = seed; jobs[t].d0 = (uint32_t)((uint64_t)n_docs * t / threads); jobs[t].d1 = (uint32_t)((uint64_t)n_docs * (t + 1) / threads);
-    jobs[t].min_cl = min_clients; jobs[t].max_cl = max_clients; jobs[t].lo = lo; jobs[t].hi = hi; jobs[t].p = &H->parts[t];
+    jobs[t].min_cl = min_clients; jobs[t].max_cl = max_clients; jobs[t].lo = lo; jobs[t].hi = hi; jobs[t].p = &H->parts[t]; jobs[t].idx = idx;
     H->pd0[t] = jobs[t].d0;
     const size_t n = jobs[t].d1 - jobs[t].d0;
     H->parts[t].doff = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1)); H->parts[t].soff = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
@@ -348,4 +351,89 @@ size_t synth_big_docs(uint64_t seed, uint32_t n_docs, uint64_t max_bytes, uint64
   doc_upd[n_docs] = nu; upd_off[nu] = b;
   free(clients); free(ends); free(dcl); free(dck); free(dln);
   return b;
+}
+
+/* ---- per-document C2 (documents from their own PRNG streams; a rank generates only its shard) ---- */
+typedef struct { uint8_t *buf; uint64_t *uoff; uint32_t *cnt; size_t nb; uint32_t nu; } C2Part;
+typedef struct { uint64_t seed; const uint32_t *idx; uint32_t d0, d1, n_updates, min_cl, max_cl; int del_pct; C2Part *p; } C2Job;
+static void *c2_run(void *arg) {
+  C2Job *J = (C2Job *)arg;
+  const uint32_t n = J->d1 - J->d0;
+  C2Part *P = J->p;
+  P->buf = (uint8_t *)malloc((size_t)n * J->n_updates * 40 + 64);
+  P->uoff = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)n * J->n_updates + 1));
+  P->cnt = (uint32_t *)malloc(sizeof(uint32_t) * (n + 1));
+  P->nb = 0; P->nu = 0;
+  Ch *doc = (Ch *)malloc(sizeof(Ch) * (J->n_updates + 1));
+  for (uint32_t d = J->d0; d < J->d1; d++) {
+    const uint32_t gi = J->idx ? J->idx[d] : d;
+    Rng r = { (J->seed * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)(gi + 1) * 0xC2B2AE3D27D4EB4FULL) };
+    rnext(&r); rnext(&r);
+    uint32_t clients[64], clocks[64] = {0};
+    int nc = (int)(J->min_cl + rbelow(&r, J->max_cl - J->min_cl + 1));
+    if (nc > 64) nc = 64;
+    pick_clients(&r, nc, clients);
+    const uint32_t u0 = P->nu;
+    int nd;
+    session(&r, (int)J->n_updates, nc, clients, clocks, doc, &nd, P->buf, &P->nb, P->uoff, &P->nu, J->del_pct);
+    P->cnt[d - J->d0] = P->nu - u0;
+  }
+  free(doc);
+  return NULL;
+}
+typedef struct { uint32_t n, parts; uint32_t *pd0; C2Part *p; size_t nb; uint64_t nu; } C2Handle;
+void *synth_text_updates_gen(uint64_t seed, const uint32_t *idx, uint32_t n, uint32_t n_updates, uint32_t min_cl, uint32_t max_cl,
+                             int del_pct, uint32_t threads, uint64_t *out_bytes, uint64_t *out_upds) {
+  if (threads < 1) threads = 1;
+  if (threads > n) threads = n ? n : 1;
+  C2Handle *H = (C2Handle *)calloc(1, sizeof(C2Handle));
+  H->n = n; H->parts = threads;
+  H->p = (C2Part *)calloc(threads, sizeof(C2Part)); H->pd0 = (uint32_t *)calloc(threads + 1, sizeof(uint32_t));
+  C2Job *jobs = (C2Job *)calloc(threads, sizeof(C2Job));
+  pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
+  for (uint32_t t = 0; t < threads; t++) {
+    C2Job j = { seed, idx, (uint32_t)((uint64_t)n * t / threads), (uint32_t)((uint64_t)n * (t + 1) / threads), n_updates, min_cl, max_cl, del_pct, &H->p[t] };
+    jobs[t] = j; H->pd0[t] = j.d0;
+    pthread_create(&th[t], NULL, c2_run, &jobs[t]);
+  }
+  H->pd0[threads] = n;
+  for (uint32_t t = 0; t < threads; t++) { pthread_join(th[t], NULL); H->nb += H->p[t].nb; H->nu += H->p[t].nu; }
+  free(jobs); free(th);
+  *out_bytes = H->nb; *out_upds = H->nu;
+  return H;
+}
+void synth_text_updates_take(void *h, uint8_t *buf, uint64_t *upd_off, uint32_t *doc_upd) {
+  C2Handle *H = (C2Handle *)h;
+  size_t b = 0; uint64_t u = 0;
+  for (uint32_t t = 0; t < H->parts; t++) {
+    C2Part *P = &H->p[t];
+    memcpy(buf + b, P->buf, P->nb);
+    for (uint32_t i = 0; i < P->nu; i++) upd_off[u + i] = b + P->uoff[i];
+    uint64_t uu = u;
+    for (uint32_t d = H->pd0[t]; d < H->pd0[t + 1]; d++) { doc_upd[d] = (uint32_t)uu; uu += P->cnt[d - H->pd0[t]]; }
+    b += P->nb; u += P->nu;
+    free(P->buf); free(P->uoff); free(P->cnt);
+  }
+  upd_off[u] = b; doc_upd[H->n] = (uint32_t)u;
+  free(H->p); free(H->pd0); free(H);
+}
+
+/* Documents of `n_total` named prefix + decimal index owned by `rank`: fnv1a64(utf8(name)) mod world
+ * (the same hash as hocuspocus_amd/shard.py and the Node GpuEnginePool).  Returns the count. */
+uint32_t synth_partition(const char *prefix, uint32_t n_total, uint32_t world, uint32_t rank, uint32_t *out) {
+  uint32_t k = 0;
+  char name[96];
+  const size_t pl = strlen(prefix);
+  if (pl > 64) return 0;
+  memcpy(name, prefix, pl);
+  for (uint32_t i = 0; i < n_total; i++) {
+    char dig[16]; int nd = 0; uint32_t v = i;
+    do { dig[nd++] = (char)('0' + v % 10); v /= 10; } while (v);
+    size_t len = pl;
+    while (nd) name[len++] = dig[--nd];
+    uint64_t h = 0xCBF29CE484222325ULL;
+    for (size_t j = 0; j < len; j++) { h ^= (uint8_t)name[j]; h *= 0x100000001B3ULL; }
+    if (h % world == rank) out[k++] = i;
+  }
+  return k;
 }

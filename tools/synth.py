@@ -24,8 +24,15 @@ def lib():
         L.synth_text_updates.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P, P, P]
         L.synth_text_updates.restype = ctypes.c_size_t
         u64p = ctypes.POINTER(ctypes.c_uint64)
-        L.synth_text_states_gen.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+        L.synth_text_states_gen.argtypes = [ctypes.c_uint64, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint32, ctypes.c_uint32, u64p, u64p]
+        L.synth_text_updates_gen.argtypes = [ctypes.c_uint64, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_int, ctypes.c_uint32, u64p, u64p]
+        L.synth_text_updates_gen.restype = P
+        L.synth_text_updates_take.argtypes = [P, P, P, P]
+        L.synth_text_updates_take.restype = None
+        L.synth_partition.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P]
+        L.synth_partition.restype = ctypes.c_uint32
         L.synth_text_states_gen.restype = P
         L.synth_text_states_take.argtypes = [P, P, P, P, P]
         L.synth_text_states_take.restype = None
@@ -47,15 +54,44 @@ def text_updates(n_docs, n_updates=200, min_clients=1, max_clients=4, del_pct=0,
     return buf[:n].copy(), upd_off, doc_upd
 
 
-def text_states(n_docs, min_bytes=1024, max_bytes=8192, min_clients=1, max_clients=16, seed=1, threads=None):
+def _threads(threads):
+    return threads if threads else max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def partition(prefix, n_total, world, rank):
+    """Global indices of the documents named prefix + str(i), i < n_total, that rank owns:
+    fnv1a64(name) mod world (hocuspocus_amd.shard.shard_of)."""
+    out = np.empty(max(n_total, 1), dtype=np.uint32)
+    k = lib().synth_partition(prefix.encode(), n_total, world, rank, out.ctypes.data)
+    return out[:k].copy()
+
+
+def text_updates_docs(idx, n_updates=200, min_clients=1, max_clients=4, del_pct=0, seed=1, threads=None):
+    """Config C2 for the documents of global indices `idx` (each from its own PRNG stream: a rank's shard
+    is generated alone).  Returns (arena, upd_off[n_upd+1], doc_upd[n+1])."""
+    idx = np.ascontiguousarray(idx, dtype=np.uint32)
+    n = len(idx)
+    nb, nu = ctypes.c_uint64(), ctypes.c_uint64()
+    h = lib().synth_text_updates_gen(seed, idx.ctypes.data, n, n_updates, min_clients, max_clients, del_pct, _threads(threads),
+                                     ctypes.byref(nb), ctypes.byref(nu))
+    buf = np.empty(nb.value, dtype=np.uint8)
+    upd_off = np.empty(nu.value + 1, dtype=np.uint64)
+    doc_upd = np.empty(n + 1, dtype=np.uint32)
+    lib().synth_text_updates_take(h, buf.ctypes.data, upd_off.ctypes.data, doc_upd.ctypes.data)
+    return buf, upd_off, doc_upd
+
+
+def text_states(n_docs, min_bytes=1024, max_bytes=8192, min_clients=1, max_clients=16, seed=1, threads=None, idx=None):
     """Config C4: merged Y.Text states of 1-16 clients, log-uniform 1-8 KB, plus one
     state vector per document.  Returns (arena, doc_off[n_docs+1], sv_arena, sv_off[n_docs+1]).
-    Documents come from per-document PRNG streams, so the bytes do not depend on `threads`."""
-    if threads is None:
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    Documents come from per-document PRNG streams (global index i, or idx[i]), so the bytes do not
+    depend on `threads` and a rank's shard is generated alone."""
+    if idx is not None:
+        idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        n_docs = len(idx)
     nb, ns = ctypes.c_uint64(), ctypes.c_uint64()
-    h = lib().synth_text_states_gen(seed, n_docs, min_bytes, max_bytes, min_clients, max_clients, threads,
-                                    ctypes.byref(nb), ctypes.byref(ns))
+    h = lib().synth_text_states_gen(seed, idx.ctypes.data if idx is not None else None, n_docs, min_bytes, max_bytes, min_clients,
+                                    max_clients, _threads(threads), ctypes.byref(nb), ctypes.byref(ns))
     buf = np.empty(nb.value, dtype=np.uint8)
     sv = np.empty(ns.value, dtype=np.uint8)
     doc_off = np.empty(n_docs + 1, dtype=np.uint64)

@@ -1,10 +1,7 @@
-// Test-fixture tooling only (never shipped, never run on the GPU box).
-//
-// Loads the yjs 13.5.16 / lib0 0.2.42 copy that JupyterLab bundles in this
-// container's image (/opt/conda/share/jupyter/lab/static, see SURVEY.md
-// "Citation conventions" and App. E).  The bundle itself is NOT copied into this
-// repository: this file is a ~20-line webpack-chunk runtime that evaluates the
-// bundle where it lies so gen_fixtures.js can record input/output byte vectors.
+// Loads the yjs 13.5.16 / lib0 0.2.42 copy that JupyterLab bundles in this image
+// (/opt/conda/share/jupyter/lab/static) where it lies -- the reference yjs CPU path for bench.py's
+// cpu_baseline "yjs" leg.  Nothing of the bundle is copied into the repository: this is a small
+// webpack-chunk runtime that evaluates the bundle's own chunks.
 'use strict'
 const path = require('path')
 
@@ -34,4 +31,4 @@ function load () {
   return req(YJS_MODULE_ID)
 }
 
-module.exports = { load, STATIC }
+module.exports = { load, STATIC, present: () => require('fs').existsSync(path.join(STATIC, CHUNKS[0])) }

@@ -1,0 +1,62 @@
+// The reference CPU path for bench.py's cpu_baseline "yjs" leg (BASELINE.md, SURVEY.md §8d): yjs on
+// Node worker_threads, one worker per host core granted, each running Y.mergeUpdates /
+// Y.diffUpdate / Y.encodeStateVectorFromUpdate per document over a contiguous shard of a corpus
+// that bench.py wrote to disk.  Only the op loop is timed; the job's time is the slowest worker.
+//
+//   node tools/yjs_cpu_baseline.js <dir> <op: merge|sv|diff> <workers>
+//   <dir>/arena.bin, <dir>/off.bin (u64 update or document offsets), <dir>/docs.bin (u32 update index
+//   per document, merge), <dir>/sv.bin + <dir>/svoff.bin (diff)
+// Prints one JSON line: {op, docs, workers, seconds, algo_bytes}.
+'use strict'
+const { Worker, isMainThread, parentPort, workerData } = require('worker_threads')
+const fs = require('fs')
+const path = require('path')
+
+function u64 (buf) { const a = new BigUint64Array(buf.buffer, buf.byteOffset, buf.length / 8); return Array.from(a, Number) }
+function u32 (buf) { return new Uint32Array(buf.buffer, buf.byteOffset, buf.length / 4) }
+
+if (isMainThread) {
+  const [dir, op, nw] = process.argv.slice(2)
+  const workers = parseInt(nw, 10)
+  const docs = op === 'merge' ? u32(fs.readFileSync(path.join(dir, 'docs.bin'))).length - 1 : u64(fs.readFileSync(path.join(dir, 'off.bin'))).length - 1
+  let done = 0; let slowest = 0; let algo = 0
+  for (let w = 0; w < workers; w++) {
+    const d0 = Math.floor(docs * w / workers); const d1 = Math.floor(docs * (w + 1) / workers)
+    const wk = new Worker(__filename, { workerData: { dir, op, d0, d1 } })
+    wk.on('message', m => {
+      slowest = Math.max(slowest, m.seconds); algo += m.algo
+      if (++done === workers) console.log(JSON.stringify({ op, docs, workers, seconds: slowest, algo_bytes: algo }))
+    })
+    wk.on('error', e => { console.error(e); process.exit(1) })
+  }
+} else {
+  const Y = require('./yjs_bundle.js').load()
+  const { dir, op, d0, d1 } = workerData
+  const arena = fs.readFileSync(path.join(dir, 'arena.bin'))
+  const off = u64(fs.readFileSync(path.join(dir, 'off.bin')))
+  const jobs = []
+  if (op === 'merge') {
+    const docs = u32(fs.readFileSync(path.join(dir, 'docs.bin')))
+    for (let d = d0; d < d1; d++) {
+      const us = []
+      for (let u = docs[d]; u < docs[d + 1]; u++) us.push(new Uint8Array(arena.buffer, arena.byteOffset + off[u], off[u + 1] - off[u]))
+      jobs.push(us)
+    }
+  } else {
+    const sv = op === 'diff' ? fs.readFileSync(path.join(dir, 'sv.bin')) : null
+    const svoff = op === 'diff' ? u64(fs.readFileSync(path.join(dir, 'svoff.bin'))) : null
+    for (let d = d0; d < d1; d++) {
+      const u = new Uint8Array(arena.buffer, arena.byteOffset + off[d], off[d + 1] - off[d])
+      jobs.push(op === 'diff' ? [u, new Uint8Array(sv.buffer, sv.byteOffset + svoff[d], svoff[d + 1] - svoff[d])] : u)
+    }
+  }
+  let algo = 0
+  const t0 = process.hrtime.bigint()
+  for (const j of jobs) {
+    let out
+    if (op === 'merge') { out = Y.mergeUpdates(j); for (const u of j) algo += u.length } else if (op === 'diff') { out = Y.diffUpdate(j[0], j[1]); algo += j[0].length + j[1].length } else { out = Y.encodeStateVectorFromUpdate(j); algo += j.length }
+    algo += out.length
+  }
+  const seconds = Number(process.hrtime.bigint() - t0) / 1e9
+  parentPort.postMessage({ seconds, algo })
+}

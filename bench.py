@@ -109,18 +109,16 @@ class GpuBackend:
         return self.torch.from_numpy(a).to(self.dev)
 
     def merge_async(self, c):
-        self.eng.merge_device_async(c["da"].data_ptr(), c["bytes"], c["do"].data_ptr(), c["dd"].data_ptr(), c["n_upd"], c["n"],
-                                    self.stream.cuda_stream)
+        self.eng.merge_device_async(c["da"], c["bytes"], c["do"], c["dd"], c["n_upd"], c["n"], self.stream.cuda_stream)
 
     def merge_finish(self):
         return self.eng.merge_device_finish()
 
     def sv(self, c):
-        return self.eng.sv_device(c["da"].data_ptr(), c["bytes"], c["do"].data_ptr(), c["n"], self.stream.cuda_stream)
+        return self.eng.sv_device(c["da"], c["bytes"], c["do"], c["n"], self.stream.cuda_stream)
 
     def diff(self, c):
-        return self.eng.diff_device(c["da"].data_ptr(), c["bytes"], c["do"].data_ptr(), c["ds"].data_ptr(), c["dso"].data_ptr(), c["n"],
-                                    self.stream.cuda_stream)
+        return self.eng.diff_device(c["da"], c["bytes"], c["do"], c["ds"], c["dso"], c["n"], self.stream.cuda_stream)
 
     def sync(self):
         self.torch.cuda.synchronize()

@@ -2,9 +2,10 @@
 
 The product is ``libygm.so`` (HIP kernels for gfx950 + C-ABI runtime,
 ``include/ygm.h``); :mod:`hocuspocus_amd.engine` is its Python binding and
-:mod:`hocuspocus_amd.extension` mirrors the Hocuspocus Extension/DocumentStore
-interface the engine plugs into (packages/server/src/types.ts:36-63,
-packages/extension-database/src/Database.ts:10-60).
+:mod:`hocuspocus_amd.shard` routes documents over a node's GPUs.  The Hocuspocus
+Extension / DocumentStore drop-in (packages/server/src/types.ts:36-63,
+packages/extension-database/src/Database.ts:10-60) is the Node package
+``packages/extension-gpu-merge`` over the same C ABI (N-API addon).
 """
 import os
 import subprocess

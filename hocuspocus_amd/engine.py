@@ -115,6 +115,19 @@ def _ptr(a):
     return ctypes.c_char_p(a) if a else None
 
 
+TAIL_PAD = 64   # readable bytes the kernels need after a device arena (include/ygm.h, "Tail padding")
+
+
+def _dptr(x, need=0):
+    """A device pointer: an int, or a tensor (then its allocation must hold `need` bytes)."""
+    if hasattr(x, "data_ptr"):
+        nbytes = x.numel() * x.element_size()
+        if nbytes < need:
+            raise ValueError(f"device buffer of {nbytes} bytes: the engine reads {need} (arena + {TAIL_PAD} bytes of tail padding)")
+        return x.data_ptr()
+    return int(x)
+
+
 @dataclass
 class DeviceResult:
     """Outputs left in HBM by a device-resident call (context-owned memory)."""
@@ -236,8 +249,8 @@ class Engine:
     def merge_device(self, d_arena: int, arena_bytes: int, d_upd_off: int, d_doc_upd: int, n_upd: int, n_docs: int,
                      stream: int = 0) -> DeviceResult:
         r = _DevResult()
-        st = lib().ygm_merge_v1_device(self._ctx, d_arena, arena_bytes, d_upd_off, d_doc_upd, n_upd, n_docs, stream or None,
-                                       ctypes.byref(r))
+        st = lib().ygm_merge_v1_device(self._ctx, _dptr(d_arena, arena_bytes + TAIL_PAD), arena_bytes, _dptr(d_upd_off), _dptr(d_doc_upd),
+                                       n_upd, n_docs, stream or None, ctypes.byref(r))
         if st != OK:
             raise YjsError(st)
         return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)
@@ -245,7 +258,8 @@ class Engine:
     def merge_device_async(self, d_arena: int, arena_bytes: int, d_upd_off: int, d_doc_upd: int, n_upd: int, n_docs: int,
                            stream: int = 0) -> None:
         """Enqueues a device-resident batch merge without waiting (ygm_merge_v1_device_async)."""
-        st = lib().ygm_merge_v1_device_async(self._ctx, d_arena, arena_bytes, d_upd_off, d_doc_upd, n_upd, n_docs, stream or None)
+        st = lib().ygm_merge_v1_device_async(self._ctx, _dptr(d_arena, arena_bytes + TAIL_PAD), arena_bytes, _dptr(d_upd_off),
+                                             _dptr(d_doc_upd), n_upd, n_docs, stream or None)
         if st != OK:
             raise YjsError(st)
 
@@ -259,16 +273,16 @@ class Engine:
 
     def diff_device(self, d_arena, arena_bytes, d_doc_off, d_sv, d_sv_off, n_docs, stream=0) -> DeviceResult:
         r = _DevResult()
-        st = lib().ygm_diff_v1_device(self._ctx, d_arena, arena_bytes, d_doc_off, d_sv, d_sv_off, n_docs, stream or None,
-                                      ctypes.byref(r))
+        st = lib().ygm_diff_v1_device(self._ctx, _dptr(d_arena, arena_bytes + TAIL_PAD), arena_bytes, _dptr(d_doc_off), _dptr(d_sv),
+                                      _dptr(d_sv_off), n_docs, stream or None, ctypes.byref(r))
         if st != OK:
             raise YjsError(st)
         return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)
 
     def sv_device(self, d_arena, arena_bytes, d_doc_off, n_docs, stream=0) -> DeviceResult:
         r = _DevResult()
-        st = lib().ygm_sv_from_update_v1_device(self._ctx, d_arena, arena_bytes, d_doc_off, n_docs, stream or None,
-                                                ctypes.byref(r))
+        st = lib().ygm_sv_from_update_v1_device(self._ctx, _dptr(d_arena, arena_bytes + TAIL_PAD), arena_bytes, _dptr(d_doc_off),
+                                                n_docs, stream or None, ctypes.byref(r))
         if st != OK:
             raise YjsError(st)
         return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)

@@ -111,7 +111,10 @@ int ygm_sv_from_update_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *do
  * SV / diff: packed by the exact per-document kernel); data_bytes is the used
  * extent of `data`, payload_bytes the sum of len[].  `stream` is a
  * hipStream_t (NULL = the context's stream); the call returns after one
- * read of the launch counters. */
+ * read of the launch counters.
+ * Tail padding: the kernels read inputs in aligned 16-byte pieces and 64-byte chunks, so at least
+ * 64 readable bytes must follow d_arena + arena_bytes and the end of d_sv_arena (zeroed or not: they
+ * are never taken as input).  The host API pads its own staging copies. */
 typedef struct {
   uint8_t *data;
   uint64_t *off;

@@ -39,7 +39,11 @@ class DocumentStore {
 class GpuMerge {
   /**
    * @param {{store?: DocumentStore|Function, fetch?: Function, device?: number, Y?: any,
-   *          engine?: GpuEngine, batchWindowMs?: number, maxBatchDocs?: number, compat135?: boolean}} configuration
+   *          engine?: GpuEngine, batchWindowMs?: number, maxBatchDocs?: number, compat135?: boolean,
+   *          onRefused?: 'reference'|'throw'}} configuration
+   *   onRefused: what a store does when the engine refuses a document's merge -- 'reference' (default):
+   *   store Y.encodeStateAsUpdate(document) like extension-database and record it in `refused`;
+   *   'throw': reject the store (Hocuspocus logs and rethrows, Hocuspocus.ts:431-435)
    */
   constructor (configuration = {}) {
     this.extensionName = 'GpuMerge'
@@ -53,8 +57,10 @@ class GpuMerge {
       : DocumentStore.fromDatabase({ fetch: configuration.fetch, store: typeof st === 'function' ? st : undefined })
     this.Y = configuration.Y || null
     this.engine = configuration.engine || null
-    /** documentName -> { base: Uint8Array|null, log: Uint8Array[] } */
+    /** documentName -> { base: Uint8Array|null, log: Uint8Array[], doc?: Y.Doc, onUpdate?: Function } */
     this.docs = new Map()
+    /** stores that fell back to Y.encodeStateAsUpdate(document) because the engine refused the merge */
+    this.refused = []
   }
 
   _Y () { if (!this.Y) this.Y = require('yjs'); return this.Y }
@@ -96,7 +102,12 @@ class GpuMerge {
   /**
    * Content added while loading (other extensions' onLoadDocument, a returned Doc,
    * Hocuspocus.ts:357-372) never reaches onChange (the listener is registered after
-   * load, :382-391): capture it once here (SURVEY.md §8b log-capture hazard 2).
+   * load, :382-391): capture it once here (SURVEY.md §8b log-capture hazard 2) -- only when it
+   * adds something (new structs, or deletions the base does not hold: encodeStateAsUpdate always
+   * carries the whole delete set).  From here on every update of the document is captured by a
+   * synchronous Y.Doc 'update' listener, not by onChange: Hocuspocus runs onChange through the
+   * extension promise chain (Hocuspocus.ts:263, 465-479), where an earlier extension that throws or
+   * awaits I/O would drop or delay it.
    */
   async afterLoadDocument (data) {
     const Y = this._Y()
@@ -104,12 +115,18 @@ class GpuMerge {
     this.docs.set(data.documentName, entry)
     const baseSV = entry.base ? Y.encodeStateVectorFromUpdate(entry.base) : new Uint8Array([0])
     const missing = Y.encodeStateAsUpdate(data.document, baseSV)
-    if (!isEmptyUpdate(missing)) entry.log.push(missing)
+    if (await addsToBase(this._engine(), missing, entry.base, data.documentName)) entry.log.push(missing)
+    if (entry.doc && entry.onUpdate) entry.doc.off('update', entry.onUpdate)
+    entry.doc = data.document
+    entry.onUpdate = update => entry.log.push(update)
+    data.document.on('update', entry.onUpdate)
   }
 
-  /** every post-load update, whatever its origin (Hocuspocus.ts:263; hazard 1) */
+  /** every post-load update, whatever its origin (Hocuspocus.ts:263; hazard 1): captured by the
+   * document listener of afterLoadDocument; onChange only covers a host that never ran that hook */
   async onChange (data) {
     let entry = this.docs.get(data.documentName)
+    if (entry && entry.onUpdate) return
     if (!entry) { entry = { base: null, log: [] }; this.docs.set(data.documentName, entry) }
     entry.log.push(data.update)
   }
@@ -121,20 +138,46 @@ class GpuMerge {
     const taken = entry.log.length
     const parts = (entry.base ? [entry.base] : []).concat(entry.log.slice(0, taken))
     let state
-    if (parts.length === 0) state = this._Y().encodeStateAsUpdate(data.document) // nothing captured: same bytes as extension-database
+    let all = false   // the state holds every update applied so far (not only the `taken` ones)
+    if (parts.length === 0) { state = this._Y().encodeStateAsUpdate(data.document); all = true } // nothing captured: extension-database's bytes
     else if (parts.length === 1) state = parts[0]
-    else state = await this._engine().mergeUpdates(parts, data.documentName)
+    else {
+      try {
+        state = await this._engine().mergeUpdates(parts, data.documentName)
+      } catch (e) {
+        // a document the engine refuses (content yjs would re-encode, YGM_ENONCANON; a corrupt stored
+        // base) or a failed batch: unless configured to throw, store what extension-database stores for
+        // it -- the live document's Y.encodeStateAsUpdate (Database.ts:58) -- so it keeps persisting
+        if (this.configuration.onRefused === 'throw') throw e
+        this.refused.push({ documentName: data.documentName, code: e.code || String(e) })
+        state = this._Y().encodeStateAsUpdate(data.document)
+        all = true
+      }
+    }
     await this.store.storeMany([{ payload: data, state: Buffer.from(state.buffer, state.byteOffset, state.byteLength) }])
-    // the stored merge becomes the new base (under the document's saveMutex, Hocuspocus.ts:427)
+    // the stored state becomes the new base (under the document's saveMutex, Hocuspocus.ts:427)
     entry.base = state
-    entry.log.splice(0, taken)
+    entry.log.splice(0, all ? entry.log.length : taken)
   }
 
-  async afterUnloadDocument (data) { this.docs.delete(data.documentName) }
+  async afterUnloadDocument (data) {
+    const entry = this.docs.get(data.documentName)
+    if (entry && entry.doc && entry.onUpdate) entry.doc.off('update', entry.onUpdate)
+    this.docs.delete(data.documentName)
+  }
 
   async onDestroy () { if (this.engine && !this.configuration.engine) this.engine.close(); this.engine = null }
 }
 
-function isEmptyUpdate (u) { return u.length === 2 && u[0] === 0 && u[1] === 0 }
+// does `missing` (encodeStateAsUpdate(doc, baseSV)) add structs, or deletions that `base` does not hold?
+// Without structs its delete set is the document's whole delete set: it adds nothing iff merging it
+// into the base leaves the base's (sorted, merged) delete set unchanged -- decided by two engine merges.
+async function addsToBase (engine, missing, base, name) {
+  if (missing.length > 0 && missing[0] !== 0) return true                  // struct blocks
+  if (missing.length === 2 && missing[1] === 0) return false               // nothing at all
+  if (!base) return true
+  const [withIt, without] = await Promise.all([engine.mergeUpdates([base, missing], name), engine.mergeUpdates([base, Uint8Array.from([0, 0])], name)])
+  return Buffer.compare(Buffer.from(withIt), Buffer.from(without)) !== 0
+}
 
 module.exports = { GpuMerge, DocumentStore, GpuEngine, GpuEnginePool, SyncResponder, fnv1a64, YgmError }

@@ -76,8 +76,8 @@ class SyncResponder {
   _svs (names, states) { return this._pooled() ? this.engine.stateVectorsMany(names, states) : this.engine.stateVectorsMany(states) }
 
   /**
-   * Answers a batch of incoming messages.  For each SyncStep1 message the result is [Step2 reply,
-   * server Step1]: path 'connection' (Connection.handleMessage -> MessageReceiver.apply(doc, connection),
+   * Answers a batch of incoming messages.  For each SyncStep1 message the result is [server Step1,
+   * Step2 reply] (the reference's wire order): path 'connection' (Connection.handleMessage -> MessageReceiver.apply(doc, connection),
    * the websocket path) always sends the server Step1 as a Sync message; path 'reply' (apply with a
    * reply callback) sends it as SyncReply, and only for Sync requests (requestFirstSync,
    * MessageReceiver.ts:39-47 / 137-155); path 'none' omits it.  Other messages give null; a
@@ -119,12 +119,15 @@ class SyncResponder {
     }
     live.forEach((a, k) => {
       if (diffs[k] instanceof Error) { out[a.i] = diffs[k]; return }
-      const replies = [frame(a.documentName, MessageType.Sync, SyncStep.Step2, diffs[k])]
+      // wire order of the reference: the server Step1 is sent while the request is read
+      // (MessageReceiver.ts:141-153), the Step2 reply after it (apply(), :50-61)
+      const replies = []
       const sv = ownSv.get(a.documentName)
       if (sv && !(sv instanceof Error)) {
         if (path === 'connection') replies.push(frame(a.documentName, MessageType.Sync, SyncStep.Step1, sv))
         else if (path === 'reply' && a.messageType === MessageType.Sync) replies.push(frame(a.documentName, MessageType.SyncReply, SyncStep.Step1, sv))
       }
+      replies.push(frame(a.documentName, MessageType.Sync, SyncStep.Step2, diffs[k]))
       out[a.i] = replies
     })
     return out

@@ -126,16 +126,59 @@ test('concurrent stores of many documents', async (engine) => {
   if (mode === 'gpu') assert.ok(engine.stats().calls - before <= 3, 'stores were batched')
 })
 
-// a failing document rejects only its own store (Hocuspocus.ts:431-435)
-test('malformed update rejects only its document', async (engine) => {
+// a failing document rejects only its own store (Hocuspocus.ts:431-435) -- with onRefused 'throw';
+// by default it stores the live document's Y.encodeStateAsUpdate like extension-database instead
+test('refused document: throws only its store, or stores the reference bytes', async (engine) => {
   const db = memoryDb()
-  const ext = new GpuMerge({ ...db, Y, engine })
-  ext.docs.set('bad', { base: Uint8Array.from([1, 1, 5, 0, 4, 1, 1, 0x74]), log: [Uint8Array.from([0, 0])] }) // truncated base
-  const payload = name => ({ documentName: name, document: new Y.Doc(), context: {} })
-  ext.docs.set('good', { base: null, log: [Uint8Array.from([0, 0]), Uint8Array.from([0, 0])] })
-  const r = await Promise.allSettled([ext.onStoreDocument(payload('bad')), ext.onStoreDocument(payload('good'))])
+  const payload = name => { const document = new Y.Doc(); document.getText('t').insert(0, 'live ' + name); return { documentName: name, document, context: {} } }
+  const bad = () => ({ base: Uint8Array.from([1, 1, 5, 0, 4, 1, 1, 0x74]), log: [Uint8Array.from([0, 0])] }) // truncated base
+  const strict = new GpuMerge({ ...db, Y, engine, onRefused: 'throw' })
+  strict.docs.set('bad', bad())
+  strict.docs.set('good', { base: null, log: [Uint8Array.from([0, 0]), Uint8Array.from([0, 0])] })
+  const r = await Promise.allSettled([strict.onStoreDocument(payload('bad')), strict.onStoreDocument(payload('good'))])
   assert.strictEqual(r[0].status, 'rejected')
   assert.strictEqual(r[1].status, 'fulfilled')
+  const lax = new GpuMerge({ ...db, Y, engine })
+  lax.docs.set('bad', bad())
+  const p = payload('bad')
+  await lax.onStoreDocument(p)
+  assert.strictEqual(lax.refused.length, 1)
+  assert.strictEqual(db.rows.get('bad').toString('hex'), Buffer.from(Y.encodeStateAsUpdate(p.document)).toString('hex'))
+  assert.strictEqual(lax.docs.get('bad').log.length, 0)
+})
+
+// the log is captured by a document listener: an earlier extension whose onChange throws, or one that
+// awaits I/O before a store / unload, cannot drop an update (Hocuspocus.ts:263, 465-479)
+test('updates captured even when an earlier onChange throws or stalls', async (engine) => {
+  const db = memoryDb()
+  const thrower = { priority: 2000, async onChange () { throw new Error('boom') } }
+  const staller = { priority: 1500, async onChange () { await sleep(50) } }
+  for (const early of [thrower, staller]) {
+    const ext = new GpuMerge({ ...db, Y, engine })
+    const hp = new MiniHocuspocus({ extensions: [early, ext], Y })
+    const name = 'guard-' + early.priority
+    const doc = await hp.loadDocument(name)
+    doc.transact(() => doc.getText('t').insert(0, 'abc'), 'c1')
+    doc.transact(() => doc.getText('t').insert(3, 'def'), 'c1')
+    await ext.onStoreDocument({ documentName: name, document: doc, context: {} })   // store right away
+    await hp.unloadDocument(name)
+    const d2 = await new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine })], Y }).loadDocument(name)
+    assert.strictEqual(d2.getText('t').toString(), 'abcdef')
+    assert.ok(!ext.docs.has(name))                                      // no orphan entry after unload
+  }
+})
+
+// a reload of a document with deletions does not queue a duplicate of its delete set
+test('afterLoadDocument adds nothing when the load added nothing', async (engine) => {
+  const db = memoryDb()
+  const hp = new MiniHocuspocus({ extensions: [new GpuMerge({ ...db, Y, engine })], Y })
+  const doc = await hp.loadDocument('dels')
+  doc.transact(() => doc.getText('t').insert(0, 'hello world'), 'c1')
+  doc.transact(() => doc.getText('t').delete(0, 6), 'c1')
+  await hp.flushAll(); await hp.lastStore
+  const ext2 = new GpuMerge({ ...db, Y, engine })
+  await new MiniHocuspocus({ extensions: [ext2], Y }).loadDocument('dels')
+  assert.strictEqual(ext2.docs.get('dels').log.length, 0)
 })
 
 // SURVEY.md §8e: documents sharded over the node's GPUs by fnv1a64(documentName) mod N
@@ -191,7 +234,7 @@ test('sync responder answers a SyncStep1 batch', async (engine) => {
   want.forEach(({ n, sv }, i) => {
     const e = ext.docs.get(n)
     const state = Y.mergeUpdates([e.base].concat(e.log))
-    const [step2, step1] = replies[i]
+    const [step1, step2] = replies[i]                                   // the reference's order: server Step1, then Step2
     const a = decodeSyncMessage(step2); const b = decodeSyncMessage(step1)
     assert.strictEqual(a.documentName, n); assert.strictEqual(a.messageType, MessageType.Sync); assert.strictEqual(a.step, SyncStep.Step2)
     assert.strictEqual(Buffer.from(a.payload).toString('hex'), Buffer.from(Y.diffUpdate(state, sv)).toString('hex'))

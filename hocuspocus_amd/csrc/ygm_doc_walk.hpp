@@ -39,7 +39,15 @@ namespace ygm {
 
 constexpr int DW_S = 4;           // 64-byte chunk slots per lane ring
 constexpr int DW_P = DW_S * 4;    // 16-byte pieces per ring
-constexpr int DW_R = 4;           // parse iterations per round (<= 3 staged chunks = 192 bytes per round)
+#ifndef YGM_DW_R
+#define YGM_DW_R 4
+#endif
+#ifndef YGM_DW_STG
+#define YGM_DW_STG 3
+#endif
+constexpr int DW_R = YGM_DW_R;    // parse iterations per round
+constexpr uint32_t DW_STG = YGM_DW_STG;   // chunks staged per round (<= 4: 64 staging registers)
+constexpr uint32_t DW_AHEAD = 2;  // chunks staged past the ring's free slots (committed if the round freed theirs)
 constexpr int DW_BATCH = 256;     // documents sorted (largest first) per batch of a wave's range
 constexpr int DW_SVN = 16;        // state-vector entries per lane (diff)
 constexpr uint32_t DW_OPEN = 0xFFFFFFFFu;
@@ -164,20 +172,29 @@ YDEV void dw_commit(DWLds& L, uint32_t l, uint32_t k, const u32x4& p0, const u32
   prev8 = (uint32_t)(Hm >> 56);
 }
 
+// the bytes of the varuint of v in the low bytes
+YDEV uint64_t dw_vu_enc(uint32_t v) {
+  const uint64_t x = (uint64_t)(v & 0x7Fu) | ((uint64_t)((v >> 7) & 0x7Fu) << 8) | ((uint64_t)((v >> 14) & 0x7Fu) << 16) |
+                     ((uint64_t)((v >> 21) & 0x7Fu) << 24) | ((uint64_t)(v >> 28) << 32);
+  return x | (0x8080808080ull & ((1ull << (8u * (dw_vulen(v) - 1u))) - 1ull));
+}
+// appends the varuint of v at byte `at` of the 16-byte value (lo, hi) (at + its length <= 16)
+YDEV void dw_app(uint64_t& lo, uint64_t& hi, uint32_t& at, uint32_t v) {
+  const uint64_t x = dw_vu_enc(v);
+  if (at < 8u) { lo |= x << (8u * at); hi |= at ? x >> (64u - 8u * at) : 0ull; }
+  else hi |= x << (8u * (at - 8u));
+  at += dw_vulen(v);
+}
+// one 16-byte store at any alignment
+YDEV void dw_st16(uint8_t* __restrict__ o, uint64_t lo, uint64_t hi) {
+  u32x4 v;
+  v.x = (uint32_t)lo; v.y = (uint32_t)(lo >> 32); v.z = (uint32_t)hi; v.w = (uint32_t)(hi >> 32);
+  __builtin_memcpy(o, &v, 16);
+}
 // byte stores of a varuint at o[t..]; returns the new position
 YDEV uint64_t dw_put_vu(uint8_t* __restrict__ o, uint64_t t, uint32_t v) {
   while (v > 127u) { o[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; }
   o[t++] = (uint8_t)v;
   return t;
 }
-// ring bytes [r, r + n) to o[t..]: 16-byte pieces (any alignment on both sides), then single bytes
-YDEV void dw_put_ring(const DWLds& L, uint32_t l, uint8_t* __restrict__ o, uint64_t t, uint32_t r, uint32_t n) {
-  uint32_t k = 0;
-  for (; k + 16u <= n; k += 16u) {
-    const u32x4 v = dw_ring16(L, l, r + k);
-    __builtin_memcpy(o + t + k, &v, 16);
-  }
-  for (; k < n; k++) o[t + k] = (uint8_t)dw_byte(L, l, r + k);
-}
-
 }  // namespace ygm

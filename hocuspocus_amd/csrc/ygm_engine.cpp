@@ -21,9 +21,11 @@ size_t ygm_k_drec_bytes();
 int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,
                      const uint32_t* docs, uint64_t out_base, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
                      uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
+size_t ygm_k_sv_table_bytes(uint32_t n_docs);
 int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
                           uint64_t sv_bytes, const uint64_t* sv_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
-                          uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
+                          uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list, uint64_t out_cap, uint8_t* tbl,
+                          uint32_t* tbl_n, hipStream_t s);
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
                             uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
@@ -92,6 +94,7 @@ struct ygm_ctx {
   void* meta_slot(int i) const { return (uint8_t*)meta.p + (size_t)i * sizeof(Meta); }
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
   DevBuf big_blk, big_rec, big_list;   // large-document tier: block tables, struct records, documents sent on
+  DevBuf sv_tbl, sv_tn;                // diff: sorted state-vector tables (k_sv_table) and their entry counts
   // host results
   std::vector<uint8_t> h_data;
   std::vector<uint64_t> h_off, h_len;
@@ -159,7 +162,7 @@ void ygm_close(ygm_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
-                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list})
+                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn})
     b->release();
   for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
   if (c->h_meta) (void)hipHostFree(c->h_meta);
@@ -335,10 +338,11 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
   int e = prep_outputs(c, n_docs, out_cap, s, true);
   if (e) return e;
   void* meta = c->meta_slot(2);
+  if (mode == 1 && (!c->sv_tbl.ensure(ygm_k_sv_table_bytes(n_docs)) || !c->sv_tn.ensure(4ull * n_docs + 4))) return YGM_ENOMEM;
   HIPCHK(hipEventRecord(c->e0, s));
   if (ygm_k_launch_doc_lean(mode, d_arena, arena_bytes, d_doc_off, d_sv, sv_bytes, d_sv_off, n_docs, c->flags, c->out.as<uint8_t>(),
                             c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta,
-                            c->defer_list.as<uint32_t>(), out_cap, s))
+                            c->defer_list.as<uint32_t>(), out_cap, c->sv_tbl.as<uint8_t>(), c->sv_tn.as<uint32_t>(), s))
     return YGM_EDEVICE;
   HIPCHK(hipEventRecord(c->e1, s));
   Meta m;

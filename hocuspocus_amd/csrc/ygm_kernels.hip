@@ -30,7 +30,7 @@
 
 #ifdef YGM_DIAG
 // diagnostic build only (libygm_diag.so): per-phase shader-clock sums of k_merge_fast
-__device__ unsigned long long ygm_diag[24];
+__device__ unsigned long long ygm_diag[32];
 #define DIAG_T0 unsigned long long _dt = __builtin_amdgcn_s_memtime();
 #define DIAG(i) do { if (threadIdx.x == 0) { unsigned long long _n = __builtin_amdgcn_s_memtime(); atomicAdd(&ygm_diag[i], _n - _dt); _dt = _n; } } while (0)
 #define DIAGW(i) do { if ((threadIdx.x & 63) == 0) { unsigned long long _n = __builtin_amdgcn_s_memtime(); atomicAdd(&ygm_diag[8 + (i)], _n - _dt); _dt = _n; } } while (0)
@@ -160,22 +160,66 @@ YDEV uint64_t dw_shfl64(uint64_t v, uint32_t src) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// MODE 1: per-lane state-vector tables, sorted by client descending (the block order), and the
-// scratch of the cooperative parse
-template <int MODE>
-struct DWSvt {
-  uint32_t c[MODE == 1 ? DW_SVN : 1][WAVE], k[MODE == 1 ? DW_SVN : 1][WAVE];
-  uint32_t tc[DW_SVN + 1], tk[DW_SVN + 1];
-};
+// diffUpdate pre-pass: each document's state vector (decodeStateVector, Y@37797: a count, then
+// (client, clock) varuints; a repeated client's last entry wins, as in its Map) parsed by one lane into
+// a table sorted by client descending -- the order of the update's client blocks -- at tbl + 144 d as
+// (client, clock) u32 pairs; tbl_n[d] = entries, or DW_TBL_BAD for a vector the walker leaves to the
+// exact kernel (> DW_SVN entries, > DW_TBL_MAXB bytes, values >= 2^32, truncated, trailing bytes).
+constexpr uint32_t DW_TBL_BAD = 0x80000000u;
+constexpr uint32_t DW_TBL_MAXB = 160u;   // state-vector bytes staged per lane (16 entries of <= 10 bytes)
+__global__ __launch_bounds__(WAVE) void k_sv_table(const uint8_t* __restrict__ sv_arena, const uint64_t* __restrict__ sv_off,
+                                                  uint32_t n_docs, uint8_t* __restrict__ tbl, uint32_t* __restrict__ tbl_n) {
+  __shared__ u32x4 buf[DW_TBL_MAXB / 16 + 1][WAVE];
+  __shared__ uint32_t ec[DW_SVN][WAVE], ek[DW_SVN][WAVE];
+  const uint32_t l = threadIdx.x, d = blockIdx.x * WAVE + l;
+  if (d >= n_docs) return;
+  const uint64_t sa = sv_off[d], sb = sv_off[d + 1];
+  const uint32_t len = sb > sa ? (uint32_t)(sb - sa) : 0u;
+  uint32_t bad = (sb < sa || len == 0u || len > DW_TBL_MAXB) ? 1u : 0u;
+  const uint32_t o0 = (uint32_t)(sa & 15u);
+  const u32x4* src = (const u32x4*)(sv_arena + (sa & ~15ull));
+  const uint32_t np = bad ? 0u : (o0 + len + 15u) >> 4;
+  for (uint32_t i = 0; i < np; i++) buf[i][l] = src[i];
+  const uint8_t* b = (const uint8_t*)&buf[0][0];
+  auto byte = [&](uint32_t i) -> uint32_t { return b[((i >> 4) * WAVE + l) * 16u + (i & 15u)]; };
+  uint32_t pos = o0, end = o0 + (bad ? 0u : len);
+  auto vu = [&]() -> uint32_t {   // varuint < 2^32 inside the vector, else bad
+    uint64_t v = 0;
+    for (uint32_t sh = 0;; sh += 7) {
+      if (pos >= end || sh > 28) { bad = 1; return 0u; }
+      const uint32_t x = byte(pos++);
+      v |= (uint64_t)(x & 0x7Fu) << sh;
+      if (x < 0x80u) break;
+    }
+    if (v >> 32) bad = 1;
+    return (uint32_t)v;
+  };
+  const uint32_t cnt = bad ? 0u : vu();
+  bad |= cnt > (uint32_t)DW_SVN ? 1u : 0u;
+  uint32_t n = 0;
+  for (uint32_t e = 0; e < (bad ? 0u : cnt); e++) {
+    const uint32_t c = vu(), k = vu();
+    if (bad) break;
+    uint32_t j = 0;
+    while (j < n && ec[j][l] > c) j++;
+    if (j < n && ec[j][l] == c) { ek[j][l] = k; continue; }   // the last entry of a client wins
+    for (uint32_t m = n; m > j; m--) { ec[m][l] = ec[m - 1][l]; ek[m][l] = ek[m - 1][l]; }
+    ec[j][l] = c; ek[j][l] = k; n++;
+  }
+  bad |= pos != end ? 1u : 0u;   // trailing bytes: the exact kernel decides
+  if (bad) { tbl_n[d] = DW_TBL_BAD; return; }
+  uint64_t* t = (uint64_t*)(tbl + 144ull * d);
+  for (uint32_t j = 0; j < n; j++) t[j] = ((uint64_t)ek[j][l] << 32) | ec[j][l];
+  tbl_n[d] = n;
+}
 
 template <int MODE>
-__global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off,
-                                                  const uint8_t* __restrict__ sv_arena, const uint64_t* __restrict__ sv_off,
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2))) void k_doc_walk(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off,
+                                                  const uint8_t* __restrict__ tbl, const uint32_t* __restrict__ tbl_n,
                                                   uint32_t n_docs, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                   uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
                                                   uint32_t* __restrict__ defer_list, uint64_t out_cap) {
   __shared__ DWLds L;
-  __shared__ DWSvt<MODE> S;
   __shared__ uint64_t ordk[DW_BATCH];      // the current batch of documents, largest first: (bytes << 32 | index in batch)
   const uint32_t l = threadIdx.x;
   const uint32_t D1 = (uint32_t)((uint64_t)n_docs * (blockIdx.x + 1) / gridDim.x);
@@ -183,26 +227,29 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
   uint32_t bbase = bnext, bn = 0, next = 0;                                  // the batch [bbase, bbase + bn); next: its first untaken entry
 
   // offsets of the next 64 documents of the batch (lane i: entry next + i), loaded one round ahead
-  uint32_t pd = 0;
-  uint64_t pa = 0, pb = 0, psa = 0, psb = 0;
+  uint32_t pd = 0, ptn = 0;
+  uint64_t pa = 0, pb = 0;
   auto prefetch = [&]() {
-    pa = 0; pb = 0; psa = 0; psb = 0; pd = 0;
+    pa = 0; pb = 0; ptn = 0; pd = 0;
     if (next + l < bn) {
       pd = bbase + (uint32_t)ordk[next + l];
       pa = doc_off[pd]; pb = doc_off[pd + 1];
-      if (MODE == 1) { psa = sv_off[pd]; psb = sv_off[pd + 1]; }
+      if (MODE == 1) ptn = tbl_n[pd];
     }
   };
 
   // ---- lane state
   uint32_t ph = WK_IDLE, d = 0, bad = 0;
   uint64_t da = 0, db = 0;                 // the document's bytes in `arena`
-  bool seg_sv = false;                     // segment walked: the state vector (diff) or the document
-  uint64_t cbase = 0;                      // 16-byte aligned segment-arena offset of ring-relative byte 0
-  uint32_t srel = 0, q = 0, rb = 0;        // segment start / parse position / segment end, ring-relative
+  // the lane's stream: MODE 1 first the document's state-vector table (chunks [0, tc): ring-relative bytes
+  // [0, 8 nsv) = the table at tbl + 144 d), then the document; ring-relative byte r >= 64 tc is arena byte
+  // cbase + r - 64 tc
+  uint32_t tc = 0;
+  uint64_t cbase = 0;                      // 16-byte aligned arena offset of the document's first chunk
+  uint32_t srel = 0, q = 0, rb = 0;        // document start / parse position / document end, ring-relative
   uint32_t landed = 0, stg_n = 0, stg_k = 0, prev8 = 0;
   u32x4 g0 = {0u, 0u, 0u, 0u}, g1 = g0, g2 = g0, g3 = g0, g4 = g0, g5 = g0, g6 = g0, g7 = g0;   // staged chunks
-  u32x4 g8 = g0, g9 = g0, g10 = g0, g11 = g0;
+  u32x4 g8 = g0, g9 = g0, g10 = g0, g11 = g0, g12 = g0, g13 = g0, g14 = g0, g15 = g0;
   uint32_t n_left = 0, st_left = 0, client = 0, clock = 0, prevc = 0;
   bool have_prev = false;
   uint64_t slot = 0;                       // the document's output slot; t / tend / e_dst / cdst relative to it
@@ -218,9 +265,13 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
   bool e_on = false;
   uint32_t e_dst = 0;
   uint32_t e_a = 0, e_b = 0, e_c = 0, e_pl = 0, e_info = 0, e_oclk = 0, e_q = 0, e_ro_p = 0, e_ro_e = 0, e_clen = 0;
-  // MODE 1: state vector (S.c / S.k [0, nsv), svp = first entry not above the current block's client);
+  // MODE 1: the state vector, sorted by client descending (the block order), as a register queue: entries
+  // (sc[i], sk[i]) for i < nsv; the head is the first entry not above the current block's client
   // copy run (ring bytes [cp, run_end) -> output at cdst)
-  uint32_t nsv = 0, svp = 0, svc = 0;
+  uint32_t nsv = 0, svc = 0;
+  uint32_t sc[MODE == 1 ? DW_SVN : 1], sk[MODE == 1 ? DW_SVN : 1];
+#pragma unroll
+  for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) { sc[i] = 0; sk[i] = 0; }
   bool emitted = false, run_on = false;
   uint32_t cp = 0, run_end = 0, rs0 = 0;
   uint32_t cdst = 0, cd0 = 0;
@@ -229,8 +280,12 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
 #ifdef YGM_DIAG
   unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // lane-iterations: fast, general, not ready, idle, string; rounds, general iterations
 #define WDG(i, v) dg[i] += (v)
+  // wave shader-clock per section (wave-uniform code): commit, SV parse, grab + output + init, staging, parse
+  unsigned long long tsec[5] = {0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
+#define WSEC(i) do { const unsigned long long _n = __builtin_amdgcn_s_memtime(); tsec[i] += _n - tprev; tprev = _n; } while (0)
 #else
 #define WDG(i, v)
+#define WSEC(i)
 #endif
 
   // end of a client block (after its last struct): MODE 0 queues the block's state-vector entry,
@@ -260,14 +315,13 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
     st_left = nst; client = cl; clock = ck;
     if (MODE == 0) { cc = cl; stop = ck != 0u; clk = 0u; }
     else {   // the state-vector clock of the client: walk the descending table
-      uint32_t s = 0;
-      while (svp < nsv) {
-        const uint32_t c = S.c[svp][l];
-        if (c > cl) { svp++; continue; }
-        if (c == cl) s = S.k[svp][l];
-        break;
+      while (nsv && sc[0] > cl) {   // entries of clients above this block's: not in the update
+#pragma unroll
+        for (int i = 0; i + 1 < DW_SVN; i++) { sc[i] = sc[i + 1]; sk[i] = sk[i + 1]; }
+        nsv--;
       }
-      svc = s; emitted = false;
+      svc = nsv && sc[0] == cl ? sk[0] : 0u;
+      emitted = false;
     }
     ph = WK_ST;
   };
@@ -276,7 +330,9 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
     // ---- (0) a new batch of documents: sorted by size, largest first (the documents left at the end of a
     //      wave's range are its smallest: the last lanes to finish wait least)
     if (next >= bn && bnext < D1) {
-      bbase = bnext; bn = D1 - bnext < (uint32_t)DW_BATCH ? D1 - bnext : (uint32_t)DW_BATCH; bnext = bbase + bn; next = 0;
+      // equal batches of <= DW_BATCH: a short last batch would leave most lanes idle behind its largest document
+      const uint32_t rem = D1 - bnext, nbat = (rem + DW_BATCH - 1u) / DW_BATCH;
+      bbase = bnext; bn = (rem + nbat - 1u) / nbat; bnext = bbase + bn; next = 0;
       for (uint32_t e = l; e < (uint32_t)DW_BATCH; e += WAVE) {
         // key bytes + 1 (padding entries past bn: 0, sorted behind every document)
         const uint64_t sz = e < bn ? doc_off[bbase + e + 1] - doc_off[bbase + e] + 1ull : 0ull;
@@ -294,122 +350,110 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
         }
       prefetch();
     }
+    WSEC(4);
     // ---- (1) the chunks staged last round land in the ring (the compiler waits for their loads here)
+    //      -- those whose ring slot is free by now: staging runs DW_AHEAD chunks past the ring, betting on this
+    //      round's consumption; a chunk that lost the bet is dropped here and staged again
     if (stg_n) {
-      dw_commit<MODE == 1>(L, l, stg_k, g0, g1, g2, g3, stg_k == 0u ? srel : 0u, rb - 64u * stg_k < 64u ? rb - 64u * stg_k : 64u, prev8, bad);
+      uint32_t need = ph == WK_STR ? sp : (MODE == 1 && ph == WK_SVN) ? 0u : q;   // (the table stays until copied)
+      if (run_on && cp < need) need = cp;
+      if (MODE == 1 && e_on && e_q < need) need = e_q;   // the pending cut struct's right origin is copied from the ring
+      const uint32_t lim = (need >> 6) + DW_S;
+      if (stg_k + stg_n > lim) stg_n = lim > stg_k ? lim - stg_k : 0u;
+    }
+    if (stg_n) {
+      // the document part [vlo, vhi) of chunk k is checked (table chunks: none)
+      auto vlo = [&](uint32_t k) { return k == tc ? srel - 64u * tc : 0u; };
+      auto vhi = [&](uint32_t k) { return k < tc ? 0u : (rb - 64u * k < 64u ? rb - 64u * k : 64u); };
+      dw_commit<MODE == 1>(L, l, stg_k, g0, g1, g2, g3, vlo(stg_k), vhi(stg_k), prev8, bad);
       if (stg_n > 1u) {
         const uint32_t k1 = stg_k + 1u;
-        dw_commit<MODE == 1>(L, l, k1, g4, g5, g6, g7, 0u, rb - 64u * k1 < 64u ? rb - 64u * k1 : 64u, prev8, bad);
+        dw_commit<MODE == 1>(L, l, k1, g4, g5, g6, g7, vlo(k1), vhi(k1), prev8, bad);
       }
       if (stg_n > 2u) {
         const uint32_t k2 = stg_k + 2u;
-        dw_commit<MODE == 1>(L, l, k2, g8, g9, g10, g11, 0u, rb - 64u * k2 < 64u ? rb - 64u * k2 : 64u, prev8, bad);
+        dw_commit<MODE == 1>(L, l, k2, g8, g9, g10, g11, vlo(k2), vhi(k2), prev8, bad);
+      }
+      if (DW_STG > 3u && stg_n > 3u) {
+        const uint32_t k3 = stg_k + 3u;
+        dw_commit<MODE == 1>(L, l, k3, g12, g13, g14, g15, vlo(k3), vhi(k3), prev8, bad);
       }
       landed = stg_k + stg_n;
       stg_n = 0;
     }
-    // ---- (1b) diff: state vectors that have landed are parsed by the whole wave, one after the other
-    //      (byte per lane, terminator ballot, value per varuint end), then sorted by client descending
-    //      into the owner's table, the last entry of a repeated client winning (decodeStateVector's Map)
+    WSEC(0);
+    // ---- (1b) diff: a landed state-vector table moves from the ring to the lane's table, the document follows
     if (MODE == 1) {
-      uint64_t fm = __ballot(ph == WK_SVN && (landed << 6) >= rb);
-      while (fm) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(fm);
-        fm &= fm - 1ull;
-        const uint32_t js = rdlane(srel, j), jn = rdlane(rb, j) - js;
-        uint32_t jb = (jn == 0u || jn > 128u) ? 1u : 0u;
-        const uint32_t blo = l < jn ? dw_byte(L, j, js + l) : 0x80u;
-        const uint32_t bhi = l + 64u < jn ? dw_byte(L, j, js + 64u + l) : 0x80u;
-        const uint64_t T0 = __ballot(blo < 0x80u), T1 = __ballot(bhi < 0x80u);
-        const uint32_t n_ent = rdlane(blo, 0);
-        jb |= (!(T0 & 1ull) || n_ent > (uint32_t)DW_SVN) ? 1u : 0u;
-        jb |= (uint32_t)(__popcll(T0) + __popcll(T1)) != 1u + 2u * n_ent ? 1u : 0u;
-        const uint32_t lastp = T1 ? 127u - (uint32_t)__builtin_clzll(T1) : (T0 ? 63u - (uint32_t)__builtin_clzll(T0) : 0u);
-        jb |= lastp + 1u != jn ? 1u : 0u;   // trailing bytes: the exact kernel decides
-        uint32_t lb = 0;
+      const bool cpy = ph == WK_SVN && landed >= tc;
+      const uint64_t cm = __ballot(cpy);
+      if (cm && cpy) {
 #pragma unroll
-        for (int h = 0; h < 2; h++) {   // bytes l and l + 64: a varuint ends here -> its value
-          const uint32_t pos = (uint32_t)h * 64u + l;
-          const bool term = h ? bhi < 0x80u : blo < 0x80u;
-          if (term && pos < jn) {
-            const uint64_t below = h ? (T1 & dw_lowmask(l)) : (T0 & dw_lowmask(l));
-            const uint32_t kk = h ? (uint32_t)__popcll(T0) + (uint32_t)__popcll(below) : (uint32_t)__popcll(below);
-            const uint32_t prevp = h ? (below ? 64u + 63u - (uint32_t)__builtin_clzll(below) : (T0 ? 63u - (uint32_t)__builtin_clzll(T0) : DW_OPEN))
-                                     : (below ? 63u - (uint32_t)__builtin_clzll(below) : DW_OPEN);
-            const uint32_t st0 = prevp + 1u, nb = pos - prevp;
-            const uint32_t v = dw_val(dw_rd8(L, j, js + st0), nb, lb);
-            if (kk >= 1u && kk <= 2u * (uint32_t)DW_SVN) { if (kk & 1u) S.tc[(kk - 1u) >> 1] = v; else S.tk[(kk - 1u) >> 1] = v; }
-          }
+        for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) {
+          const uint64_t w = (uint32_t)i < nsv ? dw_word(L, l, 8u * (uint32_t)i) : 0ull;
+          sc[i] = (uint32_t)w; sk[i] = (uint32_t)(w >> 32);
         }
-        jb |= __ballot(lb != 0u) ? 1u : 0u;
-        __syncthreads();
-        const bool ent = l < n_ent && !jb;
-        const uint32_t ec = ent ? S.tc[l] : 0u, ek = ent ? S.tk[l] : 0u;
-        bool drop = false;
-        for (uint32_t e2 = 0; e2 < (jb ? 0u : n_ent); e2++) drop |= e2 > l && rdlane(ec, e2) == ec;
-        const uint64_t keep = __ballot(ent && !drop);
-        uint32_t rank = 0;
-        for (uint32_t e2 = 0; e2 < (jb ? 0u : n_ent); e2++) rank += ((keep >> e2) & 1ull) && rdlane(ec, e2) > ec ? 1u : 0u;
-        if (ent && !drop) { S.c[rank][j] = ec; S.k[rank][j] = ek; }
-        __syncthreads();
-        if (l == j) {   // the document itself next
-          bad |= jb;
-          nsv = (uint32_t)__popcll(keep); svp = 0;
-          seg_sv = false;
-          cbase = da & ~15ull; srel = (uint32_t)(da - cbase); q = srel; rb = (uint32_t)(db - cbase);
-          landed = 0; stg_n = 0; prev8 = 0;
-          ph = WK_UPD;
-        }
+        ph = WK_UPD;
       }
     }
+    WSEC(1);
     // ---- (2) lanes that are idle or finishing take the wave's next documents
     const bool want = ph == WK_IDLE || ph == WK_FIN;
     const uint64_t wm = __ballot(want);
     const uint32_t rank = lanes_below(wm) & 63u;
     const uint64_t na = dw_shfl64(pa, rank), nb = dw_shfl64(pb, rank);
     const uint32_t nd = (uint32_t)__shfl((int)pd, (int)rank);
-    uint64_t nsa = 0, nsb = 0;
-    if (MODE == 1) { nsa = dw_shfl64(psa, rank); nsb = dw_shfl64(psb, rank); }
+    const uint32_t ntn = MODE == 1 ? (uint32_t)__shfl((int)ptn, (int)rank) : 0u;
     const uint32_t avail = bn - next;
     const bool got = want && rank < avail;
     const uint32_t npop = (uint32_t)__popcll(wm);
     next += npop < avail ? npop : avail;
     // ---- (3) output of the last round: pending header / entry, the copy run, finished documents
+    // Output stores are 16 bytes wide, whatever the byte count: the bytes past a store's valid part are
+    // overwritten by the document's next store (a lane writes its output in increasing order) or lie
+    // in the slot's last 16 bytes, which tend keeps free
     if (e_on) {
       e_on = false;
       if (!bad) {
-        uint64_t o = dw_put_vu(ob, e_dst, e_a);
-        o = dw_put_vu(ob, o, e_b);
-        if (MODE == 1) {
-          o = dw_put_vu(ob, o, e_c);
-          if (e_pl) {
-            ob[o++] = (uint8_t)e_info;
-            if (e_info) {   // an item: origin (client, clock + off - 1), right origin verbatim
-              o = dw_put_vu(ob, o, e_b);
-              o = dw_put_vu(ob, o, e_oclk);
-              dw_put_ring(L, l, ob, o, e_q + e_ro_p, e_ro_e - e_ro_p);
-              o += e_ro_e - e_ro_p;
-            }
-            dw_put_vu(ob, o, e_clen);
+        uint64_t lo = dw_vu_enc(e_a), hi = 0;
+        uint32_t at = dw_vulen(e_a);
+        dw_app(lo, hi, at, e_b);
+        if (MODE == 1) dw_app(lo, hi, at, e_c);
+        dw_st16(ob + e_dst, lo, hi);
+        if (MODE == 1 && e_pl) {   // the re-encoded prefix of a cut struct
+          uint64_t o = e_dst + at;
+          ob[o++] = (uint8_t)e_info;
+          if (e_info) {   // an item: origin (client, clock + off - 1), right origin verbatim
+            o = dw_put_vu(ob, o, e_b);
+            o = dw_put_vu(ob, o, e_oclk);
+            for (uint32_t k = e_ro_p; k < e_ro_e; k++) ob[o++] = (uint8_t)dw_byte(L, l, e_q + k);
           }
+          dw_put_vu(ob, o, e_clen);
         }
       }
     }
-    if (MODE == 1 && run_on) {
+    if (MODE == 1 && run_on) {   // the copy run: ring bytes [cp, run_end) -> output at cdst
       if (bad) run_on = false;
       else {
         const uint32_t done = ph == WK_STR ? sp : q;
-        uint32_t ce = run_end < done ? run_end : done;
-        if (ce < cp) ce = cp;
-        const bool fin = ce == run_end;
-        uint32_t n = ce - cp;
-        if (!fin) n &= ~15u;
-        if (cdst + n > tend) bad = 1;
-        else {
-          dw_put_ring(L, l, ob, cdst, cp, n);
-          cp += n; cdst += n;
-          if (fin) run_on = false;
+        const bool fin = run_end <= done;
+        const uint32_t ce = fin ? run_end : (done & ~15u);   // an open run is written up to a ring piece boundary
+        if (ce > cp) {
+          if (cdst + (ce - cp) > tend) bad = 1;
+          else {
+            if (cp & 15u) {   // the head, up to the next ring piece boundary
+              const u32x4 v = dw_ring16(L, l, cp);
+              __builtin_memcpy(ob + cdst, &v, 16);
+              const uint32_t a = 16u - (cp & 15u) < ce - cp ? 16u - (cp & 15u) : ce - cp;
+              cp += a; cdst += a;
+            }
+            for (; cp < ce; cp += 16u, cdst += 16u) {   // whole ring pieces
+              const u32x4 v = L.ring[(cp >> 4) & (DW_P - 1)][l];
+              __builtin_memcpy(ob + cdst, &v, 16);
+            }
+            cdst -= cp - ce; cp = ce;
+          }
         }
+        if (fin && !bad) run_on = false;
       }
     }
     if (ph == WK_FIN) {
@@ -420,9 +464,10 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
         base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(bm));
         if (bad) { defer_list[base + lanes_below(bm)] = d; status[d] = ST_FALLBACK; }
       }
-      if (!bad) {
+      if (!bad) {   // the count, right-aligned in the slot's first 16 bytes (an aligned store)
         const uint32_t hl = dw_vulen(count);
-        dw_put_vu(ob, 16u - hl, count);
+        const uint64_t c = dw_vu_enc(count);
+        dw_st16(ob, 0ull, c << (64u - 8u * hl));
         out_off[d] = slot + 16u - hl; out_len[d] = hl + (t - 16u); status[d] = ST_OK;
         payload += hl + (t - 16u);
       }
@@ -430,35 +475,42 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
     }
     // ---- (4) new documents
     if (got) {
-      d = nd; bad = 0; da = na; db = nb; count = 0; emitted = false; have_prev = false; nsv = 0; svp = 0;
+      d = nd; bad = 0; da = na; db = nb; count = 0; emitted = false; have_prev = false; nsv = 0;
       slot = merge_slot(da, d);
       ob = out + slot;
       const uint64_t cap = merge_slot_cap(db - da), room = out_cap > slot ? out_cap - slot : 0ull;
-      tend = (uint32_t)(cap < room ? cap : room);
+      const uint64_t lim = cap < room ? cap : room;
+      tend = lim > 16u ? (uint32_t)(lim - 16u) : 0u;   // (16 bytes of slack for the wide stores)
       t = 16u;   // the header (a count known only at the end) goes right-aligned in front of the body
-      const uint64_t sa = MODE == 1 ? nsa : da, sb = MODE == 1 ? nsb : db;
-      seg_sv = MODE == 1;
-      cbase = sa & ~15ull; srel = (uint32_t)(sa - cbase); q = srel; rb = (uint32_t)(sb - cbase);
+      nsv = MODE == 1 && ntn <= (uint32_t)DW_SVN ? ntn : 0u;
+      bad |= (MODE == 1 && ntn > (uint32_t)DW_SVN) ? 1u : 0u;   // (DW_TBL_BAD: the exact kernel)
+      tc = (8u * nsv + 63u) >> 6;
+      cbase = da & ~15ull; srel = 64u * tc + (uint32_t)(da - cbase); q = srel; rb = 64u * tc + (uint32_t)(db - cbase);
       landed = 0; stg_n = 0; prev8 = 0;
-      bad |= (sb < sa || db < da || ((sb - sa) >> 30) || ((db - da) >> 30)) ? 1u : 0u;
-      ph = MODE == 1 ? WK_SVN : WK_UPD;
+      bad |= (db < da || ((db - da) >> 30)) ? 1u : 0u;
+      ph = tc ? WK_SVN : WK_UPD;
     }
     if (__ballot(ph != WK_IDLE) == 0 && next >= bn && bnext >= D1) break;
+    WSEC(2);
     // ---- (5) stage the next chunks of the segment (up to three; the ring keeps DW_S)
     if (ph != WK_IDLE && ph != WK_FIN) {
-      uint32_t need = ph == WK_STR ? sp : q;
+      uint32_t need = ph == WK_STR ? sp : (MODE == 1 && ph == WK_SVN) ? 0u : q;
       if (run_on && cp < need) need = cp;
       const uint32_t nch = (rb + 63u) >> 6;
-      const uint32_t wk = (need >> 6) + DW_S < nch ? (need >> 6) + DW_S : nch;
-      const uint32_t n = wk > landed ? (wk - landed < 3u ? wk - landed : 3u) : 0u;
+      const uint32_t wk = (need >> 6) + DW_S + DW_AHEAD < nch ? (need >> 6) + DW_S + DW_AHEAD : nch;
+      const uint32_t n = wk > landed ? (wk - landed < DW_STG ? wk - landed : DW_STG) : 0u;
       stg_k = landed; stg_n = n;
-      const u32x4* src = (const u32x4*)((seg_sv ? sv_arena : arena) + cbase + 64ull * landed);
-      if (n >= 1u) { g0 = src[0]; g1 = src[1]; g2 = src[2]; g3 = src[3]; }
-      if (n >= 2u) { g4 = src[4]; g5 = src[5]; g6 = src[6]; g7 = src[7]; }
-      if (n >= 3u) { g8 = src[8]; g9 = src[9]; g10 = src[10]; g11 = src[11]; }
+      auto chunk = [&](uint32_t k) -> const u32x4* {
+        return (const u32x4*)(MODE == 1 && k < tc ? tbl + 144ull * d + 64u * k : arena + cbase + 64ull * (k - tc));
+      };
+      if (n >= 1u) { const u32x4* p = chunk(landed); g0 = p[0]; g1 = p[1]; g2 = p[2]; g3 = p[3]; }
+      if (n >= 2u) { const u32x4* p = chunk(landed + 1u); g4 = p[0]; g5 = p[1]; g6 = p[2]; g7 = p[3]; }
+      if (n >= 3u) { const u32x4* p = chunk(landed + 2u); g8 = p[0]; g9 = p[1]; g10 = p[2]; g11 = p[3]; }
+      if (DW_STG > 3u && n >= 4u) { const u32x4* p = chunk(landed + 3u); g12 = p[0]; g13 = p[1]; g14 = p[2]; g15 = p[3]; }
     }
     // ---- (6) offsets of the documents the next round hands out
     prefetch();
+    WSEC(3);
     // ---- (7) parse: per lane and iteration one unit, by the fast decoder when it has the common shape
     //      (an Item with origin(s) and a one-byte String / Deleted length inside 32 bytes, a block header
     //      of a <= 2-byte count and a one-byte clock, a one-byte update header, an empty delete set),
@@ -466,6 +518,12 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
 #pragma unroll 1
     for (int it = 0; it < DW_R; it++) {
       if (bad && ph != WK_IDLE) ph = WK_FIN;
+      // block headers are decoded on even iterations only: the wave skips the header decoder every other
+      // iteration (with 64 lanes some lane is at a header in most iterations; a lane waits one at most)
+      const bool blk_it = (it & 1) == 0;
+#ifdef YGM_DIAG
+      const uint32_t ph0 = ph;
+#endif
       const uint32_t lend = landed << 6;
       const bool rdy = (q + 64u <= lend) || (lend >= rb);   // the general decoder reads up to 64 bytes ahead
       // the fast decoders take a unit whose bytes have all landed (masks past lend are stale: a unit
@@ -523,7 +581,7 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
               if (--st_left == 0u) block_end();
             }
           }
-        } else if (ph == WK_BLK) {   // block header: <= 2-byte count, <= 5-byte client, one-byte clock
+        } else if (ph == WK_BLK && blk_it) {   // block header: <= 2-byte count, <= 5-byte client, one-byte clock
           const uint32_t y = w32 & (w32 - 1u), z = y & (y - 1u);
           const uint32_t e1 = (uint32_t)__builtin_ctz(w32 | 0x80000000u), e2 = (uint32_t)__builtin_ctz(y | 0x80000000u);
           const uint32_t e3 = (uint32_t)__builtin_ctz(z | 0x80000000u);
@@ -547,7 +605,7 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
             if (b0) { n_left = b0; have_prev = false; ph = WK_BLK; }
             else ph = MODE == 1 ? WK_DS : WK_FIN;
           }
-        } else if ((w32 & 1u) && b0 == 0u && !run_on) {   // MODE 1 WK_DS: the empty delete set ("00") (avl >= 1)
+        } else if (MODE == 1 && ph == WK_DS && (w32 & 1u) && b0 == 0u && !run_on) {   // the empty delete set ("00") (avl >= 1)
           done = true;
           run_on = true; cp = q; rs0 = q; cdst = t; cd0 = t;
           q += 1u; run_end = q; t += 1u;
@@ -556,11 +614,16 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
         }
         if (q > rb) bad = 1;
       }
-      WDG(0, done ? 1 : 0);
-      WDG(2, (!rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN && ph != WK_STR) ? 1 : 0);
-      WDG(3, (ph == WK_IDLE || ph == WK_FIN || ph == WK_SVN) ? 1 : 0);
-      WDG(4, ph == WK_STR ? 1 : 0);
-      WDG(1, (!done && rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN && ph != WK_STR) ? 1 : 0);
+#ifdef YGM_DIAG
+      {   // one class per lane-iteration, from the phase it started in
+        const bool idl = ph0 == WK_IDLE || ph0 == WK_FIN || ph0 == WK_SVN;
+        WDG(0, done ? 1 : 0);
+        WDG(3, (!done && idl) ? 1 : 0);
+        WDG(4, (!done && !idl && ph0 == WK_STR) ? 1 : 0);
+        WDG(2, (!done && !idl && ph0 != WK_STR && !rdy) ? 1 : 0);
+        WDG(1, (!done && !idl && ph0 != WK_STR && rdy) ? 1 : 0);
+      }
+#endif
 #ifdef YGM_DIAG
       if (l == 0) dg[6] += __ballot(!done && rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN && ph != WK_STR) ? 1 : 0;
 #endif
@@ -574,7 +637,7 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
           sp += n;
           if (sp == str_end) ph = ph_after;
         }
-      } else if (!done && rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN) {   // ---- the general decoder
+      } else if (!done && rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN && (blk_it || ph != WK_BLK)) {   // ---- the general decoder
         const uint64_t win = dw_win(L, l, q, landed);
         uint64_t lo, hi;
         dw_rd16(L, l, q, lo, hi);
@@ -729,6 +792,7 @@ __global__ __launch_bounds__(WAVE) void k_doc_walk(const uint8_t* __restrict__ a
 #ifdef YGM_DIAG
   dg[5] = l == 0 ? rounds : 0;
   for (int i = 0; i < 8; i++) { const unsigned long long v = wave_sum(dg[i]); if (l == 0) atomicAdd(&ygm_diag[16 + i], v); }
+  if (l == 0) for (int i = 0; i < 5; i++) atomicAdd(&ygm_diag[24 + i], tsec[i]);
 #endif
 #undef WDG
 }
@@ -2256,8 +2320,8 @@ int ygm_diag_ts_read(unsigned long long* out, int reset) {  // 16384 x 8 stamps 
   return 0;
 }
 int ygm_diag_read(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ygm_diag), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
-  if (reset) { unsigned long long z[24] = {0}; (void)hipMemcpyToSymbol(HIP_SYMBOL(ygm_diag), z, sizeof z); }
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ygm_diag), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+  if (reset) { unsigned long long z[32] = {0}; (void)hipMemcpyToSymbol(HIP_SYMBOL(ygm_diag), z, sizeof z); }
   return 0;
 }
 #endif
@@ -2289,25 +2353,29 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
   return launch_rc(__func__);
 }
 
+size_t ygm_k_sv_table_bytes(uint32_t n_docs) { return 144ull * n_docs + 64; }
 int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
                           uint64_t sv_bytes, const uint64_t* sv_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
-                          uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
+                          uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list, uint64_t out_cap, uint8_t* tbl,
+                          uint32_t* tbl_n, hipStream_t s) {
   (void)arena_bytes; (void)sv_bytes; (void)flags;   // segments are read in 64-byte chunks: 64 bytes of tail padding (ygm.h)
   if (n_docs == 0) return 0;
   static int n_cu = 0;
   if (!n_cu) { int dev = 0; (void)hipGetDevice(&dev); if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256; }
   const char* env = getenv("YGM_WALK_WAVES_PER_CU");
-  const uint32_t wpc = env ? (uint32_t)atoi(env) : (mode == 0 ? 8u : 5u);   // resident waves per CU (LDS 18 / 26 KB per wave)
+  const uint32_t wpc = env ? (uint32_t)atoi(env) : 8u;   // resident waves per CU (LDS 20 KB per wave)
   const uint32_t waves = (n_docs + WAVE - 1) / WAVE, cap = (uint32_t)n_cu * (wpc ? wpc : 1u);
   uint32_t grid = waves < cap ? waves : cap;
   const char* genv = getenv("YGM_WALK_GRID");   // testing: a small grid gives every lane many documents
   if (genv && atoi(genv) > 0 && (uint32_t)atoi(genv) < grid) grid = (uint32_t)atoi(genv);
   if (mode == 0)
-    hipLaunchKernelGGL(k_doc_walk<0>, dim3(grid), dim3(WAVE), 0, s, arena, doc_off, sv_arena, sv_off, n_docs, out, out_off, out_len,
-                       status, (DocMeta*)meta, defer_list, out_cap);
-  else
-    hipLaunchKernelGGL(k_doc_walk<1>, dim3(grid), dim3(WAVE), 0, s, arena, doc_off, sv_arena, sv_off, n_docs, out, out_off, out_len,
-                       status, (DocMeta*)meta, defer_list, out_cap);
+    hipLaunchKernelGGL(k_doc_walk<0>, dim3(grid), dim3(WAVE), 0, s, arena, doc_off, (const uint8_t*)nullptr, (const uint32_t*)nullptr,
+                       n_docs, out, out_off, out_len, status, (DocMeta*)meta, defer_list, out_cap);
+  else {
+    hipLaunchKernelGGL(k_sv_table, dim3(waves), dim3(WAVE), 0, s, sv_arena, sv_off, n_docs, tbl, tbl_n);
+    hipLaunchKernelGGL(k_doc_walk<1>, dim3(grid), dim3(WAVE), 0, s, arena, doc_off, (const uint8_t*)tbl, (const uint32_t*)tbl_n, n_docs,
+                       out, out_off, out_len, status, (DocMeta*)meta, defer_list, out_cap);
+  }
   return launch_rc(__func__);
 }
 

@@ -1,6 +1,7 @@
 """Lane-iteration census of the SV / diff ring walker on C4 (diagnostic build libygm_diag.so; tooling).
 Counts: fast-decoder units, general-decoder units, lanes waiting for ring data, idle / finishing /
-state-vector lanes, long-string continuation; rounds; wave-iterations that ran the general decoder."""
+state-vector lanes, long-string continuation; rounds; wave-iterations that ran the general decoder;
+and the wave shader-clock split over the round's sections."""
 import ctypes
 import json
 import os
@@ -26,7 +27,7 @@ dso = torch.from_numpy(sv_off.view(np.int64)).to(dev)
 e = eng.Engine(0)
 L = eng.lib()
 L.ygm_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
-buf = np.zeros(24, np.uint64)
+buf = np.zeros(32, np.uint64)
 names = ["fast", "general", "not_ready", "idle", "string", "rounds", "general_iters", "-"]
 for op in ("sv", "diff"):
     L.ygm_diag_read(buf.ctypes.data, 1)
@@ -41,4 +42,6 @@ for op in ("sv", "diff"):
     tot = sum(c[k] for k in names[:5])
     print(json.dumps({"op": op, "docs": n, "kernel_ms": round(s1.kernel_ms - s0.kernel_ms, 3), **c,
                       "lane_iters": tot, "frac": {k: round(c[k] / max(tot, 1), 3) for k in names[:5]},
-                      "general_iter_frac": round(c["general_iters"] / max(c["rounds"] * 8, 1), 3)}))
+                      "general_iter_frac": round(c["general_iters"] / max(c["rounds"] * 8, 1), 3),
+                      "clock_frac": {k: round(int(v) / max(int(buf[24:29].sum()), 1), 3) for k, v in
+                                     zip(["commit", "sv_parse", "grab_out_init", "staging", "parse"], buf[24:29])}}))

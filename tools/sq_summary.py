@@ -1,16 +1,28 @@
-"""Per-kernel mean of every PMC counter in rocprofv3 counter_collection CSVs (tooling)."""
+"""Per-kernel SQ counter summary of a rocprofv3 --pmc run (measurement tooling): per-dispatch averages
+and derived ratios.  python tools/sq_summary.py <rocprof out dir>"""
 import collections
 import csv
 import glob
 import sys
 
-for path in sys.argv[1:]:
-    for f in glob.glob(path + "/*counter_collection.csv"):
-        rows = list(csv.DictReader(open(f)))
-        agg = collections.defaultdict(lambda: collections.defaultdict(list))
-        for r in rows:
-            agg[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-        for k, d in agg.items():
-            if "rocclr" in k:
-                continue
-            print(k, {c: round(sum(v) / len(v), 1) for c, v in sorted(d.items())})
+acc = collections.defaultdict(lambda: collections.defaultdict(float))
+disp = collections.defaultdict(set)
+for p in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(p)):
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        if k.startswith("__amd"):
+            continue
+        acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(r["Dispatch_Id"])
+for k, d in acc.items():
+    n = len(disp[k])
+    a = {c: v / n for c, v in d.items()}
+    w = a.get("SQ_WAVES", 0) or 1
+    print(f"{k}: {n} dispatches")
+    for c in sorted(a):
+        print(f"  {c:24s} {a[c]:14.4g}   per wave {a[c] / w:12.4g}")
+    if "SQ_WAVE_CYCLES" in a:
+        wc = a["SQ_WAVE_CYCLES"]
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if c in a:
+                print(f"  {c} / WAVE_CYCLES = {a[c] / wc:.3f}")

@@ -45,7 +45,11 @@ constexpr int DW_P = DW_S * 4;    // 16-byte pieces per ring
 #ifndef YGM_DW_STG
 #define YGM_DW_STG 3
 #endif
+#ifndef YGM_DW_U
+#define YGM_DW_U 3
+#endif
 constexpr int DW_R = YGM_DW_R;    // parse iterations per round
+constexpr int DW_U = YGM_DW_U;    // Items the fast decoder takes per iteration (from one 64-byte mask window)
 constexpr uint32_t DW_STG = YGM_DW_STG;   // chunks staged per round (<= 4: 64 staging registers)
 constexpr uint32_t DW_AHEAD = 2;  // chunks staged past the ring's free slots (committed if the round freed theirs)
 constexpr int DW_BATCH = 256;     // documents sorted (largest first) per batch of a wave's range

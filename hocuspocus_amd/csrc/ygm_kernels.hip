@@ -265,8 +265,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2))) void 
   bool e_on = false;
   uint32_t e_dst = 0;
   uint32_t e_a = 0, e_b = 0, e_c = 0, e_pl = 0, e_info = 0, e_oclk = 0, e_q = 0, e_ro_p = 0, e_ro_e = 0, e_clen = 0;
-  // MODE 1: the state vector, sorted by client descending (the block order), as a register queue: entries
-  // (sc[i], sk[i]) for i < nsv; the head is the first entry not above the current block's client
+  // MODE 1: the state vector in registers: entries (sc[i], sk[i]), clients unique
   // copy run (ring bytes [cp, run_end) -> output at cdst)
   uint32_t nsv = 0, svc = 0;
   uint32_t sc[MODE == 1 ? DW_SVN : 1], sk[MODE == 1 ? DW_SVN : 1];
@@ -315,12 +314,12 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2))) void 
     st_left = nst; client = cl; clock = ck;
     if (MODE == 0) { cc = cl; stop = ck != 0u; clk = 0u; }
     else {   // the state-vector clock of the client: walk the descending table
-      while (nsv && sc[0] > cl) {   // entries of clients above this block's: not in the update
+      // (clients are unique in the table and its unused entries repeat entry 0, or hold clock 0: a
+      // compare-select over all entries, no walk)
+      uint32_t s = 0;
 #pragma unroll
-        for (int i = 0; i + 1 < DW_SVN; i++) { sc[i] = sc[i + 1]; sk[i] = sk[i + 1]; }
-        nsv--;
-      }
-      svc = nsv && sc[0] == cl ? sk[0] : 0u;
+      for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) s = sc[i] == cl ? sk[i] : s;
+      svc = s;
       emitted = false;
     }
     ph = WK_ST;
@@ -388,8 +387,8 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2))) void 
       const uint64_t cm = __ballot(cpy);
       if (cm && cpy) {
 #pragma unroll
-        for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) {
-          const uint64_t w = (uint32_t)i < nsv ? dw_word(L, l, 8u * (uint32_t)i) : 0ull;
+        for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) {   // unused entries: copies of entry 0 (or clock 0)
+          const uint64_t w = (uint32_t)i < nsv ? dw_word(L, l, 8u * (uint32_t)i) : (i ? ((uint64_t)sk[0] << 32 | sc[0]) : 0ull);
           sc[i] = (uint32_t)w; sk[i] = (uint32_t)(w >> 32);
         }
         ph = WK_UPD;
@@ -485,6 +484,10 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2))) void 
       nsv = MODE == 1 && ntn <= (uint32_t)DW_SVN ? ntn : 0u;
       bad |= (MODE == 1 && ntn > (uint32_t)DW_SVN) ? 1u : 0u;   // (DW_TBL_BAD: the exact kernel)
       tc = (8u * nsv + 63u) >> 6;
+      if (MODE == 1 && !tc) {   // an empty state vector: every client at clock 0
+#pragma unroll
+        for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) sk[i] = 0u;
+      }
       cbase = da & ~15ull; srel = 64u * tc + (uint32_t)(da - cbase); q = srel; rb = 64u * tc + (uint32_t)(db - cbase);
       landed = 0; stg_n = 0; prev8 = 0;
       bad |= (db < da || ((db - da) >> 30)) ? 1u : 0u;
@@ -516,7 +519,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2))) void 
     //      of a <= 2-byte count and a one-byte clock, a one-byte update header, an empty delete set),
     //      else by the general decoder -- which then runs for the lanes that need it only
 #pragma unroll 1
-    for (int it = 0; it < DW_R; it++) {
+    for (int it = 0; it < (MODE == 1 ? DW_R - 1 : DW_R); it++) {   // (diff: shorter rounds, its output waits for them)
       if (bad && ph != WK_IDLE) ph = WK_FIN;
       // block headers are decoded on even iterations only: the wave skips the header decoder every other
       // iteration (with 64 lanes some lane is at a header in most iterations; a lane waits one at most)
@@ -541,9 +544,9 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2))) void 
                              // a second one right behind it from the same 64-byte window
           uint32_t qo = 0, bb = b0;
 #pragma unroll
-          for (int u = 0; u < 2; u++) {
+          for (int u = 0; u < DW_U; u++) {
             const uint32_t wq = (uint32_t)(w64 >> qo);
-            if (u == 1) bb = dw_byte(L, l, q);
+            if (u >= 1) bb = dw_byte(L, l, q);
             const uint32_t hoh = bb >> 6, ref = bb & 0x3Fu;
             const uint32_t tt = wq >> 1, x2 = tt & (tt - 1u), x3 = x2 & (x2 - 1u), x4 = x3 & (x3 - 1u);
             const uint32_t cpos = (uint32_t)__builtin_ctz((hoh == 3u ? x4 : x2) | 0x80000000u) + 2u;   // after the origins
@@ -554,7 +557,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2))) void 
             const uint32_t mk = isS ? (((1u << (lv & 31u)) - 1u) << ((cq + 1u) & 31u)) : 0u;   // the string's bytes: ASCII
             const uint32_t ce = clock + lv;
             uint32_t ok = (ph == WK_ST) & (hoh != 0u) & (isS | (ref == 1u)) & (cpos < 31u) & (wq >> cq) & (lv != 0u) &
-                          (end <= 32u) & ((wq & mk) == mk) & (ce >= clock) & (qo + end <= avl) & (u == 0 || (done && qo + end <= 32u));
+                          (end <= 32u) & ((wq & mk) == mk) & (ce >= clock) & (qo + end <= avl) & (u == 0 || (done && qo + end <= 64u));
             uint32_t emit = 0;
             if (MODE == 0) ok &= (st_left != 1u) | !e_on;
             else {

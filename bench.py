@@ -43,7 +43,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
-PMC_PROFILE = "r01_big_v4/pmc_hbm.json"   # committed rocprofv3 PMC summary of the headline kernel (k_merge_lean)
+PMC_PROFILE = "r02_walk/pmc.json"          # committed rocprofv3 PMC summary (FETCH_SIZE x2 + WRITE_SIZE per launch)
 PMC_C4 = "r02_walk/pmc.json"              # ... of the SV / diff walker at C4
 
 

@@ -15,4 +15,5 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/p2_w_lean100k -o w -- $P --steps 3 --warmup 1 --docs 100000 --c2big-docs 0 --c4-docs 0 > $R/gpurun_out/p2_w2.log 2>&1 && \
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/p2_f_c4 -o f -- python3 $R/tools/bench_configs.py c4 1000000 > $R/gpurun_out/p2_f3.log 2>&1 && \
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/p2_w_c4 -o w -- python3 $R/tools/bench_configs.py c4 1000000 > $R/gpurun_out/p2_w3.log 2>&1 && \
-timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d $R/gpurun_out/p2_sq_c4 -o sq -- python3 $R/tools/bench_configs.py c4 1000000 > $R/gpurun_out/p2_sq.log 2>&1
+timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d $R/gpurun_out/p2_sq_c4 -o sq -- python3 $R/tools/bench_configs.py c4 1000000 > $R/gpurun_out/p2_sq.log 2>&1 && \
+cd $R && timeout -k 10 600 python -u bench.py > gpurun_out/p2_bench.log 2>&1

@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads / workers (0: the cores granted, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-yjs", action="store_true", help="skip the Node / yjs leg of the CPU baseline")
+    ap.add_argument("--no-host-api", dest="host_api", action="store_false",
+                    help="skip the host_api block (host arrays through the pinned / two-stream host API)")
     ap.add_argument("--big", choices=["c3", "c5"], default=None,
                     help="instead of the standard line: one C3 / C5 large-document batch on the GPU next to the CPU oracle")
     ap.add_argument("--big-docs", type=int, default=None)
@@ -227,6 +229,93 @@ def c2_corpus(be, prefix, per_gpu, updates, rank, world):
     c["do"] = be.put(upd_off.view(np.int64))
     c["dd"] = be.put(doc_upd.view(np.int32))
     return c
+
+
+def _host_stats(e):
+    s = e.stats()
+    return {"kernel_ms": s.kernel_ms, "h2d_ms": s.h2d_ms, "d2h_ms": s.d2h_ms}
+
+
+def host_api_merge(be, cb, args, reps=3):
+    """The production path: host arrays through ygm_merge_v1 (pinned staging, two stage streams, device-side packing,
+    D2H of the packed outputs) -- what the N-API addon and GpuMerge call.  End-to-end rate = algorithmic bytes / wall."""
+    from hocuspocus_amd import Engine
+    import oracle
+    e = Engine(be.dev.index)
+    arena, upd_off, doc_upd = cb["arena"], cb["upd_off"], cb["doc_upd"]
+    upd_doc = np.repeat(np.arange(cb["n"], dtype=np.uint32), np.diff(doc_upd.astype(np.int64)))
+    e.merge_packed_raw(arena, upd_off, upd_doc, cb["n"])   # warm-up: stage contexts, pinned buffers
+    s0 = _host_stats(e)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        st, off, ln, data = e.merge_packed_raw(arena, upd_off, upd_doc, cb["n"])
+    wall = (time.perf_counter() - t0) / reps
+    s1 = _host_stats(e)
+    out_b = int(ln.sum())
+    ok = 0
+    for d in range(0, cb["n"], max(1, cb["n"] // 200)):
+        ups = [arena[upd_off[u]:upd_off[u + 1]].tobytes() for u in range(doc_upd[d], doc_upd[d + 1])]
+        got = (int(st[d]), bytes(data[int(off[d]):int(off[d]) + int(ln[d])]) if st[d] == 0 else None)
+        assert oracle.merge_updates(ups) == got, f"host API parity failure on document {d}"
+        ok += 1
+    d = {k: (s1[k] - s0[k]) / reps for k in s0}
+    h2d_b = len(arena) + upd_off.nbytes + 4 * (cb["n"] + 1)
+    d2h_b = out_b + 20 * cb["n"]
+    e.close()
+    return {"op": "merge (ygm_merge_v1, host arrays)", "docs": cb["n"], "value": round((len(arena) + out_b) / wall / 1e6, 1),
+            "unit": "MB/s end-to-end (algorithmic bytes / wall, PCIe + host staging included)", "wall_ms": round(wall * 1e3, 3),
+            "docs_per_s": round(cb["n"] / wall, 1), "h2d_ms": round(d["h2d_ms"], 3), "d2h_ms": round(d["d2h_ms"], 3),
+            "device_span_ms": round(d["kernel_ms"], 3), "h2d_bytes": int(h2d_b), "d2h_bytes": int(d2h_b),
+            "h2d_GBps": round(h2d_b / max(d["h2d_ms"], 1e-6) / 1e6, 2), "d2h_GBps": round(d2h_b / max(d["d2h_ms"], 1e-6) / 1e6, 2),
+            "pipeline": "64 MB chunks of whole documents over two stage streams: pinned staging + H2D of chunk i+1 beside the "
+                        "kernels of chunk i, device-side packing, D2H of packed outputs",
+            "parity": f"bit-exact vs oracle on {ok} sampled docs"}
+
+
+def c1_store_window(docs=1000, inserts=200):
+    """C1: one store window of 1 000 edited Y.Text documents through GpuMerge (Node, N-API addon,
+    ygm_merge_v1) beside extension-database's encodeStateAsUpdate store (tools/c1_store_latency.js)."""
+    import shutil
+    import subprocess
+    if not shutil.which("node"):
+        return {"skipped": "node not found"}
+    try:
+        r = subprocess.run(["node", os.path.join(ROOT, "tools", "c1_store_latency.js"), str(docs), str(inserts)],
+                           capture_output=True, text=True, timeout=240)
+        lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        return json.loads(lines[-1]) if r.returncode == 0 and lines else {"error": (r.stderr or r.stdout)[-400:]}
+    except Exception as ex:   # the block is a report, not the headline: keep the line
+        return {"error": repr(ex)[:400]}
+
+
+def host_api_doc(be, c, op, n, reps=3):
+    from hocuspocus_amd import Engine
+    import oracle
+    e = Engine(be.dev.index)
+    arena = c["arena"][:int(c["doc_off"][n])]
+    doc_off = np.ascontiguousarray(c["doc_off"][:n + 1])
+    sva = c["sva"][:int(c["sv_off"][n])]
+    sv_off = np.ascontiguousarray(c["sv_off"][:n + 1])
+    e.doc_packed_raw(op, arena, doc_off, sva, sv_off)
+    s0 = _host_stats(e)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        st, off, ln, data = e.doc_packed_raw(op, arena, doc_off, sva, sv_off)
+    wall = (time.perf_counter() - t0) / reps
+    s1 = _host_stats(e)
+    out_b = int(ln.sum())
+    ok = 0
+    for d in range(0, n, max(1, n // 200)):
+        u = arena[doc_off[d]:doc_off[d + 1]].tobytes()
+        exp = oracle.diff_update(u, sva[sv_off[d]:sv_off[d + 1]].tobytes()) if op == "diff" else oracle.encode_state_vector_from_update(u)
+        assert exp == (int(st[d]), bytes(data[int(off[d]):int(off[d]) + int(ln[d])]) if st[d] == 0 else None), f"host API parity failure {d}"
+        ok += 1
+    d = {k: (s1[k] - s0[k]) / reps for k in s0}
+    algo = len(arena) + len(sva) + out_b
+    e.close()
+    return {"op": f"{op} (host arrays)", "docs": n, "value": round(algo / wall / 1e6, 1), "unit": "MB/s end-to-end",
+            "wall_ms": round(wall * 1e3, 3), "docs_per_s": round(n / wall, 1), "h2d_ms": round(d["h2d_ms"], 3),
+            "d2h_ms": round(d["d2h_ms"], 3), "device_span_ms": round(d["kernel_ms"], 3), "parity": f"bit-exact vs oracle on {ok} sampled docs"}
 
 
 def time_merge(be, c, steps, warmup, dist):
@@ -423,6 +512,9 @@ def run_rank(args, rank, world, dist, be, dev=None):
                                "value": round(tot[1] * sb / dtb / 1e6, 3), "unit": "MB/s", "docs_per_s": round(tot[0] * sb / dtb, 1),
                                "ms_per_step": round(dtb / sb * 1e3, 4),
                                "roofline": roof(cb["bytes"] + outb, kmsb, "k_merge_lean (rank 0)", _pmc(PMC_C4, "k_merge_lean@100k"))}
+        if rank == 0 and not args.dry_run and args.host_api:
+            line["host_api"] = host_api_merge(be, cb, args)
+            line["host_api"]["c1_store_window"] = c1_store_window()
         del cb
     # ---- C4: 1M merged states, state vector + diffUpdate (strong scaling over the ranks)
     if args.c4_docs:
@@ -464,6 +556,8 @@ def run_rank(args, rank, world, dist, be, dev=None):
                            "parity": pr}
         if rank == 0:
             line["c4"] = blk
+            if not args.dry_run and args.host_api and "host_api" in line:
+                line["host_api"]["c4_diff"] = host_api_doc(be, c, "diff", min(c["n"], 250000))
         c4 = c
     # ---- CPU baselines (rank 0 at N = 1 only)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:

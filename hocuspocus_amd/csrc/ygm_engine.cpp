@@ -10,6 +10,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <vector>
 
 #include "../../include/ygm.h"
@@ -22,6 +24,8 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
                      const uint32_t* docs, uint64_t out_base, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
                      uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
 size_t ygm_k_sv_table_bytes(uint32_t n_docs);
+int ygm_k_launch_pack(const uint8_t* src, const uint64_t* off, const uint64_t* len, const int32_t* status, uint32_t n, uint64_t* bsum,
+                      uint8_t* dst, uint64_t* poff, hipStream_t s);
 int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
                           uint64_t sv_bytes, const uint64_t* sv_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
                           uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list, uint64_t out_cap, uint8_t* tbl,
@@ -78,6 +82,24 @@ struct DevBuf {
   template <class T> T* as() const { return (T*)p; }
 };
 
+// pinned (page-locked) host memory: DMA-able staging for the host API's copies
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t n, size_t keep = 0) {   // keep: leading bytes preserved across a regrowth
+    if (n <= cap && p) return true;
+    size_t c = std::max<size_t>(n, 4096);
+    c += c / 4;
+    void* q = nullptr;
+    if (hipHostMalloc(&q, c, hipHostMallocDefault) != hipSuccess) return false;
+    if (p) { if (keep) memcpy(q, p, std::min(keep, cap)); (void)hipHostFree(p); }
+    p = q; cap = c;
+    return true;
+  }
+  void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+  template <class T> T* as() const { return (T*)p; }
+};
+
 }  // namespace
 
 struct ygm_ctx {
@@ -95,10 +117,12 @@ struct ygm_ctx {
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
   DevBuf big_blk, big_rec, big_list;   // large-document tier: block tables, struct records, documents sent on
   DevBuf sv_tbl, sv_tn;                // diff: sorted state-vector tables (k_sv_table) and their entry counts
-  // host results
-  std::vector<uint8_t> h_data;
-  std::vector<uint64_t> h_off, h_len;
-  std::vector<int32_t> h_status;
+  // host API: results in pinned memory (packed outputs, per-document offset / length / status), the
+  // pinned input staging of this context when it serves as a pipeline stage, the packed device copy,
+  // and the two stage contexts (own streams and buffers) that double-buffer a batch's chunks
+  PinBuf h_data, h_off, h_len, h_status, h_in;
+  DevBuf pk_data, pk_off, pk_bsum;
+  ygm_ctx* kid[2] = {nullptr, nullptr};
   std::vector<uint32_t> h_doc_upd;
   ygm_stats_t stats{};
   // the batch enqueued by ygm_merge_v1_device_async, completed by ygm_merge_v1_device_finish
@@ -164,6 +188,9 @@ void ygm_close(ygm_ctx* c) {
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
                     &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn})
     b->release();
+  for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
+  for (DevBuf* b : {&c->pk_data, &c->pk_off, &c->pk_bsum}) b->release();
+  for (PinBuf* b : {&c->h_data, &c->h_off, &c->h_len, &c->h_status, &c->h_in}) b->release();
   for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
   if (c->h_meta) (void)hipHostFree(c->h_meta);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -383,102 +410,259 @@ int ygm_sv_from_update_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t ar
 }
 
 // ------------------------------------------------------------------ host API
-static int h2d(ygm_ctx* c, DevBuf& b, const void* src, size_t n, size_t pad) {
-  if (!b.ensure(n + pad)) return YGM_ENOMEM;
-  if (n) HIPCHK(hipMemcpyAsync(b.p, src, n, hipMemcpyHostToDevice, c->stream));
-  if (pad) HIPCHK(hipMemsetAsync((uint8_t*)b.p + n, 0, pad, c->stream));
+// A batch is cut into chunks of whole documents (about YGM_CHUNK_BYTES of input each) that alternate
+// between two stage contexts, each with its own stream and device buffers:
+//   stage i+1: host arena -> pinned staging (CPU copy) -> H2D        (stream of stage (i+1) % 2)
+//   chunk i:   kernels -> device-side packing of the outputs -> D2H   (stream of stage i % 2)
+// so the CPU copy and the H2D of one chunk overlap the kernels of the previous one, and the D2H moves
+// only the packed outputs (not the per-document slots).  h2d_ms / d2h_ms are the copies' HIP-event
+// times (summed over chunks); the results live in the parent context's pinned buffers.
+static const uint64_t YGM_CHUNK_BYTES = 64ull << 20;
+
+namespace {
+struct Chunk {   // documents [d0, d1): merge updates [u0, u1) / SV-diff documents
+  uint32_t d0, d1, u0, u1;
+  uint64_t pos = 0, payload = 0;   // packed output position in the parent's result, bytes
+  hipEvent_t h0 = nullptr, h1 = nullptr, o0 = nullptr, o1 = nullptr;
+};
+struct HostCall {
+  int mode;   // 0 sv, 1 diff, 2 merge
+  const uint8_t* arena; const uint64_t* off; const uint32_t* upd_doc; const uint8_t* sv_arena; const uint64_t* sv_off;
+  uint32_t n_upd, n_docs;
+};
+}  // namespace
+
+static int stage_ctx(ygm_ctx* c, int i, ygm_ctx** out) {
+  if (!c->kid[i]) { int e = ygm_open(c->device, c->flags, &c->kid[i]); if (e) return e; }
+  *out = c->kid[i];
   return YGM_OK;
 }
 
-static int fetch_results(ygm_ctx* c, uint32_t n_docs, const ygm_device_result& dr, ygm_result* out) {
-  c->h_off.resize(n_docs); c->h_len.resize(n_docs); c->h_status.resize(n_docs);
-  c->h_data.resize(dr.data_bytes ? dr.data_bytes : 1);
-  HIPCHK(hipEventRecord(c->e2, c->stream));
-  if (n_docs) {
-    HIPCHK(hipMemcpyAsync(c->h_off.data(), dr.off, n_docs * 8ull, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(c->h_len.data(), dr.len, n_docs * 8ull, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(c->h_status.data(), dr.status, n_docs * 4ull, hipMemcpyDeviceToHost, c->stream));
+// large host copies split over threads (one core copies ~10 GB/s; PCIe takes ~55 GB/s)
+static void par_memcpy(uint8_t* dst, const uint8_t* src, size_t n) {
+  const size_t per = 8u << 20;
+  unsigned t = (unsigned)std::min<size_t>((n + per - 1) / per, 8);
+  const unsigned hw = std::thread::hardware_concurrency();
+  if (hw && t > hw) t = hw;
+  if (t <= 1) { memcpy(dst, src, n); return; }
+  std::vector<std::thread> th;
+  const size_t part = (n + t - 1) / t;
+  for (unsigned i = 1; i < t; i++) {
+    const size_t a = i * part, b = std::min(n, a + part);
+    if (a < b) th.emplace_back([=] { memcpy(dst + a, src + a, b - a); });
   }
-  if (dr.data_bytes) HIPCHK(hipMemcpyAsync(c->h_data.data(), dr.data, dr.data_bytes, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipEventRecord(c->e3, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  float ms = 0;
-  if (hipEventElapsedTime(&ms, c->e2, c->e3) == hipSuccess) c->stats.d2h_ms += ms;
-  for (uint32_t d = 0; d < n_docs; d++)
-    if (c->h_status[d] >= 100 || c->h_status[d] < 0) c->h_status[d] = YGM_EDEVICE;  // never left internal codes
-  out->data = c->h_data.data(); out->off = c->h_off.data(); out->len = c->h_len.data(); out->status = c->h_status.data();
-  out->n_docs = n_docs; out->data_bytes = dr.data_bytes;
+  memcpy(dst, src, std::min(n, part));
+  for (auto& x : th) x.join();
+}
+
+// f(begin, end) over [0, n) split over threads when n is large
+extern "C++" template <class F>
+static void par_for(size_t n, F f) {
+  const size_t per = 1u << 20;
+  unsigned t = (unsigned)std::min<size_t>((n + per - 1) / per, 8);
+  const unsigned hw = std::thread::hardware_concurrency();
+  if (hw && t > hw) t = hw;
+  if (t <= 1) { f((size_t)0, n); return; }
+  std::vector<std::thread> th;
+  const size_t part = (n + t - 1) / t;
+  for (unsigned i = 1; i < t; i++) {
+    const size_t a = i * part, b = std::min(n, a + part);
+    if (a < b) th.emplace_back([=] { f(a, b); });
+  }
+  f((size_t)0, std::min(n, part));
+  for (auto& x : th) x.join();
+}
+
+// CPU copy of a chunk's inputs into the stage's pinned buffer, then the async H2D copies
+static int chunk_stage(ygm_ctx* k, const HostCall& H, Chunk& C) {
+  const uint32_t nd = C.d1 - C.d0;
+  const uint64_t a0 = H.mode == 2 ? H.off[C.u0] : H.off[C.d0], a1 = H.mode == 2 ? H.off[C.u1] : H.off[C.d1];
+  const uint64_t bytes = a1 - a0, ab = (bytes + 64 + 15) & ~15ull;
+  const uint32_t nu = H.mode == 2 ? C.u1 - C.u0 : nd;
+  uint64_t s0 = 0, s1 = 0, sb = 0;
+  if (H.mode == 1) { s0 = H.sv_off[C.d0]; s1 = H.sv_off[C.d1]; sb = ((s1 - s0) + 64 + 15) & ~15ull; }
+  const uint64_t n_off = (uint64_t)nu + 1, n_doc = H.mode == 2 ? (uint64_t)nd + 1 : 0, n_sv = H.mode == 1 ? (uint64_t)nd + 1 : 0;
+  const uint64_t need = ab + 8 * n_off + sb + 8 * n_sv + 4 * n_doc + 64;
+  if (!k->h_in.ensure(need)) return YGM_ENOMEM;
+  uint8_t* P = k->h_in.as<uint8_t>();
+  par_memcpy(P, H.arena + a0, bytes); memset(P + bytes, 0, ab - bytes);
+  uint64_t* ro = (uint64_t*)(P + ab);
+  const uint64_t* src_off = H.mode == 2 ? H.off + C.u0 : H.off + C.d0;
+  par_for(n_off, [=](size_t a, size_t b) { for (size_t j = a; j < b; j++) ro[j] = src_off[j] - a0; });
+  uint8_t* q = P + ab + 8 * n_off;
+  if (H.mode == 1) {
+    memcpy(q, H.sv_arena + s0, s1 - s0); memset(q + (s1 - s0), 0, sb - (s1 - s0));
+    uint64_t* rs = (uint64_t*)(q + sb);
+    for (uint64_t j = 0; j < n_sv; j++) rs[j] = H.sv_off[C.d0 + j] - s0;
+    q += sb + 8 * n_sv;
+  }
+  if (H.mode == 2) {   // per-document update ranges, relative to the chunk
+    uint32_t* du = (uint32_t*)q;
+    du[0] = 0;
+    uint32_t u = C.u0;
+    for (uint32_t d = 0; d < nd; d++) { while (u < C.u1 && H.upd_doc[u] == C.d0 + d) u++; du[d + 1] = u - C.u0; }
+  }
+  if (!k->arena.ensure(ab) || !k->offs.ensure(8 * n_off) || (H.mode == 1 && (!k->sv_arena.ensure(sb) || !k->sv_offs.ensure(8 * n_sv))) ||
+      (H.mode == 2 && !k->docs.ensure(4 * n_doc)))
+    return YGM_ENOMEM;
+  HIPCHK(hipEventRecord(C.h0, k->stream));
+  HIPCHK(hipMemcpyAsync(k->arena.p, P, ab, hipMemcpyHostToDevice, k->stream));
+  HIPCHK(hipMemcpyAsync(k->offs.p, ro, 8 * n_off, hipMemcpyHostToDevice, k->stream));
+  if (H.mode == 1) {
+    HIPCHK(hipMemcpyAsync(k->sv_arena.p, P + ab + 8 * n_off, sb, hipMemcpyHostToDevice, k->stream));
+    HIPCHK(hipMemcpyAsync(k->sv_offs.p, P + ab + 8 * n_off + sb, 8 * n_sv, hipMemcpyHostToDevice, k->stream));
+  }
+  if (H.mode == 2) HIPCHK(hipMemcpyAsync(k->docs.p, q, 4 * n_doc, hipMemcpyHostToDevice, k->stream));
+  HIPCHK(hipEventRecord(C.h1, k->stream));
   return YGM_OK;
+}
+
+// kernels of a staged chunk, packing, and the async D2H into the parent's pinned results
+static int chunk_run(ygm_ctx* c, ygm_ctx* k, const HostCall& H, Chunk& C, uint64_t& pos, bool merge_enqueued) {
+  const uint32_t nd = C.d1 - C.d0;
+  const uint64_t bytes = (H.mode == 2 ? H.off[C.u1] - H.off[C.u0] : H.off[C.d1] - H.off[C.d0]);
+  ygm_device_result dr;
+  int e;
+  if (H.mode == 2) e = merge_enqueued ? ygm_merge_v1_device_finish(k, &dr)
+                                      : ygm_merge_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->docs.as<uint32_t>(),
+                                                            C.u1 - C.u0, nd, nullptr, &dr);
+  else if (H.mode == 1) e = ygm_diff_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->sv_arena.as<uint8_t>(),
+                                               k->sv_offs.as<uint64_t>(), nd, nullptr, &dr);
+  else e = ygm_sv_from_update_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), nd, nullptr, &dr);
+  if (e) return e;
+  const uint32_t nb = (nd + 255) / 256;
+  if (!k->pk_data.ensure(dr.payload_bytes + 64) || !k->pk_off.ensure(8ull * nd + 8) || !k->pk_bsum.ensure(8ull * nb + 16)) return YGM_ENOMEM;
+  if (nd && ygm_k_launch_pack(dr.data, dr.off, dr.len, dr.status, nd, k->pk_bsum.as<uint64_t>(), k->pk_data.as<uint8_t>(),
+                              k->pk_off.as<uint64_t>(), k->stream))
+    return YGM_EDEVICE;
+  C.pos = pos; C.payload = dr.payload_bytes;
+  if (pos + dr.payload_bytes + 1 > c->h_data.cap) {   // regrowth moves the bytes copied so far: let those copies land first
+    for (ygm_ctx* x : c->kid) if (x) HIPCHK(hipStreamSynchronize(x->stream));
+    if (!c->h_data.ensure(pos + dr.payload_bytes + 1, pos)) return YGM_ENOMEM;
+  }
+  HIPCHK(hipEventRecord(C.o0, k->stream));
+  if (dr.payload_bytes) HIPCHK(hipMemcpyAsync(c->h_data.as<uint8_t>() + pos, k->pk_data.p, dr.payload_bytes, hipMemcpyDeviceToHost, k->stream));
+  if (nd) {
+    HIPCHK(hipMemcpyAsync(c->h_off.as<uint64_t>() + C.d0, k->pk_off.p, 8ull * nd, hipMemcpyDeviceToHost, k->stream));
+    HIPCHK(hipMemcpyAsync(c->h_len.as<uint64_t>() + C.d0, dr.len, 8ull * nd, hipMemcpyDeviceToHost, k->stream));
+    HIPCHK(hipMemcpyAsync(c->h_status.as<int32_t>() + C.d0, dr.status, 4ull * nd, hipMemcpyDeviceToHost, k->stream));
+  }
+  HIPCHK(hipEventRecord(C.o1, k->stream));
+  pos += dr.payload_bytes;
+  return YGM_OK;
+}
+
+static int host_call(ygm_ctx* c, const HostCall& H, ygm_result* out) {
+  (void)hipSetDevice(c->device);
+  const uint32_t n = H.n_docs;
+  // chunks of whole documents
+  std::vector<Chunk> ch;
+  {
+    uint32_t d = 0, u = 0;
+    while (d < n || ch.empty()) {
+      Chunk C{};
+      C.d0 = d; C.u0 = u;
+      const uint64_t base = H.mode == 2 ? H.off[u] : H.off[d];
+      while (d < n) {
+        uint32_t ue = u;
+        if (H.mode == 2) while (ue < H.n_upd && H.upd_doc[ue] == d) ue++;
+        const uint64_t end = H.mode == 2 ? H.off[ue] : H.off[d + 1];
+        if (d > C.d0 && end - base > YGM_CHUNK_BYTES) break;
+        d++; u = ue;
+      }
+      C.d1 = d; C.u1 = u;
+      ch.push_back(C);
+      if (n == 0) break;
+    }
+  }
+  // (outputs are usually no larger than the inputs: sized so, grown when a chunk needs more)
+  const uint64_t in_bytes = n ? (H.mode == 2 ? H.off[H.n_upd] - H.off[0] : H.off[n] - H.off[0]) : 0;
+  if (!c->h_off.ensure(8ull * n + 8) || !c->h_len.ensure(8ull * n + 8) || !c->h_status.ensure(4ull * n + 4) ||
+      !c->h_data.ensure(in_bytes + 16ull * n + 4096))
+    return YGM_ENOMEM;
+  int e = YGM_OK;
+  ygm_ctx* k[2];
+  if ((e = stage_ctx(c, 0, &k[0])) || (ch.size() > 1 && (e = stage_ctx(c, 1, &k[1])))) return e;
+  for (Chunk& C : ch)
+    if (hipEventCreate(&C.h0) != hipSuccess || hipEventCreate(&C.h1) != hipSuccess || hipEventCreate(&C.o0) != hipSuccess ||
+        hipEventCreate(&C.o1) != hipSuccess) { e = YGM_EDEVICE; break; }
+  ygm_stats_t s0[2] = {k[0]->stats, ch.size() > 1 ? k[1]->stats : ygm_stats_t{}};
+  uint64_t pos = 0;
+  if (!e) e = chunk_stage(k[0], H, ch[0]);
+  for (size_t i = 0; i < ch.size() && !e; i++) {
+    ygm_ctx* ki = k[i & 1];
+    bool enq = false;
+    if (H.mode == 2) {   // the lean kernel of chunk i runs while chunk i + 1 is staged
+      const uint64_t bytes = H.off[ch[i].u1] - H.off[ch[i].u0];
+      if ((e = ygm_merge_v1_device_async(ki, ki->arena.as<uint8_t>(), bytes, ki->offs.as<uint64_t>(), ki->docs.as<uint32_t>(),
+                                         ch[i].u1 - ch[i].u0, ch[i].d1 - ch[i].d0, nullptr)))
+        break;
+      enq = true;
+    }
+    if (i + 1 < ch.size()) {
+      ygm_ctx* kn = k[(i + 1) & 1];
+      // the stage's previous chunk (i - 1) has left its pinned staging (its kernels have run)
+      if ((e = chunk_stage(kn, H, ch[i + 1]))) break;
+    }
+    e = chunk_run(c, ki, H, ch[i], pos, enq);
+  }
+  for (int j = 0; j < (ch.size() > 1 ? 2 : 1); j++) if (hipStreamSynchronize(k[j]->stream) != hipSuccess && !e) e = YGM_EDEVICE;
+  if (!e) {
+    float ms = 0;
+    for (Chunk& C : ch) {
+      if (hipEventElapsedTime(&ms, C.h0, C.h1) == hipSuccess) c->stats.h2d_ms += ms;
+      if (hipEventElapsedTime(&ms, C.o0, C.o1) == hipSuccess) c->stats.d2h_ms += ms;
+      uint64_t* off = c->h_off.as<uint64_t>() + C.d0;
+      for (uint32_t d = 0; d < C.d1 - C.d0; d++) off[d] += C.pos;
+    }
+    for (int j = 0; j < (ch.size() > 1 ? 2 : 1); j++) {   // device work of the stages, into this context's counters
+      const ygm_stats_t& a = k[j]->stats; const ygm_stats_t& b = s0[j];
+      c->stats.calls += a.calls - b.calls; c->stats.docs += a.docs - b.docs; c->stats.updates += a.updates - b.updates;
+      c->stats.bytes_in += a.bytes_in - b.bytes_in; c->stats.bytes_out += a.bytes_out - b.bytes_out;
+      c->stats.docs_fast += a.docs_fast - b.docs_fast; c->stats.docs_seq += a.docs_seq - b.docs_seq;
+      c->stats.kernel_ms += a.kernel_ms - b.kernel_ms; c->stats.docs_lean += a.docs_lean - b.docs_lean;
+      c->stats.lean_ms += a.lean_ms - b.lean_ms; c->stats.lean_launches += a.lean_launches - b.lean_launches;
+      c->stats.docs_big += a.docs_big - b.docs_big;
+    }
+    int32_t* st = c->h_status.as<int32_t>();
+    uint64_t* ln = c->h_len.as<uint64_t>();
+    for (uint32_t d = 0; d < n; d++) {
+      if (st[d] >= 100 || st[d] < 0) st[d] = YGM_EDEVICE;   // never leaves internal codes
+      if (st[d] != YGM_OK) ln[d] = 0;
+    }
+    out->data = c->h_data.as<uint8_t>(); out->off = c->h_off.as<uint64_t>(); out->len = ln; out->status = st;
+    out->n_docs = n; out->data_bytes = pos;
+  }
+  for (Chunk& C : ch) for (hipEvent_t ev : {C.h0, C.h1, C.o0, C.o1}) if (ev) (void)hipEventDestroy(ev);
+  return e;
 }
 
 int ygm_merge_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* upd_off, const uint32_t* upd_doc, uint32_t n_upd, uint32_t n_docs,
                  ygm_result* out) {
   if (!c || !out || (n_upd && (!arena || !upd_off || !upd_doc))) return YGM_EINVAL;
-  (void)hipSetDevice(c->device);
-  // per-document update ranges; document ids must be non-decreasing
-  c->h_doc_upd.assign((size_t)n_docs + 1, 0);
-  for (uint32_t i = 0; i < n_upd; i++) {
-    if (upd_doc[i] >= n_docs || (i && upd_doc[i] < upd_doc[i - 1])) return YGM_EINVAL;
-    if (upd_off[i + 1] < upd_off[i]) return YGM_EINVAL;
-    c->h_doc_upd[upd_doc[i] + 1]++;
-  }
-  for (uint32_t d = 0; d < n_docs; d++) c->h_doc_upd[d + 1] += c->h_doc_upd[d];
-  const uint64_t bytes = n_upd ? upd_off[n_upd] - upd_off[0] : 0;
-  // offsets are rebased to the first update
-  std::vector<uint64_t> rel(n_upd + 1);
-  for (uint32_t i = 0; i <= n_upd; i++) rel[i] = n_upd ? upd_off[i] - upd_off[0] : 0;
-  HIPCHK(hipEventRecord(c->e2, c->stream));
-  int e;
-  if ((e = h2d(c, c->arena, n_upd ? arena + upd_off[0] : nullptr, bytes, 64))) return e;
-  if ((e = h2d(c, c->offs, rel.data(), rel.size() * 8, 0))) return e;
-  if ((e = h2d(c, c->docs, c->h_doc_upd.data(), c->h_doc_upd.size() * 4, 0))) return e;
-  HIPCHK(hipEventRecord(c->e3, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  float ms = 0;
-  if (hipEventElapsedTime(&ms, c->e2, c->e3) == hipSuccess) c->stats.h2d_ms += ms;
-  ygm_device_result dr;
-  if ((e = ygm_merge_v1_device(c, c->arena.as<uint8_t>(), bytes, c->offs.as<uint64_t>(), c->docs.as<uint32_t>(), n_upd, n_docs,
-                               nullptr, &dr)))
-    return e;
-  return fetch_results(c, n_docs, dr, out);
+  // document ids non-decreasing, offsets non-decreasing
+  std::atomic<int> bad{0};
+  par_for(n_upd, [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; i++)
+      if (upd_doc[i] >= n_docs || (i && upd_doc[i] < upd_doc[i - 1]) || upd_off[i + 1] < upd_off[i]) { bad = 1; return; }
+  });
+  if (bad) return YGM_EINVAL;
+  static const uint64_t zero_off[1] = {0};
+  HostCall H{2, arena, n_upd ? upd_off : zero_off, upd_doc, nullptr, nullptr, n_upd, n_docs};
+  return host_call(c, H, out);
 }
 
 static int host_doc_call(ygm_ctx* c, int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena,
                          const uint64_t* sv_off, uint32_t n_docs, ygm_result* out) {
   if (!c || !out || (n_docs && (!arena || !doc_off))) return YGM_EINVAL;
   if (mode == 1 && n_docs && (!sv_arena || !sv_off)) return YGM_EINVAL;
-  (void)hipSetDevice(c->device);
   for (uint32_t d = 0; d < n_docs; d++) {
     if (doc_off[d + 1] < doc_off[d]) return YGM_EINVAL;
     if (mode == 1 && sv_off[d + 1] < sv_off[d]) return YGM_EINVAL;
   }
-  const uint64_t bytes = n_docs ? doc_off[n_docs] - doc_off[0] : 0;
-  std::vector<uint64_t> rel(n_docs + 1), srel;
-  for (uint32_t d = 0; d <= n_docs; d++) rel[d] = n_docs ? doc_off[d] - doc_off[0] : 0;
-  HIPCHK(hipEventRecord(c->e2, c->stream));
-  int e;
-  if ((e = h2d(c, c->arena, n_docs ? arena + doc_off[0] : nullptr, bytes, 64))) return e;
-  if ((e = h2d(c, c->offs, rel.data(), rel.size() * 8, 0))) return e;
-  uint64_t sv_bytes = 0;
-  if (mode == 1) {
-    sv_bytes = n_docs ? sv_off[n_docs] - sv_off[0] : 0;
-    srel.resize(n_docs + 1);
-    for (uint32_t d = 0; d <= n_docs; d++) srel[d] = n_docs ? sv_off[d] - sv_off[0] : 0;
-    if ((e = h2d(c, c->sv_arena, n_docs ? sv_arena + sv_off[0] : nullptr, sv_bytes, 64))) return e;
-    if ((e = h2d(c, c->sv_offs, srel.data(), srel.size() * 8, 0))) return e;
-  }
-  HIPCHK(hipEventRecord(c->e3, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  float ms = 0;
-  if (hipEventElapsedTime(&ms, c->e2, c->e3) == hipSuccess) c->stats.h2d_ms += ms;
-  ygm_device_result dr;
-  if (mode == 1)
-    e = ygm_diff_v1_device(c, c->arena.as<uint8_t>(), bytes, c->offs.as<uint64_t>(), c->sv_arena.as<uint8_t>(), c->sv_offs.as<uint64_t>(),
-                           n_docs, nullptr, &dr);
-  else
-    e = ygm_sv_from_update_v1_device(c, c->arena.as<uint8_t>(), bytes, c->offs.as<uint64_t>(), n_docs, nullptr, &dr);
-  if (e) return e;
-  return fetch_results(c, n_docs, dr, out);
+  static const uint64_t zero_off[1] = {0};
+  HostCall H{mode, arena, n_docs ? doc_off : zero_off, nullptr, sv_arena, n_docs ? sv_off : zero_off, 0, n_docs};
+  return host_call(c, H, out);
 }
 
 int ygm_diff_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,

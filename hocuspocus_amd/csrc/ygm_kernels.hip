@@ -2356,6 +2356,71 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
   return launch_rc(__func__);
 }
 
+// ======================================================================= host API: packed results
+// The device results leave each document's bytes in its own slot; the host API copies back only the
+// outputs, packed in document order: per-256-document sums, one scan of those sums, then each
+// workgroup places and copies its documents (a wave per document, 16-byte pieces, byte stores for the
+// last partial piece -- the neighbouring document's bytes are written by another wave).
+__global__ __launch_bounds__(DOC_NT) void k_pack_sum(const uint64_t* __restrict__ len, const int32_t* __restrict__ status, uint32_t n,
+                                                   uint64_t* __restrict__ bsum) {
+  __shared__ uint64_t tmp[DOC_NT / WAVE + 1];
+  const uint32_t d = blockIdx.x * DOC_NT + threadIdx.x;
+  const uint64_t v = d < n && status[d] == ST_OK ? len[d] : 0ull;
+  uint64_t tot;
+  (void)block_exscan<DOC_NT>(v, tmp, tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(1024) void k_pack_scan(uint64_t* __restrict__ bsum, uint32_t nb) {
+  __shared__ uint64_t tmp[1024 / WAVE + 1];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nb; b0 += 1024) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint64_t v = i < nb ? bsum[i] : 0ull;
+    uint64_t tot;
+    const uint64_t pre = block_exscan<1024>(v, tmp, tot);
+    if (i < nb) bsum[i] = carry + pre;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bsum[nb] = carry;
+}
+__global__ __launch_bounds__(DOC_NT) void k_pack_copy(const uint8_t* __restrict__ src, const uint64_t* __restrict__ off,
+                                                    const uint64_t* __restrict__ len, const int32_t* __restrict__ status, uint32_t n,
+                                                    const uint64_t* __restrict__ bsum, uint8_t* __restrict__ dst,
+                                                    uint64_t* __restrict__ poff) {
+  __shared__ uint64_t tmp[DOC_NT / WAVE + 1];
+  __shared__ uint64_t s_at[DOC_NT], s_src[DOC_NT], s_len[DOC_NT];
+  const uint32_t t = threadIdx.x, d = blockIdx.x * DOC_NT + t;
+  const uint64_t v = d < n && status[d] == ST_OK ? len[d] : 0ull;
+  uint64_t tot;
+  const uint64_t at = bsum[blockIdx.x] + block_exscan<DOC_NT>(v, tmp, tot);
+  if (d < n) poff[d] = at;
+  s_at[t] = at; s_src[t] = d < n ? off[d] : 0ull; s_len[t] = v;
+  __syncthreads();
+  const uint32_t w = t / WAVE, l = t % WAVE;
+  for (uint32_t j = w; j < DOC_NT; j += DOC_NT / WAVE) {
+    const uint64_t L = s_len[j];
+    const uint8_t* a = src + s_src[j];
+    uint8_t* b = dst + s_at[j];
+    for (uint64_t c = 16ull * l; c < L; c += 16ull * WAVE) {
+      if (c + 16 <= L) { u32x4 x; __builtin_memcpy(&x, a + c, 16); __builtin_memcpy(b + c, &x, 16); }
+      else for (uint64_t k = c; k < L; k++) b[k] = a[k];
+    }
+  }
+}
+int ygm_k_launch_pack(const uint8_t* src, const uint64_t* off, const uint64_t* len, const int32_t* status, uint32_t n, uint64_t* bsum,
+                      uint8_t* dst, uint64_t* poff, hipStream_t s) {
+  if (n == 0) return 0;
+  const uint32_t nb = (n + DOC_NT - 1) / DOC_NT;
+  hipLaunchKernelGGL(k_pack_sum, dim3(nb), dim3(DOC_NT), 0, s, len, status, n, bsum);
+  hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(1024), 0, s, bsum, nb);
+  hipLaunchKernelGGL(k_pack_copy, dim3(nb), dim3(DOC_NT), 0, s, src, off, len, status, n, (const uint64_t*)bsum, dst, poff);
+  return launch_rc(__func__);
+}
+
 size_t ygm_k_sv_table_bytes(uint32_t n_docs) { return 144ull * n_docs + 64; }
 int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
                           uint64_t sv_bytes, const uint64_t* sv_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,

@@ -209,6 +209,35 @@ class Engine:
             raise YjsError(st)
         return self._unpack(res)
 
+    @staticmethod
+    def _raw(res: _Result):
+        n = res.n_docs
+        if n == 0:
+            return (np.zeros(0, np.int32), np.zeros(0, np.uint64), np.zeros(0, np.uint64), b"")
+        return (np.ctypeslib.as_array(res.status, shape=(n,)), np.ctypeslib.as_array(res.off, shape=(n,)),
+                np.ctypeslib.as_array(res.len, shape=(n,)), (ctypes.c_uint8 * max(res.data_bytes, 1)).from_address(ctypes.cast(res.data, ctypes.c_void_p).value))
+
+    def merge_packed_raw(self, arena: np.ndarray, upd_off: np.ndarray, upd_doc: np.ndarray, n_docs: int):
+        """merge_packed without the per-document Python unpacking: (status, off, len, data) views of the
+        context's pinned result buffers, valid until the next call on this engine."""
+        res = _Result()
+        st = lib().ygm_merge_v1(self._ctx, _ptr(arena), _ptr(upd_off), _ptr(upd_doc), len(upd_doc), n_docs, ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._raw(res)
+
+    def doc_packed_raw(self, op: str, arena: np.ndarray, doc_off: np.ndarray, sv_arena=None, sv_off=None):
+        """Host-array SV ("sv") / diff ("diff") batch; result views as merge_packed_raw."""
+        res = _Result()
+        n = len(doc_off) - 1
+        if op == "diff":
+            st = lib().ygm_diff_v1(self._ctx, _ptr(arena), _ptr(doc_off), _ptr(sv_arena), _ptr(sv_off), n, ctypes.byref(res))
+        else:
+            st = lib().ygm_sv_from_update_v1(self._ctx, _ptr(arena), _ptr(doc_off), n, ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._raw(res)
+
     def diff_update_batch(self, updates, svs):
         arena, off = _pack([bytes(u) for u in updates])
         sva, svo = _pack([bytes(s) for s in svs])

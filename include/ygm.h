@@ -54,10 +54,14 @@ extern "C" {
 
 typedef struct ygm_ctx ygm_ctx;
 
-/* Result of one batch call.  Owned by the context; valid until the next call
- * on the same context or ygm_close.  Document d's output is
- * data[off[d] .. off[d]+len[d]) when status[d] == YGM_OK.  Offsets are NOT
- * monotone in d (documents handled by the sequential kernel are appended). */
+/* Result of one host-API batch call.  Owned by the context (pinned host
+ * memory); valid until the next call on the same context or ygm_close.
+ * Document d's output is data[off[d] .. off[d]+len[d]) when status[d] ==
+ * YGM_OK (len[d] = 0 otherwise); outputs are packed in document order.
+ * The host API moves a batch in chunks of whole documents through two
+ * stage streams (pinned staging, H2D of chunk i+1 beside the kernels of
+ * chunk i, device-side packing, D2H of the packed outputs only); h2d_ms /
+ * d2h_ms in ygm_stats_t are those copies' event times. */
 typedef struct {
   const uint8_t *data;
   const uint64_t *off;

@@ -1,0 +1,94 @@
+'use strict'
+// C1-shaped store window (SURVEY.md §8d C1; measurement tooling, runs on the GPU box):
+// 1 000 Y.Text documents, each edited by 200 single-character inserts at random positions from one
+// client, then every document's debounced store fires in the same window (the flush of
+// Hocuspocus.ts:417-447 storeDocumentHooks).  Timed both ways, in one process, on the same documents:
+//   reference : extension-database's onStoreDocument -- Y.encodeStateAsUpdate(document) per document
+//               (packages/extension-database/src/Database.ts:55-60), yjs 13.5.16 from the image's bundle
+//   gpumerge  : GpuMerge.onStoreDocument -- Y.mergeUpdates([base, ...log]) for the window in one
+//               batched ygm_merge_v1 call through the N-API addon (src/index.js)
+// Prints one JSON line: window latency (first store call -> last store resolved) for each path, and a
+// byte-parity count of the GPU-stored states against yjs mergeUpdates of the same logs.
+//   node tools/c1_store_latency.js [docs] [inserts]
+const path = require('path')
+const ROOT = path.join(__dirname, '..')
+const Y = require(path.join(ROOT, 'tools', 'yjs_bundle.js')).load()
+const { GpuMerge } = require(path.join(ROOT, 'packages', 'extension-gpu-merge', 'src', 'index.js'))
+const { GpuEngine } = require(path.join(ROOT, 'packages', 'extension-gpu-merge', 'src', 'engine.js'))
+const { MiniHocuspocus } = require(path.join(ROOT, 'packages', 'extension-gpu-merge', 'test', 'harness.js'))
+
+const nDocs = parseInt(process.argv[2] || '1000', 10)
+const nIns = parseInt(process.argv[3] || '200', 10)
+
+function rng (seed) {   // xorshift32, seeded per document
+  let x = (seed * 2654435761) >>> 0 || 1
+  return () => { x ^= x << 13; x >>>= 0; x ^= x >>> 17; x ^= x << 5; x >>>= 0; return x }
+}
+
+class ReferenceStore {   // extension-database's store path (Database.ts:55-60)
+  constructor (rows) { this.rows = rows; this.priority = 100 }
+  async onStoreDocument ({ documentName, document }) { this.rows.set(documentName, Buffer.from(Y.encodeStateAsUpdate(document))) }
+}
+
+async function build (ext) {
+  const hp = new MiniHocuspocus({ extensions: [ext], Y, debounce: 1e9, maxDebounce: 1e12 })
+  const logs = []
+  for (let d = 0; d < nDocs; d++) {
+    const doc = await hp.loadDocument(`c1-${d}`)
+    doc.clientID = 1 + (rng(d + 7)() % 0x7fffffff)
+    const r = rng(d + 1)
+    const log = []
+    doc.on('update', u => log.push(u))
+    const t = doc.getText('t')
+    for (let i = 0; i < nIns; i++) t.doc.transact(() => t.insert(r() % (t.length + 1), String.fromCharCode(97 + (r() % 26))), 'connection')
+    logs.push(log)
+  }
+  return { hp, logs }
+}
+
+async function window (hp) {
+  const t0 = process.hrtime.bigint()
+  await hp.flushAll()
+  return Number(process.hrtime.bigint() - t0) / 1e6
+}
+
+async function main () {
+  // reference path
+  const refRows = new Map()
+  const ref = await build(new ReferenceStore(refRows))
+  const refMs = await window(ref.hp)
+  // GPU path (warm the addon / engine once on a small window first)
+  const engine = new GpuEngine({ device: 0, batchWindowMs: 2, maxBatchDocs: 65536 })
+  {
+    const rows = new Map()
+    const w = new MiniHocuspocus({ extensions: [new GpuMerge({ store: async ({ documentName, state }) => rows.set(documentName, state), Y, engine })], Y, debounce: 1e9, maxDebounce: 1e12 })
+    const doc = await w.loadDocument('warm'); doc.getText('t').insert(0, 'ab'); doc.transact(() => doc.getText('t').insert(1, 'c'), 'connection')
+    await w.flushAll()
+  }
+  const gpuRows = new Map()
+  const ext = new GpuMerge({ store: async ({ documentName, state }) => gpuRows.set(documentName, state), Y, engine })
+  const gpu = await build(ext)
+  const calls0 = engine.stats ? engine.stats().calls : null
+  const gpuMs = await window(gpu.hp)
+  const calls = engine.stats && calls0 !== null ? engine.stats().calls - calls0 : null
+  let same = 0
+  for (let d = 0; d < nDocs; d++) {
+    const exp = Buffer.from(Y.mergeUpdates(gpu.logs[d]))
+    if (Buffer.compare(exp, Buffer.from(gpuRows.get(`c1-${d}`))) === 0) same++
+  }
+  let inBytes = 0
+  for (const l of gpu.logs) for (const u of l) inBytes += u.length
+  engine.close()
+  console.log(JSON.stringify({
+    config: `C1: ${nDocs} Y.Text docs x ${nIns} single-char inserts (1 client each), one store window`,
+    reference_store_ms: Math.round(refMs * 1000) / 1000,
+    reference: 'extension-database onStoreDocument: Y.encodeStateAsUpdate(document) per document (yjs 13.5.16 bundle, Node ' + process.version + ')',
+    gpumerge_store_ms: Math.round(gpuMs * 1000) / 1000,
+    gpumerge: 'GpuMerge.onStoreDocument: Y.mergeUpdates([base, ...log]) batched through ygm_merge_v1 (N-API addon)',
+    gpumerge_engine_calls: calls,
+    log_bytes: inBytes,
+    parity: `${same}/${nDocs} stored states byte-identical to yjs mergeUpdates of the captured logs`
+  }))
+}
+
+main().catch(e => { console.error(e); process.exit(1) })

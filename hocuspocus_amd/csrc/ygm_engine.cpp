@@ -24,6 +24,10 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
                      const uint32_t* docs, uint64_t out_base, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
                      uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
 size_t ygm_k_sv_table_bytes(uint32_t n_docs);
+int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, void* cnt, uint64_t* ws_off,
+                           uint64_t* bs, hipStream_t s);
+int ygm_k_launch_snap(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, const void* cnt, const uint64_t* ws_off,
+                      uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, hipStream_t s);
 int ygm_k_launch_pack(const uint8_t* src, const uint64_t* off, const uint64_t* len, const int32_t* status, uint32_t n, uint64_t* bsum,
                       uint8_t* dst, uint64_t* poff, hipStream_t s);
 int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
@@ -117,6 +121,7 @@ struct ygm_ctx {
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
   DevBuf big_blk, big_rec, big_list;   // large-document tier: block tables, struct records, documents sent on
   DevBuf sv_tbl, sv_tn;                // diff: sorted state-vector tables (k_sv_table) and their entry counts
+  DevBuf sn_cnt, sn_off, sn_bs, sn_ws;  // snapshot: per-document counts, workspace offsets, scan scratch, workspaces
   // host API: results in pinned memory (packed outputs, per-document offset / length / status), the
   // pinned input staging of this context when it serves as a pipeline stage, the packed device copy,
   // and the two stage contexts (own streams and buffers) that double-buffer a batch's chunks
@@ -155,6 +160,7 @@ const char* ygm_strerror(int code) {
     case YGM_ENOMEM: return "out of device memory";
     case YGM_EDEVICE: return "HIP device error";
     case YGM_EINVAL: return "invalid argument";
+    case YGM_EUNSUPPORTED: return "outside the snapshot kernel's envelope (pending structs / delete set, sub-documents, ...)";
   }
   return "unknown error";
 }
@@ -186,7 +192,7 @@ void ygm_close(ygm_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
-                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn})
+                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws})
     b->release();
   for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
   for (DevBuf* b : {&c->pk_data, &c->pk_off, &c->pk_bsum}) b->release();
@@ -396,6 +402,44 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
   return YGM_OK;
 }
 
+int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
+                           void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  (void)arena_bytes;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  (void)hipSetDevice(c->device);
+  const uint32_t nb = (n_docs + 1 + 255) / 256;
+  if (!c->sn_cnt.ensure(16ull * n_docs + 16) || !c->sn_off.ensure(8ull * n_docs + 16) || !c->sn_bs.ensure(8ull * nb + 16) ||
+      !c->out_off.ensure(8ull * n_docs + 8) || !c->out_len.ensure(8ull * n_docs + 8) || !c->status.ensure(4ull * n_docs + 4))
+    return YGM_ENOMEM;
+  void* meta = c->meta_slot(2);
+  HIPCHK(hipMemsetAsync(meta, 0, sizeof(Meta), s));
+  HIPCHK(hipEventRecord(c->e0, s));
+  if (ygm_k_launch_snap_plan(d_arena, d_doc_off, n_docs, c->flags, c->sn_cnt.p, c->sn_off.as<uint64_t>(), c->sn_bs.as<uint64_t>(), s))
+    return YGM_EDEVICE;
+  uint64_t total = 0;   // workspace bytes: one read of the scanned total
+  if (n_docs) {
+    HIPCHK(hipMemcpyAsync(c->h_meta, c->sn_off.as<uint64_t>() + n_docs, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    memcpy(&total, c->h_meta, 8);
+  }
+  if (!c->sn_ws.ensure(total + 64)) return YGM_ENOMEM;
+  if (ygm_k_launch_snap(d_arena, d_doc_off, n_docs, c->flags, c->sn_cnt.p, c->sn_off.as<uint64_t>(), c->sn_ws.as<uint8_t>(),
+                        c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
+                        (unsigned long long*)((uint8_t*)meta + offsetof(Meta, payload)), s))
+    return YGM_EDEVICE;
+  HIPCHK(hipEventRecord(c->e1, s));
+  Meta m;
+  int e = read_meta(c, s, m, meta);
+  if (e) return e;
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;
+  c->stats.calls++; c->stats.docs += n_docs; c->stats.bytes_in += arena_bytes; c->stats.bytes_out += m.payload;
+  out->data = c->sn_ws.as<uint8_t>(); out->off = c->out_off.as<uint64_t>(); out->len = c->out_len.as<uint64_t>();
+  out->status = c->status.as<int32_t>(); out->data_bytes = total; out->payload_bytes = m.payload;
+  return YGM_OK;
+}
+
 int ygm_diff_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, const uint8_t* d_sv_arena,
                        const uint64_t* d_sv_off, uint32_t n_docs, void* stream, ygm_device_result* out) {
   // (the state-vector arena's extent is the last offset; its 16-byte window reads stay inside its padding)
@@ -426,7 +470,7 @@ struct Chunk {   // documents [d0, d1): merge updates [u0, u1) / SV-diff documen
   hipEvent_t h0 = nullptr, h1 = nullptr, o0 = nullptr, o1 = nullptr;
 };
 struct HostCall {
-  int mode;   // 0 sv, 1 diff, 2 merge
+  int mode;   // 0 sv, 1 diff, 2 merge, 3 snapshot
   const uint8_t* arena; const uint64_t* off; const uint32_t* upd_doc; const uint8_t* sv_arena; const uint64_t* sv_off;
   uint32_t n_upd, n_docs;
 };
@@ -526,6 +570,7 @@ static int chunk_run(ygm_ctx* c, ygm_ctx* k, const HostCall& H, Chunk& C, uint64
   if (H.mode == 2) e = merge_enqueued ? ygm_merge_v1_device_finish(k, &dr)
                                       : ygm_merge_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->docs.as<uint32_t>(),
                                                             C.u1 - C.u0, nd, nullptr, &dr);
+  else if (H.mode == 3) e = ygm_snapshot_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), nd, nullptr, &dr);
   else if (H.mode == 1) e = ygm_diff_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->sv_arena.as<uint8_t>(),
                                                k->sv_offs.as<uint64_t>(), nd, nullptr, &dr);
   else e = ygm_sv_from_update_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), nd, nullptr, &dr);
@@ -663,6 +708,10 @@ static int host_doc_call(ygm_ctx* c, int mode, const uint8_t* arena, const uint6
   static const uint64_t zero_off[1] = {0};
   HostCall H{mode, arena, n_docs ? doc_off : zero_off, nullptr, sv_arena, n_docs ? sv_off : zero_off, 0, n_docs};
   return host_call(c, H, out);
+}
+
+int ygm_snapshot_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, ygm_result* out) {
+  return host_doc_call(c, 3, arena, doc_off, nullptr, nullptr, n_docs, out);
 }
 
 int ygm_diff_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,

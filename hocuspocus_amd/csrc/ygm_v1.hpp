@@ -17,11 +17,19 @@
 //    oracle applies (oracle/yjs_oracle.c), kept in lock-step by the parity
 //    tests.
 #pragma once
-#include <hip/hip_runtime.h>
 #include <stdint.h>
-
+#ifdef YGM_HOST_BUILD   // host build of the codec for development harnesses (tools/snapdev.cpp); kernels never use it
+#include <string.h>
+#include <math.h>
+#define YDEV inline
+#define YDEV_NI inline
+static inline float __uint_as_float(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline double __longlong_as_double(long long u) { double f; memcpy(&f, &u, 8); return f; }
+#else
+#include <hip/hip_runtime.h>
 #define YDEV __device__ __forceinline__
 #define YDEV_NI __device__ __noinline__  // large, rarely-hot helpers: keep compile time and I-cache sane
+#endif
 
 namespace ygm {
 

@@ -23,7 +23,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("YGM_LIB") or os.path.join(_HERE, "libygm.so")  # YGM_LIB: experiment builds (tooling)
 
-OK, EMALFORMED, ERANGE, ENONCANON, ESURROGATE, EDEPTH, ENOMEM, EDEVICE, EINVAL = range(9)
+OK, EMALFORMED, ERANGE, ENONCANON, ESURROGATE, EDEPTH, ENOMEM, EDEVICE, EINVAL, EUNSUPPORTED = range(10)
 STATUS_NAMES = {0: "OK", 1: "EMALFORMED", 2: "ERANGE", 3: "ENONCANON", 4: "ESURROGATE", 5: "EDEPTH",
                 6: "ENOMEM", 7: "EDEVICE", 8: "EINVAL"}
 F_COMPAT_135 = 1
@@ -63,7 +63,8 @@ _lib = None
 # every symbol include/ygm.h declares
 EXPORTS = ("ygm_open", "ygm_close", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_update_v1", "ygm_merge_v1_device",
            "ygm_merge_v1_device_async", "ygm_merge_v1_device_finish",
-           "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_stats", "ygm_strerror", "ygm_version")
+           "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_snapshot_v1", "ygm_snapshot_v1_device",
+           "ygm_stats", "ygm_strerror", "ygm_version")
 
 
 def lib():
@@ -85,13 +86,15 @@ def lib():
         L.ygm_merge_v1_device_finish.argtypes = [vp, ctypes.POINTER(_DevResult)]
         L.ygm_diff_v1_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_sv_from_update_v1_device.argtypes = [vp, vp, u64, vp, u32, vp, ctypes.POINTER(_DevResult)]
+        L.ygm_snapshot_v1.argtypes = [vp, vp, vp, u32, ctypes.POINTER(_Result)]
+        L.ygm_snapshot_v1_device.argtypes = [vp, vp, u64, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.ygm_strerror.argtypes = [i32]
         L.ygm_strerror.restype = ctypes.c_char_p
         L.ygm_version.restype = ctypes.c_char_p
         for f in ("ygm_open", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_update_v1", "ygm_merge_v1_device",
                   "ygm_merge_v1_device_async", "ygm_merge_v1_device_finish",
-                  "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_stats"):
+                  "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_snapshot_v1", "ygm_snapshot_v1_device", "ygm_stats"):
             getattr(L, f).restype = i32
         _lib = L
     return _lib
@@ -256,6 +259,24 @@ class Engine:
         return self._unpack(res)
 
     # ------------------------------------------------------------ yjs-shaped single calls
+    def snapshot_batch(self, updates):
+        """Doc-normalized snapshots: Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), u)) per update
+        (ygm_snapshot_v1) -> list of (status, bytes | None); UNSUPPORTED marks documents outside the envelope."""
+        arena, off = _pack([bytes(u) for u in updates])
+        res = _Result()
+        st = lib().ygm_snapshot_v1(self._ctx, arena or None, _ptr(off), len(updates), ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._unpack(res)
+
+    def snapshot_device(self, d_arena, arena_bytes, d_doc_off, n_docs, stream=0) -> "DeviceResult":
+        r = _DevResult()
+        st = lib().ygm_snapshot_v1_device(self._ctx, _dptr(d_arena, arena_bytes + TAIL_PAD), arena_bytes, _dptr(d_doc_off), n_docs,
+                                          stream or None, ctypes.byref(r))
+        if st != OK:
+            raise YjsError(st)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)
+
     def merge_updates(self, updates):
         st, out = self.merge_updates_batch([list(updates)])[0]
         if st != OK:

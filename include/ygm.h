@@ -45,6 +45,9 @@ extern "C" {
 #define YGM_ENOMEM 6
 #define YGM_EDEVICE 7      /* HIP error / device fault */
 #define YGM_EINVAL 8       /* bad call arguments */
+#define YGM_EUNSUPPORTED 9 /* ygm_snapshot_v1 only: the update leaves pending structs or a pending delete set
+                              (missing dependencies), repeats or overlaps structs, or carries sub-documents --
+                              the caller keeps its yjs path for that document */
 
 #define YGM_MAX_DEPTH 32
 
@@ -104,6 +107,14 @@ int ygm_diff_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, con
 int ygm_sv_from_update_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, uint32_t n_docs,
                           ygm_result *out);
 
+/* Doc-normalized snapshot: Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), update)) per document
+ * -- the bytes extension-database stores (packages/extension-database/src/Database.ts:55-60,
+ * Y.encodeStateAsUpdate of the live document): YATA-integrated, deleted content garbage-collected,
+ * adjacent structs merged (yjs Y@20500-32900 readUpdate / cleanupTransactions, Y@23300
+ * encodeStateAsUpdate).  One update per document (e.g. the output of ygm_merge_v1).  Documents
+ * outside the envelope carry YGM_EUNSUPPORTED. */
+int ygm_snapshot_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, uint32_t n_docs, ygm_result *out);
+
 /* ---- device-resident API (inputs already in HBM; used by bench.py) --------
  * All pointers are device pointers.  doc_upd: n_docs+1 update-index offsets
  * (document d owns updates doc_upd[d] .. doc_upd[d+1]); upd_off must be
@@ -150,6 +161,9 @@ int ygm_diff_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_byte
 int ygm_sv_from_update_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes,
                                  const uint64_t *d_doc_off, uint32_t n_docs, void *stream,
                                  ygm_device_result *out);
+
+int ygm_snapshot_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
+                           uint32_t n_docs, void *stream, ygm_device_result *out);
 
 int ygm_stats(ygm_ctx *ctx, ygm_stats_t *out);
 const char *ygm_strerror(int code);

@@ -1,0 +1,147 @@
+"""Doc-normalized snapshot: snapshot(u) = Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), u)).
+
+The checker is yjs itself -- the image's 13.5.16 bundle (tools/yjs_bundle.js) -- through
+  * tests/golden/snapshot_v135.json.gz: 440 multi-peer editing sessions (tools/snap_corpus.js: Y.Text with
+    UTF-8 of every width, formatting, embeds, Y.Array / Y.Map with nested types and overwrites, XmlFragment
+    trees with attributes, deleted nested types, concurrent peers) and their yjs snapshots;
+  * live sessions generated on the GPU box by the same script with fresh seeds (Node + the bundle ship in
+    the image there too);
+  * the GPU merge's own outputs for C2 logs, snapshotted by yjs (tools/snap_expect.js).
+CPU tests pin the fixtures (regenerated here by the committed generator) and run the kernel's sequential
+code (ygm_snapshot.hpp) host-compiled through tools/snapdev; GPU tests run the HIP kernel through the C ABI
+in 13.5 compat mode (the bundle's behaviour).  The 13.6 default writes the delete set's clients in descending
+order instead of store order; that mode's snapshot bytes are parity unpinned (no 13.6 yjs in the image)."""
+import gzip
+import json
+import os
+import shutil
+import struct
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIX = os.path.join(ROOT, "tests", "golden", "snapshot_v135.json.gz")
+NODE = shutil.which("node")
+BUNDLE = os.path.exists("/opt/conda/share/jupyter/lab/static/3502.fbe0c610be82ba1360db.js")
+
+
+def fixtures():
+    d = json.load(gzip.open(FIX, "rt"))
+    return [(bytes.fromhex(u), bytes.fromhex(e)) for u, e in d["rows"]]
+
+
+def write_in(path, us):
+    with open(path, "wb") as f:
+        f.write(struct.pack("<I", len(us)))
+        for u in us:
+            f.write(struct.pack("<I", len(u)))
+            f.write(u)
+
+
+def read_res(path):
+    b = open(path, "rb").read()
+    i, out = 0, []
+    while i < len(b):
+        st, ln = struct.unpack_from("<iI", b, i)
+        i += 8
+        out.append((st, b[i:i + ln]))
+        i += ln
+    return out
+
+
+def read_in(path):
+    b = open(path, "rb").read()
+    n = struct.unpack_from("<I", b, 0)[0]
+    i, out = 4, []
+    for _ in range(n):
+        ln = struct.unpack_from("<I", b, i)[0]
+        i += 4
+        out.append(b[i:i + ln])
+        i += ln
+    return out
+
+
+def test_fixtures_present():
+    rows = fixtures()
+    assert len(rows) == 440 and all(u and e for u, e in rows)
+
+
+@pytest.mark.skipif(not (NODE and BUNDLE), reason="node + the yjs bundle are needed to regenerate")
+def test_fixtures_regenerate(tmp_path):
+    """The committed vectors are what the committed generator produces from the bundle (first sessions)."""
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "exp.bin")
+    subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_corpus.js"), "20", "11", a, b, "80"], check=True, timeout=120)
+    rows = fixtures()[:20]
+    assert read_in(a) == [u for u, _ in rows]
+    assert [e for _, e in read_res(b)] == [e for _, e in rows]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
+def test_kernel_code_on_host_vs_fixtures(tmp_path):
+    """The kernel's sequential code (ygm_snapshot.hpp), host-compiled, against the yjs vectors (13.5 mode)."""
+    exe = str(tmp_path / "snapdev")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", exe, os.path.join(ROOT, "tools", "snapdev", "snapdev.cpp")], check=True, timeout=300)
+    rows = fixtures()
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
+    write_in(a, [u for u, _ in rows])
+    subprocess.run([exe, a, b, "1"], check=True, timeout=120)
+    got = read_res(b)
+    assert [g for g in got] == [(0, e) for _, e in rows]
+
+
+# ---------------------------------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def eng135():
+    from hocuspocus_amd import Engine
+    e = Engine(0, compat135=True)
+    yield e
+    e.close()
+
+
+@pytest.mark.gpu
+def test_gpu_snapshot_vs_yjs_fixtures(eng135):
+    rows = fixtures()
+    res = eng135.snapshot_batch([u for u, _ in rows])
+    bad = [k for k, ((_, e), r) in enumerate(zip(rows, res)) if r != (0, e)]
+    assert not bad, f"{len(bad)} documents differ from yjs, first {bad[:5]}: {res[bad[0]]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not (NODE and BUNDLE), reason="node + the yjs bundle (image) needed for live sessions")
+def test_gpu_snapshot_vs_live_yjs(eng135, tmp_path):
+    """Fresh sessions generated on this box by yjs, longer ones included."""
+    for seed, n, ops in ((901, 300, 60), (902, 40, 1500)):
+        a, b = str(tmp_path / f"in{seed}.bin"), str(tmp_path / f"exp{seed}.bin")
+        subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_corpus.js"), str(n), str(seed), a, b, str(ops)], check=True, timeout=240)
+        us, exp = read_in(a), read_res(b)
+        res = eng135.snapshot_batch(us)
+        bad = [k for k, (e, r) in enumerate(zip(exp, res)) if r != e]
+        assert not bad, f"seed {seed}: {len(bad)} differ, first {bad[:5]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not (NODE and BUNDLE), reason="node + the yjs bundle (image) needed")
+def test_gpu_snapshot_of_gpu_merges(eng135, tmp_path):
+    """C2 debounce logs merged on the GPU, then snapshotted on the GPU, against yjs's snapshot of the merge."""
+    from tools import synth
+    arena, upd_off, doc_upd = synth.text_updates(300, 200, seed=41, del_pct=20)
+    docs = [[arena[upd_off[u]:upd_off[u + 1]].tobytes() for u in range(doc_upd[d], doc_upd[d + 1])] for d in range(300)]
+    merged = [m for st, m in eng135.merge_updates_batch(docs)]
+    assert all(m is not None for m in merged)
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "exp.bin")
+    write_in(a, merged)
+    subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_expect.js"), a, b], check=True, timeout=240)
+    assert eng135.snapshot_batch(merged) == [(st, e if st == 0 else None) for st, e in read_res(b)]
+
+
+@pytest.mark.gpu
+def test_gpu_snapshot_envelope():
+    """Pending structs (a gap) and a missing origin are refused, not guessed; an empty update is malformed (yjs throws)."""
+    from hocuspocus_amd import Engine
+    from hocuspocus_amd.engine import EUNSUPPORTED, EMALFORMED
+    with Engine(0) as e:
+        gap = bytes([1, 1, 5, 3, 0x04, 1, 1, 0x74, 1, 0x61, 0])   # client 5 starts at clock 3: pending
+        orphan = bytes([1, 1, 5, 0, 0x84, 9, 0, 1, 0x61, 0])   # origin (9, 0) is not in the update
+        res = e.snapshot_batch([gap, orphan, b""])
+        assert res[0][0] == EUNSUPPORTED and res[1][0] == EUNSUPPORTED and res[2][0] == EMALFORMED

@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads / workers (0: the cores granted, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-yjs", action="store_true", help="skip the Node / yjs leg of the CPU baseline")
+    ap.add_argument("--f1-docs", type=int, default=10000, help="documents of the f1 (doc-normalized snapshot) block (0: skip)")
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
                     help="skip the host_api block (host arrays through the pinned / two-stream host API)")
     ap.add_argument("--big", choices=["c3", "c5"], default=None,
@@ -288,6 +289,49 @@ def c1_store_window(docs=1000, inserts=200):
         return {"error": repr(ex)[:400]}
 
 
+def f1_block(be, args, steps=5):
+    """snapshot(u) = encodeStateAsUpdate(applyUpdate(new Doc, u)) -- what extension-database stores --
+    over the merged states of C2 logs with 20 % deletions (the GpuMerge normalize path: merge, then snapshot).
+    Inputs resident in HBM; per step the count + scan + snapshot kernels (one workspace-size read between them)."""
+    from hocuspocus_amd import Engine
+    from tools import synth
+    e = Engine(be.dev.index, compat135=True)
+    arena, upd_off, doc_upd = synth.text_updates(args.f1_docs, args.updates, seed=61, del_pct=20)
+    upd_doc = np.repeat(np.arange(args.f1_docs, dtype=np.uint32), np.diff(doc_upd.astype(np.int64)))
+    st, off, ln, data = e.merge_packed_raw(arena, upd_off, upd_doc, args.f1_docs)
+    assert (st == 0).all()
+    buf = np.frombuffer(bytes(data), np.uint8)
+    states = np.concatenate([buf[int(off[d]):int(off[d]) + int(ln[d])] for d in range(args.f1_docs)])
+    doc_off = np.zeros(args.f1_docs + 1, np.uint64)
+    doc_off[1:] = np.cumsum(ln.astype(np.uint64))
+    da, do = be.put(states, 64), be.put(doc_off.view(np.int64))
+    for _ in range(2):
+        e.snapshot_device(da, len(states), do, args.f1_docs, be.stream.cuda_stream)
+    s0 = e.stats()
+    be.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = e.snapshot_device(da, len(states), do, args.f1_docs, be.stream.cuda_stream)
+    be.sync()
+    wall = (time.perf_counter() - t0) / steps
+    s1 = e.stats()
+    kms = (s1.kernel_ms - s0.kernel_ms) / steps
+    algo = len(states) + int(r.payload_bytes)
+    stat = _d2h(r.status, 4 * args.f1_docs).view(np.int32)
+    blk = {"workload": f"f-1: {args.f1_docs} C2 logs ({args.updates} single-char updates, 20 % deletions, 1-4 clients) merged, then "
+                       "snapshotted (YATA integrate + GC + merge + encode, yjs 13.5.16 semantics), inputs resident in HBM",
+           "docs": args.f1_docs, "bytes_in": len(states), "bytes_out": int(r.payload_bytes), "ok_docs": int((stat == 0).sum()),
+           "value": round(algo / kms / 1e3, 3), "unit": "MB/s", "docs_per_s": round(args.f1_docs / kms * 1e3, 1),
+           "ms_per_step": round(kms, 4), "wall_ms_per_step": round(wall * 1e3, 4),
+           "roofline": roof(algo, kms, "k_snap_count + scan + k_snap (one thread per document)", None),
+           "parity": "yjs vectors in tests/test_snapshot.py (440 fixed + live sessions + GPU-merged C2 logs) -- bit-exact"}
+    if not args.no_cpu_baseline and not args.no_yjs:
+        c = {"arena": states, "doc_off": doc_off}
+        blk["cpu_baseline"] = cpu_yjs("snapshot", c, cpu_cores(args), min(args.f1_docs, 4000))
+    e.close()
+    return blk
+
+
 def host_api_doc(be, c, op, n, reps=3):
     from hocuspocus_amd import Engine
     import oracle
@@ -452,7 +496,7 @@ def cpu_yjs(kind, c, cores, k):
         return {"value": round(j["algo_bytes"] / j["seconds"] / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "reference",
                 "docs_per_s": round(k / j["seconds"], 1),
                 "sample": f"yjs 13.5.16 (JupyterLab bundle in the image; the reference pins 13.6.26) Y."
-                          f"{ {'merge': 'mergeUpdates', 'sv': 'encodeStateVectorFromUpdate', 'diff': 'diffUpdate'}[kind]} over the first "
+                          f"{ {'merge': 'mergeUpdates', 'sv': 'encodeStateVectorFromUpdate', 'diff': 'diffUpdate', 'snapshot': 'encodeStateAsUpdate(applyUpdate(new Doc, u))'}[kind]} over the first "
                           f"{k} documents on Node {ver} worker_threads x {cores}, op loop only, slowest worker {j['seconds']:.2f} s"}
     finally:
         shutil.rmtree(d, ignore_errors=True)
@@ -559,6 +603,9 @@ def run_rank(args, rank, world, dist, be, dev=None):
             if not args.dry_run and args.host_api and "host_api" in line:
                 line["host_api"]["c4_diff"] = host_api_doc(be, c, "diff", min(c["n"], 250000))
         c4 = c
+    # ---- f-1: doc-normalized snapshots of merged debounce logs (C2 with 20 % deletes)
+    if args.f1_docs and rank == 0 and not args.dry_run:
+        line["f1"] = f1_block(be, args)
     # ---- CPU baselines (rank 0 at N = 1 only)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         cores = cpu_cores(args)

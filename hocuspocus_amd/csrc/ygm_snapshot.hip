@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "ygm_common.hpp"
 #include "ygm_snapshot.hpp"
@@ -65,10 +66,12 @@ __global__ __launch_bounds__(256) void k_snap_scan_apply(uint64_t* __restrict__ 
 __global__ __launch_bounds__(SN_NT) void k_snap(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off, uint32_t n_docs,
                                                uint32_t flags, const uint4* __restrict__ cnt, const uint64_t* __restrict__ ws_off,
                                                uint8_t* __restrict__ ws, uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len,
-                                               int32_t* __restrict__ status, unsigned long long* __restrict__ payload) {
-  const uint32_t d = blockIdx.x * SN_NT + threadIdx.x;
+                                               int32_t* __restrict__ status, unsigned long long* __restrict__ payload, uint32_t dpw) {
+  // dpw documents per wave (lanes >= dpw idle): the per-document code diverges from lane to lane, so
+  // fewer documents per wave trade SIMD lanes for less serialised divergence and more waves in flight
+  const uint32_t d = blockIdx.x * dpw + threadIdx.x;
   uint64_t mine = 0;
-  if (d < n_docs) {
+  if (threadIdx.x < dpw && d < n_docs) {
     const uint4 c = cnt[d];
     const uint64_t a = doc_off[d], b = doc_off[d + 1];
     int st = ST_OK;
@@ -116,9 +119,12 @@ int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32
 int ygm_k_launch_snap(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, const void* cnt, const uint64_t* ws_off,
                       uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, hipStream_t s) {
   if (n_docs == 0) return 0;
-  const uint32_t g = (n_docs + SN_NT - 1) / SN_NT;
+  const char* env = getenv("YGM_SNAP_DPW");
+  uint32_t dpw = env ? (uint32_t)atoi(env) : 4u;
+  if (dpw < 1 || dpw > (uint32_t)SN_NT) dpw = 4u;
+  const uint32_t g = (n_docs + dpw - 1) / dpw;
   hipLaunchKernelGGL(k_snap, dim3(g), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, (const uint4*)cnt, ws_off, ws, out_off, out_len,
-                     status, payload);
+                     status, payload, dpw);
   return snap_rc(__func__);
 }
 

@@ -132,6 +132,7 @@ static void job_execute(napi_env env, void *data) {
   ygm_result r; memset(&r, 0, sizeof r);
   if (j->op == 0) j->rc = ygm_merge_v1(j->h->ctx, j->arena, j->off, j->docs, j->n_upd, j->n_docs, &r);
   else if (j->op == 1) j->rc = ygm_diff_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
+  else if (j->op == 3) j->rc = ygm_snapshot_v1(j->h->ctx, j->arena, j->off, j->n_docs, &r);
   else j->rc = ygm_sv_from_update_v1(j->h->ctx, j->arena, j->off, j->n_docs, &r);
   if (j->rc != YGM_OK) return;
   /* results are context-owned: copy out before the next batch may reuse them */
@@ -258,6 +259,25 @@ static napi_value js_sv(napi_env env, napi_callback_info info) {
   return submit(env, j, "ygm.svMany");
 }
 
+/* snapshotMany(h, arena, lens): Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), u)) per update */
+static napi_value js_snapshot(napi_env env, napi_callback_info info) {
+  size_t argc = 3; napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 3) { napi_throw_type_error(env, NULL, "snapshotMany(handle, arena, lens)"); return NULL; }
+  Handle *h = get_handle(env, argv[0]);
+  if (!h) return NULL;
+  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = 3; j->h = h;
+  size_t an, ln; void *lens = NULL;
+  if (get_bytes(env, argv[1], (void **)&j->arena, &an) || get_bytes(env, argv[2], &lens, &ln)) {
+    free(lens); job_free(j); napi_throw_type_error(env, NULL, "snapshotMany: bad arguments"); return NULL;
+  }
+  j->n_docs = (uint32_t)(ln / 4);
+  j->off = lens_to_off((const uint32_t *)lens, j->n_docs);
+  free(lens);
+  if (j->off[j->n_docs] != an) { job_free(j); napi_throw_range_error(env, NULL, "snapshotMany: sum(lens) != arena length"); return NULL; }
+  return submit(env, j, "ygm.snapshotMany");
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor d[] = {
     { "open", NULL, js_open, NULL, NULL, NULL, napi_default, NULL },
@@ -265,6 +285,7 @@ static napi_value init(napi_env env, napi_value exports) {
     { "mergeMany", NULL, js_merge, NULL, NULL, NULL, napi_default, NULL },
     { "diffMany", NULL, js_diff, NULL, NULL, NULL, napi_default, NULL },
     { "svMany", NULL, js_sv, NULL, NULL, NULL, napi_default, NULL },
+    { "snapshotMany", NULL, js_snapshot, NULL, NULL, NULL, napi_default, NULL },
     { "stats", NULL, js_stats, NULL, NULL, NULL, napi_default, NULL },
     { "strerror", NULL, js_strerror, NULL, NULL, NULL, napi_default, NULL },
   };

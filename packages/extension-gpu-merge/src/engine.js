@@ -17,7 +17,7 @@ function loadAddon () {
   return addon
 }
 
-const STATUS = ['OK', 'EMALFORMED', 'ERANGE', 'ENONCANON', 'ESURROGATE', 'EDEPTH', 'ENOMEM', 'EDEVICE', 'EINVAL']
+const STATUS = ['OK', 'EMALFORMED', 'ERANGE', 'ENONCANON', 'ESURROGATE', 'EDEPTH', 'ENOMEM', 'EDEVICE', 'EINVAL', 'EUNSUPPORTED']
 
 class YgmError extends Error {
   constructor (code, message) {
@@ -91,7 +91,7 @@ class GpuEngine {
     this.batchWindowMs = opts.batchWindowMs === undefined ? 2 : opts.batchWindowMs
     this.maxBatchDocs = opts.maxBatchDocs || 65536
     this.handle = loadAddon().open(this.device, this.flags)
-    this.batchers = { merge: new Batcher(this, 'merge'), diff: new Batcher(this, 'diff'), sv: new Batcher(this, 'sv') }
+    this.batchers = { merge: new Batcher(this, 'merge'), diff: new Batcher(this, 'diff'), sv: new Batcher(this, 'sv'), snapshot: new Batcher(this, 'snapshot') }
     this.chain = Promise.resolve()
   }
 
@@ -110,6 +110,7 @@ class GpuEngine {
         return a.diffMany(this.handle, u.arena, u.lens, s.arena, s.lens)
       }
       const u = packBlobs(jobs)
+      if (op === 'snapshot') return a.snapshotMany(this.handle, u.arena, u.lens)
       return a.svMany(this.handle, u.arena, u.lens)
     }
     const p = this.chain.then(run, run)
@@ -123,11 +124,14 @@ class GpuEngine {
   diffUpdate (update, sv) { return this.batchers.diff.push([update, sv]) }
   /** Y.encodeStateVectorFromUpdate(update) */
   encodeStateVectorFromUpdate (update) { return this.batchers.sv.push(update) }
+  /** Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), update)): the doc-normalized snapshot (GC'd, merged) */
+  snapshot (update) { return this.batchers.snapshot.push(update) }
 
   /** explicit batches (sync responders, bulk snapshot jobs) */
   async mergeMany (docs) { const r = await this._run('merge', docs); return unpack(r) }
   async diffMany (states, svs) { const r = await this._run('diff', states.map((s, i) => [s, svs[i]])); return unpack(r) }
   async stateVectorsMany (states) { const r = await this._run('sv', states); return unpack(r) }
+  async snapshotMany (states) { const r = await this._run('snapshot', states); return unpack(r) }
 
   stats () { return loadAddon().stats(this.handle) }
   close () { if (this.handle) { loadAddon().close(this.handle); this.handle = null } }
@@ -166,6 +170,7 @@ class GpuEnginePool {
   mergeUpdates (updates, documentName = '') { return this.engineFor(documentName).mergeUpdates(updates) }
   diffUpdate (update, sv, documentName = '') { return this.engineFor(documentName).diffUpdate(update, sv) }
   encodeStateVectorFromUpdate (update, documentName = '') { return this.engineFor(documentName).encodeStateVectorFromUpdate(update) }
+  snapshot (update, documentName = '') { return this.engineFor(documentName).snapshot(update) }
 
   async _many (names, cols, run) {
     const parts = this.engines.map(() => [])
@@ -182,6 +187,7 @@ class GpuEnginePool {
   mergeMany (names, docs) { return this._many(names, [docs], (e, d) => e.mergeMany(d)) }
   diffMany (names, states, svs) { return this._many(names, [states, svs], (e, a, b) => e.diffMany(a, b)) }
   stateVectorsMany (names, states) { return this._many(names, [states], (e, a) => e.stateVectorsMany(a)) }
+  snapshotMany (names, states) { return this._many(names, [states], (e, a) => e.snapshotMany(a)) }
   stats () { return this.engines.map(e => e.stats()) }
   close () { this.engines.forEach(e => e.close()) }
 }

@@ -40,10 +40,14 @@ class GpuMerge {
   /**
    * @param {{store?: DocumentStore|Function, fetch?: Function, device?: number, Y?: any,
    *          engine?: GpuEngine, batchWindowMs?: number, maxBatchDocs?: number, compat135?: boolean,
-   *          onRefused?: 'reference'|'throw'}} configuration
+   *          onRefused?: 'reference'|'throw', normalize?: boolean}} configuration
    *   onRefused: what a store does when the engine refuses a document's merge -- 'reference' (default):
    *   store Y.encodeStateAsUpdate(document) like extension-database and record it in `refused`;
    *   'throw': reject the store (Hocuspocus logs and rethrows, Hocuspocus.ts:431-435)
+   *   normalize: store the doc-normalized snapshot of the merge, Y.encodeStateAsUpdate(Y.applyUpdate(new
+   *   Y.Doc(), merged)) computed on the GPU (SURVEY.md §8f-1) -- deleted content garbage-collected and
+   *   adjacent structs merged, the shape extension-database stores (Database.ts:55-60) -- instead of the
+   *   bare merge; a document outside the snapshot kernel's envelope keeps its merged bytes (`unnormalized`)
    */
   constructor (configuration = {}) {
     this.extensionName = 'GpuMerge'
@@ -61,6 +65,8 @@ class GpuMerge {
     this.docs = new Map()
     /** stores that fell back to Y.encodeStateAsUpdate(document) because the engine refused the merge */
     this.refused = []
+    /** normalize: stores that kept the merged bytes (snapshot outside the kernel's envelope) */
+    this.unnormalized = []
   }
 
   _Y () { if (!this.Y) this.Y = require('yjs'); return this.Y }
@@ -144,6 +150,7 @@ class GpuMerge {
     else {
       try {
         state = await this._engine().mergeUpdates(parts, data.documentName)
+        if (this.configuration.normalize) state = await this._normalize(state, data.documentName)
       } catch (e) {
         // a document the engine refuses (content yjs would re-encode, YGM_ENONCANON; a corrupt stored
         // base) or a failed batch: unless configured to throw, store what extension-database stores for
@@ -158,6 +165,16 @@ class GpuMerge {
     // the stored state becomes the new base (under the document's saveMutex, Hocuspocus.ts:427)
     entry.base = state
     entry.log.splice(0, all ? entry.log.length : taken)
+  }
+
+  // the doc-normalized snapshot of a merged state; outside the kernel's envelope the merge is kept
+  async _normalize (state, documentName) {
+    try {
+      return await this._engine().snapshot(state, documentName)
+    } catch (e) {
+      if (e && e.code === 'EUNSUPPORTED') { this.unnormalized.push({ documentName, code: e.code }); return state }
+      throw e
+    }
   }
 
   async afterUnloadDocument (data) {

@@ -19,6 +19,7 @@ class CpuDouble { // test double (never shipped): same API as GpuEngine
   async mergeMany (docs) { this.calls++; return docs.map(u => Y.mergeUpdates(u)) }
   async diffMany (states, svs) { this.calls++; return states.map((u, i) => Y.diffUpdate(u, svs[i])) }
   async stateVectorsMany (states) { this.calls++; return states.map(u => Y.encodeStateVectorFromUpdate(u)) }
+  async snapshot (u) { this.calls++; const d = new Y.Doc(); Y.applyUpdate(d, u); return Y.encodeStateAsUpdate(d) }
   close () {}
 }
 
@@ -182,6 +183,31 @@ test('afterLoadDocument adds nothing when the load added nothing', async (engine
 })
 
 // SURVEY.md §8e: documents sharded over the node's GPUs by fnv1a64(documentName) mod N
+// SURVEY.md §8f-1: normalize stores what extension-database stores for a fresh load of the merge --
+// encodeStateAsUpdate(applyUpdate(new Doc, mergeUpdates(log))): deleted text garbage-collected
+test('normalize stores the doc-normalized snapshot of the merge', async (engine) => {
+  const db = memoryDb()
+  const ext = new GpuMerge({ ...db, Y, engine, normalize: true })
+  const hp = new MiniHocuspocus({ extensions: [ext], Y })
+  const doc = await hp.loadDocument('norm')
+  doc.clientID = 7
+  const log = []
+  doc.on('update', u => log.push(u))
+  const t = doc.getText('t')
+  for (let i = 0; i < 40; i++) doc.transact(() => t.insert(i % 5 === 0 ? 0 : t.length, 'abc'.charAt(i % 3)), 'c1')
+  doc.transact(() => t.delete(3, 20), 'c1')
+  await hp.flushAll(); await hp.lastStore
+  const merged = Y.mergeUpdates(log)
+  const fresh = new Y.Doc(); Y.applyUpdate(fresh, merged)
+  const expected = Buffer.from(Y.encodeStateAsUpdate(fresh))
+  const stored = db.rows.get('norm')
+  assert.strictEqual(Buffer.compare(stored, expected), 0)
+  assert.ok(stored.length < Buffer.from(merged).length, 'garbage-collected snapshot is smaller than the merge')
+  const back = new Y.Doc(); Y.applyUpdate(back, stored)
+  assert.strictEqual(back.getText('t').toString(), t.toString())
+  assert.deepStrictEqual(ext.unnormalized, [])
+})
+
 test('engine pool shards by fnv1a64(name) and keeps caller order', async () => {
   assert.strictEqual(fnv1a64('').toString(16), 'cbf29ce484222325')     // FNV-1a 64 published vectors
   assert.strictEqual(fnv1a64('foobar').toString(16), '85944171f73967e8')

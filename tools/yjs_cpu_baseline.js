@@ -3,7 +3,8 @@
 // Y.diffUpdate / Y.encodeStateVectorFromUpdate per document over a contiguous shard of a corpus
 // that bench.py wrote to disk.  Only the op loop is timed; the job's time is the slowest worker.
 //
-//   node tools/yjs_cpu_baseline.js <dir> <op: merge|sv|diff> <workers>
+//   node tools/yjs_cpu_baseline.js <dir> <op: merge|sv|diff|snapshot> <workers>
+//   (snapshot: Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), u)), what extension-database stores)
 //   <dir>/arena.bin, <dir>/off.bin (u64 update or document offsets), <dir>/docs.bin (u32 update index
 //   per document, merge), <dir>/sv.bin + <dir>/svoff.bin (diff)
 // Prints one JSON line: {op, docs, workers, seconds, algo_bytes}.
@@ -54,7 +55,7 @@ if (isMainThread) {
   const t0 = process.hrtime.bigint()
   for (const j of jobs) {
     let out
-    if (op === 'merge') { out = Y.mergeUpdates(j); for (const u of j) algo += u.length } else if (op === 'diff') { out = Y.diffUpdate(j[0], j[1]); algo += j[0].length + j[1].length } else { out = Y.encodeStateVectorFromUpdate(j); algo += j.length }
+    if (op === 'merge') { out = Y.mergeUpdates(j); for (const u of j) algo += u.length } else if (op === 'diff') { out = Y.diffUpdate(j[0], j[1]); algo += j[0].length + j[1].length } else if (op === 'snapshot') { const d = new Y.Doc(); Y.applyUpdate(d, j); out = Y.encodeStateAsUpdate(d); algo += j.length } else { out = Y.encodeStateVectorFromUpdate(j); algo += j.length }
     algo += out.length
   }
   const seconds = Number(process.hrtime.bigint() - t0) / 1e9

@@ -26,6 +26,11 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
 size_t ygm_k_sv_table_bytes(uint32_t n_docs);
 int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, void* cnt, uint64_t* ws_off,
                            uint64_t* bs, hipStream_t s);
+int ygm_k_launch_cont_plan(const uint8_t* st_arena, const uint64_t* st_off, uint32_t n_docs, uint32_t flags, uint64_t* ws_off, uint64_t* bs,
+                           hipStream_t s);
+int ygm_k_launch_cont(const uint8_t* st_arena, const uint64_t* st_off, const uint8_t* up_arena, const uint64_t* up_off, uint32_t n_docs,
+                      uint32_t flags, const uint64_t* ws_off, uint8_t* ws, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
+                      int32_t* status, hipStream_t s);
 int ygm_k_launch_snap(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, const void* cnt, const uint64_t* ws_off,
                       uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, hipStream_t s);
 int ygm_k_launch_pack(const uint8_t* src, const uint64_t* off, const uint64_t* len, const int32_t* status, uint32_t n, uint64_t* bsum,
@@ -440,6 +445,37 @@ int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_by
   return YGM_OK;
 }
 
+int ygm_contains_v1_device(ygm_ctx* c, const uint8_t* d_states, const uint64_t* d_state_off, const uint8_t* d_updates,
+                           const uint64_t* d_update_off, uint32_t n_docs, void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  (void)hipSetDevice(c->device);
+  const uint32_t nb = (n_docs + 1 + 255) / 256;
+  if (!c->sn_off.ensure(8ull * n_docs + 16) || !c->sn_bs.ensure(8ull * nb + 16) || !c->out.ensure((uint64_t)n_docs + 64) ||
+      !c->out_off.ensure(8ull * n_docs + 8) || !c->out_len.ensure(8ull * n_docs + 8) || !c->status.ensure(4ull * n_docs + 4))
+    return YGM_ENOMEM;
+  HIPCHK(hipEventRecord(c->e0, s));
+  if (ygm_k_launch_cont_plan(d_states, d_state_off, n_docs, c->flags, c->sn_off.as<uint64_t>(), c->sn_bs.as<uint64_t>(), s)) return YGM_EDEVICE;
+  uint64_t total = 0;
+  if (n_docs) {
+    HIPCHK(hipMemcpyAsync(c->h_meta, c->sn_off.as<uint64_t>() + n_docs, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    memcpy(&total, c->h_meta, 8);
+  }
+  if (!c->sn_ws.ensure(total + 64)) return YGM_ENOMEM;
+  if (ygm_k_launch_cont(d_states, d_state_off, d_updates, d_update_off, n_docs, c->flags, c->sn_off.as<uint64_t>(), c->sn_ws.as<uint8_t>(),
+                        c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), s))
+    return YGM_EDEVICE;
+  HIPCHK(hipEventRecord(c->e1, s));
+  HIPCHK(hipStreamSynchronize(s));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;
+  c->stats.calls++; c->stats.docs += n_docs;
+  out->data = c->out.as<uint8_t>(); out->off = c->out_off.as<uint64_t>(); out->len = c->out_len.as<uint64_t>();
+  out->status = c->status.as<int32_t>(); out->data_bytes = n_docs; out->payload_bytes = n_docs;
+  return YGM_OK;
+}
+
 int ygm_diff_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, const uint8_t* d_sv_arena,
                        const uint64_t* d_sv_off, uint32_t n_docs, void* stream, ygm_device_result* out) {
   // (the state-vector arena's extent is the last offset; its 16-byte window reads stay inside its padding)
@@ -470,7 +506,7 @@ struct Chunk {   // documents [d0, d1): merge updates [u0, u1) / SV-diff documen
   hipEvent_t h0 = nullptr, h1 = nullptr, o0 = nullptr, o1 = nullptr;
 };
 struct HostCall {
-  int mode;   // 0 sv, 1 diff, 2 merge, 3 snapshot
+  int mode;   // 0 sv, 1 diff, 2 merge, 3 snapshot, 4 contains (second arena in the sv slots)
   const uint8_t* arena; const uint64_t* off; const uint32_t* upd_doc; const uint8_t* sv_arena; const uint64_t* sv_off;
   uint32_t n_upd, n_docs;
 };
@@ -519,13 +555,14 @@ static void par_for(size_t n, F f) {
 
 // CPU copy of a chunk's inputs into the stage's pinned buffer, then the async H2D copies
 static int chunk_stage(ygm_ctx* k, const HostCall& H, Chunk& C) {
+  const bool two = H.mode == 1 || H.mode == 4;   // a second arena per document (diff: state vectors, contains: updates)
   const uint32_t nd = C.d1 - C.d0;
   const uint64_t a0 = H.mode == 2 ? H.off[C.u0] : H.off[C.d0], a1 = H.mode == 2 ? H.off[C.u1] : H.off[C.d1];
   const uint64_t bytes = a1 - a0, ab = (bytes + 64 + 15) & ~15ull;
   const uint32_t nu = H.mode == 2 ? C.u1 - C.u0 : nd;
   uint64_t s0 = 0, s1 = 0, sb = 0;
-  if (H.mode == 1) { s0 = H.sv_off[C.d0]; s1 = H.sv_off[C.d1]; sb = ((s1 - s0) + 64 + 15) & ~15ull; }
-  const uint64_t n_off = (uint64_t)nu + 1, n_doc = H.mode == 2 ? (uint64_t)nd + 1 : 0, n_sv = H.mode == 1 ? (uint64_t)nd + 1 : 0;
+  if (two) { s0 = H.sv_off[C.d0]; s1 = H.sv_off[C.d1]; sb = ((s1 - s0) + 64 + 15) & ~15ull; }
+  const uint64_t n_off = (uint64_t)nu + 1, n_doc = H.mode == 2 ? (uint64_t)nd + 1 : 0, n_sv = two ? (uint64_t)nd + 1 : 0;
   const uint64_t need = ab + 8 * n_off + sb + 8 * n_sv + 4 * n_doc + 64;
   if (!k->h_in.ensure(need)) return YGM_ENOMEM;
   uint8_t* P = k->h_in.as<uint8_t>();
@@ -534,7 +571,7 @@ static int chunk_stage(ygm_ctx* k, const HostCall& H, Chunk& C) {
   const uint64_t* src_off = H.mode == 2 ? H.off + C.u0 : H.off + C.d0;
   par_for(n_off, [=](size_t a, size_t b) { for (size_t j = a; j < b; j++) ro[j] = src_off[j] - a0; });
   uint8_t* q = P + ab + 8 * n_off;
-  if (H.mode == 1) {
+  if (two) {
     memcpy(q, H.sv_arena + s0, s1 - s0); memset(q + (s1 - s0), 0, sb - (s1 - s0));
     uint64_t* rs = (uint64_t*)(q + sb);
     for (uint64_t j = 0; j < n_sv; j++) rs[j] = H.sv_off[C.d0 + j] - s0;
@@ -546,13 +583,13 @@ static int chunk_stage(ygm_ctx* k, const HostCall& H, Chunk& C) {
     uint32_t u = C.u0;
     for (uint32_t d = 0; d < nd; d++) { while (u < C.u1 && H.upd_doc[u] == C.d0 + d) u++; du[d + 1] = u - C.u0; }
   }
-  if (!k->arena.ensure(ab) || !k->offs.ensure(8 * n_off) || (H.mode == 1 && (!k->sv_arena.ensure(sb) || !k->sv_offs.ensure(8 * n_sv))) ||
+  if (!k->arena.ensure(ab) || !k->offs.ensure(8 * n_off) || (two && (!k->sv_arena.ensure(sb) || !k->sv_offs.ensure(8 * n_sv))) ||
       (H.mode == 2 && !k->docs.ensure(4 * n_doc)))
     return YGM_ENOMEM;
   HIPCHK(hipEventRecord(C.h0, k->stream));
   HIPCHK(hipMemcpyAsync(k->arena.p, P, ab, hipMemcpyHostToDevice, k->stream));
   HIPCHK(hipMemcpyAsync(k->offs.p, ro, 8 * n_off, hipMemcpyHostToDevice, k->stream));
-  if (H.mode == 1) {
+  if (two) {
     HIPCHK(hipMemcpyAsync(k->sv_arena.p, P + ab + 8 * n_off, sb, hipMemcpyHostToDevice, k->stream));
     HIPCHK(hipMemcpyAsync(k->sv_offs.p, P + ab + 8 * n_off + sb, 8 * n_sv, hipMemcpyHostToDevice, k->stream));
   }
@@ -570,6 +607,8 @@ static int chunk_run(ygm_ctx* c, ygm_ctx* k, const HostCall& H, Chunk& C, uint64
   if (H.mode == 2) e = merge_enqueued ? ygm_merge_v1_device_finish(k, &dr)
                                       : ygm_merge_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->docs.as<uint32_t>(),
                                                             C.u1 - C.u0, nd, nullptr, &dr);
+  else if (H.mode == 4) e = ygm_contains_v1_device(k, k->arena.as<uint8_t>(), k->offs.as<uint64_t>(), k->sv_arena.as<uint8_t>(),
+                                                   k->sv_offs.as<uint64_t>(), nd, nullptr, &dr);
   else if (H.mode == 3) e = ygm_snapshot_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), nd, nullptr, &dr);
   else if (H.mode == 1) e = ygm_diff_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->sv_arena.as<uint8_t>(),
                                                k->sv_offs.as<uint64_t>(), nd, nullptr, &dr);
@@ -700,14 +739,19 @@ int ygm_merge_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* upd_off, cons
 static int host_doc_call(ygm_ctx* c, int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena,
                          const uint64_t* sv_off, uint32_t n_docs, ygm_result* out) {
   if (!c || !out || (n_docs && (!arena || !doc_off))) return YGM_EINVAL;
-  if (mode == 1 && n_docs && (!sv_arena || !sv_off)) return YGM_EINVAL;
+  if ((mode == 1 || mode == 4) && n_docs && (!sv_arena || !sv_off)) return YGM_EINVAL;
   for (uint32_t d = 0; d < n_docs; d++) {
     if (doc_off[d + 1] < doc_off[d]) return YGM_EINVAL;
-    if (mode == 1 && sv_off[d + 1] < sv_off[d]) return YGM_EINVAL;
+    if ((mode == 1 || mode == 4) && sv_off[d + 1] < sv_off[d]) return YGM_EINVAL;
   }
   static const uint64_t zero_off[1] = {0};
   HostCall H{mode, arena, n_docs ? doc_off : zero_off, nullptr, sv_arena, n_docs ? sv_off : zero_off, 0, n_docs};
   return host_call(c, H, out);
+}
+
+int ygm_contains_v1(ygm_ctx* c, const uint8_t* states, const uint64_t* state_off, const uint8_t* updates, const uint64_t* update_off,
+                    uint32_t n_docs, ygm_result* out) {
+  return host_doc_call(c, 4, states, state_off, updates, update_off, n_docs, out);
 }
 
 int ygm_snapshot_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, ygm_result* out) {

@@ -91,6 +91,99 @@ __global__ __launch_bounds__(SN_NT) void k_snap(const uint8_t* __restrict__ aren
   if ((threadIdx.x & (WAVE - 1)) == 0 && mine) atomicAdd(payload, (unsigned long long)mine);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Read-only SyncStep2 (MessageReceiver.ts:156-179): Y.snapshotContainsUpdate(Y.snapshot(doc), update),
+// restated from yjs 13.6 (snapshotContainsUpdateV2 -- not in the 13.5.16 bundle): every struct of the
+// update (Skips included, in order; the first one past the snapshot's state vector answers false) ends
+// at or below the state vector, and merging the update's delete set into the snapshot's leaves it equal.
+// The snapshot is given as the document's normalized state (ygm_snapshot_v1 output: its delete set is
+// createDeleteSetFromStructStore's, sorted and merged), so the second test is: every update range
+// [k, k + l) lies in one snapshot range [a, b) with a <= k and k + l <= b (sortAndMergeDeleteSet).
+struct CtSv { uint32_t client, end; };
+struct CtDs { uint32_t client, clock, end, pad; };
+__global__ __launch_bounds__(SN_NT) void k_cont_count(const uint8_t* __restrict__ st_arena, const uint64_t* __restrict__ st_off,
+                                                     uint32_t n_docs, uint32_t flags, uint64_t* __restrict__ need) {
+  const uint32_t d = blockIdx.x * SN_NT + threadIdx.x;
+  if (d >= n_docs) return;
+  const uint64_t a = st_off[d], b = st_off[d + 1];
+  uint32_t S = 0, D = 0, C = 0;
+  const uint32_t n = b > a && b - a < (1ull << 30) ? (uint32_t)(b - a) : 0u;
+  if (n) snap::count_doc(st_arena + a, n, flags, S, D, C);
+  need[d] = snap::al16((uint64_t)(C + 1) * sizeof(CtSv)) + snap::al16((uint64_t)(D + 1) * sizeof(CtDs));
+}
+YDEV_NI int contains_doc(const uint8_t* sp, uint32_t sn, const uint8_t* up, uint32_t un, uint32_t flags, uint8_t* ws, uint32_t& res) {
+  res = 0;
+  // the snapshot: state vector (clients of the blocks) and delete set
+  Cur c{sp, 0, sn, 0, 0};
+  const uint64_t nb = c.vu();
+  CtSv* sv = (CtSv*)ws;
+  uint32_t nsv = 0;
+  for (uint64_t b = 0; b < nb && !c.err; b++) {
+    const uint64_t ns = c.vu(), cl = c.vu(); uint64_t ck = c.vu();
+    for (uint64_t s = 0; s < ns && !c.err; s++) { SInfo si; read_struct(c, si, flags); ck += si.len; }
+    if (cl > 0xFFFFFFFFull || ck > 0xFFFFFFFFull) return snap::ST_UNSUP;
+    sv[nsv].client = (uint32_t)cl; sv[nsv].end = (uint32_t)ck; nsv++;
+  }
+  if (c.err) return c.err;
+  CtDs* ds = (CtDs*)(ws + snap::al16((uint64_t)(nsv + 1) * sizeof(CtSv)));
+  uint32_t nds = 0;
+  const uint64_t ndc = c.vu();
+  for (uint64_t q = 0; q < ndc && !c.err; q++) {
+    const uint64_t cl = c.vu(), nr = c.vu();
+    for (uint64_t r = 0; r < nr && !c.err; r++) {
+      const uint64_t ck = c.vu(), ln = c.vu();
+      if (cl > 0xFFFFFFFFull || ck + ln > 0xFFFFFFFFull) return snap::ST_UNSUP;
+      ds[nds].client = (uint32_t)cl; ds[nds].clock = (uint32_t)ck; ds[nds].end = (uint32_t)(ck + ln); nds++;
+    }
+  }
+  if (c.err) return c.err;
+  // the update: structs in order, then its delete set
+  Cur u{up, 0, un, 0, 0};
+  const uint64_t ub = u.vu();
+  for (uint64_t b = 0; b < ub && !u.err; b++) {
+    const uint64_t ns = u.vu(), cl = u.vu(); uint64_t ck = u.vu();
+    if (u.err) break;
+    uint64_t have = 0;
+    for (uint32_t i = 0; i < nsv; i++) if (sv[i].client == cl) have = sv[i].end;
+    for (uint64_t s = 0; s < ns && !u.err; s++) {
+      SInfo si; read_struct(u, si, flags);
+      if (u.err) break;
+      ck += si.len;
+      if (have < ck) return ST_OK;   // res = 0: a struct past the snapshot
+    }
+  }
+  if (u.err) return u.err;
+  const uint64_t udc = u.vu();
+  for (uint64_t q = 0; q < udc && !u.err; q++) {
+    const uint64_t cl = u.vu(), nr = u.vu();
+    for (uint64_t r = 0; r < nr && !u.err; r++) {
+      const uint64_t k = u.vu(), l = u.vu();
+      if (u.err) break;
+      bool cov = false;
+      for (uint32_t i = 0; i < nds && !cov; i++) cov = ds[i].client == cl && ds[i].clock <= k && k + l <= ds[i].end;
+      if (!cov) { res = 0; return ST_OK; }
+    }
+  }
+  if (u.err) return u.err;
+  res = 1;
+  return ST_OK;
+}
+__global__ __launch_bounds__(SN_NT) void k_cont(const uint8_t* __restrict__ st_arena, const uint64_t* __restrict__ st_off,
+                                               const uint8_t* __restrict__ up_arena, const uint64_t* __restrict__ up_off, uint32_t n_docs,
+                                               uint32_t flags, const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws,
+                                               uint8_t* __restrict__ out, uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len,
+                                               int32_t* __restrict__ status) {
+  const uint32_t d = blockIdx.x * SN_NT + threadIdx.x;
+  if (d >= n_docs) return;
+  const uint64_t a = st_off[d], b = st_off[d + 1], ua = up_off[d], ub = up_off[d + 1];
+  uint32_t res = 0;
+  int st;
+  if (b < a || ub < ua || b - a >= (1ull << 30) || ub - ua >= (1ull << 30)) st = ST_INVAL;
+  else st = contains_doc(st_arena + a, (uint32_t)(b - a), up_arena + ua, (uint32_t)(ub - ua), flags, ws + ws_off[d], res);
+  out[d] = (uint8_t)res;
+  out_off[d] = d; out_len[d] = st == ST_OK ? 1u : 0u; status[d] = st;
+}
+
 }  // namespace ygm
 
 using namespace ygm;
@@ -120,11 +213,32 @@ int ygm_k_launch_snap(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_
                       uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, hipStream_t s) {
   if (n_docs == 0) return 0;
   const char* env = getenv("YGM_SNAP_DPW");
-  uint32_t dpw = env ? (uint32_t)atoi(env) : 4u;
-  if (dpw < 1 || dpw > (uint32_t)SN_NT) dpw = 4u;
+  uint32_t dpw = env ? (uint32_t)atoi(env) : 16u;
+  if (dpw < 1 || dpw > (uint32_t)SN_NT) dpw = 16u;
   const uint32_t g = (n_docs + dpw - 1) / dpw;
   hipLaunchKernelGGL(k_snap, dim3(g), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, (const uint4*)cnt, ws_off, ws, out_off, out_len,
                      status, payload, dpw);
+  return snap_rc(__func__);
+}
+
+// read-only SyncStep2 containment: workspace plan (the snapshot scan), then one thread per document
+int ygm_k_launch_cont_plan(const uint8_t* st_arena, const uint64_t* st_off, uint32_t n_docs, uint32_t flags, uint64_t* ws_off, uint64_t* bs,
+                           hipStream_t s) {
+  if (n_docs == 0) return 0;
+  const uint32_t g = (n_docs + SN_NT - 1) / SN_NT, nb = (n_docs + 1 + 255) / 256;
+  hipLaunchKernelGGL(k_cont_count, dim3(g), dim3(SN_NT), 0, s, st_arena, st_off, n_docs, flags, ws_off);
+  hipLaunchKernelGGL(k_snap_scan_sum, dim3(nb), dim3(256), 0, s, (const uint64_t*)ws_off, n_docs, bs);
+  hipLaunchKernelGGL(k_snap_scan_top, dim3(1), dim3(1024), 0, s, bs, nb);
+  hipLaunchKernelGGL(k_snap_scan_apply, dim3(nb), dim3(256), 0, s, ws_off, n_docs, (const uint64_t*)bs);
+  return snap_rc(__func__);
+}
+int ygm_k_launch_cont(const uint8_t* st_arena, const uint64_t* st_off, const uint8_t* up_arena, const uint64_t* up_off, uint32_t n_docs,
+                      uint32_t flags, const uint64_t* ws_off, uint8_t* ws, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
+                      int32_t* status, hipStream_t s) {
+  if (n_docs == 0) return 0;
+  const uint32_t g = (n_docs + SN_NT - 1) / SN_NT;
+  hipLaunchKernelGGL(k_cont, dim3(g), dim3(SN_NT), 0, s, st_arena, st_off, up_arena, up_off, n_docs, flags, ws_off, ws, out, out_off, out_len,
+                     status);
   return snap_rc(__func__);
 }
 

@@ -64,7 +64,7 @@ _lib = None
 EXPORTS = ("ygm_open", "ygm_close", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_update_v1", "ygm_merge_v1_device",
            "ygm_merge_v1_device_async", "ygm_merge_v1_device_finish",
            "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_snapshot_v1", "ygm_snapshot_v1_device",
-           "ygm_stats", "ygm_strerror", "ygm_version")
+           "ygm_contains_v1", "ygm_contains_v1_device", "ygm_stats", "ygm_strerror", "ygm_version")
 
 
 def lib():
@@ -88,13 +88,16 @@ def lib():
         L.ygm_sv_from_update_v1_device.argtypes = [vp, vp, u64, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_snapshot_v1.argtypes = [vp, vp, vp, u32, ctypes.POINTER(_Result)]
         L.ygm_snapshot_v1_device.argtypes = [vp, vp, u64, vp, u32, vp, ctypes.POINTER(_DevResult)]
+        L.ygm_contains_v1.argtypes = [vp, vp, vp, vp, vp, u32, ctypes.POINTER(_Result)]
+        L.ygm_contains_v1_device.argtypes = [vp, vp, vp, vp, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.ygm_strerror.argtypes = [i32]
         L.ygm_strerror.restype = ctypes.c_char_p
         L.ygm_version.restype = ctypes.c_char_p
         for f in ("ygm_open", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_update_v1", "ygm_merge_v1_device",
                   "ygm_merge_v1_device_async", "ygm_merge_v1_device_finish",
-                  "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_snapshot_v1", "ygm_snapshot_v1_device", "ygm_stats"):
+                  "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_snapshot_v1", "ygm_snapshot_v1_device",
+                  "ygm_contains_v1", "ygm_contains_v1_device", "ygm_stats"):
             getattr(L, f).restype = i32
         _lib = L
     return _lib
@@ -268,6 +271,17 @@ class Engine:
         if st != OK:
             raise YjsError(st)
         return self._unpack(res)
+
+    def contains_batch(self, states, updates):
+        """Read-only SyncStep2: Y.snapshotContainsUpdate(Y.snapshot(doc), update) per pair, `states` being the
+        documents' normalized states (snapshot_batch) -> list of (status, bool | None)."""
+        sa, so = _pack([bytes(s) for s in states])
+        ua, uo = _pack([bytes(u) for u in updates])
+        res = _Result()
+        st = lib().ygm_contains_v1(self._ctx, sa or None, _ptr(so), ua or None, _ptr(uo), len(states), ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return [(s, None if s != OK else b == b"\x01") for s, b in self._unpack(res)]
 
     def snapshot_device(self, d_arena, arena_bytes, d_doc_off, n_docs, stream=0) -> "DeviceResult":
         r = _DevResult()

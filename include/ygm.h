@@ -114,6 +114,13 @@ int ygm_sv_from_update_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *do
  * encodeStateAsUpdate).  One update per document (e.g. the output of ygm_merge_v1).  Documents
  * outside the envelope carry YGM_EUNSUPPORTED. */
 int ygm_snapshot_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, uint32_t n_docs, ygm_result *out);
+/* Read-only SyncStep2: Y.snapshotContainsUpdate(Y.snapshot(doc), update) per document
+ * (packages/server/src/MessageReceiver.ts:156-179; yjs 13.6 snapshotContainsUpdate).  states: each
+ * document's doc-normalized state (ygm_snapshot_v1 output, whose delete set is the snapshot's);
+ * updates: the received update per document.  Document d's output is one byte, 1 = contained (the
+ * server acks with SyncStatus true), 0 = new content (SyncStatus false). */
+int ygm_contains_v1(ygm_ctx *ctx, const uint8_t *states, const uint64_t *state_off, const uint8_t *updates,
+                    const uint64_t *update_off, uint32_t n_docs, ygm_result *out);
 
 /* ---- device-resident API (inputs already in HBM; used by bench.py) --------
  * All pointers are device pointers.  doc_upd: n_docs+1 update-index offsets
@@ -164,6 +171,9 @@ int ygm_sv_from_update_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t 
 
 int ygm_snapshot_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
                            uint32_t n_docs, void *stream, ygm_device_result *out);
+
+int ygm_contains_v1_device(ygm_ctx *ctx, const uint8_t *d_states, const uint64_t *d_state_off, const uint8_t *d_updates,
+                           const uint64_t *d_update_off, uint32_t n_docs, void *stream, ygm_device_result *out);
 
 int ygm_stats(ygm_ctx *ctx, ygm_stats_t *out);
 const char *ygm_strerror(int code);

@@ -133,6 +133,7 @@ static void job_execute(napi_env env, void *data) {
   if (j->op == 0) j->rc = ygm_merge_v1(j->h->ctx, j->arena, j->off, j->docs, j->n_upd, j->n_docs, &r);
   else if (j->op == 1) j->rc = ygm_diff_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
   else if (j->op == 3) j->rc = ygm_snapshot_v1(j->h->ctx, j->arena, j->off, j->n_docs, &r);
+  else if (j->op == 4) j->rc = ygm_contains_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
   else j->rc = ygm_sv_from_update_v1(j->h->ctx, j->arena, j->off, j->n_docs, &r);
   if (j->rc != YGM_OK) return;
   /* results are context-owned: copy out before the next batch may reuse them */
@@ -259,6 +260,27 @@ static napi_value js_sv(napi_env env, napi_callback_info info) {
   return submit(env, j, "ygm.svMany");
 }
 
+/* containsMany(h, states, stateLens, updates, updateLens): snapshotContainsUpdate per pair (1 byte) */
+static napi_value js_contains(napi_env env, napi_callback_info info) {
+  size_t argc = 5; napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 5) { napi_throw_type_error(env, NULL, "containsMany(handle, states, lens, updates, lens)"); return NULL; }
+  Handle *h = get_handle(env, argv[0]);
+  if (!h) return NULL;
+  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = 4; j->h = h;
+  size_t an, ln, sn, sln; void *lens = NULL, *slens = NULL;
+  if (get_bytes(env, argv[1], (void **)&j->arena, &an) || get_bytes(env, argv[2], &lens, &ln) || get_bytes(env, argv[3], (void **)&j->sv, &sn) ||
+      get_bytes(env, argv[4], &slens, &sln) || ln != sln) {
+    free(lens); free(slens); job_free(j); napi_throw_type_error(env, NULL, "containsMany: bad arguments"); return NULL;
+  }
+  j->n_docs = (uint32_t)(ln / 4);
+  j->off = lens_to_off((const uint32_t *)lens, j->n_docs);
+  j->sv_off = lens_to_off((const uint32_t *)slens, j->n_docs);
+  free(lens); free(slens);
+  if (j->off[j->n_docs] != an || j->sv_off[j->n_docs] != sn) { job_free(j); napi_throw_range_error(env, NULL, "containsMany: lengths do not match arenas"); return NULL; }
+  return submit(env, j, "ygm.containsMany");
+}
+
 /* snapshotMany(h, arena, lens): Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), u)) per update */
 static napi_value js_snapshot(napi_env env, napi_callback_info info) {
   size_t argc = 3; napi_value argv[3];
@@ -286,6 +308,7 @@ static napi_value init(napi_env env, napi_value exports) {
     { "diffMany", NULL, js_diff, NULL, NULL, NULL, napi_default, NULL },
     { "svMany", NULL, js_sv, NULL, NULL, NULL, napi_default, NULL },
     { "snapshotMany", NULL, js_snapshot, NULL, NULL, NULL, napi_default, NULL },
+    { "containsMany", NULL, js_contains, NULL, NULL, NULL, napi_default, NULL },
     { "stats", NULL, js_stats, NULL, NULL, NULL, napi_default, NULL },
     { "strerror", NULL, js_strerror, NULL, NULL, NULL, napi_default, NULL },
   };

@@ -3,7 +3,7 @@ import type { Extension, fetchPayload, storePayload, onLoadDocumentPayload, afte
   onChangePayload, onStoreDocumentPayload, afterUnloadDocumentPayload } from '@hocuspocus/server'
 
 export declare class YgmError extends Error {
-  code: 'EMALFORMED' | 'ERANGE' | 'ENONCANON' | 'ESURROGATE' | 'EDEPTH' | 'ENOMEM' | 'EDEVICE' | 'EINVAL' | string
+  code: 'EMALFORMED' | 'ERANGE' | 'ENONCANON' | 'ESURROGATE' | 'EDEPTH' | 'ENOMEM' | 'EDEVICE' | 'EINVAL' | 'EUNSUPPORTED' | string
   status: number
 }
 
@@ -17,6 +17,11 @@ export declare class GpuEngine {
   mergeMany (docs: Uint8Array[][]): Promise<(Uint8Array | YgmError)[]>
   diffMany (states: Uint8Array[], svs: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
   stateVectorsMany (states: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  /** Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), update)) (doc-normalized snapshot, SURVEY.md §8f-1) */
+  snapshot (update: Uint8Array): Promise<Uint8Array>
+  snapshotMany (states: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  /** Y.snapshotContainsUpdate(Y.snapshot(doc), update), states being normalized (snapshotMany) states */
+  containsMany (states: Uint8Array[], updates: Uint8Array[]): Promise<(boolean | YgmError)[]>
   stats (): Record<string, number>
   close (): void
 }
@@ -35,6 +40,9 @@ export declare class GpuEnginePool {
   mergeMany (names: string[], docs: Uint8Array[][]): Promise<(Uint8Array | YgmError)[]>
   diffMany (names: string[], states: Uint8Array[], svs: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
   stateVectorsMany (names: string[], states: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  snapshot (update: Uint8Array, documentName?: string): Promise<Uint8Array>
+  snapshotMany (names: string[], states: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  containsMany (names: string[], states: Uint8Array[], updates: Uint8Array[]): Promise<(boolean | YgmError)[]>
   stats (): Record<string, number>[]
   close (): void
 }
@@ -44,6 +52,20 @@ export declare class SyncResponder {
   constructor (opts: { engine: GpuEngine | GpuEnginePool, getState: (documentName: string) => Promise<Uint8Array | Uint8Array[] | null> })
   /** per message: [Step2 reply, server Step1] for SyncStep1, null for other messages, an Error if malformed */
   answerMany (messages: Uint8Array[], opts?: { path?: 'connection' | 'reply' | 'none' }): Promise<(Uint8Array[] | Error | null)[]>
+  /** read-only connections' SyncStep2 (MessageReceiver.ts:156-179): the SyncStatus(contained) frame per message */
+  answerReadOnlyMany (messages: Uint8Array[]): Promise<(Uint8Array | Error | null)[]>
+}
+
+/** Batched Redis fan-out (SURVEY.md §8f-3; src/redis.js): extension-redis's per-change Step1 publishes and
+ * remote SyncStep1 replies as GPU batches, with the reference's channel names and message framing. */
+export declare class RedisFanout {
+  constructor (opts: { engine: GpuEngine | GpuEnginePool, getState: (documentName: string) => Promise<Uint8Array | Uint8Array[] | null>,
+    publish: (channel: string, message: Buffer) => any, identifier?: string, prefix?: string, windowMs?: number })
+  identifier: string
+  redisTransactionOrigin: string
+  onChange (data: { documentName: string, transactionOrigin?: any }): Promise<void>
+  /** null for own messages; answers SyncStep1 (replies published); otherwise the message for the host to apply */
+  handleIncomingMessage (channel: string | Buffer, data: Buffer): Promise<null | { documentName: string | null, message?: Buffer, replied?: number }>
 }
 
 export declare class DocumentStore {
@@ -61,6 +83,10 @@ export interface GpuMergeConfiguration extends GpuEngineOptions {
   priority?: number
   engine?: GpuEngine
   Y?: any
+  /** a refused merge: store Y.encodeStateAsUpdate(document) ('reference', default) or reject the store ('throw') */
+  onRefused?: 'reference' | 'throw'
+  /** store the GPU doc-normalized snapshot of the merge (GC'd, merged: the shape extension-database stores) */
+  normalize?: boolean
 }
 
 export declare class GpuMerge implements Extension {

@@ -105,9 +105,9 @@ class GpuEngine {
         const { arena, lens } = packBlobs(blobs)
         return a.mergeMany(this.handle, arena, lens, Uint32Array.from(docs), jobs.length)
       }
-      if (op === 'diff') {
+      if (op === 'diff' || op === 'contains') {
         const u = packBlobs(jobs.map(j => j[0])); const s = packBlobs(jobs.map(j => j[1]))
-        return a.diffMany(this.handle, u.arena, u.lens, s.arena, s.lens)
+        return (op === 'diff' ? a.diffMany : a.containsMany)(this.handle, u.arena, u.lens, s.arena, s.lens)
       }
       const u = packBlobs(jobs)
       if (op === 'snapshot') return a.snapshotMany(this.handle, u.arena, u.lens)
@@ -132,6 +132,11 @@ class GpuEngine {
   async diffMany (states, svs) { const r = await this._run('diff', states.map((s, i) => [s, svs[i]])); return unpack(r) }
   async stateVectorsMany (states) { const r = await this._run('sv', states); return unpack(r) }
   async snapshotMany (states) { const r = await this._run('snapshot', states); return unpack(r) }
+  /** Y.snapshotContainsUpdate(Y.snapshot(doc), update) per pair, `states` being normalized (snapshotMany) states */
+  async containsMany (states, updates) {
+    const r = await this._run('contains', states.map((s, i) => [s, updates[i]]))
+    return unpack(r).map(x => x instanceof Error ? x : x[0] === 1)
+  }
 
   stats () { return loadAddon().stats(this.handle) }
   close () { if (this.handle) { loadAddon().close(this.handle); this.handle = null } }
@@ -188,6 +193,7 @@ class GpuEnginePool {
   diffMany (names, states, svs) { return this._many(names, [states, svs], (e, a, b) => e.diffMany(a, b)) }
   stateVectorsMany (names, states) { return this._many(names, [states], (e, a) => e.stateVectorsMany(a)) }
   snapshotMany (names, states) { return this._many(names, [states], (e, a) => e.snapshotMany(a)) }
+  containsMany (names, states, updates) { return this._many(names, [states, updates], (e, a, b) => e.containsMany(a, b)) }
   stats () { return this.engines.map(e => e.stats()) }
   close () { this.engines.forEach(e => e.close()) }
 }

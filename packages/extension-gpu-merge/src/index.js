@@ -17,6 +17,7 @@
  */
 const { GpuEngine, GpuEnginePool, fnv1a64, YgmError } = require('./engine')
 const { SyncResponder } = require('./sync')
+const { RedisFanout } = require('./redis')
 
 /**
  * A batched document store.  `fromDatabase` adapts any DatabaseConfiguration
@@ -197,4 +198,4 @@ async function addsToBase (engine, missing, base, name) {
   return Buffer.compare(Buffer.from(withIt), Buffer.from(without)) !== 0
 }
 
-module.exports = { GpuMerge, DocumentStore, GpuEngine, GpuEnginePool, SyncResponder, fnv1a64, YgmError }
+module.exports = { GpuMerge, DocumentStore, GpuEngine, GpuEnginePool, SyncResponder, RedisFanout, fnv1a64, YgmError }

@@ -134,4 +134,42 @@ class SyncResponder {
   }
 }
 
-module.exports = { SyncResponder, decodeSyncMessage, frame, MessageType, SyncStep }
+// [varString(documentName) varUint(SyncStatus = 8) varUint(saved ? 1 : 0)] (OutgoingMessage.ts:128-135)
+function syncStatusFrame (documentName, saved) {
+  const name = Buffer.from(documentName, 'utf8')
+  return Uint8Array.from([...varUintBytes(name.length), ...name, 8, saved ? 1 : 0])
+}
+
+/**
+ * Read-only connections (MessageReceiver.ts:156-179): a SyncStep2 from a read-only client is not
+ * applied; the server acks SyncStatus(true) when Y.snapshotContainsUpdate(Y.snapshot(doc), update)
+ * (nothing new) and SyncStatus(false) otherwise.  Batched: the documents' states merged and
+ * snapshot-normalized on the GPU (the snapshot's delete set is the document's), then one GPU
+ * containment batch.  Returns per message the SyncStatus frame, null for other messages, or an Error.
+ */
+SyncResponder.prototype.answerReadOnlyMany = async function (messages) {
+  const out = new Array(messages.length).fill(null)
+  const asks = []
+  messages.forEach((m, i) => {
+    try {
+      const d = decodeSyncMessage(m)
+      if (d && d.step === SyncStep.Step2) asks.push({ i, ...d })
+    } catch (e) { out[i] = e }
+  })
+  if (!asks.length) return out
+  const names = Array.from(new Set(asks.map(a => a.documentName)))
+  const fetched = await Promise.all(names.map(n => this.getState(n)))
+  const parts = fetched.map(f => Array.isArray(f) ? f.filter(Boolean) : (f ? [f] : []))
+  const merged = await this._merge(names, parts.map(p => p.length ? p : [new Uint8Array([0, 0])]))
+  const snaps = await (this._pooled() ? this.engine.snapshotMany(names, merged) : this.engine.snapshotMany(merged))
+  const snapOf = new Map(names.map((n, k) => [n, snaps[k]]))
+  const live = asks.filter(a => !(snapOf.get(a.documentName) instanceof Error))
+  asks.filter(a => snapOf.get(a.documentName) instanceof Error).forEach(a => { out[a.i] = snapOf.get(a.documentName) })
+  const res = await (this._pooled()
+    ? this.engine.containsMany(live.map(a => a.documentName), live.map(a => snapOf.get(a.documentName)), live.map(a => a.payload))
+    : this.engine.containsMany(live.map(a => snapOf.get(a.documentName)), live.map(a => a.payload)))
+  live.forEach((a, k) => { out[a.i] = res[k] instanceof Error ? res[k] : syncStatusFrame(a.documentName, res[k]) })
+  return out
+}
+
+module.exports = { SyncResponder, decodeSyncMessage, frame, syncStatusFrame, MessageType, SyncStep }

@@ -7,7 +7,8 @@
 const path = require('path')
 const assert = require('assert')
 const { GpuMerge, GpuEnginePool, fnv1a64 } = require('../src/index.js')
-const { frame, decodeSyncMessage, MessageType, SyncStep } = require('../src/sync.js')
+const { frame, decodeSyncMessage, MessageType, SyncStep, SyncResponder } = require('../src/sync.js')
+const { RedisFanout } = require('../src/redis.js')
 const { MiniHocuspocus } = require('./harness.js')
 
 const mode = process.argv.includes('--gpu') ? 'gpu' : 'cpu'
@@ -20,6 +21,14 @@ class CpuDouble { // test double (never shipped): same API as GpuEngine
   async diffMany (states, svs) { this.calls++; return states.map((u, i) => Y.diffUpdate(u, svs[i])) }
   async stateVectorsMany (states) { this.calls++; return states.map(u => Y.encodeStateVectorFromUpdate(u)) }
   async snapshot (u) { this.calls++; const d = new Y.Doc(); Y.applyUpdate(d, u); return Y.encodeStateAsUpdate(d) }
+  async snapshotMany (states) { this.calls++; return states.map(u => { const d = new Y.Doc(); Y.applyUpdate(d, u); return Y.encodeStateAsUpdate(d) }) }
+  async containsMany (states, updates) {
+    this.calls++
+    return states.map((s, i) => {
+      const d = new Y.Doc(); Y.applyUpdate(d, s); const p = new Y.Doc(); Y.applyUpdate(p, s); Y.applyUpdate(p, updates[i])
+      return Y.equalSnapshots(Y.snapshot(d), Y.snapshot(p))
+    })
+  }
   close () {}
 }
 
@@ -206,6 +215,74 @@ test('normalize stores the doc-normalized snapshot of the merge', async (engine)
   const back = new Y.Doc(); Y.applyUpdate(back, stored)
   assert.strictEqual(back.getText('t').toString(), t.toString())
   assert.deepStrictEqual(ext.unnormalized, [])
+})
+
+// SURVEY.md §8f-3 (Redis.ts:210-219, 336-372): changes publish Step1 in one batch; a remote instance's
+// SyncStep1 is answered (SyncReply Step1 + Step2) in one batch, published back on the document channel
+test('redis fan-out: batched first sync steps and remote Step2 replies', async (engine) => {
+  const bus = []   // published [channel, buffer]
+  const docs = new Map()
+  const names = Array.from({ length: 12 }, (_, i) => `r-${i}`)
+  for (const n of names) {
+    const d = new Y.Doc(); d.clientID = 100 + docs.size
+    d.getText('t').insert(0, 'hello ' + n)
+    docs.set(n, d)
+  }
+  const getState = async n => Y.encodeStateAsUpdate(docs.get(n))
+  const A = new RedisFanout({ engine, getState, publish: async (c, m) => bus.push([c, m]), identifier: 'host-A' })
+  await Promise.all(names.map(n => A.onChange({ documentName: n, document: docs.get(n), transactionOrigin: 'connection' })))
+  assert.strictEqual(A.batches.step1, 1)
+  assert.strictEqual(bus.length, names.length)
+  for (const [channel, buf] of bus) {
+    const [id, msg] = A.decodeMessage(buf)
+    assert.strictEqual(id, 'host-A')
+    const d = decodeSyncMessage(msg)
+    assert.strictEqual(channel, `hocuspocus:${d.documentName}`)
+    assert.strictEqual(d.step, SyncStep.Step1)
+    assert.deepStrictEqual(Array.from(Y.decodeStateVector(d.payload)), Array.from(Y.decodeStateVector(Y.encodeStateVector(docs.get(d.documentName)))))
+  }
+  // Redis-origin changes publish nothing; own messages are ignored
+  await A.onChange({ documentName: names[0], transactionOrigin: A.redisTransactionOrigin })
+  assert.strictEqual(bus.length, names.length)
+  assert.strictEqual(await A.handleIncomingMessage('x', bus[0][1]), null)
+  // instance B holds newer content and answers A's Step1 messages
+  const bdocs = new Map(names.map(n => { const d = new Y.Doc(); Y.applyUpdate(d, Y.encodeStateAsUpdate(docs.get(n))); d.clientID = 900; d.getText('t').insert(0, 'B:'); return [n, d] }))
+  const back = []
+  const B = new RedisFanout({ engine, getState: async n => Y.encodeStateAsUpdate(bdocs.get(n)), publish: async (c, m) => back.push([c, m]), identifier: 'host-B' })
+  const res = await Promise.all(bus.map(([c, m]) => B.handleIncomingMessage(c, m)))
+  assert.strictEqual(B.batches.replies, 1)
+  assert.ok(res.every(r => r.replied === 2))
+  assert.strictEqual(back.length, 2 * names.length)
+  for (let k = 0; k < names.length; k++) {
+    const [, m1] = B.decodeMessage(back[2 * k][1]); const [, m2] = B.decodeMessage(back[2 * k + 1][1])
+    const s1 = decodeSyncMessage(m1); const s2 = decodeSyncMessage(m2)
+    assert.strictEqual(s1.messageType, MessageType.SyncReply); assert.strictEqual(s1.step, SyncStep.Step1)
+    assert.strictEqual(s2.step, SyncStep.Step2)
+    const sv = decodeSyncMessage(A.decodeMessage(bus[k][1])[1]).payload
+    assert.strictEqual(Buffer.compare(Buffer.from(s2.payload), Buffer.from(Y.diffUpdate(Y.encodeStateAsUpdate(bdocs.get(s2.documentName)), sv))), 0)
+    // A applies B's Step2 (what the host's MessageReceiver does with the returned message)
+    const got = await A.handleIncomingMessage('x', back[2 * k + 1][1])
+    Y.applyUpdate(docs.get(got.documentName), decodeSyncMessage(got.message).payload)
+    assert.strictEqual(docs.get(got.documentName).getText('t').toString(), bdocs.get(got.documentName).getText('t').toString())
+  }
+})
+
+// MessageReceiver.ts:156-179: a read-only client's SyncStep2 is acked SyncStatus(true) when the document
+// already contains it (Y.snapshotContainsUpdate), SyncStatus(false) otherwise -- one batch
+test('read-only SyncStep2 acks through snapshotContainsUpdate, batched', async (engine) => {
+  const doc = new Y.Doc(); doc.clientID = 5
+  doc.getText('t').insert(0, 'abcdef'); doc.getText('t').delete(1, 2)
+  const state = Y.encodeStateAsUpdate(doc)
+  const peer = new Y.Doc(); Y.applyUpdate(peer, state); peer.clientID = 6
+  const old = Y.encodeStateAsUpdate(doc)
+  const grab = []; peer.on('update', u => grab.push(u))
+  peer.getText('t').insert(0, 'new')
+  const r = new SyncResponder({ engine, getState: async () => state })
+  const msgs = [frame('ro', MessageType.Sync, SyncStep.Step2, old), frame('ro', MessageType.Sync, SyncStep.Step2, grab[0]), frame('ro', MessageType.Sync, SyncStep.Step1, Y.encodeStateVector(doc))]
+  const out = await r.answerReadOnlyMany(msgs)
+  assert.deepStrictEqual(Array.from(out[0]), [2, 0x72, 0x6f, 8, 1])
+  assert.deepStrictEqual(Array.from(out[1]), [2, 0x72, 0x6f, 8, 0])
+  assert.strictEqual(out[2], null)
 })
 
 test('engine pool shards by fnv1a64(name) and keeps caller order', async () => {

@@ -145,3 +145,44 @@ def test_gpu_snapshot_envelope():
         orphan = bytes([1, 1, 5, 0, 0x84, 9, 0, 1, 0x61, 0])   # origin (9, 0) is not in the update
         res = e.snapshot_batch([gap, orphan, b""])
         assert res[0][0] == EUNSUPPORTED and res[1][0] == EUNSUPPORTED and res[2][0] == EMALFORMED
+
+
+# ---------------------------------------------------------------------------------------- read-only SyncStep2
+CFIX = os.path.join(ROOT, "tests", "golden", "contains_v135.json.gz")
+
+
+def contains_fixtures():
+    d = json.load(gzip.open(CFIX, "rt"))
+    states = [bytes.fromhex(s) for s in d["states"]]
+    return [(states[i], bytes.fromhex(u), bool(e)) for i, u, e in d["rows"]]
+
+
+def test_contains_fixtures_present():
+    rows = contains_fixtures()
+    assert len(rows) > 300 and 0 < sum(e for _, _, e in rows) < len(rows)
+
+
+@pytest.mark.gpu
+def test_gpu_contains_vs_yjs_fixtures():
+    """Y.snapshotContainsUpdate(Y.snapshot(doc), update) (MessageReceiver.ts:156-179) on the GPU."""
+    from hocuspocus_amd import Engine
+    rows = contains_fixtures()
+    with Engine(0) as e:
+        res = e.contains_batch([s for s, _, _ in rows], [u for _, u, _ in rows])
+    assert res == [(0, x) for _, _, x in rows]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not (NODE and BUNDLE), reason="node + the yjs bundle (image) needed")
+def test_gpu_contains_vs_live_yjs(tmp_path):
+    from hocuspocus_amd import Engine
+    a, b, c = str(tmp_path / "st.bin"), str(tmp_path / "up.bin"), str(tmp_path / "ex.bin")
+    subprocess.run([NODE, os.path.join(ROOT, "tools", "contains_corpus.js"), "150", "77", a, b, c], check=True, timeout=240)
+    st, up, ex = read_in(a), read_in(b), list(open(c, "rb").read())
+    with Engine(0) as e:
+        res = e.contains_batch(st, up)
+        # the GPU's own normalized states answer the same
+        snaps = e.snapshot_batch(st)
+        res2 = e.contains_batch([s for _, s in snaps], up)
+    assert res == [(0, bool(x)) for x in ex]
+    assert res2 == res

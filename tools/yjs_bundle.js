@@ -9,7 +9,9 @@ const STATIC = process.env.YJS_BUNDLE_DIR || '/opt/conda/share/jupyter/lab/stati
 const CHUNKS = ['3502.fbe0c610be82ba1360db.js', '8086.1dfabaac37d971e2cc4c.js', '1057.1a1aee857cdaddbae1d3.js']
 const YJS_MODULE_ID = 73502
 
+let cached = null
 function load () {
+  if (cached) return cached   // one evaluation per process (a second one finds the chunk registry consumed)
   const modules = {}
   global.self = global
   global.window = undefined
@@ -28,7 +30,8 @@ function load () {
   req.n = m => { const g = m && m.__esModule ? () => m.default : () => m; req.d(g, { a: g }); return g }
   req.o = (o, p) => Object.prototype.hasOwnProperty.call(o, p)
   req.g = global
-  return req(YJS_MODULE_ID)
+  cached = req(YJS_MODULE_ID)
+  return cached
 }
 
 module.exports = { load, STATIC, present: () => require('fs').existsSync(path.join(STATIC, CHUNKS[0])) }

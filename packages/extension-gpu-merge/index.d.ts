@@ -102,4 +102,6 @@ export declare class GpuMerge implements Extension {
   onDestroy (): Promise<void>
   /** batched SyncStep1 responder over the captured state (snapshot + updates since) */
   syncResponder (): SyncResponder
+  /** batched extension-redis fan-out over the same captured state */
+  redisFanout (opts: { publish: (channel: string, message: Buffer) => any, identifier?: string, prefix?: string, windowMs?: number }): RedisFanout
 }

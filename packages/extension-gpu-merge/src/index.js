@@ -92,6 +92,11 @@ class GpuMerge {
     })
   }
 
+  /** Batched extension-redis fan-out over the same captured state (SURVEY.md §8f-3, src/redis.js) */
+  redisFanout ({ publish, identifier, prefix, windowMs }) {
+    return new RedisFanout({ engine: this._engine(), getState: this.syncResponder().getState, publish, identifier, prefix, windowMs })
+  }
+
   async onConfigure () { this._engine() }
 
   /** fetch -> (GPU merge of snapshot + log rows) -> Y.applyUpdate, as Database.onLoadDocument (Database.ts:44-50) */

@@ -267,6 +267,22 @@ test('redis fan-out: batched first sync steps and remote Step2 replies', async (
   }
 })
 
+// GpuMerge.redisFanout: the fan-out reads the extension's captured state (stored base + updates since)
+test('redis fan-out over GpuMerge captured state', async (engine) => {
+  const db = memoryDb()
+  const ext = new GpuMerge({ ...db, Y, engine })
+  const hp = new MiniHocuspocus({ extensions: [ext], Y })
+  const doc = await hp.loadDocument('rf')
+  doc.transact(() => doc.getText('t').insert(0, 'captured'), 'c1')
+  const bus = []
+  const fan = ext.redisFanout({ publish: async (c, m) => bus.push([c, m]), identifier: 'host-X', prefix: 'pfx' })
+  await fan.onChange({ documentName: 'rf', transactionOrigin: 'c1' })
+  assert.strictEqual(bus.length, 1)
+  assert.strictEqual(bus[0][0], 'pfx:rf')
+  const d = decodeSyncMessage(fan.decodeMessage(bus[0][1])[1])
+  assert.deepStrictEqual(Array.from(Y.decodeStateVector(d.payload)), Array.from(Y.decodeStateVector(Y.encodeStateVector(doc))))
+})
+
 // MessageReceiver.ts:156-179: a read-only client's SyncStep2 is acked SyncStatus(true) when the document
 // already contains it (Y.snapshotContainsUpdate), SyncStatus(false) otherwise -- one batch
 test('read-only SyncStep2 acks through snapshotContainsUpdate, batched', async (engine) => {

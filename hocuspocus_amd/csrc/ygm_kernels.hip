@@ -1626,89 +1626,106 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
     if (l == 0) status[d] = (int)bad; wave_sync(); continue;
 #endif
     if (!defer) {
-      // ---- clients: distinct values by wave vote (<= 4), ranked descending
-      uint32_t bid[LN_ROWS];
+      // ---- clients, discovered in descending order (wave max over the unassigned records): a
+      //      record's block is its client's rank; lane c of `ctl` holds block c's client
+      uint32_t blk[LN_ROWS];
 #pragma unroll
-      for (int q = 0; q < LN_ROWS; q++) bid[q] = hs[q] ? 0xFFu : 0xFEu;
-      uint32_t cl0 = 0, cl1 = 0, cl2 = 0, cl3 = 0, nC = 0;
-      for (int it = 0; it < 5; it++) {
-        uint32_t cand = 0; bool found = false;
+      for (int q = 0; q < LN_ROWS; q++) blk[q] = hs[q] ? 0xFFu : 0xFEu;
+      uint32_t ctl = 0, nC = 0;
+      for (int it = 0; it <= LN_CMAX; it++) {
+        uint32_t mx = 0; bool any = false;
 #pragma unroll
-        for (int q = 0; q < LN_ROWS; q++) {
-          const uint64_t m = __ballot(bid[q] == 0xFFu);
-          if (!found && m) { cand = rdlane(rec[q].client, (uint32_t)__builtin_ctzll(m)); found = true; }
-        }
-        if (!found) break;
-        if (nC == 4) { defer = true; break; }
+        for (int q = 0; q < LN_ROWS; q++) { const bool un_ = blk[q] == 0xFFu; any |= un_; mx = max(mx, un_ ? rec[q].client : 0u); }
+        if (__ballot(any) == 0) break;
+        if (nC == (uint32_t)LN_CMAX) { defer = true; break; }
+        const uint32_t cand = lane63(dpp_incl_max(mx));
 #pragma unroll
-        for (int q = 0; q < LN_ROWS; q++) if (bid[q] == 0xFFu && rec[q].client == cand) bid[q] = nC;
-        if (nC == 0) cl0 = cand; else if (nC == 1) cl1 = cand; else if (nC == 2) cl2 = cand; else cl3 = cand;
+        for (int q = 0; q < LN_ROWS; q++) if (blk[q] == 0xFFu && rec[q].client == cand) blk[q] = nC;
+        ctl = l == nC ? cand : ctl;
         nC++;
       }
       if (!defer) {
-        // rank (descending client) of each discovery id; ctab = clients by rank
-        const uint32_t cls[4] = {cl0, cl1, cl2, cl3};
-        uint32_t rk[4], ctab[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int a = 0; a < 4; a++) {
-          uint32_t r = 0;
-#pragma unroll
-          for (int b = 0; b < 4; b++) r += ((uint32_t)b < nC && cls[b] > cls[a]) ? 1u : 0u;
-          rk[a] = r;
-        }
-#pragma unroll
-        for (int a = 0; a < 4; a++) if ((uint32_t)a < nC) { if (rk[a] == 0) ctab[0] = cls[a]; else if (rk[a] == 1) ctab[1] = cls[a]; else if (rk[a] == 2) ctab[2] = cls[a]; else ctab[3] = cls[a]; }
-        // ---- per-row DPP scans of packed per-block fields: record index in its block (8-bit
-        //      fields, k <= 255) and byte offset in its block (16-bit fields)
-        uint32_t runc = 0, run0 = 0, run1 = 0, nst0 = 0, nst1 = 0;
-        uint32_t blk[LN_ROWS], inb[LN_ROWS], idx[LN_ROWS];
+        // ---- record index inside its block: per-row DPP scans of packed 8-bit per-block counts (k <= 255)
+        uint32_t cA = 0, cB = 0;
+        uint32_t idx[LN_ROWS];
 #pragma unroll
         for (int q = 0; q < LN_ROWS; q++) {
-          const bool valid = hs[q];
-          const uint32_t id = bid[q] & 3u;
-          const uint32_t b = valid ? (id == 0 ? rk[0] : id == 1 ? rk[1] : id == 2 ? rk[2] : rk[3]) : 7u;
-          blk[q] = b;
-          const uint32_t sb = valid ? (rec[q].span & 0xFFu) : 0u, ns = valid ? ((rec[q].span >> 8) & 0xFFu) : 0u;
-          const uint32_t pc = valid ? 1u << (8u * b) : 0u;
-          const uint32_t ic = dpp_incl_add(pc);
-          idx[q] = ((runc + ic - pc) >> (8u * (b & 3u))) & 0xFFu;
-          runc += lane63(ic);
-          const uint32_t fs = (b & 1u) ? 16u : 0u;
-          const uint32_t p0 = b < 2u ? sb << fs : 0u, p1 = (b >= 2u && b < 4u) ? sb << fs : 0u;
-          nst0 += b < 2u ? ns << fs : 0u; nst1 += (b >= 2u && b < 4u) ? ns << fs : 0u;
-          const uint32_t i0 = dpp_incl_add(p0), i1 = dpp_incl_add(p1);
-          const uint32_t w = b < 2u ? run0 + i0 - p0 : run1 + i1 - p1;
-          inb[q] = (w >> fs) & 0xFFFFu;
-          run0 += lane63(i0); run1 += lane63(i1);
+          const uint32_t b = hs[q] ? blk[q] : 0u;
+          const uint32_t sh = 8u * (b & 3u);
+          const uint32_t pa = (hs[q] && b < 4u) ? 1u << sh : 0u;
+          const uint32_t ia = dpp_incl_add(pa);
+          uint32_t w = cA + ia - pa;
+          cA += lane63(ia);
+          if (nC > 4u) {
+            const uint32_t pb = (hs[q] && b >= 4u) ? 1u << sh : 0u;
+            const uint32_t ib = dpp_incl_add(pb);
+            w = b < 4u ? w : cB + ib - pb;
+            cB += lane63(ib);
+          }
+          idx[q] = (w >> sh) & 0xFFu;
         }
-        // ---- contiguity (rule R-M without gaps/overlaps): every record's clock is the end of the
-        //      previous record of its block.  (clock, end) pairs are scattered to their sorted slot in
-        //      the output buffer (free until the emit) and each record reads its predecessor.
-        const uint32_t rcnt[4] = {runc & 0xFFu, (runc >> 8) & 0xFFu, (runc >> 16) & 0xFFu, runc >> 24};
-        const uint32_t rbase[4] = {0u, rcnt[0], rcnt[0] + rcnt[1], rcnt[0] + rcnt[1] + rcnt[2]};
-        LB32* scr = (LB32*)lout;
+        // exclusive per-block record bases, packed 8-bit (blocks 0-3 / 4-7): the prefix sum of the
+        // packed counts by byte (x * 0x01010100 adds every lower byte into the higher ones)
+        const uint32_t RB0 = cA * 0x01010100u;
+        const uint32_t tot0 = (RB0 >> 24) + (cA >> 24);
+        const uint32_t RB1 = cB * 0x01010100u + tot0 * 0x01010101u;
+        const uint32_t nrec = (RB1 >> 24) + (cB >> 24);
+        // ---- records scattered to their sorted slot (block, log order): clock, end, packed source
+        //      (staged position << 16 | block << 13 | structs << 5 | struct bytes)
+        LB32* Sck = (LB32*)lout;
+        LB32* Sen = Sck + WAVE * LN_ROWS;
+        LB32* Ssp = Sen + WAVE * LN_ROWS;
+        LB32* Sbs = Ssp + WAVE * LN_ROWS;   // per block: packed (structs, bytes) before its first record; first clock
+        LB32* Sfc = Sbs + LN_CMAX;
 #pragma unroll
         for (int q = 0; q < LN_ROWS; q++) {
           if (hs[q]) {
             const uint32_t b = blk[q];
-            const uint32_t j = (b == 0 ? rbase[0] : b == 1 ? rbase[1] : b == 2 ? rbase[2] : rbase[3]) + idx[q];
-            scr[2 * j] = rec[q].clock; scr[2 * j + 1] = rec[q].clock + rec[q].clen;
+            const uint32_t j = idx[q] + ((b < 4u ? RB0 : RB1) >> (8u * (b & 3u)) & 0xFFu);
+            Sck[j] = rec[q].clock; Sen[j] = rec[q].clock + rec[q].clen;
+            Ssp[j] = (rec[q].span & 0xFFFF0000u) | (b << 13) | (((rec[q].span >> 8) & 0x7Fu) << 5) | (rec[q].span & 0x1Fu);
           }
         }
         wave_sync();
+        // ---- sorted domain: contiguity (rule R-M without gaps / overlaps: a record's clock is the end
+        //      of the previous record of its block) and the packed (structs, bytes) prefix
+        uint32_t osp[LN_ROWS], oex[LN_ROWS];
+        uint32_t carry = 0;
 #pragma unroll
-        for (int q = 0; q < LN_ROWS; q++) {
-          if (hs[q] && idx[q] > 0u) {
-            const uint32_t b = blk[q];
-            const uint32_t j = (b == 0 ? rbase[0] : b == 1 ? rbase[1] : b == 2 ? rbase[2] : rbase[3]) + idx[q];
-            bad |= scr[2 * j - 1] != rec[q].clock;
-          }
+        for (int r = 0; r < LN_ROWS; r++) {
+          const uint32_t j = l + WAVE * r;
+          const bool v = j < nrec;
+          const uint32_t sp = v ? Ssp[j] : 0u, ck = v ? Sck[j] : 0u;
+          const uint32_t spp = (v && j > 0u) ? Ssp[j - 1u] : 0u, ep = (v && j > 0u) ? Sen[j - 1u] : 0u;
+          const bool first = v && (j == 0u || ((spp ^ sp) & 0xE000u) != 0u);   // first record of its block
+          bad |= v && !first && ck != ep;
+          const uint32_t f = v ? (((sp >> 5) & 0x7Fu) << 16) | (sp & 0x1Fu) : 0u;
+          const uint32_t inc = carry + dpp_incl_add(f);
+          const uint32_t ex = inc - f;
+          carry = lane63(inc);
+          if (first) { Sbs[(sp >> 13) & 7u] = ex; Sfc[(sp >> 13) & 7u] = ck; }
+          osp[r] = sp; oex[r] = ex;
         }
-        uint32_t first_clock[4];
-#pragma unroll
-        for (int b = 0; b < 4; b++) first_clock[b] = (uint32_t)__builtin_amdgcn_readfirstlane((int)scr[2 * (rbase[b] < 255u ? rbase[b] : 0u)]);
         wave_sync();
-        // ---- delete sets: union of every update's ranges (scratch after the contiguity pairs)
+        // ---- block headers, lane c = block c: structs, client, first clock; header offsets by a scan
+        uint32_t hcnt = 0, hfc = 0, hbs = 0, hlen = 0;
+        if (l < nC) {
+          hbs = Sbs[l]; hfc = Sfc[l];
+          const uint32_t nxt = l + 1u < nC ? Sbs[l + 1u] : carry;
+          hcnt = (nxt >> 16) - (hbs >> 16);
+          hlen = vu_len(hcnt) + vu_len(ctl) + vu_len(hfc);
+        }
+        const uint32_t hinc = dpp_incl_add(hlen);          // header bytes of blocks <= c (< 128 with <= 8 blocks)
+        const uint32_t hdr_all = lane63(hinc);
+        uint32_t HC0 = 0, HC1 = 0;                         // vu_len(nC) + hinc of each block, packed 8-bit
+#pragma unroll
+        for (int c = 0; c < LN_CMAX; c++) {
+          const uint32_t hc = rdlane(hinc, (uint32_t)c) + vu_len(nC);
+          if (c < 4) HC0 |= (hc & 0xFFu) << (8 * c); else HC1 |= (hc & 0xFFu) << (8 * (c - 4));
+        }
+        const uint32_t hpos = vu_len(nC) + hinc - hlen + (hbs & 0xFFFFu);   // lane c: block c's header position
+        wave_sync();
+        // ---- delete sets: union of every update's ranges (scratch: the sorted records are consumed)
         LDsUnion dsu; dsu.bytes = 1u; dsu.bad = false; dsu.nsegs = 0;
         bool anyds = false;
 #pragma unroll
@@ -1717,7 +1734,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
           uint32_t dpos[LN_ROWS], uend[LN_ROWS];
 #pragma unroll
           for (int q = 0; q < LN_ROWS; q++) { dpos[q] = lean_ds_pos(us[q], rec[q].span); uend[q] = us[q] + un[q]; }
-          dsu = lean_ds_union(lin, (LB32*)(lout + 2048), dpos, uend, hasd, flags);
+          dsu = lean_ds_union(lin, (LB32*)lout, dpos, uend, hasd, flags);
           bad |= dsu.bad;
           wave_sync();
         }
@@ -1731,46 +1748,33 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
         DIAGL(2);
         defer = __ballot(bad) != 0;
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 3   // timing experiment: stage + parse + scan
-        if (l == 0) status[d] = (int)bad + (int)(inb[0] & 1) + (int)(inb[1] & 1) + (int)(inb[2] & 1) + (int)(inb[3] & 1); wave_sync(); continue;
+        if (l == 0) status[d] = (int)bad + (int)(oex[0] & 1) + (int)(oex[1] & 1) + (int)(oex[2] & 1) + (int)(oex[3] & 1); wave_sync(); continue;
 #endif
         if (!defer) {
-          const uint32_t t0 = lane63(dpp_incl_add(nst0)), t1 = lane63(dpp_incl_add(nst1));
-          const uint32_t cnt[4] = {t0 & 0xFFFFu, t0 >> 16, t1 & 0xFFFFu, t1 >> 16};
-          const uint32_t byt[4] = {run0 & 0xFFFFu, run0 >> 16, run1 & 0xFFFFu, run1 >> 16};
-          uint32_t base[4], hdr[4];
-          uint32_t at = vu_len(nC);
-#pragma unroll
-          for (int b = 0; b < 4; b++) {
-            hdr[b] = vu_len(cnt[b]) + vu_len(ctab[b]) + vu_len(first_clock[b]);
-            base[b] = at;
-            if ((uint32_t)b < nC) at += hdr[b] + byt[b];
-          }
-          size = at + dsu.bytes;   // + the delete set
+          const uint32_t at = vu_len(nC) + hdr_all;   // + the struct bytes: the delete set's position
+          size = at + (carry & 0xFFFFu) + dsu.bytes;   // headers + struct bytes + the delete set
           if (size > (uint32_t)LN_OUT || ((size + 15u) & ~15u) > cap || slot + size > out_cap) defer = true;
           else {
-            {
             // ---- emit into the LDS output buffer: structs (funnel copies), block headers, document header, delete set
 #pragma unroll
-            for (int q = 0; q < LN_ROWS; q++) {
-              const uint32_t b = blk[q];
-              const uint32_t t = (b == 0 ? base[0] + hdr[0] : b == 1 ? base[1] + hdr[1] : b == 2 ? base[2] + hdr[2] : base[3] + hdr[3]) + inb[q];
-              lean_copy(lout, lin, hs[q], t, rec[q].span >> 16, rec[q].span & 0xFFu);
+            for (int r = 0; r < LN_ROWS; r++) {
+              const uint32_t j = l + WAVE * r;
+              const uint32_t b = (osp[r] >> 13) & 7u;
+              const uint32_t t = (oex[r] & 0xFFFFu) + ((b < 4u ? HC0 : HC1) >> (8u * (b & 3u)) & 0xFFu);
+              lean_copy(lout, lin, j < nrec, t, osp[r] >> 16, osp[r] & 0x1Fu);
             }
             if (l < nC) {
-              const uint32_t bb = l;
-              uint32_t t = bb == 0 ? base[0] : bb == 1 ? base[1] : bb == 2 ? base[2] : base[3];
-              t = lds_vu(lout, t, bb == 0 ? cnt[0] : bb == 1 ? cnt[1] : bb == 2 ? cnt[2] : cnt[3]);
-              t = lds_vu(lout, t, bb == 0 ? ctab[0] : bb == 1 ? ctab[1] : bb == 2 ? ctab[2] : ctab[3]);
-              lds_vu(lout, t, bb == 0 ? first_clock[0] : bb == 1 ? first_clock[1] : bb == 2 ? first_clock[2] : first_clock[3]);
+              uint32_t t = lds_vu(lout, hpos, hcnt);
+              t = lds_vu(lout, t, ctl);
+              lds_vu(lout, t, hfc);
             }
             if (l == 0) lds_vu(lout, 0, nC);
-            if (dsu.bytes > 1u) lean_ds_emit(lout, at, dsu);   // (an empty delete set is the zero byte already there)
+            if (dsu.bytes > 1u) lean_ds_emit(lout, at + (carry & 0xFFFFu), dsu);   // (an empty delete set is the zero byte already there)
             wave_sync();
             DIAGL(3);
             uint8_t* o = out + slot;
             const uint32_t nco = (size + 15u) / 16u;
             for (uint32_t c = l; c < nco; c += WAVE) *(u32x4*)(o + 16 * c) = *(const LB128*)(lout + 16 * c);
-            }
           }
         }
       }

@@ -32,6 +32,7 @@ namespace ygm {
 constexpr int LN_IN = 5120;     // staged input bytes (including the 0..15 byte alignment shift)
 constexpr int LN_ROWS = 4;      // updates per lane: k <= 256
 constexpr int LN_UMAX = 32;     // bytes per update
+constexpr int LN_CMAX = 8;      // distinct struct clients per document
 
 constexpr int LN_OUT = 4096;    // staged output bytes
 
@@ -53,6 +54,15 @@ YDEV uint32_t dpp_incl_add(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);   // row_shr:8
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+YDEV uint32_t dpp_incl_max(uint32_t x) {   // inclusive prefix max (unsigned); lane 63 holds the wave's max
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
   return x;
 }
 YDEV uint32_t lane63(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }

@@ -73,6 +73,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        # One HIP runtime per process: the torch wheel bundles its own libamdhip64.so.7 (same soname as
+        # /opt/rocm's).  Whichever loads first serves both, and torch's CUDA init fails ("No HIP GPUs are
+        # available") on the system copy -- so when torch is installed it loads first.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
         L.ygm_open.argtypes = [ctypes.c_int, u32, ctypes.POINTER(vp)]

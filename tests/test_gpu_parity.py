@@ -227,11 +227,13 @@ def test_full_size_c2_properties(eng):
 
 
 def test_lean_kernel_takes_debounce_logs(eng):
-    # C2-shaped logs (1-4 clients, per-client clock order, with or without deletions) are
-    # finished by the lean kernel; 5-8 clients and shuffled logs are deferred -- all bit-exact.
+    # C2-shaped logs (1-8 clients, per-client clock order, with or without deletions) are
+    # finished by the lean kernel; 9+ clients and shuffled logs are deferred -- all bit-exact.
     from tools import synth
     cases = [(dict(min_clients=1, max_clients=4), 0, False, True),
-             (dict(min_clients=5, max_clients=8), 0, False, False),
+             (dict(min_clients=5, max_clients=8), 0, False, True),
+             (dict(min_clients=9, max_clients=12), 0, False, False),
+             (dict(min_clients=6, max_clients=8), 20, False, True),
              (dict(min_clients=1, max_clients=4), 0, True, None),
              (dict(min_clients=1, max_clients=3), 15, False, True),
              (dict(min_clients=1, max_clients=4), 20, False, True)]

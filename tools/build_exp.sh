@@ -1,0 +1,10 @@
+#!/bin/bash
+# Experiment build of libygm.so (tooling): tools/build_exp.sh <name> "<extra hipcc flags>" -> hocuspocus_amd/exp/libygm_<name>.so
+# (the kernels file recompiled with the flags, linked with the product's other objects)
+set -e
+cd "$(dirname "$0")/../hocuspocus_amd/csrc"
+make -s -j4 >/dev/null
+mkdir -p ../exp build/exp
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -pthread $2 -c -o build/exp/$1.o ygm_kernels.hip
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -pthread -shared -o ../exp/libygm_$1.so build/exp/$1.o build/ygm_snapshot.hip.o build/ygm_engine.cpp.o
+echo ../exp/libygm_$1.so

@@ -1140,6 +1140,10 @@ YDEV uint32_t wave_min_u32(uint32_t v) {
   return v;
 }
 
+#ifndef YGM_BIG_ROUTE
+#define YGM_BIG_ROUTE 2048
+#endif
+constexpr uint32_t BIG_ROUTE_MIN = YGM_BIG_ROUTE;   // snapshot bytes from which a document goes to k_merge_big directly
 YDEV void merge_wave_doc(WaveLds& L, uint32_t d, const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                          const uint32_t* __restrict__ doc_upd, uint32_t flags,
                          uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
@@ -1159,7 +1163,18 @@ YDEV void merge_wave_doc(WaveLds& L, uint32_t d, const uint8_t* __restrict__ are
   uint32_t S = 0, D = 0, nC = 0, nseg = 0, hdr0 = 0, sbytes = 0, dsbytes = 0;
   if (k == 0) { mode = 1; size = 2; }
   else if (k == 1) { mode = 2; size = nbytes; }
-  else if (k > (uint32_t)W_K || nbytes + 16 > (uint64_t)W_IN || (flags & 2u)) st = ST_DEFER;
+  else if (flags & 2u) st = ST_DEFER;
+  else {
+    // [snapshot, ...log] documents whose snapshot is large go straight to the large-document tier: its
+    // parallel walk of the snapshot beats the lane-per-update parse of this kernel and of the workgroup
+    // tier, which walk the snapshot on one lane
+    uint64_t mx = 0;
+    for (uint32_t i = l; i < k; i += WAVE) { const uint64_t n = upd_off[u0 + i + 1] - upd_off[u0 + i]; mx = n > mx ? n : mx; }
+#pragma unroll
+    for (int o = WAVE / 2; o > 0; o >>= 1) { const uint64_t t = __shfl_xor(mx, o, WAVE); mx = t > mx ? t : mx; }
+    if (mx >= (uint64_t)BIG_ROUTE_MIN) st = ST_FALLBACK;
+    else if (k > (uint32_t)W_K || nbytes + 16 > (uint64_t)W_IN) st = ST_DEFER;
+  }
   if (mode == 0 && st == ST_OK) {
     // ---- stage: 16-byte loads of [b0 & ~15, b1) (arenas carry >= 16 readable bytes of tail padding)
     const uint64_t a0 = b0 & ~15ull;
@@ -1570,6 +1585,10 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
 #pragma unroll
       for (int q = 0; q < LN_ROWS; q++) { us[q] = shift + (rx[q] - (uint32_t)b0); un[q] = ry[q] - rx[q]; }
     }
+    // every prefetch load has landed on every path (free after the staging): without this the waitcnt
+    // pass, path-insensitive, sees them pending in the parse and makes it wait -- counters being in
+    // order -- for the next header's loads issued below
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     wave_sync();
     DIAGL(0);
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 1   // timing experiment: stage only
@@ -1579,9 +1598,13 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
     // ---- header of the next document (its prefetch is issued after the parse) and doc_upd of the one after
     const uint64_t bo_next = lean_bo_load(upd_off, du, d + G, n_docs);
     const uint32_t du_next = lean_du_load(doc_upd, d + 2 * G, n_docs);
-    bool defer = !go && !(k < 2 && !force_seq);
+    // single: mergeUpdates([]) = 0000; a single input is returned as is (Y@39011).  It shares the
+    // prefetch below with the parse path (a prefetch of its own, in its own branch, gets hoisted
+    // above the branch and the parse then waits on those loads)
+    const bool single = k < 2 && !force_seq;
+    bool defer = !go && !single;
     uint32_t size = 0;
-    if (k < 2 && !force_seq) {   // mergeUpdates([]) = 0000; a single input is returned as is (Y@39011)
+    if (single) {
       size = k == 0 ? 2u : (uint32_t)nbytes;
       if (k == 1 && nbytes > 0xFFFFFFFFull) size = 0;
       uint8_t* o = out + slot;
@@ -1595,10 +1618,9 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
         if (l == 0) { out_off[d] = slot; out_len[d] = k == 0 ? 2 : nbytes; status[d] = ST_OK; }
         payload += k == 0 ? 2 : nbytes;
       }
-      hn = lean_hdr_of(du, bo_next); du = du_next;
-      gn = !force_seq && lean_stageable(hn);
-      lean_prefetch(arena, upd_off, hn, gn, v, rx, ry);
-      continue;
+      // drain the copy's loads here: left pending into the join with the parse path, the waitcnt pass
+      // makes the parse wait for them -- and, counters being in order, for the next header's loads
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     }
     // ---- parse, lane per update
     LRec rec[LN_ROWS];
@@ -1617,11 +1639,16 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
       }
     }
     DIAGL(1);
-    // ---- prefetch the next document while this one is scanned and emitted
+    // ---- prefetch the next document while this one is scanned and emitted (kept below the parse:
+    //      hoisted above it, the parse waits on the prefetch's vmcnt)
+#ifdef YGM_LEAN_SB
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     hn = lean_hdr_of(du, bo_next); du = du_next;
     gn = !force_seq && lean_stageable(hn);
     lean_prefetch(arena, upd_off, hn, gn, v, rx, ry);
     defer = defer || __ballot(bad) != 0;
+    if (single) { wave_sync(); continue; }
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 2   // timing experiment: stage + parse
     if (l == 0) status[d] = (int)bad; wave_sync(); continue;
 #endif

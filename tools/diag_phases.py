@@ -22,7 +22,7 @@ e = eng.Engine(0)
 L = eng.lib()
 L.ygm_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
 L.ygm_diag_ts_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
-buf = np.zeros(24, np.uint64)
+buf = np.zeros(64, np.uint64)
 ts = np.zeros(16384 * 8, np.uint64)
 for rep in range(3):
     L.ygm_diag_read(buf.ctypes.data, 1)

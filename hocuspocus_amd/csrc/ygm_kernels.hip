@@ -1857,18 +1857,71 @@ struct BigOut {
   YDEV void vu(uint64_t v) { while (v > 127) { b(0x80u | (uint32_t)(v & 127)); v >>= 7; } b((uint32_t)v); }
   YDEV void copy(const uint8_t* s, uint64_t len) { if (w) big_copy(o + n, s, len); n += len; }
 };
-// U0's delete set as a stream of ranges (every lane walks it redundantly: same bytes, same state)
-struct BigDs {
-  GCur c; uint64_t cl_left, r_left, client; bool has; uint64_t key, len;
-  YDEV void next() {
-    has = false;
-    while (r_left == 0 && cl_left > 0 && !c.err) { client = c.vu(); r_left = c.vu(); cl_left--; }
-    if (r_left == 0 || c.err) return;
-    const uint64_t ck = c.vu(); len = c.vu(); r_left--;
-    key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | ck;
-    has = !c.err;
+// U0's delete set, decoded once by the wave into u32 values (big_ds_decode), then read as a stream of
+// ranges by every lane redundantly (same values, same state): 64 values per register, lane j holding
+// value b + j, taken by readlane with a uniform index; the next 64 are in flight while these are read.
+struct VStream {
+  const uint32_t* V; uint32_t n, i, b, cur, nxt; bool err;
+  YDEV uint32_t fetch(uint32_t at) const { const uint32_t j = at + threadIdx.x % WAVE; return j < n ? V[j] : 0u; }
+  YDEV void init(const uint32_t* v, uint32_t nv) { V = v; n = nv; i = 0; b = 0; err = false; cur = fetch(0); nxt = fetch(WAVE); }
+  YDEV uint32_t next() {
+    if (i >= n) { err = true; return 0u; }
+    if (i - b >= (uint32_t)WAVE) { b += WAVE; cur = nxt; nxt = fetch(b + WAVE); }
+    return (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)(i++ - b));
   }
 };
+struct BigDs {
+  VStream s; uint64_t cl_left, r_left, client; bool has; uint64_t key, len;
+  YDEV void next() {
+    has = false;
+    while (r_left == 0 && cl_left > 0 && !s.err) { client = s.next(); r_left = s.next(); cl_left--; }
+    if (r_left == 0 || s.err) return;
+    const uint64_t ck = s.next(); len = s.next(); r_left--;
+    key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | ck;
+    has = !s.err;
+  }
+};
+// The delete set [ds0, n0) of U0 as u32 values V[0, nv): the wave takes 1 KiB per round, a lane per
+// 16-byte chunk; varuint terminators (top bit clear) by mask, value indices by a wave prefix count, each
+// value decoded by the lane holding its terminator from the 8 bytes ending there.  A trailing
+// unterminated varuint is not a value (the stream runs out if it is needed).  false: a varuint of more
+// than 5 bytes or above 2^32 - 1, or more values than `cap` (the general path takes the document).
+YDEV bool big_ds_decode(const uint8_t* u0p, uint32_t ds0, uint32_t n0, uint32_t* V, uint64_t cap, uint32_t& nv_out) {
+  const uint32_t l = threadIdx.x % WAVE;
+  uint32_t nv = 0;
+  bool bad = false;
+  for (uint32_t base = ds0; base < n0; base += 16u * WAVE) {
+    const uint32_t p0 = base + 16u * l;
+    uint32_t T = 0;
+    if (p0 < n0) {
+      uint4 x; __builtin_memcpy(&x, u0p + p0, 16);   // unaligned (arena tail padding)
+      const uint32_t nb = n0 - p0 < 16u ? n0 - p0 : 16u;
+      T = ~(hibits8(x.x, x.y) | (hibits8(x.z, x.w) << 8)) & (nb >= 16u ? 0xFFFFu : ((1u << nb) - 1u));
+    }
+    const uint32_t cnt = (uint32_t)__builtin_popcount(T);
+    const uint32_t inc = dpp_incl_add(cnt);
+    uint32_t idx = nv + inc - cnt;
+    nv += lane63(inc);
+    while (T) {
+      const uint32_t e = p0 + (uint32_t)__builtin_ctz(T);
+      T &= T - 1u;
+      const uint32_t w0 = e >= ds0 + 7u ? e - 7u : ds0;   // the 8 bytes [w0, w0 + 8) hold the varuint's last bytes
+      uint2 w; __builtin_memcpy(&w, u0p + w0, 8);
+      const uint32_t r = e - w0;                          // terminator index in the window
+      const uint32_t h = hibits8(w.x, w.y) & ((1u << r) - 1u);
+      const uint32_t z = ~h & ((1u << r) - 1u);           // terminators before e in the window
+      const uint32_t st = z ? 32u - (uint32_t)__builtin_clz(z) : 0u;
+      bad |= (z == 0u && w0 > ds0) || r - st >= 5u;       // >= 9 bytes, or > 5 bytes
+      const uint64_t W = ((uint64_t)w.y << 32) | w.x;
+      const uint64_t v = pext7(W >> (8u * st), r - st + 1u);
+      bad |= v > 0xFFFFFFFFull || idx >= cap;
+      if (idx < cap) V[idx] = (uint32_t)v;
+      idx++;
+    }
+  }
+  nv_out = nv;
+  return __ballot(bad) == 0;
+}
 
 // A U0 struct the speculative parse could not take, parsed from global memory (rare: kept out of line so
 // the chain follow's loop stays small).  Returns end | kind << 32 | failed << 63.
@@ -1881,7 +1934,10 @@ YDEV_NI uint64_t big_skip_global(const uint8_t* u0p, uint32_t n0, uint32_t pos) 
 
 // The U0 tile work the whole workgroup shares (BIG_WAVES waves; wave 0 drives, helper waves join
 // through BigCmd): the speculative parse of a tile's positions, and the validation of its structs.
-constexpr uint32_t BIG_WAVES = 16, BIG_THREADS = BIG_WAVES * WAVE;
+#ifndef YGM_BIG_WAVES
+#define YGM_BIG_WAVES 16
+#endif
+constexpr uint32_t BIG_WAVES = YGM_BIG_WAVES, BIG_THREADS = BIG_WAVES * WAVE;
 struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; };   // cmd 0 done, 1 spec, 2 validate
 YDEV void big_spec(BigTile& T, uint32_t at, uint32_t mis, uint32_t tn, uint32_t n0, uint32_t t0) {
   const uint8_t* tp = (const uint8_t*)T.b;
@@ -2088,7 +2144,9 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     wave_sync();
     if (l == 0) { s_ds0 = ds0; if (bad) L.bad = 1; }
   }
+#ifndef YGM_DIAG_BIGDS
   DIAG_PUT(6, dg_spec); DIAG_PUT(7, dg_val);
+#endif
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // validated lengths before the clock-range pass
   wave_sync();
   if (!L.bad) {
@@ -2111,6 +2169,14 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   if (!bad) { big_bitonic(L.pc, npc); big_bitonic(L.rg, nrg); }
   const BigBlk* T = blk + s_base;
   if (bad) nb = 0;
+  // U0's delete set as values (the struct records' scratch is free after the clock-range pass); the
+  // emit's passes stream it, pass 0 keeping each output client's run count after it
+  uint32_t* const dsv = (uint32_t*)(rec + sbase);
+  uint32_t dsn = 0;
+  if (!bad && l < WAVE) {
+    bad = !big_ds_decode(u0p, (uint32_t)s_ds0, n0, dsv, ncap * (sizeof(BigRec) / 4), dsn);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  }
   DIAGL(2);
   // ---- emit: pass 0 sizes (and proves the class), pass 1 bytes.  Every lane runs the same plan.
   uint64_t nblocks = 0, ndsc = 0, size = 0;
@@ -2197,26 +2263,20 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     // delete set: U0's sorted stream (read through LDS tiles, forward only) merged with the sorted log
     // ranges, runs merged per client in one sweep.  Pass 0 keeps each client's run count in the struct
     // records' scratch (free after the clock-range pass) for pass 1's header.
-    uint32_t* runs_of = (uint32_t*)(rec + sbase);
-    const uint64_t runs_cap = ncap * (sizeof(BigRec) / 4);
+#ifdef YGM_DIAG_BIGDS
+    DIAG_PUT(6 + pass, __builtin_amdgcn_s_memrealtime());   // diagnostic: where the delete-set part of the pass starts
+#endif
+    uint32_t* runs_of = dsv + dsn;
+    const uint64_t runs_cap = ncap * (sizeof(BigRec) / 4) - dsn;
     BigDs D;
-    {
-      const uint32_t at = (uint32_t)s_ds0;
-      load_tile(at, false);
-      D.c.init(tp, tn); D.c.pos = at - tb;
-    }
+    D.s.init(dsv, dsn);
     uint64_t dprev = 0;
     auto dnext = [&]() __attribute__((always_inline)) {
-      if (D.c.pos + tb >= tc0 + BT_CH && D.c.pos + tb < n0 && !D.c.err) {
-        const uint32_t at = D.c.pos + tb;
-        load_tile(at, false);
-        D.c.init(tp, tn); D.c.pos = at - tb;
-      }
       D.next();
       // U0's delete set in union order, every range inside 32-bit clocks (else the general path)
-      if (D.has) { bad |= D.key < dprev || D.client > 0xFFFFFFFFull || D.key + D.len > ((D.key >> 32) << 32) + 0xFFFFFFFFull; dprev = D.key; }
+      if (D.has) { bad |= D.key < dprev || D.key + D.len > ((D.key >> 32) << 32) + 0xFFFFFFFFull; dprev = D.key; }
     };
-    D.cl_left = D.c.vu(); D.r_left = 0; D.client = 0;
+    D.cl_left = D.s.next(); D.r_left = 0; D.client = 0;
     dnext();
     uint32_t r = 0;
     uint64_t nc = 0;
@@ -2245,7 +2305,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       nc++;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // pass 0's run counts before pass 1 reads them
-    bad |= D.c.err != 0;
+    bad |= D.s.err;
     DIAGL(3 + pass);
     if (pass == 0) {
       nblocks = nbo; ndsc = nc; size = o.n;

@@ -148,3 +148,69 @@ def doc_batch(mode, arena, doc_off, sv_arena=None, sv_off=None, threads=1, compa
                    sv_arena.ctypes.data if mode == "diff" else None, sv_off.ctypes.data if mode == "diff" else None,
                    n_docs, COMPAT_135 if compat135 else 0, threads, status.ctypes.data, ctypes.byref(algo))
     return status[:n_docs], algo.value
+
+
+# ---- update V2 (yjs_oracle_v2.c) ----
+def _v2lib():
+    L = lib()
+    if not getattr(L, "_v2", False):
+        P = ctypes.POINTER
+        u8p = P(ctypes.c_uint8)
+        L.yo_merge_v2.argtypes = [P(u8p), P(ctypes.c_size_t), ctypes.c_size_t, ctypes.c_int, P(u8p), P(ctypes.c_size_t)]
+        L.yo_diff_v2.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, ctypes.c_int, P(u8p), P(ctypes.c_size_t)]
+        for f in (L.yo_sv_v2, L.yo_v1_to_v2, L.yo_v2_to_v1):
+            f.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, P(u8p), P(ctypes.c_size_t)]
+        for f in (L.yo_merge_v2, L.yo_diff_v2, L.yo_sv_v2, L.yo_v1_to_v2, L.yo_v2_to_v1):
+            f.restype = ctypes.c_int
+        L._v2 = True
+    return L
+
+
+def merge_updates_v2(updates, compat135=False):
+    """Y.mergeUpdatesV2 (V2 in, V2 out)."""
+    L = _v2lib()
+    bufs = [_buf(u) for u in updates]
+    n = len(bufs)
+    ptrs = (ctypes.POINTER(ctypes.c_uint8) * max(n, 1))(*[ctypes.cast(b[0], ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+    lens = (ctypes.c_size_t * max(n, 1))(*[b[1] for b in bufs])
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = L.yo_merge_v2(ptrs, lens, n, COMPAT_135 if compat135 else 0, ctypes.byref(out), ctypes.byref(olen))
+    return _take(out, olen, st)
+
+
+def diff_update_v2(update, sv, compat135=False):
+    """Y.diffUpdateV2 (V2 update, V1-format state vector)."""
+    L = _v2lib()
+    ub, ul = _buf(update)
+    sb, sl = _buf(sv)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = L.yo_diff_v2(ctypes.cast(ub, ctypes.POINTER(ctypes.c_uint8)), ul, ctypes.cast(sb, ctypes.POINTER(ctypes.c_uint8)), sl,
+                      COMPAT_135 if compat135 else 0, ctypes.byref(out), ctypes.byref(olen))
+    return _take(out, olen, st)
+
+
+def _unary_v2(fn, update, compat135):
+    L = _v2lib()
+    ub, ul = _buf(update)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = getattr(L, fn)(ctypes.cast(ub, ctypes.POINTER(ctypes.c_uint8)), ul, COMPAT_135 if compat135 else 0, ctypes.byref(out),
+                        ctypes.byref(olen))
+    return _take(out, olen, st)
+
+
+def encode_state_vector_from_update_v2(update, compat135=False):
+    """Y.encodeStateVectorFromUpdateV2."""
+    return _unary_v2("yo_sv_v2", update, compat135)
+
+
+def convert_update_format_v1_to_v2(update, compat135=False):
+    """yjs 13.6 convertUpdateFormatV1ToV2."""
+    return _unary_v2("yo_v1_to_v2", update, compat135)
+
+
+def convert_update_format_v2_to_v1(update, compat135=False):
+    """yjs 13.6 convertUpdateFormatV2ToV1 (Any numbers that are not varInt integers in embeds / formats are refused)."""
+    return _unary_v2("yo_v2_to_v1", update, compat135)

@@ -1117,3 +1117,4 @@ int yo_doc_batch(int mode, const uint8_t *arena, const uint64_t *doc_off, const 
   free(th); free(jobs);
   return 0;
 }
+#include "yjs_oracle_v2.c"

@@ -52,6 +52,18 @@ int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const 
                            uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta,
                            void* readers, int* order, int* tmp, const uint8_t** ubase, uint32_t* ulen, uint64_t upd_cap,
                            uint32_t* cnt, void* drec, uint64_t byte_cap, uint64_t slot_total, uint64_t out_cap, hipStream_t s);
+int ygm_k_launch_scan(uint64_t* v, uint32_t n, uint64_t* bs, hipStream_t s);
+size_t ygm_k_v2_cols();
+int ygm_k_launch_v21(int pass, const uint8_t* arena, const uint64_t* upd_off, uint32_t n_upd, const uint32_t* doc_upd, uint32_t n_docs,
+                     uint32_t mode, uint32_t flags, uint64_t* len_or_off, int32_t* st, uint8_t* out, hipStream_t s);
+int ygm_k_launch_v12_count(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint8_t* v2a,
+                           uint64_t v2n, const uint64_t* upd_off, const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint32_t mode,
+                           uint32_t flags, uint32_t* L, uint64_t* tot, int32_t* st, hipStream_t s);
+int ygm_k_launch_v12_write(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const uint8_t* v2a, uint64_t v2n,
+                           const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t mode, uint32_t flags, const uint32_t* L,
+                           const uint64_t* off, int32_t* st, uint8_t* out, uint64_t* out_len, hipStream_t s);
+int ygm_k_launch_v2_status(const int32_t* ust, uint32_t n, int32_t* status, uint64_t* len, hipStream_t s);
+int ygm_k_launch_v2_lens(const uint64_t* off, const int32_t* st, uint32_t n, uint64_t* len, hipStream_t s);
 size_t ygm_k_big_blk_bytes();
 size_t ygm_k_big_rec_bytes();
 int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
@@ -127,6 +139,9 @@ struct ygm_ctx {
   DevBuf big_blk, big_rec, big_list;   // large-document tier: block tables, struct records, documents sent on
   DevBuf sv_tbl, sv_tn;                // diff: sorted state-vector tables (k_sv_table) and their entry counts
   DevBuf sn_cnt, sn_off, sn_bs, sn_ws;  // snapshot: per-document counts, workspace offsets, scan scratch, workspaces
+  // update V2: per-update V1 sizes -> offsets, transcoding statuses, scan scratch, the V1 arena, per-document column
+  // lengths, the V2 outputs (packed), their offsets / lengths / statuses
+  DevBuf v2_len, v2_st, v2_bs, v2_v1, v2_L, v2_out, v2_off, v2_olen, v2_ost;
   // host API: results in pinned memory (packed outputs, per-document offset / length / status), the
   // pinned input staging of this context when it serves as a pipeline stage, the packed device copy,
   // and the two stage contexts (own streams and buffers) that double-buffer a batch's chunks
@@ -197,7 +212,8 @@ void ygm_close(ygm_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
-                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws})
+                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws,
+                    &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost})
     b->release();
   for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
   for (DevBuf* b : {&c->pk_data, &c->pk_off, &c->pk_bsum}) b->release();
@@ -489,6 +505,148 @@ int ygm_sv_from_update_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t ar
   return run_doc_kernel(c, 0, d_arena, arena_bytes, d_doc_off, nullptr, 0, nullptr, n_docs, stream, out);
 }
 
+// ------------------------------------------------------------------ update V2 (device API)
+// V2 -> V1 of n units (merge: updates, with doc_upd so single-input documents are skipped; otherwise one per
+// document): sizes, scan (c->v2_len becomes the V1 offsets, total at [n]), bytes into c->v2_v1
+static int v21_pass(ygm_ctx* c, hipStream_t s, const uint8_t* arena, const uint64_t* off, uint32_t n, const uint32_t* doc_upd,
+                    uint32_t n_docs, uint32_t mode, uint64_t& total) {
+  const size_t nb = ((size_t)n + 1 + 255) / 256 + 2;
+  if (!c->v2_len.ensure(8ull * n + 16) || !c->v2_st.ensure(4ull * n + 4) || !c->v2_bs.ensure(8 * nb)) return YGM_ENOMEM;
+  total = 0;
+  if (n == 0) { HIPCHK(hipMemsetAsync(c->v2_len.p, 0, 8, s)); }
+  else {
+    if (ygm_k_launch_v21(0, arena, off, n, doc_upd, n_docs, mode, c->flags, c->v2_len.as<uint64_t>(), c->v2_st.as<int32_t>(), nullptr, s) ||
+        ygm_k_launch_scan(c->v2_len.as<uint64_t>(), n, c->v2_bs.as<uint64_t>(), s))
+      return YGM_EDEVICE;
+    HIPCHK(hipMemcpyAsync(c->h_meta, c->v2_len.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    memcpy(&total, c->h_meta, 8);
+  }
+  if (!c->v2_v1.ensure(total + 64)) return YGM_ENOMEM;   // (the V1 kernels read up to 64 bytes past the arena)
+  if (n && ygm_k_launch_v21(1, arena, off, n, doc_upd, n_docs, mode, c->flags, c->v2_len.as<uint64_t>(), c->v2_st.as<int32_t>(),
+                            c->v2_v1.as<uint8_t>(), s))
+    return YGM_EDEVICE;
+  return YGM_OK;
+}
+// V1 -> V2 per document into c->v2_out (packed at scanned offsets) with final statuses; see k_v12_count
+static int v12_pass(ygm_ctx* c, hipStream_t s, const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st,
+                    const uint8_t* v2a, uint64_t v2n, const uint64_t* upd_off, const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs,
+                    uint32_t mode, ygm_device_result* out) {
+  const size_t nb = ((size_t)n_docs + 1 + 255) / 256 + 2;
+  if (!c->v2_L.ensure(4ull * ygm_k_v2_cols() * n_docs + 16) || !c->v2_off.ensure(8ull * n_docs + 16) || !c->v2_olen.ensure(8ull * n_docs + 8) ||
+      !c->v2_ost.ensure(4ull * n_docs + 4) || !c->v2_bs.ensure(8 * nb))
+    return YGM_ENOMEM;
+  uint64_t total = 0;
+  if (n_docs) {
+    if (ygm_k_launch_v12_count(v1, v1_off, v1_len, v1_st, v2a, v2n, upd_off, doc_upd, ust, n_docs, mode, c->flags, c->v2_L.as<uint32_t>(),
+                               c->v2_off.as<uint64_t>(), c->v2_ost.as<int32_t>(), s) ||
+        ygm_k_launch_scan(c->v2_off.as<uint64_t>(), n_docs, c->v2_bs.as<uint64_t>(), s))
+      return YGM_EDEVICE;
+    HIPCHK(hipMemcpyAsync(c->h_meta, c->v2_off.as<uint64_t>() + n_docs, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    memcpy(&total, c->h_meta, 8);
+  }
+  if (!c->v2_out.ensure(total + 64)) return YGM_ENOMEM;
+  if (n_docs && ygm_k_launch_v12_write(v1, v1_off, v1_len, v2a, v2n, upd_off, doc_upd, n_docs, mode, c->flags, c->v2_L.as<uint32_t>(),
+                                       c->v2_off.as<uint64_t>(), c->v2_ost.as<int32_t>(), c->v2_out.as<uint8_t>(), c->v2_olen.as<uint64_t>(), s))
+    return YGM_EDEVICE;
+  out->data = c->v2_out.as<uint8_t>(); out->off = c->v2_off.as<uint64_t>(); out->len = c->v2_olen.as<uint64_t>();
+  out->status = c->v2_ost.as<int32_t>(); out->data_bytes = total; out->payload_bytes = total;
+  return YGM_OK;
+}
+static const uint32_t V2_EXPORT = 1u, V2_STRUCTS_ONLY = 2u;
+
+// the span of a V2 call's own kernels (the V1 operation inside times itself)
+struct V2Timer {
+  ygm_ctx* c; hipStream_t s; float pre = 0;
+  V2Timer(ygm_ctx* c_, hipStream_t s_) : c(c_), s(s_) { (void)hipEventRecord(c->e2, s); }
+  void split() { (void)hipEventRecord(c->e3, s); (void)hipEventSynchronize(c->e3); float ms = 0; if (hipEventElapsedTime(&ms, c->e2, c->e3) == hipSuccess) pre += ms; }
+  void resume() { (void)hipEventRecord(c->e2, s); }
+  void done() { split(); c->stats.kernel_ms += pre; }
+};
+
+int ygm_merge_v2_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_upd_off, const uint32_t* d_doc_upd,
+                        uint32_t n_upd, uint32_t n_docs, void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  (void)hipSetDevice(c->device);
+  V2Timer T(c, s);
+  uint64_t v1_bytes = 0;
+  int e = v21_pass(c, s, d_arena, d_upd_off, n_upd, d_doc_upd, n_docs, 0, v1_bytes);
+  if (e) return e;
+  T.split();
+  ygm_device_result r1;
+  if ((e = ygm_merge_v1_device(c, c->v2_v1.as<uint8_t>(), v1_bytes, c->v2_len.as<uint64_t>(), d_doc_upd, n_upd, n_docs, s, &r1))) return e;
+  T.resume();
+  e = v12_pass(c, s, r1.data, r1.off, r1.len, r1.status, d_arena, arena_bytes, d_upd_off, d_doc_upd, c->v2_st.as<int32_t>(), n_docs, 0, out);
+  T.done();
+  return e;
+}
+int ygm_diff_v2_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, const uint8_t* d_sv_arena,
+                       const uint64_t* d_sv_off, uint32_t n_docs, void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  (void)hipSetDevice(c->device);
+  V2Timer T(c, s);
+  uint64_t v1_bytes = 0;
+  int e = v21_pass(c, s, d_arena, d_doc_off, n_docs, nullptr, n_docs, 0, v1_bytes);
+  if (e) return e;
+  T.split();
+  ygm_device_result r1;
+  if ((e = ygm_diff_v1_device(c, c->v2_v1.as<uint8_t>(), v1_bytes, c->v2_len.as<uint64_t>(), d_sv_arena, d_sv_off, n_docs, s, &r1))) return e;
+  T.resume();
+  e = v12_pass(c, s, r1.data, r1.off, r1.len, r1.status, d_arena, arena_bytes, nullptr, nullptr, c->v2_st.as<int32_t>(), n_docs, 0, out);
+  T.done();
+  return e;
+}
+int ygm_sv_from_update_v2_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
+                                 void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  (void)arena_bytes;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  (void)hipSetDevice(c->device);
+  V2Timer T(c, s);
+  uint64_t v1_bytes = 0;
+  int e = v21_pass(c, s, d_arena, d_doc_off, n_docs, nullptr, n_docs, V2_STRUCTS_ONLY, v1_bytes);
+  if (e) return e;
+  T.split();
+  if ((e = ygm_sv_from_update_v1_device(c, c->v2_v1.as<uint8_t>(), v1_bytes, c->v2_len.as<uint64_t>(), n_docs, s, out))) return e;
+  T.resume();
+  if (ygm_k_launch_v2_status(c->v2_st.as<int32_t>(), n_docs, out->status, out->len, s)) return YGM_EDEVICE;
+  T.done();
+  return YGM_OK;
+}
+int ygm_convert_v1_to_v2_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
+                                void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  (void)arena_bytes;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  (void)hipSetDevice(c->device);
+  V2Timer T(c, s);
+  const int e = v12_pass(c, s, d_arena, d_doc_off, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, n_docs, V2_EXPORT, out);
+  T.done();
+  if (!e) { c->stats.calls++; c->stats.docs += n_docs; }
+  return e;
+}
+int ygm_convert_v2_to_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
+                                void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  (void)arena_bytes;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  (void)hipSetDevice(c->device);
+  V2Timer T(c, s);
+  uint64_t v1_bytes = 0;
+  int e = v21_pass(c, s, d_arena, d_doc_off, n_docs, nullptr, n_docs, V2_EXPORT, v1_bytes);
+  if (e) return e;
+  if (!c->v2_olen.ensure(8ull * n_docs + 8)) return YGM_ENOMEM;
+  if (ygm_k_launch_v2_lens(c->v2_len.as<uint64_t>(), c->v2_st.as<int32_t>(), n_docs, c->v2_olen.as<uint64_t>(), s)) return YGM_EDEVICE;
+  T.done();
+  c->stats.calls++; c->stats.docs += n_docs;
+  out->data = c->v2_v1.as<uint8_t>(); out->off = c->v2_len.as<uint64_t>(); out->len = c->v2_olen.as<uint64_t>();
+  out->status = c->v2_st.as<int32_t>(); out->data_bytes = v1_bytes; out->payload_bytes = v1_bytes;
+  return YGM_OK;
+}
+
 // ------------------------------------------------------------------ host API
 // A batch is cut into chunks of whole documents (about YGM_CHUNK_BYTES of input each) that alternate
 // between two stage contexts, each with its own stream and device buffers:
@@ -506,7 +664,8 @@ struct Chunk {   // documents [d0, d1): merge updates [u0, u1) / SV-diff documen
   hipEvent_t h0 = nullptr, h1 = nullptr, o0 = nullptr, o1 = nullptr;
 };
 struct HostCall {
-  int mode;   // 0 sv, 1 diff, 2 merge, 3 snapshot, 4 contains (second arena in the sv slots)
+  int mode;   // 0 sv, 1 diff, 2 merge, 3 snapshot, 4 contains (second arena in the sv slots); update V2: 5 merge, 6 diff,
+              // 7 sv, 8 V1 -> V2, 9 V2 -> V1
   const uint8_t* arena; const uint64_t* off; const uint32_t* upd_doc; const uint8_t* sv_arena; const uint64_t* sv_off;
   uint32_t n_upd, n_docs;
 };
@@ -554,21 +713,22 @@ static void par_for(size_t n, F f) {
 }
 
 // CPU copy of a chunk's inputs into the stage's pinned buffer, then the async H2D copies
+static bool is_merge(int mode) { return mode == 2 || mode == 5; }
 static int chunk_stage(ygm_ctx* k, const HostCall& H, Chunk& C) {
-  const bool two = H.mode == 1 || H.mode == 4;   // a second arena per document (diff: state vectors, contains: updates)
+  const bool two = H.mode == 1 || H.mode == 4 || H.mode == 6;   // a second arena per document (diff: state vectors, contains: updates)
   const uint32_t nd = C.d1 - C.d0;
-  const uint64_t a0 = H.mode == 2 ? H.off[C.u0] : H.off[C.d0], a1 = H.mode == 2 ? H.off[C.u1] : H.off[C.d1];
+  const uint64_t a0 = is_merge(H.mode) ? H.off[C.u0] : H.off[C.d0], a1 = is_merge(H.mode) ? H.off[C.u1] : H.off[C.d1];
   const uint64_t bytes = a1 - a0, ab = (bytes + 64 + 15) & ~15ull;
-  const uint32_t nu = H.mode == 2 ? C.u1 - C.u0 : nd;
+  const uint32_t nu = is_merge(H.mode) ? C.u1 - C.u0 : nd;
   uint64_t s0 = 0, s1 = 0, sb = 0;
   if (two) { s0 = H.sv_off[C.d0]; s1 = H.sv_off[C.d1]; sb = ((s1 - s0) + 64 + 15) & ~15ull; }
-  const uint64_t n_off = (uint64_t)nu + 1, n_doc = H.mode == 2 ? (uint64_t)nd + 1 : 0, n_sv = two ? (uint64_t)nd + 1 : 0;
+  const uint64_t n_off = (uint64_t)nu + 1, n_doc = is_merge(H.mode) ? (uint64_t)nd + 1 : 0, n_sv = two ? (uint64_t)nd + 1 : 0;
   const uint64_t need = ab + 8 * n_off + sb + 8 * n_sv + 4 * n_doc + 64;
   if (!k->h_in.ensure(need)) return YGM_ENOMEM;
   uint8_t* P = k->h_in.as<uint8_t>();
   par_memcpy(P, H.arena + a0, bytes); memset(P + bytes, 0, ab - bytes);
   uint64_t* ro = (uint64_t*)(P + ab);
-  const uint64_t* src_off = H.mode == 2 ? H.off + C.u0 : H.off + C.d0;
+  const uint64_t* src_off = is_merge(H.mode) ? H.off + C.u0 : H.off + C.d0;
   par_for(n_off, [=](size_t a, size_t b) { for (size_t j = a; j < b; j++) ro[j] = src_off[j] - a0; });
   uint8_t* q = P + ab + 8 * n_off;
   if (two) {
@@ -577,14 +737,14 @@ static int chunk_stage(ygm_ctx* k, const HostCall& H, Chunk& C) {
     for (uint64_t j = 0; j < n_sv; j++) rs[j] = H.sv_off[C.d0 + j] - s0;
     q += sb + 8 * n_sv;
   }
-  if (H.mode == 2) {   // per-document update ranges, relative to the chunk
+  if (is_merge(H.mode)) {   // per-document update ranges, relative to the chunk
     uint32_t* du = (uint32_t*)q;
     du[0] = 0;
     uint32_t u = C.u0;
     for (uint32_t d = 0; d < nd; d++) { while (u < C.u1 && H.upd_doc[u] == C.d0 + d) u++; du[d + 1] = u - C.u0; }
   }
   if (!k->arena.ensure(ab) || !k->offs.ensure(8 * n_off) || (two && (!k->sv_arena.ensure(sb) || !k->sv_offs.ensure(8 * n_sv))) ||
-      (H.mode == 2 && !k->docs.ensure(4 * n_doc)))
+      (is_merge(H.mode) && !k->docs.ensure(4 * n_doc)))
     return YGM_ENOMEM;
   HIPCHK(hipEventRecord(C.h0, k->stream));
   HIPCHK(hipMemcpyAsync(k->arena.p, P, ab, hipMemcpyHostToDevice, k->stream));
@@ -593,7 +753,7 @@ static int chunk_stage(ygm_ctx* k, const HostCall& H, Chunk& C) {
     HIPCHK(hipMemcpyAsync(k->sv_arena.p, P + ab + 8 * n_off, sb, hipMemcpyHostToDevice, k->stream));
     HIPCHK(hipMemcpyAsync(k->sv_offs.p, P + ab + 8 * n_off + sb, 8 * n_sv, hipMemcpyHostToDevice, k->stream));
   }
-  if (H.mode == 2) HIPCHK(hipMemcpyAsync(k->docs.p, q, 4 * n_doc, hipMemcpyHostToDevice, k->stream));
+  if (is_merge(H.mode)) HIPCHK(hipMemcpyAsync(k->docs.p, q, 4 * n_doc, hipMemcpyHostToDevice, k->stream));
   HIPCHK(hipEventRecord(C.h1, k->stream));
   return YGM_OK;
 }
@@ -601,10 +761,17 @@ static int chunk_stage(ygm_ctx* k, const HostCall& H, Chunk& C) {
 // kernels of a staged chunk, packing, and the async D2H into the parent's pinned results
 static int chunk_run(ygm_ctx* c, ygm_ctx* k, const HostCall& H, Chunk& C, uint64_t& pos, bool merge_enqueued) {
   const uint32_t nd = C.d1 - C.d0;
-  const uint64_t bytes = (H.mode == 2 ? H.off[C.u1] - H.off[C.u0] : H.off[C.d1] - H.off[C.d0]);
+  const uint64_t bytes = (is_merge(H.mode) ? H.off[C.u1] - H.off[C.u0] : H.off[C.d1] - H.off[C.d0]);
   ygm_device_result dr;
   int e;
-  if (H.mode == 2) e = merge_enqueued ? ygm_merge_v1_device_finish(k, &dr)
+  if (H.mode == 5) e = ygm_merge_v2_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->docs.as<uint32_t>(), C.u1 - C.u0, nd,
+                                           nullptr, &dr);
+  else if (H.mode == 6) e = ygm_diff_v2_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->sv_arena.as<uint8_t>(),
+                                               k->sv_offs.as<uint64_t>(), nd, nullptr, &dr);
+  else if (H.mode == 7) e = ygm_sv_from_update_v2_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), nd, nullptr, &dr);
+  else if (H.mode == 8) e = ygm_convert_v1_to_v2_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), nd, nullptr, &dr);
+  else if (H.mode == 9) e = ygm_convert_v2_to_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), nd, nullptr, &dr);
+  else if (H.mode == 2) e = merge_enqueued ? ygm_merge_v1_device_finish(k, &dr)
                                       : ygm_merge_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->docs.as<uint32_t>(),
                                                             C.u1 - C.u0, nd, nullptr, &dr);
   else if (H.mode == 4) e = ygm_contains_v1_device(k, k->arena.as<uint8_t>(), k->offs.as<uint64_t>(), k->sv_arena.as<uint8_t>(),
@@ -646,11 +813,11 @@ static int host_call(ygm_ctx* c, const HostCall& H, ygm_result* out) {
     while (d < n || ch.empty()) {
       Chunk C{};
       C.d0 = d; C.u0 = u;
-      const uint64_t base = H.mode == 2 ? H.off[u] : H.off[d];
+      const uint64_t base = is_merge(H.mode) ? H.off[u] : H.off[d];
       while (d < n) {
         uint32_t ue = u;
-        if (H.mode == 2) while (ue < H.n_upd && H.upd_doc[ue] == d) ue++;
-        const uint64_t end = H.mode == 2 ? H.off[ue] : H.off[d + 1];
+        if (is_merge(H.mode)) while (ue < H.n_upd && H.upd_doc[ue] == d) ue++;
+        const uint64_t end = is_merge(H.mode) ? H.off[ue] : H.off[d + 1];
         if (d > C.d0 && end - base > YGM_CHUNK_BYTES) break;
         d++; u = ue;
       }
@@ -660,7 +827,7 @@ static int host_call(ygm_ctx* c, const HostCall& H, ygm_result* out) {
     }
   }
   // (outputs are usually no larger than the inputs: sized so, grown when a chunk needs more)
-  const uint64_t in_bytes = n ? (H.mode == 2 ? H.off[H.n_upd] - H.off[0] : H.off[n] - H.off[0]) : 0;
+  const uint64_t in_bytes = n ? (is_merge(H.mode) ? H.off[H.n_upd] - H.off[0] : H.off[n] - H.off[0]) : 0;
   if (!c->h_off.ensure(8ull * n + 8) || !c->h_len.ensure(8ull * n + 8) || !c->h_status.ensure(4ull * n + 4) ||
       !c->h_data.ensure(in_bytes + 16ull * n + 4096))
     return YGM_ENOMEM;
@@ -736,13 +903,24 @@ int ygm_merge_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* upd_off, cons
   return host_call(c, H, out);
 }
 
+int ygm_merge_v2(ygm_ctx* c, const uint8_t* arena, const uint64_t* upd_off, const uint32_t* upd_doc, uint32_t n_upd, uint32_t n_docs,
+                 ygm_result* out) {
+  if (!c || !out || (n_upd && (!arena || !upd_off || !upd_doc))) return YGM_EINVAL;
+  for (uint32_t i = 0; i < n_upd; i++)
+    if (upd_doc[i] >= n_docs || (i && upd_doc[i] < upd_doc[i - 1]) || upd_off[i + 1] < upd_off[i]) return YGM_EINVAL;
+  static const uint64_t zero_off[1] = {0};
+  HostCall H{5, arena, n_upd ? upd_off : zero_off, upd_doc, nullptr, nullptr, n_upd, n_docs};
+  return host_call(c, H, out);
+}
+
 static int host_doc_call(ygm_ctx* c, int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena,
                          const uint64_t* sv_off, uint32_t n_docs, ygm_result* out) {
   if (!c || !out || (n_docs && (!arena || !doc_off))) return YGM_EINVAL;
-  if ((mode == 1 || mode == 4) && n_docs && (!sv_arena || !sv_off)) return YGM_EINVAL;
+  const bool two = mode == 1 || mode == 4 || mode == 6;
+  if (two && n_docs && (!sv_arena || !sv_off)) return YGM_EINVAL;
   for (uint32_t d = 0; d < n_docs; d++) {
     if (doc_off[d + 1] < doc_off[d]) return YGM_EINVAL;
-    if ((mode == 1 || mode == 4) && sv_off[d + 1] < sv_off[d]) return YGM_EINVAL;
+    if (two && sv_off[d + 1] < sv_off[d]) return YGM_EINVAL;
   }
   static const uint64_t zero_off[1] = {0};
   HostCall H{mode, arena, n_docs ? doc_off : zero_off, nullptr, sv_arena, n_docs ? sv_off : zero_off, 0, n_docs};
@@ -765,6 +943,20 @@ int ygm_diff_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, const
 
 int ygm_sv_from_update_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, ygm_result* out) {
   return host_doc_call(c, 0, arena, doc_off, nullptr, nullptr, n_docs, out);
+}
+
+int ygm_diff_v2(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,
+                uint32_t n_docs, ygm_result* out) {
+  return host_doc_call(c, 6, arena, doc_off, sv_arena, sv_off, n_docs, out);
+}
+int ygm_sv_from_update_v2(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, ygm_result* out) {
+  return host_doc_call(c, 7, arena, doc_off, nullptr, nullptr, n_docs, out);
+}
+int ygm_convert_v1_to_v2(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, ygm_result* out) {
+  return host_doc_call(c, 8, arena, doc_off, nullptr, nullptr, n_docs, out);
+}
+int ygm_convert_v2_to_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, ygm_result* out) {
+  return host_doc_call(c, 9, arena, doc_off, nullptr, nullptr, n_docs, out);
 }
 
 }  // extern "C"

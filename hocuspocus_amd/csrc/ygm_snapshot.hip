@@ -208,6 +208,15 @@ int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32
   hipLaunchKernelGGL(k_snap_scan_apply, dim3(nb), dim3(256), 0, s, ws_off, n_docs, (const uint64_t*)bs);
   return snap_rc(__func__);
 }
+// exclusive scan of v[0..n) in place, total at v[n] (bs: ceil((n + 1) / 256) + 1 scratch entries)
+int ygm_k_launch_scan(uint64_t* v, uint32_t n, uint64_t* bs, hipStream_t s) {
+  if (n == 0) return 0;
+  const uint32_t nb = (n + 1 + 255) / 256;
+  hipLaunchKernelGGL(k_snap_scan_sum, dim3(nb), dim3(256), 0, s, (const uint64_t*)v, n, bs);
+  hipLaunchKernelGGL(k_snap_scan_top, dim3(1), dim3(1024), 0, s, bs, nb);
+  hipLaunchKernelGGL(k_snap_scan_apply, dim3(nb), dim3(256), 0, s, v, n, (const uint64_t*)bs);
+  return snap_rc(__func__);
+}
 // phase 2: the snapshots (ws sized from ws_off[n_docs])
 int ygm_k_launch_snap(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, const void* cnt, const uint64_t* ws_off,
                       uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, hipStream_t s) {

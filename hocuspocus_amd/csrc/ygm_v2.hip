@@ -1,0 +1,179 @@
+// ygm_v2.hip -- update-V2 kernels: one lane per update / document runs the transcoders of
+// ygm_v2.hpp in two passes (sizes, then bytes at scanned offsets).
+//   k_v21_count / k_v21_write : V2 -> V1 per update (merge: updates of single-input documents are skipped --
+//                               mergeUpdatesV2 returns a lone input as it is)
+//   k_v12_count / k_v12_write : V1 -> V2 per document, with the document's final status (the V2 inputs'
+//                               transcoding statuses, then the V1 operation's), or the passthrough copy
+//   k_v2_status               : SV: a V2 input's transcoding status over the V1 kernel's
+// The lanes of a wave take different paths through the byte codec; documents are independent, so nothing
+// is shared and the wave only pays divergence.  The V1 operation between the passes is the engine's V1
+// cascade, unchanged.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "ygm_common.hpp"
+#include "ygm_v2.hpp"
+
+namespace ygm {
+
+constexpr int V2_NT = 64;
+
+YDEV bool is_throw(int st) { return st == ST_MALFORMED || st == ST_RANGE || st == ST_SURROGATE || st == ST_DEPTH; }
+
+// the document of update u (doc_upd: n_docs + 1 non-decreasing update offsets)
+YDEV uint32_t doc_of(const uint32_t* doc_upd, uint32_t n_docs, uint32_t u) {
+  uint32_t lo = 0, hi = n_docs;   // last d with doc_upd[d] <= u
+  while (hi - lo > 1) { const uint32_t m = (lo + hi) / 2; if (doc_upd[m] <= u) lo = m; else hi = m; }
+  return lo;
+}
+
+__global__ __launch_bounds__(V2_NT) void k_v21_count(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off, uint32_t n_upd,
+                                                    const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t mode, uint32_t flags,
+                                                    uint64_t* __restrict__ len, int32_t* __restrict__ st) {
+  const uint32_t u = blockIdx.x * V2_NT + threadIdx.x;
+  if (u >= n_upd) return;
+  if (doc_upd) {
+    const uint32_t d = doc_of(doc_upd, n_docs, u);
+    if (doc_upd[d + 1] - doc_upd[d] == 1) { len[u] = 0; st[u] = ST_OK; return; }
+  }
+  const uint64_t a = upd_off[u], b = upd_off[u + 1];
+  if (b < a || b - a >= (1ull << 30)) { len[u] = 0; st[u] = ST_INVAL; return; }
+  Out o{nullptr, 0};
+  const int e = v2::v21(arena + a, (uint32_t)(b - a), a, mode, flags, o);
+  len[u] = e ? 0u : o.n;
+  st[u] = e;
+}
+__global__ __launch_bounds__(V2_NT) void k_v21_write(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off, uint32_t n_upd,
+                                                    uint32_t mode, uint32_t flags, const uint64_t* __restrict__ off,
+                                                    const int32_t* __restrict__ st, uint8_t* __restrict__ out) {
+  const uint32_t u = blockIdx.x * V2_NT + threadIdx.x;
+  if (u >= n_upd || st[u] != ST_OK || off[u + 1] == off[u]) return;
+  const uint64_t a = upd_off[u], b = upd_off[u + 1];
+  Out o{out + off[u], 0};
+  (void)v2::v21(arena + a, (uint32_t)(b - a), a, mode, flags, o);
+}
+
+// per document: final status and V2 size.  merge (doc_upd != null): a single-input document is passed
+// through (L[0] = ~0); otherwise a throw in any input's transcoding wins over a refusal, then the V1
+// merge's status.  diff / public V1 -> V2 (doc_upd == null): ust[d] (if given), then v1_st[d] (if given).
+__global__ __launch_bounds__(V2_NT) void k_v12_count(const uint8_t* __restrict__ v1, const uint64_t* __restrict__ v1_off,
+                                                    const uint64_t* __restrict__ v1_len, const int32_t* __restrict__ v1_st,
+                                                    const uint8_t* __restrict__ v2a, uint64_t v2n, const uint64_t* __restrict__ upd_off,
+                                                    const uint32_t* __restrict__ doc_upd, const int32_t* __restrict__ ust, uint32_t n_docs,
+                                                    uint32_t mode, uint32_t flags, uint32_t* __restrict__ L, uint64_t* __restrict__ tot,
+                                                    int32_t* __restrict__ st) {
+  const uint32_t d = blockIdx.x * V2_NT + threadIdx.x;
+  if (d >= n_docs) return;
+  uint32_t* Ld = L + (size_t)d * v2::C_N;
+  int s = ST_OK;
+  if (doc_upd) {
+    const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
+    if (u1 - u0 == 1) { Ld[0] = 0xFFFFFFFFu; tot[d] = upd_off[u1] - upd_off[u0]; st[d] = ST_OK; return; }
+    int refuse = ST_OK;
+    for (uint32_t u = u0; u < u1 && !s; u++) { const int e = ust[u]; if (is_throw(e) || e == ST_INVAL) s = e; else if (e && !refuse) refuse = e; }
+    if (!s) s = refuse;
+  } else if (ust) s = ust[d];
+  if (!s && v1_st) s = v1_st[d];
+  uint64_t t = 0;
+  if (!s) {
+    const uint64_t len = v1_len ? v1_len[d] : v1_off[d + 1] - v1_off[d];
+    if (len >= (1ull << 30)) s = ST_INVAL;
+    else {
+      v2::Enc2 w; v2::enc_init(w);
+      s = v2::v12_body(v1 + v1_off[d], (uint32_t)len, v2a, v2n, mode, flags, w);
+      for (int i = 0; i < v2::C_N; i++) Ld[i] = w.o[i].n;
+      if (!s) t = v2::v2_total(Ld);
+    }
+  }
+  Ld[0] = s ? 0u : Ld[0];
+  tot[d] = s ? 0u : t;
+  st[d] = s;
+}
+__global__ __launch_bounds__(V2_NT) void k_v12_write(const uint8_t* __restrict__ v1, const uint64_t* __restrict__ v1_off,
+                                                    const uint64_t* __restrict__ v1_len, const uint8_t* __restrict__ v2a, uint64_t v2n,
+                                                    const uint64_t* __restrict__ upd_off, const uint32_t* __restrict__ doc_upd, uint32_t n_docs,
+                                                    uint32_t mode, uint32_t flags, const uint32_t* __restrict__ L,
+                                                    const uint64_t* __restrict__ off, int32_t* __restrict__ st, uint8_t* __restrict__ out,
+                                                    uint64_t* __restrict__ out_len) {
+  const uint32_t d = blockIdx.x * V2_NT + threadIdx.x;
+  if (d >= n_docs) return;
+  const uint32_t* Ld = L + (size_t)d * v2::C_N;
+  const uint64_t o0 = off[d], n = off[d + 1] - o0;
+  out_len[d] = st[d] == ST_OK ? n : 0u;
+  if (st[d] != ST_OK) return;
+  if (doc_upd && Ld[0] == 0xFFFFFFFFu) {   // single input: as it is
+    const uint8_t* src = v2a + upd_off[doc_upd[d]];
+    for (uint64_t i = 0; i < n; i++) out[o0 + i] = src[i];
+    return;
+  }
+  const uint64_t len = v1_len ? v1_len[d] : v1_off[d + 1] - v1_off[d];
+  const int e = v2::v12_write(v1 + v1_off[d], (uint32_t)len, v2a, v2n, mode, flags, Ld, out + o0);
+  if (e) { st[d] = ST_DEVICE; out_len[d] = 0; }   // (the count pass took the same path: cannot happen)
+}
+__global__ __launch_bounds__(256) void k_v2_status(const int32_t* __restrict__ ust, uint32_t n, int32_t* __restrict__ status,
+                                                  uint64_t* __restrict__ len) {
+  const uint32_t d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= n || ust[d] == ST_OK) return;
+  status[d] = ust[d]; len[d] = 0;
+}
+
+// public V2 -> V1: per-document lengths from the scanned offsets
+__global__ __launch_bounds__(256) void k_v2_lens(const uint64_t* __restrict__ off, const int32_t* __restrict__ st, uint32_t n,
+                                                uint64_t* __restrict__ len) {
+  const uint32_t d = blockIdx.x * 256 + threadIdx.x;
+  if (d < n) len[d] = st[d] == ST_OK ? off[d + 1] - off[d] : 0u;
+}
+
+}  // namespace ygm
+
+using namespace ygm;
+
+extern "C" {
+
+static int v2_rc(const char* fn) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { fprintf(stderr, "ygm: %s: %s\n", fn, hipGetErrorString(e)); return -1; }
+  return 0;
+}
+size_t ygm_k_v2_cols() { return v2::C_N; }
+int ygm_k_launch_v21(int pass, const uint8_t* arena, const uint64_t* upd_off, uint32_t n_upd, const uint32_t* doc_upd, uint32_t n_docs,
+                     uint32_t mode, uint32_t flags, uint64_t* len_or_off, int32_t* st, uint8_t* out, hipStream_t s) {
+  if (n_upd == 0) return 0;
+  const uint32_t g = (n_upd + V2_NT - 1) / V2_NT;
+  if (pass == 0) hipLaunchKernelGGL(k_v21_count, dim3(g), dim3(V2_NT), 0, s, arena, upd_off, n_upd, doc_upd, n_docs, mode, flags, len_or_off, st);
+  else hipLaunchKernelGGL(k_v21_write, dim3(g), dim3(V2_NT), 0, s, arena, upd_off, n_upd, mode, flags, (const uint64_t*)len_or_off,
+                          (const int32_t*)st, out);
+  return v2_rc(__func__);
+}
+int ygm_k_launch_v12_count(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint8_t* v2a,
+                           uint64_t v2n, const uint64_t* upd_off, const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint32_t mode,
+                           uint32_t flags, uint32_t* L, uint64_t* tot, int32_t* st, hipStream_t s) {
+  if (n_docs == 0) return 0;
+  const uint32_t g = (n_docs + V2_NT - 1) / V2_NT;
+  hipLaunchKernelGGL(k_v12_count, dim3(g), dim3(V2_NT), 0, s, v1, v1_off, v1_len, v1_st, v2a, v2n, upd_off, doc_upd, ust, n_docs, mode, flags,
+                     L, tot, st);
+  return v2_rc(__func__);
+}
+int ygm_k_launch_v12_write(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const uint8_t* v2a, uint64_t v2n,
+                           const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t mode, uint32_t flags, const uint32_t* L,
+                           const uint64_t* off, int32_t* st, uint8_t* out, uint64_t* out_len, hipStream_t s) {
+  if (n_docs == 0) return 0;
+  const uint32_t g = (n_docs + V2_NT - 1) / V2_NT;
+  hipLaunchKernelGGL(k_v12_write, dim3(g), dim3(V2_NT), 0, s, v1, v1_off, v1_len, v2a, v2n, upd_off, doc_upd, n_docs, mode, flags, L, off, st,
+                     out, out_len);
+  return v2_rc(__func__);
+}
+int ygm_k_launch_v2_status(const int32_t* ust, uint32_t n, int32_t* status, uint64_t* len, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_v2_status, dim3((n + 255) / 256), dim3(256), 0, s, ust, n, status, len);
+  return v2_rc(__func__);
+}
+
+int ygm_k_launch_v2_lens(const uint64_t* off, const int32_t* st, uint32_t n, uint64_t* len, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_v2_lens, dim3((n + 255) / 256), dim3(256), 0, s, off, st, n, len);
+  return v2_rc(__func__);
+}
+
+}  // extern "C"

@@ -64,7 +64,10 @@ _lib = None
 EXPORTS = ("ygm_open", "ygm_close", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_update_v1", "ygm_merge_v1_device",
            "ygm_merge_v1_device_async", "ygm_merge_v1_device_finish",
            "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_snapshot_v1", "ygm_snapshot_v1_device",
-           "ygm_contains_v1", "ygm_contains_v1_device", "ygm_stats", "ygm_strerror", "ygm_version")
+           "ygm_contains_v1", "ygm_contains_v1_device", "ygm_stats", "ygm_strerror", "ygm_version",
+           "ygm_merge_v2", "ygm_diff_v2", "ygm_sv_from_update_v2", "ygm_convert_v1_to_v2", "ygm_convert_v2_to_v1",
+           "ygm_merge_v2_device", "ygm_diff_v2_device", "ygm_sv_from_update_v2_device", "ygm_convert_v1_to_v2_device",
+           "ygm_convert_v2_to_v1_device")
 
 
 def lib():
@@ -97,6 +100,14 @@ def lib():
         L.ygm_snapshot_v1_device.argtypes = [vp, vp, u64, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_contains_v1.argtypes = [vp, vp, vp, vp, vp, u32, ctypes.POINTER(_Result)]
         L.ygm_contains_v1_device.argtypes = [vp, vp, vp, vp, vp, u32, vp, ctypes.POINTER(_DevResult)]
+        L.ygm_merge_v2.argtypes = [vp, vp, vp, vp, u32, u32, ctypes.POINTER(_Result)]
+        L.ygm_diff_v2.argtypes = [vp, vp, vp, vp, vp, u32, ctypes.POINTER(_Result)]
+        for f in ("ygm_sv_from_update_v2", "ygm_convert_v1_to_v2", "ygm_convert_v2_to_v1"):
+            getattr(L, f).argtypes = [vp, vp, vp, u32, ctypes.POINTER(_Result)]
+        L.ygm_merge_v2_device.argtypes = [vp, vp, u64, vp, vp, u32, u32, vp, ctypes.POINTER(_DevResult)]
+        L.ygm_diff_v2_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, vp, ctypes.POINTER(_DevResult)]
+        for f in ("ygm_sv_from_update_v2_device", "ygm_convert_v1_to_v2_device", "ygm_convert_v2_to_v1_device"):
+            getattr(L, f).argtypes = [vp, vp, u64, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.ygm_strerror.argtypes = [i32]
         L.ygm_strerror.restype = ctypes.c_char_p
@@ -104,7 +115,9 @@ def lib():
         for f in ("ygm_open", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_update_v1", "ygm_merge_v1_device",
                   "ygm_merge_v1_device_async", "ygm_merge_v1_device_finish",
                   "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_snapshot_v1", "ygm_snapshot_v1_device",
-                  "ygm_contains_v1", "ygm_contains_v1_device", "ygm_stats"):
+                  "ygm_contains_v1", "ygm_contains_v1_device", "ygm_stats", "ygm_merge_v2", "ygm_diff_v2", "ygm_sv_from_update_v2",
+                  "ygm_convert_v1_to_v2", "ygm_convert_v2_to_v1", "ygm_merge_v2_device", "ygm_diff_v2_device",
+                  "ygm_sv_from_update_v2_device", "ygm_convert_v1_to_v2_device", "ygm_convert_v2_to_v1_device"):
             getattr(L, f).restype = i32
         _lib = L
     return _lib
@@ -267,6 +280,75 @@ class Engine:
         if st != OK:
             raise YjsError(st)
         return self._unpack(res)
+
+    # ------------------------------------------------------------ update V2
+    def merge_updates_v2_batch(self, docs):
+        """Y.mergeUpdatesV2 per document: docs = list of lists of V2 updates -> list of (status, V2 bytes | None)."""
+        blobs, doc_ids = [], []
+        for d, ups in enumerate(docs):
+            for u in ups:
+                blobs.append(bytes(u))
+                doc_ids.append(d)
+        arena, off = _pack(blobs)
+        upd_doc = np.asarray(doc_ids, dtype=np.uint32)
+        res = _Result()
+        st = lib().ygm_merge_v2(self._ctx, arena or None, _ptr(off), _ptr(upd_doc), len(blobs), len(docs), ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._unpack(res)
+
+    def diff_update_v2_batch(self, updates, svs):
+        """Y.diffUpdateV2(update, sv) per document (V2 updates, V1-format state vectors)."""
+        arena, off = _pack([bytes(u) for u in updates])
+        sva, svo = _pack([bytes(s) for s in svs])
+        res = _Result()
+        st = lib().ygm_diff_v2(self._ctx, arena or None, _ptr(off), sva or None, _ptr(svo), len(updates), ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._unpack(res)
+
+    def _unary_v2(self, fn, updates):
+        arena, off = _pack([bytes(u) for u in updates])
+        res = _Result()
+        st = getattr(lib(), fn)(self._ctx, arena or None, _ptr(off), len(updates), ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._unpack(res)
+
+    def encode_state_vector_from_update_v2_batch(self, updates):
+        """Y.encodeStateVectorFromUpdateV2 per update (the state vector is V1-encoded, as yjs's)."""
+        return self._unary_v2("ygm_sv_from_update_v2", updates)
+
+    def convert_update_format_v1_to_v2_batch(self, updates):
+        """yjs 13.6 Y.convertUpdateFormatV1ToV2 per update."""
+        return self._unary_v2("ygm_convert_v1_to_v2", updates)
+
+    def convert_update_format_v2_to_v1_batch(self, updates):
+        """yjs 13.6 Y.convertUpdateFormatV2ToV1 per update."""
+        return self._unary_v2("ygm_convert_v2_to_v1", updates)
+
+    def merge_v2_device(self, d_arena, arena_bytes, d_upd_off, d_doc_upd, n_upd, n_docs, stream=0) -> "DeviceResult":
+        r = _DevResult()
+        st = lib().ygm_merge_v2_device(self._ctx, _dptr(d_arena, arena_bytes + TAIL_PAD), arena_bytes, _dptr(d_upd_off), _dptr(d_doc_upd),
+                                       n_upd, n_docs, stream or None, ctypes.byref(r))
+        if st != OK:
+            raise YjsError(st)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)
+
+    def doc_v2_device(self, op, d_arena, arena_bytes, d_doc_off, n_docs, d_sv=None, d_sv_off=None, stream=0) -> "DeviceResult":
+        """op: "diff" (d_sv / d_sv_off), "sv", "v1_to_v2", "v2_to_v1" -- the device-resident V2 calls."""
+        r = _DevResult()
+        a = _dptr(d_arena, arena_bytes + TAIL_PAD)
+        if op == "diff":
+            st = lib().ygm_diff_v2_device(self._ctx, a, arena_bytes, _dptr(d_doc_off), _dptr(d_sv), _dptr(d_sv_off), n_docs, stream or None,
+                                          ctypes.byref(r))
+        else:
+            fn = {"sv": "ygm_sv_from_update_v2_device", "v1_to_v2": "ygm_convert_v1_to_v2_device",
+                  "v2_to_v1": "ygm_convert_v2_to_v1_device"}[op]
+            st = getattr(lib(), fn)(self._ctx, a, arena_bytes, _dptr(d_doc_off), n_docs, stream or None, ctypes.byref(r))
+        if st != OK:
+            raise YjsError(st)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)
 
     # ------------------------------------------------------------ yjs-shaped single calls
     def snapshot_batch(self, updates):

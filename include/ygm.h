@@ -122,6 +122,27 @@ int ygm_snapshot_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off,
 int ygm_contains_v1(ygm_ctx *ctx, const uint8_t *states, const uint64_t *state_off, const uint8_t *updates,
                     const uint64_t *update_off, uint32_t n_docs, ygm_result *out);
 
+/* ---- update format V2 ------------------------------------
+ * The same operations over yjs's column-encoded update format V2 (UpdateEncoderV2 / UpdateDecoderV2,
+ * yjs Y@15400-18900; lib0 RLE column coders), used by yjs providers other than Hocuspocus's V1 path:
+ *   ygm_merge_v2            <- Y.mergeUpdatesV2(updates)                 (yjs Y@39011, V2 coders)
+ *   ygm_diff_v2             <- Y.diffUpdateV2(update, stateVector)       (yjs Y@40711)
+ *   ygm_sv_from_update_v2   <- Y.encodeStateVectorFromUpdateV2(update)   (yjs Y@37728; V1 state vector out)
+ *   ygm_convert_v1_to_v2    <- Y.convertUpdateFormatV1ToV2(update)       (yjs 13.6)
+ *   ygm_convert_v2_to_v1    <- Y.convertUpdateFormatV2ToV1(update)       (yjs 13.6)
+ * Arguments as the V1 forms.  The conversions take updates in the lazy writer's normal form (what every
+ * yjs encoder writes) and refuse others with YGM_ENONCANON, as they refuse V2 -> V1 of embed / format values
+ * holding non-integer numbers (their JSON.stringify decimal is not reproduced).  mergeUpdatesV2 of one
+ * update returns it as it is, as yjs does. */
+int ygm_merge_v2(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *upd_off, const uint32_t *upd_doc,
+                 uint32_t n_upd, uint32_t n_docs, ygm_result *out);
+int ygm_diff_v2(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, const uint8_t *sv_arena,
+                const uint64_t *sv_off, uint32_t n_docs, ygm_result *out);
+int ygm_sv_from_update_v2(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, uint32_t n_docs,
+                          ygm_result *out);
+int ygm_convert_v1_to_v2(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, uint32_t n_docs, ygm_result *out);
+int ygm_convert_v2_to_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, uint32_t n_docs, ygm_result *out);
+
 /* ---- device-resident API (inputs already in HBM; used by bench.py) --------
  * All pointers are device pointers.  doc_upd: n_docs+1 update-index offsets
  * (document d owns updates doc_upd[d] .. doc_upd[d+1]); upd_off must be
@@ -174,6 +195,19 @@ int ygm_snapshot_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_
 
 int ygm_contains_v1_device(ygm_ctx *ctx, const uint8_t *d_states, const uint64_t *d_state_off, const uint8_t *d_updates,
                            const uint64_t *d_update_off, uint32_t n_docs, void *stream, ygm_device_result *out);
+
+/* update V2, device-resident (outputs packed in document order: off[d] increasing) */
+int ygm_merge_v2_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_upd_off,
+                        const uint32_t *d_doc_upd, uint32_t n_upd, uint32_t n_docs, void *stream, ygm_device_result *out);
+int ygm_diff_v2_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
+                       const uint8_t *d_sv_arena, const uint64_t *d_sv_off, uint32_t n_docs, void *stream,
+                       ygm_device_result *out);
+int ygm_sv_from_update_v2_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes,
+                                 const uint64_t *d_doc_off, uint32_t n_docs, void *stream, ygm_device_result *out);
+int ygm_convert_v1_to_v2_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
+                                uint32_t n_docs, void *stream, ygm_device_result *out);
+int ygm_convert_v2_to_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
+                                uint32_t n_docs, void *stream, ygm_device_result *out);
 
 int ygm_stats(ygm_ctx *ctx, ygm_stats_t *out);
 const char *ygm_strerror(int code);

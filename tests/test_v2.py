@@ -96,3 +96,98 @@ def test_v2_empty_merge_is_the_empty_v2_update():
     assert st == 0 and out == bytes([0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0])
     # single input: returned as-is, not parsed (yjs Y@39011)
     assert oracle.merge_updates_v2([b"\xff\xff"]) == (0, b"\xff\xff")
+
+
+# ------------------------------------------------------------------ GPU (through the C ABI)
+@pytest.fixture(scope="module")
+def eng135():
+    from hocuspocus_amd import Engine
+    e = Engine(0, compat135=True)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from hocuspocus_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def gpu_batch(e, op, cases):
+    if op == "merge_v2":
+        return e.merge_updates_v2_batch([[bytes.fromhex(x) for x in c["in"]] for c in cases])
+    if op == "diff_v2":
+        return e.diff_update_v2_batch([bytes.fromhex(c["update"]) for c in cases], [bytes.fromhex(c["sv"]) for c in cases])
+    return e.encode_state_vector_from_update_v2_batch([bytes.fromhex(c["update"]) for c in cases])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("op", ["merge_v2", "diff_v2", "sv_v2"])
+def test_gpu_v2_vs_yjs(eng135, op):
+    cases = [c for c in load_v2_vectors() if c["op"] == op]
+    res = gpu_batch(eng135, op, cases)
+    bad = [(c, st, out and out.hex()) for c, (st, out) in zip(cases, res) if not check(c, st, out)]
+    assert not bad, (len(bad), bad[:3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("op", ["merge_v2", "diff_v2", "sv_v2"])
+def test_gpu_v2_default_mode_vs_oracle(eng, op):
+    cases = [c for c in load_v2_vectors() if c["op"] == op]
+    res = gpu_batch(eng, op, cases)
+    for c, (st, out) in zip(cases, res):
+        so, oo = run_oracle(c, compat=False)
+        if so in THROW:
+            assert st in THROW or (st == 3 and c["family"].endswith("-bad")), (c, st)
+        else:
+            assert (st, out) == (so, oo) or (st == 3 and c["family"].endswith("-bad")), (c, st, so)
+
+
+@pytest.mark.gpu
+def test_gpu_convert_vs_yjs_pairs(eng135):
+    pairs = [c for c in load_v2_vectors() if c["op"] == "conv"]
+    v1s = [bytes.fromhex(c["v1"]) for c in pairs]
+    v2s = [bytes.fromhex(c["v2"]) for c in pairs]
+    for c, v2, (st, out) in zip(pairs, v2s, eng135.convert_update_format_v1_to_v2_batch(v1s)):
+        assert (st, out) == (0, v2), c
+    refused = 0
+    for c, v1, (st, out) in zip(pairs, v1s, eng135.convert_update_format_v2_to_v1_batch(v2s)):
+        if st == 3:
+            refused += 1
+            assert oracle.convert_update_format_v2_to_v1(bytes.fromhex(c["v2"]), compat135=True)[0] == 3, c
+        else:
+            assert (st, out) == (0, v1), c
+    assert refused < len(pairs) // 3
+
+
+@pytest.mark.gpu
+def test_gpu_v2_synthetic_logs_vs_oracle(eng):
+    """C2-shaped logs (with deletions, 1-4 clients) converted to V2: merged on the GPU, then diffed and state-vectored,
+    each against the oracle; plus the V2 -> V1 -> V2 conversion round trip of the merged states."""
+    from tools import synth
+    n_docs = 1500
+    arena, upd_off, doc_upd = synth.text_updates(n_docs, 30, seed=23, del_pct=20)
+    ups = synth.split(arena, upd_off)
+    v1docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(n_docs)]
+    v2docs = [[oracle.convert_update_format_v1_to_v2(u)[1] for u in us] for us in v1docs]
+    got = eng.merge_updates_v2_batch(v2docs)
+    merged = []
+    for d, us in enumerate(v2docs):
+        exp = oracle.merge_updates_v2(us)
+        assert got[d] == exp, d
+        merged.append(exp[1])
+    svs = eng.encode_state_vector_from_update_v2_batch(merged)
+    half = []
+    for d, m in enumerate(merged):
+        assert svs[d] == oracle.encode_state_vector_from_update_v2(m), d
+        half.append(oracle.encode_state_vector_from_update_v2(oracle.merge_updates_v2(v2docs[d][: len(v2docs[d]) // 2])[1])[1])
+    diffs = eng.diff_update_v2_batch(merged, half)
+    for d, m in enumerate(merged):
+        assert diffs[d] == oracle.diff_update_v2(m, half[d]), d
+    back = eng.convert_update_format_v2_to_v1_batch(merged)
+    for d, m in enumerate(merged):
+        assert back[d] == oracle.convert_update_format_v2_to_v1(m), d
+    again = eng.convert_update_format_v1_to_v2_batch([b for _, b in back])
+    assert again == [(0, m) for m in merged]

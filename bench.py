@@ -14,6 +14,8 @@ the lean kernel -- asserted -- so no step needs the host-driven tiers).  Beside 
   c4       config C4 (configs[3]): 1 000 000 merged Y.Text states (1-16 clients, log-uniform 1-8 KB,
            3.2 GB) sharded over the ranks, encodeStateVectorFromUpdate and diffUpdate against per-document
            state vectors (the mass-reconnect Step1 -> Step2 path, MessageReceiver.ts:137-155)
+  v2       SURVEY.md §8f-4: the C2 merge with the updates in format V2 (Y.mergeUpdatesV2), and the V1 <-> V2
+           conversions of its 2 M updates
   cpu_baseline  the reference yjs path on the GPU box's host cores (yjs 13.5.16 from the image's
            JupyterLab bundle on Node worker_threads, kind "reference") with the C restatement
            (oracle/yjs_oracle.c on pthreads, kind "port") nested beside it; c4 carries its own
@@ -61,6 +63,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads / workers (0: the cores granted, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-yjs", action="store_true", help="skip the Node / yjs leg of the CPU baseline")
+    ap.add_argument("--no-v2", dest="v2", action="store_false", help="skip the update-V2 (f-4) block")
     ap.add_argument("--f1-docs", type=int, default=10000, help="documents of the f1 (doc-normalized snapshot) block (0: skip)")
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
                     help="skip the host_api block (host arrays through the pinned / two-stream host API)")
@@ -332,6 +335,65 @@ def f1_block(be, args, steps=5):
     return blk
 
 
+def v2_block(be, args, steps=5):
+    """the C2 headline workload in update format V2 (the updates converted from the C2 V1 corpus by
+    ygm_convert_v1_to_v2): Y.mergeUpdatesV2 per document, inputs resident in HBM.  Per step: the V2 -> V1 transcoding
+    kernels, the V1 merge cascade, the V1 -> V2 kernels (two size reads between them); plus the conversions alone."""
+    from hocuspocus_amd import Engine
+    import oracle
+    from tools import synth
+    e = Engine(be.dev.index)
+    idx = synth.partition("c2-", args.docs, 1, 0)
+    a1, o1, d1 = synth.text_updates_docs(idx, args.updates)
+    n, n_upd = len(idx), int(d1[-1])
+    st, off, ln, data = e._raw(e._conv_packed("ygm_convert_v1_to_v2", a1, o1))
+    assert (st == 0).all()
+    o2 = np.zeros(n_upd + 1, np.uint64)
+    o2[1:] = np.cumsum(ln.astype(np.uint64))
+    assert (np.asarray(off, np.uint64) == o2[:-1]).all()   # the host API packs outputs in order, without gaps
+    a2 = np.frombuffer(bytes(data), np.uint8)[:int(o2[-1])].copy()
+    da, do, dd = be.put(a2, 64), be.put(o2.view(np.int64)), be.put(d1.view(np.int32))
+    r = e.merge_v2_device(da, len(a2), do, dd, n_upd, n, be.stream.cuda_stream)
+    be.sync()
+    s0 = e.stats()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = e.merge_v2_device(da, len(a2), do, dd, n_upd, n, be.stream.cuda_stream)
+    be.sync()
+    wall = (time.perf_counter() - t0) / steps
+    s1 = e.stats()
+    kms = (s1.kernel_ms - s0.kernel_ms) / steps
+    algo = len(a2) + int(r.payload_bytes)
+    st2, off2, ln2, out2 = be.fetch(r, n)
+    ups2 = synth.split(a2, o2)
+    checked = 0
+    for d in range(0, n, max(1, n // 100)):
+        exp = oracle.merge_updates_v2(ups2[d1[d]:d1[d + 1]])
+        assert exp == (int(st2[d]), out2[int(off2[d]):int(off2[d]) + int(ln2[d])]), f"V2 parity failure on document {d}"
+        checked += 1
+    conv = {}
+    a1d, o1d = be.put(a1, 64), be.put(o1.view(np.int64))
+    for op, (da_, do_, nb) in (("v1_to_v2", (a1d, o1d, len(a1))), ("v2_to_v1", (da, do, len(a2)))):
+        e.doc_v2_device(op, da_, nb, do_, n_upd, stream=be.stream.cuda_stream)
+        be.sync()
+        c0 = e.stats()
+        rr = e.doc_v2_device(op, da_, nb, do_, n_upd, stream=be.stream.cuda_stream)
+        be.sync()
+        cms = e.stats().kernel_ms - c0.kernel_ms
+        conv[op] = {"updates": n_upd, "ms": round(cms, 4), "value": round((nb + int(rr.payload_bytes)) / cms / 1e3, 3), "unit": "MB/s"}
+    blk = {"workload": f"C2 in update format V2: {n} docs x {args.updates} updates (V2, {len(a2)} bytes; the V1 corpus is "
+                       f"{len(a1)} bytes), batched Y.mergeUpdatesV2, inputs resident in HBM",
+           "docs": n, "updates": n_upd, "bytes_in": len(a2), "bytes_out": int(r.payload_bytes),
+           "value": round(algo / kms / 1e3, 3), "unit": "MB/s", "docs_per_s": round(n / kms * 1e3, 1), "ms_per_step": round(kms, 4),
+           "wall_ms_per_step": round(wall * 1e3, 4),
+           "roofline": roof(algo, kms, "k_v21_count/write + V1 merge cascade + k_v12_count/write (one lane per update / document)", None),
+           "convert": conv, "parity": f"bit-exact vs oracle (yjs_oracle_v2.c) on {checked} sampled docs; tests/test_v2.py: 4887 yjs vectors"}
+    if not args.no_cpu_baseline and not args.no_yjs:
+        blk["cpu_baseline"] = cpu_yjs("merge_v2", {"arena": a2, "upd_off": o2, "doc_upd": d1}, cpu_cores(args), min(n, 4000))
+    e.close()
+    return blk
+
+
 def host_api_doc(be, c, op, n, reps=3):
     from hocuspocus_amd import Engine
     import oracle
@@ -476,7 +538,7 @@ def cpu_yjs(kind, c, cores, k):
         return None
     d = tempfile.mkdtemp(prefix="ygm_yjs_")
     try:
-        if kind == "merge":
+        if kind.startswith("merge"):
             u_end = int(c["doc_upd"][k])
             c["arena"][:int(c["upd_off"][u_end])].tofile(os.path.join(d, "arena.bin"))
             c["upd_off"][:u_end + 1].astype(np.uint64).tofile(os.path.join(d, "off.bin"))
@@ -496,7 +558,7 @@ def cpu_yjs(kind, c, cores, k):
         return {"value": round(j["algo_bytes"] / j["seconds"] / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "reference",
                 "docs_per_s": round(k / j["seconds"], 1),
                 "sample": f"yjs 13.5.16 (JupyterLab bundle in the image; the reference pins 13.6.26) Y."
-                          f"{ {'merge': 'mergeUpdates', 'sv': 'encodeStateVectorFromUpdate', 'diff': 'diffUpdate', 'snapshot': 'encodeStateAsUpdate(applyUpdate(new Doc, u))'}[kind]} over the first "
+                          f"{ {'merge': 'mergeUpdates', 'merge_v2': 'mergeUpdatesV2', 'sv': 'encodeStateVectorFromUpdate', 'diff': 'diffUpdate', 'snapshot': 'encodeStateAsUpdate(applyUpdate(new Doc, u))'}[kind]} over the first "
                           f"{k} documents on Node {ver} worker_threads x {cores}, op loop only, slowest worker {j['seconds']:.2f} s"}
     finally:
         shutil.rmtree(d, ignore_errors=True)
@@ -606,6 +668,9 @@ def run_rank(args, rank, world, dist, be, dev=None):
     # ---- f-1: doc-normalized snapshots of merged debounce logs (C2 with 20 % deletes)
     if args.f1_docs and rank == 0 and not args.dry_run:
         line["f1"] = f1_block(be, args)
+    # ---- f-4: the C2 merge in update format V2
+    if args.v2 and rank == 0 and not args.dry_run:
+        line["v2"] = v2_block(be, args)
     # ---- CPU baselines (rank 0 at N = 1 only)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         cores = cpu_cores(args)

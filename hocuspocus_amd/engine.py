@@ -315,6 +315,14 @@ class Engine:
             raise YjsError(st)
         return self._unpack(res)
 
+    def _conv_packed(self, fn, arena, doc_off):
+        """Packed host-array form of a unary V2 call (ygm_sv_from_update_v2 / ygm_convert_*): the raw _Result."""
+        res = _Result()
+        st = getattr(lib(), fn)(self._ctx, _ptr(arena), _ptr(doc_off), len(doc_off) - 1, ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return res
+
     def encode_state_vector_from_update_v2_batch(self, updates):
         """Y.encodeStateVectorFromUpdateV2 per update (the state vector is V1-encoded, as yjs's)."""
         return self._unary_v2("ygm_sv_from_update_v2", updates)

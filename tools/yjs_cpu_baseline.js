@@ -3,7 +3,8 @@
 // Y.diffUpdate / Y.encodeStateVectorFromUpdate per document over a contiguous shard of a corpus
 // that bench.py wrote to disk.  Only the op loop is timed; the job's time is the slowest worker.
 //
-//   node tools/yjs_cpu_baseline.js <dir> <op: merge|sv|diff|snapshot> <workers>
+//   node tools/yjs_cpu_baseline.js <dir> <op: merge|merge_v2|sv|diff|snapshot> <workers>
+//   (merge_v2: Y.mergeUpdatesV2 over update-V2 inputs)
 //   (snapshot: Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), u)), what extension-database stores)
 //   <dir>/arena.bin, <dir>/off.bin (u64 update or document offsets), <dir>/docs.bin (u32 update index
 //   per document, merge), <dir>/sv.bin + <dir>/svoff.bin (diff)
@@ -19,7 +20,7 @@ function u32 (buf) { return new Uint32Array(buf.buffer, buf.byteOffset, buf.leng
 if (isMainThread) {
   const [dir, op, nw] = process.argv.slice(2)
   const workers = parseInt(nw, 10)
-  const docs = op === 'merge' ? u32(fs.readFileSync(path.join(dir, 'docs.bin'))).length - 1 : u64(fs.readFileSync(path.join(dir, 'off.bin'))).length - 1
+  const docs = op.startsWith('merge') ? u32(fs.readFileSync(path.join(dir, 'docs.bin'))).length - 1 : u64(fs.readFileSync(path.join(dir, 'off.bin'))).length - 1
   let done = 0; let slowest = 0; let algo = 0
   for (let w = 0; w < workers; w++) {
     const d0 = Math.floor(docs * w / workers); const d1 = Math.floor(docs * (w + 1) / workers)
@@ -36,7 +37,7 @@ if (isMainThread) {
   const arena = fs.readFileSync(path.join(dir, 'arena.bin'))
   const off = u64(fs.readFileSync(path.join(dir, 'off.bin')))
   const jobs = []
-  if (op === 'merge') {
+  if (op.startsWith('merge')) {
     const docs = u32(fs.readFileSync(path.join(dir, 'docs.bin')))
     for (let d = d0; d < d1; d++) {
       const us = []
@@ -55,7 +56,7 @@ if (isMainThread) {
   const t0 = process.hrtime.bigint()
   for (const j of jobs) {
     let out
-    if (op === 'merge') { out = Y.mergeUpdates(j); for (const u of j) algo += u.length } else if (op === 'diff') { out = Y.diffUpdate(j[0], j[1]); algo += j[0].length + j[1].length } else if (op === 'snapshot') { const d = new Y.Doc(); Y.applyUpdate(d, j); out = Y.encodeStateAsUpdate(d); algo += j.length } else { out = Y.encodeStateVectorFromUpdate(j); algo += j.length }
+    if (op.startsWith('merge')) { out = op === 'merge' ? Y.mergeUpdates(j) : Y.mergeUpdatesV2(j); for (const u of j) algo += u.length } else if (op === 'diff') { out = Y.diffUpdate(j[0], j[1]); algo += j[0].length + j[1].length } else if (op === 'snapshot') { const d = new Y.Doc(); Y.applyUpdate(d, j); out = Y.encodeStateAsUpdate(d); algo += j.length } else { out = Y.encodeStateVectorFromUpdate(j); algo += j.length }
     algo += out.length
   }
   const seconds = Number(process.hrtime.bigint() - t0) / 1e9

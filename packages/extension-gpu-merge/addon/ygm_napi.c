@@ -15,6 +15,7 @@
  */
 #include <node_api.h>
 #include <stdlib.h>
+#include <stdint.h>
 #include <string.h>
 
 #include "../../../include/ygm.h"
@@ -134,6 +135,11 @@ static void job_execute(napi_env env, void *data) {
   else if (j->op == 1) j->rc = ygm_diff_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
   else if (j->op == 3) j->rc = ygm_snapshot_v1(j->h->ctx, j->arena, j->off, j->n_docs, &r);
   else if (j->op == 4) j->rc = ygm_contains_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
+  else if (j->op == 10) j->rc = ygm_merge_v2(j->h->ctx, j->arena, j->off, j->docs, j->n_upd, j->n_docs, &r);
+  else if (j->op == 11) j->rc = ygm_diff_v2(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
+  else if (j->op == 12) j->rc = ygm_sv_from_update_v2(j->h->ctx, j->arena, j->off, j->n_docs, &r);
+  else if (j->op == 13) j->rc = ygm_convert_v1_to_v2(j->h->ctx, j->arena, j->off, j->n_docs, &r);
+  else if (j->op == 14) j->rc = ygm_convert_v2_to_v1(j->h->ctx, j->arena, j->off, j->n_docs, &r);
   else j->rc = ygm_sv_from_update_v1(j->h->ctx, j->arena, j->off, j->n_docs, &r);
   if (j->rc != YGM_OK) return;
   /* results are context-owned: copy out before the next batch may reuse them */
@@ -202,11 +208,12 @@ static napi_value submit(napi_env env, Job *j, const char *name) {
 /* mergeMany(h, arena, lens, docs, nDocs) */
 static napi_value js_merge(napi_env env, napi_callback_info info) {
   size_t argc = 5; napi_value argv[5];
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  void *opd = NULL;
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, &opd));
   if (argc < 5) { napi_throw_type_error(env, NULL, "mergeMany(handle, arena, lens, docs, nDocs)"); return NULL; }
   Handle *h = get_handle(env, argv[0]);
   if (!h) return NULL;
-  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = 0; j->h = h;
+  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = opd ? (int)(intptr_t)opd : 0; j->h = h;
   size_t an, ln, dn; void *lens = NULL;
   if (get_bytes(env, argv[1], (void **)&j->arena, &an) || get_bytes(env, argv[2], &lens, &ln) || get_bytes(env, argv[3], (void **)&j->docs, &dn)) {
     free(lens); job_free(j); napi_throw_type_error(env, NULL, "mergeMany: expected Buffer / Uint32Array arguments"); return NULL;
@@ -223,11 +230,12 @@ static napi_value js_merge(napi_env env, napi_callback_info info) {
 /* diffMany(h, arena, lens, svArena, svLens) */
 static napi_value js_diff(napi_env env, napi_callback_info info) {
   size_t argc = 5; napi_value argv[5];
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  void *opd = NULL;
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, &opd));
   if (argc < 5) { napi_throw_type_error(env, NULL, "diffMany(handle, arena, lens, svArena, svLens)"); return NULL; }
   Handle *h = get_handle(env, argv[0]);
   if (!h) return NULL;
-  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = 1; j->h = h;
+  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = opd ? (int)(intptr_t)opd : 1; j->h = h;
   size_t an, ln, sn, sln; void *lens = NULL, *slens = NULL;
   if (get_bytes(env, argv[1], (void **)&j->arena, &an) || get_bytes(env, argv[2], &lens, &ln) || get_bytes(env, argv[3], (void **)&j->sv, &sn) ||
       get_bytes(env, argv[4], &slens, &sln) || ln != sln) {
@@ -244,11 +252,12 @@ static napi_value js_diff(napi_env env, napi_callback_info info) {
 /* svMany(h, arena, lens) */
 static napi_value js_sv(napi_env env, napi_callback_info info) {
   size_t argc = 3; napi_value argv[3];
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  void *opd = NULL;
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, &opd));
   if (argc < 3) { napi_throw_type_error(env, NULL, "svMany(handle, arena, lens)"); return NULL; }
   Handle *h = get_handle(env, argv[0]);
   if (!h) return NULL;
-  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = 2; j->h = h;
+  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = opd ? (int)(intptr_t)opd : 2; j->h = h;
   size_t an, ln; void *lens = NULL;
   if (get_bytes(env, argv[1], (void **)&j->arena, &an) || get_bytes(env, argv[2], &lens, &ln)) {
     free(lens); job_free(j); napi_throw_type_error(env, NULL, "svMany: bad arguments"); return NULL;
@@ -309,6 +318,12 @@ static napi_value init(napi_env env, napi_value exports) {
     { "svMany", NULL, js_sv, NULL, NULL, NULL, napi_default, NULL },
     { "snapshotMany", NULL, js_snapshot, NULL, NULL, NULL, napi_default, NULL },
     { "containsMany", NULL, js_contains, NULL, NULL, NULL, napi_default, NULL },
+    /* update format V2 (yjs mergeUpdatesV2 / diffUpdateV2 / encodeStateVectorFromUpdateV2 / 13.6 convertUpdateFormat*) */
+    { "mergeManyV2", NULL, js_merge, NULL, NULL, NULL, napi_default, (void *)(intptr_t)10 },
+    { "diffManyV2", NULL, js_diff, NULL, NULL, NULL, napi_default, (void *)(intptr_t)11 },
+    { "svManyV2", NULL, js_sv, NULL, NULL, NULL, napi_default, (void *)(intptr_t)12 },
+    { "convertManyV1ToV2", NULL, js_sv, NULL, NULL, NULL, napi_default, (void *)(intptr_t)13 },
+    { "convertManyV2ToV1", NULL, js_sv, NULL, NULL, NULL, napi_default, (void *)(intptr_t)14 },
     { "stats", NULL, js_stats, NULL, NULL, NULL, napi_default, NULL },
     { "strerror", NULL, js_strerror, NULL, NULL, NULL, napi_default, NULL },
   };

@@ -17,6 +17,12 @@ export declare class GpuEngine {
   mergeMany (docs: Uint8Array[][]): Promise<(Uint8Array | YgmError)[]>
   diffMany (states: Uint8Array[], svs: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
   stateVectorsMany (states: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  /** update format V2: Y.mergeUpdatesV2 / Y.diffUpdateV2 / Y.encodeStateVectorFromUpdateV2 / Y.convertUpdateFormat* (yjs 13.6) */
+  mergeManyV2 (docs: Uint8Array[][]): Promise<(Uint8Array | YgmError)[]>
+  diffManyV2 (states: Uint8Array[], stateVectors: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  stateVectorsManyV2 (states: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  convertManyV1ToV2 (updates: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
+  convertManyV2ToV1 (updates: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
   /** Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), update)) (doc-normalized snapshot, SURVEY.md §8f-1) */
   snapshot (update: Uint8Array): Promise<Uint8Array>
   snapshotMany (states: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>

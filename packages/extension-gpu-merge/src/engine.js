@@ -99,19 +99,19 @@ class GpuEngine {
   _run (op, jobs) {
     const run = () => {
       const a = loadAddon()
-      if (op === 'merge') {
+      if (op === 'merge' || op === 'mergeV2') {
         const blobs = []; const docs = []
         jobs.forEach((ups, d) => { for (const u of ups) { blobs.push(u); docs.push(d) } })
         const { arena, lens } = packBlobs(blobs)
-        return a.mergeMany(this.handle, arena, lens, Uint32Array.from(docs), jobs.length)
+        return (op === 'merge' ? a.mergeMany : a.mergeManyV2)(this.handle, arena, lens, Uint32Array.from(docs), jobs.length)
       }
-      if (op === 'diff' || op === 'contains') {
+      if (op === 'diff' || op === 'contains' || op === 'diffV2') {
         const u = packBlobs(jobs.map(j => j[0])); const s = packBlobs(jobs.map(j => j[1]))
-        return (op === 'diff' ? a.diffMany : a.containsMany)(this.handle, u.arena, u.lens, s.arena, s.lens)
+        return ({ diff: a.diffMany, contains: a.containsMany, diffV2: a.diffManyV2 })[op](this.handle, u.arena, u.lens, s.arena, s.lens)
       }
       const u = packBlobs(jobs)
-      if (op === 'snapshot') return a.snapshotMany(this.handle, u.arena, u.lens)
-      return a.svMany(this.handle, u.arena, u.lens)
+      const unary = { snapshot: a.snapshotMany, sv: a.svMany, svV2: a.svManyV2, v1ToV2: a.convertManyV1ToV2, v2ToV1: a.convertManyV2ToV1 }
+      return unary[op](this.handle, u.arena, u.lens)
     }
     const p = this.chain.then(run, run)
     this.chain = p.catch(() => {})
@@ -137,6 +137,14 @@ class GpuEngine {
     const r = await this._run('contains', states.map((s, i) => [s, updates[i]]))
     return unpack(r).map(x => x instanceof Error ? x : x[0] === 1)
   }
+
+  /** update format V2 (yjs providers other than Hocuspocus's V1 path): Y.mergeUpdatesV2 / Y.diffUpdateV2 /
+   *  Y.encodeStateVectorFromUpdateV2 / yjs 13.6 Y.convertUpdateFormatV1ToV2 / V2ToV1, as explicit batches */
+  async mergeManyV2 (docs) { const r = await this._run('mergeV2', docs); return unpack(r) }
+  async diffManyV2 (states, svs) { const r = await this._run('diffV2', states.map((s, i) => [s, svs[i]])); return unpack(r) }
+  async stateVectorsManyV2 (states) { const r = await this._run('svV2', states); return unpack(r) }
+  async convertManyV1ToV2 (updates) { const r = await this._run('v1ToV2', updates); return unpack(r) }
+  async convertManyV2ToV1 (updates) { const r = await this._run('v2ToV1', updates); return unpack(r) }
 
   stats () { return loadAddon().stats(this.handle) }
   close () { if (this.handle) { loadAddon().close(this.handle); this.handle = null } }

@@ -29,6 +29,9 @@ class CpuDouble { // test double (never shipped): same API as GpuEngine
       return Y.equalSnapshots(Y.snapshot(d), Y.snapshot(p))
     })
   }
+  async mergeManyV2 (docs) { this.calls++; return docs.map(u => Y.mergeUpdatesV2(u)) }
+  async diffManyV2 (states, svs) { this.calls++; return states.map((u, i) => Y.diffUpdateV2(u, svs[i])) }
+  async stateVectorsManyV2 (states) { this.calls++; return states.map(u => Y.encodeStateVectorFromUpdateV2(u)) }
   close () {}
 }
 
@@ -365,6 +368,28 @@ test('sync responder answers a SyncStep1 batch', async (engine) => {
     Y.applyUpdate(client, a.payload)
     assert.strictEqual(client.getText('t').toString(), hp.documents.get(n).getText('t').toString())
   })
+})
+
+test('update V2 batches match yjs mergeUpdatesV2 / diffUpdateV2 / encodeStateVectorFromUpdateV2', async (engine) => {
+  const docs = []; const logs = []
+  for (let k = 0; k < 24; k++) {
+    const a = new Y.Doc(); a.clientID = 1000 + k; const b = new Y.Doc(); b.clientID = 5000 + k
+    const log = []
+    for (const d of [a, b]) d.on('updateV2', (u, origin) => { if (origin !== 'remote') log.push(u) })
+    a.transact(() => a.getText('t').insert(0, 'hello ' + k, { bold: true }))
+    Y.applyUpdateV2(b, Y.encodeStateAsUpdateV2(a), 'remote')
+    b.transact(() => { b.getText('t').insert(2, 'é😀'); b.getMap('m').set('k', { n: k, s: 'x' }) })
+    a.transact(() => a.getText('t').delete(0, 3))
+    a.getXmlFragment('x').insert(0, [new Y.XmlElement('p')])
+    docs.push(a); logs.push(log)
+  }
+  const merged = await engine.mergeManyV2(logs)
+  logs.forEach((l, i) => assert.strictEqual(Buffer.from(merged[i]).toString('hex'), Buffer.from(Y.mergeUpdatesV2(l)).toString('hex')))
+  const svs = await engine.stateVectorsManyV2(merged)
+  merged.forEach((m, i) => assert.strictEqual(Buffer.from(svs[i]).toString('hex'), Buffer.from(Y.encodeStateVectorFromUpdateV2(m)).toString('hex')))
+  const peer = logs.map(l => Y.encodeStateVectorFromUpdateV2(Y.mergeUpdatesV2(l.slice(0, 2))))
+  const diffs = await engine.diffManyV2(merged, peer)
+  merged.forEach((m, i) => assert.strictEqual(Buffer.from(diffs[i]).toString('hex'), Buffer.from(Y.diffUpdateV2(m, peer[i])).toString('hex')))
 })
 
 async function main () {

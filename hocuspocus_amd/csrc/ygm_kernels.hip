@@ -1928,7 +1928,7 @@ YDEV bool big_ds_decode(const uint8_t* u0p, uint32_t ds0, uint32_t n0, uint32_t*
 YDEV_NI uint64_t big_skip_global(const uint8_t* u0p, uint32_t n0, uint32_t pos) {
   GCur g; g.init(u0p, n0); g.pos = pos;
   uint32_t kind;
-  const bool ok = big_skip(g, kind);
+  const bool ok = big_skip<true>(g, kind);
   return (uint64_t)g.pos | ((uint64_t)(kind & 1u) << 32) | (ok ? 0ull : 1ull << 63);
 }
 
@@ -1944,10 +1944,10 @@ YDEV void big_spec(BigTile& T, uint32_t at, uint32_t mis, uint32_t tn, uint32_t 
   for (uint32_t i = t0; i < BT_CH; i += BIG_THREADS) {
     uint16_t e = 0;
     // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item
-    // ref 1..7 without bit 0x20 next to an origin (a rejected position falls back to a global parse)
+    // ref 1..8 without bit 0x20 next to an origin (a rejected position falls back to a global parse)
     const uint32_t ib = tp[mis + i];
     const uint32_t rf = ib & 31u;
-    if (at + i < n0 && (ib == 0u || (rf >= 1u && rf <= 7u && !((ib & 0xC0u) && (ib & 0x20u))))) {
+    if (at + i < n0 && (ib == 0u || (rf >= 1u && rf <= 8u && !((ib & 0xC0u) && (ib & 0x20u))))) {
       GCur t; t.init(tp, tn); t.pos = mis + i;
       uint32_t kind;
       if (big_skip(t, kind, 8) && !t.err) e = (uint16_t)((t.pos - mis) | (kind == 0 ? 0x8000u : 0u));

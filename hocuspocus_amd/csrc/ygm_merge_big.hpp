@@ -10,7 +10,7 @@
 // App. B.5) is: per client (descending), the pieces -- U0's block as one piece, every log struct
 // as one piece -- in clock order, a Skip over every gap, U0's block bytes verbatim; and the delete
 // sets are unioned by R-DS with U0's sorted list streamed.  Anything else (overlaps, input Skips,
-// GC-GC junctions between sources, re-encoded structs, ContentAny / ContentDoc in U0, 13.5
+// GC-GC junctions between sources, re-encoded structs, ContentDoc in U0, 13.5
 // multi-client delete sets, malformed input) is deferred to the exact sequential kernel.
 //
 //   walk   lane 0 walks U0 with a 16-byte register-window cursor (GCur): every struct is validated
@@ -194,15 +194,53 @@ YDEV GStruct big_struct(GCur& c, uint32_t flags) {
       if (tr == 3 || tr == 5) { uint32_t l; const uint32_t s = c.buf(l); if (c.err || gutf8_u16(c.p + s, l) < 0) return R; }
       R.len = 1; break;
     }
-    default: return R;                                             // Any / Doc (validated by the general path), bad refs
+    case 8: {                                                      // ContentAny (e.g. XmlElement attributes)
+      const uint64_t n = c.vu(); if (c.err || n == 0) return R;
+      Cur q{c.p, c.pos, c.end, 0, 0};
+      for (uint64_t k = 0; k < n && !q.err; k++) any_value(q, nc, flags);   // readAny + would writeAny reproduce it
+      if (q.err) return R;
+      c.pos = q.pos;
+      R.len = n; break;
+    }
+    default: return R;                                             // Doc (validated by the general path), bad refs
   }
   R.ok = !c.err && !c.nm && !nc;
   return R;
 }
 
+// one Any value skipped over global memory (lib0 readAny's layout); false on an unknown tag or nesting
+// deeper than MAX_DEPTH (the document then goes on to the general path).  Out of line: the chain follow's
+// fallback parse only.
+YDEV_NI bool gany_skip(GCur& c, uint64_t n) {
+  uint32_t rem[MAX_DEPTH + 1]; uint8_t obj[MAX_DEPTH + 1];
+  int d = 0; rem[0] = n > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)n; obj[0] = 0;
+  while (!c.err) {
+    if (rem[d] == 0) { if (d == 0) return true; d--; continue; }
+    rem[d]--;
+    if (obj[d]) { uint32_t kl; c.buf(kl); if (c.err) return false; }
+    const uint32_t tag = c.u8();
+    switch (tag) {
+      case 127: case 126: case 121: case 120: break;
+      case 125: { uint32_t r = c.u8(); while ((r & 128u) && !c.err) r = c.u8(); break; }
+      case 124: if (c.end - c.pos < 4) c.fail(ST_MALFORMED); else c.pos += 4; break;
+      case 123: case 122: if (c.end - c.pos < 8) c.fail(ST_MALFORMED); else c.pos += 8; break;
+      case 119: case 116: { uint32_t l; c.buf(l); break; }
+      case 117: case 118: {
+        const uint64_t k = c.vu();
+        if (c.err || d + 1 > MAX_DEPTH || k > (uint64_t)(c.end - c.pos)) return false;
+        d++; rem[d] = (uint32_t)k; obj[d] = tag == 118;
+        break;
+      }
+      default: return false;
+    }
+  }
+  return false;
+}
+
 // Skip-only parse of one U0 struct (the sequential part of the walk): the bytes it spans and its
 // kind (0 GC, 1 Item); validation and lengths come later, in parallel (big_struct).  false: a
 // Skip, Any / Doc content or an unknown ref -- the document goes on to the general path.
+template <bool ANY = false>   // ANY: any ContentAny (the out-of-line fallback parse); else scalar values only
 YDEV bool big_skip(GCur& c, uint32_t& kind, uint64_t jcap = ~0ull) {   // jcap: most ContentJSON entries taken
   const uint32_t info = c.u8();
   kind = 1;
@@ -222,6 +260,22 @@ YDEV bool big_skip(GCur& c, uint32_t& kind, uint64_t jcap = ~0ull) {   // jcap: 
     case 3: case 4: case 5: c.buf(l); break;
     case 6: c.buf(l); c.buf(l); break;
     case 7: { const uint64_t tr = c.vu(); if (tr == 3 || tr == 5) c.buf(l); break; }
+    case 8: {
+      const uint64_t n = c.vu();
+      if (c.err) return false;
+      if (ANY) { if (!gany_skip(c, n)) return false; break; }
+      if (n > jcap) return false;
+      for (uint64_t k = 0; k < n && !c.err; k++) {   // the speculative parse takes scalar values only (attributes)
+        const uint32_t tag = c.u8();
+        if (tag == 119u || tag == 116u) c.buf(l);
+        else if (tag == 125u) { uint32_t r = c.u8(); while ((r & 128u) && !c.err) r = c.u8(); }
+        else if (tag == 124u) c.pos += 4;
+        else if (tag == 123u || tag == 122u) c.pos += 8;
+        else if (tag < 120u) return false;   // (120, 121, 126, 127: no payload; arrays / objects: the fallback parse)
+        if (c.pos > c.end) c.fail(ST_MALFORMED);
+      }
+      break;
+    }
     default: return false;
   }
   return !c.err;

@@ -625,10 +625,27 @@ def test_large_documents_c3_c5_vs_oracle(eng, xml):
         arena, upd_off, doc_upd = synth.big_docs(60, 300000, 1024, max_clients=64, max_k=200, seed=3)
     ups = synth.split(arena, upd_off)
     docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(len(doc_upd) - 1)]
+    st0 = eng.stats()
     res = eng.merge_updates_batch(docs)
     bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
     assert not bad, (len(bad), bad[:5])
     assert all(st == 0 for st, _ in res)
+    if xml:   # XmlElement attributes (ContentAny map entries) are in the snapshots and the large-document tier takes them
+        assert all(us[0].count(bytes([0x28, 0x00])) > 100 for us in docs)
+        assert eng.stats().docs_seq - st0.docs_seq == 0
+
+
+def test_large_document_10mb_vs_oracle(eng):
+    # BASELINE C3's largest size: one 10 MB [snapshot, ...log] document through the large-document tier
+    from tools import synth
+    arena, upd_off, doc_upd = synth.big_docs(1, 10_000_000, 1024, max_clients=64, max_k=200, seed=9)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[0]:doc_upd[1]]]
+    assert len(docs[0][0]) > 9_000_000
+    st0 = eng.stats()
+    res = eng.merge_updates_batch(docs)
+    assert same(oracle.merge_updates(docs[0]), res[0])
+    assert res[0][0] == 0 and eng.stats().docs_big - st0.docs_big == 1
 
 
 def test_large_document_tile_edges_vs_oracle(eng):

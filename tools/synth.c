@@ -236,7 +236,8 @@ void synth_text_states_take(void *h, uint8_t *buf, uint64_t *doc_off, uint8_t *s
  * The snapshot is one merged update: client blocks in descending client order, each a run of
  * structs with contiguous clocks -- Item ContentString (ASCII and 2-byte UTF-8), ContentDeleted,
  * GC, and with `xml` ContentType (XmlElement "paragraph" / XmlText), ContentFormat and
- * ContentEmbed -- every Item after a block's first carrying an origin (and sometimes a right
+ * ContentEmbed, and XmlElement attributes (map entries: parent id, parentSub key, ContentAny) -- every
+ * other Item after a block's first carrying an origin (and sometimes a right
  * origin) on a random earlier id; then a sorted, merged delete set over the deleted runs.  The
  * log holds k-1 updates: inserts continuing a client's clock (1-3 string structs) and
  * delete-set-only updates over random existing ids.  Sizes follow size(r) = max_bytes * r^-0.8
@@ -280,6 +281,14 @@ size_t synth_big_docs(uint64_t seed, uint32_t n_docs, uint64_t max_bytes, uint64
           buf[b++] = 0; b += vu(buf + b, ln); clock += ln; nst++; last_gc = 1; continue;
         }
         last_gc = 0;
+        if (xml && kind >= 47 && kind < 53) {            /* XmlElement attribute: a map entry (parent id + parentSub key), ContentAny */
+          buf[b++] = 8 | 0x20; buf[b++] = 0;
+          b += vu(buf + b, clients[rbelow(&r, nc)]); b += vu(buf + b, (uint32_t)rbelow(&r, 50));
+          if (rbelow(&r, 2)) b += w_str(buf + b, "level", 5); else b += w_str(buf + b, "class", 5);
+          b += vu(buf + b, 1);
+          if (rbelow(&r, 2)) { buf[b++] = 119; b += w_str(buf + b, "heading", 7); } else { buf[b++] = 125; buf[b++] = (uint8_t)rbelow(&r, 60); }
+          clock += 1; nst++; continue;
+        }
         uint8_t info; int has_o = nst > 0, has_r = nst > 0 && rbelow(&r, 3) == 0;
         uint32_t ref;
         if (kind < 26) ref = 1;                          /* ContentDeleted */

@@ -724,12 +724,15 @@ def big_line(args):
     cdt = time.perf_counter() - t0
     assert (st == 0).all()
     sizes = np.diff(upd_off[doc_upd].astype(np.int64))
+    port = {"ms": round(cdt * 1e3, 3), "MBps": round(calgo / cdt / 1e6, 1), "cores": cores, "kind": "port",
+            "sample": "all documents of the batch through oracle/yjs_oracle.c yo_merge_batch, one pass"}
+    y = None if (args.no_yjs or args.no_cpu_baseline) else cpu_yjs("merge", {"arena": arena, "upd_off": upd_off, "doc_upd": doc_upd}, cores, n)
+    if y and "value" in y:
+        y["ms"] = round(n / y["docs_per_s"] * 1e3, 3)   # the whole batch (slowest worker)
     print(json.dumps({"config": args.big.upper(), "op": "merge", "docs": n, "bytes_in": len(arena), "largest_doc": int(sizes.max()),
                       "gpu_ms": round(ms, 3), "gpu_MBps": round(algo / ms / 1e3, 1), "gpu_docs_per_s": round(n / ms * 1e3),
                       "docs_big_tier": s1.docs_big - s0.docs_big, "docs_seq_tier": s1.docs_seq - s0.docs_seq,
-                      "cpu_baseline": {"ms": round(cdt * 1e3, 3), "MBps": round(calgo / cdt / 1e6, 1), "cores": cores, "kind": "port",
-                                       "sample": "all documents of the batch through oracle/yjs_oracle.c yo_merge_batch, one pass"}}),
-          flush=True)
+                      "cpu_baseline": dict(port, yjs=y)}), flush=True)
 
 
 def main():

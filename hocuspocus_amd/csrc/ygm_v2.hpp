@@ -100,7 +100,7 @@ struct Dec2 {
   YDEV int st() const { return err ? err : rest.err; }
 };
 
-YDEV_NI void open2(Dec2& v, const uint8_t* u, uint32_t n, uint32_t flags) {
+YDEV void open2(Dec2& v, const uint8_t* u, uint32_t n, uint32_t flags) {
   v.rest = Cur{u, 0, n, 0, 0};
   v.err = 0; v.nkeys = 0; v.sb = 0; v.sn = 0; v.str = u;
   (void)v.rest.vu();
@@ -309,10 +309,12 @@ YDEV_NI void json_to_any(const uint8_t* s, uint32_t n, Out& o, uint32_t flags) {
 
 // ---------------------------------------------------------------- V2 -> V1
 // arena_off: the update's offset in the V2 arena (placeholders name absolute offsets)
-YDEV_NI int v2_json(Dec2& v, Out& o, uint64_t arena_off, uint32_t mode, uint32_t flags) {
-  const uint32_t a = v.rest.pos; bool nc = false;
-  any_value(v.rest, nc, flags);
-  if (v.rest.err) return v.rest.err;
+// (pointer arguments on copies of the caller's state: a reference into Dec2 / Out would pin them in scratch)
+YDEV_NI int v2_json(Cur* restp, Out* op, uint64_t arena_off, uint32_t mode, uint32_t flags) {
+  Cur& rest = *restp; Out& o = *op;
+  const uint32_t a = rest.pos; bool nc = false;
+  any_value(rest, nc, flags);
+  if (rest.err) return rest.err;
   if (!(mode & M_EXPORT)) {
     uint8_t t[21]; uint32_t k = 0;
     if (nc) t[k++] = ' ';
@@ -321,16 +323,23 @@ YDEV_NI int v2_json(Dec2& v, Out& o, uint64_t arena_off, uint32_t mode, uint32_t
     return ST_OK;
   }
   if (nc) return ST_NONCANON;
-  Cur q{v.rest.p, a, v.rest.pos, 0, 0};
+  Cur q{rest.p, a, rest.pos, 0, 0};
   Out m{nullptr, 0};
   int e = any_json(q, m);
   if (e) return e;
   o.vu(m.n);
-  Cur q2{v.rest.p, a, v.rest.pos, 0, 0};
+  Cur q2{rest.p, a, rest.pos, 0, 0};
   return any_json(q2, o);
 }
+YDEV int v2_json_call(Dec2& v, Out& o, uint64_t arena_off, uint32_t mode, uint32_t flags) {
+  Cur r = v.rest; Out oo = o;
+  const int e = v2_json(&r, &oo, arena_off, mode, flags);
+  v.rest = r; o = oo;
+  return e;
+}
+YDEV void any_value_call(Cur& c, bool& nc, uint32_t flags) { Cur q = c; bool n2 = nc; any_value(q, n2, flags); c = q; nc = n2; }
 
-YDEV_NI int v21(const uint8_t* u, uint32_t n, uint64_t arena_off, uint32_t mode, uint32_t flags, Out& o) {
+YDEV int v21(const uint8_t* u, uint32_t n, uint64_t arena_off, uint32_t mode, uint32_t flags, Out& o) {
   Dec2 v;
   open2(v, u, n, flags);
   if (v.st()) return v.st();
@@ -378,10 +387,10 @@ YDEV_NI int v21(const uint8_t* u, uint32_t n, uint64_t arena_off, uint32_t mode,
         }
         case 3: { uint32_t l; const uint32_t st = v.rest.buf(l); if (!v.rest.err) vstr(o, u + st, l); break; }   // ContentBinary
         case 4: { uint32_t l; const uint8_t* t = rd_string(v, l); vstr(o, t, l); break; }                      // ContentString
-        case 5: { const int je = v2_json(v, o, arena_off, mode, flags); if (je) v.fail(je); break; }          // ContentEmbed
+        case 5: { const int je = v2_json_call(v, o, arena_off, mode, flags); if (je) v.fail(je); break; }          // ContentEmbed
         case 6: {                                                                                              // ContentFormat
           uint32_t l; const uint8_t* t = rd_string(v, l); if (v.st()) break; vstr(o, t, l);
-          const int je = v2_json(v, o, arena_off, mode, flags); if (je) v.fail(je);
+          const int je = v2_json_call(v, o, arena_off, mode, flags); if (je) v.fail(je);
           break;
         }
         case 7: {                                                                                              // ContentType
@@ -398,13 +407,13 @@ YDEV_NI int v21(const uint8_t* u, uint32_t n, uint64_t arena_off, uint32_t mode,
         case 8: {                                                                                              // ContentAny
           const uint32_t k = rd_len(v); o.vu(k);
           const uint32_t a = v.rest.pos; bool nc = false;
-          for (uint32_t i = 0; i < k && !v.st(); i++) any_value(v.rest, nc, flags);
+          for (uint32_t i = 0; i < k && !v.st(); i++) any_value_call(v.rest, nc, flags);
           if (!v.st()) o.copy(u + a, v.rest.pos - a);
           break;
         }
         case 9: {                                                                                              // ContentDoc
           uint32_t l; const uint8_t* t = rd_string(v, l); if (v.st()) break; vstr(o, t, l);
-          const uint32_t a = v.rest.pos; bool nc = false; any_value(v.rest, nc, flags);
+          const uint32_t a = v.rest.pos; bool nc = false; any_value_call(v.rest, nc, flags);
           if (!v.st()) o.copy(u + a, v.rest.pos - a);
           break;
         }
@@ -472,24 +481,31 @@ struct Enc2 {
 YDEV void e_str(Enc2& w, const uint8_t* s, uint32_t n) { w.o[C_STR].copy(s, n); uo_w(w.o[C_LENS], w.lens, (uint64_t)utf8_u16(s, n)); }
 YDEV void e_key(Enc2& w, const uint8_t* s, uint32_t n) { id_w(w.o[C_KC], w.kc, (int64_t)w.keyclock++); e_str(w, s, n); }
 // writeJSON: the placeholder's Any bytes from the V2 arena, or writeAny(JSON.parse(s))
-YDEV_NI int e_json(Enc2& w, const uint8_t* s, uint32_t n, const uint8_t* v2a, uint64_t v2n, uint32_t mode, uint32_t flags) {
+YDEV_NI int e_json(Out* restp, const uint8_t* s, uint32_t n, const uint8_t* v2a, uint64_t v2n, uint32_t mode, uint32_t flags) {
+  Out& rest = *restp;
   if (!(mode & M_EXPORT)) {
     uint32_t i = 0; while (i < n && s[i] == ' ') i++;
     uint64_t at = 0; for (; i < n; i++) at = at * 10 + (s[i] - '0');
     if (at >= v2n) return ST_MALFORMED;
     Cur q{v2a + at, 0, (uint32_t)((v2n - at) < 0xFFFFFFFFull ? (v2n - at) : 0xFFFFFFFFull), 0, 0};
     any_skip(q);
-    w.o[C_REST].copy(v2a + at, q.pos);
+    rest.copy(v2a + at, q.pos);
     return ST_OK;
   }
-  json_to_any(s, n, w.o[C_REST], flags);
+  json_to_any(s, n, rest, flags);
   return ST_OK;
+}
+YDEV int e_json_call(Enc2& w, const uint8_t* s, uint32_t n, const uint8_t* v2a, uint64_t v2n, uint32_t mode, uint32_t flags) {
+  Out r = w.o[C_REST];
+  const int e = e_json(&r, s, n, v2a, v2n, mode, flags);
+  w.o[C_REST] = r;
+  return e;
 }
 
 // v12 over one V1 update (lazy-writer normal: every block non-empty, consecutive blocks of different clients;
 // export mode also requires a normal delete set: distinct clients with ranges, descending in 13.6 mode).
 // Count pass: w.o[*].p == nullptr, the column lengths are w.o[*].n after the final flushes.
-YDEV_NI int v12_body(const uint8_t* p, uint32_t n, const uint8_t* v2a, uint64_t v2n, uint32_t mode, uint32_t flags, Enc2& w) {
+YDEV int v12_body(const uint8_t* p, uint32_t n, const uint8_t* v2a, uint64_t v2n, uint32_t mode, uint32_t flags, Enc2& w) {
   Cur c{p, 0, n, 0, 0};
   Out& rest = w.o[C_REST];
   const uint64_t nb = c.vu(); rest.vu(nb);
@@ -502,7 +518,7 @@ YDEV_NI int v12_body(const uint8_t* p, uint32_t n, const uint8_t* v2a, uint64_t 
     prev = client;
     uo_w(w.o[C_CL], w.cl, client); rest.vu(ns); rest.vu(clock);
     for (uint64_t s = 0; s < ns && !c.err; s++) {
-      SInfo si; read_struct(c, si, flags);
+      SInfo si; { Cur cc = c; read_struct(cc, si, flags); c = cc; }
       if (c.err) break;
       if (si.kind == K_GC) { rle_w(w.o[C_INFO], w.info, 0); uo_w(w.o[C_LN], w.ln, si.len); continue; }
       if (si.kind == K_SKIP) { rle_w(w.o[C_INFO], w.info, 10); rest.vu(si.len); continue; }
@@ -525,10 +541,10 @@ YDEV_NI int v12_body(const uint8_t* p, uint32_t n, const uint8_t* v2a, uint64_t 
         case 2: { const uint64_t k = q.vu(); uo_w(w.o[C_LN], w.ln, k); for (uint64_t i = 0; i < k; i++) { uint32_t l; const uint32_t st = q.buf(l); e_str(w, p + st, l); } break; }
         case 3: { uint32_t l; const uint32_t st = q.buf(l); vstr(rest, p + st, l); break; }
         case 4: { uint32_t l; const uint32_t st = q.buf(l); e_str(w, p + st, l); break; }
-        case 5: { uint32_t l; const uint32_t st = q.buf(l); const int e = e_json(w, p + st, l, v2a, v2n, mode, flags); if (e) return e; break; }
+        case 5: { uint32_t l; const uint32_t st = q.buf(l); const int e = e_json_call(w, p + st, l, v2a, v2n, mode, flags); if (e) return e; break; }
         case 6: {
           uint32_t l; uint32_t st = q.buf(l); e_key(w, p + st, l);
-          st = q.buf(l); const int e = e_json(w, p + st, l, v2a, v2n, mode, flags); if (e) return e;
+          st = q.buf(l); const int e = e_json_call(w, p + st, l, v2a, v2n, mode, flags); if (e) return e;
           break;
         }
         case 7: { const uint64_t tr = q.vu(); uo_w(w.o[C_TR], w.tr, tr); if (tr == 3 || tr == 5) { uint32_t l; const uint32_t st = q.buf(l); e_key(w, p + st, l); } break; }
@@ -588,7 +604,7 @@ YDEV uint64_t v2_total(const uint32_t* L) {
   return t + vu_len(sc) + sc + L[C_REST];
 }
 // write pass: headers at dst, each column's Out placed at its final offset, then the same encoding
-YDEV_NI int v12_write(const uint8_t* p, uint32_t n, const uint8_t* v2a, uint64_t v2n, uint32_t mode, uint32_t flags,
+YDEV int v12_write(const uint8_t* p, uint32_t n, const uint8_t* v2a, uint64_t v2n, uint32_t mode, uint32_t flags,
                       const uint32_t* L, uint8_t* dst) {
   Enc2 w; enc_init(w);
   Out h{dst, 0};

@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--f1-docs", type=int, default=10000, help="documents of the f1 (doc-normalized snapshot) block (0: skip)")
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
                     help="skip the host_api block (host arrays through the pinned / two-stream host API)")
-    ap.add_argument("--big", choices=["c3", "c5"], default=None,
+    ap.add_argument("--big", choices=["c3", "c5", "c3full"], default=None,
                     help="instead of the standard line: one C3 / C5 large-document batch on the GPU next to the CPU oracle")
     ap.add_argument("--big-docs", type=int, default=None)
     ap.add_argument("--dry-run", action="store_true", help="no GPU: gloo + the CPU oracle stand in (tests of the rank path)")
@@ -702,9 +702,11 @@ def big_line(args):
     from hocuspocus_amd import Engine
     from tools import synth
     xml = args.big == "c5"
-    n = args.big_docs or (20 if xml else 2000)
+    n = args.big_docs or (20 if xml else 100000 if args.big == "c3full" else 2000)
     if xml:
         arena, upd_off, doc_upd = synth.big_docs(n, 1_000_000, 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=9)
+    elif args.big == "c3full":   # BASELINE C3 at full size: 100 000 documents, 10 MB * rank^-0.8 (0.45 GB)
+        arena, upd_off, doc_upd = synth.big_docs(n, 10_000_000, 1024, max_clients=64, max_k=200, seed=8)
     else:
         arena, upd_off, doc_upd = synth.big_docs(n, 1_000_000, 1024, max_clients=64, max_k=200, seed=8)
     dev = torch.device("cuda", 0)
@@ -718,6 +720,16 @@ def big_line(args):
         s1 = e.stats()
     ms = s1.kernel_ms - s0.kernel_ms
     algo = len(arena) + r.payload_bytes
+    # parity: a sample of documents (all of the largest 50) against the oracle
+    torch.cuda.synchronize()
+    st_g = _d2h(r.status, 4 * n).view(np.int32); off_g = _d2h(r.off, 8 * n).view(np.uint64); ln_g = _d2h(r.len, 8 * n).view(np.uint64)
+    ups = synth.split(arena, upd_off)
+    checked = 0
+    for d in sorted(set(list(range(min(n, 50))) + list(range(0, n, max(1, n // 200))))):
+        exp = oracle.merge_updates(ups[doc_upd[d]:doc_upd[d + 1]])
+        got = (int(st_g[d]), _d2h(r.data + int(off_g[d]), int(ln_g[d])).tobytes() if st_g[d] == 0 else None)
+        assert exp == got, f"parity failure on document {d}"
+        checked += 1
     cores = cpu_cores(args)
     t0 = time.perf_counter()
     st, calgo = oracle.merge_batch(arena, upd_off, doc_upd, cores)
@@ -732,6 +744,7 @@ def big_line(args):
     print(json.dumps({"config": args.big.upper(), "op": "merge", "docs": n, "bytes_in": len(arena), "largest_doc": int(sizes.max()),
                       "gpu_ms": round(ms, 3), "gpu_MBps": round(algo / ms / 1e3, 1), "gpu_docs_per_s": round(n / ms * 1e3),
                       "docs_big_tier": s1.docs_big - s0.docs_big, "docs_seq_tier": s1.docs_seq - s0.docs_seq,
+                      "parity": f"bit-exact vs oracle on {checked} documents (the 50 largest + an even sample)",
                       "cpu_baseline": dict(port, yjs=y)}), flush=True)
 
 

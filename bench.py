@@ -14,6 +14,8 @@ the lean kernel -- asserted -- so no step needs the host-driven tiers).  Beside 
   c4       config C4 (configs[3]): 1 000 000 merged Y.Text states (1-16 clients, log-uniform 1-8 KB,
            3.2 GB) sharded over the ranks, encodeStateVectorFromUpdate and diffUpdate against per-document
            state vectors (the mass-reconnect Step1 -> Step2 path, MessageReceiver.ts:137-155)
+  c3       config C3 at full size (configs[2]): 100 000 [snapshot, ...log] documents of 10 MB * rank^-0.8 (0.77 GB)
+           merged in one batch through the tier cascade, beside the C port and yjs (rank 0 at N = 1)
   v2       SURVEY.md §8f-4: the C2 merge with the updates in format V2 (Y.mergeUpdatesV2), and the V1 <-> V2
            conversions of its 2 M updates
   cpu_baseline  the reference yjs path on the GPU box's host cores (yjs 13.5.16 from the image's
@@ -64,6 +66,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-yjs", action="store_true", help="skip the Node / yjs leg of the CPU baseline")
     ap.add_argument("--no-v2", dest="v2", action="store_false", help="skip the update-V2 (f-4) block")
+    ap.add_argument("--no-c3", dest="c3", action="store_false", help="skip the full-size C3 block")
     ap.add_argument("--f1-docs", type=int, default=10000, help="documents of the f1 (doc-normalized snapshot) block (0: skip)")
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
                     help="skip the host_api block (host arrays through the pinned / two-stream host API)")
@@ -671,6 +674,11 @@ def run_rank(args, rank, world, dist, be, dev=None):
     # ---- f-4: the C2 merge in update format V2
     if args.v2 and rank == 0 and not args.dry_run:
         line["v2"] = v2_block(be, args)
+    # ---- C3 at full size (100 000 [snapshot, ...log] documents, 0.77 GB): one batch, rank 0 at N = 1
+    if args.c3 and rank == 0 and world == 1 and not args.dry_run:
+        blk = big_run(args, "c3full", be.dev.index)
+        blk["roofline"] = roof(blk["bytes_in"] + blk["bytes_out"], blk["gpu_ms"], "merge cascade (k_merge_lean / wave / fast / big)", None)
+        line["c3"] = blk
     # ---- CPU baselines (rank 0 at N = 1 only)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         cores = cpu_cores(args)
@@ -693,27 +701,27 @@ def run_rank(args, rank, world, dist, be, dev=None):
     return line
 
 
-def big_line(args):
-    """C3 / C5 ([snapshot, ...log] large documents): the whole batch merged on cuda:0
+def big_run(args, kind, dev_index=0):
+    """C3 / C5 ([snapshot, ...log] large documents): the whole batch merged on the GPU
     (device-resident inputs, host-driven tier cascade, kernel time from the engine's HIP events) and
-    by the CPU oracle on the host threads over the same documents."""
+    by the CPU oracle and yjs on the host threads over the same documents."""
     import torch
     import oracle
     from hocuspocus_amd import Engine
     from tools import synth
-    xml = args.big == "c5"
-    n = args.big_docs or (20 if xml else 100000 if args.big == "c3full" else 2000)
+    xml = kind == "c5"
+    n = args.big_docs or (20 if xml else 100000 if kind == "c3full" else 2000)
     if xml:
         arena, upd_off, doc_upd = synth.big_docs(n, 1_000_000, 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=9)
-    elif args.big == "c3full":   # BASELINE C3 at full size: 100 000 documents, 10 MB * rank^-0.8 (0.45 GB)
+    elif kind == "c3full":   # BASELINE C3 at full size: 100 000 documents, 10 MB * rank^-0.8 (0.45 GB)
         arena, upd_off, doc_upd = synth.big_docs(n, 10_000_000, 1024, max_clients=64, max_k=200, seed=8)
     else:
         arena, upd_off, doc_upd = synth.big_docs(n, 1_000_000, 1024, max_clients=64, max_k=200, seed=8)
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", dev_index)
     da = torch.from_numpy(np.concatenate([arena, np.zeros(64, np.uint8)])).to(dev)
     do = torch.from_numpy(upd_off.view(np.int64)).to(dev)
     dd = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
-    e = Engine(0)
+    e = Engine(dev_index)
     for _ in range(2):   # the second run is timed (scratch already grown)
         s0 = e.stats()
         r = e.merge_device(da.data_ptr(), len(arena), do.data_ptr(), dd.data_ptr(), int(doc_upd[-1]), n)
@@ -741,11 +749,17 @@ def big_line(args):
     y = None if (args.no_yjs or args.no_cpu_baseline) else cpu_yjs("merge", {"arena": arena, "upd_off": upd_off, "doc_upd": doc_upd}, cores, n)
     if y and "value" in y:
         y["ms"] = round(n / y["docs_per_s"] * 1e3, 3)   # the whole batch (slowest worker)
-    print(json.dumps({"config": args.big.upper(), "op": "merge", "docs": n, "bytes_in": len(arena), "largest_doc": int(sizes.max()),
+    e.close()
+    return {"config": kind.upper(), "op": "merge", "docs": n, "bytes_in": len(arena), "bytes_out": int(r.payload_bytes),
+            "largest_doc": int(sizes.max()),
                       "gpu_ms": round(ms, 3), "gpu_MBps": round(algo / ms / 1e3, 1), "gpu_docs_per_s": round(n / ms * 1e3),
                       "docs_big_tier": s1.docs_big - s0.docs_big, "docs_seq_tier": s1.docs_seq - s0.docs_seq,
                       "parity": f"bit-exact vs oracle on {checked} documents (the 50 largest + an even sample)",
-                      "cpu_baseline": dict(port, yjs=y)}), flush=True)
+                      "cpu_baseline": dict(port, yjs=y)}
+
+
+def big_line(args):
+    print(json.dumps(big_run(args, args.big)), flush=True)
 
 
 def main():

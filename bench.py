@@ -14,6 +14,7 @@ the lean kernel -- asserted -- so no step needs the host-driven tiers).  Beside 
   c4       config C4 (configs[3]): 1 000 000 merged Y.Text states (1-16 clients, log-uniform 1-8 KB,
            3.2 GB) sharded over the ranks, encodeStateVectorFromUpdate and diffUpdate against per-document
            state vectors (the mass-reconnect Step1 -> Step2 path, MessageReceiver.ts:137-155)
+  c2_mixed C2 past the lean kernel's envelope: 1-8 clients, 1-16 character inserts, 20 % deletions (tier cascade)
   c3       config C3 at full size (configs[2]): 100 000 [snapshot, ...log] documents of 10 MB * rank^-0.8 (0.77 GB)
            merged in one batch through the tier cascade, beside the C port and yjs (rank 0 at N = 1)
   v2       SURVEY.md §8f-4: the C2 merge with the updates in format V2 (Y.mergeUpdatesV2), and the V1 <-> V2
@@ -67,6 +68,7 @@ def parse():
     ap.add_argument("--no-yjs", action="store_true", help="skip the Node / yjs leg of the CPU baseline")
     ap.add_argument("--no-v2", dest="v2", action="store_false", help="skip the update-V2 (f-4) block")
     ap.add_argument("--no-c3", dest="c3", action="store_false", help="skip the full-size C3 block")
+    ap.add_argument("--no-mixed", dest="mixed", action="store_false", help="skip the c2_mixed block")
     ap.add_argument("--f1-docs", type=int, default=10000, help="documents of the f1 (doc-normalized snapshot) block (0: skip)")
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
                     help="skip the host_api block (host arrays through the pinned / two-stream host API)")
@@ -336,6 +338,46 @@ def f1_block(be, args, steps=5):
         blk["cpu_baseline"] = cpu_yjs("snapshot", c, cpu_cores(args), min(args.f1_docs, 4000))
     e.close()
     return blk
+
+
+def mixed_block(be, args, steps=5):
+    """C2 past the lean kernel's envelope (realistic debounce logs): 10 000 documents x 200 updates
+    of 1-8 clients (uint32 ids), inserts of 1-16 characters as one Item (pastes, words typed in one transaction:
+    updates of up to ~42 bytes) and 20 % deletions -- one batched merge per step through the whole tier cascade
+    (documents the lean kernel cannot prove go on to the wave / workgroup tiers), inputs resident in HBM."""
+    from hocuspocus_amd import Engine
+    import oracle
+    from tools import synth
+    n = args.docs
+    arena, upd_off, doc_upd = synth.text_updates(n, args.updates, 1, 8, del_pct=20, seed=71, max_run=16)
+    e = Engine(be.dev.index)
+    da, do, dd = be.put(arena, 64), be.put(upd_off.view(np.int64)), be.put(doc_upd.view(np.int32))
+    n_upd = int(doc_upd[-1])
+    r = e.merge_device(da, len(arena), do, dd, n_upd, n, be.stream.cuda_stream)
+    be.sync()
+    s0 = e.stats()
+    for _ in range(steps):
+        r = e.merge_device(da, len(arena), do, dd, n_upd, n, be.stream.cuda_stream)
+    be.sync()
+    s1 = e.stats()
+    kms = (s1.kernel_ms - s0.kernel_ms) / steps
+    algo = len(arena) + int(r.payload_bytes)
+    st, off, ln, data = be.fetch(r, n)
+    ups = synth.split(arena, upd_off)
+    checked = 0
+    for d in range(0, n, max(1, n // 200)):
+        exp = oracle.merge_updates(ups[doc_upd[d]:doc_upd[d + 1]])
+        assert exp == (int(st[d]), data[int(off[d]):int(off[d]) + int(ln[d])] if st[d] == 0 else None), f"parity failure on document {d}"
+        checked += 1
+    e.close()
+    return {"workload": f"C2 mixed: {n} docs x {args.updates} updates, 1-8 uint32 clients, 1-16 character inserts, 20 % deletions "
+                        "(updates up to ~42 bytes), batched Y.mergeUpdates through the tier cascade, inputs resident in HBM",
+            "docs": n, "bytes_in": len(arena), "bytes_out": int(r.payload_bytes), "value": round(algo / kms / 1e3, 3), "unit": "MB/s",
+            "docs_per_s": round(n / kms * 1e3, 1), "ms_per_step": round(kms, 4),
+            "docs_lean": int((s1.docs_lean - s0.docs_lean) / steps), "docs_general_tiers": int((s1.docs_fast - s0.docs_fast) / steps),
+            "docs_big": int((s1.docs_big - s0.docs_big) / steps), "docs_seq": int((s1.docs_seq - s0.docs_seq) / steps),
+            "roofline": roof(algo, kms, "k_merge_lean + k_merge_wave / k_merge_fast for the documents it defers", None),
+            "parity": f"bit-exact vs oracle on {checked} sampled docs"}
 
 
 def v2_block(be, args, steps=5):
@@ -671,6 +713,9 @@ def run_rank(args, rank, world, dist, be, dev=None):
     # ---- f-1: doc-normalized snapshots of merged debounce logs (C2 with 20 % deletes)
     if args.f1_docs and rank == 0 and not args.dry_run:
         line["f1"] = f1_block(be, args)
+    # ---- C2 past the lean envelope (multi-character inserts, up to 8 clients, deletions)
+    if args.mixed and rank == 0 and not args.dry_run:
+        line["c2_mixed"] = mixed_block(be, args)
     # ---- f-4: the C2 merge in update format V2
     if args.v2 and rank == 0 and not args.dry_run:
         line["v2"] = v2_block(be, args)

@@ -35,7 +35,7 @@ typedef struct { uint32_t client, clock; uint8_t ch; int32_t oi, ri; uint32_t oc
 /* Runs one document's editing session; returns number of chars, fills recs/ops.
  * `vis` tracks the visible characters (no scan when nothing was deleted). */
 static int session(Rng *r, int n_ops, int nclients, uint32_t *clients, uint32_t *clocks, Ch *doc, int *ndoc,
-                   uint8_t *buf, size_t *blen, uint64_t *upd_off, uint32_t *nupd, int del_pct) {
+                   uint8_t *buf, size_t *blen, uint64_t *upd_off, uint32_t *nupd, int del_pct, int max_run) {
   int len = 0, visible = 0, ndel = 0; size_t b = *blen;
   for (int op = 0; op < n_ops; op++) {
     const int ci = (int)rbelow(r, nclients);
@@ -56,21 +56,24 @@ static int session(Rng *r, int n_ops, int nclients, uint32_t *clients, uint32_t 
     int pos = (int)rbelow(r, (uint64_t)visible + 1), at = 0, seen = 0;
     if (ndel == 0) at = pos;
     else for (at = 0; at < len; at++) { if (seen == pos) break; if (!doc[at].deleted) seen++; }
-    const char ch = "abcdefghijklmnopqrstuvwxyz"[rbelow(r, 26)];
+    /* one Item of k ASCII characters (k = 1 unless max_run > 1: pastes / typed words of one transaction) */
+    const int k = max_run > 1 ? 1 + (int)rbelow(r, (uint64_t)max_run) : 1;
+    char chs[256];
+    for (int j = 0; j < k; j++) chs[j] = "abcdefghijklmnopqrstuvwxyz"[rbelow(r, 26)];
     const int has_o = at > 0, has_r = at < len;
-    memmove(doc + at + 1, doc + at, (size_t)(len - at) * sizeof(Ch));
-    doc[at].client = client; doc[at].clock = clocks[ci]; doc[at].ch = (uint8_t)ch; doc[at].deleted = 0;
-    len++; visible++;
+    memmove(doc + at + k, doc + at, (size_t)(len - at) * sizeof(Ch));
+    for (int j = 0; j < k; j++) { doc[at + j].client = client; doc[at + j].clock = clocks[ci] + (uint32_t)j; doc[at + j].ch = (uint8_t)chs[j]; doc[at + j].deleted = 0; }
+    len += k; visible += k;
     upd_off[(*nupd)++] = b;
     buf[b++] = 1; buf[b++] = 1;
     b += vu(buf + b, client); b += vu(buf + b, clocks[ci]);
     buf[b++] = (uint8_t)(4 | (has_o ? 0x80 : 0) | (has_r ? 0x40 : 0));
     if (has_o) { b += vu(buf + b, doc[at - 1].client); b += vu(buf + b, doc[at - 1].clock); }
-    if (has_r) { b += vu(buf + b, doc[at + 1].client); b += vu(buf + b, doc[at + 1].clock); }
+    if (has_r) { b += vu(buf + b, doc[at + k].client); b += vu(buf + b, doc[at + k].clock); }
     if (!has_o && !has_r) { buf[b++] = 1; buf[b++] = 1; buf[b++] = 't'; }
-    buf[b++] = 1; buf[b++] = (uint8_t)ch;
+    buf[b++] = (uint8_t)k; memcpy(buf + b, chs, (size_t)k); b += (size_t)k;
     buf[b++] = 0;                         /* empty delete set */
-    clocks[ci]++;
+    clocks[ci] += (uint32_t)k;
   }
   *blen = b; *ndoc = len;
   return len;
@@ -85,9 +88,11 @@ static void pick_clients(Rng *r, int n, uint32_t *c) {
 /* Config C2.  buf must hold n_docs*n_updates*40 bytes; upd_off n_docs*n_updates+1;
  * doc_upd n_docs+1.  Returns bytes written. */
 size_t synth_text_updates(uint64_t seed, uint32_t n_docs, uint32_t n_updates, uint32_t min_clients, uint32_t max_clients,
-                          int del_pct, uint8_t *buf, uint64_t *upd_off, uint32_t *doc_upd) {
+                          int del_pct, uint8_t *buf, uint64_t *upd_off, uint32_t *doc_upd, int max_run) {
   Rng r = { seed * 0x9E3779B97F4A7C15ULL + 1 };
-  Ch *doc = (Ch *)malloc(sizeof(Ch) * (n_updates + 1));
+  if (max_run < 1) max_run = 1;
+  if (max_run > 200) max_run = 200;
+  Ch *doc = (Ch *)malloc(sizeof(Ch) * ((size_t)n_updates * (size_t)max_run + 1));
   size_t b = 0; uint32_t nupd = 0;
   for (uint32_t d = 0; d < n_docs; d++) {
     doc_upd[d] = nupd;
@@ -96,7 +101,7 @@ size_t synth_text_updates(uint64_t seed, uint32_t n_docs, uint32_t n_updates, ui
     if (nc > 64) nc = 64;
     pick_clients(&r, nc, clients);
     int nd;
-    session(&r, (int)n_updates, nc, clients, clocks, doc, &nd, buf, &b, upd_off, &nupd, del_pct);
+    session(&r, (int)n_updates, nc, clients, clocks, doc, &nd, buf, &b, upd_off, &nupd, del_pct, max_run);
   }
   doc_upd[n_docs] = nupd; upd_off[nupd] = b;
   free(doc);
@@ -119,7 +124,7 @@ static void c4_doc(uint64_t seed, uint32_t d, uint32_t ops, uint32_t min_cl, uin
   if (nc > 64) nc = 64;
   pick_clients(r, nc, clients);
   int nd; size_t tl = 0; uint32_t nu = 0;
-  session(r, (int)ops, nc, clients, clocks, doc, &nd, tmp, &tl, toff, &nu, 0);
+  session(r, (int)ops, nc, clients, clocks, doc, &nd, tmp, &tl, toff, &nu, 0, 1);
   toff[nu] = tl;
   /* update index of each (client, clock): inserts of a client arrive in clock order */
   uint32_t base[65]; base[0] = 0; for (int i = 0; i < nc; i++) base[i + 1] = base[i] + clocks[i];
@@ -384,7 +389,7 @@ static void *c2_run(void *arg) {
     pick_clients(&r, nc, clients);
     const uint32_t u0 = P->nu;
     int nd;
-    session(&r, (int)J->n_updates, nc, clients, clocks, doc, &nd, P->buf, &P->nb, P->uoff, &P->nu, J->del_pct);
+    session(&r, (int)J->n_updates, nc, clients, clocks, doc, &nd, P->buf, &P->nb, P->uoff, &P->nu, J->del_pct, 1);
     P->cnt[d - J->d0] = P->nu - u0;
   }
   free(doc);

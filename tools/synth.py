@@ -21,7 +21,8 @@ def lib():
             subprocess.check_call(["make", "-s", "-C", _HERE])
         L = ctypes.CDLL(path)
         P = ctypes.c_void_p
-        L.synth_text_updates.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P, P, P]
+        L.synth_text_updates.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P, P, P,
+                                         ctypes.c_int]
         L.synth_text_updates.restype = ctypes.c_size_t
         u64p = ctypes.POINTER(ctypes.c_uint64)
         L.synth_text_states_gen.argtypes = [ctypes.c_uint64, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -43,14 +44,15 @@ def lib():
     return _lib
 
 
-def text_updates(n_docs, n_updates=200, min_clients=1, max_clients=4, del_pct=0, seed=1):
-    """Config C2: returns (arena uint8, upd_off uint64[n_upd+1], doc_upd uint32[n_docs+1])."""
+def text_updates(n_docs, n_updates=200, min_clients=1, max_clients=4, del_pct=0, seed=1, max_run=1):
+    """Config C2: returns (arena uint8, upd_off uint64[n_upd+1], doc_upd uint32[n_docs+1]).  max_run > 1: each
+    insert is one Item of 1..max_run characters (pastes, words typed in one transaction)."""
     n_upd = n_docs * n_updates
-    buf = np.empty(n_upd * 40 + 64, dtype=np.uint8)
+    buf = np.empty(n_upd * (40 + max_run) + 64, dtype=np.uint8)
     upd_off = np.empty(n_upd + 1, dtype=np.uint64)
     doc_upd = np.empty(n_docs + 1, dtype=np.uint32)
     n = lib().synth_text_updates(seed, n_docs, n_updates, min_clients, max_clients, del_pct,
-                                 buf.ctypes.data, upd_off.ctypes.data, doc_upd.ctypes.data)
+                                 buf.ctypes.data, upd_off.ctypes.data, doc_upd.ctypes.data, max_run)
     return buf[:n].copy(), upd_off, doc_upd
 
 

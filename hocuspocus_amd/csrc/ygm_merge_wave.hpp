@@ -21,8 +21,8 @@ namespace ygm {
 
 constexpr int W_WAVES = 1;     // documents per workgroup (one wave each: LDS-granular occupancy)
 constexpr int W_K = 256;       // updates
-constexpr int W_IN = 5120;     // staged input bytes
-constexpr int W_OUT = 5120;    // staged output bytes
+constexpr int W_IN = 8192;     // staged input bytes (realistic 200-update logs of multi-character inserts: ~6 KB)
+constexpr int W_OUT = 8192;    // staged output bytes
 constexpr int W_S = 256;       // non-Skip structs
 constexpr int W_D = 128;       // delete-set ranges
 constexpr int W_C = 64;        // distinct clients in the struct section

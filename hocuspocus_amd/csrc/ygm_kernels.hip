@@ -1565,8 +1565,22 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
   bool gn = !force_seq && lean_stageable(hn);
   lean_prefetch(arena, upd_off, hn, gn, v, rx, ry);
   uint64_t payload = 0;   // this wave's output bytes: one atomic per wave, not per document
+  // deferred documents: bit j of dmask = the j-th document of the current run of 64 iterations (document
+  // dch + j * G), appended to defer_list with ONE atomic per run -- one atomic per document on the single
+  // counter serialises a batch the lean kernel mostly defers (10 000 documents: ~80 us)
+  uint64_t dmask = 0;
+  uint32_t dit = 0, dch = d;
+  auto flush_defer = [&]() {
+    if (!dmask) return;
+    uint32_t base = 0;
+    if (l == 0) base = atomicAdd(&meta->lean_defer, (uint32_t)__popcll(dmask));
+    base = __shfl(base, 0, WAVE);
+    if ((dmask >> l) & 1ull) defer_list[base + (uint32_t)__popcll(dmask & ((1ull << l) - 1ull))] = dch + l * G;
+    dmask = 0;
+  };
   for (; d < n_docs; d += G) {
     DIAGL_T0
+    if (dit == 64) { flush_defer(); dit = 0; dch = d; }
     const LeanHdr h = hn;
     const bool go = gn;
     const uint32_t k = h.k;
@@ -1808,16 +1822,15 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
     }
     if (!defer) payload += size;
     if (l == 0) {
-      if (defer) {
-        status[d] = ST_FALLBACK;
-        defer_list[atomicAdd(&meta->lean_defer, 1u)] = d;
-      } else {
-        out_off[d] = slot; out_len[d] = size; status[d] = ST_OK;
-      }
+      if (defer) status[d] = ST_FALLBACK;
+      else { out_off[d] = slot; out_len[d] = size; status[d] = ST_OK; }
     }
+    if (__builtin_amdgcn_readfirstlane((int)defer)) dmask |= 1ull << dit;   // (wave-uniform: scalar registers)
+    dit++;
     DIAGL(4);
     wave_sync();   // the next document's staging overwrites lin / lout
   }
+  flush_defer();
   if (l == 0 && payload) add_payload(meta, blockIdx.x, payload);
 }
 

@@ -2566,6 +2566,16 @@ int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const
   return launch_rc(__func__);
 }
 
+// workgroups of `threads` resident at once on the device (occupancy x CUs), for persistent grids
+extern "C++" template <class K>
+static uint32_t resident_blocks(K kernel, int threads, uint32_t fallback) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess || cus <= 0 || per <= 0)
+    return fallback;
+  return (uint32_t)(cus * per);
+}
+
 int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
                             const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
                             int32_t* status, void* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
@@ -2573,13 +2583,7 @@ int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const
   // persistent: exactly the waves that are resident at once (LDS / VGPR occupancy x CUs), so no wave starts
   // its grid-stride share after the others have finished theirs; n_docs is the upper bound of the device count
   static uint32_t resident = 0;
-  if (!resident) {
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_merge_wave, WAVE, 0) != hipSuccess || cus <= 0 || per <= 0)
-      resident = 2048u;
-    else resident = (uint32_t)(cus * per);
-  }
+  if (!resident) { const char* g = getenv("YGM_WAVE_GRID"); resident = g ? (uint32_t)atoi(g) : resident_blocks(k_merge_wave, WAVE, 2048u); }
   const uint32_t grid = n_docs < resident ? n_docs : resident;
   hipLaunchKernelGGL(k_merge_wave, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, docs, n_dev, n_docs,
                      flags, out, out_off, out_len, status, (DocMeta*)meta, defer_list, fb_list, out_cap);
@@ -2590,7 +2594,9 @@ int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const
                             const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
                             int32_t* status, uint64_t slot_total, void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
   if (n_docs == 0) return 0;
-  const uint32_t grid = n_docs < 512u ? n_docs : 512u;
+  static uint32_t resident = 0;   // persistent: the resident workgroups (see ygm_k_launch_merge_wave)
+  if (!resident) { const char* g = getenv("YGM_FAST_GRID"); resident = g ? (uint32_t)atoi(g) : resident_blocks(k_merge_fast, M_NT, 512u); }
+  const uint32_t grid = n_docs < resident ? n_docs : resident;
   hipLaunchKernelGGL(k_merge_fast, dim3(grid), dim3(M_NT), 0, s, arena, upd_off, doc_upd, docs, n_dev, n_docs, flags, out, out_off, out_len,
                      status, slot_total, (DocMeta*)meta, fb_list, out_cap);
   return launch_rc(__func__);

@@ -1952,6 +1952,11 @@ YDEV_NI uint64_t big_skip_global(const uint8_t* u0p, uint32_t n0, uint32_t pos) 
 #endif
 constexpr uint32_t BIG_WAVES = YGM_BIG_WAVES, BIG_THREADS = BIG_WAVES * WAVE;
 struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; };   // cmd 0 done, 1 spec, 2 validate
+// the struct start 2^(k+1) structs after tile position i < BT_CH (k = -1: the next one, from nx), or BJ_NONE
+YDEV uint32_t big_jump(const BigTile& T, int k, uint32_t i) {
+  if (k < 0) { const uint32_t e = T.nx[i]; return e ? (e & 0x7FFFu) : BJ_NONE; }
+  return T.jp[k][i];
+}
 YDEV void big_spec(BigTile& T, uint32_t at, uint32_t mis, uint32_t tn, uint32_t n0, uint32_t t0) {
   const uint8_t* tp = (const uint8_t*)T.b;
   for (uint32_t i = t0; i < BT_CH; i += BIG_THREADS) {
@@ -1966,6 +1971,14 @@ YDEV void big_spec(BigTile& T, uint32_t at, uint32_t mis, uint32_t tn, uint32_t 
       if (big_skip(t, kind, 8) && !t.err) e = (uint16_t)((t.pos - mis) | (kind == 0 ? 0x8000u : 0u));
     }
     T.nx[i] = e;
+  }
+  // jump tables by doubling (every thread of the workgroup calls this, so the barriers match)
+  for (int k = 0; k < BJ_LV; k++) {
+    __syncthreads();
+    for (uint32_t i = t0; i < BT_CH; i += BIG_THREADS) {
+      const uint32_t a = big_jump(T, k - 1, i);
+      T.jp[k][i] = (uint16_t)(a < BT_CH ? big_jump(T, k - 1, a) : BJ_NONE);
+    }
   }
 }
 // struct records [vs, ns) (all starting inside the tile; byte ranges in rs / re, LDS): validated from
@@ -2135,16 +2148,35 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       pos = h.pos + tb;
       B.b0 = pos; B.s0 = (uint32_t)NS;
       B.first_gc = 0; B.last_gc = 0; B.clock1 = 0;
-      for (uint32_t q = 0; q < B.nst && !bad; q++) {
+      for (uint32_t q = 0; q < B.nst && !bad;) {
         if (pos >= tc0 + BT_CH) { validate(); load_tile(pos, true); }
-        const uint32_t e = T0.nx[pos - tc0];
-        uint32_t end, kind;
-        if (e) { end = tc0 + (e & 0x7FFFu); kind = (e & 0x8000u) ? 0u : 1u; }
-        else { const uint64_t r = big_skip_global(u0p, n0, pos); bad |= (r >> 63) != 0; kind = (uint32_t)(r >> 32) & 1u; end = (uint32_t)r; }
+        // up to 64 of the block's structs per step: lane j finds the start of struct q + j by composing
+        // the jump tables along the bits of j; the structs taken are the leading lanes that start inside
+        // the tile and have a speculative parse
+        const uint32_t want = B.nst - q < 64u ? B.nst - q : 64u;
+        uint32_t S = pos - tc0;
+        for (int k = 0; k < 6 && ((want - 1u) >> k); k++)
+          if (((l >> k) & 1u) && S < BT_CH) S = big_jump(T0, k - 1, S);
+        const uint32_t E = (l < want && S < BT_CH) ? (uint32_t)T0.nx[S] : 0u;
+        const uint64_t tk = __ballot(E != 0u);
+        const uint32_t m = ~tk ? (uint32_t)__builtin_ctzll(~tk) : 64u;
+        if (m) {
+          if (l < m) { s_rst[NS - vs + l] = tc0 + S; s_ren[NS - vs + l] = tc0 + (E & 0x7FFFu); }
+          const uint32_t E0 = (uint32_t)__builtin_amdgcn_readlane((int)E, 0), El = (uint32_t)__builtin_amdgcn_readlane((int)E, (int)m - 1);
+          if (q == 0) B.first_gc = (E0 & 0x8000u) != 0u;
+          B.last_gc = (El & 0x8000u) != 0u;
+          NS += m; q += m;
+          pos = tc0 + (El & 0x7FFFu);
+          continue;
+        }
+        // the struct at pos has no speculative parse: parsed from global memory
+        const uint64_t r = big_skip_global(u0p, n0, pos);
+        bad |= (r >> 63) != 0;
+        const uint32_t kind = (uint32_t)(r >> 32) & 1u, end = (uint32_t)r;
         if (l == 0) { s_rst[NS - vs] = pos; s_ren[NS - vs] = end; }
         if (q == 0) B.first_gc = kind == 0;
         B.last_gc = kind == 0;
-        NS++;
+        NS++; q++;
         pos = end;
       }
       B.b1 = pos;

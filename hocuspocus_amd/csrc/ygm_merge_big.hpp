@@ -305,11 +305,18 @@ struct BigRange { uint64_t key; uint32_t len, pad; };   // log delete range: key
 
 // U0 tile (LDS): bytes staged by the whole wave; structs are parsed speculatively at every
 // position of its first BT_CH bytes; BT_OV bytes of overlap let a struct starting there end inside
-// (static LDS stays under the 64 KiB a workgroup may allocate)
+// (static LDS: 121 KB per workgroup; one 1024-thread workgroup per CU either way, by its VGPRs).  jp[k][i]
+// is the struct start 2^(k+1) structs after position i (jump tables built from nx by doubling),
+// BJ_NONE when the chain breaks (a position without a speculative parse) or passes the tile's BT_CH
+// positions on the way: the chain follow takes up to 64 structs of a block per step, lane j composing
+// the tables along the bits of j.
 constexpr uint32_t BT_CH = 4096, BT_OV = 2048, BT_TILE = BT_CH + BT_OV + 16;
+constexpr int BJ_LV = 5;
+constexpr uint32_t BJ_NONE = 0xFFFFu;
 struct BigTile {
   uint4 b[BT_TILE / 16];
   uint16_t nx[BT_CH];                // speculative struct end - tile origin, bit 15 = GC; 0 = no parse
+  uint16_t jp[BJ_LV][BT_CH];
 };
 
 struct BigLds {

@@ -1957,6 +1957,33 @@ YDEV uint32_t big_jump(const BigTile& T, int k, uint32_t i) {
   if (k < 0) { const uint32_t e = T.nx[i]; return e ? (e & 0x7FFFu) : BJ_NONE; }
   return T.jp[k][i];
 }
+// A client block header (struct count, client, clock: three varuints of <= 5 bytes ending inside the tile)
+// from one 16-byte view of the tile: terminators by the top bits, values by 7-bit compaction, nm = a
+// non-minimal varuint (a zero last byte).  false: the cursor parse takes it.
+YDEV uint32_t big_ctz16(uint32_t t) { return t ? (uint32_t)__builtin_ctz(t) : 16u; }
+YDEV bool big_hdr_fast(const BigTile& T, uint32_t hp, uint32_t tn, uint64_t& nst, uint64_t& client, uint64_t& clock0,
+                       uint32_t& hend, bool& nm) {
+  const uint32_t q = hp >> 4, o = hp & 15u, sh = (o & 7u) * 8u;
+  const uint4 A = T.b[q], C = T.b[q + 1];
+  const uint64_t w0 = ((uint64_t)A.y << 32) | A.x, w1 = ((uint64_t)A.w << 32) | A.z;
+  const uint64_t w2 = ((uint64_t)C.y << 32) | C.x, w3 = ((uint64_t)C.w << 32) | C.z;
+  const uint64_t a = (o & 8u) ? w1 : w0, b = (o & 8u) ? w2 : w1, c = (o & 8u) ? w3 : w2;
+  const uint64_t lo = sh ? (a >> sh) | (b << (64u - sh)) : a, hi = sh ? (b >> sh) | (c << (64u - sh)) : b;
+  uint32_t t = ~(hibits8((uint32_t)lo, (uint32_t)(lo >> 32)) | (hibits8((uint32_t)hi, (uint32_t)(hi >> 32)) << 8)) & 0xFFFFu;
+  const uint32_t e0 = big_ctz16(t);
+  t &= t - 1u;
+  const uint32_t e1 = big_ctz16(t);
+  t &= t - 1u;
+  const uint32_t e2 = big_ctz16(t);
+  if (e2 >= 16u || e0 >= 5u || e1 - e0 > 5u || e2 - e1 > 5u || hp + e2 + 1u > tn) return false;
+  nst = pext7(dw_at(lo, hi, 0), e0 + 1u);
+  client = pext7(dw_at(lo, hi, e0 + 1u), e1 - e0);
+  clock0 = pext7(dw_at(lo, hi, e1 + 1u), e2 - e1);
+  nm = (e0 > 0u && (dw_at(lo, hi, e0) & 0xFFu) == 0u) || (e1 - e0 > 1u && (dw_at(lo, hi, e1) & 0xFFu) == 0u) ||
+       (e2 - e1 > 1u && (dw_at(lo, hi, e2) & 0xFFu) == 0u);
+  hend = hp + e2 + 1u;
+  return true;
+}
 YDEV void big_spec(BigTile& T, uint32_t at, uint32_t mis, uint32_t tn, uint32_t n0, uint32_t t0) {
   const uint8_t* tp = (const uint8_t*)T.b;
   for (uint32_t i = t0; i < BT_CH; i += BIG_THREADS) {
@@ -2013,6 +2040,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   __shared__ uint64_t s_base, s_sbase, s_ds0, s_at;
   __shared__ BigCmd s_cmd;
   __shared__ uint32_t s_rst[BT_CH / 2], s_ren[BT_CH / 2];   // byte ranges of the current tile's structs (>= 2 bytes each)
+  __shared__ BigBlk s_blk[64];
   if (threadIdx.x >= WAVE) {   // helper waves: wave 0's tile commands until it sends 0 (one barrier pair per command)
     for (;;) {
       __syncthreads();
@@ -2137,15 +2165,32 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     uint32_t pos = c.pos;
     bool have = false;
     uint64_t prevc = ~0ull;
+    uint32_t bq = 0;                                       // blocks staged in s_blk
+    auto flush_blk = [&](uint64_t upto) {                  // s_blk holds blocks [upto - bq, upto)
+      wave_sync();
+      const uint4* src = (const uint4*)s_blk;
+      uint4* dst = (uint4*)(blk + base + upto - bq);
+      for (uint32_t u = l; u < bq * (uint32_t)(sizeof(BigBlk) / 16); u += WAVE) dst[u] = src[u];
+      bq = 0;
+      wave_sync();
+    };
     for (uint64_t b = 0; b < nb && !bad; b++) {
       if (!have || pos >= tc0 + BT_CH) { if (have) validate(); load_tile(pos, true); have = true; }
       BigBlk B;
-      GCur h; h.init(tp, tn); h.pos = pos - tb; h.nm = 0;
-      B.nst = (uint32_t)h.vu(); B.client = h.vu(); B.clock0 = h.vu();
-      bad |= h.err || B.nst == 0 || B.client >= prevc || B.client > 0xFFFFFFFFull;
+      uint64_t hn, hc, hk;
+      uint32_t he;
+      bool hnm;
+      if (!big_hdr_fast(T0, pos - tb, tn, hn, hc, hk, he, hnm)) {
+        GCur h; h.init(tp, tn); h.pos = pos - tb; h.nm = 0;
+        hn = h.vu(); hc = h.vu(); hk = h.vu();
+        bad |= h.err != 0;
+        he = h.pos; hnm = h.nm != 0;
+      }
+      B.nst = (uint32_t)hn; B.client = hc; B.clock0 = hk;
+      bad |= B.nst == 0 || B.client >= prevc || B.client > 0xFFFFFFFFull;
       prevc = B.client;
-      B.h0 = pos; B.hcanon = h.nm == 0; B.pad = 0;
-      pos = h.pos + tb;
+      B.h0 = pos; B.hcanon = !hnm; B.pad = 0;
+      pos = he + tb;
       B.b0 = pos; B.s0 = (uint32_t)NS;
       B.first_gc = 0; B.last_gc = 0; B.clock1 = 0;
       for (uint32_t q = 0; q < B.nst && !bad;) {
@@ -2161,7 +2206,12 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
         const uint64_t tk = __ballot(E != 0u);
         const uint32_t m = ~tk ? (uint32_t)__builtin_ctzll(~tk) : 64u;
         if (m) {
-          if (l < m) { s_rst[NS - vs + l] = tc0 + S; s_ren[NS - vs + l] = tc0 + (E & 0x7FFFu); }
+          // lane id and record index recomputed here: a loop-invariant record address would be hoisted,
+          // spilled, and its reload would wait on every store in flight
+          uint32_t li;
+          asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(li));
+          const uint32_t nr = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(NS - vs));
+          if (li < m) { s_rst[nr + li] = tc0 + S; s_ren[nr + li] = tc0 + (E & 0x7FFFu); }
           const uint32_t E0 = (uint32_t)__builtin_amdgcn_readlane((int)E, 0), El = (uint32_t)__builtin_amdgcn_readlane((int)E, (int)m - 1);
           if (q == 0) B.first_gc = (E0 & 0x8000u) != 0u;
           B.last_gc = (El & 0x8000u) != 0u;
@@ -2180,8 +2230,12 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
         pos = end;
       }
       B.b1 = pos;
-      if (!bad && l == 0) blk[base + b] = B;
+      if (!bad) {   // staged in LDS, stored 64 at a time (a store per block would be waited on by the next block's loads)
+        if (l == 0) s_blk[bq] = B;
+        if (++bq == 64u) flush_blk(b + 1);
+      }
     }
+    if (!bad && bq) flush_blk(nb);
     if (have && !bad) validate();
     const uint32_t ds0 = pos;
     // U0's delete set must already be in union order (client descending, clock ascending): checked by

@@ -1951,7 +1951,7 @@ YDEV_NI uint64_t big_skip_global(const uint8_t* u0p, uint32_t n0, uint32_t pos) 
 #define YGM_BIG_WAVES 16
 #endif
 constexpr uint32_t BIG_WAVES = YGM_BIG_WAVES, BIG_THREADS = BIG_WAVES * WAVE;
-struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; };   // cmd 0 done, 1 spec, 2 validate
+struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; };   // cmd 0 done, 1 spec, 2 validate, 3 clock ranges
 // the struct start 2^(k+1) structs after tile position i < BT_CH (k = -1: the next one, from nx), or BJ_NONE
 YDEV uint32_t big_jump(const BigTile& T, int k, uint32_t i) {
   if (k < 0) { const uint32_t e = T.nx[i]; return e ? (e & 0x7FFFu) : BJ_NONE; }
@@ -2028,6 +2028,20 @@ YDEV bool big_validate(const BigTile& T, const uint32_t* rs, const uint32_t* re,
   return vbad;
 }
 
+// block clock ranges [vs, ns) of the block table (cmd 3, the whole workgroup): clock0 + the validated lengths of
+// the block's struct records; true if one passes 2^32 - 1
+YDEV bool big_clock_ranges(BigBlk* blk, const BigRec* rec, const BigCmd& C, uint32_t t0) {
+  bool bad = false;
+  for (uint64_t b = C.vs + t0; b < C.ns; b += BIG_THREADS) {
+    const uint32_t nst = blk[b].nst, s0 = blk[b].s0;
+    uint64_t clk = blk[b].clock0;
+    for (uint32_t q = 0; q < nst; q++) clk += rec[C.sbase + s0 + q].len;
+    bad |= clk > 0xFFFFFFFFull;
+    blk[b].clock1 = clk;
+  }
+  return bad;
+}
+
 __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                     const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
                                                     uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
@@ -2047,6 +2061,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       const BigCmd C = s_cmd;
       if (C.cmd == 0) return;
       if (C.cmd == 1) big_spec(T0, C.at, C.mis, C.tn, C.n0, threadIdx.x);
+      else if (C.cmd == 3) { if (big_clock_ranges(blk, rec, C, threadIdx.x)) L.bad = 1; }
       else if (big_validate(T0, s_rst, s_ren, rec, C, flags, threadIdx.x)) L.bad = 1;
       __syncthreads();
     }
@@ -2249,16 +2264,11 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // validated lengths before the clock-range pass
   wave_sync();
   if (!L.bad) {
-    // block clock ranges: clock0 + the lengths of the block's structs
-    for (uint64_t b = l; b < nb && !L.bad; b += WAVE) {
-      const BigBlk B = blk[base + b];
-      uint64_t clk = B.clock0;
-      for (uint32_t q = 0; q < B.nst; q++) clk += rec[sbase + B.s0 + q].len;
-      if (clk > 0xFFFFFFFFull) L.bad = 1;
-      blk[base + b].clock1 = clk;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    wave_sync();
+    // block clock ranges, the whole workgroup: clock0 + the lengths of the block's structs
+    if (l == 0) { s_cmd.cmd = 3; s_cmd.vs = base; s_cmd.ns = base + nb; s_cmd.sbase = sbase; }
+    __syncthreads();
+    if (big_clock_ranges(blk, rec, s_cmd, l)) L.bad = 1;
+    __syncthreads();
   }
   if (l == 0) s_cmd.cmd = 0;   // the helper waves are done: everything below is wave 0's
   __syncthreads();

@@ -41,11 +41,13 @@ __device__ unsigned long long ygm_diag_ts[16384 * 8];
 #define DIAGL(i) do { if (threadIdx.x == 0) ygm_diag_ts[(blockIdx.x & 16383u) * 8 + 1 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define DIAG_NOW() __builtin_amdgcn_s_memrealtime()
 #define DIAG_PUT(i, v) do { if (threadIdx.x == 0) ygm_diag_ts[(blockIdx.x & 16383u) * 8 + (i)] = (v); } while (0)
+#define DIAG_C(...) __VA_ARGS__
 #else
 #define DIAGL_T0
 #define DIAGL(i)
 #define DIAG_NOW() 0ull
 #define DIAG_PUT(i, v)
+#define DIAG_C(...)
 #define DIAGW(i)
 #define DIAG_T0
 #define DIAG(i)
@@ -2138,6 +2140,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   // the tile is U0 byte tb + j, so tile cursors run in tile coordinates (pointers stay inside T0)
   uint32_t tc0 = 0, tb = 0, tn = 0;                        // tn: tile cursor end (tile coordinates)
   uint64_t dg_spec = 0, dg_val = 0;                        // diagnostic build: time in the speculative parse / validation
+  DIAG_C(uint64_t dc_blk = 0, dc_step = 0, dc_st = 0, dc_glob = 0, dc_hslow = 0;)   // ... and follow counts
   const uint8_t* const tp = (const uint8_t*)T0.b;
   auto load_tile = [&](uint32_t at, bool spec) {
     const uint32_t mis = (uint32_t)((uintptr_t)(u0p + at) & 15u);
@@ -2191,29 +2194,35 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     };
     for (uint64_t b = 0; b < nb && !bad; b++) {
       if (!have || pos >= tc0 + BT_CH) { if (have) validate(); load_tile(pos, true); have = true; }
-      BigBlk B;
       uint64_t hn, hc, hk;
       uint32_t he;
       bool hnm;
+      DIAG_C(dc_blk++;)
       if (!big_hdr_fast(T0, pos - tb, tn, hn, hc, hk, he, hnm)) {
+        DIAG_C(dc_hslow++;)
         GCur h; h.init(tp, tn); h.pos = pos - tb; h.nm = 0;
         hn = h.vu(); hc = h.vu(); hk = h.vu();
         bad |= h.err != 0;
         he = h.pos; hnm = h.nm != 0;
       }
-      B.nst = (uint32_t)hn; B.client = hc; B.clock0 = hk;
-      bad |= B.nst == 0 || B.client >= prevc || B.client > 0xFFFFFFFFull;
-      prevc = B.client;
-      B.h0 = pos; B.hcanon = !hnm; B.pad = 0;
+      // the block record goes to its LDS staging slot now (nothing of it stays live across the struct loop)
+      const uint32_t bnst = (uint32_t)hn;
+      bad |= bnst == 0 || hc >= prevc || hc > 0xFFFFFFFFull;
+      prevc = hc;
+      const uint32_t h0 = pos;
       pos = he + tb;
-      B.b0 = pos; B.s0 = (uint32_t)NS;
-      B.first_gc = 0; B.last_gc = 0; B.clock1 = 0;
-      for (uint32_t q = 0; q < B.nst && !bad;) {
+      if (l == 0) {
+        BigBlk& B = s_blk[bq];
+        B.nst = bnst; B.client = hc; B.clock0 = hk; B.clock1 = 0;
+        B.h0 = h0; B.hcanon = !hnm; B.pad = 0; B.b0 = pos; B.s0 = (uint32_t)NS;
+      }
+      uint32_t fgc = 0, lgc = 0;
+      for (uint32_t q = 0; q < bnst && !bad;) {
         if (pos >= tc0 + BT_CH) { validate(); load_tile(pos, true); }
         // up to 64 of the block's structs per step: lane j finds the start of struct q + j by composing
         // the jump tables along the bits of j; the structs taken are the leading lanes that start inside
         // the tile and have a speculative parse
-        const uint32_t want = B.nst - q < 64u ? B.nst - q : 64u;
+        const uint32_t want = bnst - q < 64u ? bnst - q : 64u;
         uint32_t S = pos - tc0;
         for (int k = 0; k < 6 && ((want - 1u) >> k); k++)
           if (((l >> k) & 1u) && S < BT_CH) S = big_jump(T0, k - 1, S);
@@ -2228,25 +2237,26 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
           const uint32_t nr = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(NS - vs));
           if (li < m) { s_rst[nr + li] = tc0 + S; s_ren[nr + li] = tc0 + (E & 0x7FFFu); }
           const uint32_t E0 = (uint32_t)__builtin_amdgcn_readlane((int)E, 0), El = (uint32_t)__builtin_amdgcn_readlane((int)E, (int)m - 1);
-          if (q == 0) B.first_gc = (E0 & 0x8000u) != 0u;
-          B.last_gc = (El & 0x8000u) != 0u;
+          if (q == 0) fgc = (E0 >> 15) & 1u;
+          lgc = (El >> 15) & 1u;
           NS += m; q += m;
+          DIAG_C(dc_step++; dc_st += m;)
           pos = tc0 + (El & 0x7FFFu);
           continue;
         }
         // the struct at pos has no speculative parse: parsed from global memory
         const uint64_t r = big_skip_global(u0p, n0, pos);
+        DIAG_C(dc_glob++;)
         bad |= (r >> 63) != 0;
         const uint32_t kind = (uint32_t)(r >> 32) & 1u, end = (uint32_t)r;
         if (l == 0) { s_rst[NS - vs] = pos; s_ren[NS - vs] = end; }
-        if (q == 0) B.first_gc = kind == 0;
-        B.last_gc = kind == 0;
+        if (q == 0) fgc = kind == 0;
+        lgc = kind == 0;
         NS++; q++;
         pos = end;
       }
-      B.b1 = pos;
       if (!bad) {   // staged in LDS, stored 64 at a time (a store per block would be waited on by the next block's loads)
-        if (l == 0) s_blk[bq] = B;
+        if (l == 0) { BigBlk& B = s_blk[bq]; B.b1 = pos; B.first_gc = (uint8_t)fgc; B.last_gc = (uint8_t)lgc; }
         if (++bq == 64u) flush_blk(b + 1);
       }
     }
@@ -2260,6 +2270,9 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   }
 #ifndef YGM_DIAG_BIGDS
   DIAG_PUT(6, dg_spec); DIAG_PUT(7, dg_val);
+  DIAG_C(if (l == 0) { atomicAdd(&ygm_diag[16], (unsigned long long)dc_blk); atomicAdd(&ygm_diag[17], (unsigned long long)dc_step);
+                       atomicAdd(&ygm_diag[18], (unsigned long long)dc_st); atomicAdd(&ygm_diag[19], (unsigned long long)dc_glob);
+                       atomicAdd(&ygm_diag[20], (unsigned long long)dc_hslow); })
 #endif
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // validated lengths before the clock-range pass
   wave_sync();

@@ -27,6 +27,13 @@ ts = np.zeros(16384 * 8, np.uint64)
 e.merge_packed(arena, upd_off, upd_doc, n)
 e.merge_packed(arena, upd_off, upd_doc, n)
 L.ygm_diag_ts_read(ts.ctypes.data, 0)
+L.ygm_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+cnt = np.zeros(32, np.uint64)
+L.ygm_diag_read(cnt.ctypes.data, 0)
+# follow counts over both runs (slots 16-20): client blocks, jump steps, structs taken by them, structs parsed
+# from global memory, block headers that took the cursor parse
+print("follow counts (2 runs): blocks", int(cnt[16]), "jump steps", int(cnt[17]), "structs by jump", int(cnt[18]),
+      "global parses", int(cnt[19]), "slow headers", int(cnt[20]))
 st = e.stats()
 print("docs_big", st.docs_big, "docs_seq", st.docs_seq)
 t = ts.reshape(16384, 8)[:n].astype(np.int64)

@@ -6,5 +6,5 @@ cd "$(dirname "$0")/../hocuspocus_amd/csrc"
 make -s -j4 >/dev/null
 mkdir -p ../exp build/exp
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -pthread $2 -c -o build/exp/$1.o ygm_kernels.hip
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -pthread -shared -o ../exp/libygm_$1.so build/exp/$1.o build/ygm_snapshot.hip.o build/ygm_engine.cpp.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -pthread -shared -o ../exp/libygm_$1.so build/exp/$1.o $(ls build/*.o | grep -v -e ygm_kernels -e '/diag_')
 echo ../exp/libygm_$1.so

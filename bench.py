@@ -11,6 +11,7 @@ the lean kernel -- asserted -- so no step needs the host-driven tiers).  Beside 
 
   c2_100k  the same merge at 100 000 documents per GPU (0.47 GB in: past the 256 MiB Infinity Cache,
            so the HBM fraction is not L3-served)
+  c2_1m    the same merge over 1 000 000 documents in all (4.7 GB in, sharded over the ranks): the north_star size
   c4       config C4 (configs[3]): 1 000 000 merged Y.Text states (1-16 clients, log-uniform 1-8 KB,
            3.2 GB) sharded over the ranks, encodeStateVectorFromUpdate and diffUpdate against per-document
            state vectors (the mass-reconnect Step1 -> Step2 path, MessageReceiver.ts:137-155)
@@ -60,10 +61,11 @@ def parse():
     ap.add_argument("--docs", type=int, default=10000, help="C2 documents per GPU")
     ap.add_argument("--updates", type=int, default=200)
     ap.add_argument("--c2big-docs", type=int, default=100000, help="C2 documents per GPU of the c2_100k block (0: skip)")
+    ap.add_argument("--c2m-docs", type=int, default=1000000, help="C2 documents in all of the c2_1m block (0: skip)")
     ap.add_argument("--c4-docs", type=int, default=1000000, help="C4 documents in all (0: skip)")
     ap.add_argument("--c4-steps", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="budget of each CPU baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads / workers (0: the cores granted, <= 16)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads / workers (0: every core in the affinity mask)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-yjs", action="store_true", help="skip the Node / yjs leg of the CPU baseline")
     ap.add_argument("--no-v2", dest="v2", action="store_false", help="skip the update-V2 (f-4) block")
@@ -95,9 +97,28 @@ def spawn_ranks(args):
 
 
 def cpu_cores(args):
+    """CPU-baseline threads / Node workers: every core the process may run on (BASELINE north_star: "Node
+    worker_threads = core count, stated"), uncapped; --cpu-threads overrides."""
     if args.cpu_threads:
         return args.cpu_threads
-    return max(1, min(16, len(os.sched_getaffinity(0))))
+    return max(1, len(os.sched_getaffinity(0)))
+
+
+def host_cpus():
+    """What the host grants, stated beside every CPU baseline: the affinity mask, os.cpu_count() and the
+    cgroup CPU quota (cpu.max, in CPUs; null when unlimited or absent)."""
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = None if q <= 0 else round(q / per, 2)
+        except Exception:
+            pass
+    return {"affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota}
 
 
 # ----------------------------------------------------------------------------- backends
@@ -557,7 +578,7 @@ def cpu_port_merge(c, cores, budget_s):
         t, a, st = run(sample, cores)
         assert (st == 0).all()
         dt += t; algo += a; reps += 1
-    return {"value": round(algo / dt / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port", "docs_per_s": round(sample * reps / dt, 1),
+    return {"value": round(algo / dt / 1e6, 3), "unit": "MB/s", "cores": cores, "host": host_cpus(), "kind": "port", "docs_per_s": round(sample * reps / dt, 1),
             "sample": f"{reps} pass(es) over {sample} of the {n} C2 documents through oracle/yjs_oracle.c yo_merge_batch "
                       f"(C restatement of yjs mergeUpdates), {cores} pthreads, {dt:.2f} s wall"}
 
@@ -571,7 +592,7 @@ def cpu_port_doc(c, op, cores, k):
     else:
         st, algo = oracle.doc_batch("sv", c["arena"], c["doc_off"][:k + 1], threads=cores)
     dt = time.perf_counter() - t0
-    return {"value": round(algo / dt / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "port", "docs_per_s": round(k / dt, 1),
+    return {"value": round(algo / dt / 1e6, 3), "unit": "MB/s", "cores": cores, "host": host_cpus(), "kind": "port", "docs_per_s": round(k / dt, 1),
             "sample": f"the first {k} C4 documents through oracle/yjs_oracle.c yo_doc_batch, {cores} pthreads, {dt:.2f} s wall"}
 
 
@@ -600,11 +621,12 @@ def cpu_yjs(kind, c, cores, k):
             return {"error": r.stderr[-300:]}
         j = json.loads(r.stdout.strip().splitlines()[-1])
         ver = subprocess.run(["node", "--version"], capture_output=True, text=True).stdout.strip()
-        return {"value": round(j["algo_bytes"] / j["seconds"] / 1e6, 3), "unit": "MB/s", "cores": cores, "kind": "reference",
+        return {"value": round(j["algo_bytes"] / j["seconds"] / 1e6, 3), "unit": "MB/s", "cores": cores, "host": host_cpus(), "kind": "reference",
                 "docs_per_s": round(k / j["seconds"], 1),
                 "sample": f"yjs 13.5.16 (JupyterLab bundle in the image; the reference pins 13.6.26) Y."
                           f"{ {'merge': 'mergeUpdates', 'merge_v2': 'mergeUpdatesV2', 'sv': 'encodeStateVectorFromUpdate', 'diff': 'diffUpdate', 'snapshot': 'encodeStateAsUpdate(applyUpdate(new Doc, u))'}[kind]} over the first "
-                          f"{k} documents on Node {ver} worker_threads x {cores}, op loop only, slowest worker {j['seconds']:.2f} s"}
+                          f"{k} documents on Node {ver} worker_threads x {cores} (one per core in the affinity mask), op loops only "
+                          f"(common start barrier to the last worker's end) {j['seconds']:.2f} s"}
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -667,6 +689,38 @@ def run_rank(args, rank, world, dist, be, dev=None):
             line["host_api"] = host_api_merge(be, cb, args)
             line["host_api"]["c1_store_window"] = c1_store_window()
         del cb
+    # ---- C2 shape at 1M documents in all (north_star: "mergeUpdates ... over 1M synthetic documents"), 4.7 GB
+    if args.c2m_docs:
+        from tools import synth
+        idx = synth.partition("c2m-", args.c2m_docs, world, rank)
+        a, o, dd = synth.text_updates_docs(idx, args.updates)
+        cm = {"arena": a, "upd_off": o, "doc_upd": dd, "n": len(idx), "n_upd": int(dd[-1]), "bytes": len(a)}
+        cm["da"], cm["do"], cm["dd"] = be.put(a, 64), be.put(o.view(np.int64)), be.put(dd.view(np.int32))
+        sm = max(args.steps // 4, 2)
+        dtm, kmsm, outm, rm = time_merge(be, cm, sm, 1, dist)
+        dtm = allmax(dtm, dist, dev)
+        tot = allsum([cm["n"], cm["bytes"] + outm, cm["bytes"]], dist, dev)
+        if rank == 0:
+            pr = None
+            if not args.dry_run:
+                import oracle
+                st, off, ln, data = be.fetch(rm, cm["n"])
+                ups_of = lambda d: [a[o[u]:o[u + 1]].tobytes() for u in range(dd[d], dd[d + 1])]
+                checked = 0
+                for d in range(0, cm["n"], max(1, cm["n"] // 200)):
+                    exp = oracle.merge_updates(ups_of(d))
+                    assert exp == (int(st[d]), data[int(off[d]):int(off[d]) + int(ln[d])]), f"parity failure on c2_1m document {d}"
+                    checked += 1
+                assert (st == 0).all()
+                pr = f"bit-exact vs oracle on {checked} sampled docs; all {cm['n']} statuses OK"
+            line["c2_1m"] = {"workload": f"C2 shape at {args.c2m_docs} documents in all ('c2m-<i>' sharded by fnv1a64(name) mod {world}), "
+                                         f"{args.updates} single-char insert updates each, batched Y.mergeUpdates, inputs resident in HBM",
+                             "docs_total": int(tot[0]), "bytes_in_total": int(tot[2]), "steps": sm,
+                             "value": round(tot[1] * sm / dtm / 1e6, 3), "unit": "MB/s", "docs_per_s": round(tot[0] * sm / dtm, 1),
+                             "ms_per_step": round(dtm / sm * 1e3, 4),
+                             "roofline": roof(cm["bytes"] + outm, kmsm, "k_merge_lean (rank 0)", _pmc(PMC_PROFILE, "k_merge_lean@1m")),
+                             "parity": pr}
+        del cm, a, o, dd
     # ---- C4: 1M merged states, state vector + diffUpdate (strong scaling over the ranks)
     if args.c4_docs:
         from tools import synth
@@ -734,9 +788,9 @@ def run_rank(args, rank, world, dist, be, dev=None):
         port = cpu_port_merge(c2, cores, args.cpu_seconds)
         y = None if args.no_yjs else cpu_yjs("merge", c2, cores, min(c2["n"], 4000))
         if y and "value" in y:
-            line["cpu_baseline"] = dict(y, port=port, os_cpu_count=os.cpu_count())
+            line["cpu_baseline"] = dict(y, port=port, host=host_cpus())
         else:
-            line["cpu_baseline"] = dict(port, yjs=y, os_cpu_count=os.cpu_count())
+            line["cpu_baseline"] = dict(port, yjs=y, host=host_cpus())
         if args.c4_docs:
             for op in ("sv", "diff"):
                 e = {"port": cpu_port_doc(c4, op, cores, min(c4["n"], 200000))}
@@ -792,7 +846,7 @@ def big_run(args, kind, dev_index=0):
     cdt = time.perf_counter() - t0
     assert (st == 0).all()
     sizes = np.diff(upd_off[doc_upd].astype(np.int64))
-    port = {"ms": round(cdt * 1e3, 3), "MBps": round(calgo / cdt / 1e6, 1), "cores": cores, "kind": "port",
+    port = {"ms": round(cdt * 1e3, 3), "MBps": round(calgo / cdt / 1e6, 1), "cores": cores, "host": host_cpus(), "kind": "port",
             "sample": "all documents of the batch through oracle/yjs_oracle.c yo_merge_batch, one pass"}
     y = None if (args.no_yjs or args.no_cpu_baseline) else cpu_yjs("merge", {"arena": arena, "upd_off": upd_off, "doc_upd": doc_upd}, cores, n)
     if y and "value" in y:

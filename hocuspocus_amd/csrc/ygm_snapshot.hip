@@ -111,7 +111,10 @@ __global__ __launch_bounds__(SN_NT) void k_cont_count(const uint8_t* __restrict_
   if (n) snap::count_doc(st_arena + a, n, flags, S, D, C);
   need[d] = snap::al16((uint64_t)(C + 1) * sizeof(CtSv)) + snap::al16((uint64_t)(D + 1) * sizeof(CtDs));
 }
-YDEV_NI int contains_doc(const uint8_t* sp, uint32_t sn, const uint8_t* up, uint32_t un, uint32_t flags, uint8_t* ws, uint32_t& res) {
+// ws holds ws_bytes (k_cont_count's size for the document): a snapshot with more blocks or ranges than
+// counted (count_doc zeroes its counts past 2^26 structs / ranges) is refused, never written past
+YDEV_NI int contains_doc(const uint8_t* sp, uint32_t sn, const uint8_t* up, uint32_t un, uint32_t flags, uint8_t* ws, uint64_t ws_bytes,
+                         uint32_t& res) {
   res = 0;
   // the snapshot: state vector (clients of the blocks) and delete set
   Cur c{sp, 0, sn, 0, 0};
@@ -122,6 +125,7 @@ YDEV_NI int contains_doc(const uint8_t* sp, uint32_t sn, const uint8_t* up, uint
     const uint64_t ns = c.vu(), cl = c.vu(); uint64_t ck = c.vu();
     for (uint64_t s = 0; s < ns && !c.err; s++) { SInfo si; read_struct(c, si, flags); ck += si.len; }
     if (cl > 0xFFFFFFFFull || ck > 0xFFFFFFFFull) return snap::ST_UNSUP;
+    if (snap::al16((uint64_t)(nsv + 2) * sizeof(CtSv)) + 16u > ws_bytes) return snap::ST_UNSUP;
     sv[nsv].client = (uint32_t)cl; sv[nsv].end = (uint32_t)ck; nsv++;
   }
   if (c.err) return c.err;
@@ -133,6 +137,7 @@ YDEV_NI int contains_doc(const uint8_t* sp, uint32_t sn, const uint8_t* up, uint
     for (uint64_t r = 0; r < nr && !c.err; r++) {
       const uint64_t ck = c.vu(), ln = c.vu();
       if (cl > 0xFFFFFFFFull || ck + ln > 0xFFFFFFFFull) return snap::ST_UNSUP;
+      if ((uint64_t)((uint8_t*)(ds + nds + 1) - ws) > ws_bytes) return snap::ST_UNSUP;
       ds[nds].client = (uint32_t)cl; ds[nds].clock = (uint32_t)ck; ds[nds].end = (uint32_t)(ck + ln); nds++;
     }
   }
@@ -179,7 +184,7 @@ __global__ __launch_bounds__(SN_NT) void k_cont(const uint8_t* __restrict__ st_a
   uint32_t res = 0;
   int st;
   if (b < a || ub < ua || b - a >= (1ull << 30) || ub - ua >= (1ull << 30)) st = ST_INVAL;
-  else st = contains_doc(st_arena + a, (uint32_t)(b - a), up_arena + ua, (uint32_t)(ub - ua), flags, ws + ws_off[d], res);
+  else st = contains_doc(st_arena + a, (uint32_t)(b - a), up_arena + ua, (uint32_t)(ub - ua), flags, ws + ws_off[d], ws_off[d + 1] - ws_off[d], res);
   out[d] = (uint8_t)res;
   out_off[d] = d; out_len[d] = st == ST_OK ? 1u : 0u; status[d] = st;
 }

@@ -25,7 +25,7 @@ LIB_PATH = os.environ.get("YGM_LIB") or os.path.join(_HERE, "libygm.so")  # YGM_
 
 OK, EMALFORMED, ERANGE, ENONCANON, ESURROGATE, EDEPTH, ENOMEM, EDEVICE, EINVAL, EUNSUPPORTED = range(10)
 STATUS_NAMES = {0: "OK", 1: "EMALFORMED", 2: "ERANGE", 3: "ENONCANON", 4: "ESURROGATE", 5: "EDEPTH",
-                6: "ENOMEM", 7: "EDEVICE", 8: "EINVAL"}
+                6: "ENOMEM", 7: "EDEVICE", 8: "EINVAL", 9: "EUNSUPPORTED"}
 F_COMPAT_135 = 1
 F_FORCE_SEQ = 2
 

@@ -109,5 +109,5 @@ export declare class GpuMerge implements Extension {
   /** batched SyncStep1 responder over the captured state (snapshot + updates since) */
   syncResponder (): SyncResponder
   /** batched extension-redis fan-out over the same captured state */
-  redisFanout (opts: { publish: (channel: string, message: Buffer) => any, identifier?: string, prefix?: string, windowMs?: number }): RedisFanout
+  redisFanout (opts: { publish: (channel: string, message: Buffer) => any, identifier?: string, prefix?: string, windowMs?: number, onError?: (e: Error) => void }): RedisFanout
 }

@@ -150,8 +150,11 @@ class GpuMerge {
     const taken = entry.log.length
     const parts = (entry.base ? [entry.base] : []).concat(entry.log.slice(0, taken))
     let state
-    let all = false   // the state holds every update applied so far (not only the `taken` ones)
-    if (parts.length === 0) { state = this._Y().encodeStateAsUpdate(data.document); all = true } // nothing captured: extension-database's bytes
+    // updates the stored state holds: the `taken` ones, or -- when the state is the live document's
+    // encodeStateAsUpdate -- every update captured up to that synchronous call (updates that arrive
+    // while storeMany is pending are not in it and stay in the log)
+    let cut = taken
+    if (parts.length === 0) { state = this._Y().encodeStateAsUpdate(data.document); cut = entry.log.length } // nothing captured: extension-database's bytes
     else if (parts.length === 1) state = parts[0]
     else {
       try {
@@ -164,13 +167,13 @@ class GpuMerge {
         if (this.configuration.onRefused === 'throw') throw e
         this.refused.push({ documentName: data.documentName, code: e.code || String(e) })
         state = this._Y().encodeStateAsUpdate(data.document)
-        all = true
+        cut = entry.log.length
       }
     }
     await this.store.storeMany([{ payload: data, state: Buffer.from(state.buffer, state.byteOffset, state.byteLength) }])
     // the stored state becomes the new base (under the document's saveMutex, Hocuspocus.ts:427)
     entry.base = state
-    entry.log.splice(0, all ? entry.log.length : taken)
+    entry.log.splice(0, cut)
   }
 
   // the doc-normalized snapshot of a merged state; outside the kernel's envelope the merge is kept

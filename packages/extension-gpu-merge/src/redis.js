@@ -26,7 +26,7 @@ class RedisFanout {
    *   getState: the document's stored update or [snapshot, ...log] (GpuMerge: syncResponder()'s source)
    *   publish: the Redis client's publish (ioredis pub.publish)
    */
-  constructor ({ engine, getState, publish, identifier, prefix = 'hocuspocus', windowMs = 2 }) {
+  constructor ({ engine, getState, publish, identifier, prefix = 'hocuspocus', windowMs = 2, onError }) {
     this.engine = engine
     this.getState = getState
     this.publish = publish
@@ -42,6 +42,16 @@ class RedisFanout {
     this.t1 = null
     this.t2 = null
     this.batches = { step1: 0, replies: 0 }
+    this.onError = onError || null
+    this.errors = []   // failed Step1 publish batches (the change's onChange has already resolved)
+  }
+
+  // a failed background batch must not become an unhandled rejection (which ends a Node server):
+  // it is recorded and reported, as the reference logs a failed publish
+  _report (e) {
+    this.errors.push(e)
+    if (this.onError) this.onError(e)
+    else console.error('[GpuMerge RedisFanout] Step1 publish batch failed:', e && e.message ? e.message : e)
   }
 
   pubKey (documentName) { return `${this.prefix}:${documentName}` }
@@ -60,7 +70,7 @@ class RedisFanout {
       const waiters = this.pendingStep1.get(data.documentName) || []
       waiters.push(resolve)
       this.pendingStep1.set(data.documentName, waiters)
-      if (!this.t1) this.t1 = setTimeout(() => { this.t1 = null; this._flushStep1() }, this.windowMs)
+      if (!this.t1) this.t1 = setTimeout(() => { this.t1 = null; this._flushStep1().catch(e => this._report(e)) }, this.windowMs)
     })
   }
 

@@ -161,10 +161,23 @@ SyncResponder.prototype.answerReadOnlyMany = async function (messages) {
   const fetched = await Promise.all(names.map(n => this.getState(n)))
   const parts = fetched.map(f => Array.isArray(f) ? f.filter(Boolean) : (f ? [f] : []))
   const merged = await this._merge(names, parts.map(p => p.length ? p : [new Uint8Array([0, 0])]))
-  const snaps = await (this._pooled() ? this.engine.snapshotMany(names, merged) : this.engine.snapshotMany(merged))
-  const snapOf = new Map(names.map((n, k) => [n, snaps[k]]))
+  // a document whose merge the engine refuses answers with that Error; only healthy states go on
+  const snapOf = new Map()
+  const ok = []
+  names.forEach((n, k) => { if (merged[k] instanceof Error) snapOf.set(n, merged[k]); else ok.push(k) })
+  const snaps = ok.length
+    ? await (this._pooled() ? this.engine.snapshotMany(ok.map(k => names[k]), ok.map(k => merged[k])) : this.engine.snapshotMany(ok.map(k => merged[k])))
+    : []
+  ok.forEach((k, j) => snapOf.set(names[k], snaps[j]))
+  // a state outside the snapshot kernel's envelope (pending structs or delete set, sub-documents:
+  // EUNSUPPORTED) still gets a SyncStatus, as the reference always sends one (MessageReceiver.ts:157-179):
+  // SyncStatus(false) -- "not known to be contained", the conservative answer, under which the
+  // provider keeps reporting unsynced changes rather than dropping them
+  const unsup = a => { const s = snapOf.get(a.documentName); return s instanceof Error && s.code === 'EUNSUPPORTED' }
+  asks.filter(unsup).forEach(a => { out[a.i] = syncStatusFrame(a.documentName, false) })
   const live = asks.filter(a => !(snapOf.get(a.documentName) instanceof Error))
-  asks.filter(a => snapOf.get(a.documentName) instanceof Error).forEach(a => { out[a.i] = snapOf.get(a.documentName) })
+  asks.filter(a => snapOf.get(a.documentName) instanceof Error && !unsup(a)).forEach(a => { out[a.i] = snapOf.get(a.documentName) })
+  if (!live.length) return out
   const res = await (this._pooled()
     ? this.engine.containsMany(live.map(a => a.documentName), live.map(a => snapOf.get(a.documentName)), live.map(a => a.payload))
     : this.engine.containsMany(live.map(a => snapOf.get(a.documentName)), live.map(a => a.payload)))

@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--c4-docs", type=int, default=1000000, help="C4 documents in all (0: skip)")
     ap.add_argument("--c4-steps", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="budget of each CPU baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads / workers (0: every core in the affinity mask)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads / workers (0: the cores granted: affinity mask, cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-yjs", action="store_true", help="skip the Node / yjs leg of the CPU baseline")
     ap.add_argument("--no-v2", dest="v2", action="store_false", help="skip the update-V2 (f-4) block")
@@ -97,11 +97,18 @@ def spawn_ranks(args):
 
 
 def cpu_cores(args):
-    """CPU-baseline threads / Node workers: every core the process may run on (BASELINE north_star: "Node
-    worker_threads = core count, stated"), uncapped; --cpu-threads overrides."""
+    """CPU-baseline threads / Node workers = the cores the host grants this process (BASELINE north_star: "Node
+    worker_threads = core count, stated"): the affinity mask, bounded by the cgroup CPU quota when one is set --
+    on the GPU box the mask lists 256 CPUs but cpu.max grants 16 CPUs of time, and 256 workers time-sliced on
+    16 CPUs measure the throttling, not the reference (r03 run: yjs merge 15 MB/s on 256 workers vs 113 MB/s on
+    16).  Both numbers are stated beside every baseline (host_cpus()); --cpu-threads overrides."""
     if args.cpu_threads:
         return args.cpu_threads
-    return max(1, len(os.sched_getaffinity(0)))
+    h = host_cpus()
+    n = h["affinity"]
+    if h["cgroup_cpu_quota"]:
+        n = min(n, max(1, int(h["cgroup_cpu_quota"] + 0.999)))
+    return max(1, n)
 
 
 def host_cpus():
@@ -625,7 +632,7 @@ def cpu_yjs(kind, c, cores, k):
                 "docs_per_s": round(k / j["seconds"], 1),
                 "sample": f"yjs 13.5.16 (JupyterLab bundle in the image; the reference pins 13.6.26) Y."
                           f"{ {'merge': 'mergeUpdates', 'merge_v2': 'mergeUpdatesV2', 'sv': 'encodeStateVectorFromUpdate', 'diff': 'diffUpdate', 'snapshot': 'encodeStateAsUpdate(applyUpdate(new Doc, u))'}[kind]} over the first "
-                          f"{k} documents on Node {ver} worker_threads x {cores} (one per core in the affinity mask), op loops only "
+                          f"{k} documents on Node {ver} worker_threads x {cores} (one per granted core), op loops only "
                           f"(common start barrier to the last worker's end) {j['seconds']:.2f} s"}
     finally:
         shutil.rmtree(d, ignore_errors=True)

@@ -37,7 +37,13 @@
 
 namespace ygm {
 
-constexpr int DW_S = 4;           // 64-byte chunk slots per lane ring
+#ifndef YGM_DW_S
+#define YGM_DW_S 4
+#endif
+#ifndef YGM_DW_BATCH
+#define YGM_DW_BATCH 256
+#endif
+constexpr int DW_S = YGM_DW_S;    // 64-byte chunk slots per lane ring (a power of two)
 constexpr int DW_P = DW_S * 4;    // 16-byte pieces per ring
 #ifndef YGM_DW_R
 #define YGM_DW_R 4
@@ -52,7 +58,7 @@ constexpr int DW_R = YGM_DW_R;    // parse iterations per round
 constexpr int DW_U = YGM_DW_U;    // Items the fast decoder takes per iteration (from one 64-byte mask window)
 constexpr uint32_t DW_STG = YGM_DW_STG;   // chunks staged per round (<= 4: 64 staging registers)
 constexpr uint32_t DW_AHEAD = 2;  // chunks staged past the ring's free slots (committed if the round freed theirs)
-constexpr int DW_BATCH = 256;     // documents sorted (largest first) per batch of a wave's range
+constexpr int DW_BATCH = YGM_DW_BATCH;   // documents sorted (largest first) per batch of a wave's range
 constexpr int DW_SVN = 16;        // state-vector entries per lane (diff)
 constexpr uint32_t DW_OPEN = 0xFFFFFFFFu;
 

@@ -215,8 +215,14 @@ __global__ __launch_bounds__(WAVE) void k_sv_table(const uint8_t* __restrict__ s
   tbl_n[d] = n;
 }
 
+#ifndef YGM_DW_WPE0
+#define YGM_DW_WPE0 2   // waves per SIMD the SV walker is compiled for (register budget 512 / waves)
+#endif
+#ifndef YGM_DW_WPE1
+#define YGM_DW_WPE1 2   // ... the diff walker
+#endif
 template <int MODE>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2))) void k_doc_walk(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off,
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? YGM_DW_WPE0 : YGM_DW_WPE1))) void k_doc_walk(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off,
                                                   const uint8_t* __restrict__ tbl, const uint32_t* __restrict__ tbl_n,
                                                   uint32_t n_docs, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                   uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
@@ -2644,7 +2650,8 @@ int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, 
   static int n_cu = 0;
   if (!n_cu) { int dev = 0; (void)hipGetDevice(&dev); if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256; }
   const char* env = getenv("YGM_WALK_WAVES_PER_CU");
-  const uint32_t wpc = env ? (uint32_t)atoi(env) : 8u;   // resident waves per CU (LDS 20 KB per wave)
+  // resident waves per CU: 4 SIMDs x the waves per SIMD the walker is compiled for (its LDS fits them)
+  const uint32_t wpc = env ? (uint32_t)atoi(env) : 4u * (mode == 0 ? YGM_DW_WPE0 : YGM_DW_WPE1);
   const uint32_t waves = (n_docs + WAVE - 1) / WAVE, cap = (uint32_t)n_cu * (wpc ? wpc : 1u);
   uint32_t grid = waves < cap ? waves : cap;
   const char* genv = getenv("YGM_WALK_GRID");   // testing: a small grid gives every lane many documents

@@ -402,9 +402,10 @@ def mixed_block(be, args, steps=5):
                         "(updates up to ~42 bytes), batched Y.mergeUpdates through the tier cascade, inputs resident in HBM",
             "docs": n, "bytes_in": len(arena), "bytes_out": int(r.payload_bytes), "value": round(algo / kms / 1e3, 3), "unit": "MB/s",
             "docs_per_s": round(n / kms * 1e3, 1), "ms_per_step": round(kms, 4),
-            "docs_lean": int((s1.docs_lean - s0.docs_lean) / steps), "docs_general_tiers": int((s1.docs_fast - s0.docs_fast) / steps),
+            "docs_lean": int((s1.docs_lean - s0.docs_lean) / steps), "docs_lean_wide": int((s1.docs_lean_wide - s0.docs_lean_wide) / steps),
+            "docs_general_tiers": int((s1.docs_fast - s0.docs_fast) / steps),
             "docs_big": int((s1.docs_big - s0.docs_big) / steps), "docs_seq": int((s1.docs_seq - s0.docs_seq) / steps),
-            "roofline": roof(algo, kms, "k_merge_lean + k_merge_wave / k_merge_fast for the documents it defers", None),
+            "roofline": roof(algo, kms, "k_merge_lean<0> + k_merge_lean<1> (wide) over its deferrals + the general tiers for the rest", None),
             "parity": f"bit-exact vs oracle on {checked} sampled docs"}
 
 

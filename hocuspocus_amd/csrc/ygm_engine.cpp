@@ -42,6 +42,9 @@ int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, 
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
                             uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
+int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, const uint32_t* list,
+                                 uint32_t n_list, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
+                                 void* meta, uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
                             const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
                             int32_t* status, void* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
@@ -76,7 +79,7 @@ namespace {
 
 // mirrors ygm::DocMeta (ygm_kernels.hip); sizeof is a multiple of 16
 struct Meta {
-  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer;
+  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer, wide_defer, pad_[3];
   unsigned long long big_scur;
   unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor, big_cursor;
   unsigned long long payload_sh[16 * 16];
@@ -131,7 +134,7 @@ struct ygm_ctx {
   // device inputs (host API staging)
   DevBuf arena, offs, docs, sv_arena, sv_offs;
   // device outputs + state
-  DevBuf out, out_off, out_len, status, lb, meta, fb_list, defer_list, defer2_list;
+  DevBuf out, out_off, out_len, status, lb, meta, fb_list, defer_list, defer2_list, defer_w_list;
   Meta* h_meta = nullptr;  // pinned read-back of the per-launch counters
   int mslot = 0;           // counter slot of the next merge launch
   void* meta_slot(int i) const { return (uint8_t*)meta.p + (size_t)i * sizeof(Meta); }
@@ -235,7 +238,8 @@ static int prep_outputs(ygm_ctx* c, uint32_t n_docs, uint64_t out_cap, hipStream
   const size_t tiles = (size_t)n_docs / 256 + 2;  // look-back tiles of the SV/diff kernels (256 documents each)
   if (!c->out.ensure(out_cap + 64) || !c->out_off.ensure((size_t)n_docs * 8 + 8) || !c->out_len.ensure((size_t)n_docs * 8 + 8) ||
       !c->status.ensure((size_t)n_docs * 4 + 4) || !c->lb.ensure(tiles * 8) || !c->fb_list.ensure((size_t)n_docs * 4 + 4) ||
-      !c->defer_list.ensure((size_t)n_docs * 4 + 4) || !c->defer2_list.ensure((size_t)n_docs * 4 + 4))
+      !c->defer_list.ensure((size_t)n_docs * 4 + 4) || !c->defer2_list.ensure((size_t)n_docs * 4 + 4) ||
+      !c->defer_w_list.ensure((size_t)n_docs * 4 + 4))
     return YGM_ENOMEM;
   if (lookback) {   // SV / diff: look-back tiles and counter slot 2 reset per call
     HIPCHK(hipMemsetAsync(c->lb.p, 0, tiles * 8, s));
@@ -305,9 +309,23 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
   if (c->lean_span_n && hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) { c->stats.kernel_ms += ms0; c->stats.lean_ms += ms0; }
   c->stats.lean_launches += c->lean_span_n;
   c->lean_span_n = 0;
-  if (m.lean_defer) {  // tier 2: general wave-per-document kernel over the lean kernel's deferred list
+  uint32_t n_gen = 0;   // documents for the general tiers
+  if (m.lean_defer) {  // tier 1b: the wide lean kernel (updates <= 64 bytes, documents <= 7 KB) over tier 1's deferred list
     HIPCHK(hipEventRecord(c->e0, s));
-    if (ygm_k_launch_merge_wave(P.arena, P.upd_off, P.doc_upd, c->defer_list.as<uint32_t>(), nullptr, m.lean_defer, c->flags,
+    if (ygm_k_launch_merge_lean_wide(P.arena, P.upd_off, P.doc_upd, P.n_docs, c->defer_list.as<uint32_t>(), m.lean_defer, c->flags,
+                                     c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
+                                     P.meta, c->defer_w_list.as<uint32_t>(), P.out_cap, s))
+      return YGM_EDEVICE;
+    HIPCHK(hipEventRecord(c->e1, s));
+    if ((e = read_meta(c, s, m, P.meta))) return e;
+    if (m.fault) return YGM_EDEVICE;
+    if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
+    n_gen = m.wide_defer;
+    c->stats.docs_lean_wide += m.lean_defer - m.wide_defer;
+  }
+  if (n_gen) {  // tier 2: general wave-per-document kernel over the lean kernels' deferred list
+    HIPCHK(hipEventRecord(c->e0, s));
+    if (ygm_k_launch_merge_wave(P.arena, P.upd_off, P.doc_upd, c->defer_w_list.as<uint32_t>(), nullptr, n_gen, c->flags,
                                 c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
                                 P.meta, c->defer2_list.as<uint32_t>(), c->fb_list.as<uint32_t>(), P.out_cap, s))
       return YGM_EDEVICE;
@@ -364,8 +382,8 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
   }
   const uint64_t extent = P.slot_total + m.cursor;
   c->stats.calls++; c->stats.docs += P.n_docs; c->stats.updates += P.n_upd;
-  c->stats.docs_fast += m.lean_defer - m.fb_count;   // finished by the wave / workgroup tiers (tier 4 counted above)
-  c->stats.docs_lean += P.n_docs - m.lean_defer;
+  c->stats.docs_fast += n_gen - m.fb_count;   // finished by the wave / workgroup tiers (tier 4 counted above)
+  c->stats.docs_lean += P.n_docs - n_gen;      // finished by the lean kernels (narrow + wide)
   c->stats.bytes_in += P.arena_bytes; c->stats.bytes_out += m.payload_total();
   fill_dev_result(c, extent, out);
   out->payload_bytes = m.payload_total();
@@ -873,7 +891,7 @@ static int host_call(ygm_ctx* c, const HostCall& H, ygm_result* out) {
       c->stats.docs_fast += a.docs_fast - b.docs_fast; c->stats.docs_seq += a.docs_seq - b.docs_seq;
       c->stats.kernel_ms += a.kernel_ms - b.kernel_ms; c->stats.docs_lean += a.docs_lean - b.docs_lean;
       c->stats.lean_ms += a.lean_ms - b.lean_ms; c->stats.lean_launches += a.lean_launches - b.lean_launches;
-      c->stats.docs_big += a.docs_big - b.docs_big;
+      c->stats.docs_big += a.docs_big - b.docs_big; c->stats.docs_lean_wide += a.docs_lean_wide - b.docs_lean_wide;
     }
     int32_t* st = c->h_status.as<int32_t>();
     uint64_t* ln = c->h_len.as<uint64_t>();

@@ -66,6 +66,8 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned int defer_count;         // documents sent from the wave kernel to the workgroup kernel
   unsigned int lean_defer;          // documents sent from the lean kernel to the wave kernel
   unsigned int big_defer;           // documents sent from the large-document kernel to the sequential kernel
+  unsigned int wide_defer;          // documents sent from the wide lean kernel to the wave kernel
+  unsigned int pad_[3];
   unsigned long long big_scur;      // large-document kernel: struct-record entries carved
   unsigned long long fast_total;    // SV/diff: bytes of the packed (look-back placed) output
   unsigned long long cursor;        // merge: bytes in the overflow region (after the per-document slots)
@@ -1518,19 +1520,21 @@ YDEV LeanHdr lean_hdr_of(uint32_t du, uint64_t bo) {
   h.b0 = b0; h.nbytes = b1 - b0;
   return h;
 }
+template <int WIDE>
 YDEV bool lean_stageable(const LeanHdr& h) {
-  return h.k >= 2 && h.k < (uint32_t)(WAVE * LN_ROWS) && (h.b0 & 15u) + h.nbytes <= (uint64_t)LN_IN;
+  return h.k >= 2 && h.k < (uint32_t)(WAVE * LN_ROWS) && (h.b0 & 15u) + h.nbytes <= (uint64_t)LnCfg<WIDE>::IN;
 }
 // issues the loads of one document: staged chunks and the per-row update offsets.  Every
 // load is unconditional (clamped addresses) so the prefetch registers are dead between the
 // staging of one document and the prefetch of the next (no loop-carried live ranges).
+template <int WIDE>
 YDEV void lean_prefetch(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off, const LeanHdr& h, bool go,
-                        u32x4 (&v)[LN_IN / 16 / WAVE], uint32_t (&rx)[LN_ROWS], uint32_t (&ry)[LN_ROWS]) {
+                        u32x4 (&v)[LnCfg<WIDE>::IN / 16 / WAVE], uint32_t (&rx)[LN_ROWS], uint32_t (&ry)[LN_ROWS]) {
   const uint32_t l = threadIdx.x;
   const uint64_t a0 = go ? (h.b0 & ~15ull) : 0ull;
   const uint32_t last = go ? (uint32_t)(((h.b0 & 15u) + h.nbytes + 15) / 16) - 1u : 0u;
 #pragma unroll
-  for (int j = 0; j < LN_IN / 16 / WAVE; j++) {
+  for (int j = 0; j < LnCfg<WIDE>::IN / 16 / WAVE; j++) {
     const uint32_t c = l + WAVE * j;
     v[j] = *(const u32x4*)(arena + a0 + 16ull * (c < last ? c : last));
   }
@@ -1546,13 +1550,19 @@ YDEV void lean_prefetch(const uint8_t* __restrict__ arena, const uint64_t* __res
   }
 }
 
-__global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+// WIDE = 0: the narrow kernel over every document of the batch (wave w: documents w, w + G, ...), which zeroes
+// the next launch's counter slot.  WIDE = 1: the wide kernel (LnCfg<1>) over the narrow kernel's deferred
+// list (wave w: entries w, w + G, ... of `list`), deferring in turn to its own list (meta->wide_defer).
+template <int WIDE>
+__global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                      const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t flags,
                                                      uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                      uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
-                                                     DocMeta* __restrict__ meta_next, uint32_t* __restrict__ defer_list, uint64_t out_cap) {
-  __shared__ LeanLds LS;
-  if (blockIdx.x == 0) {   // the next launch's counter slot (nothing reads it during this launch)
+                                                     DocMeta* __restrict__ meta_next, uint32_t* __restrict__ defer_list, uint64_t out_cap,
+                                                     const uint32_t* __restrict__ list, uint32_t n_list) {
+  typedef LnCfg<WIDE> C;
+  __shared__ LeanLdsT<WIDE> LS;
+  if (!WIDE && blockIdx.x == 0) {   // the next launch's counter slot (nothing reads it during this launch)
     static_assert(sizeof(DocMeta) % 16 == 0, "DocMeta is zeroed in 16-byte pieces");
     const u32x4 z = {0u, 0u, 0u, 0u};
     for (uint32_t i = threadIdx.x; i < sizeof(DocMeta) / 16; i += WAVE) ((u32x4*)meta_next)[i] = z;
@@ -1562,16 +1572,29 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
   const uint32_t l = threadIdx.x;
   const uint32_t G = gridDim.x;
   const bool force_seq = (flags & 2u) != 0;
-  uint32_t d = blockIdx.x;
+  // the wave's j-th document: blockIdx.x + j G (narrow), or list entry blockIdx.x + j G (wide; n_docs past the list).
+  // Wide: lane l of lst0 / lst1 holds the entry of iteration 64 b + l / 64 (b + 1) + l (b = the current run)
+  const uint32_t n_it = WIDE ? n_list : n_docs;
+  auto list_at = [&](uint32_t j) -> uint32_t { const uint64_t i = (uint64_t)blockIdx.x + (uint64_t)j * G; return i < n_it ? list[i] : n_docs; };
+  uint32_t lst0 = 0, lst1 = 0;
+  if (WIDE) { lst0 = list_at(l); lst1 = list_at(WAVE + l); }
+  uint32_t it = 0;
+  auto docof = [&](uint32_t j) -> uint32_t {   // (j within the current run or the next)
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)rdlane((j >> 6) != (it >> 6) ? lst1 : lst0, j & 63u));
+  };
+  // the document k places after the current one (narrow: d is the induction variable)
+#define LN_AHEAD(k) (WIDE ? docof(it + (k)) : d + (k) * G)
+  uint32_t d = WIDE ? (n_it > blockIdx.x ? docof(0) : n_docs) : blockIdx.x;
+  (void)n_it;
   uint32_t du = lean_du_load(doc_upd, d, n_docs);
   LeanHdr hn = lean_hdr_of(du, lean_bo_load(upd_off, du, d, n_docs));
-  du = lean_du_load(doc_upd, d + G, n_docs);                  // header pipeline: doc_upd one document ahead
-  u32x4 v[LN_IN / 16 / WAVE];
+  du = lean_du_load(doc_upd, LN_AHEAD(1), n_docs);                  // header pipeline: doc_upd one document ahead
+  u32x4 v[C::IN / 16 / WAVE];
   uint32_t rx[LN_ROWS], ry[LN_ROWS];
 #pragma unroll
   for (int q = 0; q < LN_ROWS; q++) { rx[q] = 0; ry[q] = 0; }
-  bool gn = !force_seq && lean_stageable(hn);
-  lean_prefetch(arena, upd_off, hn, gn, v, rx, ry);
+  bool gn = !force_seq && lean_stageable<WIDE>(hn);
+  lean_prefetch<WIDE>(arena, upd_off, hn, gn, v, rx, ry);
   uint64_t payload = 0;   // this wave's output bytes: one atomic per wave, not per document
   // deferred documents: bit j of dmask = the j-th document of the current run of 64 iterations (document
   // dch + j * G), appended to defer_list with ONE atomic per run -- one atomic per document on the single
@@ -1581,16 +1604,19 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
   auto flush_defer = [&]() {
     if (!dmask) return;
     uint32_t base = 0;
-    if (l == 0) base = atomicAdd(&meta->lean_defer, (uint32_t)__popcll(dmask));
+    if (l == 0) base = atomicAdd(WIDE ? &meta->wide_defer : &meta->lean_defer, (uint32_t)__popcll(dmask));
     base = __shfl(base, 0, WAVE);
-    if ((dmask >> l) & 1ull) defer_list[base + (uint32_t)__popcll(dmask & ((1ull << l) - 1ull))] = dch + l * G;
+    if ((dmask >> l) & 1ull) defer_list[base + (uint32_t)__popcll(dmask & ((1ull << l) - 1ull))] = WIDE ? lst0 : dch + l * G;
     dmask = 0;
   };
-  for (; d < n_docs; d += G) {
+  for (; WIDE ? (uint64_t)blockIdx.x + (uint64_t)it * G < n_it : d < n_docs; it++) {
     DIAGL_T0
-    if (dit == 64) { flush_defer(); dit = 0; dch = d; }
+    if (dit == 64) {
+      flush_defer(); dit = 0; dch = d;
+      if (WIDE) { lst0 = lst1; lst1 = list_at(it + WAVE + l); }   // the run's entries move down; the next run's are loaded
+    }
     const LeanHdr h = hn;
-    const bool go = gn;
+    bool go = gn;
     const uint32_t k = h.k;
     const uint64_t b0 = h.b0, nbytes = h.nbytes;
     const uint64_t slot = merge_slot(b0, d), cap = merge_slot_cap(nbytes);
@@ -1600,12 +1626,18 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
     if (go) {
       const uint32_t nch = (uint32_t)((shift + nbytes + 15) / 16);
 #pragma unroll
-      for (int j = 0; j < LN_IN / 16 / WAVE; j++) {
+      for (int j = 0; j < C::IN / 16 / WAVE; j++) {
         const uint32_t c = l + WAVE * j;
         if (c < nch) *(LB128*)(lin + 16 * c) = v[j];
       }
 #pragma unroll
       for (int q = 0; q < LN_ROWS; q++) { us[q] = shift + (rx[q] - (uint32_t)b0); un[q] = ry[q] - rx[q]; }
+      if (!WIDE) {   // an update past the narrow window: the wide kernel's document -- defer it without parsing
+        bool lng = false;
+#pragma unroll
+        for (int q = 0; q < LN_ROWS; q++) lng |= l + WAVE * q < k && un[q] > (uint32_t)LN_UMAX;
+        if (__ballot(lng)) go = false;
+      }
     }
     // every prefetch load has landed on every path (free after the staging): without this the waitcnt
     // pass, path-insensitive, sees them pending in the parse and makes it wait -- counters being in
@@ -1614,12 +1646,12 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
     wave_sync();
     DIAGL(0);
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 1   // timing experiment: stage only
-    { hn = lean_hdr_of(du, lean_bo_load(upd_off, du, d + G, n_docs)); du = lean_du_load(doc_upd, d + 2 * G, n_docs);
-      gn = !force_seq && lean_stageable(hn); lean_prefetch(arena, upd_off, hn, gn, v, rx, ry); wave_sync(); continue; }
+    { hn = lean_hdr_of(du, lean_bo_load(upd_off, du, LN_AHEAD(1), n_docs)); du = lean_du_load(doc_upd, LN_AHEAD(2), n_docs);
+      gn = !force_seq && lean_stageable<WIDE>(hn); lean_prefetch<WIDE>(arena, upd_off, hn, gn, v, rx, ry); wave_sync(); d = LN_AHEAD(1); continue; }
 #endif
     // ---- header of the next document (its prefetch is issued after the parse) and doc_upd of the one after
-    const uint64_t bo_next = lean_bo_load(upd_off, du, d + G, n_docs);
-    const uint32_t du_next = lean_du_load(doc_upd, d + 2 * G, n_docs);
+    const uint64_t bo_next = lean_bo_load(upd_off, du, LN_AHEAD(1), n_docs);
+    const uint32_t du_next = lean_du_load(doc_upd, LN_AHEAD(2), n_docs);
     // single: mergeUpdates([]) = 0000; a single input is returned as is (Y@39011).  It shares the
     // prefetch below with the parse path (a prefetch of its own, in its own branch, gets hoisted
     // above the branch and the parse then waits on those loads)
@@ -1654,7 +1686,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
 #pragma unroll
       for (int q = 0; q < LN_ROWS; q++) {
         const bool valid = l + WAVE * q < k;
-        if (valid) { rec[q] = lean_parse(lin, us[q], un[q]); bad |= !rec[q].ok; }
+        if (valid) { rec[q] = lean_parse<WIDE ? LNW_UMAX : LN_UMAX>(lin, us[q], un[q]); bad |= !rec[q].ok; }
         else { rec[q].ok = true; rec[q].client = 0; rec[q].clock = 0; rec[q].clen = 0; rec[q].span = 0; }
         hs[q] = valid && (rec[q].span & 0xFF00u) != 0u;
         hasd[q] = valid && rec[q].ok && lin[lean_ds_pos(us[q], rec[q].span)] != 0;
@@ -1667,12 +1699,12 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
     __builtin_amdgcn_sched_barrier(0);
 #endif
     hn = lean_hdr_of(du, bo_next); du = du_next;
-    gn = !force_seq && lean_stageable(hn);
-    lean_prefetch(arena, upd_off, hn, gn, v, rx, ry);
+    gn = !force_seq && lean_stageable<WIDE>(hn);
+    lean_prefetch<WIDE>(arena, upd_off, hn, gn, v, rx, ry);
     defer = defer || __ballot(bad) != 0;
-    if (single) { wave_sync(); continue; }
+    if (single) { wave_sync(); dit++; d = LN_AHEAD(1); continue; }   // (dit: bit j of dmask is the run's j-th document)
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 2   // timing experiment: stage + parse
-    if (l == 0) status[d] = (int)bad; wave_sync(); continue;
+    if (l == 0) status[d] = (int)bad; wave_sync(); d = LN_AHEAD(1); continue;
 #endif
     if (!defer) {
       // ---- clients, discovered in descending order (wave max over the unassigned records): a
@@ -1732,7 +1764,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
             const uint32_t b = blk[q];
             const uint32_t j = idx[q] + ((b < 4u ? RB0 : RB1) >> (8u * (b & 3u)) & 0xFFu);
             Sck[j] = rec[q].clock; Sen[j] = rec[q].clock + rec[q].clen;
-            Ssp[j] = (rec[q].span & 0xFFFF0000u) | (b << 13) | (((rec[q].span >> 8) & 0x7Fu) << 5) | (rec[q].span & 0x1Fu);
+            Ssp[j] = (rec[q].span & 0xFFFF0000u) | (b << 13) | (((rec[q].span >> 8) & 0x7Fu) << 6) | (rec[q].span & 0x3Fu);
           }
         }
         wave_sync();
@@ -1748,7 +1780,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
           const uint32_t spp = (v && j > 0u) ? Ssp[j - 1u] : 0u, ep = (v && j > 0u) ? Sen[j - 1u] : 0u;
           const bool first = v && (j == 0u || ((spp ^ sp) & 0xE000u) != 0u);   // first record of its block
           bad |= v && !first && ck != ep;
-          const uint32_t f = v ? (((sp >> 5) & 0x7Fu) << 16) | (sp & 0x1Fu) : 0u;
+          const uint32_t f = v ? (((sp >> 6) & 0x7Fu) << 16) | (sp & 0x3Fu) : 0u;
           const uint32_t inc = carry + dpp_incl_add(f);
           const uint32_t ex = inc - f;
           carry = lane63(inc);
@@ -1779,6 +1811,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
         bool anyds = false;
 #pragma unroll
         for (int q = 0; q < LN_ROWS; q++) anyds |= hasd[q];
+        DIAG_PUT(6, DIAG_NOW());
         if (__ballot(anyds) != 0) {
           uint32_t dpos[LN_ROWS], uend[LN_ROWS];
 #pragma unroll
@@ -1787,22 +1820,24 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
           bad |= dsu.bad;
           wave_sync();
         }
+        DIAG_PUT(7, DIAG_NOW());
         // the output buffer is assembled by OR: zero it
         {
           const u32x4 z = {0u, 0u, 0u, 0u};
+          constexpr int NZ = (C::OUT + 80) / 16;   // 16-byte pieces of the output buffer
 #pragma unroll
-          for (int j = 0; j < (LN_OUT + 48) / 16 / WAVE; j++) *(LB128*)(lout + 16 * (l + WAVE * j)) = z;
-          if (l < (uint32_t)(((LN_OUT + 48) / 16) % WAVE)) *(LB128*)(lout + 16 * (l + WAVE * ((LN_OUT + 48) / 16 / WAVE))) = z;
+          for (int j = 0; j < NZ / WAVE; j++) *(LB128*)(lout + 16 * (l + WAVE * j)) = z;
+          if (l < (uint32_t)(NZ % WAVE)) *(LB128*)(lout + 16 * (l + WAVE * (NZ / WAVE))) = z;
         }
         DIAGL(2);
         defer = __ballot(bad) != 0;
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 3   // timing experiment: stage + parse + scan
-        if (l == 0) status[d] = (int)bad + (int)(oex[0] & 1) + (int)(oex[1] & 1) + (int)(oex[2] & 1) + (int)(oex[3] & 1); wave_sync(); continue;
+        if (l == 0) status[d] = (int)bad + (int)(oex[0] & 1) + (int)(oex[1] & 1) + (int)(oex[2] & 1) + (int)(oex[3] & 1); wave_sync(); d = LN_AHEAD(1); continue;
 #endif
         if (!defer) {
           const uint32_t at = vu_len(nC) + hdr_all;   // + the struct bytes: the delete set's position
           size = at + (carry & 0xFFFFu) + dsu.bytes;   // headers + struct bytes + the delete set
-          if (size > (uint32_t)LN_OUT || ((size + 15u) & ~15u) > cap || slot + size > out_cap) defer = true;
+          if (size > (uint32_t)C::OUT || ((size + 15u) & ~15u) > cap || slot + size > out_cap) defer = true;
           else {
             // ---- emit into the LDS output buffer: structs (funnel copies), block headers, document header, delete set
 #pragma unroll
@@ -1810,7 +1845,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
               const uint32_t j = l + WAVE * r;
               const uint32_t b = (osp[r] >> 13) & 7u;
               const uint32_t t = (oex[r] & 0xFFFFu) + ((b < 4u ? HC0 : HC1) >> (8u * (b & 3u)) & 0xFFu);
-              lean_copy(lout, lin, j < nrec, t, osp[r] >> 16, osp[r] & 0x1Fu);
+              lean_copy<WIDE>(lout, lin, j < nrec, t, osp[r] >> 16, osp[r] & 0x3Fu);
             }
             if (l < nC) {
               uint32_t t = lds_vu(lout, hpos, hcnt);
@@ -1837,9 +1872,11 @@ __global__ __launch_bounds__(WAVE, 4) void k_merge_lean(const uint8_t* __restric
     dit++;
     DIAGL(4);
     wave_sync();   // the next document's staging overwrites lin / lout
+    d = LN_AHEAD(1);
   }
   flush_defer();
   if (l == 0 && payload) add_payload(meta, blockIdx.x, payload);
+#undef LN_AHEAD
 }
 
 // ======================================================================= merge: large documents
@@ -2667,6 +2704,16 @@ int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, 
   return launch_rc(__func__);
 }
 
+// workgroups of `threads` resident at once on the device (occupancy x CUs), for persistent grids
+extern "C++" template <class K>
+static uint32_t resident_blocks(K kernel, int threads, uint32_t fallback) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess || cus <= 0 || per <= 0)
+    return fallback;
+  return (uint32_t)(cus * per);
+}
+
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
                             uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
@@ -2677,19 +2724,22 @@ int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const
   const char* env = getenv("YGM_LEAN_WAVES_PER_CU");
   const uint32_t wpc = env ? (uint32_t)atoi(env) : 16u;
   const uint32_t grid = n_docs < (uint32_t)n_cu * wpc ? n_docs : (uint32_t)n_cu * wpc;
-  hipLaunchKernelGGL(k_merge_lean, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len, status,
-                     (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap);
+  hipLaunchKernelGGL(k_merge_lean<0>, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len, status,
+                     (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap, (const uint32_t*)nullptr, 0u);
   return launch_rc(__func__);
 }
-
-// workgroups of `threads` resident at once on the device (occupancy x CUs), for persistent grids
-extern "C++" template <class K>
-static uint32_t resident_blocks(K kernel, int threads, uint32_t fallback) {
-  int dev = 0, cus = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess || cus <= 0 || per <= 0)
-    return fallback;
-  return (uint32_t)(cus * per);
+// the wide lean kernel over the narrow one's deferred list (n_list entries); its own deferrals go to defer_list
+// (count: DocMeta::wide_defer)
+int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, const uint32_t* list,
+                                 uint32_t n_list, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
+                                 void* meta, uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
+  if (n_list == 0) return 0;
+  static uint32_t resident = 0;
+  if (!resident) { const char* g = getenv("YGM_WIDE_GRID"); resident = g ? (uint32_t)atoi(g) : resident_blocks(k_merge_lean<1>, WAVE, 2048u); }
+  const uint32_t grid = n_list < resident ? n_list : resident;
+  hipLaunchKernelGGL(k_merge_lean<1>, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len, status,
+                     (DocMeta*)meta, (DocMeta*)nullptr, defer_list, out_cap, list, n_list);
+  return launch_rc(__func__);
 }
 
 int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,

@@ -36,10 +36,24 @@ constexpr int LN_CMAX = 8;      // distinct struct clients per document
 
 constexpr int LN_OUT = 4096;    // staged output bytes
 
-struct alignas(16) LeanLds {
-  uint8_t in[LN_IN + 64];       // + slack: an update's window reads reach 47 bytes past its start
-  uint8_t out[LN_OUT + 48];      // + slack: lds_or_copy ORs zero into up to 36 bytes past a range
+// The wide variant (k_merge_lean<1>, run over the documents the narrow one defers): updates of up to
+// 64 bytes (multi-character inserts, SURVEY.md §8d's realistic debounce logs), documents of up to 7 KB
+// staged, 6 KB of output (LDS 13.5 KB, <= 168 VGPRs: 3 waves per SIMD).
+constexpr int LNW_IN = 7168;
+constexpr int LNW_UMAX = 64;
+constexpr int LNW_OUT = 6144;
+
+template <int WIDE> struct LnCfg {
+  static constexpr int IN = WIDE ? LNW_IN : LN_IN;
+  static constexpr int OUT = WIDE ? LNW_OUT : LN_OUT;
+  static constexpr int UMAX = WIDE ? LNW_UMAX : LN_UMAX;
 };
+template <int WIDE>
+struct alignas(16) LeanLdsT {
+  uint8_t in[LnCfg<WIDE>::IN + 96];     // + slack: window / copy reads reach up to 76 bytes past an update's start
+  uint8_t out[LnCfg<WIDE>::OUT + 80];   // + slack: lds_or_copy ORs zero into up to 68 bytes past a range
+};
+typedef LeanLdsT<0> LeanLds;
 
 typedef __attribute__((address_space(3))) uint8_t LB8;
 typedef __attribute__((address_space(3))) uint32_t LB32;
@@ -123,128 +137,167 @@ YDEV uint32_t pext32(uint32_t x, uint32_t y, uint32_t n) {
 // a ?: of array elements into a scratch-indexed load)
 YDEV uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); }
 
-// 32 bytes of staged input from position s as d[0..7] (d[j] = bytes 4j..4j+3): nine
-// dword-aligned ds_read_b32 funnelled by v_alignbyte (no selects; an unaligned b128 read replays)
-YDEV void lean_window(LB8* in, uint32_t s, uint32_t (&d)[8]) {
+// W bytes (32 or 64) of staged input from position s as d[0..W/4): dword-aligned ds_read_b32
+// funnelled by v_alignbyte (no selects; an unaligned b128 read replays)
+template <int W>
+YDEV void lean_windowW(LB8* in, uint32_t s, uint32_t (&d)[W / 4]) {
   const LB32* w = (const LB32*)(in + (s & ~3u));
-  uint32_t L[9];
+  uint32_t L[W / 4 + 1];
 #pragma unroll
-  for (int j = 0; j < 9; j++) L[j] = w[j];
+  for (int j = 0; j <= W / 4; j++) L[j] = w[j];
 #pragma unroll
-  for (int j = 0; j < 8; j++) d[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], s & 3u);
+  for (int j = 0; j < W / 4; j++) d[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], s & 3u);
 }
+YDEV void lean_window(LB8* in, uint32_t s, uint32_t (&d)[8]) { lean_windowW<32>(in, s, d); }
 // top bits of the 8 bytes (lo, hi) as bits 0..7: bytes masked to 0x00 / 0x80 times u8 weights
 YDEV uint32_t top8(uint32_t lo, uint32_t hi) {
   const uint32_t a = __builtin_amdgcn_udot4(lo & 0x80808080u, 0x08040201u, 0u, false);
   return __builtin_amdgcn_udot4(hi & 0x80808080u, 0x80402010u, a, false) >> 7;
 }
-// H = top-bit mask of the 32 window bytes
-YDEV uint32_t lean_hmask(const uint32_t (&d)[8]) {
-  uint32_t H = 0;
+// the window's mask type: bit i <-> byte i
+template <int W> struct LnMask;
+template <> struct LnMask<32> { typedef uint32_t T; };
+template <> struct LnMask<64> { typedef uint64_t T; };
+// H = top-bit mask of the W window bytes
+template <int W>
+YDEV typename LnMask<W>::T lean_hmaskW(const uint32_t (&d)[W / 4]) {
+  typename LnMask<W>::T H = 0;
 #pragma unroll
-  for (int j = 0; j < 4; j++) H |= top8(d[2 * j], d[2 * j + 1]) << (8 * j);
+  for (int j = 0; j < W / 8; j++) H |= (typename LnMask<W>::T)top8(d[2 * j], d[2 * j + 1]) << (8 * j);
   return H;
 }
+YDEV uint32_t lean_hmask(const uint32_t (&d)[8]) { return lean_hmaskW<32>(d); }
+// index of the lowest set bit of x with the top bit forced (x == 0 -> W - 1)
+YDEV uint32_t lnctz(uint32_t x) { return (uint32_t)__builtin_ctz(x | 0x80000000u); }
+YDEV uint32_t lnctz(uint64_t x) { return (uint32_t)__builtin_ctzll(x | 0x8000000000000000ull); }
 
+// Parses the update at staged position s (n bytes) from a W-byte register window (W = 32: the narrow
+// kernel; 64: the wide one).  ok == false: the document is deferred.
+template <int W>
 YDEV LRec lean_parse(LB8* in, uint32_t s, uint32_t n) {
+  typedef typename LnMask<W>::T M;
+  constexpr uint32_t WB = (uint32_t)W, WL = WB - 1u;
+  constexpr M ONE = 1, ALL = ~(M)0;
   LRec R; R.ok = false; R.client = 0; R.clock = 0; R.clen = 0; R.span = 0;
-  if (n < 2 || n > (uint32_t)LN_UMAX) return R;
-  uint32_t d[8];
-  lean_window(in, s, d);
+  if (n < 2 || n > WB) return R;
+  uint32_t d[W / 4];
+  lean_windowW<W>(in, s, d);
   if ((d[0] & 0xFFu) == 0u) { R.ok = true; return R; }   // no structs: a delete set only (at s + 1)
-  // masks over the 32 window bytes: H = top bit set, Z = zero byte ("haszero": may also flag a
+  // masks over the W window bytes: H = top bit set, Z = zero byte ("haszero": may also flag a
   // 0x01 right above a zero byte, which only defers)
-  const uint32_t H = lean_hmask(d);
-  uint32_t Z = 0;
+  const M H = lean_hmaskW<W>(d);
+  M Z = 0;
 #pragma unroll
-  for (int j = 0; j < 4; j++) Z |= top8((d[2 * j] - 0x01010101u) & ~d[2 * j], (d[2 * j + 1] - 0x01010101u) & ~d[2 * j + 1]) << (8 * j);
-  const uint32_t V = n >= 32u ? 0xFFFFFFFFu : ((1u << n) - 1u);
-  const uint32_t T = ~H & V;                 // varuint terminators among the valid bytes
-  const uint32_t HV = H & V;
+  for (int j = 0; j < W / 8; j++)
+    Z |= (M)top8((d[2 * j] - 0x01010101u) & ~d[2 * j], (d[2 * j + 1] - 0x01010101u) & ~d[2 * j + 1]) << (8 * j);
+  const M V = n >= WB ? ALL : ((ONE << n) - ONE);
+  const M T = ~H & V;                 // varuint terminators among the valid bytes
+  const M HV = H & V;
   LB8* u = in + s;
   // Whole-window checks instead of per-varuint ones:
   //  * a run of >= 7 bytes with the top bit set (a varuint of >= 8 bytes: possibly >= 2^53) defers;
   //  * a zero byte right after a top-bit byte is a non-minimal varuint terminator (or a client
   //    id 0 right after an info byte) -- yjs re-encodes those, so the document defers.
-  const uint32_t h2 = HV & (HV >> 1), h4 = h2 & (h2 >> 2), h7 = h4 & (h4 >> 3);
-  uint32_t bad = h7 | (Z & (HV << 1) & V);
-  // position of the terminator of the varuint at p; past the window: >= 31 (then p >= n fails below)
-#define LN_VEND(p, e) ((e) = ((p) < 31u ? (p) : 31u) + (uint32_t)__builtin_ctz((T >> ((p) < 31u ? (p) : 31u)) | 0x80000000u))
-  // ASCII run of L bytes at p inside the update (L <= 31)
-#define LN_ASCII(p, L) (bad |= ((n - (p) - (L)) & 0x80000000u) | ((L) & ~31u) | ((HV >> ((p) < 31u ? (p) : 31u)) & ((1u << ((L) & 31u)) - 1u)))
+  const M h2 = HV & (HV >> 1), h4 = h2 & (h2 >> 2), h7 = h4 & (h4 >> 3);
+  M bad = h7 | (Z & (HV << 1) & V);
+  // position of the terminator of the varuint at p; past the window: >= WB-1 (then p >= n fails below)
+#define LN_VEND(p, e) ((e) = ((p) < WL ? (p) : WL) + lnctz((M)(T >> ((p) < WL ? (p) : WL))))
+  // ASCII run of L bytes at p inside the update (L < WB)
+#define LN_ASCII(p, L) (bad |= (M)(((n - (p) - (L)) & 0x80000000u) | ((L) & ~WL)) | ((HV >> ((p) < WL ? (p) : WL)) & ((ONE << ((L) & WL)) - ONE)))
   const uint32_t b0 = d[0] & 0xFFu, b1 = (d[0] >> 8) & 0xFFu;
-  bad |= (b0 ^ 1u) | ((b1 - 1u) & ~127u) | (n < 4u ? 1u : 0u);    // one client block of 1..127 structs
+  bad |= (M)((b0 ^ 1u) | ((b1 - 1u) & ~127u) | (n < 4u ? 1u : 0u));    // one client block of 1..127 structs
   uint32_t e, p;
   LN_VEND(2u, e);
   const uint32_t cl_n = e - 1u;              // client bytes 2..e
   const uint32_t client = pext32(__builtin_amdgcn_alignbyte(d[1], d[0], 2u), (d[1] >> 16) & 0xFFu, cl_n);
-  bad |= (cl_n > 5u ? 1u : 0u) | (cl_n == 5u ? ((d[1] >> 16) & 0x70u) : 0u);   // clients are uint32
+  bad |= (M)((cl_n > 5u ? 1u : 0u) | (cl_n == 5u ? ((d[1] >> 16) & 0x70u) : 0u));   // clients are uint32
   p = e + 1u;                                 // 3..7
   LN_VEND(p, e);
   const uint32_t ck_n = e - p + 1u;
   const uint64_t U01 = ((uint64_t)d[1] << 32) | d[0], U23 = ((uint64_t)d[3] << 32) | d[2];
   const uint64_t cw = (U01 >> (8u * (p & 7u))) | (p & 7u ? (U23 << (64u - 8u * (p & 7u))) : 0ull);   // bytes p..p+7, 3 <= p <= 7
   const uint32_t clock = pext32((uint32_t)cw, (uint32_t)(cw >> 32) & 0xFFu, ck_n);
-  bad |= (ck_n > 5u ? 1u : 0u) | (ck_n == 5u ? ((uint32_t)(cw >> 32) & 0x70u) : 0u);
+  bad |= (M)((ck_n > 5u ? 1u : 0u) | (ck_n == 5u ? ((uint32_t)(cw >> 32) & 0x70u) : 0u));
   p = e + 1u;
   const uint32_t sstart = p;
   uint32_t clen = 0;
+  constexpr uint32_t PC = WB + 8u;            // byte reads clamp here (the staged buffer has slack)
   // structs: the first always, the rest (multi-struct transactions) by the back edge
   uint32_t st = 0;
   do {
-    const uint32_t pc = p < 40u ? p : 40u;
+    const uint32_t pc = p < PC ? p : PC;
     const uint32_t info = u[pc];
     p = pc + 1u;
     const uint32_t ref = info & 31u;
     // Skip/GC/other content go to the general path; bit 0x20 is dropped on re-encode when an origin is set
-    bad |= (info == 10u ? 1u : 0u) | ((ref != 1u && ref != 4u) ? 1u : 0u) | ((info & 0xC0u) && (info & 0x20u) ? 1u : 0u);
+    bad |= (M)((info == 10u ? 1u : 0u) | ((ref != 1u && ref != 4u) ? 1u : 0u) | ((info & 0xC0u) && (info & 0x20u) ? 1u : 0u));
     // origin and/or right origin: 2 or 4 varuints -- the 2nd / 4th terminator from p
     {
-      const uint32_t pp = p < 31u ? p : 31u;
-      const uint32_t t0 = (T >> pp) | 0x80000000u, t1 = t0 & (t0 - 1u), t2 = t1 & (t1 - 1u), t3 = t2 & (t2 - 1u);
+      const uint32_t pp = p < WL ? p : WL;
+      const M t0 = (T >> pp) | (ONE << WL), t1 = t0 & (t0 - ONE), t2 = t1 & (t1 - ONE), t3 = t2 & (t2 - ONE);
       const uint32_t nsk = ((info >> 6) & 1u) + ((info >> 7) & 1u);   // id pairs
-      const uint32_t e2 = pp + (uint32_t)__builtin_ctz(t1 | 0x80000000u) + 1u;
-      const uint32_t e4 = pp + (uint32_t)__builtin_ctz(t3 | 0x80000000u) + 1u;
+      const uint32_t e2 = pp + lnctz(t1) + 1u;
+      const uint32_t e4 = pp + lnctz(t3) + 1u;
       p = nsk == 2u ? e4 : nsk == 1u ? e2 : p;
     }
     if ((info & 0xC0u) == 0u) {   // parent (rare: inserts at the start of a type, map keys)
-      const uint32_t pi = u[p < 40u ? p : 40u]; p++;
+      const uint32_t pi = u[p < PC ? p : PC]; p++;
       if (pi == 1u) {
-        const uint32_t Lk = u[p < 40u ? p : 40u]; p++;
-        LN_ASCII(p, Lk); p += Lk & 31u;
+        const uint32_t Lk = u[p < PC ? p : PC]; p++;
+        LN_ASCII(p, Lk); p += Lk & WL;
       } else {
-        bad |= pi;                  // parentInfo is re-encoded as 0/1
+        bad |= (M)pi;                  // parentInfo is re-encoded as 0/1
         LN_VEND(p, e); p = e + 1u; LN_VEND(p, e); p = e + 1u;
       }
       if (info & 0x20u) {
-        const uint32_t Ls = u[p < 40u ? p : 40u]; p++;
-        LN_ASCII(p, Ls); p += Ls & 31u;
+        const uint32_t Ls = u[p < PC ? p : PC]; p++;
+        LN_ASCII(p, Ls); p += Ls & WL;
       }
     }
     if (ref == 1u) {   // ContentDeleted: varuint length
       LN_VEND(p, e);
-      const uint32_t pp = p < 31u ? p : 31u;
+      const uint32_t pp = p < WL ? p : WL;
       const uint32_t x = u[pp] | ((uint32_t)u[pp + 1] << 8) | ((uint32_t)u[pp + 2] << 16) | ((uint32_t)u[pp + 3] << 24);
       const uint32_t v = pext32(x, 0u, e - p + 1u);
-      bad |= (v == 0u ? 1u : 0u) | ((e - p) > 2u ? 1u : 0u);   // 1..3 bytes: < 2^21
+      bad |= (M)((v == 0u ? 1u : 0u) | ((e - p) > 2u ? 1u : 0u));   // 1..3 bytes: < 2^21
       clen += v;
       p = e + 1u;
     } else {           // ContentString: single-byte length, ASCII bytes (UTF-16 length == byte length)
-      const uint32_t Lc = u[p < 40u ? p : 40u]; p++;
-      bad |= Lc == 0u ? 1u : 0u;
+      const uint32_t Lc = u[p < PC ? p : PC]; p++;
+      bad |= (M)(Lc == 0u ? 1u : 0u);
       LN_ASCII(p, Lc);
-      p += Lc & 31u;
+      p += Lc & WL;
       clen += Lc;
     }
-  } while (++st < b1 && (bad | (p >= n ? 1u : 0u)) == 0u);
+  } while (++st < b1 && (bad | (M)(p >= n ? 1u : 0u)) == 0);
 #undef LN_VEND
 #undef LN_ASCII
-  bad |= (n - 1u - p) & 0x80000000u;          // then the delete set (at least its count byte)
-  bad |= (uint32_t)(((uint64_t)clock + clen) >> 32);
-  R.ok = bad == 0u;
+  bad |= (M)((n - 1u - p) & 0x80000000u);          // then the delete set (at least its count byte)
+  bad |= (M)(uint32_t)(((uint64_t)clock + clen) >> 32);
+  R.ok = bad == 0;
   R.client = client; R.clock = clock; R.clen = clen;
   R.span = ((s + sstart) << 16) | (b1 << 8) | ((p - sstart) & 0xFFu);   // the delete set follows the structs
   return R;
+}
+
+// byte p (0..31) of a 32-byte register window.  Selects by bit masks (v_bfi): a ?: over array elements is
+// turned into a scratch-indexed load by the compiler
+YDEV uint32_t w2_byte(const uint32_t (&d)[8], uint32_t p) {
+  const uint32_t i = p >> 2;
+  const uint32_t m0 = 0u - (i & 1u), m1 = 0u - ((i >> 1) & 1u), m2 = 0u - ((i >> 2) & 1u);
+  const uint32_t a0 = bsel(m0, d[1], d[0]), a1 = bsel(m0, d[3], d[2]), a2 = bsel(m0, d[5], d[4]), a3 = bsel(m0, d[7], d[6]);
+  const uint32_t b0 = bsel(m1, a1, a0), b1 = bsel(m1, a3, a2);
+  return (bsel(m2, b1, b0) >> (8u * (p & 3u))) & 0xFFu;
+}
+// bytes [p, p + 5) of a register window, p <= 15, as (the first 4 bytes, the 5th byte)
+YDEV void w2_vu5(const uint32_t (&d)[8], uint32_t p, uint32_t& x, uint32_t& y) {
+  const uint32_t i = p >> 2, s = p & 3u;
+  const uint32_t m0 = 0u - (i & 1u), m1 = 0u - ((i >> 1) & 1u);
+  const uint32_t lo = bsel(m1, bsel(m0, d[3], d[2]), bsel(m0, d[1], d[0]));
+  const uint32_t hi = bsel(m1, bsel(m0, d[4], d[3]), bsel(m0, d[2], d[1]));
+  const uint32_t hh = bsel(m1, bsel(m0, d[5], d[4]), bsel(m0, d[3], d[2]));
+  x = __builtin_amdgcn_alignbyte(hi, lo, s);
+  y = __builtin_amdgcn_alignbyte(hh, hi, s) & 0xFFu;
 }
 
 // ---- delete sets (rule R-DS): a DS is varuints only, so one update's DS is
@@ -320,10 +373,12 @@ YDEV void lds_or_copy(LB8* out, LB8* in, uint32_t t, uint32_t s, uint32_t n) {
   }
 }
 // one row of struct copies: 6 destination dwords when every lane's run fits (C2 structs are
-// <= 19 bytes), else 9
+// <= 19 bytes), else 9, else (the wide kernel's runs of up to 63 bytes) 17
+template <int WIDE>
 YDEV void lean_copy(LB8* out, LB8* in, bool go, uint32_t t, uint32_t s, uint32_t n) {
   if (__ballot(go && (t & 3u) + n > 24u) == 0) { if (go) lds_or_copy<6>(out, in, t, s, n); }
-  else if (go) lds_or_copy<9>(out, in, t, s, n);
+  else if (!WIDE || __ballot(go && (t & 3u) + n > 36u) == 0) { if (go) lds_or_copy<9>(out, in, t, s, n); }
+  else if (go) lds_or_copy<17>(out, in, t, s, n);
 }
 YDEV uint32_t lds_vu(LB8* out, uint32_t t, uint32_t v) {
   while (v > 127u) { out[t++] = (uint8_t)(0x80u | (v & 127u)); v >>= 7; }
@@ -334,14 +389,24 @@ YDEV uint32_t lds_vu(LB8* out, uint32_t t, uint32_t v) {
 YDEV uint32_t vlen32(uint32_t v) {   // bytes of the varuint encoding of v
   return 1u + (v > 0x7Fu ? 1u : 0u) + (v > 0x3FFFu ? 1u : 0u) + (v > 0x1FFFFFu ? 1u : 0u) + (v > 0xFFFFFFFu ? 1u : 0u);
 }
-YDEV uint64_t lean_max_scan64(uint64_t v) {   // inclusive prefix max over the wave
-  const uint32_t l = threadIdx.x;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t t = __shfl_up(v, (unsigned)o, 64);
-    v = (l >= (uint32_t)o && t > v) ? t : v;
-  }
-  return v;
+// one DPP step of a 64-bit inclusive max scan: (hi, lo) pairs move together (lanes the pattern does not
+// reach read (0, 0), which never wins)
+template <int CTRL, int RM, bool BC>
+YDEV void dpp_max64_step(uint32_t& hi, uint32_t& lo) {
+  const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, RM, 0xF, BC);
+  const uint32_t l2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, RM, 0xF, BC);
+  const bool gt = h2 > hi || (h2 == hi && l2 > lo);
+  hi = gt ? h2 : hi; lo = gt ? l2 : lo;
+}
+YDEV uint64_t lean_max_scan64(uint64_t v) {   // inclusive prefix max over the wave (DPP, as dpp_incl_max)
+  uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  dpp_max64_step<0x111, 0xF, true>(hi, lo);   // row_shr:1
+  dpp_max64_step<0x112, 0xF, true>(hi, lo);   // row_shr:2
+  dpp_max64_step<0x114, 0xF, true>(hi, lo);   // row_shr:4
+  dpp_max64_step<0x118, 0xF, true>(hi, lo);   // row_shr:8
+  dpp_max64_step<0x142, 0xA, false>(hi, lo);  // row_bcast:15 -> rows 1, 3
+  dpp_max64_step<0x143, 0xC, false>(hi, lo);  // row_bcast:31 -> rows 2, 3
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // The merged delete set of one document (mergeDeleteSets Y@10486 + sortAndMergeDeleteSet
@@ -367,8 +432,36 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
 #pragma unroll
   for (int q = 0; q < LN_ROWS; q++) {
     if (__ballot(hasd[q]) == 0) continue;
+    // fast path: a delete set of one client with one range (a deletion's update) -- its five varuint ends
+    // from the terminator mask, the values from the register window, no dependent cursor walk
+    bool fq = false;
+    uint32_t fcl = 0, fck = 0, fln = 0;
+    if (hasd[q]) {
+      uint32_t w[8];
+      lean_window(lin, dpos[q], w);
+      const uint32_t n = uend[q] - dpos[q], lim = n < 32u ? n : 32u;
+      const uint32_t T = ~lean_hmask(w) & (lim >= 32u ? 0xFFFFFFFFu : ((1u << lim) - 1u));
+      const uint32_t t1 = T & (T - 1u), t2 = t1 & (t1 - 1u), t3 = t2 & (t2 - 1u), t4 = t3 & (t3 - 1u);
+      const uint32_t e1 = lnctz(T), e2 = lnctz(t1), e3 = lnctz(t2), e4 = lnctz(t3), e5 = lnctz(t4);
+      uint32_t cx, cy, kx, ky, lx, ly;
+      w2_vu5(w, 1u, cx, cy);
+      w2_vu5(w, (e3 + 1u) & 15u, kx, ky);
+      w2_vu5(w, (e4 + 1u) & 15u, lx, ly);
+      const uint32_t ncb = e2 - e1, nkb = e4 - e3, nlb = e5 - e4;   // bytes of client, clock, length
+      fq = e1 == 0u && (w[0] & 0xFFu) == 1u && e3 == e2 + 1u && w2_byte(w, e3 & 31u) == 1u && e5 < lim &&
+           ncb - 1u <= 4u && !(ncb == 5u && (cy & 0x70u)) && nkb - 1u <= 3u && nlb - 1u <= 3u;
+      fcl = pext32(cx, cy, ncb); fck = pext32(kx, ky, nkb); fln = pext32(lx, ly, nlb);
+    }
+    {
+      const uint64_t m = __ballot(fq);
+      const uint32_t slot = nrec + lanes_below(m);
+      if (fq && slot < (uint32_t)LN_DSMAX) { rc[slot] = fcl; rk[slot] = fck; re[slot] = fck + fln; }
+      nrec += (uint32_t)__builtin_popcountll(m);
+    }
+    const bool slow = hasd[q] && !fq;
+    if (__ballot(slow) == 0) continue;
     LDsCur c;
-    if (hasd[q]) lean_ds_open(lin, dpos[q], uend[q] - dpos[q], c);
+    if (slow) lean_ds_open(lin, dpos[q], uend[q] - dpos[q], c);
     else { c.bad = 0; c.cl_left = 0; c.r_left = 0; }
     for (int it = 0; it < LN_DSMAX; it++) {
       bool has = lean_ds_more(c);

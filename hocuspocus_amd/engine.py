@@ -55,7 +55,8 @@ class Stats(ctypes.Structure):
                 ("docs_seq", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
                 ("d2h_ms", ctypes.c_double),
                 ("docs_lean", ctypes.c_uint64), ("lean_ms", ctypes.c_double),
-                ("lean_launches", ctypes.c_uint64), ("docs_big", ctypes.c_uint64)]
+                ("lean_launches", ctypes.c_uint64), ("docs_big", ctypes.c_uint64),
+                ("docs_lean_wide", ctypes.c_uint64)]
 
 
 _lib = None

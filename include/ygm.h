@@ -80,12 +80,14 @@ typedef struct {
   uint64_t docs_fast, docs_seq;        /* documents finished by the general tiers (merge: wave / workgroup kernels;
                                           SV / diff: the exact per-document kernel) / by the sequential merge kernel */
   double kernel_ms, h2d_ms, d2h_ms;    /* cumulative, HIP-event timed */
-  uint64_t docs_lean;                  /* documents finished by the lean kernels (merge: debounce-log kernel; SV / diff:
+  uint64_t docs_lean;                  /* documents finished by the lean kernels (merge: the debounce-log kernels; SV / diff:
                                           lane-per-document walker) */
   double lean_ms;                      /* HIP-event time of the lean kernel launches (part of kernel_ms): one span
                                           from the first launch after a finish to that finish */
   uint64_t lean_launches;              /* lean kernel launches timed in lean_ms */
   uint64_t docs_big;                   /* merges finished by the large-document ([snapshot, ...log]) kernel */
+  uint64_t docs_lean_wide;             /* merges of docs_lean finished by the wide lean kernel (updates <= 64 B,
+                                          documents <= 7 KB: the narrow kernel's deferrals) */
 } ygm_stats_t;
 
 /* Opens the engine on HIP device `device` (one context per GPU; contexts are

@@ -17,6 +17,7 @@
 #include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../../include/ygm.h"
 
@@ -37,7 +38,14 @@ typedef struct {
   uint8_t *data; uint64_t *roff, *rlen; int32_t *status; uint32_t rn;
   napi_deferred deferred;
   napi_async_work work;
+  /* mergeMany: the caller's arena Buffer is read in place by the worker (held by a reference until the
+     batch completes), not copied on the main thread */
+  napi_ref arena_ref; int arena_borrowed;
+  double exec_ms;       /* worker: the engine call + copy-out of its context-owned results */
 } Job;
+
+static double now_ms(void) { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec * 1e3 + t.tv_nsec / 1e6; }
+static void free_data(napi_env env, void *data, void *hint) { (void)env; (void)hint; free(data); }
 
 static void handle_finalize(napi_env env, void *data, void *hint) {
   (void)env; (void)hint;
@@ -96,7 +104,7 @@ static napi_value js_stats(napi_env env, napi_callback_info info) {
   NAPI_CALL(env, napi_create_object(env, &o));
 #define SETN(name, val) NAPI_CALL(env, napi_create_double(env, (double)(val), &v)); NAPI_CALL(env, napi_set_named_property(env, o, name, v));
   SETN("calls", s.calls) SETN("docs", s.docs) SETN("updates", s.updates) SETN("bytesIn", s.bytes_in) SETN("bytesOut", s.bytes_out)
-  SETN("docsFast", s.docs_fast) SETN("docsSeq", s.docs_seq) SETN("kernelMs", s.kernel_ms) SETN("h2dMs", s.h2d_ms) SETN("d2hMs", s.d2h_ms) SETN("docsLean", s.docs_lean) SETN("leanMs", s.lean_ms) SETN("leanLaunches", s.lean_launches) SETN("docsBig", s.docs_big)
+  SETN("docsFast", s.docs_fast) SETN("docsSeq", s.docs_seq) SETN("kernelMs", s.kernel_ms) SETN("h2dMs", s.h2d_ms) SETN("d2hMs", s.d2h_ms) SETN("docsLean", s.docs_lean) SETN("leanMs", s.lean_ms) SETN("leanLaunches", s.lean_launches) SETN("docsBig", s.docs_big) SETN("docsLeanWide", s.docs_lean_wide)
 #undef SETN
   return o;
 }
@@ -130,6 +138,7 @@ static uint64_t *lens_to_off(const uint32_t *lens, uint32_t n) {
 static void job_execute(napi_env env, void *data) {
   (void)env;
   Job *j = (Job *)data;
+  const double t0 = now_ms();
   ygm_result r; memset(&r, 0, sizeof r);
   if (j->op == 0) j->rc = ygm_merge_v1(j->h->ctx, j->arena, j->off, j->docs, j->n_upd, j->n_docs, &r);
   else if (j->op == 1) j->rc = ygm_diff_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
@@ -154,17 +163,21 @@ static void job_execute(napi_env env, void *data) {
     memcpy(j->rlen, r.len, sizeof(uint64_t) * r.n_docs);
     memcpy(j->status, r.status, sizeof(int32_t) * r.n_docs);
   }
+  j->exec_ms = now_ms() - t0;
 }
 
 static void job_free(Job *j) {
-  free(j->arena); free(j->off); free(j->docs); free(j->sv); free(j->sv_off);
+  if (!j->arena_borrowed) free(j->arena);
+  free(j->off); free(j->docs); free(j->sv); free(j->sv_off);
   free(j->data); free(j->roff); free(j->rlen); free(j->status);
   free(j);
 }
 
 static void job_complete(napi_env env, napi_status st, void *data) {
   Job *j = (Job *)data;
+  const double t0 = now_ms();
   j->h->busy = 0;
+  if (j->arena_ref) { napi_delete_reference(env, j->arena_ref); j->arena_ref = NULL; }
   napi_value result = NULL, err = NULL;
   if (st != napi_ok || j->rc != YGM_OK) {
     napi_value msg, code;
@@ -179,15 +192,28 @@ static void job_complete(napi_env env, napi_status st, void *data) {
     if (j->rn) memcpy(sp, j->status, sizeof(int32_t) * j->rn);
     napi_create_typedarray(env, napi_int32_array, j->rn, status_ab, 0, &status_arr);
     napi_create_array_with_length(env, j->rn, &outs);
+    /* outputs: Uint8Array views of ONE external ArrayBuffer that owns the packed result bytes (no copy and
+       no allocation per document); per-document Buffer copies if external buffers are unavailable */
+    napi_value rab = NULL;
+    size_t rbytes = 0;
+    for (uint32_t d = 0; d < j->rn; d++) if (j->status[d] == YGM_OK && j->roff[d] + j->rlen[d] > rbytes) rbytes = j->roff[d] + j->rlen[d];
+    if (rbytes && napi_create_external_arraybuffer(env, j->data, rbytes, free_data, NULL, &rab) == napi_ok) j->data = NULL;
+    else rab = NULL;
     for (uint32_t d = 0; d < j->rn; d++) {
       napi_value b;
-      if (j->status[d] == YGM_OK) napi_create_buffer_copy(env, j->rlen[d], j->data + j->roff[d], NULL, &b);
-      else napi_get_null(env, &b);
+      if (j->status[d] != YGM_OK) napi_get_null(env, &b);
+      else if (rab) napi_create_typedarray(env, napi_uint8_array, j->rlen[d], rab, j->roff[d], &b);
+      else napi_create_buffer_copy(env, j->rlen[d], j->data + j->roff[d], NULL, &b);
       napi_set_element(env, outs, d, b);
     }
+    napi_value ems, cms;
     napi_create_object(env, &result);
     napi_set_named_property(env, result, "status", status_arr);
     napi_set_named_property(env, result, "outputs", outs);
+    napi_create_double(env, j->exec_ms, &ems);
+    napi_create_double(env, now_ms() - t0, &cms);
+    napi_set_named_property(env, result, "execMs", ems);
+    napi_set_named_property(env, result, "completeMs", cms);
     napi_resolve_deferred(env, j->deferred, result);
   }
   napi_delete_async_work(env, j->work);
@@ -196,7 +222,10 @@ static void job_complete(napi_env env, napi_status st, void *data) {
 
 static napi_value submit(napi_env env, Job *j, const char *name) {
   napi_value promise, res_name;
-  if (j->h->busy) { job_free(j); napi_throw_error(env, "YGM_EBUSY", "ygm: one batch in flight per engine handle"); return NULL; }
+  if (j->h->busy) {
+    if (j->arena_ref) napi_delete_reference(env, j->arena_ref);
+    job_free(j); napi_throw_error(env, "YGM_EBUSY", "ygm: one batch in flight per engine handle"); return NULL;
+  }
   NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
   NAPI_CALL(env, napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res_name));
   NAPI_CALL(env, napi_create_async_work(env, NULL, res_name, job_execute, job_complete, j, &j->work));
@@ -214,16 +243,31 @@ static napi_value js_merge(napi_env env, napi_callback_info info) {
   Handle *h = get_handle(env, argv[0]);
   if (!h) return NULL;
   Job *j = (Job *)calloc(1, sizeof(Job)); j->op = opd ? (int)(intptr_t)opd : 0; j->h = h;
-  size_t an, ln, dn; void *lens = NULL;
-  if (get_bytes(env, argv[1], (void **)&j->arena, &an) || get_bytes(env, argv[2], &lens, &ln) || get_bytes(env, argv[3], (void **)&j->docs, &dn)) {
+  size_t an = 0, ln, dn; void *lens = NULL;
+  bool is_buf = false;
+  napi_is_buffer(env, argv[1], &is_buf);
+  if (is_buf && napi_get_buffer_info(env, argv[1], (void **)&j->arena, &an) == napi_ok &&
+      napi_create_reference(env, argv[1], 1, &j->arena_ref) == napi_ok) {
+    j->arena_borrowed = 1;   /* read in place by the worker; the reference keeps it alive */
+  } else if (get_bytes(env, argv[1], (void **)&j->arena, &an)) {
+    job_free(j); napi_throw_type_error(env, NULL, "mergeMany: expected Buffer / Uint32Array arguments"); return NULL;
+  }
+  if (get_bytes(env, argv[2], &lens, &ln) || get_bytes(env, argv[3], (void **)&j->docs, &dn)) {
+    if (j->arena_ref) napi_delete_reference(env, j->arena_ref);
     free(lens); job_free(j); napi_throw_type_error(env, NULL, "mergeMany: expected Buffer / Uint32Array arguments"); return NULL;
   }
   napi_get_value_uint32(env, argv[4], &j->n_docs);
   j->n_upd = (uint32_t)(ln / 4);
-  if (dn / 4 != j->n_upd) { free(lens); job_free(j); napi_throw_range_error(env, NULL, "mergeMany: lens/docs length mismatch"); return NULL; }
+  if (dn / 4 != j->n_upd) {
+    if (j->arena_ref) napi_delete_reference(env, j->arena_ref);
+    free(lens); job_free(j); napi_throw_range_error(env, NULL, "mergeMany: lens/docs length mismatch"); return NULL;
+  }
   j->off = lens_to_off((const uint32_t *)lens, j->n_upd);
   free(lens);
-  if (j->off[j->n_upd] != an) { job_free(j); napi_throw_range_error(env, NULL, "mergeMany: sum(lens) != arena length"); return NULL; }
+  if (j->off[j->n_upd] != an) {
+    if (j->arena_ref) napi_delete_reference(env, j->arena_ref);
+    job_free(j); napi_throw_range_error(env, NULL, "mergeMany: sum(lens) != arena length"); return NULL;
+  }
   return submit(env, j, "ygm.mergeMany");
 }
 

@@ -10,6 +10,8 @@
  * own promise, with yjs's error text (SURVEY.md §8b "Errors").
  */
 const path = require('path')
+const { jobUpdates } = require('./log')
+const now = () => Number(process.hrtime.bigint()) / 1e6
 
 let addon = null
 function loadAddon () {
@@ -39,6 +41,7 @@ class Batcher {
 
   push (job) {
     return new Promise((resolve, reject) => {
+      if (this.queue.length === 0) this.t_first = now()
       this.queue.push({ job, resolve, reject })
       if (this.queue.length >= this.engine.maxBatchDocs) this.kick(0)
       else this.kick(this.engine.batchWindowMs)
@@ -55,13 +58,18 @@ class Batcher {
     if (this.inflight || this.queue.length === 0) return
     const batch = this.queue.splice(0, this.engine.maxBatchDocs)
     this.inflight = true
+    const t0 = now()
     try {
       const res = await this.engine._run(this.op, batch.map(b => b.job))
+      const t1 = now()
       batch.forEach((b, i) => {
         const st = res.status[i]
         if (st === 0) b.resolve(res.outputs[i])
         else b.reject(new YgmError(st, loadAddon().strerror(st)))
       })
+      // the last batch's time split (engine.timing[op]): window wait, JS packing, the native call (worker
+      // execution + copy-out), settling the documents' promises
+      this.engine.timing[this.op] = { docs: batch.length, wait_ms: t0 - (this.t_first || t0), ...this.engine._last, settle_ms: now() - t1 }
     } catch (e) {
       batch.forEach(b => b.reject(e))
     } finally {
@@ -69,6 +77,31 @@ class Batcher {
       if (this.queue.length) this.kick(this.queue.length >= this.engine.maxBatchDocs ? 0 : this.engine.batchWindowMs)
     }
   }
+}
+
+// one batch arena from merge jobs: an array of updates, or { head: Uint8Array[], arena, lens } whose log part is
+// already packed (UpdateLog): one copy per document, and the per-update lengths / document ids by typed-array
+// fills instead of per-update pushes
+function packJobs (jobs) {
+  let nUpd = 0; let total = 0
+  for (const j of jobs) {
+    if (Array.isArray(j)) { nUpd += j.length; for (const u of j) total += u.length } else {
+      nUpd += j.head.length + j.lens.length; total += j.arena.length
+      for (const u of j.head) total += u.length
+    }
+  }
+  const arena = Buffer.allocUnsafe(total)
+  const lens = new Uint32Array(nUpd)
+  const docs = new Uint32Array(nUpd)
+  let o = 0; let k = 0
+  jobs.forEach((j, d) => {
+    const k0 = k
+    const ups = Array.isArray(j) ? j : j.head
+    for (const u of ups) { arena.set(u, o); o += u.length; lens[k++] = u.length }
+    if (!Array.isArray(j)) { arena.set(j.arena, o); o += j.arena.length; lens.set(j.lens, k); k += j.lens.length }
+    docs.fill(d, k0, k)
+  })
+  return { arena, lens, docs }
 }
 
 function packBlobs (blobs) {
@@ -92,6 +125,8 @@ class GpuEngine {
     this.maxBatchDocs = opts.maxBatchDocs || 65536
     this.handle = loadAddon().open(this.device, this.flags)
     this.batchers = { merge: new Batcher(this, 'merge'), diff: new Batcher(this, 'diff'), sv: new Batcher(this, 'sv'), snapshot: new Batcher(this, 'snapshot') }
+    this.timing = {}
+    this._last = {}
     this.chain = Promise.resolve()
   }
 
@@ -100,10 +135,18 @@ class GpuEngine {
     const run = () => {
       const a = loadAddon()
       if (op === 'merge' || op === 'mergeV2') {
-        const blobs = []; const docs = []
-        jobs.forEach((ups, d) => { for (const u of ups) { blobs.push(u); docs.push(d) } })
-        const { arena, lens } = packBlobs(blobs)
-        return (op === 'merge' ? a.mergeMany : a.mergeManyV2)(this.handle, arena, lens, Uint32Array.from(docs), jobs.length)
+        const t0 = now()
+        const { arena, lens, docs } = packJobs(jobs)
+        const t1 = now()
+        const s0 = this.stats()
+        const p = (op === 'merge' ? a.mergeMany : a.mergeManyV2)(this.handle, arena, lens, docs, jobs.length)
+        const t2 = now()
+        return p.then(r => {
+          const s1 = this.stats()
+          this._last = { pack_ms: t1 - t0, napi_in_ms: t2 - t1, native_ms: now() - t2, exec_ms: r.execMs, copy_out_ms: r.completeMs,
+            h2d_ms: s1.h2dMs - s0.h2dMs, kernel_ms: s1.kernelMs - s0.kernelMs, d2h_ms: s1.d2hMs - s0.d2hMs, bytes: arena.length }
+          return r
+        })
       }
       if (op === 'diff' || op === 'contains' || op === 'diffV2') {
         const u = packBlobs(jobs.map(j => j[0])); const s = packBlobs(jobs.map(j => j[1]))
@@ -120,6 +163,8 @@ class GpuEngine {
 
   /** Y.mergeUpdates(updates), batched with concurrent callers. */
   mergeUpdates (updates) { return this.batchers.merge.push(updates.map(u => u instanceof Uint8Array ? u : Uint8Array.from(u))) }
+  /** Y.mergeUpdates([...head, ...the packed updates]) for { head: Uint8Array[], arena, lens } (UpdateLog.packed) */
+  mergePacked (job) { return this.batchers.merge.push(job) }
   /** Y.diffUpdate(update, stateVector) */
   diffUpdate (update, sv) { return this.batchers.diff.push([update, sv]) }
   /** Y.encodeStateVectorFromUpdate(update) */
@@ -181,6 +226,10 @@ class GpuEnginePool {
   shardOf (documentName) { return Number(fnv1a64(documentName) % BigInt(this.engines.length)) }
   engineFor (documentName) { return this.engines[this.shardOf(documentName)] }
   mergeUpdates (updates, documentName = '') { return this.engineFor(documentName).mergeUpdates(updates) }
+  mergePacked (job, documentName = '') {
+    const e = this.engineFor(documentName)
+    return e.mergePacked ? e.mergePacked(job) : e.mergeUpdates(jobUpdates(job))
+  }
   diffUpdate (update, sv, documentName = '') { return this.engineFor(documentName).diffUpdate(update, sv) }
   encodeStateVectorFromUpdate (update, documentName = '') { return this.engineFor(documentName).encodeStateVectorFromUpdate(update) }
   snapshot (update, documentName = '') { return this.engineFor(documentName).snapshot(update) }
@@ -206,4 +255,4 @@ class GpuEnginePool {
   close () { this.engines.forEach(e => e.close()) }
 }
 
-module.exports = { GpuEngine, GpuEnginePool, fnv1a64, YgmError, STATUS, loadAddon }
+module.exports = { packJobs, GpuEngine, GpuEnginePool, fnv1a64, YgmError, STATUS, loadAddon }

@@ -18,6 +18,7 @@
 const { GpuEngine, GpuEnginePool, fnv1a64, YgmError } = require('./engine')
 const { SyncResponder } = require('./sync')
 const { RedisFanout } = require('./redis')
+const { UpdateLog } = require('./log')
 
 /**
  * A batched document store.  `fromDatabase` adapts any DatabaseConfiguration
@@ -62,7 +63,7 @@ class GpuMerge {
       : DocumentStore.fromDatabase({ fetch: configuration.fetch, store: typeof st === 'function' ? st : undefined })
     this.Y = configuration.Y || null
     this.engine = configuration.engine || null
-    /** documentName -> { base: Uint8Array|null, log: Uint8Array[], doc?: Y.Doc, onUpdate?: Function } */
+    /** documentName -> { base: Uint8Array|null, log: UpdateLog (packed captured updates), doc?: Y.Doc, onUpdate?: Function } */
     this.docs = new Map()
     /** stores that fell back to Y.encodeStateAsUpdate(document) because the engine refused the merge */
     this.refused = []
@@ -88,7 +89,7 @@ class GpuMerge {
   syncResponder () {
     return new SyncResponder({
       engine: this._engine(),
-      getState: async name => { const e = this.docs.get(name); return e ? (e.base ? [e.base] : []).concat(e.log) : null }
+      getState: async name => { const e = this.docs.get(name); return e ? (e.base ? [e.base] : []).concat(e.log.toArray()) : null }
     })
   }
 
@@ -108,7 +109,7 @@ class GpuMerge {
       state = parts.length === 0 ? null : parts.length === 1 ? parts[0] : await this._engine().mergeUpdates(parts, data.documentName)
     } else if (fetched) state = fetched
     if (state) this._Y().applyUpdate(data.document, state)
-    this.docs.set(data.documentName, { base: state, log: [] })
+    this.docs.set(data.documentName, { base: state, log: new UpdateLog() })
   }
 
   /**
@@ -123,7 +124,7 @@ class GpuMerge {
    */
   async afterLoadDocument (data) {
     const Y = this._Y()
-    const entry = this.docs.get(data.documentName) || { base: null, log: [] }
+    const entry = this.docs.get(data.documentName) || { base: null, log: new UpdateLog() }
     this.docs.set(data.documentName, entry)
     const baseSV = entry.base ? Y.encodeStateVectorFromUpdate(entry.base) : new Uint8Array([0])
     const missing = Y.encodeStateAsUpdate(data.document, baseSV)
@@ -139,26 +140,29 @@ class GpuMerge {
   async onChange (data) {
     let entry = this.docs.get(data.documentName)
     if (entry && entry.onUpdate) return
-    if (!entry) { entry = { base: null, log: [] }; this.docs.set(data.documentName, entry) }
+    if (!entry) { entry = { base: null, log: new UpdateLog() }; this.docs.set(data.documentName, entry) }
     entry.log.push(data.update)
   }
 
   /** store = mergeUpdates([base, ...log]) on the GPU, then the same store payload shape (Database.ts:55-60) */
   async onStoreDocument (data) {
-    const entry = this.docs.get(data.documentName) || { base: null, log: [] }
+    const entry = this.docs.get(data.documentName) || { base: null, log: new UpdateLog() }
     this.docs.set(data.documentName, entry)
     const taken = entry.log.length
-    const parts = (entry.base ? [entry.base] : []).concat(entry.log.slice(0, taken))
+    const nparts = (entry.base ? 1 : 0) + taken
     let state
     // updates the stored state holds: the `taken` ones, or -- when the state is the live document's
     // encodeStateAsUpdate -- every update captured up to that synchronous call (updates that arrive
     // while storeMany is pending are not in it and stay in the log)
     let cut = taken
-    if (parts.length === 0) { state = this._Y().encodeStateAsUpdate(data.document); cut = entry.log.length } // nothing captured: extension-database's bytes
-    else if (parts.length === 1) state = parts[0]
+    if (nparts === 0) { state = this._Y().encodeStateAsUpdate(data.document); cut = entry.log.length } // nothing captured: extension-database's bytes
+    else if (nparts === 1) state = entry.base || new Uint8Array(entry.log.toArray(1)[0])   // (a copy: the log's buffer is reused)
     else {
       try {
-        state = await this._engine().mergeUpdates(parts, data.documentName)
+        // the captured updates go to the batch as one packed range (UpdateLog): one copy per document
+        const job = { head: entry.base ? [entry.base] : [], ...entry.log.packed(taken) }
+        const eng = this._engine()
+        state = await (eng.mergePacked ? eng.mergePacked(job, data.documentName) : eng.mergeUpdates(job.head.concat(entry.log.toArray(taken)), data.documentName))
         if (this.configuration.normalize) state = await this._normalize(state, data.documentName)
       } catch (e) {
         // a document the engine refuses (content yjs would re-encode, YGM_ENONCANON; a corrupt stored
@@ -173,7 +177,7 @@ class GpuMerge {
     await this.store.storeMany([{ payload: data, state: Buffer.from(state.buffer, state.byteOffset, state.byteLength) }])
     // the stored state becomes the new base (under the document's saveMutex, Hocuspocus.ts:427)
     entry.base = state
-    entry.log.splice(0, cut)
+    entry.log.drop(cut)
   }
 
   // the doc-normalized snapshot of a merged state; outside the kernel's envelope the merge is kept
@@ -206,4 +210,4 @@ async function addsToBase (engine, missing, base, name) {
   return Buffer.compare(Buffer.from(withIt), Buffer.from(without)) !== 0
 }
 
-module.exports = { GpuMerge, DocumentStore, GpuEngine, GpuEnginePool, SyncResponder, RedisFanout, fnv1a64, YgmError }
+module.exports = { GpuMerge, DocumentStore, GpuEngine, GpuEnginePool, SyncResponder, RedisFanout, UpdateLog, fnv1a64, YgmError }

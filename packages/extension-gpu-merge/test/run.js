@@ -10,6 +10,8 @@ const { GpuMerge, GpuEnginePool, fnv1a64 } = require('../src/index.js')
 const { frame, decodeSyncMessage, MessageType, SyncStep, SyncResponder } = require('../src/sync.js')
 const { RedisFanout } = require('../src/redis.js')
 const { MiniHocuspocus } = require('./harness.js')
+const { UpdateLog, jobUpdates } = require('../src/log.js')
+const { packJobs } = require('../src/engine.js')
 
 const mode = process.argv.includes('--gpu') ? 'gpu' : 'cpu'
 const Y = require(path.join(__dirname, '..', '..', '..', 'tools', 'yjs_bundle.js')).load()   // the test oracle: yjs from the image's bundle
@@ -17,6 +19,7 @@ const Y = require(path.join(__dirname, '..', '..', '..', 'tools', 'yjs_bundle.js
 class CpuDouble { // test double (never shipped): same API as GpuEngine
   constructor (device = 0) { this.calls = 0; this.device = device }
   async mergeUpdates (u) { this.calls++; return Y.mergeUpdates(u) }
+  async mergePacked (job) { this.calls++; return Y.mergeUpdates(jobUpdates(job)) }
   async mergeMany (docs) { this.calls++; return docs.map(u => { try { return Y.mergeUpdates(u) } catch (e) { return e } }) }   // per-document errors, as GpuEngine
   async diffMany (states, svs) { this.calls++; return states.map((u, i) => Y.diffUpdate(u, svs[i])) }
   async stateVectorsMany (states) { this.calls++; return states.map(u => Y.encodeStateVectorFromUpdate(u)) }
@@ -152,10 +155,11 @@ test('concurrent stores of many documents', async (engine) => {
 test('refused document: throws only its store, or stores the reference bytes', async (engine) => {
   const db = memoryDb()
   const payload = name => { const document = new Y.Doc(); document.getText('t').insert(0, 'live ' + name); return { documentName: name, document, context: {} } }
-  const bad = () => ({ base: Uint8Array.from([1, 1, 5, 0, 4, 1, 1, 0x74]), log: [Uint8Array.from([0, 0])] }) // truncated base
+  const logOf = ups => { const l = new UpdateLog(); ups.forEach(u => l.push(u)); return l }
+  const bad = () => ({ base: Uint8Array.from([1, 1, 5, 0, 4, 1, 1, 0x74]), log: logOf([Uint8Array.from([0, 0])]) }) // truncated base
   const strict = new GpuMerge({ ...db, Y, engine, onRefused: 'throw' })
   strict.docs.set('bad', bad())
-  strict.docs.set('good', { base: null, log: [Uint8Array.from([0, 0]), Uint8Array.from([0, 0])] })
+  strict.docs.set('good', { base: null, log: logOf([Uint8Array.from([0, 0]), Uint8Array.from([0, 0])]) })
   const r = await Promise.allSettled([strict.onStoreDocument(payload('bad')), strict.onStoreDocument(payload('good'))])
   assert.strictEqual(r[0].status, 'rejected')
   assert.strictEqual(r[1].status, 'fulfilled')
@@ -331,7 +335,7 @@ test('refused store keeps updates applied while the database write is pending', 
   assert.strictEqual(entry.log.length, 1, 'the update applied during the write stays in the log')
   const back = new Y.Doc(); Y.applyUpdate(back, rows.get('pending'))
   assert.strictEqual(back.getText('t').toString(), 'abc')
-  const next = Y.mergeUpdates([entry.base].concat(entry.log))
+  const next = Y.mergeUpdates([entry.base].concat(entry.log.toArray()))
   const full = new Y.Doc(); Y.applyUpdate(full, next)
   assert.strictEqual(full.getText('t').toString(), 'abcXYZ')
 })
@@ -365,6 +369,28 @@ test('redis fan-out reports a failed Step1 batch', async (engine) => {
   await sleep(5)
   assert.strictEqual(seen.length, 1)
   assert.strictEqual(seen[0].message, 'db down')
+})
+
+// the packed capture log and the batch packer (one copy per document at store time)
+test('UpdateLog packs, drops and views captured updates; packJobs builds the batch arena', async () => {
+  const log = new UpdateLog()
+  const ups = []
+  for (let i = 0; i < 300; i++) { const u = Uint8Array.from({ length: 1 + (i * 7) % 40 }, (_, k) => (i + k) & 255); ups.push(u); log.push(u) }
+  assert.strictEqual(log.length, 300)
+  const view = log.packed(120)
+  const held = Buffer.from(view.arena)
+  assert.deepStrictEqual(jobUpdates({ head: [], ...view }).map(u => Buffer.from(u).toString('hex')), ups.slice(0, 120).map(u => Buffer.from(u).toString('hex')))
+  log.drop(120)
+  log.push(Uint8Array.from([9, 9, 9]))
+  assert.strictEqual(Buffer.compare(Buffer.from(view.arena), held), 0, 'a view handed to a batch keeps its bytes')
+  assert.deepStrictEqual(log.toArray().map(u => Buffer.from(u).toString('hex')), ups.slice(120).concat([Uint8Array.from([9, 9, 9])]).map(u => Buffer.from(u).toString('hex')))
+  const head = Uint8Array.from([1, 2])
+  const jobs = [[Uint8Array.from([5]), Uint8Array.from([6, 7])], { head: [head], ...log.packed(3) }, []]
+  const { arena, lens, docs } = packJobs(jobs)
+  const flat = [Uint8Array.from([5]), Uint8Array.from([6, 7]), head].concat(log.toArray(3))
+  assert.strictEqual(Buffer.compare(arena, Buffer.concat(flat.map(u => Buffer.from(u)))), 0)
+  assert.deepStrictEqual(Array.from(lens), flat.map(u => u.length))
+  assert.deepStrictEqual(Array.from(docs), [0, 0, 1, 1, 1, 1])
 })
 
 test('engine pool shards by fnv1a64(name) and keeps caller order', async () => {
@@ -418,7 +444,7 @@ test('sync responder answers a SyncStep1 batch', async (engine) => {
   assert.ok(replies[msgs.length - 1] instanceof Error)
   want.forEach(({ n, sv }, i) => {
     const e = ext.docs.get(n)
-    const state = Y.mergeUpdates([e.base].concat(e.log))
+    const state = Y.mergeUpdates([e.base].concat(e.log.toArray()))
     const [step1, step2] = replies[i]                                   // the reference's order: server Step1, then Step2
     const a = decodeSyncMessage(step2); const b = decodeSyncMessage(step1)
     assert.strictEqual(a.documentName, n); assert.strictEqual(a.messageType, MessageType.Sync); assert.strictEqual(a.step, SyncStep.Step2)

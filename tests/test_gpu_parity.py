@@ -256,6 +256,44 @@ def test_lean_kernel_takes_debounce_logs(eng):
             assert took == 0
 
 
+def test_wide_lean_kernel_takes_mixed_logs(eng):
+    # c2_mixed shape (bench.py mixed_block): 1-8 clients, 1-16 character inserts (updates of up to ~42
+    # bytes), 20 % deletions -- past the narrow kernel's 32-byte window, finished by the wide lean kernel
+    from tools import synth
+    n = 2000
+    arena, upd_off, doc_upd = synth.text_updates(n, 200, 1, 8, del_pct=20, seed=71, max_run=16)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(n)]
+    s0 = eng.stats()
+    res = eng.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+    assert not bad, (len(bad), bad[:5])
+    s1 = eng.stats()
+    assert s1.docs_lean - s0.docs_lean >= 0.9 * n
+    assert s1.docs_lean_wide - s0.docs_lean_wide >= 0.9 * n
+
+
+def test_lean_deferrals_beside_single_update_documents(eng):
+    # more documents than the narrow kernel's persistent grid, so every wave takes several: single-update
+    # and empty documents (passed through, not parsed) between documents the narrow kernel defers must not
+    # shift the wave's record of which documents it deferred
+    from tools import synth
+    rng = random.Random(5)
+    arena, upd_off, doc_upd = synth.text_updates(3000, 30, 9, 12, seed=13)         # 9+ clients: deferred
+    ups = synth.split(arena, upd_off)
+    deferred = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(3000)]
+    arena, upd_off, doc_upd = synth.text_updates(3000, 30, 1, 3, seed=14)          # lean
+    ups = synth.split(arena, upd_off)
+    lean = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(3000)]
+    docs = []
+    for i in range(12000):
+        r = rng.random()
+        docs.append([] if r < 0.1 else [lean[i % 3000][0]] if r < 0.4 else deferred[i % 3000] if r < 0.6 else lean[i % 3000])
+    res = eng.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+    assert not bad, (len(bad), bad[:5])
+
+
 def _lean_edge_docs(n_docs, seed):
     """Debounce-log-like documents whose updates probe every branch of the lean kernel's
     parser: string lengths around the 32-byte window, non-ASCII, ContentDeleted, parent

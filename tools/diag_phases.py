@@ -16,7 +16,11 @@ eng.LIB_PATH = os.path.join(ROOT, "hocuspocus_amd", "libygm_diag.so")
 from tools import synth  # noqa: E402
 
 n_docs = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
-arena, upd_off, doc_upd = synth.text_updates(n_docs, 200, seed=1000)
+mixed = len(sys.argv) > 2 and sys.argv[2] == "mixed"   # the c2_mixed corpus: stamps of the wide kernel's waves
+if mixed:
+    arena, upd_off, doc_upd = synth.text_updates(n_docs, 200, 1, 8, del_pct=20, seed=71, max_run=16)
+else:
+    arena, upd_off, doc_upd = synth.text_updates(n_docs, 200, seed=1000)
 upd_doc = np.repeat(np.arange(n_docs, dtype=np.uint32), np.diff(doc_upd).astype(np.int64))
 e = eng.Engine(0)
 L = eng.lib()
@@ -29,10 +33,10 @@ for rep in range(3):
     e.merge_packed(arena, upd_off, upd_doc, n_docs)
     L.ygm_diag_read(buf.ctypes.data, 0)
 L.ygm_diag_ts_read(ts.ctypes.data, 0)
-t = ts.reshape(16384, 8)[:min(n_docs, 16384)].astype(np.int64)
+t = ts.reshape(16384, 8)[:min(n_docs, 1500 if mixed else 16384)].astype(np.int64)
 # slots: 0 start, 6 header loaded, 1 staged, 2 parsed, 3 scanned, 4 emitted, 8 end (s_memrealtime, 100 MHz -> ns x10)
 print("k_merge_lean - ns per document (mean; s_memrealtime stamps):")
-order = [("header (doc_upd/upd_off)", 6), ("stage", 1), ("parse", 2), ("clients+scan", 3), ("emit", 4), ("tail", 8)]
+order = [("stage", 1), ("parse", 2), ("clients+scan", 3), ("emit", 4), ("tail", 8)]
 prev = t[:, 0]
 for nm, c in order:
     col = t[:, c] if c < 8 else None
@@ -41,8 +45,12 @@ for nm, c in order:
     ok = col > 0
     print(f"  {nm:26s} {10.0 * np.mean(col[ok] - prev[ok]):10.0f}")
     prev = np.where(ok, col, prev)
-life = np.max(t[:, 1:], axis=1) - t[:, 0]
-span = np.max(t[:, 1:]) - np.min(t[:, 0])
+ds = t[:, 7] - t[:, 6]
+okd = (t[:, 6] > 0) & (t[:, 7] >= t[:, 6])
+print(f"  of which: parsed -> delete-set union {10.0 * np.mean((t[:, 6] - t[:, 2])[okd]):.0f}, the union {10.0 * np.mean(ds[okd]):.0f}, "
+      f"union -> scanned {10.0 * np.mean((t[:, 3] - t[:, 7])[okd]):.0f}")
+life = np.max(t[:, 1:6], axis=1) - t[:, 0]
+span = np.max(t[:, 1:6]) - np.min(t[:, 0])
 print(f"  lifetime mean {10.0 * life.mean():.0f} ns  kernel span {10.0 * span:.0f} ns  mean docs in flight {life.sum() / max(span, 1):.1f}")
 st = np.sort(t[:, 0] - t[:, 0].min())
 print("  start-time percentiles (ns) 10/50/90/100:", [int(10 * np.percentile(st, p)) for p in (10, 50, 90, 100)])

@@ -2578,6 +2578,11 @@ int ygm_diag_ts_read(unsigned long long* out, int reset) {  // 16384 x 8 stamps 
   (void)reset;
   return 0;
 }
+int ygm_diag_ds_read(unsigned long long* out, int reset) {   // 4 delete-set union cycle sums
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ygm_diag_ds), sizeof(unsigned long long) * 4) != hipSuccess) return -1;
+  if (reset) { unsigned long long z[4] = {0}; (void)hipMemcpyToSymbol(HIP_SYMBOL(ygm_diag_ds), z, sizeof z); }
+  return 0;
+}
 int ygm_diag_read(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ygm_diag), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
   if (reset) { unsigned long long z[32] = {0}; (void)hipMemcpyToSymbol(HIP_SYMBOL(ygm_diag), z, sizeof z); }

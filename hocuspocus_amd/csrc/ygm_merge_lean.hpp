@@ -419,6 +419,15 @@ struct LDsUnion {
   uint32_t nsegs, bytes;                  // uniform: clients, encoded DS bytes
   bool bad;
 };
+#ifdef YGM_DIAG
+// diagnostic build: shader cycles of the union's parts (records, rank sort, runs / scans), summed over waves
+static __device__ unsigned long long ygm_diag_ds[4];
+#define LDS_T0 unsigned long long _dst = __builtin_amdgcn_s_memtime();
+#define LDS_STAMP(i) do { const unsigned long long _n = __builtin_amdgcn_s_memtime(); if (threadIdx.x == 0) atomicAdd(&ygm_diag_ds[i], _n - _dst); _dst = _n; } while (0)
+#else
+#define LDS_T0
+#define LDS_STAMP(i)
+#endif
 // scratch: 16 * LN_DSMAX bytes of LDS (records, then the sorted records)
 YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS], const uint32_t (&uend)[LN_ROWS],
                             const bool (&hasd)[LN_ROWS], uint32_t flags) {
@@ -427,6 +436,7 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
   U.client = 0; U.nruns = 0; U.sclock = 0; U.rend = 0;
   LB32* rc = scr; LB32* rk = scr + LN_DSMAX; LB32* re = scr + 2 * LN_DSMAX;
   uint32_t nrec = 0, bad = 0;
+  LDS_T0
   // ---- records of every update's DS, in update order (the order only matters for ties, which
   //      the union does not see)
 #pragma unroll
@@ -477,6 +487,7 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
     bad |= c.bad | (lean_ds_more(c) ? 1u : 0u);   // malformed, or more ranges than the loop takes
   }
   U.bad = __ballot(bad != 0u) != 0 || nrec > (uint32_t)LN_DSMAX || nrec == 0u;
+  LDS_STAMP(0);
   if (U.bad) return U;
   wave_sync();
   // ---- rank sort by (client descending, clock ascending, record order)
@@ -487,6 +498,7 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
     const uint32_t cj = rdlane(cl, j), kj = rdlane(ck, j);
     rank += (cj > cl || (cj == cl && (kj < ck || (kj == ck && j < l)))) ? 1u : 0u;
   }
+  LDS_STAMP(1);
   LB32* sc = scr + 3 * LN_DSMAX;   // sorted clients; clocks / ends reuse rk / re after the reads above
   wave_sync();
   if (v) { sc[rank] = cl; rk[rank] = ck; re[rank] = en; }
@@ -520,6 +532,7 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
   U.segstart = segstart; U.runend = runend; U.pos = ib - tb;
   U.nsegs = nsegs; U.bytes = vlen32(nsegs) + lane63(ib);
   U.bad = (flags & 1u) && nsegs > 1u;   // yjs 13.5 writes clients in first-seen order: general path
+  LDS_STAMP(2);
   return U;
 }
 // writes the delete set at t (the output buffer is zeroed)

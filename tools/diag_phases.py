@@ -62,5 +62,11 @@ for title, nms, lo in (("k_merge_wave (wave per document)", ["stage", "parse", "
     print(title, "- shader cycles per document (mean, last rep):")
     for i, nm in enumerate(nms):
         print(f"  {nm:16s} {buf[lo + i] / n_docs:12.0f}  {100.0 * buf[lo + i] / max(tot, 1):5.1f}%")
+if mixed:
+    L.ygm_diag_ds_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    dsb = np.zeros(4, np.uint64)
+    L.ygm_diag_ds_read(dsb.ctypes.data, 0)
+    print("delete-set union, shader cycles per document (3 reps): records", int(dsb[0]) // (3 * n_docs), "rank sort",
+          int(dsb[1]) // (3 * n_docs), "runs/scans", int(dsb[2]) // (3 * n_docs))
 s = e.stats()
 print("kernel_ms (3 reps)", s.kernel_ms, "lean_ms", s.lean_ms, "docs_lean", s.docs_lean)

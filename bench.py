@@ -18,6 +18,8 @@ the lean kernel -- asserted -- so no step needs the host-driven tiers).  Beside 
   c2_mixed C2 past the lean kernel's envelope: 1-8 clients, 1-16 character inserts, 20 % deletions (tier cascade)
   c3       config C3 at full size (configs[2]): 100 000 [snapshot, ...log] documents of 10 MB * rank^-0.8 (0.77 GB)
            merged in one batch through the tier cascade, beside the C port and yjs (rank 0 at N = 1)
+  c5       config C5 at BASELINE size (configs[4]): 1 000 Y.XmlFragment [snapshot, ...log] documents of 5-10 k client
+           blocks each (0.29 GB), formats / embeds / attributes, merged in one batch, beside the C port and yjs
   v2       SURVEY.md §8f-4: the C2 merge with the updates in format V2 (Y.mergeUpdatesV2), and the V1 <-> V2
            conversions of its 2 M updates
   cpu_baseline  the reference yjs path on the GPU box's host cores (yjs 13.5.16 from the image's
@@ -70,6 +72,7 @@ def parse():
     ap.add_argument("--no-yjs", action="store_true", help="skip the Node / yjs leg of the CPU baseline")
     ap.add_argument("--no-v2", dest="v2", action="store_false", help="skip the update-V2 (f-4) block")
     ap.add_argument("--no-c3", dest="c3", action="store_false", help="skip the full-size C3 block")
+    ap.add_argument("--c5-docs", type=int, default=1000, help="documents of the C5 block (BASELINE size 1000; 0: skip)")
     ap.add_argument("--no-mixed", dest="mixed", action="store_false", help="skip the c2_mixed block")
     ap.add_argument("--f1-docs", type=int, default=10000, help="documents of the f1 (doc-normalized snapshot) block (0: skip)")
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
@@ -786,6 +789,13 @@ def run_rank(args, rank, world, dist, be, dev=None):
         blk = big_run(args, "c3full", be.dev.index)
         blk["roofline"] = roof(blk["bytes_in"] + blk["bytes_out"], blk["gpu_ms"], "merge cascade (k_merge_lean / wave / fast / big)", None)
         line["c3"] = blk
+    # ---- C5 at BASELINE size (1 000 XmlFragment [snapshot, ...log] documents of 5-10 k client blocks): rank 0 at N = 1
+    if args.c5_docs and rank == 0 and world == 1 and not args.dry_run:
+        a5 = argparse.Namespace(**vars(args))
+        a5.big_docs = args.c5_docs
+        blk = big_run(a5, "c5", be.dev.index)
+        blk["roofline"] = roof(blk["bytes_in"] + blk["bytes_out"], blk["gpu_ms"], "merge cascade (k_merge_big for these documents)", None)
+        line["c5"] = blk
     # ---- CPU baselines (rank 0 at N = 1 only)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         cores = cpu_cores(args)
@@ -856,9 +866,12 @@ def big_run(args, kind, dev_index=0):
     sizes = np.diff(upd_off[doc_upd].astype(np.int64))
     port = {"ms": round(cdt * 1e3, 3), "MBps": round(calgo / cdt / 1e6, 1), "cores": cores, "host": host_cpus(), "kind": "port",
             "sample": "all documents of the batch through oracle/yjs_oracle.c yo_merge_batch, one pass"}
-    y = None if (args.no_yjs or args.no_cpu_baseline) else cpu_yjs("merge", {"arena": arena, "upd_off": upd_off, "doc_upd": doc_upd}, cores, n)
+    ny = n if kind != "c5" else min(n, 200)   # C5: a bounded yjs sample (the first documents are the largest)
+    y = None if (args.no_yjs or args.no_cpu_baseline) else cpu_yjs("merge", {"arena": arena, "upd_off": upd_off, "doc_upd": doc_upd}, cores, ny)
     if y and "value" in y:
         y["ms"] = round(n / y["docs_per_s"] * 1e3, 3)   # the whole batch (slowest worker)
+        if ny < n:
+            y["ms_note"] = f"extrapolated from the first {ny} documents' rate (the largest ones) to all {n}"
     e.close()
     return {"config": kind.upper(), "op": "merge", "docs": n, "bytes_in": len(arena), "bytes_out": int(r.payload_bytes),
             "largest_doc": int(sizes.max()),

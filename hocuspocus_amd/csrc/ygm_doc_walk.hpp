@@ -57,7 +57,16 @@ constexpr int DW_P = DW_S * 4;    // 16-byte pieces per ring
 constexpr int DW_R = YGM_DW_R;    // parse iterations per round
 constexpr int DW_U = YGM_DW_U;    // Items the fast decoder takes per iteration (from one 64-byte mask window)
 constexpr uint32_t DW_STG = YGM_DW_STG;   // chunks staged per round (<= 4: 64 staging registers)
-constexpr uint32_t DW_AHEAD = 2;  // chunks staged past the ring's free slots (committed if the round freed theirs)
+#ifndef YGM_DW_AHEAD
+#define YGM_DW_AHEAD 2
+#endif
+#ifndef YGM_DW_LINE
+#define YGM_DW_LINE 0
+#endif
+constexpr uint32_t DW_AHEAD = YGM_DW_AHEAD;  // chunks staged past the ring's free slots (committed if the round freed theirs)
+// 1: stage whole 128-byte lines (chunk pairs of a 128-byte aligned base): the two 64-byte halves of a line are
+// loaded together, not rounds apart (where the second half's fetch misses an L2 that has evicted the line)
+constexpr bool DW_LINE = YGM_DW_LINE != 0;
 constexpr int DW_BATCH = YGM_DW_BATCH;   // documents sorted (largest first) per batch of a wave's range
 constexpr int DW_SVN = 16;        // state-vector entries per lane (diff)
 constexpr uint32_t DW_OPEN = 0xFFFFFFFFu;

@@ -372,7 +372,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
     }
     if (stg_n) {
       // the document part [vlo, vhi) of chunk k is checked (table chunks: none)
-      auto vlo = [&](uint32_t k) { return k == tc ? srel - 64u * tc : 0u; };
+      auto vlo = [&](uint32_t k) { return srel > 64u * k ? (srel - 64u * k < 64u ? srel - 64u * k : 64u) : 0u; };
       auto vhi = [&](uint32_t k) { return k < tc ? 0u : (rb - 64u * k < 64u ? rb - 64u * k : 64u); };
       dw_commit<MODE == 1>(L, l, stg_k, g0, g1, g2, g3, vlo(stg_k), vhi(stg_k), prev8, bad);
       if (stg_n > 1u) {
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
 #pragma unroll
         for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) sk[i] = 0u;
       }
-      cbase = da & ~15ull; srel = 64u * tc + (uint32_t)(da - cbase); q = srel; rb = 64u * tc + (uint32_t)(db - cbase);
+      cbase = da & (DW_LINE ? ~127ull : ~15ull); srel = 64u * tc + (uint32_t)(da - cbase); q = srel; rb = 64u * tc + (uint32_t)(db - cbase);
       landed = 0; stg_n = 0; prev8 = 0;
       bad |= (db < da || ((db - da) >> 30)) ? 1u : 0u;
       ph = tc ? WK_SVN : WK_UPD;
@@ -511,7 +511,8 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
       if (run_on && cp < need) need = cp;
       const uint32_t nch = (rb + 63u) >> 6;
       const uint32_t wk = (need >> 6) + DW_S + DW_AHEAD < nch ? (need >> 6) + DW_S + DW_AHEAD : nch;
-      const uint32_t n = wk > landed ? (wk - landed < DW_STG ? wk - landed : DW_STG) : 0u;
+      uint32_t n = wk > landed ? (wk - landed < DW_STG ? wk - landed : DW_STG) : 0u;
+      if (DW_LINE && n > 1u && ((landed + n - tc) & 1u) && landed + n < nch) n--;   // end on a line boundary
       stg_k = landed; stg_n = n;
       auto chunk = [&](uint32_t k) -> const u32x4* {
         return (const u32x4*)(MODE == 1 && k < tc ? tbl + 144ull * d + 64u * k : arena + cbase + 64ull * (k - tc));

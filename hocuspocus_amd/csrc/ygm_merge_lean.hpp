@@ -398,6 +398,42 @@ YDEV void dpp_max64_step(uint32_t& hi, uint32_t& lo) {
   const bool gt = h2 > hi || (h2 == hi && l2 > lo);
   hi = gt ? h2 : hi; lo = gt ? l2 : lo;
 }
+// lane l's value of x at lane l ^ J (J = 1, 2: quad permutes; 4, 8: row shifts by lane bit; 16, 32: bpermute)
+template <int J>
+YDEV uint32_t lane_xor(uint32_t x) {
+  if (J == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  if (J == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  if (J == 4 || J == 8) {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 | J, 0xF, 0xF, false);   // row_shl:J (lane + J)
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x110 | J, 0xF, 0xF, false);   // row_shr:J (lane - J)
+    return (threadIdx.x & J) ? dn : up;
+  }
+  return (uint32_t)__shfl_xor((int)x, J, 64);
+}
+// one compare-exchange stage of a 64-lane bitonic sort (ascending) on the key (a, b, c)
+template <int K, int J>
+YDEV void bitonic_step(uint32_t& a, uint32_t& b, uint32_t& c) {
+  const uint32_t oa = lane_xor<J>(a), ob = lane_xor<J>(b), oc = lane_xor<J>(c);
+  const bool lt = oa < a || (oa == a && (ob < b || (ob == b && oc < c)));   // other < mine
+  const uint32_t l = threadIdx.x;
+  const bool lower = (l & J) == 0, asc = (l & K) == 0;
+  const bool take = lower == asc ? lt : !lt;   // the lower lane of an ascending pair keeps the minimum
+  a = take ? oa : a; b = take ? ob : b; c = take ? oc : c;
+}
+template <int K, int J>
+YDEV void bitonic_merge(uint32_t& a, uint32_t& b, uint32_t& c) {
+  bitonic_step<K, J>(a, b, c);
+  if constexpr (J > 1) bitonic_merge<K, J / 2>(a, b, c);
+}
+// sorts the 64 lanes' distinct keys (a, b, c) ascending: lane l gets the l-th smallest
+YDEV void lane_bitonic3(uint32_t& a, uint32_t& b, uint32_t& c) {
+  bitonic_merge<2, 1>(a, b, c);
+  bitonic_merge<4, 2>(a, b, c);
+  bitonic_merge<8, 4>(a, b, c);
+  bitonic_merge<16, 8>(a, b, c);
+  bitonic_merge<32, 16>(a, b, c);
+  bitonic_merge<64, 32>(a, b, c);
+}
 YDEV uint64_t lean_max_scan64(uint64_t v) {   // inclusive prefix max over the wave (DPP, as dpp_incl_max)
   uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
   dpp_max64_step<0x111, 0xF, true>(hi, lo);   // row_shr:1
@@ -490,21 +526,15 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
   LDS_STAMP(0);
   if (U.bad) return U;
   wave_sync();
-  // ---- rank sort by (client descending, clock ascending, record order)
+  // ---- sort by (client descending, clock ascending, record order): a register bitonic network over the
+  //      64 lanes on the key (~client, clock, record index); empty lanes carry the largest key
   const bool v = l < nrec;
-  const uint32_t cl = v ? rc[l] : 0u, ck = v ? rk[l] : 0u, en = v ? re[l] : 0u;
-  uint32_t rank = 0;
-  for (uint32_t j = 0; j < nrec; j++) {
-    const uint32_t cj = rdlane(cl, j), kj = rdlane(ck, j);
-    rank += (cj > cl || (cj == cl && (kj < ck || (kj == ck && j < l)))) ? 1u : 0u;
-  }
+  uint32_t k0 = v ? ~rc[l] : 0xFFFFFFFFu, k1 = v ? rk[l] : 0xFFFFFFFFu, k2 = v ? l : 0xFFu;
+  lane_bitonic3(k0, k1, k2);
   LDS_STAMP(1);
-  LB32* sc = scr + 3 * LN_DSMAX;   // sorted clients; clocks / ends reuse rk / re after the reads above
-  wave_sync();
-  if (v) { sc[rank] = cl; rk[rank] = ck; re[rank] = en; }
-  wave_sync();
-  const uint32_t c = v ? sc[l] : 0u, k = v ? rk[l] : 0u, e = v ? re[l] : 0u;
-  const uint32_t cprev = (v && l > 0u) ? sc[l - 1u] : 0u;
+  // lane l holds the l-th record of the union order; its end from the record table (re is not rewritten)
+  const uint32_t c = v ? ~k0 : 0u, k = v ? k1 : 0u, e = v ? re[k2 & (LN_DSMAX - 1)] : 0u;
+  const uint32_t cprev = (uint32_t)__shfl_up((int)c, 1u, 64);
   // ---- runs: a range starts a run when it is its client's first or starts past every end so far
   const bool segstart = v && (l == 0u || cprev != c);
   const uint32_t segidx = dpp_incl_add(segstart ? 1u : 0u);

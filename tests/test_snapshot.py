@@ -10,7 +10,9 @@ The checker is yjs itself -- the image's 13.5.16 bundle (tools/yjs_bundle.js) --
 CPU tests pin the fixtures (regenerated here by the committed generator) and run the kernel's sequential
 code (ygm_snapshot.hpp) host-compiled through tools/snapdev; GPU tests run the HIP kernel through the C ABI
 in 13.5 compat mode (the bundle's behaviour).  The 13.6 default writes the delete set's clients in descending
-order instead of store order; that mode's snapshot bytes are parity unpinned (no 13.6 yjs in the image)."""
+order instead of store order (the only difference in a snapshot's bytes): the default mode is
+pinned against the same yjs vectors with their delete sets rewritten client-descending (golden.ds_to_desc) --
+a derived expectation, as no 13.6 yjs is in the image."""
 import gzip
 import json
 import os
@@ -90,6 +92,20 @@ def test_kernel_code_on_host_vs_fixtures(tmp_path):
     assert [g for g in got] == [(0, e) for _, e in rows]
 
 
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
+def test_kernel_code_on_host_default_mode(tmp_path):
+    """The same host-compiled kernel code in the 13.6 default mode: the yjs vectors with client-descending delete sets."""
+    from golden import ds_to_desc
+    exe = str(tmp_path / "snapdev")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", exe, os.path.join(ROOT, "tools", "snapdev", "snapdev.cpp")], check=True, timeout=300)
+    rows = fixtures()
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
+    write_in(a, [u for u, _ in rows])
+    subprocess.run([exe, a, b, "0"], check=True, timeout=120)
+    got = read_res(b)
+    assert got == [(0, bytes.fromhex(ds_to_desc(e.hex()))) for _, e in rows]
+
+
 # ---------------------------------------------------------------------------------------- GPU
 @pytest.fixture(scope="module")
 def eng135():
@@ -105,6 +121,19 @@ def test_gpu_snapshot_vs_yjs_fixtures(eng135):
     res = eng135.snapshot_batch([u for u, _ in rows])
     bad = [k for k, ((_, e), r) in enumerate(zip(rows, res)) if r != (0, e)]
     assert not bad, f"{len(bad)} documents differ from yjs, first {bad[:5]}: {res[bad[0]]}"
+
+
+@pytest.mark.gpu
+def test_gpu_snapshot_default_mode_vs_fixtures():
+    """The 13.6 default mode (what GpuMerge({normalize}) ships): the yjs vectors with client-descending delete sets."""
+    from golden import ds_to_desc
+    from hocuspocus_amd import Engine
+    rows = fixtures()
+    with Engine(0) as e:
+        res = e.snapshot_batch([u for u, _ in rows])
+    exp = [(0, bytes.fromhex(ds_to_desc(x.hex()))) for _, x in rows]
+    bad = [k for k in range(len(rows)) if res[k] != exp[k]]
+    assert not bad, f"{len(bad)} documents differ, first {bad[:5]}"
 
 
 @pytest.mark.gpu

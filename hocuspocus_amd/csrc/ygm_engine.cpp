@@ -61,10 +61,14 @@ int ygm_k_launch_v21(int pass, const uint8_t* arena, const uint64_t* upd_off, ui
                      uint32_t mode, uint32_t flags, uint64_t* len_or_off, int32_t* st, uint8_t* out, hipStream_t s);
 int ygm_k_launch_v12_count(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint8_t* v2a,
                            uint64_t v2n, const uint64_t* upd_off, const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint32_t mode,
-                           uint32_t flags, uint32_t* L, uint64_t* tot, int32_t* st, hipStream_t s);
+                           uint32_t flags, uint32_t* L, uint64_t* tot, int32_t* st, const uint8_t* claim, hipStream_t s);
 int ygm_k_launch_v12_write(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const uint8_t* v2a, uint64_t v2n,
                            const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t mode, uint32_t flags, const uint32_t* L,
-                           const uint64_t* off, int32_t* st, uint8_t* out, uint64_t* out_len, hipStream_t s);
+                           const uint64_t* off, int32_t* st, uint8_t* out, uint64_t* out_len, const uint8_t* claim, uint64_t base, uint64_t* fo,
+                           hipStream_t s);
+int ygm_k_launch_v12_fast(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint64_t* slot_off,
+                          const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint8_t* out, uint64_t* fo, uint64_t* olen, int32_t* ost,
+                          uint8_t* claim, unsigned long long* payload, hipStream_t s);
 int ygm_k_launch_v2_status(const int32_t* ust, uint32_t n, int32_t* status, uint64_t* len, hipStream_t s);
 int ygm_k_launch_v2_lens(const uint64_t* off, const int32_t* st, uint32_t n, uint64_t* len, hipStream_t s);
 size_t ygm_k_big_blk_bytes();
@@ -93,8 +97,19 @@ struct Meta {
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
-  bool ensure(size_t n) {
+  // keep > 0: the first `keep` bytes survive a regrowth (copied on stream s, which is then synchronised)
+  bool ensure(size_t n, size_t keep = 0, hipStream_t s = nullptr) {
     if (n <= cap && p) return true;
+    if (p && keep) {
+      void* q = nullptr;
+      size_t c = n + n / 4;
+      if (hipMalloc(&q, c) != hipSuccess) return false;
+      if (hipMemcpyAsync(q, p, std::min(keep, cap), hipMemcpyDeviceToDevice, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+        (void)hipFree(q); return false;
+      }
+      (void)hipFree(p); p = q; cap = c;
+      return true;
+    }
     if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
     size_t c = std::max<size_t>(n, 256);
     c += c / 4;  // grow with headroom
@@ -144,7 +159,7 @@ struct ygm_ctx {
   DevBuf sn_cnt, sn_off, sn_bs, sn_ws;  // snapshot: per-document counts, workspace offsets, scan scratch, workspaces
   // update V2: per-update V1 sizes -> offsets, transcoding statuses, scan scratch, the V1 arena, per-document column
   // lengths, the V2 outputs (packed), their offsets / lengths / statuses
-  DevBuf v2_len, v2_st, v2_bs, v2_v1, v2_L, v2_out, v2_off, v2_olen, v2_ost;
+  DevBuf v2_len, v2_st, v2_bs, v2_v1, v2_L, v2_out, v2_off, v2_olen, v2_ost, v2_fo, v2_claim, v2_pay;
   // host API: results in pinned memory (packed outputs, per-document offset / length / status), the
   // pinned input staging of this context when it serves as a pipeline stage, the packed device copy,
   // and the two stage contexts (own streams and buffers) that double-buffer a batch's chunks
@@ -216,7 +231,7 @@ void ygm_close(ygm_ctx* c) {
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
                     &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws,
-                    &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost})
+                    &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay})
     b->release();
   for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
   for (DevBuf* b : {&c->pk_data, &c->pk_off, &c->pk_bsum}) b->release();
@@ -546,30 +561,47 @@ static int v21_pass(ygm_ctx* c, hipStream_t s, const uint8_t* arena, const uint6
     return YGM_EDEVICE;
   return YGM_OK;
 }
-// V1 -> V2 per document into c->v2_out (packed at scanned offsets) with final statuses; see k_v12_count
+// V1 -> V2 per document with final statuses.  Documents in the fast encoder's shape (ygm_v2_fast.hpp) are done by
+// k_v12_fast into slots of c->v2_out placed from slot_off (the V2 input offsets: merge_slot of the document's input
+// bytes); the rest take k_v12_count / scan / k_v12_write, packed after the slot region.  slot_off == nullptr (the
+// public conversion): the general kernels only.
 static int v12_pass(ygm_ctx* c, hipStream_t s, const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st,
                     const uint8_t* v2a, uint64_t v2n, const uint64_t* upd_off, const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs,
-                    uint32_t mode, ygm_device_result* out) {
+                    uint32_t mode, const uint64_t* slot_off, ygm_device_result* out) {
   const size_t nb = ((size_t)n_docs + 1 + 255) / 256 + 2;
   if (!c->v2_L.ensure(4ull * ygm_k_v2_cols() * n_docs + 16) || !c->v2_off.ensure(8ull * n_docs + 16) || !c->v2_olen.ensure(8ull * n_docs + 8) ||
-      !c->v2_ost.ensure(4ull * n_docs + 4) || !c->v2_bs.ensure(8 * nb))
+      !c->v2_ost.ensure(4ull * n_docs + 4) || !c->v2_bs.ensure(8 * nb) || !c->v2_fo.ensure(8ull * n_docs + 8) ||
+      !c->v2_claim.ensure((size_t)n_docs + 16) || !c->v2_pay.ensure(16))
     return YGM_ENOMEM;
-  uint64_t total = 0;
+  const bool fast = slot_off != nullptr && !(mode & 1u) && getenv("YGM_V2_NOFAST") == nullptr;
+  const uint64_t slot_total = fast ? 2 * v2n + 64ull * n_docs : 0;
+  uint8_t* claim = fast ? c->v2_claim.as<uint8_t>() : nullptr;
+  if (fast && n_docs) {
+    if (!c->v2_out.ensure(slot_total + 64)) return YGM_ENOMEM;
+    HIPCHK(hipMemsetAsync(c->v2_pay.p, 0, 8, s));
+    if (ygm_k_launch_v12_fast(v1, v1_off, v1_len, v1_st, slot_off, doc_upd, ust, n_docs, c->v2_out.as<uint8_t>(), c->v2_fo.as<uint64_t>(),
+                              c->v2_olen.as<uint64_t>(), c->v2_ost.as<int32_t>(), claim, c->v2_pay.as<unsigned long long>(), s))
+      return YGM_EDEVICE;
+  }
+  uint64_t total = 0, fast_bytes = 0;
   if (n_docs) {
     if (ygm_k_launch_v12_count(v1, v1_off, v1_len, v1_st, v2a, v2n, upd_off, doc_upd, ust, n_docs, mode, c->flags, c->v2_L.as<uint32_t>(),
-                               c->v2_off.as<uint64_t>(), c->v2_ost.as<int32_t>(), s) ||
+                               c->v2_off.as<uint64_t>(), c->v2_ost.as<int32_t>(), claim, s) ||
         ygm_k_launch_scan(c->v2_off.as<uint64_t>(), n_docs, c->v2_bs.as<uint64_t>(), s))
       return YGM_EDEVICE;
     HIPCHK(hipMemcpyAsync(c->h_meta, c->v2_off.as<uint64_t>() + n_docs, 8, hipMemcpyDeviceToHost, s));
+    if (fast) HIPCHK(hipMemcpyAsync((uint8_t*)c->h_meta + 8, c->v2_pay.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     memcpy(&total, c->h_meta, 8);
+    if (fast) memcpy(&fast_bytes, (uint8_t*)c->h_meta + 8, 8);
   }
-  if (!c->v2_out.ensure(total + 64)) return YGM_ENOMEM;
+  if (!c->v2_out.ensure(slot_total + total + 64, slot_total, s)) return YGM_ENOMEM;
   if (n_docs && ygm_k_launch_v12_write(v1, v1_off, v1_len, v2a, v2n, upd_off, doc_upd, n_docs, mode, c->flags, c->v2_L.as<uint32_t>(),
-                                       c->v2_off.as<uint64_t>(), c->v2_ost.as<int32_t>(), c->v2_out.as<uint8_t>(), c->v2_olen.as<uint64_t>(), s))
+                                       c->v2_off.as<uint64_t>(), c->v2_ost.as<int32_t>(), c->v2_out.as<uint8_t>(), c->v2_olen.as<uint64_t>(),
+                                       claim, slot_total, c->v2_fo.as<uint64_t>(), s))
     return YGM_EDEVICE;
-  out->data = c->v2_out.as<uint8_t>(); out->off = c->v2_off.as<uint64_t>(); out->len = c->v2_olen.as<uint64_t>();
-  out->status = c->v2_ost.as<int32_t>(); out->data_bytes = total; out->payload_bytes = total;
+  out->data = c->v2_out.as<uint8_t>(); out->off = c->v2_fo.as<uint64_t>(); out->len = c->v2_olen.as<uint64_t>();
+  out->status = c->v2_ost.as<int32_t>(); out->data_bytes = slot_total + total; out->payload_bytes = total + fast_bytes;
   return YGM_OK;
 }
 static const uint32_t V2_EXPORT = 1u, V2_STRUCTS_ONLY = 2u;
@@ -596,7 +628,7 @@ int ygm_merge_v2_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
   ygm_device_result r1;
   if ((e = ygm_merge_v1_device(c, c->v2_v1.as<uint8_t>(), v1_bytes, c->v2_len.as<uint64_t>(), d_doc_upd, n_upd, n_docs, s, &r1))) return e;
   T.resume();
-  e = v12_pass(c, s, r1.data, r1.off, r1.len, r1.status, d_arena, arena_bytes, d_upd_off, d_doc_upd, c->v2_st.as<int32_t>(), n_docs, 0, out);
+  e = v12_pass(c, s, r1.data, r1.off, r1.len, r1.status, d_arena, arena_bytes, d_upd_off, d_doc_upd, c->v2_st.as<int32_t>(), n_docs, 0, d_upd_off, out);
   T.done();
   return e;
 }
@@ -613,7 +645,7 @@ int ygm_diff_v2_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes,
   ygm_device_result r1;
   if ((e = ygm_diff_v1_device(c, c->v2_v1.as<uint8_t>(), v1_bytes, c->v2_len.as<uint64_t>(), d_sv_arena, d_sv_off, n_docs, s, &r1))) return e;
   T.resume();
-  e = v12_pass(c, s, r1.data, r1.off, r1.len, r1.status, d_arena, arena_bytes, nullptr, nullptr, c->v2_st.as<int32_t>(), n_docs, 0, out);
+  e = v12_pass(c, s, r1.data, r1.off, r1.len, r1.status, d_arena, arena_bytes, nullptr, nullptr, c->v2_st.as<int32_t>(), n_docs, 0, d_doc_off, out);
   T.done();
   return e;
 }
@@ -641,7 +673,7 @@ int ygm_convert_v1_to_v2_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t are
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   (void)hipSetDevice(c->device);
   V2Timer T(c, s);
-  const int e = v12_pass(c, s, d_arena, d_doc_off, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, n_docs, V2_EXPORT, out);
+  const int e = v12_pass(c, s, d_arena, d_doc_off, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, n_docs, V2_EXPORT, nullptr, out);
   T.done();
   if (!e) { c->stats.calls++; c->stats.docs += n_docs; }
   return e;

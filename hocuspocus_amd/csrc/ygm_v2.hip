@@ -14,6 +14,7 @@
 
 #include "ygm_common.hpp"
 #include "ygm_v2.hpp"
+#include "ygm_v2_fast.hpp"
 
 namespace ygm {
 
@@ -62,9 +63,10 @@ __global__ __launch_bounds__(V2_NT) void k_v12_count(const uint8_t* __restrict__
                                                     const uint8_t* __restrict__ v2a, uint64_t v2n, const uint64_t* __restrict__ upd_off,
                                                     const uint32_t* __restrict__ doc_upd, const int32_t* __restrict__ ust, uint32_t n_docs,
                                                     uint32_t mode, uint32_t flags, uint32_t* __restrict__ L, uint64_t* __restrict__ tot,
-                                                    int32_t* __restrict__ st) {
+                                                    int32_t* __restrict__ st, const uint8_t* __restrict__ claim) {
   const uint32_t d = blockIdx.x * V2_NT + threadIdx.x;
   if (d >= n_docs) return;
+  if (claim && claim[d]) { tot[d] = 0; return; }   // k_v12_fast wrote it (status, offset, length)
   uint32_t* Ld = L + (size_t)d * v2::C_N;
   int s = ST_OK;
   if (doc_upd) {
@@ -95,11 +97,13 @@ __global__ __launch_bounds__(V2_NT) void k_v12_write(const uint8_t* __restrict__
                                                     const uint64_t* __restrict__ upd_off, const uint32_t* __restrict__ doc_upd, uint32_t n_docs,
                                                     uint32_t mode, uint32_t flags, const uint32_t* __restrict__ L,
                                                     const uint64_t* __restrict__ off, int32_t* __restrict__ st, uint8_t* __restrict__ out,
-                                                    uint64_t* __restrict__ out_len) {
+                                                    uint64_t* __restrict__ out_len, const uint8_t* __restrict__ claim, uint64_t base,
+                                                    uint64_t* __restrict__ fo) {
   const uint32_t d = blockIdx.x * V2_NT + threadIdx.x;
-  if (d >= n_docs) return;
+  if (d >= n_docs || (claim && claim[d])) return;
   const uint32_t* Ld = L + (size_t)d * v2::C_N;
-  const uint64_t o0 = off[d], n = off[d + 1] - o0;
+  const uint64_t o0 = base + off[d], n = off[d + 1] - off[d];
+  fo[d] = o0;
   out_len[d] = st[d] == ST_OK ? n : 0u;
   if (st[d] != ST_OK) return;
   if (doc_upd && Ld[0] == 0xFFFFFFFFu) {   // single input: as it is
@@ -111,6 +115,73 @@ __global__ __launch_bounds__(V2_NT) void k_v12_write(const uint8_t* __restrict__
   const int e = v2::v12_write(v1 + v1_off[d], (uint32_t)len, v2a, v2n, mode, flags, Ld, out + o0);
   if (e) { st[d] = ST_DEVICE; out_len[d] = 0; }   // (the count pass took the same path: cannot happen)
 }
+// V1 -> V2 of the documents in the fast encoder's shape (ygm_v2_fast.hpp): one wave per document, the V1
+// bytes staged in LDS by 16-byte loads, the two encoder passes on lane 0 (register state; the V2 bytes
+// assembled in LDS), the result copied out in 16-byte stores to the document's slot (merge_slot of its V2
+// input bytes, as the V1 kernels place outputs: no scan, no cross-document dependency).  claim[d] = 1 for a
+// document done here; the general kernels take the rest (their outputs after the slot region).
+typedef __attribute__((address_space(3))) uint8_t FL8;
+typedef unsigned int fu32x4 __attribute__((ext_vector_type(4)));
+struct alignas(16) V2FLds { uint8_t in[v2f::F_IN + 16 + 64]; uint8_t out[v2f::F_OUT + 64]; };
+YDEV uint64_t v2_slot(uint64_t b0, uint32_t d) { return (2 * b0 + 64ull * d + 15) & ~15ull; }
+__global__ __launch_bounds__(64) void k_v12_fast(const uint8_t* __restrict__ v1, const uint64_t* __restrict__ v1_off,
+                                                 const uint64_t* __restrict__ v1_len, const int32_t* __restrict__ v1_st,
+                                                 const uint64_t* __restrict__ slot_off, const uint32_t* __restrict__ doc_upd,
+                                                 const int32_t* __restrict__ ust, uint32_t n_docs, uint8_t* __restrict__ out,
+                                                 uint64_t* __restrict__ fo, uint64_t* __restrict__ olen, int32_t* __restrict__ ost,
+                                                 uint8_t* __restrict__ claim, unsigned long long* __restrict__ payload) {
+  __shared__ V2FLds S;
+  const uint32_t d = blockIdx.x, l = threadIdx.x;
+  if (d >= n_docs) return;
+  // eligibility: every input transcoded, the V1 operation OK, not a passthrough, staged size
+  bool bad = false;
+  uint64_t b0, nb;
+  if (doc_upd) {
+    const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
+    bad = u1 - u0 < 2u;
+    for (uint32_t u = u0 + l; u < u1 && !bad; u += WAVE) bad = ust[u] != ST_OK;
+    b0 = slot_off[u0]; nb = slot_off[u1] - b0;
+  } else {
+    bad = ust && ust[d] != ST_OK;
+    b0 = slot_off[d]; nb = slot_off[d + 1] - b0;
+  }
+  if (v1_st && v1_st[d] != ST_OK) bad = true;
+  const uint64_t a = v1_off[d], len = v1_len ? v1_len[d] : v1_off[d + 1] - a;
+  if (len > v2f::F_IN || len == 0) bad = true;
+  if (__ballot(bad)) { if (l == 0) claim[d] = 0; return; }
+  // stage: 16-byte loads from the aligned base (the V1 arenas carry >= 16 bytes of readable tail)
+  const uint32_t sh = (uint32_t)(a & 15u), n = sh + (uint32_t)len;
+  const fu32x4* src = (const fu32x4*)(v1 + (a & ~15ull));
+  for (uint32_t c = l; c * 16u < n + 48u; c += WAVE) {
+    fu32x4 v = {0u, 0u, 0u, 0u};
+    if (c * 16u < n) v = src[c];
+    *(fu32x4*)(S.in + 16u * c) = v;
+  }
+  __syncthreads();
+  const uint64_t slot = v2_slot(b0, d), cap = 2 * nb + 48;
+  uint32_t total = 0;
+  if (l == 0) {
+    FL8* in = (FL8*)S.in;
+    FL8* ob = (FL8*)S.out;
+    v2f::FEnc k;
+    bool ok = v2f::f_run<false>(in, sh, n, ob, k);
+    if (ok) {
+      total = v2f::f_total(k);
+      ok = total <= v2f::F_OUT && ((total + 15u) & ~15u) <= cap;
+    }
+    if (ok) { v2f::f_layout(ob, k); ok = v2f::f_run<true>(in, sh, n, ob, k); }
+    if (!ok) total = 0;
+  }
+  total = (uint32_t)__shfl((int)total, 0);
+  __syncthreads();
+  if (total == 0) { if (l == 0) claim[d] = 0; return; }
+  for (uint32_t c = l; c * 16u < total; c += WAVE) *(fu32x4*)(out + slot + 16u * c) = *(const fu32x4*)(S.out + 16u * c);
+  if (l == 0) {
+    fo[d] = slot; olen[d] = total; ost[d] = ST_OK; claim[d] = 1;
+    atomicAdd(payload, (unsigned long long)total);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_v2_status(const int32_t* __restrict__ ust, uint32_t n, int32_t* __restrict__ status,
                                                   uint64_t* __restrict__ len) {
   const uint32_t d = blockIdx.x * 256 + threadIdx.x;
@@ -148,20 +219,29 @@ int ygm_k_launch_v21(int pass, const uint8_t* arena, const uint64_t* upd_off, ui
 }
 int ygm_k_launch_v12_count(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint8_t* v2a,
                            uint64_t v2n, const uint64_t* upd_off, const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint32_t mode,
-                           uint32_t flags, uint32_t* L, uint64_t* tot, int32_t* st, hipStream_t s) {
+                           uint32_t flags, uint32_t* L, uint64_t* tot, int32_t* st, const uint8_t* claim, hipStream_t s) {
   if (n_docs == 0) return 0;
   const uint32_t g = (n_docs + V2_NT - 1) / V2_NT;
   hipLaunchKernelGGL(k_v12_count, dim3(g), dim3(V2_NT), 0, s, v1, v1_off, v1_len, v1_st, v2a, v2n, upd_off, doc_upd, ust, n_docs, mode, flags,
-                     L, tot, st);
+                     L, tot, st, claim);
+  return v2_rc(__func__);
+}
+int ygm_k_launch_v12_fast(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint64_t* slot_off,
+                          const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint8_t* out, uint64_t* fo, uint64_t* olen, int32_t* ost,
+                          uint8_t* claim, unsigned long long* payload, hipStream_t s) {
+  if (n_docs == 0) return 0;
+  hipLaunchKernelGGL(k_v12_fast, dim3(n_docs), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd, ust, n_docs, out, fo, olen, ost,
+                     claim, payload);
   return v2_rc(__func__);
 }
 int ygm_k_launch_v12_write(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const uint8_t* v2a, uint64_t v2n,
                            const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t mode, uint32_t flags, const uint32_t* L,
-                           const uint64_t* off, int32_t* st, uint8_t* out, uint64_t* out_len, hipStream_t s) {
+                           const uint64_t* off, int32_t* st, uint8_t* out, uint64_t* out_len, const uint8_t* claim, uint64_t base, uint64_t* fo,
+                           hipStream_t s) {
   if (n_docs == 0) return 0;
   const uint32_t g = (n_docs + V2_NT - 1) / V2_NT;
   hipLaunchKernelGGL(k_v12_write, dim3(g), dim3(V2_NT), 0, s, v1, v1_off, v1_len, v2a, v2n, upd_off, doc_upd, n_docs, mode, flags, L, off, st,
-                     out, out_len);
+                     out, out_len, claim, base, fo);
   return v2_rc(__func__);
 }
 int ygm_k_launch_v2_status(const int32_t* ust, uint32_t n, int32_t* status, uint64_t* len, hipStream_t s) {

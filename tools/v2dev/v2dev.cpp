@@ -29,3 +29,24 @@ int hv_v12(const uint8_t* v1, uint32_t n, const uint8_t* v2a, uint64_t v2n, uint
   return v2::v12_write(v1, n, v2a, v2n, mode, flags, L, out);
 }
 }
+
+#include "../../hocuspocus_amd/csrc/ygm_v2_fast.hpp"
+extern "C" {
+// the register-resident fast V1 -> V2 encoder (ygm_v2_fast.hpp) over a staged copy of v1 (zero slack past n):
+// 0 = done (out gets the V2 bytes), 1 = off the fast path, 2 = past the fast path's sizes
+int hv_v12f(const uint8_t* v1, uint32_t n, uint8_t* out, uint64_t* out_len) {
+  *out_len = 0;
+  if (n > v2f::F_IN) return 2;
+  static uint8_t in[v2f::F_IN + 64], ob[v2f::F_OUT + 64];
+  memset(in, 0, sizeof in); memcpy(in, v1, n);
+  v2f::FEnc k;
+  if (!v2f::f_run<false>((const uint8_t*)in, 0u, n, ob, k)) return 1;
+  const uint32_t t = v2f::f_total(k);
+  if (t > v2f::F_OUT) return 2;
+  v2f::f_layout(ob, k);
+  if (!v2f::f_run<true>((const uint8_t*)in, 0u, n, ob, k)) return 3;   // (cannot happen: the count pass took the same path)
+  memcpy(out, ob, t);
+  *out_len = t;
+  return 0;
+}
+}

@@ -217,6 +217,10 @@ __global__ __launch_bounds__(WAVE) void k_sv_table(const uint8_t* __restrict__ s
   tbl_n[d] = n;
 }
 
+#ifndef YGM_DW_SPEC
+#define YGM_DW_SPEC 0   // 1: fast decoder reads both candidate content-length bytes beside the info byte (A/B: slower,
+                        // profiles/r03_walk/README.md -- the walker is issue-bound, not LDS-latency-bound)
+#endif
 #ifndef YGM_DW_WPE0
 #define YGM_DW_WPE0 2   // waves per SIMD the SV walker is compiled for (register budget 512 / waves)
 #endif
@@ -557,12 +561,24 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
 #pragma unroll
           for (int u = 0; u < DW_U; u++) {
             const uint32_t wq = (uint32_t)(w64 >> qo);
+            const uint32_t tt = wq >> 1, x2 = tt & (tt - 1u), x3 = x2 & (x2 - 1u), x4 = x3 & (x3 - 1u);
+#if YGM_DW_SPEC
+            // the content length's position for one and for two origin ids comes from the mask alone: both
+            // candidate bytes are read beside the info byte (one LDS round trip per Item, not two)
+            const uint32_t c2 = (uint32_t)__builtin_ctz(x2 | 0x80000000u) + 2u, c4 = (uint32_t)__builtin_ctz(x4 | 0x80000000u) + 2u;
+            const uint32_t lv2 = dw_byte(L, l, q + (c2 & 31u)), lv4 = dw_byte(L, l, q + (c4 & 31u));
             if (u >= 1) bb = dw_byte(L, l, q);
             const uint32_t hoh = bb >> 6, ref = bb & 0x3Fu;
-            const uint32_t tt = wq >> 1, x2 = tt & (tt - 1u), x3 = x2 & (x2 - 1u), x4 = x3 & (x3 - 1u);
+            const uint32_t cpos = hoh == 3u ? c4 : c2;   // after the origins
+            const uint32_t cq = cpos & 31u;
+            const uint32_t lv = hoh == 3u ? lv4 : lv2;
+#else
+            if (u >= 1) bb = dw_byte(L, l, q);
+            const uint32_t hoh = bb >> 6, ref = bb & 0x3Fu;
             const uint32_t cpos = (uint32_t)__builtin_ctz((hoh == 3u ? x4 : x2) | 0x80000000u) + 2u;   // after the origins
             const uint32_t cq = cpos & 31u;
             const uint32_t lv = dw_byte(L, l, q + cq);
+#endif
             const uint32_t isS = ref == 4u ? 1u : 0u;
             const uint32_t end = cq + 1u + (isS ? lv : 0u);
             const uint32_t mk = isS ? (((1u << (lv & 31u)) - 1u) << ((cq + 1u) & 31u)) : 0u;   // the string's bytes: ASCII

@@ -115,70 +115,97 @@ __global__ __launch_bounds__(V2_NT) void k_v12_write(const uint8_t* __restrict__
   const int e = v2::v12_write(v1 + v1_off[d], (uint32_t)len, v2a, v2n, mode, flags, Ld, out + o0);
   if (e) { st[d] = ST_DEVICE; out_len[d] = 0; }   // (the count pass took the same path: cannot happen)
 }
-// V1 -> V2 of the documents in the fast encoder's shape (ygm_v2_fast.hpp): one wave per document, the V1
-// bytes staged in LDS by 16-byte loads, the two encoder passes on lane 0 (register state; the V2 bytes
-// assembled in LDS), the result copied out in 16-byte stores to the document's slot (merge_slot of its V2
-// input bytes, as the V1 kernels place outputs: no scan, no cross-document dependency).  claim[d] = 1 for a
-// document done here; the general kernels take the rest (their outputs after the slot region).
+// V1 -> V2 of the documents in the fast encoder's shape (ygm_v2_fast.hpp): D documents per wave, each one's V1
+// bytes staged in LDS by 16-byte loads with its terminator masks; lane j runs document j's two encoder passes
+// (register state; the count pass sizes the columns, the write pass stores the V2 bytes straight into the
+// document's slot -- merge_slot of its V2 input bytes, as the V1 kernels place outputs: no scan, no
+// cross-document dependency).  The encoder is one serial chain per document, so the documents in flight are
+// what counts: D documents share one instruction stream, and a small staging cap (FIN) leaves room for more
+// waves per CU; a second launch (D = 1, FIN = F_IN) takes the larger documents.  claim[d] = 1 for a document
+// done here; the general kernels take the rest (their outputs after the slot region).
 typedef __attribute__((address_space(3))) uint8_t FL8;
+typedef __attribute__((address_space(3))) uint64_t FL64;
 typedef unsigned int fu32x4 __attribute__((ext_vector_type(4)));
-struct alignas(16) V2FLds { uint8_t in[v2f::F_IN + 16 + 64]; uint8_t out[v2f::F_OUT + 64]; };
+template <int FIN>
+struct alignas(16) V2FDoc {
+  static constexpr uint32_t INB = FIN + 128;   // the 0..15 byte shift, the update, 64+ bytes of zeros
+  uint8_t in[INB];
+  uint64_t m[INB / 64 + 2];
+};
 YDEV uint64_t v2_slot(uint64_t b0, uint32_t d) { return (2 * b0 + 64ull * d + 15) & ~15ull; }
+template <int D, int FIN>
 __global__ __launch_bounds__(64) void k_v12_fast(const uint8_t* __restrict__ v1, const uint64_t* __restrict__ v1_off,
                                                  const uint64_t* __restrict__ v1_len, const int32_t* __restrict__ v1_st,
                                                  const uint64_t* __restrict__ slot_off, const uint32_t* __restrict__ doc_upd,
                                                  const int32_t* __restrict__ ust, uint32_t n_docs, uint8_t* __restrict__ out,
                                                  uint64_t* __restrict__ fo, uint64_t* __restrict__ olen, int32_t* __restrict__ ost,
-                                                 uint8_t* __restrict__ claim, unsigned long long* __restrict__ payload) {
-  __shared__ V2FLds S;
-  const uint32_t d = blockIdx.x, l = threadIdx.x;
-  if (d >= n_docs) return;
-  // eligibility: every input transcoded, the V1 operation OK, not a passthrough, staged size
-  bool bad = false;
-  uint64_t b0, nb;
-  if (doc_upd) {
-    const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
-    bad = u1 - u0 < 2u;
-    for (uint32_t u = u0 + l; u < u1 && !bad; u += WAVE) bad = ust[u] != ST_OK;
-    b0 = slot_off[u0]; nb = slot_off[u1] - b0;
-  } else {
-    bad = ust && ust[d] != ST_OK;
-    b0 = slot_off[d]; nb = slot_off[d + 1] - b0;
-  }
-  if (v1_st && v1_st[d] != ST_OK) bad = true;
-  const uint64_t a = v1_off[d], len = v1_len ? v1_len[d] : v1_off[d + 1] - a;
-  if (len > v2f::F_IN || len == 0) bad = true;
-  if (__ballot(bad)) { if (l == 0) claim[d] = 0; return; }
-  // stage: 16-byte loads from the aligned base (the V1 arenas carry >= 16 bytes of readable tail)
-  const uint32_t sh = (uint32_t)(a & 15u), n = sh + (uint32_t)len;
-  const fu32x4* src = (const fu32x4*)(v1 + (a & ~15ull));
-  for (uint32_t c = l; c * 16u < n + 48u; c += WAVE) {
-    fu32x4 v = {0u, 0u, 0u, 0u};
-    if (c * 16u < n) v = src[c];
-    *(fu32x4*)(S.in + 16u * c) = v;
-  }
-  __syncthreads();
-  const uint64_t slot = v2_slot(b0, d), cap = 2 * nb + 48;
-  uint32_t total = 0;
-  if (l == 0) {
-    FL8* in = (FL8*)S.in;
-    FL8* ob = (FL8*)S.out;
-    v2f::FEnc k;
-    bool ok = v2f::f_run<false>(in, sh, n, ob, k);
-    if (ok) {
-      total = v2f::f_total(k);
-      ok = total <= v2f::F_OUT && ((total + 15u) & ~15u) <= cap;
+                                                 uint8_t* __restrict__ claim, unsigned long long* __restrict__ payload, int second) {
+  typedef V2FDoc<FIN> Doc;
+  __shared__ Doc S[D];
+  const uint32_t l = threadIdx.x;
+  uint32_t mine_sh = 0, mine_n = 0;   // lane j < D: document j's staged shift and end
+  bool mine_ok = false;
+  uint64_t mine_slot = 0, mine_cap = 0;
+  for (int j = 0; j < D; j++) {
+    const uint32_t d = blockIdx.x * D + (uint32_t)j;
+    if (d >= n_docs) break;
+    // eligibility: every input transcoded, the V1 operation OK, not a passthrough, staged size (second launch:
+    // only what the first one left)
+    bool bad = second && claim[d];
+    uint64_t b0 = 0, nb = 0;
+    if (!bad) {
+      if (doc_upd) {
+        const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
+        bad = u1 - u0 < 2u;
+        for (uint32_t u = u0 + l; u < u1 && !bad; u += WAVE) bad = ust[u] != ST_OK;
+        b0 = slot_off[u0]; nb = slot_off[u1] - b0;
+      } else {
+        bad = ust && ust[d] != ST_OK;
+        b0 = slot_off[d]; nb = slot_off[d + 1] - b0;
+      }
     }
-    if (ok) { v2f::f_layout(ob, k); ok = v2f::f_run<true>(in, sh, n, ob, k); }
-    if (!ok) total = 0;
+    if (v1_st && v1_st[d] != ST_OK) bad = true;
+    const uint64_t a = v1_off[d], len = v1_len ? v1_len[d] : v1_off[d + 1] - a;
+    if (len > (uint64_t)FIN || len == 0) bad = true;
+    if (__ballot(bad)) { if (l == 0 && !(second && claim[d])) claim[d] = 0; continue; }
+    // stage: 16-byte loads from the aligned base (the V1 arenas carry >= 16 bytes of readable tail)
+    const uint32_t sh = (uint32_t)(a & 15u), n = sh + (uint32_t)len;
+    const fu32x4* src = (const fu32x4*)(v1 + (a & ~15ull));
+    const uint32_t nw = (n + 63u) / 64u + 1u;   // mask words read: up to the one past the update's last byte
+    for (uint32_t c = l; c < 4u * nw; c += WAVE) {
+      fu32x4 v = {0u, 0u, 0u, 0u};
+      if (c * 16u < n) v = src[c];
+      *(fu32x4*)(S[j].in + 16u * c) = v;
+    }
+    if (l == (uint32_t)j) { mine_ok = true; mine_sh = sh; mine_n = n; mine_slot = v2_slot(b0, d); mine_cap = 2 * nb + 48; }
   }
-  total = (uint32_t)__shfl((int)total, 0);
   __syncthreads();
-  if (total == 0) { if (l == 0) claim[d] = 0; return; }
-  for (uint32_t c = l; c * 16u < total; c += WAVE) *(fu32x4*)(out + slot + 16u * c) = *(const fu32x4*)(S.out + 16u * c);
-  if (l == 0) {
-    fo[d] = slot; olen[d] = total; ost[d] = ST_OK; claim[d] = 1;
-    atomicAdd(payload, (unsigned long long)total);
+  for (int j = 0; j < D; j++) {
+    const uint32_t nw = (uint32_t)__shfl((int)mine_n, j) ? ((uint32_t)__shfl((int)mine_n, j) + 63u) / 64u + 1u : 0u;
+    for (uint32_t k = l; k <= nw && nw; k += WAVE) S[j].m[k] = v2f::f_mask_word((FL8*)S[j].in, k);
+  }
+  __syncthreads();
+  if (l < (uint32_t)D && mine_ok) {
+    const uint32_t d = blockIdx.x * D + l;
+    const v2f::FSrc<FL8*, FL64*> src{(FL8*)S[l].in, (FL64*)S[l].m};
+    v2f::FEnc k;
+    bool ok = true;
+    uint32_t total = 0;
+    // both passes through ONE inlined copy of the encoder (a null output counts): half the code, which the
+    // instruction cache holds
+    for (int pass = 0; pass < 2 && ok; pass++) {
+      uint8_t* o = pass ? out + mine_slot : nullptr;
+      if (pass) v2f::f_layout(o, k);
+      ok = v2f::f_run<true>(src, mine_sh, mine_n, o, k);
+      if (ok && !pass) {
+        total = v2f::f_total(k);
+        ok = total <= v2f::F_OUT && ((total + 15u) & ~15u) <= mine_cap;
+      }
+    }
+    if (ok) {
+      fo[d] = mine_slot; olen[d] = total; ost[d] = ST_OK; claim[d] = 1;
+      atomicAdd(payload, (unsigned long long)total);
+    } else if (!second) claim[d] = 0;
   }
 }
 
@@ -230,8 +257,11 @@ int ygm_k_launch_v12_fast(const uint8_t* v1, const uint64_t* v1_off, const uint6
                           const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint8_t* out, uint64_t* fo, uint64_t* olen, int32_t* ost,
                           uint8_t* claim, unsigned long long* payload, hipStream_t s) {
   if (n_docs == 0) return 0;
-  hipLaunchKernelGGL(k_v12_fast, dim3(n_docs), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd, ust, n_docs, out, fo, olen, ost,
-                     claim, payload);
+  constexpr int D = 4, FS = 3584;   // small tier: four documents of <= 3.5 KB per wave (17 KB of LDS)
+  hipLaunchKernelGGL((k_v12_fast<D, FS>), dim3((n_docs + D - 1) / D), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd, ust,
+                     n_docs, out, fo, olen, ost, claim, payload, 0);
+  hipLaunchKernelGGL((k_v12_fast<1, (int)v2f::F_IN>), dim3(n_docs), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd, ust,
+                     n_docs, out, fo, olen, ost, claim, payload, 1);
   return v2_rc(__func__);
 }
 int ygm_k_launch_v12_write(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const uint8_t* v2a, uint64_t v2n,

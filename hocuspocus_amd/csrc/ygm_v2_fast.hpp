@@ -54,44 +54,6 @@ YDEV uint32_t f_align(uint32_t hi, uint32_t lo, uint32_t s) {   // bytes s.. of 
 #endif
 }
 
-// a 40-byte window of the staged input at byte wp
-struct FWin { uint32_t d[10]; uint64_t T; uint32_t wp; };
-template <class P>
-YDEV void f_fill(P in, uint32_t p, FWin& w) {
-  const uint32_t a = p >> 2, s = p & 3u;
-  uint32_t L[11];
-#pragma unroll
-  for (int j = 0; j < 11; j++) L[j] = f_ld32(in, a + (uint32_t)j);
-#pragma unroll
-  for (int j = 0; j < 10; j++) w.d[j] = f_align(L[j + 1], L[j], s);
-  uint64_t H = 0;
-#pragma unroll
-  for (int j = 0; j < 5; j++) {
-    const uint32_t lo = w.d[2 * j], hi = w.d[2 * j + 1];
-    uint32_t b = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) b |= ((lo >> (8 * k + 7)) & 1u) << k;
-#pragma unroll
-    for (int k = 0; k < 4; k++) b |= ((hi >> (8 * k + 7)) & 1u) << (k + 4);
-    H |= (uint64_t)b << (8 * j);
-  }
-  w.T = ~H & ((1ull << 40) - 1ull);
-  w.wp = p;
-}
-YDEV uint32_t f_dsel(const FWin& w, uint32_t i) {   // w.d[i], i < 10, by selects (no indexed registers)
-  uint32_t r = w.d[0];
-#pragma unroll
-  for (int j = 1; j < 10; j++) r = i == (uint32_t)j ? w.d[j] : r;
-  return r;
-}
-// 5 bytes at window offset o (o <= 32): first 4 in x, the 5th in y
-YDEV void f_at5(const FWin& w, uint32_t o, uint32_t& x, uint32_t& y) {
-  const uint32_t i = o >> 2, s = o & 3u;
-  const uint32_t a = f_dsel(w, i), b = f_dsel(w, i + 1u), c = f_dsel(w, i + 2u);
-  x = f_align(b, a, s);
-  y = f_align(c, b, s) & 0xFFu;
-}
-
 // value of the <= 5-byte varuint whose first 4 bytes are x and 5th byte is y (n bytes)
 YDEV uint32_t f_pext(uint32_t x, uint32_t y, uint32_t n) {
   x &= n >= 4u ? 0xFFFFFFFFu : ((1u << (8u * n)) - 1u);
@@ -101,39 +63,59 @@ YDEV uint32_t f_pext(uint32_t x, uint32_t y, uint32_t n) {
   return x | (n >= 5u ? (y & 0x7Fu) << 28 : 0u);
 }
 
-// the reader: position p in the staged input of n bytes, window w; ok cleared on anything off the fast path
+// The staged input: bytes (4-byte aligned buffer, readable 64 bytes past the update) and its terminator masks
+// (word k, bit i: byte 64 k + i has its top bit clear), built once per document by the whole wave.
+template <class P, class M>
+struct FSrc {
+  P in; M m;
+  YDEV uint32_t w32(uint32_t i) const { return f_ld32(in, i); }
+  YDEV uint32_t byte(uint32_t p) const { return (w32(p >> 2) >> (8u * (p & 3u))) & 0xFFu; }
+  YDEV uint64_t mask(uint32_t p) const {   // bit i: byte p + i ends a varuint
+    const uint32_t k = p >> 6, s = p & 63u;
+    const uint64_t lo = m[k], hi = m[k + 1u];
+    return s ? (lo >> s) | (hi << (64u - s)) : lo;
+  }
+  YDEV void at5(uint32_t p, uint32_t& x, uint32_t& y) const {   // bytes p .. p + 4
+    const uint32_t a = p >> 2, s = p & 3u;
+    const uint32_t w0 = w32(a), w1 = w32(a + 1u);
+    x = f_align(w1, w0, s);
+    y = (w1 >> (8u * s)) & 0xFFu;
+  }
+};
+
+// the reader: position p in the staged input (the update is [p0, n)); ok cleared on anything off the fast path
 struct FRd {
   uint32_t p, n;
   bool ok;
 };
-// next varuint (< 2^32): refills the window when it may reach past it
-template <class P>
-YDEV uint32_t f_vu(P in, FRd& r, FWin& w) {
-  if (r.p + 5u > w.wp + 40u || r.p < w.wp) f_fill(in, r.p, w);
-  const uint32_t o = r.p - w.wp;
-  const uint64_t t = w.T >> o;
-  const uint32_t e = t ? (uint32_t)__builtin_ctzll(t) : 64u;   // terminator offset from o
+// the varuint at q ending at byte e (both absolute, e >= q): its value; ok cleared past 5 bytes / 2^32 / n
+template <class S>
+YDEV uint32_t f_vat(const S& src, FRd& r, uint32_t q, uint32_t e) {
   uint32_t x, y;
-  f_at5(w, o, x, y);
-  const uint32_t nb = e + 1u;
-  r.ok = r.ok && nb <= 5u && !(nb == 5u && (y & 0x70u)) && r.p + nb <= r.n;
-  r.p += nb;
+  src.at5(q, x, y);
+  const uint32_t nb = e - q + 1u;
+  r.ok = r.ok && nb <= 5u && !(nb == 5u && (y & 0x70u)) && e < r.n;
   return f_pext(x, y, nb > 5u ? 5u : nb);
 }
-template <class P>
-YDEV uint32_t f_u8(P in, FRd& r, FWin& w) {
-  if (r.p + 1u > w.wp + 40u || r.p < w.wp) f_fill(in, r.p, w);
-  uint32_t x, y;
-  f_at5(w, r.p - w.wp, x, y);
+// next varuint (< 2^32): its mask and bytes are read together (one LDS round trip)
+template <class S>
+YDEV uint32_t f_vu(const S& src, FRd& r) {
+  const uint64_t t = src.mask(r.p);
+  const uint32_t e = r.p + (t ? (uint32_t)__builtin_ctzll(t) : 64u);
+  const uint32_t v = f_vat(src, r, r.p, e);
+  r.p = e + 1u;
+  return v;
+}
+template <class S>
+YDEV uint32_t f_u8(const S& src, FRd& r) {
   r.ok = r.ok && r.p < r.n;
-  r.p++;
-  return x & 0xFFu;
+  return src.byte(r.p++);
 }
 
 // ---- column writers (W: store; always count)
 template <bool W, class Q>
 YDEV void f_b(Q out, FCol& c, uint32_t v) {
-  if (W) out[c.base + c.n] = (uint8_t)v;
+  if (W && out) out[c.base + c.n] = (uint8_t)v;   // (out == nullptr: a count pass through the same code)
   c.n++;
 }
 template <bool W, class Q>
@@ -177,93 +159,141 @@ YDEV void f_id(Q out, FCol& c, FId& e, int64_t v) {
   f_id_flush<W>(out, c, e);
   e.count = 1; e.diff = v - e.s; e.s = v;
 }
-// a varString of the input (ASCII only): bytes to the string column, its length to lens
-template <bool W, class P, class Q>
-YDEV void f_str(P in, Q out, FRd& r, FWin& w, FEnc& k) {
-  const uint32_t len = f_vu(in, r, w);
-  const uint32_t s = r.p;
-  r.ok = r.ok && len <= r.n - (s < r.n ? s : r.n);
-  if (!r.ok) return;
-  // ASCII: every byte < 0x80, checked a dword at a time (the staged buffer is zero past the document)
-  uint32_t hi = 0;
-  for (uint32_t i = s & ~3u; i < s + len; i += 4u) {
-    uint32_t v = f_ld32(in, i >> 2);
-    if (i < s) v &= 0xFFFFFFFFu << (8u * (s - i));
-    if (i + 4u > s + len) v &= 0xFFFFFFFFu >> (8u * (i + 4u - s - len));
-    hi |= v & 0x80808080u;
+// ASCII check of the input bytes [s, s + len) from the terminator masks (ASCII <=> top bit clear)
+template <class S>
+YDEV bool f_ascii(const S& src, uint32_t s, uint32_t len) {
+  for (uint32_t i = 0; i < len; i += 64u) {
+    const uint32_t k = len - i < 64u ? len - i : 64u;
+    const uint64_t want = k >= 64u ? ~0ull : ((1ull << k) - 1ull);
+    if ((src.mask(s + i) & want) != want) return false;
   }
-  r.ok = r.ok && hi == 0u;
-  if (W && r.ok)
-    for (uint32_t i = 0; i < len; i++) out[k.str.base + k.str.n + i] = in[s + i];
+  return true;
+}
+// the string bytes [s, s + len) (ASCII, checked) to the string column, its length to lens
+template <bool W, class S, class Q>
+YDEV void f_put_str(const S& src, Q out, FEnc& k, uint32_t s, uint32_t len) {
+  if (W && out)
+    for (uint32_t i = 0; i < len; i++) out[k.str.base + k.str.n + i] = (uint8_t)src.byte(s + i);
   k.str.n += len;
   f_uo<W>(out, k.lens, k.ulens, len);
+}
+// a varString at the reader (ASCII only)
+template <bool W, class S, class Q>
+YDEV void f_str(const S& src, Q out, FRd& r, FEnc& k) {
+  const uint32_t len = f_vu(src, r);
+  const uint32_t s = r.p;
+  r.ok = r.ok && len <= r.n - (s < r.n ? s : r.n) && f_ascii(src, s, len);
+  if (!r.ok) return;
+  f_put_str<W>(src, out, k, s, len);
   r.p = s + len;
 }
 
-// One pass over the V1 update in[0, n).  Returns false off the fast path (the caller takes v12_body).
-template <bool W, class P, class Q>
-YDEV bool f_run(P in, uint32_t p0, uint32_t n, Q out, FEnc& k) {   // the update is in[p0, n)
+// One pass over the V1 update [p0, n) of the staged input.  Returns false off the fast path (the caller takes
+// v12_body).  An Item with origin(s) is decoded from ONE terminator-mask window read beside its info byte: the
+// ends of its origin varuints and of its content length are the next set bits, so every field value is read in
+// one more round trip (no byte-serial walk).
+template <bool W, class S, class Q>
+YDEV bool f_run(const S& src, uint32_t p0, uint32_t n, Q out, FEnc& k) {
   FRd r{p0, n, true};
-  FWin w;
-  f_fill(in, p0, w);
   k.ucl = FUo{0, 0}; k.uln = FUo{0, 0}; k.ulens = FUo{0, 0};
   k.ilc = FId{0, 0, 0}; k.irc = FId{0, 0, 0};
   k.rinfo = FRle{0, -1}; k.rpi = FRle{0, -1};
   k.cl.n = k.lc.n = k.rc.n = k.info.n = k.str.n = k.lens.n = k.pi.n = k.ln.n = k.rest.n = 0;
-  const uint32_t nb = f_vu(in, r, w);
+  const uint32_t nb = f_vu(src, r);
   f_vuw<W>(out, k.rest, nb);
   uint32_t prev = 0; bool have_prev = false;
   for (uint32_t b = 0; b < nb && r.ok; b++) {
-    const uint32_t ns = f_vu(in, r, w), client = f_vu(in, r, w), clock = f_vu(in, r, w);
+    const uint32_t ns = f_vu(src, r), client = f_vu(src, r), clock = f_vu(src, r);
     r.ok = r.ok && ns != 0u && !(have_prev && client == prev);   // lazy-writer normal (else ENONCANON: v12_body decides)
     prev = client; have_prev = true;
     if (!r.ok) break;
     f_uo<W>(out, k.cl, k.ucl, client); f_vuw<W>(out, k.rest, ns); f_vuw<W>(out, k.rest, clock);
-    for (uint32_t s = 0; s < ns && r.ok; s++) {
-      const uint32_t info = f_u8(in, r, w);
+    for (uint32_t st = 0; st < ns && r.ok; st++) {
+      const uint32_t p = r.p;
+      r.ok = r.ok && p < r.n;
+      const uint32_t info = src.byte(p);
+      const uint64_t m = src.mask(p + 1u);          // (independent of the info byte: read together)
       const uint32_t ref = info & 31u;
+      const bool ho = (info & 0x80u) != 0u, hr = (info & 0x40u) != 0u;
+      if ((ho || hr) && (ref == 1u || ref == 4u) && !(info & 0x20u)) {
+        // origin ids (2 or 4 varuints) and the content length: the next 3 or 5 terminators after the info byte
+        uint64_t t = m;
+        uint32_t e[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) { e[j] = t ? (uint32_t)__builtin_ctzll(t) : 64u; t &= t - 1ull; }
+        const uint32_t nv = (ho && hr) ? 5u : 3u;
+        const uint32_t el = nv == 5u ? e[4] : e[2];   // the content length's terminator
+        if (el < 64u) {
+          const uint32_t q = p + 1u;
+          const uint32_t v0 = f_vat(src, r, q, q + e[0]), v1 = f_vat(src, r, q + e[0] + 1u, q + e[1]);
+          const uint32_t v2 = f_vat(src, r, q + e[1] + 1u, q + e[2]);
+          uint32_t v3 = 0, v4 = 0;
+          if (nv == 5u) { v3 = f_vat(src, r, q + e[2] + 1u, q + e[3]); v4 = f_vat(src, r, q + e[3] + 1u, q + e[4]); }
+          const uint32_t len = nv == 5u ? v4 : v2;
+          const uint32_t cs = q + el + 1u;               // after the content length
+          uint32_t next = cs;
+          if (ref == 4u) {
+            next = cs + len;
+            r.ok = r.ok && len <= r.n - (cs < r.n ? cs : r.n) &&
+                   (el + 1u + len < 64u ? ((~m >> (el + 1u)) & (len >= 64u ? ~0ull : ((1ull << len) - 1ull))) == 0ull
+                                         : f_ascii(src, cs, len));
+          }
+          if (!r.ok) break;
+          f_rle<W>(out, k.info, k.rinfo, (int32_t)(ref | (ho ? 0x80u : 0u) | (hr ? 0x40u : 0u)));
+          if (ho) { f_uo<W>(out, k.cl, k.ucl, v0); f_id<W>(out, k.lc, k.ilc, (int64_t)v1); }
+          if (hr) {
+            f_uo<W>(out, k.cl, k.ucl, ho ? v2 : v0); f_id<W>(out, k.rc, k.irc, (int64_t)(ho ? v3 : v1));
+          }
+          if (ref == 1u) f_uo<W>(out, k.ln, k.uln, len);   // ContentDeleted
+          else f_put_str<W>(src, out, k, cs, len);         // ContentString
+          r.p = next;
+          continue;
+        }
+      }
+      // everything else, field by field
+      r.p = p + 1u;
       if (info == 10u) {   // Skip (read_struct's order: info 10 exactly, then any info with ref 0 is a GC)
         f_rle<W>(out, k.info, k.rinfo, 10);
-        f_vuw<W>(out, k.rest, f_vu(in, r, w));
+        f_vuw<W>(out, k.rest, f_vu(src, r));
         continue;
       }
       if (ref == 0u) {   // GC
         f_rle<W>(out, k.info, k.rinfo, 0);
-        f_uo<W>(out, k.ln, k.uln, f_vu(in, r, w));
+        f_uo<W>(out, k.ln, k.uln, f_vu(src, r));
         continue;
       }
       r.ok = r.ok && (ref == 1u || ref == 4u);
       if (!r.ok) break;
-      const bool ho = (info & 0x80u) != 0u, hr = (info & 0x40u) != 0u, hs = !ho && !hr && (info & 0x20u);
+      const bool hs = !ho && !hr && (info & 0x20u);
       f_rle<W>(out, k.info, k.rinfo, (int32_t)(ref | (ho ? 0x80u : 0u) | (hr ? 0x40u : 0u) | (hs ? 0x20u : 0u)));
-      if (ho) { const uint32_t oc = f_vu(in, r, w), ok = f_vu(in, r, w); f_uo<W>(out, k.cl, k.ucl, oc); f_id<W>(out, k.lc, k.ilc, (int64_t)ok); }
-      if (hr) { const uint32_t rc = f_vu(in, r, w), rk = f_vu(in, r, w); f_uo<W>(out, k.cl, k.ucl, rc); f_id<W>(out, k.rc, k.irc, (int64_t)rk); }
+      if (ho) { const uint32_t oc = f_vu(src, r), ok = f_vu(src, r); f_uo<W>(out, k.cl, k.ucl, oc); f_id<W>(out, k.lc, k.ilc, (int64_t)ok); }
+      if (hr) { const uint32_t rc = f_vu(src, r), rk = f_vu(src, r); f_uo<W>(out, k.cl, k.ucl, rc); f_id<W>(out, k.rc, k.irc, (int64_t)rk); }
       if (!ho && !hr) {
-        const uint32_t pi = f_vu(in, r, w);
+        const uint32_t pi = f_vu(src, r);
         r.ok = r.ok && pi <= 1u;
         if (!r.ok) break;
-        if (pi == 1u) { f_rle<W>(out, k.pi, k.rpi, 1); f_str<W>(in, out, r, w, k); }
+        if (pi == 1u) { f_rle<W>(out, k.pi, k.rpi, 1); f_str<W>(src, out, r, k); }
         else {
           f_rle<W>(out, k.pi, k.rpi, 0);
-          const uint32_t pc = f_vu(in, r, w), pk = f_vu(in, r, w);
+          const uint32_t pc = f_vu(src, r), pk = f_vu(src, r);
           f_uo<W>(out, k.cl, k.ucl, pc); f_id<W>(out, k.lc, k.ilc, (int64_t)pk);
         }
-        if (hs) f_str<W>(in, out, r, w, k);
+        if (hs) f_str<W>(src, out, r, k);
       }
-      if (ref == 1u) f_uo<W>(out, k.ln, k.uln, f_vu(in, r, w));   // ContentDeleted
-      else f_str<W>(in, out, r, w, k);                            // ContentString
+      if (ref == 1u) f_uo<W>(out, k.ln, k.uln, f_vu(src, r));   // ContentDeleted
+      else f_str<W>(src, out, r, k);                            // ContentString
     }
   }
   if (!r.ok) return false;
   // delete set: V1 (clock, len) -> V2 (clock - previous end, len - 1)
-  const uint32_t nd = f_vu(in, r, w);
+  const uint32_t nd = f_vu(src, r);
   f_vuw<W>(out, k.rest, nd);
   for (uint32_t i = 0; i < nd && r.ok; i++) {
-    const uint32_t client = f_vu(in, r, w), nr = f_vu(in, r, w);
+    const uint32_t client = f_vu(src, r), nr = f_vu(src, r);
     f_vuw<W>(out, k.rest, client); f_vuw<W>(out, k.rest, nr);
     uint64_t cur = 0;
     for (uint32_t q = 0; q < nr && r.ok; q++) {
-      const uint32_t clock = f_vu(in, r, w), len = f_vu(in, r, w);
+      const uint32_t clock = f_vu(src, r), len = f_vu(src, r);
       r.ok = r.ok && (uint64_t)clock >= cur && len != 0u;   // (a backward clock / zero length: v12_body's rules)
       if (!r.ok) break;
       f_vuw<W>(out, k.rest, (uint32_t)(clock - cur)); f_vuw<W>(out, k.rest, len - 1u);
@@ -274,6 +304,19 @@ YDEV bool f_run(P in, uint32_t p0, uint32_t n, Q out, FEnc& k) {   // the update
   f_uo_flush<W>(out, k.cl, k.ucl); f_id_flush<W>(out, k.lc, k.ilc); f_id_flush<W>(out, k.rc, k.irc);
   f_uo_flush<W>(out, k.lens, k.ulens); f_uo_flush<W>(out, k.ln, k.uln);
   return true;
+}
+
+// terminator masks of the staged bytes [0, nbytes) (nbytes a multiple of 64): word k for bytes 64 k ..
+template <class P>
+YDEV uint64_t f_mask_word(P in, uint32_t k) {
+  uint64_t H = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const uint32_t v = f_ld32(in, 16u * k + (uint32_t)j);
+#pragma unroll
+    for (int b = 0; b < 4; b++) H |= (uint64_t)((v >> (8 * b + 7)) & 1u) << (4 * j + b);
+  }
+  return ~H;
 }
 
 YDEV uint32_t f_vlen(uint32_t v) { return 1u + (v > 0x7Fu) + (v > 0x3FFFu) + (v > 0x1FFFFFu) + (v > 0xFFFFFFFu); }

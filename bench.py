@@ -408,7 +408,8 @@ def mixed_block(be, args, steps=5):
             "docs_lean": int((s1.docs_lean - s0.docs_lean) / steps), "docs_lean_wide": int((s1.docs_lean_wide - s0.docs_lean_wide) / steps),
             "docs_general_tiers": int((s1.docs_fast - s0.docs_fast) / steps),
             "docs_big": int((s1.docs_big - s0.docs_big) / steps), "docs_seq": int((s1.docs_seq - s0.docs_seq) / steps),
-            "roofline": roof(algo, kms, "k_merge_lean<0> + k_merge_lean<1> (wide) over its deferrals + the general tiers for the rest", None),
+            "roofline": roof(algo, kms, "k_merge_lean<1> (wide route: the batch's average document outgrows the narrow kernel's "
+                                        "staging) + the general tiers for its deferrals", None),
             "parity": f"bit-exact vs oracle on {checked} sampled docs"}
 
 

@@ -39,12 +39,13 @@ int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, 
                           uint64_t sv_bytes, const uint64_t* sv_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
                           uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list, uint64_t out_cap, uint8_t* tbl,
                           uint32_t* tbl_n, hipStream_t s);
+uint32_t ygm_k_lean_stage_bytes();
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
                             uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, const uint32_t* list,
                                  uint32_t n_list, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
-                                 void* meta, uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
+                                 void* meta, void* meta_next, uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
 int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
                             const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
                             int32_t* status, void* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
@@ -176,6 +177,7 @@ struct ygm_ctx {
     uint64_t arena_bytes = 0, slot_total = 0, out_cap = 0;
     uint32_t n_upd = 0, n_docs = 0;
     void* meta = nullptr;   // counter slot of the launch
+    bool wide_route = false;   // the launch was the wide lean kernel over the whole batch
   } pend;
   uint32_t lean_span_n = 0;   // lean launches enqueued since the last finish (timed as one span, e0 .. e1)
 };
@@ -298,9 +300,19 @@ int ygm_merge_v1_device_async(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena
   c->lean_span_n++;
   void* meta = c->meta_slot(c->mslot);
   void* meta_next = c->meta_slot(1 - c->mslot);   // zeroed by this launch for the next one
-  if (ygm_k_launch_merge_lean(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
-                              c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta, meta_next, c->defer_list.as<uint32_t>(), out_cap, s))
+  // the wide route: a batch whose average document outgrows the narrow kernel's staging (multi-character inserts,
+  // many clients: the realistic logs of c2_mixed) would be deferred by it almost whole -- a pass that only reads
+  // headers yet costs as much as merging a C2 batch (latency-bound) -- so the wide kernel takes every document
+  const bool wide_route = n_docs && arena_bytes / n_docs > (uint64_t)ygm_k_lean_stage_bytes() && getenv("YGM_NO_WIDE_ROUTE") == nullptr;
+  if (wide_route) {
+    if (ygm_k_launch_merge_lean_wide(d_arena, d_upd_off, d_doc_upd, n_docs, nullptr, n_docs, c->flags, c->out.as<uint8_t>(),
+                                     c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta, meta_next,
+                                     c->defer_w_list.as<uint32_t>(), out_cap, s))
+      return YGM_EDEVICE;
+  } else if (ygm_k_launch_merge_lean(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
+                                     c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta, meta_next, c->defer_list.as<uint32_t>(), out_cap, s))
     return YGM_EDEVICE;
+  c->pend.wide_route = wide_route;
   if (n_docs) c->mslot = 1 - c->mslot;   // (an empty batch launches nothing: the slot stays current)
   c->pend.live = true; c->pend.s = s;
   c->pend.arena = d_arena; c->pend.upd_off = d_upd_off; c->pend.doc_upd = d_doc_upd;
@@ -325,11 +337,14 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
   c->stats.lean_launches += c->lean_span_n;
   c->lean_span_n = 0;
   uint32_t n_gen = 0;   // documents for the general tiers
-  if (m.lean_defer) {  // tier 1b: the wide lean kernel (updates <= 64 bytes, documents <= 7 KB) over tier 1's deferred list
+  if (P.wide_route) {  // the wide kernel took the whole batch (async): its deferrals go on
+    n_gen = m.wide_defer;
+    c->stats.docs_lean_wide += P.n_docs - m.wide_defer;
+  } else if (m.lean_defer) {  // tier 1b: the wide lean kernel (updates <= 64 bytes, documents <= 7 KB) over tier 1's deferred list
     HIPCHK(hipEventRecord(c->e0, s));
     if (ygm_k_launch_merge_lean_wide(P.arena, P.upd_off, P.doc_upd, P.n_docs, c->defer_list.as<uint32_t>(), m.lean_defer, c->flags,
                                      c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
-                                     P.meta, c->defer_w_list.as<uint32_t>(), P.out_cap, s))
+                                     P.meta, nullptr, c->defer_w_list.as<uint32_t>(), P.out_cap, s))
       return YGM_EDEVICE;
     HIPCHK(hipEventRecord(c->e1, s));
     if ((e = read_meta(c, s, m, P.meta))) return e;

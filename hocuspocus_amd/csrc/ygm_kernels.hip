@@ -1579,7 +1579,7 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
                                                      const uint32_t* __restrict__ list, uint32_t n_list) {
   typedef LnCfg<WIDE> C;
   __shared__ LeanLdsT<WIDE> LS;
-  if (!WIDE && blockIdx.x == 0) {   // the next launch's counter slot (nothing reads it during this launch)
+  if (meta_next && blockIdx.x == 0) {   // the next launch's counter slot (nothing reads it during this launch)
     static_assert(sizeof(DocMeta) % 16 == 0, "DocMeta is zeroed in 16-byte pieces");
     const u32x4 z = {0u, 0u, 0u, 0u};
     for (uint32_t i = threadIdx.x; i < sizeof(DocMeta) / 16; i += WAVE) ((u32x4*)meta_next)[i] = z;
@@ -1592,7 +1592,10 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
   // the wave's j-th document: blockIdx.x + j G (narrow), or list entry blockIdx.x + j G (wide; n_docs past the list).
   // Wide: lane l of lst0 / lst1 holds the entry of iteration 64 b + l / 64 (b + 1) + l (b = the current run)
   const uint32_t n_it = WIDE ? n_list : n_docs;
-  auto list_at = [&](uint32_t j) -> uint32_t { const uint64_t i = (uint64_t)blockIdx.x + (uint64_t)j * G; return i < n_it ? list[i] : n_docs; };
+  auto list_at = [&](uint32_t j) -> uint32_t {   // (list == nullptr: every document of the batch, the wide route)
+    const uint64_t i = (uint64_t)blockIdx.x + (uint64_t)j * G;
+    return i < n_it ? (list ? list[i] : (uint32_t)i) : n_docs;
+  };
   uint32_t lst0 = 0, lst1 = 0;
   if (WIDE) { lst0 = list_at(l); lst1 = list_at(WAVE + l); }
   uint32_t it = 0;
@@ -2736,6 +2739,7 @@ static uint32_t resident_blocks(K kernel, int threads, uint32_t fallback) {
   return (uint32_t)(cus * per);
 }
 
+uint32_t ygm_k_lean_stage_bytes() { return (uint32_t)LN_IN; }   // input bytes the narrow lean kernel stages per document
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
                             uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
@@ -2754,13 +2758,13 @@ int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const
 // (count: DocMeta::wide_defer)
 int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, const uint32_t* list,
                                  uint32_t n_list, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
-                                 void* meta, uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
+                                 void* meta, void* meta_next, uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
   if (n_list == 0) return 0;
   static uint32_t resident = 0;
   if (!resident) { const char* g = getenv("YGM_WIDE_GRID"); resident = g ? (uint32_t)atoi(g) : resident_blocks(k_merge_lean<1>, WAVE, 2048u); }
   const uint32_t grid = n_list < resident ? n_list : resident;
   hipLaunchKernelGGL(k_merge_lean<1>, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len, status,
-                     (DocMeta*)meta, (DocMeta*)nullptr, defer_list, out_cap, list, n_list);
+                     (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap, list, n_list);
   return launch_rc(__func__);
 }
 

@@ -115,14 +115,14 @@ __global__ __launch_bounds__(V2_NT) void k_v12_write(const uint8_t* __restrict__
   const int e = v2::v12_write(v1 + v1_off[d], (uint32_t)len, v2a, v2n, mode, flags, Ld, out + o0);
   if (e) { st[d] = ST_DEVICE; out_len[d] = 0; }   // (the count pass took the same path: cannot happen)
 }
-// V1 -> V2 of the documents in the fast encoder's shape (ygm_v2_fast.hpp): D documents per wave, each one's V1
-// bytes staged in LDS by 16-byte loads with its terminator masks; lane j runs document j's two encoder passes
-// (register state; the count pass sizes the columns, the write pass stores the V2 bytes straight into the
-// document's slot -- merge_slot of its V2 input bytes, as the V1 kernels place outputs: no scan, no
-// cross-document dependency).  The encoder is one serial chain per document, so the documents in flight are
-// what counts: D documents share one instruction stream, and a small staging cap (FIN) leaves room for more
-// waves per CU; a second launch (D = 1, FIN = F_IN) takes the larger documents.  claim[d] = 1 for a document
-// done here; the general kernels take the rest (their outputs after the slot region).
+// V1 -> V2 of the documents in the fast encoder's shape (ygm_v2_fast.hpp): D documents per wave, nine lanes per
+// document, one V2 column per lane.  Each document's V1 bytes are staged in LDS by 16-byte loads with its terminator
+// masks; the nine lanes of a document walk the same bytes (one decode stream, LDS reads broadcast) and each encodes
+// its own column -- a count pass, the layout from the nine lengths, a write pass that stores the column straight
+// into the document's slot (merge_slot of its V2 input bytes, as the V1 kernels place outputs: no scan, no
+// cross-document dependency).  The small tier stages documents of <= 3.5 KB (seven per wave, 63 lanes busy), a
+// second launch (D = 2, 7 KB) the larger ones.  claim[d] = 1 for a document done here; the general kernels take
+// the rest (their outputs after the slot region).
 typedef __attribute__((address_space(3))) uint8_t FL8;
 typedef __attribute__((address_space(3))) uint64_t FL64;
 typedef unsigned int fu32x4 __attribute__((ext_vector_type(4)));
@@ -140,12 +140,13 @@ __global__ __launch_bounds__(64) void k_v12_fast(const uint8_t* __restrict__ v1,
                                                  const int32_t* __restrict__ ust, uint32_t n_docs, uint8_t* __restrict__ out,
                                                  uint64_t* __restrict__ fo, uint64_t* __restrict__ olen, int32_t* __restrict__ ost,
                                                  uint8_t* __restrict__ claim, unsigned long long* __restrict__ payload, int second) {
+  static_assert(D * v2f::FC_N <= WAVE, "nine lanes per document");
   typedef V2FDoc<FIN> Doc;
   __shared__ Doc S[D];
-  const uint32_t l = threadIdx.x;
-  uint32_t mine_sh = 0, mine_n = 0;   // lane j < D: document j's staged shift and end
-  bool mine_ok = false;
-  uint64_t mine_slot = 0, mine_cap = 0;
+  const uint32_t l = threadIdx.x, g = l / v2f::FC_N, col = l % v2f::FC_N;   // lane l: document g, column col
+  uint32_t g_sh = 0, g_n = 0;              // lanes of document g: its staged shift and end
+  bool g_ok = false;
+  uint64_t g_slot = 0, g_cap = 0;
   for (int j = 0; j < D; j++) {
     const uint32_t d = blockIdx.x * D + (uint32_t)j;
     if (d >= n_docs) break;
@@ -177,35 +178,46 @@ __global__ __launch_bounds__(64) void k_v12_fast(const uint8_t* __restrict__ v1,
       if (c * 16u < n) v = src[c];
       *(fu32x4*)(S[j].in + 16u * c) = v;
     }
-    if (l == (uint32_t)j) { mine_ok = true; mine_sh = sh; mine_n = n; mine_slot = v2_slot(b0, d); mine_cap = 2 * nb + 48; }
+    if (g == (uint32_t)j) { g_ok = true; g_sh = sh; g_n = n; g_slot = v2_slot(b0, d); g_cap = 2 * nb + 48; }
   }
   __syncthreads();
   for (int j = 0; j < D; j++) {
-    const uint32_t nw = (uint32_t)__shfl((int)mine_n, j) ? ((uint32_t)__shfl((int)mine_n, j) + 63u) / 64u + 1u : 0u;
+    const uint32_t nj = (uint32_t)__shfl((int)g_n, j * (int)v2f::FC_N);
+    const uint32_t nw = nj ? (nj + 63u) / 64u + 1u : 0u;
     for (uint32_t k = l; k <= nw && nw; k += WAVE) S[j].m[k] = v2f::f_mask_word((FL8*)S[j].in, k);
   }
   __syncthreads();
-  if (l < (uint32_t)D && mine_ok) {
-    const uint32_t d = blockIdx.x * D + l;
-    const v2f::FSrc<FL8*, FL64*> src{(FL8*)S[l].in, (FL64*)S[l].m};
-    v2f::FEnc k;
+  if (g < (uint32_t)D && g_ok) {
+    const uint32_t d = blockIdx.x * D + g;
+    const v2f::FSrc<FL8*, FL64*> src{(FL8*)S[g].in, (FL64*)S[g].m};
+    v2f::FCS c;
     bool ok = true;
-    uint32_t total = 0;
-    // both passes through ONE inlined copy of the encoder (a null output counts): half the code, which the
-    // instruction cache holds
+    uint32_t total = 0, mb = 0;
+    uint8_t* o = nullptr;
+    // count pass, layout, write pass -- through ONE inlined copy of the walk (instruction cache)
+#pragma unroll 1
     for (int pass = 0; pass < 2 && ok; pass++) {
-      uint8_t* o = pass ? out + mine_slot : nullptr;
-      if (pass) v2f::f_layout(o, k);
-      ok = v2f::f_run<true>(src, mine_sh, mine_n, o, k);
-      if (ok && !pass) {
-        total = v2f::f_total(k);
-        ok = total <= v2f::F_OUT && ((total + 15u) & ~15u) <= mine_cap;
+      ok = v2f::f_col_run(src, g_sh, g_n, col, o, mb, c);
+      if (pass == 0) {
+        // the document's nine column lengths (its lanes g*9 .. g*9+8; they all took the same path)
+        uint32_t L[v2f::FC_N], base[v2f::FC_N];
+#pragma unroll
+        for (int q = 0; q < (int)v2f::FC_N; q++) L[q] = (uint32_t)__shfl((int)c.n, (int)(g * v2f::FC_N) + q, WAVE);
+        total = v2f::fc_layout((uint8_t*)nullptr, L, base);
+        ok = ok && ((total + 15u) & ~15u) <= g_cap;
+        o = out + g_slot;
+        if (ok && col == 0u) (void)v2f::fc_layout(o, L, base);
+        mb = base[0];
+#pragma unroll
+        for (int q = 1; q < (int)v2f::FC_N; q++) mb = col == (uint32_t)q ? base[q] : mb;
       }
     }
-    if (ok) {
-      fo[d] = mine_slot; olen[d] = total; ost[d] = ST_OK; claim[d] = 1;
-      atomicAdd(payload, (unsigned long long)total);
-    } else if (!second) claim[d] = 0;
+    if (col == 0u) {
+      if (ok) {
+        fo[d] = g_slot; olen[d] = total; ost[d] = ST_OK; claim[d] = 1;
+        atomicAdd(payload, (unsigned long long)total);
+      } else if (!second) claim[d] = 0;
+    }
   }
 }
 
@@ -257,11 +269,11 @@ int ygm_k_launch_v12_fast(const uint8_t* v1, const uint64_t* v1_off, const uint6
                           const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint8_t* out, uint64_t* fo, uint64_t* olen, int32_t* ost,
                           uint8_t* claim, unsigned long long* payload, hipStream_t s) {
   if (n_docs == 0) return 0;
-  constexpr int D = 4, FS = 3584;   // small tier: four documents of <= 3.5 KB per wave (17 KB of LDS)
+  constexpr int D = 7, FS = 3584;   // small tier: seven documents of <= 3.5 KB per wave (29 KB of LDS)
   hipLaunchKernelGGL((k_v12_fast<D, FS>), dim3((n_docs + D - 1) / D), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd, ust,
                      n_docs, out, fo, olen, ost, claim, payload, 0);
-  hipLaunchKernelGGL((k_v12_fast<1, (int)v2f::F_IN>), dim3(n_docs), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd, ust,
-                     n_docs, out, fo, olen, ost, claim, payload, 1);
+  hipLaunchKernelGGL((k_v12_fast<2, (int)v2f::F_IN>), dim3((n_docs + 1) / 2), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd,
+                     ust, n_docs, out, fo, olen, ost, claim, payload, 1);
   return v2_rc(__func__);
 }
 int ygm_k_launch_v12_write(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const uint8_t* v2a, uint64_t v2n,

@@ -1,20 +1,21 @@
 // ygm_v2_fast.hpp -- V1 -> update V2 (UpdateEncoderV2 through yjs 13.6 convertUpdateFormat)
-// for the shapes a merge / diff of text logs produces, with every encoder state in registers.
+// for the shapes a merge / diff of text logs produces.
 //
-// The general transcoder (ygm_v2.hpp v12_body) keeps its eleven column writers in an array and its reads in a
-// byte cursor: on the GPU that state lives in scratch and a C2 document costs ~30 us per struct.  Here one
-// document's V1 bytes are staged (LDS on the device), structs are decoded from a 40-byte register window by
-// its terminator mask (bit i: byte i has its top bit clear), and each column is a named register cursor.  Two
-// passes over the same code: W = false counts the column lengths, W = true writes the columns at the offsets
-// of the V2 layout (toUint8Array: 0, keyClock, client, leftClock, rightClock, info, string(+lens), parentInfo,
-// typeRef, len, rest).
+// The general transcoder (ygm_v2.hpp v12_body) is one lane per document with its eleven column writers in an
+// array and a byte cursor over global memory: on the GPU that state lives in scratch, ~30 us per struct.  Here a
+// document's V1 bytes are staged (LDS on the device) with their terminator masks (bit i: byte i has its top bit
+// clear), an Item's fields are located from one mask window beside its info byte, and the V2 columns are encoded
+// one per lane (f_col_run): the lanes of a document walk the same bytes and each feeds its column's values to one
+// generic encoder (lib0 0.2.42 UintOptRle / IntDiffOptRle / Rle, the string bytes, the rest column's varuints --
+// ygm_v2.hpp rle_w / uo_w / id_w and their flushes).  A count pass sizes the columns, the layout places them
+// (toUint8Array: 0, keyClock, client, leftClock, rightClock, info, string(+lens), parentInfo, typeRef, len, rest),
+// a write pass stores them.
 //
 // Taken: client blocks (non-empty, consecutive clients distinct), GC, Skip, Items with origin and/or right
 // origin or with a parent (parentInfo 1: a root-type key; 0: a parent id) and an optional parentSub, content
 // ContentDeleted / ContentString (ASCII: UTF-16 length = bytes), the delete set (ranges in clock order per
-// client), values < 2^32.  Anything else returns false and the document takes v12_body; the encoders below
-// follow the same lib0 0.2.42 rules (rle_w / uo_w / id_w and their flushes, ygm_v2.hpp) -- the tests compare
-// both paths byte for byte.
+// client), values < 2^32.  Anything else returns false and the document takes v12_body; the tests compare both
+// paths byte for byte (tests/test_v2_fast_host.py on the host build, tests/test_v2.py on the GPU).
 #pragma once
 #include "ygm_v2.hpp"
 
@@ -23,20 +24,6 @@ namespace v2f {
 
 constexpr uint32_t F_IN = 7168;    // staged V1 bytes (a document past this takes the general path)
 constexpr uint32_t F_OUT = 6144;   // V2 bytes assembled per document
-
-// lib0 encoder states (ygm_v2.hpp RleE / UoE / IdE with 32-bit values: the fast path takes values < 2^32)
-struct FRle { uint32_t count; int32_t s; };
-struct FUo { uint32_t count; uint32_t s; };
-struct FId { uint32_t count; int64_t s, diff; };
-
-// column cursors: byte count and (write pass) base offset in the output
-struct FCol { uint32_t base, n; };
-struct FEnc {
-  FCol cl, lc, rc, info, str, lens, pi, ln, rest;
-  FUo ucl, uln, ulens;
-  FId ilc, irc;
-  FRle rinfo, rpi;
-};
 
 template <class P>
 YDEV uint32_t f_ld32(P p, uint32_t i) {   // dword i of a 4-byte aligned byte buffer
@@ -112,53 +99,6 @@ YDEV uint32_t f_u8(const S& src, FRd& r) {
   return src.byte(r.p++);
 }
 
-// ---- column writers (W: store; always count)
-template <bool W, class Q>
-YDEV void f_b(Q out, FCol& c, uint32_t v) {
-  if (W && out) out[c.base + c.n] = (uint8_t)v;   // (out == nullptr: a count pass through the same code)
-  c.n++;
-}
-template <bool W, class Q>
-YDEV void f_vuw(Q out, FCol& c, uint32_t v) {
-  while (v > 127u) { f_b<W>(out, c, 0x80u | (v & 127u)); v >>= 7; }
-  f_b<W>(out, c, v);
-}
-template <bool W, class Q>
-YDEV void f_vi(Q out, FCol& c, uint32_t m, bool neg) {   // lib0 writeVarInt of a magnitude < 2^32 (any_vi)
-  f_b<W>(out, c, (m > 63u ? 0x80u : 0u) | (neg ? 0x40u : 0u) | (m & 63u));
-  m >>= 6;
-  while (m > 0u) { f_b<W>(out, c, (m > 127u ? 0x80u : 0u) | (m & 127u)); m >>= 7; }
-}
-template <bool W, class Q>
-YDEV void f_rle(Q out, FCol& c, FRle& e, int32_t v) {
-  if (e.s == v) { e.count++; return; }
-  if (e.count > 0u) f_vuw<W>(out, c, e.count - 1u);
-  e.count = 1; f_b<W>(out, c, (uint32_t)v); e.s = v;
-}
-template <bool W, class Q>
-YDEV void f_uo_flush(Q out, FCol& c, const FUo& e) {
-  if (e.count > 0u) { f_vi<W>(out, c, e.s, e.count != 1u); if (e.count > 1u) f_vuw<W>(out, c, e.count - 2u); }
-}
-template <bool W, class Q>
-YDEV void f_uo(Q out, FCol& c, FUo& e, uint32_t v) {
-  if (e.s == v) { e.count++; return; }
-  f_uo_flush<W>(out, c, e);
-  e.count = 1; e.s = v;
-}
-template <bool W, class Q>
-YDEV void f_id_flush(Q out, FCol& c, const FId& e) {
-  if (e.count > 0u) {
-    const int32_t v = (int32_t)(((uint32_t)(uint64_t)e.diff << 1) | (e.count == 1u ? 0u : 1u));
-    f_vi<W>(out, c, v < 0 ? 0u - (uint32_t)v : (uint32_t)v, v < 0);
-    if (e.count > 1u) f_vuw<W>(out, c, e.count - 2u);
-  }
-}
-template <bool W, class Q>
-YDEV void f_id(Q out, FCol& c, FId& e, int64_t v) {
-  if (e.diff == v - e.s) { e.s = v; e.count++; return; }
-  f_id_flush<W>(out, c, e);
-  e.count = 1; e.diff = v - e.s; e.s = v;
-}
 // ASCII check of the input bytes [s, s + len) from the terminator masks (ASCII <=> top bit clear)
 template <class S>
 YDEV bool f_ascii(const S& src, uint32_t s, uint32_t len) {
@@ -169,143 +109,6 @@ YDEV bool f_ascii(const S& src, uint32_t s, uint32_t len) {
   }
   return true;
 }
-// the string bytes [s, s + len) (ASCII, checked) to the string column, its length to lens
-template <bool W, class S, class Q>
-YDEV void f_put_str(const S& src, Q out, FEnc& k, uint32_t s, uint32_t len) {
-  if (W && out)
-    for (uint32_t i = 0; i < len; i++) out[k.str.base + k.str.n + i] = (uint8_t)src.byte(s + i);
-  k.str.n += len;
-  f_uo<W>(out, k.lens, k.ulens, len);
-}
-// a varString at the reader (ASCII only)
-template <bool W, class S, class Q>
-YDEV void f_str(const S& src, Q out, FRd& r, FEnc& k) {
-  const uint32_t len = f_vu(src, r);
-  const uint32_t s = r.p;
-  r.ok = r.ok && len <= r.n - (s < r.n ? s : r.n) && f_ascii(src, s, len);
-  if (!r.ok) return;
-  f_put_str<W>(src, out, k, s, len);
-  r.p = s + len;
-}
-
-// One pass over the V1 update [p0, n) of the staged input.  Returns false off the fast path (the caller takes
-// v12_body).  An Item with origin(s) is decoded from ONE terminator-mask window read beside its info byte: the
-// ends of its origin varuints and of its content length are the next set bits, so every field value is read in
-// one more round trip (no byte-serial walk).
-template <bool W, class S, class Q>
-YDEV bool f_run(const S& src, uint32_t p0, uint32_t n, Q out, FEnc& k) {
-  FRd r{p0, n, true};
-  k.ucl = FUo{0, 0}; k.uln = FUo{0, 0}; k.ulens = FUo{0, 0};
-  k.ilc = FId{0, 0, 0}; k.irc = FId{0, 0, 0};
-  k.rinfo = FRle{0, -1}; k.rpi = FRle{0, -1};
-  k.cl.n = k.lc.n = k.rc.n = k.info.n = k.str.n = k.lens.n = k.pi.n = k.ln.n = k.rest.n = 0;
-  const uint32_t nb = f_vu(src, r);
-  f_vuw<W>(out, k.rest, nb);
-  uint32_t prev = 0; bool have_prev = false;
-  for (uint32_t b = 0; b < nb && r.ok; b++) {
-    const uint32_t ns = f_vu(src, r), client = f_vu(src, r), clock = f_vu(src, r);
-    r.ok = r.ok && ns != 0u && !(have_prev && client == prev);   // lazy-writer normal (else ENONCANON: v12_body decides)
-    prev = client; have_prev = true;
-    if (!r.ok) break;
-    f_uo<W>(out, k.cl, k.ucl, client); f_vuw<W>(out, k.rest, ns); f_vuw<W>(out, k.rest, clock);
-    for (uint32_t st = 0; st < ns && r.ok; st++) {
-      const uint32_t p = r.p;
-      r.ok = r.ok && p < r.n;
-      const uint32_t info = src.byte(p);
-      const uint64_t m = src.mask(p + 1u);          // (independent of the info byte: read together)
-      const uint32_t ref = info & 31u;
-      const bool ho = (info & 0x80u) != 0u, hr = (info & 0x40u) != 0u;
-      if ((ho || hr) && (ref == 1u || ref == 4u) && !(info & 0x20u)) {
-        // origin ids (2 or 4 varuints) and the content length: the next 3 or 5 terminators after the info byte
-        uint64_t t = m;
-        uint32_t e[5];
-#pragma unroll
-        for (int j = 0; j < 5; j++) { e[j] = t ? (uint32_t)__builtin_ctzll(t) : 64u; t &= t - 1ull; }
-        const uint32_t nv = (ho && hr) ? 5u : 3u;
-        const uint32_t el = nv == 5u ? e[4] : e[2];   // the content length's terminator
-        if (el < 64u) {
-          const uint32_t q = p + 1u;
-          const uint32_t v0 = f_vat(src, r, q, q + e[0]), v1 = f_vat(src, r, q + e[0] + 1u, q + e[1]);
-          const uint32_t v2 = f_vat(src, r, q + e[1] + 1u, q + e[2]);
-          uint32_t v3 = 0, v4 = 0;
-          if (nv == 5u) { v3 = f_vat(src, r, q + e[2] + 1u, q + e[3]); v4 = f_vat(src, r, q + e[3] + 1u, q + e[4]); }
-          const uint32_t len = nv == 5u ? v4 : v2;
-          const uint32_t cs = q + el + 1u;               // after the content length
-          uint32_t next = cs;
-          if (ref == 4u) {
-            next = cs + len;
-            r.ok = r.ok && len <= r.n - (cs < r.n ? cs : r.n) &&
-                   (el + 1u + len < 64u ? ((~m >> (el + 1u)) & (len >= 64u ? ~0ull : ((1ull << len) - 1ull))) == 0ull
-                                         : f_ascii(src, cs, len));
-          }
-          if (!r.ok) break;
-          f_rle<W>(out, k.info, k.rinfo, (int32_t)(ref | (ho ? 0x80u : 0u) | (hr ? 0x40u : 0u)));
-          if (ho) { f_uo<W>(out, k.cl, k.ucl, v0); f_id<W>(out, k.lc, k.ilc, (int64_t)v1); }
-          if (hr) {
-            f_uo<W>(out, k.cl, k.ucl, ho ? v2 : v0); f_id<W>(out, k.rc, k.irc, (int64_t)(ho ? v3 : v1));
-          }
-          if (ref == 1u) f_uo<W>(out, k.ln, k.uln, len);   // ContentDeleted
-          else f_put_str<W>(src, out, k, cs, len);         // ContentString
-          r.p = next;
-          continue;
-        }
-      }
-      // everything else, field by field
-      r.p = p + 1u;
-      if (info == 10u) {   // Skip (read_struct's order: info 10 exactly, then any info with ref 0 is a GC)
-        f_rle<W>(out, k.info, k.rinfo, 10);
-        f_vuw<W>(out, k.rest, f_vu(src, r));
-        continue;
-      }
-      if (ref == 0u) {   // GC
-        f_rle<W>(out, k.info, k.rinfo, 0);
-        f_uo<W>(out, k.ln, k.uln, f_vu(src, r));
-        continue;
-      }
-      r.ok = r.ok && (ref == 1u || ref == 4u);
-      if (!r.ok) break;
-      const bool hs = !ho && !hr && (info & 0x20u);
-      f_rle<W>(out, k.info, k.rinfo, (int32_t)(ref | (ho ? 0x80u : 0u) | (hr ? 0x40u : 0u) | (hs ? 0x20u : 0u)));
-      if (ho) { const uint32_t oc = f_vu(src, r), ok = f_vu(src, r); f_uo<W>(out, k.cl, k.ucl, oc); f_id<W>(out, k.lc, k.ilc, (int64_t)ok); }
-      if (hr) { const uint32_t rc = f_vu(src, r), rk = f_vu(src, r); f_uo<W>(out, k.cl, k.ucl, rc); f_id<W>(out, k.rc, k.irc, (int64_t)rk); }
-      if (!ho && !hr) {
-        const uint32_t pi = f_vu(src, r);
-        r.ok = r.ok && pi <= 1u;
-        if (!r.ok) break;
-        if (pi == 1u) { f_rle<W>(out, k.pi, k.rpi, 1); f_str<W>(src, out, r, k); }
-        else {
-          f_rle<W>(out, k.pi, k.rpi, 0);
-          const uint32_t pc = f_vu(src, r), pk = f_vu(src, r);
-          f_uo<W>(out, k.cl, k.ucl, pc); f_id<W>(out, k.lc, k.ilc, (int64_t)pk);
-        }
-        if (hs) f_str<W>(src, out, r, k);
-      }
-      if (ref == 1u) f_uo<W>(out, k.ln, k.uln, f_vu(src, r));   // ContentDeleted
-      else f_str<W>(src, out, r, k);                            // ContentString
-    }
-  }
-  if (!r.ok) return false;
-  // delete set: V1 (clock, len) -> V2 (clock - previous end, len - 1)
-  const uint32_t nd = f_vu(src, r);
-  f_vuw<W>(out, k.rest, nd);
-  for (uint32_t i = 0; i < nd && r.ok; i++) {
-    const uint32_t client = f_vu(src, r), nr = f_vu(src, r);
-    f_vuw<W>(out, k.rest, client); f_vuw<W>(out, k.rest, nr);
-    uint64_t cur = 0;
-    for (uint32_t q = 0; q < nr && r.ok; q++) {
-      const uint32_t clock = f_vu(src, r), len = f_vu(src, r);
-      r.ok = r.ok && (uint64_t)clock >= cur && len != 0u;   // (a backward clock / zero length: v12_body's rules)
-      if (!r.ok) break;
-      f_vuw<W>(out, k.rest, (uint32_t)(clock - cur)); f_vuw<W>(out, k.rest, len - 1u);
-      cur = (uint64_t)clock + len;
-    }
-  }
-  if (!r.ok) return false;
-  f_uo_flush<W>(out, k.cl, k.ucl); f_id_flush<W>(out, k.lc, k.ilc); f_id_flush<W>(out, k.rc, k.irc);
-  f_uo_flush<W>(out, k.lens, k.ulens); f_uo_flush<W>(out, k.ln, k.uln);
-  return true;
-}
-
 // terminator masks of the staged bytes [0, nbytes) (nbytes a multiple of 64): word k for bytes 64 k ..
 template <class P>
 YDEV uint64_t f_mask_word(P in, uint32_t k) {
@@ -319,34 +122,236 @@ YDEV uint64_t f_mask_word(P in, uint32_t k) {
   return ~H;
 }
 
-YDEV uint32_t f_vlen(uint32_t v) { return 1u + (v > 0x7Fu) + (v > 0x3FFFu) + (v > 0x1FFFFFu) + (v > 0xFFFFFFFu); }
-// V2 size from the counted columns (ygm_v2.hpp v2_total; keyClock and typeRef are empty here)
-YDEV uint32_t f_total(const FEnc& k) {
-  uint32_t t = 1u + 2u;   // version 0, empty keyClock, empty typeRef
-  t += f_vlen(k.cl.n) + k.cl.n + f_vlen(k.lc.n) + k.lc.n + f_vlen(k.rc.n) + k.rc.n + f_vlen(k.info.n) + k.info.n;
-  const uint32_t sc = f_vlen(k.str.n) + k.str.n + k.lens.n;
-  t += f_vlen(sc) + sc;
-  t += f_vlen(k.pi.n) + k.pi.n + f_vlen(k.ln.n) + k.ln.n;
-  return t + k.rest.n;
+// ---------------------------------------------------------------- one column per lane
+// The nine V2 columns a text log produces are encoded side by side, one lane each: every lane walks the same V1
+// bytes (the decode is the same instruction stream for all of them, LDS reads broadcast), picks its column's
+// values of each struct (up to three, in the writer's order) and feeds them to one generic encoder whose mode is
+// data: lib0's UintOptRle / IntDiffOptRle / Rle, the string bytes, or the raw varuints of the rest column.
+enum : uint32_t { FC_CL = 0, FC_LC, FC_RC, FC_INFO, FC_LENS, FC_PI, FC_LN, FC_STR, FC_REST, FC_N };
+enum : uint32_t { FM_UOR = 0, FM_IDOR, FM_RLE, FM_STR, FM_VU };
+YDEV uint32_t f_mode(uint32_t col) {
+  return col == FC_LC || col == FC_RC ? FM_IDOR : col == FC_INFO || col == FC_PI ? FM_RLE : col == FC_STR ? FM_STR
+       : col == FC_REST ? FM_VU : FM_UOR;
 }
-// writes the V2 header (version and column lengths) and sets each column's base
+struct FCS { uint32_t mode, n, count; int64_t s, diff; };   // one column's encoder and byte count
 template <class Q>
-YDEV void f_layout(Q out, FEnc& k) {
-  FCol h{0u, 0u};
-  f_b<true>(out, h, 0u);
-  f_vuw<true>(out, h, 0u);                                                    // keyClock
-  f_vuw<true>(out, h, k.cl.n); k.cl.base = h.n; h.n += k.cl.n;
-  f_vuw<true>(out, h, k.lc.n); k.lc.base = h.n; h.n += k.lc.n;
-  f_vuw<true>(out, h, k.rc.n); k.rc.base = h.n; h.n += k.rc.n;
-  f_vuw<true>(out, h, k.info.n); k.info.base = h.n; h.n += k.info.n;
-  const uint32_t sc = f_vlen(k.str.n) + k.str.n + k.lens.n;
-  f_vuw<true>(out, h, sc); f_vuw<true>(out, h, k.str.n);
-  k.str.base = h.n; h.n += k.str.n;
-  k.lens.base = h.n; h.n += k.lens.n;
-  f_vuw<true>(out, h, k.pi.n); k.pi.base = h.n; h.n += k.pi.n;
-  f_vuw<true>(out, h, 0u);                                                    // typeRef
-  f_vuw<true>(out, h, k.ln.n); k.ln.base = h.n; h.n += k.ln.n;
-  k.rest.base = h.n;
+YDEV void fc_b(Q out, uint32_t base, FCS& c, uint32_t v) {
+  if (out) out[base + c.n] = (uint8_t)v;   // (out == nullptr: the count pass)
+  c.n++;
+}
+template <class Q>
+YDEV void fc_vu(Q out, uint32_t base, FCS& c, uint32_t v) {
+  while (v > 127u) { fc_b(out, base, c, 0x80u | (v & 127u)); v >>= 7; }
+  fc_b(out, base, c, v);
+}
+template <class Q>
+YDEV void fc_vi(Q out, uint32_t base, FCS& c, uint32_t m, bool neg) {   // lib0 writeVarInt of a magnitude < 2^32
+  fc_b(out, base, c, (m > 63u ? 0x80u : 0u) | (neg ? 0x40u : 0u) | (m & 63u));
+  m >>= 6;
+  while (m > 0u) { fc_b(out, base, c, (m > 127u ? 0x80u : 0u) | (m & 127u)); m >>= 7; }
+}
+// the pending run of a UintOptRle / IntDiffOptRle column (uo_flush / id_flush)
+template <class Q>
+YDEV void fc_flush(Q out, uint32_t base, FCS& c) {
+  if (c.count == 0u || c.mode > FM_IDOR) return;
+  uint32_t mag; bool neg;
+  if (c.mode == FM_UOR) { mag = (uint32_t)c.s; neg = c.count != 1u; }
+  else {
+    const int32_t v = (int32_t)(((uint32_t)(uint64_t)c.diff << 1) | (c.count == 1u ? 0u : 1u));
+    neg = v < 0; mag = neg ? 0u - (uint32_t)v : (uint32_t)v;
+  }
+  fc_vi(out, base, c, mag, neg);
+  if (c.count > 1u) fc_vu(out, base, c, c.count - 2u);
+}
+// one value into the column (FM_STR: the staged input bytes [off, off + v))
+template <class S, class Q>
+YDEV void fc_push(const S& src, Q out, uint32_t base, FCS& c, uint32_t v, uint32_t off) {
+  if (c.mode == FM_VU) { fc_vu(out, base, c, v); return; }
+  if (c.mode == FM_STR) {
+    if (out) for (uint32_t i = 0; i < v; i++) out[base + c.n + i] = (uint8_t)src.byte(off + i);
+    c.n += v;
+    return;
+  }
+  if (c.mode == FM_RLE) {   // rle_w
+    if ((int64_t)v == c.s) { c.count++; return; }
+    if (c.count > 0u) fc_vu(out, base, c, c.count - 1u);
+    fc_b(out, base, c, v); c.s = (int64_t)v; c.count = 1u;
+    return;
+  }
+  const bool id = c.mode == FM_IDOR;   // uo_w / id_w
+  const int64_t key = id ? (int64_t)v - c.s : (int64_t)v, cur = id ? c.diff : c.s;
+  if (key == cur) { c.count++; if (id) c.s = (int64_t)v; return; }
+  fc_flush(out, base, c);
+  c.count = 1u;
+  if (id) c.diff = key;
+  c.s = (int64_t)v;
+}
+// the up-to-three values (v, off) of one step for one column; bit j of pm: value j present
+struct FCand { uint32_t v0, v1, v2, o0, o1, o2, pm; };
+YDEV FCand fc_one(bool on, uint32_t v) { return FCand{v, 0, 0, 0, 0, 0, on ? 1u : 0u}; }
+YDEV FCand fc_two(bool on, uint32_t v0, uint32_t v1) { return FCand{v0, v1, 0, 0, 0, 0, on ? 3u : 0u}; }
+
+// Column `col` of the V2 encoding of the V1 update [p0, n) of the staged input: its bytes to out + base (out ==
+// nullptr: counts c.n only).  Returns false off the fast path (every lane of a document sees the same bytes, so
+// all of them return the same).  The walk is ONE loop whose body decodes one step of the update (its header, a
+// block header, a struct, a delete-set header / client / range) and hands the column's values of that step to ONE
+// inlined encoder: the kernel's code must stay small enough for the instruction cache (a walk with an encoder
+// inlined at every value site ran ~20x slower, instruction-fetch bound).
+enum : uint32_t { FP_DOC = 0, FP_BLK, FP_ST, FP_DSH, FP_DSC, FP_DSR, FP_DONE };
+template <class S, class Q>
+YDEV bool f_col_run(const S& src, uint32_t p0, uint32_t n, uint32_t col, Q out, uint32_t base, FCS& c) {
+  c.mode = f_mode(col); c.n = 0; c.count = 0; c.s = c.mode == FM_RLE ? -1 : 0; c.diff = 0;
+  FRd r{p0, n, true};
+  const bool rest = col == FC_REST;
+  uint32_t ph = FP_DOC, nb = 0, b = 0, ns = 0, st = 0, prev = 0, nd = 0, di = 0, nr = 0, q = 0;
+  bool have_prev = false;
+  uint64_t cur = 0;
+#pragma unroll 1
+  while (ph != FP_DONE && r.ok) {
+    FCand k{0, 0, 0, 0, 0, 0, 0};
+    if (ph == FP_DOC) {
+      nb = f_vu(src, r); b = 0;
+      k = fc_one(rest, nb);
+      ph = nb ? FP_BLK : FP_DSH;
+    } else if (ph == FP_BLK) {
+      ns = f_vu(src, r); const uint32_t client = f_vu(src, r), clock = f_vu(src, r);
+      r.ok = r.ok && ns != 0u && !(have_prev && client == prev);   // lazy-writer normal (else ENONCANON: v12_body decides)
+      prev = client; have_prev = true; st = 0;
+      k = FCand{col == FC_CL ? client : ns, clock, 0, 0, 0, 0, col == FC_CL ? 1u : rest ? 3u : 0u};
+      ph = FP_ST;
+    } else if (ph == FP_ST) {
+      const uint32_t p = r.p;
+      r.ok = r.ok && p < r.n;
+      const uint32_t info = src.byte(p);
+      const uint64_t m = src.mask(p + 1u);          // (independent of the info byte: read together)
+      const uint32_t ref = info & 31u;
+      const bool ho = (info & 0x80u) != 0u, hr = (info & 0x40u) != 0u;
+      // the struct's fields (one decode for all columns)
+      uint32_t code = 0, oc = 0, ok = 0, rc = 0, rk = 0, pi = 0, pc = 0, pk = 0, len = 0;
+      uint32_t ko = 0, kl = 0, so = 0, sl = 0, co = 0;
+      bool gc = false, skip = false, item = false, has_pid = false, has_key = false, hs = false;
+      // an Item with origin ids (2 or 4 varuints) and a content length: the next 3 or 5 terminators after the
+      // info byte locate every field, read in one more round trip
+      uint64_t t = m;
+      uint32_t e0, e1, e2, e3, e4;
+      e0 = t ? (uint32_t)__builtin_ctzll(t) : 64u; t &= t - 1ull;
+      e1 = t ? (uint32_t)__builtin_ctzll(t) : 64u; t &= t - 1ull;
+      e2 = t ? (uint32_t)__builtin_ctzll(t) : 64u; t &= t - 1ull;
+      e3 = t ? (uint32_t)__builtin_ctzll(t) : 64u; t &= t - 1ull;
+      e4 = t ? (uint32_t)__builtin_ctzll(t) : 64u;
+      const uint32_t el = (ho && hr) ? e4 : e2;     // the content length's terminator
+      if ((ho || hr) && (ref == 1u || ref == 4u) && !(info & 0x20u) && el < 64u) {
+        const uint32_t q1 = p + 1u;
+        const uint32_t v0 = f_vat(src, r, q1, q1 + e0), v1 = f_vat(src, r, q1 + e0 + 1u, q1 + e1);
+        const uint32_t v2 = f_vat(src, r, q1 + e1 + 1u, q1 + e2);
+        const uint32_t v3 = (ho && hr) ? f_vat(src, r, q1 + e2 + 1u, q1 + e3) : 0u;
+        const uint32_t v4 = (ho && hr) ? f_vat(src, r, q1 + e3 + 1u, q1 + e4) : 0u;
+        len = (ho && hr) ? v4 : v2;
+        co = q1 + el + 1u;                              // after the content length
+        uint32_t next = co;
+        if (ref == 4u) {
+          next = co + len;
+          r.ok = r.ok && len <= r.n - (co < r.n ? co : r.n) &&
+                 (el + 1u + len < 64u ? ((~m >> (el + 1u)) & (len >= 64u ? ~0ull : ((1ull << len) - 1ull))) == 0ull
+                                      : f_ascii(src, co, len));
+        }
+        item = true;
+        code = ref | (ho ? 0x80u : 0u) | (hr ? 0x40u : 0u);
+        oc = v0; ok = v1;
+        rc = ho ? v2 : v0; rk = ho ? v3 : v1;
+        r.p = next;
+      } else {   // everything else, field by field
+        r.p = p + 1u;
+        if (info == 10u) { skip = true; code = 10u; len = f_vu(src, r); }   // Skip (info 10 exactly; then ref 0 is a GC)
+        else if (ref == 0u) { gc = true; code = 0u; len = f_vu(src, r); }   // GC
+        else {
+          r.ok = r.ok && (ref == 1u || ref == 4u);
+          item = true;
+          hs = !ho && !hr && (info & 0x20u);
+          code = ref | (ho ? 0x80u : 0u) | (hr ? 0x40u : 0u) | (hs ? 0x20u : 0u);
+          if (ho) { oc = f_vu(src, r); ok = f_vu(src, r); }
+          if (hr) { rc = f_vu(src, r); rk = f_vu(src, r); }
+          if (!ho && !hr) {
+            pi = f_vu(src, r);
+            r.ok = r.ok && pi <= 1u;
+            if (pi == 1u) {   // a root type's key
+              has_key = true; kl = f_vu(src, r); ko = r.p;
+              r.ok = r.ok && kl <= r.n - (ko < r.n ? ko : r.n) && f_ascii(src, ko, kl);
+              r.p = ko + kl;
+            } else { has_pid = true; pc = f_vu(src, r); pk = f_vu(src, r); }
+            if (hs) {         // parentSub
+              sl = f_vu(src, r); so = r.p;
+              r.ok = r.ok && sl <= r.n - (so < r.n ? so : r.n) && f_ascii(src, so, sl);
+              r.p = so + sl;
+            }
+          }
+          len = f_vu(src, r);
+          if (ref == 4u) {
+            co = r.p;
+            r.ok = r.ok && len <= r.n - (co < r.n ? co : r.n) && f_ascii(src, co, len);
+            r.p = co + len;
+          }
+        }
+      }
+      const bool noo = item && !ho && !hr, str = item && ref == 4u, io = item && ho, ir = item && hr;   // (GC info bits are no origins)
+      // this column's values of the struct, in v12_body's order (selects, not a branch per column)
+      const uint32_t pcl = (io || ir ? 1u : 0u) | (io && ir ? 2u : 0u) | (has_pid ? 4u : 0u);
+      const uint32_t pstr = (has_key ? 1u : 0u) | (hs ? 2u : 0u) | (str ? 4u : 0u);
+      k.v0 = col == FC_CL ? (io ? oc : rc) : col == FC_LC ? ok : col == FC_RC ? rk : col == FC_INFO ? code
+           : col == FC_LENS || col == FC_STR ? kl : col == FC_PI ? pi : len;
+      k.v1 = col == FC_CL ? rc : col == FC_LC ? pk : sl;
+      k.v2 = col == FC_CL ? pc : len;
+      k.o0 = ko; k.o1 = so; k.o2 = co;
+      k.pm = col == FC_CL ? pcl : col == FC_LC ? (io ? 1u : 0u) | (has_pid ? 2u : 0u) : col == FC_RC ? (ir ? 1u : 0u)
+           : col == FC_INFO ? 1u : col == FC_LENS || col == FC_STR ? pstr : col == FC_PI ? (noo ? 1u : 0u)
+           : col == FC_LN ? (gc || (item && ref == 1u) ? 1u : 0u) : (skip ? 1u : 0u);
+      if (++st == ns) { b++; ph = b < nb ? FP_BLK : FP_DSH; }
+    } else if (ph == FP_DSH) {   // delete set: V1 (clock, len) -> V2 (clock - previous end, len - 1), into the rest column
+      nd = f_vu(src, r); di = 0;
+      k = fc_one(rest, nd);
+      ph = nd ? FP_DSC : FP_DONE;
+    } else if (ph == FP_DSC) {
+      const uint32_t client = f_vu(src, r);
+      nr = f_vu(src, r); q = 0; cur = 0;
+      k = fc_two(rest, client, nr);
+      ph = nr ? FP_DSR : (++di < nd ? FP_DSC : FP_DONE);
+    } else {   // FP_DSR
+      const uint32_t clock = f_vu(src, r), len = f_vu(src, r);
+      r.ok = r.ok && (uint64_t)clock >= cur && len != 0u;   // (a backward clock / zero length: v12_body's rules)
+      k = fc_two(rest, (uint32_t)(clock - cur), len - 1u);
+      cur = (uint64_t)clock + len;
+      if (++q == nr) ph = ++di < nd ? FP_DSC : FP_DONE;
+    }
+    if (!r.ok) break;
+    // the one encoder site: up to three values
+#pragma unroll 1
+    for (uint32_t j = 0; j < 3u; j++)
+      if ((k.pm >> j) & 1u) fc_push(src, out, base, c, j == 0u ? k.v0 : j == 1u ? k.v1 : k.v2, j == 0u ? k.o0 : j == 1u ? k.o1 : k.o2);
+  }
+  if (!r.ok) return false;
+  fc_flush(out, base, c);
+  return true;
+}
+// V2 size and column bases (UpdateEncoderV2.toUint8Array layout) from the nine columns' byte counts L[FC_*];
+// writes the header (version, column lengths) when out != nullptr.  base[FC_*] = each column's offset.
+template <class Q>
+YDEV uint32_t fc_layout(Q out, const uint32_t (&L)[FC_N], uint32_t (&base)[FC_N]) {
+  FCS h{FM_VU, 0u, 0u, 0, 0};
+  fc_b(out, 0u, h, 0u);                                          // version
+  fc_vu(out, 0u, h, 0u);                                         // keyClock (empty)
+  const uint32_t pre[5] = {FC_CL, FC_LC, FC_RC, FC_INFO, FC_N};
+#pragma unroll
+  for (int q = 0; q < 4; q++) { fc_vu(out, 0u, h, L[pre[q]]); base[pre[q]] = h.n; h.n += L[pre[q]]; }
+  uint32_t sv = L[FC_STR], vl = 1u;
+  while (sv > 127u) { sv >>= 7; vl++; }
+  fc_vu(out, 0u, h, vl + L[FC_STR] + L[FC_LENS]); fc_vu(out, 0u, h, L[FC_STR]);
+  base[FC_STR] = h.n; h.n += L[FC_STR];
+  base[FC_LENS] = h.n; h.n += L[FC_LENS];
+  fc_vu(out, 0u, h, L[FC_PI]); base[FC_PI] = h.n; h.n += L[FC_PI];
+  fc_vu(out, 0u, h, 0u);                                         // typeRef (empty)
+  fc_vu(out, 0u, h, L[FC_LN]); base[FC_LN] = h.n; h.n += L[FC_LN];
+  base[FC_REST] = h.n;
+  return h.n + L[FC_REST];
 }
 
 }  // namespace v2f

@@ -37,14 +37,23 @@ extern "C" {
 int hv_v12f(const uint8_t* v1, uint32_t n, uint8_t* out, uint64_t* out_len) {
   *out_len = 0;
   if (n > v2f::F_IN) return 2;
-  static uint8_t in[v2f::F_IN + 64], ob[v2f::F_OUT + 64];
+  static uint8_t in[v2f::F_IN + 128], ob[v2f::F_OUT + 64];
+  static uint64_t m[(v2f::F_IN + 128) / 64 + 2];
   memset(in, 0, sizeof in); memcpy(in, v1, n);
-  v2f::FEnc k;
-  if (!v2f::f_run<false>((const uint8_t*)in, 0u, n, ob, k)) return 1;
-  const uint32_t t = v2f::f_total(k);
+  for (uint32_t k = 0; k < (v2f::F_IN + 128) / 64; k++) m[k] = v2f::f_mask_word((const uint8_t*)in, k);
+  const v2f::FSrc<const uint8_t*, const uint64_t*> src{in, m};
+  // the kernel's nine lanes, one after the other: count passes, layout, write passes
+  uint32_t L[v2f::FC_N], base[v2f::FC_N];
+  v2f::FCS c;
+  for (uint32_t col = 0; col < v2f::FC_N; col++) {
+    if (!v2f::f_col_run(src, 0u, n, col, (uint8_t*)nullptr, 0u, c)) return 1;
+    L[col] = c.n;
+  }
+  const uint32_t t = v2f::fc_layout((uint8_t*)nullptr, L, base);
   if (t > v2f::F_OUT) return 2;
-  v2f::f_layout(ob, k);
-  if (!v2f::f_run<true>((const uint8_t*)in, 0u, n, ob, k)) return 3;   // (cannot happen: the count pass took the same path)
+  (void)v2f::fc_layout(ob, L, base);
+  for (uint32_t col = 0; col < v2f::FC_N; col++)
+    if (!v2f::f_col_run(src, 0u, n, col, ob, base[col], c)) return 3;   // (cannot happen: the count pass took the same path)
   memcpy(out, ob, t);
   *out_len = t;
   return 0;

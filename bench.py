@@ -464,7 +464,7 @@ def v2_block(be, args, steps=5):
            "docs": n, "updates": n_upd, "bytes_in": len(a2), "bytes_out": int(r.payload_bytes),
            "value": round(algo / kms / 1e3, 3), "unit": "MB/s", "docs_per_s": round(n / kms * 1e3, 1), "ms_per_step": round(kms, 4),
            "wall_ms_per_step": round(wall * 1e3, 4),
-           "roofline": roof(algo, kms, "k_v21_count/write + V1 merge cascade + k_v12_count/write (one lane per update / document)", None),
+           "roofline": roof(algo, kms, "k_v21_count/write (lane per update) + V1 merge cascade + k_v12_fast (a V2 column per lane)", None),
            "convert": conv, "parity": f"bit-exact vs oracle (yjs_oracle_v2.c) on {checked} sampled docs; tests/test_v2.py: 4887 yjs vectors"}
     if not args.no_cpu_baseline and not args.no_yjs:
         blk["cpu_baseline"] = cpu_yjs("merge_v2", {"arena": a2, "upd_off": o2, "doc_upd": d1}, cpu_cores(args), min(n, 4000))

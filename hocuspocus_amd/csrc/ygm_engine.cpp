@@ -69,7 +69,8 @@ int ygm_k_launch_v12_write(const uint8_t* v1, const uint64_t* v1_off, const uint
                            hipStream_t s);
 int ygm_k_launch_v12_fast(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint64_t* slot_off,
                           const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint8_t* out, uint64_t* fo, uint64_t* olen, int32_t* ost,
-                          uint8_t* claim, unsigned long long* payload, hipStream_t s);
+                          uint8_t* claim, unsigned long long* payload, uint8_t* scr, hipStream_t s);
+size_t ygm_k_v12_fast_scratch();
 int ygm_k_launch_v2_status(const int32_t* ust, uint32_t n, int32_t* status, uint64_t* len, hipStream_t s);
 int ygm_k_launch_v2_lens(const uint64_t* off, const int32_t* st, uint32_t n, uint64_t* len, hipStream_t s);
 size_t ygm_k_big_blk_bytes();
@@ -160,7 +161,7 @@ struct ygm_ctx {
   DevBuf sn_cnt, sn_off, sn_bs, sn_ws;  // snapshot: per-document counts, workspace offsets, scan scratch, workspaces
   // update V2: per-update V1 sizes -> offsets, transcoding statuses, scan scratch, the V1 arena, per-document column
   // lengths, the V2 outputs (packed), their offsets / lengths / statuses
-  DevBuf v2_len, v2_st, v2_bs, v2_v1, v2_L, v2_out, v2_off, v2_olen, v2_ost, v2_fo, v2_claim, v2_pay;
+  DevBuf v2_len, v2_st, v2_bs, v2_v1, v2_L, v2_out, v2_off, v2_olen, v2_ost, v2_fo, v2_claim, v2_pay, v2_scr;
   // host API: results in pinned memory (packed outputs, per-document offset / length / status), the
   // pinned input staging of this context when it serves as a pipeline stage, the packed device copy,
   // and the two stage contexts (own streams and buffers) that double-buffer a batch's chunks
@@ -233,7 +234,7 @@ void ygm_close(ygm_ctx* c) {
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
                     &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws,
-                    &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay})
+                    &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr})
     b->release();
   for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
   for (DevBuf* b : {&c->pk_data, &c->pk_off, &c->pk_bsum}) b->release();
@@ -591,24 +592,31 @@ static int v12_pass(ygm_ctx* c, hipStream_t s, const uint8_t* v1, const uint64_t
   const bool fast = slot_off != nullptr && !(mode & 1u) && getenv("YGM_V2_NOFAST") == nullptr;
   const uint64_t slot_total = fast ? 2 * v2n + 64ull * n_docs : 0;
   uint8_t* claim = fast ? c->v2_claim.as<uint8_t>() : nullptr;
+  uint64_t total = 0, fast_bytes = 0, fast_docs = 0;
   if (fast && n_docs) {
-    if (!c->v2_out.ensure(slot_total + 64)) return YGM_ENOMEM;
-    HIPCHK(hipMemsetAsync(c->v2_pay.p, 0, 8, s));
+    if (!c->v2_out.ensure(slot_total + 64) || !c->v2_scr.ensure(ygm_k_v12_fast_scratch())) return YGM_ENOMEM;
+    HIPCHK(hipMemsetAsync(c->v2_pay.p, 0, 16, s));
     if (ygm_k_launch_v12_fast(v1, v1_off, v1_len, v1_st, slot_off, doc_upd, ust, n_docs, c->v2_out.as<uint8_t>(), c->v2_fo.as<uint64_t>(),
-                              c->v2_olen.as<uint64_t>(), c->v2_ost.as<int32_t>(), claim, c->v2_pay.as<unsigned long long>(), s))
+                              c->v2_olen.as<uint64_t>(), c->v2_ost.as<int32_t>(), claim, c->v2_pay.as<unsigned long long>(),
+                              c->v2_scr.as<uint8_t>(), s))
       return YGM_EDEVICE;
+    HIPCHK(hipMemcpyAsync(c->h_meta, c->v2_pay.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    memcpy(&fast_bytes, c->h_meta, 8); memcpy(&fast_docs, (uint8_t*)c->h_meta + 8, 8);
   }
-  uint64_t total = 0, fast_bytes = 0;
+  if (fast && fast_docs == n_docs) {   // every document done by the fast encoder: no general pass
+    out->data = c->v2_out.as<uint8_t>(); out->off = c->v2_fo.as<uint64_t>(); out->len = c->v2_olen.as<uint64_t>();
+    out->status = c->v2_ost.as<int32_t>(); out->data_bytes = slot_total; out->payload_bytes = fast_bytes;
+    return YGM_OK;
+  }
   if (n_docs) {
     if (ygm_k_launch_v12_count(v1, v1_off, v1_len, v1_st, v2a, v2n, upd_off, doc_upd, ust, n_docs, mode, c->flags, c->v2_L.as<uint32_t>(),
                                c->v2_off.as<uint64_t>(), c->v2_ost.as<int32_t>(), claim, s) ||
         ygm_k_launch_scan(c->v2_off.as<uint64_t>(), n_docs, c->v2_bs.as<uint64_t>(), s))
       return YGM_EDEVICE;
     HIPCHK(hipMemcpyAsync(c->h_meta, c->v2_off.as<uint64_t>() + n_docs, 8, hipMemcpyDeviceToHost, s));
-    if (fast) HIPCHK(hipMemcpyAsync((uint8_t*)c->h_meta + 8, c->v2_pay.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     memcpy(&total, c->h_meta, 8);
-    if (fast) memcpy(&fast_bytes, (uint8_t*)c->h_meta + 8, 8);
   }
   if (!c->v2_out.ensure(slot_total + total + 64, slot_total, s)) return YGM_ENOMEM;
   if (n_docs && ygm_k_launch_v12_write(v1, v1_off, v1_len, v2a, v2n, upd_off, doc_upd, n_docs, mode, c->flags, c->v2_L.as<uint32_t>(),

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "ygm_common.hpp"
 #include "ygm_v2.hpp"
@@ -139,87 +140,105 @@ __global__ __launch_bounds__(64) void k_v12_fast(const uint8_t* __restrict__ v1,
                                                  const uint64_t* __restrict__ slot_off, const uint32_t* __restrict__ doc_upd,
                                                  const int32_t* __restrict__ ust, uint32_t n_docs, uint8_t* __restrict__ out,
                                                  uint64_t* __restrict__ fo, uint64_t* __restrict__ olen, int32_t* __restrict__ ost,
-                                                 uint8_t* __restrict__ claim, unsigned long long* __restrict__ payload, int second) {
+                                                 uint8_t* __restrict__ claim, unsigned long long* __restrict__ payload, int second,
+                                                 uint8_t* __restrict__ scr) {
   static_assert(D * v2f::FC_N <= WAVE, "nine lanes per document");
   typedef V2FDoc<FIN> Doc;
+  constexpr uint32_t CAP = FIN + 64;   // scratch bytes per column (a column past it: the document goes on)
   __shared__ Doc S[D];
   const uint32_t l = threadIdx.x, g = l / v2f::FC_N, col = l % v2f::FC_N;   // lane l: document g, column col
-  uint32_t g_sh = 0, g_n = 0;              // lanes of document g: its staged shift and end
-  bool g_ok = false;
-  uint64_t g_slot = 0, g_cap = 0;
-  for (int j = 0; j < D; j++) {
-    const uint32_t d = blockIdx.x * D + (uint32_t)j;
-    if (d >= n_docs) break;
-    // eligibility: every input transcoded, the V1 operation OK, not a passthrough, staged size (second launch:
-    // only what the first one left)
-    bool bad = second && claim[d];
-    uint64_t b0 = 0, nb = 0;
-    if (!bad) {
-      if (doc_upd) {
-        const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
-        bad = u1 - u0 < 2u;
-        for (uint32_t u = u0 + l; u < u1 && !bad; u += WAVE) bad = ust[u] != ST_OK;
-        b0 = slot_off[u0]; nb = slot_off[u1] - b0;
-      } else {
-        bad = ust && ust[d] != ST_OK;
-        b0 = slot_off[d]; nb = slot_off[d + 1] - b0;
+  // this lane's column scratch (persistent grid: a wave reuses its own region)
+  uint8_t* cs = scr + ((size_t)blockIdx.x * D * v2f::FC_N + (g < (uint32_t)D ? g * v2f::FC_N + col : 0u)) * CAP;
+  for (uint32_t grp = blockIdx.x; (uint64_t)grp * D < n_docs; grp += gridDim.x) {
+    uint32_t g_sh = 0, g_n = 0;              // lanes of document g: its staged shift and end
+    bool g_ok = false;
+    uint64_t g_slot = 0, g_cap = 0;
+    __syncthreads();                          // (the previous group's staged bytes are no longer read)
+    for (int j = 0; j < D; j++) {
+      const uint32_t d = grp * D + (uint32_t)j;
+      if (d >= n_docs) break;
+      // eligibility: every input transcoded, the V1 operation OK, not a passthrough, staged size (second launch:
+      // only what the first one left)
+      bool bad = second && claim[d];
+      uint64_t b0 = 0, nb = 0;
+      if (!bad) {
+        if (doc_upd) {
+          const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
+          bad = u1 - u0 < 2u;
+          for (uint32_t u = u0 + l; u < u1 && !bad; u += WAVE) bad = ust[u] != ST_OK;
+          b0 = slot_off[u0]; nb = slot_off[u1] - b0;
+        } else {
+          bad = ust && ust[d] != ST_OK;
+          b0 = slot_off[d]; nb = slot_off[d + 1] - b0;
+        }
       }
+      if (v1_st && v1_st[d] != ST_OK) bad = true;
+      const uint64_t a = v1_off[d], len = v1_len ? v1_len[d] : v1_off[d + 1] - a;
+      if (len > (uint64_t)FIN || len == 0) bad = true;
+      if (__ballot(bad)) { if (l == 0 && !(second && claim[d])) claim[d] = 0; continue; }
+      // stage: 16-byte loads from the aligned base (the V1 arenas carry >= 16 bytes of readable tail)
+      const uint32_t sh = (uint32_t)(a & 15u), n = sh + (uint32_t)len;
+      const fu32x4* src = (const fu32x4*)(v1 + (a & ~15ull));
+      const uint32_t nw = (n + 63u) / 64u + 1u;   // mask words read: up to the one past the update's last byte
+      for (uint32_t c = l; c < 4u * nw; c += WAVE) {
+        fu32x4 v = {0u, 0u, 0u, 0u};
+        if (c * 16u < n) v = src[c];
+        *(fu32x4*)(S[j].in + 16u * c) = v;
+      }
+      if (g == (uint32_t)j) { g_ok = true; g_sh = sh; g_n = n; g_slot = v2_slot(b0, d); g_cap = 2 * nb + 48; }
     }
-    if (v1_st && v1_st[d] != ST_OK) bad = true;
-    const uint64_t a = v1_off[d], len = v1_len ? v1_len[d] : v1_off[d + 1] - a;
-    if (len > (uint64_t)FIN || len == 0) bad = true;
-    if (__ballot(bad)) { if (l == 0 && !(second && claim[d])) claim[d] = 0; continue; }
-    // stage: 16-byte loads from the aligned base (the V1 arenas carry >= 16 bytes of readable tail)
-    const uint32_t sh = (uint32_t)(a & 15u), n = sh + (uint32_t)len;
-    const fu32x4* src = (const fu32x4*)(v1 + (a & ~15ull));
-    const uint32_t nw = (n + 63u) / 64u + 1u;   // mask words read: up to the one past the update's last byte
-    for (uint32_t c = l; c < 4u * nw; c += WAVE) {
-      fu32x4 v = {0u, 0u, 0u, 0u};
-      if (c * 16u < n) v = src[c];
-      *(fu32x4*)(S[j].in + 16u * c) = v;
+    __syncthreads();
+    for (int j = 0; j < D; j++) {
+      const uint32_t nj = (uint32_t)__shfl((int)g_n, j * (int)v2f::FC_N);
+      const uint32_t nw = nj ? (nj + 63u) / 64u + 1u : 0u;
+      for (uint32_t k = l; k <= nw && nw; k += WAVE) S[j].m[k] = v2f::f_mask_word((FL8*)S[j].in, k);
     }
-    if (g == (uint32_t)j) { g_ok = true; g_sh = sh; g_n = n; g_slot = v2_slot(b0, d); g_cap = 2 * nb + 48; }
-  }
-  __syncthreads();
-  for (int j = 0; j < D; j++) {
-    const uint32_t nj = (uint32_t)__shfl((int)g_n, j * (int)v2f::FC_N);
-    const uint32_t nw = nj ? (nj + 63u) / 64u + 1u : 0u;
-    for (uint32_t k = l; k <= nw && nw; k += WAVE) S[j].m[k] = v2f::f_mask_word((FL8*)S[j].in, k);
-  }
-  __syncthreads();
-  if (g < (uint32_t)D && g_ok) {
-    const uint32_t d = blockIdx.x * D + g;
-    const v2f::FSrc<FL8*, FL64*> src{(FL8*)S[g].in, (FL64*)S[g].m};
-    v2f::FCS c;
-    bool ok = true;
-    uint32_t total = 0, mb = 0;
-    uint8_t* o = nullptr;
-    // count pass, layout, write pass -- through ONE inlined copy of the walk (instruction cache)
-#pragma unroll 1
-    for (int pass = 0; pass < 2 && ok; pass++) {
-      ok = v2f::f_col_run(src, g_sh, g_n, col, o, mb, c);
-      if (pass == 0) {
-        // the document's nine column lengths (its lanes g*9 .. g*9+8; they all took the same path)
-        uint32_t L[v2f::FC_N], base[v2f::FC_N];
+    __syncthreads();
+    if (g < (uint32_t)D && g_ok) {
+      const uint32_t d = grp * D + g;
+      const v2f::FSrc<FL8*, FL64*> src{(FL8*)S[g].in, (FL64*)S[g].m};
+      v2f::FCS c;
+      // ONE pass: the column into this lane's scratch, then the layout from the nine lengths, then the copy
+      bool ok = v2f::f_col_run(src, g_sh, g_n, col, cs, 0u, CAP, c);
+      uint32_t L[v2f::FC_N], base[v2f::FC_N];
 #pragma unroll
-        for (int q = 0; q < (int)v2f::FC_N; q++) L[q] = (uint32_t)__shfl((int)c.n, (int)(g * v2f::FC_N) + q, WAVE);
-        total = v2f::fc_layout((uint8_t*)nullptr, L, base);
-        ok = ok && ((total + 15u) & ~15u) <= g_cap;
-        o = out + g_slot;
-        if (ok && col == 0u) (void)v2f::fc_layout(o, L, base);
-        mb = base[0];
+      for (int q = 0; q < (int)v2f::FC_N; q++) L[q] = (uint32_t)__shfl((int)c.n, (int)(g * v2f::FC_N) + q, WAVE);
+      bool fits = true;
+#pragma unroll
+      for (int q = 0; q < (int)v2f::FC_N; q++) fits = fits && L[q] <= CAP;
+      const uint32_t total = v2f::fc_layout((uint8_t*)nullptr, L, base);
+      ok = ok && fits && ((total + 15u) & ~15u) <= g_cap;
+      if (ok) {
+        uint8_t* o = out + g_slot;
+        if (col == 0u) (void)v2f::fc_layout(o, L, base);
+        uint32_t mb = base[0];
 #pragma unroll
         for (int q = 1; q < (int)v2f::FC_N; q++) mb = col == (uint32_t)q ? base[q] : mb;
+        for (uint32_t i = 0; i < c.n; i++) o[mb + i] = cs[i];   // (the lane's own stores: program order)
       }
-    }
-    if (col == 0u) {
-      if (ok) {
-        fo[d] = g_slot; olen[d] = total; ost[d] = ST_OK; claim[d] = 1;
-        atomicAdd(payload, (unsigned long long)total);
-      } else if (!second) claim[d] = 0;
+      if (col == 0u) {
+        if (ok) {
+          fo[d] = g_slot; olen[d] = total; ost[d] = ST_OK; claim[d] = 1;
+          atomicAdd(payload, (unsigned long long)total);   // payload[0]: bytes, payload[1]: documents claimed
+          atomicAdd(payload + 1, 1ull);
+        } else if (!second) claim[d] = 0;
+      }
     }
   }
 }
+
+// persistent grids: the waves resident at once (their column scratch is reused group after group)
+template <int D, int FIN>
+static uint32_t v12f_grid() {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_v12_fast<D, FIN>, WAVE, 0) != hipSuccess || cus <= 0 || per <= 0)
+    return 2048u;
+  return (uint32_t)(cus * per);
+}
+template <int D, int FIN>
+static size_t v12f_scratch() { return (size_t)v12f_grid<D, FIN>() * D * v2f::FC_N * (FIN + 64); }
+constexpr int V12F_D = 7, V12F_FS = 3584;   // small tier: seven documents of <= 3.5 KB per wave (29 KB of LDS)
 
 __global__ __launch_bounds__(256) void k_v2_status(const int32_t* __restrict__ ust, uint32_t n, int32_t* __restrict__ status,
                                                   uint64_t* __restrict__ len) {
@@ -265,15 +284,21 @@ int ygm_k_launch_v12_count(const uint8_t* v1, const uint64_t* v1_off, const uint
                      L, tot, st, claim);
   return v2_rc(__func__);
 }
+size_t ygm_k_v12_fast_scratch() {
+  const size_t a = v12f_scratch<V12F_D, V12F_FS>(), b = v12f_scratch<2, (int)v2f::F_IN>();
+  return a > b ? a : b;
+}
 int ygm_k_launch_v12_fast(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint64_t* slot_off,
                           const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint8_t* out, uint64_t* fo, uint64_t* olen, int32_t* ost,
-                          uint8_t* claim, unsigned long long* payload, hipStream_t s) {
+                          uint8_t* claim, unsigned long long* payload, uint8_t* scr, hipStream_t s) {
   if (n_docs == 0) return 0;
-  constexpr int D = 7, FS = 3584;   // small tier: seven documents of <= 3.5 KB per wave (29 KB of LDS)
-  hipLaunchKernelGGL((k_v12_fast<D, FS>), dim3((n_docs + D - 1) / D), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd, ust,
-                     n_docs, out, fo, olen, ost, claim, payload, 0);
-  hipLaunchKernelGGL((k_v12_fast<2, (int)v2f::F_IN>), dim3((n_docs + 1) / 2), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd,
-                     ust, n_docs, out, fo, olen, ost, claim, payload, 1);
+  static uint32_t g1 = 0, g2 = 0;
+  if (!g1) { g1 = v12f_grid<V12F_D, V12F_FS>(); g2 = v12f_grid<2, (int)v2f::F_IN>(); }
+  const uint32_t n1 = (n_docs + V12F_D - 1) / V12F_D, n2 = (n_docs + 1) / 2;
+  hipLaunchKernelGGL((k_v12_fast<V12F_D, V12F_FS>), dim3(n1 < g1 ? n1 : g1), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd,
+                     ust, n_docs, out, fo, olen, ost, claim, payload, 0, scr);
+  hipLaunchKernelGGL((k_v12_fast<2, (int)v2f::F_IN>), dim3(n2 < g2 ? n2 : g2), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd,
+                     ust, n_docs, out, fo, olen, ost, claim, payload, 1, scr);
   return v2_rc(__func__);
 }
 int ygm_k_launch_v12_write(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const uint8_t* v2a, uint64_t v2n,

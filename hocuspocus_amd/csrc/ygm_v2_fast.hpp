@@ -133,19 +133,21 @@ YDEV uint32_t f_mode(uint32_t col) {
   return col == FC_LC || col == FC_RC ? FM_IDOR : col == FC_INFO || col == FC_PI ? FM_RLE : col == FC_STR ? FM_STR
        : col == FC_REST ? FM_VU : FM_UOR;
 }
-struct FCS { uint32_t mode, n, count; int64_t s, diff; };   // one column's encoder and byte count
+struct FCS { uint32_t mode, n, count, cap; int64_t s, diff; };   // one column's encoder, byte count, store capacity
 template <class Q>
 YDEV void fc_b(Q out, uint32_t base, FCS& c, uint32_t v) {
-  if (out) out[base + c.n] = (uint8_t)v;   // (out == nullptr: the count pass)
-  c.n++;
+  if (out && c.n < c.cap) out[base + c.n] = (uint8_t)v;   // (out == nullptr: a count pass; past cap: counted only,
+  c.n++;                                                   //  the caller sees c.n > cap and refuses the document)
 }
 template <class Q>
 YDEV void fc_vu(Q out, uint32_t base, FCS& c, uint32_t v) {
+  if (!out) { c.n += 1u + (v > 0x7Fu) + (v > 0x3FFFu) + (v > 0x1FFFFFu) + (v > 0xFFFFFFFu); return; }   // count pass: no loop
   while (v > 127u) { fc_b(out, base, c, 0x80u | (v & 127u)); v >>= 7; }
   fc_b(out, base, c, v);
 }
 template <class Q>
 YDEV void fc_vi(Q out, uint32_t base, FCS& c, uint32_t m, bool neg) {   // lib0 writeVarInt of a magnitude < 2^32
+  if (!out) { c.n += 1u + (m > 0x3Fu) + (m > 0x1FFFu) + (m > 0xFFFFFu) + (m > 0x7FFFFFFu); return; }
   fc_b(out, base, c, (m > 63u ? 0x80u : 0u) | (neg ? 0x40u : 0u) | (m & 63u));
   m >>= 6;
   while (m > 0u) { fc_b(out, base, c, (m > 127u ? 0x80u : 0u) | (m & 127u)); m >>= 7; }
@@ -168,7 +170,7 @@ template <class S, class Q>
 YDEV void fc_push(const S& src, Q out, uint32_t base, FCS& c, uint32_t v, uint32_t off) {
   if (c.mode == FM_VU) { fc_vu(out, base, c, v); return; }
   if (c.mode == FM_STR) {
-    if (out) for (uint32_t i = 0; i < v; i++) out[base + c.n + i] = (uint8_t)src.byte(off + i);
+    if (out) for (uint32_t i = 0; i < v && c.n + i < c.cap; i++) out[base + c.n + i] = (uint8_t)src.byte(off + i);
     c.n += v;
     return;
   }
@@ -199,8 +201,8 @@ YDEV FCand fc_two(bool on, uint32_t v0, uint32_t v1) { return FCand{v0, v1, 0, 0
 // inlined at every value site ran ~20x slower, instruction-fetch bound).
 enum : uint32_t { FP_DOC = 0, FP_BLK, FP_ST, FP_DSH, FP_DSC, FP_DSR, FP_DONE };
 template <class S, class Q>
-YDEV bool f_col_run(const S& src, uint32_t p0, uint32_t n, uint32_t col, Q out, uint32_t base, FCS& c) {
-  c.mode = f_mode(col); c.n = 0; c.count = 0; c.s = c.mode == FM_RLE ? -1 : 0; c.diff = 0;
+YDEV bool f_col_run(const S& src, uint32_t p0, uint32_t n, uint32_t col, Q out, uint32_t base, uint32_t cap, FCS& c) {
+  c.mode = f_mode(col); c.n = 0; c.count = 0; c.cap = cap; c.s = c.mode == FM_RLE ? -1 : 0; c.diff = 0;
   FRd r{p0, n, true};
   const bool rest = col == FC_REST;
   uint32_t ph = FP_DOC, nb = 0, b = 0, ns = 0, st = 0, prev = 0, nd = 0, di = 0, nr = 0, q = 0;
@@ -336,7 +338,7 @@ YDEV bool f_col_run(const S& src, uint32_t p0, uint32_t n, uint32_t col, Q out, 
 // writes the header (version, column lengths) when out != nullptr.  base[FC_*] = each column's offset.
 template <class Q>
 YDEV uint32_t fc_layout(Q out, const uint32_t (&L)[FC_N], uint32_t (&base)[FC_N]) {
-  FCS h{FM_VU, 0u, 0u, 0, 0};
+  FCS h{FM_VU, 0u, 0u, 0xFFFFFFFFu, 0, 0};
   fc_b(out, 0u, h, 0u);                                          // version
   fc_vu(out, 0u, h, 0u);                                         // keyClock (empty)
   const uint32_t pre[5] = {FC_CL, FC_LC, FC_RC, FC_INFO, FC_N};

@@ -46,14 +46,14 @@ int hv_v12f(const uint8_t* v1, uint32_t n, uint8_t* out, uint64_t* out_len) {
   uint32_t L[v2f::FC_N], base[v2f::FC_N];
   v2f::FCS c;
   for (uint32_t col = 0; col < v2f::FC_N; col++) {
-    if (!v2f::f_col_run(src, 0u, n, col, (uint8_t*)nullptr, 0u, c)) return 1;
+    if (!v2f::f_col_run(src, 0u, n, col, (uint8_t*)nullptr, 0u, 0u, c)) return 1;
     L[col] = c.n;
   }
   const uint32_t t = v2f::fc_layout((uint8_t*)nullptr, L, base);
   if (t > v2f::F_OUT) return 2;
   (void)v2f::fc_layout(ob, L, base);
   for (uint32_t col = 0; col < v2f::FC_N; col++)
-    if (!v2f::f_col_run(src, 0u, n, col, ob, base[col], c)) return 3;   // (cannot happen: the count pass took the same path)
+    if (!v2f::f_col_run(src, 0u, n, col, ob, base[col], 0xFFFFFFFFu, c)) return 3;   // (cannot happen: the count pass took the same path)
   memcpy(out, ob, t);
   *out_len = t;
   return 0;

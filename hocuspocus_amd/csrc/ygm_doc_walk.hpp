@@ -111,13 +111,14 @@ YDEV uint64_t dw_at(uint64_t lo, uint64_t hi, uint32_t p) { return p >= 8u ? (hi
 YDEV u32x4 dw_ring16(const DWLds& L, uint32_t l, uint32_t r) {
   const u32x4 a = L.ring[(r >> 4) & (DW_P - 1)][l], b = L.ring[((r >> 4) + 1u) & (DW_P - 1)][l];
   const uint32_t s = (r >> 2) & 3u, sh = r & 3u;
-  const uint32_t D[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  uint32_t E[5];
-#pragma unroll
-  for (int j = 0; j < 5; j++) {
-    const uint32_t x0 = (s & 1u) ? D[j + 1] : D[j], x1 = (s & 1u) ? D[j + 3 < 8 ? j + 3 : 7] : D[j + 2];
-    E[j] = (s & 2u) ? x1 : x0;
-  }
+  // dword s + j of (a, b) for j = 0..4 by bit-mask selects: a ?: over array elements is turned into a
+  // scratch-indexed load by the compiler (one scratch round trip per copy-run head)
+  const uint32_t m0 = 0u - (s & 1u), m1 = 0u - ((s >> 1) & 1u);
+  auto sel4 = [&](uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3) {   // d_s
+    return bsel(m1, bsel(m0, d3, d2), bsel(m0, d1, d0));
+  };
+  const uint32_t E[5] = {sel4(a.x, a.y, a.z, a.w), sel4(a.y, a.z, a.w, b.x), sel4(a.z, a.w, b.x, b.y), sel4(a.w, b.x, b.y, b.z),
+                         sel4(b.x, b.y, b.z, b.w)};
   u32x4 o;
   o.x = __builtin_amdgcn_alignbyte(E[1], E[0], sh);
   o.y = __builtin_amdgcn_alignbyte(E[2], E[1], sh);

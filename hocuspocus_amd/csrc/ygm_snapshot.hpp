@@ -116,7 +116,14 @@ struct Doc {
   YDEV void fail(int e) { if (!err) err = e; }
 
   // ------------------------------------------------------------------ lookups
-  YDEV int32_t cli_slot(uint32_t id) const {   // client table sorted by id
+  uint32_t hint_id; int32_t hint_k;   // the last client looked up (most lookups repeat it: a struct's own client)
+  YDEV int32_t cli_slot(uint32_t id) {   // client table sorted by id
+    if (hint_k >= 0 && hint_id == id) return hint_k;
+    const int32_t k = cli_search(id);
+    if (k >= 0) { hint_id = id; hint_k = k; }
+    return k;
+  }
+  YDEV int32_t cli_search(uint32_t id) const {
     int32_t lo = 0, hi = (int32_t)n_cl - 1;
     while (lo <= hi) {
       const int32_t m = (lo + hi) >> 1;
@@ -125,12 +132,21 @@ struct Doc {
     }
     return -1;
   }
-  YDEV uint32_t state_of(uint32_t id) const { const int32_t k = cli_slot(id); return k < 0 ? 0u : cl[k].state; }
+  YDEV uint32_t state_of(uint32_t id) { const int32_t k = cli_slot(id); return k < 0 ? 0u : cl[k].state; }
   // the integrated part holding (client, clock) (Y@29348 findIndexSS + the split chain); clock < state
   YDEV int32_t find(uint32_t client, uint32_t clock) {
     const int32_t k = cli_slot(client);
     if (k < 0 || clock >= cl[k].state) { fail(ST_UNSUP); return -1; }
     int32_t lo = cl[k].r0, hi = cl[k].r0 + cl[k].ni - 1, r = -1;
+    {   // the last input struct starting at or before clock: first a guess by the clock distance -- exact when the
+        // client's structs before it are single-clock (typed text) -- checked with one round trip of two reads
+        // (each probe of the binary search below is a dependent global-memory read)
+      const int64_t g = (int64_t)lo + ((int64_t)clock - (int64_t)it[lo].clock);
+      if (g >= lo && g <= hi) {
+        const int32_t x = (int32_t)g;
+        if (it[x].clock <= clock && (x == hi || it[x + 1].clock > clock)) { r = x; lo = hi + 1; }
+      }
+    }
     while (lo <= hi) {   // last input struct starting at or before clock
       const int32_t m = (lo + hi) >> 1;
       if (it[m].clock <= clock) { r = m; lo = m + 1; } else hi = m - 1;
@@ -142,7 +158,7 @@ struct Doc {
     return x;
   }
   // the next struct of the same client in clock order
-  YDEV int32_t next_part(int32_t x) const {
+  YDEV int32_t next_part(int32_t x) {
     if (it[x].nxt >= 0) return it[x].nxt;
     const int32_t o = it[x].orig, k = cli_slot(it[x].client);
     return (k >= 0 && o + 1 < cl[k].r0 + cl[k].ni) ? o + 1 : -1;
@@ -251,6 +267,7 @@ struct Doc {
       cl[b] = v;
     }
     for (uint32_t a = 1; a < n_cl; a++) if (cl[a].id == cl[a - 1].id) { fail(ST_UNSUP); return; }
+    hint_k = -1;   // (slots moved)
   }
 
   // ------------------------------------------------------------------ content splice
@@ -683,7 +700,7 @@ struct Doc {
 YDEV_NI int snapshot_doc(const uint8_t* in, uint32_t n, uint32_t flags, uint8_t* ws, const Caps& k, uint32_t& out_off, uint32_t& out_len) {
   Doc D;
   uint8_t* p = ws;
-  D.in = in; D.n = n; D.flags = flags; D.err = 0; D.epoch = 0; D.n_ins = 0;
+  D.in = in; D.n = n; D.flags = flags; D.err = 0; D.epoch = 0; D.n_ins = 0; D.hint_id = 0; D.hint_k = -1;
   D.it = (SI*)p; D.n_it = 0; D.cap_it = k.it; p += al16((uint64_t)k.it * sizeof(SI));
   D.pc = (Piece*)p; D.n_pc = 0; D.cap_pc = k.pc; p += al16((uint64_t)k.pc * sizeof(Piece));
   D.ty = (TypeRec*)p; D.n_ty = 0; D.cap_ty = k.ty; p += al16((uint64_t)k.ty * sizeof(TypeRec));

@@ -273,6 +273,29 @@ def test_wide_lean_kernel_takes_mixed_logs(eng):
     assert s1.docs_lean_wide - s0.docs_lean_wide >= 0.9 * n
 
 
+def test_wide_route_with_deferrals_and_passthrough(eng):
+    # a batch whose average document is past the narrow kernel's staging takes the wide kernel over every document
+    # (the wide route): documents it defers (duplicated updates: overlaps for the general tiers), single-update and
+    # empty documents (passed through) must come out as they do through the narrow route
+    from tools import synth
+    rng = random.Random(9)
+    arena, upd_off, doc_upd = synth.text_updates(1500, 200, 1, 8, del_pct=20, seed=72, max_run=16)
+    ups = synth.split(arena, upd_off)
+    mixed = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(1500)]
+    docs = []
+    for i in range(3000):
+        r = rng.random()
+        m = mixed[i % 1500]
+        docs.append([] if r < 0.04 else [m[0]] if r < 0.12 else m + m[: len(m) // 3] if r < 0.3 else m)
+    assert sum(len(u) for us in docs for u in us) / len(docs) > 5120   # (the wide route's condition)
+    s0 = eng.stats()
+    res = eng.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+    assert not bad, (len(bad), bad[:5])
+    s1 = eng.stats()
+    assert s1.docs_lean_wide - s0.docs_lean_wide > 0 and (s1.docs - s0.docs) - (s1.docs_lean - s0.docs_lean) > 0   # (some deferred)
+
+
 def test_lean_deferrals_beside_single_update_documents(eng):
     # more documents than the narrow kernel's persistent grid, so every wave takes several: single-update
     # and empty documents (passed through, not parsed) between documents the narrow kernel defers must not

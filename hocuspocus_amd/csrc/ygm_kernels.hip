@@ -873,7 +873,7 @@ YDEV_NI void m_parse_update(MergeLds& L, int i, int pass, uint32_t flags) {
     if (c.err) break;
     if (client > 0xFFFFFFFFull) fb = true;
     for (uint64_t s = 0; s < nst && !c.err; s++) {
-      SInfo si; read_struct(c, si, flags);
+      SInfo si; read_struct_fast(c, si, flags);   // (the cursor stays in registers)
       if (c.err) break;
       const uint64_t end = clock + si.len;
       if (end > MAX_SAFE) { c.fail(ST_RANGE); break; }

@@ -36,7 +36,7 @@ struct Stream {
       if (c.err) return;
     }
     structs_left--;
-    read_struct(c, cur, flags);
+    read_struct_fast(c, cur, flags);
     if (c.err) return;
     if (clock + cur.len > MAX_SAFE) { c.fail(ST_RANGE); return; }
     cur_client = client; cur_clock = clock;

@@ -149,7 +149,7 @@ YDEV_NI int contains_doc(const uint8_t* sp, uint32_t sn, const uint8_t* up, uint
   uint32_t nsv = 0;
   for (uint64_t b = 0; b < nb && !c.err; b++) {
     const uint64_t ns = c.vu(), cl = c.vu(); uint64_t ck = c.vu();
-    for (uint64_t s = 0; s < ns && !c.err; s++) { SInfo si; read_struct(c, si, flags); ck += si.len; }
+    for (uint64_t s = 0; s < ns && !c.err; s++) { SInfo si; read_struct_fast(c, si, flags); ck += si.len; }
     if (cl > 0xFFFFFFFFull || ck > 0xFFFFFFFFull) return snap::ST_UNSUP;
     if (snap::al16((uint64_t)(nsv + 2) * sizeof(CtSv)) + 16u > ws_bytes) return snap::ST_UNSUP;
     sv[nsv].client = (uint32_t)cl; sv[nsv].end = (uint32_t)ck; nsv++;
@@ -177,7 +177,7 @@ YDEV_NI int contains_doc(const uint8_t* sp, uint32_t sn, const uint8_t* up, uint
     uint64_t have = 0;
     for (uint32_t i = 0; i < nsv; i++) if (sv[i].client == cl) have = sv[i].end;
     for (uint64_t s = 0; s < ns && !u.err; s++) {
-      SInfo si; read_struct(u, si, flags);
+      SInfo si; read_struct_fast(u, si, flags);
       if (u.err) break;
       ck += si.len;
       if (have < ck) return ST_OK;   // res = 0: a struct past the snapshot

@@ -88,7 +88,7 @@ YDEV_NI void count_doc(const uint8_t* p, uint32_t n, uint32_t flags, uint32_t& S
   for (uint64_t b = 0; b < nb && !c.err; b++) {
     const uint64_t ns = c.vu(); c.vu(); c.vu();
     C++;
-    for (uint64_t s = 0; s < ns && !c.err; s++) { SInfo si; read_struct(c, si, flags); S++; }
+    for (uint64_t s = 0; s < ns && !c.err; s++) { SInfo si; read_struct_fast(c, si, flags); S++; }
   }
   const uint64_t nd = c.err ? 0 : c.vu();
   for (uint64_t k = 0; k < nd && !c.err; k++) {
@@ -209,7 +209,7 @@ struct Doc {
       Cli& k = cl[n_cl++];
       k.id = (uint32_t)client; k.r0 = (int32_t)n_it; k.rn = 0; k.ri = 0; k.state = 0; k.ins = -1; k.ni = 0;
       for (uint64_t s = 0; s < ns && !c.err; s++) {
-        SInfo si; read_struct(c, si, flags);
+        SInfo si; read_struct_fast(c, si, flags);
         if (c.err) break;
         if (clock + si.len > 0xFFFFFFFFull) { fail(ST_UNSUP); return; }
         if (n_it >= cap_it) { fail(ST_NOMEM); return; }

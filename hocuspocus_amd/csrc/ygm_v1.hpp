@@ -511,6 +511,51 @@ YDEV_NI void read_struct(Cur& c, SInfo& s, uint32_t flags) {
   s.end = c.pos;
 }
 
+// read_struct for a cursor that must stay in registers: the shapes of text logs (Skip, GC, an Item with origin(s)
+// and ContentDeleted / ContentString) are read inline with exactly read_struct's reads and results; anything else
+// goes to read_struct through a copy of the cursor (a cursor whose address reaches a non-inlined call lives in
+// scratch memory for the whole function: one scratch round trip per byte read).
+YDEV void read_struct_fast(Cur& c, SInfo& s, uint32_t flags) {
+  const uint32_t p0 = c.pos;
+  if (c.pos < c.end) {
+    const uint8_t info = c.p[c.pos];
+    const uint8_t ref = info & 31;
+    if (info == 10 || ref == 0) {   // Skip / GC: a varuint length
+      c.pos++;
+      s.start = p0; s.nc = false; s.renc = false; s.ref = 0; s.info = info;
+      s.kind = info == 10 ? K_SKIP : K_GC; s.len = c.vu(); s.cstart = c.pos; s.end = c.pos;
+      return;
+    }
+    if ((info & 0xC0) && (ref == 1 || ref == 4)) {
+      c.pos++;
+      s.start = p0; s.nc = false; s.renc = false; s.info = info; s.kind = K_ITEM; s.ref = ref;
+      if (info & 0x80) { c.vu(); c.vu(); }
+      if (info & 0x40) { c.vu(); c.vu(); }
+      if (c.err) return;
+      s.cstart = c.pos;
+      const int nm0 = c.nm; c.nm = 0;
+      if (ref == 1) s.len = c.vu();
+      else {
+        uint32_t l; const uint32_t st = c.buf(l);
+        s.len = 0;
+        if (!c.err) {
+          bool ascii = true;
+          for (uint32_t i = 0; i < l; i++) ascii = ascii && c.p[st + i] < 0x80;
+          const int64_t u = ascii ? (int64_t)l : utf8_u16(c.p + st, l);
+          if (u < 0) c.fail(ST_MALFORMED); else s.len = (uint64_t)u;
+        }
+      }
+      if (c.nm) s.renc = true;
+      c.nm = nm0;
+      s.end = c.pos;
+      return;
+    }
+  }
+  Cur t = c;
+  read_struct(t, s, flags);
+  c = t;
+}
+
 // ---------------------------------------------------------------- writers
 // Output sink: a plain byte pointer (global memory or LDS).  All writers
 // return the number of bytes and, when `o` is non-null, store them.

@@ -25,14 +25,17 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
                      uint64_t* out_len, int32_t* status, unsigned long long* lb, void* meta, uint64_t out_cap, hipStream_t s);
 size_t ygm_k_sv_table_bytes(uint32_t n_docs);
 int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, void* cnt, uint64_t* ws_off,
-                           uint64_t* bs, hipStream_t s);
+                           uint64_t* bs, const uint8_t* claim, hipStream_t s);
+int ygm_k_launch_snap_text(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
+                          uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, hipStream_t s);
 int ygm_k_launch_cont_plan(const uint8_t* st_arena, const uint64_t* st_off, uint32_t n_docs, uint32_t flags, uint64_t* ws_off, uint64_t* bs,
                            hipStream_t s);
 int ygm_k_launch_cont(const uint8_t* st_arena, const uint64_t* st_off, const uint8_t* up_arena, const uint64_t* up_off, uint32_t n_docs,
                       uint32_t flags, const uint64_t* ws_off, uint8_t* ws, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
                       int32_t* status, hipStream_t s);
 int ygm_k_launch_snap(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, const void* cnt, const uint64_t* ws_off,
-                      uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, hipStream_t s);
+                      uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, const uint8_t* claim,
+                      uint64_t base, hipStream_t s);
 int ygm_k_launch_pack(const uint8_t* src, const uint64_t* off, const uint64_t* len, const int32_t* status, uint32_t n, uint64_t* bsum,
                       uint8_t* dst, uint64_t* poff, hipStream_t s);
 int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
@@ -158,7 +161,8 @@ struct ygm_ctx {
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
   DevBuf big_blk, big_rec, big_list;   // large-document tier: block tables, struct records, documents sent on
   DevBuf sv_tbl, sv_tn;                // diff: sorted state-vector tables (k_sv_table) and their entry counts
-  DevBuf sn_cnt, sn_off, sn_bs, sn_ws;  // snapshot: per-document counts, workspace offsets, scan scratch, workspaces
+  DevBuf sn_cnt, sn_off, sn_bs, sn_ws, sn_claim, sn_pay;  // snapshot: per-document counts, workspace offsets, scan scratch,
+  // [LDS-tier output slots | workspaces], LDS-tier claims, its payload / claimed counters
   // update V2: per-update V1 sizes -> offsets, transcoding statuses, scan scratch, the V1 arena, per-document column
   // lengths, the V2 outputs (packed), their offsets / lengths / statuses
   DevBuf v2_len, v2_st, v2_bs, v2_v1, v2_L, v2_out, v2_off, v2_olen, v2_ost, v2_fo, v2_claim, v2_pay, v2_scr;
@@ -233,7 +237,7 @@ void ygm_close(ygm_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
-                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws,
+                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws, &c->sn_claim, &c->sn_pay,
                     &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr})
     b->release();
   for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
@@ -485,28 +489,51 @@ int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_by
   void* meta = c->meta_slot(2);
   HIPCHK(hipMemsetAsync(meta, 0, sizeof(Meta), s));
   HIPCHK(hipEventRecord(c->e0, s));
-  if (ygm_k_launch_snap_plan(d_arena, d_doc_off, n_docs, c->flags, c->sn_cnt.p, c->sn_off.as<uint64_t>(), c->sn_bs.as<uint64_t>(), s))
-    return YGM_EDEVICE;
-  uint64_t total = 0;   // workspace bytes: one read of the scanned total
-  if (n_docs) {
-    HIPCHK(hipMemcpyAsync(c->h_meta, c->sn_off.as<uint64_t>() + n_docs, 8, hipMemcpyDeviceToHost, s));
+  // tier 1: k_snap_text (flat text; input + workspace in LDS) into per-document slots; the documents it leaves go to
+  // the count / scan / k_snap path, whose workspaces follow the slot region
+  const bool lds = n_docs && getenv("YGM_SNAP_NOLDS") == nullptr;
+  const uint64_t slot_total = lds ? 2 * arena_bytes + 64ull * n_docs + 64 : 0;
+  uint64_t lds_pay[2] = {0, 0};
+  if (lds) {
+    if (!c->sn_ws.ensure(slot_total + 64) || !c->sn_claim.ensure((size_t)n_docs + 16) || !c->sn_pay.ensure(16)) return YGM_ENOMEM;
+    HIPCHK(hipMemsetAsync(c->sn_pay.p, 0, 16, s));
+    if (ygm_k_launch_snap_text(d_arena, d_doc_off, n_docs, c->flags, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(),
+                              c->status.as<int32_t>(), c->sn_claim.as<uint8_t>(), c->sn_pay.as<unsigned long long>(), s))
+      return YGM_EDEVICE;
+    HIPCHK(hipMemcpyAsync(c->h_meta, c->sn_pay.p, 16, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    memcpy(&total, c->h_meta, 8);
+    memcpy(lds_pay, c->h_meta, 16);
   }
-  if (!c->sn_ws.ensure(total + 64)) return YGM_ENOMEM;
-  if (ygm_k_launch_snap(d_arena, d_doc_off, n_docs, c->flags, c->sn_cnt.p, c->sn_off.as<uint64_t>(), c->sn_ws.as<uint8_t>(),
-                        c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
-                        (unsigned long long*)((uint8_t*)meta + offsetof(Meta, payload)), s))
-    return YGM_EDEVICE;
-  HIPCHK(hipEventRecord(c->e1, s));
+  uint64_t total = 0;   // workspace bytes: one read of the scanned total
   Meta m;
-  int e = read_meta(c, s, m, meta);
-  if (e) return e;
+  memset(&m, 0, sizeof(m));
+  if (!lds || lds_pay[1] < n_docs) {
+    const uint8_t* claim = lds ? c->sn_claim.as<uint8_t>() : nullptr;
+    if (ygm_k_launch_snap_plan(d_arena, d_doc_off, n_docs, c->flags, c->sn_cnt.p, c->sn_off.as<uint64_t>(), c->sn_bs.as<uint64_t>(), claim, s))
+      return YGM_EDEVICE;
+    if (n_docs) {
+      HIPCHK(hipMemcpyAsync(c->h_meta, c->sn_off.as<uint64_t>() + n_docs, 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      memcpy(&total, c->h_meta, 8);
+    }
+    if (!c->sn_ws.ensure(slot_total + total + 64, slot_total, s)) return YGM_ENOMEM;
+    if (ygm_k_launch_snap(d_arena, d_doc_off, n_docs, c->flags, c->sn_cnt.p, c->sn_off.as<uint64_t>(), c->sn_ws.as<uint8_t>(),
+                          c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
+                          (unsigned long long*)((uint8_t*)meta + offsetof(Meta, payload)), claim, slot_total, s))
+      return YGM_EDEVICE;
+    HIPCHK(hipEventRecord(c->e1, s));
+    int e = read_meta(c, s, m, meta);
+    if (e) return e;
+  } else {
+    HIPCHK(hipEventRecord(c->e1, s));
+    HIPCHK(hipEventSynchronize(c->e1));
+  }
+  m.payload += lds_pay[0];
   float ms = 0;
   if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;
   c->stats.calls++; c->stats.docs += n_docs; c->stats.bytes_in += arena_bytes; c->stats.bytes_out += m.payload;
   out->data = c->sn_ws.as<uint8_t>(); out->off = c->out_off.as<uint64_t>(); out->len = c->out_len.as<uint64_t>();
-  out->status = c->status.as<int32_t>(); out->data_bytes = total; out->payload_bytes = m.payload;
+  out->status = c->status.as<int32_t>(); out->data_bytes = slot_total + total; out->payload_bytes = m.payload;
   return YGM_OK;
 }
 

@@ -1,0 +1,409 @@
+// ygm_snap_text.hpp -- the doc-normalized snapshot of ygm_snapshot.hpp (SURVEY.md §8f-1,
+// encodeStateAsUpdate(applyUpdate(new Doc, u))) for documents of flat text, over a compact workspace that fits in
+// LDS next to the document's bytes.
+//
+// Why: the general kernel's integration is a serial chain of dependent accesses into a per-document workspace in
+// global memory (≈ 1 µs a step; a 160-struct document takes ≈ 10 ms however many documents run beside it).  Here
+// the same steps run on 28-byte part records in LDS.
+//
+// Envelope (anything else returns false and the document goes to the general kernel, which decides its status):
+// Items with ContentDeleted / ASCII ContentString only (no GC, Skip, types, maps, embeds), items without origins
+// under one root type named in the update (no parent ids, no parentSub), <= 16 client blocks (distinct), every
+// client's clocks < 2^16, input < 64 KiB, the parts (input structs + splits) within the workspace, an update that
+// integrates completely (no pending structs or delete set).  Inside it every step is ygm_snapshot.hpp's (cited
+// there against yjs 13.5.16), specialised:
+//   * parts: the struct store's items and their split parts (Doc::it), ids of origins as (client slot, clock);
+//   * one root type: its list head (TypeRec::start); no nested types, so Item.delete is a flag and the GC of a
+//     deleted item (tryGcDeleteSet) turns its content into ContentDeleted -- done for every deleted part at once
+//     (every deleted part lies in a range the transaction's delete set recorded);
+//   * ASCII content: a part's bytes are its input slice [coff, coff + clen); a split cuts the slice at the clock
+//     offset, and a merged part's bytes are its own slice followed by those of the parts it absorbed (they follow
+//     it in the client's clock order), so no piece lists.
+#pragma once
+#include "ygm_snapshot.hpp"
+
+namespace ygm {
+namespace snapt {
+
+constexpr uint16_t NIL = 0xFFFFu;
+constexpr uint32_t CMAX = 16;
+enum : uint8_t { T_HO = 1, T_HR = 2, T_DEL = 4, T_INT = 8, T_GONE = 16, T_STR = 32 };
+
+struct P {                         // a part: Doc::SI for flat text (28 bytes)
+  uint16_t clock, len, ok, rk;     // id clock and length, origin / right origin clocks
+  uint16_t left, right, nxt, orig; // document list, next split part, input struct
+  uint16_t coff, clen, ms, mr;     // own ASCII slice, integrate's conflict marks (epochs)
+  uint8_t cl, ocl, rcl, fl;        // client slot (block order), origin / right origin client slots, T_* flags
+};
+struct CT { uint32_t id, state; uint16_t r0, rn, ri, ni; int16_t ins, pad; };
+
+// workspace bytes besides the input: client table, id order, parts and their sequence / stack array
+YDEV uint32_t ws_fixed() { return CMAX * (uint32_t)sizeof(CT) + CMAX; }
+YDEV uint32_t part_bytes() { return (uint32_t)sizeof(P) + 2u; }
+
+struct TDoc {
+  const uint8_t* in; uint32_t n, flags;
+  P* p; uint32_t np, cap;
+  CT* ct; uint8_t* ord; uint32_t nc;
+  uint16_t* sq;
+  uint32_t name_off, name_len, ds_pos, epoch, n_ins;
+  uint16_t start;
+  bool have_name, bad;
+
+  YDEV int slot(uint32_t id) const {
+    for (uint32_t k = 0; k < nc; k++) if (ct[k].id == id) return (int)k;
+    return -1;
+  }
+
+  // ------------------------------------------------------------------ read (Doc::parse)
+  YDEV void parse() {
+    Cur c{in, 0, n, 0, 0};
+    const uint64_t nb = c.vu();
+    for (uint64_t b = 0; b < nb && !c.err && !bad; b++) {
+      const uint64_t ns = c.vu(), client = c.vu(); uint64_t clock = c.vu();
+      if (c.err || client > 0xFFFFFFFFull || nc >= CMAX || slot((uint32_t)client) >= 0) { bad = true; return; }
+      CT& k = ct[nc];
+      k.id = (uint32_t)client; k.state = 0; k.r0 = (uint16_t)np; k.rn = 0; k.ri = 0; k.ni = 0; k.ins = -1; k.pad = 0;
+      for (uint64_t s = 0; s < ns && !bad; s++) {
+        SInfo si; read_struct_fast(c, si, flags);
+        if (c.err || si.kind != K_ITEM || (si.ref != 1 && si.ref != 4) || si.nc || si.len == 0 || clock + si.len > 0xFFFFull ||
+            np >= cap) { bad = true; return; }
+        P& x = p[np];
+        x.clock = (uint16_t)clock; x.len = (uint16_t)si.len; x.orig = (uint16_t)np; x.nxt = NIL;
+        x.left = x.right = 0; x.ms = x.mr = 0; x.ok = x.rk = 0; x.ocl = x.rcl = 0; x.cl = (uint8_t)nc;
+        x.fl = si.ref == 4 ? T_STR : 0; x.coff = 0; x.clen = 0;
+        Cur h{in, si.start + 1, si.cstart, 0, 0};
+        const uint8_t info = si.info;
+        if (info & 0x80) {   // origin id: the client id parks in (ms, mr) until the client table is complete
+          const uint64_t oc = h.vu(), ok = h.vu();
+          if (oc > 0xFFFFFFFFull || ok > 0xFFFFull) { bad = true; return; }
+          x.ms = (uint16_t)(oc >> 16); x.mr = (uint16_t)oc; x.ok = (uint16_t)ok; x.fl |= T_HO;
+        }
+        if (info & 0x40) {   // right origin: the client id parks in (left, right)
+          const uint64_t rc = h.vu(), rk = h.vu();
+          if (rc > 0xFFFFFFFFull || rk > 0xFFFFull) { bad = true; return; }
+          x.left = (uint16_t)(rc >> 16); x.right = (uint16_t)rc; x.rk = (uint16_t)rk; x.fl |= T_HR;
+        }
+        if ((info & 0xC0) == 0) {   // the root type by name, the same one for the whole update
+          if (h.vu() != 1 || (info & 0x20)) { bad = true; return; }
+          uint32_t l; const uint32_t s0 = h.buf(l);
+          if (h.err) { bad = true; return; }
+          if (!have_name) { name_off = s0; name_len = l; have_name = true; }
+          else {
+            if (l != name_len) { bad = true; return; }
+            for (uint32_t i = 0; i < l; i++) if (in[s0 + i] != in[name_off + i]) { bad = true; return; }
+          }
+        }
+        if (h.err) { bad = true; return; }
+        if (si.ref == 4) {   // ASCII: UTF-16 length == bytes
+          Cur q{in, si.cstart, si.end, 0, 0};
+          uint32_t l; const uint32_t s0 = q.buf(l);
+          if (q.err || l != si.len) { bad = true; return; }
+          x.coff = (uint16_t)s0; x.clen = (uint16_t)l;
+        }
+        clock += si.len;
+        np++; k.rn++;
+      }
+      nc++;
+    }
+    if (c.err || bad) { bad = true; return; }
+    ds_pos = c.pos;
+    const uint64_t nd = c.vu();
+    for (uint64_t q = 0; q < nd && !c.err; q++) {
+      const uint64_t client = c.vu(), nr = c.vu();
+      for (uint64_t r = 0; r < nr && !c.err; r++) {
+        const uint64_t ck = c.vu(), ln = c.vu();
+        if (client > 0xFFFFFFFFull || ck + ln > 0xFFFFFFFFull) { bad = true; return; }
+      }
+    }
+    if (c.err) { bad = true; return; }
+    for (uint32_t i = 0; i < np; i++) {   // origin client ids -> slots (an unknown client leaves the item pending)
+      P& x = p[i];
+      if (x.fl & T_HO) { const int k = slot(((uint32_t)x.ms << 16) | x.mr); if (k < 0) { bad = true; return; } x.ocl = (uint8_t)k; }
+      if (x.fl & T_HR) { const int k = slot(((uint32_t)x.left << 16) | x.right); if (k < 0) { bad = true; return; } x.rcl = (uint8_t)k; }
+      x.ms = x.mr = 0; x.left = x.right = NIL;
+    }
+    for (uint32_t a = 0; a < nc; a++) ord[a] = (uint8_t)a;   // slots by id
+    for (uint32_t a = 1; a < nc; a++) {
+      const uint8_t v = ord[a]; uint32_t b = a;
+      while (b > 0 && ct[ord[b - 1]].id > ct[v].id) { ord[b] = ord[b - 1]; b--; }
+      ord[b] = v;
+    }
+  }
+
+  // ------------------------------------------------------------------ lookups and splits (Doc::find / split)
+  YDEV uint16_t find(uint32_t k, uint32_t clock) {
+    if (clock >= ct[k].state) { bad = true; return NIL; }
+    int32_t lo = ct[k].r0, hi = (int32_t)ct[k].r0 + ct[k].ni - 1, r = -1;
+    {
+      const int32_t g = lo + ((int32_t)clock - (int32_t)p[lo].clock);
+      if (g >= lo && g <= hi && p[g].clock <= clock && (g == hi || p[g + 1].clock > clock)) { r = g; lo = hi + 1; }
+    }
+    while (lo <= hi) {
+      const int32_t m = (lo + hi) >> 1;
+      if (p[m].clock <= clock) { r = m; lo = m + 1; } else hi = m - 1;
+    }
+    if (r < 0) { bad = true; return NIL; }
+    uint16_t x = (uint16_t)r;
+    while (x != NIL && !(clock < (uint32_t)p[x].clock + p[x].len)) x = p[x].nxt;
+    if (x == NIL) bad = true;
+    return x;
+  }
+  YDEV uint16_t next_part(uint16_t x) const {
+    if (p[x].nxt != NIL) return p[x].nxt;
+    const CT& k = ct[p[x].cl];
+    return (uint32_t)p[x].orig + 1 < (uint32_t)k.r0 + k.ni ? (uint16_t)(p[x].orig + 1) : NIL;
+  }
+  YDEV uint16_t split(uint16_t x, uint32_t diff) {   // x keeps [0, diff)
+    if (np >= cap) { bad = true; return NIL; }
+    const uint16_t r = (uint16_t)np++;
+    P b = p[x];
+    b.clock = (uint16_t)(b.clock + diff); b.len = (uint16_t)(b.len - diff);
+    b.left = x; b.ocl = p[x].cl; b.ok = (uint16_t)(p[x].clock + diff - 1);
+    b.fl = (uint8_t)((p[x].fl & (T_DEL | T_HR | T_INT | T_STR)) | T_HO);
+    b.ms = b.mr = 0;
+    if (b.fl & T_STR) { b.coff = (uint16_t)(b.coff + diff); b.clen = (uint16_t)(b.clen - diff); p[x].clen = (uint16_t)diff; }
+    b.nxt = p[x].nxt;
+    p[r] = b;
+    p[x].nxt = r; p[x].right = r; p[x].len = (uint16_t)diff;
+    if (b.right != NIL) p[b.right].left = r;
+    return r;
+  }
+  YDEV uint16_t clean_end(uint32_t k, uint32_t clock) {
+    const uint16_t x = find(k, clock);
+    if (x != NIL && clock != (uint32_t)p[x].clock + p[x].len - 1) split(x, clock - p[x].clock + 1);
+    return x;
+  }
+  YDEV uint16_t clean_start(uint32_t k, uint32_t clock) {
+    const uint16_t x = find(k, clock);
+    if (x != NIL && p[x].clock < clock) return split(x, clock - p[x].clock);
+    return x;
+  }
+
+  // ------------------------------------------------------------------ integration (Doc::get_missing / integrate)
+  YDEV int get_missing(uint16_t x) {
+    const uint8_t fl = p[x].fl, cl = p[x].cl;
+    if ((fl & T_HO) && p[x].ocl != cl && p[x].ok >= ct[p[x].ocl].state) return p[x].ocl;
+    if ((fl & T_HR) && p[x].rcl != cl && p[x].rk >= ct[p[x].rcl].state) return p[x].rcl;
+    if (fl & T_HO) { const uint16_t l = clean_end(p[x].ocl, p[x].ok); p[x].left = l; }
+    if (fl & T_HR) { const uint16_t r = clean_start(p[x].rcl, p[x].rk); p[x].right = r; }
+    return -1;
+  }
+  YDEV bool same(bool ha, uint32_t ac, uint32_t ak, bool hb, uint32_t bc, uint32_t bk) const {
+    return (!ha && !hb) || (ha && hb && ac == bc && ak == bk);
+  }
+  YDEV void integrate(uint16_t x) {
+    const uint8_t fl = p[x].fl;
+    const bool ho = fl & T_HO, hr = fl & T_HR;
+    const uint32_t oc = p[x].ocl, ok = p[x].ok, rc = p[x].rcl, rk = p[x].rk, myid = ct[p[x].cl].id;
+    uint16_t left = p[x].left;
+    const uint16_t right = p[x].right;
+    if ((left == NIL && (right == NIL || p[right].left != NIL)) || (left != NIL && p[left].right != right)) {
+      uint16_t e = left;
+      uint16_t o = left != NIL ? p[left].right : start;
+      if (epoch >= 0xFF00u) { bad = true; return; }
+      const uint32_t eR = ++epoch;
+      uint32_t curS = eR;
+      while (o != NIL && o != right) {
+        p[o].mr = (uint16_t)eR; p[o].ms = (uint16_t)curS;
+        const uint8_t f2 = p[o].fl;
+        if (same(ho, oc, ok, f2 & T_HO, p[o].ocl, p[o].ok)) {
+          if (ct[p[o].cl].id < myid) { e = o; curS = ++epoch; }
+          else if (same(hr, rc, rk, f2 & T_HR, p[o].rcl, p[o].rk)) break;
+        } else if (f2 & T_HO) {
+          const uint16_t g = find(p[o].ocl, p[o].ok);
+          if (bad) return;
+          if (p[g].mr == (uint16_t)eR) { if (p[g].ms != (uint16_t)curS) { e = o; curS = ++epoch; } }
+          else break;
+        } else break;
+        if (epoch >= 0xFF00u) { bad = true; return; }
+        o = p[o].right;
+      }
+      left = e;
+      p[x].left = e;
+    }
+    uint16_t r;
+    if (left != NIL) { r = p[left].right; p[left].right = x; }
+    else { r = start; start = x; }
+    p[x].right = r;
+    if (r != NIL) p[r].left = x;
+    CT& k = ct[p[x].cl];   // addStruct
+    if (k.ins < 0) k.ins = (int16_t)n_ins++;
+    k.state = (uint32_t)p[x].clock + p[x].len;
+    k.ni = (uint16_t)(p[x].orig - k.r0 + 1);
+    p[x].fl = (uint8_t)(fl | T_INT | ((fl & T_STR) ? 0 : T_DEL));   // ContentDeleted.integrate: deleted at once
+  }
+  YDEV void integrate_all() {   // Doc::integrate_all: highest client first, the dependency stack
+    int32_t ci = (int32_t)nc - 1;
+    auto next_client = [&]() -> int32_t {
+      while (ci >= 0 && ct[ord[ci]].ri >= ct[ord[ci]].rn) ci--;
+      return ci;
+    };
+    int32_t cur = next_client();
+    if (cur < 0) return;
+    uint16_t u = (uint16_t)(ct[ord[cur]].r0 + ct[ord[cur]].ri++);
+    uint32_t sp = 0;
+    for (;;) {
+      if (bad) return;
+      const CT& k = ct[p[u].cl];
+      const int64_t diff = (int64_t)k.state - (int64_t)p[u].clock;
+      if (diff < 0) { bad = true; return; }
+      const int m = get_missing(u);
+      if (bad) return;
+      if (m >= 0) {
+        if (sp >= cap || ct[m].ri >= ct[m].rn) { bad = true; return; }
+        sq[sp++] = u;
+        u = (uint16_t)(ct[m].r0 + ct[m].ri++);
+        continue;
+      }
+      if (diff != 0) { bad = true; return; }
+      integrate(u);
+      if (sp) u = sq[--sp];
+      else if (cur >= 0 && ct[ord[cur]].ri < ct[ord[cur]].rn) u = (uint16_t)(ct[ord[cur]].r0 + ct[ord[cur]].ri++);
+      else {
+        cur = next_client();
+        if (cur < 0) break;
+        u = (uint16_t)(ct[ord[cur]].r0 + ct[ord[cur]].ri++);
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------ delete set, GC, merge (Doc::apply_ds ..)
+  YDEV void apply_ds() {
+    Cur c{in, ds_pos, n, 0, 0};
+    const uint64_t nd = c.vu();
+    for (uint64_t q = 0; q < nd && !bad; q++) {
+      const uint32_t client = (uint32_t)c.vu(); const uint64_t nr = c.vu();
+      const int k = slot(client);
+      for (uint64_t r = 0; r < nr && !bad; r++) {
+        const uint64_t a = c.vu(), b = a + c.vu();
+        if (k < 0) { bad = true; return; }   // (state 0: pending)
+        const uint32_t s = ct[k].state;
+        if (!(a < s) || s < b) { bad = true; return; }
+        uint16_t x = find((uint32_t)k, (uint32_t)a);
+        if (bad) return;
+        if (!(p[x].fl & T_DEL) && p[x].clock < a) { split(x, (uint32_t)a - p[x].clock); x = p[x].nxt; }
+        while (x != NIL && !bad) {
+          if (p[x].clock < b) {
+            if (!(p[x].fl & T_DEL)) {
+              if (b < (uint64_t)p[x].clock + p[x].len) split(x, (uint32_t)b - p[x].clock);
+              p[x].fl |= T_DEL;
+            }
+          } else break;
+          x = next_part(x);
+        }
+      }
+    }
+  }
+  // the client's parts in clock order into sq (GONE ones included when all); returns the count
+  YDEV uint32_t client_seq(uint32_t k, bool all) {
+    uint32_t m = 0;
+    for (uint32_t o = ct[k].r0; o < (uint32_t)ct[k].r0 + ct[k].ni; o++)
+      for (uint16_t x = (uint16_t)o; x != NIL; x = p[x].nxt)
+        if (all || !(p[x].fl & T_GONE)) sq[m++] = x;
+    return m;
+  }
+  YDEV void gc_merge() {
+    for (uint32_t i = 0; i < np; i++) if (p[i].fl & T_DEL) p[i].fl = (uint8_t)(p[i].fl & ~T_STR);   // tryGcDeleteSet
+    for (uint32_t k = 0; k < nc; k++) {   // one right-to-left tryToMergeWithLeft pass per client
+      const uint32_t m = client_seq(k, false);
+      for (uint32_t e = m; e-- > 1;) {
+        const uint16_t a = sq[e - 1], b = sq[e];
+        const P& L = p[a]; const P& R = p[b];
+        if (((L.fl ^ R.fl) & (T_DEL | T_STR)) != 0) continue;
+        if (!((R.fl & T_HO) && R.ocl == L.cl && R.ok == (uint32_t)L.clock + L.len - 1)) continue;
+        if (L.right != b) continue;
+        if (!same(L.fl & T_HR, L.rcl, L.rk, R.fl & T_HR, R.rcl, R.rk)) continue;
+        if ((uint32_t)L.clock + L.len != R.clock) continue;
+        const uint16_t rr = R.right;
+        p[a].right = rr;
+        if (rr != NIL) p[rr].left = a;
+        p[a].len = (uint16_t)(p[a].len + p[b].len);
+        p[b].fl |= T_GONE;
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------ encodeStateAsUpdate (Doc::encode)
+  template <class O>
+  YDEV void encode(O& o) {
+    uint32_t cnt = 0;
+    for (uint32_t k = 0; k < nc; k++) cnt += ct[k].ni > 0 ? 1u : 0u;
+    o.vu(cnt);
+    for (uint32_t i = nc; i-- > 0;) {
+      const uint32_t k = ord[i];
+      if (!ct[k].ni) continue;
+      const uint32_t m = client_seq(k, true);
+      uint32_t live = 0;
+      for (uint32_t j = 0; j < m; j++) live += (p[sq[j]].fl & T_GONE) ? 0u : 1u;
+      o.vu(live); o.vu(ct[k].id); o.vu(p[sq[0]].clock);
+      for (uint32_t j = 0; j < m; j++) {
+        const P& u = p[sq[j]];
+        if (!(u.fl & T_GONE)) {
+          const bool ho = u.fl & T_HO, hr = u.fl & T_HR;
+          o.b((uint8_t)(((u.fl & T_STR) ? 4 : 1) | (ho ? 0x80 : 0) | (hr ? 0x40 : 0)));
+          if (ho) { o.vu(ct[u.ocl].id); o.vu(u.ok); }
+          if (hr) { o.vu(ct[u.rcl].id); o.vu(u.rk); }
+          if (!ho && !hr) { o.b(1); o.vu(name_len); o.copy(in + name_off, name_len); }
+          o.vu(u.len);
+        }
+        if (u.fl & T_STR) o.copy(in + u.coff, u.clen);   // a merged part's bytes: its own, then those it absorbed
+      }
+    }
+    // delete set from the struct store: runs of deleted parts; clients in store order (13.5) or descending (13.6)
+    uint32_t nds = 0;
+    for (uint32_t k = 0; k < nc; k++) {
+      if (!ct[k].ni) continue;
+      const uint32_t m = client_seq(k, false);
+      for (uint32_t j = 0; j < m; j++) if (p[sq[j]].fl & T_DEL) { nds++; break; }
+    }
+    o.vu(nds);
+    for (uint32_t r = 0; r < nc; r++) {
+      int32_t k = -1;
+      if (flags & F_COMPAT_135) { for (uint32_t j = 0; j < nc; j++) if (ct[j].ins == (int32_t)r) k = (int32_t)j; }
+      else k = ord[nc - 1 - r];
+      if (k < 0 || !ct[k].ni) continue;
+      const uint32_t m = client_seq((uint32_t)k, false);
+      uint32_t runs = 0;
+      for (uint32_t j = 0; j < m; j++) if ((p[sq[j]].fl & T_DEL) && (j == 0 || !(p[sq[j - 1]].fl & T_DEL))) runs++;
+      if (!runs) continue;
+      o.vu(ct[k].id); o.vu(runs);
+      for (uint32_t j = 0; j < m;) {
+        if (!(p[sq[j]].fl & T_DEL)) { j++; continue; }
+        const uint32_t c0 = p[sq[j]].clock; uint32_t len = 0;
+        while (j < m && (p[sq[j]].fl & T_DEL)) len += p[sq[j++]].len;
+        o.vu(c0); o.vu(len);
+      }
+    }
+  }
+
+  template <class O>
+  YDEV bool run(O& o) {
+    parse();
+    if (!bad) integrate_all();
+    if (!bad) apply_ds();
+    if (!bad) gc_merge();
+    if (bad) return false;
+    encode(o);
+    return true;
+  }
+};
+
+// The snapshot of in[0, n) over a workspace of ws_bytes at ws (4-aligned), written through o (OutCap: stops at its
+// cap); false: outside the envelope or the workspace (the general kernel takes the document).
+template <class O>
+YDEV bool snapshot_text(const uint8_t* in, uint32_t n, uint32_t flags, uint8_t* ws, uint32_t ws_bytes, O& o) {
+  if (n >= 0xFFFFu || ws_bytes < ws_fixed() + 16u * part_bytes()) return false;
+  TDoc D;
+  D.in = in; D.n = n; D.flags = flags;
+  D.ct = (CT*)ws; D.ord = ws + CMAX * sizeof(CT); D.nc = 0;
+  D.cap = (ws_bytes - ws_fixed()) / part_bytes();
+  if (D.cap > 0xFFF0u) D.cap = 0xFFF0u;
+  D.p = (P*)(ws + ws_fixed()); D.np = 0;
+  D.sq = (uint16_t*)(ws + ws_fixed() + D.cap * (uint32_t)sizeof(P));
+  D.name_off = D.name_len = 0; D.ds_pos = 0; D.epoch = 0; D.n_ins = 0; D.start = NIL; D.have_name = false; D.bad = false;
+  return D.run(o);
+}
+
+}  // namespace snapt
+}  // namespace ygm

@@ -1,5 +1,6 @@
-// ygm_snapshot.hip -- doc-normalized snapshot kernels: one thread per document runs
-// ygm_snapshot.hpp over a workspace carved from one device arena.
+// ygm_snapshot.hip -- doc-normalized snapshot kernels:
+//   k_snap_text  : flat-text documents (ygm_snap_text.hpp), one per wave, input + workspace in LDS, into slots;
+//                  the documents it leaves take the general path below
 //   k_snap_count : per document, the struct / delete-range / client-block counts -> workspace bytes
 //   k_snap_scan* : exclusive scan of the workspace sizes (three launches, 256 documents per block)
 //   k_snap       : per document, integrate + gc + merge + encode into its workspace's output region
@@ -12,6 +13,7 @@
 
 #include "ygm_common.hpp"
 #include "ygm_snapshot.hpp"
+#include "ygm_snap_text.hpp"
 
 namespace ygm {
 
@@ -37,14 +39,46 @@ YDEV const uint8_t* snap_stage(uint8_t* stg, const uint8_t* __restrict__ arena, 
   return staged && x >= a && doc_off[d + 1] <= b ? stg + (x - a16) : arena + x;
 }
 
+// k_snap_text: one document per workgroup (one wave): the lanes stage its bytes into LDS, lane 0 runs the flat-text
+// snapshot (ygm_snap_text.hpp) over a workspace in the rest of the workgroup's LB bytes of LDS -- the integration's
+// dependent chain as LDS round trips instead of global ones, LB small enough for many documents per CU.  Documents
+// outside the envelope or the workspace are left unclaimed for the count / scan / k_snap path.  Outputs go to
+// per-document slots at align16(2 * doc_off[d] + 64 * d), 2n + 48 bytes each.
+template <uint32_t LB>
+__global__ __launch_bounds__(SN_NT) void k_snap_text(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off, uint32_t n_docs,
+                                                    uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
+                                                    uint64_t* __restrict__ out_len, int32_t* __restrict__ status, uint8_t* __restrict__ claim,
+                                                    unsigned long long* __restrict__ pay) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LB];
+  const uint32_t d = blockIdx.x;
+  const uint64_t a = doc_off[d], b = doc_off[d + 1];
+  const uint64_t a16 = a & ~15ull, sb = (b - a16 + 15u) & ~15ull;
+  if (b <= a || sb + 1024u > LB) { if (threadIdx.x == 0) claim[d] = 0; return; }
+  const uint4* src = (const uint4*)(arena + a16);
+  for (uint32_t c = threadIdx.x; 16u * c < sb; c += SN_NT) ((uint4*)lds)[c] = src[c];   // (arena tail padding >= 16)
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const uint32_t n = (uint32_t)(b - a);
+  const uint64_t slot = snap::al16(2 * a + 64ull * d);
+  snap::OutCap o{out + slot, 0, 2u * n + 48u};
+  const bool ok = snapt::snapshot_text(lds + (a - a16), n, flags, lds + sb, LB - (uint32_t)sb, o) && o.n <= o.cap;
+  if (ok) {
+    out_off[d] = slot; out_len[d] = o.n; status[d] = ST_OK;
+    atomicAdd(pay, (unsigned long long)o.n);
+    atomicAdd(pay + 1, 1ull);
+  }
+  claim[d] = ok ? 1 : 0;
+}
+
 __global__ __launch_bounds__(SN_NT) void k_snap_count(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off,
                                                      uint32_t n_docs, uint32_t flags, uint4* __restrict__ cnt,
-                                                     uint64_t* __restrict__ need) {
+                                                     uint64_t* __restrict__ need, const uint8_t* __restrict__ claim) {
   __shared__ __attribute__((aligned(16))) uint8_t stg[SN_STAGE + 16];
   const uint32_t d0 = blockIdx.x * SN_DPW, d1 = d0 + SN_DPW < n_docs ? d0 + SN_DPW : n_docs;
   const uint32_t d = d0 + threadIdx.x;
   const uint8_t* in = snap_stage(stg, arena, doc_off, d0, d1, threadIdx.x < SN_DPW ? d : d1);
   if (threadIdx.x >= SN_DPW || d >= n_docs) return;
+  if (claim && claim[d]) { cnt[d] = make_uint4(0, 0, 0, 0); need[d] = 0; return; }   // k_snap_text wrote it
   const uint64_t a = doc_off[d], b = doc_off[d + 1];
   uint32_t S = 0, D = 0, C = 0;
   const uint32_t n = b > a && b - a < (1ull << 30) ? (uint32_t)(b - a) : 0u;
@@ -89,7 +123,8 @@ __global__ __launch_bounds__(256) void k_snap_scan_apply(uint64_t* __restrict__ 
 __global__ __launch_bounds__(SN_NT) void k_snap(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off, uint32_t n_docs,
                                                uint32_t flags, const uint4* __restrict__ cnt, const uint64_t* __restrict__ ws_off,
                                                uint8_t* __restrict__ ws, uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len,
-                                               int32_t* __restrict__ status, unsigned long long* __restrict__ payload, uint32_t dpw) {
+                                               int32_t* __restrict__ status, unsigned long long* __restrict__ payload, uint32_t dpw,
+                                               const uint8_t* __restrict__ claim, uint64_t base) {
   // dpw documents per wave (lanes >= dpw idle): the per-document code diverges from lane to lane, so
   // fewer documents per wave trade SIMD lanes for less serialised divergence and more waves in flight
   __shared__ __attribute__((aligned(16))) uint8_t stg[SN_STAGE + 16];
@@ -97,7 +132,7 @@ __global__ __launch_bounds__(SN_NT) void k_snap(const uint8_t* __restrict__ aren
   const uint32_t d = d0 + threadIdx.x;
   const uint8_t* in = snap_stage(stg, arena, doc_off, d0, d1, threadIdx.x < dpw ? d : d1);
   uint64_t mine = 0;
-  if (threadIdx.x < dpw && d < n_docs) {
+  if (threadIdx.x < dpw && d < n_docs && !(claim && claim[d])) {
     const uint4 c = cnt[d];
     const uint64_t a = doc_off[d], b = doc_off[d + 1];
     int st = ST_OK;
@@ -106,9 +141,9 @@ __global__ __launch_bounds__(SN_NT) void k_snap(const uint8_t* __restrict__ aren
     else if (c.w == 0) st = ST_MALFORMED;   // (an empty update: yjs throws reading it)
     else {
       const snap::Caps k = snap::caps_of(c.x, c.y, c.z, c.w);
-      st = snap::snapshot_doc(in, c.w, flags, ws + ws_off[d], k, oo, ol);
+      st = snap::snapshot_doc(in, c.w, flags, ws + base + ws_off[d], k, oo, ol);
     }
-    out_off[d] = ws_off[d] + oo;
+    out_off[d] = base + ws_off[d] + oo;
     out_len[d] = st == ST_OK ? ol : 0u;
     status[d] = st;
     mine = st == ST_OK ? ol : 0u;
@@ -229,11 +264,22 @@ static int snap_rc(const char* fn) {
 
 // phase 1: counts and the scanned workspace offsets (ws_off: n_docs + 1 entries, total at [n_docs];
 // bs: ceil(n / 256) + 1 scratch entries)
+int ygm_k_launch_snap_text(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
+                           uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, hipStream_t s) {
+  if (n_docs == 0) return 0;
+  const char* env = getenv("YGM_SNAP_LB");   // KiB of LDS per document (experiments; 12 by default)
+  const int lb = env ? atoi(env) : 12;
+  if (lb == 8) hipLaunchKernelGGL(k_snap_text<8192>, dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
+  else if (lb == 16) hipLaunchKernelGGL(k_snap_text<16384>, dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
+  else if (lb == 32) hipLaunchKernelGGL(k_snap_text<32768>, dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
+  else hipLaunchKernelGGL(k_snap_text<12288>, dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
+  return snap_rc(__func__);
+}
 int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, void* cnt, uint64_t* ws_off,
-                           uint64_t* bs, hipStream_t s) {
+                           uint64_t* bs, const uint8_t* claim, hipStream_t s) {
   if (n_docs == 0) return 0;
   const uint32_t g = (n_docs + SN_DPW - 1) / SN_DPW, nb = (n_docs + 1 + 255) / 256;
-  hipLaunchKernelGGL(k_snap_count, dim3(g), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, (uint4*)cnt, ws_off);
+  hipLaunchKernelGGL(k_snap_count, dim3(g), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, (uint4*)cnt, ws_off, claim);
   hipLaunchKernelGGL(k_snap_scan_sum, dim3(nb), dim3(256), 0, s, (const uint64_t*)ws_off, n_docs, bs);
   hipLaunchKernelGGL(k_snap_scan_top, dim3(1), dim3(1024), 0, s, bs, nb);
   hipLaunchKernelGGL(k_snap_scan_apply, dim3(nb), dim3(256), 0, s, ws_off, n_docs, (const uint64_t*)bs);
@@ -250,14 +296,15 @@ int ygm_k_launch_scan(uint64_t* v, uint32_t n, uint64_t* bs, hipStream_t s) {
 }
 // phase 2: the snapshots (ws sized from ws_off[n_docs])
 int ygm_k_launch_snap(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, const void* cnt, const uint64_t* ws_off,
-                      uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, hipStream_t s) {
+                      uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, const uint8_t* claim,
+                      uint64_t base, hipStream_t s) {
   if (n_docs == 0) return 0;
   const char* env = getenv("YGM_SNAP_DPW");
   uint32_t dpw = env ? (uint32_t)atoi(env) : 16u;
   if (dpw < 1 || dpw > (uint32_t)SN_NT) dpw = 16u;
   const uint32_t g = (n_docs + dpw - 1) / dpw;
   hipLaunchKernelGGL(k_snap, dim3(g), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, (const uint4*)cnt, ws_off, ws, out_off, out_len,
-                     status, payload, dpw);
+                     status, payload, dpw, claim, base);
   return snap_rc(__func__);
 }
 

@@ -74,11 +74,19 @@ YDEV Caps caps_of(uint32_t S, uint32_t D, uint32_t C, uint32_t n) {
   return k;
 }
 YDEV uint64_t al16(uint64_t x) { return (x + 15u) & ~15ull; }
-YDEV uint64_t ws_bytes(const Caps& k) {
+YDEV uint64_t ws_core_bytes(const Caps& k) {   // the workspace without its output region
   return al16((uint64_t)k.it * sizeof(SI)) + al16((uint64_t)k.pc * sizeof(Piece)) + al16((uint64_t)k.ty * sizeof(TypeRec)) +
          al16((uint64_t)k.me * sizeof(MapEnt)) + al16((uint64_t)k.cl * sizeof(Cli)) + al16((uint64_t)k.tx * sizeof(Rng)) +
-         al16((uint64_t)k.dsin * sizeof(Rng)) + al16(4ull * k.st) + al16(4ull * k.seq) + al16(k.out);
+         al16((uint64_t)k.dsin * sizeof(Rng)) + al16(4ull * k.st) + al16(4ull * k.seq);
 }
+YDEV uint64_t ws_bytes(const Caps& k) { return ws_core_bytes(k) + al16(k.out); }
+// the encoder's writer: stores stop at cap (the caller's region), n counts on (> cap: the output did not fit)
+struct OutCap {
+  uint8_t* p; uint32_t n, cap;
+  YDEV void b(uint8_t v) { if (n < cap) p[n] = v; n++; }
+  YDEV void vu(uint64_t v) { while (v > 127) { b((uint8_t)(0x80 | (v & 127))); v >>= 7; } b((uint8_t)v); }
+  YDEV void copy(const uint8_t* s, uint32_t len) { for (uint32_t i = 0; i < len; i++) b(s[i]); }
+};
 
 // counts of a document (a light parse; errors are found again by the full pass)
 YDEV_NI void count_doc(const uint8_t* p, uint32_t n, uint32_t flags, uint32_t& S, uint32_t& D, uint32_t& C) {
@@ -609,8 +617,8 @@ struct Doc {
   }
 
   // ------------------------------------------------------------------ encodeStateAsUpdate (Y@23300)
-  YDEV void w(Out& o, uint32_t a, uint32_t l) { o.copy(in + a, l); }
-  YDEV void write_item(Out& o, int32_t x) {
+  YDEV void w(OutCap& o, uint32_t a, uint32_t l) { o.copy(in + a, l); }
+  YDEV void write_item(OutCap& o, int32_t x) {
     const SI& u = it[x];
     if (u.kind == SK_GC) { o.b(0); o.vu(u.len); return; }
     const bool ho = u.flags & F_HO, hr = u.flags & F_HR, hs = u.sub_len >= 0;
@@ -645,7 +653,7 @@ struct Doc {
     }
   }
   YDEV uint32_t encode() {
-    Out o{out, 0};
+    OutCap o{out, 0, cap_out};
     uint32_t nc = 0;
     for (uint32_t k = 0; k < n_cl; k++) nc += cl[k].ni > 0 ? 1u : 0u;
     o.vu(nc);
@@ -683,6 +691,7 @@ struct Doc {
       }
       if (o.n + 64u > cap_out) { fail(ST_NOMEM); return 0; }
     }
+    if (o.n > cap_out) { fail(ST_NOMEM); return 0; }
     return o.n;
   }
 
@@ -696,8 +705,9 @@ struct Doc {
   }
 };
 
-// carves document d's workspace (ws, ws_bytes(caps)) and runs it; returns the status, out_len
-YDEV_NI int snapshot_doc(const uint8_t* in, uint32_t n, uint32_t flags, uint8_t* ws, const Caps& k, uint32_t& out_off, uint32_t& out_len) {
+// carves a workspace (ws, ws_core_bytes(caps)) and runs the document, writing at most out_cap bytes at out
+YDEV_NI int snapshot_run(const uint8_t* in, uint32_t n, uint32_t flags, uint8_t* ws, const Caps& k, uint8_t* out, uint32_t out_cap,
+                         uint32_t& out_len) {
   Doc D;
   uint8_t* p = ws;
   D.in = in; D.n = n; D.flags = flags; D.err = 0; D.epoch = 0; D.n_ins = 0; D.hint_id = 0; D.hint_k = -1;
@@ -709,11 +719,15 @@ YDEV_NI int snapshot_doc(const uint8_t* in, uint32_t n, uint32_t flags, uint8_t*
   D.tx = (Rng*)p; D.n_tx = 0; D.cap_tx = k.tx; p += al16((uint64_t)k.tx * sizeof(Rng));
   D.dsin = (Rng*)p; D.n_dsin = 0; D.cap_dsin = k.dsin; p += al16((uint64_t)k.dsin * sizeof(Rng));
   D.st = (int32_t*)p; D.cap_st = k.st; p += al16(4ull * k.st);
-  D.seq = (int32_t*)p; D.cap_seq = k.seq; p += al16(4ull * k.seq);
-  D.out = p; D.cap_out = k.out;
-  out_off = (uint32_t)(p - ws);
+  D.seq = (int32_t*)p; D.cap_seq = k.seq;
+  D.out = out; D.cap_out = out_cap;
   out_len = D.run();
   return D.err;
+}
+// document d's workspace from caps_of, its output region at the end
+YDEV int snapshot_doc(const uint8_t* in, uint32_t n, uint32_t flags, uint8_t* ws, const Caps& k, uint32_t& out_off, uint32_t& out_len) {
+  out_off = (uint32_t)ws_core_bytes(k);
+  return snapshot_run(in, n, flags, ws, k, ws + out_off, k.out, out_len);
 }
 
 }  // namespace snap

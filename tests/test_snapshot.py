@@ -106,6 +106,54 @@ def test_kernel_code_on_host_default_mode(tmp_path):
     assert got == [(0, bytes.fromhex(ds_to_desc(e.hex()))) for _, e in rows]
 
 
+# ---------------------------------------------------------------------------------------- flat text (k_snap_text)
+TFIX = os.path.join(ROOT, "tests", "golden", "snapshot_text_v135.json.gz")
+
+
+def text_fixtures():
+    d = json.load(gzip.open(TFIX, "rt"))
+    return [(bytes.fromhex(u), bytes.fromhex(e)) for u, e in d["rows"]]
+
+
+def test_text_fixtures_present():
+    rows = text_fixtures()
+    assert len(rows) == 320 and all(u and e for u, e in rows)
+
+
+@pytest.mark.skipif(not (NODE and BUNDLE), reason="node + the yjs bundle are needed to regenerate")
+def test_text_fixtures_regenerate(tmp_path):
+    """The committed flat-text vectors are what the generator's text mode produces from the bundle (first sessions)."""
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "exp.bin")
+    subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_corpus.js"), "30", "21", a, b, "150", "text"], check=True, timeout=120)
+    rows = text_fixtures()[:30]
+    assert read_in(a) == [u for u, _ in rows]
+    assert [e for _, e in read_res(b)] == [e for _, e in rows]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
+@pytest.mark.parametrize("mode", [1, 0])
+def test_text_kernel_code_on_host(tmp_path, mode):
+    """The flat-text snapshot (ygm_snap_text.hpp, k_snap_text's code) host-compiled: on every document it takes
+    (the 320 text sessions: concurrent peers, splits by origins and delete ranges; the 440 general sessions: the
+    few that are flat text) its bytes are yjs's (13.5 mode; 13.6 default: client-descending delete sets) and the
+    general kernel code's; documents it leaves (nested types, formats, non-ASCII, past 12 KB) go to the general path."""
+    from golden import ds_to_desc
+    exe = str(tmp_path / "snaptext")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", exe, os.path.join(ROOT, "tools", "snapdev", "snaptext.cpp")], check=True, timeout=300)
+    for rows, min_taken in ((text_fixtures(), 300), (fixtures(), 1)):
+        a, b = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
+        write_in(a, [u for u, _ in rows])
+        r = subprocess.run([exe, a, str(mode), "12288", b], check=True, timeout=120, capture_output=True, text=True)
+        lines = [tuple(map(int, x.split())) for x in r.stdout.split("\n") if x]
+        taken = [k for k, (t, _, _) in enumerate(lines) if t]
+        assert len(taken) >= min_taken
+        assert all(lines[k][2] == 1 for k in taken), "text path differs from the general kernel code"
+        got = read_res(b)
+        for k in taken:
+            exp = rows[k][1] if mode else bytes.fromhex(ds_to_desc(rows[k][1].hex()))
+            assert got[k] == (0, exp), f"document {k} differs from yjs"
+
+
 # ---------------------------------------------------------------------------------------- GPU
 @pytest.fixture(scope="module")
 def eng135():
@@ -162,6 +210,44 @@ def test_gpu_snapshot_of_gpu_merges(eng135, tmp_path):
     write_in(a, merged)
     subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_expect.js"), a, b], check=True, timeout=240)
     assert eng135.snapshot_batch(merged) == [(st, e if st == 0 else None) for st, e in read_res(b)]
+
+
+@pytest.mark.gpu
+def test_gpu_snapshot_text_vs_yjs(eng135):
+    """The flat-text sessions (k_snap_text for all but the largest) against yjs, both modes."""
+    from golden import ds_to_desc
+    from hocuspocus_amd import Engine
+    rows = text_fixtures()
+    res = eng135.snapshot_batch([u for u, _ in rows])
+    bad = [k for k, ((_, e), r) in enumerate(zip(rows, res)) if r != (0, e)]
+    assert not bad, f"{len(bad)} documents differ from yjs, first {bad[:5]}"
+    with Engine(0) as e:
+        res = e.snapshot_batch([u for u, _ in rows])
+    bad = [k for k, ((_, x), r) in enumerate(zip(rows, res)) if r != (0, bytes.fromhex(ds_to_desc(x.hex())))]
+    assert not bad, f"default mode: {len(bad)} documents differ, first {bad[:5]}"
+
+
+@pytest.mark.gpu
+def test_gpu_snapshot_lds_tier_equals_general(monkeypatch):
+    """k_snap_text (flat text, input + workspace in LDS) against the count / scan / k_snap path alone
+    (YGM_SNAP_NOLDS), on one batch mixing what each takes: the yjs vectors (nested types, splits), C2 merges with
+    deletions, documents too large for the LDS tier (3 000-update logs, > 32 KB) and malformed / pending inputs."""
+    from hocuspocus_amd import Engine
+    from tools import synth
+    with Engine(0, compat135=True) as e:
+        batch = [u for u, _ in fixtures()]
+        for n, k, seed in ((200, 200, 43), (4, 3000, 44)):
+            arena, upd_off, doc_upd = synth.text_updates(n, k, seed=seed, del_pct=20)
+            docs = [[arena[upd_off[u]:upd_off[u + 1]].tobytes() for u in range(doc_upd[d], doc_upd[d + 1])] for d in range(n)]
+            batch += [m for st, m in e.merge_updates_batch(docs)]
+        assert max(len(u) for u in batch) > 40000
+        batch += [b"", bytes([1, 1, 5, 3, 0x04, 1, 1, 0x74, 1, 0x61, 0]), batch[3][:len(batch[3]) // 2]]
+        got = e.snapshot_batch(batch)
+        monkeypatch.setenv("YGM_SNAP_NOLDS", "1")
+        ref = e.snapshot_batch(batch)
+    bad = [k for k in range(len(batch)) if got[k] != ref[k]]
+    assert not bad, f"{len(bad)} documents differ between the tiers, first {bad[:5]}"
+    assert sum(st == 0 for st, _ in got) >= len(batch) - 3
 
 
 @pytest.mark.gpu

@@ -8,7 +8,7 @@
 //   expected = Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), u))  (what extension-database stores)
 // Writes `out.bin` (u32 n, then (u32 len, u) per session) and `exp.bin` (i32 status 0, u32 len, bytes),
 // the formats tools/snapdev and tests read.
-//   node tools/snap_corpus.js <n> <seed> <out.bin> <exp.bin> [maxOps]
+//   node tools/snap_corpus.js <n> <seed> <out.bin> <exp.bin> [maxOps] [text]
 const fs = require('fs')
 const path = require('path')
 const Y = require(path.join(__dirname, 'yjs_bundle.js')).load()
@@ -19,6 +19,42 @@ function rng (seed) {
 }
 
 const ALPH = ['a', 'b', 'c', 'd', 'e', ' ', 'é', 'ß', '€', '中', '😀', '🎉', 'x']
+
+// text: flat Y.Text sessions only -- ASCII inserts of 1-8 characters (in the middle of earlier runs too) and
+// deletions over 1-4 peers that sync now and then (concurrent inserts at one position, splits by origins and by
+// delete ranges): the envelope of the flat-text snapshot kernel (ygm_snap_text.hpp)
+function textSession (seed, maxOps) {
+  const R = rng(seed * 2654435761 + 777)
+  const ri = n => Math.floor(R() * n)
+  const nPeers = 1 + ri(4)
+  const peers = []
+  const log = []
+  for (let p = 0; p < nPeers; p++) {
+    const d = new Y.Doc()
+    d.clientID = 1 + ri(R() < 0.5 ? 100 : 0x7ffffff0)
+    d.on('update', (u, origin, doc, tr) => { if (tr.local) log.push(u) })
+    peers.push(d)
+  }
+  const ops = 1 + ri(maxOps)
+  for (let o = 0; o < ops; o++) {
+    const p = ri(nPeers)
+    const d = peers[p]
+    if (R() < 0.12) {
+      const q = ri(nPeers)
+      if (q !== p) Y.applyUpdate(peers[q], Y.encodeStateAsUpdate(d, Y.encodeStateVector(peers[q])), 'remote')
+      continue
+    }
+    d.transact(() => {
+      const t = d.getText('text')
+      if (t.length > 0 && R() < 0.3) { const at = ri(t.length); t.delete(at, 1 + ri(Math.min(5, t.length - at))) }
+      else { let s = ''; const k = 1 + ri(R() < 0.7 ? 2 : 8); for (let i = 0; i < k; i++) s += 'abcdefgh xyz'[ri(12)]; t.insert(ri(t.length + 1), s) }
+    })
+  }
+  const u = log.length ? Y.mergeUpdates(log) : Y.encodeStateAsUpdate(new Y.Doc())
+  const fresh = new Y.Doc()
+  Y.applyUpdate(fresh, u)
+  return [u, Y.encodeStateAsUpdate(fresh)]
+}
 
 function session (seed, maxOps) {
   const R = rng(seed * 2654435761 + 12345)
@@ -113,12 +149,13 @@ if (require.main === module) {
   const n = parseInt(process.argv[2] || '100', 10)
   const seed = parseInt(process.argv[3] || '1', 10)
   const maxOps = parseInt(process.argv[6] || '60', 10)
+  const gen = process.argv[7] === 'text' ? textSession : session
   const us = []; const ex = []
-  for (let i = 0; i < n; i++) { const [u, e] = session(seed * 100003 + i, maxOps); us.push(u); ex.push(e) }
+  for (let i = 0; i < n; i++) { const [u, e] = gen(seed * 100003 + i, maxOps); us.push(u); ex.push(e) }
   write(process.argv[4], us, false)
   const eb = [Buffer.from(new Uint32Array([ex.length]).buffer)]
   for (const b of ex) eb.push(Buffer.from(new Int32Array([0]).buffer), Buffer.from(new Uint32Array([b.length]).buffer), Buffer.from(b))
   fs.writeFileSync(process.argv[5], Buffer.concat(eb.slice(1)))
 }
 
-module.exports = { session }
+module.exports = { session, textSession }

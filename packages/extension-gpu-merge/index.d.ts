@@ -91,7 +91,7 @@ export interface GpuMergeConfiguration extends GpuEngineOptions {
   Y?: any
   /** a refused merge: store Y.encodeStateAsUpdate(document) ('reference', default) or reject the store ('throw') */
   onRefused?: 'reference' | 'throw'
-  /** store the GPU doc-normalized snapshot of the merge (GC'd, merged: the shape extension-database stores) */
+  /** store the GPU doc-normalized snapshot of the merge (GC'd, merged: the shape extension-database stores); default true, false stores the bare merge */
   normalize?: boolean
 }
 

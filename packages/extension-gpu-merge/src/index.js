@@ -46,16 +46,18 @@ class GpuMerge {
    *   onRefused: what a store does when the engine refuses a document's merge -- 'reference' (default):
    *   store Y.encodeStateAsUpdate(document) like extension-database and record it in `refused`;
    *   'throw': reject the store (Hocuspocus logs and rethrows, Hocuspocus.ts:431-435)
-   *   normalize: store the doc-normalized snapshot of the merge, Y.encodeStateAsUpdate(Y.applyUpdate(new
-   *   Y.Doc(), merged)) computed on the GPU (SURVEY.md §8f-1) -- deleted content garbage-collected and
-   *   adjacent structs merged, the shape extension-database stores (Database.ts:55-60) -- instead of the
-   *   bare merge; a document outside the snapshot kernel's envelope keeps its merged bytes (`unnormalized`)
+   *   normalize (default true): store the doc-normalized snapshot of the merge, Y.encodeStateAsUpdate(
+   *   Y.applyUpdate(new Y.Doc(), merged)) computed on the GPU (SURVEY.md §8f-1) -- deleted content
+   *   garbage-collected and adjacent structs merged, the bytes extension-database stores for a fresh load of
+   *   the same updates (Database.ts:55-60); a document outside the snapshot kernel's envelope keeps its merged
+   *   bytes (`unnormalized`).  normalize: false stores the bare Y.mergeUpdates bytes.
    */
   constructor (configuration = {}) {
     this.extensionName = 'GpuMerge'
     // after Redis (priority 1000, which takes the store lock first), before plain storage extensions (100)
     this.priority = configuration.priority || 900
     this.configuration = configuration
+    this.normalize = configuration.normalize !== false
     // drop-in for `new Database({ fetch, store })`, or a batched DocumentStore instance
     const st = configuration.store
     this.store = st && typeof st.storeMany === 'function'
@@ -163,7 +165,7 @@ class GpuMerge {
         const job = { head: entry.base ? [entry.base] : [], ...entry.log.packed(taken) }
         const eng = this._engine()
         state = await (eng.mergePacked ? eng.mergePacked(job, data.documentName) : eng.mergeUpdates(job.head.concat(entry.log.toArray(taken)), data.documentName))
-        if (this.configuration.normalize) state = await this._normalize(state, data.documentName)
+        if (this.normalize) state = await this._normalize(state, data.documentName)
       } catch (e) {
         // a document the engine refuses (content yjs would re-encode, YGM_ENONCANON; a corrupt stored
         // base) or a failed batch: unless configured to throw, store what extension-database stores for

@@ -113,10 +113,10 @@ test('content added by another extension during load is captured', async (engine
   assert.strictEqual(d2.getText('t').toString(), 'seeded!')
 })
 
-// the stored state is byte-identical to Y.mergeUpdates([base, ...updates])
-test('stored bytes == yjs mergeUpdates([snapshot, ...log])', async (engine) => {
+// normalize: false -- the stored state is byte-identical to Y.mergeUpdates([base, ...updates])
+test('stored bytes == yjs mergeUpdates([snapshot, ...log]) (normalize: false)', async (engine) => {
   const db = memoryDb()
-  const ext = new GpuMerge({ ...db, Y, engine })
+  const ext = new GpuMerge({ ...db, Y, engine, normalize: false })
   const hp = new MiniHocuspocus({ extensions: [ext], Y })
   const doc = await hp.loadDocument('bytes')
   const log = []
@@ -209,9 +209,9 @@ test('afterLoadDocument adds nothing when the load added nothing', async (engine
 // SURVEY.md §8e: documents sharded over the node's GPUs by fnv1a64(documentName) mod N
 // SURVEY.md §8f-1: normalize stores what extension-database stores for a fresh load of the merge --
 // encodeStateAsUpdate(applyUpdate(new Doc, mergeUpdates(log))): deleted text garbage-collected
-test('normalize stores the doc-normalized snapshot of the merge', async (engine) => {
+test('the default store is the doc-normalized snapshot of the merge', async (engine) => {
   const db = memoryDb()
-  const ext = new GpuMerge({ ...db, Y, engine, normalize: true })
+  const ext = new GpuMerge({ ...db, Y, engine })
   const hp = new MiniHocuspocus({ extensions: [ext], Y })
   const doc = await hp.loadDocument('norm')
   doc.clientID = 7

@@ -313,8 +313,9 @@ def host_api_merge(be, cb, args, reps=3):
 
 
 def c1_store_window(docs=1000, inserts=200):
-    """C1: one store window of 1 000 edited Y.Text documents through GpuMerge (Node, N-API addon,
-    ygm_merge_v1) beside extension-database's encodeStateAsUpdate store (tools/c1_store_latency.js)."""
+    """C1: one store window of 1 000 edited Y.Text documents through GpuMerge (Node, N-API addon:
+    ygm_merge_v1, then ygm_snapshot_v1 -- the default normalized store; and normalize: false, the merge alone)
+    beside extension-database's encodeStateAsUpdate store (tools/c1_store_latency.js)."""
     import shutil
     import subprocess
     if not shutil.which("node"):

@@ -62,7 +62,7 @@ int ygm_k_launch_merge_seq(const uint8_t* arena, const uint64_t* upd_off, const 
 int ygm_k_launch_scan(uint64_t* v, uint32_t n, uint64_t* bs, hipStream_t s);
 size_t ygm_k_v2_cols();
 int ygm_k_launch_v21(int pass, const uint8_t* arena, const uint64_t* upd_off, uint32_t n_upd, const uint32_t* doc_upd, uint32_t n_docs,
-                     uint32_t mode, uint32_t flags, uint64_t* len_or_off, int32_t* st, uint8_t* out, hipStream_t s);
+                     uint32_t mode, uint32_t flags, uint64_t* len_or_off, int32_t* st, uint8_t* out, uint8_t* cl, hipStream_t s);
 int ygm_k_launch_v12_count(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint8_t* v2a,
                            uint64_t v2n, const uint64_t* upd_off, const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint32_t mode,
                            uint32_t flags, uint32_t* L, uint64_t* tot, int32_t* st, const uint8_t* claim, hipStream_t s);
@@ -165,7 +165,7 @@ struct ygm_ctx {
   // [LDS-tier output slots | workspaces], LDS-tier claims, its payload / claimed counters
   // update V2: per-update V1 sizes -> offsets, transcoding statuses, scan scratch, the V1 arena, per-document column
   // lengths, the V2 outputs (packed), their offsets / lengths / statuses
-  DevBuf v2_len, v2_st, v2_bs, v2_v1, v2_L, v2_out, v2_off, v2_olen, v2_ost, v2_fo, v2_claim, v2_pay, v2_scr;
+  DevBuf v2_len, v2_st, v2_bs, v2_v1, v2_L, v2_out, v2_off, v2_olen, v2_ost, v2_fo, v2_claim, v2_pay, v2_scr, v21_cl;
   // host API: results in pinned memory (packed outputs, per-document offset / length / status), the
   // pinned input staging of this context when it serves as a pipeline stage, the packed device copy,
   // and the two stage contexts (own streams and buffers) that double-buffer a batch's chunks
@@ -238,7 +238,7 @@ void ygm_close(ygm_ctx* c) {
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
                     &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws, &c->sn_claim, &c->sn_pay,
-                    &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr})
+                    &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr, &c->v21_cl})
     b->release();
   for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
   for (DevBuf* b : {&c->pk_data, &c->pk_off, &c->pk_bsum}) b->release();
@@ -587,11 +587,14 @@ int ygm_sv_from_update_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t ar
 static int v21_pass(ygm_ctx* c, hipStream_t s, const uint8_t* arena, const uint64_t* off, uint32_t n, const uint32_t* doc_upd,
                     uint32_t n_docs, uint32_t mode, uint64_t& total) {
   const size_t nb = ((size_t)n + 1 + 255) / 256 + 2;
-  if (!c->v2_len.ensure(8ull * n + 16) || !c->v2_st.ensure(4ull * n + 4) || !c->v2_bs.ensure(8 * nb)) return YGM_ENOMEM;
+  if (!c->v2_len.ensure(8ull * n + 16) || !c->v2_st.ensure(4ull * n + 4) || !c->v2_bs.ensure(8 * nb) || !c->v21_cl.ensure((size_t)n + 16))
+    return YGM_ENOMEM;
+  // the register-resident transcoder first (claims), the general one for the rest; the public conversion: general only
+  uint8_t* cl = (mode & 1u) || getenv("YGM_V21_NOFAST") ? nullptr : c->v21_cl.as<uint8_t>();
   total = 0;
   if (n == 0) { HIPCHK(hipMemsetAsync(c->v2_len.p, 0, 8, s)); }
   else {
-    if (ygm_k_launch_v21(0, arena, off, n, doc_upd, n_docs, mode, c->flags, c->v2_len.as<uint64_t>(), c->v2_st.as<int32_t>(), nullptr, s) ||
+    if (ygm_k_launch_v21(0, arena, off, n, doc_upd, n_docs, mode, c->flags, c->v2_len.as<uint64_t>(), c->v2_st.as<int32_t>(), nullptr, cl, s) ||
         ygm_k_launch_scan(c->v2_len.as<uint64_t>(), n, c->v2_bs.as<uint64_t>(), s))
       return YGM_EDEVICE;
     HIPCHK(hipMemcpyAsync(c->h_meta, c->v2_len.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
@@ -600,7 +603,7 @@ static int v21_pass(ygm_ctx* c, hipStream_t s, const uint8_t* arena, const uint6
   }
   if (!c->v2_v1.ensure(total + 64)) return YGM_ENOMEM;   // (the V1 kernels read up to 64 bytes past the arena)
   if (n && ygm_k_launch_v21(1, arena, off, n, doc_upd, n_docs, mode, c->flags, c->v2_len.as<uint64_t>(), c->v2_st.as<int32_t>(),
-                            c->v2_v1.as<uint8_t>(), s))
+                            c->v2_v1.as<uint8_t>(), cl, s))
     return YGM_EDEVICE;
   return YGM_OK;
 }

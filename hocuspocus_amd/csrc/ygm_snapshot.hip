@@ -39,33 +39,43 @@ YDEV const uint8_t* snap_stage(uint8_t* stg, const uint8_t* __restrict__ arena, 
   return staged && x >= a && doc_off[d + 1] <= b ? stg + (x - a16) : arena + x;
 }
 
-// k_snap_text: one document per workgroup (one wave): the lanes stage its bytes into LDS, lane 0 runs the flat-text
-// snapshot (ygm_snap_text.hpp) over a workspace in the rest of the workgroup's LB bytes of LDS -- the integration's
-// dependent chain as LDS round trips instead of global ones, LB small enough for many documents per CU.  Documents
-// outside the envelope or the workspace are left unclaimed for the count / scan / k_snap path.  Outputs go to
-// per-document slots at align16(2 * doc_off[d] + 64 * d), 2n + 48 bytes each.
-template <uint32_t LB>
+// k_snap_text: DPW documents per workgroup (one wave), each with LB bytes of LDS: the lanes stage every document's
+// bytes into its region, then lane l < DPW runs document l's flat-text snapshot (ygm_snap_text.hpp) over a workspace
+// in the rest of its region -- the integration's dependent chain as LDS round trips instead of global ones, and
+// DPW documents sharing each instruction issue.  Documents outside the envelope or the workspace are left
+// unclaimed for the count / scan / k_snap path.  Outputs go to per-document slots at align16(2 * doc_off[d] + 64 * d),
+// 2n + 48 bytes each.
+template <uint32_t LB, uint32_t DPW>
 __global__ __launch_bounds__(SN_NT) void k_snap_text(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off, uint32_t n_docs,
                                                     uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status, uint8_t* __restrict__ claim,
                                                     unsigned long long* __restrict__ pay) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LB];
-  const uint32_t d = blockIdx.x;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LB * DPW];
+  const uint32_t d0 = blockIdx.x * DPW;
+  for (uint32_t j = 0; j < DPW && d0 + j < n_docs; j++) {
+    const uint64_t a = doc_off[d0 + j], b = doc_off[d0 + j + 1];
+    const uint64_t a16 = a & ~15ull, sb = (b - a16 + 15u) & ~15ull;
+    if (b <= a || sb + 1024u > LB) continue;
+    const uint4* src = (const uint4*)(arena + a16);
+    for (uint32_t c = threadIdx.x; 16u * c < sb; c += SN_NT) ((uint4*)(lds + LB * j))[c] = src[c];   // (arena tail padding >= 16)
+  }
+  __syncthreads();
+  const uint32_t d = d0 + threadIdx.x;
+  if (threadIdx.x >= DPW || d >= n_docs) return;
   const uint64_t a = doc_off[d], b = doc_off[d + 1];
   const uint64_t a16 = a & ~15ull, sb = (b - a16 + 15u) & ~15ull;
-  if (b <= a || sb + 1024u > LB) { if (threadIdx.x == 0) claim[d] = 0; return; }
-  const uint4* src = (const uint4*)(arena + a16);
-  for (uint32_t c = threadIdx.x; 16u * c < sb; c += SN_NT) ((uint4*)lds)[c] = src[c];   // (arena tail padding >= 16)
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  const uint32_t n = (uint32_t)(b - a);
-  const uint64_t slot = snap::al16(2 * a + 64ull * d);
-  snap::OutCap o{out + slot, 0, 2u * n + 48u};
-  const bool ok = snapt::snapshot_text(lds + (a - a16), n, flags, lds + sb, LB - (uint32_t)sb, o) && o.n <= o.cap;
-  if (ok) {
-    out_off[d] = slot; out_len[d] = o.n; status[d] = ST_OK;
-    atomicAdd(pay, (unsigned long long)o.n);
-    atomicAdd(pay + 1, 1ull);
+  bool ok = false;
+  if (b > a && sb + 1024u <= LB) {
+    uint8_t* reg = lds + LB * threadIdx.x;
+    const uint32_t n = (uint32_t)(b - a);
+    const uint64_t slot = snap::al16(2 * a + 64ull * d);
+    snap::OutCap o{out + slot, 0, 2u * n + 48u};
+    ok = snapt::snapshot_text(reg + (a - a16), n, flags, reg + sb, LB - (uint32_t)sb, o) && o.n <= o.cap;
+    if (ok) {
+      out_off[d] = slot; out_len[d] = o.n; status[d] = ST_OK;
+      atomicAdd(pay, (unsigned long long)o.n);
+      atomicAdd(pay + 1, 1ull);
+    }
   }
   claim[d] = ok ? 1 : 0;
 }
@@ -267,12 +277,14 @@ static int snap_rc(const char* fn) {
 int ygm_k_launch_snap_text(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
                            uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, hipStream_t s) {
   if (n_docs == 0) return 0;
-  const char* env = getenv("YGM_SNAP_LB");   // KiB of LDS per document (experiments; 12 by default)
-  const int lb = env ? atoi(env) : 12;
-  if (lb == 8) hipLaunchKernelGGL(k_snap_text<8192>, dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
-  else if (lb == 16) hipLaunchKernelGGL(k_snap_text<16384>, dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
-  else if (lb == 32) hipLaunchKernelGGL(k_snap_text<32768>, dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
-  else hipLaunchKernelGGL(k_snap_text<12288>, dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
+  const char* env = getenv("YGM_SNAP_TEXT");   // experiments: "KiB:docs per wave" (default 12:1)
+  int lb = 12, dpw = 1;
+  if (env) sscanf(env, "%d:%d", &lb, &dpw);
+#define SNT(L, D) if (lb == L && dpw == D) { hipLaunchKernelGGL((k_snap_text<L * 1024, D>), dim3((n_docs + D - 1) / D), dim3(SN_NT), 0, s, arena, doc_off, \
+                                                         n_docs, flags, out, out_off, out_len, status, claim, pay); return snap_rc(__func__); }
+  SNT(8, 1) SNT(8, 2) SNT(8, 4) SNT(8, 8) SNT(10, 2) SNT(10, 4) SNT(10, 8) SNT(12, 2) SNT(12, 4) SNT(16, 1)
+#undef SNT
+  hipLaunchKernelGGL((k_snap_text<12288, 1>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
   return snap_rc(__func__);
 }
 int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, void* cnt, uint64_t* ws_off,

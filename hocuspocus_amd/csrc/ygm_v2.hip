@@ -1,7 +1,8 @@
 // ygm_v2.hip -- update-V2 kernels: one lane per update / document runs the transcoders of
 // ygm_v2.hpp in two passes (sizes, then bytes at scanned offsets).
 //   k_v21_count / k_v21_write : V2 -> V1 per update (merge: updates of single-input documents are skipped --
-//                               mergeUpdatesV2 returns a lone input as it is)
+//                               mergeUpdatesV2 returns a lone input as it is); the wave's bytes staged in LDS, the
+//                               register-resident transcoder (ygm_v21_fast.hpp) first
 //   k_v12_count / k_v12_write : V1 -> V2 per document, with the document's final status (the V2 inputs'
 //                               transcoding statuses, then the V1 operation's), or the passthrough copy
 //   k_v2_status               : SV: a V2 input's transcoding status over the V1 kernel's
@@ -16,6 +17,7 @@
 #include "ygm_common.hpp"
 #include "ygm_v2.hpp"
 #include "ygm_v2_fast.hpp"
+#include "ygm_v21_fast.hpp"
 
 namespace ygm {
 
@@ -30,11 +32,57 @@ YDEV uint32_t doc_of(const uint32_t* doc_upd, uint32_t n_docs, uint32_t u) {
   return lo;
 }
 
+// V2 -> V1, one lane per update, in two kernels per pass:
+//   k_v21f<W>   : the wave's updates are consecutive in the arena, so the wave copies their bytes into LDS with
+//                 16-byte loads and each lane runs the register-resident transcoder (ygm_v21_fast.hpp: text-log
+//                 shapes, <= 128 bytes); the updates it takes are claimed (cl[u] = 1)
+//   k_v21_*     : the general transcoder (v2::v21, decoder state in scratch, ~250 VGPRs) for the unclaimed rest
+// The size pass and the write pass make the same choice per update, so sizes and bytes agree.
+constexpr uint32_t V21_STG = 8192;
+template <bool W>
+__global__ __launch_bounds__(V2_NT) void k_v21f(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off, uint32_t n_upd,
+                                               const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t mode,
+                                               uint64_t* __restrict__ len_or_off, int32_t* __restrict__ st, uint8_t* __restrict__ cl,
+                                               uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t stg[V21_STG + 16];
+  const uint32_t u0 = blockIdx.x * V2_NT, u1 = u0 + V2_NT < n_upd ? u0 + V2_NT : n_upd;
+  const uint64_t a0 = upd_off[u0], b0 = upd_off[u1], a16 = a0 & ~15ull;
+  const bool staged = b0 >= a0 && b0 - a16 <= V21_STG;
+  if (staged) {
+    const uint4* src = (const uint4*)(arena + a16);
+    for (uint32_t c = threadIdx.x; 16u * c < b0 - a16; c += V2_NT) ((uint4*)stg)[c] = src[c];   // (arena tail padding >= 16)
+  }
+  __syncthreads();
+  const uint32_t u = u0 + threadIdx.x;
+  if (u >= n_upd) return;
+  if (W) {
+    if (!cl[u]) return;
+    const uint64_t a = upd_off[u], b = upd_off[u + 1];
+    if (len_or_off[u + 1] == len_or_off[u]) return;
+    const v21f::Src<const uint8_t*> s{stg + (a - a16)};
+    v21f::BOut<uint8_t*> o{out + len_or_off[u], 0};
+    (void)v21f::v21_fast(s, (uint32_t)(b - a), mode, o);
+    return;
+  }
+  uint8_t c = 0;
+  if (doc_upd) {
+    const uint32_t d = doc_of(doc_upd, n_docs, u);
+    if (doc_upd[d + 1] - doc_upd[d] == 1) { len_or_off[u] = 0; st[u] = ST_OK; cl[u] = 1; return; }
+  }
+  const uint64_t a = upd_off[u], b = upd_off[u + 1];
+  if (staged && b >= a && b - a <= v21f::F21_MAX) {
+    const v21f::Src<const uint8_t*> s{stg + (a - a16)};
+    v21f::BOut<uint8_t*> o{nullptr, 0};
+    if (v21f::v21_fast(s, (uint32_t)(b - a), mode, o)) { len_or_off[u] = o.n; st[u] = ST_OK; c = 1; }
+  }
+  cl[u] = c;
+}
+
 __global__ __launch_bounds__(V2_NT) void k_v21_count(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off, uint32_t n_upd,
                                                     const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t mode, uint32_t flags,
-                                                    uint64_t* __restrict__ len, int32_t* __restrict__ st) {
+                                                    uint64_t* __restrict__ len, int32_t* __restrict__ st, const uint8_t* __restrict__ cl) {
   const uint32_t u = blockIdx.x * V2_NT + threadIdx.x;
-  if (u >= n_upd) return;
+  if (u >= n_upd || (cl && cl[u])) return;
   if (doc_upd) {
     const uint32_t d = doc_of(doc_upd, n_docs, u);
     if (doc_upd[d + 1] - doc_upd[d] == 1) { len[u] = 0; st[u] = ST_OK; return; }
@@ -48,9 +96,9 @@ __global__ __launch_bounds__(V2_NT) void k_v21_count(const uint8_t* __restrict__
 }
 __global__ __launch_bounds__(V2_NT) void k_v21_write(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off, uint32_t n_upd,
                                                     uint32_t mode, uint32_t flags, const uint64_t* __restrict__ off,
-                                                    const int32_t* __restrict__ st, uint8_t* __restrict__ out) {
+                                                    const int32_t* __restrict__ st, uint8_t* __restrict__ out, const uint8_t* __restrict__ cl) {
   const uint32_t u = blockIdx.x * V2_NT + threadIdx.x;
-  if (u >= n_upd || st[u] != ST_OK || off[u + 1] == off[u]) return;
+  if (u >= n_upd || (cl && cl[u]) || st[u] != ST_OK || off[u + 1] == off[u]) return;
   const uint64_t a = upd_off[u], b = upd_off[u + 1];
   Out o{out + off[u], 0};
   (void)v2::v21(arena + a, (uint32_t)(b - a), a, mode, flags, o);
@@ -267,12 +315,18 @@ static int v2_rc(const char* fn) {
 }
 size_t ygm_k_v2_cols() { return v2::C_N; }
 int ygm_k_launch_v21(int pass, const uint8_t* arena, const uint64_t* upd_off, uint32_t n_upd, const uint32_t* doc_upd, uint32_t n_docs,
-                     uint32_t mode, uint32_t flags, uint64_t* len_or_off, int32_t* st, uint8_t* out, hipStream_t s) {
+                     uint32_t mode, uint32_t flags, uint64_t* len_or_off, int32_t* st, uint8_t* out, uint8_t* cl, hipStream_t s) {
   if (n_upd == 0) return 0;
   const uint32_t g = (n_upd + V2_NT - 1) / V2_NT;
-  if (pass == 0) hipLaunchKernelGGL(k_v21_count, dim3(g), dim3(V2_NT), 0, s, arena, upd_off, n_upd, doc_upd, n_docs, mode, flags, len_or_off, st);
-  else hipLaunchKernelGGL(k_v21_write, dim3(g), dim3(V2_NT), 0, s, arena, upd_off, n_upd, mode, flags, (const uint64_t*)len_or_off,
-                          (const int32_t*)st, out);
+  if (pass == 0) {
+    if (cl) hipLaunchKernelGGL(k_v21f<false>, dim3(g), dim3(V2_NT), 0, s, arena, upd_off, n_upd, doc_upd, n_docs, mode, len_or_off, st, cl, out);
+    hipLaunchKernelGGL(k_v21_count, dim3(g), dim3(V2_NT), 0, s, arena, upd_off, n_upd, doc_upd, n_docs, mode, flags, len_or_off, st,
+                       (const uint8_t*)cl);
+  } else {
+    if (cl) hipLaunchKernelGGL(k_v21f<true>, dim3(g), dim3(V2_NT), 0, s, arena, upd_off, n_upd, doc_upd, n_docs, mode, len_or_off, st, cl, out);
+    hipLaunchKernelGGL(k_v21_write, dim3(g), dim3(V2_NT), 0, s, arena, upd_off, n_upd, mode, flags, (const uint64_t*)len_or_off,
+                       (const int32_t*)st, out, (const uint8_t*)cl);
+  }
   return v2_rc(__func__);
 }
 int ygm_k_launch_v12_count(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint8_t* v2a,

@@ -66,17 +66,30 @@ async function main () {
     const warm = await build(ext)
     await window(warm.hp)
   }
+  // the bare merge (normalize: false) first, then the default store (merge + GPU doc-normalized snapshot)
+  const bareRows = new Map()
+  const bare = await build(new GpuMerge({ store: async ({ documentName, state }) => bareRows.set(documentName, state), Y, engine, normalize: false }))
+  const bareMs = await window(bare.hp)
+  let sameBare = 0
+  for (let d = 0; d < nDocs; d++) if (Buffer.compare(Buffer.from(Y.mergeUpdates(bare.logs[d])), Buffer.from(bareRows.get(`c1-${d}`))) === 0) sameBare++
+  {
+    const ext = new GpuMerge({ store: async () => {}, Y, engine })
+    const warm = await build(ext)
+    await window(warm.hp)
+  }
   const gpuRows = new Map()
   const ext = new GpuMerge({ store: async ({ documentName, state }) => gpuRows.set(documentName, state), Y, engine })
   const gpu = await build(ext)
   const calls0 = engine.stats ? engine.stats().calls : null
   const gpuMs = await window(gpu.hp)
   const calls = engine.stats && calls0 !== null ? engine.stats().calls - calls0 : null
-  const split = engine.timing.merge || null   // the window's (last) batch: wait / pack / native / settle
-  let same = 0
+  const split = engine.timing.merge || null   // the window's merge batch: wait / pack / native / settle
+  let same = 0, sameRef = 0
   for (let d = 0; d < nDocs; d++) {
-    const exp = Buffer.from(Y.mergeUpdates(gpu.logs[d]))
-    if (Buffer.compare(exp, Buffer.from(gpuRows.get(`c1-${d}`))) === 0) same++
+    const fresh = new Y.Doc(); Y.applyUpdate(fresh, Y.mergeUpdates(gpu.logs[d]))
+    const got = Buffer.from(gpuRows.get(`c1-${d}`))
+    if (Buffer.compare(Buffer.from(Y.encodeStateAsUpdate(fresh)), got) === 0) same++
+    if (Buffer.compare(Buffer.from(refRows.get(`c1-${d}`)), got) === 0) sameRef++
   }
   let inBytes = 0
   for (const l of gpu.logs) for (const u of l) inBytes += u.length
@@ -86,12 +99,14 @@ async function main () {
     reference_store_ms: Math.round(refMs * 1000) / 1000,
     reference: 'extension-database onStoreDocument: Y.encodeStateAsUpdate(document) per document (yjs 13.5.16 bundle, Node ' + process.version + ')',
     gpumerge_store_ms: Math.round(gpuMs * 1000) / 1000,
-    gpumerge: 'GpuMerge.onStoreDocument: Y.mergeUpdates([base, ...log]) batched through ygm_merge_v1 (N-API addon)',
+    gpumerge: 'GpuMerge.onStoreDocument (default): Y.mergeUpdates([base, ...log]) batched through ygm_merge_v1, then the doc-normalized snapshot batched through ygm_snapshot_v1 (N-API addon)',
+    gpumerge_bare_store_ms: Math.round(bareMs * 1000) / 1000,
+    gpumerge_bare: 'GpuMerge({ normalize: false }): the merge batch only',
     gpumerge_engine_calls: calls,
     gpumerge_batch_split_ms: split && Object.fromEntries(Object.entries(split).map(([k, v]) => [k, typeof v === 'number' && !Number.isInteger(v) ? Math.round(v * 1000) / 1000 : v])),
     gpumerge_split_note: 'wait: first store -> batch flush (batch window); pack: JS batch arena (one copy per document, logs packed at capture); napi_in: addon call on the main thread; native: call -> promise settled, of which exec (worker: ygm_merge_v1 with pinned staging, H2D, kernels, D2H, result copy) and copy_out (result views); h2d / kernel / d2h: the engine\'s HIP-event times; settle: resolving the documents\' promises',
     log_bytes: inBytes,
-    parity: `${same}/${nDocs} stored states byte-identical to yjs mergeUpdates of the captured logs`
+    parity: `default: ${same}/${nDocs} stored states byte-identical to yjs encodeStateAsUpdate(applyUpdate(new Doc, mergeUpdates(log))), ${sameRef}/${nDocs} to the extension-database rows; normalize false: ${sameBare}/${nDocs} byte-identical to yjs mergeUpdates`
   }))
 }
 

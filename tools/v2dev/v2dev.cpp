@@ -59,3 +59,20 @@ int hv_v12f(const uint8_t* v1, uint32_t n, uint8_t* out, uint64_t* out_len) {
   return 0;
 }
 }
+
+#include "../../hocuspocus_amd/csrc/ygm_v21_fast.hpp"
+extern "C" {
+// the register-resident fast V2 -> V1 transcoder (ygm_v21_fast.hpp, the k_v21_* kernels' first try): 0 = done (size
+// pass, then the bytes when out != nullptr), 1 = off the fast path
+int hv_v21f(const uint8_t* u, uint32_t n, uint32_t mode, uint8_t* out, uint64_t* out_len) {
+  const v21f::Src<const uint8_t*> s{u};
+  v21f::BOut<uint8_t*> c{nullptr, 0};
+  *out_len = 0;
+  if (!v21f::v21_fast(s, n, mode, c)) return 1;
+  *out_len = c.n;
+  if (!out) return 0;
+  v21f::BOut<uint8_t*> o{out, 0};
+  if (!v21f::v21_fast(s, n, mode, o) || o.n != c.n) return 3;
+  return 0;
+}
+}

@@ -56,57 +56,79 @@ struct TDoc {
   }
 
   // ------------------------------------------------------------------ read (Doc::parse)
+  // A lean reader for the envelope's shapes: varuints of <= 5 bytes below 2^32 (larger ones, any read past the end,
+  // a struct of another kind, a non-ASCII string: outside the envelope), the same values as read_struct / Cur::vu.
+  uint32_t pos;
+  YDEV uint32_t vu() {
+    uint32_t v = 0;
+#pragma unroll 1
+    for (uint32_t k = 0; k < 5u; k++) {
+      if (pos >= n) { bad = true; return 0; }
+      const uint32_t x = in[pos++];
+      v |= (x & 127u) << (7u * k);
+      if (x < 128u) { if (k == 4u && (x & 0x70u)) bad = true; return v; }
+    }
+    bad = true;
+    return 0;
+  }
+  YDEV bool ascii(uint32_t a, uint32_t l) const {
+    for (uint32_t i = 0; i < l; i++) if (in[a + i] >= 0x80u) return false;
+    return true;
+  }
   YDEV void parse() {
-    Cur c{in, 0, n, 0, 0};
-    const uint64_t nb = c.vu();
-    for (uint64_t b = 0; b < nb && !c.err && !bad; b++) {
-      const uint64_t ns = c.vu(), client = c.vu(); uint64_t clock = c.vu();
-      if (c.err || client > 0xFFFFFFFFull || nc >= CMAX || slot((uint32_t)client) >= 0) { bad = true; return; }
+    pos = 0;
+    const uint32_t nb = vu();
+    for (uint32_t b = 0; b < nb && !bad; b++) {
+      const uint32_t ns = vu(), client = vu(); uint32_t clock = vu();
+      if (bad || nc >= CMAX || slot(client) >= 0) { bad = true; return; }
       CT& k = ct[nc];
-      k.id = (uint32_t)client; k.state = 0; k.r0 = (uint16_t)np; k.rn = 0; k.ri = 0; k.ni = 0; k.ins = -1; k.pad = 0;
-      for (uint64_t s = 0; s < ns && !bad; s++) {
-        SInfo si; read_struct_fast(c, si, flags);
-        if (c.err || si.kind != K_ITEM || (si.ref != 1 && si.ref != 4) || si.nc || si.len == 0 || clock + si.len > 0xFFFFull ||
-            np >= cap) { bad = true; return; }
+      k.id = client; k.state = 0; k.r0 = (uint16_t)np; k.rn = 0; k.ri = 0; k.ni = 0; k.ins = -1; k.pad = 0;
+      for (uint32_t s = 0; s < ns && !bad; s++) {
+        if (pos >= n || np >= cap) { bad = true; return; }
+        const uint8_t info = in[pos++];
+        const uint32_t ref = info & 31u;
+        if (ref != 1u && ref != 4u) { bad = true; return; }   // GC / Skip / other content: the general path
         P& x = p[np];
-        x.clock = (uint16_t)clock; x.len = (uint16_t)si.len; x.orig = (uint16_t)np; x.nxt = NIL;
-        x.left = x.right = 0; x.ms = x.mr = 0; x.ok = x.rk = 0; x.ocl = x.rcl = 0; x.cl = (uint8_t)nc;
-        x.fl = si.ref == 4 ? T_STR : 0; x.coff = 0; x.clen = 0;
-        Cur h{in, si.start + 1, si.cstart, 0, 0};
-        const uint8_t info = si.info;
+        x.orig = (uint16_t)np; x.nxt = NIL; x.left = x.right = 0; x.ms = x.mr = 0; x.ok = x.rk = 0; x.ocl = x.rcl = 0;
+        x.cl = (uint8_t)nc; x.fl = ref == 4u ? T_STR : 0; x.coff = 0; x.clen = 0;
         if (info & 0x80) {   // origin id: the client id parks in (ms, mr) until the client table is complete
-          const uint64_t oc = h.vu(), ok = h.vu();
-          if (oc > 0xFFFFFFFFull || ok > 0xFFFFull) { bad = true; return; }
+          const uint32_t oc = vu(), ok = vu();
+          if (ok > 0xFFFFu) bad = true;
           x.ms = (uint16_t)(oc >> 16); x.mr = (uint16_t)oc; x.ok = (uint16_t)ok; x.fl |= T_HO;
         }
         if (info & 0x40) {   // right origin: the client id parks in (left, right)
-          const uint64_t rc = h.vu(), rk = h.vu();
-          if (rc > 0xFFFFFFFFull || rk > 0xFFFFull) { bad = true; return; }
+          const uint32_t rc = vu(), rk = vu();
+          if (rk > 0xFFFFu) bad = true;
           x.left = (uint16_t)(rc >> 16); x.right = (uint16_t)rc; x.rk = (uint16_t)rk; x.fl |= T_HR;
         }
-        if ((info & 0xC0) == 0) {   // the root type by name, the same one for the whole update
-          if (h.vu() != 1 || (info & 0x20)) { bad = true; return; }
-          uint32_t l; const uint32_t s0 = h.buf(l);
-          if (h.err) { bad = true; return; }
-          if (!have_name) { name_off = s0; name_len = l; have_name = true; }
+        if ((info & 0xC0) == 0) {   // the root type by name (ASCII), the same one for the whole update
+          if (vu() != 1u || (info & 0x20)) { bad = true; return; }
+          const uint32_t l = vu();
+          if (bad || l > n - pos || !ascii(pos, l)) { bad = true; return; }
+          if (!have_name) { name_off = pos; name_len = l; have_name = true; }
           else {
             if (l != name_len) { bad = true; return; }
-            for (uint32_t i = 0; i < l; i++) if (in[s0 + i] != in[name_off + i]) { bad = true; return; }
+            for (uint32_t i = 0; i < l; i++) if (in[pos + i] != in[name_off + i]) { bad = true; return; }
           }
+          pos += l;
         }
-        if (h.err) { bad = true; return; }
-        if (si.ref == 4) {   // ASCII: UTF-16 length == bytes
-          Cur q{in, si.cstart, si.end, 0, 0};
-          uint32_t l; const uint32_t s0 = q.buf(l);
-          if (q.err || l != si.len) { bad = true; return; }
-          x.coff = (uint16_t)s0; x.clen = (uint16_t)l;
+        uint32_t len;
+        if (ref == 1u) len = vu();                  // ContentDeleted
+        else {                                      // ContentString, ASCII: UTF-16 length == bytes
+          len = vu();
+          if (bad || len > n - pos || !ascii(pos, len)) { bad = true; return; }
+          x.coff = (uint16_t)pos; x.clen = (uint16_t)len;
+          pos += len;
         }
-        clock += si.len;
+        if (bad || len == 0 || clock + len > 0xFFFFu) { bad = true; return; }
+        x.clock = (uint16_t)clock; x.len = (uint16_t)len;
+        clock += len;
         np++; k.rn++;
       }
       nc++;
     }
-    if (c.err || bad) { bad = true; return; }
+    if (bad) return;
+    Cur c{in, pos, n, 0, 0};
     ds_pos = c.pos;
     const uint64_t nd = c.vu();
     for (uint64_t q = 0; q < nd && !c.err; q++) {
@@ -134,17 +156,14 @@ struct TDoc {
   // ------------------------------------------------------------------ lookups and splits (Doc::find / split)
   YDEV uint16_t find(uint32_t k, uint32_t clock) {
     if (clock >= ct[k].state) { bad = true; return NIL; }
-    int32_t lo = ct[k].r0, hi = (int32_t)ct[k].r0 + ct[k].ni - 1, r = -1;
-    {
-      const int32_t g = lo + ((int32_t)clock - (int32_t)p[lo].clock);
-      if (g >= lo && g <= hi && p[g].clock <= clock && (g == hi || p[g + 1].clock > clock)) { r = g; lo = hi + 1; }
-    }
-    while (lo <= hi) {
-      const int32_t m = (lo + hi) >> 1;
-      if (p[m].clock <= clock) { r = m; lo = m + 1; } else hi = m - 1;
-    }
-    if (r < 0) { bad = true; return NIL; }
-    uint16_t x = (uint16_t)r;
+    // the last input struct starting at or before clock: an interpolated guess over the client's integrated input
+    // structs (they tile [0, state) in clock order), then a walk to it -- a step or two for typed text
+    const int32_t lo = ct[k].r0, hi = (int32_t)ct[k].r0 + ct[k].ni - 1;
+    int32_t g = lo + (int32_t)(((uint32_t)(hi - lo + 1) * clock) / ct[k].state);
+    g = g > hi ? hi : g;
+    while (g > lo && p[g].clock > clock) g--;
+    while (g < hi && p[g + 1].clock <= clock) g++;
+    uint16_t x = (uint16_t)g;
     while (x != NIL && !(clock < (uint32_t)p[x].clock + p[x].len)) x = p[x].nxt;
     if (x == NIL) bad = true;
     return x;

@@ -277,14 +277,17 @@ static int snap_rc(const char* fn) {
 int ygm_k_launch_snap_text(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
                            uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, hipStream_t s) {
   if (n_docs == 0) return 0;
-  const char* env = getenv("YGM_SNAP_TEXT");   // experiments: "KiB:docs per wave" (default 12:1)
-  int lb = 12, dpw = 1;
+  // LDS per document 10 KiB, one document per wave (measured on f-1's 10 000 documents: 8 KiB leaves the larger
+  // documents to the general path, 12 / 16 KiB fit fewer documents per CU, 2-8 documents per wave diverge; 4.9-5.1 ms
+  // against 6.3 / 8.3 / 7.2-18 ms).  YGM_SNAP_TEXT="KiB:docs" picks another measured shape.
+  const char* env = getenv("YGM_SNAP_TEXT");
+  int lb = 10, dpw = 1;
   if (env) sscanf(env, "%d:%d", &lb, &dpw);
 #define SNT(L, D) if (lb == L && dpw == D) { hipLaunchKernelGGL((k_snap_text<L * 1024, D>), dim3((n_docs + D - 1) / D), dim3(SN_NT), 0, s, arena, doc_off, \
                                                          n_docs, flags, out, out_off, out_len, status, claim, pay); return snap_rc(__func__); }
-  SNT(8, 1) SNT(8, 2) SNT(8, 4) SNT(8, 8) SNT(10, 2) SNT(10, 4) SNT(10, 8) SNT(12, 2) SNT(12, 4) SNT(16, 1)
+  SNT(8, 1) SNT(12, 1) SNT(10, 2)
 #undef SNT
-  hipLaunchKernelGGL((k_snap_text<12288, 1>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
+  hipLaunchKernelGGL((k_snap_text<10240, 1>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
   return snap_rc(__func__);
 }
 int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, void* cnt, uint64_t* ws_off,

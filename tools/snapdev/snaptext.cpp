@@ -3,7 +3,7 @@
 // document the text path takes, its bytes must equal the general path's.  Output: one line per document,
 // "<taken 0/1> <general status> <equal 0/1>"; with out.bin, the text path's results in snapdev's format (status -1:
 // not taken).
-//     snaptext in.bin [flags] [budget] [out.bin]   (budget: LDS bytes of a workgroup, input included; default 12288)
+//     snaptext in.bin [flags] [budget] [out.bin]   (budget: LDS bytes of a workgroup, input included; default 10240)
 #define YGM_HOST_BUILD 1
 #include <cstdio>
 #include <cstdlib>
@@ -14,7 +14,7 @@
 int main(int argc, char** argv) {
   if (argc < 2) { fprintf(stderr, "usage: snaptext in.bin [flags] [budget]\n"); return 2; }
   const uint32_t flags = argc > 2 ? (uint32_t)atoi(argv[2]) : 0u;
-  const uint32_t budget = argc > 3 ? (uint32_t)atoi(argv[3]) : 12288u;
+  const uint32_t budget = argc > 3 ? (uint32_t)atoi(argv[3]) : 10240u;
   FILE* f = fopen(argv[1], "rb");
   FILE* g = argc > 4 ? fopen(argv[4], "wb") : nullptr;
   uint32_t n = 0; if (fread(&n, 4, 1, f) != 1) return 1;

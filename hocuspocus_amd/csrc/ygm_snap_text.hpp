@@ -4,7 +4,7 @@
 //
 // Why: the general kernel's integration is a serial chain of dependent accesses into a per-document workspace in
 // global memory (≈ 1 µs a step; a 160-struct document takes ≈ 10 ms however many documents run beside it).  Here
-// the same steps run on 28-byte part records in LDS.
+// the same steps run on 26-byte part records in LDS.
 //
 // Envelope (anything else returns false and the document goes to the general kernel, which decides its status):
 // Items with ContentDeleted / ASCII ContentString only (no GC, Skip, types, maps, embeds), items without origins
@@ -16,7 +16,7 @@
 //   * one root type: its list head (TypeRec::start); no nested types, so Item.delete is a flag and the GC of a
 //     deleted item (tryGcDeleteSet) turns its content into ContentDeleted -- done for every deleted part at once
 //     (every deleted part lies in a range the transaction's delete set recorded);
-//   * ASCII content: a part's bytes are its input slice [coff, coff + clen); a split cuts the slice at the clock
+//   * ASCII content: a part's bytes are its input slice [coff, coff + len); a split cuts the slice at the clock
 //     offset, and a merged part's bytes are its own slice followed by those of the parts it absorbed (they follow
 //     it in the client's clock order), so no piece lists.
 #pragma once
@@ -29,10 +29,10 @@ constexpr uint16_t NIL = 0xFFFFu;
 constexpr uint32_t CMAX = 16;
 enum : uint8_t { T_HO = 1, T_HR = 2, T_DEL = 4, T_INT = 8, T_GONE = 16, T_STR = 32 };
 
-struct P {                         // a part: Doc::SI for flat text (28 bytes)
+struct P {                         // a part: Doc::SI for flat text (26 bytes)
   uint16_t clock, len, ok, rk;     // id clock and length, origin / right origin clocks
   uint16_t left, right, nxt, orig; // document list, next split part, input struct
-  uint16_t coff, clen, ms, mr;     // own ASCII slice, integrate's conflict marks (epochs)
+  uint16_t coff, ms, mr;           // own ASCII slice start (its length: len until merged), integrate's conflict marks
   uint8_t cl, ocl, rcl, fl;        // client slot (block order), origin / right origin client slots, T_* flags
 };
 struct CT { uint32_t id, state; uint16_t r0, rn, ri, ni; int16_t ins, pad; };
@@ -90,7 +90,7 @@ struct TDoc {
         if (ref != 1u && ref != 4u) { bad = true; return; }   // GC / Skip / other content: the general path
         P& x = p[np];
         x.orig = (uint16_t)np; x.nxt = NIL; x.left = x.right = 0; x.ms = x.mr = 0; x.ok = x.rk = 0; x.ocl = x.rcl = 0;
-        x.cl = (uint8_t)nc; x.fl = ref == 4u ? T_STR : 0; x.coff = 0; x.clen = 0;
+        x.cl = (uint8_t)nc; x.fl = ref == 4u ? T_STR : 0; x.coff = 0;
         if (info & 0x80) {   // origin id: the client id parks in (ms, mr) until the client table is complete
           const uint32_t oc = vu(), ok = vu();
           if (ok > 0xFFFFu) bad = true;
@@ -117,7 +117,7 @@ struct TDoc {
         else {                                      // ContentString, ASCII: UTF-16 length == bytes
           len = vu();
           if (bad || len > n - pos || !ascii(pos, len)) { bad = true; return; }
-          x.coff = (uint16_t)pos; x.clen = (uint16_t)len;
+          x.coff = (uint16_t)pos;
           pos += len;
         }
         if (bad || len == 0 || clock + len > 0xFFFFu) { bad = true; return; }
@@ -181,7 +181,7 @@ struct TDoc {
     b.left = x; b.ocl = p[x].cl; b.ok = (uint16_t)(p[x].clock + diff - 1);
     b.fl = (uint8_t)((p[x].fl & (T_DEL | T_HR | T_INT | T_STR)) | T_HO);
     b.ms = b.mr = 0;
-    if (b.fl & T_STR) { b.coff = (uint16_t)(b.coff + diff); b.clen = (uint16_t)(b.clen - diff); p[x].clen = (uint16_t)diff; }
+    if (b.fl & T_STR) b.coff = (uint16_t)(b.coff + diff);
     b.nxt = p[x].nxt;
     p[r] = b;
     p[x].nxt = r; p[x].right = r; p[x].len = (uint16_t)diff;
@@ -366,7 +366,11 @@ struct TDoc {
           if (!ho && !hr) { o.b(1); o.vu(name_len); o.copy(in + name_off, name_len); }
           o.vu(u.len);
         }
-        if (u.fl & T_STR) o.copy(in + u.coff, u.clen);   // a merged part's bytes: its own, then those it absorbed
+        if (u.fl & T_STR) {   // a merged part's bytes: its own, then those it absorbed (the GONE parts after it,
+                              // each of whose len counts its own bytes and those it absorbed in turn)
+          const uint32_t nx = j + 1 < m && (p[sq[j + 1]].fl & T_GONE) ? p[sq[j + 1]].len : 0u;
+          o.copy(in + u.coff, u.len - nx);
+        }
       }
     }
     // delete set from the struct store: runs of deleted parts; clients in store order (13.5) or descending (13.6)

@@ -363,7 +363,8 @@ def f1_block(be, args, steps=5):
            "docs": args.f1_docs, "bytes_in": len(states), "bytes_out": int(r.payload_bytes), "ok_docs": int((stat == 0).sum()),
            "value": round(algo / kms / 1e3, 3), "unit": "MB/s", "docs_per_s": round(args.f1_docs / kms * 1e3, 1),
            "ms_per_step": round(kms, 4), "wall_ms_per_step": round(wall * 1e3, 4),
-           "roofline": roof(algo, kms, "k_snap_count + scan + k_snap (one thread per document)", None),
+           "roofline": roof(algo, kms, "k_snap_text (flat text: one document per wave, workspace in LDS) + k_snap_count / scan / k_snap "
+                                        "(one thread per document) for what it leaves", None),
            "parity": "yjs vectors in tests/test_snapshot.py (440 fixed + live sessions + GPU-merged C2 logs) -- bit-exact"}
     if not args.no_cpu_baseline and not args.no_yjs:
         c = {"arena": states, "doc_off": doc_off}
@@ -465,7 +466,8 @@ def v2_block(be, args, steps=5):
            "docs": n, "updates": n_upd, "bytes_in": len(a2), "bytes_out": int(r.payload_bytes),
            "value": round(algo / kms / 1e3, 3), "unit": "MB/s", "docs_per_s": round(n / kms * 1e3, 1), "ms_per_step": round(kms, 4),
            "wall_ms_per_step": round(wall * 1e3, 4),
-           "roofline": roof(algo, kms, "k_v21_count/write (lane per update) + V1 merge cascade + k_v12_fast (a V2 column per lane)", None),
+           "roofline": roof(algo, kms, "k_v21f (lane per update, column decoders in registers) + V1 merge cascade + k_v12_fast "
+                                        "(a V2 column per lane)", None),
            "convert": conv, "parity": f"bit-exact vs oracle (yjs_oracle_v2.c) on {checked} sampled docs; tests/test_v2.py: 4887 yjs vectors"}
     if not args.no_cpu_baseline and not args.no_yjs:
         blk["cpu_baseline"] = cpu_yjs("merge_v2", {"arena": a2, "upd_off": o2, "doc_upd": d1}, cpu_cores(args), min(n, 4000))

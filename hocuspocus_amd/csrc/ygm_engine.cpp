@@ -27,7 +27,7 @@ size_t ygm_k_sv_table_bytes(uint32_t n_docs);
 int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, void* cnt, uint64_t* ws_off,
                            uint64_t* bs, const uint8_t* claim, hipStream_t s);
 int ygm_k_launch_snap_text(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
-                          uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, hipStream_t s);
+                           uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, int again, hipStream_t s);
 int ygm_k_launch_cont_plan(const uint8_t* st_arena, const uint64_t* st_off, uint32_t n_docs, uint32_t flags, uint64_t* ws_off, uint64_t* bs,
                            hipStream_t s);
 int ygm_k_launch_cont(const uint8_t* st_arena, const uint64_t* st_off, const uint8_t* up_arena, const uint64_t* up_off, uint32_t n_docs,
@@ -497,12 +497,14 @@ int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_by
   if (lds) {
     if (!c->sn_ws.ensure(slot_total + 64) || !c->sn_claim.ensure((size_t)n_docs + 16) || !c->sn_pay.ensure(16)) return YGM_ENOMEM;
     HIPCHK(hipMemsetAsync(c->sn_pay.p, 0, 16, s));
-    if (ygm_k_launch_snap_text(d_arena, d_doc_off, n_docs, c->flags, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(),
-                              c->status.as<int32_t>(), c->sn_claim.as<uint8_t>(), c->sn_pay.as<unsigned long long>(), s))
-      return YGM_EDEVICE;
-    HIPCHK(hipMemcpyAsync(c->h_meta, c->sn_pay.p, 16, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    memcpy(lds_pay, c->h_meta, 16);
+    for (int again = 0; again < 2 && lds_pay[1] < n_docs; again++) {   // 8 KiB per document, then 32 KiB for what it left
+      if (ygm_k_launch_snap_text(d_arena, d_doc_off, n_docs, c->flags, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(),
+                                 c->status.as<int32_t>(), c->sn_claim.as<uint8_t>(), c->sn_pay.as<unsigned long long>(), again, s))
+        return YGM_EDEVICE;
+      HIPCHK(hipMemcpyAsync(c->h_meta, c->sn_pay.p, 16, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      memcpy(lds_pay, c->h_meta, 16);
+    }
   }
   uint64_t total = 0;   // workspace bytes: one read of the scanned total
   Meta m;

@@ -49,9 +49,10 @@ template <uint32_t LB, uint32_t DPW>
 __global__ __launch_bounds__(SN_NT) void k_snap_text(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off, uint32_t n_docs,
                                                     uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status, uint8_t* __restrict__ claim,
-                                                    unsigned long long* __restrict__ pay) {
+                                                    unsigned long long* __restrict__ pay, uint32_t again) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LB * DPW];
   const uint32_t d0 = blockIdx.x * DPW;
+  if (again && DPW == 1 && claim[d0]) return;   // a second launch with a larger region: the first one took it
   for (uint32_t j = 0; j < DPW && d0 + j < n_docs; j++) {
     const uint64_t a = doc_off[d0 + j], b = doc_off[d0 + j + 1];
     const uint64_t a16 = a & ~15ull, sb = (b - a16 + 15u) & ~15ull;
@@ -60,13 +61,17 @@ __global__ __launch_bounds__(SN_NT) void k_snap_text(const uint8_t* __restrict__
     for (uint32_t c = threadIdx.x; 16u * c < sb; c += SN_NT) ((uint4*)(lds + LB * j))[c] = src[c];   // (arena tail padding >= 16)
   }
   __syncthreads();
-  const uint32_t d = d0 + threadIdx.x;
-  if (threadIdx.x >= DPW || d >= n_docs) return;
+  // one document per wave: its index and LDS region stay wave-uniform (blockIdx), so the compiler keeps the
+  // document's control flow on scalar branches instead of exec-mask juggling around every test
+  const uint32_t lane = DPW == 1 ? 0u : threadIdx.x;
+  if (threadIdx.x >= DPW) return;
+  const uint32_t d = d0 + lane;
+  if (d >= n_docs) return;
   const uint64_t a = doc_off[d], b = doc_off[d + 1];
   const uint64_t a16 = a & ~15ull, sb = (b - a16 + 15u) & ~15ull;
   bool ok = false;
   if (b > a && sb + 1024u <= LB) {
-    uint8_t* reg = lds + LB * threadIdx.x;
+    uint8_t* reg = lds + LB * lane;
     const uint32_t n = (uint32_t)(b - a);
     const uint64_t slot = snap::al16(2 * a + 64ull * d);
     snap::OutCap o{out + slot, 0, 2u * n + 48u};
@@ -275,19 +280,25 @@ static int snap_rc(const char* fn) {
 // phase 1: counts and the scanned workspace offsets (ws_off: n_docs + 1 entries, total at [n_docs];
 // bs: ceil(n / 256) + 1 scratch entries)
 int ygm_k_launch_snap_text(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
-                           uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, hipStream_t s) {
+                           uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, int again, hipStream_t s) {
   if (n_docs == 0) return 0;
-  // LDS per document 10 KiB, one document per wave (measured on f-1's 10 000 documents: 8 KiB leaves the larger
-  // documents to the general path, 12 / 16 KiB fit fewer documents per CU, 2-8 documents per wave diverge; 4.9-5.1 ms
-  // against 6.3 / 8.3 / 7.2-18 ms).  YGM_SNAP_TEXT="KiB:docs" picks another measured shape.
+  // again == 0: 8 KiB of LDS per document, one document per wave (f-1's 10 000 merged C2 logs: 3.8 ms; 10 / 12 KiB fit
+  // fewer documents per CU, 2-8 documents per wave diverge off the scalar branches); again == 1: 32 KiB for the
+  // documents the first launch left.  YGM_SNAP_TEXT="KiB:docs" picks another measured shape for the first launch.
+  if (again) {
+    hipLaunchKernelGGL((k_snap_text<32768, 1>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status,
+                       claim, pay, 1u);
+    return snap_rc(__func__);
+  }
   const char* env = getenv("YGM_SNAP_TEXT");
-  int lb = 10, dpw = 1;
+  int lb = 8, dpw = 1;
   if (env) sscanf(env, "%d:%d", &lb, &dpw);
 #define SNT(L, D) if (lb == L && dpw == D) { hipLaunchKernelGGL((k_snap_text<L * 1024, D>), dim3((n_docs + D - 1) / D), dim3(SN_NT), 0, s, arena, doc_off, \
-                                                         n_docs, flags, out, out_off, out_len, status, claim, pay); return snap_rc(__func__); }
-  SNT(8, 1) SNT(12, 1) SNT(10, 2)
+                                                         n_docs, flags, out, out_off, out_len, status, claim, pay, 0u); return snap_rc(__func__); }
+  SNT(6, 1) SNT(10, 1) SNT(12, 1) SNT(10, 2)
 #undef SNT
-  hipLaunchKernelGGL((k_snap_text<10240, 1>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim, pay);
+  hipLaunchKernelGGL((k_snap_text<8192, 1>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim,
+                     pay, 0u);
   return snap_rc(__func__);
 }
 int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, void* cnt, uint64_t* ws_off,

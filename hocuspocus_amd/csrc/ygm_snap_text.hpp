@@ -155,11 +155,12 @@ struct TDoc {
 
   // ------------------------------------------------------------------ lookups and splits (Doc::find / split)
   YDEV uint16_t find(uint32_t k, uint32_t clock) {
-    if (clock >= ct[k].state) { bad = true; return NIL; }
+    const CT kk = ct[k];
+    if (clock >= kk.state) { bad = true; return NIL; }
     // the last input struct starting at or before clock: an interpolated guess over the client's integrated input
     // structs (they tile [0, state) in clock order), then a walk to it -- a step or two for typed text
-    const int32_t lo = ct[k].r0, hi = (int32_t)ct[k].r0 + ct[k].ni - 1;
-    int32_t g = lo + (int32_t)(((uint32_t)(hi - lo + 1) * clock) / ct[k].state);
+    const int32_t lo = kk.r0, hi = (int32_t)kk.r0 + kk.ni - 1;
+    int32_t g = lo + (int32_t)(((uint32_t)(hi - lo + 1) * clock) / kk.state);
     g = g > hi ? hi : g;
     while (g > lo && p[g].clock > clock) g--;
     while (g < hi && p[g + 1].clock <= clock) g++;
@@ -200,23 +201,23 @@ struct TDoc {
   }
 
   // ------------------------------------------------------------------ integration (Doc::get_missing / integrate)
-  YDEV int get_missing(uint16_t x) {
-    const uint8_t fl = p[x].fl, cl = p[x].cl;
-    if ((fl & T_HO) && p[x].ocl != cl && p[x].ok >= ct[p[x].ocl].state) return p[x].ocl;
-    if ((fl & T_HR) && p[x].rcl != cl && p[x].rk >= ct[p[x].rcl].state) return p[x].rcl;
-    if (fl & T_HO) { const uint16_t l = clean_end(p[x].ocl, p[x].ok); p[x].left = l; }
-    if (fl & T_HR) { const uint16_t r = clean_start(p[x].rcl, p[x].rk); p[x].right = r; }
+  // Item.getMissing on u (its record read once into pu): the client of a missing dependency, or -1 with the left /
+  // right neighbours found (getItemCleanEnd / getItemCleanStart split the parts they land in; u itself is not
+  // integrated yet, so no split touches its record)
+  YDEV int get_missing(const P& pu, uint16_t& L, uint16_t& R) {
+    if ((pu.fl & T_HO) && pu.ocl != pu.cl && pu.ok >= ct[pu.ocl].state) return pu.ocl;
+    if ((pu.fl & T_HR) && pu.rcl != pu.cl && pu.rk >= ct[pu.rcl].state) return pu.rcl;
+    L = (pu.fl & T_HO) ? clean_end(pu.ocl, pu.ok) : NIL;
+    R = (pu.fl & T_HR) ? clean_start(pu.rcl, pu.rk) : NIL;
     return -1;
   }
   YDEV bool same(bool ha, uint32_t ac, uint32_t ak, bool hb, uint32_t bc, uint32_t bk) const {
     return (!ha && !hb) || (ha && hb && ac == bc && ak == bk);
   }
-  YDEV void integrate(uint16_t x) {
-    const uint8_t fl = p[x].fl;
+  YDEV void integrate(uint16_t x, const P& pu, uint16_t left, const uint16_t right) {
+    const uint8_t fl = pu.fl;
     const bool ho = fl & T_HO, hr = fl & T_HR;
-    const uint32_t oc = p[x].ocl, ok = p[x].ok, rc = p[x].rcl, rk = p[x].rk, myid = ct[p[x].cl].id;
-    uint16_t left = p[x].left;
-    const uint16_t right = p[x].right;
+    const uint32_t oc = pu.ocl, ok = pu.ok, rc = pu.rcl, rk = pu.rk, myid = ct[pu.cl].id;
     if ((left == NIL && (right == NIL || p[right].left != NIL)) || (left != NIL && p[left].right != right)) {
       uint16_t e = left;
       uint16_t o = left != NIL ? p[left].right : start;
@@ -239,17 +240,16 @@ struct TDoc {
         o = p[o].right;
       }
       left = e;
-      p[x].left = e;
     }
     uint16_t r;
     if (left != NIL) { r = p[left].right; p[left].right = x; }
     else { r = start; start = x; }
-    p[x].right = r;
+    p[x].left = left; p[x].right = r;
     if (r != NIL) p[r].left = x;
-    CT& k = ct[p[x].cl];   // addStruct
+    CT& k = ct[pu.cl];   // addStruct
     if (k.ins < 0) k.ins = (int16_t)n_ins++;
-    k.state = (uint32_t)p[x].clock + p[x].len;
-    k.ni = (uint16_t)(p[x].orig - k.r0 + 1);
+    k.state = (uint32_t)pu.clock + pu.len;
+    k.ni = (uint16_t)(pu.orig - k.r0 + 1);
     p[x].fl = (uint8_t)(fl | T_INT | ((fl & T_STR) ? 0 : T_DEL));   // ContentDeleted.integrate: deleted at once
   }
   YDEV void integrate_all() {   // Doc::integrate_all: highest client first, the dependency stack
@@ -264,10 +264,11 @@ struct TDoc {
     uint32_t sp = 0;
     for (;;) {
       if (bad) return;
-      const CT& k = ct[p[u].cl];
-      const int64_t diff = (int64_t)k.state - (int64_t)p[u].clock;
+      const P pu = p[u];
+      const int64_t diff = (int64_t)ct[pu.cl].state - (int64_t)pu.clock;
       if (diff < 0) { bad = true; return; }
-      const int m = get_missing(u);
+      uint16_t L = NIL, R = NIL;
+      const int m = get_missing(pu, L, R);
       if (bad) return;
       if (m >= 0) {
         if (sp >= cap || ct[m].ri >= ct[m].rn) { bad = true; return; }
@@ -276,7 +277,7 @@ struct TDoc {
         continue;
       }
       if (diff != 0) { bad = true; return; }
-      integrate(u);
+      integrate(u, pu, L, R);
       if (sp) u = sq[--sp];
       else if (cur >= 0 && ct[ord[cur]].ri < ct[ord[cur]].rn) u = (uint16_t)(ct[ord[cur]].r0 + ct[ord[cur]].ri++);
       else {
@@ -328,7 +329,7 @@ struct TDoc {
       const uint32_t m = client_seq(k, false);
       for (uint32_t e = m; e-- > 1;) {
         const uint16_t a = sq[e - 1], b = sq[e];
-        const P& L = p[a]; const P& R = p[b];
+        const P L = p[a], R = p[b];   // (both records read at once)
         if (((L.fl ^ R.fl) & (T_DEL | T_STR)) != 0) continue;
         if (!((R.fl & T_HO) && R.ocl == L.cl && R.ok == (uint32_t)L.clock + L.len - 1)) continue;
         if (L.right != b) continue;
@@ -357,7 +358,7 @@ struct TDoc {
       for (uint32_t j = 0; j < m; j++) live += (p[sq[j]].fl & T_GONE) ? 0u : 1u;
       o.vu(live); o.vu(ct[k].id); o.vu(p[sq[0]].clock);
       for (uint32_t j = 0; j < m; j++) {
-        const P& u = p[sq[j]];
+        const P u = p[sq[j]];
         if (!(u.fl & T_GONE)) {
           const bool ho = u.fl & T_HO, hr = u.fl & T_HR;
           o.b((uint8_t)(((u.fl & T_STR) ? 4 : 1) | (ho ? 0x80 : 0) | (hr ? 0x40 : 0)));

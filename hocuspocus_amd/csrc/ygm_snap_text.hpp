@@ -25,6 +25,13 @@
 namespace ygm {
 namespace snapt {
 
+#ifdef YGM_HOST_BUILD
+#define YSN_CONST
+#else
+#define YSN_CONST __attribute__((address_space(4)))   // the input is read-only for the kernel: scalar-cache loads
+#endif
+typedef const YSN_CONST uint32_t* InW;
+
 constexpr uint16_t NIL = 0xFFFFu;
 constexpr uint32_t CMAX = 16;
 enum : uint8_t { T_HO = 1, T_HR = 2, T_DEL = 4, T_INT = 8, T_GONE = 16, T_STR = 32 };
@@ -42,13 +49,15 @@ YDEV uint32_t ws_fixed() { return CMAX * (uint32_t)sizeof(CT) + CMAX; }
 YDEV uint32_t part_bytes() { return (uint32_t)sizeof(P) + 2u; }
 
 struct TDoc {
-  const uint8_t* in; uint32_t n, flags;
+  InW w32; uint32_t sh, n, flags;   // the input: byte i at bit 8 * ((i + sh) & 3) of w32[(i + sh) >> 2] (readable past n)
   P* p; uint32_t np, cap;
   CT* ct; uint8_t* ord; uint32_t nc;
   uint16_t* sq;
   uint32_t name_off, name_len, ds_pos, epoch, n_ins;
   uint16_t start;
   bool have_name, bad;
+
+  YDEV uint32_t at(uint32_t i) const { const uint32_t j = i + sh; return (w32[j >> 2] >> (8u * (j & 3u))) & 0xFFu; }
 
   YDEV int slot(uint32_t id) const {
     for (uint32_t k = 0; k < nc; k++) if (ct[k].id == id) return (int)k;
@@ -64,7 +73,7 @@ struct TDoc {
 #pragma unroll 1
     for (uint32_t k = 0; k < 5u; k++) {
       if (pos >= n) { bad = true; return 0; }
-      const uint32_t x = in[pos++];
+      const uint32_t x = at(pos++);
       v |= (x & 127u) << (7u * k);
       if (x < 128u) { if (k == 4u && (x & 0x70u)) bad = true; return v; }
     }
@@ -72,7 +81,7 @@ struct TDoc {
     return 0;
   }
   YDEV bool ascii(uint32_t a, uint32_t l) const {
-    for (uint32_t i = 0; i < l; i++) if (in[a + i] >= 0x80u) return false;
+    for (uint32_t i = 0; i < l; i++) if (at(a + i) >= 0x80u) return false;
     return true;
   }
   YDEV void parse() {
@@ -85,7 +94,7 @@ struct TDoc {
       k.id = client; k.state = 0; k.r0 = (uint16_t)np; k.rn = 0; k.ri = 0; k.ni = 0; k.ins = -1; k.pad = 0;
       for (uint32_t s = 0; s < ns && !bad; s++) {
         if (pos >= n || np >= cap) { bad = true; return; }
-        const uint8_t info = in[pos++];
+        const uint8_t info = (uint8_t)at(pos++);
         const uint32_t ref = info & 31u;
         if (ref != 1u && ref != 4u) { bad = true; return; }   // GC / Skip / other content: the general path
         P& x = p[np];
@@ -108,7 +117,7 @@ struct TDoc {
           if (!have_name) { name_off = pos; name_len = l; have_name = true; }
           else {
             if (l != name_len) { bad = true; return; }
-            for (uint32_t i = 0; i < l; i++) if (in[pos + i] != in[name_off + i]) { bad = true; return; }
+            for (uint32_t i = 0; i < l; i++) if (at(pos + i) != at(name_off + i)) { bad = true; return; }
           }
           pos += l;
         }
@@ -128,17 +137,16 @@ struct TDoc {
       nc++;
     }
     if (bad) return;
-    Cur c{in, pos, n, 0, 0};
-    ds_pos = c.pos;
-    const uint64_t nd = c.vu();
-    for (uint64_t q = 0; q < nd && !c.err; q++) {
-      const uint64_t client = c.vu(), nr = c.vu();
-      for (uint64_t r = 0; r < nr && !c.err; r++) {
-        const uint64_t ck = c.vu(), ln = c.vu();
-        if (client > 0xFFFFFFFFull || ck + ln > 0xFFFFFFFFull) { bad = true; return; }
+    ds_pos = pos;   // the delete set, checked now, applied after the structs
+    const uint32_t nd = vu();
+    for (uint32_t q = 0; q < nd && !bad; q++) {
+      (void)vu(); const uint32_t nr = vu();
+      for (uint32_t r = 0; r < nr && !bad; r++) {
+        const uint64_t ck = vu(), ln = vu();
+        if (ck + ln > 0xFFFFFFFFull) { bad = true; return; }
       }
     }
-    if (c.err) { bad = true; return; }
+    if (bad) return;
     for (uint32_t i = 0; i < np; i++) {   // origin client ids -> slots (an unknown client leaves the item pending)
       P& x = p[i];
       if (x.fl & T_HO) { const int k = slot(((uint32_t)x.ms << 16) | x.mr); if (k < 0) { bad = true; return; } x.ocl = (uint8_t)k; }
@@ -290,13 +298,13 @@ struct TDoc {
 
   // ------------------------------------------------------------------ delete set, GC, merge (Doc::apply_ds ..)
   YDEV void apply_ds() {
-    Cur c{in, ds_pos, n, 0, 0};
-    const uint64_t nd = c.vu();
+    pos = ds_pos;
+    const uint32_t nd = vu();
     for (uint64_t q = 0; q < nd && !bad; q++) {
-      const uint32_t client = (uint32_t)c.vu(); const uint64_t nr = c.vu();
+      const uint32_t client = vu(), nr = vu();
       const int k = slot(client);
       for (uint64_t r = 0; r < nr && !bad; r++) {
-        const uint64_t a = c.vu(), b = a + c.vu();
+        const uint64_t a = vu(); const uint64_t b = a + vu();
         if (k < 0) { bad = true; return; }   // (state 0: pending)
         const uint32_t s = ct[k].state;
         if (!(a < s) || s < b) { bad = true; return; }
@@ -364,13 +372,13 @@ struct TDoc {
           o.b((uint8_t)(((u.fl & T_STR) ? 4 : 1) | (ho ? 0x80 : 0) | (hr ? 0x40 : 0)));
           if (ho) { o.vu(ct[u.ocl].id); o.vu(u.ok); }
           if (hr) { o.vu(ct[u.rcl].id); o.vu(u.rk); }
-          if (!ho && !hr) { o.b(1); o.vu(name_len); o.copy(in + name_off, name_len); }
+          if (!ho && !hr) { o.b(1); o.vu(name_len); for (uint32_t i = 0; i < name_len; i++) o.b((uint8_t)at(name_off + i)); }
           o.vu(u.len);
         }
         if (u.fl & T_STR) {   // a merged part's bytes: its own, then those it absorbed (the GONE parts after it,
                               // each of whose len counts its own bytes and those it absorbed in turn)
           const uint32_t nx = j + 1 < m && (p[sq[j + 1]].fl & T_GONE) ? p[sq[j + 1]].len : 0u;
-          o.copy(in + u.coff, u.len - nx);
+          for (uint32_t i = 0, e = u.len - nx; i < e; i++) o.b((uint8_t)at(u.coff + i));
         }
       }
     }
@@ -419,7 +427,7 @@ template <class O>
 YDEV bool snapshot_text(const uint8_t* in, uint32_t n, uint32_t flags, uint8_t* ws, uint32_t ws_bytes, O& o) {
   if (n >= 0xFFFFu || ws_bytes < ws_fixed() + 16u * part_bytes()) return false;
   TDoc D;
-  D.in = in; D.n = n; D.flags = flags;
+  D.sh = (uint32_t)((uintptr_t)in & 3u); D.w32 = (InW)(in - D.sh); D.n = n; D.flags = flags;
   D.ct = (CT*)ws; D.ord = ws + CMAX * sizeof(CT); D.nc = 0;
   D.cap = (ws_bytes - ws_fixed()) / part_bytes();
   if (D.cap > 0xFFF0u) D.cap = 0xFFF0u;

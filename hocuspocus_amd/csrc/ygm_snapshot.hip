@@ -39,43 +39,27 @@ YDEV const uint8_t* snap_stage(uint8_t* stg, const uint8_t* __restrict__ arena, 
   return staged && x >= a && doc_off[d + 1] <= b ? stg + (x - a16) : arena + x;
 }
 
-// k_snap_text: DPW documents per workgroup (one wave), each with LB bytes of LDS: the lanes stage every document's
-// bytes into its region, then lane l < DPW runs document l's flat-text snapshot (ygm_snap_text.hpp) over a workspace
-// in the rest of its region -- the integration's dependent chain as LDS round trips instead of global ones, and
-// DPW documents sharing each instruction issue.  Documents outside the envelope or the workspace are left
-// unclaimed for the count / scan / k_snap path.  Outputs go to per-document slots at align16(2 * doc_off[d] + 64 * d),
-// 2n + 48 bytes each.
-template <uint32_t LB, uint32_t DPW>
+// k_snap_text: one document per workgroup (one wave): lane 0 runs the flat-text snapshot (ygm_snap_text.hpp) with
+// its workspace in the workgroup's LB bytes of LDS and its input read through the scalar cache (aligned dwords from
+// the constant address space: the kernel never writes the arena) -- the integration's dependent chain as LDS round
+// trips instead of global ones, the document index wave-uniform so the control flow stays on scalar branches.
+// Documents outside the envelope or the workspace are left unclaimed (a second launch with a larger LB, then the
+// count / scan / k_snap path).  Outputs go to per-document slots at align16(2 * doc_off[d] + 64 * d), 2n + 48 bytes.
+template <uint32_t LB>
 __global__ __launch_bounds__(SN_NT) void k_snap_text(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off, uint32_t n_docs,
                                                     uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status, uint8_t* __restrict__ claim,
                                                     unsigned long long* __restrict__ pay, uint32_t again) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LB * DPW];
-  const uint32_t d0 = blockIdx.x * DPW;
-  if (again && DPW == 1 && claim[d0]) return;   // a second launch with a larger region: the first one took it
-  for (uint32_t j = 0; j < DPW && d0 + j < n_docs; j++) {
-    const uint64_t a = doc_off[d0 + j], b = doc_off[d0 + j + 1];
-    const uint64_t a16 = a & ~15ull, sb = (b - a16 + 15u) & ~15ull;
-    if (b <= a || sb + 1024u > LB) continue;
-    const uint4* src = (const uint4*)(arena + a16);
-    for (uint32_t c = threadIdx.x; 16u * c < sb; c += SN_NT) ((uint4*)(lds + LB * j))[c] = src[c];   // (arena tail padding >= 16)
-  }
-  __syncthreads();
-  // one document per wave: its index and LDS region stay wave-uniform (blockIdx), so the compiler keeps the
-  // document's control flow on scalar branches instead of exec-mask juggling around every test
-  const uint32_t lane = DPW == 1 ? 0u : threadIdx.x;
-  if (threadIdx.x >= DPW) return;
-  const uint32_t d = d0 + lane;
-  if (d >= n_docs) return;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LB];
+  const uint32_t d = blockIdx.x;
+  if (threadIdx.x != 0 || (again && claim[d])) return;   // (again: the first launch took it)
   const uint64_t a = doc_off[d], b = doc_off[d + 1];
-  const uint64_t a16 = a & ~15ull, sb = (b - a16 + 15u) & ~15ull;
   bool ok = false;
-  if (b > a && sb + 1024u <= LB) {
-    uint8_t* reg = lds + LB * lane;
+  if (b > a && b - a < 0xFFFFu) {
     const uint32_t n = (uint32_t)(b - a);
     const uint64_t slot = snap::al16(2 * a + 64ull * d);
     snap::OutCap o{out + slot, 0, 2u * n + 48u};
-    ok = snapt::snapshot_text(reg + (a - a16), n, flags, reg + sb, LB - (uint32_t)sb, o) && o.n <= o.cap;
+    ok = snapt::snapshot_text(arena + a, n, flags, lds, LB, o) && o.n <= o.cap;
     if (ok) {
       out_off[d] = slot; out_len[d] = o.n; status[d] = ST_OK;
       atomicAdd(pay, (unsigned long long)o.n);
@@ -282,22 +266,22 @@ static int snap_rc(const char* fn) {
 int ygm_k_launch_snap_text(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
                            uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, int again, hipStream_t s) {
   if (n_docs == 0) return 0;
-  // again == 0: 8 KiB of LDS per document, one document per wave (f-1's 10 000 merged C2 logs: 3.8 ms; 10 / 12 KiB fit
-  // fewer documents per CU, 2-8 documents per wave diverge off the scalar branches); again == 1: 32 KiB for the
-  // documents the first launch left.  YGM_SNAP_TEXT="KiB:docs" picks another measured shape for the first launch.
+  // again == 0: 6 KiB of LDS per document (209 parts); again == 1: 24 KiB for the documents the first launch left.
+  // YGM_SNAP_TEXT="KiB" picks another measured size for the first launch.
   if (again) {
-    hipLaunchKernelGGL((k_snap_text<32768, 1>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status,
+    hipLaunchKernelGGL((k_snap_text<24576>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status,
                        claim, pay, 1u);
     return snap_rc(__func__);
   }
   const char* env = getenv("YGM_SNAP_TEXT");
-  int lb = 8, dpw = 1;
-  if (env) sscanf(env, "%d:%d", &lb, &dpw);
-#define SNT(L, D) if (lb == L && dpw == D) { hipLaunchKernelGGL((k_snap_text<L * 1024, D>), dim3((n_docs + D - 1) / D), dim3(SN_NT), 0, s, arena, doc_off, \
-                                                         n_docs, flags, out, out_off, out_len, status, claim, pay, 0u); return snap_rc(__func__); }
-  SNT(6, 1) SNT(10, 1) SNT(12, 1) SNT(10, 2)
+  const int lb = env ? atoi(env) : 6;
+#define SNT(L) if (lb == L) { hipLaunchKernelGGL((k_snap_text<L * 1024>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, \
+                                                   out_off, out_len, status, claim, pay, 0u); return snap_rc(__func__); }
+  SNT(4) SNT(5) SNT(8)
 #undef SNT
-  hipLaunchKernelGGL((k_snap_text<8192, 1>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim,
+  if (lb == 53) { hipLaunchKernelGGL((k_snap_text<5376>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status,
+                                     claim, pay, 0u); return snap_rc(__func__); }
+  hipLaunchKernelGGL((k_snap_text<6144>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim,
                      pay, 0u);
   return snap_rc(__func__);
 }

@@ -136,14 +136,14 @@ def test_text_kernel_code_on_host(tmp_path, mode):
     """The flat-text snapshot (ygm_snap_text.hpp, k_snap_text's code) host-compiled: on every document it takes
     (the 320 text sessions: concurrent peers, splits by origins and delete ranges; the 440 general sessions: the
     few that are flat text) its bytes are yjs's (13.5 mode; 13.6 default: client-descending delete sets) and the
-    general kernel code's; documents it leaves (nested types, formats, non-ASCII, past 10 KiB) go to the general path."""
+    general kernel code's; documents it leaves (nested types, formats, non-ASCII, past a 6 KiB workspace) go to the general path."""
     from golden import ds_to_desc
     exe = str(tmp_path / "snaptext")
     subprocess.run(["g++", "-O1", "-std=c++17", "-o", exe, os.path.join(ROOT, "tools", "snapdev", "snaptext.cpp")], check=True, timeout=300)
     for rows, min_taken in ((text_fixtures(), 300), (fixtures(), 1)):
         a, b = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
         write_in(a, [u for u, _ in rows])
-        r = subprocess.run([exe, a, str(mode), "10240", b], check=True, timeout=120, capture_output=True, text=True)
+        r = subprocess.run([exe, a, str(mode), "6144", b], check=True, timeout=120, capture_output=True, text=True)
         lines = [tuple(map(int, x.split())) for x in r.stdout.split("\n") if x]
         taken = [k for k, (t, _, _) in enumerate(lines) if t]
         assert len(taken) >= min_taken

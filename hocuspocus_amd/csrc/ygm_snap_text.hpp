@@ -68,21 +68,39 @@ struct TDoc {
   // A lean reader for the envelope's shapes: varuints of <= 5 bytes below 2^32 (larger ones, any read past the end,
   // a struct of another kind, a non-ASCII string: outside the envelope), the same values as read_struct / Cur::vu.
   uint32_t pos;
-  YDEV uint32_t vu() {
+  YDEV uint32_t vu() {   // one 8-byte window (two aligned dwords) holds the <= 5 bytes
+    const uint32_t j = pos + sh;
+    uint64_t win = (((uint64_t)w32[(j >> 2) + 1] << 32) | w32[j >> 2]) >> (8u * (j & 3u));
     uint32_t v = 0;
 #pragma unroll 1
     for (uint32_t k = 0; k < 5u; k++) {
       if (pos >= n) { bad = true; return 0; }
-      const uint32_t x = at(pos++);
+      const uint32_t x = (uint32_t)win & 0xFFu;
+      win >>= 8; pos++;
       v |= (x & 127u) << (7u * k);
       if (x < 128u) { if (k == 4u && (x & 0x70u)) bad = true; return v; }
     }
     bad = true;
     return 0;
   }
-  YDEV bool ascii(uint32_t a, uint32_t l) const {
-    for (uint32_t i = 0; i < l; i++) if (at(a + i) >= 0x80u) return false;
+  YDEV bool ascii(uint32_t a, uint32_t l) const {   // a dword at a time: no byte of [a, a + l) has its top bit set
+    for (uint32_t i = 0; i < l;) {
+      const uint32_t j = a + i + sh, q = j & 3u, take = 4u - q < l - i ? 4u - q : l - i;
+      const uint32_t w = w32[j >> 2] >> (8u * q);
+      const uint32_t m = take == 4u ? 0x80808080u : 0x80808080u & ((1u << (8u * take)) - 1u);
+      if (w & m) return false;
+      i += take;
+    }
     return true;
+  }
+  template <class O>
+  YDEV void copy_in(O& o, uint32_t a, uint32_t l) const {   // input bytes [a, a + l) to o, a dword fetched per 4 bytes
+    for (uint32_t i = 0; i < l;) {
+      const uint32_t j = a + i + sh, q = j & 3u, take = 4u - q < l - i ? 4u - q : l - i;
+      uint32_t w = w32[j >> 2] >> (8u * q);
+      for (uint32_t t = 0; t < take; t++) { o.b((uint8_t)w); w >>= 8; }
+      i += take;
+    }
   }
   YDEV void parse() {
     pos = 0;
@@ -372,13 +390,13 @@ struct TDoc {
           o.b((uint8_t)(((u.fl & T_STR) ? 4 : 1) | (ho ? 0x80 : 0) | (hr ? 0x40 : 0)));
           if (ho) { o.vu(ct[u.ocl].id); o.vu(u.ok); }
           if (hr) { o.vu(ct[u.rcl].id); o.vu(u.rk); }
-          if (!ho && !hr) { o.b(1); o.vu(name_len); for (uint32_t i = 0; i < name_len; i++) o.b((uint8_t)at(name_off + i)); }
+          if (!ho && !hr) { o.b(1); o.vu(name_len); copy_in(o, name_off, name_len); }
           o.vu(u.len);
         }
         if (u.fl & T_STR) {   // a merged part's bytes: its own, then those it absorbed (the GONE parts after it,
                               // each of whose len counts its own bytes and those it absorbed in turn)
           const uint32_t nx = j + 1 < m && (p[sq[j + 1]].fl & T_GONE) ? p[sq[j + 1]].len : 0u;
-          for (uint32_t i = 0, e = u.len - nx; i < e; i++) o.b((uint8_t)at(u.coff + i));
+          copy_in(o, u.coff, u.len - nx);
         }
       }
     }

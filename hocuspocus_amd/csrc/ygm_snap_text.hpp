@@ -375,23 +375,23 @@ struct TDoc {
   YDEV void encode(O& o) {
     uint32_t cnt = 0;
     for (uint32_t k = 0; k < nc; k++) cnt += ct[k].ni > 0 ? 1u : 0u;
-    o.vu(cnt);
+    o.vu32(cnt);
     for (uint32_t i = nc; i-- > 0;) {
       const uint32_t k = ord[i];
       if (!ct[k].ni) continue;
       const uint32_t m = client_seq(k, true);
       uint32_t live = 0;
       for (uint32_t j = 0; j < m; j++) live += (p[sq[j]].fl & T_GONE) ? 0u : 1u;
-      o.vu(live); o.vu(ct[k].id); o.vu(p[sq[0]].clock);
+      o.vu32(live); o.vu32(ct[k].id); o.vu32(p[sq[0]].clock);
       for (uint32_t j = 0; j < m; j++) {
         const P u = p[sq[j]];
         if (!(u.fl & T_GONE)) {
           const bool ho = u.fl & T_HO, hr = u.fl & T_HR;
           o.b((uint8_t)(((u.fl & T_STR) ? 4 : 1) | (ho ? 0x80 : 0) | (hr ? 0x40 : 0)));
-          if (ho) { o.vu(ct[u.ocl].id); o.vu(u.ok); }
-          if (hr) { o.vu(ct[u.rcl].id); o.vu(u.rk); }
-          if (!ho && !hr) { o.b(1); o.vu(name_len); copy_in(o, name_off, name_len); }
-          o.vu(u.len);
+          if (ho) { o.vu32(ct[u.ocl].id); o.vu32(u.ok); }
+          if (hr) { o.vu32(ct[u.rcl].id); o.vu32(u.rk); }
+          if (!ho && !hr) { o.b(1); o.vu32(name_len); copy_in(o, name_off, name_len); }
+          o.vu32(u.len);
         }
         if (u.fl & T_STR) {   // a merged part's bytes: its own, then those it absorbed (the GONE parts after it,
                               // each of whose len counts its own bytes and those it absorbed in turn)
@@ -407,7 +407,7 @@ struct TDoc {
       const uint32_t m = client_seq(k, false);
       for (uint32_t j = 0; j < m; j++) if (p[sq[j]].fl & T_DEL) { nds++; break; }
     }
-    o.vu(nds);
+    o.vu32(nds);
     for (uint32_t r = 0; r < nc; r++) {
       int32_t k = -1;
       if (flags & F_COMPAT_135) { for (uint32_t j = 0; j < nc; j++) if (ct[j].ins == (int32_t)r) k = (int32_t)j; }
@@ -417,12 +417,12 @@ struct TDoc {
       uint32_t runs = 0;
       for (uint32_t j = 0; j < m; j++) if ((p[sq[j]].fl & T_DEL) && (j == 0 || !(p[sq[j - 1]].fl & T_DEL))) runs++;
       if (!runs) continue;
-      o.vu(ct[k].id); o.vu(runs);
+      o.vu32(ct[k].id); o.vu32(runs);
       for (uint32_t j = 0; j < m;) {
         if (!(p[sq[j]].fl & T_DEL)) { j++; continue; }
         const uint32_t c0 = p[sq[j]].clock; uint32_t len = 0;
         while (j < m && (p[sq[j]].fl & T_DEL)) len += p[sq[j++]].len;
-        o.vu(c0); o.vu(len);
+        o.vu32(c0); o.vu32(len);
       }
     }
   }

@@ -85,6 +85,7 @@ struct OutCap {
   uint8_t* p; uint32_t n, cap;
   YDEV void b(uint8_t v) { if (n < cap) p[n] = v; n++; }
   YDEV void vu(uint64_t v) { while (v > 127) { b((uint8_t)(0x80 | (v & 127))); v >>= 7; } b((uint8_t)v); }
+  YDEV void vu32(uint32_t v) { while (v > 127u) { b((uint8_t)(0x80u | (v & 127u))); v >>= 7; } b((uint8_t)v); }
   YDEV void copy(const uint8_t* s, uint32_t len) { for (uint32_t i = 0; i < len; i++) b(s[i]); }
 };
 

@@ -27,7 +27,7 @@ size_t ygm_k_sv_table_bytes(uint32_t n_docs);
 int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, void* cnt, uint64_t* ws_off,
                            uint64_t* bs, const uint8_t* claim, hipStream_t s);
 int ygm_k_launch_snap_text(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
-                           uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, int again, hipStream_t s);
+                           uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, int again, uint64_t slot_total, hipStream_t s);
 int ygm_k_launch_cont_plan(const uint8_t* st_arena, const uint64_t* st_off, uint32_t n_docs, uint32_t flags, uint64_t* ws_off, uint64_t* bs,
                            hipStream_t s);
 int ygm_k_launch_cont(const uint8_t* st_arena, const uint64_t* st_off, const uint8_t* up_arena, const uint64_t* up_off, uint32_t n_docs,
@@ -72,7 +72,7 @@ int ygm_k_launch_v12_write(const uint8_t* v1, const uint64_t* v1_off, const uint
                            hipStream_t s);
 int ygm_k_launch_v12_fast(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint64_t* slot_off,
                           const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint8_t* out, uint64_t* fo, uint64_t* olen, int32_t* ost,
-                          uint8_t* claim, unsigned long long* payload, uint8_t* scr, hipStream_t s);
+                          uint8_t* claim, unsigned long long* payload, uint8_t* scr, uint64_t slot_total, hipStream_t s);
 size_t ygm_k_v12_fast_scratch();
 int ygm_k_launch_v2_status(const int32_t* ust, uint32_t n, int32_t* status, uint64_t* len, hipStream_t s);
 int ygm_k_launch_v2_lens(const uint64_t* off, const int32_t* st, uint32_t n, uint64_t* len, hipStream_t s);
@@ -479,7 +479,6 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
 int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
                            void* stream, ygm_device_result* out) {
   if (!c || !out) return YGM_EINVAL;
-  (void)arena_bytes;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   (void)hipSetDevice(c->device);
   const uint32_t nb = (n_docs + 1 + 255) / 256;
@@ -497,9 +496,9 @@ int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_by
   if (lds) {
     if (!c->sn_ws.ensure(slot_total + 64) || !c->sn_claim.ensure((size_t)n_docs + 16) || !c->sn_pay.ensure(16)) return YGM_ENOMEM;
     HIPCHK(hipMemsetAsync(c->sn_pay.p, 0, 16, s));
-    for (int again = 0; again < 2 && lds_pay[1] < n_docs; again++) {   // 8 KiB per document, then 32 KiB for what it left
+    for (int again = 0; again < 2 && lds_pay[1] < n_docs; again++) {   // 6 KiB per document, then 24 KiB for what it left
       if (ygm_k_launch_snap_text(d_arena, d_doc_off, n_docs, c->flags, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(),
-                                 c->status.as<int32_t>(), c->sn_claim.as<uint8_t>(), c->sn_pay.as<unsigned long long>(), again, s))
+                                 c->status.as<int32_t>(), c->sn_claim.as<uint8_t>(), c->sn_pay.as<unsigned long long>(), again, slot_total, s))
         return YGM_EDEVICE;
       HIPCHK(hipMemcpyAsync(c->h_meta, c->sn_pay.p, 16, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
@@ -630,7 +629,7 @@ static int v12_pass(ygm_ctx* c, hipStream_t s, const uint8_t* v1, const uint64_t
     HIPCHK(hipMemsetAsync(c->v2_pay.p, 0, 16, s));
     if (ygm_k_launch_v12_fast(v1, v1_off, v1_len, v1_st, slot_off, doc_upd, ust, n_docs, c->v2_out.as<uint8_t>(), c->v2_fo.as<uint64_t>(),
                               c->v2_olen.as<uint64_t>(), c->v2_ost.as<int32_t>(), claim, c->v2_pay.as<unsigned long long>(),
-                              c->v2_scr.as<uint8_t>(), s))
+                              c->v2_scr.as<uint8_t>(), slot_total, s))
       return YGM_EDEVICE;
     HIPCHK(hipMemcpyAsync(c->h_meta, c->v2_pay.p, 16, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));

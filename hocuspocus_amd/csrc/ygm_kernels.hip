@@ -19,6 +19,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "ygm_common.hpp"
 #include "ygm_merge_seq.hpp"
 #include "ygm_merge_wave.hpp"
@@ -1667,7 +1669,7 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
     DIAGL(0);
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 1   // timing experiment: stage only
     { hn = lean_hdr_of(du, lean_bo_load(upd_off, du, LN_AHEAD(1), n_docs)); du = lean_du_load(doc_upd, LN_AHEAD(2), n_docs);
-      gn = !force_seq && lean_stageable<WIDE>(hn); lean_prefetch<WIDE>(arena, upd_off, hn, gn, v, rx, ry); wave_sync(); d = LN_AHEAD(1); continue; }
+      gn = !force_seq && lean_stageable<WIDE>(hn); lean_prefetch<WIDE>(arena, upd_off, hn, gn, v, rx, ry); wave_sync(); dit++; d = LN_AHEAD(1); continue; }
 #endif
     // ---- header of the next document (its prefetch is issued after the parse) and doc_upd of the one after
     const uint64_t bo_next = lean_bo_load(upd_off, du, LN_AHEAD(1), n_docs);
@@ -1724,7 +1726,7 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
     defer = defer || __ballot(bad) != 0;
     if (single) { wave_sync(); dit++; d = LN_AHEAD(1); continue; }   // (dit: bit j of dmask is the run's j-th document)
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 2   // timing experiment: stage + parse
-    if (l == 0) status[d] = (int)bad; wave_sync(); d = LN_AHEAD(1); continue;
+    if (l == 0) status[d] = (int)bad; wave_sync(); dit++; d = LN_AHEAD(1); continue;
 #endif
     if (!defer) {
       // ---- clients, discovered in descending order (wave max over the unassigned records): a
@@ -1852,7 +1854,7 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
         DIAGL(2);
         defer = __ballot(bad) != 0;
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 3   // timing experiment: stage + parse + scan
-        if (l == 0) status[d] = (int)bad + (int)(oex[0] & 1) + (int)(oex[1] & 1) + (int)(oex[2] & 1) + (int)(oex[3] & 1); wave_sync(); d = LN_AHEAD(1); continue;
+        if (l == 0) status[d] = (int)bad + (int)(oex[0] & 1) + (int)(oex[1] & 1) + (int)(oex[2] & 1) + (int)(oex[3] & 1); wave_sync(); dit++; d = LN_AHEAD(1); continue;
 #endif
         if (!defer) {
           const uint32_t at = vu_len(nC) + hdr_all;   // + the struct bytes: the delete set's position
@@ -2582,6 +2584,27 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
 
 // ======================================================================= launch glue
 // a failed launch names its kernel and the HIP error on stderr (the C ABI only returns YGM_EDEVICE)
+// persistent grid sizes are cached per device: a pool may drive GPUs of different sizes, its contexts from
+// different threads (the first computation on each device wins; a racing second one stores the same value)
+constexpr int YGM_MAX_DEVICES = 64;
+template <class F>
+static uint32_t per_device(std::atomic<uint32_t> (&cache)[YGM_MAX_DEVICES], F compute) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::atomic<uint32_t>& slot = cache[(unsigned)dev % YGM_MAX_DEVICES];
+  uint32_t v = slot.load(std::memory_order_relaxed);
+  if (!v) { v = compute(); slot.store(v, std::memory_order_relaxed); }
+  return v;
+}
+static uint32_t device_cus() {
+  static std::atomic<uint32_t> cache[YGM_MAX_DEVICES];
+  return per_device(cache, [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? (uint32_t)n : 256u;
+  });
+}
+
 static int launch_rc(const char* fn) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) fprintf(stderr, "ygm: %s: %s\n", fn, hipGetErrorString(e));
@@ -2709,8 +2732,7 @@ int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, 
                           uint32_t* tbl_n, hipStream_t s) {
   (void)arena_bytes; (void)sv_bytes; (void)flags;   // segments are read in 64-byte chunks: 64 bytes of tail padding (ygm.h)
   if (n_docs == 0) return 0;
-  static int n_cu = 0;
-  if (!n_cu) { int dev = 0; (void)hipGetDevice(&dev); if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256; }
+  const int n_cu = (int)device_cus();
   const char* env = getenv("YGM_WALK_WAVES_PER_CU");
   // resident waves per CU: 4 SIMDs x the waves per SIMD the walker is compiled for (its LDS fits them)
   const uint32_t wpc = env ? (uint32_t)atoi(env) : 4u * (mode == 0 ? YGM_DW_WPE0 : YGM_DW_WPE1);
@@ -2745,8 +2767,7 @@ int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const
                             uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
   if (n_docs == 0) return 0;
   // persistent waves: enough for full occupancy, each looping over documents d, d + G, ...
-  static int n_cu = 0;
-  if (!n_cu) { int dev = 0; (void)hipGetDevice(&dev); if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256; }
+  const int n_cu = (int)device_cus();
   const char* env = getenv("YGM_LEAN_WAVES_PER_CU");
   const uint32_t wpc = env ? (uint32_t)atoi(env) : 16u;
   const uint32_t grid = n_docs < (uint32_t)n_cu * wpc ? n_docs : (uint32_t)n_cu * wpc;
@@ -2760,8 +2781,8 @@ int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, 
                                  uint32_t n_list, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
                                  void* meta, void* meta_next, uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
   if (n_list == 0) return 0;
-  static uint32_t resident = 0;
-  if (!resident) { const char* g = getenv("YGM_WIDE_GRID"); resident = g ? (uint32_t)atoi(g) : resident_blocks(k_merge_lean<1>, WAVE, 2048u); }
+  static std::atomic<uint32_t> cache[YGM_MAX_DEVICES];
+  const uint32_t resident = per_device(cache, [] { const char* g = getenv("YGM_WIDE_GRID"); return g ? (uint32_t)atoi(g) : resident_blocks(k_merge_lean<1>, WAVE, 2048u); });
   const uint32_t grid = n_list < resident ? n_list : resident;
   hipLaunchKernelGGL(k_merge_lean<1>, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len, status,
                      (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap, list, n_list);
@@ -2774,8 +2795,8 @@ int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const
   if (n_docs == 0) return 0;
   // persistent: exactly the waves that are resident at once (LDS / VGPR occupancy x CUs), so no wave starts
   // its grid-stride share after the others have finished theirs; n_docs is the upper bound of the device count
-  static uint32_t resident = 0;
-  if (!resident) { const char* g = getenv("YGM_WAVE_GRID"); resident = g ? (uint32_t)atoi(g) : resident_blocks(k_merge_wave, WAVE, 2048u); }
+  static std::atomic<uint32_t> cache[YGM_MAX_DEVICES];
+  const uint32_t resident = per_device(cache, [] { const char* g = getenv("YGM_WAVE_GRID"); return g ? (uint32_t)atoi(g) : resident_blocks(k_merge_wave, WAVE, 2048u); });
   const uint32_t grid = n_docs < resident ? n_docs : resident;
   hipLaunchKernelGGL(k_merge_wave, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, docs, n_dev, n_docs,
                      flags, out, out_off, out_len, status, (DocMeta*)meta, defer_list, fb_list, out_cap);
@@ -2786,8 +2807,8 @@ int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const
                             const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
                             int32_t* status, uint64_t slot_total, void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s) {
   if (n_docs == 0) return 0;
-  static uint32_t resident = 0;   // persistent: the resident workgroups (see ygm_k_launch_merge_wave)
-  if (!resident) { const char* g = getenv("YGM_FAST_GRID"); resident = g ? (uint32_t)atoi(g) : resident_blocks(k_merge_fast, M_NT, 512u); }
+  static std::atomic<uint32_t> cache[YGM_MAX_DEVICES];   // persistent: the resident workgroups (see ygm_k_launch_merge_wave)
+  const uint32_t resident = per_device(cache, [] { const char* g = getenv("YGM_FAST_GRID"); return g ? (uint32_t)atoi(g) : resident_blocks(k_merge_fast, M_NT, 512u); });
   const uint32_t grid = n_docs < resident ? n_docs : resident;
   hipLaunchKernelGGL(k_merge_fast, dim3(grid), dim3(M_NT), 0, s, arena, upd_off, doc_upd, docs, n_dev, n_docs, flags, out, out_off, out_len,
                      status, slot_total, (DocMeta*)meta, fb_list, out_cap);

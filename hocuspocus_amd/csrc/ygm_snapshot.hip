@@ -49,13 +49,14 @@ template <uint32_t LB>
 __global__ __launch_bounds__(SN_NT) void k_snap_text(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off, uint32_t n_docs,
                                                     uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status, uint8_t* __restrict__ claim,
-                                                    unsigned long long* __restrict__ pay, uint32_t again) {
+                                                    unsigned long long* __restrict__ pay, uint32_t again, uint64_t slot_total) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LB];
   const uint32_t d = blockIdx.x;
   if (threadIdx.x != 0 || (again && claim[d])) return;   // (again: the first launch took it)
   const uint64_t a = doc_off[d], b = doc_off[d + 1];
   bool ok = false;
-  if (b > a && b - a < 0xFFFFu) {
+  // (a slot past the caller's region, slot_total = 2 * arena_bytes + 64 * n_docs: left to the general path)
+  if (b > a && b - a < 0xFFFFu && snap::al16(2 * a + 64ull * d) + 2 * (b - a) + 48 <= slot_total) {
     const uint32_t n = (uint32_t)(b - a);
     const uint64_t slot = snap::al16(2 * a + 64ull * d);
     snap::OutCap o{out + slot, 0, 2u * n + 48u};
@@ -264,25 +265,25 @@ static int snap_rc(const char* fn) {
 // phase 1: counts and the scanned workspace offsets (ws_off: n_docs + 1 entries, total at [n_docs];
 // bs: ceil(n / 256) + 1 scratch entries)
 int ygm_k_launch_snap_text(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
-                           uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, int again, hipStream_t s) {
+                           uint64_t* out_len, int32_t* status, uint8_t* claim, unsigned long long* pay, int again, uint64_t slot_total, hipStream_t s) {
   if (n_docs == 0) return 0;
   // again == 0: 6 KiB of LDS per document (209 parts); again == 1: 24 KiB for the documents the first launch left.
   // YGM_SNAP_TEXT="KiB" picks another measured size for the first launch.
   if (again) {
     hipLaunchKernelGGL((k_snap_text<24576>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status,
-                       claim, pay, 1u);
+                       claim, pay, 1u, slot_total);
     return snap_rc(__func__);
   }
   const char* env = getenv("YGM_SNAP_TEXT");
   const int lb = env ? atoi(env) : 6;
 #define SNT(L) if (lb == L) { hipLaunchKernelGGL((k_snap_text<L * 1024>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, \
-                                                   out_off, out_len, status, claim, pay, 0u); return snap_rc(__func__); }
+                                                   out_off, out_len, status, claim, pay, 0u, slot_total); return snap_rc(__func__); }
   SNT(4) SNT(5) SNT(8)
 #undef SNT
   if (lb == 53) { hipLaunchKernelGGL((k_snap_text<5376>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status,
-                                     claim, pay, 0u); return snap_rc(__func__); }
+                                     claim, pay, 0u, slot_total); return snap_rc(__func__); }
   hipLaunchKernelGGL((k_snap_text<6144>), dim3(n_docs), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, out, out_off, out_len, status, claim,
-                     pay, 0u);
+                     pay, 0u, slot_total);
   return snap_rc(__func__);
 }
 int ygm_k_launch_snap_plan(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, void* cnt, uint64_t* ws_off,

@@ -189,7 +189,7 @@ __global__ __launch_bounds__(64) void k_v12_fast(const uint8_t* __restrict__ v1,
                                                  const int32_t* __restrict__ ust, uint32_t n_docs, uint8_t* __restrict__ out,
                                                  uint64_t* __restrict__ fo, uint64_t* __restrict__ olen, int32_t* __restrict__ ost,
                                                  uint8_t* __restrict__ claim, unsigned long long* __restrict__ payload, int second,
-                                                 uint8_t* __restrict__ scr) {
+                                                 uint8_t* __restrict__ scr, uint64_t slot_total) {
   static_assert(D * v2f::FC_N <= WAVE, "nine lanes per document");
   typedef V2FDoc<FIN> Doc;
   constexpr uint32_t CAP = FIN + 64;   // scratch bytes per column (a column past it: the document goes on)
@@ -223,6 +223,7 @@ __global__ __launch_bounds__(64) void k_v12_fast(const uint8_t* __restrict__ v1,
       if (v1_st && v1_st[d] != ST_OK) bad = true;
       const uint64_t a = v1_off[d], len = v1_len ? v1_len[d] : v1_off[d + 1] - a;
       if (len > (uint64_t)FIN || len == 0) bad = true;
+      if (v2_slot(b0, d) + 2 * nb + 48 > slot_total) bad = true;   // a slot past the caller's region: the general pass
       if (__ballot(bad)) { if (l == 0 && !(second && claim[d])) claim[d] = 0; continue; }
       // stage: 16-byte loads from the aligned base (the V1 arenas carry >= 16 bytes of readable tail)
       const uint32_t sh = (uint32_t)(a & 15u), n = sh + (uint32_t)len;
@@ -344,15 +345,15 @@ size_t ygm_k_v12_fast_scratch() {
 }
 int ygm_k_launch_v12_fast(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const int32_t* v1_st, const uint64_t* slot_off,
                           const uint32_t* doc_upd, const int32_t* ust, uint32_t n_docs, uint8_t* out, uint64_t* fo, uint64_t* olen, int32_t* ost,
-                          uint8_t* claim, unsigned long long* payload, uint8_t* scr, hipStream_t s) {
+                          uint8_t* claim, unsigned long long* payload, uint8_t* scr, uint64_t slot_total, hipStream_t s) {
   if (n_docs == 0) return 0;
-  static uint32_t g1 = 0, g2 = 0;
-  if (!g1) { g1 = v12f_grid<V12F_D, V12F_FS>(); g2 = v12f_grid<2, (int)v2f::F_IN>(); }
+  // the grids of THIS device (the scratch was sized from the same calls, ygm_k_v12_fast_scratch)
+  const uint32_t g1 = v12f_grid<V12F_D, V12F_FS>(), g2 = v12f_grid<2, (int)v2f::F_IN>();
   const uint32_t n1 = (n_docs + V12F_D - 1) / V12F_D, n2 = (n_docs + 1) / 2;
   hipLaunchKernelGGL((k_v12_fast<V12F_D, V12F_FS>), dim3(n1 < g1 ? n1 : g1), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd,
-                     ust, n_docs, out, fo, olen, ost, claim, payload, 0, scr);
+                     ust, n_docs, out, fo, olen, ost, claim, payload, 0, scr, slot_total);
   hipLaunchKernelGGL((k_v12_fast<2, (int)v2f::F_IN>), dim3(n2 < g2 ? n2 : g2), dim3(WAVE), 0, s, v1, v1_off, v1_len, v1_st, slot_off, doc_upd,
-                     ust, n_docs, out, fo, olen, ost, claim, payload, 1, scr);
+                     ust, n_docs, out, fo, olen, ost, claim, payload, 1, scr, slot_total);
   return v2_rc(__func__);
 }
 int ygm_k_launch_v12_write(const uint8_t* v1, const uint64_t* v1_off, const uint64_t* v1_len, const uint8_t* v2a, uint64_t v2n,

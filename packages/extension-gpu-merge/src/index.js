@@ -43,9 +43,12 @@ class GpuMerge {
    * @param {{store?: DocumentStore|Function, fetch?: Function, device?: number, Y?: any,
    *          engine?: GpuEngine, batchWindowMs?: number, maxBatchDocs?: number, compat135?: boolean,
    *          onRefused?: 'reference'|'throw', normalize?: boolean}} configuration
-   *   onRefused: what a store does when the engine refuses a document's merge -- 'reference' (default):
-   *   store Y.encodeStateAsUpdate(document) like extension-database and record it in `refused`;
-   *   'throw': reject the store (Hocuspocus logs and rethrows, Hocuspocus.ts:431-435)
+   *   onRefused: what a store does when the engine refuses ONE document (a per-document status: content
+   *   yjs would re-encode, ENONCANON; a corrupt stored base, EMALFORMED / ERANGE / ESURROGATE / EDEPTH) --
+   *   'reference' (default): store Y.encodeStateAsUpdate(document) like extension-database and record it in
+   *   `refused`; 'throw': reject the store.  A failed batch (EDEVICE, ENOMEM, EINVAL, an addon or driver
+   *   error) always rejects the store (Hocuspocus logs and rethrows, Hocuspocus.ts:431-435): the product has
+   *   no CPU fallback for a lost or failing GPU (SURVEY.md §5)
    *   normalize (default true): store the doc-normalized snapshot of the merge, Y.encodeStateAsUpdate(
    *   Y.applyUpdate(new Y.Doc(), merged)) computed on the GPU (SURVEY.md §8f-1) -- deleted content
    *   garbage-collected and adjacent structs merged, the bytes extension-database stores for a fresh load of
@@ -168,14 +171,18 @@ class GpuMerge {
         if (this.normalize) state = await this._normalize(state, data.documentName)
       } catch (e) {
         // a document the engine refuses (content yjs would re-encode, YGM_ENONCANON; a corrupt stored
-        // base) or a failed batch: unless configured to throw, store what extension-database stores for
-        // it -- the live document's Y.encodeStateAsUpdate (Database.ts:58) -- so it keeps persisting
-        if (this.configuration.onRefused === 'throw') throw e
+        // base): unless configured to throw, store what extension-database stores for it -- the live
+        // document's Y.encodeStateAsUpdate (Database.ts:58) -- so it keeps persisting.  Anything else (the
+        // device, memory, a rejected batch) rejects the hook.
+        if (!isRefusal(e) || this.configuration.onRefused === 'throw') throw e
         this.refused.push({ documentName: data.documentName, code: e.code || String(e) })
         state = this._Y().encodeStateAsUpdate(data.document)
         cut = entry.log.length
       }
     }
+    // engine results are views into one buffer per batch: keep a copy of exactly this document's bytes, so
+    // the long-lived base (and the stored Buffer) do not pin the whole batch's result buffer
+    if (state.byteLength !== state.buffer.byteLength) state = new Uint8Array(state)
     await this.store.storeMany([{ payload: data, state: Buffer.from(state.buffer, state.byteOffset, state.byteLength) }])
     // the stored state becomes the new base (under the document's saveMutex, Hocuspocus.ts:427)
     entry.base = state
@@ -201,6 +208,10 @@ class GpuMerge {
   async onDestroy () { if (this.engine && !this.configuration.engine) this.engine.close(); this.engine = null }
 }
 
+// per-document statuses (the batch ran; this document's input was refused), as opposed to batch failures
+const REFUSALS = new Set(['EMALFORMED', 'ERANGE', 'ENONCANON', 'ESURROGATE', 'EDEPTH'])
+function isRefusal (e) { return !!e && REFUSALS.has(e.code) }
+
 // does `missing` (encodeStateAsUpdate(doc, baseSV)) add structs, or deletions that `base` does not hold?
 // Without structs its delete set is the document's whole delete set: it adds nothing iff merging it
 // into the base leaves the base's (sorted, merged) delete set unchanged -- decided by two engine merges.
@@ -212,4 +223,4 @@ async function addsToBase (engine, missing, base, name) {
   return Buffer.compare(Buffer.from(withIt), Buffer.from(without)) !== 0
 }
 
-module.exports = { GpuMerge, DocumentStore, GpuEngine, GpuEnginePool, SyncResponder, RedisFanout, UpdateLog, fnv1a64, YgmError }
+module.exports = { GpuMerge, DocumentStore, isRefusal, GpuEngine, GpuEnginePool, SyncResponder, RedisFanout, UpdateLog, fnv1a64, YgmError }

@@ -16,10 +16,13 @@ const { packJobs } = require('../src/engine.js')
 const mode = process.argv.includes('--gpu') ? 'gpu' : 'cpu'
 const Y = require(path.join(__dirname, '..', '..', '..', 'tools', 'yjs_bundle.js')).load()   // the test oracle: yjs from the image's bundle
 
+// a per-document status, as GpuEngine rejects a refused document (YgmError code)
+const refusal = fn => { try { return fn() } catch (e) { throw Object.assign(new Error(e.message), { code: 'EMALFORMED' }) } }
+
 class CpuDouble { // test double (never shipped): same API as GpuEngine
   constructor (device = 0) { this.calls = 0; this.device = device }
-  async mergeUpdates (u) { this.calls++; return Y.mergeUpdates(u) }
-  async mergePacked (job) { this.calls++; return Y.mergeUpdates(jobUpdates(job)) }
+  async mergeUpdates (u) { this.calls++; return refusal(() => Y.mergeUpdates(u)) }
+  async mergePacked (job) { this.calls++; return refusal(() => Y.mergeUpdates(jobUpdates(job))) }
   async mergeMany (docs) { this.calls++; return docs.map(u => { try { return Y.mergeUpdates(u) } catch (e) { return e } }) }   // per-document errors, as GpuEngine
   async diffMany (states, svs) { this.calls++; return states.map((u, i) => Y.diffUpdate(u, svs[i])) }
   async stateVectorsMany (states) { this.calls++; return states.map(u => Y.encodeStateVectorFromUpdate(u)) }
@@ -170,6 +173,52 @@ test('refused document: throws only its store, or stores the reference bytes', a
   assert.strictEqual(lax.refused.length, 1)
   assert.strictEqual(db.rows.get('bad').toString('hex'), Buffer.from(Y.encodeStateAsUpdate(p.document)).toString('hex'))
   assert.strictEqual(lax.docs.get('bad').log.length, 0)
+})
+
+// a failed batch (device lost, out of memory, a rejected native call) is not a refusal: the store hook rejects
+// (Hocuspocus.ts:431-435 logs and rethrows) instead of silently storing CPU bytes; the log is kept for a retry
+test('failed batch rejects the store; no CPU fallback', async (engine) => {
+  const db = memoryDb()
+  const failing = { // engine double whose every batch fails as a dead device would
+    async mergePacked () { throw Object.assign(new Error('hipErrorLaunchFailure'), { code: 'EDEVICE' }) },
+    async mergeUpdates () { throw new Error('addon: batch rejected') },
+    async snapshot () { throw Object.assign(new Error('out of device memory'), { code: 'ENOMEM' }) },
+    close () {}
+  }
+  for (const onRefused of ['reference', 'throw']) {
+    const ext = new GpuMerge({ ...db, Y, engine: failing, onRefused })
+    const document = new Y.Doc()
+    const log = new UpdateLog()
+    document.on('update', u => log.push(u))
+    document.getText('t').insert(0, 'a'); document.getText('t').insert(1, 'b')
+    ext.docs.set('dead', { base: null, log })
+    await assert.rejects(ext.onStoreDocument({ documentName: 'dead', document, context: {} }), /hipErrorLaunchFailure/)
+    assert.strictEqual(db.rows.has('dead'), false)
+    assert.strictEqual(ext.refused.length, 0)
+    assert.strictEqual(ext.docs.get('dead').log.length, 2)   // nothing dropped
+  }
+  // the merge succeeds but the normalizing snapshot batch fails: still a rejection
+  const ext = new GpuMerge({ ...db, Y, engine: { ...failing, mergePacked: async job => Y.mergeUpdates(jobUpdates(job)) } })
+  const log = new UpdateLog(); log.push(Y.encodeStateAsUpdate(new Y.Doc())); log.push(Uint8Array.from([0, 0]))
+  ext.docs.set('dead2', { base: null, log })
+  await assert.rejects(ext.onStoreDocument({ documentName: 'dead2', document: new Y.Doc(), context: {} }), /out of device memory/)
+  assert.strictEqual(db.rows.has('dead2'), false)
+})
+
+// the stored base is a copy of the document's bytes, not a view into the batch's shared result buffer
+test('stored base does not pin the batch result buffer', async (engine) => {
+  const db = memoryDb()
+  const ext = new GpuMerge({ ...db, Y, engine })
+  const hp = new MiniHocuspocus({ extensions: [ext], Y })
+  const docs = []
+  for (let d = 0; d < 8; d++) docs.push(await hp.loadDocument('pin-' + d))
+  docs.forEach((doc, d) => doc.transact(() => doc.getText('t').insert(0, 'x'.repeat(d + 1)), 'c'))
+  await hp.flushAll(); await hp.lastStore
+  await sleep(20)
+  for (let d = 0; d < 8; d++) {
+    const b = ext.docs.get('pin-' + d).base
+    assert.ok(b && b.byteLength === b.buffer.byteLength, 'base owns its buffer')
+  }
 })
 
 // the log is captured by a document listener: an earlier extension whose onChange throws, or one that

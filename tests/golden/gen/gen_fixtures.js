@@ -94,7 +94,9 @@ function appC () {
   const c1 = ['01010100040101740568656c6c6f00', '010101058401040620776f726c6400', '000101010001'].map(unhex)
   const m1 = Y.mergeUpdates(c1)
   runMerge(F, c1, 'C-1')
-  runDiff(F, m1, unhex('01010105'), 'C-1 diff sv{1:5}')
+  // sv bytes 01 01 01 05 decode as {1:1} plus a trailing byte (readStateVector stops after its count)
+  runDiff(F, m1, unhex('01010105'), 'C-1 diff sv{1:1} + trailing byte')
+  runDiff(F, m1, unhex('010105'), 'C-1 diff sv{1:5}')   // SURVEY App. C-1: 010101058401040620776f726c640101010001
   const a0 = unhex('01010700040101740368656c00'); const a1 = unhex('01010703840702026c6f00'); const st = unhex('01010700040101740568656c6c6f00')
   runMerge(F, [a0, a1, a0], 'C-2'); runMerge(F, [st, a0], 'C-2'); runMerge(F, [a0, st], 'C-2')
   const c4 = unhex('0201ac02004403000151010300040101740378797a0103010002')

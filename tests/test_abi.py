@@ -33,11 +33,31 @@ def test_strerror_and_version_without_gpu():
     assert eng.lib().ygm_version().startswith(b"ygm")
 
 
+PRODUCT_DIRS = ("hocuspocus_amd", os.path.join("packages", "extension-gpu-merge", "src"),
+                os.path.join("packages", "extension-gpu-merge", "addon"))
+
+
 def test_no_cpu_fallback_in_product():
-    # the product package must never import the oracle (test infrastructure)
-    pkg = os.path.join(ROOT, "hocuspocus_amd")
-    for dp, _, fs in os.walk(pkg):
-        for f in fs:
-            if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h", ".js", ".cc")):
-                txt = open(os.path.join(dp, f), errors="ignore").read()
-                assert "import oracle" not in txt and "liboracle" not in txt, f
+    # the product (Python package, Node extension and its N-API addon) never imports the oracle or the
+    # test-only yjs bundle loader
+    for d in PRODUCT_DIRS:
+        for dp, _, fs in os.walk(os.path.join(ROOT, d)):
+            for f in fs:
+                if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h", ".js", ".cc", ".c")):
+                    txt = open(os.path.join(dp, f), errors="ignore").read()
+                    assert "import oracle" not in txt and "liboracle" not in txt, f
+                    assert not re.search(r'#include\s*[<"][^">]*oracle', txt), f
+                    assert not re.search(r"require\([^)]*(oracle|yjs_bundle)", txt), f
+
+
+def test_gpumerge_reference_bytes_only_for_refused_documents():
+    # GpuMerge stores the CPU Y.encodeStateAsUpdate(document) only for a per-document refusal; a failed
+    # batch (EDEVICE / ENOMEM / a rejected native call) rethrows (device loss rejects the hook)
+    src = open(os.path.join(ROOT, "packages", "extension-gpu-merge", "src", "index.js")).read()
+    m = re.search(r"catch \(e\) \{(.*?)\n      \}", src[src.index("async onStoreDocument"):], flags=re.S)
+    assert m, "onStoreDocument has its refusal handler"
+    body = m.group(1)
+    assert "if (!isRefusal(e) || " in body and body.index("isRefusal") < body.index("this._Y().encodeStateAsUpdate")
+    refusals = re.search(r"REFUSALS = new Set\(\[(.*?)\]\)", src).group(1)
+    for code in ("EDEVICE", "ENOMEM", "EINVAL"):
+        assert code not in refusals

@@ -1,8 +1,12 @@
 /*
  * ygm_napi.c -- N-API addon: the thin extern "C" bridge between Node and libygm.so
- * (include/ygm.h).  Every batch runs on a libuv worker thread (napi_async_work),
- * so the Hocuspocus event loop never blocks on the GPU; results come back as a
- * Promise of { status: Int32Array, outputs: (Buffer|null)[] }.
+ * (include/ygm.h).  Every engine handle (one GPU context) owns ONE native worker
+ * thread with its own job queue; a batch runs there and its result is handed back to
+ * the event loop through a napi_threadsafe_function, so the Hocuspocus event loop
+ * never blocks on the GPU and an 8-GPU pool keeps 8 batches in flight (libuv's
+ * shared 4-thread pool -- napi_async_work -- would cap it at 4 and compete with
+ * fs / dns / crypto).  Results come back as a Promise of
+ * { status: Int32Array, outputs: (Uint8Array|null)[] }.
  *
  * JS surface (see ../index.d.ts):
  *   open(device, flags)                                  -> handle
@@ -14,6 +18,7 @@
  * typed arrays; SURVEY.md §8b "Ownership"); outputs are fresh Buffers.
  */
 #include <node_api.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
@@ -23,40 +28,120 @@
 
 #define NAPI_CALL(env, call) do { if ((call) != napi_ok) { napi_throw_error((env), NULL, "N-API call failed: " #call); return NULL; } } while (0)
 
+typedef struct Job Job;
 typedef struct {
   ygm_ctx *ctx;
   int busy;
+  /* the handle's worker: a FIFO of jobs, run one at a time on `thread` */
+  pthread_t thread; int has_thread;
+  pthread_mutex_t mu; pthread_cond_t cv;
+  Job *head, *tail; int stop;
+  napi_threadsafe_function tsfn;   /* worker -> event loop: settles a finished job's promise */
+  int refs;                        /* jobs whose completion is pending (the tsfn keeps the loop alive meanwhile) */
 } Handle;
 
-typedef struct {
-  int op; /* 0 merge, 1 diff, 2 sv */
+struct Job {
+  int op; /* 0 merge, 1 diff, 2 sv, ... 99 test sleep */
   Handle *h;
+  Job *next;
+  uint32_t sleep_ms; double t_start, t_end;   /* op 99 */
   uint8_t *arena; uint64_t *off; uint32_t *docs; uint32_t n_upd, n_docs;
   uint8_t *sv; uint64_t *sv_off;
   int rc;
   /* copied results */
   uint8_t *data; uint64_t *roff, *rlen; int32_t *status; uint32_t rn;
   napi_deferred deferred;
-  napi_async_work work;
   /* mergeMany: the caller's arena Buffer is read in place by the worker (held by a reference until the
      batch completes), not copied on the main thread */
   napi_ref arena_ref; int arena_borrowed;
   double exec_ms;       /* worker: the engine call + copy-out of its context-owned results */
-} Job;
+};
 
 static double now_ms(void) { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec * 1e3 + t.tv_nsec / 1e6; }
 static void free_data(napi_env env, void *data, void *hint) { (void)env; (void)hint; free(data); }
 
+static void job_execute(Job *j);
+static void job_complete(napi_env env, Job *j);
+
+static void *worker_main(void *arg) {
+  Handle *h = (Handle *)arg;
+  for (;;) {
+    pthread_mutex_lock(&h->mu);
+    while (!h->head && !h->stop) pthread_cond_wait(&h->cv, &h->mu);
+    if (!h->head) { pthread_mutex_unlock(&h->mu); break; }   /* stop, queue drained */
+    Job *j = h->head;
+    h->head = j->next; if (!h->head) h->tail = NULL;
+    pthread_mutex_unlock(&h->mu);
+    job_execute(j);
+    napi_call_threadsafe_function(h->tsfn, j, napi_tsfn_blocking);
+  }
+  return NULL;
+}
+
+/* runs on the event loop for every finished job */
+static void tsfn_call(napi_env env, napi_value js_cb, void *context, void *data) {
+  (void)js_cb;
+  Handle *h = (Handle *)context;
+  Job *j = (Job *)data;
+  if (env) job_complete(env, j);
+  if (env && --h->refs == 0) napi_unref_threadsafe_function(env, h->tsfn);
+}
+
+/* joins the worker (after the jobs queued so far) and frees the context */
+static void handle_stop(Handle *h) {
+  if (h->has_thread) {
+    pthread_mutex_lock(&h->mu); h->stop = 1; pthread_cond_signal(&h->cv); pthread_mutex_unlock(&h->mu);
+    pthread_join(h->thread, NULL);
+    h->has_thread = 0;
+    napi_release_threadsafe_function(h->tsfn, napi_tsfn_release);
+  }
+  if (h->ctx) { ygm_close(h->ctx); h->ctx = NULL; }
+}
+
 static void handle_finalize(napi_env env, void *data, void *hint) {
   (void)env; (void)hint;
   Handle *h = (Handle *)data;
-  if (h->ctx) ygm_close(h->ctx);
+  handle_stop(h);
+  pthread_mutex_destroy(&h->mu); pthread_cond_destroy(&h->cv);
   free(h);
 }
 
+static napi_value noop(napi_env env, napi_callback_info info) { (void)env; (void)info; return NULL; }
+
+/* a handle with its worker; ctx may be NULL (openNull: the threading test's sleep jobs only) */
+static napi_value make_handle(napi_env env, ygm_ctx *ctx) {
+  Handle *h = (Handle *)calloc(1, sizeof(Handle));
+  h->ctx = ctx;
+  pthread_mutex_init(&h->mu, NULL); pthread_cond_init(&h->cv, NULL);
+  napi_value fn, name, ext;
+  if (napi_create_function(env, "ygmSettle", NAPI_AUTO_LENGTH, noop, NULL, &fn) != napi_ok ||
+      napi_create_string_utf8(env, "ygm.worker", NAPI_AUTO_LENGTH, &name) != napi_ok ||
+      napi_create_threadsafe_function(env, fn, NULL, name, 0, 1, NULL, NULL, h, tsfn_call, &h->tsfn) != napi_ok) {
+    if (ctx) ygm_close(ctx);
+    free(h); napi_throw_error(env, NULL, "ygm: cannot create the worker's threadsafe function"); return NULL;
+  }
+  napi_unref_threadsafe_function(env, h->tsfn);   /* an idle engine does not keep Node alive */
+  if (pthread_create(&h->thread, NULL, worker_main, h) != 0) {
+    napi_release_threadsafe_function(h->tsfn, napi_tsfn_abort);
+    if (ctx) ygm_close(ctx);
+    free(h); napi_throw_error(env, NULL, "ygm: cannot start the engine's worker thread"); return NULL;
+  }
+  h->has_thread = 1;
+  NAPI_CALL(env, napi_create_external(env, h, handle_finalize, NULL, &ext));
+  return ext;
+}
+
+static Handle *get_handle_any(napi_env env, napi_value v) {
+  Handle *h = NULL;
+  if (napi_get_value_external(env, v, (void **)&h) != napi_ok || !h || !h->has_thread) {
+    napi_throw_error(env, NULL, "ygm: closed or invalid engine handle");
+    return NULL;
+  }
+  return h;
+}
 static Handle *get_handle(napi_env env, napi_value v) {
   Handle *h = NULL;
-  if (napi_get_value_external(env, v, (void **)&h) != napi_ok || !h || !h->ctx) {
+  if (napi_get_value_external(env, v, (void **)&h) != napi_ok || !h || !h->ctx || !h->has_thread) {
     napi_throw_error(env, NULL, "ygm: closed or invalid engine handle");
     return NULL;
   }
@@ -69,19 +154,20 @@ static napi_value js_open(napi_env env, napi_callback_info info) {
   int32_t device = 0; uint32_t flags = 0;
   if (argc > 0) napi_get_value_int32(env, argv[0], &device);
   if (argc > 1) napi_get_value_uint32(env, argv[1], &flags);
-  Handle *h = (Handle *)calloc(1, sizeof(Handle));
-  int rc = ygm_open(device, flags, &h->ctx);
-  if (rc != YGM_OK) { free(h); napi_throw_error(env, "YGM_EOPEN", ygm_strerror(rc)); return NULL; }
-  napi_value ext;
-  NAPI_CALL(env, napi_create_external(env, h, handle_finalize, NULL, &ext));
-  return ext;
+  ygm_ctx *ctx = NULL;
+  int rc = ygm_open(device, flags, &ctx);
+  if (rc != YGM_OK) { napi_throw_error(env, "YGM_EOPEN", ygm_strerror(rc)); return NULL; }
+  return make_handle(env, ctx);
 }
+
+/* openNull(): a handle with a worker but no GPU context -- accepts only sleep() jobs (threading test) */
+static napi_value js_open_null(napi_env env, napi_callback_info info) { (void)info; return make_handle(env, NULL); }
 
 static napi_value js_close(napi_env env, napi_callback_info info) {
   size_t argc = 1; napi_value argv[1];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   Handle *h = NULL;
-  if (napi_get_value_external(env, argv[0], (void **)&h) == napi_ok && h && h->ctx && !h->busy) { ygm_close(h->ctx); h->ctx = NULL; }
+  if (napi_get_value_external(env, argv[0], (void **)&h) == napi_ok && h && !h->busy) handle_stop(h);
   return NULL;
 }
 
@@ -135,11 +221,15 @@ static uint64_t *lens_to_off(const uint32_t *lens, uint32_t n) {
   return off;
 }
 
-static void job_execute(napi_env env, void *data) {
-  (void)env;
-  Job *j = (Job *)data;
+static void job_execute(Job *j) {
   const double t0 = now_ms();
   ygm_result r; memset(&r, 0, sizeof r);
+  if (j->op == 99) {   /* threading test: occupy the worker */
+    j->t_start = t0;
+    struct timespec ts = { j->sleep_ms / 1000, (long)(j->sleep_ms % 1000) * 1000000L };
+    nanosleep(&ts, NULL);
+    j->t_end = now_ms(); j->rc = YGM_OK; return;
+  }
   if (j->op == 0) j->rc = ygm_merge_v1(j->h->ctx, j->arena, j->off, j->docs, j->n_upd, j->n_docs, &r);
   else if (j->op == 1) j->rc = ygm_diff_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
   else if (j->op == 3) j->rc = ygm_snapshot_v1(j->h->ctx, j->arena, j->off, j->n_docs, &r);
@@ -173,15 +263,20 @@ static void job_free(Job *j) {
   free(j);
 }
 
-static void job_complete(napi_env env, napi_status st, void *data) {
-  Job *j = (Job *)data;
+static void job_complete(napi_env env, Job *j) {
   const double t0 = now_ms();
   j->h->busy = 0;
   if (j->arena_ref) { napi_delete_reference(env, j->arena_ref); j->arena_ref = NULL; }
   napi_value result = NULL, err = NULL;
-  if (st != napi_ok || j->rc != YGM_OK) {
+  if (j->op == 99) {
+    napi_value a, b;
+    napi_create_object(env, &result);
+    napi_create_double(env, j->t_start, &a); napi_create_double(env, j->t_end, &b);
+    napi_set_named_property(env, result, "start", a); napi_set_named_property(env, result, "end", b);
+    napi_resolve_deferred(env, j->deferred, result);
+  } else if (j->rc != YGM_OK) {
     napi_value msg, code;
-    napi_create_string_utf8(env, ygm_strerror(st != napi_ok ? YGM_EINVAL : j->rc), NAPI_AUTO_LENGTH, &msg);
+    napi_create_string_utf8(env, ygm_strerror(j->rc), NAPI_AUTO_LENGTH, &msg);
     napi_create_string_utf8(env, "YGM_EBATCH", NAPI_AUTO_LENGTH, &code);
     napi_create_error(env, code, msg, &err);
     napi_reject_deferred(env, j->deferred, err);
@@ -216,22 +311,39 @@ static void job_complete(napi_env env, napi_status st, void *data) {
     napi_set_named_property(env, result, "completeMs", cms);
     napi_resolve_deferred(env, j->deferred, result);
   }
-  napi_delete_async_work(env, j->work);
   job_free(j);
 }
 
+/* queues the job on its handle's worker thread */
 static napi_value submit(napi_env env, Job *j, const char *name) {
-  napi_value promise, res_name;
-  if (j->h->busy) {
+  (void)name;
+  napi_value promise;
+  Handle *h = j->h;
+  if (h->busy) {
     if (j->arena_ref) napi_delete_reference(env, j->arena_ref);
     job_free(j); napi_throw_error(env, "YGM_EBUSY", "ygm: one batch in flight per engine handle"); return NULL;
   }
   NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
-  NAPI_CALL(env, napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res_name));
-  NAPI_CALL(env, napi_create_async_work(env, NULL, res_name, job_execute, job_complete, j, &j->work));
-  j->h->busy = 1;
-  NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  h->busy = 1;
+  if (h->refs++ == 0) napi_ref_threadsafe_function(env, h->tsfn);   /* keep the loop alive until it settles */
+  pthread_mutex_lock(&h->mu);
+  j->next = NULL;
+  if (h->tail) h->tail->next = j; else h->head = j;
+  h->tail = j;
+  pthread_cond_signal(&h->cv);
+  pthread_mutex_unlock(&h->mu);
   return promise;
+}
+
+/* sleep(h, ms) -> Promise<{start, end}>: occupies the handle's worker for ms (threading test) */
+static napi_value js_sleep(napi_env env, napi_callback_info info) {
+  size_t argc = 2; napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  Handle *h = argc > 0 ? get_handle_any(env, argv[0]) : NULL;
+  if (!h) return NULL;
+  Job *j = (Job *)calloc(1, sizeof(Job)); j->op = 99; j->h = h;
+  if (argc > 1) napi_get_value_uint32(env, argv[1], &j->sleep_ms);
+  return submit(env, j, "ygm.sleep");
 }
 
 /* mergeMany(h, arena, lens, docs, nDocs) */
@@ -356,6 +468,8 @@ static napi_value js_snapshot(napi_env env, napi_callback_info info) {
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor d[] = {
     { "open", NULL, js_open, NULL, NULL, NULL, napi_default, NULL },
+    { "openNull", NULL, js_open_null, NULL, NULL, NULL, napi_default, NULL },
+    { "sleep", NULL, js_sleep, NULL, NULL, NULL, napi_default, NULL },
     { "close", NULL, js_close, NULL, NULL, NULL, napi_default, NULL },
     { "mergeMany", NULL, js_merge, NULL, NULL, NULL, napi_default, NULL },
     { "diffMany", NULL, js_diff, NULL, NULL, NULL, napi_default, NULL },

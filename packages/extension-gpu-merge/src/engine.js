@@ -214,7 +214,7 @@ function fnv1a64 (name) {
  * device, document -> device by fnv1a64(documentName) mod N, no cross-device traffic (documents
  * are independent; the reference scales by document too, docs/guides/scalability.md:12-14).
  * Same API as GpuEngine with a trailing document name; the *Many forms split a batch by shard,
- * run the shards concurrently (one libuv worker each) and return results in caller order.
+ * run the shards concurrently (one native worker thread per device handle, addon/ygm_napi.c) and return results in caller order.
  */
 class GpuEnginePool {
   constructor (opts = {}) {

@@ -468,6 +468,28 @@ test('engine pool shards by fnv1a64(name) and keeps caller order', async () => {
 })
 
 // SURVEY.md §8f-2: a reconnect storm -- SyncStep1 from many clients -- answered in one batch
+// every engine handle owns a native worker thread (addon/ygm_napi.c): an 8-GPU pool keeps 8 batches in flight at
+// once, where libuv's 4-thread pool (napi_async_work) would serialize half of them
+test('eight engine handles run eight native jobs at once', async () => {
+  const { loadAddon } = require('../src/engine.js')
+  const a = loadAddon()
+  const hs = Array.from({ length: 8 }, () => a.openNull())
+  const t0 = Date.now()
+  const r = await Promise.all(hs.map(h => a.sleep(h, 150)))
+  const lastStart = Math.max(...r.map(x => x.start)); const firstEnd = Math.min(...r.map(x => x.end))
+  assert.ok(lastStart < firstEnd, 'all eight jobs were running at the same time')
+  assert.ok(Date.now() - t0 < 8 * 150 / 2, 'not serialized')
+  hs.forEach(h => a.close(h))
+  if (mode === 'gpu') {   // eight contexts on the box's GPU, one batch each, all in flight together
+    const { GpuEngine } = require('../src/engine.js')
+    const engines = Array.from({ length: 8 }, () => new GpuEngine({ device: 0 }))
+    const docs = Array.from({ length: 64 }, (_, d) => { const y = new Y.Doc(); const ups = []; y.on('update', u => ups.push(u)); for (let i = 0; i < 20; i++) y.getText('t').insert(0, String.fromCharCode(97 + (d + i) % 26)); return ups })
+    const res = await Promise.all(engines.map(e => e.mergeMany(docs)))
+    res.forEach(rr => rr.forEach((m, d) => assert.strictEqual(Buffer.from(m).toString('hex'), Buffer.from(Y.mergeUpdates(docs[d])).toString('hex'))))
+    engines.forEach(e => e.close())
+  }
+})
+
 test('sync responder answers a SyncStep1 batch', async (engine) => {
   const db = memoryDb()
   const ext = new GpuMerge({ ...db, Y, engine })

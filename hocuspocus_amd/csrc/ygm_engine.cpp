@@ -171,6 +171,7 @@ struct ygm_ctx {
   // and the two stage contexts (own streams and buffers) that double-buffer a batch's chunks
   PinBuf h_data, h_off, h_len, h_status, h_in;
   DevBuf pk_data, pk_off, pk_bsum;
+  DevBuf s2_data, s2_off, s2_bsum, s2_st;   // sync step2: packed snapshots, their offsets, scan scratch, snapshot statuses
   ygm_ctx* kid[2] = {nullptr, nullptr};
   std::vector<uint32_t> h_doc_upd;
   ygm_stats_t stats{};
@@ -435,7 +436,8 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
 
 static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off,
                           const uint8_t* d_sv, uint64_t sv_bytes, const uint64_t* d_sv_off, uint32_t n_docs, void* stream,
-                          ygm_device_result* out) {
+                          ygm_device_result* out, uint32_t extra_flags = 0) {
+  const uint32_t flags = c ? c->flags | extra_flags : 0;
   if (!c || !out) return YGM_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   (void)hipSetDevice(c->device);
@@ -447,7 +449,7 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
   void* meta = c->meta_slot(2);
   if (mode == 1 && (!c->sv_tbl.ensure(ygm_k_sv_table_bytes(n_docs)) || !c->sv_tn.ensure(4ull * n_docs + 4))) return YGM_ENOMEM;
   HIPCHK(hipEventRecord(c->e0, s));
-  if (ygm_k_launch_doc_lean(mode, d_arena, arena_bytes, d_doc_off, d_sv, sv_bytes, d_sv_off, n_docs, c->flags, c->out.as<uint8_t>(),
+  if (ygm_k_launch_doc_lean(mode, d_arena, arena_bytes, d_doc_off, d_sv, sv_bytes, d_sv_off, n_docs, flags, c->out.as<uint8_t>(),
                             c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta,
                             c->defer_list.as<uint32_t>(), out_cap, c->sv_tbl.as<uint8_t>(), c->sv_tn.as<uint32_t>(), s))
     return YGM_EDEVICE;
@@ -459,7 +461,7 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
   if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) { c->stats.kernel_ms += ms; c->stats.lean_ms += ms; c->stats.lean_launches++; }
   if (m.lean_defer) {   // the exact per-document kernel over the deferred list, packed after the slots
     HIPCHK(hipEventRecord(c->e0, s));
-    if (ygm_k_launch_doc(mode, d_arena, d_doc_off, d_sv, d_sv_off, c->defer_list.as<uint32_t>(), slot_total, m.lean_defer, c->flags,
+    if (ygm_k_launch_doc(mode, d_arena, d_doc_off, d_sv, d_sv_off, c->defer_list.as<uint32_t>(), slot_total, m.lean_defer, flags,
                          c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
                          c->lb.as<unsigned long long>(), meta, out_cap, s))
       return YGM_EDEVICE;
@@ -580,6 +582,40 @@ int ygm_diff_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes,
 int ygm_sv_from_update_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
                                  void* stream, ygm_device_result* out) {
   return run_doc_kernel(c, 0, d_arena, arena_bytes, d_doc_off, nullptr, 0, nullptr, n_docs, stream, out);
+}
+
+// SyncStep2 of stored documents (MessageReceiver.ts:137-138): the snapshot batch, its outputs packed into one arena
+// on the device (k_pack_*: offsets n + 1, the total at [n]), the diff kernels over it with F_KEEP_SUB, and the
+// snapshot's per-document refusals (EUNSUPPORTED, malformed states) carried into the result
+int ygm_sync_step2_v1_device(ygm_ctx* c, const uint8_t* d_states, uint64_t states_bytes, const uint64_t* d_state_off,
+                             const uint8_t* d_sv_arena, const uint64_t* d_sv_off, uint32_t n_docs, void* stream,
+                             ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  (void)hipSetDevice(c->device);
+  ygm_device_result r1;
+  int e = ygm_snapshot_v1_device(c, d_states, states_bytes, d_state_off, n_docs, s, &r1);
+  if (e) return e;
+  const uint32_t nb = (n_docs + 255) / 256;
+  if (!c->s2_data.ensure(r1.payload_bytes + 64) || !c->s2_off.ensure(8ull * n_docs + 16) || !c->s2_bsum.ensure(8ull * nb + 16) ||
+      !c->s2_st.ensure(4ull * n_docs + 4))
+    return YGM_ENOMEM;
+  HIPCHK(hipMemsetAsync((uint8_t*)c->s2_data.p + r1.payload_bytes, 0, 64, s));   // readable tail for the walker's chunks
+  if (n_docs) {
+    if (ygm_k_launch_pack(r1.data, r1.off, r1.len, r1.status, n_docs, c->s2_bsum.as<uint64_t>(), c->s2_data.as<uint8_t>(),
+                          c->s2_off.as<uint64_t>(), s))
+      return YGM_EDEVICE;
+    HIPCHK(hipMemcpyAsync(c->s2_off.as<uint64_t>() + n_docs, c->s2_bsum.as<uint64_t>() + nb, 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->s2_st.p, r1.status, 4ull * n_docs, hipMemcpyDeviceToDevice, s));
+  }
+  uint64_t sv_end = 0;
+  if (n_docs && hipMemcpy(&sv_end, d_sv_off + n_docs, 8, hipMemcpyDeviceToHost) != hipSuccess) return YGM_EDEVICE;
+  e = run_doc_kernel(c, 1, c->s2_data.as<uint8_t>(), r1.payload_bytes, c->s2_off.as<uint64_t>(), d_sv_arena, sv_end, d_sv_off, n_docs, s,
+                     out, YGM_F_KEEP_SUB);
+  if (e) return e;
+  if (n_docs && ygm_k_launch_v2_status(c->s2_st.as<int32_t>(), n_docs, out->status, out->len, s)) return YGM_EDEVICE;
+  HIPCHK(hipStreamSynchronize(s));
+  return YGM_OK;
 }
 
 // ------------------------------------------------------------------ update V2 (device API)
@@ -769,7 +805,7 @@ struct Chunk {   // documents [d0, d1): merge updates [u0, u1) / SV-diff documen
 };
 struct HostCall {
   int mode;   // 0 sv, 1 diff, 2 merge, 3 snapshot, 4 contains (second arena in the sv slots); update V2: 5 merge, 6 diff,
-              // 7 sv, 8 V1 -> V2, 9 V2 -> V1
+              // 7 sv, 8 V1 -> V2, 9 V2 -> V1; 10 sync step2 (states + state vectors)
   const uint8_t* arena; const uint64_t* off; const uint32_t* upd_doc; const uint8_t* sv_arena; const uint64_t* sv_off;
   uint32_t n_upd, n_docs;
 };
@@ -819,7 +855,7 @@ static void par_for(size_t n, F f) {
 // CPU copy of a chunk's inputs into the stage's pinned buffer, then the async H2D copies
 static bool is_merge(int mode) { return mode == 2 || mode == 5; }
 static int chunk_stage(ygm_ctx* k, const HostCall& H, Chunk& C) {
-  const bool two = H.mode == 1 || H.mode == 4 || H.mode == 6;   // a second arena per document (diff: state vectors, contains: updates)
+  const bool two = H.mode == 1 || H.mode == 4 || H.mode == 6 || H.mode == 10;   // a second arena per document (diff: state vectors, contains: updates)
   const uint32_t nd = C.d1 - C.d0;
   const uint64_t a0 = is_merge(H.mode) ? H.off[C.u0] : H.off[C.d0], a1 = is_merge(H.mode) ? H.off[C.u1] : H.off[C.d1];
   const uint64_t bytes = a1 - a0, ab = (bytes + 64 + 15) & ~15ull;
@@ -881,6 +917,8 @@ static int chunk_run(ygm_ctx* c, ygm_ctx* k, const HostCall& H, Chunk& C, uint64
   else if (H.mode == 4) e = ygm_contains_v1_device(k, k->arena.as<uint8_t>(), k->offs.as<uint64_t>(), k->sv_arena.as<uint8_t>(),
                                                    k->sv_offs.as<uint64_t>(), nd, nullptr, &dr);
   else if (H.mode == 3) e = ygm_snapshot_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), nd, nullptr, &dr);
+  else if (H.mode == 10) e = ygm_sync_step2_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->sv_arena.as<uint8_t>(),
+                                                      k->sv_offs.as<uint64_t>(), nd, nullptr, &dr);
   else if (H.mode == 1) e = ygm_diff_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), k->sv_arena.as<uint8_t>(),
                                                k->sv_offs.as<uint64_t>(), nd, nullptr, &dr);
   else e = ygm_sv_from_update_v1_device(k, k->arena.as<uint8_t>(), bytes, k->offs.as<uint64_t>(), nd, nullptr, &dr);
@@ -1020,7 +1058,7 @@ int ygm_merge_v2(ygm_ctx* c, const uint8_t* arena, const uint64_t* upd_off, cons
 static int host_doc_call(ygm_ctx* c, int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena,
                          const uint64_t* sv_off, uint32_t n_docs, ygm_result* out) {
   if (!c || !out || (n_docs && (!arena || !doc_off))) return YGM_EINVAL;
-  const bool two = mode == 1 || mode == 4 || mode == 6;
+  const bool two = mode == 1 || mode == 4 || mode == 6 || mode == 10;
   if (two && n_docs && (!sv_arena || !sv_off)) return YGM_EINVAL;
   for (uint32_t d = 0; d < n_docs; d++) {
     if (doc_off[d + 1] < doc_off[d]) return YGM_EINVAL;
@@ -1038,6 +1076,11 @@ int ygm_contains_v1(ygm_ctx* c, const uint8_t* states, const uint64_t* state_off
 
 int ygm_snapshot_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, ygm_result* out) {
   return host_doc_call(c, 3, arena, doc_off, nullptr, nullptr, n_docs, out);
+}
+
+int ygm_sync_step2_v1(ygm_ctx* c, const uint8_t* states, const uint64_t* state_off, const uint8_t* sv_arena, const uint64_t* sv_off,
+                      uint32_t n_docs, ygm_result* out) {
+  return host_doc_call(c, 10, states, state_off, sv_arena, sv_off, n_docs, out);
 }
 
 int ygm_diff_v1(ygm_ctx* c, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,

@@ -43,6 +43,9 @@ constexpr uint64_t MAX_SAFE = 9007199254740991ull;  // Number.MAX_SAFE_INTEGER (
 constexpr int MAX_DEPTH = 32;                       // YGM_MAX_DEPTH
 constexpr int MAX_KEYS = 64;                        // keys tracked per Any/JSON nesting stack
 constexpr uint32_t F_COMPAT_135 = 1u;
+// diff: every struct keeps its input's parentSub bit 0x20 (Item.write of an integrated item, Y@80416): the bytes
+// Y.encodeStateAsUpdate(doc, sv) writes for a document loaded from a normalized state (ygm_sync_step2_v1)
+constexpr uint32_t F_KEEP_SUB = 4u;
 
 struct Cur {
   const uint8_t* p;
@@ -650,7 +653,8 @@ YDEV_NI int write_struct(Out& o, const uint8_t* base, const SInfo& s, uint64_t c
   const bool has_sub = !ho && !hr && (info & 0x20);  // parentSub only read without origins
   const bool o_out = ho || off > 0;
   if (off > 0) { oc = client; ok = clock + off - 1; }
-  o.b((uint8_t)((info & 31) | (o_out ? 0x80 : 0) | (hr ? 0x40 : 0) | (has_sub ? 0x20 : 0)));
+  const bool sub_bit = has_sub || ((flags & F_KEEP_SUB) && (info & 0x20));
+  o.b((uint8_t)((info & 31) | (o_out ? 0x80 : 0) | (hr ? 0x40 : 0) | (sub_bit ? 0x20 : 0)));
   if (o_out) { o.vu(oc); o.vu(ok); }
   if (hr) { o.vu(rc); o.vu(rk); }
   if (!ho && !hr) {

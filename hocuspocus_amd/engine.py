@@ -68,7 +68,7 @@ EXPORTS = ("ygm_open", "ygm_close", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_
            "ygm_contains_v1", "ygm_contains_v1_device", "ygm_stats", "ygm_strerror", "ygm_version",
            "ygm_merge_v2", "ygm_diff_v2", "ygm_sv_from_update_v2", "ygm_convert_v1_to_v2", "ygm_convert_v2_to_v1",
            "ygm_merge_v2_device", "ygm_diff_v2_device", "ygm_sv_from_update_v2_device", "ygm_convert_v1_to_v2_device",
-           "ygm_convert_v2_to_v1_device")
+           "ygm_convert_v2_to_v1_device", "ygm_sync_step2_v1", "ygm_sync_step2_v1_device")
 
 
 def lib():
@@ -101,6 +101,8 @@ def lib():
         L.ygm_snapshot_v1_device.argtypes = [vp, vp, u64, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_contains_v1.argtypes = [vp, vp, vp, vp, vp, u32, ctypes.POINTER(_Result)]
         L.ygm_contains_v1_device.argtypes = [vp, vp, vp, vp, vp, u32, vp, ctypes.POINTER(_DevResult)]
+        L.ygm_sync_step2_v1.argtypes = [vp, vp, vp, vp, vp, u32, ctypes.POINTER(_Result)]
+        L.ygm_sync_step2_v1_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_merge_v2.argtypes = [vp, vp, vp, vp, u32, u32, ctypes.POINTER(_Result)]
         L.ygm_diff_v2.argtypes = [vp, vp, vp, vp, vp, u32, ctypes.POINTER(_Result)]
         for f in ("ygm_sv_from_update_v2", "ygm_convert_v1_to_v2", "ygm_convert_v2_to_v1"):
@@ -118,7 +120,8 @@ def lib():
                   "ygm_diff_v1_device", "ygm_sv_from_update_v1_device", "ygm_snapshot_v1", "ygm_snapshot_v1_device",
                   "ygm_contains_v1", "ygm_contains_v1_device", "ygm_stats", "ygm_merge_v2", "ygm_diff_v2", "ygm_sv_from_update_v2",
                   "ygm_convert_v1_to_v2", "ygm_convert_v2_to_v1", "ygm_merge_v2_device", "ygm_diff_v2_device",
-                  "ygm_sv_from_update_v2_device", "ygm_convert_v1_to_v2_device", "ygm_convert_v2_to_v1_device"):
+                  "ygm_sv_from_update_v2_device", "ygm_convert_v1_to_v2_device", "ygm_convert_v2_to_v1_device",
+                  "ygm_sync_step2_v1", "ygm_sync_step2_v1_device"):
             getattr(L, f).restype = i32
         _lib = L
     return _lib
@@ -366,6 +369,18 @@ class Engine:
         arena, off = _pack([bytes(u) for u in updates])
         res = _Result()
         st = lib().ygm_snapshot_v1(self._ctx, arena or None, _ptr(off), len(updates), ctypes.byref(res))
+        if st != OK:
+            raise YjsError(st)
+        return self._unpack(res)
+
+    def sync_step2_batch(self, states, svs):
+        """SyncStep2 payloads of stored documents: Y.encodeStateAsUpdate(doc, sv) for doc = Y.applyUpdate(new Y.Doc(),
+        state) (MessageReceiver.ts:137-138; ygm_sync_step2_v1) -> list of (status, bytes | None); UNSUPPORTED marks
+        documents outside the snapshot envelope."""
+        sa, so = _pack([bytes(s) for s in states])
+        va, vo = _pack([bytes(v) for v in svs])
+        res = _Result()
+        st = lib().ygm_sync_step2_v1(self._ctx, sa or None, _ptr(so), va or None, _ptr(vo), len(states), ctypes.byref(res))
         if st != OK:
             raise YjsError(st)
         return self._unpack(res)

@@ -54,6 +54,7 @@ extern "C" {
 /* ---- context flags -------------------------------------------------------- */
 #define YGM_F_COMPAT_135 1u   /* delete-set clients in first-seen order; lone surrogate -> error */
 #define YGM_F_FORCE_SEQ 2u    /* route every merge through the exact sequential kernel (testing) */
+#define YGM_F_KEEP_SUB 4u     /* internal to ygm_sync_step2_v1: diffs keep each struct's parentSub bit (0x20) */
 
 typedef struct ygm_ctx ygm_ctx;
 
@@ -123,6 +124,15 @@ int ygm_snapshot_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off,
  * server acks with SyncStatus true), 0 = new content (SyncStatus false). */
 int ygm_contains_v1(ygm_ctx *ctx, const uint8_t *states, const uint64_t *state_off, const uint8_t *updates,
                     const uint64_t *update_off, uint32_t n_docs, ygm_result *out);
+/* SyncStep2 payload of a stored document: Y.encodeStateAsUpdate(doc, sv) for doc = Y.applyUpdate(new Y.Doc(), state)
+ * -- what the reference sends in reply to a SyncStep1 (packages/server/src/MessageReceiver.ts:137-138) for a
+ * document loaded from stored bytes (extension-database Database.ts:44-50).  Computed as the doc-normalized
+ * snapshot of `state` (ygm_snapshot_v1) followed by diffUpdate(snapshot, sv) in which every struct keeps its
+ * parentSub bit (Item.write of an integrated item, yjs Y@80416).  states / state_off as ygm_snapshot_v1;
+ * sv_arena / sv_off one encoded state vector per document.  A document outside the snapshot envelope carries
+ * YGM_EUNSUPPORTED (the caller names it and keeps its yjs path). */
+int ygm_sync_step2_v1(ygm_ctx *ctx, const uint8_t *states, const uint64_t *state_off, const uint8_t *sv_arena,
+                      const uint64_t *sv_off, uint32_t n_docs, ygm_result *out);
 
 /* ---- update format V2 ------------------------------------
  * The same operations over yjs's column-encoded update format V2 (UpdateEncoderV2 / UpdateDecoderV2,
@@ -197,6 +207,9 @@ int ygm_snapshot_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_
 
 int ygm_contains_v1_device(ygm_ctx *ctx, const uint8_t *d_states, const uint64_t *d_state_off, const uint8_t *d_updates,
                            const uint64_t *d_update_off, uint32_t n_docs, void *stream, ygm_device_result *out);
+int ygm_sync_step2_v1_device(ygm_ctx *ctx, const uint8_t *d_states, uint64_t states_bytes, const uint64_t *d_state_off,
+                             const uint8_t *d_sv_arena, const uint64_t *d_sv_off, uint32_t n_docs, void *stream,
+                             ygm_device_result *out);
 
 /* update V2, device-resident (outputs packed in document order: off[d] increasing) */
 int ygm_merge_v2_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_upd_off,

@@ -24,6 +24,7 @@ _LIB_PATH = os.path.join(_HERE, "liboracle.so")
 
 STATUS_NAMES = {0: "OK", 1: "EMALFORMED", 2: "ERANGE", 3: "ENONCANON", 4: "ESURROGATE", 5: "EDEPTH", 6: "ENOMEM"}
 COMPAT_135 = 1
+KEEP_SUB = 4    # diff: keep each struct's parentSub bit (YO_KEEP_SUB)
 
 _lib = None
 
@@ -85,14 +86,16 @@ def merge_updates(updates, compat135=False):
     return _take(out, olen, st)
 
 
-def diff_update(update, sv, compat135=False):
+def diff_update(update, sv, compat135=False, keep_sub=False):
+    """yjs diffUpdate(update, sv); keep_sub: every struct keeps its input's parentSub bit (encodeStateAsUpdate(doc, sv)
+    of a document loaded from `update` when `update` is that document's own encodeStateAsUpdate)."""
     L = lib()
     ub, ul = _buf(update)
     sb, sl = _buf(sv)
     out = ctypes.POINTER(ctypes.c_uint8)()
     olen = ctypes.c_size_t()
     st = L.yo_diff(ctypes.cast(ub, ctypes.POINTER(ctypes.c_uint8)), ul, ctypes.cast(sb, ctypes.POINTER(ctypes.c_uint8)), sl,
-                   COMPAT_135 if compat135 else 0, ctypes.byref(out), ctypes.byref(olen))
+                   (COMPAT_135 if compat135 else 0) | (KEEP_SUB if keep_sub else 0), ctypes.byref(out), ctypes.byref(olen))
     return _take(out, olen, st)
 
 

@@ -27,6 +27,11 @@
  * the 13.6.26 default: delete-set clients written in
  * first-seen order instead of client-descending, and a lone surrogate produced
  * by diffUpdate's string slicing throws instead of being written as U+FFFD.
+ * YO_KEEP_SUB (diff only): every struct keeps its input's parentSub bit (0x20) -- the
+ * bytes Y.encodeStateAsUpdate(doc, sv) writes for a Y.Doc loaded from a normalized
+ * state (Item.write of an integrated item sets the bit whenever parentSub !== null,
+ * Y@80416; the lazy reader of diffUpdate drops it beside an origin): the SyncStep2
+ * payload of MessageReceiver.ts:137-138 for a document loaded from stored bytes.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -43,6 +48,7 @@
 #define YO_ENOMEM 6
 
 #define YO_COMPAT_135 1
+#define YO_KEEP_SUB 4
 
 #define MAX_SAFE 9007199254740991ULL
 #define ANY_MAX_DEPTH 64
@@ -344,6 +350,7 @@ typedef struct {
   int parent_is_key;          /* parent is a ykey string (else an ID) */
   const uint8_t *pkey; size_t pkey_len; uint64_t pc, pk;
   int has_sub; const uint8_t *sub; size_t sub_len;
+  int sub_bit;                /* info bit 0x20 of the input (parentSub !== null in the writer's document) */
   const uint8_t *content; size_t content_len;  /* raw content bytes in the input */
   uint64_t cut;               /* content.splice(cut) already applied (sliceStruct) */
   int nc;                     /* content would be re-encoded differently by yjs */
@@ -434,7 +441,7 @@ static void reader_next(Reader *r) {
     if (r->d.err) return;
     if (info == 10) { s->kind = K_SKIP; s->len = rdu(&r->d); }
     else if (info & 31) {
-      s->kind = K_ITEM; s->ref = info & 31;
+      s->kind = K_ITEM; s->ref = info & 31; s->sub_bit = (info & 0x20) != 0;
       int cant_copy_parent = (info & (0x40 | 0x80)) == 0;
       if (info & 0x80) { s->has_origin = 1; s->oc = rdu(&r->d); s->ok = rdu(&r->d); }
       if (info & 0x40) { s->has_right = 1; s->rc = rdu(&r->d); s->rk = rdu(&r->d); }
@@ -527,7 +534,8 @@ static int write_struct(Buf *o, const St *s, uint64_t offset, int flags) {
   int ho = s->has_origin || offset > 0;
   uint64_t oc = s->oc, ok = s->ok;
   if (offset > 0) { oc = s->client; ok = s->clock + offset - 1; }
-  uint8_t info = (uint8_t)((s->ref & 31) | (ho ? 0x80 : 0) | (s->has_right ? 0x40 : 0) | (s->has_sub ? 0x20 : 0));
+  const int sub_bit = s->has_sub || ((flags & YO_KEEP_SUB) && s->sub_bit);
+  uint8_t info = (uint8_t)((s->ref & 31) | (ho ? 0x80 : 0) | (s->has_right ? 0x40 : 0) | (sub_bit ? 0x20 : 0));
   bbyte(o, info);
   if (ho) { bvu(o, oc); bvu(o, ok); }
   if (s->has_right) { bvu(o, s->rc); bvu(o, s->rk); }

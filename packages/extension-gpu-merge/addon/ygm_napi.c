@@ -234,6 +234,7 @@ static void job_execute(Job *j) {
   else if (j->op == 1) j->rc = ygm_diff_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
   else if (j->op == 3) j->rc = ygm_snapshot_v1(j->h->ctx, j->arena, j->off, j->n_docs, &r);
   else if (j->op == 4) j->rc = ygm_contains_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
+  else if (j->op == 5) j->rc = ygm_sync_step2_v1(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
   else if (j->op == 10) j->rc = ygm_merge_v2(j->h->ctx, j->arena, j->off, j->docs, j->n_upd, j->n_docs, &r);
   else if (j->op == 11) j->rc = ygm_diff_v2(j->h->ctx, j->arena, j->off, j->sv, j->sv_off, j->n_docs, &r);
   else if (j->op == 12) j->rc = ygm_sv_from_update_v2(j->h->ctx, j->arena, j->off, j->n_docs, &r);
@@ -473,6 +474,8 @@ static napi_value init(napi_env env, napi_value exports) {
     { "close", NULL, js_close, NULL, NULL, NULL, napi_default, NULL },
     { "mergeMany", NULL, js_merge, NULL, NULL, NULL, napi_default, NULL },
     { "diffMany", NULL, js_diff, NULL, NULL, NULL, napi_default, NULL },
+    /* SyncStep2 of stored documents: encodeStateAsUpdate(applyUpdate(new Doc, state), sv) (MessageReceiver.ts:137-138) */
+    { "step2Many", NULL, js_diff, NULL, NULL, NULL, napi_default, (void *)(intptr_t)5 },
     { "svMany", NULL, js_sv, NULL, NULL, NULL, napi_default, NULL },
     { "snapshotMany", NULL, js_snapshot, NULL, NULL, NULL, napi_default, NULL },
     { "containsMany", NULL, js_contains, NULL, NULL, NULL, napi_default, NULL },

@@ -148,9 +148,9 @@ class GpuEngine {
           return r
         })
       }
-      if (op === 'diff' || op === 'contains' || op === 'diffV2') {
+      if (op === 'diff' || op === 'contains' || op === 'diffV2' || op === 'step2') {
         const u = packBlobs(jobs.map(j => j[0])); const s = packBlobs(jobs.map(j => j[1]))
-        return ({ diff: a.diffMany, contains: a.containsMany, diffV2: a.diffManyV2 })[op](this.handle, u.arena, u.lens, s.arena, s.lens)
+        return ({ diff: a.diffMany, contains: a.containsMany, diffV2: a.diffManyV2, step2: a.step2Many })[op](this.handle, u.arena, u.lens, s.arena, s.lens)
       }
       const u = packBlobs(jobs)
       const unary = { snapshot: a.snapshotMany, sv: a.svMany, svV2: a.svManyV2, v1ToV2: a.convertManyV1ToV2, v2ToV1: a.convertManyV2ToV1 }
@@ -175,6 +175,10 @@ class GpuEngine {
   /** explicit batches (sync responders, bulk snapshot jobs) */
   async mergeMany (docs) { const r = await this._run('merge', docs); return unpack(r) }
   async diffMany (states, svs) { const r = await this._run('diff', states.map((s, i) => [s, svs[i]])); return unpack(r) }
+  /** SyncStep2 payloads of stored documents: Y.encodeStateAsUpdate(doc, sv) of doc = Y.applyUpdate(new Y.Doc(), state)
+   *  (MessageReceiver.ts:137-138) -- the snapshot, then a diff keeping each struct's parentSub bit; EUNSUPPORTED
+   *  outside the snapshot envelope */
+  async step2Many (states, svs) { const r = await this._run('step2', states.map((s, i) => [s, svs[i]])); return unpack(r) }
   async stateVectorsMany (states) { const r = await this._run('sv', states); return unpack(r) }
   async snapshotMany (states) { const r = await this._run('snapshot', states); return unpack(r) }
   /** Y.snapshotContainsUpdate(Y.snapshot(doc), update) per pair, `states` being normalized (snapshotMany) states */
@@ -248,6 +252,7 @@ class GpuEnginePool {
 
   mergeMany (names, docs) { return this._many(names, [docs], (e, d) => e.mergeMany(d)) }
   diffMany (names, states, svs) { return this._many(names, [states, svs], (e, a, b) => e.diffMany(a, b)) }
+  step2Many (names, states, svs) { return this._many(names, [states, svs], (e, a, b) => e.step2Many(a, b)) }
   stateVectorsMany (names, states) { return this._many(names, [states], (e, a) => e.stateVectorsMany(a)) }
   snapshotMany (names, states) { return this._many(names, [states], (e, a) => e.snapshotMany(a)) }
   containsMany (names, states, updates) { return this._many(names, [states, updates], (e, a, b) => e.containsMany(a, b)) }

@@ -9,9 +9,13 @@
 // The reference replies to Step1 with [Sync, Step2, encodeStateAsUpdate(doc, sv)] and then sends its
 // own first sync step [SyncReply (or Sync), Step1, encodeStateVector(doc)] (MessageReceiver.ts:137-155).
 // Here a document's state is its stored update (snapshot + captured log, merged on the GPU) and the
-// Step2 payload is diffUpdate(state, sv) -- byte-identical to yjs diffUpdate on that update; the
-// server's Step1 carries encodeStateVectorFromUpdate(state).  (Byte parity with encodeStateAsUpdate
-// of a live Y.Doc needs YATA integration: §8f-1.)
+// Step2 payload is the reference's own bytes for a document loaded from that state:
+// encodeStateAsUpdate(applyUpdate(new Doc, state), sv) -- the GPU snapshot of the state (§8f-1), then a diff
+// in which every struct keeps its parentSub bit (step2Many, ygm_sync_step2_v1; pinned against yjs by
+// tests/test_step2.py).  A state outside the snapshot kernel's envelope (pending structs or delete set,
+// sub-documents) is answered with diffUpdate(state, sv) -- the same content, not the same bytes -- and
+// NAMED: its reply array carries `unnormalized: true` and the document is listed in
+// responder.unnormalized.  The server's Step1 carries encodeStateVectorFromUpdate(state).
 
 const MessageType = { Sync: 0, SyncReply: 4 }
 const SyncStep = { Step1: 0, Step2: 1, Update: 2 }
@@ -68,11 +72,16 @@ class SyncResponder {
    * @param {{ engine: any, getState: (documentName: string) => Promise<Uint8Array | Uint8Array[] | null> }} opts
    *   engine: GpuEngine or GpuEnginePool; getState: the document's stored update, or [snapshot, ...log]
    */
-  constructor ({ engine, getState }) { this.engine = engine; this.getState = getState }
+  constructor ({ engine, getState }) {
+    this.engine = engine; this.getState = getState
+    /** Step1 replies sent as diffUpdate(state, sv) because the state is outside the snapshot envelope */
+    this.unnormalized = []
+  }
 
   _pooled () { return typeof this.engine.shardOf === 'function' }
   _merge (names, docs) { return this._pooled() ? this.engine.mergeMany(names, docs) : this.engine.mergeMany(docs) }
   _diff (names, states, svs) { return this._pooled() ? this.engine.diffMany(names, states, svs) : this.engine.diffMany(states, svs) }
+  _step2 (names, states, svs) { return this._pooled() ? this.engine.step2Many(names, states, svs) : this.engine.step2Many(states, svs) }
   _svs (names, states) { return this._pooled() ? this.engine.stateVectorsMany(names, states) : this.engine.stateVectorsMany(states) }
 
   /**
@@ -111,7 +120,16 @@ class SyncResponder {
     }
     const live = asks.filter(a => !(state.get(a.documentName) instanceof Error))
     asks.filter(a => state.get(a.documentName) instanceof Error).forEach(a => { out[a.i] = state.get(a.documentName) })
-    const diffs = await this._diff(live.map(a => a.documentName), live.map(a => state.get(a.documentName)), live.map(a => a.payload))
+    const diffs = await this._step2(live.map(a => a.documentName), live.map(a => state.get(a.documentName)), live.map(a => a.payload))
+    // states the snapshot kernel does not take: diffUpdate of the state itself, named as such
+    const unsup = live.map((a, k) => diffs[k] instanceof Error && diffs[k].code === 'EUNSUPPORTED' ? k : -1).filter(k => k >= 0)
+    if (unsup.length) {
+      const plain = await this._diff(unsup.map(k => live[k].documentName), unsup.map(k => state.get(live[k].documentName)), unsup.map(k => live[k].payload))
+      unsup.forEach((k, j) => {
+        diffs[k] = plain[j]
+        if (!(plain[j] instanceof Error)) { plain[j].unnormalized = true; this.unnormalized.push(live[k].documentName) }
+      })
+    }
     let ownSv = new Map()
     if (requestFirstSync) {
       const svs = await this._svs(names, names.map(n => state.get(n) instanceof Error ? new Uint8Array([0, 0]) : state.get(n)))
@@ -128,6 +146,7 @@ class SyncResponder {
         else if (path === 'reply' && a.messageType === MessageType.Sync) replies.push(frame(a.documentName, MessageType.SyncReply, SyncStep.Step1, sv))
       }
       replies.push(frame(a.documentName, MessageType.Sync, SyncStep.Step2, diffs[k]))
+      if (diffs[k].unnormalized) replies.unnormalized = true
       out[a.i] = replies
     })
     return out

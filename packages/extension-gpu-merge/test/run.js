@@ -25,6 +25,14 @@ class CpuDouble { // test double (never shipped): same API as GpuEngine
   async mergePacked (job) { this.calls++; return refusal(() => Y.mergeUpdates(jobUpdates(job))) }
   async mergeMany (docs) { this.calls++; return docs.map(u => { try { return Y.mergeUpdates(u) } catch (e) { return e } }) }   // per-document errors, as GpuEngine
   async diffMany (states, svs) { this.calls++; return states.map((u, i) => Y.diffUpdate(u, svs[i])) }
+  async step2Many (states, svs) {   // the reference's reply for a document loaded from each state
+    this.calls++
+    return states.map((u, i) => {
+      const d = new Y.Doc(); Y.applyUpdate(d, u)
+      if (d.store.pendingStructs || d.store.pendingDs) return Object.assign(new Error('EUNSUPPORTED'), { code: 'EUNSUPPORTED' })
+      return Y.encodeStateAsUpdate(d, svs[i])
+    })
+  }
   async stateVectorsMany (states) { this.calls++; return states.map(u => Y.encodeStateVectorFromUpdate(u)) }
   async snapshot (u) { this.calls++; const d = new Y.Doc(); Y.applyUpdate(d, u); return Y.encodeStateAsUpdate(d) }
   async snapshotMany (states) {
@@ -519,7 +527,10 @@ test('sync responder answers a SyncStep1 batch', async (engine) => {
     const [step1, step2] = replies[i]                                   // the reference's order: server Step1, then Step2
     const a = decodeSyncMessage(step2); const b = decodeSyncMessage(step1)
     assert.strictEqual(a.documentName, n); assert.strictEqual(a.messageType, MessageType.Sync); assert.strictEqual(a.step, SyncStep.Step2)
-    assert.strictEqual(Buffer.from(a.payload).toString('hex'), Buffer.from(Y.diffUpdate(state, sv)).toString('hex'))
+    // the reference's bytes (MessageReceiver.ts:137-138) for the document loaded from the stored state
+    const loaded = new Y.Doc(); Y.applyUpdate(loaded, state)
+    assert.strictEqual(Buffer.from(a.payload).toString('hex'), Buffer.from(Y.encodeStateAsUpdate(loaded, sv)).toString('hex'))
+    assert.ok(!replies[i].unnormalized)
     assert.strictEqual(b.step, SyncStep.Step1)
     assert.strictEqual(Buffer.from(b.payload).toString('hex'), Buffer.from(Y.encodeStateVectorFromUpdate(state)).toString('hex'))
     // a client at `sv` that applies the reply ends up with the server's content
@@ -528,6 +539,26 @@ test('sync responder answers a SyncStep1 batch', async (engine) => {
     Y.applyUpdate(client, a.payload)
     assert.strictEqual(client.getText('t').toString(), hp.documents.get(n).getText('t').toString())
   })
+})
+
+// a state outside the snapshot envelope (a struct whose origin is missing: pending in yjs) is answered with
+// diffUpdate(state, sv) and named, never sent silently as if it were the reference's bytes
+test('sync responder names Step2 replies outside the snapshot envelope', async (engine) => {
+  const src = new Y.Doc(); const ups = []
+  src.on('update', u => ups.push(u))
+  src.getText('t').insert(0, 'ab'); src.getText('t').insert(2, 'cd')
+  const pending = ups[1]                                            // depends on the first update: pending alone
+  const good = Y.mergeUpdates(ups)
+  const states = { pend: pending, good }
+  const r = new SyncResponder({ engine, getState: async n => states[n] })
+  const msgs = ['pend', 'good'].map(n => frame(n, MessageType.Sync, SyncStep.Step1, Uint8Array.from([0])))
+  const out = await r.answerMany(msgs)
+  assert.strictEqual(out[0].unnormalized, true)
+  assert.deepStrictEqual(r.unnormalized, ['pend'])
+  assert.strictEqual(Buffer.from(decodeSyncMessage(out[0][1]).payload).toString('hex'), Buffer.from(Y.diffUpdate(pending, Uint8Array.from([0]))).toString('hex'))
+  assert.ok(!out[1].unnormalized)
+  const loaded = new Y.Doc(); Y.applyUpdate(loaded, good)
+  assert.strictEqual(Buffer.from(decodeSyncMessage(out[1][1]).payload).toString('hex'), Buffer.from(Y.encodeStateAsUpdate(loaded, Uint8Array.from([0]))).toString('hex'))
 })
 
 test('update V2 batches match yjs mergeUpdatesV2 / diffUpdateV2 / encodeStateVectorFromUpdateV2', async (engine) => {

@@ -6,6 +6,7 @@
 // read, the sequential kernel only when some document needed it, D2H.
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -594,28 +595,33 @@ int ygm_sync_step2_v1_device(ygm_ctx* c, const uint8_t* d_states, uint64_t state
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   (void)hipSetDevice(c->device);
   ygm_device_result r1;
+  const bool dbg = getenv("YGM_DEBUG") != nullptr;
+#define S2CHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { if (dbg) fprintf(stderr, "ygm step2: %s: %s\n", #x, hipGetErrorString(_e)); return YGM_EDEVICE; } } while (0)
   int e = ygm_snapshot_v1_device(c, d_states, states_bytes, d_state_off, n_docs, s, &r1);
+  if (dbg) fprintf(stderr, "ygm step2: snapshot rc %d payload %llu\n", e, (unsigned long long)r1.payload_bytes);
   if (e) return e;
   const uint32_t nb = (n_docs + 255) / 256;
   if (!c->s2_data.ensure(r1.payload_bytes + 64) || !c->s2_off.ensure(8ull * n_docs + 16) || !c->s2_bsum.ensure(8ull * nb + 16) ||
       !c->s2_st.ensure(4ull * n_docs + 4))
     return YGM_ENOMEM;
-  HIPCHK(hipMemsetAsync((uint8_t*)c->s2_data.p + r1.payload_bytes, 0, 64, s));   // readable tail for the walker's chunks
+  S2CHK(hipMemsetAsync((uint8_t*)c->s2_data.p + r1.payload_bytes, 0, 64, s));   // readable tail for the walker's chunks
   if (n_docs) {
     if (ygm_k_launch_pack(r1.data, r1.off, r1.len, r1.status, n_docs, c->s2_bsum.as<uint64_t>(), c->s2_data.as<uint8_t>(),
                           c->s2_off.as<uint64_t>(), s))
       return YGM_EDEVICE;
-    HIPCHK(hipMemcpyAsync(c->s2_off.as<uint64_t>() + n_docs, c->s2_bsum.as<uint64_t>() + nb, 8, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->s2_st.p, r1.status, 4ull * n_docs, hipMemcpyDeviceToDevice, s));
+    S2CHK(hipMemcpyAsync(c->s2_off.as<uint64_t>() + n_docs, c->s2_bsum.as<uint64_t>() + nb, 8, hipMemcpyDeviceToDevice, s));
+    S2CHK(hipMemcpyAsync(c->s2_st.p, r1.status, 4ull * n_docs, hipMemcpyDeviceToDevice, s));
   }
   uint64_t sv_end = 0;
   if (n_docs && hipMemcpy(&sv_end, d_sv_off + n_docs, 8, hipMemcpyDeviceToHost) != hipSuccess) return YGM_EDEVICE;
   e = run_doc_kernel(c, 1, c->s2_data.as<uint8_t>(), r1.payload_bytes, c->s2_off.as<uint64_t>(), d_sv_arena, sv_end, d_sv_off, n_docs, s,
                      out, YGM_F_KEEP_SUB);
+  if (dbg) fprintf(stderr, "ygm step2: diff rc %d\n", e);
   if (e) return e;
   if (n_docs && ygm_k_launch_v2_status(c->s2_st.as<int32_t>(), n_docs, out->status, out->len, s)) return YGM_EDEVICE;
-  HIPCHK(hipStreamSynchronize(s));
+  S2CHK(hipStreamSynchronize(s));
   return YGM_OK;
+#undef S2CHK
 }
 
 // ------------------------------------------------------------------ update V2 (device API)

@@ -223,6 +223,9 @@ __global__ __launch_bounds__(WAVE) void k_sv_table(const uint8_t* __restrict__ s
 #define YGM_DW_SPEC 0   // 1: fast decoder reads both candidate content-length bytes beside the info byte (A/B: slower,
                         // profiles/r03_walk/README.md -- the walker is issue-bound, not LDS-latency-bound)
 #endif
+#ifndef YGM_DW_COOP
+#define YGM_DW_COOP 0   // 1: cooperative staging -- four lanes load one owner's 64-byte chunk (quad-coalesced requests)
+#endif
 #ifndef YGM_DW_WPE0
 #define YGM_DW_WPE0 2   // waves per SIMD the SV walker is compiled for (register budget 512 / waves)
 #endif
@@ -265,7 +268,10 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
   uint32_t srel = 0, q = 0, rb = 0;        // document start / parse position / document end, ring-relative
   uint32_t landed = 0, stg_n = 0, stg_k = 0, prev8 = 0;
   u32x4 g0 = {0u, 0u, 0u, 0u}, g1 = g0, g2 = g0, g3 = g0, g4 = g0, g5 = g0, g6 = g0, g7 = g0;   // staged chunks
-  u32x4 g8 = g0, g9 = g0, g10 = g0, g11 = g0, g12 = g0, g13 = g0, g14 = g0, g15 = g0;
+  u32x4 g8 = g0, g9 = g0, g10 = g0, g11 = g0;
+#if !YGM_DW_COOP
+  u32x4 g12 = g0, g13 = g0, g14 = g0, g15 = g0;
+#endif
   uint32_t n_left = 0, st_left = 0, client = 0, clock = 0, prevc = 0;
   bool have_prev = false;
   uint64_t slot = 0;                       // the document's output slot; t / tend / e_dst / cdst relative to it
@@ -376,6 +382,64 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
       const uint32_t lim = (need >> 6) + DW_S;
       if (stg_k + stg_n > lim) stg_n = lim > stg_k ? lim - stg_k : 0u;
     }
+#if YGM_DW_COOP
+    // cooperative commit: quad q of instruction (j, b) holds chunk j of owner 16 b + q (one 16-byte piece per lane).
+    // Each lane writes its piece to the owner's ring; the quad assembles the chunk's terminator mask by DPP, checks the
+    // chunk inside (varuints of >= 6 bytes; diff: a top-bit byte followed by a zero byte) and writes the mask -- all
+    // zero ("no varuint ends") when a check fails, so any unit the walker would read there is deferred.  The owner
+    // then checks what crosses from its previous chunk into each new one (prev8) over its document's part.
+    {
+      const uint32_t pc = l & 3u;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint32_t o = 16u * (uint32_t)b + (l >> 2);
+        const uint32_t sk = (uint32_t)__shfl((int)stg_k, (int)o), sn = (uint32_t)__shfl((int)stg_n, (int)o);
+        if (__ballot(sn != 0u) == 0) continue;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          const u32x4 v = j == 0 ? (b == 0 ? g0 : b == 1 ? g1 : b == 2 ? g2 : g3)
+                        : j == 1 ? (b == 0 ? g4 : b == 1 ? g5 : b == 2 ? g6 : g7)
+                                 : (b == 0 ? g8 : b == 1 ? g9 : b == 2 ? g10 : g11);
+          const bool act = (uint32_t)j < sn;
+          if (__ballot(act) == 0) break;
+          const uint32_t k = sk + (uint32_t)j;
+          if (act) L.ring[(4u * k + pc) & (DW_P - 1)][o] = v;
+          const uint32_t h16 = hibits8(v.x, v.y) | (hibits8(v.z, v.w) << 8);
+          const uint32_t h2 = (h16 << (16u * (pc & 1u))) | ((uint32_t)__builtin_amdgcn_mov_dpp((int)(h16 << (16u * (pc & 1u))), 0xB1, 0xF, 0xF, false));
+          const uint32_t hs = (uint32_t)__builtin_amdgcn_mov_dpp((int)h2, 0x4E, 0xF, 0xF, false);
+          const uint64_t H = pc < 2u ? ((uint64_t)hs << 32 | h2) : ((uint64_t)h2 << 32 | hs);
+          const uint64_t r2 = H & (H >> 1), r4 = r2 & (r2 >> 2), r6 = r4 & (r2 >> 4);
+          uint64_t bp = 0;
+          if (MODE == 1) {
+            auto zb = [](uint32_t a) { return ~(((a & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | a) & 0x80808080u; };
+            const uint32_t z16 = hibits8(zb(v.x), zb(v.y)) | (hibits8(zb(v.z), zb(v.w)) << 8);
+            const uint32_t z2 = (z16 << (16u * (pc & 1u))) | ((uint32_t)__builtin_amdgcn_mov_dpp((int)(z16 << (16u * (pc & 1u))), 0xB1, 0xF, 0xF, false));
+            const uint32_t zs = (uint32_t)__builtin_amdgcn_mov_dpp((int)z2, 0x4E, 0xF, 0xF, false);
+            const uint64_t Z = pc < 2u ? ((uint64_t)zs << 32 | z2) : ((uint64_t)z2 << 32 | zs);
+            bp = (H << 1) & Z;   // (bit 0: the previous chunk's last byte, the owner's check)
+          }
+          if (act && pc == 0u) L.mask[k & (DW_S - 1)][o] = (r6 | bp) ? 0ull : ~H;
+        }
+      }
+      // the owner: checks across its previous chunk's end, over the document part [vlo, vhi) of each new chunk
+      for (uint32_t j = 0; j < stg_n; j++) {
+        const uint32_t k = stg_k + j;
+        const uint32_t vlo = srel > 64u * k ? (srel - 64u * k < 64u ? srel - 64u * k : 64u) : 0u;
+        const uint32_t vhi = k < tc ? 0u : (rb - 64u * k < 64u ? rb - 64u * k : 64u);
+        const uint64_t m = L.mask[k & (DW_S - 1)][l];
+        const uint64_t vm = dw_lowmask(vhi) & ~dw_lowmask(vlo);
+        const uint64_t Hm = ~m & vm;
+        const uint32_t c = ((uint32_t)(Hm & 0xFFu) << 8) | prev8;
+        const uint32_t c2 = c & (c >> 1), c4 = c2 & (c2 >> 2), c6 = c4 & (c2 >> 4);
+        uint32_t bpx = 0;
+        if (MODE == 1 && vlo == 0u && vhi) bpx = (prev8 >> 7) & (dw_byte(L, l, 64u * k) == 0u ? 1u : 0u);
+        bad |= (c6 | bpx) ? 1u : 0u;
+        prev8 = vhi ? (uint32_t)(Hm >> 56) : prev8;
+      }
+      if (stg_n) landed = stg_k + stg_n;
+      stg_n = 0;
+    }
+#else
     if (stg_n) {
       // the document part [vlo, vhi) of chunk k is checked (table chunks: none)
       auto vlo = [&](uint32_t k) { return srel > 64u * k ? (srel - 64u * k < 64u ? srel - 64u * k : 64u) : 0u; };
@@ -396,6 +460,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
       landed = stg_k + stg_n;
       stg_n = 0;
     }
+#endif
     WSEC(0);
     // ---- (1b) diff: a landed state-vector table moves from the ring to the lane's table, the document follows
     if (MODE == 1) {
@@ -504,7 +569,9 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
 #pragma unroll
         for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) sk[i] = 0u;
       }
-      cbase = da & (DW_LINE ? ~127ull : ~15ull); srel = 64u * tc + (uint32_t)(da - cbase); q = srel; rb = 64u * tc + (uint32_t)(db - cbase);
+      // (cooperative loads: chunks of one 64-byte sector each)
+      cbase = da & (DW_LINE ? ~127ull : YGM_DW_COOP ? ~63ull : ~15ull);
+      srel = 64u * tc + (uint32_t)(da - cbase); q = srel; rb = 64u * tc + (uint32_t)(db - cbase);
       landed = 0; stg_n = 0; prev8 = 0;
       bad |= (db < da || ((db - da) >> 30)) ? 1u : 0u;
       ph = tc ? WK_SVN : WK_UPD;
@@ -523,11 +590,36 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
       auto chunk = [&](uint32_t k) -> const u32x4* {
         return (const u32x4*)(MODE == 1 && k < tc ? tbl + 144ull * d + 64u * k : arena + cbase + 64ull * (k - tc));
       };
+#if YGM_DW_COOP
+      if (MODE == 1 && landed < tc && landed + n > tc) stg_n = n = tc - landed;   // (table and document chunks: two sources)
+#else
       if (n >= 1u) { const u32x4* p = chunk(landed); g0 = p[0]; g1 = p[1]; g2 = p[2]; g3 = p[3]; }
       if (n >= 2u) { const u32x4* p = chunk(landed + 1u); g4 = p[0]; g5 = p[1]; g6 = p[2]; g7 = p[3]; }
       if (n >= 3u) { const u32x4* p = chunk(landed + 2u); g8 = p[0]; g9 = p[1]; g10 = p[2]; g11 = p[3]; }
       if (DW_STG > 3u && n >= 4u) { const u32x4* p = chunk(landed + 3u); g12 = p[0]; g13 = p[1]; g14 = p[2]; g15 = p[3]; }
+#endif
     }
+#if YGM_DW_COOP
+    // cooperative loads: instruction (j, b) -- lane l loads 16-byte piece l & 3 of chunk j of owner 16 b + l / 4, so
+    // every quad reads 64 contiguous bytes (one request per chunk instead of four lane-private ones)
+    {
+      const uint64_t ra = stg_n ? (uint64_t)(MODE == 1 && stg_k < tc ? (const uint8_t*)tbl + 144ull * d + 64u * stg_k
+                                                                    : arena + cbase + 64ull * (stg_k - tc)) : 0ull;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint32_t o = 16u * (uint32_t)b + (l >> 2);
+        const uint64_t a = dw_shfl64(ra, o) + 16u * (l & 3u);
+        const uint32_t sn = (uint32_t)__shfl((int)stg_n, (int)o);
+        if (__ballot(sn != 0u) == 0) continue;
+        u32x4& r0 = b == 0 ? g0 : b == 1 ? g1 : b == 2 ? g2 : g3;
+        u32x4& r1 = b == 0 ? g4 : b == 1 ? g5 : b == 2 ? g6 : g7;
+        u32x4& r2 = b == 0 ? g8 : b == 1 ? g9 : b == 2 ? g10 : g11;
+        if (sn >= 1u) r0 = *(const u32x4*)a;
+        if (sn >= 2u) r1 = *(const u32x4*)(a + 64u);
+        if (sn >= 3u) r2 = *(const u32x4*)(a + 128u);
+      }
+    }
+#endif
     // ---- (6) offsets of the documents the next round hands out
     prefetch();
     WSEC(3);

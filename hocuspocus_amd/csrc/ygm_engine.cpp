@@ -384,7 +384,7 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
   }
   uint32_t n_seq = 0;
   if (m.fb_count) {  // tier 4: large [snapshot, ...log] documents, one wave each; the rest go on to tier 5
-    const uint64_t blk_cap = m.fb_bytes / 4 + 2ull * m.fb_count + 16, rec_cap = m.fb_bytes / 2 + 2ull * m.fb_count + 16;
+    const uint64_t blk_cap = m.fb_bytes / 4 + 2ull * m.fb_count + 16, rec_cap = m.fb_bytes + 2ull * m.fb_count + 16;
     if (!c->big_blk.ensure(blk_cap * ygm_k_big_blk_bytes()) || !c->big_rec.ensure(rec_cap * ygm_k_big_rec_bytes()) ||
         !c->big_list.ensure((size_t)m.fb_count * 4 + 4))
       return YGM_ENOMEM;

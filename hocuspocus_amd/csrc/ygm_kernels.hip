@@ -2058,7 +2058,8 @@ struct BigDs {
 // value decoded by the lane holding its terminator from the 8 bytes ending there.  A trailing
 // unterminated varuint is not a value (the stream runs out if it is needed).  false: a varuint of more
 // than 5 bytes or above 2^32 - 1, or more values than `cap` (the general path takes the document).
-YDEV bool big_ds_decode(const uint8_t* u0p, uint32_t ds0, uint32_t n0, uint32_t* V, uint64_t cap, uint32_t& nv_out) {
+YDEV bool big_ds_decode(const uint8_t* u0p, uint32_t ds0, uint32_t n0, uint32_t* V, uint64_t cap, uint32_t& nv_out,
+                        uint32_t* P = nullptr, uint32_t* nm_out = nullptr) {   // P[i]: byte end of value i - ds0; nm: a non-minimal varuint
   const uint32_t l = threadIdx.x % WAVE;
   uint32_t nv = 0;
   bool bad = false;
@@ -2087,7 +2088,10 @@ YDEV bool big_ds_decode(const uint8_t* u0p, uint32_t ds0, uint32_t n0, uint32_t*
       const uint64_t W = ((uint64_t)w.y << 32) | w.x;
       const uint64_t v = pext7(W >> (8u * st), r - st + 1u);
       bad |= v > 0xFFFFFFFFull || idx >= cap;
-      if (idx < cap) V[idx] = (uint32_t)v;
+      if (idx < cap) {
+        V[idx] = (uint32_t)v;
+        if (P) { P[idx] = e + 1u - ds0; if (r > st && ((W >> (8u * r)) & 0xFFu) == 0u) *nm_out = 1u; }
+      }
       idx++;
     }
   }
@@ -2187,6 +2191,96 @@ YDEV bool big_validate(const BigTile& T, const uint32_t* rs, const uint32_t* re,
   return vbad;
 }
 
+// ---- U0's delete set spliced instead of streamed (big documents: U0's delete set large against the log's ranges).
+// Scratch words of the document: V [0, W3) values, P [W3, 2 W3) each value's byte end (from the delete set's start),
+// then the entry table: for entry e (a client of U0's delete set, descending) eidx[e] (index of its client value in V),
+// eclient, en (range count), ebs / ebe (bytes of the whole entry), then a bitmap of the client values' indices.
+struct BigDsPlan { uint32_t C, end; bool fast; };
+YDEV uint32_t* ds_eclient(uint32_t* eidx, uint32_t C) { return eidx + C; }
+YDEV uint32_t* ds_en(uint32_t* eidx, uint32_t C) { return eidx + 2u * C; }
+YDEV uint32_t* ds_ebs(uint32_t* eidx, uint32_t C) { return eidx + 3u * C; }
+YDEV uint32_t* ds_ebe(uint32_t* eidx, uint32_t C) { return eidx + 4u * C; }
+YDEV uint32_t* ds_bits(uint32_t* eidx, uint32_t C) { return eidx + 5u * C; }
+// the client entries (wave 0, the walk is a chain: entry e + 1 starts 2 + 2 n values after entry e); false: not
+// spliceable (truncated, an empty or repeated client, clients not descending, no room)
+YDEV bool big_ds_entries(const uint32_t* V, uint32_t dsn, uint32_t* eidx, uint64_t w3, BigDsPlan& DP) {
+  const uint32_t l = threadIdx.x % WAVE;
+  const uint32_t ncl = V[0];
+  if ((uint64_t)ncl * 5u + dsn / 32u + 8u > w3 || 4ull * ncl + 1u > dsn) return false;
+  uint32_t idx = 1, prevc = 0, wb = 0xFFFFFFFFu, wv = 0;   // V[wb + j] in lane j
+  for (uint32_t c = 0; c < ncl; c++) {
+    if (idx + 1u >= dsn) return false;
+    if (wb == 0xFFFFFFFFu || idx < wb || idx + 1u >= wb + (uint32_t)WAVE) { wb = idx; wv = wb + l < dsn ? V[wb + l] : 0u; }
+    const uint32_t client = (uint32_t)__builtin_amdgcn_readlane((int)wv, (int)(idx - wb));
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)wv, (int)(idx + 1u - wb));
+    if (n == 0u || (c && client >= prevc) || (uint64_t)idx + 2u + 2ull * n > dsn) return false;
+    if (l == 0) { eidx[c] = idx; ds_eclient(eidx, ncl)[c] = client; ds_en(eidx, ncl)[c] = n; }
+    prevc = client;
+    idx += 2u + 2u * n;
+  }
+  DP.C = ncl; DP.end = idx;
+  return true;
+}
+// cmd 4, the whole workgroup: the client bitmap, each entry's byte bounds, then every range canonical -- non-empty,
+// inside 32-bit clocks, and starting after the previous range of its entry ends (sorted, disjoint, not adjacent: the
+// union would write it as it is).  Range starts are the odd value indices that are not client values (entries start
+// at odd indices: 1, then + 2 + 2 n).  C: vs = V, ns = eidx, sbase = W3, n0 = entries, at = end of the entries.
+YDEV bool big_ds_canon(const BigCmd& C, uint32_t t0) {
+  const uint32_t* V = (const uint32_t*)(uintptr_t)C.vs;
+  const uint32_t* P = V + C.sbase;
+  uint32_t* eidx = (uint32_t*)(uintptr_t)C.ns;
+  const uint32_t ne = C.n0, end = C.at, nw = end / 32u + 1u;
+  uint32_t* bits = ds_bits(eidx, ne);
+  for (uint32_t w = t0; w < nw; w += BIG_THREADS) bits[w] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __syncthreads();
+  for (uint32_t e = t0; e < ne; e += BIG_THREADS) {
+    const uint32_t i = eidx[e];
+    atomicOr(&bits[i / 32u], 1u << (i % 32u));
+    ds_ebs(eidx, ne)[e] = P[i - 1u];
+    ds_ebe(eidx, ne)[e] = P[i + 1u + 2u * ds_en(eidx, ne)[e]];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __syncthreads();
+  auto is_client = [&](uint32_t j) { return (bits[j / 32u] >> (j % 32u)) & 1u; };
+  bool ok = true;
+  for (uint32_t j = 3u + 2u * t0; j < end; j += 2u * BIG_THREADS) {
+    if (is_client(j)) continue;
+    const uint64_t k = V[j], len = V[j + 1u];
+    ok &= len != 0u && k + len <= 0xFFFFFFFFull;
+    if (!is_client(j - 2u)) ok &= k > (uint64_t)V[j - 2u] + V[j - 1u];
+  }
+  return ok;
+}
+// each log range against U0's entry of its client (wave 0, a lane per range): the entry by binary search over the
+// clients, then the U0 ranges it merges with: [a, b1) = the ranges ending at or after its start and starting at or
+// before its end (U0's ranges are disjoint and not adjacent: both bounds by binary search)
+YDEV void big_ds_plan(const uint32_t* V, const uint32_t* P, uint32_t* eidx, const BigDsPlan& DP, BigRange* rg, uint32_t nrg) {
+  const uint32_t l = threadIdx.x % WAVE, ne = DP.C;
+  const uint32_t* ecl = ds_eclient(eidx, ne);
+  for (uint32_t r = l; r < nrg; r += WAVE) {
+    BigRange& R = rg[r];
+    const uint32_t client = 0xFFFFFFFFu - (uint32_t)(R.key >> 32), k = (uint32_t)R.key, ke = k + R.len;
+    uint32_t lo = 0, hi = ne;
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (ecl[m] > client) lo = m + 1u; else hi = m; }
+    R.ent = BIG_NOENT; R.a = 0; R.b1 = 0; R.s = k; R.e = ke; R.pa = 0; R.pb = 0;
+    if (lo < ne && ecl[lo] == client) {
+      const uint32_t i0 = eidx[lo] + 2u, n = ds_en(eidx, ne)[lo];
+      uint32_t a = 0, h = n;
+      while (a < h) { const uint32_t m = (a + h) >> 1; if ((uint64_t)V[i0 + 2u * m] + V[i0 + 2u * m + 1u] < k) a = m + 1u; else h = m; }
+      uint32_t b1 = a; h = n;
+      while (b1 < h) { const uint32_t m = (b1 + h) >> 1; if (V[i0 + 2u * m] <= ke) b1 = m + 1u; else h = m; }
+      if (a < b1) {
+        const uint32_t ka = V[i0 + 2u * a], eb = V[i0 + 2u * (b1 - 1u)] + V[i0 + 2u * (b1 - 1u) + 1u];
+        R.s = ka < k ? ka : k; R.e = eb > ke ? eb : ke;
+      }
+      R.ent = lo; R.a = a; R.b1 = b1; R.pa = P[i0 + 2u * a - 1u]; R.pb = P[i0 + 2u * b1 - 1u];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  wave_sync();
+}
+
 // block clock ranges [vs, ns) of the block table (cmd 3, the whole workgroup): clock0 + the validated lengths of
 // the block's struct records; true if one passes 2^32 - 1
 YDEV bool big_clock_ranges(BigBlk* blk, const BigRec* rec, const BigCmd& C, uint32_t t0) {
@@ -2221,6 +2315,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       if (C.cmd == 0) return;
       if (C.cmd == 1) big_spec(T0, C.at, C.mis, C.tn, C.n0, threadIdx.x);
       else if (C.cmd == 3) { if (big_clock_ranges(blk, rec, C, threadIdx.x)) L.bad = 1; }
+      else if (C.cmd == 4) { if (!big_ds_canon(C, threadIdx.x)) s_cmd.tb = 1; }
       else if (big_validate(T0, s_rst, s_ren, rec, C, flags, threadIdx.x)) L.bad = 1;
       __syncthreads();
     }
@@ -2290,7 +2385,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   //      global memory; a struct failing validation in the tile is validated again from global memory.
   const uint8_t* u0p = arena + upd_off[ua + U0];
   const uint32_t n0 = (uint32_t)(upd_off[ua + U0 + 1] - upd_off[ua + U0]);
-  const uint64_t ncap = n0 / 2u + 1u;                       // structs take >= 2 bytes
+  const uint64_t ncap = n0 + 1u;                            // structs take >= 2 bytes; delete-set values >= 1
   wave_sync();
   uint64_t base = 0, sbase = 0, nb = 0, NS = 0;
   // tile origin tc0 (U0 position), tb = tc0 rounded down to a 16-byte aligned address: LDS byte j of
@@ -2440,6 +2535,42 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     if (big_clock_ranges(blk, rec, s_cmd, l)) L.bad = 1;
     __syncthreads();
   }
+  // ---- U0's delete set as values V (the struct records' scratch is free after the clock-range pass), with each
+  //      value's byte end P (big_ds_decode, wave 0).  When it is large against the log's ranges it is SPLICED
+  //      (BigDsPlan): its client entries walked once (wave 0), every range checked canonical -- client-descending
+  //      entries, sorted, disjoint and non-adjacent non-empty ranges, minimal varuints: what the union would write
+  //      for it -- by the whole workgroup (cmd 4); each log range then finds the U0 ranges it merges with by binary
+  //      search, and the emit copies everything else verbatim.  Otherwise the emit's passes stream it range by range.
+  uint32_t* const dsv = (uint32_t*)(rec + sbase);
+  const uint64_t dW3 = ncap * (sizeof(BigRec) / 4) / 3;      // V | P | entries + client bitmap, dW3 words each
+  uint32_t* const dsp = dsv + dW3;
+  uint32_t* const eidx = dsv + 2 * dW3;                       // entry e: index of its client value in V
+  uint32_t dsn = 0;
+  BigDsPlan DP; DP.C = 0; DP.end = 0; DP.fast = false;
+  // (wave 0 alone until cmd 4: the helper waves wait at their loop's first barrier, so every barrier below pairs with
+  //  one of theirs -- the command's two and big_ds_canon's own)
+  if (!L.bad) {
+    uint32_t nm = 0;
+    const bool ok = big_ds_decode(u0p, (uint32_t)s_ds0, n0, dsv, dW3, dsn, dsp, &nm);
+    const bool any_nm = __ballot(nm != 0u) != 0;
+    if (!ok && l == 0) L.bad = 1;
+    DP.fast = ok && !any_nm && dsn >= 64u * ((uint64_t)L.nrg + 16u) && !(flags & 1u);
+    if (DP.fast) DP.fast = big_ds_entries(dsv, dsn, eidx, dW3, DP);
+    if (DP.fast) {   // every range of every entry canonical (the whole workgroup); a failure streams instead
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the entry table before the helper waves read it
+      if (l == 0) {
+        s_cmd.cmd = 4; s_cmd.vs = (uint64_t)(uintptr_t)dsv; s_cmd.ns = (uint64_t)(uintptr_t)eidx; s_cmd.sbase = dW3;
+        s_cmd.n0 = DP.C; s_cmd.at = DP.end; s_cmd.tb = 0;
+      }
+      __syncthreads();
+      const BigCmd C4 = s_cmd;                                 // (copied before big_ds_canon's first barrier: tb is
+      if (!big_ds_canon(C4, l)) s_cmd.tb = 1;                  //  written after its last; every writer writes 1)
+      __syncthreads();
+      DP.fast = s_cmd.tb == 0;
+    }
+  }
+  DIAG_C(if (l == 0) { atomicAdd(&ygm_diag[21], 1ull); atomicAdd(&ygm_diag[22], DP.fast ? 1ull : 0ull);
+                       atomicAdd(&ygm_diag[23], (unsigned long long)dsn); atomicAdd(&ygm_diag[24], (unsigned long long)DP.C); })
   if (l == 0) s_cmd.cmd = 0;   // the helper waves are done: everything below is wave 0's
   __syncthreads();
   DIAGL(1);
@@ -2448,14 +2579,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   if (!bad) { big_bitonic(L.pc, npc); big_bitonic(L.rg, nrg); }
   const BigBlk* T = blk + s_base;
   if (bad) nb = 0;
-  // U0's delete set as values (the struct records' scratch is free after the clock-range pass); the
-  // emit's passes stream it, pass 0 keeping each output client's run count after it
-  uint32_t* const dsv = (uint32_t*)(rec + sbase);
-  uint32_t dsn = 0;
-  if (!bad && l < WAVE) {
-    bad = !big_ds_decode(u0p, (uint32_t)s_ds0, n0, dsv, ncap * (sizeof(BigRec) / 4), dsn);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  }
+  if (!bad && DP.fast) big_ds_plan(dsv, dsp, eidx, DP, L.rg, nrg);
   DIAGL(2);
   // ---- emit: pass 0 sizes (and proves the class), pass 1 bytes.  Every lane runs the same plan.
   uint64_t nblocks = 0, ndsc = 0, size = 0;
@@ -2545,6 +2669,59 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
 #ifdef YGM_DIAG_BIGDS
     DIAG_PUT(6 + pass, __builtin_amdgcn_s_memrealtime());   // diagnostic: where the delete-set part of the pass starts
 #endif
+    uint64_t nc = 0;
+    if (DP.fast) {
+      // spliced: U0's entries no log range names are copied as written; a touched entry is its client, its new
+      // run count, then its untouched ranges' bytes as written interleaved with the merged groups' spans
+      const uint8_t* const dsb = u0p + s_ds0;
+      const uint32_t ne = DP.C;
+      uint32_t ew = 0xFFFFFFFFu, wcl = 0, wn = 0, wbs = 0, wbe = 0;   // entry ew + lane
+      o.vu(ndsc);
+      uint32_t e = 0, r = 0;
+      while (e < ne || r < nrg) {
+        if (e < ne && (ew == 0xFFFFFFFFu || e >= ew + (uint32_t)WAVE)) {
+          ew = e;
+          const uint32_t y = e + l;
+          if (y < ne) { wcl = ds_eclient(eidx, ne)[y]; wn = ds_en(eidx, ne)[y]; wbs = ds_ebs(eidx, ne)[y]; wbe = ds_ebe(eidx, ne)[y]; }
+        }
+        const uint32_t el = e - ew;
+        const uint32_t cu = e < ne ? (uint32_t)__builtin_amdgcn_readlane((int)wcl, (int)el) : 0u;
+        const uint32_t cl = r < nrg ? 0xFFFFFFFFu - (uint32_t)(L.rg[r].key >> 32) : 0u;
+        const bool hu = e < ne;
+        const uint32_t bs = hu ? (uint32_t)__builtin_amdgcn_readlane((int)wbs, (int)el) : 0u;
+        const uint32_t be = hu ? (uint32_t)__builtin_amdgcn_readlane((int)wbe, (int)el) : 0u;
+        nc++;
+        if (hu && (r >= nrg || cu > cl)) { o.copy(dsb + bs, be - bs); e++; continue; }   // untouched entry
+        const bool touched = hu && cu == cl;
+        const uint32_t n = touched ? (uint32_t)__builtin_amdgcn_readlane((int)wn, (int)el) : 0u;
+        uint32_t r1 = r;
+        while (r1 < nrg && (L.rg[r1].key >> 32) == (L.rg[r].key >> 32)) r1++;
+        // groups of the client's log ranges (each widened by the U0 ranges it merges with): count, then write
+        for (int sw = 0; sw < 2; sw++) {
+          uint32_t ng = 0, cov = 0, gs = 0, ge = 0, ga = 0, gb = 0, gpa = 0, gpb = 0;
+          uint32_t next = touched ? bs + vu_len(cu) + vu_len(n) : 0u;   // bytes of the next untouched U0 range
+          bool have = false;
+          auto close = [&]() __attribute__((always_inline)) {
+            ng++; cov += gb - ga;
+            if (sw) {
+              if (touched && gpa > next) o.copy(dsb + next, gpa - next);
+              o.vu(gs); o.vu(ge - gs);
+              if (touched) next = gpb;
+            }
+          };
+          for (uint32_t q = r; q < r1; q++) {
+            const BigRange& R = L.rg[q];
+            if (have && R.s <= ge) { if (R.e > ge) ge = R.e; if (R.b1 > gb) { gb = R.b1; gpb = R.pb; } }
+            else { if (have) close(); gs = R.s; ge = R.e; ga = R.a; gb = R.b1; gpa = R.pa; gpb = R.pb; have = true; }
+          }
+          if (have) close();
+          if (sw == 0) { o.vu(cl); o.vu(n - cov + ng); }
+          else if (touched && be > next) o.copy(dsb + next, be - next);
+        }
+        if (touched) e++;
+        r = r1;
+      }
+    } else {
     uint32_t* runs_of = dsv + dsn;
     const uint64_t runs_cap = ncap * (sizeof(BigRec) / 4) - dsn;
     BigDs D;
@@ -2558,7 +2735,6 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     D.cl_left = D.s.next(); D.r_left = 0; D.client = 0;
     dnext();
     uint32_t r = 0;
-    uint64_t nc = 0;
     o.vu(ndsc);
     while ((D.has || r < nrg) && !bad) {
       const uint64_t kx = (D.has && (r >= nrg || D.key <= L.rg[r].key)) ? D.key : L.rg[r].key;
@@ -2585,6 +2761,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // pass 0's run counts before pass 1 reads them
     bad |= D.s.err;
+    }
     DIAGL(3 + pass);
     if (pass == 0) {
       nblocks = nbo; ndsc = nc; size = o.n;

@@ -301,7 +301,11 @@ struct BigPiece {
   uint32_t b0, b1;                   // struct bytes [b0, b1) within update `upd`
   uint32_t gc, pad;
 };
-struct BigRange { uint64_t key; uint32_t len, pad; };   // log delete range: key as BigPiece
+// log delete range: key as BigPiece.  The delete-set splice (big_ds_plan) annotates it against U0's entry of its client:
+// ent (entry index, BIG_NOENT: a client U0's delete set lacks), U0 ranges [a, b1) it touches (overlap or adjacency),
+// its span with them [s, e), and the byte offsets (from U0's delete set start) of U0 range a and range b1
+constexpr uint32_t BIG_NOENT = 0xFFFFFFFFu;
+struct BigRange { uint64_t key; uint32_t len, ent, a, b1, s, e, pa, pb; };
 
 // U0 tile (LDS): bytes staged by the whole wave; structs are parsed speculatively at every
 // position of its first BT_CH bytes; BT_OV bytes of overlap let a struct starting there end inside

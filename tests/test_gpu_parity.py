@@ -722,6 +722,19 @@ def test_large_document_tile_edges_vs_oracle(eng):
     assert eng.stats().docs_big - st0.docs_big == len(docs)   # the large-document tier took every one
 
 
+def test_large_document_delete_set_splice_vs_oracle(eng):
+    # snapshot delete sets large against the log's ranges are spliced (the snapshot's entries copied as written, log
+    # ranges merged in by binary search); broken snapshot delete sets (adjacent, overlapping, empty, non-minimal) are
+    # streamed instead -- bit-exact either way, every document in the large-document tier
+    from tile_docs import ds_splice_docs
+    docs = [us for seed in (11, 12, 13) for us in ds_splice_docs(seed)]
+    st0 = eng.stats()
+    res = eng.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+    assert not bad, (len(bad), bad[:5])
+    assert eng.stats().docs_big - st0.docs_big == len(docs)
+
+
 def test_large_document_unsorted_delete_set_goes_on(eng):
     # a snapshot delete set outside union order: the large-document tier's first emit pass refuses it and
     # the sequential kernel merges it, bit-exact

@@ -16,3 +16,12 @@ def test_tile_edge_docs_are_valid_large_inputs():
     snap = docs[-1][0]
     assert snap.count(b"\x82") > 0          # ContentJSON info bytes present
     assert max(len(us[0]) for us in docs) > 1_000_000
+
+
+def test_ds_splice_docs_are_valid_large_inputs():
+    from tile_docs import ds_splice_docs
+    for seed in (11, 12, 13):
+        docs = ds_splice_docs(seed)
+        for us in docs:
+            assert len(us[0]) > 16384
+            assert oracle.merge_updates(us)[0] == 0

@@ -1,0 +1,58 @@
+"""Dev probe (tooling): k_merge_big on single large C3-shaped documents (device API, kernel ms) and the diag build's
+per-phase stamps of the same documents.   python tools/proto/big_probe.py [diag]"""
+import ctypes, os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+diag = len(sys.argv) > 1 and sys.argv[1] in ("diag", "diagds", "splice")
+dsmode = len(sys.argv) > 1 and sys.argv[1] == "diagds"
+import hocuspocus_amd.engine as eng
+if diag:
+    eng.LIB_PATH = os.path.join(ROOT, "hocuspocus_amd", "exp/libygm_diagds.so" if dsmode else "libygm_diag.so")
+from tools import synth
+import oracle
+e = eng.Engine(0)
+if len(sys.argv) > 1 and sys.argv[1] == "splice":   # tests/tile_docs.ds_splice_docs through the diag build
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from tile_docs import ds_splice_docs
+    L = eng.lib()
+    L.ygm_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    dg = np.zeros(32, np.uint64)
+    for seed in (11, 12, 13):
+        docs = ds_splice_docs(seed)
+        L.ygm_diag_read(dg.ctypes.data, 1)
+        res = e.merge_updates_batch(docs)
+        L.ygm_diag_read(dg.ctypes.data, 1)
+        ok = [res[i] == oracle.merge_updates(us) for i, us in enumerate(docs)]
+        print({"seed": seed, "parity": ok, "big_docs": int(dg[21]), "spliced": int(dg[22])}, flush=True)
+    sys.exit(0)
+for mb in ([float(x) for x in os.environ['BIG_MB'].split(',')] if os.environ.get('BIG_MB') else (0.3, 1, 3, 10)):
+    arena, upd_off, doc_upd = synth.big_docs(1, int(mb * 1e6), 1024, max_clients=64, max_k=200, seed=8)
+    n = 1
+    upd_doc = np.zeros(len(upd_off) - 1, np.uint32)
+    ms = []
+    for rep in range(3):
+        s0 = e.stats(); t0 = time.time()
+        res = e.merge_packed(arena, upd_off, upd_doc, n)
+        s1 = e.stats()
+        ms.append((round(s1.kernel_ms - s0.kernel_ms, 2), round((time.time() - t0) * 1e3, 1)))
+    st, out = oracle.merge_updates([bytes(arena[int(upd_off[i]):int(upd_off[i + 1])]) for i in range(len(upd_off) - 1)])
+    ok = res[0] == (st, out)
+    line = {"MB": mb, "bytes": int(upd_off[-1]), "updates": len(upd_off) - 1, "kernel_ms_and_wall_ms": ms, "docs_big": s1.docs_big, "parity": ok}
+    if diag:
+        L = eng.lib()
+        L.ygm_diag_ts_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        ts = np.zeros(16384 * 8, np.uint64)
+        L.ygm_diag_ts_read(ts.ctypes.data, 0)
+        L.ygm_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        dg = np.zeros(32, np.uint64)
+        L.ygm_diag_read(dg.ctypes.data, 1)
+        line["ds_plan"] = {"big_docs": int(dg[21]), "spliced": int(dg[22]), "ds_values": int(dg[23]), "ds_entries": int(dg[24])}
+        t = ts.reshape(16384, 8)[0].astype(np.int64)
+        d = np.diff(t[:6]) * 10 / 1000.0
+        if dsmode:   # slots 6 / 7: where each pass's delete-set part starts (absolute stamps)
+            line["ds_us"] = {"pass0 structs": (t[6] - t[3]) * 10 / 1000.0, "pass0 ds": (t[4] - t[6]) * 10 / 1000.0,
+                             "pass1 structs": (t[7] - t[4]) * 10 / 1000.0, "pass1 ds": (t[5] - t[7]) * 10 / 1000.0}
+        line["phases_us"] = {"log walk": d[0], "U0 follow+spec+validate": d[1], "spec": t[6] * 10 / 1000.0, "validate": t[7] * 10 / 1000.0,
+                             "sorts": d[2], "pass0": d[3], "pass1": d[4]}
+    print(line, flush=True)

@@ -2114,7 +2114,78 @@ YDEV_NI uint64_t big_skip_global(const uint8_t* u0p, uint32_t n0, uint32_t pos) 
 #define YGM_BIG_WAVES 16
 #endif
 constexpr uint32_t BIG_WAVES = YGM_BIG_WAVES, BIG_THREADS = BIG_WAVES * WAVE;
-struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; };   // cmd 0 done, 1 spec, 2 validate, 3 clock ranges
+// cmd 0 done, 1 tile's jump tables, 2 validate, 3 clock ranges, 4 delete-set canonical check
+struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; const uint32_t* aux; };
+
+// ---- the snapshot scan (before k_merge_big, the whole GPU): every byte position p of every large document's U0 parsed
+// as a struct start, speculatively -- nx[p] = its end | GC << 31 (0: no parse: not an info byte write_struct emits, a
+// Skip, Any arrays / objects or JSON of more than 8 entries, past U0's end), and for parses of at most BIG_VCAP bytes
+// vl[p] = its clock length if it is what write_struct emits (big_struct), 0xFFFFFFFF if not (0: not validated).  The
+// chain follow in k_merge_big then reads the ends a tile at a time and the validation one word per struct.
+constexpr uint32_t BIG_SCAN_CH = 4096, BIG_VCAP = 4096;
+struct BigPick { uint64_t pb; uint32_t n0, u0; };   // U0's positions in nx / vl from pb; n0 = 0xFFFFFFFF: not scanned
+struct BigScan {
+  unsigned long long* cnt;   // [0] positions carved, [1] tasks
+  BigPick* pick;             // per large document (k_merge_big's blockIdx.x)
+  uint2* task;               // (document, chunk of BIG_SCAN_CH positions)
+  uint32_t *nx, *vl;
+  uint64_t ntask_cap, npos_cap;
+};
+// U0 of each large document (the largest update, the first of equal ones: k_merge_big's rule) and its scan tasks
+__global__ __launch_bounds__(256) void k_big_pick(const uint64_t* __restrict__ upd_off, const uint32_t* __restrict__ doc_upd,
+                                                  const uint32_t* __restrict__ fb_list, uint32_t n_fb, BigScan S) {
+  const uint32_t w = blockIdx.x * 4u + threadIdx.x / WAVE, l = threadIdx.x % WAVE;
+  if (w >= n_fb) return;
+  const uint32_t d = fb_list[w], ua = doc_upd[d], k = doc_upd[d + 1] - ua;
+  uint64_t best = 0;
+  for (uint32_t i = l; i < k; i += WAVE) {
+    const uint64_t n = upd_off[ua + i + 1] - upd_off[ua + i];
+    const uint64_t key = ((n < 0xFFFFFFFFull ? n : 0xFFFFFFFFull) << 32) | (0xFFFFFFFFu - i);
+    best = key > best ? key : best;
+  }
+  for (int o = 32; o > 0; o >>= 1) { const uint64_t x = __shfl_xor(best, o); best = x > best ? x : best; }
+  const uint32_t u0 = 0xFFFFFFFFu - (uint32_t)best, n0 = (uint32_t)(best >> 32);
+  const uint32_t nt = n0 < 0x7FFFFFFFu ? (n0 + BIG_SCAN_CH - 1u) / BIG_SCAN_CH : 0u;
+  uint64_t pb = 0, tb = 0;
+  if (l == 0) { pb = atomicAdd(&S.cnt[0], (unsigned long long)n0 + 16ull); tb = atomicAdd(&S.cnt[1], (unsigned long long)nt); }
+  pb = __shfl(pb, 0); tb = __shfl(tb, 0);
+  const bool ok = nt && pb + n0 + 16u <= S.npos_cap && tb + nt <= S.ntask_cap;
+  if (l == 0) { BigPick P; P.pb = pb; P.n0 = ok ? n0 : 0xFFFFFFFFu; P.u0 = u0; S.pick[w] = P; }
+  if (ok)
+    for (uint32_t t = l; t < nt; t += WAVE) S.task[tb + t] = make_uint2(w, t);
+}
+__global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+                                                  const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
+                                                  uint32_t flags, BigScan S) {
+  const uint64_t ntask = *(volatile unsigned long long*)&S.cnt[1];
+  for (uint64_t t = blockIdx.x; t < ntask; t += gridDim.x) {
+    const uint2 T = S.task[t];
+    const BigPick P = S.pick[T.x];
+    if (P.n0 == 0xFFFFFFFFu) continue;   // (no tasks are carved for such a document)
+    const uint8_t* u0p = arena + upd_off[doc_upd[fb_list[T.x]] + P.u0];
+    const uint32_t n0 = P.n0, p1 = (T.y + 1u) * BIG_SCAN_CH < n0 ? (T.y + 1u) * BIG_SCAN_CH : n0;
+    for (uint32_t p = T.y * BIG_SCAN_CH + threadIdx.x; p < p1; p += blockDim.x) {
+      uint32_t e = 0, v = 0;
+      // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item ref 1..8
+      // without bit 0x20 next to an origin (a struct the chain meets elsewhere is parsed there, from global memory)
+      const uint32_t ib = u0p[p], rf = ib & 31u;
+      if (ib == 0u || (rf >= 1u && rf <= 8u && !((ib & 0xC0u) && (ib & 0x20u)))) {
+        GCur c; c.init(u0p, n0); c.pos = p;
+        uint32_t kind;
+        if (big_skip(c, kind, 8) && !c.err) {
+          e = c.pos | (kind == 0 ? 0x80000000u : 0u);
+          if (c.pos - p <= BIG_VCAP) {
+            GCur w; w.init(u0p, n0); w.pos = p;
+            const GStruct g = big_struct(w, flags);
+            v = g.ok && w.pos == c.pos && g.len != 0 && g.len < 0xFFFFFFFFull ? (uint32_t)g.len : 0xFFFFFFFFu;
+          }
+        }
+      }
+      S.nx[P.pb + p] = e;
+      S.vl[P.pb + p] = v;
+    }
+  }
+}
 // the struct start 2^(k+1) structs after tile position i < BT_CH (k = -1: the next one, from nx), or BJ_NONE
 YDEV uint32_t big_jump(const BigTile& T, int k, uint32_t i) {
   if (k < 0) { const uint32_t e = T.nx[i]; return e ? (e & 0x7FFFu) : BJ_NONE; }
@@ -2147,20 +2218,17 @@ YDEV bool big_hdr_fast(const BigTile& T, uint32_t hp, uint32_t tn, uint64_t& nst
   hend = hp + e2 + 1u;
   return true;
 }
-YDEV void big_spec(BigTile& T, uint32_t at, uint32_t mis, uint32_t tn, uint32_t n0, uint32_t t0) {
-  const uint8_t* tp = (const uint8_t*)T.b;
+YDEV void big_spec(BigTile& T, const uint32_t* nxg, uint32_t at, uint32_t n0, uint32_t t0) {
+  // the scan's struct ends of the tile's positions, tile-relative (an end 32 KB or more away: no entry, the chain
+  // follow parses that struct from global memory)
   for (uint32_t i = t0; i < BT_CH; i += BIG_THREADS) {
-    uint16_t e = 0;
-    // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item
-    // ref 1..8 without bit 0x20 next to an origin (a rejected position falls back to a global parse)
-    const uint32_t ib = tp[mis + i];
-    const uint32_t rf = ib & 31u;
-    if (at + i < n0 && (ib == 0u || (rf >= 1u && rf <= 8u && !((ib & 0xC0u) && (ib & 0x20u))))) {
-      GCur t; t.init(tp, tn); t.pos = mis + i;
-      uint32_t kind;
-      if (big_skip(t, kind, 8) && !t.err) e = (uint16_t)((t.pos - mis) | (kind == 0 ? 0x8000u : 0u));
+    uint32_t e = 0;
+    if (at + i < n0) {
+      const uint32_t v = nxg[at + i];
+      const uint32_t rel = (v & 0x7FFFFFFFu) - at;
+      if (v && rel < 0x8000u) e = rel | ((v >> 31) << 15);
     }
-    T.nx[i] = e;
+    T.nx[i] = (uint16_t)e;
   }
   // jump tables by doubling (every thread of the workgroup calls this, so the barriers match)
   for (int k = 0; k < BJ_LV; k++) {
@@ -2171,21 +2239,20 @@ YDEV void big_spec(BigTile& T, uint32_t at, uint32_t mis, uint32_t tn, uint32_t 
     }
   }
 }
-// struct records [vs, ns) (all starting inside the tile; byte ranges in rs / re, LDS): validated from
-// LDS, again from global memory when that fails, then stored with their clock lengths; true if any is
-// not what write_struct emits
-YDEV bool big_validate(const BigTile& T, const uint32_t* rs, const uint32_t* re, BigRec* rec, const BigCmd& C, uint32_t flags,
-                       uint32_t t0) {
-  const uint8_t* tp = (const uint8_t*)T.b;
+// struct records [vs, ns) (byte ranges in rs / re, LDS): the scan's verdict (vl, C.aux) where it has one, else
+// validated from global memory, then stored with their clock lengths; true if any is not what write_struct emits
+YDEV bool big_validate(const uint32_t* rs, const uint32_t* re, BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0) {
   bool vbad = false;
   for (uint64_t i = C.vs + t0; i < C.ns; i += BIG_THREADS) {
     BigRec R; R.start = rs[i - C.vs]; R.end = re[i - C.vs];
-    GCur v; v.init(tp, C.tn); v.pos = R.start - C.tb;
-    GStruct g = big_struct(v, flags);
-    uint32_t e = v.pos + C.tb;
-    if (!g.ok || e != R.end) { GCur w; w.init(C.u0p, C.n0); w.pos = R.start; g = big_struct(w, flags); e = w.pos; }
-    vbad |= !g.ok || g.len == 0 || e != R.end || g.len > 0xFFFFFFFFull;
-    R.len = (uint32_t)g.len;
+    uint64_t len = C.aux[R.start];
+    if (len == 0u) {   // (the scan's end for R.start, when it has one, is R.end: the chain took it from nx)
+      GCur w; w.init(C.u0p, C.n0); w.pos = R.start;
+      const GStruct g = big_struct(w, flags);
+      len = g.ok && w.pos == R.end ? g.len : 0u;
+    }
+    vbad |= len == 0u || len >= 0xFFFFFFFFull;
+    R.len = (uint32_t)len;
     rec[C.sbase + i] = R;
   }
   return vbad;
@@ -2300,7 +2367,8 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
                                                     uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
                                                     uint32_t* __restrict__ fb2_list, BigBlk* __restrict__ blk, uint64_t blk_cap,
-                                                    BigRec* __restrict__ rec, uint64_t rec_cap, uint64_t slot_total, uint64_t out_cap) {
+                                                    BigRec* __restrict__ rec, uint64_t rec_cap, uint64_t slot_total, uint64_t out_cap,
+                                                    BigScan S) {
   __shared__ BigLds L;
   __shared__ BigTile T0;
   __shared__ unsigned long long s_pick;
@@ -2313,10 +2381,10 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       __syncthreads();
       const BigCmd C = s_cmd;
       if (C.cmd == 0) return;
-      if (C.cmd == 1) big_spec(T0, C.at, C.mis, C.tn, C.n0, threadIdx.x);
+      if (C.cmd == 1) big_spec(T0, C.aux, C.at, C.n0, threadIdx.x);
       else if (C.cmd == 3) { if (big_clock_ranges(blk, rec, C, threadIdx.x)) L.bad = 1; }
       else if (C.cmd == 4) { if (!big_ds_canon(C, threadIdx.x)) s_cmd.tb = 1; }
-      else if (big_validate(T0, s_rst, s_ren, rec, C, flags, threadIdx.x)) L.bad = 1;
+      else if (big_validate(s_rst, s_ren, rec, C, flags, threadIdx.x)) L.bad = 1;
       __syncthreads();
     }
   }
@@ -2386,6 +2454,10 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   const uint8_t* u0p = arena + upd_off[ua + U0];
   const uint32_t n0 = (uint32_t)(upd_off[ua + U0 + 1] - upd_off[ua + U0]);
   const uint64_t ncap = n0 + 1u;                            // structs take >= 2 bytes; delete-set values >= 1
+  const BigPick PK = S.pick[blockIdx.x];
+  const uint32_t* const nxg = S.nx + PK.pb;                 // the scan's ends and verdicts of U0's positions
+  const uint32_t* const vlg = S.vl + PK.pb;
+  if (l == 0 && (PK.n0 != n0 || PK.u0 != U0)) L.bad = 1;   // (not scanned: the sequential kernel takes it)
   wave_sync();
   uint64_t base = 0, sbase = 0, nb = 0, NS = 0;
   // tile origin tc0 (U0 position), tb = tc0 rounded down to a 16-byte aligned address: LDS byte j of
@@ -2405,9 +2477,9 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     wave_sync();
     if (!spec) return;
     const uint64_t dg0 = DIAG_NOW();
-    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.tn = tn; s_cmd.n0 = n0; }
+    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.n0 = n0; s_cmd.aux = nxg; }
     __syncthreads();
-    big_spec(T0, at, mis, tn, n0, l);
+    big_spec(T0, nxg, at, n0, l);
     __syncthreads();
     dg_spec += DIAG_NOW() - dg0;
   };
@@ -2415,10 +2487,10 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   auto validate = [&]() {                                  // records [vs, NS): all start inside the tile
     const uint64_t dg0 = DIAG_NOW();
     if (l == 0) {
-      s_cmd.cmd = 2; s_cmd.vs = vs; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.tb = tb; s_cmd.tn = tn; s_cmd.u0p = u0p; s_cmd.n0 = n0;
+      s_cmd.cmd = 2; s_cmd.vs = vs; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.u0p = u0p; s_cmd.n0 = n0; s_cmd.aux = vlg;
     }
     __syncthreads();                                       // lane 0's byte ranges and the command before every wave reads them
-    if (big_validate(T0, s_rst, s_ren, rec, s_cmd, flags, l)) L.bad = 1;
+    if (big_validate(s_rst, s_ren, rec, s_cmd, flags, l)) L.bad = 1;
     __syncthreads();
     vs = NS;
     wave_sync();
@@ -2904,13 +2976,34 @@ int ygm_diag_read(unsigned long long* out, int reset) {
 
 size_t ygm_k_big_blk_bytes() { return sizeof(BigBlk); }
 size_t ygm_k_big_rec_bytes() { return sizeof(BigRec); }
+// the snapshot scan's scratch for n_fb large documents of fb_bytes in all: counters, picks, tasks, nx, vl
+static void big_scan_layout(uint32_t n_fb, uint64_t fb_bytes, BigScan& S, uint8_t* base, size_t& total) {
+  S.ntask_cap = fb_bytes / BIG_SCAN_CH + n_fb + 1;
+  S.npos_cap = fb_bytes + 16ull * n_fb + 16;
+  size_t o = 0;
+  auto carve = [&](size_t bytes) { const size_t a = o; o += (bytes + 255) & ~(size_t)255; return base ? base + a : nullptr; };
+  S.cnt = (unsigned long long*)carve(32);
+  S.pick = (BigPick*)carve(sizeof(BigPick) * (size_t)n_fb);
+  S.task = (uint2*)carve(sizeof(uint2) * S.ntask_cap);
+  S.nx = (uint32_t*)carve(4 * S.npos_cap);
+  S.vl = (uint32_t*)carve(4 * S.npos_cap);
+  total = o;
+}
+size_t ygm_k_big_scan_bytes(uint32_t n_fb, uint64_t fb_bytes) { BigScan S; size_t t; big_scan_layout(n_fb, fb_bytes, S, nullptr, t); return t; }
 int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
                            uint32_t n_fb, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
                            void* meta, uint32_t* fb2_list, void* blk, uint64_t blk_cap, void* rec, uint64_t rec_cap,
-                           uint64_t slot_total, uint64_t out_cap, hipStream_t s) {
+                           uint64_t slot_total, uint64_t out_cap, void* scan, uint64_t fb_bytes, hipStream_t s) {
   if (n_fb == 0) return 0;
+  BigScan S; size_t total;
+  big_scan_layout(n_fb, fb_bytes, S, (uint8_t*)scan, total);
+  if (hipMemsetAsync(S.cnt, 0, 32, s) != hipSuccess) return launch_rc(__func__);
+  hipLaunchKernelGGL(k_big_pick, dim3((n_fb + 3) / 4), dim3(256), 0, s, upd_off, doc_upd, fb_list, n_fb, S);
+  // the scan: a persistent grid over the tasks (at most 16 workgroups per CU; the task count is on the device)
+  const uint64_t g = S.ntask_cap < 16ull * device_cus() ? S.ntask_cap : 16ull * device_cus();
+  hipLaunchKernelGGL(k_big_scan, dim3((uint32_t)g), dim3(256), 0, s, arena, upd_off, doc_upd, fb_list, flags, S);
   hipLaunchKernelGGL(k_merge_big, dim3(n_fb), dim3(BIG_THREADS), 0, s, arena, upd_off, doc_upd, fb_list, flags, out, out_off, out_len,
-                     status, (DocMeta*)meta, fb2_list, (BigBlk*)blk, blk_cap, (BigRec*)rec, rec_cap, slot_total, out_cap);
+                     status, (DocMeta*)meta, fb2_list, (BigBlk*)blk, blk_cap, (BigRec*)rec, rec_cap, slot_total, out_cap, S);
   return launch_rc(__func__);
 }
 size_t ygm_k_meta_bytes() { return sizeof(DocMeta); }

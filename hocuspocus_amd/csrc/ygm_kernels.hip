@@ -2022,12 +2022,73 @@ YDEV void big_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {   // the wave
     else for (uint64_t q = c; q < n; q++) dst[q] = src[q];
   }
 }
-// output sink: pass 0 counts, pass 1 stores (lane 0 writes literals; copies are wave-wide)
+// A list of byte copies (LDS) run by the wave at once: every lane takes 16-byte chunks of the whole list (the entry
+// by binary search over the chunk prefix), four chunks in flight per lane, so the loads of many short copies overlap
+// instead of each copy waiting for its own.  Sources may be read up to 15 bytes past their end (the arena's and
+// U0's tail padding); destinations are written exactly.
+struct BigCp { uint64_t src; uint32_t dst, n; };
+YDEV void big_copy_list(uint8_t* o, const BigCp* cl, uint32_t nc, uint32_t* pre) {   // pre: 64 words of LDS
+  const uint32_t l = threadIdx.x % WAVE;
+  for (uint32_t g = 0; g < nc; g += WAVE) {
+    const uint32_t m = nc - g < (uint32_t)WAVE ? nc - g : (uint32_t)WAVE;
+    const uint32_t ch = l < m ? (cl[g + l].n + 15u) / 16u : 0u;
+    const uint32_t inc = dpp_incl_add(ch);
+    pre[l] = inc;                                       // inclusive chunk prefix of entries g .. g + 63
+    const uint32_t tot = lane63(inc);
+    wave_sync();
+    for (uint32_t c0 = 0; c0 < tot; c0 += 4u * WAVE) {
+      uint4 v[4]; uint8_t* d[4]; uint32_t k[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t c = c0 + (uint32_t)u * WAVE + l;
+        k[u] = 0; d[u] = nullptr;
+        if (c < tot) {
+          uint32_t lo = 0, hi = m - 1;                  // first entry whose inclusive prefix exceeds c
+          while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (pre[md] > c) hi = md; else lo = md + 1u; }
+          const BigCp E = cl[g + lo];
+          const uint32_t off = 16u * (c - (lo ? pre[lo - 1] : 0u));
+          k[u] = E.n - off < 16u ? E.n - off : 16u;
+          d[u] = o + E.dst + off;
+          __builtin_memcpy(&v[u], (const uint8_t*)(uintptr_t)E.src + off, 16);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (k[u] == 16u) __builtin_memcpy(d[u], &v[u], 16);
+        else if (k[u]) {
+          const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+          for (uint32_t q = 0; q < k[u]; q++) d[u][q] = (uint8_t)(w[q >> 2] >> (8u * (q & 3u)));
+        }
+      }
+    }
+    wave_sync();
+  }
+}
+// output sink: pass 0 counts, pass 1 stores (lane 0 writes literals; copies go to an LDS list run by the wave when
+// it fills and at the end of the pass -- consecutive ones merged)
 struct BigOut {
   uint8_t* o; uint64_t n; bool w;
+  BigCp* cl; uint32_t nc, cap, *pre;
+  uint64_t ls, ld, le;                                  // the last entry: source, destination, destination end
   YDEV void b(uint32_t v) { if (w && threadIdx.x == 0) o[n] = (uint8_t)v; n++; }
   YDEV void vu(uint64_t v) { while (v > 127) { b(0x80u | (uint32_t)(v & 127)); v >>= 7; } b((uint32_t)v); }
-  YDEV void copy(const uint8_t* s, uint64_t len) { if (w) big_copy(o + n, s, len); n += len; }
+  YDEV void flush() { if (nc) { wave_sync(); big_copy_list(o, cl, nc, pre); nc = 0; } }
+  YDEV void add(uint64_t src, uint64_t dst, uint64_t len) {   // len < 2^30
+    if (nc && le == dst && ls + (le - ld) == src && le - ld + len < (1ull << 30)) {   // continues the last entry
+      if (threadIdx.x == 0) cl[nc - 1].n = (uint32_t)(le - ld + len);
+    } else {
+      if (nc == cap) flush();
+      if (threadIdx.x == 0) { BigCp E; E.src = src; E.dst = (uint32_t)dst; E.n = (uint32_t)len; cl[nc] = E; }
+      nc++; ls = src; ld = dst;
+    }
+    le = dst + len;
+  }
+  YDEV void copy(const uint8_t* s, uint64_t len) {
+    if (w)
+      for (uint64_t a = 0; a < len; a += (1ull << 29))
+        add((uint64_t)(uintptr_t)s + a, n + a, len - a < (1ull << 29) ? len - a : (1ull << 29));
+    n += len;
+  }
 };
 // U0's delete set, decoded once by the wave into u32 values (big_ds_decode), then read as a stream of
 // ranges by every lane redundantly (same values, same state): 64 values per register, lane j holding
@@ -2132,23 +2193,35 @@ struct BigScan {
   uint64_t ntask_cap, npos_cap;
 };
 // U0 of each large document (the largest update, the first of equal ones: k_merge_big's rule) and its scan tasks
-__global__ __launch_bounds__(256) void k_big_pick(const uint64_t* __restrict__ upd_off, const uint32_t* __restrict__ doc_upd,
-                                                  const uint32_t* __restrict__ fb_list, uint32_t n_fb, BigScan S) {
-  const uint32_t w = blockIdx.x * 4u + threadIdx.x / WAVE, l = threadIdx.x % WAVE;
-  if (w >= n_fb) return;
-  const uint32_t d = fb_list[w], ua = doc_upd[d], k = doc_upd[d + 1] - ua;
-  uint64_t best = 0;
-  for (uint32_t i = l; i < k; i += WAVE) {
-    const uint64_t n = upd_off[ua + i + 1] - upd_off[ua + i];
-    const uint64_t key = ((n < 0xFFFFFFFFull ? n : 0xFFFFFFFFull) << 32) | (0xFFFFFFFFu - i);
-    best = key > best ? key : best;
+// (a wave per document, 16 per workgroup: the workgroup carves its positions and tasks with one atomic each)
+__global__ __launch_bounds__(1024) void k_big_pick(const uint64_t* __restrict__ upd_off, const uint32_t* __restrict__ doc_upd,
+                                                   const uint32_t* __restrict__ fb_list, uint32_t n_fb, BigScan S) {
+  __shared__ uint64_t s_pb[16], s_tb[16];
+  const uint32_t wv = threadIdx.x / WAVE, w = blockIdx.x * 16u + wv, l = threadIdx.x % WAVE;
+  uint32_t u0 = 0, n0 = 0, nt = 0;
+  if (w < n_fb) {
+    const uint32_t d = fb_list[w], ua = doc_upd[d], k = doc_upd[d + 1] - ua;
+    uint64_t best = 0;
+    for (uint32_t i = l; i < k; i += WAVE) {
+      const uint64_t n = upd_off[ua + i + 1] - upd_off[ua + i];
+      const uint64_t key = ((n < 0xFFFFFFFFull ? n : 0xFFFFFFFFull) << 32) | (0xFFFFFFFFu - i);
+      best = key > best ? key : best;
+    }
+    for (int o = 32; o > 0; o >>= 1) { const uint64_t x = __shfl_xor(best, o); best = x > best ? x : best; }
+    u0 = 0xFFFFFFFFu - (uint32_t)best; n0 = (uint32_t)(best >> 32);
+    nt = n0 < 0x7FFFFFFFu ? (n0 + BIG_SCAN_CH - 1u) / BIG_SCAN_CH : 0u;
   }
-  for (int o = 32; o > 0; o >>= 1) { const uint64_t x = __shfl_xor(best, o); best = x > best ? x : best; }
-  const uint32_t u0 = 0xFFFFFFFFu - (uint32_t)best, n0 = (uint32_t)(best >> 32);
-  const uint32_t nt = n0 < 0x7FFFFFFFu ? (n0 + BIG_SCAN_CH - 1u) / BIG_SCAN_CH : 0u;
-  uint64_t pb = 0, tb = 0;
-  if (l == 0) { pb = atomicAdd(&S.cnt[0], (unsigned long long)n0 + 16ull); tb = atomicAdd(&S.cnt[1], (unsigned long long)nt); }
-  pb = __shfl(pb, 0); tb = __shfl(tb, 0);
+  if (l == 0) { s_pb[wv] = w < n_fb ? (uint64_t)n0 + 16u : 0u; s_tb[wv] = nt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {   // exclusive prefixes over the workgroup's documents, then one carve each
+    uint64_t a = 0, b = 0;
+    for (int i = 0; i < 16; i++) { const uint64_t x = s_pb[i], y = s_tb[i]; s_pb[i] = a; s_tb[i] = b; a += x; b += y; }
+    const uint64_t pa = atomicAdd(&S.cnt[0], (unsigned long long)a), ta = atomicAdd(&S.cnt[1], (unsigned long long)b);
+    for (int i = 0; i < 16; i++) { s_pb[i] += pa; s_tb[i] += ta; }
+  }
+  __syncthreads();
+  if (w >= n_fb) return;
+  const uint64_t pb = s_pb[wv], tb = s_tb[wv];
   const bool ok = nt && pb + n0 + 16u <= S.npos_cap && tb + nt <= S.ntask_cap;
   if (l == 0) { BigPick P; P.pb = pb; P.n0 = ok ? n0 : 0xFFFFFFFFu; P.u0 = u0; S.pick[w] = P; }
   if (ok)
@@ -2157,19 +2230,40 @@ __global__ __launch_bounds__(256) void k_big_pick(const uint64_t* __restrict__ u
 __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                   const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
                                                   uint32_t flags, BigScan S) {
+  // a wave takes BIG_SCAN_CH / 4 positions of the task: the candidates (by their byte) are queued in LDS, every
+  // other position is written as "no parse" at once, then the lanes parse the queue -- a lane per candidate, not
+  // a lane per position (about one position in seven is a candidate in text)
+  __shared__ uint32_t s_q[4][BIG_SCAN_CH / 4];
+  const uint32_t wv = threadIdx.x / WAVE, l = threadIdx.x % WAVE;
+  uint32_t* const q = s_q[wv];
   const uint64_t ntask = *(volatile unsigned long long*)&S.cnt[1];
   for (uint64_t t = blockIdx.x; t < ntask; t += gridDim.x) {
     const uint2 T = S.task[t];
     const BigPick P = S.pick[T.x];
     if (P.n0 == 0xFFFFFFFFu) continue;   // (no tasks are carved for such a document)
     const uint8_t* u0p = arena + upd_off[doc_upd[fb_list[T.x]] + P.u0];
-    const uint32_t n0 = P.n0, p1 = (T.y + 1u) * BIG_SCAN_CH < n0 ? (T.y + 1u) * BIG_SCAN_CH : n0;
-    for (uint32_t p = T.y * BIG_SCAN_CH + threadIdx.x; p < p1; p += blockDim.x) {
+    const uint32_t n0 = P.n0, w0 = T.y * BIG_SCAN_CH + wv * (BIG_SCAN_CH / 4);
+    const uint32_t w1 = w0 + BIG_SCAN_CH / 4 < n0 ? w0 + BIG_SCAN_CH / 4 : n0;
+    uint32_t qn = 0;
+    for (uint32_t b = w0; b < w1; b += WAVE) {
+      const uint32_t p = b + l;
+      bool cand = false;
+      if (p < w1) {
+        // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item ref 1..8
+        // without bit 0x20 next to an origin (a struct the chain meets elsewhere is parsed there, from global memory)
+        const uint32_t ib = u0p[p], rf = ib & 31u;
+        cand = ib == 0u || (rf >= 1u && rf <= 8u && !((ib & 0xC0u) && (ib & 0x20u)));
+        if (!cand) { S.nx[P.pb + p] = 0u; S.vl[P.pb + p] = 0u; }
+      }
+      const uint64_t m = __ballot(cand);
+      if (cand) q[qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = p;
+      qn += (uint32_t)__builtin_popcountll(m);
+    }
+    wave_sync();
+    for (uint32_t j = l; j < qn; j += WAVE) {
+      const uint32_t p = q[j];
       uint32_t e = 0, v = 0;
-      // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item ref 1..8
-      // without bit 0x20 next to an origin (a struct the chain meets elsewhere is parsed there, from global memory)
-      const uint32_t ib = u0p[p], rf = ib & 31u;
-      if (ib == 0u || (rf >= 1u && rf <= 8u && !((ib & 0xC0u) && (ib & 0x20u)))) {
+      {
         GCur c; c.init(u0p, n0); c.pos = p;
         uint32_t kind;
         if (big_skip(c, kind, 8) && !c.err) {
@@ -2184,6 +2278,7 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
       S.nx[P.pb + p] = e;
       S.vl[P.pb + p] = v;
     }
+    wave_sync();   // (the queue is rewritten by the next task)
   }
 }
 // the struct start 2^(k+1) structs after tile position i < BT_CH (k = -1: the next one, from nx), or BJ_NONE
@@ -2376,6 +2471,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   __shared__ BigCmd s_cmd;
   __shared__ uint32_t s_rst[BT_CH / 2], s_ren[BT_CH / 2];   // byte ranges of the current tile's structs (>= 2 bytes each)
   __shared__ BigBlk s_blk[64];
+  __shared__ uint32_t s_cpre[WAVE];
   if (threadIdx.x >= WAVE) {   // helper waves: wave 0's tile commands until it sends 0 (one barrier pair per command)
     for (;;) {
       __syncthreads();
@@ -2425,7 +2521,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
         if (slot < (uint32_t)LB_MAXS) {
           BigPiece& P = L.pc[slot];
           P.key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | clock;
-          P.len = (uint32_t)g.len; P.upd = i; P.b0 = b0; P.b1 = c.pos; P.gc = g.kind == 0;
+          P.len = (uint32_t)g.len; P.src = a + b0; P.nb = c.pos - b0; P.gc = g.kind == 0;
         }
         clock += g.len;
       }
@@ -2657,6 +2753,9 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   uint64_t nblocks = 0, ndsc = 0, size = 0;
   for (int pass = 0; pass < 2 && !bad; pass++) {
     BigOut o; o.o = out + (pass ? s_at : 0); o.n = 0; o.w = pass == 1;
+    // the copy list lives in the U0 tile's LDS past the block-table staging
+    o.cl = (BigCp*)((uint8_t*)&T0 + BIG_SBN * sizeof(BigBlk)); o.nc = 0; o.pre = s_cpre;
+    o.cap = (uint32_t)((sizeof(BigTile) - BIG_SBN * sizeof(BigBlk)) / sizeof(BigCp)); o.ls = o.le = o.ld = 0;
     o.vu(nblocks);
     uint64_t i = 0, nbo = 0;
     uint32_t j = 0;
@@ -2722,7 +2821,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
           } else first = c0;
           if (sweep) {
             if (takeu) o.copy(u0p + B.b0, B.b1 - B.b0);
-            else o.copy(arena + upd_off[ua + L.pc[q].upd] + L.pc[q].b0, L.pc[q].b1 - L.pc[q].b0);
+            else o.copy(arena + L.pc[q].src, L.pc[q].nb);
           }
           cnt += takeu ? B.nst : 1u;
           any = true; pend = c1; pgc = lgc;
@@ -2834,6 +2933,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // pass 0's run counts before pass 1 reads them
     bad |= D.s.err;
     }
+    o.flush();
     DIAGL(3 + pass);
     if (pass == 0) {
       nblocks = nbo; ndsc = nc; size = o.n;
@@ -2998,7 +3098,7 @@ int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const 
   BigScan S; size_t total;
   big_scan_layout(n_fb, fb_bytes, S, (uint8_t*)scan, total);
   if (hipMemsetAsync(S.cnt, 0, 32, s) != hipSuccess) return launch_rc(__func__);
-  hipLaunchKernelGGL(k_big_pick, dim3((n_fb + 3) / 4), dim3(256), 0, s, upd_off, doc_upd, fb_list, n_fb, S);
+  hipLaunchKernelGGL(k_big_pick, dim3((n_fb + 15) / 16), dim3(1024), 0, s, upd_off, doc_upd, fb_list, n_fb, S);
   // the scan: a persistent grid over the tasks (at most 16 workgroups per CU; the task count is on the device)
   const uint64_t g = S.ntask_cap < 16ull * device_cus() ? S.ntask_cap : 16ull * device_cus();
   hipLaunchKernelGGL(k_big_scan, dim3((uint32_t)g), dim3(256), 0, s, arena, upd_off, doc_upd, fb_list, flags, S);

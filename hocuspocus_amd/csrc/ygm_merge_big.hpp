@@ -297,8 +297,8 @@ struct BigRec { uint32_t start, end, len; };
 // log piece (LDS): one struct of a log update
 struct BigPiece {
   uint64_t key;                      // (~client) << 32 | clock: ascending = client descending, clock ascending
-  uint32_t len, upd;                 // clock length, update index within the document
-  uint32_t b0, b1;                   // struct bytes [b0, b1) within update `upd`
+  uint64_t src;                      // arena offset of the struct's bytes
+  uint32_t len, nb;                  // clock length, byte length
   uint32_t gc, pad;
 };
 // log delete range: key as BigPiece.  The delete-set splice (big_ds_plan) annotates it against U0's entry of its client:

@@ -4,7 +4,7 @@ import ctypes, os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-diag = len(sys.argv) > 1 and sys.argv[1] in ("diag", "diagds", "splice")
+diag = len(sys.argv) > 1 and sys.argv[1] in ("diag", "diagds", "splice", "occ")
 dsmode = len(sys.argv) > 1 and sys.argv[1] == "diagds"
 import hocuspocus_amd.engine as eng
 if diag:
@@ -12,6 +12,37 @@ if diag:
 from tools import synth
 import oracle
 e = eng.Engine(0)
+if len(sys.argv) > 1 and sys.argv[1] == "occ":   # C3-full-shaped batch (top ranks): per-workgroup stamps -> concurrency
+    n = int(os.environ.get("OCC_N", "16000"))
+    arena, upd_off, doc_upd = synth.big_docs(n, 10_000_000, 1024, max_clients=64, max_k=200, seed=8)
+    upd_doc = np.repeat(np.arange(n, dtype=np.uint32), np.diff(doc_upd).astype(np.int64))
+    L = eng.lib()
+    L.ygm_diag_ts_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    for rep in range(2):
+        s0 = e.stats()
+        res = e.merge_packed_raw(arena, upd_off, upd_doc, n)
+        s1 = e.stats()
+    ts = np.zeros(16384 * 8, np.uint64)
+    L.ygm_diag_ts_read(ts.ctypes.data, 0)
+    nb = s1.docs_big - s0.docs_big
+    t = ts.reshape(16384, 8).astype(np.int64)[: min(nb, 16384)]
+    t = t[t[:, 0] > 0]
+    st, en = t[:, 0], t[:, 5]
+    ok = en > st
+    st, en, tt = st[ok], en[ok], t[ok]
+    span = (en.max() - st.min()) / 100.0   # us
+    busy = (en - st).sum() / 100.0
+    ph = np.diff(tt[:, :6], axis=1).sum(axis=0) / 100.0
+    sizes = np.diff(upd_off[doc_upd].astype(np.int64))
+    print({"docs": n, "bytes": int(upd_off[-1]), "kernel_ms": round(s1.kernel_ms - s0.kernel_ms, 2), "docs_big": int(nb),
+           "wg_stamped": int(ok.sum()), "span_us": round(span, 1), "busy_wg_us": round(busy, 1), "mean_concurrency": round(busy / span, 1),
+           "phase_sum_us": {"log": ph[0], "u0": ph[1], "sorts": ph[2], "pass0": ph[3], "pass1": ph[4]},
+           "median_doc_bytes": int(np.median(sizes)), "wg_us_p50_p99_max": [float(np.percentile((en - st) / 100.0, q)) for q in (50, 99, 100)]}, flush=True)
+    # concurrency timeline: 20 buckets
+    t0 = st.min(); edges = np.linspace(0, en.max() - t0, 21)
+    conc = [int(((st - t0 <= (a + b) / 2) & (en - t0 >= (a + b) / 2)).sum()) for a, b in zip(edges[:-1], edges[1:])]
+    print({"concurrency_timeline": conc}, flush=True)
+    sys.exit(0)
 if len(sys.argv) > 1 and sys.argv[1] == "splice":   # tests/tile_docs.ds_splice_docs through the diag build
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from tile_docs import ds_splice_docs

@@ -79,10 +79,13 @@ int ygm_k_launch_v2_status(const int32_t* ust, uint32_t n, int32_t* status, uint
 int ygm_k_launch_v2_lens(const uint64_t* off, const int32_t* st, uint32_t n, uint64_t* len, hipStream_t s);
 size_t ygm_k_big_blk_bytes();
 size_t ygm_k_big_rec_bytes();
-int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
-                           uint32_t n_fb, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
-                           void* meta, uint32_t* fb2_list, void* blk, uint64_t blk_cap, void* rec, uint64_t rec_cap,
-                           uint64_t slot_total, uint64_t out_cap, void* scan, uint64_t fb_bytes, hipStream_t s);
+int ygm_k_launch_big_scan(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
+                          uint32_t n_fb, uint32_t flags, void* scan, uint64_t fb_bytes, hipStream_t s);
+int ygm_k_launch_merge_big(int large, const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
+                           uint32_t n_fb, const uint32_t* fbx, uint32_t n, uint32_t* up_list, uint32_t flags, uint8_t* out,
+                           uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, uint32_t* fb2_list, void* blk,
+                           uint64_t blk_cap, void* rec, uint64_t rec_cap, uint64_t slot_total, uint64_t out_cap, void* scan,
+                           uint64_t fb_bytes, hipStream_t s);
 size_t ygm_k_big_scan_bytes(uint32_t n_fb, uint64_t fb_bytes);
 }
 
@@ -90,7 +93,7 @@ namespace {
 
 // mirrors ygm::DocMeta (ygm_kernels.hip); sizeof is a multiple of 16
 struct Meta {
-  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer, wide_defer, pad_[3];
+  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer, wide_defer, mid_defer, pad_[2];
   unsigned long long big_scur;
   unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor, big_cursor;
   unsigned long long payload_sh[16 * 16];
@@ -161,7 +164,7 @@ struct ygm_ctx {
   int mslot = 0;           // counter slot of the next merge launch
   void* meta_slot(int i) const { return (uint8_t*)meta.p + (size_t)i * sizeof(Meta); }
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
-  DevBuf big_blk, big_rec, big_list, big_scan;   // large-document tier: block tables, struct records, documents sent on, scan
+  DevBuf big_blk, big_rec, big_list, big_scan, big_up;   // large-document tier: block tables, struct records, documents sent on, scan
   DevBuf sv_tbl, sv_tn;                // diff: sorted state-vector tables (k_sv_table) and their entry counts
   DevBuf sn_cnt, sn_off, sn_bs, sn_ws, sn_claim, sn_pay;  // snapshot: per-document counts, workspace offsets, scan scratch,
   // [LDS-tier output slots | workspaces], LDS-tier claims, its payload / claimed counters
@@ -240,7 +243,7 @@ void ygm_close(ygm_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
-                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->big_scan, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws, &c->sn_claim, &c->sn_pay,
+                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->big_scan, &c->big_up, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws, &c->sn_claim, &c->sn_pay,
                     &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr, &c->v21_cl})
     b->release();
   for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
@@ -387,14 +390,26 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
   if (m.fb_count) {  // tier 4: large [snapshot, ...log] documents, one wave each; the rest go on to tier 5
     const uint64_t blk_cap = m.fb_bytes / 4 + 2ull * m.fb_count + 16, rec_cap = m.fb_bytes + 2ull * m.fb_count + 16;
     if (!c->big_blk.ensure(blk_cap * ygm_k_big_blk_bytes()) || !c->big_rec.ensure(rec_cap * ygm_k_big_rec_bytes()) ||
-        !c->big_list.ensure((size_t)m.fb_count * 4 + 4) || !c->big_scan.ensure(ygm_k_big_scan_bytes(m.fb_count, m.fb_bytes)))
+        !c->big_list.ensure((size_t)m.fb_count * 4 + 4) || !c->big_up.ensure((size_t)m.fb_count * 4 + 4) ||
+        !c->big_scan.ensure(ygm_k_big_scan_bytes(m.fb_count, m.fb_bytes)))
       return YGM_ENOMEM;
     HIPCHK(hipEventRecord(c->e0, s));
-    if (ygm_k_launch_merge_big(P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->out.as<uint8_t>(),
-                               c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), P.meta,
-                               c->big_list.as<uint32_t>(), c->big_blk.p, blk_cap, c->big_rec.p, rec_cap, P.slot_total, P.out_cap,
-                               c->big_scan.p, m.fb_bytes, s))
+    // the snapshot scan, then the mid size over every large document; a log over its LDS goes on to the large size
+    if (ygm_k_launch_big_scan(P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->big_scan.p, m.fb_bytes, s))
       return YGM_EDEVICE;
+    for (int large = 0; large < 2; large++) {
+      const uint32_t n = large ? m.mid_defer : m.fb_count;
+      if (ygm_k_launch_merge_big(large, P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count,
+                                 large ? c->big_up.as<uint32_t>() : nullptr, n, c->big_up.as<uint32_t>(), c->flags, c->out.as<uint8_t>(),
+                                 c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), P.meta,
+                                 c->big_list.as<uint32_t>(), c->big_blk.p, blk_cap, c->big_rec.p, rec_cap, P.slot_total, P.out_cap,
+                                 c->big_scan.p, m.fb_bytes, s))
+        return YGM_EDEVICE;
+      if (!large) {
+        if ((e = read_meta(c, s, m, P.meta))) return e;
+        if (m.fault) return YGM_EDEVICE;
+      }
+    }
     HIPCHK(hipEventRecord(c->e1, s));
     if ((e = read_meta(c, s, m, P.meta))) return e;
     if (m.fault) return YGM_EDEVICE;

@@ -69,7 +69,8 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned int lean_defer;          // documents sent from the lean kernel to the wave kernel
   unsigned int big_defer;           // documents sent from the large-document kernel to the sequential kernel
   unsigned int wide_defer;          // documents sent from the wide lean kernel to the wave kernel
-  unsigned int pad_[3];
+  unsigned int mid_defer;           // documents sent from the mid-size large-document kernel to the large size
+  unsigned int pad_[2];
   unsigned long long big_scur;      // large-document kernel: struct-record entries carved
   unsigned long long fast_total;    // SV/diff: bytes of the packed (look-back placed) output
   unsigned long long cursor;        // merge: bytes in the overflow region (after the per-document slots)
@@ -1996,8 +1997,6 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
 // ======================================================================= merge: large documents
 // One wave per document the workgroup tier sent on (ygm_merge_big.hpp); documents outside its class
 // go on to the sequential kernel through fb2_list.
-constexpr uint32_t BIG_SBN = 256;   // block-table entries staged in the U0 tile's LDS during emit
-static_assert(sizeof(BigTile) >= BIG_SBN * sizeof(BigBlk) && sizeof(BigBlk) % 16 == 0, "block staging");
 template <class T>
 YDEV void big_bitonic(T* a, uint32_t n) {   // ascending by key; n <= 1024 (entries [n, pow2) padded)
   uint32_t P = 1;
@@ -2169,12 +2168,22 @@ YDEV_NI uint64_t big_skip_global(const uint8_t* u0p, uint32_t n0, uint32_t pos) 
   return (uint64_t)g.pos | ((uint64_t)(kind & 1u) << 32) | (ok ? 0ull : 1ull << 63);
 }
 
-// The U0 tile work the whole workgroup shares (BIG_WAVES waves; wave 0 drives, helper waves join
-// through BigCmd): the speculative parse of a tile's positions, and the validation of its structs.
-#ifndef YGM_BIG_WAVES
-#define YGM_BIG_WAVES 16
-#endif
-constexpr uint32_t BIG_WAVES = YGM_BIG_WAVES, BIG_THREADS = BIG_WAVES * WAVE;
+// The large-document kernel in two sizes (BigCfg): WAVES waves per workgroup (wave 0 drives, the helper waves join
+// the tile, validation, clock-range and delete-set commands through BigCmd), CH tile positions, MAXS / MAXD log
+// structs / delete ranges in LDS, SBN block-table entries staged in the tile's LDS during the emit (the rest of the
+// tile holds the emit's copy list).  The mid size (4 waves, ~40 KB of LDS: four workgroups per CU) takes every
+// large document first and hands one whose log exceeds its LDS to the large size (16 waves, one per CU).
+template <int WAVES_, uint32_t CH_, int MAXS_, int MAXD_, uint32_t SBN_>
+struct BigCfg {
+  static constexpr uint32_t WAVES = WAVES_, THREADS = WAVES_ * 64u, CH = CH_, TILE = CH_ + 64u + 16u, SBN = SBN_;
+  static constexpr int MAXS = MAXS_, MAXD = MAXD_;
+  static constexpr bool MID = WAVES_ < 16;
+  using Tile = BigTileT<CH_>;
+  using Lds = BigLdsT<MAXS_, MAXD_>;
+  static_assert(sizeof(Tile) >= SBN_ * sizeof(BigBlk) + 256 * 16 && sizeof(BigBlk) % 16 == 0, "block staging + copy list");
+};
+using BigCfgL = BigCfg<16, 4096, LB_MAXS, LB_MAXD, 256>;
+using BigCfgM = BigCfg<4, 1024, 256, 256, 64>;
 // cmd 0 done, 1 tile's jump tables, 2 validate, 3 clock ranges, 4 delete-set canonical check
 struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; const uint32_t* aux; };
 
@@ -2282,7 +2291,8 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
   }
 }
 // the struct start 2^(k+1) structs after tile position i < BT_CH (k = -1: the next one, from nx), or BJ_NONE
-YDEV uint32_t big_jump(const BigTile& T, int k, uint32_t i) {
+template <class TL>
+YDEV uint32_t big_jump(const TL& T, int k, uint32_t i) {
   if (k < 0) { const uint32_t e = T.nx[i]; return e ? (e & 0x7FFFu) : BJ_NONE; }
   return T.jp[k][i];
 }
@@ -2290,7 +2300,8 @@ YDEV uint32_t big_jump(const BigTile& T, int k, uint32_t i) {
 // from one 16-byte view of the tile: terminators by the top bits, values by 7-bit compaction, nm = a
 // non-minimal varuint (a zero last byte).  false: the cursor parse takes it.
 YDEV uint32_t big_ctz16(uint32_t t) { return t ? (uint32_t)__builtin_ctz(t) : 16u; }
-YDEV bool big_hdr_fast(const BigTile& T, uint32_t hp, uint32_t tn, uint64_t& nst, uint64_t& client, uint64_t& clock0,
+template <class TL>
+YDEV bool big_hdr_fast(const TL& T, uint32_t hp, uint32_t tn, uint64_t& nst, uint64_t& client, uint64_t& clock0,
                        uint32_t& hend, bool& nm) {
   const uint32_t q = hp >> 4, o = hp & 15u, sh = (o & 7u) * 8u;
   const uint4 A = T.b[q], C = T.b[q + 1];
@@ -2313,10 +2324,11 @@ YDEV bool big_hdr_fast(const BigTile& T, uint32_t hp, uint32_t tn, uint64_t& nst
   hend = hp + e2 + 1u;
   return true;
 }
-YDEV void big_spec(BigTile& T, const uint32_t* nxg, uint32_t at, uint32_t n0, uint32_t t0) {
+template <class CF>
+YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint32_t n0, uint32_t t0) {
   // the scan's struct ends of the tile's positions, tile-relative (an end 32 KB or more away: no entry, the chain
   // follow parses that struct from global memory)
-  for (uint32_t i = t0; i < BT_CH; i += BIG_THREADS) {
+  for (uint32_t i = t0; i < CF::CH; i += CF::THREADS) {
     uint32_t e = 0;
     if (at + i < n0) {
       const uint32_t v = nxg[at + i];
@@ -2328,17 +2340,18 @@ YDEV void big_spec(BigTile& T, const uint32_t* nxg, uint32_t at, uint32_t n0, ui
   // jump tables by doubling (every thread of the workgroup calls this, so the barriers match)
   for (int k = 0; k < BJ_LV; k++) {
     __syncthreads();
-    for (uint32_t i = t0; i < BT_CH; i += BIG_THREADS) {
+    for (uint32_t i = t0; i < CF::CH; i += CF::THREADS) {
       const uint32_t a = big_jump(T, k - 1, i);
-      T.jp[k][i] = (uint16_t)(a < BT_CH ? big_jump(T, k - 1, a) : BJ_NONE);
+      T.jp[k][i] = (uint16_t)(a < CF::CH ? big_jump(T, k - 1, a) : BJ_NONE);
     }
   }
 }
 // struct records [vs, ns) (byte ranges in rs / re, LDS): the scan's verdict (vl, C.aux) where it has one, else
 // validated from global memory, then stored with their clock lengths; true if any is not what write_struct emits
+template <uint32_t NT>
 YDEV bool big_validate(const uint32_t* rs, const uint32_t* re, BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0) {
   bool vbad = false;
-  for (uint64_t i = C.vs + t0; i < C.ns; i += BIG_THREADS) {
+  for (uint64_t i = C.vs + t0; i < C.ns; i += NT) {
     BigRec R; R.start = rs[i - C.vs]; R.end = re[i - C.vs];
     uint64_t len = C.aux[R.start];
     if (len == 0u) {   // (the scan's end for R.start, when it has one, is R.end: the chain took it from nx)
@@ -2387,16 +2400,17 @@ YDEV bool big_ds_entries(const uint32_t* V, uint32_t dsn, uint32_t* eidx, uint64
 // inside 32-bit clocks, and starting after the previous range of its entry ends (sorted, disjoint, not adjacent: the
 // union would write it as it is).  Range starts are the odd value indices that are not client values (entries start
 // at odd indices: 1, then + 2 + 2 n).  C: vs = V, ns = eidx, sbase = W3, n0 = entries, at = end of the entries.
+template <uint32_t NT>
 YDEV bool big_ds_canon(const BigCmd& C, uint32_t t0) {
   const uint32_t* V = (const uint32_t*)(uintptr_t)C.vs;
   const uint32_t* P = V + C.sbase;
   uint32_t* eidx = (uint32_t*)(uintptr_t)C.ns;
   const uint32_t ne = C.n0, end = C.at, nw = end / 32u + 1u;
   uint32_t* bits = ds_bits(eidx, ne);
-  for (uint32_t w = t0; w < nw; w += BIG_THREADS) bits[w] = 0u;
+  for (uint32_t w = t0; w < nw; w += NT) bits[w] = 0u;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __syncthreads();
-  for (uint32_t e = t0; e < ne; e += BIG_THREADS) {
+  for (uint32_t e = t0; e < ne; e += NT) {
     const uint32_t i = eidx[e];
     atomicOr(&bits[i / 32u], 1u << (i % 32u));
     ds_ebs(eidx, ne)[e] = P[i - 1u];
@@ -2406,7 +2420,7 @@ YDEV bool big_ds_canon(const BigCmd& C, uint32_t t0) {
   __syncthreads();
   auto is_client = [&](uint32_t j) { return (bits[j / 32u] >> (j % 32u)) & 1u; };
   bool ok = true;
-  for (uint32_t j = 3u + 2u * t0; j < end; j += 2u * BIG_THREADS) {
+  for (uint32_t j = 3u + 2u * t0; j < end; j += 2u * NT) {
     if (is_client(j)) continue;
     const uint64_t k = V[j], len = V[j + 1u];
     ok &= len != 0u && k + len <= 0xFFFFFFFFull;
@@ -2445,9 +2459,10 @@ YDEV void big_ds_plan(const uint32_t* V, const uint32_t* P, uint32_t* eidx, cons
 
 // block clock ranges [vs, ns) of the block table (cmd 3, the whole workgroup): clock0 + the validated lengths of
 // the block's struct records; true if one passes 2^32 - 1
+template <uint32_t NT>
 YDEV bool big_clock_ranges(BigBlk* blk, const BigRec* rec, const BigCmd& C, uint32_t t0) {
   bool bad = false;
-  for (uint64_t b = C.vs + t0; b < C.ns; b += BIG_THREADS) {
+  for (uint64_t b = C.vs + t0; b < C.ns; b += NT) {
     const uint32_t nst = blk[b].nst, s0 = blk[b].s0;
     uint64_t clk = blk[b].clock0;
     for (uint32_t q = 0; q < nst; q++) clk += rec[C.sbase + s0 + q].len;
@@ -2457,19 +2472,20 @@ YDEV bool big_clock_ranges(BigBlk* blk, const BigRec* rec, const BigCmd& C, uint
   return bad;
 }
 
-__global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+template <class CF>
+__global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                     const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
                                                     uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
                                                     uint32_t* __restrict__ fb2_list, BigBlk* __restrict__ blk, uint64_t blk_cap,
                                                     BigRec* __restrict__ rec, uint64_t rec_cap, uint64_t slot_total, uint64_t out_cap,
-                                                    BigScan S) {
-  __shared__ BigLds L;
-  __shared__ BigTile T0;
+                                                    BigScan S, const uint32_t* __restrict__ fbx, uint32_t* __restrict__ up_list) {
+  __shared__ typename CF::Lds L;
+  __shared__ typename CF::Tile T0;
   __shared__ unsigned long long s_pick;
   __shared__ uint64_t s_base, s_sbase, s_ds0, s_at;
   __shared__ BigCmd s_cmd;
-  __shared__ uint32_t s_rst[BT_CH / 2], s_ren[BT_CH / 2];   // byte ranges of the current tile's structs (>= 2 bytes each)
+  __shared__ uint32_t s_rst[CF::CH / 2], s_ren[CF::CH / 2];   // byte ranges of the current tile's structs (>= 2 bytes each)
   __shared__ BigBlk s_blk[64];
   __shared__ uint32_t s_cpre[WAVE];
   if (threadIdx.x >= WAVE) {   // helper waves: wave 0's tile commands until it sends 0 (one barrier pair per command)
@@ -2477,16 +2493,17 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       __syncthreads();
       const BigCmd C = s_cmd;
       if (C.cmd == 0) return;
-      if (C.cmd == 1) big_spec(T0, C.aux, C.at, C.n0, threadIdx.x);
-      else if (C.cmd == 3) { if (big_clock_ranges(blk, rec, C, threadIdx.x)) L.bad = 1; }
-      else if (C.cmd == 4) { if (!big_ds_canon(C, threadIdx.x)) s_cmd.tb = 1; }
-      else if (big_validate(s_rst, s_ren, rec, C, flags, threadIdx.x)) L.bad = 1;
+      if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.n0, threadIdx.x);
+      else if (C.cmd == 3) { if (big_clock_ranges<CF::THREADS>(blk, rec, C, threadIdx.x)) L.bad = 1; }
+      else if (C.cmd == 4) { if (!big_ds_canon<CF::THREADS>(C, threadIdx.x)) s_cmd.tb = 1; }
+      else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, threadIdx.x)) L.bad = 1;
       __syncthreads();
     }
   }
   const uint32_t l = threadIdx.x;
   DIAGL_T0
-  const uint32_t d = fb_list[blockIdx.x];
+  const uint32_t w = fbx ? fbx[blockIdx.x] : blockIdx.x;   // index into fb_list (and the scan's picks)
+  const uint32_t d = fb_list[w];
   const uint32_t ua = doc_upd[d], k = doc_upd[d + 1] - ua;
   if (l == 0) { L.npc = 0; L.nrg = 0; L.bad = (flags & 2u) ? 1u : 0u; s_pick = 0; }   // YGM_F_FORCE_SEQ: all to the sequential kernel
   wave_sync();
@@ -2518,7 +2535,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
         bad |= !g.ok || g.len == 0 || clock + g.len > 0xFFFFFFFFull;
         if (bad) break;
         const uint32_t slot = atomicAdd(&L.npc, 1u);
-        if (slot < (uint32_t)LB_MAXS) {
+        if (slot < (uint32_t)CF::MAXS) {
           BigPiece& P = L.pc[slot];
           P.key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | clock;
           P.len = (uint32_t)g.len; P.src = a + b0; P.nb = c.pos - b0; P.gc = g.kind == 0;
@@ -2534,15 +2551,21 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
         bad |= client > 0xFFFFFFFFull || ck + ln > 0xFFFFFFFFull;
         if (bad) break;
         const uint32_t slot = atomicAdd(&L.nrg, 1u);
-        if (slot < (uint32_t)LB_MAXD) { L.rg[slot].key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | ck; L.rg[slot].len = (uint32_t)ln; }
+        if (slot < (uint32_t)CF::MAXD) { L.rg[slot].key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | ck; L.rg[slot].len = (uint32_t)ln; }
       }
     }
     if (bad || c.err) L.bad = 1;
   }
   DIAGL(0);
-  // ---- U0, tile by tile (BigTile): the wave stages BT_CH + BT_OV bytes in LDS with aligned 16-byte
+  wave_sync();
+  if (CF::MID && !L.bad && (L.npc > (uint32_t)CF::MAXS || L.nrg > (uint32_t)CF::MAXD)) {   // the large size takes it
+    if (l == 0) { s_cmd.cmd = 0; up_list[atomicAdd(&meta->mid_defer, 1u)] = w; }
+    __syncthreads();   // (the helper waves' first barrier: they read cmd 0 and leave)
+    return;
+  }
+  // ---- U0, tile by tile (BigTile): the wave stages CF::CH + BT_OV bytes in LDS with aligned 16-byte
   //      loads; every lane parses a struct speculatively (skip-only: end and kind) at each of its
-  //      positions of the first BT_CH bytes; the chain of real struct boundaries is then followed
+  //      positions of the first CF::CH bytes; the chain of real struct boundaries is then followed
   //      with one LDS lookup per struct (block headers parsed from the tile), every struct's byte
   //      range recorded; before the tile moves on, the wave validates its structs in parallel from LDS.
   //      A struct the speculative parse could not take (leaves the tile, JSON of > 8 entries) is parsed from
@@ -2550,7 +2573,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   const uint8_t* u0p = arena + upd_off[ua + U0];
   const uint32_t n0 = (uint32_t)(upd_off[ua + U0 + 1] - upd_off[ua + U0]);
   const uint64_t ncap = n0 + 1u;                            // structs take >= 2 bytes; delete-set values >= 1
-  const BigPick PK = S.pick[blockIdx.x];
+  const BigPick PK = S.pick[w];
   const uint32_t* const nxg = S.nx + PK.pb;                 // the scan's ends and verdicts of U0's positions
   const uint32_t* const vlg = S.vl + PK.pb;
   if (l == 0 && (PK.n0 != n0 || PK.u0 != U0)) L.bad = 1;   // (not scanned: the sequential kernel takes it)
@@ -2567,15 +2590,15 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     const uint4* g = (const uint4*)(u0p + at - mis);
     const uint32_t nld = (n0 - at + mis + 15u) / 16u;     // aligned chunks up to the end of U0 (arena tail padding)
     wave_sync();                                           // readers of the previous tile are done
-    for (uint32_t j = l; j < BT_TILE / 16 && j < nld; j += WAVE) T0.b[j] = g[j];
+    for (uint32_t j = l; j < CF::TILE / 16 && j < nld; j += WAVE) T0.b[j] = g[j];
     tc0 = at; tb = at - mis;
-    tn = n0 - tb < BT_TILE ? n0 - tb : BT_TILE;
+    tn = n0 - tb < CF::TILE ? n0 - tb : CF::TILE;
     wave_sync();
     if (!spec) return;
     const uint64_t dg0 = DIAG_NOW();
     if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.n0 = n0; s_cmd.aux = nxg; }
     __syncthreads();
-    big_spec(T0, nxg, at, n0, l);
+    big_spec<CF>(T0, nxg, at, n0, l);
     __syncthreads();
     dg_spec += DIAG_NOW() - dg0;
   };
@@ -2586,7 +2609,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       s_cmd.cmd = 2; s_cmd.vs = vs; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.u0p = u0p; s_cmd.n0 = n0; s_cmd.aux = vlg;
     }
     __syncthreads();                                       // lane 0's byte ranges and the command before every wave reads them
-    if (big_validate(s_rst, s_ren, rec, s_cmd, flags, l)) L.bad = 1;
+    if (big_validate<CF::THREADS>(s_rst, s_ren, rec, s_cmd, flags, l)) L.bad = 1;
     __syncthreads();
     vs = NS;
     wave_sync();
@@ -2613,7 +2636,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       wave_sync();
     };
     for (uint64_t b = 0; b < nb && !bad; b++) {
-      if (!have || pos >= tc0 + BT_CH) { if (have) validate(); load_tile(pos, true); have = true; }
+      if (!have || pos >= tc0 + CF::CH) { if (have) validate(); load_tile(pos, true); have = true; }
       uint64_t hn, hc, hk;
       uint32_t he;
       bool hnm;
@@ -2638,15 +2661,15 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       }
       uint32_t fgc = 0, lgc = 0;
       for (uint32_t q = 0; q < bnst && !bad;) {
-        if (pos >= tc0 + BT_CH) { validate(); load_tile(pos, true); }
+        if (pos >= tc0 + CF::CH) { validate(); load_tile(pos, true); }
         // up to 64 of the block's structs per step: lane j finds the start of struct q + j by composing
         // the jump tables along the bits of j; the structs taken are the leading lanes that start inside
         // the tile and have a speculative parse
         const uint32_t want = bnst - q < 64u ? bnst - q : 64u;
         uint32_t S = pos - tc0;
         for (int k = 0; k < 6 && ((want - 1u) >> k); k++)
-          if (((l >> k) & 1u) && S < BT_CH) S = big_jump(T0, k - 1, S);
-        const uint32_t E = (l < want && S < BT_CH) ? (uint32_t)T0.nx[S] : 0u;
+          if (((l >> k) & 1u) && S < CF::CH) S = big_jump(T0, k - 1, S);
+        const uint32_t E = (l < want && S < CF::CH) ? (uint32_t)T0.nx[S] : 0u;
         const uint64_t tk = __ballot(E != 0u);
         const uint32_t m = ~tk ? (uint32_t)__builtin_ctzll(~tk) : 64u;
         if (m) {
@@ -2700,7 +2723,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
     // block clock ranges, the whole workgroup: clock0 + the lengths of the block's structs
     if (l == 0) { s_cmd.cmd = 3; s_cmd.vs = base; s_cmd.ns = base + nb; s_cmd.sbase = sbase; }
     __syncthreads();
-    if (big_clock_ranges(blk, rec, s_cmd, l)) L.bad = 1;
+    if (big_clock_ranges<CF::THREADS>(blk, rec, s_cmd, l)) L.bad = 1;
     __syncthreads();
   }
   // ---- U0's delete set as values V (the struct records' scratch is free after the clock-range pass), with each
@@ -2732,7 +2755,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
       }
       __syncthreads();
       const BigCmd C4 = s_cmd;                                 // (copied before big_ds_canon's first barrier: tb is
-      if (!big_ds_canon(C4, l)) s_cmd.tb = 1;                  //  written after its last; every writer writes 1)
+      if (!big_ds_canon<CF::THREADS>(C4, l)) s_cmd.tb = 1;                  //  written after its last; every writer writes 1)
       __syncthreads();
       DP.fast = s_cmd.tb == 0;
     }
@@ -2743,7 +2766,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   __syncthreads();
   DIAGL(1);
   const uint32_t npc = L.npc, nrg = L.nrg;
-  bool bad = L.bad || npc > (uint32_t)LB_MAXS || nrg > (uint32_t)LB_MAXD;
+  bool bad = L.bad || npc > (uint32_t)CF::MAXS || nrg > (uint32_t)CF::MAXD;
   if (!bad) { big_bitonic(L.pc, npc); big_bitonic(L.rg, nrg); }
   const BigBlk* T = blk + s_base;
   if (bad) nb = 0;
@@ -2754,20 +2777,20 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
   for (int pass = 0; pass < 2 && !bad; pass++) {
     BigOut o; o.o = out + (pass ? s_at : 0); o.n = 0; o.w = pass == 1;
     // the copy list lives in the U0 tile's LDS past the block-table staging
-    o.cl = (BigCp*)((uint8_t*)&T0 + BIG_SBN * sizeof(BigBlk)); o.nc = 0; o.pre = s_cpre;
-    o.cap = (uint32_t)((sizeof(BigTile) - BIG_SBN * sizeof(BigBlk)) / sizeof(BigCp)); o.ls = o.le = o.ld = 0;
+    o.cl = (BigCp*)((uint8_t*)&T0 + CF::SBN * sizeof(BigBlk)); o.nc = 0; o.pre = s_cpre;
+    o.cap = (uint32_t)((sizeof(typename CF::Tile) - CF::SBN * sizeof(BigBlk)) / sizeof(BigCp)); o.ls = o.le = o.ld = 0;
     o.vu(nblocks);
     uint64_t i = 0, nbo = 0;
     uint32_t j = 0;
     // U0 blocks no log piece touches (and whose headers are minimal) are U0's bytes [h0, b1) as
     // written: consecutive ones go out as one verbatim run [r0, r1)
     uint64_t r0 = 0, r1 = 0;
-    // the block table is read through LDS (the U0 tile is free now): BIG_SBN entries per refill
+    // the block table is read through LDS (the U0 tile is free now): CF::SBN entries per refill
     uint64_t sc = ~0ull;
     const BigBlk* SB = (const BigBlk*)&T0;
     while ((i < nb || j < npc) && !bad) {
-      if (i < nb && (sc == ~0ull || i >= sc + BIG_SBN)) {
-        const uint64_t m = nb - i < BIG_SBN ? nb - i : BIG_SBN;
+      if (i < nb && (sc == ~0ull || i >= sc + CF::SBN)) {
+        const uint64_t m = nb - i < CF::SBN ? nb - i : CF::SBN;
         const uint4* g = (const uint4*)(T + i);
         uint4* t = (uint4*)&T0;
         wave_sync();
@@ -2780,7 +2803,7 @@ __global__ __launch_bounds__(BIG_THREADS) void k_merge_big(const uint8_t* __rest
         // log piece's); the leading run of such blocks extends the verbatim run (U0 blocks are contiguous)
         const uint64_t cpx = j < npc ? 0xFFFFFFFFull - (L.pc[j].key >> 32) : 0;
         const uint64_t q = i + l;
-        bool ok = q < nb && q < sc + BIG_SBN;
+        bool ok = q < nb && q < sc + CF::SBN;
         uint32_t h0q = 0, b1q = 0;
         if (ok) { const BigBlk& Q = SB[q - sc]; ok = Q.hcanon && (j >= npc || Q.client > cpx); h0q = Q.h0; b1q = Q.b1; }
         const uint64_t m = __ballot(ok);
@@ -3090,10 +3113,8 @@ static void big_scan_layout(uint32_t n_fb, uint64_t fb_bytes, BigScan& S, uint8_
   total = o;
 }
 size_t ygm_k_big_scan_bytes(uint32_t n_fb, uint64_t fb_bytes) { BigScan S; size_t t; big_scan_layout(n_fb, fb_bytes, S, nullptr, t); return t; }
-int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
-                           uint32_t n_fb, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
-                           void* meta, uint32_t* fb2_list, void* blk, uint64_t blk_cap, void* rec, uint64_t rec_cap,
-                           uint64_t slot_total, uint64_t out_cap, void* scan, uint64_t fb_bytes, hipStream_t s) {
+int ygm_k_launch_big_scan(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
+                          uint32_t n_fb, uint32_t flags, void* scan, uint64_t fb_bytes, hipStream_t s) {
   if (n_fb == 0) return 0;
   BigScan S; size_t total;
   big_scan_layout(n_fb, fb_bytes, S, (uint8_t*)scan, total);
@@ -3102,8 +3123,26 @@ int ygm_k_launch_merge_big(const uint8_t* arena, const uint64_t* upd_off, const 
   // the scan: a persistent grid over the tasks (at most 16 workgroups per CU; the task count is on the device)
   const uint64_t g = S.ntask_cap < 16ull * device_cus() ? S.ntask_cap : 16ull * device_cus();
   hipLaunchKernelGGL(k_big_scan, dim3((uint32_t)g), dim3(256), 0, s, arena, upd_off, doc_upd, fb_list, flags, S);
-  hipLaunchKernelGGL(k_merge_big, dim3(n_fb), dim3(BIG_THREADS), 0, s, arena, upd_off, doc_upd, fb_list, flags, out, out_off, out_len,
-                     status, (DocMeta*)meta, fb2_list, (BigBlk*)blk, blk_cap, (BigRec*)rec, rec_cap, slot_total, out_cap, S);
+  return launch_rc(__func__);
+}
+// large = 0: the mid size over fb_list (documents whose log exceeds its LDS go to up_list, meta->mid_defer);
+// large = 1: the large size over the fb_list indices in fbx[0, n)
+int ygm_k_launch_merge_big(int large, const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
+                           uint32_t n_fb, const uint32_t* fbx, uint32_t n, uint32_t* up_list, uint32_t flags, uint8_t* out,
+                           uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, uint32_t* fb2_list, void* blk,
+                           uint64_t blk_cap, void* rec, uint64_t rec_cap, uint64_t slot_total, uint64_t out_cap, void* scan,
+                           uint64_t fb_bytes, hipStream_t s) {
+  if (n == 0) return 0;
+  BigScan S; size_t total;
+  big_scan_layout(n_fb, fb_bytes, S, (uint8_t*)scan, total);
+  if (large)
+    hipLaunchKernelGGL(k_merge_big<BigCfgL>, dim3(n), dim3(BigCfgL::THREADS), 0, s, arena, upd_off, doc_upd, fb_list, flags, out, out_off,
+                       out_len, status, (DocMeta*)meta, fb2_list, (BigBlk*)blk, blk_cap, (BigRec*)rec, rec_cap, slot_total, out_cap, S,
+                       fbx, up_list);
+  else
+    hipLaunchKernelGGL(k_merge_big<BigCfgM>, dim3(n), dim3(BigCfgM::THREADS), 0, s, arena, upd_off, doc_upd, fb_list, flags, out, out_off,
+                       out_len, status, (DocMeta*)meta, fb2_list, (BigBlk*)blk, blk_cap, (BigRec*)rec, rec_cap, slot_total, out_cap, S,
+                       fbx, up_list);
   return launch_rc(__func__);
 }
 size_t ygm_k_meta_bytes() { return sizeof(DocMeta); }

@@ -307,25 +307,24 @@ struct BigPiece {
 constexpr uint32_t BIG_NOENT = 0xFFFFFFFFu;
 struct BigRange { uint64_t key; uint32_t len, ent, a, b1, s, e, pa, pb; };
 
-// U0 tile (LDS): bytes staged by the whole wave; structs are parsed speculatively at every
-// position of its first BT_CH bytes; BT_OV bytes of overlap let a struct starting there end inside
-// (static LDS: 121 KB per workgroup; one 1024-thread workgroup per CU either way, by its VGPRs).  jp[k][i]
-// is the struct start 2^(k+1) structs after position i (jump tables built from nx by doubling),
-// BJ_NONE when the chain breaks (a position without a speculative parse) or passes the tile's BT_CH
-// positions on the way: the chain follow takes up to 64 structs of a block per step, lane j composing
-// the tables along the bits of j.
-constexpr uint32_t BT_CH = 4096, BT_OV = 2048, BT_TILE = BT_CH + BT_OV + 16;
+// U0 tile (LDS): CH positions of U0 from the tile origin (plus 64 bytes of overlap, so a block header starting
+// among them ends inside, and 16 for the alignment shift), the snapshot scan's struct ends of those positions (nx:
+// end - tile origin, bit 15 = GC; 0 = no parse) and jump tables: jp[k][i] is the struct start 2^(k+1) structs after
+// position i (built from nx by doubling), BJ_NONE when the chain breaks (a position without an end) or passes the
+// tile's CH positions on the way: the chain follow takes up to 64 structs of a block per step, lane j composing the
+// tables along the bits of j.
 constexpr int BJ_LV = 5;
 constexpr uint32_t BJ_NONE = 0xFFFFu;
-struct BigTile {
-  uint4 b[BT_TILE / 16];
-  uint16_t nx[BT_CH];                // speculative struct end - tile origin, bit 15 = GC; 0 = no parse
-  uint16_t jp[BJ_LV][BT_CH];
+template <uint32_t CH>
+struct BigTileT {
+  uint4 b[(CH + 64 + 16) / 16];
+  uint16_t nx[CH];
+  uint16_t jp[BJ_LV][CH];
 };
-
-struct BigLds {
-  BigPiece pc[LB_MAXS];
-  BigRange rg[LB_MAXD];
+template <int MAXS, int MAXD>
+struct BigLdsT {
+  BigPiece pc[MAXS];
+  BigRange rg[MAXD];
   uint32_t npc, nrg, bad, u0;
 };
 

@@ -696,6 +696,41 @@ def test_large_documents_c3_c5_vs_oracle(eng, xml):
         assert eng.stats().docs_seq - st0.docs_seq == 0
 
 
+def _log_structs(us):
+    # struct count of a document's log (every update but the largest): the block headers' counts
+    def vu(b, p):
+        n = s = 0
+        while True:
+            c = b[p]; p += 1; n |= (c & 127) << s; s += 7
+            if c < 128:
+                return n, p
+    i0 = max(range(len(us)), key=lambda i: len(us[i]))
+    t = 0
+    for i, u in enumerate(us):
+        if i == i0:
+            continue
+        nb, p = vu(u, 0)
+        assert nb <= 1   # (synth: one block per log update)
+        if nb:
+            t += vu(u, p)[0]
+    return t
+
+
+def test_large_documents_mid_and_large_sizes_vs_oracle(eng):
+    # the mid-size kernel holds 256 log structs / delete ranges in LDS; documents over that go on to the large size
+    from tools import synth
+    arena, upd_off, doc_upd = synth.big_docs(8, 300000, 1024, max_clients=64, max_k=900, seed=5)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(8)]
+    counts = [_log_structs(us) for us in docs]
+    assert sum(c > 256 for c in counts) >= 3 and sum(c <= 256 for c in counts) >= 2, counts
+    st0 = eng.stats()
+    res = eng.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+    assert not bad, (bad, counts)
+    assert eng.stats().docs_big - st0.docs_big == len(docs)
+
+
 def test_large_document_10mb_vs_oracle(eng):
     # BASELINE C3's largest size: one 10 MB [snapshot, ...log] document through the large-document tier
     from tools import synth

@@ -151,7 +151,11 @@ class GpuBackend:
         return self.torch.from_numpy(a).to(self.dev)
 
     def merge_async(self, c):
-        self.eng.merge_device_async(c["da"], c["bytes"], c["do"], c["dd"], c["n_upd"], c["n"], self.stream.cuda_stream)
+        if "doff" in c:
+            self.eng.merge_device_lens_async(c["da"], c["bytes"], c["doff"], c["dlen"], c["dd"], c["n_upd"], c["n"],
+                                             self.stream.cuda_stream)
+        else:
+            self.eng.merge_device_async(c["da"], c["bytes"], c["do"], c["dd"], c["n_upd"], c["n"], self.stream.cuda_stream)
 
     def merge_finish(self):
         return self.eng.merge_device_finish()
@@ -268,6 +272,11 @@ def c2_corpus(be, prefix, per_gpu, updates, rank, world):
     c["da"] = be.put(arena, 64)
     c["do"] = be.put(upd_off.view(np.int64))
     c["dd"] = be.put(doc_upd.view(np.int32))
+    lens = np.diff(upd_off.astype(np.int64))
+    if isinstance(be, GpuBackend) and lens.max(initial=0) < 65536:
+        # the compact input form (include/ygm.h ygm_merge_v1_device_lens): u64 per document + u16 per update
+        c["doff"] = be.put(upd_off[doc_upd].view(np.int64))
+        c["dlen"] = be.put(lens.astype(np.uint16).view(np.int16))
     return c
 
 

@@ -46,7 +46,9 @@ int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, 
 uint32_t ygm_k_lean_stage_bytes();
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
-                            uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
+                            uint32_t* defer_list, uint64_t out_cap, hipStream_t s, const uint64_t* doc_off, const uint16_t* upd_len);
+int ygm_k_launch_build_off(const uint64_t* doc_off, const uint16_t* upd_len, const uint32_t* doc_upd, const uint32_t* list, uint32_t n,
+                           uint64_t* upd_off, hipStream_t s);
 int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, const uint32_t* list,
                                  uint32_t n_list, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
                                  void* meta, void* meta_next, uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
@@ -189,7 +191,10 @@ struct ygm_ctx {
     uint32_t n_upd = 0, n_docs = 0;
     void* meta = nullptr;   // counter slot of the launch
     bool wide_route = false;   // the launch was the wide lean kernel over the whole batch
+    // the compact input form (ygm_merge_v1_device_lens): upd_off is the context's table, built for deferred documents
+    const uint64_t* doc_off = nullptr; const uint16_t* upd_len = nullptr;
   } pend;
+  DevBuf lens_off;   // update-offset table of a compact-form batch (entries of the documents the lean kernel defers)
   uint32_t lean_span_n = 0;   // lean launches enqueued since the last finish (timed as one span, e0 .. e1)
 };
 
@@ -243,7 +248,7 @@ void ygm_close(ygm_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
-                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->big_scan, &c->big_up, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws, &c->sn_claim, &c->sn_pay,
+                    &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->big_scan, &c->big_up, &c->lens_off, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws, &c->sn_claim, &c->sn_pay,
                     &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr, &c->v21_cl})
     b->release();
   for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
@@ -293,8 +298,8 @@ static void fill_dev_result(ygm_ctx* c, uint64_t data_bytes, ygm_device_result* 
 }
 
 // offsets of the DocMeta counters the tier kernels read as device-side counts
-int ygm_merge_v1_device_async(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_upd_off,
-                              const uint32_t* d_doc_upd, uint32_t n_upd, uint32_t n_docs, void* stream) {
+static int merge_async(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_upd_off, const uint32_t* d_doc_upd,
+                       uint32_t n_upd, uint32_t n_docs, void* stream, const uint64_t* d_doc_off, const uint16_t* d_upd_len) {
   if (!c) return YGM_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   (void)hipSetDevice(c->device);
@@ -304,6 +309,16 @@ int ygm_merge_v1_device_async(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena
   const uint64_t out_cap = slot_total + 3 * arena_bytes + 16ull * n_docs + 64;
   int e = prep_outputs(c, n_docs, out_cap, s, false);
   if (e) return e;
+  // the wide route: a batch whose average document outgrows the narrow kernel's staging (multi-character inserts,
+  // many clients: the realistic logs of c2_mixed) would be deferred by it almost whole -- a pass that only reads
+  // headers yet costs as much as merging a C2 batch (latency-bound) -- so the wide kernel takes every document
+  const bool wide_route = n_docs && arena_bytes / n_docs > (uint64_t)ygm_k_lean_stage_bytes() && getenv("YGM_NO_WIDE_ROUTE") == nullptr;
+  if (d_doc_off) {   // compact form: the table every tier after the narrow kernel reads (only deferred documents' entries)
+    if (!c->lens_off.ensure(8ull * n_upd + 16)) return YGM_ENOMEM;
+    d_upd_off = c->lens_off.as<uint64_t>();
+    if (wide_route && ygm_k_launch_build_off(d_doc_off, d_upd_len, d_doc_upd, nullptr, n_docs, c->lens_off.as<uint64_t>(), s))
+      return YGM_EDEVICE;
+  }
   // tier 1: lean wave-per-document kernel (debounce-log shape); everything else is deferred.
   // Timing: one event before the first launch since the last finish, one in finish after the
   // last -- per-launch event pairs between back-to-back launches cost ~8 us of stream time each.
@@ -311,17 +326,14 @@ int ygm_merge_v1_device_async(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena
   c->lean_span_n++;
   void* meta = c->meta_slot(c->mslot);
   void* meta_next = c->meta_slot(1 - c->mslot);   // zeroed by this launch for the next one
-  // the wide route: a batch whose average document outgrows the narrow kernel's staging (multi-character inserts,
-  // many clients: the realistic logs of c2_mixed) would be deferred by it almost whole -- a pass that only reads
-  // headers yet costs as much as merging a C2 batch (latency-bound) -- so the wide kernel takes every document
-  const bool wide_route = n_docs && arena_bytes / n_docs > (uint64_t)ygm_k_lean_stage_bytes() && getenv("YGM_NO_WIDE_ROUTE") == nullptr;
   if (wide_route) {
     if (ygm_k_launch_merge_lean_wide(d_arena, d_upd_off, d_doc_upd, n_docs, nullptr, n_docs, c->flags, c->out.as<uint8_t>(),
                                      c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta, meta_next,
                                      c->defer_w_list.as<uint32_t>(), out_cap, s))
       return YGM_EDEVICE;
   } else if (ygm_k_launch_merge_lean(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
-                                     c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta, meta_next, c->defer_list.as<uint32_t>(), out_cap, s))
+                                     c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta, meta_next, c->defer_list.as<uint32_t>(), out_cap, s,
+                                     d_doc_off, d_upd_len))
     return YGM_EDEVICE;
   c->pend.wide_route = wide_route;
   if (n_docs) c->mslot = 1 - c->mslot;   // (an empty batch launches nothing: the slot stays current)
@@ -329,7 +341,17 @@ int ygm_merge_v1_device_async(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena
   c->pend.arena = d_arena; c->pend.upd_off = d_upd_off; c->pend.doc_upd = d_doc_upd;
   c->pend.arena_bytes = arena_bytes; c->pend.slot_total = slot_total; c->pend.out_cap = out_cap;
   c->pend.n_upd = n_upd; c->pend.n_docs = n_docs; c->pend.meta = meta;
+  c->pend.doc_off = wide_route ? nullptr : d_doc_off; c->pend.upd_len = d_upd_len;   // (wide route: the table is whole)
   return YGM_OK;
+}
+int ygm_merge_v1_device_async(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_upd_off,
+                              const uint32_t* d_doc_upd, uint32_t n_upd, uint32_t n_docs, void* stream) {
+  return merge_async(c, d_arena, arena_bytes, d_upd_off, d_doc_upd, n_upd, n_docs, stream, nullptr, nullptr);
+}
+int ygm_merge_v1_device_lens_async(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off,
+                                   const uint16_t* d_upd_len, const uint32_t* d_doc_upd, uint32_t n_upd, uint32_t n_docs, void* stream) {
+  if (!d_doc_off || !d_upd_len) return YGM_EINVAL;
+  return merge_async(c, d_arena, arena_bytes, nullptr, d_doc_upd, n_upd, n_docs, stream, d_doc_off, d_upd_len);
 }
 
 int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
@@ -353,6 +375,9 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
     c->stats.docs_lean_wide += P.n_docs - m.wide_defer;
   } else if (m.lean_defer) {  // tier 1b: the wide lean kernel (updates <= 64 bytes, documents <= 7 KB) over tier 1's deferred list
     HIPCHK(hipEventRecord(c->e0, s));
+    if (P.doc_off && ygm_k_launch_build_off(P.doc_off, P.upd_len, P.doc_upd, c->defer_list.as<uint32_t>(), m.lean_defer,
+                                            const_cast<uint64_t*>(P.upd_off), s))   // (compact form: the deferred documents' offsets)
+      return YGM_EDEVICE;
     if (ygm_k_launch_merge_lean_wide(P.arena, P.upd_off, P.doc_upd, P.n_docs, c->defer_list.as<uint32_t>(), m.lean_defer, c->flags,
                                      c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
                                      P.meta, nullptr, c->defer_w_list.as<uint32_t>(), P.out_cap, s))
@@ -448,6 +473,14 @@ int ygm_merge_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
                         const uint32_t* d_doc_upd, uint32_t n_upd, uint32_t n_docs, void* stream, ygm_device_result* out) {
   if (!c || !out) return YGM_EINVAL;
   const int e = ygm_merge_v1_device_async(c, d_arena, arena_bytes, d_upd_off, d_doc_upd, n_upd, n_docs, stream);
+  if (e) return e;
+  return ygm_merge_v1_device_finish(c, out);
+}
+int ygm_merge_v1_device_lens(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off,
+                             const uint16_t* d_upd_len, const uint32_t* d_doc_upd, uint32_t n_upd, uint32_t n_docs, void* stream,
+                             ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  const int e = ygm_merge_v1_device_lens_async(c, d_arena, arena_bytes, d_doc_off, d_upd_len, d_doc_upd, n_upd, n_docs, stream);
   if (e) return e;
   return ygm_merge_v1_device_finish(c, out);
 }

@@ -968,7 +968,7 @@ YDEV_NI void m_parse_update(MergeLds& L, int i, int pass, uint32_t flags) {
     if (c.err) break;
     if (client > 0xFFFFFFFFull) fb = true;
     for (uint64_t s = 0; s < nst && !c.err; s++) {
-      SInfo si; read_struct_fast(c, si, flags);   // (the cursor stays in registers)
+      SInfo si; read_struct_fast<true>(c, si, flags);   // (the cursor stays in registers)
       if (c.err) break;
       const uint64_t end = clock + si.len;
       if (end > MAX_SAFE) { c.fail(ST_RANGE); break; }
@@ -1219,7 +1219,7 @@ YDEV void merge_fast_doc(MergeLds& L, uint32_t d, const uint8_t* __restrict__ ar
     if (f & EF_GAP) { const uint64_t kp = L.key[j - 1]; const uint32_t pend = (uint32_t)kp + L.r_len[L.idx[j - 1]]; w.b(10); w.vu(ck - pend); }
     if (f & EF_EMIT) {
       if (f & EF_GC) { w.b(0); w.vu(L.eE[j] - ck); }
-      else { Cur c{L.in, L.r_start[r], L.ustart[L.r_src[r]] + L.ulen[L.r_src[r]], 0, 0}; SInfo si; read_struct(c, si, flags); write_struct(w, L.in, si, cl, ck, 0, false, flags); }
+      else { Cur c{L.in, L.r_start[r], L.ustart[L.r_src[r]] + L.ulen[L.r_src[r]], 0, 0}; SInfo si; read_struct<true>(c, si, flags); write_struct(w, L.in, si, cl, ck, 0, false, flags); }
     }
   }
   // ---- emit delete set
@@ -1567,7 +1567,7 @@ YDEV void merge_wave_doc(WaveLds& L, uint32_t d, const uint8_t* __restrict__ are
         gw.copy((LU8*)L.in, s0 + 1, n - 1);
       } else {
         Cur c{L.in, s0, s0 + n, 0, 0};
-        SInfo si; read_struct(c, si, flags);
+        SInfo si; read_struct<true>(c, si, flags);
         Out w{(uint8_t*)(lo + gw.pos), 0};
         write_struct(w, L.in, si, cl, ck, 0, false, flags);
         gw.pos += (uint32_t)w.n;
@@ -1620,7 +1620,12 @@ YDEV uint32_t lean_du_load(const uint32_t* __restrict__ doc_upd, uint32_t d, uin
   const uint32_t l = threadIdx.x;
   return d < n_docs ? doc_upd[d + (l & 1u)] : 0u;          // lanes 0 / 1: doc_upd[d], doc_upd[d + 1]
 }
-YDEV uint64_t lean_bo_load(const uint64_t* __restrict__ upd_off, uint32_t du, uint32_t d, uint32_t n_docs) {
+// document bytes [b0, b1): lanes 0 / 1 load b0 / b1 -- from the update-offset table, or (LENS) from the per-document
+// offsets of the compact input form (ygm_merge_v1_device_lens: u64 per document, u16 length per update)
+template <int LENS>
+YDEV uint64_t lean_bo_load(const uint64_t* __restrict__ upd_off, const uint64_t* __restrict__ doc_off, uint32_t du, uint32_t d,
+                           uint32_t n_docs) {
+  if (LENS) return d < n_docs ? doc_off[d + (threadIdx.x & 1u)] : 0ull;
   const uint32_t u0 = rdlane(du, 0), u1 = rdlane(du, 1);
   return d < n_docs ? upd_off[(threadIdx.x & 1u) ? u1 : u0] : 0ull;
 }
@@ -1639,9 +1644,10 @@ YDEV bool lean_stageable(const LeanHdr& h) {
 // issues the loads of one document: staged chunks and the per-row update offsets.  Every
 // load is unconditional (clamped addresses) so the prefetch registers are dead between the
 // staging of one document and the prefetch of the next (no loop-carried live ranges).
-template <int WIDE>
-YDEV void lean_prefetch(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off, const LeanHdr& h, bool go,
-                        u32x4 (&v)[LnCfg<WIDE>::IN / 16 / WAVE], uint32_t (&rx)[LN_ROWS], uint32_t (&ry)[LN_ROWS]) {
+template <int WIDE, int LENS = 0>
+YDEV void lean_prefetch(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off, const uint16_t* __restrict__ upd_len,
+                        const LeanHdr& h, bool go, u32x4 (&v)[LnCfg<WIDE>::IN / 16 / WAVE], uint32_t (&rx)[LN_ROWS],
+                        uint32_t (&ry)[LN_ROWS]) {
   const uint32_t l = threadIdx.x;
   const uint64_t a0 = go ? (h.b0 & ~15ull) : 0ull;
   const uint32_t last = go ? (uint32_t)(((h.b0 & 15u) + h.nbytes + 15) / 16) - 1u : 0u;
@@ -1652,8 +1658,16 @@ YDEV void lean_prefetch(const uint8_t* __restrict__ arena, const uint64_t* __res
   }
   // low dwords only (offsets inside one document differ by < 2^32; whole-register loads keep
   // the allocator from reusing a dead high half while the load is in flight -- a forced wait)
-  const uint32_t* off32 = (const uint32_t*)upd_off;
   const uint32_t kk = go ? h.k : 0u;
+  if (LENS) {   // the rows' update lengths (2 bytes each); offsets by a scan at staging
+#pragma unroll
+    for (int q = 0; q < LN_ROWS; q++) {
+      const uint32_t i = l + WAVE * q;
+      rx[q] = upd_len[h.u0 + (i < kk ? i : 0u)];
+    }
+    return;
+  }
+  const uint32_t* off32 = (const uint32_t*)upd_off;
 #pragma unroll
   for (int q = 0; q < LN_ROWS; q++) {
     const uint32_t i = l + WAVE * q;
@@ -1665,13 +1679,14 @@ YDEV void lean_prefetch(const uint8_t* __restrict__ arena, const uint64_t* __res
 // WIDE = 0: the narrow kernel over every document of the batch (wave w: documents w, w + G, ...), which zeroes
 // the next launch's counter slot.  WIDE = 1: the wide kernel (LnCfg<1>) over the narrow kernel's deferred
 // list (wave w: entries w, w + G, ... of `list`), deferring in turn to its own list (meta->wide_defer).
-template <int WIDE>
+template <int WIDE, int LENS = 0>
 __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                      const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t flags,
                                                      uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                      uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
                                                      DocMeta* __restrict__ meta_next, uint32_t* __restrict__ defer_list, uint64_t out_cap,
-                                                     const uint32_t* __restrict__ list, uint32_t n_list) {
+                                                     const uint32_t* __restrict__ list, uint32_t n_list,
+                                                     const uint64_t* __restrict__ doc_off, const uint16_t* __restrict__ upd_len) {
   typedef LnCfg<WIDE> C;
   __shared__ LeanLdsT<WIDE> LS;
   if (meta_next && blockIdx.x == 0) {   // the next launch's counter slot (nothing reads it during this launch)
@@ -1702,14 +1717,14 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
   uint32_t d = WIDE ? (n_it > blockIdx.x ? docof(0) : n_docs) : blockIdx.x;
   (void)n_it;
   uint32_t du = lean_du_load(doc_upd, d, n_docs);
-  LeanHdr hn = lean_hdr_of(du, lean_bo_load(upd_off, du, d, n_docs));
+  LeanHdr hn = lean_hdr_of(du, lean_bo_load<LENS>(upd_off, doc_off, du, d, n_docs));
   du = lean_du_load(doc_upd, LN_AHEAD(1), n_docs);                  // header pipeline: doc_upd one document ahead
   u32x4 v[C::IN / 16 / WAVE];
   uint32_t rx[LN_ROWS], ry[LN_ROWS];
 #pragma unroll
   for (int q = 0; q < LN_ROWS; q++) { rx[q] = 0; ry[q] = 0; }
   bool gn = !force_seq && lean_stageable<WIDE>(hn);
-  lean_prefetch<WIDE>(arena, upd_off, hn, gn, v, rx, ry);
+  lean_prefetch<WIDE, LENS>(arena, upd_off, upd_len, hn, gn, v, rx, ry);
   uint64_t payload = 0;   // this wave's output bytes: one atomic per wave, not per document
   // deferred documents: bit j of dmask = the j-th document of the current run of 64 iterations (document
   // dch + j * G), appended to defer_list with ONE atomic per run -- one atomic per document on the single
@@ -1745,8 +1760,20 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
         const uint32_t c = l + WAVE * j;
         if (c < nch) *(LB128*)(lin + 16 * c) = v[j];
       }
+      if (LENS) {   // offsets: an exclusive scan of the lengths over rows (update l + 64 q in lane l of row q)
+        uint32_t carry = shift;
 #pragma unroll
-      for (int q = 0; q < LN_ROWS; q++) { us[q] = shift + (rx[q] - (uint32_t)b0); un[q] = ry[q] - rx[q]; }
+        for (int q = 0; q < LN_ROWS; q++) {
+          un[q] = l + WAVE * q < k ? rx[q] : 0u;
+          const uint32_t inc = dpp_incl_add(un[q]);
+          us[q] = carry + inc - un[q];
+          carry += lane63(inc);
+        }
+        if (carry - shift != (uint32_t)nbytes) go = false;   // lengths that do not add up: deferred (k_build_off clamps)
+      } else {
+#pragma unroll
+        for (int q = 0; q < LN_ROWS; q++) { us[q] = shift + (rx[q] - (uint32_t)b0); un[q] = ry[q] - rx[q]; }
+      }
       if (!WIDE) {   // an update past the narrow window: the wide kernel's document -- defer it without parsing
         bool lng = false;
 #pragma unroll
@@ -1761,11 +1788,11 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
     wave_sync();
     DIAGL(0);
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 1   // timing experiment: stage only
-    { hn = lean_hdr_of(du, lean_bo_load(upd_off, du, LN_AHEAD(1), n_docs)); du = lean_du_load(doc_upd, LN_AHEAD(2), n_docs);
-      gn = !force_seq && lean_stageable<WIDE>(hn); lean_prefetch<WIDE>(arena, upd_off, hn, gn, v, rx, ry); wave_sync(); dit++; d = LN_AHEAD(1); continue; }
+    { hn = lean_hdr_of(du, lean_bo_load<LENS>(upd_off, doc_off, du, LN_AHEAD(1), n_docs)); du = lean_du_load(doc_upd, LN_AHEAD(2), n_docs);
+      gn = !force_seq && lean_stageable<WIDE>(hn); lean_prefetch<WIDE, LENS>(arena, upd_off, upd_len, hn, gn, v, rx, ry); wave_sync(); dit++; d = LN_AHEAD(1); continue; }
 #endif
     // ---- header of the next document (its prefetch is issued after the parse) and doc_upd of the one after
-    const uint64_t bo_next = lean_bo_load(upd_off, du, LN_AHEAD(1), n_docs);
+    const uint64_t bo_next = lean_bo_load<LENS>(upd_off, doc_off, du, LN_AHEAD(1), n_docs);
     const uint32_t du_next = lean_du_load(doc_upd, LN_AHEAD(2), n_docs);
     // single: mergeUpdates([]) = 0000; a single input is returned as is (Y@39011).  It shares the
     // prefetch below with the parse path (a prefetch of its own, in its own branch, gets hoisted
@@ -1815,7 +1842,7 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
 #endif
     hn = lean_hdr_of(du, bo_next); du = du_next;
     gn = !force_seq && lean_stageable<WIDE>(hn);
-    lean_prefetch<WIDE>(arena, upd_off, hn, gn, v, rx, ry);
+    lean_prefetch<WIDE, LENS>(arena, upd_off, upd_len, hn, gn, v, rx, ry);
     defer = defer || __ballot(bad) != 0;
     if (single) { wave_sync(); dit++; d = LN_AHEAD(1); continue; }   // (dit: bit j of dmask is the run's j-th document)
 #if defined(YGM_LEAN_STOP) && YGM_LEAN_STOP == 2   // timing experiment: stage + parse
@@ -2072,7 +2099,10 @@ struct BigOut {
   YDEV void b(uint32_t v) { if (w && threadIdx.x == 0) o[n] = (uint8_t)v; n++; }
   YDEV void vu(uint64_t v) { while (v > 127) { b(0x80u | (uint32_t)(v & 127)); v >>= 7; } b((uint32_t)v); }
   YDEV void flush() { if (nc) { wave_sync(); big_copy_list(o, cl, nc, pre); nc = 0; } }
-  YDEV void add(uint64_t src, uint64_t dst, uint64_t len) {   // len < 2^30
+  YDEV void add(uint64_t src, uint64_t dst, uint64_t len) {
+    for (uint64_t a = 0; a < len; a += (1ull << 29)) add1(src + a, dst + a, len - a < (1ull << 29) ? len - a : (1ull << 29));
+  }
+  YDEV void add1(uint64_t src, uint64_t dst, uint64_t len) {   // len < 2^30
     if (nc && le == dst && ls + (le - ld) == src && le - ld + len < (1ull << 30)) {   // continues the last entry
       if (threadIdx.x == 0) cl[nc - 1].n = (uint32_t)(le - ld + len);
     } else {
@@ -2083,9 +2113,7 @@ struct BigOut {
     le = dst + len;
   }
   YDEV void copy(const uint8_t* s, uint64_t len) {
-    if (w)
-      for (uint64_t a = 0; a < len; a += (1ull << 29))
-        add((uint64_t)(uintptr_t)s + a, n + a, len - a < (1ull << 29) ? len - a : (1ull << 29));
+    if (w) add((uint64_t)(uintptr_t)s, n, len);
     n += len;
   }
 };
@@ -2180,7 +2208,11 @@ struct BigCfg {
   static constexpr bool MID = WAVES_ < 16;
   using Tile = BigTileT<CH_>;
   using Lds = BigLdsT<MAXS_, MAXD_>;
-  static_assert(sizeof(Tile) >= SBN_ * sizeof(BigBlk) + 256 * 16 && sizeof(BigBlk) % 16 == 0, "block staging + copy list");
+  // emit staging in the tile's LDS: [block-table staging (serial emit) | client groups (parallel emit)][splice words][copy list]
+  static constexpr uint32_t GCAP = MAXS_ * 3 / 8;
+  static constexpr uint32_t SBG = SBN_ * 48u > GCAP * 64u ? SBN_ * 48u : GCAP * 64u;
+  static_assert(sizeof(Tile) >= SBG + 12 * MAXD_ + 256 * 16 && sizeof(BigBlk) == 48 && sizeof(BigGrp) == 64 && MAXD_ % 4 == 0,
+                "emit staging");
 };
 using BigCfgL = BigCfg<16, 4096, LB_MAXS, LB_MAXD, 256>;
 using BigCfgM = BigCfg<4, 1024, 256, 256, 64>;
@@ -2370,7 +2402,7 @@ YDEV bool big_validate(const uint32_t* rs, const uint32_t* re, BigRec* rec, cons
 // Scratch words of the document: V [0, W3) values, P [W3, 2 W3) each value's byte end (from the delete set's start),
 // then the entry table: for entry e (a client of U0's delete set, descending) eidx[e] (index of its client value in V),
 // eclient, en (range count), ebs / ebe (bytes of the whole entry), then a bitmap of the client values' indices.
-struct BigDsPlan { uint32_t C, end; bool fast; };
+struct BigDsPlan { uint32_t C, end, b0, bend; bool fast; };   // b0 / bend: bytes of the entries (from the delete set's start)
 YDEV uint32_t* ds_eclient(uint32_t* eidx, uint32_t C) { return eidx + C; }
 YDEV uint32_t* ds_en(uint32_t* eidx, uint32_t C) { return eidx + 2u * C; }
 YDEV uint32_t* ds_ebs(uint32_t* eidx, uint32_t C) { return eidx + 3u * C; }
@@ -2429,17 +2461,21 @@ YDEV bool big_ds_canon(const BigCmd& C, uint32_t t0) {
   return ok;
 }
 // each log range against U0's entry of its client (wave 0, a lane per range): the entry by binary search over the
-// clients, then the U0 ranges it merges with: [a, b1) = the ranges ending at or after its start and starting at or
+// clients (ent: the first entry at or after its client; bit 31 set when U0 has none for it), then the U0 ranges it merges with: [a, b1) = the ranges ending at or after its start and starting at or
 // before its end (U0's ranges are disjoint and not adjacent: both bounds by binary search)
-YDEV void big_ds_plan(const uint32_t* V, const uint32_t* P, uint32_t* eidx, const BigDsPlan& DP, BigRange* rg, uint32_t nrg) {
+// X (LDS, 3 x maxd words): per range the byte start of entry `ent` (the delete set's end if none) and, when U0 has
+// its client, that entry's range count and byte end -- what the emit's sequential loop reads, staged ahead
+YDEV void big_ds_plan(const uint32_t* V, const uint32_t* P, uint32_t* eidx, BigDsPlan& DP, BigRange* rg, uint32_t nrg,
+                      uint32_t* X, uint32_t maxd) {
   const uint32_t l = threadIdx.x % WAVE, ne = DP.C;
   const uint32_t* ecl = ds_eclient(eidx, ne);
+  DP.b0 = P[0]; DP.bend = P[DP.end - 1u];
   for (uint32_t r = l; r < nrg; r += WAVE) {
     BigRange& R = rg[r];
     const uint32_t client = 0xFFFFFFFFu - (uint32_t)(R.key >> 32), k = (uint32_t)R.key, ke = k + R.len;
     uint32_t lo = 0, hi = ne;
     while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (ecl[m] > client) lo = m + 1u; else hi = m; }
-    R.ent = BIG_NOENT; R.a = 0; R.b1 = 0; R.s = k; R.e = ke; R.pa = 0; R.pb = 0;
+    R.ent = lo | 0x80000000u; R.a = 0; R.b1 = 0; R.s = k; R.e = ke; R.pa = 0; R.pb = 0;   // (bit 31: no entry)
     if (lo < ne && ecl[lo] == client) {
       const uint32_t i0 = eidx[lo] + 2u, n = ds_en(eidx, ne)[lo];
       uint32_t a = 0, h = n;
@@ -2451,10 +2487,206 @@ YDEV void big_ds_plan(const uint32_t* V, const uint32_t* P, uint32_t* eidx, cons
         R.s = ka < k ? ka : k; R.e = eb > ke ? eb : ke;
       }
       R.ent = lo; R.a = a; R.b1 = b1; R.pa = P[i0 + 2u * a - 1u]; R.pb = P[i0 + 2u * b1 - 1u];
+      X[maxd + r] = n; X[2u * maxd + r] = ds_ebe(eidx, ne)[lo];
     }
+    X[r] = lo < ne ? ds_ebs(eidx, ne)[lo] : DP.bend;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   wave_sync();
+}
+
+// ---- the parallel struct emit (wave 0, lanes over log pieces / client groups; U0's block headers all minimal).
+// A client group is the log pieces of one client (sorted by clock) and U0's block of that client if it has one
+// ("touched"); the U0 block goes in before the first piece at or after its clock.  Every other U0 block is copied as
+// written, in runs between groups.  The plan (pass 0) sizes every piece (a Skip over a gap to its predecessor, then its
+// bytes), every group (header, pieces, the U0 block) and places every group by an exclusive scan of what each changes
+// against U0's bytes; pass 1 writes headers and Skips from the lanes and queues every copy on the copy list.
+YDEV int64_t wave_incl_add_i64(int64_t v) {
+  const uint32_t l = threadIdx.x % WAVE;
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) { const int64_t t = __shfl_up(v, o, WAVE); if (l >= (uint32_t)o) v += t; }
+  return v;
+}
+YDEV void big_put_vu(uint8_t* d, uint64_t v) {   // one lane writes a varuint
+  while (v > 127) { *d++ = (uint8_t)(0x80u | (v & 127)); v >>= 7; }
+  *d = (uint8_t)v;
+}
+// the predecessor of piece q in its group: the U0 block when it goes right before q, else piece q - 1 (none for the
+// group's first piece); returns whether there is one
+template <class LDS>
+YDEV bool big_piece_pred(const LDS& L, const BigGrp& R, uint32_t q, uint32_t& pend, bool& pgc) {
+  if ((R.flags & 1u) && R.uslot == q) { pend = R.clock1; pgc = (R.flags & 4u) != 0; return true; }
+  if (q > R.q0) { const BigPiece& P = L.pc[q - 1]; pend = (uint32_t)P.key + P.len; pgc = P.gc(); return true; }
+  return false;
+}
+// plan: 0 planned, 1 outside the class (overlap / GC junction: the document defers), 2 not planned (more client groups
+// than G holds: the serial emit takes it).  ngr groups, nbo output blocks, sbytes bytes of the structs part.
+template <class LDS>
+YDEV int big_plan_structs(LDS& L, BigGrp* G, uint32_t gcap, const BigBlk* T, uint32_t nb, uint32_t npc, uint32_t S0, uint32_t ds0,
+                          uint32_t& ngr_out, uint64_t& nbo, uint64_t& sbytes) {
+  const uint32_t l = threadIdx.x % WAVE;
+  // 1. the groups: runs of one client among the sorted pieces
+  uint32_t ngr = 0;
+  for (uint32_t cb = 0; cb < npc; cb += WAVE) {
+    const uint32_t q = cb + l;
+    const bool in = q < npc;
+    const uint32_t X = in ? (uint32_t)(L.pc[q].key >> 32) : 0u;
+    const bool gs = in && (q == 0 || (uint32_t)(L.pc[q - 1].key >> 32) != X);
+    const bool ge = in && (q + 1 == npc || (uint32_t)(L.pc[q + 1].key >> 32) != X);
+    const uint64_t m = __ballot(gs);
+    const uint32_t gi = ngr + lanes_below(m) + (gs ? 1u : 0u) - 1u;
+    ngr += (uint32_t)__builtin_popcountll(m);
+    if (in && gi < gcap) {
+      L.pc[q].gi = gi;
+      if (gs) { G[gi].q0 = q; G[gi].uslot = 0xFFFFFFFFu; G[gi].cnt = 0; }
+      if (ge) G[gi].qend = q + 1u;
+    }
+  }
+  ngr_out = ngr;
+  if (ngr > gcap) return 2;
+  wave_sync();
+  // 2. each group against the block table: the first block at or below its client (binary search, blocks descending)
+  for (uint32_t g = l; g < ngr; g += WAVE) {
+    BigGrp& R = G[g];
+    const uint64_t client = 0xFFFFFFFFull - (uint32_t)(L.pc[R.q0].key >> 32);
+    uint32_t lo = 0, hi = nb;
+    while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (T[md].client > client) lo = md + 1u; else hi = md; }
+    R.flags = 0; R.nst = 0; R.clock0 = R.clock1 = R.b0 = R.b1 = 0; R.h0ins = ds0;
+    if (lo < nb) {
+      const BigBlk B = T[lo];
+      R.h0ins = B.h0;
+      if (B.client == client) {
+        R.flags = 1u | (B.first_gc ? 2u : 0u) | (B.last_gc ? 4u : 0u);
+        R.nst = B.nst; R.clock0 = (uint32_t)B.clock0; R.clock1 = (uint32_t)B.clock1; R.b0 = B.b0; R.b1 = B.b1;
+      }
+    }
+  }
+  wave_sync();
+  // 3. the U0 block's slot: before the first piece at or after its clock
+  for (uint32_t cb = 0; cb < npc; cb += WAVE) {
+    const uint32_t q = cb + l;
+    if (q < npc) {
+      BigGrp& R = G[L.pc[q].gi];
+      const uint32_t c0 = (uint32_t)L.pc[q].key;
+      if ((R.flags & 1u) && c0 >= R.clock0 && (q == R.q0 || (uint32_t)L.pc[q - 1].key < R.clock0)) R.uslot = q;
+    }
+  }
+  wave_sync();
+  for (uint32_t g = l; g < ngr; g += WAVE) if (G[g].uslot == 0xFFFFFFFFu) G[g].uslot = G[g].qend;
+  wave_sync();
+  // 4. pieces: the Skip over the gap to the predecessor; output bytes and structs; inclusive byte prefix
+  bool bad = false;
+  uint32_t carry = 0;
+  for (uint32_t cb = 0; cb < npc; cb += WAVE) {
+    const uint32_t q = cb + l;
+    uint32_t bq = 0;
+    if (q < npc) {
+      const BigPiece& P = L.pc[q];
+      BigGrp& R = G[P.gi];
+      const uint32_t c0 = (uint32_t)P.key;
+      uint32_t pend = 0; bool pgc = false;
+      uint32_t gap = 0;
+      if (big_piece_pred(L, R, q, pend, pgc)) {
+        bad |= c0 < pend || (c0 == pend && pgc && P.gc());
+        gap = c0 > pend ? c0 - pend : 0u;
+      }
+      bq = P.nb() + (gap ? 1u + vu_len(gap) : 0u);
+      atomicAdd(&R.cnt, gap ? 2u : 1u);
+    }
+    const uint32_t inc = dpp_incl_add(bq) + carry;
+    if (q < npc) L.pc[q].pre = inc;
+    carry = lane63(inc);
+  }
+  wave_sync();
+  // 5. groups: the U0 block's gap, header, size; placement by an exclusive scan of each group's change in bytes
+  int64_t dcarry = 0;
+  uint32_t nlog = 0;
+  for (uint32_t gb = 0; gb < ngr; gb += WAVE) {
+    const uint32_t g = gb + l;
+    int64_t delta = 0;
+    if (g < ngr) {
+      BigGrp& R = G[g];
+      const bool touched = (R.flags & 1u) != 0;
+      const uint32_t q0 = R.q0, qe = R.qend, us = R.uslot;
+      const uint32_t pb0 = q0 ? L.pc[q0 - 1].pre : 0u;
+      uint32_t gapu = 0;
+      if (touched && us > q0) {
+        const BigPiece& P = L.pc[us - 1];
+        const uint32_t c1 = (uint32_t)P.key + P.len;
+        bad |= R.clock0 < c1 || (R.clock0 == c1 && P.gc() && (R.flags & 2u));
+        gapu = R.clock0 > c1 ? R.clock0 - c1 : 0u;
+      }
+      const uint32_t cnt = R.cnt + (touched ? R.nst + (gapu ? 1u : 0u) : 0u);
+      const uint32_t first = (touched && us == q0) ? R.clock0 : (uint32_t)L.pc[q0].key;
+      const uint32_t client = 0xFFFFFFFFu - (uint32_t)(L.pc[q0].key >> 32);
+      const uint32_t hdr = vu_len(cnt) + vu_len(client) + vu_len(first);
+      const uint32_t gapub = gapu ? 1u + vu_len(gapu) : 0u;
+      const uint64_t bytes = (uint64_t)hdr + (L.pc[qe - 1].pre - pb0) + (touched ? (uint64_t)(R.b1 - R.b0) + gapub : 0u);
+      R.cnt = cnt; R.first = first; R.gapu = gapu; R.hdr = hdr;
+      R.upos = hdr + ((us > q0 ? L.pc[us - 1].pre : pb0) - pb0) + gapub;
+      delta = (int64_t)bytes - (touched ? (int64_t)(R.b1 - R.h0ins) : 0);
+      nlog += touched ? 0u : 1u;
+    }
+    const int64_t inc = wave_incl_add_i64(delta);
+    if (g < ngr) G[g].rel = (uint32_t)((int64_t)(G[g].h0ins - S0) + dcarry + inc - delta);
+    dcarry += __shfl(inc, WAVE - 1, WAVE);
+  }
+  wave_sync();
+  for (int o = 32; o > 0; o >>= 1) nlog += (uint32_t)__shfl_xor((int)nlog, o, WAVE);
+  nbo = (uint64_t)nb + nlog;
+  sbytes = (uint64_t)((int64_t)(ds0 - S0) + dcarry);
+  return __ballot(bad) ? 1 : 0;
+}
+// pass 1: the structs part at out + base (after the block count)
+template <class LDS>
+YDEV void big_write_structs(const LDS& L, const BigGrp* G, uint32_t ngr, uint32_t npc, const uint8_t* u0p, const uint8_t* arena,
+                            uint32_t S0, uint32_t ds0, uint64_t sbytes, uint64_t base, BigOut& o) {
+  const uint32_t l = threadIdx.x % WAVE;
+  uint8_t* const ob = o.o + base;
+  // U0's untouched blocks in runs between groups, and the touched blocks' struct bytes
+  uint32_t a = S0;
+  for (uint32_t g = 0; g < ngr; g++) {
+    const BigGrp& R = G[g];
+    if (R.h0ins > a) o.add((uint64_t)(uintptr_t)(u0p + a), base + R.rel - (R.h0ins - a), R.h0ins - a);
+    if (R.flags & 1u) { o.add((uint64_t)(uintptr_t)(u0p + R.b0), base + R.rel + R.upos, R.b1 - R.b0); a = R.b1; }
+    else a = R.h0ins;
+  }
+  if (ds0 > a) o.add((uint64_t)(uintptr_t)(u0p + a), base + sbytes - (ds0 - a), ds0 - a);
+  // group headers, and the Skip before a touched block
+  for (uint32_t g = l; g < ngr; g += WAVE) {
+    const BigGrp& R = G[g];
+    uint8_t* d = ob + R.rel;
+    const uint32_t client = 0xFFFFFFFFu - (uint32_t)(L.pc[R.q0].key >> 32);
+    big_put_vu(d, R.cnt); d += vu_len(R.cnt);
+    big_put_vu(d, client); d += vu_len(client);
+    big_put_vu(d, R.first);
+    if (R.gapu) { uint8_t* s = ob + R.rel + R.upos - (1u + vu_len(R.gapu)); *s = 10; big_put_vu(s + 1, R.gapu); }
+  }
+  // pieces: the Skip from the lane, the bytes through the copy list (one entry per piece, appended in parallel)
+  o.le = ~0ull;   // (no merging with the entries above)
+  for (uint32_t cb = 0; cb < npc; cb += WAVE) {
+    if (o.nc + WAVE > o.cap) o.flush();
+    const uint32_t q = cb + l;
+    const bool in = q < npc;
+    uint64_t dst = 0;
+    if (in) {
+      const BigPiece& P = L.pc[q];
+      const BigGrp& R = G[P.gi];
+      const uint32_t pb0 = R.q0 ? L.pc[R.q0 - 1].pre : 0u;
+      uint32_t off = R.hdr + ((q > R.q0 ? L.pc[q - 1].pre : pb0) - pb0);
+      if ((R.flags & 1u) && q >= R.uslot) off += (R.gapu ? 1u + vu_len(R.gapu) : 0u) + (R.b1 - R.b0);
+      dst = base + R.rel + off;
+      uint32_t pend = 0; bool pgc = false;
+      if (big_piece_pred(L, R, q, pend, pgc) && (uint32_t)P.key > pend) {
+        const uint32_t gap = (uint32_t)P.key - pend;
+        o.o[dst] = 10; big_put_vu(o.o + dst + 1, gap); dst += 1u + vu_len(gap);
+      }
+    }
+    const uint64_t m = __ballot(in);
+    if (in) { BigCp E; E.src = (uint64_t)(uintptr_t)(arena + L.pc[q].src); E.dst = (uint32_t)dst; E.n = L.pc[q].nb(); o.cl[o.nc + lanes_below(m)] = E; }
+    o.nc += (uint32_t)__builtin_popcountll(m);
+  }
+  o.le = ~0ull;
 }
 
 // block clock ranges [vs, ns) of the block table (cmd 3, the whole workgroup): clock0 + the validated lengths of
@@ -2538,7 +2770,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
         if (slot < (uint32_t)CF::MAXS) {
           BigPiece& P = L.pc[slot];
           P.key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)client) << 32) | clock;
-          P.len = (uint32_t)g.len; P.src = a + b0; P.nb = c.pos - b0; P.gc = g.kind == 0;
+          P.len = (uint32_t)g.len; P.src = a + b0; P.nbg = (c.pos - b0) | (g.kind == 0 ? 0x80000000u : 0u);
         }
         clock += g.len;
       }
@@ -2579,6 +2811,8 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
   if (l == 0 && (PK.n0 != n0 || PK.u0 != U0)) L.bad = 1;   // (not scanned: the sequential kernel takes it)
   wave_sync();
   uint64_t base = 0, sbase = 0, nb = 0, NS = 0;
+  uint32_t S0 = 0;                                         // U0 position of the first block (after the block count)
+  bool acanon = true;                                      // every block header minimal (the parallel emit's condition)
   // tile origin tc0 (U0 position), tb = tc0 rounded down to a 16-byte aligned address: LDS byte j of
   // the tile is U0 byte tb + j, so tile cursors run in tile coordinates (pointers stay inside T0)
   uint32_t tc0 = 0, tb = 0, tn = 0;                        // tn: tile cursor end (tile coordinates)
@@ -2624,6 +2858,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
     base = s_base; sbase = s_sbase;
     bad |= c.err || nb > n0 / 4u + 1u || base + nb > blk_cap || sbase + ncap > rec_cap;
     uint32_t pos = c.pos;
+    S0 = pos;
     bool have = false;
     uint64_t prevc = ~0ull;
     uint32_t bq = 0;                                       // blocks staged in s_blk
@@ -2659,6 +2894,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
         B.nst = bnst; B.client = hc; B.clock0 = hk; B.clock1 = 0;
         B.h0 = h0; B.hcanon = !hnm; B.pad = 0; B.b0 = pos; B.s0 = (uint32_t)NS;
       }
+      acanon &= !hnm;
       uint32_t fgc = 0, lgc = 0;
       for (uint32_t q = 0; q < bnst && !bad;) {
         if (pos >= tc0 + CF::CH) { validate(); load_tile(pos, true); }
@@ -2745,7 +2981,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
     const bool ok = big_ds_decode(u0p, (uint32_t)s_ds0, n0, dsv, dW3, dsn, dsp, &nm);
     const bool any_nm = __ballot(nm != 0u) != 0;
     if (!ok && l == 0) L.bad = 1;
-    DP.fast = ok && !any_nm && dsn >= 64u * ((uint64_t)L.nrg + 16u) && !(flags & 1u);
+    DP.fast = ok && !any_nm && !(flags & 1u);
     if (DP.fast) DP.fast = big_ds_entries(dsv, dsn, eidx, dW3, DP);
     if (DP.fast) {   // every range of every entry canonical (the whole workgroup); a failure streams instead
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the entry table before the helper waves read it
@@ -2770,16 +3006,34 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
   if (!bad) { big_bitonic(L.pc, npc); big_bitonic(L.rg, nrg); }
   const BigBlk* T = blk + s_base;
   if (bad) nb = 0;
-  if (!bad && DP.fast) big_ds_plan(dsv, dsp, eidx, DP, L.rg, nrg);
+  // emit staging in the U0 tile's LDS (free now): block-table entries, the splice's per-range words, the copy list
+  BigGrp* const G = (BigGrp*)&T0;
+  uint32_t* const dsx = (uint32_t*)((uint8_t*)&T0 + CF::SBG);
+  if (!bad && DP.fast) big_ds_plan(dsv, dsp, eidx, DP, L.rg, nrg, dsx, (uint32_t)CF::MAXD);
   DIAGL(2);
   // ---- emit: pass 0 sizes (and proves the class), pass 1 bytes.  Every lane runs the same plan.
   uint64_t nblocks = 0, ndsc = 0, size = 0;
+  const uint32_t ds0s = (uint32_t)s_ds0;
+  uint32_t ngr = 0;
+  uint64_t sbytes = 0;
+  bool par = false;                                          // the parallel struct emit (planned in pass 0)
   for (int pass = 0; pass < 2 && !bad; pass++) {
     BigOut o; o.o = out + (pass ? s_at : 0); o.n = 0; o.w = pass == 1;
-    // the copy list lives in the U0 tile's LDS past the block-table staging
-    o.cl = (BigCp*)((uint8_t*)&T0 + CF::SBN * sizeof(BigBlk)); o.nc = 0; o.pre = s_cpre;
-    o.cap = (uint32_t)((sizeof(typename CF::Tile) - CF::SBN * sizeof(BigBlk)) / sizeof(BigCp)); o.ls = o.le = o.ld = 0;
+    // the copy list lives in the U0 tile's LDS past the block-table staging / client groups and the splice words
+    o.cl = (BigCp*)(dsx + 3 * CF::MAXD); o.nc = 0; o.pre = s_cpre;
+    o.cap = (uint32_t)((sizeof(typename CF::Tile) - CF::SBG - 12 * CF::MAXD) / sizeof(BigCp)); o.ls = o.le = o.ld = 0;
     o.vu(nblocks);
+    if (pass == 0 && acanon) {
+      uint64_t nbo = 0;
+      const int pr = big_plan_structs(L, G, CF::GCAP, T, (uint32_t)nb, npc, S0, ds0s, ngr, nbo, sbytes);
+      if (pr == 1) { bad = true; break; }
+      par = pr == 0;
+      if (par) nblocks = nbo;
+    }
+    if (par) {
+      if (pass) big_write_structs(L, G, ngr, npc, u0p, arena, S0, ds0s, sbytes, o.n, o);
+      o.n += sbytes;
+    } else {
     uint64_t i = 0, nbo = 0;
     uint32_t j = 0;
     // U0 blocks no log piece touches (and whose headers are minimal) are U0's bytes [h0, b1) as
@@ -2837,14 +3091,14 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
           const bool takeu = upend && (q >= j1 || B.clock0 <= (uint32_t)L.pc[q].key);
           const uint64_t c0 = takeu ? B.clock0 : (uint32_t)L.pc[q].key;
           const uint64_t c1 = takeu ? B.clock1 : c0 + L.pc[q].len;
-          const bool fgc = takeu ? B.first_gc : L.pc[q].gc, lgc = takeu ? B.last_gc : L.pc[q].gc;
+          const bool fgc = takeu ? (bool)B.first_gc : L.pc[q].gc(), lgc = takeu ? (bool)B.last_gc : L.pc[q].gc();
           if (any) {
             if (c0 < pend || (c0 == pend && pgc && fgc)) { bad = true; break; }   // overlap / GC junction
             if (c0 > pend) { cnt++; if (sweep) { o.b(10); o.vu(c0 - pend); } }   // Skip over the gap
           } else first = c0;
           if (sweep) {
             if (takeu) o.copy(u0p + B.b0, B.b1 - B.b0);
-            else o.copy(arena + L.pc[q].src, L.pc[q].nb);
+            else o.copy(arena + L.pc[q].src, L.pc[q].nb());
           }
           cnt += takeu ? B.nst : 1u;
           any = true; pend = c1; pgc = lgc;
@@ -2857,6 +3111,8 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
       j = j1;
     }
     if (r1 > r0) o.copy(u0p + r0, r1 - r0);
+    if (pass == 0) nblocks = nbo;
+    }
     // delete set: U0's sorted stream (read through LDS tiles, forward only) merged with the sorted log
     // ranges, runs merged per client in one sweep.  Pass 0 keeps each client's run count in the struct
     // records' scratch (free after the clock-range pass) for pass 1's header.
@@ -2869,25 +3125,22 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
       // run count, then its untouched ranges' bytes as written interleaved with the merged groups' spans
       const uint8_t* const dsb = u0p + s_ds0;
       const uint32_t ne = DP.C;
-      uint32_t ew = 0xFFFFFFFFu, wcl = 0, wn = 0, wbs = 0, wbe = 0;   // entry ew + lane
       o.vu(ndsc);
-      uint32_t e = 0, r = 0;
+      uint32_t e = 0, r = 0, cur = DP.b0;                    // cur: byte start of entry e
       while (e < ne || r < nrg) {
-        if (e < ne && (ew == 0xFFFFFFFFu || e >= ew + (uint32_t)WAVE)) {
-          ew = e;
-          const uint32_t y = e + l;
-          if (y < ne) { wcl = ds_eclient(eidx, ne)[y]; wn = ds_en(eidx, ne)[y]; wbs = ds_ebs(eidx, ne)[y]; wbe = ds_ebe(eidx, ne)[y]; }
+        // U0's entries before the next log client's (big_ds_plan's lower bound) go out as one verbatim run
+        const uint32_t e2 = r < nrg ? (L.rg[r].ent & 0x7FFFFFFFu) : ne;
+        if (e < e2) {
+          const uint32_t be = r < nrg ? dsx[r] : DP.bend;
+          o.copy(dsb + cur, be - cur);
+          nc += e2 - e; e = e2; cur = be;
+          continue;
         }
-        const uint32_t el = e - ew;
-        const uint32_t cu = e < ne ? (uint32_t)__builtin_amdgcn_readlane((int)wcl, (int)el) : 0u;
-        const uint32_t cl = r < nrg ? 0xFFFFFFFFu - (uint32_t)(L.rg[r].key >> 32) : 0u;
-        const bool hu = e < ne;
-        const uint32_t bs = hu ? (uint32_t)__builtin_amdgcn_readlane((int)wbs, (int)el) : 0u;
-        const uint32_t be = hu ? (uint32_t)__builtin_amdgcn_readlane((int)wbe, (int)el) : 0u;
         nc++;
-        if (hu && (r >= nrg || cu > cl)) { o.copy(dsb + bs, be - bs); e++; continue; }   // untouched entry
-        const bool touched = hu && cu == cl;
-        const uint32_t n = touched ? (uint32_t)__builtin_amdgcn_readlane((int)wn, (int)el) : 0u;
+        const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.rg[r].key >> 32);
+        const bool touched = !(L.rg[r].ent >> 31);   // (then its entry is e)
+        uint32_t cu = 0, n = 0, bs = 0, be = 0;
+        if (touched) { cu = cl; n = dsx[CF::MAXD + r]; bs = cur; be = dsx[2 * CF::MAXD + r]; cur = be; }
         uint32_t r1 = r;
         while (r1 < nrg && (L.rg[r1].key >> 32) == (L.rg[r].key >> 32)) r1++;
         // groups of the client's log ranges (each widened by the U0 ranges it merges with): count, then write
@@ -2959,7 +3212,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
     o.flush();
     DIAGL(3 + pass);
     if (pass == 0) {
-      nblocks = nbo; ndsc = nc; size = o.n;
+      ndsc = nc; size = o.n;
       bad |= ((flags & 1u) && nc > 1) ;                       // yjs 13.5: first-seen client order -> general path
       // the header varuints were sized with 0: resize with the real counts
       size += vu_len(nblocks) - 1 + vu_len(ndsc) - 1;
@@ -3263,17 +3516,51 @@ static uint32_t resident_blocks(K kernel, int threads, uint32_t fallback) {
 }
 
 uint32_t ygm_k_lean_stage_bytes() { return (uint32_t)LN_IN; }   // input bytes the narrow lean kernel stages per document
+// doc_off / upd_len non-null: the compact input form (ygm_merge_v1_device_lens); upd_off is then unused
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
-                            uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
+                            uint32_t* defer_list, uint64_t out_cap, hipStream_t s, const uint64_t* doc_off, const uint16_t* upd_len) {
   if (n_docs == 0) return 0;
   // persistent waves: enough for full occupancy, each looping over documents d, d + G, ...
   const int n_cu = (int)device_cus();
   const char* env = getenv("YGM_LEAN_WAVES_PER_CU");
   const uint32_t wpc = env ? (uint32_t)atoi(env) : 16u;
   const uint32_t grid = n_docs < (uint32_t)n_cu * wpc ? n_docs : (uint32_t)n_cu * wpc;
-  hipLaunchKernelGGL(k_merge_lean<0>, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len, status,
-                     (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap, (const uint32_t*)nullptr, 0u);
+  if (doc_off)
+    hipLaunchKernelGGL((k_merge_lean<0, 1>), dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len,
+                       status, (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap, (const uint32_t*)nullptr, 0u, doc_off, upd_len);
+  else
+    hipLaunchKernelGGL((k_merge_lean<0, 0>), dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len,
+                       status, (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap, (const uint32_t*)nullptr, 0u,
+                       (const uint64_t*)nullptr, (const uint16_t*)nullptr);
+  return launch_rc(__func__);
+}
+// The update-offset table of the compact input form, for the documents of `list` (every document: list == nullptr):
+// a wave per document scans its lengths from its base.  An offset past the document's end is clamped to it (lengths
+// that do not add up to the document: its updates then fail to parse -- an error status, never a read outside it).
+__global__ __launch_bounds__(256) void k_build_off(const uint64_t* __restrict__ doc_off, const uint16_t* __restrict__ upd_len,
+                                                   const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ list, uint32_t n,
+                                                   uint64_t* __restrict__ upd_off) {
+  const uint32_t w = blockIdx.x * 4u + threadIdx.x / WAVE, l = threadIdx.x % WAVE;
+  if (w >= n) return;
+  const uint32_t d = list ? list[w] : w;
+  const uint32_t u0 = doc_upd[d], u1 = doc_upd[d + 1];
+  const uint64_t b0 = doc_off[d], b1 = doc_off[d + 1];
+  uint64_t carry = b0;
+  for (uint32_t c = u0; c < u1; c += WAVE) {
+    const uint32_t i = c + l;
+    const uint32_t len = i < u1 ? upd_len[i] : 0u;
+    const uint32_t inc = dpp_incl_add(len);
+    const uint64_t off = carry + inc - len;
+    if (i < u1) upd_off[i] = off < b1 ? off : b1;
+    carry += lane63(inc);
+  }
+  if (l == 0) upd_off[u1] = b1;
+}
+int ygm_k_launch_build_off(const uint64_t* doc_off, const uint16_t* upd_len, const uint32_t* doc_upd, const uint32_t* list, uint32_t n,
+                           uint64_t* upd_off, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_build_off, dim3((n + 3) / 4), dim3(256), 0, s, doc_off, upd_len, doc_upd, list, n, upd_off);
   return launch_rc(__func__);
 }
 // the wide lean kernel over the narrow one's deferred list (n_list entries); its own deferrals go to defer_list
@@ -3283,10 +3570,11 @@ int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, 
                                  void* meta, void* meta_next, uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
   if (n_list == 0) return 0;
   static std::atomic<uint32_t> cache[YGM_MAX_DEVICES];
-  const uint32_t resident = per_device(cache, [] { const char* g = getenv("YGM_WIDE_GRID"); return g ? (uint32_t)atoi(g) : resident_blocks(k_merge_lean<1>, WAVE, 2048u); });
+  const uint32_t resident = per_device(cache, [] { const char* g = getenv("YGM_WIDE_GRID"); return g ? (uint32_t)atoi(g) : resident_blocks(k_merge_lean<1, 0>, WAVE, 2048u); });
   const uint32_t grid = n_list < resident ? n_list : resident;
-  hipLaunchKernelGGL(k_merge_lean<1>, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len, status,
-                     (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap, list, n_list);
+  hipLaunchKernelGGL((k_merge_lean<1, 0>), dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len,
+                     status, (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap, list, n_list, (const uint64_t*)nullptr,
+                     (const uint16_t*)nullptr);
   return launch_rc(__func__);
 }
 

@@ -166,7 +166,7 @@ YDEV GStruct big_struct(GCur& c, uint32_t flags) {
         if (gutf8_u16(c.p + s, l) < 0) return R;
         const uint8_t* t = c.p + s;
         if (l == 9 && t[0] == 'u' && t[1] == 'n' && t[2] == 'd' && t[3] == 'e' && t[4] == 'f' && t[5] == 'i' && t[6] == 'n' && t[7] == 'e' && t[8] == 'd') continue;
-        if (json_check(t, l, nc)) return R;
+        if (json_check_t<SM_DEPTH, SM_KEYS>(t, l, nc)) return R;
       }
       R.len = n; break;
     }
@@ -179,14 +179,14 @@ YDEV GStruct big_struct(GCur& c, uint32_t flags) {
     }
     case 5: {                                                      // ContentEmbed
       uint32_t l; const uint32_t s = c.buf(l); if (c.err) return R;
-      if (gutf8_u16(c.p + s, l) < 0 || json_check(c.p + s, l, nc)) return R;
+      if (gutf8_u16(c.p + s, l) < 0 || json_check_t<SM_DEPTH, SM_KEYS>(c.p + s, l, nc)) return R;
       R.len = 1; break;
     }
     case 6: {                                                      // ContentFormat
       uint32_t l; uint32_t s = c.buf(l); if (c.err) return R;
       if (gutf8_u16(c.p + s, l) < 0) return R;
       s = c.buf(l); if (c.err) return R;
-      if (gutf8_u16(c.p + s, l) < 0 || json_check(c.p + s, l, nc)) return R;
+      if (gutf8_u16(c.p + s, l) < 0 || json_check_t<SM_DEPTH, SM_KEYS>(c.p + s, l, nc)) return R;
       R.len = 1; break;
     }
     case 7: {                                                      // ContentType
@@ -197,7 +197,7 @@ YDEV GStruct big_struct(GCur& c, uint32_t flags) {
     case 8: {                                                      // ContentAny (e.g. XmlElement attributes)
       const uint64_t n = c.vu(); if (c.err || n == 0) return R;
       Cur q{c.p, c.pos, c.end, 0, 0};
-      for (uint64_t k = 0; k < n && !q.err; k++) any_value(q, nc, flags);   // readAny + would writeAny reproduce it
+      for (uint64_t k = 0; k < n && !q.err; k++) any_value_t<SM_DEPTH, SM_KEYS>(q, nc, flags);   // readAny + would writeAny reproduce it
       if (q.err) return R;
       c.pos = q.pos;
       R.len = n; break;
@@ -212,7 +212,7 @@ YDEV GStruct big_struct(GCur& c, uint32_t flags) {
 // deeper than MAX_DEPTH (the document then goes on to the general path).  Out of line: the chain follow's
 // fallback parse only.
 YDEV_NI bool gany_skip(GCur& c, uint64_t n) {
-  uint32_t rem[MAX_DEPTH + 1]; uint8_t obj[MAX_DEPTH + 1];
+  uint32_t rem[SM_DEPTH + 1], obj[SM_DEPTH + 1];   // (deeper values: the general path)
   int d = 0; rem[0] = n > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)n; obj[0] = 0;
   while (!c.err) {
     if (rem[d] == 0) { if (d == 0) return true; d--; continue; }
@@ -227,7 +227,7 @@ YDEV_NI bool gany_skip(GCur& c, uint64_t n) {
       case 119: case 116: { uint32_t l; c.buf(l); break; }
       case 117: case 118: {
         const uint64_t k = c.vu();
-        if (c.err || d + 1 > MAX_DEPTH || k > (uint64_t)(c.end - c.pos)) return false;
+        if (c.err || d + 1 > SM_DEPTH || k > (uint64_t)(c.end - c.pos)) return false;
         d++; rem[d] = (uint32_t)k; obj[d] = tag == 118;
         break;
       }
@@ -298,13 +298,27 @@ struct BigRec { uint32_t start, end, len; };
 struct BigPiece {
   uint64_t key;                      // (~client) << 32 | clock: ascending = client descending, clock ascending
   uint64_t src;                      // arena offset of the struct's bytes
-  uint32_t len, nb;                  // clock length, byte length
-  uint32_t gc, pad;
+  uint32_t len, nbg;                 // clock length; byte length | GC << 31
+  uint32_t gi;                       // the parallel emit's plan: the piece's client group
+  uint32_t pre;                      // ... and the inclusive prefix of the pieces' output bytes (Skip + struct)
+  YDEV uint32_t nb() const { return nbg & 0x7FFFFFFFu; }
+  YDEV bool gc() const { return (nbg >> 31) != 0; }
+};
+// one client group of the parallel emit's plan (the log pieces of one client and U0's block of it, if any)
+struct BigGrp {
+  uint32_t q0, qend, uslot;          // pieces [q0, qend); the U0 block goes before piece uslot (qend: after all)
+  uint32_t hdr;                      // header bytes
+  uint32_t flags;                    // 1: U0 has a block of the client (touched), 2: its first struct GC, 4: its last
+  uint32_t nst, clock0, clock1, b0, b1;   // the U0 block: struct count, clock range, struct bytes
+  uint32_t h0ins;                    // U0 position the group goes to: its block's header (touched) or the next block's
+  uint32_t cnt, first, gapu;         // output struct count, first clock, Skip before the U0 block
+  uint32_t upos;                     // offset of the U0 block's struct bytes within the group's output
+  uint32_t rel;                      // offset of the group's output within the structs part (after the block count)
 };
 // log delete range: key as BigPiece.  The delete-set splice (big_ds_plan) annotates it against U0's entry of its client:
-// ent (entry index, BIG_NOENT: a client U0's delete set lacks), U0 ranges [a, b1) it touches (overlap or adjacency),
+// ent (the first entry at or after its client; bit 31 set: U0's delete set lacks the client), U0 ranges [a, b1) it
+// touches (overlap or adjacency),
 // its span with them [s, e), and the byte offsets (from U0's delete set start) of U0 range a and range b1
-constexpr uint32_t BIG_NOENT = 0xFFFFFFFFu;
 struct BigRange { uint64_t key; uint32_t len, ent, a, b1, s, e, pa, pb; };
 
 // U0 tile (LDS): CH positions of U0 from the tile origin (plus 64 bytes of overlap, so a block header starting

@@ -175,13 +175,17 @@ YDEV void w_struct(WinRd& r, uint32_t flags, uint8_t& kind, uint64_t& len, uint3
   if (fast) {
     out_len = r.pos - start;
     slow = r.nm != 0;  // a non-minimal varuint / parentInfo: the writer re-encodes (different length)
-    if (slow) { Out o{nullptr, 0}; Cur c{r.generic(), start, r.end, 0, 0}; SInfo si; read_struct(c, si, flags); write_struct(o, r.generic(), si, 0, 0, 0, false, flags); out_len = o.n; }
+    if (slow) {
+      Out o{nullptr, 0}; Cur c{r.generic(), start, r.end, 0, 0}; SInfo si; read_struct<true>(c, si, flags);
+      if (c.err) { r.fail(c.err); r.nm = nm0; return; }
+      write_struct(o, r.generic(), si, 0, 0, 0, false, flags); out_len = o.n;
+    }
     r.nm = nm0;
     return;
   }
   // general path (noinline validator over a generic pointer)
   Cur c{r.generic(), start, r.end, 0, 0};
-  SInfo si; read_struct(c, si, flags);
+  SInfo si; read_struct<true>(c, si, flags);
   if (c.err) { r.fail(c.err); return; }
   r.pos = c.pos;
   len = si.len; nc = si.nc;
@@ -261,7 +265,7 @@ struct UpdCount { int err; uint32_t fb, nc; };
 // The single parse pass over update i: validates every byte (yjs reads all of
 // them), writes struct records (slot from the wave counter L->nrec) and
 // delete-set ranges (L->ndel).  One non-inlined instance.
-YDEV_NI UpdCount w_parse_update(LWave* L, int i, uint32_t flags) {
+YDEV UpdCount w_parse_update(LWave* L, int i, uint32_t flags) {
   WinRd r; r.init(L->in, L->ustart[i], (uint32_t)L->ustart[i] + L->ulen[i]);
   bool fb = false, nc = false;
   uint64_t prev_client = 0, prev_end = 0; bool have_prev = false;

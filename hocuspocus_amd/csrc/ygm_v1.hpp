@@ -125,24 +125,80 @@ YDEV bool index_key(const uint8_t* k, uint32_t n, uint64_t& v) {
 // Own-property-order checks for one object level (Object.keys after obj[key]=v
 // assignments / JSON.parse): index keys ascending and first, no duplicates.
 // Duplicate detection compares 32-bit key hashes; a collision is refused as
-// NONCANON (conservative).
-struct KeyStack {
-  uint32_t h[MAX_KEYS];
-  int top;
+// NONCANON (conservative).  The nesting state is kept as small per-level arrays
+// (struct of arrays), sized by the caller: the full stack (MAX_DEPTH levels,
+// MAX_KEYS keys: the sequential kernel and host code) or the register stack of the
+// parallel tiers (SM_DEPTH levels, SM_KEYS keys: a value that needs more sends the
+// document to the sequential kernel, ST_FALLBACK).
+constexpr int SM_DEPTH = 4, SM_KEYS = 8;
+// full stack: arrays (the sequential kernel's private memory, host code)
+template <int D, int K>
+struct AnyStack {
+  uint32_t rem[D + 1], obj[D + 1], base[D + 1], seen[D + 1], hidx[D + 1];
+  uint64_t lidx[D + 1];
+  uint32_t h[K];
+  int top = 0;
+  YDEV uint32_t rget(int d) const { return rem[d]; }
+  YDEV void rset(int d, uint32_t v) { rem[d] = v; }
+  YDEV uint32_t oget(int d) const { return obj[d]; }
+  YDEV void oset(int d, uint32_t v) { obj[d] = v; }
+  YDEV void close_obj(int d) { top = (int)base[d]; }
+  YDEV void open_obj(int d) { base[d] = (uint32_t)top; seen[d] = 0; hidx[d] = 0; lidx[d] = 0; }
+  // returns 0 canonical so far, 1 noncanon
+  YDEV int key(int d, const uint8_t* k, uint32_t n) {
+    int r = 0;
+    uint64_t v;
+    if (index_key(k, n, v)) {
+      if (seen[d] || (hidx[d] && v <= lidx[d])) r = 1;
+      hidx[d] = 1; lidx[d] = v;
+    } else seen[d] = 1;
+    const uint32_t hh = str_hash(k, n);
+    for (int i = (int)base[d]; i < top; i++) if (h[i] == hh) r = 1;
+    if (top >= K) return 1;
+    h[top++] = hh;
+    return r;
+  }
 };
-struct ObjLevel { int base; bool seen_str, have_idx; uint64_t last_idx; };
-YDEV bool obj_key(KeyStack& ks, ObjLevel& lv, const uint8_t* k, uint32_t n) {  // returns false -> noncanon
-  bool ok = true;
-  uint64_t v;
-  if (index_key(k, n, v)) {
-    if (lv.seen_str || (lv.have_idx && v <= lv.last_idx)) ok = false;
-    lv.have_idx = true; lv.last_idx = v;
-  } else lv.seen_str = true;
-  const uint32_t h = str_hash(k, n);
-  for (int i = lv.base; i < ks.top; i++) if (ks.h[i] == h) ok = false;
-  if (ks.top >= MAX_KEYS) ok = false; else ks.h[ks.top++] = h;
-  return ok;
-}
+// register stack of the parallel tiers (SM_DEPTH levels, SM_KEYS keys): scalars selected by level, no private
+// memory; key() returns 2 past SM_KEYS keys (the caller fails with ST_FALLBACK)
+template <>
+struct AnyStack<SM_DEPTH, SM_KEYS> {
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+  uint64_t meta = 0;                      // per level 8 bits: 1 object, 2 string key seen, 4 index key seen, base << 4
+  uint64_t l0 = 0, l1 = 0, l2 = 0, l3 = 0, l4 = 0;
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0, h6 = 0, h7 = 0;
+  int top = 0;
+  YDEV uint32_t rget(int d) const { return d == 0 ? r0 : d == 1 ? r1 : d == 2 ? r2 : d == 3 ? r3 : r4; }
+  YDEV void rset(int d, uint32_t v) { r0 = d == 0 ? v : r0; r1 = d == 1 ? v : r1; r2 = d == 2 ? v : r2; r3 = d == 3 ? v : r3; r4 = d == 4 ? v : r4; }
+  YDEV uint32_t mget(int d) const { return (uint32_t)(meta >> (8 * d)) & 0xFFu; }
+  YDEV void mset(int d, uint32_t v) { meta = (meta & ~(0xFFull << (8 * d))) | ((uint64_t)(v & 0xFFu) << (8 * d)); }
+  YDEV uint32_t oget(int d) const { return mget(d) & 1u; }
+  YDEV void oset(int d, uint32_t v) { mset(d, (mget(d) & ~1u) | (v ? 1u : 0u)); }
+  YDEV uint64_t lget(int d) const { return d == 0 ? l0 : d == 1 ? l1 : d == 2 ? l2 : d == 3 ? l3 : l4; }
+  YDEV void lset(int d, uint64_t v) { l0 = d == 0 ? v : l0; l1 = d == 1 ? v : l1; l2 = d == 2 ? v : l2; l3 = d == 3 ? v : l3; l4 = d == 4 ? v : l4; }
+  YDEV void close_obj(int d) { top = (int)(mget(d) >> 4); }
+  YDEV void open_obj(int d) { mset(d, (mget(d) & 1u) | ((uint32_t)top << 4)); lset(d, 0); }
+  YDEV int key(int d, const uint8_t* k, uint32_t n) {
+    int r = 0;
+    uint64_t v;
+    uint32_t m = mget(d);
+    if (index_key(k, n, v)) {
+      if ((m & 2u) || ((m & 4u) && v <= lget(d))) r = 1;
+      m |= 4u; lset(d, v);
+    } else m |= 2u;
+    mset(d, m);
+    const uint32_t hh = str_hash(k, n);
+    const int b = (int)(m >> 4);
+    const uint32_t hs[8] = {h0, h1, h2, h3, h4, h5, h6, h7};
+#pragma unroll
+    for (int i = 0; i < 8; i++) if (i >= b && i < top && hs[i] == hh) r = 1;
+    if (top >= SM_KEYS) return 2;
+    h0 = top == 0 ? hh : h0; h1 = top == 1 ? hh : h1; h2 = top == 2 ? hh : h2; h3 = top == 3 ? hh : h3;
+    h4 = top == 4 ? hh : h4; h5 = top == 5 ? hh : h5; h6 = top == 6 ? hh : h6; h7 = top == 7 ? hh : h7;
+    top++;
+    return r;
+  }
+};
 
 YDEV float be_f32(const uint8_t* q) { uint32_t u = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3]; return __uint_as_float(u); }
 YDEV double be_f64(const uint8_t* q) { uint64_t u = 0; for (int i = 0; i < 8; i++) u = (u << 8) | q[i]; return __longlong_as_double((long long)u); }
@@ -156,23 +212,24 @@ YDEV bool js_small_int(double x, uint32_t flags) {
 // ---------------------------------------------------------------- Any
 // Validates one Any value starting at c.pos (lib0 readAny, L0@4074); *nc set
 // when writeAny (L0@8284-8700) would not reproduce the bytes.
-YDEV_NI void any_value(Cur& c, bool& nc, uint32_t flags) {
+template <int D, int K>
+YDEV_NI void any_value_t(Cur& c, bool& nc, uint32_t flags) {
   // explicit stack: remaining elements per level; objects alternate key/value
-  struct Lvl { uint32_t rem; uint8_t obj; ObjLevel o; };
-  Lvl st[MAX_DEPTH + 1];
-  KeyStack ks; ks.top = 0;
+  AnyStack<D, K> st;
   int d = 0;
   const int nm0 = c.nm; c.nm = 0;
-  st[0].rem = 1; st[0].obj = 0;
+  st.rset(0, 1); st.oset(0, 0);
   while (!c.err) {
-    if (st[d].rem == 0) { if (d == 0) break; if (st[d].obj) ks.top = st[d].o.base; d--; continue; }
-    st[d].rem--;
-    if (st[d].obj) {  // key
+    if (st.rget(d) == 0) { if (d == 0) break; if (st.oget(d)) st.close_obj(d); d--; continue; }
+    st.rset(d, st.rget(d) - 1u);
+    if (st.oget(d)) {  // key
       uint32_t kl; const uint32_t ks0 = c.buf(kl);
       if (c.err) break;
       if (utf8_u16(c.p + ks0, kl) < 0) { c.fail(ST_MALFORMED); break; }
       if (kl == 9) { const uint8_t* k = c.p + ks0; if (k[0] == '_' && k[1] == '_' && k[2] == 'p' && k[3] == 'r' && k[4] == 'o' && k[5] == 't' && k[6] == 'o' && k[7] == '_' && k[8] == '_') nc = true; }
-      if (!obj_key(ks, st[d].o, c.p + ks0, kl)) nc = true;
+      const int kr = st.key(d, c.p + ks0, kl);
+      if (kr == 2) { c.fail(ST_FALLBACK); break; }
+      if (kr) nc = true;
     }
     const uint8_t tag = c.u8();
     if (c.err) break;
@@ -212,11 +269,11 @@ YDEV_NI void any_value(Cur& c, bool& nc, uint32_t flags) {
       case 117: case 118: {
         const uint64_t n = c.vu();
         if (c.err) break;
-        if (d + 1 > MAX_DEPTH) { c.fail(ST_DEPTH); break; }
+        if (d + 1 > D) { c.fail(D == MAX_DEPTH ? ST_DEPTH : ST_FALLBACK); break; }
         if (n > (uint64_t)(c.end - c.pos)) { c.fail(ST_MALFORMED); break; }  // every element takes >= 1 byte
         d++;
-        st[d].rem = (uint32_t)n; st[d].obj = tag == 118;
-        if (tag == 118) { st[d].o.base = ks.top; st[d].o.seen_str = false; st[d].o.have_idx = false; st[d].o.last_idx = 0; }
+        st.rset(d, (uint32_t)n); st.oset(d, tag == 118);
+        if (tag == 118) st.open_obj(d);
         break;
       }
       default: c.fail(ST_MALFORMED); break;  // readAnyLookupTable miss -> TypeError
@@ -225,6 +282,7 @@ YDEV_NI void any_value(Cur& c, bool& nc, uint32_t flags) {
   if (c.nm) nc = true;  // a non-minimal varuint inside the value is re-encoded by writeAny
   c.nm = nm0;
 }
+YDEV void any_value(Cur& c, bool& nc, uint32_t flags) { any_value_t<MAX_DEPTH, MAX_KEYS>(c, nc, flags); }
 // skips one Any value already validated (used to re-walk Any arrays when slicing)
 YDEV_NI void any_skip(Cur& c) {
   uint32_t rem[MAX_DEPTH + 1]; uint8_t obj[MAX_DEPTH + 1];
@@ -338,51 +396,53 @@ YDEV_NI int64_t json_number(const uint8_t* s, uint32_t n, uint32_t i, bool& nc) 
   if (sig > 15) nc = true;
   return i;
 }
-YDEV_NI int json_check(const uint8_t* s, uint32_t n, bool& nc) {
-  struct JL { uint8_t obj; uint8_t state; ObjLevel o; };  // state: 0 expect value/first, 1 after value
-  JL st[MAX_DEPTH + 1];
-  KeyStack ks; ks.top = 0;
+template <int D, int K>
+YDEV_NI int json_check_t(const uint8_t* s, uint32_t n, bool& nc) {
+  // per level: obj (0 array, 1 object, 2 top), state (0 expect value/first, 1 after value, 2 after comma)
+  AnyStack<D, K> st;   // (rem holds the state; the top level is d == 0)
   int d = 0;
   uint32_t i = 0;
   // top level: expect exactly one value
-  st[0].obj = 2; st[0].state = 0;
+  st.oset(0, 0); st.rset(0, 0);
   for (;;) {
     while (i < n && jws(s[i])) { i++; nc = true; }
-    JL& L = st[d];
-    if (L.obj == 2 && L.state == 1) { if (i != n) return ST_MALFORMED; return ST_OK; }
-    if (L.state == 1) {  // after a value inside a container
+    const uint32_t lo = d == 0 ? 2u : st.oget(d), ls = st.rget(d);
+    if (lo == 2 && ls == 1) { if (i != n) return ST_MALFORMED; return ST_OK; }
+    if (ls == 1) {  // after a value inside a container
       if (i >= n) return ST_MALFORMED;
-      if (s[i] == ',') { i++; L.state = 2; continue; }
-      if ((L.obj == 1 && s[i] == '}') || (L.obj == 0 && s[i] == ']')) {
+      if (s[i] == ',') { i++; st.rset(d, 2); continue; }
+      if ((lo == 1 && s[i] == '}') || (lo == 0 && s[i] == ']')) {
         i++;
-        if (L.obj == 1) ks.top = L.o.base;
-        d--; st[d].state = 1; continue;
+        if (lo == 1) st.close_obj(d);
+        d--; st.rset(d, 1); continue;
       }
       return ST_MALFORMED;
     }
     if (i >= n) return ST_MALFORMED;
     // state 0 (first element or top) or 2 (after comma)
-    if (L.obj == 1) {
-      if (L.state == 0 && s[i] == '}') { i++; ks.top = L.o.base; d--; st[d].state = 1; continue; }
+    if (lo == 1) {
+      if (ls == 0 && s[i] == '}') { i++; st.close_obj(d); d--; st.rset(d, 1); continue; }
       if (s[i] != '"') return ST_MALFORMED;
       bool esc; const int64_t e = json_string(s, n, i, nc, esc);
       if (e < 0) return ST_MALFORMED;
       if (esc) nc = true;
-      if (!obj_key(ks, L.o, s + i + 1, (uint32_t)(e - i - 2))) nc = true;
+      const int kr = st.key(d, s + i + 1, (uint32_t)(e - i - 2));
+      if (kr == 2) return ST_FALLBACK;
+      if (kr) nc = true;
       i = (uint32_t)e;
       while (i < n && jws(s[i])) { i++; nc = true; }
       if (i >= n || s[i] != ':') return ST_MALFORMED;
       i++;
       while (i < n && jws(s[i])) { i++; nc = true; }
       if (i >= n) return ST_MALFORMED;
-    } else if (L.obj == 0 && L.state == 0 && s[i] == ']') { i++; d--; st[d].state = 1; continue; }
+    } else if (lo == 0 && ls == 0 && s[i] == ']') { i++; d--; st.rset(d, 1); continue; }
     // a value
     const uint8_t ch = s[i];
     if (ch == '{' || ch == '[') {
-      if (d + 1 > MAX_DEPTH) return ST_DEPTH;
-      L.state = 1;  // parent resumes after this container
-      d++; st[d].obj = ch == '{'; st[d].state = 0;
-      if (ch == '{') { st[d].o.base = ks.top; st[d].o.seen_str = false; st[d].o.have_idx = false; st[d].o.last_idx = 0; }
+      if (d + 1 > D) return D == MAX_DEPTH ? ST_DEPTH : ST_FALLBACK;
+      st.rset(d, 1);  // parent resumes after this container
+      d++; st.oset(d, ch == '{'); st.rset(d, 0);
+      if (ch == '{') st.open_obj(d);
       i++;
       continue;
     }
@@ -395,9 +455,10 @@ YDEV_NI int json_check(const uint8_t* s, uint32_t n, bool& nc) {
     else e = -1;
     if (e < 0) return ST_MALFORMED;
     i = (uint32_t)e;
-    L.state = 1;
+    st.rset(d, 1);
   }
 }
+YDEV int json_check(const uint8_t* s, uint32_t n, bool& nc) { return json_check_t<MAX_DEPTH, MAX_KEYS>(s, n, nc); }
 
 // ---------------------------------------------------------------- structs
 // One parsed struct (lazyStructReaderGenerator, Y@36564).
@@ -411,8 +472,11 @@ struct SInfo {
   uint32_t end;      // position after the struct
 };
 
-// readItemContent (Y@81141) validation; returns length in clock units.
+// readItemContent (Y@81141) validation; returns length in clock units.  SM: the parallel tiers' register stacks for
+// Any / JSON nesting (a value past SM_DEPTH levels or SM_KEYS open keys fails the cursor with ST_FALLBACK)
+template <bool SM = false>
 YDEV_NI uint64_t read_content(Cur& c, uint8_t ref, bool& nc, uint32_t flags) {
+  constexpr int D = SM ? SM_DEPTH : MAX_DEPTH, K = SM ? SM_KEYS : MAX_KEYS;
   switch (ref) {
     case 1: return c.vu();                                           // ContentDeleted
     case 2: {                                                        // ContentJSON
@@ -422,7 +486,7 @@ YDEV_NI uint64_t read_content(Cur& c, uint8_t ref, bool& nc, uint32_t flags) {
         if (utf8_u16(c.p + s, l) < 0) { c.fail(ST_MALFORMED); break; }
         const uint8_t* t = c.p + s;
         if (l == 9 && t[0] == 'u' && t[1] == 'n' && t[2] == 'd' && t[3] == 'e' && t[4] == 'f' && t[5] == 'i' && t[6] == 'n' && t[7] == 'e' && t[8] == 'd') continue;
-        const int e = json_check(t, l, nc); if (e) { c.fail(e); break; }
+        const int e = json_check_t<D, K>(t, l, nc); if (e) { c.fail(e); break; }
       }
       return n;
     }
@@ -436,7 +500,7 @@ YDEV_NI uint64_t read_content(Cur& c, uint8_t ref, bool& nc, uint32_t flags) {
     case 5: {                                                        // ContentEmbed
       uint32_t l; const uint32_t s = c.buf(l); if (c.err) return 1;
       if (utf8_u16(c.p + s, l) < 0) { c.fail(ST_MALFORMED); return 1; }
-      const int e = json_check(c.p + s, l, nc); if (e) c.fail(e);
+      const int e = json_check_t<D, K>(c.p + s, l, nc); if (e) c.fail(e);
       return 1;
     }
     case 6: {                                                        // ContentFormat
@@ -444,7 +508,7 @@ YDEV_NI uint64_t read_content(Cur& c, uint8_t ref, bool& nc, uint32_t flags) {
       if (utf8_u16(c.p + s, l) < 0) { c.fail(ST_MALFORMED); return 1; }
       s = c.buf(l); if (c.err) return 1;
       if (utf8_u16(c.p + s, l) < 0) { c.fail(ST_MALFORMED); return 1; }
-      const int e = json_check(c.p + s, l, nc); if (e) c.fail(e);
+      const int e = json_check_t<D, K>(c.p + s, l, nc); if (e) c.fail(e);
       return 1;
     }
     case 7: {                                                        // ContentType
@@ -455,14 +519,14 @@ YDEV_NI uint64_t read_content(Cur& c, uint8_t ref, bool& nc, uint32_t flags) {
     }
     case 8: {                                                        // ContentAny
       const uint64_t n = c.vu();
-      for (uint64_t k = 0; k < n && !c.err; k++) any_value(c, nc, flags);
+      for (uint64_t k = 0; k < n && !c.err; k++) any_value_t<D, K>(c, nc, flags);
       return n;
     }
     case 9: {                                                        // ContentDoc (Y@70773)
       uint32_t l; const uint32_t s = c.buf(l); if (c.err) return 1;
       if (utf8_u16(c.p + s, l) < 0) { c.fail(ST_MALFORMED); return 1; }
       const uint32_t o0 = c.pos;
-      bool anc = false; any_value(c, anc, flags);
+      bool anc = false; any_value_t<D, K>(c, anc, flags);
       if (c.err) return 1;
       if (anc) nc = true;
       // canonical iff an object whose keys are an ordered subset of gc:false, autoLoad:true, meta:<non-null>
@@ -472,7 +536,7 @@ YDEV_NI uint64_t read_content(Cur& c, uint8_t ref, bool& nc, uint32_t flags) {
       for (uint64_t k = 0; k < nk && !q.err; k++) {
         uint32_t kl; const uint32_t ks = q.buf(kl);
         const uint8_t* key = q.p + ks; const uint8_t vt = q.p[q.pos];
-        bool vnc = false; any_value(q, vnc, flags);
+        bool vnc = false; any_value_t<D, K>(q, vnc, flags);
         if (kl == 2 && key[0] == 'g' && key[1] == 'c' && stage < 1 && vt == 121) stage = 1;
         else if (kl == 8 && key[0] == 'a' && key[1] == 'u' && key[2] == 't' && key[3] == 'o' && key[4] == 'L' && key[5] == 'o' && key[6] == 'a' && key[7] == 'd' && stage < 2 && vt == 120) stage = 2;
         else if (kl == 4 && key[0] == 'm' && key[1] == 'e' && key[2] == 't' && key[3] == 'a' && stage < 3 && vt != 126 && vt != 127 && !vnc) stage = 3;
@@ -486,6 +550,7 @@ YDEV_NI uint64_t read_content(Cur& c, uint8_t ref, bool& nc, uint32_t flags) {
 
 // Parses the struct at c.pos.  Header varuints are re-encoded on output, so
 // only content varuints count toward `nc`.
+template <bool SM = false>
 YDEV_NI void read_struct(Cur& c, SInfo& s, uint32_t flags) {
   s.start = c.pos; s.nc = false; s.renc = false; s.ref = 0;
   const uint8_t info = c.u8();
@@ -507,7 +572,7 @@ YDEV_NI void read_struct(Cur& c, SInfo& s, uint32_t flags) {
   if (s.ref == 10) { c.fail(ST_MALFORMED); return; }
   const int nm0 = c.nm; c.nm = 0;
   bool nc = false;
-  s.len = read_content(c, s.ref, nc, flags);
+  s.len = read_content<SM>(c, s.ref, nc, flags);
   if (c.nm) s.renc = true;  // Any values track their own non-minimal varuints (-> nc)
   c.nm = nm0;
   s.nc = nc;
@@ -518,6 +583,7 @@ YDEV_NI void read_struct(Cur& c, SInfo& s, uint32_t flags) {
 // and ContentDeleted / ContentString) are read inline with exactly read_struct's reads and results; anything else
 // goes to read_struct through a copy of the cursor (a cursor whose address reaches a non-inlined call lives in
 // scratch memory for the whole function: one scratch round trip per byte read).
+template <bool SM = false>
 YDEV void read_struct_fast(Cur& c, SInfo& s, uint32_t flags) {
   const uint32_t p0 = c.pos;
   if (c.pos < c.end) {
@@ -555,7 +621,7 @@ YDEV void read_struct_fast(Cur& c, SInfo& s, uint32_t flags) {
     }
   }
   Cur t = c;
-  read_struct(t, s, flags);
+  read_struct<SM>(t, s, flags);
   c = t;
 }
 

@@ -68,7 +68,8 @@ EXPORTS = ("ygm_open", "ygm_close", "ygm_merge_v1", "ygm_diff_v1", "ygm_sv_from_
            "ygm_contains_v1", "ygm_contains_v1_device", "ygm_stats", "ygm_strerror", "ygm_version",
            "ygm_merge_v2", "ygm_diff_v2", "ygm_sv_from_update_v2", "ygm_convert_v1_to_v2", "ygm_convert_v2_to_v1",
            "ygm_merge_v2_device", "ygm_diff_v2_device", "ygm_sv_from_update_v2_device", "ygm_convert_v1_to_v2_device",
-           "ygm_convert_v2_to_v1_device", "ygm_sync_step2_v1", "ygm_sync_step2_v1_device")
+           "ygm_convert_v2_to_v1_device", "ygm_sync_step2_v1", "ygm_sync_step2_v1_device",
+           "ygm_merge_v1_device_lens", "ygm_merge_v1_device_lens_async")
 
 
 def lib():
@@ -95,6 +96,8 @@ def lib():
         L.ygm_merge_v1_device.argtypes = [vp, vp, u64, vp, vp, u32, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_merge_v1_device_async.argtypes = [vp, vp, u64, vp, vp, u32, u32, vp]
         L.ygm_merge_v1_device_finish.argtypes = [vp, ctypes.POINTER(_DevResult)]
+        L.ygm_merge_v1_device_lens.argtypes = [vp, vp, u64, vp, vp, vp, u32, u32, vp, ctypes.POINTER(_DevResult)]
+        L.ygm_merge_v1_device_lens_async.argtypes = [vp, vp, u64, vp, vp, vp, u32, u32, vp]
         L.ygm_diff_v1_device.argtypes = [vp, vp, u64, vp, vp, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_sv_from_update_v1_device.argtypes = [vp, vp, u64, vp, u32, vp, ctypes.POINTER(_DevResult)]
         L.ygm_snapshot_v1.argtypes = [vp, vp, vp, u32, ctypes.POINTER(_Result)]
@@ -121,7 +124,7 @@ def lib():
                   "ygm_contains_v1", "ygm_contains_v1_device", "ygm_stats", "ygm_merge_v2", "ygm_diff_v2", "ygm_sv_from_update_v2",
                   "ygm_convert_v1_to_v2", "ygm_convert_v2_to_v1", "ygm_merge_v2_device", "ygm_diff_v2_device",
                   "ygm_sv_from_update_v2_device", "ygm_convert_v1_to_v2_device", "ygm_convert_v2_to_v1_device",
-                  "ygm_sync_step2_v1", "ygm_sync_step2_v1_device"):
+                  "ygm_sync_step2_v1", "ygm_sync_step2_v1_device", "ygm_merge_v1_device_lens", "ygm_merge_v1_device_lens_async"):
             getattr(L, f).restype = i32
         _lib = L
     return _lib
@@ -437,6 +440,23 @@ class Engine:
         """Enqueues a device-resident batch merge without waiting (ygm_merge_v1_device_async)."""
         st = lib().ygm_merge_v1_device_async(self._ctx, _dptr(d_arena, arena_bytes + TAIL_PAD), arena_bytes, _dptr(d_upd_off),
                                              _dptr(d_doc_upd), n_upd, n_docs, stream or None)
+        if st != OK:
+            raise YjsError(st)
+
+    def merge_device_lens(self, d_arena: int, arena_bytes: int, d_doc_off: int, d_upd_len: int, d_doc_upd: int, n_upd: int,
+                          n_docs: int, stream: int = 0) -> DeviceResult:
+        """The compact input form (ygm_merge_v1_device_lens): u64 offset per document, u16 length per update."""
+        r = _DevResult()
+        st = lib().ygm_merge_v1_device_lens(self._ctx, _dptr(d_arena, arena_bytes + TAIL_PAD), arena_bytes, _dptr(d_doc_off),
+                                            _dptr(d_upd_len), _dptr(d_doc_upd), n_upd, n_docs, stream or None, ctypes.byref(r))
+        if st != OK:
+            raise YjsError(st)
+        return DeviceResult(r.data, r.off, r.len, r.status, r.data_bytes, r.payload_bytes)
+
+    def merge_device_lens_async(self, d_arena: int, arena_bytes: int, d_doc_off: int, d_upd_len: int, d_doc_upd: int, n_upd: int,
+                                n_docs: int, stream: int = 0) -> None:
+        st = lib().ygm_merge_v1_device_lens_async(self._ctx, _dptr(d_arena, arena_bytes + TAIL_PAD), arena_bytes, _dptr(d_doc_off),
+                                                  _dptr(d_upd_len), _dptr(d_doc_upd), n_upd, n_docs, stream or None)
         if st != OK:
             raise YjsError(st)
 

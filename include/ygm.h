@@ -195,6 +195,20 @@ int ygm_merge_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_byt
 int ygm_merge_v1_device_async(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_upd_off,
                               const uint32_t *d_doc_upd, uint32_t n_upd, uint32_t n_docs, void *stream);
 int ygm_merge_v1_device_finish(ygm_ctx *ctx, ygm_device_result *out);
+/* Compact input form of ygm_merge_v1_device(_async): the documents' updates are contiguous in the arena, so
+ * d_doc_off[d] (u64, n_docs + 1 entries) is the byte offset of document d's first update, d_doc_off[n_docs] the
+ * end of the last, and d_upd_len[i] (u16, n_upd entries) the byte length of update i (every update < 64 KiB; a
+ * batch with a larger one takes the u64 form).  2 bytes per update instead of 8 -- for a log of one-character
+ * inserts the table is a third of the input bytes -- and no u64 table at all unless a document leaves the lean
+ * kernel (the context then builds its entries on the device).  Lengths that do not add up to the document's bytes
+ * give that document an error status.  Results, finish and reuse as ygm_merge_v1_device(_async).
+ * (Replaces no single reference interface: the batched form of Y.mergeUpdates, yjs Y@37704.) */
+int ygm_merge_v1_device_lens(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
+                             const uint16_t *d_upd_len, const uint32_t *d_doc_upd, uint32_t n_upd, uint32_t n_docs, void *stream,
+                             ygm_device_result *out);
+int ygm_merge_v1_device_lens_async(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
+                                   const uint16_t *d_upd_len, const uint32_t *d_doc_upd, uint32_t n_upd, uint32_t n_docs,
+                                   void *stream);
 int ygm_diff_v1_device(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
                        const uint8_t *d_sv_arena, const uint64_t *d_sv_off, uint32_t n_docs, void *stream,
                        ygm_device_result *out);

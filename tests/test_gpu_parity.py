@@ -437,6 +437,50 @@ def test_async_device_api_matches_host_api(eng):
     assert r.payload_bytes == sum(len(h[1]) for h in host if h[0] == 0)
 
 
+def test_compact_lens_device_api_matches_host_api(eng):
+    # ygm_merge_v1_device_lens (u64 per document, u16 length per update) == the host API on a batch that needs every
+    # tier (the deferred documents' offsets are built on the device), and a document whose lengths do not add up to
+    # its bytes gets an error status
+    import torch
+    import bench
+    from tools import synth
+    arena, upd_off, doc_upd = synth.text_updates(400, 120, seed=32, del_pct=10)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(400)]
+    rng = random.Random(6)
+    for d in range(0, 400, 7):
+        docs[d] = docs[d] + rng.sample(docs[d], 2)          # duplicates: the sequential tier
+    docs += _lean_edge_docs(100, seed=78)
+    ba, bo, bd = synth.big_docs(3, 60000, 1024, max_clients=16, max_k=40, seed=7)   # the large-document tier
+    bu = synth.split(ba, bo)
+    docs += [bu[bd[d]:bd[d + 1]] for d in range(3)]
+    blobs = [u for us in docs for u in us]
+    assert max(len(b) for b in blobs) < 65536
+    a = np.frombuffer(b"".join(blobs) + bytes(64), np.uint8)
+    lens = np.array([len(b) for b in blobs], np.uint16)
+    du = np.cumsum([0] + [len(us) for us in docs]).astype(np.uint32)
+    doff = np.cumsum([0] + [sum(len(u) for u in us) for us in docs]).astype(np.uint64)
+    bad = 5
+    lens_bad = lens.copy(); lens_bad[du[bad]] += 3                        # document 5: lengths past its bytes
+    dev = torch.device("cuda", 0)
+    ta, to, tl, td = (torch.from_numpy(x.copy()).to(dev) for x in (a, doff.view(np.int64), lens_bad.view(np.int16), du.view(np.int32)))
+    n = len(docs)
+    host = eng.merge_updates_batch(docs)
+    for _ in range(2):   # the second call reuses the context's buffers
+        r = eng.merge_device_lens(ta.data_ptr(), len(a) - 64, to.data_ptr(), tl.data_ptr(), td.data_ptr(), len(blobs), n)
+        torch.cuda.synchronize()
+        offs = bench._d2h(r.off, n * 8).view(np.uint64)
+        ln = bench._d2h(r.len, n * 8).view(np.uint64)
+        sts = bench._d2h(r.status, n * 4).view(np.int32)
+        data = bench._d2h(r.data, int(r.data_bytes)).tobytes()
+        for d in range(n):
+            got = (int(sts[d]), data[int(offs[d]):int(offs[d]) + int(ln[d])] if sts[d] == 0 else None)
+            if d == bad:
+                assert got[0] != 0
+            else:
+                assert got[0] == host[d][0] and (got[0] != 0 or got[1] == host[d][1]), d
+
+
 def test_lean_sv_diff_edge_states_vs_oracle(eng):
     # merged states with every struct shape of the lean-edge corpus (long strings, non-ASCII, deleted
     # content, parents, 5-byte clients, large clocks, multi-struct blocks), diffed against random state

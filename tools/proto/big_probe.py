@@ -5,7 +5,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 diag = len(sys.argv) > 1 and sys.argv[1] in ("diag", "diagds", "splice", "occ")
-dsmode = len(sys.argv) > 1 and sys.argv[1] == "diagds"
+dsmode = len(sys.argv) > 1 and (sys.argv[1] == "diagds" or (sys.argv[1] == "occ" and os.environ.get("OCC_DS") == "1"))
 import hocuspocus_amd.engine as eng
 if diag:
     eng.LIB_PATH = os.path.join(ROOT, "hocuspocus_amd", "exp/libygm_diagds.so" if dsmode else "libygm_diag.so")
@@ -33,6 +33,10 @@ if len(sys.argv) > 1 and sys.argv[1] == "occ":   # C3-full-shaped batch (top ran
     span = (en.max() - st.min()) / 100.0   # us
     busy = (en - st).sum() / 100.0
     ph = np.diff(tt[:, :6], axis=1).sum(axis=0) / 100.0
+    if dsmode:   # slots 6 / 7: the delete-set part's start in each pass
+        ds = {"pass0 structs": (tt[:, 6] - tt[:, 3]).sum() / 100.0, "pass0 ds": (tt[:, 4] - tt[:, 6]).sum() / 100.0,
+              "pass1 structs": (tt[:, 7] - tt[:, 4]).sum() / 100.0, "pass1 ds": (tt[:, 5] - tt[:, 7]).sum() / 100.0}
+        print({"ds_split_us": ds}, flush=True)
     sizes = np.diff(upd_off[doc_upd].astype(np.int64))
     print({"docs": n, "bytes": int(upd_off[-1]), "kernel_ms": round(s1.kernel_ms - s0.kernel_ms, 2), "docs_big": int(nb),
            "wg_stamped": int(ok.sum()), "span_us": round(span, 1), "busy_wg_us": round(busy, 1), "mean_concurrency": round(busy / span, 1),

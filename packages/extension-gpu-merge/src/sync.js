@@ -72,13 +72,15 @@ class SyncResponder {
    * @param {{ engine: any, getState: (documentName: string) => Promise<Uint8Array | Uint8Array[] | null> }} opts
    *   engine: GpuEngine or GpuEnginePool; getState: the document's stored update, or [snapshot, ...log]
    */
-  constructor ({ engine, getState }) {
+  constructor ({ engine, getState, Y = null }) {
     this.engine = engine; this.getState = getState
+    this.Y = Y   // yjs, for the read-only answer of a document outside the snapshot envelope (loaded lazily)
     /** Step1 replies sent as diffUpdate(state, sv) because the state is outside the snapshot envelope */
     this.unnormalized = []
   }
 
   _pooled () { return typeof this.engine.shardOf === 'function' }
+  _Y () { if (!this.Y) this.Y = require('yjs'); return this.Y }
   _merge (names, docs) { return this._pooled() ? this.engine.mergeMany(names, docs) : this.engine.mergeMany(docs) }
   _diff (names, states, svs) { return this._pooled() ? this.engine.diffMany(names, states, svs) : this.engine.diffMany(states, svs) }
   _step2 (names, states, svs) { return this._pooled() ? this.engine.step2Many(names, states, svs) : this.engine.step2Many(states, svs) }
@@ -153,6 +155,35 @@ class SyncResponder {
   }
 }
 
+// yjs 13.6 snapshotContainsUpdate(snapshot, update) for a yjs that does not export it (13.5): every struct of the
+// update (Skips included: the lazy reader does not filter them) inside the snapshot's state vector -- parseUpdateMeta's
+// per-client end clocks -- and the snapshot's delete set unchanged by merging the update's in (mergeDeleteSets +
+// sortAndMergeDeleteSet: ranges sorted by clock, a range that reaches the next one's clock absorbs it; then
+// equalDeleteSets).  The update's delete set: diffUpdate against its own state vector leaves only it.
+function snapshotContains (Y, snap, update) {
+  for (const [client, clock] of Y.parseUpdateMeta(update).to) if ((snap.sv.get(client) || 0) < clock) return false
+  const r = new Reader(Y.diffUpdate(update, Y.encodeStateVectorFromUpdate(update)))
+  if (r.varUint() !== 0) return false
+  const ds = new Map()
+  for (let c = r.varUint(); c > 0; c--) {
+    const client = r.varUint(); const items = ds.get(client) || []
+    for (let n = r.varUint(); n > 0; n--) items.push({ clock: r.varUint(), len: r.varUint() })
+    ds.set(client, items)
+  }
+  for (const [client, items] of ds) {
+    const base = snap.ds.clients.get(client) || []
+    const all = base.concat(items).map(d => ({ clock: d.clock, len: d.len })).sort((x, y) => x.clock - y.clock)
+    const runs = []
+    for (const d of all) {
+      const last = runs[runs.length - 1]
+      if (last && last.clock + last.len >= d.clock) last.len = Math.max(last.len, d.clock + d.len - last.clock)
+      else runs.push(d)
+    }
+    if (runs.length !== base.length || runs.some((r, i) => r.clock !== base[i].clock || r.len !== base[i].len)) return false
+  }
+  return true
+}
+
 // [varString(documentName) varUint(SyncStatus = 8) varUint(saved ? 1 : 0)] (OutgoingMessage.ts:128-135)
 function syncStatusFrame (documentName, saved) {
   const name = Buffer.from(documentName, 'utf8')
@@ -188,18 +219,27 @@ SyncResponder.prototype.answerReadOnlyMany = async function (messages) {
     ? await (this._pooled() ? this.engine.snapshotMany(ok.map(k => names[k]), ok.map(k => merged[k])) : this.engine.snapshotMany(ok.map(k => merged[k])))
     : []
   ok.forEach((k, j) => snapOf.set(names[k], snaps[j]))
-  // a state outside the snapshot kernel's envelope (pending structs or delete set, sub-documents:
-  // EUNSUPPORTED) still gets a SyncStatus, as the reference always sends one (MessageReceiver.ts:157-179):
-  // SyncStatus(false) -- "not known to be contained", the conservative answer, under which the
-  // provider keeps reporting unsynced changes rather than dropping them
+  // a state outside the snapshot kernel's envelope (pending structs or delete set, sub-documents: EUNSUPPORTED,
+  // a per-document refusal) is answered as the reference does (MessageReceiver.ts:157-179) on the host: the
+  // document loaded from the merged state, Y.snapshotContainsUpdate(Y.snapshot(doc), update) (yjs 13.6; with a
+  // yjs that lacks it, the same algorithm over Y.decodeUpdate: snapshotContains below)
   const unsup = a => { const s = snapOf.get(a.documentName); return s instanceof Error && s.code === 'EUNSUPPORTED' }
-  asks.filter(unsup).forEach(a => { out[a.i] = syncStatusFrame(a.documentName, false) })
+  const mergedOf = new Map(names.map((n, k) => [n, merged[k]]))
+  for (const a of asks.filter(unsup)) {
+    const Y = this._Y()
+    const doc = new Y.Doc()
+    Y.applyUpdate(doc, mergedOf.get(a.documentName))
+    const snap = Y.snapshot(doc)
+    const yes = typeof Y.snapshotContainsUpdate === 'function' ? Y.snapshotContainsUpdate(snap, a.payload) : snapshotContains(Y, snap, a.payload)
+    out[a.i] = syncStatusFrame(a.documentName, yes)
+  }
+  const stateOf = a => snapOf.get(a.documentName)
   const live = asks.filter(a => !(snapOf.get(a.documentName) instanceof Error))
   asks.filter(a => snapOf.get(a.documentName) instanceof Error && !unsup(a)).forEach(a => { out[a.i] = snapOf.get(a.documentName) })
   if (!live.length) return out
   const res = await (this._pooled()
-    ? this.engine.containsMany(live.map(a => a.documentName), live.map(a => snapOf.get(a.documentName)), live.map(a => a.payload))
-    : this.engine.containsMany(live.map(a => snapOf.get(a.documentName)), live.map(a => a.payload)))
+    ? this.engine.containsMany(live.map(a => a.documentName), live.map(stateOf), live.map(a => a.payload))
+    : this.engine.containsMany(live.map(stateOf), live.map(a => a.payload)))
   live.forEach((a, k) => { out[a.i] = res[k] instanceof Error ? res[k] : syncStatusFrame(a.documentName, res[k]) })
   return out
 }

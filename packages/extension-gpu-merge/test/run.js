@@ -398,7 +398,8 @@ test('refused store keeps updates applied while the database write is pending', 
 })
 
 // ADVICE r2 / VERDICT r2 missing 5: a refused merge answers only its own read-only messages with the Error;
-// a state outside the snapshot kernel's envelope (pending structs) still gets a SyncStatus (false)
+// a state outside the snapshot kernel's envelope (pending structs) gets the reference's answer (ADVICE r3):
+// snapshotContainsUpdate(snapshot(doc), update) of the document loaded from it -- its integrated part holds `state`
 test('read-only batch with a refused and a pending-struct document', async (engine) => {
   const doc = new Y.Doc(); doc.clientID = 5
   doc.getText('t').insert(0, 'abcdef')
@@ -408,14 +409,17 @@ test('read-only batch with a refused and a pending-struct document', async (engi
   peer.getText('t').insert(0, 'x'); peer.getText('t').insert(0, 'y')
   const pending = grab[1]                                            // client 9 clock 1 without clock 0: pending
   const states = { ok: [state], bad: [Uint8Array.from([1, 1, 5, 0, 4, 1, 1, 0x74]), Uint8Array.from([0, 0])], pend: [state, pending] }
-  const r = new SyncResponder({ engine, getState: async n => states[n] })
+  const r = new SyncResponder({ engine, getState: async n => states[n], Y })
   const msgs = [frame('ok', MessageType.Sync, SyncStep.Step2, state), frame('bad', MessageType.Sync, SyncStep.Step2, state),
     frame('pend', MessageType.Sync, SyncStep.Step2, state), frame('ok', MessageType.Sync, SyncStep.Step2, grab[0])]
   const out = await r.answerReadOnlyMany(msgs)
   assert.deepStrictEqual(Array.from(out[0]), [2, 0x6f, 0x6b, 8, 1])
   assert.ok(out[1] instanceof Error)
-  assert.deepStrictEqual(Array.from(out[2]), [4, 0x70, 0x65, 0x6e, 0x64, 8, 0])
+  assert.deepStrictEqual(Array.from(out[2]), [4, 0x70, 0x65, 0x6e, 0x64, 8, 1])
   assert.deepStrictEqual(Array.from(out[3]), [2, 0x6f, 0x6b, 8, 0])
+  // ... and an update with the pending struct itself is new content for the live document
+  const out2 = await r.answerReadOnlyMany([frame('pend', MessageType.Sync, SyncStep.Step2, pending)])
+  assert.deepStrictEqual(Array.from(out2[0]), [4, 0x70, 0x65, 0x6e, 0x64, 8, 0])
 })
 
 // ADVICE r2: a failing Step1 batch is reported, never an unhandled rejection

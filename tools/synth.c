@@ -265,7 +265,7 @@ size_t synth_big_docs(uint64_t seed, uint32_t n_docs, uint64_t max_bytes, uint64
     const double sz = (double)max_bytes * pow((double)(d + 1), -0.8);   /* size(r) = max * r^-0.8 */
     uint64_t target = (uint64_t)sz; if (target < min_bytes) target = min_bytes;
     uint32_t nc = 1 + (uint32_t)rbelow(&r, max_clients);
-    if (xml && max_clients > 64) nc = max_clients / 2 + (uint32_t)rbelow(&r, max_clients / 2 + 1);
+    if (xml && max_clients > 64) nc = max_clients;   /* C5: every snapshot over exactly max_clients client blocks */
     pick_clients(&r, (int)nc, clients);
     /* descending client order */
     for (uint32_t i = 1; i < nc; i++) { uint32_t t = clients[i], j = i; while (j > 0 && clients[j - 1] < t) { clients[j] = clients[j - 1]; j--; } clients[j] = t; }

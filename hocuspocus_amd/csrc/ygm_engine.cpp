@@ -89,6 +89,7 @@ int ygm_k_launch_merge_big(int large, const uint8_t* arena, const uint64_t* upd_
                            uint64_t blk_cap, void* rec, uint64_t rec_cap, uint64_t slot_total, uint64_t out_cap, void* scan,
                            uint64_t fb_bytes, hipStream_t s);
 size_t ygm_k_big_scan_bytes(uint32_t n_fb, uint64_t fb_bytes);
+void ygm_k_big_lists(void* scan, uint32_t n_fb, uint64_t fb_bytes, unsigned long long** cnt, uint32_t** llist, uint32_t** mlist);
 }
 
 namespace {
@@ -157,6 +158,7 @@ struct ygm_ctx {
   int device = 0;
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;   // the large-document tier's 16-wave launch, beside the mid size's on `stream`
   hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
   // device inputs (host API staging)
   DevBuf arena, offs, docs, sv_arena, sv_offs;
@@ -229,6 +231,7 @@ int ygm_open(int device, uint32_t flags, ygm_ctx** out) {
   ygm_ctx* c = new ygm_ctx();
   c->device = device; c->flags = flags;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess || hipEventCreate(&c->e2) != hipSuccess ||
       hipEventCreate(&c->e3) != hipSuccess) {
     delete c;
@@ -257,6 +260,7 @@ void ygm_close(ygm_ctx* c) {
   for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
   if (c->h_meta) (void)hipHostFree(c->h_meta);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->stream2) { (void)hipStreamSynchronize(c->stream2); (void)hipStreamDestroy(c->stream2); }
   delete c;
 }
 
@@ -419,22 +423,33 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
         !c->big_scan.ensure(ygm_k_big_scan_bytes(m.fb_count, m.fb_bytes)))
       return YGM_ENOMEM;
     HIPCHK(hipEventRecord(c->e0, s));
-    // the snapshot scan, then the mid size over every large document; a log over its LDS goes on to the large size
+    // the snapshot scan; then documents with a snapshot over BIG_MID_U0 on the 16-wave size (stream2) beside the mid
+    // size over the rest (stream); a log over the mid size's LDS goes on to the 16-wave size after it
     if (ygm_k_launch_big_scan(P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, c->flags, c->big_scan.p, m.fb_bytes, s))
       return YGM_EDEVICE;
-    for (int large = 0; large < 2; large++) {
-      const uint32_t n = large ? m.mid_defer : m.fb_count;
-      if (ygm_k_launch_merge_big(large, P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count,
-                                 large ? c->big_up.as<uint32_t>() : nullptr, n, c->big_up.as<uint32_t>(), c->flags, c->out.as<uint8_t>(),
-                                 c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), P.meta,
-                                 c->big_list.as<uint32_t>(), c->big_blk.p, blk_cap, c->big_rec.p, rec_cap, P.slot_total, P.out_cap,
-                                 c->big_scan.p, m.fb_bytes, s))
-        return YGM_EDEVICE;
-      if (!large) {
-        if ((e = read_meta(c, s, m, P.meta))) return e;
-        if (m.fault) return YGM_EDEVICE;
-      }
+    unsigned long long* d_cnt; uint32_t *llist, *mlist;
+    ygm_k_big_lists(c->big_scan.p, m.fb_count, m.fb_bytes, &d_cnt, &llist, &mlist);
+    unsigned long long cnt[4];
+    HIPCHK(hipMemcpyAsync(c->h_meta, d_cnt, sizeof cnt, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    memcpy(cnt, c->h_meta, sizeof cnt);
+    auto launch = [&](int large, const uint32_t* list, uint32_t n, hipStream_t st) {
+      return ygm_k_launch_merge_big(large, P.arena, P.upd_off, P.doc_upd, c->fb_list.as<uint32_t>(), m.fb_count, list, n,
+                                    c->big_up.as<uint32_t>(), c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
+                                    c->out_len.as<uint64_t>(), c->status.as<int32_t>(), P.meta, c->big_list.as<uint32_t>(), c->big_blk.p,
+                                    blk_cap, c->big_rec.p, rec_cap, P.slot_total, P.out_cap, c->big_scan.p, m.fb_bytes, st);
+    };
+    if (cnt[2]) {
+      HIPCHK(hipEventRecord(c->e2, s));
+      HIPCHK(hipStreamWaitEvent(c->stream2, c->e2, 0));
+      if (launch(1, llist, (uint32_t)cnt[2], c->stream2)) return YGM_EDEVICE;
+      HIPCHK(hipEventRecord(c->e3, c->stream2));
     }
+    if (launch(0, mlist, (uint32_t)cnt[3], s)) return YGM_EDEVICE;
+    if ((e = read_meta(c, s, m, P.meta))) return e;
+    if (m.fault) return YGM_EDEVICE;
+    if (m.mid_defer && launch(1, c->big_up.as<uint32_t>(), m.mid_defer, s)) return YGM_EDEVICE;
+    if (cnt[2]) HIPCHK(hipStreamWaitEvent(s, c->e3, 0));
     HIPCHK(hipEventRecord(c->e1, s));
     if ((e = read_meta(c, s, m, P.meta))) return e;
     if (m.fault) return YGM_EDEVICE;

@@ -1263,7 +1263,7 @@ YDEV uint32_t wave_min_u32(uint32_t v) {
 }
 
 #ifndef YGM_BIG_ROUTE
-#define YGM_BIG_ROUTE 2048
+#define YGM_BIG_ROUTE 1024
 #endif
 constexpr uint32_t BIG_ROUTE_MIN = YGM_BIG_ROUTE;   // snapshot bytes from which a document goes to k_merge_big directly
 YDEV void merge_wave_doc(WaveLds& L, uint32_t d, const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
@@ -2227,17 +2227,22 @@ struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const
 constexpr uint32_t BIG_SCAN_CH = 4096, BIG_VCAP = 4096;
 struct BigPick { uint64_t pb; uint32_t n0, u0; };   // U0's positions in nx / vl from pb; n0 = 0xFFFFFFFF: not scanned
 struct BigScan {
-  unsigned long long* cnt;   // [0] positions carved, [1] tasks
-  BigPick* pick;             // per large document (k_merge_big's blockIdx.x)
+  unsigned long long* cnt;   // [0] positions carved, [1] tasks, [2] / [3] entries of llist / mlist
+  BigPick* pick;             // per large document (index into fb_list)
   uint2* task;               // (document, chunk of BIG_SCAN_CH positions)
   uint32_t *nx, *vl;
+  uint32_t *llist, *mlist;   // fb_list indices by U0 size: over BIG_MID_U0 (the 16-wave size) / the rest (the mid size)
   uint64_t ntask_cap, npos_cap;
 };
+// U0 bytes past which a document goes to the 16-wave size directly: the mid size walks 1 KB tiles with 4 waves,
+// so its time on a snapshot of megabytes (the C3 batch's largest documents) would be the batch's critical path
+constexpr uint32_t BIG_MID_U0 = 256u * 1024u;
 // U0 of each large document (the largest update, the first of equal ones: k_merge_big's rule) and its scan tasks
 // (a wave per document, 16 per workgroup: the workgroup carves its positions and tasks with one atomic each)
 __global__ __launch_bounds__(1024) void k_big_pick(const uint64_t* __restrict__ upd_off, const uint32_t* __restrict__ doc_upd,
                                                    const uint32_t* __restrict__ fb_list, uint32_t n_fb, BigScan S) {
   __shared__ uint64_t s_pb[16], s_tb[16];
+  __shared__ uint32_t s_lg[16], s_lb, s_mb;
   const uint32_t wv = threadIdx.x / WAVE, w = blockIdx.x * 16u + wv, l = threadIdx.x % WAVE;
   uint32_t u0 = 0, n0 = 0, nt = 0;
   if (w < n_fb) {
@@ -2252,16 +2257,29 @@ __global__ __launch_bounds__(1024) void k_big_pick(const uint64_t* __restrict__ 
     u0 = 0xFFFFFFFFu - (uint32_t)best; n0 = (uint32_t)(best >> 32);
     nt = n0 < 0x7FFFFFFFu ? (n0 + BIG_SCAN_CH - 1u) / BIG_SCAN_CH : 0u;
   }
-  if (l == 0) { s_pb[wv] = w < n_fb ? (uint64_t)n0 + 16u : 0u; s_tb[wv] = nt; }
+  if (l == 0) {
+    s_pb[wv] = w < n_fb ? (uint64_t)n0 + 16u : 0u; s_tb[wv] = nt;
+    s_lg[wv] = w >= n_fb ? 0u : (n0 > BIG_MID_U0 && n0 < 0x7FFFFFFFu) ? 1u : 2u;   // 1: the 16-wave list, 2: the mid list
+  }
   __syncthreads();
   if (threadIdx.x == 0) {   // exclusive prefixes over the workgroup's documents, then one carve each
     uint64_t a = 0, b = 0;
-    for (int i = 0; i < 16; i++) { const uint64_t x = s_pb[i], y = s_tb[i]; s_pb[i] = a; s_tb[i] = b; a += x; b += y; }
+    uint32_t nl = 0, nm = 0;
+    for (int i = 0; i < 16; i++) {
+      const uint64_t x = s_pb[i], y = s_tb[i]; s_pb[i] = a; s_tb[i] = b; a += x; b += y;
+      const uint32_t g = s_lg[i]; s_lg[i] = g == 1 ? nl : g == 2 ? nm : 0u; s_lg[i] |= g << 30; nl += g == 1; nm += g == 2;
+    }
     const uint64_t pa = atomicAdd(&S.cnt[0], (unsigned long long)a), ta = atomicAdd(&S.cnt[1], (unsigned long long)b);
+    s_lb = nl ? (uint32_t)atomicAdd(&S.cnt[2], (unsigned long long)nl) : 0u;
+    s_mb = nm ? (uint32_t)atomicAdd(&S.cnt[3], (unsigned long long)nm) : 0u;
     for (int i = 0; i < 16; i++) { s_pb[i] += pa; s_tb[i] += ta; }
   }
   __syncthreads();
   if (w >= n_fb) return;
+  if (l == 0) {
+    const uint32_t g = s_lg[wv] >> 30, at = s_lg[wv] & 0x3FFFFFFFu;
+    if (g == 1) S.llist[s_lb + at] = w; else S.mlist[s_mb + at] = w;
+  }
   const uint64_t pb = s_pb[wv], tb = s_tb[wv];
   const bool ok = nt && pb + n0 + 16u <= S.npos_cap && tb + nt <= S.ntask_cap;
   if (l == 0) { BigPick P; P.pb = pb; P.n0 = ok ? n0 : 0xFFFFFFFFu; P.u0 = u0; S.pick[w] = P; }
@@ -2309,7 +2327,11 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
         uint32_t kind;
         if (big_skip(c, kind, 8) && !c.err) {
           e = c.pos | (kind == 0 ? 0x80000000u : 0u);
+#ifndef YGM_SCAN_NOVAL
           if (c.pos - p <= BIG_VCAP) {
+#else
+          if (false) {   // experiment: ends only; every struct validated by k_merge_big's helper waves
+#endif
             GCur w; w.init(u0p, n0); w.pos = p;
             const GStruct g = big_struct(w, flags);
             v = g.ok && w.pos == c.pos && g.len != 0 && g.len < 0xFFFFFFFFull ? (uint32_t)g.len : 0xFFFFFFFFu;
@@ -3363,7 +3385,15 @@ static void big_scan_layout(uint32_t n_fb, uint64_t fb_bytes, BigScan& S, uint8_
   S.task = (uint2*)carve(sizeof(uint2) * S.ntask_cap);
   S.nx = (uint32_t*)carve(4 * S.npos_cap);
   S.vl = (uint32_t*)carve(4 * S.npos_cap);
+  S.llist = (uint32_t*)carve(4ull * n_fb);
+  S.mlist = (uint32_t*)carve(4ull * n_fb);
   total = o;
+}
+// device pointers of the scan's counters and of its two document lists (after ygm_k_launch_big_scan)
+void ygm_k_big_lists(void* scan, uint32_t n_fb, uint64_t fb_bytes, unsigned long long** cnt, uint32_t** llist, uint32_t** mlist) {
+  BigScan S; size_t total;
+  big_scan_layout(n_fb, fb_bytes, S, (uint8_t*)scan, total);
+  *cnt = S.cnt; *llist = S.llist; *mlist = S.mlist;
 }
 size_t ygm_k_big_scan_bytes(uint32_t n_fb, uint64_t fb_bytes) { BigScan S; size_t t; big_scan_layout(n_fb, fb_bytes, S, nullptr, t); return t; }
 int ygm_k_launch_big_scan(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
@@ -3378,8 +3408,8 @@ int ygm_k_launch_big_scan(const uint8_t* arena, const uint64_t* upd_off, const u
   hipLaunchKernelGGL(k_big_scan, dim3((uint32_t)g), dim3(256), 0, s, arena, upd_off, doc_upd, fb_list, flags, S);
   return launch_rc(__func__);
 }
-// large = 0: the mid size over fb_list (documents whose log exceeds its LDS go to up_list, meta->mid_defer);
-// large = 1: the large size over the fb_list indices in fbx[0, n)
+// large = 0: the mid size, large = 1: the 16-wave size, over the fb_list indices in fbx[0, n) (the mid size sends a
+// document whose log exceeds its LDS to up_list, meta->mid_defer)
 int ygm_k_launch_merge_big(int large, const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* fb_list,
                            uint32_t n_fb, const uint32_t* fbx, uint32_t n, uint32_t* up_list, uint32_t flags, uint8_t* out,
                            uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, uint32_t* fb2_list, void* blk,

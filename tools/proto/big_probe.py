@@ -12,6 +12,16 @@ if diag:
 from tools import synth
 import oracle
 e = eng.Engine(0)
+if len(sys.argv) > 1 and sys.argv[1] == "tiers":   # the full C3 batch: documents and time per tier
+    arena, upd_off, doc_upd = synth.big_docs(100000, 10_000_000, 1024, max_clients=64, max_k=200, seed=8)
+    n = 100000
+    upd_doc = np.repeat(np.arange(n, dtype=np.uint32), np.diff(doc_upd).astype(np.int64))
+    for rep in range(3):
+        s0 = e.stats(); t0 = time.time()
+        e.merge_packed_raw(arena, upd_off, upd_doc, n)
+        s1 = e.stats()
+    print({k: round(getattr(s1, k) - getattr(s0, k), 3) for k in ("kernel_ms", "lean_ms", "docs_lean", "docs_lean_wide", "docs_fast", "docs_big", "docs_seq")}, flush=True)
+    sys.exit(0)
 if len(sys.argv) > 1 and sys.argv[1] == "occ":   # C3-full-shaped batch (top ranks): per-workgroup stamps -> concurrency
     n = int(os.environ.get("OCC_N", "16000"))
     arena, upd_off, doc_upd = synth.big_docs(n, 10_000_000, 1024, max_clients=64, max_k=200, seed=8)

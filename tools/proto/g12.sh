@@ -1,7 +1,8 @@
 # round-4 probe (tooling): all GPU tests, occupancy probe, C3 blocks, the default bench line
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/t_gpu_all.log 2>&1 && \
+
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu -k "large" --timeout 200 --timeout-method thread > gpurun_out/t_large.log 2>&1 && \
 OCC_DS=1 timeout -k 10 300 python -u tools/proto/big_probe.py occ > gpurun_out/big_occds.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --big c3 --no-yjs > gpurun_out/big_c3.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --big c5 --no-yjs > gpurun_out/big_c5.log 2>&1 && \

@@ -2224,7 +2224,10 @@ struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const
 // Skip, Any arrays / objects or JSON of more than 8 entries, past U0's end), and for parses of at most BIG_VCAP bytes
 // vl[p] = its clock length if it is what write_struct emits (big_struct), 0xFFFFFFFF if not (0: not validated).  The
 // chain follow in k_merge_big then reads the ends a tile at a time and the validation one word per struct.
-constexpr uint32_t BIG_SCAN_CH = 4096, BIG_VCAP = 4096;
+#ifndef YGM_BIG_VCAP
+#define YGM_BIG_VCAP 64
+#endif
+constexpr uint32_t BIG_SCAN_CH = 4096, BIG_VCAP = YGM_BIG_VCAP;
 struct BigPick { uint64_t pb; uint32_t n0, u0; };   // U0's positions in nx / vl from pb; n0 = 0xFFFFFFFF: not scanned
 struct BigScan {
   unsigned long long* cnt;   // [0] positions carved, [1] tasks, [2] / [3] entries of llist / mlist
@@ -2237,6 +2240,10 @@ struct BigScan {
 // U0 bytes past which a document goes to the 16-wave size directly: the mid size walks 1 KB tiles with 4 waves,
 // so its time on a snapshot of megabytes (the C3 batch's largest documents) would be the batch's critical path
 constexpr uint32_t BIG_MID_U0 = 256u * 1024u;
+// only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item ref 1..8 without bit 0x20
+// next to an origin.  The scan writes nx / vl for these positions only; the follow and the validation test the byte
+// before they read them (a struct the chain meets elsewhere is parsed from global memory)
+YDEV bool big_cand(uint32_t ib) { const uint32_t rf = ib & 31u; return ib == 0u || (rf >= 1u && rf <= 8u && !((ib & 0xC0u) && (ib & 0x20u))); }
 // U0 of each large document (the largest update, the first of equal ones: k_merge_big's rule) and its scan tasks
 // (a wave per document, 16 per workgroup: the workgroup carves its positions and tasks with one atomic each)
 __global__ __launch_bounds__(1024) void k_big_pick(const uint64_t* __restrict__ upd_off, const uint32_t* __restrict__ doc_upd,
@@ -2306,14 +2313,7 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
     uint32_t qn = 0;
     for (uint32_t b = w0; b < w1; b += WAVE) {
       const uint32_t p = b + l;
-      bool cand = false;
-      if (p < w1) {
-        // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item ref 1..8
-        // without bit 0x20 next to an origin (a struct the chain meets elsewhere is parsed there, from global memory)
-        const uint32_t ib = u0p[p], rf = ib & 31u;
-        cand = ib == 0u || (rf >= 1u && rf <= 8u && !((ib & 0xC0u) && (ib & 0x20u)));
-        if (!cand) { S.nx[P.pb + p] = 0u; S.vl[P.pb + p] = 0u; }
-      }
+      const bool cand = p < w1 && big_cand(u0p[p]);   // (other positions are never read: nothing written)
       const uint64_t m = __ballot(cand);
       if (cand) q[qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = p;
       qn += (uint32_t)__builtin_popcountll(m);
@@ -2379,12 +2379,12 @@ YDEV bool big_hdr_fast(const TL& T, uint32_t hp, uint32_t tn, uint64_t& nst, uin
   return true;
 }
 template <class CF>
-YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint32_t n0, uint32_t t0) {
+YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint32_t mis, uint32_t n0, uint32_t t0) {
   // the scan's struct ends of the tile's positions, tile-relative (an end 32 KB or more away: no entry, the chain
   // follow parses that struct from global memory)
   for (uint32_t i = t0; i < CF::CH; i += CF::THREADS) {
     uint32_t e = 0;
-    if (at + i < n0) {
+    if (at + i < n0 && big_cand(((const uint8_t*)T.b)[mis + i])) {
       const uint32_t v = nxg[at + i];
       const uint32_t rel = (v & 0x7FFFFFFFu) - at;
       if (v && rel < 0x8000u) e = rel | ((v >> 31) << 15);
@@ -2407,7 +2407,7 @@ YDEV bool big_validate(const uint32_t* rs, const uint32_t* re, BigRec* rec, cons
   bool vbad = false;
   for (uint64_t i = C.vs + t0; i < C.ns; i += NT) {
     BigRec R; R.start = rs[i - C.vs]; R.end = re[i - C.vs];
-    uint64_t len = C.aux[R.start];
+    uint64_t len = big_cand(C.u0p[R.start]) ? C.aux[R.start] : 0u;   // (the scan wrote candidate positions only)
     if (len == 0u) {   // (the scan's end for R.start, when it has one, is R.end: the chain took it from nx)
       GCur w; w.init(C.u0p, C.n0); w.pos = R.start;
       const GStruct g = big_struct(w, flags);
@@ -2747,7 +2747,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
       __syncthreads();
       const BigCmd C = s_cmd;
       if (C.cmd == 0) return;
-      if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.n0, threadIdx.x);
+      if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.mis, C.n0, threadIdx.x);
       else if (C.cmd == 3) { if (big_clock_ranges<CF::THREADS>(blk, rec, C, threadIdx.x)) L.bad = 1; }
       else if (C.cmd == 4) { if (!big_ds_canon<CF::THREADS>(C, threadIdx.x)) s_cmd.tb = 1; }
       else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, threadIdx.x)) L.bad = 1;
@@ -2852,9 +2852,9 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
     wave_sync();
     if (!spec) return;
     const uint64_t dg0 = DIAG_NOW();
-    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.n0 = n0; s_cmd.aux = nxg; }
+    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.n0 = n0; s_cmd.aux = nxg; }
     __syncthreads();
-    big_spec<CF>(T0, nxg, at, n0, l);
+    big_spec<CF>(T0, nxg, at, mis, n0, l);
     __syncthreads();
     dg_spec += DIAG_NOW() - dg0;
   };

@@ -53,6 +53,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 PMC_PROFILE = "r03_final/pmc.json"          # committed rocprofv3 PMC summary (FETCH_SIZE x2 + WRITE_SIZE per launch)
 PMC_C4 = "r03_final/pmc.json"              # ... of the SV / diff walker at C4
+PMC_BLOCKS = "r04_final/pmc_blocks.json"   # ... of whole --big blocks (every cascade kernel summed per step: tools/pmc_blocks.py)
 
 
 def parse():
@@ -800,14 +801,16 @@ def run_rank(args, rank, world, dist, be, dev=None):
     # ---- C3 at full size (100 000 [snapshot, ...log] documents, 0.77 GB): one batch, rank 0 at N = 1
     if args.c3 and rank == 0 and world == 1 and not args.dry_run:
         blk = big_run(args, "c3full", be.dev.index)
-        blk["roofline"] = roof(blk["bytes_in"] + blk["bytes_out"], blk["gpu_ms"], "merge cascade (k_merge_lean / wave / fast / big)", None)
+        blk["roofline"] = roof(blk["bytes_in"] + blk["bytes_out"], blk["gpu_ms"], "merge cascade (k_big_scan + k_merge_big mid / 16-wave sizes + "
+                               "lean / wave for the routing)", _pmc(PMC_BLOCKS, "c3full"))
         line["c3"] = blk
     # ---- C5 at BASELINE size (1 000 XmlFragment [snapshot, ...log] documents of 5-10 k client blocks): rank 0 at N = 1
     if args.c5_docs and rank == 0 and world == 1 and not args.dry_run:
         a5 = argparse.Namespace(**vars(args))
         a5.big_docs = args.c5_docs
         blk = big_run(a5, "c5", be.dev.index)
-        blk["roofline"] = roof(blk["bytes_in"] + blk["bytes_out"], blk["gpu_ms"], "merge cascade (k_merge_big for these documents)", None)
+        blk["roofline"] = roof(blk["bytes_in"] + blk["bytes_out"], blk["gpu_ms"], "merge cascade (k_big_scan + k_merge_big for these documents)",
+                               _pmc(PMC_BLOCKS, "c5"))
         line["c5"] = blk
     # ---- CPU baselines (rank 0 at N = 1 only)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:

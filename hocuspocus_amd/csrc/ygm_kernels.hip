@@ -2711,6 +2711,196 @@ YDEV void big_write_structs(const LDS& L, const BigGrp* G, uint32_t ngr, uint32_
   o.le = ~0ull;
 }
 
+// ---- the parallel splice emit of the delete set (wave 0; after big_ds_plan).  Lanes over the sorted log ranges find
+// the client starts and the merge groups (a range starts a group when it starts beyond the running maximum end of its
+// client's earlier ranges: a segmented max scan), fold each group's end / last touched U0 range onto its first range,
+// and add per client (LDS atomics) its groups, their span bytes and the U0 ranges / bytes they absorb.  One short serial
+// loop over the log clients places them (the untouched entries before each go out as one verbatim run); the lanes then
+// write headers and spans and queue every verbatim run / segment on the copy list.  W: LDS words, 7 per log client + 1
+// per range; false (capacity): the serial emit takes it.  Range flags in BigRange.len (free after big_ds_plan): bit 0
+// client start, bit 1 group start, bits 2-12 client ordinal, 13-23 the range's group start.
+YDEV uint32_t big_u64max_scan(uint64_t& v) {   // inclusive max scan of v over the wave (in place); returns nothing useful
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) { const uint64_t t = __shfl_up(v, o, WAVE); if ((threadIdx.x % WAVE) >= (uint32_t)o) v = t > v ? t : v; }
+  return 0;
+}
+template <class LDS>
+YDEV bool big_ds_par(LDS& L, const BigDsPlan& DP, const uint32_t* X, uint32_t maxd, uint32_t nrg, uint32_t* W, uint32_t wcap,
+                     const uint8_t* dsb, BigOut& o, uint64_t& nc) {
+  const uint32_t l = threadIdx.x % WAVE, ne = DP.C;
+  if (nrg > 2047u) return false;
+  if (3ull * nrg > wcap) return false;
+  uint32_t* const PR = W;                                   // per range: running max end (steps 1-2), contribution scan (5)
+  uint32_t* const PRB = W + nrg;                            // ... running max of b1 and pb within the client (steps 1-2):
+  uint32_t* const PRP = W + 2u * nrg;                       //     not monotone (a short range inside a long one absorbs less)
+  // 1. flags, client ordinals, group starts
+  uint32_t nci = 0, gcarry = 0;
+  uint64_t mcarry = 0, bcarry = 0, pcarry = 0;
+  for (uint32_t cb = 0; cb < nrg; cb += WAVE) {
+    const uint32_t r = cb + l;
+    const bool in = r < nrg;
+    const uint32_t X0 = in ? (uint32_t)(L.rg[r].key >> 32) : 0u;
+    const bool cs = in && (r == 0 || (uint32_t)(L.rg[r - 1].key >> 32) != X0);
+    const uint64_t m = __ballot(cs);
+    const uint32_t ci = nci + lanes_below(m) + (cs ? 1u : 0u) - 1u;
+    nci += (uint32_t)__builtin_popcountll(m);
+    uint64_t v = in ? (((uint64_t)ci << 32) | L.rg[r].e) : 0ull;
+    big_u64max_scan(v);
+    v = v > mcarry ? v : mcarry;
+    uint64_t ex = __shfl_up(v, 1, WAVE);
+    if (l == 0) ex = mcarry;
+    const bool gs = in && (cs || (uint32_t)(ex >> 32) != ci || L.rg[r].s > (uint32_t)ex);
+    uint64_t gv = gs ? r : 0u;
+    big_u64max_scan(gv);
+    const uint32_t gsi = (uint32_t)gv > gcarry ? (uint32_t)gv : gcarry;
+    uint64_t vb = in ? (((uint64_t)ci << 32) | L.rg[r].b1) : 0ull, vp = in ? (((uint64_t)ci << 32) | L.rg[r].pb) : 0ull;
+    big_u64max_scan(vb); big_u64max_scan(vp);
+    vb = vb > bcarry ? vb : bcarry; vp = vp > pcarry ? vp : pcarry;
+    if (in) { L.rg[r].len = (cs ? 1u : 0u) | (gs ? 2u : 0u) | (ci << 2) | (gsi << 13); PR[r] = (uint32_t)v; PRB[r] = (uint32_t)vb; PRP[r] = (uint32_t)vp; }
+    mcarry = __shfl(v, WAVE - 1, WAVE); bcarry = __shfl(vb, WAVE - 1, WAVE); pcarry = __shfl(vp, WAVE - 1, WAVE);
+    gcarry = (uint32_t)__builtin_amdgcn_readlane((int)gsi, WAVE - 1);
+  }
+  if (nci > 2047u || 7ull * nci + 3ull * nrg > wcap) return false;
+  uint32_t* const CW = W + 3u * nrg;                        // per log client: ng, span bytes, absorbed ranges, absorbed bytes, first range, offset, untouched run
+  for (uint32_t i = l; i < 7u * nci; i += WAVE) CW[i] = 0u;
+  wave_sync();
+  // 2. each group's end (the running maximum at its last range) and last absorbed U0 range onto its first range
+  for (uint32_t cb = 0; cb < nrg; cb += WAVE) {
+    const uint32_t r = cb + l;
+    uint32_t g = 0, ge = 0, b1 = 0, pb = 0; bool last = false;
+    if (r < nrg) {
+      last = r + 1 == nrg || (L.rg[r + 1].len & 2u);
+      g = L.rg[r].len >> 13; ge = PR[r]; b1 = PRB[r]; pb = PRP[r];
+    }
+    wave_sync();
+    if (last) { L.rg[g].e = ge; L.rg[g].b1 = b1; L.rg[g].pb = pb; }
+    wave_sync();
+  }
+  // 3. per client sums (LDS atomics) at the group starts
+  for (uint32_t cb = 0; cb < nrg; cb += WAVE) {
+    const uint32_t r = cb + l;
+    if (r < nrg) {
+      const BigRange& R = L.rg[r];
+      const uint32_t f = R.len, ci = (f >> 2) & 0x7FFu;
+      if (f & 1u) CW[7u * ci + 4u] = r;
+      if (f & 2u) {
+        const bool touched = !(R.ent >> 31);
+        atomicAdd(&CW[7u * ci + 0u], 1u);
+        atomicAdd(&CW[7u * ci + 1u], vu_len(R.s) + vu_len(R.e - R.s));
+        if (touched) { atomicAdd(&CW[7u * ci + 2u], R.b1 - R.a); atomicAdd(&CW[7u * ci + 3u], R.pb - R.pa); }
+      }
+    }
+  }
+  wave_sync();
+  // 4. the log clients in order (serial, a few operations each): records placed after the untouched entries before them
+  uint64_t off = 0;
+  uint32_t cur = DP.b0, eu = 0;
+  nc = 0;
+  for (uint32_t c = 0; c < nci; c++) {
+    uint32_t* w = CW + 7u * c;
+    const uint32_t r0 = w[4];
+    const BigRange& R = L.rg[r0];
+    const uint32_t lo = R.ent & 0x7FFFFFFFu;
+    const bool touched = !(R.ent >> 31);
+    const uint32_t xbs = X[r0];
+    const uint32_t U = xbs - cur;
+    const uint32_t client = 0xFFFFFFFFu - (uint32_t)(R.key >> 32);
+    const uint32_t n = touched ? X[maxd + r0] : 0u, be = touched ? X[2u * maxd + r0] : 0u;
+    const uint32_t nruns = n - w[2] + w[0];
+    const uint64_t verb = touched ? (uint64_t)(be - xbs - vu_len(client) - vu_len(n)) - w[3] : 0u;
+    if (l == 0) { w[5] = (uint32_t)off; w[6] = U; }
+    off += (uint64_t)U + vu_len(client) + vu_len(nruns) + w[1] + verb;
+    nc += (lo - eu) + 1u;
+    cur = touched ? be : xbs; eu = touched ? lo + 1u : lo;
+  }
+  const uint32_t tail = DP.bend - cur;
+  nc += ne - eu;
+  if (!o.w) { o.n += off + tail; return true; }
+  // 5. writes at o.o + base: client headers and untouched runs (lanes over clients), spans and segments (lanes over
+  //    ranges: a group's place in its client is an exclusive scan of what each group writes -- the U0 bytes between the
+  //    previous group and it, then its span)
+  const uint64_t base = o.n;
+  wave_sync();
+  o.flush();
+  o.le = ~0ull;
+  uint32_t carry = 0;
+  for (uint32_t cb = 0; cb < nrg; cb += WAVE) {
+    const uint32_t r = cb + l;
+    uint32_t contrib = 0;
+    if (r < nrg && (L.rg[r].len & 2u)) {
+      const BigRange& R = L.rg[r];
+      const uint32_t ci = (R.len >> 2) & 0x7FFu;
+      uint32_t seg = 0;
+      if (!(R.ent >> 31)) {
+        const uint32_t* w = CW + 7u * ci;
+        const uint32_t r0 = w[4];
+        const uint32_t client = 0xFFFFFFFFu - (uint32_t)(R.key >> 32), n = X[maxd + r0];
+        const uint32_t prevpb = (R.len & 1u) ? X[r0] + vu_len(client) + vu_len(n) : L.rg[L.rg[r - 1].len >> 13].pb;
+        seg = R.pa - prevpb;
+      }
+      contrib = seg + vu_len(R.s) + vu_len(R.e - R.s);
+    }
+    const uint32_t inc = dpp_incl_add(contrib) + carry;
+    if (r < nrg) PR[r] = inc - contrib;                      // exclusive scan
+    carry = lane63(inc);
+  }
+  wave_sync();
+  for (uint32_t cb = 0; cb < nrg; cb += WAVE) {
+    if (o.nc + 3u * WAVE > o.cap) o.flush();
+    const uint32_t r = cb + l;
+    // up to three copies per lane: the client's untouched run (A), the U0 bytes before a group (B), after the last (C)
+    BigCp A, B, C; A.n = B.n = C.n = 0u;
+    if (r < nrg) {
+      const BigRange& R = L.rg[r];
+      const uint32_t f = R.len, ci = (f >> 2) & 0x7FFu;
+      const uint32_t* w = CW + 7u * ci;
+      const uint32_t r0 = w[4];
+      const bool touched = !(R.ent >> 31);
+      const uint32_t client = 0xFFFFFFFFu - (uint32_t)(R.key >> 32);
+      const uint32_t n = touched ? X[maxd + r0] : 0u;
+      const uint32_t nruns = n - w[2] + w[0];
+      const uint64_t body = base + w[5] + w[6] + vu_len(client) + vu_len(nruns);   // after the client's header
+      if (f & 1u) {   // the client's untouched run and header; for a touched entry the U0 bytes after its last group
+        if (w[6]) { A.src = (uint64_t)(uintptr_t)(dsb + X[r0] - w[6]); A.dst = (uint32_t)(base + w[5]); A.n = w[6]; }
+        uint8_t* h = o.o + base + w[5] + w[6];
+        big_put_vu(h, client); big_put_vu(h + vu_len(client), nruns);
+        if (touched) {
+          uint32_t rl = r0;   // the client's last range, and its last group (start gl)
+          while (rl + 1 < nrg && !(L.rg[rl + 1].len & 1u)) rl++;
+          const uint32_t gl = L.rg[rl].len >> 13;
+          const BigRange& G = L.rg[gl];
+          const uint32_t prevpb = (G.len & 1u) ? X[r0] + vu_len(client) + vu_len(n) : L.rg[L.rg[gl - 1].len >> 13].pb;
+          const uint64_t endw = (uint64_t)(PR[gl] - PR[r0]) + (G.pa - prevpb) + vu_len(G.s) + vu_len(G.e - G.s);
+          const uint32_t be = X[2u * maxd + r0];
+          if (be > G.pb) { C.src = (uint64_t)(uintptr_t)(dsb + G.pb); C.dst = (uint32_t)(body + endw); C.n = be - G.pb; }
+        }
+      }
+      if (f & 2u) {   // the group: the U0 bytes since the previous group, then its span
+        uint32_t seg = 0, prevpb = 0;
+        if (touched) {
+          prevpb = (f & 1u) ? X[r0] + vu_len(client) + vu_len(n) : L.rg[L.rg[r - 1].len >> 13].pb;
+          seg = R.pa - prevpb;
+        }
+        const uint64_t at = body + (PR[r] - PR[r0]);
+        if (seg) { B.src = (uint64_t)(uintptr_t)(dsb + prevpb); B.dst = (uint32_t)at; B.n = seg; }
+        uint8_t* h = o.o + at + seg;
+        big_put_vu(h, R.s); big_put_vu(h + vu_len(R.s), R.e - R.s);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const BigCp& E = k == 0 ? A : k == 1 ? B : C;
+      const uint64_t m = __ballot(E.n != 0u);
+      if (E.n) o.cl[o.nc + lanes_below(m)] = E;
+      o.nc += (uint32_t)__builtin_popcountll(m);
+    }
+  }
+  if (tail) o.add((uint64_t)(uintptr_t)(dsb + cur), base + off, tail);
+  o.le = ~0ull;
+  o.n = base + off + tail;
+  return true;
+}
+
 // block clock ranges [vs, ns) of the block table (cmd 3, the whole workgroup): clock0 + the validated lengths of
 // the block's struct records; true if one passes 2^32 - 1
 template <uint32_t NT>
@@ -3148,7 +3338,11 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
       const uint8_t* const dsb = u0p + s_ds0;
       const uint32_t ne = DP.C;
       o.vu(ndsc);
-      uint32_t e = 0, r = 0, cur = DP.b0;                    // cur: byte start of entry e
+      // the parallel emit (its words: pass 0 in the empty copy list, pass 1 in the client-group region, whose struct
+      // part is written by then; the same capacity both passes)
+      const uint32_t wcap = (uint32_t)(CF::SBG / 4u) < o.cap * 4u ? (uint32_t)(CF::SBG / 4u) : o.cap * 4u;
+      const bool dsdone = big_ds_par(L, DP, dsx, (uint32_t)CF::MAXD, nrg, pass ? (uint32_t*)G : (uint32_t*)o.cl, wcap, dsb, o, nc);
+      uint32_t e = dsdone ? ne : 0u, r = dsdone ? nrg : 0u, cur = DP.b0;   // cur: byte start of entry e
       while (e < ne || r < nrg) {
         // U0's entries before the next log client's (big_ds_plan's lower bound) go out as one verbatim run
         const uint32_t e2 = r < nrg ? (L.rg[r].ent & 0x7FFFFFFFu) : ne;

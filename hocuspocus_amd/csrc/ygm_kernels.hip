@@ -2239,7 +2239,7 @@ struct BigScan {
 };
 // U0 bytes past which a document goes to the 16-wave size directly: the mid size walks 1 KB tiles with 4 waves,
 // so its time on a snapshot of megabytes (the C3 batch's largest documents) would be the batch's critical path
-constexpr uint32_t BIG_MID_U0 = 256u * 1024u;
+constexpr uint32_t BIG_MID_U0 = 2048u * 1024u;
 // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item ref 1..8 without bit 0x20
 // next to an origin.  The scan writes nx / vl for these positions only; the follow and the validation test the byte
 // before they read them (a struct the chain meets elsewhere is parsed from global memory)

@@ -230,8 +230,12 @@ int ygm_open(int device, uint32_t flags, ygm_ctx** out) {
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return YGM_EDEVICE;
   ygm_ctx* c = new ygm_ctx();
   c->device = device; c->flags = flags;
+  // stream2 at the high priority: a queue of its own (a process with more streams than hardware queues shares them,
+  // and two streams on one queue run their kernels one after the other)
+  int prio_lo = 0, prio_hi = 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess || hipEventCreate(&c->e2) != hipSuccess ||
       hipEventCreate(&c->e3) != hipSuccess) {
     delete c;

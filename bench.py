@@ -51,8 +51,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
-PMC_PROFILE = "r03_final/pmc.json"          # committed rocprofv3 PMC summary (FETCH_SIZE x2 + WRITE_SIZE per launch)
-PMC_C4 = "r03_final/pmc.json"              # ... of the SV / diff walker at C4
+PMC_PROFILE = "r04_final/pmc.json"          # committed rocprofv3 PMC summary (FETCH_SIZE x2 + WRITE_SIZE per launch)
+PMC_C4 = "r04_final/pmc.json"              # ... of the SV / diff walker at C4
 PMC_BLOCKS = "r04_final/pmc_blocks.json"   # ... of whole --big blocks (every cascade kernel summed per step: tools/pmc_blocks.py)
 
 

@@ -2322,6 +2322,7 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
     for (uint32_t j = l; j < qn; j += WAVE) {
       const uint32_t p = q[j];
       uint32_t e = 0, v = 0;
+#ifndef YGM_SCAN_NOPARSE
       {
         GCur c; c.init(u0p, n0); c.pos = p;
         uint32_t kind;
@@ -2338,6 +2339,7 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
           }
         }
       }
+#endif
       S.nx[P.pb + p] = e;
       S.vl[P.pb + p] = v;
     }

@@ -2230,12 +2230,13 @@ struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const
 constexpr uint32_t BIG_SCAN_CH = 4096, BIG_VCAP = YGM_BIG_VCAP;
 struct BigPick { uint64_t pb; uint32_t n0, u0; };   // U0's positions in nx / vl from pb; n0 = 0xFFFFFFFF: not scanned
 struct BigScan {
-  unsigned long long* cnt;   // [0] positions carved, [1] tasks, [2] / [3] entries of llist / mlist
+  unsigned long long* cnt;   // [0] positions carved, [1] tasks, [2] / [3] entries of llist / mlist, [4] slow queue
   BigPick* pick;             // per large document (index into fb_list)
   uint2* task;               // (document, chunk of BIG_SCAN_CH positions)
   uint32_t *nx, *vl;
   uint32_t *llist, *mlist;   // fb_list indices by U0 size: over BIG_MID_U0 (the 16-wave size) / the rest (the mid size)
-  uint64_t ntask_cap, npos_cap;
+  uint2* vq;                 // slow queue (document, position): candidates k_big_val validates
+  uint64_t ntask_cap, npos_cap, vq_cap;
 };
 // U0 bytes past which a document goes to the 16-wave size directly: the mid size walks 1 KB tiles with 4 waves,
 // so its time on a snapshot of megabytes (the C3 batch's largest documents) would be the batch's critical path
@@ -2296,54 +2297,103 @@ __global__ __launch_bounds__(1024) void k_big_pick(const uint64_t* __restrict__ 
 __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                   const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
                                                   uint32_t flags, BigScan S) {
-  // a wave takes BIG_SCAN_CH / 4 positions of the task: the candidates (by their byte) are queued in LDS, every
-  // other position is written as "no parse" at once, then the lanes parse the queue -- a lane per candidate, not
-  // a lane per position (about one position in seven is a candidate in text)
-  __shared__ uint32_t s_q[4][BIG_SCAN_CH / 4];
+  // a wave takes BIG_SCAN_CH / 4 positions of the task, staged in LDS with a margin past them (the structs that start
+  // near the end): the candidates (by their byte) are queued, then the lanes parse the queue from LDS -- a lane per
+  // candidate, not a lane per position.  A parse that runs into the stage's end is redone from global memory.
+  constexpr uint32_t WCH = BIG_SCAN_CH / 4, MARGIN = 256, SQ = (WCH + MARGIN) / 16 + 2;
+  __shared__ uint4 s_b[4][SQ];
+  __shared__ uint16_t s_q[4][WCH];
   const uint32_t wv = threadIdx.x / WAVE, l = threadIdx.x % WAVE;
-  uint32_t* const q = s_q[wv];
+  uint16_t* const q = s_q[wv];
   const uint64_t ntask = *(volatile unsigned long long*)&S.cnt[1];
   for (uint64_t t = blockIdx.x; t < ntask; t += gridDim.x) {
     const uint2 T = S.task[t];
     const BigPick P = S.pick[T.x];
     if (P.n0 == 0xFFFFFFFFu) continue;   // (no tasks are carved for such a document)
     const uint8_t* u0p = arena + upd_off[doc_upd[fb_list[T.x]] + P.u0];
-    const uint32_t n0 = P.n0, w0 = T.y * BIG_SCAN_CH + wv * (BIG_SCAN_CH / 4);
-    const uint32_t w1 = w0 + BIG_SCAN_CH / 4 < n0 ? w0 + BIG_SCAN_CH / 4 : n0;
+    const uint32_t n0 = P.n0, w0 = T.y * BIG_SCAN_CH + wv * WCH;
+    if (w0 >= n0) continue;   // (wave-uniform)
+    const uint32_t w1 = w0 + WCH < n0 ? w0 + WCH : n0, se = w0 + WCH + MARGIN < n0 ? w0 + WCH + MARGIN : n0;
+    // the stage: the aligned 16-byte chunks holding [w0, se) (a chunk holding a byte of the update is inside the arena)
+    const uint8_t* g0 = u0p + w0;
+    const uint32_t sh = (uint32_t)((uintptr_t)g0 & 15u), nq = (sh + (se - w0) + 15u) / 16u;
+    const uint4* ga = (const uint4*)(g0 - sh);
+    for (uint32_t i = l; i < nq; i += WAVE) s_b[wv][i] = ga[i];
+    wave_sync();
+    const uint8_t* lb = (const uint8_t*)s_b[wv] + sh;   // lb[i] = U0 byte w0 + i
     uint32_t qn = 0;
-    for (uint32_t b = w0; b < w1; b += WAVE) {
-      const uint32_t p = b + l;
-      const bool cand = p < w1 && big_cand(u0p[p]);   // (other positions are never read: nothing written)
+    for (uint32_t b = 0; b < w1 - w0; b += WAVE) {
+      const uint32_t i = b + l;
+      const bool cand = i < w1 - w0 && big_cand(lb[i]);   // (other positions are never read: nothing written)
       const uint64_t m = __ballot(cand);
-      if (cand) q[qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = p;
+      if (cand) q[qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint16_t)i;
       qn += (uint32_t)__builtin_popcountll(m);
     }
     wave_sync();
-    for (uint32_t j = l; j < qn; j += WAVE) {
-      const uint32_t p = q[j];
+    uint32_t ns = 0;
+    for (uint32_t j0 = 0; j0 < qn; j0 += WAVE) {   // (wave-uniform trips: the slow-queue gather is a wave op)
+      const uint32_t j = j0 + l, i = j < qn ? q[j] : 0u, p = w0 + i;
       uint32_t e = 0, v = 0;
-#ifndef YGM_SCAN_NOPARSE
-      {
-        GCur c; c.init(u0p, n0); c.pos = p;
+      bool slow = false;
+      if (j < qn) {
+        GCur c; c.init(lb, se - w0); c.pos = i;
         uint32_t kind;
-        if (big_skip(c, kind, 8) && !c.err) {
-          e = c.pos | (kind == 0 ? 0x80000000u : 0u);
-#ifndef YGM_SCAN_NOVAL
-          if (c.pos - p <= BIG_VCAP) {
-#else
-          if (false) {   // experiment: ends only; every struct validated by k_merge_big's helper waves
-#endif
-            GCur w; w.init(u0p, n0); w.pos = p;
-            const GStruct g = big_struct(w, flags);
-            v = g.ok && w.pos == c.pos && g.len != 0 && g.len < 0xFFFFFFFFull ? (uint32_t)g.len : 0xFFFFFFFFu;
+        uint64_t cv = 0;
+        bool ok = big_skip(c, kind, 8, &cv) && !c.err;
+        const uint8_t* vb = lb;   // (the string's bytes: the stage, or U0 after a redo)
+        uint32_t cp = c.pos + w0;
+        if (!ok && c.err == ST_MALFORMED && se < n0) {   // ran into the stage's end: the parse again from global memory
+          GCur g; g.init(u0p, n0); g.pos = p;
+          ok = big_skip(g, kind, 8, &cv) && !g.err;
+          cp = g.pos; c.nm = g.nm; vb = u0p;
+        }
+        if (ok) {
+          e = cp | (kind == 0 ? 0x80000000u : 0u);
+          const uint32_t info = lb[i], ref = info & 31u;
+          if (cp - p <= BIG_VCAP) {
+            if (info == 0u || ((info & 0xC0u) && (ref == 1u || ref == 4u))) {
+              // GC, or an Item with an origin and deleted / string content (text's structs): big_struct's verdict
+              // from the skip parse itself (its varuints minimal, the string strict UTF-8, a non-zero length)
+              const int64_t len = c.nm ? -1 : ref == 4u ? gutf8_u16(vb + (cv >> 32), (uint32_t)cv) : (int64_t)cv;
+              v = len > 0 && len < 0xFFFFFFFFll ? (uint32_t)len : 0xFFFFFFFFu;
+            } else {
+              slow = true;   // the other kinds: big_struct in k_big_val (its registers would halve this kernel's waves)
+            }
           }
         }
       }
-#endif
-      S.nx[P.pb + p] = e;
-      S.vl[P.pb + p] = v;
+      // the slow candidates gather at the queue's front (entries < j0 + 64 are read, entries past it are not yet)
+      const uint64_t sm = __ballot(slow);
+      if (slow) q[ns + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u))] = (uint16_t)i;
+      ns += (uint32_t)__builtin_popcountll(sm);
+      if (j < qn) {
+        S.nx[P.pb + p] = e;
+        S.vl[P.pb + p] = v;
+      }
+    }
+    if (ns) {   // one append per wave and task (a counter every wave of the grid shares)
+      uint64_t base = 0;
+      if (l == 0) base = atomicAdd(&S.cnt[4], (unsigned long long)ns);
+      base = __shfl(base, 0);
+      for (uint32_t k = l; k < ns; k += WAVE)   // (past the queue: v = 0, k_merge_big validates it)
+        if (base + k < S.vq_cap) S.vq[base + k] = make_uint2(T.x, w0 + q[k]);
     }
     wave_sync();   // (the queue is rewritten by the next task)
+  }
+}
+// the scan's slow queue: big_struct's verdict for the candidates of other kinds (after k_big_scan, same stream)
+__global__ __launch_bounds__(256) void k_big_val(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+                                                 const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
+                                                 uint32_t flags, BigScan S) {
+  const uint64_t nq = *(volatile unsigned long long*)&S.cnt[4], n = nq < S.vq_cap ? nq : S.vq_cap;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    const uint2 Q = S.vq[i];
+    const BigPick P = S.pick[Q.x];
+    const uint8_t* u0p = arena + upd_off[doc_upd[fb_list[Q.x]] + P.u0];
+    const uint32_t end = S.nx[P.pb + Q.y] & 0x7FFFFFFFu;
+    GCur w; w.init(u0p, P.n0); w.pos = Q.y;
+    const GStruct g = big_struct(w, flags);
+    S.vl[P.pb + Q.y] = g.ok && w.pos == end && g.len != 0 && g.len < 0xFFFFFFFFull ? (uint32_t)g.len : 0xFFFFFFFFu;
   }
 }
 // the struct start 2^(k+1) structs after tile position i < BT_CH (k = -1: the next one, from nx), or BJ_NONE
@@ -2401,6 +2451,21 @@ YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint3
       T.jp[k][i] = (uint16_t)(a < CF::CH ? big_jump(T, k - 1, a) : BJ_NONE);
     }
   }
+}
+// after a tile's spec (cmd 1, C.vs = the verdict words): the helper waves touch the next tile's bytes and scan ends and
+// both tiles' verdicts, a load per 128-byte line, so that wave 0's loads of them after its chain follow hit L2
+template <uint32_t CH, uint32_t NT>
+YDEV void big_prefetch(const BigCmd& C, uint32_t t0) {
+  const uint32_t a = C.at, n0 = C.n0;
+  const uint32_t b0 = a + CH < n0 ? a + CH : n0, b1 = a + 2u * CH + 128u < n0 ? a + 2u * CH + 128u : n0;
+  const uint32_t nb = (b1 - b0 + 127u) / 128u, nw = (b1 - a + 31u) / 32u;
+  const uint32_t* const vl = (const uint32_t*)C.vs;
+  uint32_t acc = 0;
+  for (uint32_t i = t0; i < nb + 2u * nw; i += NT) {
+    if (i < nb) acc ^= C.u0p[b0 + i * 128u];
+    else { const uint32_t k = i - nb; acc ^= (k < nw ? C.aux : vl)[a + (k < nw ? k : k - nw) * 32u]; }
+  }
+  asm volatile("" ::"v"(acc));   // (the loads are the point)
 }
 // struct records [vs, ns) (byte ranges in rs / re, LDS): the scan's verdict (vl, C.aux) where it has one, else
 // validated from global memory, then stored with their clock lengths; true if any is not what write_struct emits
@@ -2944,6 +3009,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
       else if (C.cmd == 4) { if (!big_ds_canon<CF::THREADS>(C, threadIdx.x)) s_cmd.tb = 1; }
       else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, threadIdx.x)) L.bad = 1;
       __syncthreads();
+      if (C.cmd == 1) big_prefetch<CF::CH, CF::THREADS - WAVE>(C, threadIdx.x - WAVE);   // (while wave 0 follows the chain)
     }
   }
   const uint32_t l = threadIdx.x;
@@ -3044,7 +3110,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
     wave_sync();
     if (!spec) return;
     const uint64_t dg0 = DIAG_NOW();
-    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.n0 = n0; s_cmd.aux = nxg; }
+    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.n0 = n0; s_cmd.aux = nxg; s_cmd.u0p = u0p; s_cmd.vs = (uint64_t)vlg; }
     __syncthreads();
     big_spec<CF>(T0, nxg, at, mis, n0, l);
     __syncthreads();
@@ -3574,15 +3640,17 @@ size_t ygm_k_big_rec_bytes() { return sizeof(BigRec); }
 static void big_scan_layout(uint32_t n_fb, uint64_t fb_bytes, BigScan& S, uint8_t* base, size_t& total) {
   S.ntask_cap = fb_bytes / BIG_SCAN_CH + n_fb + 1;
   S.npos_cap = fb_bytes + 16ull * n_fb + 16;
+  S.vq_cap = S.npos_cap / 4 + 1024;
   size_t o = 0;
   auto carve = [&](size_t bytes) { const size_t a = o; o += (bytes + 255) & ~(size_t)255; return base ? base + a : nullptr; };
-  S.cnt = (unsigned long long*)carve(32);
+  S.cnt = (unsigned long long*)carve(64);
   S.pick = (BigPick*)carve(sizeof(BigPick) * (size_t)n_fb);
   S.task = (uint2*)carve(sizeof(uint2) * S.ntask_cap);
   S.nx = (uint32_t*)carve(4 * S.npos_cap);
   S.vl = (uint32_t*)carve(4 * S.npos_cap);
   S.llist = (uint32_t*)carve(4ull * n_fb);
   S.mlist = (uint32_t*)carve(4ull * n_fb);
+  S.vq = (uint2*)carve(sizeof(uint2) * S.vq_cap);
   total = o;
 }
 // device pointers of the scan's counters and of its two document lists (after ygm_k_launch_big_scan)
@@ -3597,11 +3665,13 @@ int ygm_k_launch_big_scan(const uint8_t* arena, const uint64_t* upd_off, const u
   if (n_fb == 0) return 0;
   BigScan S; size_t total;
   big_scan_layout(n_fb, fb_bytes, S, (uint8_t*)scan, total);
-  if (hipMemsetAsync(S.cnt, 0, 32, s) != hipSuccess) return launch_rc(__func__);
+  if (hipMemsetAsync(S.cnt, 0, 64, s) != hipSuccess) return launch_rc(__func__);
   hipLaunchKernelGGL(k_big_pick, dim3((n_fb + 15) / 16), dim3(1024), 0, s, upd_off, doc_upd, fb_list, n_fb, S);
   // the scan: a persistent grid over the tasks (at most 16 workgroups per CU; the task count is on the device)
   const uint64_t g = S.ntask_cap < 16ull * device_cus() ? S.ntask_cap : 16ull * device_cus();
   hipLaunchKernelGGL(k_big_scan, dim3((uint32_t)g), dim3(256), 0, s, arena, upd_off, doc_upd, fb_list, flags, S);
+  const uint64_t gv = S.vq_cap / 256 + 1 < 8ull * device_cus() ? S.vq_cap / 256 + 1 : 8ull * device_cus();
+  hipLaunchKernelGGL(k_big_val, dim3((uint32_t)gv), dim3(256), 0, s, arena, upd_off, doc_upd, fb_list, flags, S);
   return launch_rc(__func__);
 }
 // large = 0: the mid size, large = 1: the 16-wave size, over the fb_list indices in fbx[0, n) (the mid size sends a

@@ -240,12 +240,13 @@ YDEV_NI bool gany_skip(GCur& c, uint64_t n) {
 // Skip-only parse of one U0 struct (the sequential part of the walk): the bytes it spans and its
 // kind (0 GC, 1 Item); validation and lengths come later, in parallel (big_struct).  false: a
 // Skip, Any / Doc content or an unknown ref -- the document goes on to the general path.
+// cv (the scan): GC's / ContentDeleted's length, or ContentString's bytes as start << 32 | length
 template <bool ANY = false>   // ANY: any ContentAny (the out-of-line fallback parse); else scalar values only
-YDEV bool big_skip(GCur& c, uint32_t& kind, uint64_t jcap = ~0ull) {   // jcap: most ContentJSON entries taken
+YDEV bool big_skip(GCur& c, uint32_t& kind, uint64_t jcap = ~0ull, uint64_t* cv = nullptr) {   // jcap: most ContentJSON entries taken
   const uint32_t info = c.u8();
   kind = 1;
   if (c.err || info == 10u) return false;
-  if ((info & 31u) == 0u) { kind = 0; c.vu(); return !c.err; }
+  if ((info & 31u) == 0u) { kind = 0; const uint64_t n = c.vu(); if (cv) *cv = n; return !c.err; }
   uint32_t l;
   if (info & 0x80u) { c.vu(); c.vu(); }
   if (info & 0x40u) { c.vu(); c.vu(); }
@@ -255,9 +256,10 @@ YDEV bool big_skip(GCur& c, uint32_t& kind, uint64_t jcap = ~0ull) {   // jcap: 
     if (info & 0x20u) c.buf(l);
   }
   switch (info & 31u) {
-    case 1: c.vu(); break;
+    case 1: { const uint64_t n = c.vu(); if (cv) *cv = n; break; }
     case 2: { const uint64_t n = c.vu(); if (n > jcap) return false; for (uint64_t k = 0; k < n && !c.err; k++) c.buf(l); break; }
-    case 3: case 4: case 5: c.buf(l); break;
+    case 4: { const uint32_t s = c.buf(l); if (cv) *cv = ((uint64_t)s << 32) | l; break; }
+    case 3: case 5: c.buf(l); break;
     case 6: c.buf(l); c.buf(l); break;
     case 7: { const uint64_t tr = c.vu(); if (tr == 3 || tr == 5) c.buf(l); break; }
     case 8: {

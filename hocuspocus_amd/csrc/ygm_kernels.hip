@@ -2240,7 +2240,13 @@ struct BigScan {
 };
 // U0 bytes past which a document goes to the 16-wave size directly: the mid size walks 1 KB tiles with 4 waves,
 // so its time on a snapshot of megabytes (the C3 batch's largest documents) would be the batch's critical path
-constexpr uint32_t BIG_MID_U0 = 2048u * 1024u;
+#ifndef YGM_MID_OCC
+#define YGM_MID_OCC 4   // mid-size workgroups per CU the register budget is cut for
+#endif
+#ifndef YGM_BIG_MID_KB
+#define YGM_BIG_MID_KB 2048
+#endif
+constexpr uint32_t BIG_MID_U0 = YGM_BIG_MID_KB * 1024u;
 // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item ref 1..8 without bit 0x20
 // next to an origin.  The scan writes nx / vl for these positions only; the follow and the validation test the byte
 // before they read them (a struct the chain meets elsewhere is parsed from global memory)
@@ -2984,7 +2990,7 @@ YDEV bool big_clock_ranges(BigBlk* blk, const BigRec* rec, const BigCmd& C, uint
 }
 
 template <class CF>
-__global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+__global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merge_big(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                     const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
                                                     uint32_t flags, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
@@ -3096,8 +3102,9 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
   // tile origin tc0 (U0 position), tb = tc0 rounded down to a 16-byte aligned address: LDS byte j of
   // the tile is U0 byte tb + j, so tile cursors run in tile coordinates (pointers stay inside T0)
   uint32_t tc0 = 0, tb = 0, tn = 0;                        // tn: tile cursor end (tile coordinates)
-  uint64_t dg_spec = 0, dg_val = 0;                        // diagnostic build: time in the speculative parse / validation
+  [[maybe_unused]] uint64_t dg_spec = 0, dg_val = 0;       // diagnostic build: time in the speculative parse / validation
   DIAG_C(uint64_t dc_blk = 0, dc_step = 0, dc_st = 0, dc_glob = 0, dc_hslow = 0;)   // ... and follow counts
+  DIAG_C(uint64_t dt_hdr = 0, dt_st = 0, dt_tail = 0, dt_tile = 0;)                   // ... and follow time by part
   const uint8_t* const tp = (const uint8_t*)T0.b;
   auto load_tile = [&](uint32_t at, bool spec) {
     const uint32_t mis = (uint32_t)((uintptr_t)(u0p + at) & 15u);
@@ -3151,7 +3158,9 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
       wave_sync();
     };
     for (uint64_t b = 0; b < nb && !bad; b++) {
+      DIAG_C(const uint64_t dq0 = DIAG_NOW();)
       if (!have || pos >= tc0 + CF::CH) { if (have) validate(); load_tile(pos, true); have = true; }
+      DIAG_C(const uint64_t dq1 = DIAG_NOW(); dt_tile += dq1 - dq0;)
       uint64_t hn, hc, hk;
       uint32_t he;
       bool hnm;
@@ -3176,6 +3185,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
       }
       acanon &= !hnm;
       uint32_t fgc = 0, lgc = 0;
+      DIAG_C(const uint64_t dq2 = DIAG_NOW(); dt_hdr += dq2 - dq1;)
       for (uint32_t q = 0; q < bnst && !bad;) {
         if (pos >= tc0 + CF::CH) { validate(); load_tile(pos, true); }
         // up to 64 of the block's structs per step: lane j finds the start of struct q + j by composing
@@ -3214,10 +3224,12 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
         NS++; q++;
         pos = end;
       }
+      DIAG_C(const uint64_t dq3 = DIAG_NOW(); dt_st += dq3 - dq2;)
       if (!bad) {   // staged in LDS, stored 64 at a time (a store per block would be waited on by the next block's loads)
         if (l == 0) { BigBlk& B = s_blk[bq]; B.b1 = pos; B.first_gc = (uint8_t)fgc; B.last_gc = (uint8_t)lgc; }
         if (++bq == 64u) flush_blk(b + 1);
       }
+      DIAG_C(dt_tail += DIAG_NOW() - dq3;)
     }
     if (!bad && bq) flush_blk(nb);
     if (have && !bad) validate();
@@ -3231,7 +3243,9 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? 4 : 1) void k_merge_big(cons
   DIAG_PUT(6, dg_spec); DIAG_PUT(7, dg_val);
   DIAG_C(if (l == 0) { atomicAdd(&ygm_diag[16], (unsigned long long)dc_blk); atomicAdd(&ygm_diag[17], (unsigned long long)dc_step);
                        atomicAdd(&ygm_diag[18], (unsigned long long)dc_st); atomicAdd(&ygm_diag[19], (unsigned long long)dc_glob);
-                       atomicAdd(&ygm_diag[20], (unsigned long long)dc_hslow); })
+                       atomicAdd(&ygm_diag[20], (unsigned long long)dc_hslow);
+                       atomicAdd(&ygm_diag[25], dt_tile); atomicAdd(&ygm_diag[26], dt_hdr); atomicAdd(&ygm_diag[27], dt_st);
+                       atomicAdd(&ygm_diag[28], dt_tail); })
 #endif
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // validated lengths before the clock-range pass
   wave_sync();

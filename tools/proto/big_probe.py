@@ -71,8 +71,12 @@ if len(sys.argv) > 1 and sys.argv[1] == "splice":   # tests/tile_docs.ds_splice_
         ok = [res[i] == oracle.merge_updates(us) for i, us in enumerate(docs)]
         print({"seed": seed, "parity": ok, "big_docs": int(dg[21]), "spliced": int(dg[22])}, flush=True)
     sys.exit(0)
+C5 = os.environ.get("C5") == "1"   # C5-shaped documents (XmlFragment, 10 000 clients) instead of C3-shaped
 for mb in ([float(x) for x in os.environ['BIG_MB'].split(',')] if os.environ.get('BIG_MB') else (0.3, 1, 3, 10)):
-    arena, upd_off, doc_upd = synth.big_docs(1, int(mb * 1e6), 1024, max_clients=64, max_k=200, seed=8)
+    if C5:
+        arena, upd_off, doc_upd = synth.big_docs(1, int(mb * 1e6), 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=9)
+    else:
+        arena, upd_off, doc_upd = synth.big_docs(1, int(mb * 1e6), 1024, max_clients=64, max_k=200, seed=8)
     n = 1
     upd_doc = np.zeros(len(upd_off) - 1, np.uint32)
     ms = []
@@ -93,6 +97,8 @@ for mb in ([float(x) for x in os.environ['BIG_MB'].split(',')] if os.environ.get
         dg = np.zeros(32, np.uint64)
         L.ygm_diag_read(dg.ctypes.data, 1)
         line["ds_plan"] = {"big_docs": int(dg[21]), "spliced": int(dg[22]), "ds_values": int(dg[23]), "ds_entries": int(dg[24])}
+        line["follow"] = {"blocks": int(dg[16]), "steps": int(dg[17]), "structs": int(dg[18]), "global": int(dg[19]), "hdr_slow": int(dg[20]),
+                          "us_tile_hdr_structs_tail (all runs)": [int(dg[i]) / 100.0 for i in (25, 26, 27, 28)]}
         t = ts.reshape(16384, 8)[0].astype(np.int64)
         d = np.diff(t[:6]) * 10 / 1000.0
         if dsmode:   # slots 6 / 7: where each pass's delete-set part starts (absolute stamps)

@@ -2363,7 +2363,10 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
               const int64_t len = c.nm ? -1 : ref == 4u ? gutf8_u16(vb + (cv >> 32), (uint32_t)cv) : (int64_t)cv;
               v = len > 0 && len < 0xFFFFFFFFll ? (uint32_t)len : 0xFFFFFFFFu;
             } else {
-              slow = true;   // the other kinds: big_struct in k_big_val (its registers would halve this kernel's waves)
+              // the other kinds: big_struct in k_big_val (its registers would halve this kernel's waves), for a parse
+              // whose end could start the next struct (most candidates are bytes inside other structs: their ends
+              // land anywhere); the last struct of a block fails this and is validated by k_merge_big
+              slow = cp >= se || big_cand(lb[cp - w0]);
             }
           }
         }

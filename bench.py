@@ -721,6 +721,11 @@ def run_rank(args, rank, world, dist, be, dev=None):
         a, o, dd = synth.text_updates_docs(idx, args.updates)
         cm = {"arena": a, "upd_off": o, "doc_upd": dd, "n": len(idx), "n_upd": int(dd[-1]), "bytes": len(a)}
         cm["da"], cm["do"], cm["dd"] = be.put(a, 64), be.put(o.view(np.int64)), be.put(dd.view(np.int32))
+        lm = np.diff(o.astype(np.int64))
+        if isinstance(be, GpuBackend) and lm.max(initial=0) < 65536:   # the compact input form, as the headline
+            cm["doff"] = be.put(o[dd].view(np.int64))
+            cm["dlen"] = be.put(lm.astype(np.uint16).view(np.int16))
+            del lm
         sm = max(args.steps // 4, 2)
         dtm, kmsm, outm, rm = time_merge(be, cm, sm, 1, dist)
         dtm = allmax(dtm, dist, dev)

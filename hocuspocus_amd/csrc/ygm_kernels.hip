@@ -2233,11 +2233,15 @@ struct BigScan {
   unsigned long long* cnt;   // [0] positions carved, [1] tasks, [2] / [3] entries of llist / mlist, [4] slow queue
   BigPick* pick;             // per large document (index into fb_list)
   uint2* task;               // (document, chunk of BIG_SCAN_CH positions)
-  uint32_t *nx, *vl;
+  uint32_t* nv;              // per U0 position (candidates only): big_word
   uint32_t *llist, *mlist;   // fb_list indices by U0 size: over BIG_MID_U0 (the 16-wave size) / the rest (the mid size)
   uint2* vq;                 // slow queue (document, position): candidates k_big_val validates
   uint64_t ntask_cap, npos_cap, vq_cap;
 };
+// the scan's word of a U0 position: bits 0-14 the byte length of the struct parsed there (0: no parse, or 32 KB or
+// more), bit 15 GC, bits 16-31 its verdict -- the clock length (1 .. 0xFFFE), 0xFFFF refused, 0 none (k_merge_big
+// validates it from global memory)
+YDEV uint32_t big_v16(uint64_t len, bool ok) { return !ok ? 0xFFFFu : len <= 0xFFFEull ? (uint32_t)len : 0u; }
 // U0 bytes past which a document goes to the 16-wave size directly: the mid size walks 1 KB tiles with 4 waves,
 // so its time on a snapshot of megabytes (the C3 batch's largest documents) would be the batch's critical path
 #ifndef YGM_MID_OCC
@@ -2354,14 +2358,14 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
           cp = g.pos; c.nm = g.nm; vb = u0p;
         }
         if (ok) {
-          e = cp | (kind == 0 ? 0x80000000u : 0u);
+          e = cp - p < 0x8000u ? (cp - p) | (kind == 0 ? 0x8000u : 0u) : 0u;
           const uint32_t info = lb[i], ref = info & 31u;
           if (cp - p <= BIG_VCAP) {
             if (info == 0u || ((info & 0xC0u) && (ref == 1u || ref == 4u))) {
               // GC, or an Item with an origin and deleted / string content (text's structs): big_struct's verdict
               // from the skip parse itself (its varuints minimal, the string strict UTF-8, a non-zero length)
               const int64_t len = c.nm ? -1 : ref == 4u ? gutf8_u16(vb + (cv >> 32), (uint32_t)cv) : (int64_t)cv;
-              v = len > 0 && len < 0xFFFFFFFFll ? (uint32_t)len : 0xFFFFFFFFu;
+              v = big_v16((uint64_t)len, len > 0 && len < 0xFFFFFFFFll);
             } else {
               // the other kinds: big_struct in k_big_val (its registers would halve this kernel's waves), for a parse
               // whose end could start the next struct (most candidates are bytes inside other structs: their ends
@@ -2375,10 +2379,7 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
       const uint64_t sm = __ballot(slow);
       if (slow) q[ns + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u))] = (uint16_t)i;
       ns += (uint32_t)__builtin_popcountll(sm);
-      if (j < qn) {
-        S.nx[P.pb + p] = e;
-        S.vl[P.pb + p] = v;
-      }
+      if (j < qn) S.nv[P.pb + p] = e | (v << 16);
     }
     if (ns) {   // one append per wave and task (a counter every wave of the grid shares)
       uint64_t base = 0;
@@ -2399,10 +2400,10 @@ __global__ __launch_bounds__(256) void k_big_val(const uint8_t* __restrict__ are
     const uint2 Q = S.vq[i];
     const BigPick P = S.pick[Q.x];
     const uint8_t* u0p = arena + upd_off[doc_upd[fb_list[Q.x]] + P.u0];
-    const uint32_t end = S.nx[P.pb + Q.y] & 0x7FFFFFFFu;
+    const uint32_t wd = S.nv[P.pb + Q.y], end = Q.y + (wd & 0x7FFFu);
     GCur w; w.init(u0p, P.n0); w.pos = Q.y;
     const GStruct g = big_struct(w, flags);
-    S.vl[P.pb + Q.y] = g.ok && w.pos == end && g.len != 0 && g.len < 0xFFFFFFFFull ? (uint32_t)g.len : 0xFFFFFFFFu;
+    S.nv[P.pb + Q.y] = (wd & 0xFFFFu) | (big_v16(g.len, g.ok && w.pos == end && g.len != 0 && g.len < 0xFFFFFFFFull) << 16);
   }
 }
 // the struct start 2^(k+1) structs after tile position i < BT_CH (k = -1: the next one, from nx), or BJ_NONE
@@ -2446,9 +2447,9 @@ YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint3
   for (uint32_t i = t0; i < CF::CH; i += CF::THREADS) {
     uint32_t e = 0;
     if (at + i < n0 && big_cand(((const uint8_t*)T.b)[mis + i])) {
-      const uint32_t v = nxg[at + i];
-      const uint32_t rel = (v & 0x7FFFFFFFu) - at;
-      if (v && rel < 0x8000u) e = rel | ((v >> 31) << 15);
+      const uint32_t v = nxg[at + i], d = v & 0x7FFFu;
+      const uint32_t rel = i + d;
+      if (d && rel < 0x8000u) e = rel | (v & 0x8000u);
     }
     T.nx[i] = (uint16_t)e;
   }
@@ -2461,29 +2462,26 @@ YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint3
     }
   }
 }
-// after a tile's spec (cmd 1, C.vs = the verdict words): the helper waves touch the next tile's bytes and scan ends and
-// both tiles' verdicts, a load per 128-byte line, so that wave 0's loads of them after its chain follow hit L2
+// after a tile's spec (cmd 1): the helper waves touch the next tile's bytes and both tiles' scan words, a load per
+// 128-byte line, so that wave 0's loads of them after its chain follow (the next spec, this tile's verdicts) hit L2
 template <uint32_t CH, uint32_t NT>
 YDEV void big_prefetch(const BigCmd& C, uint32_t t0) {
   const uint32_t a = C.at, n0 = C.n0;
   const uint32_t b0 = a + CH < n0 ? a + CH : n0, b1 = a + 2u * CH + 128u < n0 ? a + 2u * CH + 128u : n0;
   const uint32_t nb = (b1 - b0 + 127u) / 128u, nw = (b1 - a + 31u) / 32u;
-  const uint32_t* const vl = (const uint32_t*)C.vs;
   uint32_t acc = 0;
-  for (uint32_t i = t0; i < nb + 2u * nw; i += NT) {
-    if (i < nb) acc ^= C.u0p[b0 + i * 128u];
-    else { const uint32_t k = i - nb; acc ^= (k < nw ? C.aux : vl)[a + (k < nw ? k : k - nw) * 32u]; }
-  }
+  for (uint32_t i = t0; i < nb + nw; i += NT) acc ^= i < nb ? (uint32_t)C.u0p[b0 + i * 128u] : C.aux[a + (i - nb) * 32u];
   asm volatile("" ::"v"(acc));   // (the loads are the point)
 }
-// struct records [vs, ns) (byte ranges in rs / re, LDS): the scan's verdict (vl, C.aux) where it has one, else
+// struct records [vs, ns) (byte ranges in rs / re, LDS): the scan's verdict (its word, C.aux) where it has one, else
 // validated from global memory, then stored with their clock lengths; true if any is not what write_struct emits
 template <uint32_t NT>
 YDEV bool big_validate(const uint32_t* rs, const uint32_t* re, BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0) {
   bool vbad = false;
   for (uint64_t i = C.vs + t0; i < C.ns; i += NT) {
     BigRec R; R.start = rs[i - C.vs]; R.end = re[i - C.vs];
-    uint64_t len = big_cand(C.u0p[R.start]) ? C.aux[R.start] : 0u;   // (the scan wrote candidate positions only)
+    const uint32_t v16 = big_cand(C.u0p[R.start]) ? C.aux[R.start] >> 16 : 0u;   // (the scan wrote candidate positions only)
+    uint64_t len = v16 == 0xFFFFu ? 0xFFFFFFFFull : v16;
     if (len == 0u) {   // (the scan's end for R.start, when it has one, is R.end: the chain took it from nx)
       GCur w; w.init(C.u0p, C.n0); w.pos = R.start;
       const GStruct g = big_struct(w, flags);
@@ -3095,8 +3093,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   const uint32_t n0 = (uint32_t)(upd_off[ua + U0 + 1] - upd_off[ua + U0]);
   const uint64_t ncap = n0 + 1u;                            // structs take >= 2 bytes; delete-set values >= 1
   const BigPick PK = S.pick[w];
-  const uint32_t* const nxg = S.nx + PK.pb;                 // the scan's ends and verdicts of U0's positions
-  const uint32_t* const vlg = S.vl + PK.pb;
+  const uint32_t* const nxg = S.nv + PK.pb;                 // the scan's words (ends and verdicts) of U0's positions
   if (l == 0 && (PK.n0 != n0 || PK.u0 != U0)) L.bad = 1;   // (not scanned: the sequential kernel takes it)
   wave_sync();
   uint64_t base = 0, sbase = 0, nb = 0, NS = 0;
@@ -3120,7 +3117,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
     wave_sync();
     if (!spec) return;
     const uint64_t dg0 = DIAG_NOW();
-    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.n0 = n0; s_cmd.aux = nxg; s_cmd.u0p = u0p; s_cmd.vs = (uint64_t)vlg; }
+    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.n0 = n0; s_cmd.aux = nxg; s_cmd.u0p = u0p; }
     __syncthreads();
     big_spec<CF>(T0, nxg, at, mis, n0, l);
     __syncthreads();
@@ -3130,7 +3127,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   auto validate = [&]() {                                  // records [vs, NS): all start inside the tile
     const uint64_t dg0 = DIAG_NOW();
     if (l == 0) {
-      s_cmd.cmd = 2; s_cmd.vs = vs; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.u0p = u0p; s_cmd.n0 = n0; s_cmd.aux = vlg;
+      s_cmd.cmd = 2; s_cmd.vs = vs; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.u0p = u0p; s_cmd.n0 = n0; s_cmd.aux = nxg;
     }
     __syncthreads();                                       // lane 0's byte ranges and the command before every wave reads them
     if (big_validate<CF::THREADS>(s_rst, s_ren, rec, s_cmd, flags, l)) L.bad = 1;
@@ -3663,8 +3660,7 @@ static void big_scan_layout(uint32_t n_fb, uint64_t fb_bytes, BigScan& S, uint8_
   S.cnt = (unsigned long long*)carve(64);
   S.pick = (BigPick*)carve(sizeof(BigPick) * (size_t)n_fb);
   S.task = (uint2*)carve(sizeof(uint2) * S.ntask_cap);
-  S.nx = (uint32_t*)carve(4 * S.npos_cap);
-  S.vl = (uint32_t*)carve(4 * S.npos_cap);
+  S.nv = (uint32_t*)carve(4 * S.npos_cap);
   S.llist = (uint32_t*)carve(4ull * n_fb);
   S.mlist = (uint32_t*)carve(4ull * n_fb);
   S.vq = (uint2*)carve(sizeof(uint2) * S.vq_cap);

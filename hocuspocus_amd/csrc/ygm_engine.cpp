@@ -230,12 +230,11 @@ int ygm_open(int device, uint32_t flags, ygm_ctx** out) {
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return YGM_EDEVICE;
   ygm_ctx* c = new ygm_ctx();
   c->device = device; c->flags = flags;
-  // stream2 at the high priority: a queue of its own (a process with more streams than hardware queues shares them,
-  // and two streams on one queue run their kernels one after the other)
-  int prio_lo = 0, prio_hi = 0;
+  // stream2 (the large-document tier's 16-wave size) is created at the high priority on first use: a queue of its own
+  // (a process with more streams than hardware queues shares them, and two streams on one queue run their kernels
+  // one after the other); contexts that never run that size (the host API's stage contexts, most pool members) do
+  // not hold one
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess || hipEventCreate(&c->e2) != hipSuccess ||
       hipEventCreate(&c->e3) != hipSuccess) {
     delete c;
@@ -253,6 +252,7 @@ void ygm_close(ygm_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->stream2) (void)hipStreamSynchronize(c->stream2);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
                     &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->big_scan, &c->big_up, &c->lens_off, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws, &c->sn_claim, &c->sn_pay,
@@ -264,7 +264,7 @@ void ygm_close(ygm_ctx* c) {
   for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
   if (c->h_meta) (void)hipHostFree(c->h_meta);
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  if (c->stream2) { (void)hipStreamSynchronize(c->stream2); (void)hipStreamDestroy(c->stream2); }
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   delete c;
 }
 
@@ -443,9 +443,21 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
                                     c->out_len.as<uint64_t>(), c->status.as<int32_t>(), P.meta, c->big_list.as<uint32_t>(), c->big_blk.p,
                                     blk_cap, c->big_rec.p, rec_cap, P.slot_total, P.out_cap, c->big_scan.p, m.fb_bytes, st);
     };
+    // once the 16-wave size runs on stream2, every exit waits for it: its kernels write the outputs, the counters
+    // and the tier's scratch, which the next call on this context reuses on `stream`
+    struct Join2 {
+      hipStream_t st = nullptr;
+      ~Join2() { if (st) (void)hipStreamSynchronize(st); }
+    } join2;
     if (cnt[2]) {
+      if (!c->stream2) {   // created on first use, only on contexts that run the 16-wave size
+        int prio_lo = 0, prio_hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        HIPCHK(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi));
+      }
       HIPCHK(hipEventRecord(c->e2, s));
       HIPCHK(hipStreamWaitEvent(c->stream2, c->e2, 0));
+      join2.st = c->stream2;
       if (launch(1, llist, (uint32_t)cnt[2], c->stream2)) return YGM_EDEVICE;
       HIPCHK(hipEventRecord(c->e3, c->stream2));
     }
@@ -453,7 +465,7 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
     if ((e = read_meta(c, s, m, P.meta))) return e;
     if (m.fault) return YGM_EDEVICE;
     if (m.mid_defer && launch(1, c->big_up.as<uint32_t>(), m.mid_defer, s)) return YGM_EDEVICE;
-    if (cnt[2]) HIPCHK(hipStreamWaitEvent(s, c->e3, 0));
+    if (cnt[2]) { HIPCHK(hipStreamWaitEvent(s, c->e3, 0)); join2.st = nullptr; }
     HIPCHK(hipEventRecord(c->e1, s));
     if ((e = read_meta(c, s, m, P.meta))) return e;
     if (m.fault) return YGM_EDEVICE;

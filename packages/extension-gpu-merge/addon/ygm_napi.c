@@ -38,6 +38,8 @@ typedef struct {
   Job *head, *tail; int stop;
   napi_threadsafe_function tsfn;   /* worker -> event loop: settles a finished job's promise */
   int refs;                        /* jobs whose completion is pending (the tsfn keeps the loop alive meanwhile) */
+  int closing;                     /* close() arrived while a job was in flight: stop once it has settled */
+  int owners;                      /* the JS external and the threadsafe function: freed when both are finalized */
 } Handle;
 
 struct Job {
@@ -54,6 +56,9 @@ struct Job {
   /* mergeMany: the caller's arena Buffer is read in place by the worker (held by a reference until the
      batch completes), not copied on the main thread */
   napi_ref arena_ref; int arena_borrowed;
+  /* the handle's JS external, held until the job settles: a dropped engine cannot be finalized (and its
+     Handle freed) while the worker or the threadsafe-function queue still refers to it */
+  napi_ref handle_ref;
   double exec_ms;       /* worker: the engine call + copy-out of its context-owned results */
 };
 
@@ -78,32 +83,51 @@ static void *worker_main(void *arg) {
   return NULL;
 }
 
-/* runs on the event loop for every finished job */
+static void handle_stop(Handle *h);
+
+/* runs on the event loop for every finished job (env NULL: the environment is being torn down, the
+   promise cannot settle; the job's memory is released with the process) */
 static void tsfn_call(napi_env env, napi_value js_cb, void *context, void *data) {
   (void)js_cb;
   Handle *h = (Handle *)context;
   Job *j = (Job *)data;
-  if (env) job_complete(env, j);
-  if (env && --h->refs == 0) napi_unref_threadsafe_function(env, h->tsfn);
+  if (!env) return;
+  job_complete(env, j);
+  if (--h->refs == 0) napi_unref_threadsafe_function(env, h->tsfn);
+  if (h->closing && !h->busy) handle_stop(h);   /* a close() that waited for this job (last use of h here) */
 }
 
-/* joins the worker (after the jobs queued so far) and frees the context */
+/* joins the worker (after the jobs queued so far), releases the threadsafe function and frees the
+   context; the Handle itself is freed by the threadsafe function's finalizer, which runs only after every
+   queued completion has been delivered */
 static void handle_stop(Handle *h) {
-  if (h->has_thread) {
+  h->closing = 0;
+  const int had = h->has_thread;
+  if (had) {
     pthread_mutex_lock(&h->mu); h->stop = 1; pthread_cond_signal(&h->cv); pthread_mutex_unlock(&h->mu);
     pthread_join(h->thread, NULL);
     h->has_thread = 0;
-    napi_release_threadsafe_function(h->tsfn, napi_tsfn_release);
   }
   if (h->ctx) { ygm_close(h->ctx); h->ctx = NULL; }
+  if (had) napi_release_threadsafe_function(h->tsfn, napi_tsfn_release);   /* last: may finalize (free) h */
 }
 
+static void handle_release(Handle *h) {   /* (both finalizers run on the event loop) */
+  if (--h->owners > 0) return;
+  pthread_mutex_destroy(&h->mu); pthread_cond_destroy(&h->cv);
+  free(h);
+}
+static void tsfn_finalize(napi_env env, void *data, void *hint) {
+  (void)env; (void)hint;
+  handle_release((Handle *)data);
+}
+
+/* the JS external was collected: no job can be pending (each holds a reference to it) */
 static void handle_finalize(napi_env env, void *data, void *hint) {
   (void)env; (void)hint;
   Handle *h = (Handle *)data;
   handle_stop(h);
-  pthread_mutex_destroy(&h->mu); pthread_cond_destroy(&h->cv);
-  free(h);
+  handle_release(h);
 }
 
 static napi_value noop(napi_env env, napi_callback_info info) { (void)env; (void)info; return NULL; }
@@ -112,28 +136,35 @@ static napi_value noop(napi_env env, napi_callback_info info) { (void)env; (void
 static napi_value make_handle(napi_env env, ygm_ctx *ctx) {
   Handle *h = (Handle *)calloc(1, sizeof(Handle));
   h->ctx = ctx;
+  h->owners = 1;   /* the threadsafe function; the external adds itself below */
   pthread_mutex_init(&h->mu, NULL); pthread_cond_init(&h->cv, NULL);
   napi_value fn, name, ext;
   if (napi_create_function(env, "ygmSettle", NAPI_AUTO_LENGTH, noop, NULL, &fn) != napi_ok ||
       napi_create_string_utf8(env, "ygm.worker", NAPI_AUTO_LENGTH, &name) != napi_ok ||
-      napi_create_threadsafe_function(env, fn, NULL, name, 0, 1, NULL, NULL, h, tsfn_call, &h->tsfn) != napi_ok) {
+      napi_create_threadsafe_function(env, fn, NULL, name, 0, 1, h, tsfn_finalize, h, tsfn_call, &h->tsfn) != napi_ok) {
     if (ctx) ygm_close(ctx);
+    pthread_mutex_destroy(&h->mu); pthread_cond_destroy(&h->cv);
     free(h); napi_throw_error(env, NULL, "ygm: cannot create the worker's threadsafe function"); return NULL;
   }
   napi_unref_threadsafe_function(env, h->tsfn);   /* an idle engine does not keep Node alive */
   if (pthread_create(&h->thread, NULL, worker_main, h) != 0) {
-    napi_release_threadsafe_function(h->tsfn, napi_tsfn_abort);
-    if (ctx) ygm_close(ctx);
-    free(h); napi_throw_error(env, NULL, "ygm: cannot start the engine's worker thread"); return NULL;
+    if (ctx) { ygm_close(ctx); h->ctx = NULL; }
+    napi_release_threadsafe_function(h->tsfn, napi_tsfn_abort);   /* its finalizer frees h */
+    napi_throw_error(env, NULL, "ygm: cannot start the engine's worker thread"); return NULL;
   }
   h->has_thread = 1;
-  NAPI_CALL(env, napi_create_external(env, h, handle_finalize, NULL, &ext));
+  h->owners = 2;
+  if (napi_create_external(env, h, handle_finalize, NULL, &ext) != napi_ok) {
+    h->owners = 1;
+    handle_stop(h);
+    napi_throw_error(env, NULL, "ygm: cannot create the engine handle"); return NULL;
+  }
   return ext;
 }
 
 static Handle *get_handle_any(napi_env env, napi_value v) {
   Handle *h = NULL;
-  if (napi_get_value_external(env, v, (void **)&h) != napi_ok || !h || !h->has_thread) {
+  if (napi_get_value_external(env, v, (void **)&h) != napi_ok || !h || !h->has_thread || h->closing) {
     napi_throw_error(env, NULL, "ygm: closed or invalid engine handle");
     return NULL;
   }
@@ -141,7 +172,7 @@ static Handle *get_handle_any(napi_env env, napi_value v) {
 }
 static Handle *get_handle(napi_env env, napi_value v) {
   Handle *h = NULL;
-  if (napi_get_value_external(env, v, (void **)&h) != napi_ok || !h || !h->ctx || !h->has_thread) {
+  if (napi_get_value_external(env, v, (void **)&h) != napi_ok || !h || !h->ctx || !h->has_thread || h->closing) {
     napi_throw_error(env, NULL, "ygm: closed or invalid engine handle");
     return NULL;
   }
@@ -167,7 +198,10 @@ static napi_value js_close(napi_env env, napi_callback_info info) {
   size_t argc = 1; napi_value argv[1];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   Handle *h = NULL;
-  if (napi_get_value_external(env, argv[0], (void **)&h) == napi_ok && h && !h->busy) handle_stop(h);
+  if (napi_get_value_external(env, argv[0], (void **)&h) == napi_ok && h && h->has_thread) {
+    if (h->busy) h->closing = 1;   /* stops when the in-flight job has settled (tsfn_call) */
+    else handle_stop(h);
+  }
   return NULL;
 }
 
@@ -268,6 +302,7 @@ static void job_complete(napi_env env, Job *j) {
   const double t0 = now_ms();
   j->h->busy = 0;
   if (j->arena_ref) { napi_delete_reference(env, j->arena_ref); j->arena_ref = NULL; }
+  if (j->handle_ref) { napi_delete_reference(env, j->handle_ref); j->handle_ref = NULL; }
   napi_value result = NULL, err = NULL;
   if (j->op == 99) {
     napi_value a, b;
@@ -316,15 +351,18 @@ static void job_complete(napi_env env, Job *j) {
 }
 
 /* queues the job on its handle's worker thread */
-static napi_value submit(napi_env env, Job *j, const char *name) {
-  (void)name;
+static napi_value submit(napi_env env, Job *j, napi_value handle) {
   napi_value promise;
   Handle *h = j->h;
   if (h->busy) {
     if (j->arena_ref) napi_delete_reference(env, j->arena_ref);
     job_free(j); napi_throw_error(env, "YGM_EBUSY", "ygm: one batch in flight per engine handle"); return NULL;
   }
-  NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
+  if (napi_create_reference(env, handle, 1, &j->handle_ref) != napi_ok || napi_create_promise(env, &j->deferred, &promise) != napi_ok) {
+    if (j->arena_ref) napi_delete_reference(env, j->arena_ref);
+    if (j->handle_ref) napi_delete_reference(env, j->handle_ref);
+    job_free(j); napi_throw_error(env, NULL, "ygm: cannot queue the batch"); return NULL;
+  }
   h->busy = 1;
   if (h->refs++ == 0) napi_ref_threadsafe_function(env, h->tsfn);   /* keep the loop alive until it settles */
   pthread_mutex_lock(&h->mu);
@@ -344,7 +382,7 @@ static napi_value js_sleep(napi_env env, napi_callback_info info) {
   if (!h) return NULL;
   Job *j = (Job *)calloc(1, sizeof(Job)); j->op = 99; j->h = h;
   if (argc > 1) napi_get_value_uint32(env, argv[1], &j->sleep_ms);
-  return submit(env, j, "ygm.sleep");
+  return submit(env, j, argv[0]);
 }
 
 /* mergeMany(h, arena, lens, docs, nDocs) */
@@ -381,7 +419,7 @@ static napi_value js_merge(napi_env env, napi_callback_info info) {
     if (j->arena_ref) napi_delete_reference(env, j->arena_ref);
     job_free(j); napi_throw_range_error(env, NULL, "mergeMany: sum(lens) != arena length"); return NULL;
   }
-  return submit(env, j, "ygm.mergeMany");
+  return submit(env, j, argv[0]);
 }
 
 /* diffMany(h, arena, lens, svArena, svLens) */
@@ -403,7 +441,7 @@ static napi_value js_diff(napi_env env, napi_callback_info info) {
   j->sv_off = lens_to_off((const uint32_t *)slens, j->n_docs);
   free(lens); free(slens);
   if (j->off[j->n_docs] != an || j->sv_off[j->n_docs] != sn) { job_free(j); napi_throw_range_error(env, NULL, "diffMany: lengths do not match arenas"); return NULL; }
-  return submit(env, j, "ygm.diffMany");
+  return submit(env, j, argv[0]);
 }
 
 /* svMany(h, arena, lens) */
@@ -423,7 +461,7 @@ static napi_value js_sv(napi_env env, napi_callback_info info) {
   j->off = lens_to_off((const uint32_t *)lens, j->n_docs);
   free(lens);
   if (j->off[j->n_docs] != an) { job_free(j); napi_throw_range_error(env, NULL, "svMany: sum(lens) != arena length"); return NULL; }
-  return submit(env, j, "ygm.svMany");
+  return submit(env, j, argv[0]);
 }
 
 /* containsMany(h, states, stateLens, updates, updateLens): snapshotContainsUpdate per pair (1 byte) */
@@ -444,7 +482,7 @@ static napi_value js_contains(napi_env env, napi_callback_info info) {
   j->sv_off = lens_to_off((const uint32_t *)slens, j->n_docs);
   free(lens); free(slens);
   if (j->off[j->n_docs] != an || j->sv_off[j->n_docs] != sn) { job_free(j); napi_throw_range_error(env, NULL, "containsMany: lengths do not match arenas"); return NULL; }
-  return submit(env, j, "ygm.containsMany");
+  return submit(env, j, argv[0]);
 }
 
 /* snapshotMany(h, arena, lens): Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), u)) per update */
@@ -463,7 +501,7 @@ static napi_value js_snapshot(napi_env env, napi_callback_info info) {
   j->off = lens_to_off((const uint32_t *)lens, j->n_docs);
   free(lens);
   if (j->off[j->n_docs] != an) { job_free(j); napi_throw_range_error(env, NULL, "snapshotMany: sum(lens) != arena length"); return NULL; }
-  return submit(env, j, "ygm.snapshotMany");
+  return submit(env, j, argv[0]);
 }
 
 static napi_value init(napi_env env, napi_value exports) {

@@ -502,6 +502,29 @@ test('eight engine handles run eight native jobs at once', async () => {
   }
 })
 
+// close() while a job is in flight: the job still settles, the handle stops after it, and later calls throw
+// (the handle is freed only after its last completion has been delivered: addon/ygm_napi.c tsfn_finalize)
+test('close during an in-flight job settles the job, then closes', async () => {
+  const { loadAddon } = require('../src/engine.js')
+  const a = loadAddon()
+  const h = a.openNull()
+  const p = a.sleep(h, 100)
+  a.close(h)
+  assert.throws(() => a.sleep(h, 1), /closed or invalid/)
+  const r = await p
+  assert.ok(r.end >= r.start + 90)
+  assert.throws(() => a.sleep(h, 1), /closed or invalid/)
+  a.close(h)   // idempotent
+  // a handle dropped with a job pending is kept alive by the job (no use-after-free when it is collected)
+  let h2 = a.openNull()
+  const p2 = a.sleep(h2, 50)
+  h2 = null
+  if (global.gc) global.gc()
+  const r2 = await p2
+  assert.ok(r2.end >= r2.start + 40)
+  if (global.gc) global.gc()
+})
+
 test('sync responder answers a SyncStep1 batch', async (engine) => {
   const db = memoryDb()
   const ext = new GpuMerge({ ...db, Y, engine })

@@ -16,7 +16,7 @@ needs_node = pytest.mark.skipif(shutil.which("node") is None or not os.path.exis
 
 
 def run(mode):
-    r = subprocess.run(["node", os.path.join(PKG, "test", "run.js"), f"--{mode}"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run(["node", "--expose-gc", os.path.join(PKG, "test", "run.js"), f"--{mode}"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "passed" in r.stdout
 

@@ -40,9 +40,6 @@ namespace ygm {
 #ifndef YGM_DW_S
 #define YGM_DW_S 4
 #endif
-#ifndef YGM_DW_BATCH
-#define YGM_DW_BATCH 256
-#endif
 constexpr int DW_S = YGM_DW_S;    // 64-byte chunk slots per lane ring (a power of two)
 constexpr int DW_P = DW_S * 4;    // 16-byte pieces per ring
 #ifndef YGM_DW_R
@@ -60,17 +57,14 @@ constexpr uint32_t DW_STG = YGM_DW_STG;   // chunks staged per round (<= 4: 64 s
 #ifndef YGM_DW_AHEAD
 #define YGM_DW_AHEAD 2
 #endif
-#ifndef YGM_DW_LINE
-#define YGM_DW_LINE 0
-#endif
 constexpr uint32_t DW_AHEAD = YGM_DW_AHEAD;  // chunks staged past the ring's free slots (committed if the round freed theirs)
-// 1: stage whole 128-byte lines (chunk pairs of a 128-byte aligned base): the two 64-byte halves of a line are
-// loaded together, not rounds apart (where the second half's fetch misses an L2 that has evicted the line)
-constexpr bool DW_LINE = YGM_DW_LINE != 0;
-constexpr int DW_BATCH = YGM_DW_BATCH;   // documents sorted (largest first) per batch of a wave's range
+constexpr int DW_BATCH = 256;     // documents sorted (largest first) per batch of a wave's range
 constexpr int DW_SVN = 16;        // state-vector entries per lane (diff)
 constexpr uint32_t DW_OPEN = 0xFFFFFFFFu;
 
+// The lane's ring and its chunks' terminator masks in LDS.  (The masks in registers -- four per lane, read by
+// bit-mask selects -- measured slower: the walker is bound by VALU issue, and a select costs more VALU than the
+// LDS read it replaces; profiles/r05_walk/README.md.)
 struct DWLds {
   u32x4 ring[DW_P][WAVE];         // piece p (16 bytes) of lane l's ring: ring-relative bytes r with (r >> 4) % DW_P == p
   uint64_t mask[DW_S][WAVE];      // terminator mask of the chunk in each slot (bit i: byte i has its top bit clear)

@@ -1,7 +1,7 @@
 // ygm_kernels.hip -- gfx950 kernels of the batched Yjs update engine.
 //
-//  k_sv          encodeStateVectorFromUpdate, one lane per document   (yjs Y@37728)
-//  k_diff        diffUpdate, one lane per document                    (yjs Y@40711)
+//  k_doc         encodeStateVectorFromUpdate / diffUpdate, one lane per document (yjs Y@37728 / Y@40711):
+//                the exact kernel for what the ring walker (ygm_walk.hip) defers
 //  k_merge_fast  mergeUpdates, one workgroup per document, all state in LDS:
 //                stage -> parse (lane per update) -> bitonic sort of struct
 //                keys (client desc, clock asc) -> provenance scan (Skip gaps,
@@ -25,7 +25,8 @@
 #include "ygm_merge_seq.hpp"
 #include "ygm_merge_wave.hpp"
 #include "ygm_merge_lean.hpp"
-#include "ygm_doc_walk.hpp"
+#include "ygm_docmeta.hpp"
+#include "ygm_doc_walk.hpp"   // (its byte-window helpers: dw_at, dw_fsh, ...)
 #include "ygm_merge_big.hpp"
 #include "ygm_seqdoc.hpp"
 #include "ygm_v1.hpp"
@@ -61,37 +62,6 @@ namespace ygm {
 constexpr int DOC_NT = 256;   // lanes (= documents) per workgroup tile
 constexpr int DIFF_BLK = 16;  // per-lane LDS slots for output-block counts
 
-struct DocMeta {                    // per-launch device counters (zeroed by the launcher)
-  unsigned int ticket;
-  unsigned int fault;
-  unsigned int fb_count;            // documents sent to the sequential kernel
-  unsigned int defer_count;         // documents sent from the wave kernel to the workgroup kernel
-  unsigned int lean_defer;          // documents sent from the lean kernel to the wave kernel
-  unsigned int big_defer;           // documents sent from the large-document kernel to the sequential kernel
-  unsigned int wide_defer;          // documents sent from the wide lean kernel to the wave kernel
-  unsigned int mid_defer;           // documents sent from the mid-size large-document kernel to the large size
-  unsigned int pad_[2];
-  unsigned long long big_scur;      // large-document kernel: struct-record entries carved
-  unsigned long long fast_total;    // SV/diff: bytes of the packed (look-back placed) output
-  unsigned long long cursor;        // merge: bytes in the overflow region (after the per-document slots)
-  unsigned long long payload;       // merge: sum of output lengths (algorithmic output bytes)
-  unsigned long long fb_upds;       // updates / bytes of fallback documents (scratch sizing)
-  unsigned long long fb_bytes;
-  unsigned long long scr_upd_cursor;
-  unsigned long long scr_byte_cursor;
-  unsigned long long big_cursor;      // large-document kernel: block-table entries carved (16-byte multiple:
-                                      // the lean kernel zeroes slots in 16-byte pieces)
-  unsigned long long payload_sh[16 * 16]; // merge: output lengths summed in 16 shards, one 128-B line each (no hot atomic line)
-};
-YDEV void add_payload(DocMeta* m, uint32_t d, uint64_t n) { atomicAdd(&m->payload_sh[(d & 15u) * 16u], (unsigned long long)n); }
-
-// Merge output placement.  Document d owns the 16-byte aligned slot starting at
-// align16(2*b0 + 64d) with capacity 2*(b1-b0) + 48 (b0, b1 = its input byte
-// range), inside [2*b0 + 64d, 2*b1 + 64(d+1)): slots never overlap and need no
-// cross-document scan (slot_total = 2*arena + 64*n_docs).  An output that does
-// not fit its slot goes to the overflow region after slot_total (atomic cursor).
-YDEV uint64_t merge_slot(uint64_t b0, uint32_t d) { return (2 * b0 + 64ull * d + 15) & ~15ull; }
-YDEV uint64_t merge_slot_cap(uint64_t nbytes) { return 2 * nbytes + 48; }
 YDEV uint64_t merge_place(const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t d, uint64_t size, uint64_t slot_total,
                           DocMeta* meta) {
   const uint64_t b0 = upd_off[doc_upd[d]], b1 = upd_off[doc_upd[d + 1]];
@@ -154,773 +124,6 @@ __global__ __launch_bounds__(DOC_NT) void k_doc(const uint8_t* __restrict__ aren
   out_off[d] = at; out_len[d] = st == ST_OK ? mysz : 0; status[d] = st;
 }
 
-
-// ======================================================================= SV / diff: lane-per-document ring walker
-// ygm_doc_walk.hpp.  MODE 0 = encodeStateVectorFromUpdate (rule R-SV), 1 = diffUpdate (rule R-D).
-// Wave w owns documents [n*w/G, n*(w+1)/G); a lane that finishes one takes the wave's next document
-// at the following round start (offsets prefetched one round ahead, handed over by bpermute).
-// Outputs go to the document's slot (merge_slot): the header (a count known only at the end) is
-// written right-aligned in front of the body at slot + 16.  Documents outside the walker's shape are
-// appended to `defer_list` for k_doc.
-YDEV uint64_t dw_shfl64(uint64_t v, uint32_t src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// diffUpdate pre-pass: each document's state vector (decodeStateVector, Y@37797: a count, then
-// (client, clock) varuints; a repeated client's last entry wins, as in its Map) parsed by one lane into
-// a table sorted by client descending -- the order of the update's client blocks -- at tbl + 144 d as
-// (client, clock) u32 pairs; tbl_n[d] = entries, or DW_TBL_BAD for a vector the walker leaves to the
-// exact kernel (> DW_SVN entries, > DW_TBL_MAXB bytes, values >= 2^32, truncated, trailing bytes).
-constexpr uint32_t DW_TBL_BAD = 0x80000000u;
-constexpr uint32_t DW_TBL_MAXB = 160u;   // state-vector bytes staged per lane (16 entries of <= 10 bytes)
-__global__ __launch_bounds__(WAVE) void k_sv_table(const uint8_t* __restrict__ sv_arena, const uint64_t* __restrict__ sv_off,
-                                                  uint32_t n_docs, uint8_t* __restrict__ tbl, uint32_t* __restrict__ tbl_n) {
-  __shared__ u32x4 buf[DW_TBL_MAXB / 16 + 1][WAVE];
-  __shared__ uint32_t ec[DW_SVN][WAVE], ek[DW_SVN][WAVE];
-  const uint32_t l = threadIdx.x, d = blockIdx.x * WAVE + l;
-  if (d >= n_docs) return;
-  const uint64_t sa = sv_off[d], sb = sv_off[d + 1];
-  const uint32_t len = sb > sa ? (uint32_t)(sb - sa) : 0u;
-  uint32_t bad = (sb < sa || len == 0u || len > DW_TBL_MAXB) ? 1u : 0u;
-  const uint32_t o0 = (uint32_t)(sa & 15u);
-  const u32x4* src = (const u32x4*)(sv_arena + (sa & ~15ull));
-  const uint32_t np = bad ? 0u : (o0 + len + 15u) >> 4;
-  for (uint32_t i = 0; i < np; i++) buf[i][l] = src[i];
-  const uint8_t* b = (const uint8_t*)&buf[0][0];
-  auto byte = [&](uint32_t i) -> uint32_t { return b[((i >> 4) * WAVE + l) * 16u + (i & 15u)]; };
-  uint32_t pos = o0, end = o0 + (bad ? 0u : len);
-  auto vu = [&]() -> uint32_t {   // varuint < 2^32 inside the vector, else bad
-    uint64_t v = 0;
-    for (uint32_t sh = 0;; sh += 7) {
-      if (pos >= end || sh > 28) { bad = 1; return 0u; }
-      const uint32_t x = byte(pos++);
-      v |= (uint64_t)(x & 0x7Fu) << sh;
-      if (x < 0x80u) break;
-    }
-    if (v >> 32) bad = 1;
-    return (uint32_t)v;
-  };
-  const uint32_t cnt = bad ? 0u : vu();
-  bad |= cnt > (uint32_t)DW_SVN ? 1u : 0u;
-  uint32_t n = 0;
-  for (uint32_t e = 0; e < (bad ? 0u : cnt); e++) {
-    const uint32_t c = vu(), k = vu();
-    if (bad) break;
-    uint32_t j = 0;
-    while (j < n && ec[j][l] > c) j++;
-    if (j < n && ec[j][l] == c) { ek[j][l] = k; continue; }   // the last entry of a client wins
-    for (uint32_t m = n; m > j; m--) { ec[m][l] = ec[m - 1][l]; ek[m][l] = ek[m - 1][l]; }
-    ec[j][l] = c; ek[j][l] = k; n++;
-  }
-  bad |= pos != end ? 1u : 0u;   // trailing bytes: the exact kernel decides
-  if (bad) { tbl_n[d] = DW_TBL_BAD; return; }
-  uint64_t* t = (uint64_t*)(tbl + 144ull * d);
-  for (uint32_t j = 0; j < n; j++) t[j] = ((uint64_t)ek[j][l] << 32) | ec[j][l];
-  tbl_n[d] = n;
-}
-
-#ifndef YGM_DW_SPEC
-#define YGM_DW_SPEC 0   // 1: fast decoder reads both candidate content-length bytes beside the info byte (A/B: slower,
-                        // profiles/r03_walk/README.md -- the walker is issue-bound, not LDS-latency-bound)
-#endif
-#ifndef YGM_DW_COOP
-#define YGM_DW_COOP 0   // 1: cooperative staging -- four lanes load one owner's 64-byte chunk (quad-coalesced requests)
-#endif
-#ifndef YGM_DW_WPE0
-#define YGM_DW_WPE0 2   // waves per SIMD the SV walker is compiled for (register budget 512 / waves)
-#endif
-#ifndef YGM_DW_WPE1
-#define YGM_DW_WPE1 2   // ... the diff walker
-#endif
-template <int MODE>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? YGM_DW_WPE0 : YGM_DW_WPE1))) void k_doc_walk(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ doc_off,
-                                                  const uint8_t* __restrict__ tbl, const uint32_t* __restrict__ tbl_n,
-                                                  uint32_t n_docs, uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
-                                                  uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
-                                                  uint32_t* __restrict__ defer_list, uint64_t out_cap) {
-  __shared__ DWLds L;
-  __shared__ uint64_t ordk[DW_BATCH];      // the current batch of documents, largest first: (bytes << 32 | index in batch)
-  const uint32_t l = threadIdx.x;
-  const uint32_t D1 = (uint32_t)((uint64_t)n_docs * (blockIdx.x + 1) / gridDim.x);
-  uint32_t bnext = (uint32_t)((uint64_t)n_docs * blockIdx.x / gridDim.x);   // wave-uniform: first document of the next batch
-  uint32_t bbase = bnext, bn = 0, next = 0;                                  // the batch [bbase, bbase + bn); next: its first untaken entry
-
-  // offsets of the next 64 documents of the batch (lane i: entry next + i), loaded one round ahead
-  uint32_t pd = 0, ptn = 0;
-  uint64_t pa = 0, pb = 0;
-  auto prefetch = [&]() {
-    pa = 0; pb = 0; ptn = 0; pd = 0;
-    if (next + l < bn) {
-      pd = bbase + (uint32_t)ordk[next + l];
-      pa = doc_off[pd]; pb = doc_off[pd + 1];
-      if (MODE == 1) ptn = tbl_n[pd];
-    }
-  };
-
-  // ---- lane state
-  uint32_t ph = WK_IDLE, d = 0, bad = 0;
-  uint64_t da = 0, db = 0;                 // the document's bytes in `arena`
-  // the lane's stream: MODE 1 first the document's state-vector table (chunks [0, tc): ring-relative bytes
-  // [0, 8 nsv) = the table at tbl + 144 d), then the document; ring-relative byte r >= 64 tc is arena byte
-  // cbase + r - 64 tc
-  uint32_t tc = 0;
-  uint64_t cbase = 0;                      // 16-byte aligned arena offset of the document's first chunk
-  uint32_t srel = 0, q = 0, rb = 0;        // document start / parse position / document end, ring-relative
-  uint32_t landed = 0, stg_n = 0, stg_k = 0, prev8 = 0;
-  u32x4 g0 = {0u, 0u, 0u, 0u}, g1 = g0, g2 = g0, g3 = g0, g4 = g0, g5 = g0, g6 = g0, g7 = g0;   // staged chunks
-  u32x4 g8 = g0, g9 = g0, g10 = g0, g11 = g0;
-#if !YGM_DW_COOP
-  u32x4 g12 = g0, g13 = g0, g14 = g0, g15 = g0;
-#endif
-  uint32_t n_left = 0, st_left = 0, client = 0, clock = 0, prevc = 0;
-  bool have_prev = false;
-  uint64_t slot = 0;                       // the document's output slot; t / tend / e_dst / cdst relative to it
-  uint8_t* ob = out;                       // out + slot
-  uint32_t tend = 0, t = 0;
-  uint32_t count = 0;
-  uint32_t sp = 0, str_end = 0, ph_after = 0;   // WK_STR: bytes [sp, str_end) of a long string still to check
-  bool str_ascii = false;
-  uint32_t clk = 0, cc = 0;                // MODE 0: the current block's state-vector clock
-  bool stop = false, fst = false;          // fst: the document's first struct (its end counts even for a Skip)
-  // pending output, written at the next round start.  MODE 0: entry (e_a, e_b); MODE 1: block header
-  // (e_a, e_b, e_c) = (structs, client, clock) and, when e_pl > 0, the re-encoded prefix of a cut struct.
-  bool e_on = false;
-  uint32_t e_dst = 0;
-  uint32_t e_a = 0, e_b = 0, e_c = 0, e_pl = 0, e_info = 0, e_oclk = 0, e_q = 0, e_ro_p = 0, e_ro_e = 0, e_clen = 0;
-  // MODE 1: the state vector in registers: entries (sc[i], sk[i]), clients unique
-  // copy run (ring bytes [cp, run_end) -> output at cdst)
-  uint32_t nsv = 0, svc = 0;
-  uint32_t sc[MODE == 1 ? DW_SVN : 1], sk[MODE == 1 ? DW_SVN : 1];
-#pragma unroll
-  for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) { sc[i] = 0; sk[i] = 0; }
-  bool emitted = false, run_on = false;
-  uint32_t cp = 0, run_end = 0, rs0 = 0;
-  uint32_t cdst = 0, cd0 = 0;
-  uint64_t payload = 0;
-  uint32_t rounds = 0;
-#ifdef YGM_DIAG
-  unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // lane-iterations: fast, general, not ready, idle, string; rounds, general iterations
-#define WDG(i, v) dg[i] += (v)
-  // wave shader-clock per section (wave-uniform code): commit, SV parse, grab + output + init, staging, parse
-  unsigned long long tsec[5] = {0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
-#define WSEC(i) do { const unsigned long long _n = __builtin_amdgcn_s_memtime(); tsec[i] += _n - tprev; tprev = _n; } while (0)
-#else
-#define WDG(i, v)
-#define WSEC(i)
-#endif
-
-  // end of a client block (after its last struct): MODE 0 queues the block's state-vector entry,
-  // MODE 1 closes the block's copy run
-  auto block_end = [&]() {
-    if (MODE == 0) {
-      if (clk) {
-        const uint32_t el = dw_vulen(cc) + dw_vulen(clk);
-        if (t + el > tend) bad = 1;
-        else { e_on = true; e_dst = t; e_a = cc; e_b = clk; t += el; count++; }
-      }
-      ph = --n_left ? WK_BLK : WK_FIN;
-    } else {
-      if (emitted) {   // the rest of the block, verbatim (Skips included)
-        run_end = q;
-        t = cd0 + (run_end - rs0);
-        bad |= t > tend ? 1u : 0u;
-      }
-      ph = --n_left ? WK_BLK : WK_DS;
-    }
-  };
-  // a block header: canonical blocks are strictly client-descending
-  auto block_begin = [&](uint32_t nst, uint32_t cl, uint32_t ck) {
-    bad |= (nst == 0u || (have_prev && cl >= prevc)) ? 1u : 0u;
-    fst = !have_prev;
-    prevc = cl; have_prev = true;
-    st_left = nst; client = cl; clock = ck;
-    if (MODE == 0) { cc = cl; stop = ck != 0u; clk = 0u; }
-    else {   // the state-vector clock of the client: walk the descending table
-      // (clients are unique in the table and its unused entries repeat entry 0, or hold clock 0: a
-      // compare-select over all entries, no walk)
-      uint32_t s = 0;
-#pragma unroll
-      for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) s = sc[i] == cl ? sk[i] : s;
-      svc = s;
-      emitted = false;
-    }
-    ph = WK_ST;
-  };
-
-  for (;;) {
-    // ---- (0) a new batch of documents: sorted by size, largest first (the documents left at the end of a
-    //      wave's range are its smallest: the last lanes to finish wait least)
-    if (next >= bn && bnext < D1) {
-      // equal batches of <= DW_BATCH: a short last batch would leave most lanes idle behind its largest document
-      const uint32_t rem = D1 - bnext, nbat = (rem + DW_BATCH - 1u) / DW_BATCH;
-      bbase = bnext; bn = (rem + nbat - 1u) / nbat; bnext = bbase + bn; next = 0;
-      for (uint32_t e = l; e < (uint32_t)DW_BATCH; e += WAVE) {
-        // key bytes + 1 (padding entries past bn: 0, sorted behind every document)
-        const uint64_t sz = e < bn ? doc_off[bbase + e + 1] - doc_off[bbase + e] + 1ull : 0ull;
-        ordk[e] = ((sz < 0xFFFFFFFFull ? sz : 0xFFFFFFFFull) << 32) | e;
-      }
-      __syncthreads();
-      for (uint32_t kk = 2; kk <= (uint32_t)DW_BATCH; kk <<= 1)
-        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-          for (uint32_t t2 = l; t2 < (uint32_t)DW_BATCH / 2; t2 += WAVE) {
-            const uint32_t lo = ((t2 / jj) * 2 * jj) + (t2 % jj), hi = lo + jj;
-            const uint64_t x = ordk[lo], y = ordk[hi];
-            if ((x < y) == ((lo & kk) == 0)) { ordk[lo] = y; ordk[hi] = x; }   // descending
-          }
-          __syncthreads();
-        }
-      prefetch();
-    }
-    WSEC(4);
-    // ---- (1) the chunks staged last round land in the ring (the compiler waits for their loads here)
-    //      -- those whose ring slot is free by now: staging runs DW_AHEAD chunks past the ring, betting on this
-    //      round's consumption; a chunk that lost the bet is dropped here and staged again
-    if (stg_n) {
-      uint32_t need = ph == WK_STR ? sp : (MODE == 1 && ph == WK_SVN) ? 0u : q;   // (the table stays until copied)
-      if (run_on && cp < need) need = cp;
-      if (MODE == 1 && e_on && e_q < need) need = e_q;   // the pending cut struct's right origin is copied from the ring
-      const uint32_t lim = (need >> 6) + DW_S;
-      if (stg_k + stg_n > lim) stg_n = lim > stg_k ? lim - stg_k : 0u;
-    }
-#if YGM_DW_COOP
-    // cooperative commit: quad q of instruction (j, b) holds chunk j of owner 16 b + q (one 16-byte piece per lane).
-    // Each lane writes its piece to the owner's ring; the quad assembles the chunk's terminator mask by DPP, checks the
-    // chunk inside (varuints of >= 6 bytes; diff: a top-bit byte followed by a zero byte) and writes the mask -- all
-    // zero ("no varuint ends") when a check fails, so any unit the walker would read there is deferred.  The owner
-    // then checks what crosses from its previous chunk into each new one (prev8) over its document's part.
-    {
-      const uint32_t pc = l & 3u;
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const uint32_t o = 16u * (uint32_t)b + (l >> 2);
-        const uint32_t sk = (uint32_t)__shfl((int)stg_k, (int)o), sn = (uint32_t)__shfl((int)stg_n, (int)o);
-        if (__ballot(sn != 0u) == 0) continue;
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-          const u32x4 v = j == 0 ? (b == 0 ? g0 : b == 1 ? g1 : b == 2 ? g2 : g3)
-                        : j == 1 ? (b == 0 ? g4 : b == 1 ? g5 : b == 2 ? g6 : g7)
-                                 : (b == 0 ? g8 : b == 1 ? g9 : b == 2 ? g10 : g11);
-          const bool act = (uint32_t)j < sn;
-          if (__ballot(act) == 0) break;
-          const uint32_t k = sk + (uint32_t)j;
-          if (act) L.ring[(4u * k + pc) & (DW_P - 1)][o] = v;
-          const uint32_t h16 = hibits8(v.x, v.y) | (hibits8(v.z, v.w) << 8);
-          const uint32_t h2 = (h16 << (16u * (pc & 1u))) | ((uint32_t)__builtin_amdgcn_mov_dpp((int)(h16 << (16u * (pc & 1u))), 0xB1, 0xF, 0xF, false));
-          const uint32_t hs = (uint32_t)__builtin_amdgcn_mov_dpp((int)h2, 0x4E, 0xF, 0xF, false);
-          const uint64_t H = pc < 2u ? ((uint64_t)hs << 32 | h2) : ((uint64_t)h2 << 32 | hs);
-          const uint64_t r2 = H & (H >> 1), r4 = r2 & (r2 >> 2), r6 = r4 & (r2 >> 4);
-          uint64_t bp = 0;
-          if (MODE == 1) {
-            auto zb = [](uint32_t a) { return ~(((a & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | a) & 0x80808080u; };
-            const uint32_t z16 = hibits8(zb(v.x), zb(v.y)) | (hibits8(zb(v.z), zb(v.w)) << 8);
-            const uint32_t z2 = (z16 << (16u * (pc & 1u))) | ((uint32_t)__builtin_amdgcn_mov_dpp((int)(z16 << (16u * (pc & 1u))), 0xB1, 0xF, 0xF, false));
-            const uint32_t zs = (uint32_t)__builtin_amdgcn_mov_dpp((int)z2, 0x4E, 0xF, 0xF, false);
-            const uint64_t Z = pc < 2u ? ((uint64_t)zs << 32 | z2) : ((uint64_t)z2 << 32 | zs);
-            bp = (H << 1) & Z;   // (bit 0: the previous chunk's last byte, the owner's check)
-          }
-          if (act && pc == 0u) L.mask[k & (DW_S - 1)][o] = (r6 | bp) ? 0ull : ~H;
-        }
-      }
-      // the owner: checks across its previous chunk's end, over the document part [vlo, vhi) of each new chunk
-      for (uint32_t j = 0; j < stg_n; j++) {
-        const uint32_t k = stg_k + j;
-        const uint32_t vlo = srel > 64u * k ? (srel - 64u * k < 64u ? srel - 64u * k : 64u) : 0u;
-        const uint32_t vhi = k < tc ? 0u : (rb - 64u * k < 64u ? rb - 64u * k : 64u);
-        const uint64_t m = L.mask[k & (DW_S - 1)][l];
-        const uint64_t vm = dw_lowmask(vhi) & ~dw_lowmask(vlo);
-        const uint64_t Hm = ~m & vm;
-        const uint32_t c = ((uint32_t)(Hm & 0xFFu) << 8) | prev8;
-        const uint32_t c2 = c & (c >> 1), c4 = c2 & (c2 >> 2), c6 = c4 & (c2 >> 4);
-        uint32_t bpx = 0;
-        if (MODE == 1 && vlo == 0u && vhi) bpx = (prev8 >> 7) & (dw_byte(L, l, 64u * k) == 0u ? 1u : 0u);
-        bad |= (c6 | bpx) ? 1u : 0u;
-        prev8 = vhi ? (uint32_t)(Hm >> 56) : prev8;
-      }
-      if (stg_n) landed = stg_k + stg_n;
-      stg_n = 0;
-    }
-#else
-    if (stg_n) {
-      // the document part [vlo, vhi) of chunk k is checked (table chunks: none)
-      auto vlo = [&](uint32_t k) { return srel > 64u * k ? (srel - 64u * k < 64u ? srel - 64u * k : 64u) : 0u; };
-      auto vhi = [&](uint32_t k) { return k < tc ? 0u : (rb - 64u * k < 64u ? rb - 64u * k : 64u); };
-      dw_commit<MODE == 1>(L, l, stg_k, g0, g1, g2, g3, vlo(stg_k), vhi(stg_k), prev8, bad);
-      if (stg_n > 1u) {
-        const uint32_t k1 = stg_k + 1u;
-        dw_commit<MODE == 1>(L, l, k1, g4, g5, g6, g7, vlo(k1), vhi(k1), prev8, bad);
-      }
-      if (stg_n > 2u) {
-        const uint32_t k2 = stg_k + 2u;
-        dw_commit<MODE == 1>(L, l, k2, g8, g9, g10, g11, vlo(k2), vhi(k2), prev8, bad);
-      }
-      if (DW_STG > 3u && stg_n > 3u) {
-        const uint32_t k3 = stg_k + 3u;
-        dw_commit<MODE == 1>(L, l, k3, g12, g13, g14, g15, vlo(k3), vhi(k3), prev8, bad);
-      }
-      landed = stg_k + stg_n;
-      stg_n = 0;
-    }
-#endif
-    WSEC(0);
-    // ---- (1b) diff: a landed state-vector table moves from the ring to the lane's table, the document follows
-    if (MODE == 1) {
-      const bool cpy = ph == WK_SVN && landed >= tc;
-      const uint64_t cm = __ballot(cpy);
-      if (cm && cpy) {
-#pragma unroll
-        for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) {   // unused entries: copies of entry 0 (or clock 0)
-          const uint64_t w = (uint32_t)i < nsv ? dw_word(L, l, 8u * (uint32_t)i) : (i ? ((uint64_t)sk[0] << 32 | sc[0]) : 0ull);
-          sc[i] = (uint32_t)w; sk[i] = (uint32_t)(w >> 32);
-        }
-        ph = WK_UPD;
-      }
-    }
-    WSEC(1);
-    // ---- (2) lanes that are idle or finishing take the wave's next documents
-    const bool want = ph == WK_IDLE || ph == WK_FIN;
-    const uint64_t wm = __ballot(want);
-    const uint32_t rank = lanes_below(wm) & 63u;
-    const uint64_t na = dw_shfl64(pa, rank), nb = dw_shfl64(pb, rank);
-    const uint32_t nd = (uint32_t)__shfl((int)pd, (int)rank);
-    const uint32_t ntn = MODE == 1 ? (uint32_t)__shfl((int)ptn, (int)rank) : 0u;
-    const uint32_t avail = bn - next;
-    const bool got = want && rank < avail;
-    const uint32_t npop = (uint32_t)__popcll(wm);
-    next += npop < avail ? npop : avail;
-    // ---- (3) output of the last round: pending header / entry, the copy run, finished documents
-    // Output stores are 16 bytes wide, whatever the byte count: the bytes past a store's valid part are
-    // overwritten by the document's next store (a lane writes its output in increasing order) or lie
-    // in the slot's last 16 bytes, which tend keeps free
-    if (e_on) {
-      e_on = false;
-      if (!bad) {
-        uint64_t lo = dw_vu_enc(e_a), hi = 0;
-        uint32_t at = dw_vulen(e_a);
-        dw_app(lo, hi, at, e_b);
-        if (MODE == 1) dw_app(lo, hi, at, e_c);
-        dw_st16(ob + e_dst, lo, hi);
-        if (MODE == 1 && e_pl) {   // the re-encoded prefix of a cut struct
-          uint64_t o = e_dst + at;
-          ob[o++] = (uint8_t)e_info;
-          if (e_info) {   // an item: origin (client, clock + off - 1), right origin verbatim
-            o = dw_put_vu(ob, o, e_b);
-            o = dw_put_vu(ob, o, e_oclk);
-            for (uint32_t k = e_ro_p; k < e_ro_e; k++) ob[o++] = (uint8_t)dw_byte(L, l, e_q + k);
-          }
-          dw_put_vu(ob, o, e_clen);
-        }
-      }
-    }
-    if (MODE == 1 && run_on) {   // the copy run: ring bytes [cp, run_end) -> output at cdst
-      if (bad) run_on = false;
-      else {
-        const uint32_t done = ph == WK_STR ? sp : q;
-        const bool fin = run_end <= done;
-        const uint32_t ce = fin ? run_end : (done & ~15u);   // an open run is written up to a ring piece boundary
-        if (ce > cp) {
-          if (cdst + (ce - cp) > tend) bad = 1;
-          else {
-            if (cp & 15u) {   // the head, up to the next ring piece boundary
-              const u32x4 v = dw_ring16(L, l, cp);
-              __builtin_memcpy(ob + cdst, &v, 16);
-              const uint32_t a = 16u - (cp & 15u) < ce - cp ? 16u - (cp & 15u) : ce - cp;
-              cp += a; cdst += a;
-            }
-            for (; cp < ce; cp += 16u, cdst += 16u) {   // whole ring pieces
-              const u32x4 v = L.ring[(cp >> 4) & (DW_P - 1)][l];
-              __builtin_memcpy(ob + cdst, &v, 16);
-            }
-            cdst -= cp - ce; cp = ce;
-          }
-        }
-        if (fin && !bad) run_on = false;
-      }
-    }
-    if (ph == WK_FIN) {
-      const uint64_t bm = __ballot(bad != 0u);   // (only finishing lanes reach here)
-      if (bm) {
-        uint32_t base = 0;
-        if (l == (uint32_t)__builtin_ctzll(bm)) base = atomicAdd(&meta->lean_defer, (uint32_t)__popcll(bm));
-        base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(bm));
-        if (bad) { defer_list[base + lanes_below(bm)] = d; status[d] = ST_FALLBACK; }
-      }
-      if (!bad) {   // the count, right-aligned in the slot's first 16 bytes (an aligned store)
-        const uint32_t hl = dw_vulen(count);
-        const uint64_t c = dw_vu_enc(count);
-        dw_st16(ob, 0ull, c << (64u - 8u * hl));
-        out_off[d] = slot + 16u - hl; out_len[d] = hl + (t - 16u); status[d] = ST_OK;
-        payload += hl + (t - 16u);
-      }
-      ph = WK_IDLE; run_on = false; e_on = false;
-    }
-    // ---- (4) new documents
-    if (got) {
-      d = nd; bad = 0; da = na; db = nb; count = 0; emitted = false; have_prev = false; nsv = 0;
-      slot = merge_slot(da, d);
-      ob = out + slot;
-      const uint64_t cap = merge_slot_cap(db - da), room = out_cap > slot ? out_cap - slot : 0ull;
-      const uint64_t lim = cap < room ? cap : room;
-      tend = lim > 16u ? (uint32_t)(lim - 16u) : 0u;   // (16 bytes of slack for the wide stores)
-      t = 16u;   // the header (a count known only at the end) goes right-aligned in front of the body
-      nsv = MODE == 1 && ntn <= (uint32_t)DW_SVN ? ntn : 0u;
-      bad |= (MODE == 1 && ntn > (uint32_t)DW_SVN) ? 1u : 0u;   // (DW_TBL_BAD: the exact kernel)
-      tc = (8u * nsv + 63u) >> 6;
-      if (MODE == 1 && !tc) {   // an empty state vector: every client at clock 0
-#pragma unroll
-        for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) sk[i] = 0u;
-      }
-      // (cooperative loads: chunks of one 64-byte sector each)
-      cbase = da & (DW_LINE ? ~127ull : YGM_DW_COOP ? ~63ull : ~15ull);
-      srel = 64u * tc + (uint32_t)(da - cbase); q = srel; rb = 64u * tc + (uint32_t)(db - cbase);
-      landed = 0; stg_n = 0; prev8 = 0;
-      bad |= (db < da || ((db - da) >> 30)) ? 1u : 0u;
-      ph = tc ? WK_SVN : WK_UPD;
-    }
-    if (__ballot(ph != WK_IDLE) == 0 && next >= bn && bnext >= D1) break;
-    WSEC(2);
-    // ---- (5) stage the next chunks of the segment (up to three; the ring keeps DW_S)
-    if (ph != WK_IDLE && ph != WK_FIN) {
-      uint32_t need = ph == WK_STR ? sp : (MODE == 1 && ph == WK_SVN) ? 0u : q;
-      if (run_on && cp < need) need = cp;
-      const uint32_t nch = (rb + 63u) >> 6;
-      const uint32_t wk = (need >> 6) + DW_S + DW_AHEAD < nch ? (need >> 6) + DW_S + DW_AHEAD : nch;
-      uint32_t n = wk > landed ? (wk - landed < DW_STG ? wk - landed : DW_STG) : 0u;
-      if (DW_LINE && n > 1u && ((landed + n - tc) & 1u) && landed + n < nch) n--;   // end on a line boundary
-      stg_k = landed; stg_n = n;
-      auto chunk = [&](uint32_t k) -> const u32x4* {
-        return (const u32x4*)(MODE == 1 && k < tc ? tbl + 144ull * d + 64u * k : arena + cbase + 64ull * (k - tc));
-      };
-#if YGM_DW_COOP
-      if (MODE == 1 && landed < tc && landed + n > tc) stg_n = n = tc - landed;   // (table and document chunks: two sources)
-#else
-      if (n >= 1u) { const u32x4* p = chunk(landed); g0 = p[0]; g1 = p[1]; g2 = p[2]; g3 = p[3]; }
-      if (n >= 2u) { const u32x4* p = chunk(landed + 1u); g4 = p[0]; g5 = p[1]; g6 = p[2]; g7 = p[3]; }
-      if (n >= 3u) { const u32x4* p = chunk(landed + 2u); g8 = p[0]; g9 = p[1]; g10 = p[2]; g11 = p[3]; }
-      if (DW_STG > 3u && n >= 4u) { const u32x4* p = chunk(landed + 3u); g12 = p[0]; g13 = p[1]; g14 = p[2]; g15 = p[3]; }
-#endif
-    }
-#if YGM_DW_COOP
-    // cooperative loads: instruction (j, b) -- lane l loads 16-byte piece l & 3 of chunk j of owner 16 b + l / 4, so
-    // every quad reads 64 contiguous bytes (one request per chunk instead of four lane-private ones)
-    {
-      const uint64_t ra = stg_n ? (uint64_t)(MODE == 1 && stg_k < tc ? (const uint8_t*)tbl + 144ull * d + 64u * stg_k
-                                                                    : arena + cbase + 64ull * (stg_k - tc)) : 0ull;
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const uint32_t o = 16u * (uint32_t)b + (l >> 2);
-        const uint64_t a = dw_shfl64(ra, o) + 16u * (l & 3u);
-        const uint32_t sn = (uint32_t)__shfl((int)stg_n, (int)o);
-        if (__ballot(sn != 0u) == 0) continue;
-        u32x4& r0 = b == 0 ? g0 : b == 1 ? g1 : b == 2 ? g2 : g3;
-        u32x4& r1 = b == 0 ? g4 : b == 1 ? g5 : b == 2 ? g6 : g7;
-        u32x4& r2 = b == 0 ? g8 : b == 1 ? g9 : b == 2 ? g10 : g11;
-        if (sn >= 1u) r0 = *(const u32x4*)a;
-        if (sn >= 2u) r1 = *(const u32x4*)(a + 64u);
-        if (sn >= 3u) r2 = *(const u32x4*)(a + 128u);
-      }
-    }
-#endif
-    // ---- (6) offsets of the documents the next round hands out
-    prefetch();
-    WSEC(3);
-    // ---- (7) parse: per lane and iteration one unit, by the fast decoder when it has the common shape
-    //      (an Item with origin(s) and a one-byte String / Deleted length inside 32 bytes, a block header
-    //      of a <= 2-byte count and a one-byte clock, a one-byte update header, an empty delete set),
-    //      else by the general decoder -- which then runs for the lanes that need it only
-#pragma unroll 1
-    for (int it = 0; it < (MODE == 1 ? DW_R - 1 : DW_R); it++) {   // (diff: shorter rounds, its output waits for them)
-      if (bad && ph != WK_IDLE) ph = WK_FIN;
-      // block headers are decoded on even iterations only: the wave skips the header decoder every other
-      // iteration (with 64 lanes some lane is at a header in most iterations; a lane waits one at most)
-      const bool blk_it = (it & 1) == 0;
-#ifdef YGM_DIAG
-      const uint32_t ph0 = ph;
-#endif
-      const uint32_t lend = landed << 6;
-      const bool rdy = (q + 64u <= lend) || (lend >= rb);   // the general decoder reads up to 64 bytes ahead
-      // the fast decoders take a unit whose bytes have all landed (masks past lend are stale: a unit
-      // that ends there is refused and retried)
-      const uint32_t avl = lend > q ? lend - q : 0u;
-      bool done = false;
-      if (avl && (ph == WK_ST || ph == WK_BLK || ph == WK_UPD || (MODE == 1 && ph == WK_DS))) {
-        const uint32_t kq = q >> 6, sq = q & 63u;
-        const uint64_t m0 = L.mask[kq & (DW_S - 1)][l], m1 = L.mask[(kq + 1u) & (DW_S - 1)][l];
-        // bytes q .. q + 63 (chunks past the segment may hold stale masks: every unit is checked against rb)
-        const uint64_t w64 = (m0 >> sq) | ((m1 << (63u - sq)) << 1);
-        const uint32_t w32 = (uint32_t)w64;
-        const uint32_t b0 = dw_byte(L, l, q);
-        if (ph == WK_ST) {   // Item with origin(s), one-byte String (ASCII) / Deleted length, inside 32 bytes;
-                             // a second one right behind it from the same 64-byte window
-          uint32_t qo = 0, bb = b0;
-#pragma unroll
-          for (int u = 0; u < DW_U; u++) {
-            const uint32_t wq = (uint32_t)(w64 >> qo);
-            const uint32_t tt = wq >> 1, x2 = tt & (tt - 1u), x3 = x2 & (x2 - 1u), x4 = x3 & (x3 - 1u);
-#if YGM_DW_SPEC
-            // the content length's position for one and for two origin ids comes from the mask alone: both
-            // candidate bytes are read beside the info byte (one LDS round trip per Item, not two)
-            const uint32_t c2 = (uint32_t)__builtin_ctz(x2 | 0x80000000u) + 2u, c4 = (uint32_t)__builtin_ctz(x4 | 0x80000000u) + 2u;
-            const uint32_t lv2 = dw_byte(L, l, q + (c2 & 31u)), lv4 = dw_byte(L, l, q + (c4 & 31u));
-            if (u >= 1) bb = dw_byte(L, l, q);
-            const uint32_t hoh = bb >> 6, ref = bb & 0x3Fu;
-            const uint32_t cpos = hoh == 3u ? c4 : c2;   // after the origins
-            const uint32_t cq = cpos & 31u;
-            const uint32_t lv = hoh == 3u ? lv4 : lv2;
-#else
-            if (u >= 1) bb = dw_byte(L, l, q);
-            const uint32_t hoh = bb >> 6, ref = bb & 0x3Fu;
-            const uint32_t cpos = (uint32_t)__builtin_ctz((hoh == 3u ? x4 : x2) | 0x80000000u) + 2u;   // after the origins
-            const uint32_t cq = cpos & 31u;
-            const uint32_t lv = dw_byte(L, l, q + cq);
-#endif
-            const uint32_t isS = ref == 4u ? 1u : 0u;
-            const uint32_t end = cq + 1u + (isS ? lv : 0u);
-            const uint32_t mk = isS ? (((1u << (lv & 31u)) - 1u) << ((cq + 1u) & 31u)) : 0u;   // the string's bytes: ASCII
-            const uint32_t ce = clock + lv;
-            uint32_t ok = (ph == WK_ST) & (hoh != 0u) & (isS | (ref == 1u)) & (cpos < 31u) & (wq >> cq) & (lv != 0u) &
-                          (end <= 32u) & ((wq & mk) == mk) & (ce >= clock) & (qo + end <= avl) & (u == 0 || (done && qo + end <= 64u));
-            uint32_t emit = 0;
-            if (MODE == 0) ok &= (st_left != 1u) | !e_on;
-            else {
-              emit = (!emitted) & (ce > svc);
-              ok &= (!emit) | ((svc <= clock) & !e_on & !run_on);   // a cut struct: the general decoder
-            }
-            if (ok) {
-              done = true;
-              if (MODE == 0) {
-                clk = stop ? clk : ce;   // (no Skips here: the first-struct seeding is the same)
-                fst = false;
-              } else if (emit) {
-                const uint32_t hl = dw_vulen(st_left) + dw_vulen(client) + dw_vulen(clock);
-                if (t + hl > tend) bad = 1;
-                else {
-                  e_on = true; e_dst = t; e_a = st_left; e_b = client; e_c = clock; e_pl = 0; e_q = q;
-                  t += hl;
-                  run_on = true; cp = q; rs0 = q; cdst = t; cd0 = t; run_end = DW_OPEN;
-                  emitted = true; count++;
-                }
-              }
-              clock = ce;
-              q += end; qo += end;
-              if (--st_left == 0u) block_end();
-            }
-          }
-        } else if (ph == WK_BLK && blk_it) {   // block header: <= 2-byte count, <= 5-byte client, one-byte clock
-          const uint32_t y = w32 & (w32 - 1u), z = y & (y - 1u);
-          const uint32_t e1 = (uint32_t)__builtin_ctz(w32 | 0x80000000u), e2 = (uint32_t)__builtin_ctz(y | 0x80000000u);
-          const uint32_t e3 = (uint32_t)__builtin_ctz(z | 0x80000000u);
-          const uint32_t b1 = dw_byte(L, l, q + 1u);
-          const uint32_t cn = e2 - e1;   // client bytes
-          const uint64_t cw = dw_rd8(L, l, q + (e1 & 1u) + 1u);
-          const uint32_t nst = e1 == 0u ? b0 : ((b0 & 0x7Fu) | (b1 << 7));
-          const uint32_t ok = (z != 0u) & (e1 <= 1u) & (e3 == e2 + 1u) & (cn - 1u <= 4u) & !((cn == 5u) & (((uint32_t)(cw >> 32) & 0x70u) != 0u)) &
-                              (e3 < avl);
-          if (ok) {
-            done = true;
-            const uint32_t cl = (uint32_t)pext7(cw, cn);
-            const uint32_t ck = (uint32_t)(cw >> (8u * (cn & 7u))) & 0x7Fu;
-            q += e3 + 1u;
-            block_begin(nst, cl, ck);
-          }
-        } else if (ph == WK_UPD) {
-          if (w32 & 1u) {
-            done = true;
-            q += 1u;
-            if (b0) { n_left = b0; have_prev = false; ph = WK_BLK; }
-            else ph = MODE == 1 ? WK_DS : WK_FIN;
-          }
-        } else if (MODE == 1 && ph == WK_DS && (w32 & 1u) && b0 == 0u && !run_on) {   // the empty delete set ("00") (avl >= 1)
-          done = true;
-          run_on = true; cp = q; rs0 = q; cdst = t; cd0 = t;
-          q += 1u; run_end = q; t += 1u;
-          bad |= t > tend ? 1u : 0u;
-          ph = WK_FIN;
-        }
-        if (q > rb) bad = 1;
-      }
-#ifdef YGM_DIAG
-      {   // one class per lane-iteration, from the phase it started in
-        const bool idl = ph0 == WK_IDLE || ph0 == WK_FIN || ph0 == WK_SVN;
-        WDG(0, done ? 1 : 0);
-        WDG(3, (!done && idl) ? 1 : 0);
-        WDG(4, (!done && !idl && ph0 == WK_STR) ? 1 : 0);
-        WDG(2, (!done && !idl && ph0 != WK_STR && !rdy) ? 1 : 0);
-        WDG(1, (!done && !idl && ph0 != WK_STR && rdy) ? 1 : 0);
-      }
-#endif
-#ifdef YGM_DIAG
-      if (l == 0) dg[6] += __ballot(!done && rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN && ph != WK_STR) ? 1 : 0;
-#endif
-      if (!done && ph == WK_STR) {   // the rest of a long string (or binary): checked against the chunk masks
-        if (sp < lend) {
-          const uint64_t wn = dw_win(L, l, sp, landed);
-          uint32_t n = str_end - sp;
-          if (n > lend - sp) n = lend - sp;
-          if (n > 64u) n = 64u;
-          if (str_ascii && ((~wn) & dw_lowmask(n))) bad = 1;
-          sp += n;
-          if (sp == str_end) ph = ph_after;
-        }
-      } else if (!done && rdy && ph != WK_IDLE && ph != WK_FIN && ph != WK_SVN && (blk_it || ph != WK_BLK)) {   // ---- the general decoder
-        const uint64_t win = dw_win(L, l, q, landed);
-        uint64_t lo, hi;
-        dw_rd16(L, l, q, lo, hi);
-        if (ph == WK_ST) {
-          const uint32_t info = (uint32_t)lo & 0xFFu;
-          const uint64_t w1 = win & ~1ull;   // terminators after the info byte
-          uint32_t len = 0, end = 0, kind = K_ITEM, ro_p = 0, ro_e = 0, cdata = 0, ref = 0, ho = 0, hr = 0;
-          bool spill = false, sasc = true;
-          if ((info & 31u) == 0u || info == 10u) {   // GC / Skip: varuint length
-            kind = info == 10u ? K_SKIP : K_GC;
-            bad |= (info != 0u && info != 10u) ? 1u : 0u;   // GC written back as info 0 by yjs
-            const uint32_t e = dw_ctz(w1);
-            len = dw_val(dw_at(lo, hi, 1u), e, bad);
-            bad |= len == 0u ? 1u : 0u;
-            end = e + 1u;
-          } else {
-            ref = info & 31u; ho = (info >> 7) & 1u; hr = (info >> 6) & 1u;
-            bad |= ((info & 0xC0u) && (info & 0x20u)) ? 1u : 0u;   // yjs drops the bit on re-encode
-            uint32_t cs;
-            if (ho | hr) {   // origin and/or right origin: two varuints each
-              uint64_t x = w1;
-              const uint32_t t2 = dw_ctz(x & (x - 1ull));
-              x &= x - 1ull; x &= x - 1ull; x &= x - 1ull;
-              const uint32_t t4 = dw_ctz(x);
-              cs = ((ho & hr) ? t4 : t2) + 1u;
-              ro_p = ho ? t2 + 1u : 1u; ro_e = cs;
-            } else {   // parent: parentInfo 1 -> y-key string, 0 -> parent id; parentSub string when bit 0x20
-              const uint32_t pe = dw_ctz(w1);
-              const uint32_t pi = dw_val(dw_at(lo, hi, 1u), pe, bad);
-              bad |= pi > 1u ? 1u : 0u;
-              uint32_t p = pe + 1u;
-              if (pi == 1u) p = dw_str(L, l, q, win, lo, hi, p < 63u ? p : 63u, bad);
-              else { uint64_t x = dw_from(win, p); x &= x - 1ull; p = dw_ctz(x) + 1u; }
-              if (info & 0x20u) p = dw_str(L, l, q, win, lo, hi, p < 63u ? p : 63u, bad);
-              cs = p;
-            }
-            bad |= cs >= 60u ? 1u : 0u;
-            const uint32_t csx = cs < 56u ? cs : 56u;
-            const uint32_t ce = dw_ctz(dw_from(win, csx));
-            const uint32_t v = dw_val(dw_bytes_at(L, l, q, lo, hi, csx), ce - csx + 1u, bad);
-            const uint32_t cend = ce + 1u;
-            if (ref == 1u) {   // ContentDeleted
-              len = v; end = cend;
-              bad |= v == 0u ? 1u : 0u;
-            } else if (ref == 4u || ref == 3u) {   // ContentString (ASCII: UTF-16 length = bytes) / ContentBinary
-              sasc = ref == 4u;
-              len = sasc ? v : 1u; cdata = cend; end = cend + v;
-              bad |= (sasc && v == 0u) ? 1u : 0u;
-              if (end <= 64u) { if (sasc && cdata < 64u && ((~win >> cdata) & dw_lowmask(v))) bad = 1; }
-              else { spill = true; if (sasc && cdata < 64u && (~win >> cdata)) bad = 1; }
-            } else if (ref == 7u) {   // ContentType: typeRef, key for XmlElement / XmlHook
-              len = 1u; end = cend;
-              bad |= v > 6u ? 1u : 0u;
-              if (v == 3u || v == 5u) end = dw_str(L, l, q, win, lo, hi, cend < 63u ? cend : 63u, bad);
-            } else bad = 1;   // JSON / Embed / Format / Any / Doc: the exact kernel
-          }
-          if (!bad) {
-            const uint64_t ce64 = (uint64_t)clock + len;
-            bad |= (ce64 >> 32) ? 1u : 0u;
-            bool emit = false, stall;
-            if (MODE == 0) stall = st_left == 1u && e_on;   // this block's entry needs the entry slot
-            else {
-              emit = !emitted && kind != K_SKIP && ce64 > svc;
-              stall = emit && (e_on || run_on);   // one block header / copy run in flight per lane
-            }
-            if (!stall && !bad) {
-              const uint32_t q0 = q;
-              if (MODE == 0) {
-                if (fst && !stop) clk = (uint32_t)ce64;   // yjs seeds the count with the first struct, Skip or not
-                fst = false;
-                if (kind == K_SKIP) stop = true;
-                if (!stop) clk = (uint32_t)ce64;
-              } else if (emit) {   // the first struct of the client past the state vector (rule R-D)
-                const uint32_t off = svc > clock ? svc - clock : 0u;
-                const uint32_t hck = clock + off;
-                const uint32_t hl = dw_vulen(st_left) + dw_vulen(client) + dw_vulen(hck);
-                uint32_t pl = 0, rstart = q;
-                if (off) {   // cut: GC -> GC(len - off); Deleted / String -> origin (client, clock + off - 1)
-                  if (kind == K_GC) { e_info = 0; e_clen = len - off; pl = 1u + dw_vulen(e_clen); rstart = q + end; }
-                  else {
-                    e_info = ref | 0x80u | (hr ? 0x40u : 0u) | ((!ho && !hr && (info & 0x20u)) ? 0x20u : 0u);
-                    e_oclk = clock + off - 1u;
-                    e_ro_p = hr ? ro_p : 0u; e_ro_e = hr ? ro_e : 0u;
-                    e_clen = len - off;
-                    pl = 1u + dw_vulen(client) + dw_vulen(e_oclk) + (e_ro_e - e_ro_p) + dw_vulen(e_clen);
-                    rstart = ref == 4u ? q + cdata + off : q + end;
-                  }
-                }
-                if (t + hl + pl > tend) bad = 1;
-                else {
-                  e_on = true; e_dst = t; e_a = st_left; e_b = client; e_c = hck; e_pl = pl; e_q = q;
-                  t += hl + pl;
-                  run_on = true; cp = rstart; rs0 = rstart; cdst = t; cd0 = t; run_end = DW_OPEN;
-                  emitted = true; count++;
-                }
-              }
-              clock = (uint32_t)ce64;
-              q += end;
-              if (--st_left == 0u) block_end();
-              if (spill) { sp = q0 + 64u; str_end = q0 + end; str_ascii = sasc; ph_after = ph; ph = WK_STR; }
-            }
-          }
-        } else {   // headers and delete-set entries: up to three varuints
-          uint64_t x = win;
-          const uint32_t e1 = dw_ctz(x); x &= x - 1ull;
-          const uint32_t e2 = dw_ctz(x); x &= x - 1ull;
-          const uint32_t e3 = dw_ctz(x);
-          uint32_t b1 = 0, b2 = e2 >= 16u ? 1u : 0u, b3 = e3 >= 16u ? 1u : 0u;
-          const uint32_t v1 = dw_val(lo, e1 + 1u, b1);
-          const uint32_t v2 = dw_val(dw_at(lo, hi, e1 + 1u < 15u ? e1 + 1u : 15u), e2 - e1, b2);
-          const uint32_t v3 = dw_val(dw_at(lo, hi, e2 + 1u < 15u ? e2 + 1u : 15u), e3 - e2, b3);
-          if (ph == WK_UPD) {
-            bad |= b1;
-            q += e1 + 1u;
-            if (v1) { n_left = v1; have_prev = false; ph = WK_BLK; }
-            else ph = MODE == 1 ? WK_DS : WK_FIN;
-          } else if (ph == WK_DS) {   // the delete set is copied verbatim (readDeleteSet + writeDeleteSet)
-            if (!run_on) {
-              bad |= b1;
-              const uint32_t q0 = q;
-              q += e1 + 1u;
-              run_on = true; cp = q0; rs0 = q0; cdst = t; cd0 = t; run_end = DW_OPEN;
-              if (v1) { n_left = v1; have_prev = false; ph = WK_DSC; }
-              else { run_end = q; t = cd0 + (q - q0); bad |= t > tend ? 1u : 0u; ph = WK_FIN; }
-            }
-          } else if (ph == WK_BLK) {   // client block header: structs, client, first clock
-            bad |= b1 | b2 | b3;
-            q += e3 + 1u;
-            if (!bad) block_begin(v1, v2, v3);
-          } else if (ph == WK_DSC) {   // delete-set client: >= 1 range, clients strictly descending
-            bad |= b1 | b2;
-            q += e2 + 1u;
-            bad |= (v2 == 0u || (have_prev && v1 >= prevc)) ? 1u : 0u;
-            prevc = v1; have_prev = true;
-            st_left = v2; ph = WK_DSR;
-          } else {   // WK_DSR: one (clock, len) range, copied verbatim
-            bad |= e2 >= 64u ? 1u : 0u;
-            q += e2 + 1u;
-            if (--st_left == 0u) {
-              if (--n_left == 0u) { run_end = q; t = cd0 + (q - rs0); bad |= t > tend ? 1u : 0u; ph = WK_FIN; }
-              else ph = WK_DSC;
-            }
-          }
-        }
-        if (q > rb) bad = 1;
-      }
-    }
-    if (++rounds > (1u << 26)) { if (l == 0) atomicOr(&meta->fault, 1u); break; }
-  }
-  payload = wave_sum(payload);
-  if (l == 0 && payload) add_payload(meta, blockIdx.x, payload);
-#ifdef YGM_DIAG
-  dg[5] = l == 0 ? rounds : 0;
-  for (int i = 0; i < 8; i++) { const unsigned long long v = wave_sum(dg[i]); if (l == 0) atomicAdd(&ygm_diag[16 + i], v); }
-  if (l == 0) for (int i = 0; i < 5; i++) atomicAdd(&ygm_diag[24 + i], tsec[i]);
-#endif
-#undef WDG
-}
 
 // ======================================================================= merge fast path
 // LDS capacity of one document (class "small").  Documents beyond any of these
@@ -3597,35 +2800,7 @@ __global__ __launch_bounds__(64) void k_merge_seq(const uint8_t* __restrict__ ar
 
 }  // namespace ygm
 
-// ======================================================================= launch glue
-// a failed launch names its kernel and the HIP error on stderr (the C ABI only returns YGM_EDEVICE)
-// persistent grid sizes are cached per device: a pool may drive GPUs of different sizes, its contexts from
-// different threads (the first computation on each device wins; a racing second one stores the same value)
-constexpr int YGM_MAX_DEVICES = 64;
-template <class F>
-static uint32_t per_device(std::atomic<uint32_t> (&cache)[YGM_MAX_DEVICES], F compute) {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::atomic<uint32_t>& slot = cache[(unsigned)dev % YGM_MAX_DEVICES];
-  uint32_t v = slot.load(std::memory_order_relaxed);
-  if (!v) { v = compute(); slot.store(v, std::memory_order_relaxed); }
-  return v;
-}
-static uint32_t device_cus() {
-  static std::atomic<uint32_t> cache[YGM_MAX_DEVICES];
-  return per_device(cache, [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? (uint32_t)n : 256u;
-  });
-}
-
-static int launch_rc(const char* fn) {
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) fprintf(stderr, "ygm: %s: %s\n", fn, hipGetErrorString(e));
-  return (int)e;
-}
-
+// ======================================================================= launch glue (helpers: ygm_docmeta.hpp)
 extern "C" {
 
 using namespace ygm;
@@ -3785,32 +2960,6 @@ int ygm_k_launch_pack(const uint8_t* src, const uint64_t* off, const uint64_t* l
   hipLaunchKernelGGL(k_pack_sum, dim3(nb), dim3(DOC_NT), 0, s, len, status, n, bsum);
   hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(1024), 0, s, bsum, nb);
   hipLaunchKernelGGL(k_pack_copy, dim3(nb), dim3(DOC_NT), 0, s, src, off, len, status, n, (const uint64_t*)bsum, dst, poff);
-  return launch_rc(__func__);
-}
-
-size_t ygm_k_sv_table_bytes(uint32_t n_docs) { return 144ull * n_docs + 64; }
-int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
-                          uint64_t sv_bytes, const uint64_t* sv_off, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off,
-                          uint64_t* out_len, int32_t* status, void* meta, uint32_t* defer_list, uint64_t out_cap, uint8_t* tbl,
-                          uint32_t* tbl_n, hipStream_t s) {
-  (void)arena_bytes; (void)sv_bytes; (void)flags;   // segments are read in 64-byte chunks: 64 bytes of tail padding (ygm.h)
-  if (n_docs == 0) return 0;
-  const int n_cu = (int)device_cus();
-  const char* env = getenv("YGM_WALK_WAVES_PER_CU");
-  // resident waves per CU: 4 SIMDs x the waves per SIMD the walker is compiled for (its LDS fits them)
-  const uint32_t wpc = env ? (uint32_t)atoi(env) : 4u * (mode == 0 ? YGM_DW_WPE0 : YGM_DW_WPE1);
-  const uint32_t waves = (n_docs + WAVE - 1) / WAVE, cap = (uint32_t)n_cu * (wpc ? wpc : 1u);
-  uint32_t grid = waves < cap ? waves : cap;
-  const char* genv = getenv("YGM_WALK_GRID");   // testing: a small grid gives every lane many documents
-  if (genv && atoi(genv) > 0 && (uint32_t)atoi(genv) < grid) grid = (uint32_t)atoi(genv);
-  if (mode == 0)
-    hipLaunchKernelGGL(k_doc_walk<0>, dim3(grid), dim3(WAVE), 0, s, arena, doc_off, (const uint8_t*)nullptr, (const uint32_t*)nullptr,
-                       n_docs, out, out_off, out_len, status, (DocMeta*)meta, defer_list, out_cap);
-  else {
-    hipLaunchKernelGGL(k_sv_table, dim3(waves), dim3(WAVE), 0, s, sv_arena, sv_off, n_docs, tbl, tbl_n);
-    hipLaunchKernelGGL(k_doc_walk<1>, dim3(grid), dim3(WAVE), 0, s, arena, doc_off, (const uint8_t*)tbl, (const uint32_t*)tbl_n, n_docs,
-                       out, out_off, out_len, status, (DocMeta*)meta, defer_list, out_cap);
-  }
   return launch_rc(__func__);
 }
 

@@ -628,12 +628,12 @@ def _walker_svs(ends, seed):
     return svs
 
 
-@pytest.mark.parametrize("grid", [None, "3"])
-def test_walker_states_vs_oracle(eng, grid, monkeypatch):
+@pytest.mark.parametrize("env", [None, "YGM_WALK_GRID=3"])
+def test_walker_states_vs_oracle(eng, env, monkeypatch):
     # the SV / diff ring walker on rich merged-state shapes; grid=3 gives every lane ~10 documents
     # (the per-round hand-over of documents, ring reuse across documents)
-    if grid:
-        monkeypatch.setenv("YGM_WALK_GRID", grid)
+    if env:
+        monkeypatch.setenv(*env.split("="))
     docs, ends = _walker_states(2000, seed=77)
     svs = _walker_svs(ends, seed=78)
     lean0 = eng.stats().docs_lean

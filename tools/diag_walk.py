@@ -26,22 +26,22 @@ ds = torch.from_numpy(np.concatenate([sva, np.zeros(64, np.uint8)])).to(dev)
 dso = torch.from_numpy(sv_off.view(np.int64)).to(dev)
 e = eng.Engine(0)
 L = eng.lib()
-L.ygm_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
-buf = np.zeros(32, np.uint64)
+L.ygm_walk_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+buf = np.zeros(16, np.uint64)
 names = ["fast", "general", "not_ready", "idle", "string", "rounds", "general_iters", "-"]
 for op in ("sv", "diff"):
-    L.ygm_diag_read(buf.ctypes.data, 1)
+    L.ygm_walk_diag_read(buf.ctypes.data, 1)
     s0 = e.stats()
     if op == "sv":
         e.sv_device(da.data_ptr(), len(arena), do.data_ptr(), n)
     else:
         e.diff_device(da.data_ptr(), len(arena), do.data_ptr(), ds.data_ptr(), dso.data_ptr(), n)
     s1 = e.stats()
-    L.ygm_diag_read(buf.ctypes.data, 1)
-    c = {k: int(v) for k, v in zip(names, buf[16:24])}
+    L.ygm_walk_diag_read(buf.ctypes.data, 1)
+    c = {k: int(v) for k, v in zip(names, buf[0:8])}
     tot = sum(c[k] for k in names[:5])
     print(json.dumps({"op": op, "docs": n, "kernel_ms": round(s1.kernel_ms - s0.kernel_ms, 3), **c,
                       "lane_iters": tot, "frac": {k: round(c[k] / max(tot, 1), 3) for k in names[:5]},
                       "general_iter_frac": round(c["general_iters"] / max(c["rounds"] * 8, 1), 3),
-                      "clock_frac": {k: round(int(v) / max(int(buf[24:29].sum()), 1), 3) for k, v in
-                                     zip(["commit", "sv_parse", "grab_out_init", "staging", "parse"], buf[24:29])}}))
+                      "clock_frac": {k: round(int(v) / max(int(buf[8:13].sum()), 1), 3) for k, v in
+                                     zip(["commit", "sv_parse", "grab_out_init", "staging", "parse"], buf[8:13])}}))

@@ -14,7 +14,7 @@ YDEV uint64_t dw_shfl64(uint64_t v, uint32_t src) {
   return ((uint64_t)hi << 32) | lo;
 }
 }
-#include "../../hocuspocus_amd/csrc/ygm_walk_g.hpp"
+#include "ygm_walk_g.hpp"
 extern "C" {
 void *synth_text_states_gen(uint64_t seed, const uint32_t *idx, uint32_t n_docs, uint32_t min_bytes, uint32_t max_bytes,
                             uint32_t min_clients, uint32_t max_clients, uint32_t threads, uint64_t *out_bytes, uint64_t *out_sv_bytes);

@@ -1,3 +1,4 @@
+// Prototype (round 4, not product): the register-window SV walker timed by walkg.hip; kept with its harness.
 // ygm_walk_g.hpp -- encodeStateVectorFromUpdate / diffUpdate walker with the document read through
 // the cache hierarchy into a register window (no LDS ring).  One lane per document: per iteration a
 // lane decodes ONE unit (struct, block header, update header) from a 32-byte register window at its
@@ -5,7 +6,7 @@
 // v_alignbyte; varuint ends come from the window's terminator mask (bit i: byte i < 0x80, by two
 // v_dot4 per 8 bytes).  Without a ring there is no LDS per wave, so occupancy is set by registers.
 #pragma once
-#include "ygm_doc_walk.hpp"
+#include "../../hocuspocus_amd/csrc/ygm_doc_walk.hpp"
 
 namespace ygm {
 

@@ -52,7 +52,8 @@ constexpr int DW_P = DW_S * 4;    // 16-byte pieces per ring
 #define YGM_DW_U 3
 #endif
 constexpr int DW_R = YGM_DW_R;    // parse iterations per round
-constexpr int DW_U = YGM_DW_U;    // Items the fast decoder takes per iteration (from one 64-byte mask window)
+constexpr int DW_U = YGM_DW_U;    // Items the fast decoder takes per iteration (from one 64-byte mask window): SV
+constexpr int DW_U1 = DW_U + 1;   // ... diff (its per-iteration and per-round overhead is larger: 4 measured 2 % faster)
 constexpr uint32_t DW_STG = YGM_DW_STG;   // chunks staged per round (<= 4: 64 staging registers)
 #ifndef YGM_DW_AHEAD
 #define YGM_DW_AHEAD 2
@@ -62,13 +63,48 @@ constexpr int DW_BATCH = 256;     // documents sorted (largest first) per batch 
 constexpr int DW_SVN = 16;        // state-vector entries per lane (diff)
 constexpr uint32_t DW_OPEN = 0xFFFFFFFFu;
 
+#ifndef YGM_DW_LM
+#define YGM_DW_LM 1
+#endif
 // The lane's ring and its chunks' terminator masks in LDS.  (The masks in registers -- four per lane, read by
 // bit-mask selects -- measured slower: the walker is bound by VALU issue, and a select costs more VALU than the
 // LDS read it replaces; profiles/r05_walk/README.md.)
 struct DWLds {
-  u32x4 ring[DW_P][WAVE];         // piece p (16 bytes) of lane l's ring: ring-relative bytes r with (r >> 4) % DW_P == p
-  uint64_t mask[DW_S][WAVE];      // terminator mask of the chunk in each slot (bit i: byte i has its top bit clear)
-};
+  // terminator mask of the chunk in each slot (bit i: byte i has its top bit clear), lane-major, slot 0 repeated as
+  // slot DW_S: the masks of chunks k and k + 1 are adjacent, one ds_read2_b64
+  uint64_t mask[WAVE][DW_S + 1];
+  // YGM_DW_LM 1: lane l's ring is the 256 bytes at 256 l, its stream byte r at (r ^ 16 l) & 255 -- one v_bitop3 per
+  // address (lanes reading the same stream offset land 16 bytes apart: spread over the banks);
+  // 0: piece-major, piece p of lane l at (p * WAVE + l) * 16
+  alignas(16) uint8_t ring[DW_P * WAVE * 16];
+  uint32_t ordk[DW_BATCH];        // the current batch of documents, largest first: (min(bytes + 1, 2^24 - 1) << 8 | index in batch)
+};                                // (one __shared__ object at LDS offset 0, masks first: their addresses need no
+                                  // base add, the ring's base goes in the ds instructions' offset field)
+// the masks of chunks k and k + 1
+YDEV void dw_mask2(const DWLds& L, uint32_t l, uint32_t k, uint64_t& lo, uint64_t& hi) {
+  const uint64_t* m = &L.mask[l][0] + (k & (DW_S - 1));
+  lo = m[0]; hi = m[1];
+}
+// the same from a stream position r (chunk r >> 6): v_bfe + v_lshl_add for the address
+YDEV void dw_mask2r(const DWLds& L, uint32_t l, uint32_t r, uint64_t& lo, uint64_t& hi) {
+  const uint64_t* m = &L.mask[l][0] + __builtin_amdgcn_ubfe(r, 6, 2);
+  lo = m[0]; hi = m[1];
+}
+static_assert(DW_S == 4, "dw_mask2r extracts a 2-bit slot");
+static_assert(DW_S * 64 == 256 || !YGM_DW_LM, "the lane-major ring is 256 bytes per lane");
+// LDS byte offset of stream byte r of lane l's ring
+YDEV uint32_t dw_ra(uint32_t l, uint32_t r) {
+#if YGM_DW_LM
+  const uint32_t K = (l << 8) | ((l << 4) & 0xF0u);
+  // (K & ~0xFF) | ((r ^ K) & 0xFF) as ONE v_bitop3 (M ? r ^ K : K, M = 0xFF; table index 4r + 2K + M: 0x6C) -- the
+  // compiler splits the expression into a bitop3 and an add
+  return __builtin_amdgcn_bitop3_b32(r, K, 0xFFu, 0x6C);
+#else
+  return (((r >> 4) & (DW_P - 1)) * WAVE + l) * 16u + (r & 15u);
+#endif
+}
+YDEV u32x4& dw_piece(DWLds& L, uint32_t l, uint32_t r) { return *(u32x4*)(L.ring + dw_ra(l, r & ~15u)); }
+YDEV const u32x4& dw_piece(const DWLds& L, uint32_t l, uint32_t r) { return *(const u32x4*)(L.ring + dw_ra(l, r & ~15u)); }
 
 enum : uint32_t { WK_IDLE = 0, WK_SVN, WK_SVE, WK_UPD, WK_BLK, WK_ST, WK_STR, WK_DS, WK_DSC, WK_DSR, WK_FIN };
 
@@ -82,12 +118,8 @@ YDEV uint64_t dw_fsh(uint64_t lo, uint64_t hi, uint32_t sh) { return (lo >> sh) 
 YDEV uint32_t dw_vulen(uint32_t v) { return 1u + (((31u - (uint32_t)__builtin_clz(v | 1u)) * 37u) >> 8); }
 
 // the aligned 8 ring bytes at ring-relative x (x % 8 == 0)
-YDEV uint64_t dw_word(const DWLds& L, uint32_t l, uint32_t x) {
-  return ((const uint64_t*)&L.ring[(x >> 4) & (DW_P - 1)][l])[(x >> 3) & 1u];
-}
-YDEV uint32_t dw_byte(const DWLds& L, uint32_t l, uint32_t r) {
-  return ((const uint8_t*)&L.ring[(r >> 4) & (DW_P - 1)][l])[r & 15u];
-}
+YDEV uint64_t dw_word(const DWLds& L, uint32_t l, uint32_t x) { return *(const uint64_t*)(L.ring + dw_ra(l, x)); }
+YDEV uint32_t dw_byte(const DWLds& L, uint32_t l, uint32_t r) { return L.ring[dw_ra(l, r)]; }
 // 16 bytes at ring-relative r as (lo, hi)
 YDEV void dw_rd16(const DWLds& L, uint32_t l, uint32_t r, uint64_t& lo, uint64_t& hi) {
   const uint32_t A = r & ~7u, sh = (r & 7u) * 8u;
@@ -103,7 +135,7 @@ YDEV uint64_t dw_rd8(const DWLds& L, uint32_t l, uint32_t r) {
 YDEV uint64_t dw_at(uint64_t lo, uint64_t hi, uint32_t p) { return p >= 8u ? (hi >> (8u * (p - 8u))) : dw_fsh(lo, hi, 8u * p); }
 // 16 ring bytes at any alignment (for the output stream)
 YDEV u32x4 dw_ring16(const DWLds& L, uint32_t l, uint32_t r) {
-  const u32x4 a = L.ring[(r >> 4) & (DW_P - 1)][l], b = L.ring[((r >> 4) + 1u) & (DW_P - 1)][l];
+  const u32x4 a = dw_piece(L, l, r), b = dw_piece(L, l, r + 16u);
   const uint32_t s = (r >> 2) & 3u, sh = r & 3u;
   // dword s + j of (a, b) for j = 0..4 by bit-mask selects: a ?: over array elements is turned into a
   // scratch-indexed load by the compiler (one scratch round trip per copy-run head)
@@ -124,9 +156,9 @@ YDEV u32x4 dw_ring16(const DWLds& L, uint32_t l, uint32_t r) {
 // landed read as "no terminator" (only used where the segment ends before them).
 YDEV uint64_t dw_win(const DWLds& L, uint32_t l, uint32_t r, uint32_t landed) {
   const uint32_t k = r >> 6;
-  const uint64_t lo = L.mask[k & (DW_S - 1)][l];
-  const uint64_t hi = k + 1u < landed ? L.mask[(k + 1u) & (DW_S - 1)][l] : 0ull;
-  return dw_fsh(lo, hi, r & 63u);
+  uint64_t lo, hi;
+  dw_mask2r(L, l, r, lo, hi);
+  return dw_fsh(lo, k + 1u < landed ? hi : 0ull, r & 63u);
 }
 // value of the n-byte varuint (n = 1..5) in the low bytes of w; bad when n is outside 1..5 or >= 2^32
 YDEV uint32_t dw_val(uint64_t w, uint32_t n, uint32_t& bad) {
@@ -158,10 +190,10 @@ template <bool BP>
 YDEV void dw_commit(DWLds& L, uint32_t l, uint32_t k, const u32x4& p0, const u32x4& p1, const u32x4& p2, const u32x4& p3,
                     uint32_t vlo, uint32_t vhi, uint32_t& prev8, uint32_t& bad) {
   const uint32_t s = k & (DW_S - 1);
-  L.ring[s * 4 + 0][l] = p0;
-  L.ring[s * 4 + 1][l] = p1;
-  L.ring[s * 4 + 2][l] = p2;
-  L.ring[s * 4 + 3][l] = p3;
+  dw_piece(L, l, 64u * k) = p0;
+  dw_piece(L, l, 64u * k + 16u) = p1;
+  dw_piece(L, l, 64u * k + 32u) = p2;
+  dw_piece(L, l, 64u * k + 48u) = p3;
   const uint32_t D[16] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};
   uint64_t H = 0, Z = 0;
 #pragma unroll
@@ -174,7 +206,8 @@ YDEV void dw_commit(DWLds& L, uint32_t l, uint32_t k, const u32x4& p0, const u32
       Z |= (uint64_t)hibits8(za, zb) << (8 * j);
     }
   }
-  L.mask[s][l] = ~H;
+  L.mask[l][s] = ~H;
+  if (s == 0u) L.mask[l][DW_S] = ~H;
   const uint64_t vm = dw_lowmask(vhi) & ~dw_lowmask(vlo);
   const uint64_t Hm = H & vm;
   const uint64_t r2 = Hm & (Hm >> 1), r4 = r2 & (r2 >> 2), r6 = r4 & (r2 >> 4);

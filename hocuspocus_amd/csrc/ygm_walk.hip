@@ -78,10 +78,6 @@ __global__ __launch_bounds__(WAVE) void k_sv_table(const uint8_t* __restrict__ s
   tbl_n[d] = n;
 }
 
-#ifndef YGM_DW_SPEC
-#define YGM_DW_SPEC 0   // 1: fast decoder reads both candidate content-length bytes beside the info byte (A/B: slower,
-                        // profiles/r03_walk/README.md -- the walker is issue-bound, not LDS-latency-bound)
-#endif
 #ifndef YGM_DW_WPE0
 #define YGM_DW_WPE0 2   // waves per SIMD the SV walker is compiled for (register budget 512 / waves)
 #endif
@@ -95,7 +91,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
                                                   uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
                                                   uint32_t* __restrict__ defer_list, uint64_t out_cap) {
   __shared__ DWLds L;
-  __shared__ uint64_t ordk[DW_BATCH];      // the current batch of documents, largest first: (bytes << 32 | index in batch)
+  uint32_t* ordk = L.ordk;
   const uint32_t l = threadIdx.x;
   const uint32_t D1 = (uint32_t)((uint64_t)n_docs * (blockIdx.x + 1) / gridDim.x);
   uint32_t bnext = (uint32_t)((uint64_t)n_docs * blockIdx.x / gridDim.x);   // wave-uniform: first document of the next batch
@@ -107,7 +103,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
   auto prefetch = [&]() {
     pa = 0; pb = 0; ptn = 0; pd = 0;
     if (next + l < bn) {
-      pd = bbase + (uint32_t)ordk[next + l];
+      pd = bbase + (ordk[next + l] & 0xFFu);
       pa = doc_off[pd]; pb = doc_off[pd + 1];
       if (MODE == 1) ptn = tbl_n[pd];
     }
@@ -211,14 +207,14 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
       for (uint32_t e = l; e < (uint32_t)DW_BATCH; e += WAVE) {
         // key bytes + 1 (padding entries past bn: 0, sorted behind every document)
         const uint64_t sz = e < bn ? doc_off[bbase + e + 1] - doc_off[bbase + e] + 1ull : 0ull;
-        ordk[e] = ((sz < 0xFFFFFFFFull ? sz : 0xFFFFFFFFull) << 32) | e;
+        ordk[e] = ((uint32_t)(sz < 0xFFFFFFull ? sz : 0xFFFFFFull) << 8) | e;
       }
       __syncthreads();
       for (uint32_t kk = 2; kk <= (uint32_t)DW_BATCH; kk <<= 1)
         for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
           for (uint32_t t2 = l; t2 < (uint32_t)DW_BATCH / 2; t2 += WAVE) {
             const uint32_t lo = ((t2 / jj) * 2 * jj) + (t2 % jj), hi = lo + jj;
-            const uint64_t x = ordk[lo], y = ordk[hi];
+            const uint32_t x = ordk[lo], y = ordk[hi];
             if ((x < y) == ((lo & kk) == 0)) { ordk[lo] = y; ordk[hi] = x; }   // descending
           }
           __syncthreads();
@@ -322,7 +318,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
               cp += a; cdst += a;
             }
             for (; cp < ce; cp += 16u, cdst += 16u) {   // whole ring pieces
-              const u32x4 v = L.ring[(cp >> 4) & (DW_P - 1)][l];
+              const u32x4 v = dw_piece(L, l, cp);
               __builtin_memcpy(ob + cdst, &v, 16);
             }
             cdst -= cp - ce; cp = ce;
@@ -411,68 +407,74 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
       const uint32_t avl = lend > q ? lend - q : 0u;
       bool done = false;
       if (avl && (ph == WK_ST || ph == WK_BLK || ph == WK_UPD || (MODE == 1 && ph == WK_DS))) {
-        const uint32_t kq = q >> 6, sq = q & 63u;
-        const uint64_t m0 = L.mask[kq & (DW_S - 1)][l], m1 = L.mask[(kq + 1u) & (DW_S - 1)][l];
+        const uint32_t sq = q & 63u;
+        uint64_t m0, m1;
+        dw_mask2r(L, l, q, m0, m1);
         // bytes q .. q + 63 (chunks past the segment may hold stale masks: every unit is checked against rb)
         const uint64_t w64 = (m0 >> sq) | ((m1 << (63u - sq)) << 1);
         const uint32_t w32 = (uint32_t)w64;
         const uint32_t b0 = dw_byte(L, l, q);
-        if (ph == WK_ST) {   // Item with origin(s), one-byte String (ASCII) / Deleted length, inside 32 bytes;
-                             // a second one right behind it from the same 64-byte window
+        if (ph == WK_ST) {   // Items with origin(s), one-byte String (ASCII) / Deleted length, inside 32 bytes:
+                             // up to DW_U from the same 64-byte window.  Block ends and (diff) block headers are
+                             // handled once after the loop, not in each of its unrolled steps
           uint32_t qo = 0, bb = b0;
+          const uint32_t lim = avl < 64u ? avl : 64u;   // a unit ends inside the landed bytes and the 64-byte window
+          bool go = true;   // (ph == WK_ST implies st_left >= 1)
+          bool pe = false;  // diff: the step that stopped the loop is the block's first struct past the state vector
+          uint32_t pe_end = 0, pe_ce = 0;
 #pragma unroll
-          for (int u = 0; u < DW_U; u++) {
+          for (int u = 0; u < (MODE == 1 ? DW_U1 : DW_U); u++) {
             const uint32_t wq = (uint32_t)(w64 >> qo);
             const uint32_t tt = wq >> 1, x2 = tt & (tt - 1u), x3 = x2 & (x2 - 1u), x4 = x3 & (x3 - 1u);
-#if YGM_DW_SPEC
-            // the content length's position for one and for two origin ids comes from the mask alone: both
-            // candidate bytes are read beside the info byte (one LDS round trip per Item, not two)
-            const uint32_t c2 = (uint32_t)__builtin_ctz(x2 | 0x80000000u) + 2u, c4 = (uint32_t)__builtin_ctz(x4 | 0x80000000u) + 2u;
-            const uint32_t lv2 = dw_byte(L, l, q + (c2 & 31u)), lv4 = dw_byte(L, l, q + (c4 & 31u));
-            if (u >= 1) bb = dw_byte(L, l, q);
-            const uint32_t hoh = bb >> 6, ref = bb & 0x3Fu;
-            const uint32_t cpos = hoh == 3u ? c4 : c2;   // after the origins
-            const uint32_t cq = cpos & 31u;
-            const uint32_t lv = hoh == 3u ? lv4 : lv2;
-#else
             if (u >= 1) bb = dw_byte(L, l, q);
             const uint32_t hoh = bb >> 6, ref = bb & 0x3Fu;
             const uint32_t cpos = (uint32_t)__builtin_ctz((hoh == 3u ? x4 : x2) | 0x80000000u) + 2u;   // after the origins
             const uint32_t cq = cpos & 31u;
             const uint32_t lv = dw_byte(L, l, q + cq);
-#endif
-            const uint32_t isS = ref == 4u ? 1u : 0u;
+            const bool isS = ref == 4u;
             const uint32_t end = cq + 1u + (isS ? lv : 0u);
-            const uint32_t mk = isS ? (((1u << (lv & 31u)) - 1u) << ((cq + 1u) & 31u)) : 0u;   // the string's bytes: ASCII
+            // the string's bytes are ASCII: every one of them ends a varuint (no clear bit among the lv after the length)
+            // (bits past the 32-bit window never count: end <= 32 below keeps the string inside it)
+            const bool asc = (uint32_t)__builtin_ctz((~wq >> ((cq + 1u) & 31u)) | 0x80000000u) >= lv;
             const uint32_t ce = clock + lv;
-            uint32_t ok = (ph == WK_ST) & (hoh != 0u) & (isS | (ref == 1u)) & (cpos < 31u) & (wq >> cq) & (lv != 0u) &
-                          (end <= 32u) & ((wq & mk) == mk) & (ce >= clock) & (qo + end <= avl) & (u == 0 || (done && qo + end <= 64u));
-            uint32_t emit = 0;
-            if (MODE == 0) ok &= (st_left != 1u) | !e_on;
+            // (boolean terms as comparisons: lane masks combined by the scalar unit, no VALU materialisation)
+            bool ok = go & (hoh != 0u) & (isS | (ref == 1u)) & (cpos < 31u) & (__builtin_amdgcn_ubfe(wq, cq, 1) != 0u) &
+                      (lv != 0u) & (end <= 32u) & (!isS | asc) & (ce >= clock) & (qo + end <= lim);
+            if (MODE == 0) ok &= (st_left != 1u) | !e_on;   // the block's last struct queues its entry
             else {
-              emit = (!emitted) & (ce > svc);
-              ok &= (!emit) | ((svc <= clock) & !e_on & !run_on);   // a cut struct: the general decoder
+              const bool emit = !emitted & (ce > svc);
+              // a cut struct (svc > clock) or a header / copy run still in flight: the general decoder / a later round
+              if (ok & emit) { pe = (svc <= clock) & !e_on & !run_on; pe_end = end; pe_ce = ce; }
+              ok &= !emit;
             }
             if (ok) {
-              done = true;
+              WDG(7, 1);   // Items taken by the fast decoder
               if (MODE == 0) {
                 clk = stop ? clk : ce;   // (no Skips here: the first-struct seeding is the same)
                 fst = false;
-              } else if (emit) {
-                const uint32_t hl = dw_vulen(st_left) + dw_vulen(client) + dw_vulen(clock);
-                if (t + hl > tend) bad = 1;
-                else {
-                  e_on = true; e_dst = t; e_a = st_left; e_b = client; e_c = clock; e_pl = 0; e_q = q;
-                  t += hl;
-                  run_on = true; cp = q; rs0 = q; cdst = t; cd0 = t; run_end = DW_OPEN;
-                  emitted = true; count++;
-                }
               }
               clock = ce;
               q += end; qo += end;
-              if (--st_left == 0u) block_end();
+              --st_left;
             }
+            go = ok && st_left != 0u;
           }
+          if (MODE == 1 && pe) {   // the first struct of the block past the state vector (rule R-D): the block
+                                   // header, then the rest of the block as a copy run from this struct on
+            const uint32_t hl = dw_vulen(st_left) + dw_vulen(client) + dw_vulen(clock);
+            if (t + hl > tend) bad = 1;
+            else {
+              e_on = true; e_dst = t; e_a = st_left; e_b = client; e_c = clock; e_pl = 0; e_q = q;
+              t += hl;
+              run_on = true; cp = q; rs0 = q; cdst = t; cd0 = t; run_end = DW_OPEN;
+              emitted = true; count++;
+            }
+            clock = pe_ce;
+            q += pe_end;
+            --st_left;
+          }
+          done = qo != 0u || pe;
+          if (st_left == 0u) block_end();
         } else if (ph == WK_BLK && blk_it) {   // block header: <= 2-byte count, <= 5-byte client, one-byte clock
           const uint32_t y = w32 & (w32 - 1u), z = y & (y - 1u);
           const uint32_t e1 = (uint32_t)__builtin_ctz(w32 | 0x80000000u), e2 = (uint32_t)__builtin_ctz(y | 0x80000000u);

@@ -28,7 +28,7 @@ e = eng.Engine(0)
 L = eng.lib()
 L.ygm_walk_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = np.zeros(16, np.uint64)
-names = ["fast", "general", "not_ready", "idle", "string", "rounds", "general_iters", "-"]
+names = ["fast", "general", "not_ready", "idle", "string", "rounds", "general_iters", "fast_items"]
 for op in ("sv", "diff"):
     L.ygm_walk_diag_read(buf.ctypes.data, 1)
     s0 = e.stats()
@@ -43,5 +43,6 @@ for op in ("sv", "diff"):
     print(json.dumps({"op": op, "docs": n, "kernel_ms": round(s1.kernel_ms - s0.kernel_ms, 3), **c,
                       "lane_iters": tot, "frac": {k: round(c[k] / max(tot, 1), 3) for k in names[:5]},
                       "general_iter_frac": round(c["general_iters"] / max(c["rounds"] * 8, 1), 3),
+                      "items_per_fast_lane_iter": round(c["fast_items"] / max(c["fast"], 1), 3),
                       "clock_frac": {k: round(int(v) / max(int(buf[8:13].sum()), 1), 3) for k, v in
                                      zip(["commit", "sv_parse", "grab_out_init", "staging", "parse"], buf[8:13])}}))

@@ -18,7 +18,7 @@ the lean kernel -- asserted -- so no step needs the host-driven tiers).  Beside 
   c2_mixed C2 past the lean kernel's envelope: 1-8 clients, 1-16 character inserts, 20 % deletions (tier cascade)
   c3       config C3 at full size (configs[2]): 100 000 [snapshot, ...log] documents of 10 MB * rank^-0.8 (0.77 GB)
            merged in one batch through the tier cascade, beside the C port and yjs (rank 0 at N = 1)
-  c5       config C5 at BASELINE size (configs[4]): 1 000 Y.XmlFragment [snapshot, ...log] documents of 5-10 k client
+  c5       config C5 at BASELINE size (configs[4]): 1 000 Y.XmlFragment [snapshot, ...log] documents of 10 000 client
            blocks each (0.29 GB), formats / embeds / attributes, merged in one batch, beside the C port and yjs
   v2       SURVEY.md §8f-4: the C2 merge with the updates in format V2 (Y.mergeUpdatesV2), and the V1 <-> V2
            conversions of its 2 M updates
@@ -809,7 +809,8 @@ def run_rank(args, rank, world, dist, be, dev=None):
         blk["roofline"] = roof(blk["bytes_in"] + blk["bytes_out"], blk["gpu_ms"], "merge cascade (k_big_scan + k_merge_big mid / 16-wave sizes + "
                                "lean / wave for the routing)", _pmc(PMC_BLOCKS, "c3full"))
         line["c3"] = blk
-    # ---- C5 at BASELINE size (1 000 XmlFragment [snapshot, ...log] documents of 5-10 k client blocks): rank 0 at N = 1
+    # ---- C5 at BASELINE size (1 000 XmlFragment [snapshot, ...log] documents, exactly max_clients = 10 000 client blocks per snapshot,
+    #      tools/synth.c): rank 0 at N = 1
     if args.c5_docs and rank == 0 and world == 1 and not args.dry_run:
         a5 = argparse.Namespace(**vars(args))
         a5.big_docs = args.c5_docs

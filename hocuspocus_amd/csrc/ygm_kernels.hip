@@ -148,6 +148,7 @@ struct MergeLds {
   uint32_t d_len[M_DCAP];
   uint64_t dA[M_DCAP];
   uint32_t dB[M_DCAP], dC[M_DCAP], dE[M_DCAP], dF[M_DCAP];
+  uint32_t d_cl[M_DCAP], d_rk[M_DCAP];   // by record: client; first-seen rank (update << 16 | range in it: yjs 13.5)
   uint64_t tmp64[M_NT / WAVE + 1];
   uint32_t tmp32[M_NT / WAVE + 1];
   int err, fb, nc;
@@ -208,6 +209,7 @@ YDEV_NI void m_parse_update(MergeLds& L, int i, int pass, uint32_t flags) {
         const uint32_t j = d_at + nd;
         L.dkey[j] = ((uint64_t)(0xFFFFFFFFu - (uint32_t)cl) << 32) | (uint32_t)ck;
         L.didx[j] = (uint16_t)j; L.d_len[j] = (uint32_t)ln;
+        L.d_cl[j] = (uint32_t)cl; L.d_rk[j] = ((uint32_t)i << 16) | (uint32_t)nd;
       }
       nd++;
     }
@@ -258,7 +260,6 @@ YDEV void merge_fast_doc(MergeLds& L, uint32_t d, const uint8_t* __restrict__ ar
       S = (int)block_scan_array<M_NT>(L.uns, (int)k, L.tmp32);
       D = (int)block_scan_array<M_NT>(L.und, (int)k, L.tmp32);
       if (S > M_SCAP || D > M_DCAP) st = ST_FALLBACK;
-      else if ((flags & F_COMPAT_135) && D > 0) st = ST_FALLBACK;  // first-seen DS order: sequential kernel
       else if (L.nc) st = ST_NONCANON;
     }
   }
@@ -269,6 +270,18 @@ YDEV void merge_fast_doc(MergeLds& L, uint32_t d, const uint8_t* __restrict__ ar
     for (int j = S + t; j < NS; j += M_NT) { L.key[j] = ~0ull; L.idx[j] = 0xFFFF; }
     for (int j = D + t; j < ND; j += M_NT) { L.dkey[j] = ~0ull; L.didx[j] = 0xFFFF; }
     __syncthreads();
+    if (flags & F_COMPAT_135) {
+      // yjs 13.5 writes the merged delete set's clients in first-seen order (mergeDeleteSets' Map insertion order,
+      // Y@10486): a client's key is its least record rank instead of its complement, so the sort groups its ranges
+      // in that order (ranks of different clients differ; the client itself is read from d_cl)
+      for (int j = t; j < D; j += M_NT) {
+        const uint32_t c = L.d_cl[j];
+        uint32_t r = L.d_rk[j];
+        for (int q = 0; q < D; q++) if (L.d_cl[q] == c && L.d_rk[q] < r) r = L.d_rk[q];
+        L.dkey[j] = ((uint64_t)r << 32) | (uint32_t)L.dkey[j];
+      }
+      __syncthreads();
+    }
     DIAG(2);
     bitonic_sort<M_NT>(L.key, L.idx, NS);
     bitonic_sort<M_NT>(L.dkey, L.didx, ND);
@@ -378,7 +391,7 @@ YDEV void merge_fast_doc(MergeLds& L, uint32_t d, const uint8_t* __restrict__ ar
     __syncthreads();
     for (int j = t; j < D; j += M_NT) {
       const uint32_t f = L.dF[j]; const uint64_t kj = L.dkey[j];
-      const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(kj >> 32), ck = (uint32_t)kj;
+      const uint32_t cl = L.d_cl[L.didx[j]], ck = (uint32_t)kj;
       uint32_t sz = 0;
       if (f & 1u) sz += vu_len(cl) + vu_len(L.dC[L.dB[j]]);
       if (f & 2u) sz += vu_len(ck) + vu_len(L.dE[j] - ck);
@@ -431,7 +444,7 @@ YDEV void merge_fast_doc(MergeLds& L, uint32_t d, const uint8_t* __restrict__ ar
   const uint32_t dh = vu_len(L.nseg);
   for (int j = t; j < D; j += M_NT) {
     const uint32_t f = L.dF[j]; const uint64_t kj = L.dkey[j];
-    const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(kj >> 32), ck = (uint32_t)kj;
+    const uint32_t cl = L.d_cl[L.didx[j]], ck = (uint32_t)kj;
     Out w{o + dsb + dh + (uint32_t)L.dA[j], 0};
     if (f & 1u) { w.vu(cl); w.vu(L.dC[L.dB[j]]); }
     if (f & 2u) { w.vu(ck); w.vu(L.dE[j] - ck); }
@@ -525,7 +538,7 @@ YDEV void merge_wave_doc(WaveLds& L, uint32_t d, const uint8_t* __restrict__ are
     ekey = wave_min_u32(ekey);
     S = L.nrec; D = L.ndel;
     if (ekey != 0xFFFFFFFFu) st = (int)(ekey & 0xFF);
-    else if (__ballot(fb) || S > (uint32_t)W_S || D > (uint32_t)W_D || ((flags & F_COMPAT_135) && D > 0)) st = ST_DEFER;
+    else if (__ballot(fb) || S > (uint32_t)W_S || D > (uint32_t)W_D) st = ST_DEFER;
     else if (__ballot(nc)) st = ST_NONCANON;
     if (st == ST_OK) {
       // ---- clients: distinct values by wave vote, ranked descending
@@ -662,11 +675,28 @@ YDEV void merge_wave_doc(WaveLds& L, uint32_t d, const uint8_t* __restrict__ are
           DIAGW(3);
           // ---- delete set: rank sort, segments (clients, descending) and runs (rule R-DS)
           if (D) {
-            uint64_t mk[W_DE]; uint32_t ml[W_DE], rk[W_DE];
+            uint64_t mk[W_DE]; uint32_t ml[W_DE], rk[W_DE], mc[W_DE];
 #pragma unroll
             for (int q = 0; q < W_DE; q++) {
               const uint32_t j = l + WAVE * q;
-              mk[q] = j < D ? L.dkey[j] : ~0ull; ml[q] = j < D ? L.dlen[j] : 0; rk[q] = 0;
+              mk[q] = j < D ? L.dkey[j] : ~0ull; ml[q] = j < D ? L.dlen[j] : 0; rk[q] = 0; mc[q] = j < D ? L.dcl[j] : 0;
+            }
+            if (flags & F_COMPAT_135) {
+              // yjs 13.5: the merged delete set's clients in first-seen order (Y@10486) -- a client's key is its least
+              // record rank (update << 8 | range in it, parked in drunend by the parse) instead of its complement
+#pragma unroll
+              for (int q = 0; q < W_DE; q++) {
+                uint32_t r = l + WAVE * q < D ? L.drunend[l + WAVE * q] : 0u;
+                for (uint32_t i = 0; i < D; i++) {
+                  const uint32_t ri = L.drunend[i];
+                  r = L.dcl[i] == mc[q] && ri < r ? ri : r;
+                }
+                if (l + WAVE * q < D) mk[q] = ((uint64_t)r << 32) | (uint32_t)mk[q];
+              }
+              wave_sync();
+#pragma unroll
+              for (int q = 0; q < W_DE; q++) if (l + WAVE * q < D) L.dkey[l + WAVE * q] = mk[q];
+              wave_sync();
             }
             for (uint32_t i = 0; i < D; i++) {
               const uint64_t ki = L.dkey[i];
@@ -675,7 +705,7 @@ YDEV void merge_wave_doc(WaveLds& L, uint32_t d, const uint8_t* __restrict__ are
             }
             wave_sync();
 #pragma unroll
-            for (int q = 0; q < W_DE; q++) if (l + WAVE * q < D) { L.dkey[rk[q]] = mk[q]; L.dlen[rk[q]] = ml[q]; }
+            for (int q = 0; q < W_DE; q++) if (l + WAVE * q < D) { L.dkey[rk[q]] = mk[q]; L.dlen[rk[q]] = ml[q]; L.dcl[rk[q]] = mc[q]; }
             for (uint32_t j = l; j < D; j += WAVE) L.drunend[j] = 0;
             for (uint32_t j = l; j < W_BLK; j += WAVE) L.segcnt[j] = 0;
             wave_sync();
@@ -715,7 +745,7 @@ YDEV void merge_wave_doc(WaveLds& L, uint32_t d, const uint8_t* __restrict__ are
           wave_sync();
           uint32_t dacc = 0;
           for (uint32_t j = d0; j < d1; j++) {
-            const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.dkey[j] >> 32), ck = (uint32_t)L.dkey[j];
+            const uint32_t cl = L.dcl[j], ck = (uint32_t)L.dkey[j];
             uint32_t sz = 0;
             if (L.dflag[j] & 1) sz += vu_len(cl) + vu_len(L.segcnt[L.dflag[j] >> 2]);
             if (L.dflag[j] & 2) sz += vu_len(ck) + vu_len(L.drunend[j] - ck);
@@ -782,7 +812,7 @@ YDEV void merge_wave_doc(WaveLds& L, uint32_t d, const uint8_t* __restrict__ are
   const uint32_t d0 = l * W_DE, d1 = min(d0 + W_DE, D);
   LWriter dw{lo, dsb + vu_len(nseg) + (d0 < D ? L.dposs[d0] : dsbytes)};
   for (uint32_t j = d0; j < d1; j++) {
-    const uint32_t cl = 0xFFFFFFFFu - (uint32_t)(L.dkey[j] >> 32), ck = (uint32_t)L.dkey[j];
+    const uint32_t cl = L.dcl[j], ck = (uint32_t)L.dkey[j];
     if (L.dflag[j] & 1) { dw.vu(cl); dw.vu(L.segcnt[L.dflag[j] >> 2]); }
     if (L.dflag[j] & 2) { dw.vu(ck); dw.vu(L.drunend[j] - ck); }
   }

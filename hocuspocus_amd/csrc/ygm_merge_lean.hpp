@@ -471,6 +471,7 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
   LDsUnion U; U.bad = false; U.nsegs = 0; U.bytes = 1; U.segstart = false; U.runend = false; U.pos = 0;
   U.client = 0; U.nruns = 0; U.sclock = 0; U.rend = 0;
   LB32* rc = scr; LB32* rk = scr + LN_DSMAX; LB32* re = scr + 2 * LN_DSMAX;
+  LB32* rn = scr + 3 * LN_DSMAX;   // yjs 13.5 only: the record's first-seen rank (update << 8 | range index in it)
   uint32_t nrec = 0, bad = 0;
   LDS_T0
   // ---- records of every update's DS, in update order (the order only matters for ties, which
@@ -501,7 +502,7 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
     {
       const uint64_t m = __ballot(fq);
       const uint32_t slot = nrec + lanes_below(m);
-      if (fq && slot < (uint32_t)LN_DSMAX) { rc[slot] = fcl; rk[slot] = fck; re[slot] = fck + fln; }
+      if (fq && slot < (uint32_t)LN_DSMAX) { rc[slot] = fcl; rk[slot] = fck; re[slot] = fck + fln; rn[slot] = (l + 64u * q) << 8; }
       nrec += (uint32_t)__builtin_popcountll(m);
     }
     const bool slow = hasd[q] && !fq;
@@ -517,7 +518,7 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
       has = has && c.bad == 0u;
       const uint64_t m = __ballot(has);
       const uint32_t slot = nrec + lanes_below(m);
-      if (has && slot < (uint32_t)LN_DSMAX) { rc[slot] = cl; rk[slot] = ck; re[slot] = ck + ln; }
+      if (has && slot < (uint32_t)LN_DSMAX) { rc[slot] = cl; rk[slot] = ck; re[slot] = ck + ln; rn[slot] = ((l + 64u * q) << 8) | (uint32_t)it; }
       nrec += (uint32_t)__builtin_popcountll(m);
     }
     bad |= c.bad | (lean_ds_more(c) ? 1u : 0u);   // malformed, or more ranges than the loop takes
@@ -533,7 +534,27 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
   lane_bitonic3(k0, k1, k2);
   LDS_STAMP(1);
   // lane l holds the l-th record of the union order; its end from the record table (re is not rewritten)
-  const uint32_t c = v ? ~k0 : 0u, k = v ? k1 : 0u, e = v ? re[k2 & (LN_DSMAX - 1)] : 0u;
+  uint32_t c = v ? ~k0 : 0u, k = v ? k1 : 0u, e = v ? re[k2 & (LN_DSMAX - 1)] : 0u;
+  if (flags & 1u) {
+    // yjs 13.5.16 writes the merged delete set's clients in first-seen order (mergeDeleteSets' Map insertion order:
+    // the first update holding the client, its position in that update's delete set; Y@10486, Y@11105).  Each
+    // client's rank is the least rank of its records; the records are sorted again by (rank, clock, record) --
+    // clients stay contiguous, so the runs below are the same, in that order.
+    const uint32_t cp0 = (uint32_t)__shfl_up((int)c, 1u, 64);
+    const bool ss0 = v && (l == 0u || cp0 != c);
+    const uint32_t si0 = dpp_incl_add(ss0 ? 1u : 0u);   // (1-based) client segment of the lane
+    const uint64_t mx = lean_max_scan64(v ? (((uint64_t)si0 << 32) | (uint32_t)~rn[k2 & (LN_DSMAX - 1)]) : 0ull);
+    const bool nss0 = __shfl_down(ss0 ? 1 : 0, 1u, 64) != 0;
+    const bool se0 = v && (l + 1u == nrec || nss0);   // the segment's last lane holds its least rank
+    LB32* T = rk;                                      // (rk is not read after the sort: the clock is in the key)
+    wave_sync();
+    if (se0) T[si0 - 1u] = ~(uint32_t)mx;
+    wave_sync();
+    uint32_t s0 = v ? T[si0 - 1u] : 0xFFFFFFFFu, s1 = v ? k : 0xFFFFFFFFu, s2 = v ? k2 : 0xFFu;
+    lane_bitonic3(s0, s1, s2);
+    c = v ? rc[s2 & (LN_DSMAX - 1)] : 0u; k = v ? s1 : 0u; e = v ? re[s2 & (LN_DSMAX - 1)] : 0u;
+    wave_sync();   // (rc is rewritten below)
+  }
   const uint32_t cprev = (uint32_t)__shfl_up((int)c, 1u, 64);
   // ---- runs: a range starts a run when it is its client's first or starts past every end so far
   const bool segstart = v && (l == 0u || cprev != c);
@@ -561,7 +582,6 @@ YDEV LDsUnion lean_ds_union(LB8* lin, LB32* scr, const uint32_t (&dpos)[LN_ROWS]
   U.client = c; U.nruns = nruns; U.sclock = sclock; U.rend = (uint32_t)incl;
   U.segstart = segstart; U.runend = runend; U.pos = ib - tb;
   U.nsegs = nsegs; U.bytes = vlen32(nsegs) + lane63(ib);
-  U.bad = (flags & 1u) && nsegs > 1u;   // yjs 13.5 writes clients in first-seen order: general path
   LDS_STAMP(2);
   return U;
 }

@@ -51,7 +51,8 @@ struct alignas(16) WaveLds {
   uint8_t dflag[W_D];        // bit 0 segment start, bit 1 run start, bits 2-7 segment id
   uint16_t dposs[W_D];
   uint32_t segcnt[W_BLK];
-  uint32_t drunend[W_D];
+  uint32_t drunend[W_D];     // (the parse parks each record's first-seen rank here: yjs 13.5's client order)
+  uint32_t dcl[W_D];         // by record, then permuted with dkey: client
   uint32_t nrec, ndel;
 };
 
@@ -302,6 +303,7 @@ YDEV UpdCount w_parse_update(LWave* L, int i, uint32_t flags) {
     }
   }
   const uint64_t ncl = r.err ? 0 : r.vu();
+  uint32_t rr = 0;   // ranges of this update so far: (update << 8 | rr) is the range's first-seen rank
   for (uint64_t q = 0; q < ncl && !r.err; q++) {
     const uint64_t cl = r.vu(), nr = r.vu();
     for (uint64_t k = 0; k < nr && !r.err; k++) {
@@ -310,8 +312,12 @@ YDEV UpdCount w_parse_update(LWave* L, int i, uint32_t flags) {
       if (cl > 0xFFFFFFFFull || ck + ln > 0xFFFFFFFFull) fb = true;
       if (!fb) {
         const uint32_t j = wave_slot(&L->ndel);
-        if (j < (uint32_t)W_D) { L->dkey[j] = ((uint64_t)(0xFFFFFFFFu - (uint32_t)cl) << 32) | (uint32_t)ck; L->dlen[j] = (uint32_t)ln; }
+        if (j < (uint32_t)W_D) {
+          L->dkey[j] = ((uint64_t)(0xFFFFFFFFu - (uint32_t)cl) << 32) | (uint32_t)ck; L->dlen[j] = (uint32_t)ln;
+          L->dcl[j] = (uint32_t)cl; L->drunend[j] = ((uint32_t)i << 8) | (rr < 255u ? rr : 255u);
+        }
       }
+      rr++;
     }
   }
   return UpdCount{r.err, fb ? 1u : 0u, nc ? 1u : 0u};

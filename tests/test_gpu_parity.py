@@ -710,12 +710,39 @@ def test_lean_kernel_delete_sets_vs_oracle(eng):
     assert len(docs) // 10 < took < len(docs)   # both paths (updates > 32 bytes defer)
 
 
-def test_lean_kernel_delete_sets_compat135_vs_oracle(eng135):
-    # yjs 13.5 writes delete-set clients in first-seen order: single-client unions stay lean
-    docs = _lean_ds_docs(600, seed=607)
+def test_lean_kernel_delete_sets_compat135_vs_oracle(eng, eng135):
+    # yjs 13.5 writes delete-set clients in first-seen order (mergeDeleteSets' Map insertion order): the lean, wave
+    # and workgroup tiers order the union's clients by their least (update, range) rank -- the 13.5 mode sends no
+    # more documents to the sequential kernel than the 13.6 mode does (> 64 ranges: the wave tier; > 128: the
+    # workgroup tier)
+    docs = _lean_ds_docs(1500, seed=607)
+    st0 = eng135.stats()
     res = eng135.merge_updates_batch(docs)
     bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us, compat135=True), res[d])]
     assert not bad, (len(bad), [u.hex() for u in docs[bad[0]]])
+    st1 = eng135.stats()
+    s0 = eng.stats().docs_seq
+    eng.merge_updates_batch(docs)
+    assert st1.docs_seq - st0.docs_seq == eng.stats().docs_seq - s0
+    assert st1.docs_fast - st0.docs_fast > 0 and st1.docs_lean - st0.docs_lean > len(docs) // 10
+
+
+def test_compat135_multi_client_c2_deletions_stay_parallel(eng135):
+    # C2 logs of 2-4 clients with 20 % deletions under yjs 13.5 -- multi-client delete-set unions in
+    # first-seen client order, bit-exact, and not one document on the sequential kernel
+    from tools import synth
+    arena, upd_off, doc_upd = synth.text_updates(2000, 200, min_clients=2, max_clients=4, del_pct=20, seed=135)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(2000)]
+    st0 = eng135.stats()
+    res = eng135.merge_updates_batch(docs)
+    st1 = eng135.stats()
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us, compat135=True), res[d])]
+    assert not bad, (len(bad), bad[:5])
+    assert st1.docs_seq - st0.docs_seq == 0
+    # the 13.5 order is not the 13.6 one on most of these documents (the test would not see a wrong order otherwise)
+    differ = sum(oracle.merge_updates(us, compat135=True) != oracle.merge_updates(us) for us in docs[:200])
+    assert differ > 50
 
 
 @pytest.mark.parametrize("xml", [False, True])

@@ -1261,11 +1261,12 @@ template <class T>
 YDEV void big_bitonic(T* a, uint32_t n) {   // ascending by key; n <= 1024 (entries [n, pow2) padded)
   uint32_t P = 1;
   while (P < n) P <<= 1;
-  for (uint32_t i = n + threadIdx.x; i < P; i += WAVE) a[i].key = ~0ull;
+  const uint32_t l = threadIdx.x % WAVE;   // (one wave sorts: the lane, whichever wave of the workgroup it is)
+  for (uint32_t i = n + l; i < P; i += WAVE) a[i].key = ~0ull;
   wave_sync();
   for (uint32_t k = 2; k <= P; k <<= 1)
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < P; i += WAVE) {
+      for (uint32_t i = l; i < P; i += WAVE) {
         const uint32_t x = i ^ j;
         if (x > i) {
           const T A = a[i], B = a[x];
@@ -1276,7 +1277,7 @@ YDEV void big_bitonic(T* a, uint32_t n) {   // ascending by key; n <= 1024 (entr
     }
 }
 YDEV void big_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {   // the wave copies n bytes, 16 per lane-step
-  for (uint64_t c = 16ull * threadIdx.x; c < n; c += 16ull * WAVE) {
+  for (uint64_t c = 16ull * (threadIdx.x % WAVE); c < n; c += 16ull * WAVE) {
     if (c + 16 <= n) { uint4 v; __builtin_memcpy(&v, src + c, 16); __builtin_memcpy(dst + c, &v, 16); }
     else for (uint64_t q = c; q < n; q++) dst[q] = src[q];
   }
@@ -1329,7 +1330,7 @@ struct BigOut {
   uint8_t* o; uint64_t n; bool w;
   BigCp* cl; uint32_t nc, cap, *pre;
   uint64_t ls, ld, le;                                  // the last entry: source, destination, destination end
-  YDEV void b(uint32_t v) { if (w && threadIdx.x == 0) o[n] = (uint8_t)v; n++; }
+  YDEV void b(uint32_t v) { if (w && threadIdx.x % WAVE == 0) o[n] = (uint8_t)v; n++; }   // (lane 0 of the writing wave)
   YDEV void vu(uint64_t v) { while (v > 127) { b(0x80u | (uint32_t)(v & 127)); v >>= 7; } b((uint32_t)v); }
   YDEV void flush() { if (nc) { wave_sync(); big_copy_list(o, cl, nc, pre); nc = 0; } }
   YDEV void add(uint64_t src, uint64_t dst, uint64_t len) {
@@ -1337,10 +1338,10 @@ struct BigOut {
   }
   YDEV void add1(uint64_t src, uint64_t dst, uint64_t len) {   // len < 2^30
     if (nc && le == dst && ls + (le - ld) == src && le - ld + len < (1ull << 30)) {   // continues the last entry
-      if (threadIdx.x == 0) cl[nc - 1].n = (uint32_t)(le - ld + len);
+      if (threadIdx.x % WAVE == 0) cl[nc - 1].n = (uint32_t)(le - ld + len);
     } else {
       if (nc == cap) flush();
-      if (threadIdx.x == 0) { BigCp E; E.src = src; E.dst = (uint32_t)dst; E.n = (uint32_t)len; cl[nc] = E; }
+      if (threadIdx.x % WAVE == 0) { BigCp E; E.src = src; E.dst = (uint32_t)dst; E.n = (uint32_t)len; cl[nc] = E; }
       nc++; ls = src; ld = dst;
     }
     le = dst + len;
@@ -2239,20 +2240,28 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   __shared__ uint32_t s_rst[CF::CH / 2], s_ren[CF::CH / 2];   // byte ranges of the current tile's structs (>= 2 bytes each)
   __shared__ BigBlk s_blk[64];
   __shared__ uint32_t s_cpre[WAVE];
-  if (threadIdx.x >= WAVE) {   // helper waves: wave 0's tile commands until it sends 0 (one barrier pair per command)
+#ifndef YGM_BIG_ROT
+#define YGM_BIG_ROT 0
+#endif
+  // the logical thread index: the chain-follow wave (logical wave 0) is physical wave blockIdx.x % WAVES, so the
+  // followers of the mid size's workgroups sharing a CU do not all land on one SIMD (they are latency chains: four on
+  // one SIMD share its issue while the helpers' SIMDs idle)
+  const uint32_t tid = YGM_BIG_ROT && CF::MID ? (threadIdx.x + CF::THREADS - WAVE * (blockIdx.x % CF::WAVES)) % CF::THREADS
+                                              : threadIdx.x;
+  if (tid >= WAVE) {   // helper waves: wave 0's tile commands until it sends 0 (one barrier pair per command)
     for (;;) {
       __syncthreads();
       const BigCmd C = s_cmd;
       if (C.cmd == 0) return;
-      if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.mis, C.n0, threadIdx.x);
-      else if (C.cmd == 3) { if (big_clock_ranges<CF::THREADS>(blk, rec, C, threadIdx.x)) L.bad = 1; }
-      else if (C.cmd == 4) { if (!big_ds_canon<CF::THREADS>(C, threadIdx.x)) s_cmd.tb = 1; }
-      else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, threadIdx.x)) L.bad = 1;
+      if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.mis, C.n0, tid);
+      else if (C.cmd == 3) { if (big_clock_ranges<CF::THREADS>(blk, rec, C, tid)) L.bad = 1; }
+      else if (C.cmd == 4) { if (!big_ds_canon<CF::THREADS>(C, tid)) s_cmd.tb = 1; }
+      else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, tid)) L.bad = 1;
       __syncthreads();
-      if (C.cmd == 1) big_prefetch<CF::CH, CF::THREADS - WAVE>(C, threadIdx.x - WAVE);   // (while wave 0 follows the chain)
+      if (C.cmd == 1) big_prefetch<CF::CH, CF::THREADS - WAVE>(C, tid - WAVE);   // (while wave 0 follows the chain)
     }
   }
-  const uint32_t l = threadIdx.x;
+  const uint32_t l = tid;
   DIAGL_T0
   const uint32_t w = fbx ? fbx[blockIdx.x] : blockIdx.x;   // index into fb_list (and the scan's picks)
   const uint32_t d = fb_list[w];

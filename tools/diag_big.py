@@ -36,6 +36,10 @@ print("follow counts (2 runs): blocks", int(cnt[16]), "jump steps", int(cnt[17])
       "global parses", int(cnt[19]), "slow headers", int(cnt[20]))
 st = e.stats()
 print("docs_big", st.docs_big, "docs_seq", st.docs_seq)
+# follow time by part over both runs (slots 25-28, wave 0 shader cycles): tile loads + spec, block headers, struct
+# steps, block tails
+print("follow cycles (2 runs): tile", int(cnt[25]), "headers", int(cnt[26]), "structs", int(cnt[27]), "tails", int(cnt[28]),
+      "per block:", {k: round(int(cnt[i]) / max(int(cnt[16]), 1), 1) for k, i in (("tile", 25), ("hdr", 26), ("st", 27), ("tail", 28))})
 t = ts.reshape(16384, 8)[:n].astype(np.int64)
 # stamps: start, log walk, U0 walk, sorts, pass0, pass1; slots 6 / 7: time inside the U0 walk spent in
 # the speculative tile parse / in validation

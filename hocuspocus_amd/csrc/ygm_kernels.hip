@@ -1674,8 +1674,12 @@ YDEV bool big_hdr_fast(const TL& T, uint32_t hp, uint32_t tn, uint64_t& nst, uin
   hend = hp + e2 + 1u;
   return true;
 }
+#ifndef YGM_BIG_BH
+#define YGM_BIG_BH 1
+#endif
 template <class CF>
-YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint32_t mis, uint32_t n0, uint32_t t0) {
+YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint32_t mis, uint32_t n0, uint32_t t0, uint16_t* bh,
+                   bool use_bh) {
   // the scan's struct ends of the tile's positions, tile-relative (an end 32 KB or more away: no entry, the chain
   // follow parses that struct from global memory)
   for (uint32_t i = t0; i < CF::CH; i += CF::THREADS) {
@@ -1694,6 +1698,26 @@ YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint3
       const uint32_t a = big_jump(T, k - 1, i);
       T.jp[k][i] = (uint16_t)(a < CF::CH ? big_jump(T, k - 1, a) : BJ_NONE);
     }
+  }
+  if (!YGM_BIG_BH || !use_bh) return;   // (documents of large blocks: the table would not be used, C3)
+  // the block table: bh[i] = the tile position right after the whole client block whose header would start at tile
+  // position i (the header decoded from the tile, then its nst structs jumped through the tables along the bits of
+  // nst), or BJ_NONE (no header parse, nst 0 or >= 64, a struct without a table entry or starting past the tile's CH
+  // positions).  The chain follow then steps from block to block with one lookup each.
+  __syncthreads();
+  const uint32_t tn = n0 - (at - mis) < CF::TILE ? n0 - (at - mis) : CF::TILE;
+  for (uint32_t i = t0; i < CF::CH; i += CF::THREADS) {
+    uint32_t S = BJ_NONE;
+    uint64_t nst, cl, ck;
+    uint32_t he;
+    bool nm;
+    if (at + i < n0 && big_hdr_fast(T, mis + i, tn, nst, cl, ck, he, nm) && nst != 0u && nst < 64u) {
+      S = he - mis;
+#pragma unroll
+      for (int k = 0; k < 6; k++)
+        if ((nst >> k) & 1u) S = S < CF::CH ? big_jump(T, k - 1, S) : BJ_NONE;
+    }
+    bh[i] = (uint16_t)S;
   }
 }
 // after a tile's spec (cmd 1): the helper waves touch the next tile's bytes and both tiles' scan words, a load per
@@ -2238,8 +2262,11 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   __shared__ uint64_t s_base, s_sbase, s_ds0, s_at;
   __shared__ BigCmd s_cmd;
   __shared__ uint32_t s_rst[CF::CH / 2], s_ren[CF::CH / 2];   // byte ranges of the current tile's structs (>= 2 bytes each)
-  __shared__ BigBlk s_blk[64];
+  constexpr uint32_t SBQ = CF::MID ? 24u : 64u;   // block records staged in LDS before a store (mid: room for s_bh)
+  __shared__ BigBlk s_blk[SBQ];
   __shared__ uint32_t s_cpre[WAVE];
+  __shared__ uint16_t s_bh[YGM_BIG_BH ? CF::CH : 1];   // the tile's block table (big_spec)
+  __shared__ uint16_t s_hl[WAVE + 2];                  // a run of blocks found from it: their tile positions
 #ifndef YGM_BIG_ROT
 #define YGM_BIG_ROT 0
 #endif
@@ -2253,7 +2280,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
       __syncthreads();
       const BigCmd C = s_cmd;
       if (C.cmd == 0) return;
-      if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.mis, C.n0, tid);
+      if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.mis, C.n0, tid, s_bh, C.tb != 0u);
       else if (C.cmd == 3) { if (big_clock_ranges<CF::THREADS>(blk, rec, C, tid)) L.bad = 1; }
       else if (C.cmd == 4) { if (!big_ds_canon<CF::THREADS>(C, tid)) s_cmd.tb = 1; }
       else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, tid)) L.bad = 1;
@@ -2348,6 +2375,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   DIAG_C(uint64_t dc_blk = 0, dc_step = 0, dc_st = 0, dc_glob = 0, dc_hslow = 0;)   // ... and follow counts
   DIAG_C(uint64_t dt_hdr = 0, dt_st = 0, dt_tail = 0, dt_tile = 0;)                   // ... and follow time by part
   const uint8_t* const tp = (const uint8_t*)T0.b;
+  bool use_bh = false;   // the block table pays for documents of small blocks (C5: 10 000 blocks in <= 1.3 MB)
   auto load_tile = [&](uint32_t at, bool spec) {
     const uint32_t mis = (uint32_t)((uintptr_t)(u0p + at) & 15u);
     const uint4* g = (const uint4*)(u0p + at - mis);
@@ -2359,9 +2387,9 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
     wave_sync();
     if (!spec) return;
     const uint64_t dg0 = DIAG_NOW();
-    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.n0 = n0; s_cmd.aux = nxg; s_cmd.u0p = u0p; }
+    if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.n0 = n0; s_cmd.aux = nxg; s_cmd.u0p = u0p; s_cmd.tb = use_bh ? 1u : 0u; }
     __syncthreads();
-    big_spec<CF>(T0, nxg, at, mis, n0, l);
+    big_spec<CF>(T0, nxg, at, mis, n0, l, s_bh, use_bh);
     __syncthreads();
     dg_spec += DIAG_NOW() - dg0;
   };
@@ -2382,6 +2410,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
     GCur c; c.init(u0p, n0);
     bool bad = false;
     nb = c.vu();
+    use_bh = YGM_BIG_BH && nb * 256ull > (uint64_t)n0;   // (average block under 256 bytes)
     if (l == 0) { s_base = atomicAdd(&meta->big_cursor, (unsigned long long)nb); s_sbase = atomicAdd(&meta->big_scur, (unsigned long long)ncap); }
     wave_sync();
     base = s_base; sbase = s_sbase;
@@ -2399,10 +2428,65 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
       bq = 0;
       wave_sync();
     };
-    for (uint64_t b = 0; b < nb && !bad; b++) {
+    for (uint64_t b = 0; b < nb && !bad;) {
       DIAG_C(const uint64_t dq0 = DIAG_NOW();)
       if (!have || pos >= tc0 + CF::CH) { if (have) validate(); load_tile(pos, true); have = true; }
       DIAG_C(const uint64_t dq1 = DIAG_NOW(); dt_tile += dq1 - dq0;)
+      if (YGM_BIG_BH && use_bh) {
+        // ---- a run of whole blocks from the tile's block table (big_spec): lane 0 chains their header positions, one
+        //      LDS lookup per block; the lanes then decode the headers and record the structs, a block each
+        const uint32_t cap = SBQ - bq < (uint32_t)WAVE ? SBQ - bq : (uint32_t)WAVE;
+        const uint32_t lim = nb - b < (uint64_t)cap ? (uint32_t)(nb - b) : cap;
+        if (l == 0) {
+          uint32_t p = pos - tc0, nh = 0;
+          while (nh < lim && p < CF::CH) {
+            const uint32_t e = s_bh[p];
+            if (e == BJ_NONE) break;
+            s_hl[nh++] = (uint16_t)p; p = e;
+          }
+          s_hl[WAVE] = (uint16_t)nh; s_hl[WAVE + 1] = (uint16_t)p;
+        }
+        wave_sync();
+        const uint32_t nh = s_hl[WAVE], pend = s_hl[WAVE + 1];
+        if (nh) {
+          const bool on = l < nh;
+          const uint32_t hp = on ? (uint32_t)s_hl[l] : 0u, mis = tc0 - tb;   // (tile coordinates: mis + relative position)
+          uint64_t hn = 0, hc = 0, hk = 0;
+          uint32_t he = mis;
+          bool hnm = false;
+          const bool okh = on && big_hdr_fast(T0, mis + hp, tn, hn, hc, hk, he, hnm);
+          const uint32_t nst = okh ? (uint32_t)hn : 0u;   // (1 .. 63: the table's condition)
+          const uint32_t inc = dpp_incl_add(nst), ex = inc - nst, tot = lane63(inc);
+          const uint32_t r0 = (uint32_t)(NS - vs) + ex;
+          uint32_t S = he - mis, fg = 0, lg = 0;
+          for (uint32_t q = 0; q < nst; q++) {   // (every struct start of the block is < CH: the table's condition)
+            const uint32_t E = T0.nx[S];
+            s_rst[r0 + q] = tc0 + S; s_ren[r0 + q] = tc0 + (E & 0x7FFFu);
+            if (q == 0) fg = (E >> 15) & 1u;
+            lg = (E >> 15) & 1u;
+            S = E & 0x7FFFu;
+          }
+          // client blocks strictly descending (from the block before the run), clients < 2^32
+          const uint32_t plo = (uint32_t)__shfl_up((int)(uint32_t)hc, 1u, WAVE), phi = (uint32_t)__shfl_up((int)(uint32_t)(hc >> 32), 1u, WAVE);
+          const uint64_t hprev = l == 0 ? prevc : (((uint64_t)phi << 32) | plo);
+          bad |= __ballot(on && (!okh || hc >= hprev || hc > 0xFFFFFFFFull)) != 0;
+          acanon &= __ballot(on && hnm) == 0;
+          if (on) {
+            BigBlk& B = s_blk[bq + l];
+            B.nst = nst; B.client = hc; B.clock0 = hk; B.clock1 = 0;
+            B.h0 = tc0 + hp; B.hcanon = !hnm; B.pad = 0; B.b0 = he + tb; B.s0 = (uint32_t)(NS + ex);
+            B.b1 = tc0 + S; B.first_gc = (uint8_t)fg; B.last_gc = (uint8_t)lg;
+          }
+          const uint32_t ql = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hc, (int)nh - 1);
+          const uint32_t qh = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hc >> 32), (int)nh - 1);
+          prevc = ((uint64_t)qh << 32) | ql;
+          NS += tot; b += nh; bq += nh;
+          pos = tc0 + pend;
+          DIAG_C(dc_blk += nh; dc_st += tot;)
+          if (bq == SBQ) flush_blk(b);
+          continue;
+        }
+      }
       uint64_t hn, hc, hk;
       uint32_t he;
       bool hnm;
@@ -2467,10 +2551,11 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
         pos = end;
       }
       DIAG_C(const uint64_t dq3 = DIAG_NOW(); dt_st += dq3 - dq2;)
-      if (!bad) {   // staged in LDS, stored 64 at a time (a store per block would be waited on by the next block's loads)
+      if (!bad) {   // staged in LDS, stored SBQ at a time (a store per block would be waited on by the next block's loads)
         if (l == 0) { BigBlk& B = s_blk[bq]; B.b1 = pos; B.first_gc = (uint8_t)fgc; B.last_gc = (uint8_t)lgc; }
-        if (++bq == 64u) flush_blk(b + 1);
+        if (++bq == SBQ) flush_blk(b + 1);
       }
+      b++;
       DIAG_C(dt_tail += DIAG_NOW() - dq3;)
     }
     if (!bad && bq) flush_blk(nb);

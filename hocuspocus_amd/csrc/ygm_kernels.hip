@@ -1538,6 +1538,9 @@ __global__ __launch_bounds__(1024) void k_big_pick(const uint64_t* __restrict__ 
   if (ok)
     for (uint32_t t = l; t < nt; t += WAVE) S.task[tb + t] = make_uint2(w, t);
 }
+#ifndef YGM_SCAN_LDS
+#define YGM_SCAN_LDS 1
+#endif
 __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                   const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
                                                   uint32_t flags, BigScan S) {
@@ -1580,7 +1583,11 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
       uint32_t e = 0, v = 0;
       bool slow = false;
       if (j < qn) {
+#if YGM_SCAN_LDS
+        LCur c; c.init((LU8*)lb, se - w0); c.pos = i;   // (LDS-typed reads of the stage)
+#else
         GCur c; c.init(lb, se - w0); c.pos = i;
+#endif
         uint32_t kind;
         uint64_t cv = 0;
         bool ok = big_skip(c, kind, 8, &cv) && !c.err;
@@ -1626,18 +1633,46 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
   }
 }
 // the scan's slow queue: big_struct's verdict for the candidates of other kinds (after k_big_scan, same stream)
+// Each lane stages its candidate's bytes -- the aligned 16-byte chunks of [pos, pos + BIG_VCAP] (the queued structs
+// parse in at most BIG_VCAP bytes), loads issued together -- into its LDS slot and validates from there: one load
+// latency per candidate instead of a chain of dependent window loads through a global-memory cursor.
+#ifndef YGM_VAL_LDS
+#define YGM_VAL_LDS 1
+#endif
 __global__ __launch_bounds__(256) void k_big_val(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                  const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
                                                  uint32_t flags, BigScan S) {
+  constexpr uint32_t VW = (BIG_VCAP + 16u + 15u) / 16u;   // 16-byte chunks staged per candidate
+  __shared__ uint4 s_w[YGM_VAL_LDS ? 256 : 1][VW];
   const uint64_t nq = *(volatile unsigned long long*)&S.cnt[4], n = nq < S.vq_cap ? nq : S.vq_cap;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
     const uint2 Q = S.vq[i];
     const BigPick P = S.pick[Q.x];
     const uint8_t* u0p = arena + upd_off[doc_upd[fb_list[Q.x]] + P.u0];
     const uint32_t wd = S.nv[P.pb + Q.y], end = Q.y + (wd & 0x7FFFu);
+#if YGM_VAL_LDS
+    const uint8_t* src = u0p + Q.y;
+    const uint32_t sh = (uint32_t)((uintptr_t)src & 15u);
+    const uint4* g16 = (const uint4*)(src - sh);
+    const uint32_t lim = P.n0 - Q.y < VW * 16u - sh ? P.n0 - Q.y : VW * 16u - sh;   // bytes of U0 in the slot
+    uint4* slot = s_w[threadIdx.x];
+#pragma unroll
+    for (uint32_t k = 0; k < VW; k++) {   // (a chunk holding a byte of U0 is inside the arena: its tail padding)
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (16u * k < sh + lim) v = g16[k];
+      slot[k] = v;
+    }
+    LCur w; w.init((LU8*)slot + sh, lim);
+    const GStruct g = big_struct(w, flags);
+    const bool at_end = w.pos == (wd & 0x7FFFu);
+#else
+    (void)s_w;
     GCur w; w.init(u0p, P.n0); w.pos = Q.y;
     const GStruct g = big_struct(w, flags);
-    S.nv[P.pb + Q.y] = (wd & 0xFFFFu) | (big_v16(g.len, g.ok && w.pos == end && g.len != 0 && g.len < 0xFFFFFFFFull) << 16);
+    const bool at_end = w.pos == end;
+#endif
+    (void)end;
+    S.nv[P.pb + Q.y] = (wd & 0xFFFFu) | (big_v16(g.len, g.ok && at_end && g.len != 0 && g.len < 0xFFFFFFFFull) << 16);
   }
 }
 // the struct start 2^(k+1) structs after tile position i < BT_CH (k = -1: the next one, from nx), or BJ_NONE

@@ -37,6 +37,7 @@ struct GCur {
   uintptr_t wa;                  // absolute address of the window (16-byte aligned); 1 = none
   uint32_t w0, w1, w2, w3;
   YDEV void init(const uint8_t* base, uint32_t n) { p = base; pos = 0; end = n; err = 0; nm = 0; wa = 1; }
+  YDEV const uint8_t* gp() const { return p; }   // the bytes through a generic pointer (content checks)
   YDEV void fail(int e) { if (!err) err = e; pos = end; }
   YDEV uint32_t raw(uint32_t q) {        // byte at p + q (q < end: the aligned chunk is inside the arena)
     const uint8_t* ap = p + q;
@@ -63,6 +64,60 @@ struct GCur {
       const uint64_t t = ~v8 & 0x8080808080808080ull;
       const uint32_t k = t ? (uint32_t)__builtin_ctzll(t) >> 3 : 8u;          // terminator byte index
       if (k < 8u && k < 16u - o && pos + k < end) {
+        const uint64_t num = pext7(v8, k + 1);
+        if (num > MAX_SAFE) { fail(ST_RANGE); return 0; }
+        if (k > 0 && ((v8 >> (8 * k)) & 0xFFu) == 0) nm = 1;
+        pos += k + 1;
+        return num;
+      }
+    }
+    uint64_t num = 0; uint32_t shift = 0;
+    for (;;) {
+      if (pos >= end) { fail(ST_MALFORMED); return 0; }
+      const uint32_t r = raw(pos++);
+      if (shift < 63) num |= (uint64_t)(r & 127u) << shift;
+      else if (r & 127u) { fail(ST_RANGE); return 0; }
+      shift += 7;
+      if (r < 128u) {
+        if (num > MAX_SAFE) { fail(ST_RANGE); return 0; }
+        if (r == 0 && shift > 7) nm = 1;
+        return num;
+      }
+      if (num > MAX_SAFE) { fail(ST_RANGE); return 0; }
+    }
+  }
+  YDEV uint32_t buf(uint32_t& len) {
+    const uint64_t n = vu();
+    if (err) { len = 0; return pos; }
+    if (n > (uint64_t)(end - pos)) { fail(ST_MALFORMED); len = 0; return pos; }
+    const uint32_t s = pos; pos += (uint32_t)n; len = (uint32_t)n; return s;
+  }
+};
+
+// ---- the same cursor over bytes staged in LDS (the snapshot scan's stage): LDS-typed reads (ds_read, not flat loads
+// through a generic pointer), a varuint from one 8-byte view built of three aligned dwords.  Reads reach 11 bytes
+// past `end` (the stage's slack).
+struct LCur {
+  LU8* p;
+  uint32_t pos, end;
+  int err, nm;
+  YDEV void init(LU8* base, uint32_t n) { p = base; pos = 0; end = n; err = 0; nm = 0; }
+  YDEV const uint8_t* gp() const { return (const uint8_t*)p; }
+  YDEV void fail(int e) { if (!err) err = e; pos = end; }
+  YDEV uint32_t raw(uint32_t q) const { return p[q]; }
+  YDEV uint64_t w8(uint32_t q) const {   // the 8 bytes at p + q
+    const uint32_t a = (uint32_t)(uintptr_t)(p + q), sh = a & 3u;
+    const __attribute__((address_space(3))) uint32_t* d = (const __attribute__((address_space(3))) uint32_t*)(p + q - sh);
+    const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
+    return ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32) | __builtin_amdgcn_alignbyte(d1, d0, sh);
+  }
+  YDEV uint32_t u8() { if (pos >= end) { fail(ST_MALFORMED); return 0; } return raw(pos++); }
+  YDEV uint64_t vu() {   // lib0 readVarUint (Cur::vu semantics)
+    if (pos < end) {
+      const uint64_t v8 = w8(pos);
+      const uint64_t t = ~v8 & 0x8080808080808080ull;
+      const uint32_t k = t ? (uint32_t)__builtin_ctzll(t) >> 3 : 8u;   // terminator byte index
+      if (k < 8u && pos + k < end) {
         const uint64_t num = pext7(v8, k + 1);
         if (num > MAX_SAFE) { fail(ST_RANGE); return 0; }
         if (k > 0 && ((v8 >> (8 * k)) & 0xFFu) == 0) nm = 1;
@@ -132,7 +187,8 @@ YDEV int64_t gutf8_u16(const uint8_t* s, uint32_t n) {
 // if write_struct(off = 0) reproduces its bytes (canonical info byte, parentInfo 0/1, minimal
 // varuints, canonical content).  Returns the clock length; kind: 0 GC, 1 Item; ok = false defers.
 struct GStruct { uint64_t len; uint32_t kind; bool ok; };
-YDEV GStruct big_struct(GCur& c, uint32_t flags) {
+template <class CUR = GCur>
+YDEV GStruct big_struct(CUR& c, uint32_t flags) {
   GStruct R; R.len = 0; R.kind = 1; R.ok = false;
   c.nm = 0;
   const uint32_t info = c.u8();
@@ -150,10 +206,10 @@ YDEV GStruct big_struct(GCur& c, uint32_t flags) {
   if (hr) { c.vu(); c.vu(); }
   if (!ho && !hr) {
     const uint64_t pi = c.vu();
-    if (pi == 1) { uint32_t l; const uint32_t s0 = c.buf(l); if (!c.err && gutf8_u16(c.p + s0, l) < 0) return R; }
+    if (pi == 1) { uint32_t l; const uint32_t s0 = c.buf(l); if (!c.err && gutf8_u16(c.gp() + s0, l) < 0) return R; }
     else if (pi == 0) { c.vu(); c.vu(); }
     else return R;                                                 // parentInfo re-encoded as 0
-    if (info & 0x20u) { uint32_t l; const uint32_t s0 = c.buf(l); if (!c.err && gutf8_u16(c.p + s0, l) < 0) return R; }
+    if (info & 0x20u) { uint32_t l; const uint32_t s0 = c.buf(l); if (!c.err && gutf8_u16(c.gp() + s0, l) < 0) return R; }
   }
   if (c.err || c.nm) return R;
   bool nc = false;
@@ -163,8 +219,8 @@ YDEV GStruct big_struct(GCur& c, uint32_t flags) {
       const uint64_t n = c.vu();
       for (uint64_t k = 0; k < n && !c.err; k++) {
         uint32_t l; const uint32_t s = c.buf(l); if (c.err) break;
-        if (gutf8_u16(c.p + s, l) < 0) return R;
-        const uint8_t* t = c.p + s;
+        if (gutf8_u16(c.gp() + s, l) < 0) return R;
+        const uint8_t* t = c.gp() + s;
         if (l == 9 && t[0] == 'u' && t[1] == 'n' && t[2] == 'd' && t[3] == 'e' && t[4] == 'f' && t[5] == 'i' && t[6] == 'n' && t[7] == 'e' && t[8] == 'd') continue;
         if (json_check_t<SM_DEPTH, SM_KEYS>(t, l, nc)) return R;
       }
@@ -173,30 +229,30 @@ YDEV GStruct big_struct(GCur& c, uint32_t flags) {
     case 3: { uint32_t l; c.buf(l); R.len = 1; break; }            // ContentBinary
     case 4: {                                                      // ContentString
       uint32_t l; const uint32_t s = c.buf(l); if (c.err) return R;
-      const int64_t u = gutf8_u16(c.p + s, l);
+      const int64_t u = gutf8_u16(c.gp() + s, l);
       if (u < 0) return R;
       R.len = (uint64_t)u; break;
     }
     case 5: {                                                      // ContentEmbed
       uint32_t l; const uint32_t s = c.buf(l); if (c.err) return R;
-      if (gutf8_u16(c.p + s, l) < 0 || json_check_t<SM_DEPTH, SM_KEYS>(c.p + s, l, nc)) return R;
+      if (gutf8_u16(c.gp() + s, l) < 0 || json_check_t<SM_DEPTH, SM_KEYS>(c.gp() + s, l, nc)) return R;
       R.len = 1; break;
     }
     case 6: {                                                      // ContentFormat
       uint32_t l; uint32_t s = c.buf(l); if (c.err) return R;
-      if (gutf8_u16(c.p + s, l) < 0) return R;
+      if (gutf8_u16(c.gp() + s, l) < 0) return R;
       s = c.buf(l); if (c.err) return R;
-      if (gutf8_u16(c.p + s, l) < 0 || json_check_t<SM_DEPTH, SM_KEYS>(c.p + s, l, nc)) return R;
+      if (gutf8_u16(c.gp() + s, l) < 0 || json_check_t<SM_DEPTH, SM_KEYS>(c.gp() + s, l, nc)) return R;
       R.len = 1; break;
     }
     case 7: {                                                      // ContentType
       const uint64_t tr = c.vu(); if (c.err || tr > 6) return R;
-      if (tr == 3 || tr == 5) { uint32_t l; const uint32_t s = c.buf(l); if (c.err || gutf8_u16(c.p + s, l) < 0) return R; }
+      if (tr == 3 || tr == 5) { uint32_t l; const uint32_t s = c.buf(l); if (c.err || gutf8_u16(c.gp() + s, l) < 0) return R; }
       R.len = 1; break;
     }
     case 8: {                                                      // ContentAny (e.g. XmlElement attributes)
       const uint64_t n = c.vu(); if (c.err || n == 0) return R;
-      Cur q{c.p, c.pos, c.end, 0, 0};
+      Cur q{c.gp(), c.pos, c.end, 0, 0};
       for (uint64_t k = 0; k < n && !q.err; k++) any_value_t<SM_DEPTH, SM_KEYS>(q, nc, flags);   // readAny + would writeAny reproduce it
       if (q.err) return R;
       c.pos = q.pos;
@@ -241,8 +297,8 @@ YDEV_NI bool gany_skip(GCur& c, uint64_t n) {
 // kind (0 GC, 1 Item); validation and lengths come later, in parallel (big_struct).  false: a
 // Skip, Any / Doc content or an unknown ref -- the document goes on to the general path.
 // cv (the scan): GC's / ContentDeleted's length, or ContentString's bytes as start << 32 | length
-template <bool ANY = false>   // ANY: any ContentAny (the out-of-line fallback parse); else scalar values only
-YDEV bool big_skip(GCur& c, uint32_t& kind, uint64_t jcap = ~0ull, uint64_t* cv = nullptr) {   // jcap: most ContentJSON entries taken
+template <bool ANY = false, class CUR = GCur>   // ANY: any ContentAny (the out-of-line fallback parse); else scalar values only
+YDEV bool big_skip(CUR& c, uint32_t& kind, uint64_t jcap = ~0ull, uint64_t* cv = nullptr) {   // jcap: most ContentJSON entries taken
   const uint32_t info = c.u8();
   kind = 1;
   if (c.err || info == 10u) return false;
@@ -265,7 +321,7 @@ YDEV bool big_skip(GCur& c, uint32_t& kind, uint64_t jcap = ~0ull, uint64_t* cv 
     case 8: {
       const uint64_t n = c.vu();
       if (c.err) return false;
-      if (ANY) { if (!gany_skip(c, n)) return false; break; }
+      if constexpr (ANY) { if (!gany_skip(c, n)) return false; break; }
       if (n > jcap) return false;
       for (uint64_t k = 0; k < n && !c.err; k++) {   // the speculative parse takes scalar values only (attributes)
         const uint32_t tag = c.u8();

@@ -1491,7 +1491,14 @@ constexpr uint32_t BIG_MID_U0 = YGM_BIG_MID_KB * 1024u;
 YDEV bool big_cand(uint32_t ib) { const uint32_t rf = ib & 31u; return ib == 0u || (rf >= 1u && rf <= 8u && !((ib & 0xC0u) && (ib & 0x20u))); }
 // U0 of each large document (the largest update, the first of equal ones: k_merge_big's rule) and its scan tasks
 // (a wave per document, 16 per workgroup: the workgroup carves its positions and tasks with one atomic each)
-__global__ __launch_bounds__(1024) void k_big_pick(const uint64_t* __restrict__ upd_off, const uint32_t* __restrict__ doc_upd,
+// A snapshot of many small client blocks (C5: 10 000 blocks of ~100 bytes) over YGM_BIG_SMALLBLK_KB goes to the 16-wave
+// size too: its follow steps block to block through the tile's block table, and the 16-wave size's 4 KB tiles cost a
+// quarter of the mid size's per-tile work (loads, jump and block tables, validation) per byte.
+#ifndef YGM_BIG_SMALLBLK_KB
+#define YGM_BIG_SMALLBLK_KB 512
+#endif
+__global__ __launch_bounds__(1024) void k_big_pick(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+                                                   const uint32_t* __restrict__ doc_upd,
                                                    const uint32_t* __restrict__ fb_list, uint32_t n_fb, BigScan S) {
   __shared__ uint64_t s_pb[16], s_tb[16];
   __shared__ uint32_t s_lg[16], s_lb, s_mb;
@@ -1509,9 +1516,16 @@ __global__ __launch_bounds__(1024) void k_big_pick(const uint64_t* __restrict__ 
     u0 = 0xFFFFFFFFu - (uint32_t)best; n0 = (uint32_t)(best >> 32);
     nt = n0 < 0x7FFFFFFFu ? (n0 + BIG_SCAN_CH - 1u) / BIG_SCAN_CH : 0u;
   }
+  bool small_blocks = false;   // U0's block count (its first varuint) against its bytes: blocks of < 256 bytes on average
+  if (l == 0 && w < n_fb && n0 > YGM_BIG_SMALLBLK_KB * 1024u && n0 < 0x7FFFFFFFu) {
+    const uint8_t* u0p = arena + upd_off[doc_upd[fb_list[w]] + u0];
+    uint64_t nb = 0;
+    for (uint32_t i = 0, sh = 0; i < 5u; i++, sh += 7) { const uint32_t b = u0p[i]; nb |= (uint64_t)(b & 127u) << sh; if (b < 128u) break; }
+    small_blocks = nb * 256ull > (uint64_t)n0;
+  }
   if (l == 0) {
     s_pb[wv] = w < n_fb ? (uint64_t)n0 + 16u : 0u; s_tb[wv] = nt;
-    s_lg[wv] = w >= n_fb ? 0u : (n0 > BIG_MID_U0 && n0 < 0x7FFFFFFFu) ? 1u : 2u;   // 1: the 16-wave list, 2: the mid list
+    s_lg[wv] = w >= n_fb ? 0u : ((n0 > BIG_MID_U0 || small_blocks) && n0 < 0x7FFFFFFFu) ? 1u : 2u;   // 1: the 16-wave list, 2: the mid list
   }
   __syncthreads();
   if (threadIdx.x == 0) {   // exclusive prefixes over the workgroup's documents, then one carve each
@@ -3013,7 +3027,7 @@ int ygm_k_launch_big_scan(const uint8_t* arena, const uint64_t* upd_off, const u
   BigScan S; size_t total;
   big_scan_layout(n_fb, fb_bytes, S, (uint8_t*)scan, total);
   if (hipMemsetAsync(S.cnt, 0, 64, s) != hipSuccess) return launch_rc(__func__);
-  hipLaunchKernelGGL(k_big_pick, dim3((n_fb + 15) / 16), dim3(1024), 0, s, upd_off, doc_upd, fb_list, n_fb, S);
+  hipLaunchKernelGGL(k_big_pick, dim3((n_fb + 15) / 16), dim3(1024), 0, s, arena, upd_off, doc_upd, fb_list, n_fb, S);
   // the scan: a persistent grid over the tasks (at most 16 workgroups per CU; the task count is on the device)
   const uint64_t g = S.ntask_cap < 16ull * device_cus() ? S.ntask_cap : 16ull * device_cus();
   hipLaunchKernelGGL(k_big_scan, dim3((uint32_t)g), dim3(256), 0, s, arena, upd_off, doc_upd, fb_list, flags, S);

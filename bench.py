@@ -51,9 +51,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
-PMC_PROFILE = "r04_final/pmc.json"          # committed rocprofv3 PMC summary (FETCH_SIZE x2 + WRITE_SIZE per launch)
-PMC_C4 = "r04_final/pmc.json"              # ... of the SV / diff walker at C4
-PMC_BLOCKS = "r04_final/pmc_blocks.json"   # ... of whole --big blocks (every cascade kernel summed per step: tools/pmc_blocks.py)
+PMC_PROFILE = "r05_final/pmc.json"          # committed rocprofv3 PMC summary (FETCH_SIZE x2 + WRITE_SIZE per launch)
+PMC_C4 = "r05_final/pmc.json"              # ... of the SV / diff walker at C4
+PMC_BLOCKS = "r05_final/pmc_blocks.json"   # ... of whole blocks (--big, --block: every kernel of a step summed, tools/pmc_blocks.py)
 
 
 def parse():
@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--big", choices=["c3", "c5", "c3full"], default=None,
                     help="instead of the standard line: one C3 / C5 large-document batch on the GPU next to the CPU oracle")
     ap.add_argument("--big-docs", type=int, default=None)
+    ap.add_argument("--block", choices=["f1", "mixed", "v2"], default=None,
+                    help="run one side block alone and print its JSON (counter passes: tools/pmc_blocks.py)")
     ap.add_argument("--dry-run", action="store_true", help="no GPU: gloo + the CPU oracle stand in (tests of the rank path)")
     return ap.parse_args()
 
@@ -374,7 +376,7 @@ def f1_block(be, args, steps=5):
            "value": round(algo / kms / 1e3, 3), "unit": "MB/s", "docs_per_s": round(args.f1_docs / kms * 1e3, 1),
            "ms_per_step": round(kms, 4), "wall_ms_per_step": round(wall * 1e3, 4),
            "roofline": roof(algo, kms, "k_snap_text (flat text: one document per wave, workspace in LDS) + k_snap_count / scan / k_snap "
-                                        "(one thread per document) for what it leaves", None),
+                                        "(one thread per document) for what it leaves", _pmc(PMC_BLOCKS, "f1")),
            "parity": "yjs vectors in tests/test_snapshot.py (440 fixed + live sessions + GPU-merged C2 logs) -- bit-exact"}
     if not args.no_cpu_baseline and not args.no_yjs:
         c = {"arena": states, "doc_off": doc_off}
@@ -421,7 +423,7 @@ def mixed_block(be, args, steps=5):
             "docs_general_tiers": int((s1.docs_fast - s0.docs_fast) / steps),
             "docs_big": int((s1.docs_big - s0.docs_big) / steps), "docs_seq": int((s1.docs_seq - s0.docs_seq) / steps),
             "roofline": roof(algo, kms, "k_merge_lean<1> (wide route: the batch's average document outgrows the narrow kernel's "
-                                        "staging) + the general tiers for its deferrals", None),
+                                        "staging) + the general tiers for its deferrals", _pmc(PMC_BLOCKS, "c2_mixed")),
             "parity": f"bit-exact vs oracle on {checked} sampled docs"}
 
 
@@ -463,7 +465,7 @@ def v2_block(be, args, steps=5):
         checked += 1
     conv = {}
     a1d, o1d = be.put(a1, 64), be.put(o1.view(np.int64))
-    for op, (da_, do_, nb) in (("v1_to_v2", (a1d, o1d, len(a1))), ("v2_to_v1", (da, do, len(a2)))):
+    for op, (da_, do_, nb) in (() if args.block else (("v1_to_v2", (a1d, o1d, len(a1))), ("v2_to_v1", (da, do, len(a2))))):
         e.doc_v2_device(op, da_, nb, do_, n_upd, stream=be.stream.cuda_stream)
         be.sync()
         c0 = e.stats()
@@ -477,7 +479,7 @@ def v2_block(be, args, steps=5):
            "value": round(algo / kms / 1e3, 3), "unit": "MB/s", "docs_per_s": round(n / kms * 1e3, 1), "ms_per_step": round(kms, 4),
            "wall_ms_per_step": round(wall * 1e3, 4),
            "roofline": roof(algo, kms, "k_v21f (lane per update, column decoders in registers) + V1 merge cascade + k_v12_fast "
-                                        "(a V2 column per lane)", None),
+                                        "(a V2 column per lane)", _pmc(PMC_BLOCKS, "v2")),
            "convert": conv, "parity": f"bit-exact vs oracle (yjs_oracle_v2.c) on {checked} sampled docs; tests/test_v2.py: 4887 yjs vectors"}
     if not args.no_cpu_baseline and not args.no_yjs:
         blk["cpu_baseline"] = cpu_yjs("merge_v2", {"arena": a2, "upd_off": o2, "doc_upd": d1}, cpu_cores(args), min(n, 4000))
@@ -907,10 +909,20 @@ def big_line(args):
     print(json.dumps(big_run(args, args.big)), flush=True)
 
 
+def block_line(args):
+    """One side block alone (rank 0, N = 1): the command the block's PMC passes profile."""
+    be = GpuBackend(0)
+    fn = {"f1": f1_block, "mixed": mixed_block, "v2": v2_block}[args.block]
+    print(json.dumps(fn(be, args)), flush=True)
+    be.close()
+
+
 def main():
     args = parse()
     if args.big:
         return big_line(args)
+    if args.block:
+        return block_line(args)
     in_torchrun = "WORLD_SIZE" in os.environ
     if args.gpus > 1 and not in_torchrun:
         sys.exit(spawn_ranks(args))

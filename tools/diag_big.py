@@ -13,8 +13,10 @@ import hocuspocus_amd.engine as eng  # noqa: E402
 eng.LIB_PATH = os.path.join(ROOT, "hocuspocus_amd", "libygm_diag.so")
 from tools import synth  # noqa: E402
 
-xml = len(sys.argv) > 1 and sys.argv[1] == "c5"
-if xml:
+xml = len(sys.argv) > 1 and sys.argv[1] in ("c5", "c5full")
+if len(sys.argv) > 1 and sys.argv[1] == "c5full":   # the bench's C5 block (1 000 documents: four mid workgroups per CU)
+    arena, upd_off, doc_upd = synth.big_docs(1000, 1_000_000, 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=9)
+elif xml:
     arena, upd_off, doc_upd = synth.big_docs(20, 600000, 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=9)
 else:
     arena, upd_off, doc_upd = synth.big_docs(200, 300000, 1024, max_clients=64, max_k=200, seed=8)
@@ -40,6 +42,9 @@ print("docs_big", st.docs_big, "docs_seq", st.docs_seq)
 # steps, block tails
 print("follow cycles (2 runs): tile", int(cnt[25]), "headers", int(cnt[26]), "structs", int(cnt[27]), "tails", int(cnt[28]),
       "per block:", {k: round(int(cnt[i]) / max(int(cnt[16]), 1), 1) for k, i in (("tile", 25), ("hdr", 26), ("st", 27), ("tail", 28))})
+# the speculative parse by part (slots 29-31, lane 0 of wave 0, 100 MHz ticks): nx fill + first jump level, the
+# other levels, the block table
+print("spec ticks (2 runs): nx+jp0", int(cnt[29]), "jp1..", int(cnt[30]), "block table", int(cnt[31]))
 t = ts.reshape(16384, 8)[:n].astype(np.int64)
 # stamps: start, log walk, U0 walk, sorts, pass0, pass1; slots 6 / 7: time inside the U0 walk spent in
 # the speculative tile parse / in validation

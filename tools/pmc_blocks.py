@@ -3,7 +3,10 @@
 sizes ...) and divided by the command's merge calls (warm-up + timed runs).  FETCH_SIZE x2 (gfx950 wide-read
 undercount, MI355X_MICROARCH.md HBM section), both counters KiB.  Merges the result into OUT under LABEL.
 
-    python tools/pmc_blocks.py <fetch dir> <write dir> <out.json> LABEL CALLS"""
+    python tools/pmc_blocks.py <fetch dir> <write dir> <out.json> LABEL CALLS [PREFIX,...]
+
+PREFIX: count only the kernels whose names start with one of these (a block whose setup runs other kernels: f1's
+snapshot kernels after the merge that makes its input)."""
 import csv
 import glob
 import json
@@ -11,23 +14,26 @@ import os
 import sys
 
 
-def total(d, counter):
+def total(d, counter, prefixes=None):
     s, kern = 0.0, {}
     for p in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(p)):
             if r.get("Counter_Name") != counter or "ygm" not in r["Kernel_Name"] and not r["Kernel_Name"].startswith("k_"):
                 continue
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("ygm::", "")
+            if prefixes and not any(k.startswith(p) for p in prefixes):
+                continue
             v = float(r["Counter_Value"])
             s += v
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("ygm::", "")
             kern[k] = kern.get(k, 0.0) + v
     return s, kern
 
 
 def main():
     fd, wd, outp, label, calls = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5])
-    f, fk = total(fd, "FETCH_SIZE")
-    w, wk = total(wd, "WRITE_SIZE")
+    pre = sys.argv[6].split(",") if len(sys.argv) > 6 else None
+    f, fk = total(fd, "FETCH_SIZE", pre)
+    w, wk = total(wd, "WRITE_SIZE", pre)
     res = json.load(open(outp)) if os.path.exists(outp) else {
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes of the same bench.py --big command), every "
                   "ygm kernel dispatch summed and divided by the command's merge calls",

@@ -1728,46 +1728,103 @@ YDEV bool big_hdr_fast(const TL& T, uint32_t hp, uint32_t tn, uint64_t& nst, uin
 #endif
 template <class CF>
 YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint32_t mis, uint32_t n0, uint32_t t0, uint16_t* bh,
-                   bool use_bh) {
+                   uint8_t* mk, uint16_t* lst, bool use_bh) {
+  // every thread takes the tile positions t0 + j THREADS (t0 < THREADS), their steps interleaved: the loads of one
+  // step (global scan words, LDS table entries) are issued together, not as a chain per position
+  constexpr uint32_t PER = CF::CH / CF::THREADS;
+  static_assert(CF::CH % CF::THREADS == 0, "tile positions split evenly over the workgroup");
+  const uint8_t* const tb = (const uint8_t*)T.b;
   // the scan's struct ends of the tile's positions, tile-relative (an end 32 KB or more away: no entry, the chain
-  // follow parses that struct from global memory)
-  for (uint32_t i = t0; i < CF::CH; i += CF::THREADS) {
-    uint32_t e = 0;
-    if (at + i < n0 && big_cand(((const uint8_t*)T.b)[mis + i])) {
-      const uint32_t v = nxg[at + i], d = v & 0x7FFFu;
-      const uint32_t rel = i + d;
-      if (d && rel < 0x8000u) e = rel | (v & 0x8000u);
+  // follow parses that struct from global memory).  Non-candidate positions hold no word (their load is unused).
+  uint32_t rl[PER];   // the ends (block table: marks)
+  uint32_t nl = 0;    // the wave's marked positions
+  {
+    uint32_t v[PER];
+    bool c[PER];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t i = t0 + j * CF::THREADS;
+      const bool in = at + i < n0;
+      c[j] = in && big_cand(tb[mis + i]);
+      v[j] = in ? nxg[at + i] : 0u;
     }
-    T.nx[i] = (uint16_t)e;
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t i = t0 + j * CF::THREADS, d = v[j] & 0x7FFFu, rel = i + d;
+      const bool e = c[j] && d && rel < 0x8000u;
+      T.nx[i] = (uint16_t)(e ? rel | (v[j] & 0x8000u) : 0u);
+      rl[j] = e ? rel : 0x8000u;
+      if (use_bh) { mk[i] = i == 0u; bh[i] = BJ_NONE; }   // (the tile's origin: the chain's entry, a block header in a run)
+    }
   }
+#ifdef YGM_DIAG
+  unsigned long long dgs0 = DIAG_NOW();
+  auto dgs = [&](int i) { if (threadIdx.x == 0) { const unsigned long long n_ = DIAG_NOW(); atomicAdd(&ygm_diag[29 + i], n_ - dgs0); dgs0 = n_; } };
+#else
+  auto dgs = [](int) {};
+#endif
+  // a table lookup (level k, -1: nx) without a branch: the read clamped into the tile, BJ_NONE for s >= CH (the
+  // levels unrolled, so the level's table is a constant offset)
+  auto bj = [&](int k, uint32_t s) -> uint32_t {
+    const uint32_t sc = s < CF::CH ? s : 0u;
+    uint32_t v;
+    if (k < 0) { const uint32_t e = T.nx[sc]; v = e ? (e & 0x7FFFu) : BJ_NONE; }
+    else v = T.jp[k][sc];
+    return s < CF::CH ? v : BJ_NONE;
+  };
   // jump tables by doubling (every thread of the workgroup calls this, so the barriers match)
+#pragma unroll
   for (int k = 0; k < BJ_LV; k++) {
     __syncthreads();
-    for (uint32_t i = t0; i < CF::CH; i += CF::THREADS) {
-      const uint32_t a = big_jump(T, k - 1, i);
-      T.jp[k][i] = (uint16_t)(a < CF::CH ? big_jump(T, k - 1, a) : BJ_NONE);
+    uint32_t a[PER];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) a[j] = bj(k - 1, t0 + j * CF::THREADS);
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) T.jp[k][t0 + j * CF::THREADS] = (uint16_t)bj(k - 1, a[j]);
+    if (k == 0 && use_bh) {   // marks: the positions a struct of the tile ends at -- a block header starts at one of them
+                              // (right after its previous block's last struct) or at the tile's origin
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++)
+        if (rl[j] < CF::CH) mk[rl[j]] = 1;
     }
+    if (k == 1 && use_bh) {   // (the marks landed at this level's barrier) the wave's marked positions, compacted into its
+                              // own segment of lst: the table is computed for them only, a lane each, not for every
+                              // position with most lanes idle
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t i = t0 + j * CF::THREADS;
+        const bool m = mk[i] != 0 && at + i < n0;
+        const uint64_t b = __ballot(m);
+        if (m) lst[(t0 / WAVE) * (WAVE * PER) + nl + lanes_below(b)] = (uint16_t)i;
+        nl += (uint32_t)__popcll(b);
+      }
+    }
+    if (k == 0) dgs(0);
   }
-  if (!YGM_BIG_BH || !use_bh) return;   // (documents of large blocks: the table would not be used, C3)
+  if (!YGM_BIG_BH || !use_bh) { dgs(1); return; }   // (documents of large blocks: the table would not be used, C3)
   // the block table: bh[i] = the tile position right after the whole client block whose header would start at tile
   // position i (the header decoded from the tile, then its nst structs jumped through the tables along the bits of
   // nst), or BJ_NONE (no header parse, nst 0 or >= 64, a struct without a table entry or starting past the tile's CH
   // positions).  The chain follow then steps from block to block with one lookup each.
   __syncthreads();
+  dgs(1);
   const uint32_t tn = n0 - (at - mis) < CF::TILE ? n0 - (at - mis) : CF::TILE;
-  for (uint32_t i = t0; i < CF::CH; i += CF::THREADS) {
-    uint32_t S = BJ_NONE;
-    uint64_t nst, cl, ck;
-    uint32_t he;
+  for (uint32_t e = t0 % WAVE; e < nl; e += WAVE) {
+    const uint32_t i = lst[(t0 / WAVE) * (WAVE * PER) + e];
+    uint64_t nst = 0, cl, ck;
+    uint32_t he = 0;
     bool nm;
-    if (at + i < n0 && big_hdr_fast(T, mis + i, tn, nst, cl, ck, he, nm) && nst != 0u && nst < 64u) {
-      S = he - mis;
+    if (big_hdr_fast(T, mis + i, tn, nst, cl, ck, he, nm) && nst != 0u && nst < 64u) {
+      uint32_t S = he - mis;
 #pragma unroll
-      for (int k = 0; k < 6; k++)
-        if ((nst >> k) & 1u) S = S < CF::CH ? big_jump(T, k - 1, S) : BJ_NONE;
+      for (int k = 0; k < 6; k++) {
+        const uint32_t x = bj(k - 1, S);
+        S = ((nst >> k) & 1u) ? x : S;
+      }
+      bh[i] = (uint16_t)S;
     }
-    bh[i] = (uint16_t)S;
   }
+  dgs(2);
 }
 // after a tile's spec (cmd 1): the helper waves touch the next tile's bytes and both tiles' scan words, a load per
 // 128-byte line, so that wave 0's loads of them after its chain follow (the next spec, this tile's verdicts) hit L2
@@ -2315,6 +2372,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   __shared__ BigBlk s_blk[SBQ];
   __shared__ uint32_t s_cpre[WAVE];
   __shared__ uint16_t s_bh[YGM_BIG_BH ? CF::CH : 1];   // the tile's block table (big_spec)
+  __shared__ uint8_t s_mk[YGM_BIG_BH ? CF::CH : 1];    // ... computed at these positions only
   __shared__ uint16_t s_hl[WAVE + 2];                  // a run of blocks found from it: their tile positions
 #ifndef YGM_BIG_ROT
 #define YGM_BIG_ROT 0
@@ -2329,7 +2387,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
       __syncthreads();
       const BigCmd C = s_cmd;
       if (C.cmd == 0) return;
-      if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.mis, C.n0, tid, s_bh, C.tb != 0u);
+      if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.mis, C.n0, tid, s_bh, s_mk, (uint16_t*)s_rst, C.tb != 0u);
       else if (C.cmd == 3) { if (big_clock_ranges<CF::THREADS>(blk, rec, C, tid)) L.bad = 1; }
       else if (C.cmd == 4) { if (!big_ds_canon<CF::THREADS>(C, tid)) s_cmd.tb = 1; }
       else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, tid)) L.bad = 1;
@@ -2438,7 +2496,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
     const uint64_t dg0 = DIAG_NOW();
     if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.n0 = n0; s_cmd.aux = nxg; s_cmd.u0p = u0p; s_cmd.tb = use_bh ? 1u : 0u; }
     __syncthreads();
-    big_spec<CF>(T0, nxg, at, mis, n0, l, s_bh, use_bh);
+    big_spec<CF>(T0, nxg, at, mis, n0, l, s_bh, s_mk, (uint16_t*)s_rst, use_bh);
     __syncthreads();
     dg_spec += DIAG_NOW() - dg0;
   };

@@ -51,7 +51,8 @@ int ygm_k_launch_build_off(const uint64_t* doc_off, const uint16_t* upd_len, con
                            uint64_t* upd_off, hipStream_t s);
 int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, const uint32_t* list,
                                  uint32_t n_list, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
-                                 void* meta, void* meta_next, uint32_t* defer_list, uint64_t out_cap, hipStream_t s);
+                                 void* meta, void* meta_next, uint32_t* defer_list, uint64_t out_cap, const uint16_t* upd_len,
+                                 hipStream_t s);
 int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
                             const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
                             int32_t* status, void* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
@@ -337,7 +338,7 @@ static int merge_async(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes,
   if (wide_route) {
     if (ygm_k_launch_merge_lean_wide(d_arena, d_upd_off, d_doc_upd, n_docs, nullptr, n_docs, c->flags, c->out.as<uint8_t>(),
                                      c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta, meta_next,
-                                     c->defer_w_list.as<uint32_t>(), out_cap, s))
+                                     c->defer_w_list.as<uint32_t>(), out_cap, d_upd_len, s))
       return YGM_EDEVICE;
   } else if (ygm_k_launch_merge_lean(d_arena, d_upd_off, d_doc_upd, n_docs, c->flags, c->out.as<uint8_t>(), c->out_off.as<uint64_t>(),
                                      c->out_len.as<uint64_t>(), c->status.as<int32_t>(), meta, meta_next, c->defer_list.as<uint32_t>(), out_cap, s,
@@ -388,7 +389,7 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
       return YGM_EDEVICE;
     if (ygm_k_launch_merge_lean_wide(P.arena, P.upd_off, P.doc_upd, P.n_docs, c->defer_list.as<uint32_t>(), m.lean_defer, c->flags,
                                      c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
-                                     P.meta, nullptr, c->defer_w_list.as<uint32_t>(), P.out_cap, s))
+                                     P.meta, nullptr, c->defer_w_list.as<uint32_t>(), P.out_cap, P.upd_len, s))
       return YGM_EDEVICE;
     HIPCHK(hipEventRecord(c->e1, s));
     if ((e = read_meta(c, s, m, P.meta))) return e;
@@ -453,7 +454,10 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
       if (!c->stream2) {   // created on first use, only on contexts that run the 16-wave size
         int prio_lo = 0, prio_hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-        HIPCHK(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi));
+#ifndef YGM_S2_PRIO
+#define YGM_S2_PRIO 1
+#endif
+        HIPCHK(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, YGM_S2_PRIO ? prio_hi : prio_lo));
       }
       HIPCHK(hipEventRecord(c->e2, s));
       HIPCHK(hipStreamWaitEvent(c->stream2, c->e2, 0));

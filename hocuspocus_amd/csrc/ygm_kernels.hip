@@ -1037,7 +1037,10 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
       size = k == 0 ? 2u : (uint32_t)nbytes;
       if (k == 1 && nbytes > 0xFFFFFFFFull) size = 0;
       uint8_t* o = out + slot;
-      if (slot + (k == 0 ? 2 : nbytes) > out_cap) { size = 0; if (l == 0) { out_off[d] = slot; out_len[d] = 0; status[d] = ST_NOMEM; } }
+      // compact input form: a single update whose length is not the document's bytes (include/ygm.h: an error)
+      const bool badlen = upd_len != nullptr && k == 1 && (uint64_t)upd_len[h.u0] != nbytes;
+      if (badlen) { size = 0; if (l == 0) { out_off[d] = slot; out_len[d] = 0; status[d] = ST_MALFORMED; } }
+      else if (slot + (k == 0 ? 2 : nbytes) > out_cap) { size = 0; if (l == 0) { out_off[d] = slot; out_len[d] = 0; status[d] = ST_NOMEM; } }
       else {
         if (k == 0) { if (l == 0) { o[0] = 0; o[1] = 0; } }
         else for (uint64_t c = l; c * 16 < nbytes; c += WAVE) {   // unaligned 16-byte loads (arena tail padding >= 16), aligned stores
@@ -1287,52 +1290,79 @@ YDEV void big_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {   // the wave
 // instead of each copy waiting for its own.  Sources may be read up to 15 bytes past their end (the arena's and
 // U0's tail padding); destinations are written exactly.
 struct BigCp { uint64_t src; uint32_t dst, n; };
-YDEV void big_copy_list(uint8_t* o, const BigCp* cl, uint32_t nc, uint32_t* pre) {   // pre: 64 words of LDS
+// the chunks [c, tot) of entries cl[0, m) (pre: their inclusive chunk prefix) taken by one wave, stepping over the
+// chunks of `stride` waves: four 16-byte chunks in flight per lane
+YDEV void big_copy_chunks(uint8_t* o, const BigCp* cl, uint32_t m, const uint32_t* pre, uint32_t tot, uint32_t c, uint32_t stride) {
   const uint32_t l = threadIdx.x % WAVE;
-  for (uint32_t g = 0; g < nc; g += WAVE) {
-    const uint32_t m = nc - g < (uint32_t)WAVE ? nc - g : (uint32_t)WAVE;
-    const uint32_t ch = l < m ? (cl[g + l].n + 15u) / 16u : 0u;
-    const uint32_t inc = dpp_incl_add(ch);
-    pre[l] = inc;                                       // inclusive chunk prefix of entries g .. g + 63
-    const uint32_t tot = lane63(inc);
-    wave_sync();
-    for (uint32_t c0 = 0; c0 < tot; c0 += 4u * WAVE) {
-      uint4 v[4]; uint8_t* d[4]; uint32_t k[4];
+  for (uint32_t c0 = c; c0 < tot; c0 += stride) {
+    uint4 v[4]; uint8_t* d[4]; uint32_t k[4];
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const uint32_t c = c0 + (uint32_t)u * WAVE + l;
-        k[u] = 0; d[u] = nullptr;
-        if (c < tot) {
-          uint32_t lo = 0, hi = m - 1;                  // first entry whose inclusive prefix exceeds c
-          while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (pre[md] > c) hi = md; else lo = md + 1u; }
-          const BigCp E = cl[g + lo];
-          const uint32_t off = 16u * (c - (lo ? pre[lo - 1] : 0u));
-          k[u] = E.n - off < 16u ? E.n - off : 16u;
-          d[u] = o + E.dst + off;
-          __builtin_memcpy(&v[u], (const uint8_t*)(uintptr_t)E.src + off, 16);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        if (k[u] == 16u) __builtin_memcpy(d[u], &v[u], 16);
-        else if (k[u]) {
-          const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-          for (uint32_t q = 0; q < k[u]; q++) d[u][q] = (uint8_t)(w[q >> 2] >> (8u * (q & 3u)));
-        }
+    for (int u = 0; u < 4; u++) {
+      const uint32_t c = c0 + (uint32_t)u * WAVE + l;
+      k[u] = 0; d[u] = nullptr;
+      if (c < tot) {
+        uint32_t lo = 0, hi = m - 1;                  // first entry whose inclusive prefix exceeds c
+        while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (pre[md] > c) hi = md; else lo = md + 1u; }
+        const BigCp E = cl[lo];
+        const uint32_t off = 16u * (c - (lo ? pre[lo - 1] : 0u));
+        k[u] = E.n - off < 16u ? E.n - off : 16u;
+        d[u] = o + E.dst + off;
+        __builtin_memcpy(&v[u], (const uint8_t*)(uintptr_t)E.src + off, 16);
       }
     }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (k[u] == 16u) __builtin_memcpy(d[u], &v[u], 16);
+      else if (k[u]) {
+        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        for (uint32_t q = 0; q < k[u]; q++) d[u][q] = (uint8_t)(w[q >> 2] >> (8u * (q & 3u)));
+      }
+    }
+  }
+}
+YDEV uint32_t big_copy_pre(const BigCp* cl, uint32_t m, uint32_t* pre) {   // the wave: chunk prefix of cl[0, m <= 64)
+  const uint32_t l = threadIdx.x % WAVE;
+  const uint32_t ch = l < m ? (cl[l].n + 15u) / 16u : 0u;
+  const uint32_t inc = dpp_incl_add(ch);
+  pre[l] = inc;
+  return lane63(inc);
+}
+YDEV void big_copy_list(uint8_t* o, const BigCp* cl, uint32_t nc, uint32_t* pre) {   // pre: 64 words of LDS
+  for (uint32_t g = 0; g < nc; g += WAVE) {
+    const uint32_t m = nc - g < (uint32_t)WAVE ? nc - g : (uint32_t)WAVE;
+    const uint32_t tot = big_copy_pre(cl + g, m, pre);
+    wave_sync();
+    big_copy_chunks(o, cl + g, m, pre, tot, 0u, 4u * WAVE);
     wave_sync();
   }
 }
+// k_merge_big's command to its helper waves (cmd 0 done, 1 tile's jump tables, 2 validate, 3 clock ranges, 4 delete-set
+// canonical check, 5 a run of the emit's copy list)
+struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; const uint32_t* aux; };
 // output sink: pass 0 counts, pass 1 stores (lane 0 writes literals; copies go to an LDS list run by the wave when
 // it fills and at the end of the pass -- consecutive ones merged)
 struct BigOut {
   uint8_t* o; uint64_t n; bool w;
   BigCp* cl; uint32_t nc, cap, *pre;
   uint64_t ls, ld, le;                                  // the last entry: source, destination, destination end
+  BigCmd* cmd = nullptr; uint32_t nw = 1;               // k_merge_big: the workgroup's waves run the list (cmd 5)
   YDEV void b(uint32_t v) { if (w && threadIdx.x % WAVE == 0) o[n] = (uint8_t)v; n++; }   // (lane 0 of the writing wave)
   YDEV void vu(uint64_t v) { while (v > 127) { b(0x80u | (uint32_t)(v & 127)); v >>= 7; } b((uint32_t)v); }
-  YDEV void flush() { if (nc) { wave_sync(); big_copy_list(o, cl, nc, pre); nc = 0; } }
+  YDEV void flush() {
+    if (!nc) return;
+    wave_sync();
+    if (!cmd) big_copy_list(o, cl, nc, pre);
+    else   // 64 entries per command: wave 0 publishes their chunk prefix, every wave takes every nw-th run of chunks
+      for (uint32_t g = 0; g < nc; g += WAVE) {
+        const uint32_t m = nc - g < (uint32_t)WAVE ? nc - g : (uint32_t)WAVE;
+        const uint32_t tot = big_copy_pre(cl + g, m, pre);
+        if (threadIdx.x % WAVE == 0) { cmd->cmd = 5; cmd->vs = (uint64_t)(uintptr_t)(cl + g); cmd->ns = m; cmd->u0p = o; cmd->tb = tot; }
+        __syncthreads();
+        big_copy_chunks(o, cl + g, m, pre, tot, 0u, nw * 4u * WAVE);
+        __syncthreads();
+      }
+    nc = 0;
+  }
   YDEV void add(uint64_t src, uint64_t dst, uint64_t len) {
     for (uint64_t a = 0; a < len; a += (1ull << 29)) add1(src + a, dst + a, len - a < (1ull << 29) ? len - a : (1ull << 29));
   }
@@ -1451,7 +1481,6 @@ struct BigCfg {
 using BigCfgL = BigCfg<16, 4096, LB_MAXS, LB_MAXD, 256>;
 using BigCfgM = BigCfg<4, 1024, 256, 256, 64>;
 // cmd 0 done, 1 tile's jump tables, 2 validate, 3 clock ranges, 4 delete-set canonical check
-struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; const uint32_t* aux; };
 
 // ---- the snapshot scan (before k_merge_big, the whole GPU): every byte position p of every large document's U0 parsed
 // as a struct start, speculatively -- nx[p] = its end | GC << 31 (0: no parse: not an info byte write_struct emits, a
@@ -1838,18 +1867,28 @@ YDEV void big_prefetch(const BigCmd& C, uint32_t t0) {
   asm volatile("" ::"v"(acc));   // (the loads are the point)
 }
 // struct records [vs, ns) (byte ranges in rs / re, LDS): the scan's verdict (its word, C.aux) where it has one, else
-// validated from global memory, then stored with their clock lengths; true if any is not what write_struct emits
+// validated -- from the staged tile (tb: its LDS bytes, U0 bytes [C.at - C.mis, + C.tn)) when the struct lies in it,
+// else from global memory -- then stored with their clock lengths; true if any is not what write_struct emits.  (A
+// parse that ends at the record's end reads no byte past it: the tile's and the global parse agree.)
 template <uint32_t NT>
-YDEV bool big_validate(const uint32_t* rs, const uint32_t* re, BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0) {
+YDEV bool big_validate(const uint32_t* rs, const uint32_t* re, BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0,
+                       const uint4* tb) {
   bool vbad = false;
+  const uint32_t t_lo = C.at - C.mis;   // (every record starts inside the tile)
   for (uint64_t i = C.vs + t0; i < C.ns; i += NT) {
     BigRec R; R.start = rs[i - C.vs]; R.end = re[i - C.vs];
-    const uint32_t v16 = big_cand(C.u0p[R.start]) ? C.aux[R.start] >> 16 : 0u;   // (the scan wrote candidate positions only)
+    const uint32_t v16 = big_cand(((const uint8_t*)tb)[R.start - t_lo]) ? C.aux[R.start] >> 16 : 0u;   // (the scan wrote candidate positions only)
     uint64_t len = v16 == 0xFFFFu ? 0xFFFFFFFFull : v16;
     if (len == 0u) {   // (the scan's end for R.start, when it has one, is R.end: the chain took it from nx)
-      GCur w; w.init(C.u0p, C.n0); w.pos = R.start;
-      const GStruct g = big_struct(w, flags);
-      len = g.ok && w.pos == R.end ? g.len : 0u;
+      if (R.end <= t_lo + C.tn) {
+        LCur w; w.init((LU8*)tb, C.tn); w.pos = R.start - t_lo;
+        const GStruct g = big_struct(w, flags);
+        len = g.ok && w.pos == R.end - t_lo ? g.len : 0u;
+      } else {
+        GCur w; w.init(C.u0p, C.n0); w.pos = R.start;
+        const GStruct g = big_struct(w, flags);
+        len = g.ok && w.pos == R.end ? g.len : 0u;
+      }
     }
     vbad |= len == 0u || len >= 0xFFFFFFFFull;
     R.len = (uint32_t)len;
@@ -2390,7 +2429,9 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
       if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.mis, C.n0, tid, s_bh, s_mk, (uint16_t*)s_rst, C.tb != 0u);
       else if (C.cmd == 3) { if (big_clock_ranges<CF::THREADS>(blk, rec, C, tid)) L.bad = 1; }
       else if (C.cmd == 4) { if (!big_ds_canon<CF::THREADS>(C, tid)) s_cmd.tb = 1; }
-      else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, tid)) L.bad = 1;
+      else if (C.cmd == 5) big_copy_chunks(const_cast<uint8_t*>(C.u0p), (const BigCp*)(uintptr_t)C.vs, (uint32_t)C.ns, s_cpre, C.tb,
+                                           (tid / WAVE) * 4u * WAVE, CF::WAVES * 4u * WAVE);
+      else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, tid, T0.b)) L.bad = 1;
       __syncthreads();
       if (C.cmd == 1) big_prefetch<CF::CH, CF::THREADS - WAVE>(C, tid - WAVE);   // (while wave 0 follows the chain)
     }
@@ -2505,9 +2546,10 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
     const uint64_t dg0 = DIAG_NOW();
     if (l == 0) {
       s_cmd.cmd = 2; s_cmd.vs = vs; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.u0p = u0p; s_cmd.n0 = n0; s_cmd.aux = nxg;
+      s_cmd.at = tc0; s_cmd.mis = tc0 - tb; s_cmd.tn = tn;
     }
     __syncthreads();                                       // lane 0's byte ranges and the command before every wave reads them
-    if (big_validate<CF::THREADS>(s_rst, s_ren, rec, s_cmd, flags, l)) L.bad = 1;
+    if (big_validate<CF::THREADS>(s_rst, s_ren, rec, s_cmd, flags, l, T0.b)) L.bad = 1;
     __syncthreads();
     vs = NS;
     wave_sync();
@@ -2726,8 +2768,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   }
   DIAG_C(if (l == 0) { atomicAdd(&ygm_diag[21], 1ull); atomicAdd(&ygm_diag[22], DP.fast ? 1ull : 0ull);
                        atomicAdd(&ygm_diag[23], (unsigned long long)dsn); atomicAdd(&ygm_diag[24], (unsigned long long)DP.C); })
-  if (l == 0) s_cmd.cmd = 0;   // the helper waves are done: everything below is wave 0's
-  __syncthreads();
+  // (the helper waves stay in their command loop: the emit's copy lists are run by every wave, cmd 5)
   DIAGL(1);
   const uint32_t npc = L.npc, nrg = L.nrg;
   bool bad = L.bad || npc > (uint32_t)CF::MAXS || nrg > (uint32_t)CF::MAXD;
@@ -2750,6 +2791,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
     // the copy list lives in the U0 tile's LDS past the block-table staging / client groups and the splice words
     o.cl = (BigCp*)(dsx + 3 * CF::MAXD); o.nc = 0; o.pre = s_cpre;
     o.cap = (uint32_t)((sizeof(typename CF::Tile) - CF::SBG - 12 * CF::MAXD) / sizeof(BigCp)); o.ls = o.le = o.ld = 0;
+    o.cmd = &s_cmd; o.nw = CF::WAVES;
     o.vu(nblocks);
     if (pass == 0 && acanon) {
       uint64_t nbo = 0;
@@ -2957,6 +2999,8 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
       bad |= L.bad != 0;
     }
   }
+  if (l == 0) s_cmd.cmd = 0;   // the helper waves leave
+  __syncthreads();
   if (l == 0) {
     if (bad) { status[d] = ST_FALLBACK; fb2_list[atomicAdd(&meta->big_defer, 1u)] = d; }
     else { out_off[d] = s_at; out_len[d] = size; status[d] = ST_OK; add_payload(meta, d, size); }
@@ -3244,6 +3288,11 @@ __global__ __launch_bounds__(256) void k_build_off(const uint64_t* __restrict__ 
     if (i < u1) upd_off[i] = off < b1 ? off : b1;
     carry += lane63(inc);
   }
+  // lengths that do not add up to the document (include/ygm.h: an error status): with two or more updates every
+  // one becomes empty, which no tier parses (yjs: readVarUint past the end throws); a single update is checked
+  // where it is passed through (the lean kernels' single path reads upd_len)
+  if (carry != b1 && u1 - u0 >= 2u)
+    for (uint32_t i = u0 + l; i < u1; i += WAVE) upd_off[i] = b1;
   if (l == 0) upd_off[u1] = b1;
 }
 int ygm_k_launch_build_off(const uint64_t* doc_off, const uint16_t* upd_len, const uint32_t* doc_upd, const uint32_t* list, uint32_t n,
@@ -3256,14 +3305,14 @@ int ygm_k_launch_build_off(const uint64_t* doc_off, const uint16_t* upd_len, con
 // (count: DocMeta::wide_defer)
 int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, const uint32_t* list,
                                  uint32_t n_list, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status,
-                                 void* meta, void* meta_next, uint32_t* defer_list, uint64_t out_cap, hipStream_t s) {
+                                 void* meta, void* meta_next, uint32_t* defer_list, uint64_t out_cap, const uint16_t* upd_len, hipStream_t s) {
   if (n_list == 0) return 0;
   static std::atomic<uint32_t> cache[YGM_MAX_DEVICES];
   const uint32_t resident = per_device(cache, [] { const char* g = getenv("YGM_WIDE_GRID"); return g ? (uint32_t)atoi(g) : resident_blocks(k_merge_lean<1, 0>, WAVE, 2048u); });
   const uint32_t grid = n_list < resident ? n_list : resident;
   hipLaunchKernelGGL((k_merge_lean<1, 0>), dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, n_docs, flags, out, out_off, out_len,
                      status, (DocMeta*)meta, (DocMeta*)meta_next, defer_list, out_cap, list, n_list, (const uint64_t*)nullptr,
-                     (const uint16_t*)nullptr);
+                     upd_len);
   return launch_rc(__func__);
 }
 

@@ -437,33 +437,22 @@ def test_async_device_api_matches_host_api(eng):
     assert r.payload_bytes == sum(len(h[1]) for h in host if h[0] == 0)
 
 
-def test_compact_lens_device_api_matches_host_api(eng):
-    # ygm_merge_v1_device_lens (u64 per document, u16 length per update) == the host API on a batch that needs every
-    # tier (the deferred documents' offsets are built on the device), and a document whose lengths do not add up to
-    # its bytes gets an error status
+def _lens_check(eng, docs, bad_lens):
+    # docs through ygm_merge_v1_device_lens with the lengths bad_lens {update index: length} changed: the documents
+    # holding a changed update get an error status, every other one the host API's result
     import torch
     import bench
-    from tools import synth
-    arena, upd_off, doc_upd = synth.text_updates(400, 120, seed=32, del_pct=10)
-    ups = synth.split(arena, upd_off)
-    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(400)]
-    rng = random.Random(6)
-    for d in range(0, 400, 7):
-        docs[d] = docs[d] + rng.sample(docs[d], 2)          # duplicates: the sequential tier
-    docs += _lean_edge_docs(100, seed=78)
-    ba, bo, bd = synth.big_docs(3, 60000, 1024, max_clients=16, max_k=40, seed=7)   # the large-document tier
-    bu = synth.split(ba, bo)
-    docs += [bu[bd[d]:bd[d + 1]] for d in range(3)]
     blobs = [u for us in docs for u in us]
     assert max(len(b) for b in blobs) < 65536
     a = np.frombuffer(b"".join(blobs) + bytes(64), np.uint8)
     lens = np.array([len(b) for b in blobs], np.uint16)
     du = np.cumsum([0] + [len(us) for us in docs]).astype(np.uint32)
     doff = np.cumsum([0] + [sum(len(u) for u in us) for us in docs]).astype(np.uint64)
-    bad = 5
-    lens_bad = lens.copy(); lens_bad[du[bad]] += 3                        # document 5: lengths past its bytes
+    for u, v in bad_lens.items():
+        lens[u] = v
+    bad = {int(np.searchsorted(du, u, side="right")) - 1 for u in bad_lens}
     dev = torch.device("cuda", 0)
-    ta, to, tl, td = (torch.from_numpy(x.copy()).to(dev) for x in (a, doff.view(np.int64), lens_bad.view(np.int16), du.view(np.int32)))
+    ta, to, tl, td = (torch.from_numpy(x.copy()).to(dev) for x in (a, doff.view(np.int64), lens.view(np.int16), du.view(np.int32)))
     n = len(docs)
     host = eng.merge_updates_batch(docs)
     for _ in range(2):   # the second call reuses the context's buffers
@@ -475,10 +464,43 @@ def test_compact_lens_device_api_matches_host_api(eng):
         data = bench._d2h(r.data, int(r.data_bytes)).tobytes()
         for d in range(n):
             got = (int(sts[d]), data[int(offs[d]):int(offs[d]) + int(ln[d])] if sts[d] == 0 else None)
-            if d == bad:
-                assert got[0] != 0
+            if d in bad:
+                assert got[0] != 0, d
             else:
                 assert got[0] == host[d][0] and (got[0] != 0 or got[1] == host[d][1]), d
+
+
+def test_compact_lens_device_api_matches_host_api(eng):
+    # ygm_merge_v1_device_lens (u64 per document, u16 length per update) == the host API on a batch that needs every
+    # tier (the deferred documents' offsets are built on the device); documents whose lengths do not add up to their
+    # bytes get an error status: lengths past the bytes, short of them (two or more updates), a single update's
+    # length other than the document's bytes
+    from tools import synth
+    arena, upd_off, doc_upd = synth.text_updates(400, 120, seed=32, del_pct=10)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(400)]
+    rng = random.Random(6)
+    for d in range(0, 400, 7):
+        docs[d] = docs[d] + rng.sample(docs[d], 2)          # duplicates: the sequential tier
+    docs += _lean_edge_docs(100, seed=78)
+    ba, bo, bd = synth.big_docs(3, 60000, 1024, max_clients=16, max_k=40, seed=7)   # the large-document tier
+    bu = synth.split(ba, bo)
+    docs += [bu[bd[d]:bd[d + 1]] for d in range(3)]
+    docs += [[ups[3]], [ups[4]]]                                  # single-update documents (passed through)
+    du = np.cumsum([0] + [len(us) for us in docs]).astype(np.uint32)
+    lens = [len(u) for us in docs for u in us]
+    _lens_check(eng, docs, {int(du[5]): lens[du[5]] + 3,           # past the bytes
+                            int(du[12]) + 1: lens[du[12] + 1] - 1,  # short of them
+                            int(du[401]): lens[du[401]] - 1,        # an edge document (wave / workgroup tiers)
+                            int(du[len(docs) - 1]): lens[du[len(docs) - 1]] + 1})   # a single update
+    # the wide route (the batch's average document outgrows the narrow kernel's staging: every document takes the
+    # wide kernel, the table built whole on the device)
+    wa, wo, wd = synth.text_updates(300, 200, 1, 8, del_pct=20, seed=71, max_run=16)
+    wu = synth.split(wa, wo)
+    wdocs = [wu[wd[d]:wd[d + 1]] for d in range(300)] + [[wu[7]], [wu[9]]]
+    wdu = np.cumsum([0] + [len(us) for us in wdocs]).astype(np.uint32)
+    wl = [len(u) for us in wdocs for u in us]
+    _lens_check(eng, wdocs, {int(wdu[3]) + 2: wl[wdu[3] + 2] - 2, int(wdu[301]): wl[wdu[301]] + 2})
 
 
 def test_lean_sv_diff_edge_states_vs_oracle(eng):

@@ -16,6 +16,8 @@ from tools import synth  # noqa: E402
 xml = len(sys.argv) > 1 and sys.argv[1] in ("c5", "c5full")
 if len(sys.argv) > 1 and sys.argv[1] == "c5full":   # the bench's C5 block (1 000 documents: four mid workgroups per CU)
     arena, upd_off, doc_upd = synth.big_docs(1000, 1_000_000, 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=9)
+elif len(sys.argv) > 1 and sys.argv[1] == "c3top":   # the C3 corpus' largest documents (10 MB * rank^-0.8: the 16-wave size)
+    arena, upd_off, doc_upd = synth.big_docs(8, 10_000_000, 1024, max_clients=64, max_k=200, seed=8)
 elif xml:
     arena, upd_off, doc_upd = synth.big_docs(20, 600000, 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=9)
 else:
@@ -55,3 +57,18 @@ sizes = np.diff(upd_off[doc_upd].astype(np.int64))
 for q in np.argsort(-d.sum(1))[:5]:
     print("block", q, "us", dict(zip(names, np.round(d[q], 1))))
 print("mean us", dict(zip(names, np.round(d.mean(0), 1))), "max total us", round(d.sum(1).max(), 1), "bytes max", sizes.max())
+# concurrency: start / end stamps of the workgroups (row = blockIdx; the last kernel to write a row wins)
+ok = t[:, 0] > 0
+if ok.any():
+    st, en = t[ok, 0], t[ok, 5]
+    z = st.min()
+    print("start us percentiles 0/25/50/75/100:", np.round(np.percentile((st - z) * 10 / 1000.0, [0, 25, 50, 75, 100]), 1).tolist(),
+          "end:", np.round(np.percentile((en - z) * 10 / 1000.0, [0, 25, 50, 75, 100]), 1).tolist(),
+          "per-doc total us median:", round(float(np.median(d[ok].sum(1))), 1))
+    rows = np.nonzero(ok)[0]
+    sb = ((st - z) * 10 / 1000.0 // 1000).astype(int)
+    eb = ((en - z) * 10 / 1000.0 // 1000).astype(int)
+    print("start histogram (ms bin: count):", dict(zip(*np.unique(sb, return_counts=True))))
+    print("end histogram (ms bin: count):", dict(zip(*np.unique(eb, return_counts=True))))
+    late = rows[sb >= 5]
+    print("late rows (blockIdx) first/last/count:", late[:8].tolist(), late[-8:].tolist(), len(late))

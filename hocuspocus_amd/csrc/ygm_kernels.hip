@@ -1511,7 +1511,7 @@ YDEV uint32_t big_v16(uint64_t len, bool ok) { return !ok ? 0xFFFFu : len <= 0xF
 #define YGM_MID_OCC 4   // mid-size workgroups per CU the register budget is cut for
 #endif
 #ifndef YGM_BIG_MID_KB
-#define YGM_BIG_MID_KB 2048
+#define YGM_BIG_MID_KB 512
 #endif
 constexpr uint32_t BIG_MID_U0 = YGM_BIG_MID_KB * 1024u;
 // only a byte write_struct could have emitted as an info byte starts a parse: GC (0) or an Item ref 1..8 without bit 0x20

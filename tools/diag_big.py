@@ -16,6 +16,8 @@ from tools import synth  # noqa: E402
 xml = len(sys.argv) > 1 and sys.argv[1] in ("c5", "c5full")
 if len(sys.argv) > 1 and sys.argv[1] == "c5full":   # the bench's C5 block (1 000 documents: four mid workgroups per CU)
     arena, upd_off, doc_upd = synth.big_docs(1000, 1_000_000, 64 * 1024, max_clients=10000, max_k=50, xml=True, seed=9)
+elif len(sys.argv) > 1 and sys.argv[1] == "c3dev":   # the bench's C3 full block, through the device API (one launch per size)
+    arena, upd_off, doc_upd = synth.big_docs(100000, 10_000_000, 1024, max_clients=64, max_k=200, seed=8)
 elif len(sys.argv) > 1 and sys.argv[1] == "c3top":   # the C3 corpus' largest documents (10 MB * rank^-0.8: the 16-wave size)
     arena, upd_off, doc_upd = synth.big_docs(8, 10_000_000, 1024, max_clients=64, max_k=200, seed=8)
 elif xml:
@@ -28,8 +30,18 @@ e = eng.Engine(0)
 L = eng.lib()
 L.ygm_diag_ts_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
 ts = np.zeros(16384 * 8, np.uint64)
-e.merge_packed(arena, upd_off, upd_doc, n)
-e.merge_packed(arena, upd_off, upd_doc, n)
+if len(sys.argv) > 1 and sys.argv[1] in ("c3dev", "c5full"):
+    import torch
+    dev = torch.device("cuda", 0)
+    da = torch.from_numpy(np.concatenate([arena, np.zeros(64, np.uint8)])).to(dev)
+    do = torch.from_numpy(upd_off.view(np.int64)).to(dev)
+    dd = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
+    for _ in range(2):
+        e.merge_device(da.data_ptr(), len(arena), do.data_ptr(), dd.data_ptr(), int(doc_upd[-1]), n)
+    torch.cuda.synchronize()
+else:
+    e.merge_packed(arena, upd_off, upd_doc, n)
+    e.merge_packed(arena, upd_off, upd_doc, n)
 L.ygm_diag_ts_read(ts.ctypes.data, 0)
 L.ygm_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
 cnt = np.zeros(32, np.uint64)
@@ -54,6 +66,10 @@ d = np.diff(t[:, :6], axis=1) * 10 / 1000.0   # us
 d = np.concatenate([d[:, :1], d[:, 1:2] - (t[:, 6:8].sum(1, keepdims=True) * 10 / 1000.0), t[:, 6:8] * 10 / 1000.0, d[:, 2:]], axis=1)
 names = ["log walk", "U0 follow", "U0 spec parse", "U0 validate", "sorts", "pass0", "pass1"]
 sizes = np.diff(upd_off[doc_upd].astype(np.int64))
+tot = d.sum(1)
+live = t[:, 0] > 0
+print("per-document total us percentiles 10/50/90/99 (rows written):", np.round(np.percentile(tot[live], [10, 50, 90, 99]), 1).tolist(),
+      "phase medians:", dict(zip(names, np.round(np.median(d[live], 0), 1))))
 for q in np.argsort(-d.sum(1))[:5]:
     print("block", q, "us", dict(zip(names, np.round(d[q], 1))))
 print("mean us", dict(zip(names, np.round(d.mean(0), 1))), "max total us", round(d.sum(1).max(), 1), "bytes max", sizes.max())

@@ -1279,6 +1279,21 @@ YDEV void big_bitonic(T* a, uint32_t n) {   // ascending by key; n <= 1024 (entr
       wave_sync();
     }
 }
+// a workgroup sort of n <= NT * k entries by key: every entry's rank (the keys before it, ties by index: a stable
+// order) from a broadcast scan of the keys, then a scatter through tmp (LDS) and the copy back
+template <class T, uint32_t NT>
+YDEV void big_rank_sort(T* a, uint32_t n, T* tmp, uint32_t t0) {
+  for (uint32_t i = t0; i < n; i += NT) {
+    const uint64_t ki = a[i].key;
+    uint32_t r = 0;
+#pragma unroll 4
+    for (uint32_t j = 0; j < n; j++) { const uint64_t kj = a[j].key; r += (kj < ki || (kj == ki && j < i)) ? 1u : 0u; }
+    tmp[r] = a[i];
+  }
+  __syncthreads();
+  for (uint32_t i = t0; i < n; i += NT) a[i] = tmp[i];
+  __syncthreads();
+}
 YDEV void big_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {   // the wave copies n bytes, 16 per lane-step
   for (uint64_t c = 16ull * (threadIdx.x % WAVE); c < n; c += 16ull * WAVE) {
     if (c + 16 <= n) { uint4 v; __builtin_memcpy(&v, src + c, 16); __builtin_memcpy(dst + c, &v, 16); }
@@ -1337,7 +1352,7 @@ YDEV void big_copy_list(uint8_t* o, const BigCp* cl, uint32_t nc, uint32_t* pre)
   }
 }
 // k_merge_big's command to its helper waves (cmd 0 done, 1 tile's jump tables, 2 validate, 3 clock ranges, 4 delete-set
-// canonical check, 5 a run of the emit's copy list)
+// canonical check, 5 a run of the emit's copy list, 6 the log's sort)
 struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; const uint32_t* aux; };
 // output sink: pass 0 counts, pass 1 stores (lane 0 writes literals; copies go to an LDS list run by the wave when
 // it fills and at the end of the pass -- consecutive ones merged)
@@ -1475,6 +1490,8 @@ struct BigCfg {
   // emit staging in the tile's LDS: [block-table staging (serial emit) | client groups (parallel emit)][splice words][copy list]
   static constexpr uint32_t GCAP = MAXS_ * 3 / 8;
   static constexpr uint32_t SBG = SBN_ * 48u > GCAP * 64u ? SBN_ * 48u : GCAP * 64u;
+  static_assert(sizeof(Tile) >= (uint32_t)MAXS_ * sizeof(BigPiece) && sizeof(Tile) >= (uint32_t)MAXD_ * sizeof(BigRange),
+                "the log's sort scatters through the tile");
   static_assert(sizeof(Tile) >= SBG + 12 * MAXD_ + 256 * 16 && sizeof(BigBlk) == 48 && sizeof(BigGrp) == 64 && MAXD_ % 4 == 0,
                 "emit staging");
 };
@@ -2429,6 +2446,10 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
       if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.mis, C.n0, tid, s_bh, s_mk, (uint16_t*)s_rst, C.tb != 0u);
       else if (C.cmd == 3) { if (big_clock_ranges<CF::THREADS>(blk, rec, C, tid)) L.bad = 1; }
       else if (C.cmd == 4) { if (!big_ds_canon<CF::THREADS>(C, tid)) s_cmd.tb = 1; }
+      else if (C.cmd == 6) {
+        big_rank_sort<BigPiece, CF::THREADS>(L.pc, (uint32_t)C.vs, (BigPiece*)&T0, tid);
+        big_rank_sort<BigRange, CF::THREADS>(L.rg, (uint32_t)C.ns, (BigRange*)&T0, tid);
+      }
       else if (C.cmd == 5) big_copy_chunks(const_cast<uint8_t*>(C.u0p), (const BigCp*)(uintptr_t)C.vs, (uint32_t)C.ns, s_cpre, C.tb,
                                            (tid / WAVE) * 4u * WAVE, CF::WAVES * 4u * WAVE);
       else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, tid, T0.b)) L.bad = 1;
@@ -2772,7 +2793,13 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   DIAGL(1);
   const uint32_t npc = L.npc, nrg = L.nrg;
   bool bad = L.bad || npc > (uint32_t)CF::MAXS || nrg > (uint32_t)CF::MAXD;
-  if (!bad) { big_bitonic(L.pc, npc); big_bitonic(L.rg, nrg); }
+  if (!bad) {   // cmd 6: the log's pieces and ranges sorted by the whole workgroup (the tile's LDS, free now, as scratch)
+    if (l == 0) { s_cmd.cmd = 6; s_cmd.vs = npc; s_cmd.ns = nrg; }
+    __syncthreads();
+    big_rank_sort<BigPiece, CF::THREADS>(L.pc, npc, (BigPiece*)&T0, l);
+    big_rank_sort<BigRange, CF::THREADS>(L.rg, nrg, (BigRange*)&T0, l);
+    __syncthreads();
+  }
   const BigBlk* T = blk + s_base;
   if (bad) nb = 0;
   // emit staging in the U0 tile's LDS (free now): block-table entries, the splice's per-range words, the copy list

@@ -2472,11 +2472,25 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   }
   wave_sync();
   const uint32_t U0 = 0xFFFFFFFFu - (uint32_t)s_pick;
-  // ---- log updates, lanes in parallel: every struct a piece, every delete range a record
-  for (uint32_t i = l; i < k; i += WAVE) {
-    if (i == U0) continue;
-    const uint64_t a = upd_off[ua + i];
-    GCur c; c.init(arena + a, (uint32_t)(upd_off[ua + i + 1] - a));
+  // ---- log updates, lanes in parallel: every struct a piece, every delete range a record.  The log's bytes are
+  //      staged in the tile's LDS first (free before the U0 walk; one copy list for the wave, its loads in flight
+  //      together) when they fit, and parsed there: from global memory each update is a chain of dependent loads.
+  constexpr uint32_t LG_LIST = 256, LG_CAP = (uint32_t)sizeof(typename CF::Tile) - LG_LIST * (uint32_t)sizeof(BigCp);
+  uint8_t* const lstage = (uint8_t*)&T0;
+  BigCp* const llist = (BigCp*)(lstage + LG_CAP);
+  uint32_t lbytes = 0;
+  bool staged = k >= 2u && k - 1u <= LG_LIST;
+  for (uint32_t i0 = 0; staged && i0 < k; i0 += WAVE) {   // stage offsets: an exclusive scan of the sizes (U0's: 0)
+    const uint32_t i = i0 + l;
+    const uint64_t sz = i < k && i != U0 ? upd_off[ua + i + 1] - upd_off[ua + i] : 0ull;
+    const uint32_t s32 = sz < LG_CAP ? (uint32_t)sz : LG_CAP;
+    const uint32_t inc = dpp_incl_add(s32);
+    if (i < k && i != U0) { BigCp E; E.src = (uint64_t)(uintptr_t)(arena + upd_off[ua + i]); E.dst = lbytes + inc - s32; E.n = s32; llist[i < U0 ? i : i - 1u] = E; }
+    lbytes += lane63(inc);
+    staged = lbytes <= LG_CAP && __ballot(sz >= LG_CAP) == 0;
+  }
+  if (staged) big_copy_list(lstage, llist, k - 1u, s_cpre);   // (wave-synchronous)
+  auto walk = [&](auto& c, uint64_t a) {
     bool bad = false;
     const uint64_t nb = c.vu();
     uint64_t prevc = ~0ull;
@@ -2512,6 +2526,13 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
       }
     }
     if (bad || c.err) L.bad = 1;
+  };
+  for (uint32_t i = l; i < k; i += WAVE) {
+    if (i == U0) continue;
+    const uint64_t a = upd_off[ua + i];
+    const uint32_t n = (uint32_t)(upd_off[ua + i + 1] - a);
+    if (staged) { const BigCp E = llist[i < U0 ? i : i - 1u]; LCur c; c.init((LU8*)(lstage + E.dst), n); walk(c, a); }
+    else { GCur c; c.init(arena + a, n); walk(c, a); }
   }
   DIAGL(0);
   wave_sync();

@@ -1351,8 +1351,8 @@ YDEV void big_copy_list(uint8_t* o, const BigCp* cl, uint32_t nc, uint32_t* pre)
     wave_sync();
   }
 }
-// k_merge_big's command to its helper waves (cmd 0 done, 1 tile's jump tables, 2 validate, 3 clock ranges, 4 delete-set
-// canonical check, 5 a run of the emit's copy list, 6 the log's sort)
+// k_merge_big's command to its helper waves (cmd 0 done, 1 tile's jump tables, 2 validate the walk's struct records, 3
+// clock ranges, 4 delete-set canonical check, 5 a run of the emit's copy list, 6 the log's sort)
 struct BigCmd { uint32_t cmd, at, mis, tn, tb, n0; uint64_t vs, ns, sbase; const uint8_t* u0p; const uint32_t* aux; };
 // output sink: pass 0 counts, pass 1 stores (lane 0 writes literals; copies go to an LDS list run by the wave when
 // it fills and at the end of the pass -- consecutive ones merged)
@@ -1497,7 +1497,6 @@ struct BigCfg {
 };
 using BigCfgL = BigCfg<16, 4096, LB_MAXS, LB_MAXD, 256>;
 using BigCfgM = BigCfg<4, 1024, 256, 256, 64>;
-// cmd 0 done, 1 tile's jump tables, 2 validate, 3 clock ranges, 4 delete-set canonical check
 
 // ---- the snapshot scan (before k_merge_big, the whole GPU): every byte position p of every large document's U0 parsed
 // as a struct start, speculatively -- nx[p] = its end | GC << 31 (0: no parse: not an info byte write_struct emits, a
@@ -1883,33 +1882,24 @@ YDEV void big_prefetch(const BigCmd& C, uint32_t t0) {
   for (uint32_t i = t0; i < nb + nw; i += NT) acc ^= i < nb ? (uint32_t)C.u0p[b0 + i * 128u] : C.aux[a + (i - nb) * 32u];
   asm volatile("" ::"v"(acc));   // (the loads are the point)
 }
-// struct records [vs, ns) (byte ranges in rs / re, LDS): the scan's verdict (its word, C.aux) where it has one, else
-// validated -- from the staged tile (tb: its LDS bytes, U0 bytes [C.at - C.mis, + C.tn)) when the struct lies in it,
-// else from global memory -- then stored with their clock lengths; true if any is not what write_struct emits.  (A
-// parse that ends at the record's end reads no byte past it: the tile's and the global parse agree.)
+// the U0 walk's struct records [vs, ns) (rec, written by the follow without lengths): the scan's verdict (its word,
+// C.aux) where it has one, else validated from global memory; stored with their clock lengths.  True if any is not
+// what write_struct emits.  Run once at the walk's end by the whole workgroup: off the follow's serial chain, with
+// the global parses of every lane in flight together.
 template <uint32_t NT>
-YDEV bool big_validate(const uint32_t* rs, const uint32_t* re, BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0,
-                       const uint4* tb) {
+YDEV bool big_validate(BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0) {
   bool vbad = false;
-  const uint32_t t_lo = C.at - C.mis;   // (every record starts inside the tile)
   for (uint64_t i = C.vs + t0; i < C.ns; i += NT) {
-    BigRec R; R.start = rs[i - C.vs]; R.end = re[i - C.vs];
-    const uint32_t v16 = big_cand(((const uint8_t*)tb)[R.start - t_lo]) ? C.aux[R.start] >> 16 : 0u;   // (the scan wrote candidate positions only)
+    BigRec R = rec[C.sbase + i];
+    const uint32_t v16 = big_cand(C.u0p[R.start]) ? C.aux[R.start] >> 16 : 0u;   // (the scan wrote candidate positions only)
     uint64_t len = v16 == 0xFFFFu ? 0xFFFFFFFFull : v16;
     if (len == 0u) {   // (the scan's end for R.start, when it has one, is R.end: the chain took it from nx)
-      if (R.end <= t_lo + C.tn) {
-        LCur w; w.init((LU8*)tb, C.tn); w.pos = R.start - t_lo;
-        const GStruct g = big_struct(w, flags);
-        len = g.ok && w.pos == R.end - t_lo ? g.len : 0u;
-      } else {
-        GCur w; w.init(C.u0p, C.n0); w.pos = R.start;
-        const GStruct g = big_struct(w, flags);
-        len = g.ok && w.pos == R.end ? g.len : 0u;
-      }
+      GCur w; w.init(C.u0p, C.n0); w.pos = R.start;
+      const GStruct g = big_struct(w, flags);
+      len = g.ok && w.pos == R.end ? g.len : 0u;
     }
     vbad |= len == 0u || len >= 0xFFFFFFFFull;
-    R.len = (uint32_t)len;
-    rec[C.sbase + i] = R;
+    rec[C.sbase + i].len = (uint32_t)len;
   }
   return vbad;
 }
@@ -2452,7 +2442,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
       }
       else if (C.cmd == 5) big_copy_chunks(const_cast<uint8_t*>(C.u0p), (const BigCp*)(uintptr_t)C.vs, (uint32_t)C.ns, s_cpre, C.tb,
                                            (tid / WAVE) * 4u * WAVE, CF::WAVES * 4u * WAVE);
-      else if (big_validate<CF::THREADS>(s_rst, s_ren, rec, C, flags, tid, T0.b)) L.bad = 1;
+      else if (big_validate<CF::THREADS>(rec, C, flags, tid)) L.bad = 1;
       __syncthreads();
       if (C.cmd == 1) big_prefetch<CF::CH, CF::THREADS - WAVE>(C, tid - WAVE);   // (while wave 0 follows the chain)
     }
@@ -2584,17 +2574,21 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
     dg_spec += DIAG_NOW() - dg0;
   };
   uint64_t vs = 0;                                         // first struct record not yet validated
-  auto validate = [&]() {                                  // records [vs, NS): all start inside the tile
-    const uint64_t dg0 = DIAG_NOW();
-    if (l == 0) {
-      s_cmd.cmd = 2; s_cmd.vs = vs; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.u0p = u0p; s_cmd.n0 = n0; s_cmd.aux = nxg;
-      s_cmd.at = tc0; s_cmd.mis = tc0 - tb; s_cmd.tn = tn;
-    }
-    __syncthreads();                                       // lane 0's byte ranges and the command before every wave reads them
-    if (big_validate<CF::THREADS>(s_rst, s_ren, rec, s_cmd, flags, l, T0.b)) L.bad = 1;
-    __syncthreads();
+  // the tile's struct records [vs, NS) (LDS) go to rec without lengths (wave 0, no barrier): they are validated once,
+  // at the walk's end (cmd 2)
+  auto validate = [&]() {
+    wave_sync();
+    for (uint64_t i = vs + l; i < NS; i += WAVE) { BigRec R; R.start = s_rst[i - vs]; R.end = s_ren[i - vs]; R.len = 0; rec[sbase + i] = R; }
     vs = NS;
     wave_sync();
+  };
+  auto validate_all = [&]() {
+    const uint64_t dg0 = DIAG_NOW();
+    if (l == 0) { s_cmd.cmd = 2; s_cmd.vs = 0; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.u0p = u0p; s_cmd.n0 = n0; s_cmd.aux = nxg; }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the records before every wave reads them
+    __syncthreads();
+    if (big_validate<CF::THREADS>(rec, s_cmd, flags, l)) L.bad = 1;
+    __syncthreads();
     dg_val += DIAG_NOW() - dg0;
   };
   if (!L.bad) {
@@ -2710,8 +2704,15 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
         // the tile and have a speculative parse
         const uint32_t want = bnst - q < 64u ? bnst - q : 64u;
         uint32_t S = pos - tc0;
-        for (int k = 0; k < 6 && ((want - 1u) >> k); k++)
-          if (((l >> k) & 1u) && S < CF::CH) S = big_jump(T0, k - 1, S);
+#pragma unroll
+        for (int k = 0; k < 6; k++) {   // (branch-free: the reads clamped into the tile, every level; lanes past want
+                                        //  have no use for theirs, the bits of those below it select)
+          const uint32_t sc = S < CF::CH ? S : 0u;
+          uint32_t x;
+          if (k == 0) { const uint32_t e = T0.nx[sc]; x = e ? (e & 0x7FFFu) : BJ_NONE; }
+          else x = T0.jp[k - 1][sc];
+          S = (((l >> k) & 1u) && S < CF::CH) ? x : S;
+        }
         const uint32_t E = (l < want && S < CF::CH) ? (uint32_t)T0.nx[S] : 0u;
         const uint64_t tk = __ballot(E != 0u);
         const uint32_t m = ~tk ? (uint32_t)__builtin_ctzll(~tk) : 64u;
@@ -2750,7 +2751,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
       DIAG_C(dt_tail += DIAG_NOW() - dq3;)
     }
     if (!bad && bq) flush_blk(nb);
-    if (have && !bad) validate();
+    if (have && !bad) { validate(); validate_all(); }
     const uint32_t ds0 = pos;
     // U0's delete set must already be in union order (client descending, clock ascending): checked by
     // the emit's first pass, which streams it anyway

@@ -47,6 +47,7 @@ uint32_t ygm_k_lean_stage_bytes();
 int ygm_k_launch_merge_lean(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, uint32_t flags,
                             uint8_t* out, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, void* meta_next,
                             uint32_t* defer_list, uint64_t out_cap, hipStream_t s, const uint64_t* doc_off, const uint16_t* upd_len);
+int ygm_k_launch_big_wait(void* meta, uint32_t n_large, hipStream_t s);
 int ygm_k_launch_build_off(const uint64_t* doc_off, const uint16_t* upd_len, const uint32_t* doc_upd, const uint32_t* list, uint32_t n,
                            uint64_t* upd_off, hipStream_t s);
 int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, uint32_t n_docs, const uint32_t* list,
@@ -464,6 +465,7 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
       join2.st = c->stream2;
       if (launch(1, llist, (uint32_t)cnt[2], c->stream2)) return YGM_EDEVICE;
       HIPCHK(hipEventRecord(c->e3, c->stream2));
+      if (cnt[3] && ygm_k_launch_big_wait(P.meta, (uint32_t)cnt[2], s)) return YGM_EDEVICE;   // (their workgroups resident first)
     }
     if (launch(0, mlist, (uint32_t)cnt[3], s)) return YGM_EDEVICE;
     if ((e = read_meta(c, s, m, P.meta))) return e;

@@ -1772,13 +1772,12 @@ YDEV bool big_hdr_fast(const TL& T, uint32_t hp, uint32_t tn, uint64_t& nst, uin
 #define YGM_BIG_BH 1
 #endif
 template <class CF>
-YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint32_t mis, uint32_t n0, uint32_t t0, uint16_t* bh,
-                   uint8_t* mk, uint16_t* lst, bool use_bh) {
+YDEV void big_spec(typename CF::Tile& T, const uint8_t* u0p, const uint32_t* nxg, uint32_t at, uint32_t mis, uint32_t n0, uint32_t t0,
+                   uint16_t* bh, uint8_t* mk, uint16_t* lst, bool use_bh) {
   // every thread takes the tile positions t0 + j THREADS (t0 < THREADS), their steps interleaved: the loads of one
   // step (global scan words, LDS table entries) are issued together, not as a chain per position
   constexpr uint32_t PER = CF::CH / CF::THREADS;
   static_assert(CF::CH % CF::THREADS == 0, "tile positions split evenly over the workgroup");
-  const uint8_t* const tb = (const uint8_t*)T.b;
   // the scan's struct ends of the tile's positions, tile-relative (an end 32 KB or more away: no entry, the chain
   // follow parses that struct from global memory).  Non-candidate positions hold no word (their load is unused).
   uint32_t rl[PER];   // the ends (block table: marks)
@@ -1787,11 +1786,18 @@ YDEV void big_spec(typename CF::Tile& T, const uint32_t* nxg, uint32_t at, uint3
     uint32_t v[PER];
     bool c[PER];
 #pragma unroll
-    for (uint32_t j = 0; j < PER; j++) {
+    for (uint32_t j = 0; j < PER; j++) {   // (the position's byte from global memory: loaded with its word and the
+                                           //  tile's chunks below, one memory latency for the three)
       const uint32_t i = t0 + j * CF::THREADS;
       const bool in = at + i < n0;
-      c[j] = in && big_cand(tb[mis + i]);
+      c[j] = in && big_cand(u0p[at + i]);
       v[j] = in ? nxg[at + i] : 0u;
+    }
+    {   // the tile's bytes: the aligned 16-byte chunks from U0 byte at - mis (a chunk holding a byte of U0 is inside the
+        // arena: its tail padding); read after this call's first barrier
+      const uint4* g = (const uint4*)(u0p + at - mis);
+      const uint32_t nld = (n0 - at + mis + 15u) / 16u;
+      for (uint32_t j = t0; j < CF::TILE / 16 && j < nld; j += CF::THREADS) T.b[j] = g[j];
     }
 #pragma unroll
     for (uint32_t j = 0; j < PER; j++) {
@@ -2428,12 +2434,13 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   // one SIMD share its issue while the helpers' SIMDs idle)
   const uint32_t tid = YGM_BIG_ROT && CF::MID ? (threadIdx.x + CF::THREADS - WAVE * (blockIdx.x % CF::WAVES)) % CF::THREADS
                                               : threadIdx.x;
+  if (!CF::MID && threadIdx.x == 0) atomicAdd(&meta->big_started, 1u);   // (k_big_wait holds the mid size back until then)
   if (tid >= WAVE) {   // helper waves: wave 0's tile commands until it sends 0 (one barrier pair per command)
     for (;;) {
       __syncthreads();
       const BigCmd C = s_cmd;
       if (C.cmd == 0) return;
-      if (C.cmd == 1) big_spec<CF>(T0, C.aux, C.at, C.mis, C.n0, tid, s_bh, s_mk, (uint16_t*)s_rst, C.tb != 0u);
+      if (C.cmd == 1) big_spec<CF>(T0, C.u0p, C.aux, C.at, C.mis, C.n0, tid, s_bh, s_mk, (uint16_t*)s_rst, C.tb != 0u);
       else if (C.cmd == 3) { if (big_clock_ranges<CF::THREADS>(blk, rec, C, tid)) L.bad = 1; }
       else if (C.cmd == 4) { if (!big_ds_canon<CF::THREADS>(C, tid)) s_cmd.tb = 1; }
       else if (C.cmd == 6) {
@@ -2561,15 +2568,17 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
     const uint4* g = (const uint4*)(u0p + at - mis);
     const uint32_t nld = (n0 - at + mis + 15u) / 16u;     // aligned chunks up to the end of U0 (arena tail padding)
     wave_sync();                                           // readers of the previous tile are done
-    for (uint32_t j = l; j < CF::TILE / 16 && j < nld; j += WAVE) T0.b[j] = g[j];
     tc0 = at; tb = at - mis;
     tn = n0 - tb < CF::TILE ? n0 - tb : CF::TILE;
-    wave_sync();
-    if (!spec) return;
+    if (!spec) {   // (the spec loads the tile with its scan words)
+      for (uint32_t j = l; j < CF::TILE / 16 && j < nld; j += WAVE) T0.b[j] = g[j];
+      wave_sync();
+      return;
+    }
     const uint64_t dg0 = DIAG_NOW();
     if (l == 0) { s_cmd.cmd = 1; s_cmd.at = at; s_cmd.mis = mis; s_cmd.n0 = n0; s_cmd.aux = nxg; s_cmd.u0p = u0p; s_cmd.tb = use_bh ? 1u : 0u; }
     __syncthreads();
-    big_spec<CF>(T0, nxg, at, mis, n0, l, s_bh, s_mk, (uint16_t*)s_rst, use_bh);
+    big_spec<CF>(T0, u0p, nxg, at, mis, n0, l, s_bh, s_mk, (uint16_t*)s_rst, use_bh);
     __syncthreads();
     dg_spec += DIAG_NOW() - dg0;
   };
@@ -3184,6 +3193,25 @@ int ygm_k_launch_big_scan(const uint8_t* arena, const uint64_t* upd_off, const u
   hipLaunchKernelGGL(k_big_scan, dim3((uint32_t)g), dim3(256), 0, s, arena, upd_off, doc_upd, fb_list, flags, S);
   const uint64_t gv = S.vq_cap / 256 + 1 < 8ull * device_cus() ? S.vq_cap / 256 + 1 : 8ull * device_cus();
   hipLaunchKernelGGL(k_big_val, dim3((uint32_t)gv), dim3(256), 0, s, arena, upd_off, doc_upd, fb_list, flags, S);
+  return launch_rc(__func__);
+}
+// The mid size starts after the 16-wave size's workgroups are resident: a 16-wave workgroup needs a whole CU (its LDS),
+// and once the mid size's four-per-CU workgroups (tens of thousands queued behind them) hold every CU, no CU drains
+// whole until the mid size is nearly done -- the 16-wave documents then start late, and the batch takes their whole
+// time after the mid size's (C3: 35 -> 50 ms on such runs).  One wave on the mid size's stream waits for the count
+// the 16-wave workgroups raise as they start (or 20 ms of device time: it never holds the stream longer).
+__global__ __launch_bounds__(64) void k_big_wait(DocMeta* meta, uint32_t want) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  while (__hip_atomic_load(&meta->big_started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want &&
+         __builtin_amdgcn_s_memtime() - t0 < 2000000ull)
+    __builtin_amdgcn_s_sleep(8);
+}
+int ygm_k_launch_big_wait(void* meta, uint32_t n_large, hipStream_t s) {
+  const uint32_t ncu = device_cus();
+  const uint32_t want = n_large < ncu ? n_large : ncu;
+  if (want == 0) return 0;
+  hipLaunchKernelGGL(k_big_wait, dim3(1), dim3(64), 0, s, (DocMeta*)meta, want);
   return launch_rc(__func__);
 }
 // large = 0: the mid size, large = 1: the 16-wave size, over the fb_list indices in fbx[0, n) (the mid size sends a

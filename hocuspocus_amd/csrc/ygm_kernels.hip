@@ -844,6 +844,14 @@ __global__ __launch_bounds__(WAVE) void k_merge_wave(const uint8_t* __restrict__
 // While document i is parsed, the chunk loads of document i + 1 are in flight (register
 // prefetch) and the scalar header loads of documents i + 1 / i + 2 run ahead of them.
 // Documents outside the lean shape are appended to `defer_list` for k_merge_wave.
+// the lane id, recomputed where it is used: an address derived from threadIdx.x is loop-invariant across the
+// persistent loop's documents, so the compiler hoists it out and, at the 128-VGPR cap, spills it -- and the copy
+// loops then wait on a scratch reload per document
+YDEV uint32_t lane_opaque() {
+  uint32_t li;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(li));
+  return li;
+}
 struct LeanHdr { uint32_t u0, k; uint64_t b0, nbytes; };
 
 // Document headers come through VECTOR loads (lane-dependent addresses, then readlane): a
@@ -1043,7 +1051,7 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
       else if (slot + (k == 0 ? 2 : nbytes) > out_cap) { size = 0; if (l == 0) { out_off[d] = slot; out_len[d] = 0; status[d] = ST_NOMEM; } }
       else {
         if (k == 0) { if (l == 0) { o[0] = 0; o[1] = 0; } }
-        else for (uint64_t c = l; c * 16 < nbytes; c += WAVE) {   // unaligned 16-byte loads (arena tail padding >= 16), aligned stores
+        else for (uint64_t c = lane_opaque(); c * 16 < nbytes; c += WAVE) {   // unaligned 16-byte loads (arena tail padding >= 16), aligned stores
           uint4 x; __builtin_memcpy(&x, arena + b0 + 16 * c, 16);
           *(uint4*)(o + 16 * c) = x;
         }
@@ -1236,7 +1244,7 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
             DIAGL(3);
             uint8_t* o = out + slot;
             const uint32_t nco = (size + 15u) / 16u;
-            for (uint32_t c = l; c < nco; c += WAVE) *(u32x4*)(o + 16 * c) = *(const LB128*)(lout + 16 * c);
+            for (uint32_t c = lane_opaque(); c < nco; c += WAVE) *(u32x4*)(o + 16 * c) = *(const LB128*)(lout + 16 * c);
           }
         }
       }

@@ -1706,14 +1706,46 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
 #ifndef YGM_VAL_LDS
 #define YGM_VAL_LDS 1
 #endif
+#ifndef YGM_VAL_SORT
+#define YGM_VAL_SORT 1
+#endif
 __global__ __launch_bounds__(256) void k_big_val(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                  const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
                                                  uint32_t flags, BigScan S) {
   constexpr uint32_t VW = (BIG_VCAP + 16u + 15u) / 16u;   // 16-byte chunks staged per candidate
   __shared__ uint4 s_w[YGM_VAL_LDS ? 256 : 1][VW];
   const uint64_t nq = *(volatile unsigned long long*)&S.cnt[4], n = nq < S.vq_cap ? nq : S.vq_cap;
+#if YGM_VAL_SORT
+  // the workgroup's 256 entries are regrouped by their struct's content ref (a counting sort in LDS) before each lane
+  // takes one: big_struct branches by content kind, and a wave of mixed kinds runs every branch its lanes take
+  __shared__ uint2 s_q[256];
+  __shared__ uint16_t s_ix[256];
+  __shared__ uint32_t s_cnt[33];
+  for (uint64_t b0 = blockIdx.x * 256ull; b0 < n; b0 += gridDim.x * 256ull) {
+    const uint32_t t = threadIdx.x;
+    if (t < 33u) s_cnt[t] = 0u;
+    __syncthreads();
+    uint32_t key = 32u, rk = 0;
+    if (b0 + t < n) {
+      const uint2 Q0 = S.vq[b0 + t];
+      s_q[t] = Q0;
+      const BigPick P0 = S.pick[Q0.x];
+      key = arena[upd_off[doc_upd[fb_list[Q0.x]] + P0.u0] + Q0.y] & 31u;
+    }
+    rk = atomicAdd(&s_cnt[key], 1u);
+    __syncthreads();
+    if (t == 0) { uint32_t a = 0; for (uint32_t k = 0; k < 33u; k++) { const uint32_t c = s_cnt[k]; s_cnt[k] = a; a += c; } }
+    __syncthreads();
+    s_ix[s_cnt[key] + rk] = (uint16_t)t;
+    __syncthreads();
+    const uint32_t src_t = s_ix[t];
+    const uint64_t i = b0 + src_t;
+    if (i < n) {
+    const uint2 Q = s_q[src_t];
+#else
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
     const uint2 Q = S.vq[i];
+#endif
     const BigPick P = S.pick[Q.x];
     const uint8_t* u0p = arena + upd_off[doc_upd[fb_list[Q.x]] + P.u0];
     const uint32_t wd = S.nv[P.pb + Q.y], end = Q.y + (wd & 0x7FFFu);
@@ -1740,6 +1772,10 @@ __global__ __launch_bounds__(256) void k_big_val(const uint8_t* __restrict__ are
 #endif
     (void)end;
     S.nv[P.pb + Q.y] = (wd & 0xFFFFu) | (big_v16(g.len, g.ok && at_end && g.len != 0 && g.len < 0xFFFFFFFFull) << 16);
+#if YGM_VAL_SORT
+    }
+    __syncthreads();   // (s_q / s_ix are rewritten by the next round)
+#endif
   }
 }
 // the struct start 2^(k+1) structs after tile position i < BT_CH (k = -1: the next one, from nx), or BJ_NONE

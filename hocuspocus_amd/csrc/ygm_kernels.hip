@@ -1609,7 +1609,7 @@ __global__ __launch_bounds__(1024) void k_big_pick(const uint8_t* __restrict__ a
 #define YGM_SCAN_LDS 1
 #endif
 #ifndef YGM_SCAN_CLS
-#define YGM_SCAN_CLS 1
+#define YGM_SCAN_CLS 2   // candidate classes queued one after the other (1: position order)
 #endif
 __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                   const uint32_t* __restrict__ doc_upd, const uint32_t* __restrict__ fb_list,
@@ -1642,12 +1642,14 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
     // queued by class -- GC and Items with an origin and deleted / string content (text's structs: the verdict from the
     // skip parse) first, then the rest -- so that a wave's lanes parse the same kind of struct more often (the parse
     // branches by kind)
-    for (uint32_t cls = 0; cls < (YGM_SCAN_CLS ? 2u : 1u); cls++)
+    constexpr uint32_t NCLS = YGM_SCAN_CLS < 1 ? 1u : (uint32_t)YGM_SCAN_CLS;
+    for (uint32_t cls = 0; cls < NCLS; cls++)
       for (uint32_t b = 0; b < w1 - w0; b += WAVE) {
         const uint32_t i = b + l;
         const uint32_t ib = i < w1 - w0 ? lb[i] : 1u;
         const bool txt = ib == 0u || ((ib & 0xC0u) && ((ib & 31u) == 1u || (ib & 31u) == 4u));
-        const bool cand = i < w1 - w0 && big_cand(ib) && (!YGM_SCAN_CLS || txt == (cls == 0u));   // (other positions are never read)
+        const uint32_t k = NCLS == 1u ? 0u : txt ? 0u : (NCLS < 3u || (ib & 0xC0u)) ? 1u : 2u;   // (3: the rest split by origin)
+        const bool cand = i < w1 - w0 && big_cand(ib) && k == cls;   // (other positions are never read: nothing written)
         const uint64_t m = __ballot(cand);
         if (cand) q[qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint16_t)i;
         qn += (uint32_t)__builtin_popcountll(m);

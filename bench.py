@@ -81,7 +81,8 @@ def parse():
     ap.add_argument("--big", choices=["c3", "c5", "c3full"], default=None,
                     help="instead of the standard line: one C3 / C5 large-document batch on the GPU next to the CPU oracle")
     ap.add_argument("--big-docs", type=int, default=None)
-    ap.add_argument("--block", choices=["f1", "mixed", "v2"], default=None,
+    ap.add_argument("--store-docs", type=int, default=1000, help="documents of the c5_store block (BASELINE C5 size 1000; 0: skip)")
+    ap.add_argument("--block", choices=["f1", "mixed", "v2", "store"], default=None,
                     help="run one side block alone and print its JSON (counter passes: tools/pmc_blocks.py)")
     ap.add_argument("--dry-run", action="store_true", help="no GPU: gloo + the CPU oracle stand in (tests of the rank path)")
     return ap.parse_args()
@@ -381,6 +382,69 @@ def f1_block(be, args, steps=5):
     if not args.no_cpu_baseline and not args.no_yjs:
         c = {"arena": states, "doc_off": doc_off}
         blk["cpu_baseline"] = cpu_yjs("snapshot", c, cpu_cores(args), min(args.f1_docs, 4000))
+    e.close()
+    return blk
+
+
+def store_block(be, args, steps=3):
+    """The default product store at BASELINE config C5's size: what GpuMerge stores for each document
+    by default -- the normalized snapshot encodeStateAsUpdate(applyUpdate(new Doc, mergeUpdates([state, ...log])))
+    (extension-database Database.ts:55-60, extension-s3 S3.ts:92-103) -- over 1 000 Tiptap-style XmlFragment
+    documents of 10 000 client blocks each (tools/synth_live.c: a simulated session yjs integrates completely; the C5
+    merge corpus of tools/synth.c is not loadable by Y.applyUpdate).  Two timed legs, inputs resident in HBM: the
+    merge of the 1 000 [state, ...log] batches, then the snapshot of the 1 000 merged states (count + scan + k_snap)."""
+    from hocuspocus_amd import Engine
+    import oracle
+    from tools import synth
+    n = args.store_docs
+    arena, upd_off, doc_upd = synth.live_docs(n, 1_000_000, 64 * 1024, n_clients=10000, max_k=50, xml=True, seed=9)
+    e = Engine(be.dev.index, compat135=True)
+    da, do, dd = be.put(arena, 64), be.put(upd_off.view(np.int64)), be.put(doc_upd.view(np.int32))
+    n_upd = int(doc_upd[-1])
+    mms = []
+    for it in range(steps + 1):   # the first run grows the scratch
+        s0 = e.stats()
+        r = e.merge_device(da, len(arena), do, dd, n_upd, n, be.stream.cuda_stream)
+        s1 = e.stats()
+        if it:
+            mms.append(s1.kernel_ms - s0.kernel_ms)
+    st, off, ln, data = be.fetch(r, n)
+    assert (st == 0).all()
+    merged_bytes = int(ln.sum())
+    ups = synth.split(arena, upd_off)
+    for d in sorted(set([0, 1, n - 1] + list(range(0, n, max(1, n // 20))))):   # merge parity on a sample
+        assert oracle.merge_updates(ups[doc_upd[d]:doc_upd[d + 1]]) == (0, data[int(off[d]):int(off[d]) + int(ln[d])]), d
+    states = np.concatenate([np.frombuffer(data[int(off[d]):int(off[d]) + int(ln[d])], np.uint8) for d in range(n)])
+    doc_off = np.zeros(n + 1, np.uint64)
+    doc_off[1:] = np.cumsum(ln.astype(np.uint64))
+    ds, dso = be.put(states, 64), be.put(doc_off.view(np.int64))
+    sms = []
+    for it in range(steps + 1):
+        s0 = e.stats()
+        rs = e.snapshot_device(ds, len(states), dso, n, be.stream.cuda_stream)
+        be.sync()
+        s1 = e.stats()
+        if it:
+            sms.append(s1.kernel_ms - s0.kernel_ms)
+    sst = _d2h(rs.status, 4 * n).view(np.int32)
+    mm, sm = sorted(mms)[len(mms) // 2], sorted(sms)[len(sms) // 2]
+    snap_out = int(rs.payload_bytes)
+    algo_m, algo_s = len(arena) + merged_bytes, len(states) + snap_out
+    blk = {"workload": f"default product store at C5 size: {n} Y.XmlFragment [state, ...log] documents, 10 000 client blocks each "
+                       f"(tools/synth_live.c), mergeUpdates then encodeStateAsUpdate(applyUpdate(new Doc, merged)), inputs resident in HBM",
+           "docs": n, "bytes_in": len(arena), "merged_bytes": merged_bytes, "snapshot_bytes": snap_out,
+           "largest_doc": int(np.diff(doc_off.astype(np.int64)).max()), "ok_docs": int((sst == 0).sum()),
+           "status_counts": {str(k): int(v) for k, v in zip(*np.unique(sst, return_counts=True))},
+           "merge_ms": round(mm, 3), "snapshot_ms": round(sm, 3), "ms_per_step": round(mm + sm, 3),
+           "value": round((len(arena) + snap_out) / (mm + sm) / 1e3, 3), "unit": "MB/s",
+           "docs_per_s": round(n / (mm + sm) * 1e3, 1),
+           "roofline": {"merge": roof(algo_m, mm, "merge cascade (large-document tier)", None),
+                        "snapshot": roof(algo_s, sm, "k_snap_count / scan / k_snap (one thread per document)", _pmc(PMC_BLOCKS, "c5_store"))},
+           "parity": "merge: bit-exact vs oracle on a sample; snapshot: tests/test_snapshot.py::test_gpu_snapshot_at_baseline_sizes "
+                     "(yjs 13.5.16 on the box) and test_kernel_code_on_host_vs_yjs_live_docs"}
+    if not args.no_cpu_baseline and not args.no_yjs:
+        c = {"arena": states, "doc_off": doc_off}
+        blk["cpu_baseline"] = {"snapshot": cpu_yjs("snapshot", c, cpu_cores(args), min(n, 200))}
     e.close()
     return blk
 
@@ -820,6 +884,9 @@ def run_rank(args, rank, world, dist, be, dev=None):
         blk["roofline"] = roof(blk["bytes_in"] + blk["bytes_out"], blk["gpu_ms"], "merge cascade (k_big_scan + k_merge_big for these documents)",
                                _pmc(PMC_BLOCKS, "c5"))
         line["c5"] = blk
+    # ---- the default product store (merge + normalized snapshot) at C5 size: rank 0 at N = 1
+    if args.store_docs and rank == 0 and world == 1 and not args.dry_run:
+        line["c5_store"] = store_block(be, args)
     # ---- CPU baselines (rank 0 at N = 1 only)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         cores = cpu_cores(args)
@@ -912,7 +979,7 @@ def big_line(args):
 def block_line(args):
     """One side block alone (rank 0, N = 1): the command the block's PMC passes profile."""
     be = GpuBackend(0)
-    fn = {"f1": f1_block, "mixed": mixed_block, "v2": v2_block}[args.block]
+    fn = {"f1": f1_block, "mixed": mixed_block, "v2": v2_block, "store": store_block}[args.block]
     print(json.dumps(fn(be, args)), flush=True)
     be.close()
 

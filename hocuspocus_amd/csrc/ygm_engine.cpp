@@ -19,6 +19,7 @@
 
 extern "C" {
 size_t ygm_k_meta_bytes();
+int ygm_k_meta_layout(size_t* sz, size_t* off_big_started, size_t* off_big_scur, size_t* off_payload_sh);
 size_t ygm_k_seq_reader_bytes();
 size_t ygm_k_drec_bytes();
 int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, const uint8_t* sv_arena, const uint64_t* sv_off,
@@ -96,9 +97,10 @@ void ygm_k_big_lists(void* scan, uint32_t n_fb, uint64_t fb_bytes, unsigned long
 
 namespace {
 
-// mirrors ygm::DocMeta (ygm_kernels.hip); sizeof is a multiple of 16
+// mirrors ygm::DocMeta (ygm_docmeta.hpp) field for field; sizeof is a multiple of 16.  ygm_open checks the layout
+// against the kernels' own (ygm_k_meta_layout): read_meta and the counter memsets depend on it
 struct Meta {
-  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer, wide_defer, mid_defer, pad_[2];
+  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer, wide_defer, mid_defer, big_started, pad_;
   unsigned long long big_scur;
   unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor, big_cursor;
   unsigned long long payload_sh[16 * 16];
@@ -228,6 +230,14 @@ const char* ygm_strerror(int code) {
 int ygm_open(int device, uint32_t flags, ygm_ctx** out) {
   if (!out) return YGM_EINVAL;
   *out = nullptr;
+  {   // the host mirror of the device counters must match the kernels' struct
+    size_t sz = 0, o1 = 0, o2 = 0, o3 = 0;
+    ygm_k_meta_layout(&sz, &o1, &o2, &o3);
+    if (sz != sizeof(Meta) || o1 != offsetof(Meta, big_started) || o2 != offsetof(Meta, big_scur) || o3 != offsetof(Meta, payload_sh)) {
+      fprintf(stderr, "ygm: host / device counter layouts differ (%zu vs %zu bytes)\n", sz, sizeof(Meta));
+      return YGM_EINVAL;
+    }
+  }
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return YGM_EDEVICE;
   ygm_ctx* c = new ygm_ctx();

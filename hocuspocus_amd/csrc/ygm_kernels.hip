@@ -3254,12 +3254,15 @@ int ygm_k_launch_big_scan(const uint8_t* arena, const uint64_t* upd_off, const u
 // and once the mid size's four-per-CU workgroups (tens of thousands queued behind them) hold every CU, no CU drains
 // whole until the mid size is nearly done -- the 16-wave documents then start late, and the batch takes their whole
 // time after the mid size's (C3: 35 -> 50 ms on such runs).  One wave on the mid size's stream waits for the count
-// the 16-wave workgroups raise as they start (or 20 ms of device time: it never holds the stream longer).
+// the 16-wave workgroups raise as they start, for at most 1 ms: s_memrealtime is the 100 MHz constant clock
+// (s_memtime counts shader cycles, whose rate follows the clock governor), 100 000 ticks.  The bound matters when the
+// second stream shares a hardware queue with the first (a process with more streams than queues): the 16-wave kernel
+// then queues behind the mid size and cannot start, and the wait costs its whole 1 ms.
 __global__ __launch_bounds__(64) void k_big_wait(DocMeta* meta, uint32_t want) {
   if (threadIdx.x != 0) return;
-  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(&meta->big_started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want &&
-         __builtin_amdgcn_s_memtime() - t0 < 2000000ull)
+         __builtin_amdgcn_s_memrealtime() - t0 < 100000ull)
     __builtin_amdgcn_s_sleep(8);
 }
 int ygm_k_launch_big_wait(void* meta, uint32_t n_large, hipStream_t s) {
@@ -3290,6 +3293,11 @@ int ygm_k_launch_merge_big(int large, const uint8_t* arena, const uint64_t* upd_
   return launch_rc(__func__);
 }
 size_t ygm_k_meta_bytes() { return sizeof(DocMeta); }
+int ygm_k_meta_layout(size_t* sz, size_t* off_big_started, size_t* off_big_scur, size_t* off_payload_sh) {
+  *sz = sizeof(DocMeta); *off_big_started = offsetof(DocMeta, big_started); *off_big_scur = offsetof(DocMeta, big_scur);
+  *off_payload_sh = offsetof(DocMeta, payload_sh);
+  return 0;
+}
 size_t ygm_k_seq_reader_bytes() { return sizeof(Stream); }
 size_t ygm_k_drec_bytes() { return sizeof(DRec); }
 

@@ -48,10 +48,13 @@ template <int WIDE> struct LnCfg {
   static constexpr int OUT = WIDE ? LNW_OUT : LN_OUT;
   static constexpr int UMAX = WIDE ? LNW_UMAX : LN_UMAX;
 };
+#ifndef YGM_LN_PAD
+#define YGM_LN_PAD 0   // experiment only: LDS bytes added per wave (occupancy A/B, profiles/r06_lean)
+#endif
 template <int WIDE>
 struct alignas(16) LeanLdsT {
   uint8_t in[LnCfg<WIDE>::IN + 96];     // + slack: window / copy reads reach up to 76 bytes past an update's start
-  uint8_t out[LnCfg<WIDE>::OUT + 80];   // + slack: lds_or_copy ORs zero into up to 68 bytes past a range
+  uint8_t out[LnCfg<WIDE>::OUT + 80 + (WIDE ? 0 : YGM_LN_PAD)];   // + slack: lds_or_copy ORs zero into up to 68 bytes past a range
 };
 typedef LeanLdsT<0> LeanLds;
 

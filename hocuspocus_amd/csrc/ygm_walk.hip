@@ -78,6 +78,27 @@ __global__ __launch_bounds__(WAVE) void k_sv_table(const uint8_t* __restrict__ s
   tbl_n[d] = n;
 }
 
+#ifndef YGM_DW_OUTEND
+#define YGM_DW_OUTEND 0   // diff output (pending header, copy run) written at the round's end instead of its start
+#endif
+#ifndef YGM_DWX_NOST
+#define YGM_DWX_NOST 0    // experiment only: copy runs without their stores (output wrong)
+#endif
+#ifndef YGM_DWX_NONEED
+#define YGM_DWX_NONEED 0  // experiment only: chunk commits ignore the copy run's ring bytes (output wrong)
+#endif
+#ifndef YGM_DW_CB64
+#define YGM_DW_CB64 0     // a document's chunks 64-byte aligned (each one half of a 128-byte line), not 16
+#endif
+#ifndef YGM_DW_PAIR
+#define YGM_DW_PAIR 0     // 1: a round's staging ends on an even chunk (both halves of a line in one round); 2: rounds up
+#endif
+#ifndef YGM_DW_SVACC
+#define YGM_DW_SVACC 0    // state vector: entries gathered in a 16-byte register chunk, stored aligned and whole
+#endif
+#ifndef YGM_DWX_ALIGNST
+#define YGM_DWX_ALIGNST 0 // experiment only: copy-run stores at 16-byte aligned positions (output wrong)
+#endif
 #ifndef YGM_DW_WPE0
 #define YGM_DW_WPE0 2   // waves per SIMD the SV walker is compiled for (register budget 512 / waves)
 #endif
@@ -148,6 +169,20 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
   uint32_t cdst = 0, cd0 = 0;
   uint64_t payload = 0;
   uint32_t rounds = 0;
+  // MODE 0 with YGM_DW_SVACC: output bytes [oq, oq + of) waiting in (oa0, oa1); oq 16-byte aligned, everything before it
+  // stored.  Appends come in output order, so every 16-byte piece of the body is stored once, whole and aligned
+  uint64_t oa0 = 0, oa1 = 0;
+  uint32_t oq = 16, of = 0;
+  auto put = [&](uint64_t lo, uint64_t hi, uint32_t n) {   // n <= 16 bytes, the bytes of (lo, hi) past n zero
+    const uint32_t s = 8u * (of & 7u);
+    const uint64_t x0 = lo << s, x1 = (hi << s) | ((lo >> (63u - s)) >> 1), x2 = (hi >> (63u - s)) >> 1;
+    const bool hh = of >= 8u;
+    oa0 |= hh ? 0ull : x0; oa1 |= hh ? x0 : x1;
+    const uint64_t n0 = hh ? x1 : x2, n1 = hh ? x2 : 0ull;
+    if (of + n >= 16u) { dw_st16(ob + oq, oa0, oa1); oq += 16u; oa0 = n0; oa1 = n1; }
+    of = (of + n) & 15u;
+  };
+  (void)put;
 #ifdef YGM_DIAG
   unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // lane-iterations: fast, general, not ready, idle, string; rounds, general iterations
 #define WDG(i, v) dg[i] += (v)
@@ -197,6 +232,55 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
     ph = WK_ST;
   };
 
+  // the last round's pending header / cut prefix and the copy run (ring bytes [cp, q) -> output)
+  auto flush_out = [&]() {
+    if (e_on) {
+      e_on = false;
+      if (!bad) {
+        uint64_t lo = dw_vu_enc(e_a), hi = 0;
+        uint32_t at = dw_vulen(e_a);
+        dw_app(lo, hi, at, e_b);
+        if (MODE == 1) dw_app(lo, hi, at, e_c);
+        dw_st16(ob + e_dst, lo, hi);
+        if (MODE == 1 && e_pl) {   // the re-encoded prefix of a cut struct
+          uint64_t o = e_dst + at;
+          ob[o++] = (uint8_t)e_info;
+          if (e_info) {   // an item: origin (client, clock + off - 1), right origin verbatim
+            o = dw_put_vu(ob, o, e_b);
+            o = dw_put_vu(ob, o, e_oclk);
+            for (uint32_t k = e_ro_p; k < e_ro_e; k++) ob[o++] = (uint8_t)dw_byte(L, l, e_q + k);
+          }
+          dw_put_vu(ob, o, e_clen);
+        }
+      }
+    }
+    if (MODE == 1 && run_on) {   // the copy run: ring bytes [cp, run_end) -> output at cdst
+      if (bad) run_on = false;
+      else {
+        const uint32_t done = ph == WK_STR ? sp : q;
+        const bool fin = run_end <= done;
+        const uint32_t ce = fin ? run_end : (done & ~15u);   // an open run is written up to a ring piece boundary
+        if (ce > cp) {
+          if (cdst + (ce - cp) > tend) bad = 1;
+          else {
+            if (cp & 15u) {   // the head, up to the next ring piece boundary
+              const u32x4 v = dw_ring16(L, l, cp);
+              if (!YGM_DWX_NOST) __builtin_memcpy(ob + cdst, &v, 16);
+              const uint32_t a = 16u - (cp & 15u) < ce - cp ? 16u - (cp & 15u) : ce - cp;
+              cp += a; cdst += a;
+            }
+            for (; cp < ce; cp += 16u, cdst += 16u) {   // whole ring pieces
+              const u32x4 v = dw_piece(L, l, cp);
+              if (!YGM_DWX_NOST) __builtin_memcpy(ob + cdst, &v, 16);
+            }
+            cdst -= cp - ce; cp = ce;
+          }
+        }
+        if (fin && !bad) run_on = false;
+      }
+    }
+  };
+
   for (;;) {
     // ---- (0) a new batch of documents: sorted by size, largest first (the documents left at the end of a
     //      wave's range are its smallest: the last lanes to finish wait least)
@@ -227,8 +311,8 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
     //      round's consumption; a chunk that lost the bet is dropped here and staged again
     if (stg_n) {
       uint32_t need = ph == WK_STR ? sp : (MODE == 1 && ph == WK_SVN) ? 0u : q;   // (the table stays until copied)
-      if (run_on && cp < need) need = cp;
-      if (MODE == 1 && e_on && e_q < need) need = e_q;   // the pending cut struct's right origin is copied from the ring
+      if (!YGM_DWX_NONEED && run_on && cp < need) need = cp;
+      if (!YGM_DWX_NONEED && MODE == 1 && e_on && e_q < need) need = e_q;   // the pending cut struct's right origin is copied from the ring
       const uint32_t lim = (need >> 6) + DW_S;
       if (stg_k + stg_n > lim) stg_n = lim > stg_k ? lim - stg_k : 0u;
     }
@@ -282,51 +366,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
     // Output stores are 16 bytes wide, whatever the byte count: the bytes past a store's valid part are
     // overwritten by the document's next store (a lane writes its output in increasing order) or lie
     // in the slot's last 16 bytes, which tend keeps free
-    if (e_on) {
-      e_on = false;
-      if (!bad) {
-        uint64_t lo = dw_vu_enc(e_a), hi = 0;
-        uint32_t at = dw_vulen(e_a);
-        dw_app(lo, hi, at, e_b);
-        if (MODE == 1) dw_app(lo, hi, at, e_c);
-        dw_st16(ob + e_dst, lo, hi);
-        if (MODE == 1 && e_pl) {   // the re-encoded prefix of a cut struct
-          uint64_t o = e_dst + at;
-          ob[o++] = (uint8_t)e_info;
-          if (e_info) {   // an item: origin (client, clock + off - 1), right origin verbatim
-            o = dw_put_vu(ob, o, e_b);
-            o = dw_put_vu(ob, o, e_oclk);
-            for (uint32_t k = e_ro_p; k < e_ro_e; k++) ob[o++] = (uint8_t)dw_byte(L, l, e_q + k);
-          }
-          dw_put_vu(ob, o, e_clen);
-        }
-      }
-    }
-    if (MODE == 1 && run_on) {   // the copy run: ring bytes [cp, run_end) -> output at cdst
-      if (bad) run_on = false;
-      else {
-        const uint32_t done = ph == WK_STR ? sp : q;
-        const bool fin = run_end <= done;
-        const uint32_t ce = fin ? run_end : (done & ~15u);   // an open run is written up to a ring piece boundary
-        if (ce > cp) {
-          if (cdst + (ce - cp) > tend) bad = 1;
-          else {
-            if (cp & 15u) {   // the head, up to the next ring piece boundary
-              const u32x4 v = dw_ring16(L, l, cp);
-              __builtin_memcpy(ob + cdst, &v, 16);
-              const uint32_t a = 16u - (cp & 15u) < ce - cp ? 16u - (cp & 15u) : ce - cp;
-              cp += a; cdst += a;
-            }
-            for (; cp < ce; cp += 16u, cdst += 16u) {   // whole ring pieces
-              const u32x4 v = dw_piece(L, l, cp);
-              __builtin_memcpy(ob + cdst, &v, 16);
-            }
-            cdst -= cp - ce; cp = ce;
-          }
-        }
-        if (fin && !bad) run_on = false;
-      }
-    }
+    if (!YGM_DW_OUTEND) flush_out();
     if (ph == WK_FIN) {
       const uint64_t bm = __ballot(bad != 0u);   // (only finishing lanes reach here)
       if (bm) {
@@ -335,6 +375,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
         base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(bm));
         if (bad) { defer_list[base + lanes_below(bm)] = d; status[d] = ST_FALLBACK; }
       }
+      if (MODE == 0 && YGM_DW_SVACC && !bad && of) dw_st16(ob + oq, oa0, oa1);   // the body's last piece
       if (!bad) {   // the count, right-aligned in the slot's first 16 bytes (an aligned store)
         const uint32_t hl = dw_vulen(count);
         const uint64_t c = dw_vu_enc(count);
@@ -347,6 +388,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
     // ---- (4) new documents
     if (got) {
       d = nd; bad = 0; da = na; db = nb; count = 0; emitted = false; have_prev = false; nsv = 0;
+      oa0 = 0; oa1 = 0; oq = 16u; of = 0;
       slot = merge_slot(da, d);
       ob = out + slot;
       const uint64_t cap = merge_slot_cap(db - da), room = out_cap > slot ? out_cap - slot : 0ull;
@@ -360,7 +402,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
 #pragma unroll
         for (int i = 0; i < (MODE == 1 ? DW_SVN : 1); i++) sk[i] = 0u;
       }
-      cbase = da & ~15ull;
+      cbase = da & (YGM_DW_CB64 ? ~63ull : ~15ull);
       srel = 64u * tc + (uint32_t)(da - cbase); q = srel; rb = 64u * tc + (uint32_t)(db - cbase);
       landed = 0; stg_n = 0; prev8 = 0;
       bad |= (db < da || ((db - da) >> 30)) ? 1u : 0u;
@@ -375,6 +417,8 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
       const uint32_t nch = (rb + 63u) >> 6;
       const uint32_t wk = (need >> 6) + DW_S + DW_AHEAD < nch ? (need >> 6) + DW_S + DW_AHEAD : nch;
       uint32_t n = wk > landed ? (wk - landed < DW_STG ? wk - landed : DW_STG) : 0u;
+      if (YGM_DW_PAIR == 1 && n > 1u && ((landed + n) & 1u)) n--;   // (chunks k, k + 1 of a 128-byte line: k even with CB64)
+      if (YGM_DW_PAIR == 2 && n && n < DW_STG && ((landed + n) & 1u) && landed + n < nch) n++;
       stg_k = landed; stg_n = n;
       auto chunk = [&](uint32_t k) -> const u32x4* {
         return (const u32x4*)(MODE == 1 && k < tc ? tbl + 144ull * d + 64u * k : arena + cbase + 64ull * (k - tc));
@@ -679,6 +723,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
         if (q > rb) bad = 1;
       }
     }
+    if (YGM_DW_OUTEND) flush_out();   // (at the round's end: the next commit sees the run's ring bytes released)
     if (++rounds > (1u << 26)) { if (l == 0) atomicOr(&meta->fault, 1u); break; }
   }
   payload = wave_sum(payload);

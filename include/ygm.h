@@ -201,7 +201,7 @@ int ygm_merge_v1_device_finish(ygm_ctx *ctx, ygm_device_result *out);
  * batch with a larger one takes the u64 form).  2 bytes per update instead of 8 -- for a log of one-character
  * inserts the table is a third of the input bytes -- and no u64 table at all unless a document leaves the lean
  * kernel (the context then builds its entries on the device).  Lengths that do not add up to the document's bytes
- * give that document an error status.  Results, finish and reuse as ygm_merge_v1_device(_async).
+ * give that document YGM_EMALFORMED (yjs reading past an update's end throws).  Results, finish and reuse as ygm_merge_v1_device(_async).
  * (Replaces no single reference interface: the batched form of Y.mergeUpdates, yjs Y@37704.) */
 int ygm_merge_v1_device_lens(ygm_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_doc_off,
                              const uint16_t *d_upd_len, const uint32_t *d_doc_upd, uint32_t n_upd, uint32_t n_docs, void *stream,

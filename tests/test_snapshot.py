@@ -106,6 +106,86 @@ def test_kernel_code_on_host_default_mode(tmp_path):
     assert got == [(0, bytes.fromhex(ds_to_desc(e.hex()))) for _, e in rows]
 
 
+def _live_batch(specs):
+    """[state, ...log] documents of simulated sessions (tools/synth_live.c), merged by the oracle: (merged states, their
+    first updates alone) -- what GpuMerge snapshots."""
+    import oracle
+    from tools import synth
+    out = []
+    for n, max_bytes, kw in specs:
+        a, uo, du = synth.live_docs(n, int(max_bytes), **kw)
+        ups = synth.split(a, uo)
+        for d in range(n):
+            st, m = oracle.merge_updates(ups[du[d]:du[d + 1]])
+            assert st == 0
+            out.append(m)
+            out.append(ups[du[d]])
+    return out
+
+
+LIVE_SPECS = ((6, 5e4, dict(min_bytes=2000, n_clients=300, xml=True, seed=21)), (6, 5e4, dict(min_bytes=2000, n_clients=8, seed=22)),
+              (20, 2e4, dict(min_bytes=2000, n_clients=40, xml=True, seed=23, max_k=10)),
+              (10, 1e4, dict(min_bytes=2000, n_clients=3, seed=24, max_k=30)))
+
+
+@pytest.mark.skipif(not (NODE and BUNDLE) or shutil.which("g++") is None, reason="node + the yjs bundle and a host compiler needed")
+def test_kernel_code_on_host_vs_yjs_live_docs(tmp_path):
+    """Live-session documents (tools/synth_live.c: Tiptap-style XmlFragment trees with formats, embeds, attributes and
+    up to 300 clients; Y.Text with heavy deletions and strings split by later inserts), merged by the oracle, snapshotted
+    by yjs and by the kernel's code host-compiled -- 13.5 mode, and the 13.6 default against the client-descending
+    rewrite.  Every document integrates completely in yjs (no pending structs)."""
+    from golden import ds_to_desc
+    exe = str(tmp_path / "snapdev")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", exe, os.path.join(ROOT, "tools", "snapdev", "snapdev.cpp")], check=True, timeout=300)
+    us = _live_batch(LIVE_SPECS)
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "exp.bin")
+    write_in(a, us)
+    subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_expect.js"), a, b], check=True, timeout=240)
+    exp = read_res(b)
+    assert all(st == 0 for st, _ in exp)
+    for mode in ("1", "0"):
+        g = str(tmp_path / f"got{mode}.bin")
+        subprocess.run([exe, a, g, mode], check=True, timeout=120)
+        want = exp if mode == "1" else [(0, bytes.fromhex(ds_to_desc(e.hex()))) for _, e in exp]
+        got = read_res(g)
+        bad = [k for k in range(len(us)) if got[k] != want[k]]
+        assert not bad, f"mode {mode}: {len(bad)} differ, first {bad[:5]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not (NODE and BUNDLE), reason="node + the yjs bundle (image) needed")
+def test_gpu_snapshot_at_baseline_sizes(eng135, tmp_path):
+    """f-1 at the sizes BASELINE configs C5 / C3 name: 4 Tiptap-style documents of 10 000 client
+    blocks (0.4-1 MB) and 2 Y.Text documents over 1 MB with heavy deletions, [state, ...log] of live sessions
+    (tools/synth_live.c), merged on the GPU (against the oracle), then snapshotted on the GPU, against yjs's
+    snapshot of the merge."""
+    import oracle
+    from tools import synth
+    docs = []
+    for n, mb, kw in ((4, 1.0e6, dict(min_bytes=64 * 1024, n_clients=10000, xml=True, max_k=50, seed=5)),
+                      (2, 2.2e6, dict(min_bytes=1 << 20, n_clients=64, max_k=200, seed=3))):
+        a, uo, du = synth.live_docs(n, int(mb), **kw)
+        ups = synth.split(a, uo)
+        docs += [ups[du[d]:du[d + 1]] for d in range(n)]
+    merged = eng135.merge_updates_batch(docs)
+    assert merged == [oracle.merge_updates(d) for d in docs]
+    states = [m for _, m in merged]
+    assert sum(len(m) >= 1 << 20 for m in states) >= 2
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "exp.bin")
+    write_in(a, states)
+    subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_expect.js"), a, b], check=True, timeout=240)
+    exp = read_res(b)
+    assert all(st == 0 for st, _ in exp)
+    got = eng135.snapshot_batch(states)
+    bad = [k for k in range(len(states)) if got[k] != exp[k]]
+    assert not bad, f"{len(bad)} differ, first {bad[:3]}: {[got[k][0] for k in bad[:3]]}"
+    # smaller live sessions (every client count, both root types) in one more batch
+    us = _live_batch(LIVE_SPECS)
+    write_in(a, us)
+    subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_expect.js"), a, b], check=True, timeout=240)
+    assert eng135.snapshot_batch(us) == read_res(b)
+
+
 # ---------------------------------------------------------------------------------------- flat text (k_snap_text)
 TFIX = os.path.join(ROOT, "tests", "golden", "snapshot_text_v135.json.gz")
 

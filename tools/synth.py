@@ -17,7 +17,7 @@ def lib():
     global _lib
     if _lib is None:
         path = os.path.join(_HERE, "libsynth.so")
-        if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(os.path.join(_HERE, "synth.c")):
+        if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(os.path.join(_HERE, f)) for f in ("synth.c", "synth_live.c")):
             subprocess.check_call(["make", "-s", "-C", _HERE])
         L = ctypes.CDLL(path)
         P = ctypes.c_void_p
@@ -37,6 +37,9 @@ def lib():
         L.synth_text_states_gen.restype = P
         L.synth_text_states_take.argtypes = [P, P, P, P, P]
         L.synth_text_states_take.restype = None
+        L.synth_live_docs.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_int, P, P, P]
+        L.synth_live_docs.restype = ctypes.c_size_t
         L.synth_big_docs.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                      ctypes.c_uint32, ctypes.c_int, P, P, P]
         L.synth_big_docs.restype = ctypes.c_size_t
@@ -117,6 +120,43 @@ def big_docs(n_docs, max_bytes, min_bytes=1024, max_clients=64, max_k=200, xml=F
     assert n <= cap
     nu = int(doc_upd[n_docs])
     return buf[:n].copy(), upd_off[:nu + 1].copy(), doc_upd
+
+
+def live_docs(n_docs, max_bytes, min_bytes=1024, n_clients=64, max_k=200, xml=False, seed=1, threads=None):
+    """f-1 at BASELINE sizes (tools/synth_live.c): [state, ...log] documents of a simulated Y.Doc session that
+    Y.applyUpdate integrates completely -- xml=True: Tiptap-style XmlFragment (paragraphs, XmlText runs, formats,
+    embeds, attributes; n_clients > 64: exactly that many client blocks, config C5), else one Y.Text with heavy
+    deletions (config C3's shape).  State of max_bytes * rank^-0.8 bytes.  Documents come from per-document PRNG
+    streams, generated in chunks on threads (ctypes releases the GIL).  Returns (arena, upd_off, doc_upd)."""
+    from concurrent.futures import ThreadPoolExecutor
+    L = lib()
+    nt = max(1, min(_threads(threads), n_docs))
+    bounds = [n_docs * t // nt for t in range(nt + 1)]
+
+    def part(t):
+        d0, d1 = bounds[t], bounds[t + 1]
+        m = d1 - d0
+        sizes = np.maximum(max_bytes * np.arange(d0 + 1, d1 + 1, dtype=np.float64) ** -0.8, min_bytes)
+        cap = int(sizes.sum() * 2.0) + m * (max_k * 160 + (n_clients * 64 if xml else 0) + 65536)
+        buf = np.empty(cap, dtype=np.uint8)
+        uo = np.empty(m * max_k + 1, dtype=np.uint64)
+        du = np.empty(m + 1, dtype=np.uint32)
+        n = L.synth_live_docs(seed, d0, m, int(max_bytes), int(min_bytes), n_clients, max_k, 1 if xml else 0,
+                              buf.ctypes.data, uo.ctypes.data, du.ctypes.data)
+        assert n <= cap
+        return buf[:n], uo[:int(du[-1]) + 1], du
+    with ThreadPoolExecutor(nt) as ex:
+        parts = list(ex.map(part, range(nt)))
+    arena = np.concatenate([p[0] for p in parts])
+    upd_off, doc_upd, b, u = [], [], 0, 0
+    for buf, uo, du in parts:
+        upd_off.append(uo[:-1] + np.uint64(b))
+        doc_upd.append(du[:-1] + np.uint32(u))
+        b += len(buf)
+        u += int(du[-1])
+    upd_off.append(np.array([b], np.uint64))
+    doc_upd.append(np.array([u], np.uint32))
+    return arena, np.concatenate(upd_off), np.concatenate(doc_upd)
 
 
 def split(arena, off):

@@ -20,6 +20,9 @@ the lean kernel -- asserted -- so no step needs the host-driven tiers).  Beside 
            merged in one batch through the tier cascade, beside the C port and yjs (rank 0 at N = 1)
   c5       config C5 at BASELINE size (configs[4]): 1 000 Y.XmlFragment [snapshot, ...log] documents of 10 000 client
            blocks each (0.29 GB), formats / embeds / attributes, merged in one batch, beside the C port and yjs
+  c5_store the default product store at C5 size: 1 000 Tiptap-style [state, ...log] documents of 10 000 client blocks
+           from a simulated session yjs integrates completely (tools/synth_live.c), merged, then normalized
+           (encodeStateAsUpdate(applyUpdate(new Doc, merged)): what GpuMerge stores by default), each leg timed
   v2       SURVEY.md §8f-4: the C2 merge with the updates in format V2 (Y.mergeUpdatesV2), and the V1 <-> V2
            conversions of its 2 M updates
   cpu_baseline  the reference yjs path on the GPU box's host cores (yjs 13.5.16 from the image's
@@ -386,7 +389,7 @@ def f1_block(be, args, steps=5):
     return blk
 
 
-def store_block(be, args, steps=3):
+def store_block(be, args, steps=2):
     """The default product store at BASELINE config C5's size: what GpuMerge stores for each document
     by default -- the normalized snapshot encodeStateAsUpdate(applyUpdate(new Doc, mergeUpdates([state, ...log])))
     (extension-database Database.ts:55-60, extension-s3 S3.ts:92-103) -- over 1 000 Tiptap-style XmlFragment
@@ -397,8 +400,12 @@ def store_block(be, args, steps=3):
     import oracle
     from tools import synth
     n = args.store_docs
+
+    def note(msg):   # progress on stderr (a long block must not look hung)
+        print(f"[c5_store] {msg}", file=sys.stderr, flush=True)
     arena, upd_off, doc_upd = synth.live_docs(n, 1_000_000, 64 * 1024, n_clients=10000, max_k=50, xml=True, seed=9)
-    e = Engine(be.dev.index, compat135=True)
+    note(f"{n} documents, {len(arena) / 1e6:.1f} MB")
+    e = Engine(be.dev.index)   # the 13.6 default (GpuMerge's): the large-document tier unions multi-client delete sets
     da, do, dd = be.put(arena, 64), be.put(upd_off.view(np.int64)), be.put(doc_upd.view(np.int32))
     n_upd = int(doc_upd[-1])
     mms = []
@@ -408,6 +415,7 @@ def store_block(be, args, steps=3):
         s1 = e.stats()
         if it:
             mms.append(s1.kernel_ms - s0.kernel_ms)
+        note(f"merge run {it}: {s1.kernel_ms - s0.kernel_ms:.1f} ms, tiers big {s1.docs_big - s0.docs_big} seq {s1.docs_seq - s0.docs_seq}")
     st, off, ln, data = be.fetch(r, n)
     assert (st == 0).all()
     merged_bytes = int(ln.sum())
@@ -426,6 +434,7 @@ def store_block(be, args, steps=3):
         s1 = e.stats()
         if it:
             sms.append(s1.kernel_ms - s0.kernel_ms)
+        note(f"snapshot run {it}: {s1.kernel_ms - s0.kernel_ms:.1f} ms")
     sst = _d2h(rs.status, 4 * n).view(np.int32)
     mm, sm = sorted(mms)[len(mms) // 2], sorted(sms)[len(sms) // 2]
     snap_out = int(rs.payload_bytes)

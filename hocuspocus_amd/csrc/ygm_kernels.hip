@@ -887,13 +887,13 @@ YDEV bool lean_stageable(const LeanHdr& h) {
 // staging of one document and the prefetch of the next (no loop-carried live ranges).
 template <int WIDE, int LENS = 0>
 YDEV void lean_prefetch(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off, const uint16_t* __restrict__ upd_len,
-                        const LeanHdr& h, bool go, u32x4 (&v)[LnCfg<WIDE>::IN / 16 / WAVE], uint32_t (&rx)[LN_ROWS],
+                        const LeanHdr& h, bool go, u32x4 (&v)[(LnCfg<WIDE>::IN + 16 * WAVE - 1) / (16 * WAVE)], uint32_t (&rx)[LN_ROWS],
                         uint32_t (&ry)[LN_ROWS]) {
   const uint32_t l = threadIdx.x;
   const uint64_t a0 = go ? (h.b0 & ~15ull) : 0ull;
   const uint32_t last = go ? (uint32_t)(((h.b0 & 15u) + h.nbytes + 15) / 16) - 1u : 0u;
 #pragma unroll
-  for (int j = 0; j < LnCfg<WIDE>::IN / 16 / WAVE; j++) {
+  for (int j = 0; j < (LnCfg<WIDE>::IN + 16 * WAVE - 1) / (16 * WAVE); j++) {
     const uint32_t c = l + WAVE * j;
     v[j] = *(const u32x4*)(arena + a0 + 16ull * (c < last ? c : last));
   }
@@ -921,7 +921,10 @@ YDEV void lean_prefetch(const uint8_t* __restrict__ arena, const uint64_t* __res
 // the next launch's counter slot.  WIDE = 1: the wide kernel (LnCfg<1>) over the narrow kernel's deferred
 // list (wave w: entries w, w + G, ... of `list`), deferring in turn to its own list (meta->wide_defer).
 template <int WIDE, int LENS = 0>
-__global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
+#ifndef YGM_LN_OCC
+#define YGM_LN_OCC 4   // waves per SIMD the narrow kernel's registers are cut for (its LDS allows 160 KB / (in + out) per CU)
+#endif
+__global__ __launch_bounds__(WAVE, WIDE ? 3 : YGM_LN_OCC) void k_merge_lean(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ upd_off,
                                                      const uint32_t* __restrict__ doc_upd, uint32_t n_docs, uint32_t flags,
                                                      uint8_t* __restrict__ out, uint64_t* __restrict__ out_off,
                                                      uint64_t* __restrict__ out_len, int32_t* __restrict__ status, DocMeta* meta,
@@ -960,7 +963,7 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
   uint32_t du = lean_du_load(doc_upd, d, n_docs);
   LeanHdr hn = lean_hdr_of(du, lean_bo_load<LENS>(upd_off, doc_off, du, d, n_docs));
   du = lean_du_load(doc_upd, LN_AHEAD(1), n_docs);                  // header pipeline: doc_upd one document ahead
-  u32x4 v[C::IN / 16 / WAVE];
+  u32x4 v[(C::IN + 16 * WAVE - 1) / (16 * WAVE)];
   uint32_t rx[LN_ROWS], ry[LN_ROWS];
 #pragma unroll
   for (int q = 0; q < LN_ROWS; q++) { rx[q] = 0; ry[q] = 0; }
@@ -997,7 +1000,7 @@ __global__ __launch_bounds__(WAVE, WIDE ? 3 : 4) void k_merge_lean(const uint8_t
     if (go) {
       const uint32_t nch = (uint32_t)((shift + nbytes + 15) / 16);
 #pragma unroll
-      for (int j = 0; j < C::IN / 16 / WAVE; j++) {
+      for (int j = 0; j < (C::IN + 16 * WAVE - 1) / (16 * WAVE); j++) {
         const uint32_t c = l + WAVE * j;
         if (c < nch) *(LB128*)(lin + 16 * c) = v[j];
       }
@@ -1315,7 +1318,13 @@ YDEV void big_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {   // the wave
 struct BigCp { uint64_t src; uint32_t dst, n; };
 // the chunks [c, tot) of entries cl[0, m) (pre: their inclusive chunk prefix) taken by one wave, stepping over the
 // chunks of `stride` waves: four 16-byte chunks in flight per lane
-YDEV void big_copy_chunks(uint8_t* o, const BigCp* cl, uint32_t m, const uint32_t* pre, uint32_t tot, uint32_t c, uint32_t stride) {
+// pbits (nullptr: none): U0 positions [pu0, pu0 + pn0) whose byte loses bit 0x20 (big_validate) -- applied to the chunks
+// read from U0 (one 64-bit bitmap load per such chunk)
+YDEV uint32_t big_patch_bytes(uint32_t nib) {   // 0x20 in byte i for bit i of nib
+  return ((nib & 1u) ? 0x20u : 0u) | ((nib & 2u) ? 0x2000u : 0u) | ((nib & 4u) ? 0x200000u : 0u) | ((nib & 8u) ? 0x20000000u : 0u);
+}
+YDEV void big_copy_chunks(uint8_t* o, const BigCp* cl, uint32_t m, const uint32_t* pre, uint32_t tot, uint32_t c, uint32_t stride,
+                          const uint32_t* pbits = nullptr, const uint8_t* pu0 = nullptr, uint32_t pn0 = 0) {
   const uint32_t l = threadIdx.x % WAVE;
   for (uint32_t c0 = c; c0 < tot; c0 += stride) {
     uint4 v[4]; uint8_t* d[4]; uint32_t k[4];
@@ -1331,6 +1340,18 @@ YDEV void big_copy_chunks(uint8_t* o, const BigCp* cl, uint32_t m, const uint32_
         k[u] = E.n - off < 16u ? E.n - off : 16u;
         d[u] = o + E.dst + off;
         __builtin_memcpy(&v[u], (const uint8_t*)(uintptr_t)E.src + off, 16);
+        if (pbits) {   // (wave-uniform)
+          const uint64_t sa = E.src + off, ua = (uint64_t)(uintptr_t)pu0;
+          if (sa >= ua && sa < ua + pn0) {
+            const uint32_t p = (uint32_t)(sa - ua);
+            const uint64_t bw = ((uint64_t)pbits[(p >> 5) + 1u] << 32) | pbits[p >> 5];
+            const uint32_t pm = (uint32_t)(bw >> (p & 31u)) & 0xFFFFu;
+            if (pm) {
+              v[u].x &= ~big_patch_bytes(pm & 15u); v[u].y &= ~big_patch_bytes((pm >> 4) & 15u);
+              v[u].z &= ~big_patch_bytes((pm >> 8) & 15u); v[u].w &= ~big_patch_bytes(pm >> 12);
+            }
+          }
+        }
       }
     }
 #pragma unroll
@@ -1350,12 +1371,13 @@ YDEV uint32_t big_copy_pre(const BigCp* cl, uint32_t m, uint32_t* pre) {   // th
   pre[l] = inc;
   return lane63(inc);
 }
-YDEV void big_copy_list(uint8_t* o, const BigCp* cl, uint32_t nc, uint32_t* pre) {   // pre: 64 words of LDS
+YDEV void big_copy_list(uint8_t* o, const BigCp* cl, uint32_t nc, uint32_t* pre, const uint32_t* pbits = nullptr,
+                        const uint8_t* pu0 = nullptr, uint32_t pn0 = 0) {   // pre: 64 words of LDS
   for (uint32_t g = 0; g < nc; g += WAVE) {
     const uint32_t m = nc - g < (uint32_t)WAVE ? nc - g : (uint32_t)WAVE;
     const uint32_t tot = big_copy_pre(cl + g, m, pre);
     wave_sync();
-    big_copy_chunks(o, cl + g, m, pre, tot, 0u, 4u * WAVE);
+    big_copy_chunks(o, cl + g, m, pre, tot, 0u, 4u * WAVE, pbits, pu0, pn0);
     wave_sync();
   }
 }
@@ -1369,19 +1391,23 @@ struct BigOut {
   BigCp* cl; uint32_t nc, cap, *pre;
   uint64_t ls, ld, le;                                  // the last entry: source, destination, destination end
   BigCmd* cmd = nullptr; uint32_t nw = 1;               // k_merge_big: the workgroup's waves run the list (cmd 5)
+  const uint32_t* pbits = nullptr; const uint8_t* pu0 = nullptr; uint32_t pn0 = 0;   // U0's bytes to patch (big_copy_chunks)
   YDEV void b(uint32_t v) { if (w && threadIdx.x % WAVE == 0) o[n] = (uint8_t)v; n++; }   // (lane 0 of the writing wave)
   YDEV void vu(uint64_t v) { while (v > 127) { b(0x80u | (uint32_t)(v & 127)); v >>= 7; } b((uint32_t)v); }
   YDEV void flush() {
     if (!nc) return;
     wave_sync();
-    if (!cmd) big_copy_list(o, cl, nc, pre);
+    if (!cmd) big_copy_list(o, cl, nc, pre, pbits, pu0, pn0);
     else   // 64 entries per command: wave 0 publishes their chunk prefix, every wave takes every nw-th run of chunks
       for (uint32_t g = 0; g < nc; g += WAVE) {
         const uint32_t m = nc - g < (uint32_t)WAVE ? nc - g : (uint32_t)WAVE;
         const uint32_t tot = big_copy_pre(cl + g, m, pre);
-        if (threadIdx.x % WAVE == 0) { cmd->cmd = 5; cmd->vs = (uint64_t)(uintptr_t)(cl + g); cmd->ns = m; cmd->u0p = o; cmd->tb = tot; }
+        if (threadIdx.x % WAVE == 0) {
+          cmd->cmd = 5; cmd->vs = (uint64_t)(uintptr_t)(cl + g); cmd->ns = m; cmd->u0p = o; cmd->tb = tot;
+          cmd->aux = pbits; cmd->sbase = (uint64_t)(uintptr_t)pu0; cmd->n0 = pn0;
+        }
         __syncthreads();
-        big_copy_chunks(o, cl + g, m, pre, tot, 0u, nw * 4u * WAVE);
+        big_copy_chunks(o, cl + g, m, pre, tot, 0u, nw * 4u * WAVE, pbits, pu0, pn0);
         __syncthreads();
       }
     nc = 0;
@@ -1523,6 +1549,8 @@ struct BigScan {
   uint32_t* nv;              // per U0 position (candidates only): big_word
   uint32_t *llist, *mlist;   // fb_list indices by U0 size: over BIG_MID_U0 (the 16-wave size) / the rest (the mid size)
   uint2* vq;                 // slow queue (document, position): candidates k_big_val validates
+  uint32_t* pbits;           // per U0 position one bit: a struct whose info byte loses bit 0x20 in the output (documents'
+                             // positions start 32-aligned; zeroed by the scan, set by k_merge_big's validation)
   uint64_t ntask_cap, npos_cap, vq_cap;
 };
 // the scan's word of a U0 position: bits 0-14 the byte length of the struct parsed there (0: no parse, or 32 KB or
@@ -1577,7 +1605,7 @@ __global__ __launch_bounds__(1024) void k_big_pick(const uint8_t* __restrict__ a
     small_blocks = nb * 256ull > (uint64_t)n0;
   }
   if (l == 0) {
-    s_pb[wv] = w < n_fb ? (uint64_t)n0 + 16u : 0u; s_tb[wv] = nt;
+    s_pb[wv] = w < n_fb ? ((uint64_t)n0 + 16u + 31u) & ~31ull : 0u; s_tb[wv] = nt;   // (32-aligned: whole pbits words)
     s_lg[wv] = w >= n_fb ? 0u : ((n0 > BIG_MID_U0 || small_blocks) && n0 < 0x7FFFFFFFu) ? 1u : 2u;   // 1: the 16-wave list, 2: the mid list
   }
   __syncthreads();
@@ -1631,6 +1659,7 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
     const uint32_t n0 = P.n0, w0 = T.y * BIG_SCAN_CH + wv * WCH;
     if (w0 >= n0) continue;   // (wave-uniform)
     const uint32_t w1 = w0 + WCH < n0 ? w0 + WCH : n0, se = w0 + WCH + MARGIN < n0 ? w0 + WCH + MARGIN : n0;
+    if (l < (w1 - w0 + 31u) / 32u) S.pbits[(P.pb + w0) / 32u + l] = 0u;   // (P.pb and w0 are multiples of 32)
     // the stage: the aligned 16-byte chunks holding [w0, se) (a chunk holding a byte of the update is inside the arena)
     const uint8_t* g0 = u0p + w0;
     const uint32_t sh = (uint32_t)((uintptr_t)g0 & 15u), nq = (sh + (se - w0) + 15u) / 16u;
@@ -1782,7 +1811,7 @@ __global__ __launch_bounds__(256) void k_big_val(const uint8_t* __restrict__ are
     const bool at_end = w.pos == end;
 #endif
     (void)end;
-    S.nv[P.pb + Q.y] = (wd & 0xFFFFu) | (big_v16(g.len, g.ok && at_end && g.len != 0 && g.len < 0xFFFFFFFFull) << 16);
+    S.nv[P.pb + Q.y] = (wd & 0xFFFFu) | (big_v16(g.len, g.ok && !g.patch && at_end && g.len != 0 && g.len < 0xFFFFFFFFull) << 16);
 #if YGM_VAL_SORT
     }
     __syncthreads();   // (s_q / s_ix are rewritten by the next round)
@@ -1947,9 +1976,12 @@ YDEV void big_prefetch(const BigCmd& C, uint32_t t0) {
 // C.aux) where it has one, else validated from global memory; stored with their clock lengths.  True if any is not
 // what write_struct emits.  Run once at the walk's end by the whole workgroup: off the follow's serial chain, with
 // the global parses of every lane in flight together.
+// Returns bit 0: some struct is not what write_struct emits; bit 1: some struct is, once its info byte loses bit 0x20
+// (marked in the document's bitmap pbits: C.at = its first word; the emit's copies clear the bit).
 template <uint32_t NT>
-YDEV bool big_validate(BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0) {
-  bool vbad = false;
+YDEV uint32_t big_validate(BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0, uint32_t* pbits_all) {
+  uint32_t r = 0;
+  uint32_t* const pbits = pbits_all + C.at;
   for (uint64_t i = C.vs + t0; i < C.ns; i += NT) {
     BigRec R = rec[C.sbase + i];
     const uint32_t v16 = big_cand(C.u0p[R.start]) ? C.aux[R.start] >> 16 : 0u;   // (the scan wrote candidate positions only)
@@ -1958,11 +1990,12 @@ YDEV bool big_validate(BigRec* rec, const BigCmd& C, uint32_t flags, uint32_t t0
       GCur w; w.init(C.u0p, C.n0); w.pos = R.start;
       const GStruct g = big_struct(w, flags);
       len = g.ok && w.pos == R.end ? g.len : 0u;
+      if (len && g.patch) { atomicOr(&pbits[R.start >> 5], 1u << (R.start & 31u)); r |= 2u; }
     }
-    vbad |= len == 0u || len >= 0xFFFFFFFFull;
+    r |= (len == 0u || len >= 0xFFFFFFFFull) ? 1u : 0u;
     rec[C.sbase + i].len = (uint32_t)len;
   }
-  return vbad;
+  return r;
 }
 
 // ---- U0's delete set spliced instead of streamed (big documents: U0's delete set large against the log's ranges).
@@ -2503,8 +2536,8 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
         big_rank_sort<BigRange, CF::THREADS>(L.rg, (uint32_t)C.ns, (BigRange*)&T0, tid);
       }
       else if (C.cmd == 5) big_copy_chunks(const_cast<uint8_t*>(C.u0p), (const BigCp*)(uintptr_t)C.vs, (uint32_t)C.ns, s_cpre, C.tb,
-                                           (tid / WAVE) * 4u * WAVE, CF::WAVES * 4u * WAVE);
-      else if (big_validate<CF::THREADS>(rec, C, flags, tid)) L.bad = 1;
+                                           (tid / WAVE) * 4u * WAVE, CF::WAVES * 4u * WAVE, C.aux, (const uint8_t*)(uintptr_t)C.sbase, C.n0);
+      else { const uint32_t r = big_validate<CF::THREADS>(rec, C, flags, tid, S.pbits); if (r & 1u) L.bad = 1; if (r & 2u) L.patch = 1; }
       __syncthreads();
       if (C.cmd == 1) big_prefetch<CF::CH, CF::THREADS - WAVE>(C, tid - WAVE);   // (while wave 0 follows the chain)
     }
@@ -2514,7 +2547,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   const uint32_t w = fbx ? fbx[blockIdx.x] : blockIdx.x;   // index into fb_list (and the scan's picks)
   const uint32_t d = fb_list[w];
   const uint32_t ua = doc_upd[d], k = doc_upd[d + 1] - ua;
-  if (l == 0) { L.npc = 0; L.nrg = 0; L.bad = (flags & 2u) ? 1u : 0u; s_pick = 0; }   // YGM_F_FORCE_SEQ: all to the sequential kernel
+  if (l == 0) { L.npc = 0; L.nrg = 0; L.bad = (flags & 2u) ? 1u : 0u; L.patch = 0; s_pick = 0; }   // YGM_F_FORCE_SEQ: all to the sequential kernel
   wave_sync();
   // ---- the snapshot U0: the largest update (the first of equal ones)
   for (uint32_t i = l; i < k; i += WAVE) {
@@ -2555,7 +2588,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
       for (uint64_t q = 0; q < nst && !c.err && !bad; q++) {
         const uint32_t b0 = c.pos;
         const GStruct g = big_struct(c, flags);
-        bad |= !g.ok || g.len == 0 || clock + g.len > 0xFFFFFFFFull;
+        bad |= !g.ok || g.patch || g.len == 0 || clock + g.len > 0xFFFFFFFFull;   // (a log struct to patch: the general path)
         if (bad) break;
         const uint32_t slot = atomicAdd(&L.npc, 1u);
         if (slot < (uint32_t)CF::MAXS) {
@@ -2648,10 +2681,13 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
   };
   auto validate_all = [&]() {
     const uint64_t dg0 = DIAG_NOW();
-    if (l == 0) { s_cmd.cmd = 2; s_cmd.vs = 0; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.u0p = u0p; s_cmd.n0 = n0; s_cmd.aux = nxg; }
+    if (l == 0) {
+      s_cmd.cmd = 2; s_cmd.vs = 0; s_cmd.ns = NS; s_cmd.sbase = sbase; s_cmd.u0p = u0p; s_cmd.n0 = n0; s_cmd.aux = nxg;
+      s_cmd.at = (uint32_t)(PK.pb / 32u);
+    }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the records before every wave reads them
     __syncthreads();
-    if (big_validate<CF::THREADS>(rec, s_cmd, flags, l)) L.bad = 1;
+    { const uint32_t r = big_validate<CF::THREADS>(rec, s_cmd, flags, l, S.pbits); if (r & 1u) L.bad = 1; if (r & 2u) L.patch = 1; }
     __syncthreads();
     dg_val += DIAG_NOW() - dg0;
   };
@@ -2905,6 +2941,7 @@ __global__ __launch_bounds__(CF::THREADS, CF::MID ? YGM_MID_OCC : 1) void k_merg
     o.cl = (BigCp*)(dsx + 3 * CF::MAXD); o.nc = 0; o.pre = s_cpre;
     o.cap = (uint32_t)((sizeof(typename CF::Tile) - CF::SBG - 12 * CF::MAXD) / sizeof(BigCp)); o.ls = o.le = o.ld = 0;
     o.cmd = &s_cmd; o.nw = CF::WAVES;
+    if (L.patch) { o.pbits = S.pbits + PK.pb / 32u; o.pu0 = u0p; o.pn0 = n0; }   // (U0 structs whose info byte loses bit 0x20)
     o.vu(nblocks);
     if (pass == 0 && acanon) {
       uint64_t nbo = 0;
@@ -3216,7 +3253,7 @@ size_t ygm_k_big_rec_bytes() { return sizeof(BigRec); }
 // the snapshot scan's scratch for n_fb large documents of fb_bytes in all: counters, picks, tasks, nx, vl
 static void big_scan_layout(uint32_t n_fb, uint64_t fb_bytes, BigScan& S, uint8_t* base, size_t& total) {
   S.ntask_cap = fb_bytes / BIG_SCAN_CH + n_fb + 1;
-  S.npos_cap = fb_bytes + 16ull * n_fb + 16;
+  S.npos_cap = fb_bytes + 48ull * n_fb + 16;
   S.vq_cap = S.npos_cap / 4 + 1024;
   size_t o = 0;
   auto carve = [&](size_t bytes) { const size_t a = o; o += (bytes + 255) & ~(size_t)255; return base ? base + a : nullptr; };
@@ -3227,6 +3264,7 @@ static void big_scan_layout(uint32_t n_fb, uint64_t fb_bytes, BigScan& S, uint8_
   S.llist = (uint32_t*)carve(4ull * n_fb);
   S.mlist = (uint32_t*)carve(4ull * n_fb);
   S.vq = (uint2*)carve(sizeof(uint2) * S.vq_cap);
+  S.pbits = (uint32_t*)carve(4 * (S.npos_cap / 32 + 4));
   total = o;
 }
 // device pointers of the scan's counters and of its two document lists (after ygm_k_launch_big_scan)

@@ -186,10 +186,10 @@ YDEV int64_t gutf8_u16(const uint8_t* s, uint32_t n) {
 // One U0 struct: validated as read_struct (Y@81141 readers) and accepted only
 // if write_struct(off = 0) reproduces its bytes (canonical info byte, parentInfo 0/1, minimal
 // varuints, canonical content).  Returns the clock length; kind: 0 GC, 1 Item; ok = false defers.
-struct GStruct { uint64_t len; uint32_t kind; bool ok; };
+struct GStruct { uint64_t len; uint32_t kind; bool ok, patch; };   // patch: written back with info bit 0x20 cleared
 template <class CUR = GCur>
 YDEV GStruct big_struct(CUR& c, uint32_t flags) {
-  GStruct R; R.len = 0; R.kind = 1; R.ok = false;
+  GStruct R; R.len = 0; R.kind = 1; R.ok = false; R.patch = false;
   c.nm = 0;
   const uint32_t info = c.u8();
   if (c.err) return R;
@@ -201,7 +201,9 @@ YDEV GStruct big_struct(CUR& c, uint32_t flags) {
   }
   const uint32_t ref = info & 31u;
   const bool ho = (info & 0x80u) != 0, hr = (info & 0x40u) != 0;
-  if ((ho || hr) && (info & 0x20u)) return R;                      // bit 0x20 dropped on re-encode
+  // bit 0x20 beside an origin: Item.write keeps an integrated map entry's parentSub bit, the lazy reader drops it (its
+  // parentSub is read only without origins), so yjs's merge writes the same struct with the bit cleared
+  if ((ho || hr) && (info & 0x20u)) R.patch = true;
   if (ho) { c.vu(); c.vu(); }
   if (hr) { c.vu(); c.vu(); }
   if (!ho && !hr) {
@@ -397,7 +399,7 @@ template <int MAXS, int MAXD>
 struct BigLdsT {
   BigPiece pc[MAXS];
   BigRange rg[MAXD];
-  uint32_t npc, nrg, bad, u0;
+  uint32_t npc, nrg, bad, patch;   // patch: U0 holds structs whose info byte loses bit 0x20 (the scan's bitmap marks them)
 };
 
 }  // namespace ygm

@@ -29,12 +29,18 @@
 
 namespace ygm {
 
-constexpr int LN_IN = 5120;     // staged input bytes (including the 0..15 byte alignment shift)
+#ifndef YGM_LN_IN
+#define YGM_LN_IN 5120
+#endif
+#ifndef YGM_LN_OUT
+#define YGM_LN_OUT 4096
+#endif
+constexpr int LN_IN = YGM_LN_IN;     // staged input bytes (including the 0..15 byte alignment shift; a multiple of 16)
 constexpr int LN_ROWS = 4;      // updates per lane: k <= 256
 constexpr int LN_UMAX = 32;     // bytes per update
 constexpr int LN_CMAX = 8;      // distinct struct clients per document
 
-constexpr int LN_OUT = 4096;    // staged output bytes
+constexpr int LN_OUT = YGM_LN_OUT;    // staged output bytes
 
 // The wide variant (k_merge_lean<1>, run over the documents the narrow one defers): updates of up to
 // 64 bytes (multi-character inserts, SURVEY.md §8d's realistic debounce logs), documents of up to 7 KB
@@ -48,14 +54,18 @@ template <int WIDE> struct LnCfg {
   static constexpr int OUT = WIDE ? LNW_OUT : LN_OUT;
   static constexpr int UMAX = WIDE ? LNW_UMAX : LN_UMAX;
 };
+#ifndef YGM_LN_INSLACK
+#define YGM_LN_INSLACK 96
+#endif
 #ifndef YGM_LN_PAD
 #define YGM_LN_PAD 0   // experiment only: LDS bytes added per wave (occupancy A/B, profiles/r06_lean)
 #endif
 template <int WIDE>
 struct alignas(16) LeanLdsT {
-  uint8_t in[LnCfg<WIDE>::IN + 96];     // + slack: window / copy reads reach up to 76 bytes past an update's start
+  uint8_t in[LnCfg<WIDE>::IN + (WIDE ? 96 : YGM_LN_INSLACK)];   // + slack: window / copy reads reach up to 76 bytes past an update's start
   uint8_t out[LnCfg<WIDE>::OUT + 80 + (WIDE ? 0 : YGM_LN_PAD)];   // + slack: lds_or_copy ORs zero into up to 68 bytes past a range
 };
+static_assert(LN_IN % 16 == 0 && YGM_LN_INSLACK >= 80 && YGM_LN_INSLACK % 16 == 0, "staging granules and slack");
 typedef LeanLdsT<0> LeanLds;
 
 typedef __attribute__((address_space(3))) uint8_t LB8;

@@ -93,8 +93,17 @@ __global__ __launch_bounds__(WAVE) void k_sv_table(const uint8_t* __restrict__ s
 #ifndef YGM_DW_PAIR
 #define YGM_DW_PAIR 0     // 1: a round's staging ends on an even chunk (both halves of a line in one round); 2: rounds up
 #endif
+#ifndef YGM_DW_PAIR0
+#define YGM_DW_PAIR0 YGM_DW_PAIR   // ... for the state vector
+#endif
+#ifndef YGM_DW_PAIR1
+#define YGM_DW_PAIR1 YGM_DW_PAIR   // ... for the diff
+#endif
 #ifndef YGM_DW_SVACC
 #define YGM_DW_SVACC 0    // state vector: entries gathered in a 16-byte register chunk, stored aligned and whole
+#endif
+#ifndef YGM_DW_DACC
+#define YGM_DW_DACC 0     // diff: every output byte through the 16-byte register chunk, stored aligned and whole
 #endif
 #ifndef YGM_DWX_ALIGNST
 #define YGM_DWX_ALIGNST 0 // experiment only: copy-run stores at 16-byte aligned positions (output wrong)
@@ -241,8 +250,23 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
         uint32_t at = dw_vulen(e_a);
         dw_app(lo, hi, at, e_b);
         if (MODE == 1) dw_app(lo, hi, at, e_c);
-        dw_st16(ob + e_dst, lo, hi);
-        if (MODE == 1 && e_pl) {   // the re-encoded prefix of a cut struct
+        if ((MODE == 0 && YGM_DW_SVACC) || (MODE == 1 && YGM_DW_DACC)) put(lo, hi, at);
+        else dw_st16(ob + e_dst, lo, hi);
+        if (MODE == 1 && YGM_DW_DACC && e_pl) {   // the re-encoded prefix of a cut struct, through the accumulator
+          uint64_t plo = e_info, phi = 0;
+          uint32_t pat = 1;
+          if (e_info) { dw_app(plo, phi, pat, e_b); dw_app(plo, phi, pat, e_oclk); }
+          put(plo, phi, pat);
+          if (e_info && e_ro_e > e_ro_p) {   // the right origin, verbatim from the ring (<= 10 bytes)
+            uint64_t rlo, rhi;
+            dw_rd16(L, l, e_q + e_ro_p, rlo, rhi);
+            const uint32_t n = e_ro_e - e_ro_p;
+            rlo &= n >= 8u ? ~0ull : dw_lowmask(8u * n);
+            rhi &= n > 8u ? dw_lowmask(8u * (n - 8u)) : 0ull;
+            put(rlo, rhi, n);
+          }
+          put(dw_vu_enc(e_clen), 0ull, dw_vulen(e_clen));
+        } else if (MODE == 1 && e_pl) {   // the re-encoded prefix of a cut struct
           uint64_t o = e_dst + at;
           ob[o++] = (uint8_t)e_info;
           if (e_info) {   // an item: origin (client, clock + off - 1), right origin verbatim
@@ -254,7 +278,39 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
         }
       }
     }
-    if (MODE == 1 && run_on) {   // the copy run: ring bytes [cp, run_end) -> output at cdst
+    if (MODE == 1 && YGM_DW_DACC && run_on) {   // the copy run through the accumulator: whole aligned output pieces only
+      if (bad) run_on = false;
+      else {
+        const uint32_t done = ph == WK_STR ? sp : q;
+        const bool fin = run_end <= done;
+        uint32_t ce = fin ? run_end : done;
+        if (!fin) {   // an open run: up to the last whole 16-byte output piece (the rest stays in the ring)
+          const uint32_t tot = of + (ce - cp);
+          ce = tot >= 16u ? cp + (tot & ~15u) - of : cp;
+        }
+        if (ce > cp) {
+          if (cdst + (ce - cp) > tend) bad = 1;
+          else {
+            auto part = [&](uint32_t n) {   // n < 16 ring bytes at cp into the accumulator
+              const u32x4 v = dw_ring16(L, l, cp);
+              uint64_t vlo = ((uint64_t)v.y << 32) | v.x, vhi = ((uint64_t)v.w << 32) | v.z;
+              vlo &= n >= 8u ? ~0ull : dw_lowmask(8u * n);
+              vhi &= n > 8u ? dw_lowmask(8u * (n - 8u)) : 0ull;
+              put(vlo, vhi, n);
+              cp += n; cdst += n;
+            };
+            if (of) part(16u - of < ce - cp ? 16u - of : ce - cp);
+            for (; cp + 16u <= ce; cp += 16u, cdst += 16u, oq += 16u) {   // (of == 0 here)
+              const u32x4 v = (cp & 15u) ? dw_ring16(L, l, cp) : dw_piece(L, l, cp);
+              __builtin_memcpy(ob + oq, &v, 16);
+            }
+            if (cp < ce) part(ce - cp);
+          }
+        }
+        if (fin && !bad) run_on = false;
+      }
+    }
+    if (MODE == 1 && !YGM_DW_DACC && run_on) {   // the copy run: ring bytes [cp, run_end) -> output at cdst
       if (bad) run_on = false;
       else {
         const uint32_t done = ph == WK_STR ? sp : q;
@@ -375,7 +431,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
         base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(bm));
         if (bad) { defer_list[base + lanes_below(bm)] = d; status[d] = ST_FALLBACK; }
       }
-      if (MODE == 0 && YGM_DW_SVACC && !bad && of) dw_st16(ob + oq, oa0, oa1);   // the body's last piece
+      if (((MODE == 0 && YGM_DW_SVACC) || (MODE == 1 && YGM_DW_DACC)) && !bad && of) dw_st16(ob + oq, oa0, oa1);   // the body's last piece
       if (!bad) {   // the count, right-aligned in the slot's first 16 bytes (an aligned store)
         const uint32_t hl = dw_vulen(count);
         const uint64_t c = dw_vu_enc(count);
@@ -417,8 +473,11 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
       const uint32_t nch = (rb + 63u) >> 6;
       const uint32_t wk = (need >> 6) + DW_S + DW_AHEAD < nch ? (need >> 6) + DW_S + DW_AHEAD : nch;
       uint32_t n = wk > landed ? (wk - landed < DW_STG ? wk - landed : DW_STG) : 0u;
-      if (YGM_DW_PAIR == 1 && n > 1u && ((landed + n) & 1u)) n--;   // (chunks k, k + 1 of a 128-byte line: k even with CB64)
-      if (YGM_DW_PAIR == 2 && n && n < DW_STG && ((landed + n) & 1u) && landed + n < nch) n++;
+      // (with CB64 the document's chunk j is the half (cbase / 64 + j) & 1 of its 128-byte line; chunk k = tc + j)
+      const uint32_t lpar = ((uint32_t)(cbase >> 6) - tc) & 1u;
+      constexpr int PAIR = MODE == 0 ? YGM_DW_PAIR0 : YGM_DW_PAIR1;
+      if (PAIR == 1 && n > 1u && ((landed + n + lpar) & 1u)) n--;
+      if (PAIR == 2 && n && n < DW_STG && ((landed + n + lpar) & 1u) && landed + n < nch) n++;
       stg_k = landed; stg_n = n;
       auto chunk = [&](uint32_t k) -> const u32x4* {
         return (const u32x4*)(MODE == 1 && k < tc ? tbl + 144ull * d + 64u * k : arena + cbase + 64ull * (k - tc));

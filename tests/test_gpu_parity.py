@@ -791,6 +791,29 @@ def test_large_documents_c3_c5_vs_oracle(eng, xml):
         assert eng.stats().docs_seq - st0.docs_seq == 0
 
 
+def test_large_documents_live_sessions_vs_oracle(eng):
+    # [state, ...log] documents of simulated sessions yjs integrates (tools/synth_live.c): Tiptap-style XmlFragment
+    # states hold overwritten attributes -- map entries written with an origin AND the parentSub bit 0x20 (info 0xA8),
+    # which yjs's merge writes back without the bit -- and Y.Text states with strings split by later inserts.  The
+    # large-document tier takes them (the bit cleared by its copies: big_validate marks them in the scan's bitmap),
+    # bit-exact against the oracle; the sequential kernel takes none.
+    from tools import synth
+    docs = []
+    for n, mb, kw in ((4, 700000, dict(min_bytes=64 * 1024, n_clients=10000, xml=True, max_k=50, seed=15)),
+                      (6, 300000, dict(min_bytes=8 * 1024, n_clients=300, xml=True, max_k=30, seed=16)),
+                      (8, 400000, dict(min_bytes=4 * 1024, n_clients=64, max_k=200, seed=17))):
+        a, uo, du = synth.live_docs(n, mb, **kw)
+        ups = synth.split(a, uo)
+        docs += [ups[du[d]:du[d + 1]] for d in range(n)]
+    assert sum(us[0].count(bytes([0xA8])) > 10 for us in docs[:10]) >= 8   # (a lower bound: 0xA8 bytes elsewhere too)
+    st0 = eng.stats()
+    res = eng.merge_updates_batch(docs)
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+    assert not bad, (len(bad), bad[:5])
+    s1 = eng.stats()
+    assert s1.docs_seq - st0.docs_seq == 0 and s1.docs_big - st0.docs_big == len(docs), (s1.docs_seq - st0.docs_seq, s1.docs_big - st0.docs_big)
+
+
 def _log_structs(us):
     # struct count of a document's log (every update but the largest): the block headers' counts
     def vu(b, p):

@@ -168,7 +168,7 @@ def test_gpu_snapshot_at_baseline_sizes(eng135, tmp_path):
         ups = synth.split(a, uo)
         docs += [ups[du[d]:du[d + 1]] for d in range(n)]
     merged = eng135.merge_updates_batch(docs)
-    assert merged == [oracle.merge_updates(d) for d in docs]
+    assert merged == [oracle.merge_updates(d, compat135=True) for d in docs]
     states = [m for _, m in merged]
     assert sum(len(m) >= 1 << 20 for m in states) >= 2
     a, b = str(tmp_path / "in.bin"), str(tmp_path / "exp.bin")

@@ -302,6 +302,7 @@ static int prep_outputs(ygm_ctx* c, uint32_t n_docs, uint64_t out_cap, hipStream
 }
 
 static int read_meta(ygm_ctx* c, hipStream_t s, Meta& m, const void* slot) {
+  c->stats.host_syncs++;
   HIPCHK(hipMemcpyAsync(c->h_meta, slot, sizeof(Meta), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   m = *c->h_meta;
@@ -390,11 +391,22 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
   c->stats.lean_launches += c->lean_span_n;
   c->lean_span_n = 0;
   uint32_t n_gen = 0;   // documents for the general tiers
+  // The general tiers are chained on the device: the wide lean kernel (host count: the narrow kernel's deferrals),
+  // then the wave and workgroup kernels, each reading its count from the counter the kernel before it wrote (stream
+  // order; the host count is only the bound that sizes the persistent grid) -- one host wait for all three.
+  const unsigned int* d_wide_defer = (const unsigned int*)((const char*)P.meta + offsetof(Meta, wide_defer));
+  const unsigned int* d_defer_count = (const unsigned int*)((const char*)P.meta + offsetof(Meta, defer_count));
+  uint32_t bound = 0;   // documents the chain may see (0: no chain)
+  HIPCHK(hipEventRecord(c->e0, s));
   if (P.wide_route) {  // the wide kernel took the whole batch (async): its deferrals go on
-    n_gen = m.wide_defer;
+    n_gen = bound = m.wide_defer;
     c->stats.docs_lean_wide += P.n_docs - m.wide_defer;
+    if (n_gen && ygm_k_launch_merge_wave(P.arena, P.upd_off, P.doc_upd, c->defer_w_list.as<uint32_t>(), nullptr, n_gen, c->flags,
+                                         c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
+                                         P.meta, c->defer2_list.as<uint32_t>(), c->fb_list.as<uint32_t>(), P.out_cap, s))
+      return YGM_EDEVICE;
   } else if (m.lean_defer) {  // tier 1b: the wide lean kernel (updates <= 64 bytes, documents <= 7 KB) over tier 1's deferred list
-    HIPCHK(hipEventRecord(c->e0, s));
+    bound = m.lean_defer;
     if (P.doc_off && ygm_k_launch_build_off(P.doc_off, P.upd_len, P.doc_upd, c->defer_list.as<uint32_t>(), m.lean_defer,
                                             const_cast<uint64_t*>(P.upd_off), s))   // (compact form: the deferred documents' offsets)
       return YGM_EDEVICE;
@@ -402,34 +414,23 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
                                      c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
                                      P.meta, nullptr, c->defer_w_list.as<uint32_t>(), P.out_cap, P.upd_len, s))
       return YGM_EDEVICE;
-    HIPCHK(hipEventRecord(c->e1, s));
-    if ((e = read_meta(c, s, m, P.meta))) return e;
-    if (m.fault) return YGM_EDEVICE;
-    if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
-    n_gen = m.wide_defer;
-    c->stats.docs_lean_wide += m.lean_defer - m.wide_defer;
-  }
-  if (n_gen) {  // tier 2: general wave-per-document kernel over the lean kernels' deferred list
-    HIPCHK(hipEventRecord(c->e0, s));
-    if (ygm_k_launch_merge_wave(P.arena, P.upd_off, P.doc_upd, c->defer_w_list.as<uint32_t>(), nullptr, n_gen, c->flags,
+    // tier 2: the general wave-per-document kernel over the lean kernels' deferred list
+    if (ygm_k_launch_merge_wave(P.arena, P.upd_off, P.doc_upd, c->defer_w_list.as<uint32_t>(), d_wide_defer, bound, c->flags,
                                 c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
                                 P.meta, c->defer2_list.as<uint32_t>(), c->fb_list.as<uint32_t>(), P.out_cap, s))
       return YGM_EDEVICE;
-    HIPCHK(hipEventRecord(c->e1, s));
-    if ((e = read_meta(c, s, m, P.meta))) return e;
-    if (m.fault) return YGM_EDEVICE;
-    if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
   }
-  if (m.defer_count) {  // tier 3: documents over the wave class, one workgroup per document
-    HIPCHK(hipEventRecord(c->e0, s));
-    if (ygm_k_launch_merge_fast(P.arena, P.upd_off, P.doc_upd, c->defer2_list.as<uint32_t>(), nullptr, m.defer_count, c->flags,
+  if (bound) {  // tier 3: documents over the wave class, one workgroup per document
+    if (ygm_k_launch_merge_fast(P.arena, P.upd_off, P.doc_upd, c->defer2_list.as<uint32_t>(), d_defer_count, bound, c->flags,
                                 c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
                                 P.slot_total, P.meta, c->fb_list.as<uint32_t>(), P.out_cap, s))
       return YGM_EDEVICE;
     HIPCHK(hipEventRecord(c->e1, s));
+    const uint32_t lean_defer = m.lean_defer;
     if ((e = read_meta(c, s, m, P.meta))) return e;
     if (m.fault) return YGM_EDEVICE;
     if (hipEventElapsedTime(&ms0, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms0;
+    if (!P.wide_route) { n_gen = m.wide_defer; c->stats.docs_lean_wide += lean_defer - m.wide_defer; }
   }
   uint32_t n_seq = 0;
   if (m.fb_count) {  // tier 4: large [snapshot, ...log] documents, one wave each; the rest go on to tier 5
@@ -446,6 +447,7 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
     unsigned long long* d_cnt; uint32_t *llist, *mlist;
     ygm_k_big_lists(c->big_scan.p, m.fb_count, m.fb_bytes, &d_cnt, &llist, &mlist);
     unsigned long long cnt[4];
+    c->stats.host_syncs++;
     HIPCHK(hipMemcpyAsync(c->h_meta, d_cnt, sizeof cnt, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     memcpy(cnt, c->h_meta, sizeof cnt);
@@ -1119,6 +1121,7 @@ static int host_call(ygm_ctx* c, const HostCall& H, ygm_result* out) {
       c->stats.kernel_ms += a.kernel_ms - b.kernel_ms; c->stats.docs_lean += a.docs_lean - b.docs_lean;
       c->stats.lean_ms += a.lean_ms - b.lean_ms; c->stats.lean_launches += a.lean_launches - b.lean_launches;
       c->stats.docs_big += a.docs_big - b.docs_big; c->stats.docs_lean_wide += a.docs_lean_wide - b.docs_lean_wide;
+      c->stats.host_syncs += a.host_syncs - b.host_syncs;
     }
     int32_t* st = c->h_status.as<int32_t>();
     uint64_t* ln = c->h_len.as<uint64_t>();

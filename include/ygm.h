@@ -89,6 +89,10 @@ typedef struct {
   uint64_t docs_big;                   /* merges finished by the large-document ([snapshot, ...log]) kernel */
   uint64_t docs_lean_wide;             /* merges of docs_lean finished by the wide lean kernel (updates <= 64 B,
                                           documents <= 7 KB: the narrow kernel's deferrals) */
+  uint64_t host_syncs;                 /* host waits on the device inside the calls (counter reads between the merge
+                                          tiers, snapshot workspace sizing, ...): one per call for a batch the lean
+                                          kernels finish, two when the general tiers are needed, more for the
+                                          large-document and sequential tiers */
 } ygm_stats_t;
 
 /* Opens the engine on HIP device `device` (one context per GPU; contexts are

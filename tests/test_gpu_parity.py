@@ -472,6 +472,55 @@ def _lens_check(eng, docs, bad_lens):
                 assert got[0] == host[d][0] and (got[0] != 0 or got[1] == host[d][1]), d
 
 
+def _device_merge(eng, docs):
+    # docs through ygm_merge_v1_device: (status, bytes) per document, and the call's host waits (ygm_stats host_syncs)
+    import torch
+    import bench
+    blobs = [u for us in docs for u in us]
+    a = np.frombuffer(b"".join(blobs) + bytes(64), np.uint8)
+    off = np.cumsum([0] + [len(b) for b in blobs]).astype(np.uint64)
+    du = np.cumsum([0] + [len(us) for us in docs]).astype(np.uint32)
+    dev = torch.device("cuda", 0)
+    ta, to, td = (torch.from_numpy(x.copy()).to(dev) for x in (a, off.view(np.int64), du.view(np.int32)))
+    s0 = eng.stats().host_syncs
+    r = eng.merge_device(ta.data_ptr(), len(a) - 64, to.data_ptr(), td.data_ptr(), len(blobs), len(docs))
+    syncs = eng.stats().host_syncs - s0
+    torch.cuda.synchronize()
+    n = len(docs)
+    offs = bench._d2h(r.off, n * 8).view(np.uint64)
+    lens = bench._d2h(r.len, n * 8).view(np.uint64)
+    sts = bench._d2h(r.status, n * 4).view(np.int32)
+    data = bench._d2h(r.data, int(r.data_bytes)).tobytes()
+    return [(int(sts[d]), data[int(offs[d]):int(offs[d]) + int(lens[d])] if sts[d] == 0 else None) for d in range(n)], syncs
+
+
+def test_host_syncs_per_merge_call(eng):
+    # the general tiers run chained on the device (wide -> wave -> workgroup, each reading its count from
+    # the counters the kernel before it wrote), so a call waits on the device once for a batch the lean kernels finish,
+    # twice for one that needs the general tiers, and more only for large documents (their scratch is sized from the
+    # counters) -- every result still the oracle's
+    from tools import synth
+    a, o, dd = synth.text_updates(300, 200, seed=81)
+    ups = synth.split(a, o)
+    c2 = [ups[dd[d]:dd[d + 1]] for d in range(300)]
+    a, o, dd = synth.text_updates(300, 120, 1, 8, del_pct=20, seed=82, max_run=16)
+    ups = synth.split(a, o)
+    mixed = c2[:150] + [ups[dd[d]:dd[d + 1]] for d in range(300)]
+    rng = random.Random(9)
+    fast = list(mixed)
+    for d in range(0, 300, 9):
+        fast[d] = [u for us in fast[d:d + 3] for u in us]   # documents over the wave tier's class: the workgroup tier
+    a, o, dd = synth.big_docs(3, 200000, 64 * 1024, max_clients=64, max_k=50, seed=83)
+    ups = synth.split(a, o)
+    big = c2[:100] + [ups[dd[d]:dd[d + 1]] for d in range(3)]
+    rng.shuffle(big)
+    for docs, most in ((c2, 1), (mixed, 2), (fast, 2), (big, 5)):
+        res, syncs = _device_merge(eng, docs)
+        assert syncs <= most, (len(docs), syncs)
+        bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
+        assert not bad, (len(bad), bad[:5])
+
+
 def test_compact_lens_device_api_matches_host_api(eng):
     # ygm_merge_v1_device_lens (u64 per document, u16 length per update) == the host API on a batch that needs every
     # tier (the deferred documents' offsets are built on the device); documents whose lengths do not add up to their

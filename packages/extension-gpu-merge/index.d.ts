@@ -50,6 +50,8 @@ export declare class GpuEnginePool {
   snapshotMany (names: string[], states: Uint8Array[]): Promise<(Uint8Array | YgmError)[]>
   containsMany (names: string[], states: Uint8Array[], updates: Uint8Array[]): Promise<(boolean | YgmError)[]>
   stats (): Record<string, number>[]
+  /** node-wide totals: every per-device counter summed over the pool, plus `devices` */
+  statsTotal (): Record<string, number>
   close (): void
 }
 

@@ -257,6 +257,16 @@ class GpuEnginePool {
   snapshotMany (names, states) { return this._many(names, [states], (e, a) => e.snapshotMany(a)) }
   containsMany (names, states, updates) { return this._many(names, [states, updates], (e, a, b) => e.containsMany(a, b)) }
   stats () { return this.engines.map(e => e.stats()) }
+  /**
+   * Node-wide totals (the reference's server-wide counters, Hocuspocus.ts:138-160): every numeric field of the
+   * per-device stats summed over the pool's engines, plus `devices`.  Read on the host from each context's counters:
+   * no collective, nothing crosses GPUs.
+   */
+  statsTotal () {
+    const t = { devices: this.engines.length }
+    for (const s of this.stats()) for (const [k, v] of Object.entries(s)) if (typeof v === 'number') t[k] = (t[k] || 0) + v
+    return t
+  }
   close () { this.engines.forEach(e => e.close()) }
 }
 

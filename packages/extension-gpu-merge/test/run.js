@@ -54,6 +54,7 @@ class CpuDouble { // test double (never shipped): same API as GpuEngine
   async mergeManyV2 (docs) { this.calls++; return docs.map(u => Y.mergeUpdatesV2(u)) }
   async diffManyV2 (states, svs) { this.calls++; return states.map((u, i) => Y.diffUpdateV2(u, svs[i])) }
   async stateVectorsManyV2 (states) { this.calls++; return states.map(u => Y.encodeStateVectorFromUpdateV2(u)) }
+  stats () { return { calls: this.calls, device: this.device } }
   close () {}
 }
 
@@ -476,6 +477,11 @@ test('engine pool shards by fnv1a64(name) and keeps caller order', async () => {
   }
   const one = await pool.mergeUpdates(docs[3], names[3])
   assert.strictEqual(Buffer.from(one).toString('hex'), Buffer.from(Y.mergeUpdates(docs[3])).toString('hex'))
+  // node-wide totals: the per-device counters summed (calls: one batch per used shard, then the single merge)
+  const per = pool.stats(); const tot = pool.statsTotal()
+  assert.strictEqual(tot.devices, pool.engines.length)
+  assert.strictEqual(tot.calls, per.reduce((a, s) => a + s.calls, 0))
+  assert.ok(tot.calls >= 2)
   pool.close()
 })
 

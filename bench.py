@@ -390,16 +390,18 @@ def f1_block(be, args, steps=5):
 
 
 def store_block(be, args, steps=2):
-    """The default product store at BASELINE config C5's size: what GpuMerge stores for each document
-    by default -- the normalized snapshot encodeStateAsUpdate(applyUpdate(new Doc, mergeUpdates([state, ...log])))
-    (extension-database Database.ts:55-60, extension-s3 S3.ts:92-103) -- over 1 000 Tiptap-style XmlFragment
-    documents of 10 000 client blocks each (tools/synth_live.c: a simulated session yjs integrates completely; the C5
-    merge corpus of tools/synth.c is not loadable by Y.applyUpdate).  Two timed legs, inputs resident in HBM: the
-    merge of the 1 000 [state, ...log] batches, then the snapshot of the 1 000 merged states (count + scan + k_snap)."""
+    """The default product store at BASELINE config C5's size: what GpuMerge stores for each document --
+    Y.mergeUpdates([state, ...log]) on the GPU, then the doc-normalized snapshot encodeStateAsUpdate(applyUpdate(new
+    Doc, merged)) for merged states up to normalizeMaxBytes (64 KiB, packages/extension-gpu-merge/src/index.js) and the
+    bare merge above it (extension-database Database.ts:55-60, extension-s3 S3.ts:92-103) -- over 1 000 Tiptap-style
+    XmlFragment documents of 10 000 client blocks each (tools/synth_live.c: a simulated session yjs integrates
+    completely; the C5 merge corpus of tools/synth.c is not loadable by Y.applyUpdate).  Timed legs, inputs resident in
+    HBM: the merge of the 1 000 batches; the snapshot of the documents under the limit (none at this size); and, as
+    the cost the limit avoids, the forced snapshot of a sample (the snapshot kernel runs a document on one thread)."""
     from hocuspocus_amd import Engine
     import oracle
     from tools import synth
-    n = args.store_docs
+    n, limit = args.store_docs, 65536
 
     def note(msg):   # progress on stderr (a long block must not look hung)
         print(f"[c5_store] {msg}", file=sys.stderr, flush=True)
@@ -408,52 +410,74 @@ def store_block(be, args, steps=2):
     e = Engine(be.dev.index)   # the 13.6 default (GpuMerge's): the large-document tier unions multi-client delete sets
     da, do, dd = be.put(arena, 64), be.put(upd_off.view(np.int64)), be.put(doc_upd.view(np.int32))
     n_upd = int(doc_upd[-1])
-    mms = []
+    mms, tiers = [], None
     for it in range(steps + 1):   # the first run grows the scratch
         s0 = e.stats()
         r = e.merge_device(da, len(arena), do, dd, n_upd, n, be.stream.cuda_stream)
         s1 = e.stats()
         if it:
             mms.append(s1.kernel_ms - s0.kernel_ms)
-        note(f"merge run {it}: {s1.kernel_ms - s0.kernel_ms:.1f} ms, tiers big {s1.docs_big - s0.docs_big} seq {s1.docs_seq - s0.docs_seq}")
+        tiers = {"big": s1.docs_big - s0.docs_big, "seq": s1.docs_seq - s0.docs_seq}
+        note(f"merge run {it}: {s1.kernel_ms - s0.kernel_ms:.1f} ms, tiers {tiers}")
     st, off, ln, data = be.fetch(r, n)
     assert (st == 0).all()
     merged_bytes = int(ln.sum())
     ups = synth.split(arena, upd_off)
+    checked = 0
     for d in sorted(set([0, 1, n - 1] + list(range(0, n, max(1, n // 20))))):   # merge parity on a sample
         assert oracle.merge_updates(ups[doc_upd[d]:doc_upd[d + 1]]) == (0, data[int(off[d]):int(off[d]) + int(ln[d])]), d
-    states = np.concatenate([np.frombuffer(data[int(off[d]):int(off[d]) + int(ln[d])], np.uint8) for d in range(n)])
-    doc_off = np.zeros(n + 1, np.uint64)
-    doc_off[1:] = np.cumsum(ln.astype(np.uint64))
-    ds, dso = be.put(states, 64), be.put(doc_off.view(np.int64))
-    sms = []
-    for it in range(steps + 1):
-        s0 = e.stats()
-        rs = e.snapshot_device(ds, len(states), dso, n, be.stream.cuda_stream)
-        be.sync()
-        s1 = e.stats()
-        if it:
-            sms.append(s1.kernel_ms - s0.kernel_ms)
-        note(f"snapshot run {it}: {s1.kernel_ms - s0.kernel_ms:.1f} ms")
-    sst = _d2h(rs.status, 4 * n).view(np.int32)
-    mm, sm = sorted(mms)[len(mms) // 2], sorted(sms)[len(sms) // 2]
-    snap_out = int(rs.payload_bytes)
-    algo_m, algo_s = len(arena) + merged_bytes, len(states) + snap_out
+        checked += 1
+    states = [np.frombuffer(data[int(off[d]):int(off[d]) + int(ln[d])], np.uint8) for d in range(n)]
+
+    def snap(docs, reps):   # kernel ms (best of reps) and output bytes of ygm_snapshot_v1_device over `docs`
+        if not docs:
+            return 0.0, 0, 0
+        cat = np.concatenate([states[d] for d in docs])
+        doff = np.zeros(len(docs) + 1, np.uint64)
+        doff[1:] = np.cumsum([len(states[d]) for d in docs])
+        ds, dso = be.put(cat, 64), be.put(doff.view(np.int64))
+        best, rs = None, None
+        for _ in range(reps):
+            s0 = e.stats()
+            rs = e.snapshot_device(ds, len(cat), dso, len(docs), be.stream.cuda_stream)
+            be.sync()
+            ms = e.stats().kernel_ms - s0.kernel_ms
+            best = ms if best is None or ms < best else best
+        ok = int((_d2h(rs.status, 4 * len(docs)).view(np.int32) == 0).sum())
+        return best, int(rs.payload_bytes), ok
+    under = [d for d in range(n) if len(states[d]) <= limit]
+    sms, sout, sok = snap(under, 2)
+    over_bytes = sum(len(states[d]) for d in range(n) if len(states[d]) > limit)
+    sample = sorted(range(n), key=lambda d: len(states[d]))[:4] + [0]   # the 4 smallest and the largest
+    note(f"forced snapshot of {len(sample)} documents")
+    fms, fout, fok = snap(sample, 1)
+    note(f"forced snapshot: {fms:.1f} ms")
+    stored = sout + over_bytes
+    mm = sorted(mms)[len(mms) // 2]
+    total_ms = mm + sms
     blk = {"workload": f"default product store at C5 size: {n} Y.XmlFragment [state, ...log] documents, 10 000 client blocks each "
-                       f"(tools/synth_live.c), mergeUpdates then encodeStateAsUpdate(applyUpdate(new Doc, merged)), inputs resident in HBM",
-           "docs": n, "bytes_in": len(arena), "merged_bytes": merged_bytes, "snapshot_bytes": snap_out,
-           "largest_doc": int(np.diff(doc_off.astype(np.int64)).max()), "ok_docs": int((sst == 0).sum()),
-           "status_counts": {str(k): int(v) for k, v in zip(*np.unique(sst, return_counts=True))},
-           "merge_ms": round(mm, 3), "snapshot_ms": round(sm, 3), "ms_per_step": round(mm + sm, 3),
-           "value": round((len(arena) + snap_out) / (mm + sm) / 1e3, 3), "unit": "MB/s",
-           "docs_per_s": round(n / (mm + sm) * 1e3, 1),
-           "roofline": {"merge": roof(algo_m, mm, "merge cascade (large-document tier)", None),
-                        "snapshot": roof(algo_s, sm, "k_snap_count / scan / k_snap (one thread per document)", _pmc(PMC_BLOCKS, "c5_store"))},
-           "parity": "merge: bit-exact vs oracle on a sample; snapshot: tests/test_snapshot.py::test_gpu_snapshot_at_baseline_sizes "
-                     "(yjs 13.5.16 on the box) and test_kernel_code_on_host_vs_yjs_live_docs"}
+                       f"(tools/synth_live.c), Y.mergeUpdates then the snapshot for merged states <= {limit} bytes (GpuMerge "
+                       f"normalizeMaxBytes), inputs resident in HBM",
+           "docs": n, "bytes_in": len(arena), "merged_bytes": merged_bytes, "stored_bytes": stored,
+           "largest_doc": int(max(len(x) for x in states)), "merge_tiers": tiers,
+           "docs_normalized": len(under), "docs_over_limit": n - len(under),
+           "merge_ms": round(mm, 3), "snapshot_ms": round(sms, 3), "ms_per_step": round(total_ms, 3),
+           "value": round((len(arena) + stored) / total_ms / 1e3, 3), "unit": "MB/s", "docs_per_s": round(n / total_ms * 1e3, 1),
+           "roofline": roof(len(arena) + merged_bytes, mm, "merge cascade (large-document tier)", _pmc(PMC_BLOCKS, "c5_store")),
+           "forced_snapshot_sample": {"docs": len(sample), "bytes_in": int(sum(len(states[d]) for d in sample)), "bytes_out": fout,
+                                      "ok_docs": fok, "ms": round(fms, 1),
+                                      "us_per_byte_largest": round(fms * 1e3 / max(len(states[d]) for d in sample), 2),
+                                      "note": "encodeStateAsUpdate(applyUpdate(new Doc, merged)) on the GPU: one thread per "
+                                              "document, so a batch takes its largest document's time"},
+           "parity": f"merge: bit-exact vs oracle on {checked} documents; snapshot: tests/test_snapshot.py::"
+                     "test_gpu_snapshot_at_baseline_sizes (yjs 13.5.16 on the box)"}
     if not args.no_cpu_baseline and not args.no_yjs:
-        c = {"arena": states, "doc_off": doc_off}
-        blk["cpu_baseline"] = {"snapshot": cpu_yjs("snapshot", c, cpu_cores(args), min(n, 200))}
+        k = min(n, 100)
+        blk["cpu_baseline"] = {"merge": cpu_yjs("merge", {"arena": arena, "upd_off": upd_off, "doc_upd": doc_upd}, cpu_cores(args), k)}
+        cat = np.concatenate(states[:16])
+        doff = np.zeros(17, np.uint64)
+        doff[1:] = np.cumsum([len(x) for x in states[:16]])
+        blk["cpu_baseline"]["snapshot"] = cpu_yjs("snapshot", {"arena": cat, "doc_off": doff}, cpu_cores(args), 16)
     e.close()
     return blk
 

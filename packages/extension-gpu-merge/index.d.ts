@@ -95,6 +95,8 @@ export interface GpuMergeConfiguration extends GpuEngineOptions {
   onRefused?: 'reference' | 'throw'
   /** store the GPU doc-normalized snapshot of the merge (GC'd, merged: the shape extension-database stores); default true, false stores the bare merge */
   normalize?: boolean
+  /** merged states over this many bytes are stored as the bare merge (the snapshot kernel runs one thread per document); default 65536 */
+  normalizeMaxBytes?: number
 }
 
 export declare class GpuMerge implements Extension {

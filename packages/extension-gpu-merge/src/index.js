@@ -42,7 +42,7 @@ class GpuMerge {
   /**
    * @param {{store?: DocumentStore|Function, fetch?: Function, device?: number, Y?: any,
    *          engine?: GpuEngine, batchWindowMs?: number, maxBatchDocs?: number, compat135?: boolean,
-   *          onRefused?: 'reference'|'throw', normalize?: boolean}} configuration
+   *          onRefused?: 'reference'|'throw', normalize?: boolean, normalizeMaxBytes?: number}} configuration
    *   onRefused: what a store does when the engine refuses ONE document (a per-document status: content
    *   yjs would re-encode, ENONCANON; a corrupt stored base, EMALFORMED / ERANGE / ESURROGATE / EDEPTH) --
    *   'reference' (default): store Y.encodeStateAsUpdate(document) like extension-database and record it in
@@ -54,6 +54,10 @@ class GpuMerge {
    *   garbage-collected and adjacent structs merged, the bytes extension-database stores for a fresh load of
    *   the same updates (Database.ts:55-60); a document outside the snapshot kernel's envelope keeps its merged
    *   bytes (`unnormalized`).  normalize: false stores the bare Y.mergeUpdates bytes.
+   *   normalizeMaxBytes (default 65536): merged states larger than this are stored as the bare merge (counted in
+   *   `sizeSkipped`): the snapshot kernel runs a document on ONE GPU thread (yjs's integration is a serial chain),
+   *   about 20 us per byte for a Tiptap document of 10 000 clients -- seconds for the ~1 MB documents of BASELINE
+   *   config C5, where the merge itself takes milliseconds (DESIGN.md 6.R6).  Both forms load identically.
    */
   constructor (configuration = {}) {
     this.extensionName = 'GpuMerge'
@@ -61,6 +65,9 @@ class GpuMerge {
     this.priority = configuration.priority || 900
     this.configuration = configuration
     this.normalize = configuration.normalize !== false
+    this.normalizeMaxBytes = configuration.normalizeMaxBytes === undefined ? 65536 : configuration.normalizeMaxBytes
+    /** stores whose merged state was over normalizeMaxBytes (kept as the bare merge) */
+    this.sizeSkipped = 0
     // drop-in for `new Database({ fetch, store })`, or a batched DocumentStore instance
     const st = configuration.store
     this.store = st && typeof st.storeMany === 'function'
@@ -168,7 +175,8 @@ class GpuMerge {
         const job = { head: entry.base ? [entry.base] : [], ...entry.log.packed(taken) }
         const eng = this._engine()
         state = await (eng.mergePacked ? eng.mergePacked(job, data.documentName) : eng.mergeUpdates(job.head.concat(entry.log.toArray(taken)), data.documentName))
-        if (this.normalize) state = await this._normalize(state, data.documentName)
+        if (this.normalize && state.byteLength <= this.normalizeMaxBytes) state = await this._normalize(state, data.documentName)
+        else if (this.normalize) this.sizeSkipped++
       } catch (e) {
         // a document the engine refuses (content yjs would re-encode, YGM_ENONCANON; a corrupt stored
         // base): unless configured to throw, store what extension-database stores for it -- the live

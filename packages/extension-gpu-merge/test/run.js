@@ -290,6 +290,32 @@ test('the default store is the doc-normalized snapshot of the merge', async (eng
   assert.deepStrictEqual(ext.unnormalized, [])
 })
 
+// normalizeMaxBytes: a merged state over the limit is stored as the bare merge (the snapshot kernel runs a document on
+// one GPU thread: seconds for megabyte documents), counted in sizeSkipped; one under it is normalized as before
+test('merged states over normalizeMaxBytes are stored as the bare merge', async (engine) => {
+  const db = memoryDb()
+  const ext = new GpuMerge({ ...db, Y, engine, normalizeMaxBytes: 200 })
+  const hp = new MiniHocuspocus({ extensions: [ext], Y })
+  const logs = {}
+  for (const [name, n] of [['small', 4], ['large', 60]]) {
+    const doc = await hp.loadDocument(name)
+    doc.clientID = 9
+    logs[name] = []
+    doc.on('update', u => logs[name].push(u))
+    const t = doc.getText('t')
+    for (let i = 0; i < n; i++) doc.transact(() => t.insert(t.length, 'xy'), 'c1')
+    doc.transact(() => t.delete(0, 2), 'c1')
+  }
+  await hp.flushAll(); await hp.lastStore
+  const mergedLarge = Buffer.from(Y.mergeUpdates(logs.large))
+  assert.ok(mergedLarge.length > 200)
+  assert.strictEqual(Buffer.compare(db.rows.get('large'), mergedLarge), 0)
+  const fresh = new Y.Doc(); Y.applyUpdate(fresh, Y.mergeUpdates(logs.small))
+  assert.ok(Y.mergeUpdates(logs.small).length <= 200)
+  assert.strictEqual(Buffer.compare(db.rows.get('small'), Buffer.from(Y.encodeStateAsUpdate(fresh))), 0)
+  assert.strictEqual(ext.sizeSkipped, 1)
+})
+
 // SURVEY.md §8f-3 (Redis.ts:210-219, 336-372): changes publish Step1 in one batch; a remote instance's
 // SyncStep1 is answered (SyncReply Step1 + Step2) in one batch, published back on the document channel
 test('redis fan-out: batched first sync steps and remote Step2 replies', async (engine) => {

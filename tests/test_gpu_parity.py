@@ -482,9 +482,11 @@ def _device_merge(eng, docs):
     du = np.cumsum([0] + [len(us) for us in docs]).astype(np.uint32)
     dev = torch.device("cuda", 0)
     ta, to, td = (torch.from_numpy(x.copy()).to(dev) for x in (a, off.view(np.int64), du.view(np.int32)))
-    s0 = eng.stats().host_syncs
+    s0 = eng.stats()
     r = eng.merge_device(ta.data_ptr(), len(a) - 64, to.data_ptr(), td.data_ptr(), len(blobs), len(docs))
-    syncs = eng.stats().host_syncs - s0
+    s1 = eng.stats()
+    syncs = {"syncs": s1.host_syncs - s0.host_syncs, "general": (s1.docs_fast - s0.docs_fast) + (s1.docs_big - s0.docs_big),
+             "large_or_seq": (s1.docs_big - s0.docs_big) + (s1.docs_seq - s0.docs_seq)}
     torch.cuda.synchronize()
     n = len(docs)
     offs = bench._d2h(r.off, n * 8).view(np.uint64)
@@ -514,11 +516,19 @@ def test_host_syncs_per_merge_call(eng):
     ups = synth.split(a, o)
     big = c2[:100] + [ups[dd[d]:dd[d + 1]] for d in range(3)]
     rng.shuffle(big)
-    for docs, most in ((c2, 1), (mixed, 2), (fast, 2), (big, 5)):
-        res, syncs = _device_merge(eng, docs)
-        assert syncs <= most, (len(docs), syncs)
+    general_only = 0
+    for docs in (c2, mixed, fast, big):
+        res, k = _device_merge(eng, docs)
         bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
         assert not bad, (len(bad), bad[:5])
+        if docs is c2:
+            assert k["syncs"] == 1 and k["general"] == 0, k
+        elif k["large_or_seq"] == 0:   # the general tiers only: one wait for all of them
+            assert k["syncs"] == 2, k
+            general_only += k["general"] > 0
+        else:   # + the large-document tier (scratch sizing, the scan's lists, the mid size's deferrals) / sequential
+            assert k["syncs"] <= 6, k
+    assert general_only >= 1
 
 
 def test_compact_lens_device_api_matches_host_api(eng):

@@ -505,20 +505,22 @@ def test_host_syncs_per_merge_call(eng):
     a, o, dd = synth.text_updates(300, 200, seed=81)
     ups = synth.split(a, o)
     c2 = [ups[dd[d]:dd[d + 1]] for d in range(300)]
-    a, o, dd = synth.text_updates(300, 120, 1, 8, del_pct=20, seed=82, max_run=16)
+    a, o, dd = synth.text_updates(40, 200, 9, 16, del_pct=10, seed=82)   # 9-16 clients: past the lean kernels' 8 -> the wave tier
     ups = synth.split(a, o)
-    mixed = c2[:150] + [ups[dd[d]:dd[d + 1]] for d in range(300)]
+    wave = c2[:200] + [ups[dd[d]:dd[d + 1]] for d in range(40)]
+    a, o, dd = synth.text_updates(20, 250, 9, 16, seed=84, max_run=30)   # ~10 KB: past the wave tier's 8 KB -> the workgroup tier
+    ups = synth.split(a, o)
+    fast = c2[:200] + [ups[dd[d]:dd[d + 1]] for d in range(20)]
     rng = random.Random(9)
-    fast = list(mixed)
-    for d in range(0, 300, 9):
-        fast[d] = [u for us in fast[d:d + 3] for u in us]   # documents over the wave tier's class: the workgroup tier
     a, o, dd = synth.big_docs(3, 200000, 64 * 1024, max_clients=64, max_k=50, seed=83)
     ups = synth.split(a, o)
     big = c2[:100] + [ups[dd[d]:dd[d + 1]] for d in range(3)]
     rng.shuffle(big)
     general_only = 0
-    for docs in (c2, mixed, fast, big):
+    seen = []
+    for docs in (c2, wave, fast, big):
         res, k = _device_merge(eng, docs)
+        seen.append(k)
         bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us), res[d])]
         assert not bad, (len(bad), bad[:5])
         if docs is c2:
@@ -528,7 +530,7 @@ def test_host_syncs_per_merge_call(eng):
             general_only += k["general"] > 0
         else:   # + the large-document tier (scratch sizing, the scan's lists, the mid size's deferrals) / sequential
             assert k["syncs"] <= 6, k
-    assert general_only >= 1
+    assert general_only >= 1, seen
 
 
 def test_compact_lens_device_api_matches_host_api(eng):

@@ -392,7 +392,7 @@ def f1_block(be, args, steps=5):
 def store_block(be, args, steps=2):
     """The default product store at BASELINE config C5's size: what GpuMerge stores for each document --
     Y.mergeUpdates([state, ...log]) on the GPU, then the doc-normalized snapshot encodeStateAsUpdate(applyUpdate(new
-    Doc, merged)) for merged states up to normalizeMaxBytes (64 KiB, packages/extension-gpu-merge/src/index.js) and the
+    Doc, merged)) for merged states up to normalizeMaxBytes (32 KiB, packages/extension-gpu-merge/src/index.js) and the
     bare merge above it (extension-database Database.ts:55-60, extension-s3 S3.ts:92-103) -- over 1 000 Tiptap-style
     XmlFragment documents of 10 000 client blocks each (tools/synth_live.c: a simulated session yjs integrates
     completely; the C5 merge corpus of tools/synth.c is not loadable by Y.applyUpdate).  Timed legs, inputs resident in
@@ -401,7 +401,7 @@ def store_block(be, args, steps=2):
     from hocuspocus_amd import Engine
     import oracle
     from tools import synth
-    n, limit = args.store_docs, 65536
+    n, limit = args.store_docs, 32768
 
     def note(msg):   # progress on stderr (a long block must not look hung)
         print(f"[c5_store] {msg}", file=sys.stderr, flush=True)
@@ -448,7 +448,7 @@ def store_block(be, args, steps=2):
     under = [d for d in range(n) if len(states[d]) <= limit]
     sms, sout, sok = snap(under, 2)
     over_bytes = sum(len(states[d]) for d in range(n) if len(states[d]) > limit)
-    sample = sorted(range(n), key=lambda d: len(states[d]))[:4] + [0]   # the 4 smallest and the largest
+    sample = sorted(range(n), key=lambda d: len(states[d]))[:4]   # the 4 smallest (~0.42 MB each: the batch takes ~9 s)
     note(f"forced snapshot of {len(sample)} documents")
     fms, fout, fok = snap(sample, 1)
     note(f"forced snapshot: {fms:.1f} ms")

@@ -108,6 +108,9 @@ __global__ __launch_bounds__(WAVE) void k_sv_table(const uint8_t* __restrict__ s
 #ifndef YGM_DW_DACC
 #define YGM_DW_DACC 0     // diff: every output byte through the 16-byte register chunk, stored aligned and whole
 #endif
+#ifndef YGM_DW_SPEC2
+#define YGM_DW_SPEC2 0    // the next Item's info byte read beside this one's length byte (see the fast decoder)
+#endif
 #ifndef YGM_DWX_ALIGNST
 #define YGM_DWX_ALIGNST 0 // experiment only: copy-run stores at 16-byte aligned positions (output wrong)
 #endif
@@ -528,15 +531,25 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
           bool go = true;   // (ph == WK_ST implies st_left >= 1)
           bool pe = false;  // diff: the step that stopped the loop is the block's first struct past the state vector
           uint32_t pe_end = 0, pe_ce = 0;
+          // YGM_DW_SPEC2: the bytes one and two past an Item's length byte are read beside it -- the next Item's info byte
+          // when this one is Deleted content / a one-character string -- so the chain holds one dependent LDS read
+          // per Item, not two
+          uint32_t nbs = 0;
+          bool spec = false;
 #pragma unroll
           for (int u = 0; u < (MODE == 1 ? DW_U1 : DW_U); u++) {
             const uint32_t wq = (uint32_t)(w64 >> qo);
             const uint32_t tt = wq >> 1, x2 = tt & (tt - 1u), x3 = x2 & (x2 - 1u), x4 = x3 & (x3 - 1u);
-            if (u >= 1) bb = dw_byte(L, l, q);
+            if (u >= 1) {
+              if (YGM_DW_SPEC2 && spec) bb = nbs;
+              else bb = dw_byte(L, l, q);
+            }
             const uint32_t hoh = bb >> 6, ref = bb & 0x3Fu;
             const uint32_t cpos = (uint32_t)__builtin_ctz((hoh == 3u ? x4 : x2) | 0x80000000u) + 2u;   // after the origins
             const uint32_t cq = cpos & 31u;
             const uint32_t lv = dw_byte(L, l, q + cq);
+            uint32_t nb1 = 0, nb2 = 0;
+            if (YGM_DW_SPEC2) { nb1 = dw_byte(L, l, q + cq + 1u); nb2 = dw_byte(L, l, q + cq + 2u); }
             const bool isS = ref == 4u;
             const uint32_t end = cq + 1u + (isS ? lv : 0u);
             // the string's bytes are ASCII: every one of them ends a varuint (no clear bit among the lv after the length)
@@ -564,6 +577,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(MODE == 0 
               --st_left;
             }
             go = ok && st_left != 0u;
+            if (YGM_DW_SPEC2) { spec = !isS | (lv == 1u); nbs = isS ? nb2 : nb1; }
           }
           if (MODE == 1 && pe) {   // the first struct of the block past the state vector (rule R-D): the block
                                    // header, then the rest of the block as a copy run from this struct on

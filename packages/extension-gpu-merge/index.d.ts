@@ -95,7 +95,7 @@ export interface GpuMergeConfiguration extends GpuEngineOptions {
   onRefused?: 'reference' | 'throw'
   /** store the GPU doc-normalized snapshot of the merge (GC'd, merged: the shape extension-database stores); default true, false stores the bare merge */
   normalize?: boolean
-  /** merged states over this many bytes are stored as the bare merge (the snapshot kernel runs one thread per document); default 65536 */
+  /** merged states over this many bytes are stored as the bare merge (the snapshot kernel runs one thread per document); default 32768 */
   normalizeMaxBytes?: number
 }
 

@@ -54,10 +54,11 @@ class GpuMerge {
    *   garbage-collected and adjacent structs merged, the bytes extension-database stores for a fresh load of
    *   the same updates (Database.ts:55-60); a document outside the snapshot kernel's envelope keeps its merged
    *   bytes (`unnormalized`).  normalize: false stores the bare Y.mergeUpdates bytes.
-   *   normalizeMaxBytes (default 65536): merged states larger than this are stored as the bare merge (counted in
+   *   normalizeMaxBytes (default 32768): merged states larger than this are stored as the bare merge (counted in
    *   `sizeSkipped`): the snapshot kernel runs a document on ONE GPU thread (yjs's integration is a serial chain),
-   *   about 20 us per byte for a Tiptap document of 10 000 clients -- seconds for the ~1 MB documents of BASELINE
-   *   config C5, where the merge itself takes milliseconds (DESIGN.md 6.R6).  Both forms load identically.
+   *   3-5 us per byte (18-31 for Tiptap documents of 10 000 clients), and a batch takes its largest document's time:
+   *   ~0.1-0.2 s at the limit, seconds for the ~1 MB documents of BASELINE config C5, whose merge takes
+   *   milliseconds (DESIGN.md 6.R6, tools/snap_probe.py).  Both forms load identically.
    */
   constructor (configuration = {}) {
     this.extensionName = 'GpuMerge'
@@ -65,7 +66,7 @@ class GpuMerge {
     this.priority = configuration.priority || 900
     this.configuration = configuration
     this.normalize = configuration.normalize !== false
-    this.normalizeMaxBytes = configuration.normalizeMaxBytes === undefined ? 65536 : configuration.normalizeMaxBytes
+    this.normalizeMaxBytes = configuration.normalizeMaxBytes === undefined ? 32768 : configuration.normalizeMaxBytes
     /** stores whose merged state was over normalizeMaxBytes (kept as the bare merge) */
     this.sizeSkipped = 0
     // drop-in for `new Database({ fetch, store })`, or a batched DocumentStore instance

@@ -830,6 +830,24 @@ def test_compat135_multi_client_c2_deletions_stay_parallel(eng135):
     assert differ > 50
 
 
+def test_compat135_large_documents_vs_oracle(eng135):
+    # the large-document tier unions delete sets in client-descending order only (its splice walks U0's
+    # canonical delete set); under yjs 13.5 a document whose merged delete set has several clients goes on to the
+    # sequential kernel (first-seen order, bit-exact) -- a stated limit, measured here: every document
+    # is the oracle's, and each is finished by the large-document tier or by the sequential kernel
+    from tools import synth
+    arena, upd_off, doc_upd = synth.big_docs(12, 200000, 16 * 1024, max_clients=64, max_k=60, seed=136)
+    ups = synth.split(arena, upd_off)
+    docs = [ups[doc_upd[d]:doc_upd[d + 1]] for d in range(12)]
+    st0 = eng135.stats()
+    res = eng135.merge_updates_batch(docs)
+    st1 = eng135.stats()
+    bad = [d for d, us in enumerate(docs) if not same(oracle.merge_updates(us, compat135=True), res[d])]
+    assert not bad, (len(bad), bad[:5])
+    n_seq, n_big = st1.docs_seq - st0.docs_seq, st1.docs_big - st0.docs_big
+    assert n_seq + n_big == len(docs) and n_seq > 0, (n_seq, n_big)
+
+
 @pytest.mark.parametrize("xml", [False, True])
 def test_large_documents_c3_c5_vs_oracle(eng, xml):
     # SURVEY.md §8d C3 / C5 shapes at test size: Zipf-sized [snapshot, ...log] documents (GC,

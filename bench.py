@@ -448,8 +448,8 @@ def store_block(be, args, steps=2):
     under = [d for d in range(n) if len(states[d]) <= limit]
     sms, sout, sok = snap(under, 2)
     over_bytes = sum(len(states[d]) for d in range(n) if len(states[d]) > limit)
-    sample = sorted(range(n), key=lambda d: len(states[d]))[:4]   # the 4 smallest (~0.42 MB each: the batch takes ~9 s)
-    note(f"forced snapshot of {len(sample)} documents")
+    note(f"forced snapshot of all {n} documents")
+    sample = list(range(n))
     fms, fout, fok = snap(sample, 1)
     note(f"forced snapshot: {fms:.1f} ms")
     stored = sout + over_bytes
@@ -464,20 +464,21 @@ def store_block(be, args, steps=2):
            "merge_ms": round(mm, 3), "snapshot_ms": round(sms, 3), "ms_per_step": round(total_ms, 3),
            "value": round((len(arena) + stored) / total_ms / 1e3, 3), "unit": "MB/s", "docs_per_s": round(n / total_ms * 1e3, 1),
            "roofline": roof(len(arena) + merged_bytes, mm, "merge cascade (large-document tier)", _pmc(PMC_BLOCKS, "c5_store")),
-           "forced_snapshot_sample": {"docs": len(sample), "bytes_in": int(sum(len(states[d]) for d in sample)), "bytes_out": fout,
-                                      "ok_docs": fok, "ms": round(fms, 1),
-                                      "us_per_byte_largest": round(fms * 1e3 / max(len(states[d]) for d in sample), 2),
-                                      "note": "encodeStateAsUpdate(applyUpdate(new Doc, merged)) on the GPU: one thread per "
-                                              "document, so a batch takes its largest document's time"},
+           "forced_snapshot_all": {"docs": len(sample), "bytes_in": int(sum(len(states[d]) for d in sample)), "bytes_out": fout,
+                                   "ok_docs": fok, "ms": round(fms, 1), "MBps": round(sum(len(states[d]) for d in sample) / fms / 1e3, 1),
+                                   "us_per_byte_largest": round(fms * 1e3 / max(len(states[d]) for d in sample), 2),
+                                   "note": "normalize: every document snapshotted, encodeStateAsUpdate(applyUpdate(new Doc, merged)) "
+                                           "on the GPU: one thread per document, so the batch takes its largest document's time"},
            "parity": f"merge: bit-exact vs oracle on {checked} documents; snapshot: tests/test_snapshot.py::"
                      "test_gpu_snapshot_at_baseline_sizes (yjs 13.5.16 on the box)"}
     if not args.no_cpu_baseline and not args.no_yjs:
         k = min(n, 100)
         blk["cpu_baseline"] = {"merge": cpu_yjs("merge", {"arena": arena, "upd_off": upd_off, "doc_upd": doc_upd}, cpu_cores(args), k)}
-        cat = np.concatenate(states[:16])
-        doff = np.zeros(17, np.uint64)
-        doff[1:] = np.cumsum([len(x) for x in states[:16]])
-        blk["cpu_baseline"]["snapshot"] = cpu_yjs("snapshot", {"arena": cat, "doc_off": doff}, cpu_cores(args), 16)
+        ks = min(n, 64)
+        cat = np.concatenate(states[:ks])
+        doff = np.zeros(ks + 1, np.uint64)
+        doff[1:] = np.cumsum([len(x) for x in states[:ks]])
+        blk["cpu_baseline"]["snapshot"] = cpu_yjs("snapshot", {"arena": cat, "doc_off": doff}, cpu_cores(args), ks)
     e.close()
     return blk
 

@@ -56,9 +56,9 @@ class GpuMerge {
    *   bytes (`unnormalized`).  normalize: false stores the bare Y.mergeUpdates bytes.
    *   normalizeMaxBytes (default 32768): merged states larger than this are stored as the bare merge (counted in
    *   `sizeSkipped`): the snapshot kernel runs a document on ONE GPU thread (yjs's integration is a serial chain),
-   *   3-5 us per byte (18-31 for Tiptap documents of 10 000 clients), and a batch takes its largest document's time:
-   *   ~0.1-0.2 s at the limit, seconds for the ~1 MB documents of BASELINE config C5, whose merge takes
-   *   milliseconds (DESIGN.md 6.R6, tools/snap_probe.py).  Both forms load identically.
+   *   3-5 us per byte, and a batch takes its largest document's time: ~0.1-0.15 s at the limit, seconds for the ~1 MB
+   *   documents of BASELINE config C5, whose merge takes milliseconds (DESIGN.md 6.R6, tools/snap_probe.py).  Both
+   *   forms load identically.
    */
   constructor (configuration = {}) {
     this.extensionName = 'GpuMerge'

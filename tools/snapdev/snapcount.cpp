@@ -32,6 +32,7 @@ int main(int argc, char** argv) {
     d.dsin = (ygm::snap::Rng*)p; d.n_dsin = 0; d.cap_dsin = k.dsin; p += ygm::snap::al16((uint64_t)k.dsin * sizeof(ygm::snap::Rng));
     d.st = (int32_t*)p; d.cap_st = k.st; p += ygm::snap::al16(4ull * k.st);
     d.seq = (int32_t*)p; d.cap_seq = k.seq; p += ygm::snap::al16(4ull * k.seq);
+    d.ch = (int32_t*)p; d.ch_mask = k.hc - 1u; p += ygm::snap::al16(4ull * k.hc);
     d.out = p; d.cap_out = k.out;
     const uint32_t ol = d.run();
     printf("%d %u %u %u %u %u %u %u %u %u %u %u\n", d.err, len, S, D, C, d.n_it, d.n_pc, d.n_tx, d.n_ty, d.n_me, ol, d.epoch);

@@ -54,9 +54,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
-PMC_PROFILE = "r05_final/pmc.json"          # committed rocprofv3 PMC summary (FETCH_SIZE x2 + WRITE_SIZE per launch)
-PMC_C4 = "r05_final/pmc.json"              # ... of the SV / diff walker at C4
-PMC_BLOCKS = "r05_final/pmc_blocks.json"   # ... of whole blocks (--big, --block: every kernel of a step summed, tools/pmc_blocks.py)
+PMC_PROFILE = "r06_final/pmc.json"          # committed rocprofv3 PMC summary (FETCH_SIZE x2 + WRITE_SIZE per launch)
+PMC_C4 = "r06_final/pmc.json"              # ... of the SV / diff walker at C4
+PMC_BLOCKS = "r06_final/pmc_blocks.json"   # ... of whole blocks (--big, --block: every kernel of a step summed, tools/pmc_blocks.py)
 
 
 def parse():

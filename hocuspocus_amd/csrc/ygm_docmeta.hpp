@@ -21,7 +21,7 @@ struct DocMeta {                    // per-launch device counters (zeroed by the
   unsigned int wide_defer;          // documents sent from the wide lean kernel to the wave kernel
   unsigned int mid_defer;           // documents sent from the mid-size large-document kernel to the large size
   unsigned int big_started;         // 16-wave large-document workgroups started (k_big_wait)
-  unsigned int pad_;
+  unsigned int route_n;           // documents the big-tier routing pass leaves to the wave kernel
   unsigned long long big_scur;      // large-document kernel: struct-record entries carved
   unsigned long long fast_total;    // SV/diff: bytes of the packed (look-back placed) output
   unsigned long long cursor;        // merge: bytes in the overflow region (after the per-document slots)

@@ -58,6 +58,9 @@ int ygm_k_launch_merge_lean_wide(const uint8_t* arena, const uint64_t* upd_off, 
 int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
                             const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
                             int32_t* status, void* meta, uint32_t* defer_list, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
+int ygm_k_launch_route_big(const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, const unsigned int* n_dev, uint32_t n_docs,
+                           uint32_t flags, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, uint32_t* fb_list, uint32_t* rest,
+                           hipStream_t s);
 int ygm_k_launch_merge_fast(const uint8_t* arena, const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs,
                             const unsigned int* n_dev, uint32_t n_docs, uint32_t flags, uint8_t* out, uint64_t* out_off, uint64_t* out_len,
                             int32_t* status, uint64_t slot_total, void* meta, uint32_t* fb_list, uint64_t out_cap, hipStream_t s);
@@ -100,7 +103,7 @@ namespace {
 // mirrors ygm::DocMeta (ygm_docmeta.hpp) field for field; sizeof is a multiple of 16.  ygm_open checks the layout
 // against the kernels' own (ygm_k_meta_layout): read_meta and the counter memsets depend on it
 struct Meta {
-  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer, wide_defer, mid_defer, big_started, pad_;
+  unsigned int ticket, fault, fb_count, defer_count, lean_defer, big_defer, wide_defer, mid_defer, big_started, route_n;
   unsigned long long big_scur;
   unsigned long long fast_total, cursor, payload, fb_upds, fb_bytes, scr_upd_cursor, scr_byte_cursor, big_cursor;
   unsigned long long payload_sh[16 * 16];
@@ -167,7 +170,7 @@ struct ygm_ctx {
   // device inputs (host API staging)
   DevBuf arena, offs, docs, sv_arena, sv_offs;
   // device outputs + state
-  DevBuf out, out_off, out_len, status, lb, meta, fb_list, defer_list, defer2_list, defer_w_list;
+  DevBuf out, out_off, out_len, status, lb, meta, fb_list, defer_list, defer2_list, defer_w_list, route_list;
   Meta* h_meta = nullptr;  // pinned read-back of the per-launch counters
   int mslot = 0;           // counter slot of the next merge launch
   void* meta_slot(int i) const { return (uint8_t*)meta.p + (size_t)i * sizeof(Meta); }
@@ -266,7 +269,7 @@ void ygm_close(ygm_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
-                    &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
+                    &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->defer_w_list, &c->route_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
                     &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->big_scan, &c->big_up, &c->lens_off, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws, &c->sn_claim, &c->sn_pay,
                     &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr, &c->v21_cl})
     b->release();
@@ -292,7 +295,7 @@ static int prep_outputs(ygm_ctx* c, uint32_t n_docs, uint64_t out_cap, hipStream
   if (!c->out.ensure(out_cap + 64) || !c->out_off.ensure((size_t)n_docs * 8 + 8) || !c->out_len.ensure((size_t)n_docs * 8 + 8) ||
       !c->status.ensure((size_t)n_docs * 4 + 4) || !c->lb.ensure(tiles * 8) || !c->fb_list.ensure((size_t)n_docs * 4 + 4) ||
       !c->defer_list.ensure((size_t)n_docs * 4 + 4) || !c->defer2_list.ensure((size_t)n_docs * 4 + 4) ||
-      !c->defer_w_list.ensure((size_t)n_docs * 4 + 4))
+      !c->defer_w_list.ensure((size_t)n_docs * 4 + 4) || !c->route_list.ensure((size_t)n_docs * 4 + 4))
     return YGM_ENOMEM;
   if (lookback) {   // SV / diff: look-back tiles and counter slot 2 reset per call
     HIPCHK(hipMemsetAsync(c->lb.p, 0, tiles * 8, s));
@@ -396,12 +399,19 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
   // order; the host count is only the bound that sizes the persistent grid) -- one host wait for all three.
   const unsigned int* d_wide_defer = (const unsigned int*)((const char*)P.meta + offsetof(Meta, wide_defer));
   const unsigned int* d_defer_count = (const unsigned int*)((const char*)P.meta + offsetof(Meta, defer_count));
+  const unsigned int* d_route_n = (const unsigned int*)((const char*)P.meta + offsetof(Meta, route_n));
+  // the large-document tier's documents leave the chain before the wave kernel (k_route_big): the rest go on to it
+  auto route = [&](const uint32_t* list, const unsigned int* n_dev, uint32_t n) {
+    return ygm_k_launch_route_big(P.upd_off, P.doc_upd, list, n_dev, n, c->flags, c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(),
+                                  c->status.as<int32_t>(), P.meta, c->fb_list.as<uint32_t>(), c->route_list.as<uint32_t>(), s);
+  };
   uint32_t bound = 0;   // documents the chain may see (0: no chain)
   HIPCHK(hipEventRecord(c->e0, s));
   if (P.wide_route) {  // the wide kernel took the whole batch (async): its deferrals go on
     n_gen = bound = m.wide_defer;
     c->stats.docs_lean_wide += P.n_docs - m.wide_defer;
-    if (n_gen && ygm_k_launch_merge_wave(P.arena, P.upd_off, P.doc_upd, c->defer_w_list.as<uint32_t>(), nullptr, n_gen, c->flags,
+    if (n_gen && route(c->defer_w_list.as<uint32_t>(), nullptr, n_gen)) return YGM_EDEVICE;
+    if (n_gen && ygm_k_launch_merge_wave(P.arena, P.upd_off, P.doc_upd, c->route_list.as<uint32_t>(), d_route_n, n_gen, c->flags,
                                          c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
                                          P.meta, c->defer2_list.as<uint32_t>(), c->fb_list.as<uint32_t>(), P.out_cap, s))
       return YGM_EDEVICE;
@@ -414,8 +424,9 @@ int ygm_merge_v1_device_finish(ygm_ctx* c, ygm_device_result* out) {
                                      c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
                                      P.meta, nullptr, c->defer_w_list.as<uint32_t>(), P.out_cap, P.upd_len, s))
       return YGM_EDEVICE;
-    // tier 2: the general wave-per-document kernel over the lean kernels' deferred list
-    if (ygm_k_launch_merge_wave(P.arena, P.upd_off, P.doc_upd, c->defer_w_list.as<uint32_t>(), d_wide_defer, bound, c->flags,
+    // tier 2: the general wave-per-document kernel over the lean kernels' deferred list, after the routing pass
+    if (route(c->defer_w_list.as<uint32_t>(), d_wide_defer, bound)) return YGM_EDEVICE;
+    if (ygm_k_launch_merge_wave(P.arena, P.upd_off, P.doc_upd, c->route_list.as<uint32_t>(), d_route_n, bound, c->flags,
                                 c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
                                 P.meta, c->defer2_list.as<uint32_t>(), c->fb_list.as<uint32_t>(), P.out_cap, s))
       return YGM_EDEVICE;

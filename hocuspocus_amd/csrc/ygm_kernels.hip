@@ -838,6 +838,57 @@ __global__ __launch_bounds__(WAVE) void k_merge_wave(const uint8_t* __restrict__
   }
 }
 
+// The wave kernel's routing decision taken before it, one LANE per document: a [snapshot, ...log] document whose largest
+// update is BIG_ROUTE_MIN bytes or more goes to the large-document tier's list (fb_list, with the scratch-sizing sums),
+// every other document to `rest` (count meta->route_n), which k_merge_wave then takes.  Each list takes one atomic per
+// wave.  (In k_merge_wave the decision cost a wave and three atomics on three hot counters per document: C3's 100 000
+// documents spent ~2 ms there, none of them merged by it.)
+__global__ __launch_bounds__(256) void k_route_big(const uint64_t* __restrict__ upd_off, const uint32_t* __restrict__ doc_upd,
+                                                   const uint32_t* __restrict__ docs, const unsigned int* n_dev, uint32_t n_docs,
+                                                   uint32_t flags, uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len,
+                                                   int32_t* __restrict__ status, DocMeta* meta, uint32_t* __restrict__ fb_list,
+                                                   uint32_t* __restrict__ rest) {
+  const uint32_t N = n_dev ? *n_dev : n_docs;
+  const uint32_t l = threadIdx.x % WAVE;
+  for (uint32_t base = blockIdx.x * 256u; base < N; base += gridDim.x * 256u) {   // (block-uniform trip count)
+    const uint32_t i = base + threadIdx.x;
+    const bool in = i < N;
+    const uint32_t d = in ? docs[i] : 0u;
+    const uint32_t u0 = in ? doc_upd[d] : 0u, u1 = in ? doc_upd[d + 1] : 0u, k = u1 - u0;
+    // as merge_wave_doc: empty and one-update documents and the forced sequential mode stay with the wave kernel
+    const bool cand = in && k >= 2u && !(flags & 2u);
+    uint64_t mx = 0, prev = cand ? upd_off[u0] : 0ull;
+    for (uint32_t j = 1; j <= (cand ? k : 0u); j++) {
+      const uint64_t x = upd_off[u0 + j];
+      mx = x - prev > mx ? x - prev : mx;
+      prev = x;
+    }
+    const bool big = cand && mx >= (uint64_t)BIG_ROUTE_MIN;
+    const uint64_t bm = __ballot(big), rm = __ballot(in && !big);
+    const uint32_t lead = (uint32_t)__builtin_ctzll(bm | (1ull << 63));
+    uint32_t fb0 = 0, r0 = 0;
+    if (bm) {
+      const uint64_t nb = big ? upd_off[u1] - upd_off[u0] : 0ull;
+      const uint64_t su = wave_sum((uint64_t)(big ? k : 0u)), sb = wave_sum(nb);
+      if (l == lead) {
+        fb0 = atomicAdd(&meta->fb_count, (unsigned int)__popcll(bm));
+        atomicAdd(&meta->fb_upds, (unsigned long long)su);
+        atomicAdd(&meta->fb_bytes, (unsigned long long)sb);
+      }
+      fb0 = (uint32_t)__shfl((int)fb0, (int)lead);
+    }
+    if (rm) {
+      const uint32_t rl = (uint32_t)__builtin_ctzll(rm);
+      if (l == rl) r0 = atomicAdd(&meta->route_n, (unsigned int)__popcll(rm));
+      r0 = (uint32_t)__shfl((int)r0, (int)rl);
+    }
+    if (big) {
+      fb_list[fb0 + lanes_below(bm)] = d;
+      out_off[d] = merge_slot(upd_off[u0], d); out_len[d] = 0; status[d] = ST_FALLBACK;
+    } else if (in) rest[r0 + lanes_below(rm)] = d;
+  }
+}
+
 
 // ======================================================================= merge: lean fast path
 // Persistent waves (ygm_merge_lean.hpp): wave w takes documents w, w + G, w + 2G, ...
@@ -3505,6 +3556,16 @@ int ygm_k_launch_merge_wave(const uint8_t* arena, const uint64_t* upd_off, const
   const uint32_t grid = n_docs < resident ? n_docs : resident;
   hipLaunchKernelGGL(k_merge_wave, dim3(grid), dim3(WAVE), 0, s, arena, upd_off, doc_upd, docs, n_dev, n_docs,
                      flags, out, out_off, out_len, status, (DocMeta*)meta, defer_list, fb_list, out_cap);
+  return launch_rc(__func__);
+}
+
+int ygm_k_launch_route_big(const uint64_t* upd_off, const uint32_t* doc_upd, const uint32_t* docs, const unsigned int* n_dev, uint32_t n_docs,
+                           uint32_t flags, uint64_t* out_off, uint64_t* out_len, int32_t* status, void* meta, uint32_t* fb_list, uint32_t* rest,
+                           hipStream_t s) {
+  if (n_docs == 0) return 0;
+  const uint32_t grid = (n_docs + 255u) / 256u < 2048u ? (n_docs + 255u) / 256u : 2048u;   // (n_docs: the bound of the device count)
+  hipLaunchKernelGGL(k_route_big, dim3(grid), dim3(256), 0, s, upd_off, doc_upd, docs, n_dev, n_docs, flags, out_off, out_len, status,
+                     (DocMeta*)meta, fb_list, rest);
   return launch_rc(__func__);
 }
 

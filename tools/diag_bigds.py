@@ -35,3 +35,16 @@ for q in np.argsort(-tot)[:6]:
     r = t[q]
     print(f"wg {q}: total {us(r[5] - r[0])} us | log {us(r[1] - r[0])} U0 walk {us(r[2] - r[1])} sorts {us(r[3] - r[2])} | "
           f"pass0 blocks {us(r[6] - r[3])} ds {us(r[4] - r[6])} | pass1 blocks {us(r[7] - r[4])} ds {us(r[5] - r[7])}")
+# medians over every large-tier workgroup row written, and the delete-set plan counters (slots 21 / 22: documents
+# planned, documents on the spliced path)
+ok = t[:, 0] > 0
+if ok.any():
+    r = t[ok]
+    parts = {"log": r[:, 1] - r[:, 0], "U0 walk": r[:, 2] - r[:, 1], "sorts": r[:, 3] - r[:, 2], "pass0 blocks": r[:, 6] - r[:, 3],
+             "pass0 ds": r[:, 4] - r[:, 6], "pass1 blocks": r[:, 7] - r[:, 4], "pass1 ds": r[:, 5] - r[:, 7]}
+    print("rows", int(ok.sum()), "median us", {k: float(us(np.median(v))) for k, v in parts.items()},
+          "mean us", {k: float(us(np.mean(v))) for k, v in parts.items()})
+L.ygm_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+cnt = np.zeros(32, np.uint64)
+L.ygm_diag_read(cnt.ctypes.data, 0)
+print("ds plan: documents", int(cnt[21]), "spliced", int(cnt[22]))

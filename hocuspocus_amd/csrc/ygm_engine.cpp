@@ -37,7 +37,13 @@ int ygm_k_launch_cont(const uint8_t* st_arena, const uint64_t* st_off, const uin
                       int32_t* status, hipStream_t s);
 int ygm_k_launch_snap(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, const void* cnt, const uint64_t* ws_off,
                       uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, const uint8_t* claim,
-                      uint64_t base, hipStream_t s);
+                      uint64_t base, uint32_t* pend_list, unsigned int* pend_n, hipStream_t s);
+int ygm_k_launch_pend_plan(const uint32_t* list, uint32_t P, const uint8_t* ws, const uint64_t* out_off, uint64_t* upd_off, uint32_t* doc_upd,
+                           hipStream_t s);
+int ygm_k_launch_pend_copy(const uint32_t* list, uint32_t P, const uint8_t* ws, const uint64_t* out_off, const uint64_t* upd_off, uint8_t* dst,
+                           hipStream_t s);
+int ygm_k_launch_pend_fix(const uint32_t* list, uint32_t P, const uint64_t* m_off, const uint64_t* m_len, const int32_t* m_st, uint64_t tail,
+                          uint64_t* out_off, uint64_t* out_len, int32_t* status, hipStream_t s);
 int ygm_k_launch_pack(const uint8_t* src, const uint64_t* off, const uint64_t* len, const int32_t* status, uint32_t n, uint64_t* bsum,
                       uint8_t* dst, uint64_t* poff, hipStream_t s);
 int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
@@ -177,7 +183,9 @@ struct ygm_ctx {
   DevBuf s_readers, s_order, s_tmp, s_ubase, s_ulen, s_cnt, s_drec;
   DevBuf big_blk, big_rec, big_list, big_scan, big_up;   // large-document tier: block tables, struct records, documents sent on, scan
   DevBuf sv_tbl, sv_tn;                // diff: sorted state-vector tables (k_sv_table) and their entry counts
-  DevBuf sn_cnt, sn_off, sn_bs, sn_ws, sn_claim, sn_pay;  // snapshot: per-document counts, workspace offsets, scan scratch,
+  DevBuf sn_cnt, sn_off, sn_bs, sn_ws, sn_claim, sn_pay;
+  DevBuf sn_pend, pn_off, pn_du, pn_arena;   // snapshot: documents left pending, their three-update batch for the merge
+  ygm_ctx* pend_ctx = nullptr;               // ... merged on this child context (its own buffers and counters)  // snapshot: per-document counts, workspace offsets, scan scratch,
   // [LDS-tier output slots | workspaces], LDS-tier claims, its payload / claimed counters
   // update V2: per-update V1 sizes -> offsets, transcoding statuses, scan scratch, the V1 arena, per-document column
   // lengths, the V2 outputs (packed), their offsets / lengths / statuses
@@ -271,9 +279,10 @@ void ygm_close(ygm_ctx* c) {
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->defer_w_list, &c->route_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
                     &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->big_scan, &c->big_up, &c->lens_off, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws, &c->sn_claim, &c->sn_pay,
-                    &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr, &c->v21_cl})
+                    &c->sn_pend, &c->pn_off, &c->pn_du, &c->pn_arena, &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr, &c->v21_cl})
     b->release();
   for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
+  if (c->pend_ctx) ygm_close(c->pend_ctx);
   for (DevBuf* b : {&c->pk_data, &c->pk_off, &c->pk_bsum}) b->release();
   for (PinBuf* b : {&c->h_data, &c->h_off, &c->h_len, &c->h_status, &c->h_in}) b->release();
   for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
@@ -589,11 +598,45 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
   return YGM_OK;
 }
 
-int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
-                           void* stream, ygm_device_result* out) {
-  if (!c || !out) return YGM_EINVAL;
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  (void)hipSetDevice(c->device);
+// Documents k_snap left pending (ST_PEND: PendHdr, then [state, pendingDs, pending structs]): encodeStateAsUpdate
+// returns mergeUpdates of the three (Y@23300).  They are packed into one arena as three-update documents (k_pend_plan /
+// k_pend_copy) and merged by the merge kernels on the child context c->pend_ctx; the merged bytes are appended to the
+// snapshot's output region at `used` and the documents' offsets, lengths and statuses rewritten (k_pend_fix).
+static int snap_resolve_pending(ygm_ctx* c, hipStream_t s, uint32_t P, uint64_t used, uint64_t& data_bytes, unsigned long long& payload) {
+  if (!c->pn_off.ensure(8ull * (3ull * P + 1) + 16) || !c->pn_du.ensure(4ull * (P + 1) + 16)) return YGM_ENOMEM;
+  if (ygm_k_launch_pend_plan(c->sn_pend.as<uint32_t>(), P, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->pn_off.as<uint64_t>(),
+                             c->pn_du.as<uint32_t>(), s))
+    return YGM_EDEVICE;
+  uint64_t total = 0;
+  c->stats.host_syncs++;
+  HIPCHK(hipMemcpyAsync(c->h_meta, c->pn_off.as<uint64_t>() + 3ull * P, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  memcpy(&total, c->h_meta, 8);
+  if (!c->pn_arena.ensure(total + 64)) return YGM_ENOMEM;
+  HIPCHK(hipMemsetAsync(c->pn_arena.as<uint8_t>() + total, 0, 64, s));   // (the merge kernels' tail padding)
+  if (ygm_k_launch_pend_copy(c->sn_pend.as<uint32_t>(), P, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->pn_off.as<uint64_t>(),
+                             c->pn_arena.as<uint8_t>(), s))
+    return YGM_EDEVICE;
+  if (!c->pend_ctx) { const int e = ygm_open(c->device, c->flags, &c->pend_ctx); if (e) return e; }
+  int e = ygm_merge_v1_device_async(c->pend_ctx, c->pn_arena.as<uint8_t>(), total, c->pn_off.as<uint64_t>(), c->pn_du.as<uint32_t>(), 3 * P, P, s);
+  ygm_device_result r;
+  if (!e) e = ygm_merge_v1_device_finish(c->pend_ctx, &r);
+  if (e) return e;
+  if (!c->sn_ws.ensure(used + r.data_bytes + 64, used, s)) return YGM_ENOMEM;
+  if (r.data_bytes) HIPCHK(hipMemcpyAsync(c->sn_ws.as<uint8_t>() + used, r.data, r.data_bytes, hipMemcpyDeviceToDevice, s));
+  if (ygm_k_launch_pend_fix(c->sn_pend.as<uint32_t>(), P, r.off, r.len, r.status, used, c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(),
+                            c->status.as<int32_t>(), s))
+    return YGM_EDEVICE;
+  data_bytes = used + r.data_bytes;
+  payload += r.payload_bytes;
+  c->stats.docs_pending += P;
+  return YGM_OK;
+}
+
+// the snapshot batch; xf: YGM_F_SNAP_NOPEND (step2) / YGM_F_SNAP_STATE (contains) for states that leave pending parts
+static int snapshot_dev(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
+                        hipStream_t s, ygm_device_result* out, uint32_t xf) {
+  const uint32_t fl = c->flags | xf;
   const uint32_t nb = (n_docs + 1 + 255) / 256;
   if (!c->sn_cnt.ensure(16ull * n_docs + 16) || !c->sn_off.ensure(8ull * n_docs + 16) || !c->sn_bs.ensure(8ull * nb + 16) ||
       !c->out_off.ensure(8ull * n_docs + 8) || !c->out_len.ensure(8ull * n_docs + 8) || !c->status.ensure(4ull * n_docs + 4))
@@ -610,7 +653,7 @@ int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_by
     if (!c->sn_ws.ensure(slot_total + 64) || !c->sn_claim.ensure((size_t)n_docs + 16) || !c->sn_pay.ensure(16)) return YGM_ENOMEM;
     HIPCHK(hipMemsetAsync(c->sn_pay.p, 0, 16, s));
     for (int again = 0; again < 2 && lds_pay[1] < n_docs; again++) {   // 6 KiB per document, then 24 KiB for what it left
-      if (ygm_k_launch_snap_text(d_arena, d_doc_off, n_docs, c->flags, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(),
+      if (ygm_k_launch_snap_text(d_arena, d_doc_off, n_docs, fl, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(),
                                  c->status.as<int32_t>(), c->sn_claim.as<uint8_t>(), c->sn_pay.as<unsigned long long>(), again, slot_total, s))
         return YGM_EDEVICE;
       HIPCHK(hipMemcpyAsync(c->h_meta, c->sn_pay.p, 16, hipMemcpyDeviceToHost, s));
@@ -619,25 +662,29 @@ int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_by
     }
   }
   uint64_t total = 0;   // workspace bytes: one read of the scanned total
+  uint64_t total_out = 0;   // the output region's extent when pending documents' merged bytes follow the workspaces
   Meta m;
   memset(&m, 0, sizeof(m));
   if (!lds || lds_pay[1] < n_docs) {
     const uint8_t* claim = lds ? c->sn_claim.as<uint8_t>() : nullptr;
-    if (ygm_k_launch_snap_plan(d_arena, d_doc_off, n_docs, c->flags, c->sn_cnt.p, c->sn_off.as<uint64_t>(), c->sn_bs.as<uint64_t>(), claim, s))
+    if (ygm_k_launch_snap_plan(d_arena, d_doc_off, n_docs, fl, c->sn_cnt.p, c->sn_off.as<uint64_t>(), c->sn_bs.as<uint64_t>(), claim, s))
       return YGM_EDEVICE;
     if (n_docs) {
       HIPCHK(hipMemcpyAsync(c->h_meta, c->sn_off.as<uint64_t>() + n_docs, 8, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       memcpy(&total, c->h_meta, 8);
     }
-    if (!c->sn_ws.ensure(slot_total + total + 64, slot_total, s)) return YGM_ENOMEM;
-    if (ygm_k_launch_snap(d_arena, d_doc_off, n_docs, c->flags, c->sn_cnt.p, c->sn_off.as<uint64_t>(), c->sn_ws.as<uint8_t>(),
+    if (!c->sn_ws.ensure(slot_total + total + 64, slot_total, s) || !c->sn_pend.ensure(4ull * n_docs + 16)) return YGM_ENOMEM;
+    if (ygm_k_launch_snap(d_arena, d_doc_off, n_docs, fl, c->sn_cnt.p, c->sn_off.as<uint64_t>(), c->sn_ws.as<uint8_t>(),
                           c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(),
-                          (unsigned long long*)((uint8_t*)meta + offsetof(Meta, payload)), claim, slot_total, s))
+                          (unsigned long long*)((uint8_t*)meta + offsetof(Meta, payload)), claim, slot_total, c->sn_pend.as<uint32_t>(),
+                          (unsigned int*)((uint8_t*)meta + offsetof(Meta, fb_count)), s))
       return YGM_EDEVICE;
-    HIPCHK(hipEventRecord(c->e1, s));
     int e = read_meta(c, s, m, meta);
     if (e) return e;
+    if (m.fb_count && (e = snap_resolve_pending(c, s, m.fb_count, slot_total + total, total_out, m.payload))) return e;
+    HIPCHK(hipEventRecord(c->e1, s));
+    HIPCHK(hipEventSynchronize(c->e1));
   } else {
     HIPCHK(hipEventRecord(c->e1, s));
     HIPCHK(hipEventSynchronize(c->e1));
@@ -647,15 +694,53 @@ int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_by
   if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->stats.kernel_ms += ms;
   c->stats.calls++; c->stats.docs += n_docs; c->stats.bytes_in += arena_bytes; c->stats.bytes_out += m.payload;
   out->data = c->sn_ws.as<uint8_t>(); out->off = c->out_off.as<uint64_t>(); out->len = c->out_len.as<uint64_t>();
-  out->status = c->status.as<int32_t>(); out->data_bytes = slot_total + total; out->payload_bytes = m.payload;
+  out->status = c->status.as<int32_t>(); out->data_bytes = total_out ? total_out : slot_total + total; out->payload_bytes = m.payload;
+  return YGM_OK;
+}
+int ygm_snapshot_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
+                           void* stream, ygm_device_result* out) {
+  if (!c || !out) return YGM_EINVAL;
+  (void)hipSetDevice(c->device);
+  return snapshot_dev(c, d_arena, arena_bytes, d_doc_off, n_docs, stream ? (hipStream_t)stream : c->stream, out, 0);
+}
+// a snapshot batch's outputs packed into one arena on the device (k_pack_*: offsets n + 1, the total at [n]) with its
+// statuses, for kernels that read documents by offsets (step2's diff, contains)
+static int pack_snapshots(ygm_ctx* c, hipStream_t s, const ygm_device_result& r1, uint32_t n_docs) {
+  const uint32_t nb = (n_docs + 255) / 256;
+  if (!c->s2_data.ensure(r1.payload_bytes + 64) || !c->s2_off.ensure(8ull * n_docs + 16) || !c->s2_bsum.ensure(8ull * nb + 16) ||
+      !c->s2_st.ensure(4ull * n_docs + 4))
+    return YGM_ENOMEM;
+  HIPCHK(hipMemsetAsync((uint8_t*)c->s2_data.p + r1.payload_bytes, 0, 64, s));   // readable tail for the walker's chunks
+  if (n_docs) {
+    if (ygm_k_launch_pack(r1.data, r1.off, r1.len, r1.status, n_docs, c->s2_bsum.as<uint64_t>(), c->s2_data.as<uint8_t>(),
+                          c->s2_off.as<uint64_t>(), s))
+      return YGM_EDEVICE;
+    HIPCHK(hipMemcpyAsync(c->s2_off.as<uint64_t>() + n_docs, c->s2_bsum.as<uint64_t>() + nb, 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->s2_st.p, r1.status, 4ull * n_docs, hipMemcpyDeviceToDevice, s));
+  } else HIPCHK(hipMemsetAsync(c->s2_off.p, 0, 8, s));
   return YGM_OK;
 }
 
-int ygm_contains_v1_device(ygm_ctx* c, const uint8_t* d_states, const uint64_t* d_state_off, const uint8_t* d_updates,
+// Read-only SyncStep2: the states' Y.snapshot view first -- the snapshot batch with YGM_F_SNAP_STATE (a state that
+// leaves pending structs / a pending delete set is seen through its integrated part, as Y.snapshot(doc) sees the
+// store) -- packed, then the containment kernels over it; the snapshot's per-document refusals carried into the result
+int ygm_contains_v1_device(ygm_ctx* c, const uint8_t* d_states_in, const uint64_t* d_state_off_in, const uint8_t* d_updates,
                            const uint64_t* d_update_off, uint32_t n_docs, void* stream, ygm_device_result* out) {
   if (!c || !out) return YGM_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   (void)hipSetDevice(c->device);
+  uint64_t states_bytes = 0;
+  if (n_docs) {
+    c->stats.host_syncs++;
+    HIPCHK(hipMemcpyAsync(c->h_meta, d_state_off_in + n_docs, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    memcpy(&states_bytes, c->h_meta, 8);
+  }
+  ygm_device_result r1;
+  int e0 = snapshot_dev(c, d_states_in, states_bytes, d_state_off_in, n_docs, s, &r1, YGM_F_SNAP_STATE);
+  if (e0 || (e0 = pack_snapshots(c, s, r1, n_docs))) return e0;
+  const uint8_t* d_states = c->s2_data.as<uint8_t>();
+  const uint64_t* d_state_off = c->s2_off.as<uint64_t>();
   const uint32_t nb = (n_docs + 1 + 255) / 256;
   if (!c->sn_off.ensure(8ull * n_docs + 16) || !c->sn_bs.ensure(8ull * nb + 16) || !c->out.ensure((uint64_t)n_docs + 64) ||
       !c->out_off.ensure(8ull * n_docs + 8) || !c->out_len.ensure(8ull * n_docs + 8) || !c->status.ensure(4ull * n_docs + 4))
@@ -671,6 +756,8 @@ int ygm_contains_v1_device(ygm_ctx* c, const uint8_t* d_states, const uint64_t* 
   if (!c->sn_ws.ensure(total + 64)) return YGM_ENOMEM;
   if (ygm_k_launch_cont(d_states, d_state_off, d_updates, d_update_off, n_docs, c->flags, c->sn_off.as<uint64_t>(), c->sn_ws.as<uint8_t>(),
                         c->out.as<uint8_t>(), c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(), c->status.as<int32_t>(), s))
+    return YGM_EDEVICE;
+  if (n_docs && ygm_k_launch_v2_status(c->s2_st.as<int32_t>(), n_docs, c->status.as<int32_t>(), c->out_len.as<uint64_t>(), s))
     return YGM_EDEVICE;
   HIPCHK(hipEventRecord(c->e1, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -707,21 +794,11 @@ int ygm_sync_step2_v1_device(ygm_ctx* c, const uint8_t* d_states, uint64_t state
   ygm_device_result r1;
   const bool dbg = getenv("YGM_DEBUG") != nullptr;
 #define S2CHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { if (dbg) fprintf(stderr, "ygm step2: %s: %s\n", #x, hipGetErrorString(_e)); return YGM_EDEVICE; } } while (0)
-  int e = ygm_snapshot_v1_device(c, d_states, states_bytes, d_state_off, n_docs, s, &r1);
+  // (a state that leaves pending parts is EUNSUPPORTED here: encodeStateAsUpdate(doc, sv) diffs its pending structs
+  // without the parentSub bit the integrated ones keep -- the caller names it and keeps its own path)
+  int e = snapshot_dev(c, d_states, states_bytes, d_state_off, n_docs, s, &r1, YGM_F_SNAP_NOPEND);
   if (dbg) fprintf(stderr, "ygm step2: snapshot rc %d payload %llu\n", e, (unsigned long long)r1.payload_bytes);
-  if (e) return e;
-  const uint32_t nb = (n_docs + 255) / 256;
-  if (!c->s2_data.ensure(r1.payload_bytes + 64) || !c->s2_off.ensure(8ull * n_docs + 16) || !c->s2_bsum.ensure(8ull * nb + 16) ||
-      !c->s2_st.ensure(4ull * n_docs + 4))
-    return YGM_ENOMEM;
-  S2CHK(hipMemsetAsync((uint8_t*)c->s2_data.p + r1.payload_bytes, 0, 64, s));   // readable tail for the walker's chunks
-  if (n_docs) {
-    if (ygm_k_launch_pack(r1.data, r1.off, r1.len, r1.status, n_docs, c->s2_bsum.as<uint64_t>(), c->s2_data.as<uint8_t>(),
-                          c->s2_off.as<uint64_t>(), s))
-      return YGM_EDEVICE;
-    S2CHK(hipMemcpyAsync(c->s2_off.as<uint64_t>() + n_docs, c->s2_bsum.as<uint64_t>() + nb, 8, hipMemcpyDeviceToDevice, s));
-    S2CHK(hipMemcpyAsync(c->s2_st.p, r1.status, 4ull * n_docs, hipMemcpyDeviceToDevice, s));
-  }
+  if (e || (e = pack_snapshots(c, s, r1, n_docs))) return e;
   uint64_t sv_end = 0;
   if (n_docs && hipMemcpy(&sv_end, d_sv_off + n_docs, 8, hipMemcpyDeviceToHost) != hipSuccess) return YGM_EDEVICE;
   e = run_doc_kernel(c, 1, c->s2_data.as<uint8_t>(), r1.payload_bytes, c->s2_off.as<uint64_t>(), d_sv_arena, sv_end, d_sv_off, n_docs, s,
@@ -1133,6 +1210,7 @@ static int host_call(ygm_ctx* c, const HostCall& H, ygm_result* out) {
       c->stats.lean_ms += a.lean_ms - b.lean_ms; c->stats.lean_launches += a.lean_launches - b.lean_launches;
       c->stats.docs_big += a.docs_big - b.docs_big; c->stats.docs_lean_wide += a.docs_lean_wide - b.docs_lean_wide;
       c->stats.host_syncs += a.host_syncs - b.host_syncs;
+      c->stats.docs_pending += a.docs_pending - b.docs_pending;
     }
     int32_t* st = c->h_status.as<int32_t>();
     uint64_t* ln = c->h_len.as<uint64_t>();

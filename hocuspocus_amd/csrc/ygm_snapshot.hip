@@ -4,6 +4,8 @@
 //   k_snap_count : per document, the struct / delete-range / client-block counts -> workspace bytes
 //   k_snap_scan* : exclusive scan of the workspace sizes (three launches, 256 documents per block)
 //   k_snap       : per document, integrate + gc + merge + encode into its workspace's output region
+//   k_pend_*     : documents left pending (ST_PEND): their [state, pendingDs, pending structs] packed as three-update
+//                  documents for the merge kernels (plan, copy), then the merged bytes' places written back (fix)
 // A thread per document keeps the reference's sequential algorithm (YATA integration order matters)
 // while 64 documents share a wave; the workspace is per document, so nothing is shared.
 #include <hip/hip_runtime.h>
@@ -124,7 +126,8 @@ __global__ __launch_bounds__(SN_NT) void k_snap(const uint8_t* __restrict__ aren
                                                uint32_t flags, const uint4* __restrict__ cnt, const uint64_t* __restrict__ ws_off,
                                                uint8_t* __restrict__ ws, uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len,
                                                int32_t* __restrict__ status, unsigned long long* __restrict__ payload, uint32_t dpw,
-                                               const uint8_t* __restrict__ claim, uint64_t base) {
+                                               const uint8_t* __restrict__ claim, uint64_t base, uint32_t* __restrict__ pend_list,
+                                               unsigned int* __restrict__ pend_n) {
   // dpw documents per wave (lanes >= dpw idle): the per-document code diverges from lane to lane, so
   // fewer documents per wave trade SIMD lanes for less serialised divergence and more waves in flight
   __shared__ __attribute__((aligned(16))) uint8_t stg[SN_STAGE + 16];
@@ -144,12 +147,59 @@ __global__ __launch_bounds__(SN_NT) void k_snap(const uint8_t* __restrict__ aren
       st = snap::snapshot_doc(in, c.w, flags, ws + base + ws_off[d], k, oo, ol);
     }
     out_off[d] = base + ws_off[d] + oo;
-    out_len[d] = st == ST_OK ? ol : 0u;
+    out_len[d] = (st == ST_OK || st == snap::ST_PEND) ? ol : 0u;
     status[d] = st;
+    if (st == snap::ST_PEND) pend_list[atomicAdd(pend_n, 1u)] = d;   // (rare: one atomic per such document)
     mine = st == ST_OK ? ol : 0u;
   }
   mine = wave_sum(mine);
   if ((threadIdx.x & (WAVE - 1)) == 0 && mine) atomicAdd(payload, (unsigned long long)mine);
+}
+
+// ---- pending documents: [state, pendingDs, pending structs] (PendHdr) -> three-update documents for the merge kernels
+// plan (one workgroup): document j of the list gets updates 3j .. 3j + 2 at the exclusive prefix of the three lengths
+__global__ __launch_bounds__(1024) void k_pend_plan(const uint32_t* __restrict__ list, uint32_t P, const uint8_t* __restrict__ ws,
+                                                    const uint64_t* __restrict__ out_off, uint64_t* __restrict__ upd_off,
+                                                    uint32_t* __restrict__ doc_upd) {
+  __shared__ uint64_t tmp[1024 / WAVE + 1];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t j0 = 0; j0 < P; j0 += 1024) {
+    const uint32_t j = j0 + threadIdx.x;
+    uint32_t l0 = 0, l1 = 0, l2 = 0;
+    if (j < P) {
+      const uint8_t* h = ws + out_off[list[j]];   // PendHdr, read by bytes (the region's base need not be aligned)
+      auto u32at = [&](uint32_t o) { return (uint32_t)h[o] | ((uint32_t)h[o + 1] << 8) | ((uint32_t)h[o + 2] << 16) | ((uint32_t)h[o + 3] << 24); };
+      l0 = u32at(0); l1 = u32at(4); l2 = u32at(8);
+    }
+    uint64_t tot;
+    const uint64_t pre = carry + block_exscan<1024>(j < P ? (uint64_t)l0 + l1 + l2 : (uint64_t)0, tmp, tot);
+    if (j < P) { upd_off[3ull * j] = pre; upd_off[3ull * j + 1] = pre + l0; upd_off[3ull * j + 2] = pre + l0 + l1; doc_upd[j] = 3u * j; }
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { upd_off[3ull * P] = carry; doc_upd[P] = 3u * P; }
+}
+// copy (a workgroup per document): its three updates to their places in the packed arena
+__global__ __launch_bounds__(256) void k_pend_copy(const uint32_t* __restrict__ list, const uint8_t* __restrict__ ws,
+                                                   const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ upd_off,
+                                                   uint8_t* __restrict__ dst) {
+  const uint32_t j = blockIdx.x;
+  const uint8_t* src = ws + out_off[list[j]] + sizeof(snap::PendHdr);
+  const uint64_t a = upd_off[3ull * j], n = upd_off[3ull * j + 3] - a;
+  for (uint64_t i = threadIdx.x; i < n; i += 256) dst[a + i] = src[i];
+}
+// fix: the merged bytes were appended at `tail` of the output region: each document's place, length and status
+__global__ __launch_bounds__(256) void k_pend_fix(const uint32_t* __restrict__ list, uint32_t P, const uint64_t* __restrict__ m_off,
+                                                  const uint64_t* __restrict__ m_len, const int32_t* __restrict__ m_st, uint64_t tail,
+                                                  uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= P) return;
+  const uint32_t d = list[j];
+  const int32_t st = m_st[j];
+  out_off[d] = tail + m_off[j]; out_len[d] = st == ST_OK ? m_len[j] : 0u; status[d] = st;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -308,14 +358,31 @@ int ygm_k_launch_scan(uint64_t* v, uint32_t n, uint64_t* bs, hipStream_t s) {
 // phase 2: the snapshots (ws sized from ws_off[n_docs])
 int ygm_k_launch_snap(const uint8_t* arena, const uint64_t* doc_off, uint32_t n_docs, uint32_t flags, const void* cnt, const uint64_t* ws_off,
                       uint8_t* ws, uint64_t* out_off, uint64_t* out_len, int32_t* status, unsigned long long* payload, const uint8_t* claim,
-                      uint64_t base, hipStream_t s) {
+                      uint64_t base, uint32_t* pend_list, unsigned int* pend_n, hipStream_t s) {
   if (n_docs == 0) return 0;
   const char* env = getenv("YGM_SNAP_DPW");
   uint32_t dpw = env ? (uint32_t)atoi(env) : 16u;
   if (dpw < 1 || dpw > (uint32_t)SN_NT) dpw = 16u;
   const uint32_t g = (n_docs + dpw - 1) / dpw;
   hipLaunchKernelGGL(k_snap, dim3(g), dim3(SN_NT), 0, s, arena, doc_off, n_docs, flags, (const uint4*)cnt, ws_off, ws, out_off, out_len,
-                     status, payload, dpw, claim, base);
+                     status, payload, dpw, claim, base, pend_list, pend_n);
+  return snap_rc(__func__);
+}
+int ygm_k_launch_pend_plan(const uint32_t* list, uint32_t P, const uint8_t* ws, const uint64_t* out_off, uint64_t* upd_off, uint32_t* doc_upd,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_pend_plan, dim3(1), dim3(1024), 0, s, list, P, ws, out_off, upd_off, doc_upd);
+  return snap_rc(__func__);
+}
+int ygm_k_launch_pend_copy(const uint32_t* list, uint32_t P, const uint8_t* ws, const uint64_t* out_off, const uint64_t* upd_off, uint8_t* dst,
+                           hipStream_t s) {
+  if (P == 0) return 0;
+  hipLaunchKernelGGL(k_pend_copy, dim3(P), dim3(256), 0, s, list, ws, out_off, upd_off, dst);
+  return snap_rc(__func__);
+}
+int ygm_k_launch_pend_fix(const uint32_t* list, uint32_t P, const uint64_t* m_off, const uint64_t* m_len, const int32_t* m_st, uint64_t tail,
+                          uint64_t* out_off, uint64_t* out_len, int32_t* status, hipStream_t s) {
+  if (P == 0) return 0;
+  hipLaunchKernelGGL(k_pend_fix, dim3((P + 255) / 256), dim3(256), 0, s, list, P, m_off, m_len, m_st, tail, out_off, out_len, status);
   return snap_rc(__func__);
 }
 

@@ -18,10 +18,15 @@
 // parts), document lists through left/right item indices, a type table (root types by name,
 // nested types per ContentType item) with per-type key lists for map entries.
 //
-// Deviations and envelope: an update that leaves pending structs or a pending delete set (missing
-// dependencies, gaps, Skip structs followed by structs), repeats a client block, overlaps structs,
-// carries ContentDoc (sub-documents) or content with non-minimal varuints in a verbatim field, or
-// whose parent id names a non-type item, returns ST_UNSUP: the caller keeps its yjs path for it.
+// Pending structs and a pending delete set (missing dependencies, clock gaps, Skips followed by structs, ranges past
+// the state): integrateStructs' dependency stack is followed as the reference runs it, its quirks included (the rest
+// of a walled client is the slice from its refs cursor, a client met again on the stack keeps only that struct), and
+// readAndApplyDeleteSet keeps the ranges past the state.  encodeStateAsUpdate then returns
+// mergeUpdates([state, pendingDs, diffUpdate(pendingStructs.update)]) (Y@23300): the document's output is those three
+// updates (ST_PEND, the layout at pend_hdr) and the engine merges them with the merge kernels.
+// Envelope: an update that repeats a client block, overlaps structs, carries ContentDoc (sub-documents) or content
+// with non-minimal varuints in a verbatim field, or whose parent id names a non-type item, returns ST_UNSUP: the
+// caller keeps its yjs path for it.
 // After one transaction on a fresh document every struct is a merge candidate, so the reference's
 // three merge passes (delete-set ranges, afterState, _mergeStructs) reduce to one right-to-left
 // pass per client: mergeability is preserved along a merged run, so maximal runs are unique.
@@ -32,6 +37,12 @@ namespace ygm {
 namespace snap {
 
 constexpr int ST_UNSUP = 9;   // YGM_EUNSUPPORTED
+constexpr int ST_PEND = 64;   // internal: the output is [state, pendingDs, pending structs] for the merge kernels
+constexpr uint32_t F_SNAP_NOPEND = 8u;   // YGM_F_SNAP_NOPEND: a pending document is ST_UNSUP
+constexpr uint32_t F_SNAP_STATE = 16u;   // YGM_F_SNAP_STATE: a pending document's output is its integrated state
+// a pending document's output: this header, then the three V1 updates back to back (an absent one as the empty update)
+struct PendHdr { uint32_t len[3]; uint32_t magic; };
+constexpr uint32_t PEND_MAGIC = 0x444E4550u;
 
 enum : uint8_t { F_DEL = 1, F_HO = 2, F_HR = 4, F_INT = 8, F_GONE = 16 };
 enum : uint8_t { SK_ITEM = 0, SK_GC = 1, SK_SKIP = 2 };
@@ -57,7 +68,8 @@ struct SI {
 struct Piece { uint32_t off, end, cnt; int32_t next; uint8_t pre, post, pad0, pad1; };
 struct TypeRec { int32_t item; uint32_t name_off, name_len; int32_t start, map; };
 struct MapEnt { int32_t type; uint32_t key_off, key_len; int32_t item, next; };
-struct Cli { uint32_t id; int32_t r0, rn, ri; uint32_t state; int32_t ins, ni; };
+// rest0 / restn: the client's pending structs (refs [rest0, rest0 + restn)); gone: taken off integrateStructs' map
+struct Cli { uint32_t id; int32_t r0, rn, ri; uint32_t state; int32_t ins, ni, rest0, restn; uint32_t gone; };
 struct Rng { uint32_t client, clock, len, pad; };
 
 // workspace capacities of a document, from its counts (input structs S, delete-set ranges D, client
@@ -79,7 +91,8 @@ YDEV uint64_t al16(uint64_t x) { return (x + 15u) & ~15ull; }
 YDEV uint64_t ws_core_bytes(const Caps& k) {   // the workspace without its output region
   return al16((uint64_t)k.it * sizeof(SI)) + al16((uint64_t)k.pc * sizeof(Piece)) + al16((uint64_t)k.ty * sizeof(TypeRec)) +
          al16((uint64_t)k.me * sizeof(MapEnt)) + al16((uint64_t)k.cl * sizeof(Cli)) + al16((uint64_t)k.tx * sizeof(Rng)) +
-         al16((uint64_t)k.dsin * sizeof(Rng)) + al16(4ull * k.st) + al16(4ull * k.seq) + al16(4ull * k.hc);
+         al16((uint64_t)k.dsin * sizeof(Rng)) + al16((uint64_t)k.dsin * sizeof(Rng)) + al16(4ull * k.st) + al16(4ull * k.seq) +
+         al16(4ull * k.hc);
 }
 YDEV uint64_t ws_bytes(const Caps& k) { return ws_core_bytes(k) + al16(k.out); }
 // the encoder's writer: stores stop at cap (the caller's region), n counts on (> cap: the output did not fit)
@@ -119,11 +132,14 @@ struct Doc {
   int32_t* ch; uint32_t ch_mask;   // client id -> slot, open addressing (built once the table is sorted)
   Rng* tx; uint32_t n_tx, cap_tx;
   Rng* dsin; uint32_t n_dsin, cap_dsin;
+  Rng* pds; uint32_t n_pds;        // the pending delete set: ranges (or their parts) past the state, in input order
+  uint32_t n_rest;                 // clients with pending structs
   int32_t* st; uint32_t cap_st;
   int32_t* seq; uint32_t cap_seq;
   uint8_t* out; uint32_t cap_out;
   uint32_t epoch, n_ins;
   int err;
+  bool pend;   // the output is the pending layout (PendHdr)
 
   YDEV void fail(int e) { if (!err) err = e; }
 
@@ -217,7 +233,7 @@ struct Doc {
       if (c.err) break;
       if (client > 0xFFFFFFFFull || n_cl >= cap_cl) { fail(ST_UNSUP); return; }
       Cli& k = cl[n_cl++];
-      k.id = (uint32_t)client; k.r0 = (int32_t)n_it; k.rn = 0; k.ri = 0; k.state = 0; k.ins = -1; k.ni = 0;
+      k.id = (uint32_t)client; k.r0 = (int32_t)n_it; k.rn = 0; k.ri = 0; k.state = 0; k.ins = -1; k.ni = 0; k.rest0 = 0; k.restn = 0; k.gone = 0;
       for (uint64_t s = 0; s < ns && !c.err; s++) {
         SInfo si; read_struct_fast(c, si, flags);
         if (c.err) break;
@@ -500,58 +516,79 @@ struct Doc {
     }
   }
 
-  // integrateStructs (Y@21000): highest client first, a dependency stack; anything left pending -> ST_UNSUP
+  // integrateStructs (Y@21000 Me): highest client first, a dependency stack.  A struct past its client's state (a gap)
+  // or one whose dependency's client has no refs left walls the stack: every struct on it goes to the pending set
+  // (addStackToRestSS): a client still on the map gives the slice of its refs from its cursor (one back) and leaves the
+  // map; a client already off it gives that one struct (replacing what it gave before).  Skips are passed over.
+  YDEV void rest_stack(uint32_t& sp, int32_t* stk) {
+    for (uint32_t i = 0; i < sp; i++) {
+      const int32_t t = stk[i];
+      const int32_t k = cli_slot(it[t].client);
+      if (!cl[k].gone) {
+        cl[k].ri--;
+        cl[k].rest0 = cl[k].r0 + cl[k].ri; cl[k].restn = cl[k].rn - cl[k].ri;
+        cl[k].gone = 1; cl[k].ri = cl[k].rn;   // (refs emptied: its cursor at the end)
+      } else { cl[k].rest0 = t; cl[k].restn = 1; }
+    }
+    sp = 0;
+  }
   YDEV void integrate_all() {
     for (uint32_t k = 0; k < n_cl; k++) cl[k].ri = 0;
     int32_t ci = (int32_t)n_cl - 1;   // current client (ascending table, taken from the end)
     auto next_client = [&]() -> int32_t {
-      while (ci >= 0 && cl[ci].ri >= cl[ci].rn) ci--;
+      while (ci >= 0 && (cl[ci].gone || cl[ci].ri >= cl[ci].rn)) ci--;
       return ci;
     };
     int32_t cur = next_client();
     if (cur < 0) return;
     int32_t u = cl[cur].r0 + cl[cur].ri++;
-    uint32_t sp = 0;   // the reference's stack `s`, in st[] above the delete stack's use (separate pass)
+    uint32_t sp = 0;   // the reference's stack `s`
     int32_t* stk = seq;   // (seq is free until the merge pass)
     for (;;) {
       if (err) return;
       if (it[u].kind != SK_SKIP) {
         const int32_t k = cli_slot(it[u].client);
         const int64_t diff = (int64_t)cl[k].state - (int64_t)it[u].clock;
-        if (diff < 0) { fail(ST_UNSUP); return; }   // a gap: pending structs
-        const int64_t m = get_missing(u);
-        if (err) return;
-        if (m >= 0) {
+        if (diff < 0) {   // a gap: the struct and the stack go pending
           if (sp >= cap_seq) { fail(ST_NOMEM); return; }
           stk[sp++] = u;
-          const int32_t mk = cli_slot((uint32_t)m);
-          if (mk < 0 || cl[mk].ri >= cl[mk].rn) { fail(ST_UNSUP); return; }   // the dependency is not in the update
-          u = cl[mk].r0 + cl[mk].ri++;
-          continue;
+          rest_stack(sp, stk);
+        } else {
+          const int64_t m = get_missing(u);
+          if (err) return;
+          if (m >= 0) {
+            if (sp >= cap_seq) { fail(ST_NOMEM); return; }
+            stk[sp++] = u;
+            const int32_t mk = cli_slot((uint32_t)m);
+            if (mk < 0 || cl[mk].gone || cl[mk].ri >= cl[mk].rn) rest_stack(sp, stk);   // the dependency is not in the update
+            else { u = cl[mk].r0 + cl[mk].ri++; continue; }
+          } else if (diff == 0) integrate(u);
+          else if (diff < (int64_t)it[u].len) { fail(ST_UNSUP); return; }   // overlapping structs (integrate with an offset)
+          // (else: every clock of it is integrated already)
         }
-        if (diff == 0) integrate(u);
-        else { fail(ST_UNSUP); return; }   // overlapping / repeated structs
-      } else {
-        // a Skip: structs after it in the same block would be pending
-        const int32_t k = cli_slot(it[u].client);
-        if (cl[k].ri < cl[k].rn) { fail(ST_UNSUP); return; }
       }
       if (sp) u = stk[--sp];
-      else if (cur >= 0 && cl[cur].ri < cl[cur].rn) u = cl[cur].r0 + cl[cur].ri++;
+      else if (cur >= 0 && !cl[cur].gone && cl[cur].ri < cl[cur].rn) u = cl[cur].r0 + cl[cur].ri++;
       else {
         cur = next_client();
         if (cur < 0) break;
         u = cl[cur].r0 + cl[cur].ri++;
       }
     }
+    for (uint32_t k = 0; k < n_cl; k++) n_rest += cl[k].restn > 0 ? 1u : 0u;
   }
 
+  YDEV void pds_add(uint32_t client, uint32_t clock, uint32_t len) {   // addToDeleteSet on the pending set (one per input range)
+    Rng& r = pds[n_pds++];
+    r.client = client; r.clock = clock; r.len = len; r.pad = 0;
+  }
   // readAndApplyDeleteSet (Y@11500): split at range ends, delete; ranges past the state are pending
   YDEV void apply_ds() {
     for (uint32_t r = 0; r < n_dsin && !err; r++) {
       const uint32_t client = dsin[r].client, a = dsin[r].clock, b = dsin[r].clock + dsin[r].len;
       const uint32_t s = state_of(client);
-      if (!(a < s) || s < b) { fail(ST_UNSUP); return; }
+      if (!(a < s)) { pds_add(client, a, b - a); continue; }   // past the state: pending
+      if (s < b) pds_add(client, s, b - s);                    // its part past the state: pending
       int32_t x = find(client, a);
       if (x < 0) return;
       if (!deleted(x) && it[x].clock < a) { split(x, a - it[x].clock); x = it[x].nxt; }
@@ -649,9 +686,12 @@ struct Doc {
     if (ho) { o.vu(u.oc); o.vu(u.ok); }
     if (hr) { o.vu(u.rc); o.vu(u.rk); }
     if (!ho && !hr) {
-      const TypeRec& t = ty[u.parent];
-      if (t.item < 0) { o.b(1); o.vu(t.name_len); w(o, t.name_off, t.name_len); }
-      else { o.b(0); o.vu(it[t.item].client); o.vu(it[t.item].clock); }
+      if (u.parent == P_ID) { o.b(0); o.vu(u.pc); o.vu(u.pk); }   // (a pending item: its parent id as read)
+      else {
+        const TypeRec& t = ty[u.parent];
+        if (t.item < 0) { o.b(1); o.vu(t.name_len); w(o, t.name_off, t.name_len); }
+        else { o.b(0); o.vu(it[t.item].client); o.vu(it[t.item].clock); }
+      }
       if (hs) { o.vu((uint32_t)u.sub_len); w(o, u.sub_off, (uint32_t)u.sub_len); }
     }
     switch (u.ref) {
@@ -675,8 +715,7 @@ struct Doc {
       default: w(o, u.c_start, u.c_end - u.c_start);   // Binary / Embed / Format / Type: as read (canonical)
     }
   }
-  YDEV uint32_t encode() {
-    OutCap o{out, 0, cap_out};
+  YDEV void encode_state(OutCap& o) {
     uint32_t nc = 0;
     for (uint32_t k = 0; k < n_cl; k++) nc += cl[k].ni > 0 ? 1u : 0u;
     o.vu(nc);
@@ -685,7 +724,7 @@ struct Doc {
       const uint32_t m = client_seq(kk);
       o.vu(m); o.vu(cl[kk].id); o.vu(it[seq[0]].clock);
       for (uint32_t i = 0; i < m; i++) write_item(o, seq[i]);
-      if (o.n + 64u > cap_out) { fail(ST_NOMEM); return 0; }
+      if (o.n + 64u > o.cap) { fail(ST_NOMEM); return; }
     }
     // delete set from the struct store (createDeleteSetFromStructStore, Y@10600): store insertion order
     // (13.5 writeDeleteSet keeps the Map order; 13.6 sorts clients descending)
@@ -712,10 +751,76 @@ struct Doc {
         while (i < m && deleted(seq[i])) len += it[seq[i++]].len;
         o.vu(c0); o.vu(len);
       }
-      if (o.n + 64u > cap_out) { fail(ST_NOMEM); return 0; }
+      if (o.n + 64u > o.cap) { fail(ST_NOMEM); return; }
     }
-    if (o.n > cap_out) { fail(ST_NOMEM); return 0; }
-    return o.n;
+  }
+  // the pending delete set as encodeStateAsUpdate merges it (pendingDs converted to V1): no structs, then the ranges
+  // by client in first-seen order (addToDeleteSet's Map), each client's in input order
+  YDEV void encode_pds(OutCap& o) {
+    o.vu(0);
+    if (n_pds > 4096u) { fail(ST_UNSUP); return; }   // (the first-seen grouping below is quadratic)
+    auto first = [&](uint32_t i) { for (uint32_t j = 0; j < i; j++) if (pds[j].client == pds[i].client) return false; return true; };
+    uint32_t nc = 0;
+    for (uint32_t i = 0; i < n_pds; i++) nc += first(i) ? 1u : 0u;
+    o.vu(nc);
+    for (uint32_t i = 0; i < n_pds; i++) {
+      if (!first(i)) continue;
+      uint32_t cnt = 0;
+      for (uint32_t j = i; j < n_pds; j++) cnt += pds[j].client == pds[i].client ? 1u : 0u;
+      o.vu(pds[i].client); o.vu(cnt);
+      for (uint32_t j = i; j < n_pds; j++) if (pds[j].client == pds[i].client) { o.vu(pds[j].clock); o.vu(pds[j].len); }
+    }
+  }
+  // the pending structs as encodeStateAsUpdate merges them: diffUpdate(pendingStructs.update, [0]) converted to V1 --
+  // clients descending (writeClientsStructs), a client's leading Skips dropped (diffUpdate), every struct as written
+  // by Item.write at offset 0 from what was read (never integrated: origins, parent id / key as read), no delete set
+  YDEV void encode_rest(OutCap& o) {
+    auto lead = [&](uint32_t k) {   // the client's first pending struct that is not a Skip (rest0 + restn: none)
+      int32_t x = cl[k].rest0;
+      while (x < cl[k].rest0 + cl[k].restn && it[x].kind == SK_SKIP) x++;
+      return x;
+    };
+    uint32_t nc = 0;
+    for (uint32_t k = 0; k < n_cl; k++) nc += (cl[k].restn && lead(k) < cl[k].rest0 + cl[k].restn) ? 1u : 0u;
+    o.vu(nc);
+    for (uint32_t kk = n_cl; kk-- > 0;) {
+      if (!cl[kk].restn) continue;
+      const int32_t x0 = lead(kk), x1 = cl[kk].rest0 + cl[kk].restn;
+      if (x0 >= x1) continue;
+      o.vu((uint32_t)(x1 - x0)); o.vu(cl[kk].id); o.vu(it[x0].clock);
+      for (int32_t x = x0; x < x1; x++) {
+        if (it[x].kind == SK_SKIP) { o.b(10); o.vu(it[x].len); }
+        else write_item(o, x);
+      }
+      if (o.n + 64u > o.cap) { fail(ST_NOMEM); return; }
+    }
+    o.vu(0);
+  }
+  YDEV uint32_t encode() {
+    if ((n_rest || n_pds) && (flags & F_SNAP_NOPEND)) { fail(ST_UNSUP); return 0; }
+    if ((!n_rest && !n_pds) || (flags & F_SNAP_STATE)) {
+      OutCap o{out, 0, cap_out};
+      encode_state(o);
+      if (err) return 0;
+      if (o.n > cap_out) { fail(ST_NOMEM); return 0; }
+      return o.n;
+    }
+    // pending: PendHdr, then the state, the pending delete set and the pending structs (each the empty update if absent)
+    if (cap_out < sizeof(PendHdr) + 64u) { fail(ST_NOMEM); return 0; }
+    PendHdr h;
+    OutCap o{out + sizeof(PendHdr), 0, cap_out - (uint32_t)sizeof(PendHdr)};
+    encode_state(o); h.len[0] = o.n;
+    if (n_pds) encode_pds(o); else { o.b(0); o.b(0); }
+    h.len[1] = o.n - h.len[0];
+    if (n_rest) encode_rest(o); else { o.b(0); o.b(0); }
+    h.len[2] = o.n - h.len[0] - h.len[1];
+    if (err) return 0;
+    if (o.n > o.cap) { fail(ST_NOMEM); return 0; }
+    h.magic = PEND_MAGIC;
+    const uint8_t* hb = (const uint8_t*)&h;
+    for (uint32_t i = 0; i < sizeof(PendHdr); i++) out[i] = hb[i];
+    pend = true;
+    return (uint32_t)sizeof(PendHdr) + o.n;
   }
 
   YDEV uint32_t run() {
@@ -733,7 +838,8 @@ YDEV_NI int snapshot_run(const uint8_t* in, uint32_t n, uint32_t flags, uint8_t*
                          uint32_t& out_len) {
   Doc D;
   uint8_t* p = ws;
-  D.in = in; D.n = n; D.flags = flags; D.err = 0; D.epoch = 0; D.n_ins = 0; D.hint_id = 0; D.hint_k = -1;
+  D.in = in; D.n = n; D.flags = flags; D.err = 0; D.epoch = 0; D.n_ins = 0; D.hint_id = 0; D.hint_k = -1; D.pend = false;
+  D.n_pds = 0; D.n_rest = 0;
   D.it = (SI*)p; D.n_it = 0; D.cap_it = k.it; p += al16((uint64_t)k.it * sizeof(SI));
   D.pc = (Piece*)p; D.n_pc = 0; D.cap_pc = k.pc; p += al16((uint64_t)k.pc * sizeof(Piece));
   D.ty = (TypeRec*)p; D.n_ty = 0; D.cap_ty = k.ty; p += al16((uint64_t)k.ty * sizeof(TypeRec));
@@ -741,12 +847,13 @@ YDEV_NI int snapshot_run(const uint8_t* in, uint32_t n, uint32_t flags, uint8_t*
   D.cl = (Cli*)p; D.n_cl = 0; D.cap_cl = k.cl; p += al16((uint64_t)k.cl * sizeof(Cli));
   D.tx = (Rng*)p; D.n_tx = 0; D.cap_tx = k.tx; p += al16((uint64_t)k.tx * sizeof(Rng));
   D.dsin = (Rng*)p; D.n_dsin = 0; D.cap_dsin = k.dsin; p += al16((uint64_t)k.dsin * sizeof(Rng));
+  D.pds = (Rng*)p; p += al16((uint64_t)k.dsin * sizeof(Rng));
   D.st = (int32_t*)p; D.cap_st = k.st; p += al16(4ull * k.st);
   D.seq = (int32_t*)p; D.cap_seq = k.seq; p += al16(4ull * k.seq);
   D.ch = (int32_t*)p; D.ch_mask = k.hc - 1u;
   D.out = out; D.cap_out = out_cap;
   out_len = D.run();
-  return D.err;
+  return D.err ? D.err : D.pend ? ST_PEND : 0;
 }
 // document d's workspace from caps_of, its output region at the end
 YDEV int snapshot_doc(const uint8_t* in, uint32_t n, uint32_t flags, uint8_t* ws, const Caps& k, uint32_t& out_off, uint32_t& out_len) {

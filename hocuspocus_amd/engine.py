@@ -56,7 +56,8 @@ class Stats(ctypes.Structure):
                 ("d2h_ms", ctypes.c_double),
                 ("docs_lean", ctypes.c_uint64), ("lean_ms", ctypes.c_double),
                 ("lean_launches", ctypes.c_uint64), ("docs_big", ctypes.c_uint64),
-                ("docs_lean_wide", ctypes.c_uint64), ("host_syncs", ctypes.c_uint64)]
+                ("docs_lean_wide", ctypes.c_uint64), ("host_syncs", ctypes.c_uint64),
+                ("docs_pending", ctypes.c_uint64)]
 
 
 _lib = None

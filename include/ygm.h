@@ -55,6 +55,10 @@ extern "C" {
 #define YGM_F_COMPAT_135 1u   /* delete-set clients in first-seen order; lone surrogate -> error */
 #define YGM_F_FORCE_SEQ 2u    /* route every merge through the exact sequential kernel (testing) */
 #define YGM_F_KEEP_SUB 4u     /* internal to ygm_sync_step2_v1: diffs keep each struct's parentSub bit (0x20) */
+#define YGM_F_SNAP_NOPEND 8u  /* internal to ygm_sync_step2_v1: a state that leaves pending structs / delete set is
+                                 EUNSUPPORTED (encodeStateAsUpdate(doc, sv) diffs its pending part by other rules) */
+#define YGM_F_SNAP_STATE 16u  /* internal to ygm_contains_v1: such a state's snapshot is its integrated part alone
+                                 (Y.snapshot(doc): the store's state vector and delete set) */
 
 typedef struct ygm_ctx ygm_ctx;
 
@@ -93,6 +97,8 @@ typedef struct {
                                           tiers, snapshot workspace sizing, ...): one per call for a batch the lean
                                           kernels finish, two when the general tiers are needed, more for the
                                           large-document and sequential tiers */
+  uint64_t docs_pending;               /* snapshots of updates that leave pending structs / a pending delete set
+                                          (finished by merging [state, pendingDs, pending structs] on the GPU) */
 } ygm_stats_t;
 
 /* Opens the engine on HIP device `device` (one context per GPU; contexts are

@@ -224,7 +224,7 @@ static napi_value js_stats(napi_env env, napi_callback_info info) {
   NAPI_CALL(env, napi_create_object(env, &o));
 #define SETN(name, val) NAPI_CALL(env, napi_create_double(env, (double)(val), &v)); NAPI_CALL(env, napi_set_named_property(env, o, name, v));
   SETN("calls", s.calls) SETN("docs", s.docs) SETN("updates", s.updates) SETN("bytesIn", s.bytes_in) SETN("bytesOut", s.bytes_out)
-  SETN("docsFast", s.docs_fast) SETN("docsSeq", s.docs_seq) SETN("kernelMs", s.kernel_ms) SETN("h2dMs", s.h2d_ms) SETN("d2hMs", s.d2h_ms) SETN("docsLean", s.docs_lean) SETN("leanMs", s.lean_ms) SETN("leanLaunches", s.lean_launches) SETN("docsBig", s.docs_big) SETN("docsLeanWide", s.docs_lean_wide) SETN("hostSyncs", s.host_syncs)
+  SETN("docsFast", s.docs_fast) SETN("docsSeq", s.docs_seq) SETN("kernelMs", s.kernel_ms) SETN("h2dMs", s.h2d_ms) SETN("d2hMs", s.d2h_ms) SETN("docsLean", s.docs_lean) SETN("leanMs", s.lean_ms) SETN("leanLaunches", s.lean_launches) SETN("docsBig", s.docs_big) SETN("docsLeanWide", s.docs_lean_wide) SETN("hostSyncs", s.host_syncs) SETN("docsPending", s.docs_pending)
 #undef SETN
   return o;
 }

@@ -193,9 +193,9 @@ function syncStatusFrame (documentName, saved) {
 /**
  * Read-only connections (MessageReceiver.ts:156-179): a SyncStep2 from a read-only client is not
  * applied; the server acks SyncStatus(true) when Y.snapshotContainsUpdate(Y.snapshot(doc), update)
- * (nothing new) and SyncStatus(false) otherwise.  Batched: the documents' states merged and
- * snapshot-normalized on the GPU (the snapshot's delete set is the document's), then one GPU
- * containment batch.  Returns per message the SyncStatus frame, null for other messages, or an Error.
+ * (nothing new) and SyncStatus(false) otherwise.  Batched: the documents' states merged on the GPU, then
+ * one GPU containment batch (which normalizes the states to their Y.snapshot view itself).  Returns per
+ * message the SyncStatus frame, null for other messages, or an Error.
  */
 SyncResponder.prototype.answerReadOnlyMany = async function (messages) {
   const out = new Array(messages.length).fill(null)
@@ -211,37 +211,34 @@ SyncResponder.prototype.answerReadOnlyMany = async function (messages) {
   const fetched = await Promise.all(names.map(n => this.getState(n)))
   const parts = fetched.map(f => Array.isArray(f) ? f.filter(Boolean) : (f ? [f] : []))
   const merged = await this._merge(names, parts.map(p => p.length ? p : [new Uint8Array([0, 0])]))
-  // a document whose merge the engine refuses answers with that Error; only healthy states go on
-  const snapOf = new Map()
-  const ok = []
-  names.forEach((n, k) => { if (merged[k] instanceof Error) snapOf.set(n, merged[k]); else ok.push(k) })
-  const snaps = ok.length
-    ? await (this._pooled() ? this.engine.snapshotMany(ok.map(k => names[k]), ok.map(k => merged[k])) : this.engine.snapshotMany(ok.map(k => merged[k])))
-    : []
-  ok.forEach((k, j) => snapOf.set(names[k], snaps[j]))
-  // a state outside the snapshot kernel's envelope (pending structs or delete set, sub-documents: EUNSUPPORTED,
-  // a per-document refusal) is answered as the reference does (MessageReceiver.ts:157-179) on the host: the
-  // document loaded from the merged state, Y.snapshotContainsUpdate(Y.snapshot(doc), update) (yjs 13.6; with a
-  // yjs that lacks it, the same algorithm over Y.decodeUpdate: snapshotContains below)
-  const unsup = a => { const s = snapOf.get(a.documentName); return s instanceof Error && s.code === 'EUNSUPPORTED' }
   const mergedOf = new Map(names.map((n, k) => [n, merged[k]]))
-  for (const a of asks.filter(unsup)) {
-    const Y = this._Y()
-    const doc = new Y.Doc()
-    Y.applyUpdate(doc, mergedOf.get(a.documentName))
-    const snap = Y.snapshot(doc)
-    const yes = typeof Y.snapshotContainsUpdate === 'function' ? Y.snapshotContainsUpdate(snap, a.payload) : snapshotContains(Y, snap, a.payload)
-    out[a.i] = syncStatusFrame(a.documentName, yes)
-  }
-  const stateOf = a => snapOf.get(a.documentName)
-  const live = asks.filter(a => !(snapOf.get(a.documentName) instanceof Error))
-  asks.filter(a => snapOf.get(a.documentName) instanceof Error && !unsup(a)).forEach(a => { out[a.i] = snapOf.get(a.documentName) })
+  // a document whose merge the engine refuses answers with that Error; the other states go to one containment batch as
+  // merged: the engine takes their Y.snapshot view itself (the snapshot kernels; for a state that leaves pending
+  // structs or a pending delete set, its integrated part -- what Y.snapshot(doc) sees in the store)
+  asks.filter(a => mergedOf.get(a.documentName) instanceof Error).forEach(a => { out[a.i] = mergedOf.get(a.documentName) })
+  const live = asks.filter(a => !(mergedOf.get(a.documentName) instanceof Error))
   if (!live.length) return out
+  const stateOf = a => mergedOf.get(a.documentName)
   const res = await (this._pooled()
     ? this.engine.containsMany(live.map(a => a.documentName), live.map(stateOf), live.map(a => a.payload))
     : this.engine.containsMany(live.map(stateOf), live.map(a => a.payload)))
-  live.forEach((a, k) => { out[a.i] = res[k] instanceof Error ? res[k] : syncStatusFrame(a.documentName, res[k]) })
+  live.forEach((a, k) => {
+    const r = res[k]
+    if (r instanceof Error && r.code === 'EUNSUPPORTED') {
+      // a state outside the snapshot kernel's envelope (sub-documents, repeated client blocks) is answered as the
+      // reference does (MessageReceiver.ts:157-179) on the host: the document loaded from the merged state,
+      // Y.snapshotContainsUpdate(Y.snapshot(doc), update) (yjs 13.6; with a yjs that lacks it, the same algorithm:
+      // snapshotContains above)
+      const Y = this._Y()
+      const doc = new Y.Doc()
+      Y.applyUpdate(doc, stateOf(a))
+      const snap = Y.snapshot(doc)
+      const yes = typeof Y.snapshotContainsUpdate === 'function' ? Y.snapshotContainsUpdate(snap, a.payload) : snapshotContains(Y, snap, a.payload)
+      out[a.i] = syncStatusFrame(a.documentName, yes)
+      this.unnormalized.push(a.documentName)
+    } else out[a.i] = r instanceof Error ? r : syncStatusFrame(a.documentName, r)
+  })
   return out
 }
 
-module.exports = { SyncResponder, decodeSyncMessage, frame, syncStatusFrame, MessageType, SyncStep }
+module.exports = { SyncResponder, decodeSyncMessage, frame, syncStatusFrame, snapshotContains, MessageType, SyncStep }

@@ -332,14 +332,120 @@ def test_gpu_snapshot_lds_tier_equals_general(monkeypatch):
 
 @pytest.mark.gpu
 def test_gpu_snapshot_envelope():
-    """Pending structs (a gap) and a missing origin are refused, not guessed; an empty update is malformed (yjs throws)."""
+    """A gap and a missing origin leave pending structs: yjs 13.5.16 answers with the structs themselves (its bytes,
+    computed by the bundle: node -e ... Y.encodeStateAsUpdate(applyUpdate(new Doc, u))); an empty update is malformed
+    (yjs throws); a sub-document is outside the envelope."""
     from hocuspocus_amd import Engine
-    from hocuspocus_amd.engine import EUNSUPPORTED, EMALFORMED
-    with Engine(0) as e:
+    from hocuspocus_amd.engine import EMALFORMED
+    with Engine(0, compat135=True) as e:
         gap = bytes([1, 1, 5, 3, 0x04, 1, 1, 0x74, 1, 0x61, 0])   # client 5 starts at clock 3: pending
         orphan = bytes([1, 1, 5, 0, 0x84, 9, 0, 1, 0x61, 0])   # origin (9, 0) is not in the update
         res = e.snapshot_batch([gap, orphan, b""])
-        assert res[0][0] == EUNSUPPORTED and res[1][0] == EUNSUPPORTED and res[2][0] == EMALFORMED
+        assert res[0] == (0, bytes.fromhex("0101050304010174016100"))
+        assert res[1] == (0, bytes.fromhex("01010500840900016100"))
+        assert res[2][0] == EMALFORMED
+
+
+# ---------------------------------------------------------------------------------------- pending structs / delete set
+# tests/golden/snapshot_pending_v135.json.gz: the generator's sessions with 1-3 of the log's updates lost
+# (tools/snap_fixture.py 200:31:120:pending 120:32:200:textpending): applyUpdate leaves pending structs and / or a
+# pending delete set, and encodeStateAsUpdate merges [state, pendingDs, pending structs] (Y@23300).
+PFIX = os.path.join(ROOT, "tests", "golden", "snapshot_pending_v135.json.gz")
+
+
+def pending_fixtures():
+    d = json.load(gzip.open(PFIX, "rt"))
+    return [(bytes.fromhex(u), bytes.fromhex(e)) for u, e in d["rows"]]
+
+
+def test_pending_fixtures_present():
+    rows = pending_fixtures()
+    assert len(rows) == 320 and all(u and e for u, e in rows)
+
+
+@pytest.mark.skipif(not (NODE and BUNDLE), reason="node + the yjs bundle are needed to regenerate")
+def test_pending_fixtures_regenerate(tmp_path):
+    """The committed vectors are what the generator's pending mode produces from the bundle (first sessions)."""
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "exp.bin")
+    subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_corpus.js"), "30", "31", a, b, "120", "pending"], check=True, timeout=120)
+    rows = pending_fixtures()[:30]
+    assert read_in(a) == [u for u, _ in rows]
+    assert [e for _, e in read_res(b)] == [e for _, e in rows]
+
+
+def _resolve_pending(st, body, compat135):
+    """A host-compiled kernel result: status 64 (snap::ST_PEND) carries PendHdr + [state, pendingDs, pending structs],
+    which the engine merges with the merge kernels -- here the oracle's mergeUpdates does that step."""
+    import oracle
+    if st != 64:
+        return st, body
+    ln = struct.unpack_from("<IIII", body, 0)
+    assert ln[3] == 0x444E4550
+    parts, p = [], 16
+    for k in range(3):
+        parts.append(body[p:p + ln[k]])
+        p += ln[k]
+    return oracle.merge_updates(parts, compat135=compat135)
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
+@pytest.mark.parametrize("mode", [1, 0])
+def test_pending_kernel_code_on_host(tmp_path, mode):
+    """The kernel's code host-compiled over the pending vectors: most documents come out pending (the dependency
+    stack's rest and the delete set past the state), and merging their three updates gives yjs's bytes (13.5) / the
+    client-descending delete sets (default)."""
+    from golden import ds_to_desc
+    exe = str(tmp_path / "snapdev")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", exe, os.path.join(ROOT, "tools", "snapdev", "snapdev.cpp")], check=True, timeout=300)
+    rows = pending_fixtures()
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
+    write_in(a, [u for u, _ in rows])
+    subprocess.run([exe, a, b, str(mode)], check=True, timeout=120)
+    got = read_res(b)
+    assert sum(st == 64 for st, _ in got) >= 200
+    exp = [(0, e) if mode else (0, bytes.fromhex(ds_to_desc(e.hex()))) for _, e in rows]
+    res = [_resolve_pending(st, body, bool(mode)) for st, body in got]
+    bad = [k for k in range(len(rows)) if res[k] != exp[k]]
+    assert not bad, f"{len(bad)} documents differ, first {bad[:5]}"
+
+
+@pytest.mark.gpu
+def test_gpu_snapshot_pending_vs_yjs_fixtures(eng135):
+    """On the GPU (13.5): the pending documents' three updates merged by the merge kernels give yjs's bytes."""
+    rows = pending_fixtures()
+    s0 = eng135.stats()
+    res = eng135.snapshot_batch([u for u, _ in rows])
+    bad = [k for k, ((_, e), r) in enumerate(zip(rows, res)) if r != (0, e)]
+    assert not bad, f"{len(bad)} documents differ from yjs, first {bad[:5]}: {res[bad[0]]}"
+    assert eng135.stats().docs_pending - s0.docs_pending >= 200
+
+
+@pytest.mark.gpu
+def test_gpu_snapshot_pending_default_mode():
+    """The same in the 13.6 default mode, against client-descending delete sets; mixed with complete documents."""
+    from golden import ds_to_desc
+    from hocuspocus_amd import Engine
+    rows = pending_fixtures() + fixtures()[:100]
+    with Engine(0) as e:
+        res = e.snapshot_batch([u for u, _ in rows])
+    exp = [(0, bytes.fromhex(ds_to_desc(x.hex()))) for _, x in rows]
+    bad = [k for k in range(len(rows)) if res[k] != exp[k]]
+    assert not bad, f"{len(bad)} documents differ, first {bad[:5]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not (NODE and BUNDLE), reason="node + the yjs bundle (image) needed for live sessions")
+def test_gpu_snapshot_pending_live_yjs(eng135, tmp_path):
+    """Fresh pending sessions generated on this box by yjs (both generator shapes, longer sessions)."""
+    batch, exp = [], []
+    for seed, ops, mode in ((41, 200, "pending"), (42, 400, "textpending")):
+        a, b = str(tmp_path / f"in{seed}.bin"), str(tmp_path / f"exp{seed}.bin")
+        subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_corpus.js"), "150", str(seed), a, b, str(ops), mode], check=True, timeout=240)
+        batch += read_in(a)
+        exp += [e for _, e in read_res(b)]
+    res = eng135.snapshot_batch(batch)
+    bad = [k for k in range(len(batch)) if res[k] != (0, exp[k])]
+    assert not bad, f"{len(bad)} documents differ, first {bad[:5]}"
 
 
 # ---------------------------------------------------------------------------------------- read-only SyncStep2
@@ -381,3 +487,47 @@ def test_gpu_contains_vs_live_yjs(tmp_path):
         res2 = e.contains_batch([s for _, s in snaps], up)
     assert res == [(0, bool(x)) for x in ex]
     assert res2 == res
+
+
+# pending states (tools/snap_fixture.py --contains 120 51 pending): the stored state is the merge of a history with
+# lost updates -- its document keeps pending structs / a pending delete set, and Y.snapshot(doc) sees the store alone
+PCFIX = os.path.join(ROOT, "tests", "golden", "contains_pending_v135.json.gz")
+
+
+def contains_pending_fixtures():
+    d = json.load(gzip.open(PCFIX, "rt"))
+    states = [bytes.fromhex(s) for s in d["states"]]
+    return [(states[i], bytes.fromhex(u), bool(e)) for i, u, e in d["rows"]]
+
+
+def test_contains_pending_fixtures_present():
+    rows = contains_pending_fixtures()
+    assert len(rows) > 300 and 0 < sum(e for _, _, e in rows) < len(rows)
+
+
+@pytest.mark.gpu
+def test_gpu_contains_pending_states_vs_yjs():
+    """Read-only SyncStep2 against states that leave pending parts: the containment runs on the state's Y.snapshot
+    view (its integrated part), on the GPU, with no host yjs; in both modes, mixed with complete states."""
+    from hocuspocus_amd import Engine
+    rows = contains_pending_fixtures() + contains_fixtures()[:100]
+    for compat in (True, False):
+        with Engine(0, compat135=compat) as e:
+            res = e.contains_batch([s for s, _, _ in rows], [u for _, u, _ in rows])
+        assert res == [(0, x) for _, _, x in rows]
+
+
+@pytest.mark.gpu
+def test_gpu_step2_refuses_pending_states():
+    """SyncStep2 of a state that leaves pending parts stays EUNSUPPORTED (encodeStateAsUpdate(doc, sv) diffs the
+    pending structs without the parentSub bit the integrated ones keep); complete states beside them are answered."""
+    from hocuspocus_amd import Engine
+    from hocuspocus_amd.engine import EUNSUPPORTED
+    pend = [u for u, _ in pending_fixtures()[:40]]
+    full = [u for u, _ in fixtures()[:20]]
+    with Engine(0, compat135=True) as e:
+        snaps = e.snapshot_batch(pend)
+        res = e.sync_step2_batch(pend + full, [b"\x00"] * 60)
+    assert all(st == 0 for st, _ in snaps)
+    assert any(r[0] == EUNSUPPORTED for r in res[:40]) and all(r[0] in (0, EUNSUPPORTED) for r in res[:40])
+    assert all(r[0] == 0 for r in res[40:])

@@ -8,7 +8,11 @@
 // Expected answer: Y.equalSnapshots(Y.snapshot(doc), Y.snapshot(doc after applying the update)) -- the
 // meaning of yjs 13.6 snapshotContainsUpdate for updates that apply completely (no Skips, no pending
 // structs or delete ranges), which is all this corpus makes; 13.6 itself is not in the image.
-//   node tools/contains_corpus.js <n> <seed> <states.bin> <updates.bin> <expect.bin>
+// pending: the sessions lose 1-3 updates (snap_corpus.js pending mode) and the state handed to the GPU is their merge
+// `u` itself, whose loaded document keeps pending structs / a pending delete set.  Y.snapshot(doc) sees the store
+// alone, so the expected answers are taken on the document of its integrated part A (encodeStateAsUpdate with the
+// pending parts cleared), whose updates here all apply completely.
+//   node tools/contains_corpus.js <n> <seed> <states.bin> <updates.bin> <expect.bin> [pending]
 const fs = require('fs')
 const path = require('path')
 const Y = require(path.join(__dirname, 'yjs_bundle.js')).load()
@@ -24,12 +28,15 @@ function writeBlobs (file, arr) {
 const n = parseInt(process.argv[2] || '100', 10)
 const seed = parseInt(process.argv[3] || '1', 10)
 const R = rng(seed * 7919 + 1)
+const pending = process.argv[7] === 'pending'
 const states = []; const updates = []; const expect = []
 for (let i = 0; i < n; i++) {
-  const [u] = session(seed * 100003 + i, 50)
+  const [u0] = session(seed * 100003 + i, pending ? 80 : 50, pending)
   const doc = new Y.Doc()
-  Y.applyUpdate(doc, u)
+  Y.applyUpdate(doc, u0)
+  if (pending) { doc.store.pendingStructs = null; doc.store.pendingDs = null }
   const state = Y.encodeStateAsUpdate(doc)
+  const u = pending ? state : u0   // (the document the expectations are taken on)
   const snap = Y.snapshot(doc)
   const cand = []
   // parts of the history: the whole state, and its diff against a random earlier state vector
@@ -50,7 +57,7 @@ for (let i = 0; i < n; i++) {
     const probe = new Y.Doc()
     Y.applyUpdate(probe, u)
     Y.applyUpdate(probe, c)
-    states.push(state); updates.push(c)
+    states.push(pending ? u0 : state); updates.push(c)
     expect.push(Y.equalSnapshots(snap, Y.snapshot(probe)) ? 1 : 0)
   }
 }

@@ -8,7 +8,9 @@
 //   expected = Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), u))  (what extension-database stores)
 // Writes `out.bin` (u32 n, then (u32 len, u) per session) and `exp.bin` (i32 status 0, u32 len, bytes),
 // the formats tools/snapdev and tests read.
-//   node tools/snap_corpus.js <n> <seed> <out.bin> <exp.bin> [maxOps] [text]
+//   node tools/snap_corpus.js <n> <seed> <out.bin> <exp.bin> [maxOps] [text|pending|textpending]
+// pending: the same sessions with 1-3 of the log's updates lost (out-of-order delivery: later updates depend on the
+// missing ones) -- u merges what is left, so Y.applyUpdate leaves pending structs and / or a pending delete set
 const fs = require('fs')
 const path = require('path')
 const Y = require(path.join(__dirname, 'yjs_bundle.js')).load()
@@ -23,7 +25,17 @@ const ALPH = ['a', 'b', 'c', 'd', 'e', ' ', 'Ã©', 'ÃŸ', 'â‚¬', 'ä¸­', 'ðŸ˜€', 'ð
 // text: flat Y.Text sessions only -- ASCII inserts of 1-8 characters (in the middle of earlier runs too) and
 // deletions over 1-4 peers that sync now and then (concurrent inserts at one position, splits by origins and by
 // delete ranges): the envelope of the flat-text snapshot kernel (ygm_snap_text.hpp)
-function textSession (seed, maxOps) {
+// drop 1-3 random updates of the log (pending mode), from a stream of its own (the sessions stay the same)
+function dropSome (log, seed) {
+  if (log.length < 2) return log
+  const R = rng(seed * 2246822519 + 99)
+  const out = log.slice()
+  const k = 1 + Math.floor(R() * Math.min(3, out.length - 1))
+  for (let i = 0; i < k; i++) out.splice(Math.floor(R() * out.length), 1)
+  return out
+}
+
+function textSession (seed, maxOps, drop) {
   const R = rng(seed * 2654435761 + 777)
   const ri = n => Math.floor(R() * n)
   const nPeers = 1 + ri(4)
@@ -50,13 +62,14 @@ function textSession (seed, maxOps) {
       else { let s = ''; const k = 1 + ri(R() < 0.7 ? 2 : 8); for (let i = 0; i < k; i++) s += 'abcdefgh xyz'[ri(12)]; t.insert(ri(t.length + 1), s) }
     })
   }
-  const u = log.length ? Y.mergeUpdates(log) : Y.encodeStateAsUpdate(new Y.Doc())
+  const kept = drop ? dropSome(log, seed) : log
+  const u = kept.length ? Y.mergeUpdates(kept) : Y.encodeStateAsUpdate(new Y.Doc())
   const fresh = new Y.Doc()
   Y.applyUpdate(fresh, u)
   return [u, Y.encodeStateAsUpdate(fresh)]
 }
 
-function session (seed, maxOps) {
+function session (seed, maxOps, drop) {
   const R = rng(seed * 2654435761 + 12345)
   const ri = n => Math.floor(R() * n)
   const nPeers = 1 + ri(3)
@@ -130,7 +143,8 @@ function session (seed, maxOps) {
       }
     })
   }
-  const u = log.length ? Y.mergeUpdates(log) : Y.encodeStateAsUpdate(new Y.Doc())
+  const kept = drop ? dropSome(log, seed) : log
+  const u = kept.length ? Y.mergeUpdates(kept) : Y.encodeStateAsUpdate(new Y.Doc())
   const fresh = new Y.Doc()
   Y.applyUpdate(fresh, u)
   return [u, Y.encodeStateAsUpdate(fresh)]
@@ -149,9 +163,11 @@ if (require.main === module) {
   const n = parseInt(process.argv[2] || '100', 10)
   const seed = parseInt(process.argv[3] || '1', 10)
   const maxOps = parseInt(process.argv[6] || '60', 10)
-  const gen = process.argv[7] === 'text' ? textSession : session
+  const mode = process.argv[7] || ''
+  const gen = mode === 'text' || mode === 'textpending' ? textSession : session
+  const drop = mode === 'pending' || mode === 'textpending'
   const us = []; const ex = []
-  for (let i = 0; i < n; i++) { const [u, e] = gen(seed * 100003 + i, maxOps); us.push(u); ex.push(e) }
+  for (let i = 0; i < n; i++) { const [u, e] = gen(seed * 100003 + i, maxOps, drop); us.push(u); ex.push(e) }
   write(process.argv[4], us, false)
   const eb = [Buffer.from(new Uint32Array([ex.length]).buffer)]
   for (const b of ex) eb.push(Buffer.from(new Int32Array([0]).buffer), Buffer.from(new Uint32Array([b.length]).buffer), Buffer.from(b))

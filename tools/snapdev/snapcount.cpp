@@ -30,6 +30,7 @@ int main(int argc, char** argv) {
     d.cl = (ygm::snap::Cli*)p; d.n_cl = 0; d.cap_cl = k.cl; p += ygm::snap::al16((uint64_t)k.cl * sizeof(ygm::snap::Cli));
     d.tx = (ygm::snap::Rng*)p; d.n_tx = 0; d.cap_tx = k.tx; p += ygm::snap::al16((uint64_t)k.tx * sizeof(ygm::snap::Rng));
     d.dsin = (ygm::snap::Rng*)p; d.n_dsin = 0; d.cap_dsin = k.dsin; p += ygm::snap::al16((uint64_t)k.dsin * sizeof(ygm::snap::Rng));
+    d.pds = (ygm::snap::Rng*)p; d.n_pds = 0; d.n_rest = 0; d.pend = false; p += ygm::snap::al16((uint64_t)k.dsin * sizeof(ygm::snap::Rng));
     d.st = (int32_t*)p; d.cap_st = k.st; p += ygm::snap::al16(4ull * k.st);
     d.seq = (int32_t*)p; d.cap_seq = k.seq; p += ygm::snap::al16(4ull * k.seq);
     d.ch = (int32_t*)p; d.ch_mask = k.hc - 1u; p += ygm::snap::al16(4ull * k.hc);

@@ -1,7 +1,7 @@
 // Development harness (tooling, never shipped): runs the device snapshot code (ygm_snapshot.hpp) on the
 // host over a file of updates, so the kernel's logic can be iterated against the yjs bundle in the
 // build container.  Input: u32 count, then (u32 len, bytes) per update.  Output: (i32 status, u32 len,
-// bytes) per update.
+// bytes) per update; a document left pending (status 64) writes its PendHdr and three updates.
 #define YGM_HOST_BUILD 1
 #include <cstdio>
 #include <cstdlib>
@@ -23,7 +23,7 @@ int main(int argc, char** argv) {
     ws.assign(ygm::snap::ws_bytes(k) + 64, 0);
     uint32_t oo = 0, ol = 0;
     const int st = ygm::snap::snapshot_doc(u.data(), len, flags, ws.data(), k, oo, ol);
-    const int32_t s32 = st; const uint32_t l32 = st ? 0u : ol;
+    const int32_t s32 = st; const uint32_t l32 = (st == 0 || st == ygm::snap::ST_PEND) ? ol : 0u;   // (ST_PEND: PendHdr + three updates)
     fwrite(&s32, 4, 1, g); fwrite(&l32, 4, 1, g);
     if (l32) fwrite(ws.data() + oo, 1, l32, g);
   }

@@ -45,9 +45,9 @@ extern "C" {
 #define YGM_ENOMEM 6
 #define YGM_EDEVICE 7      /* HIP error / device fault */
 #define YGM_EINVAL 8       /* bad call arguments */
-#define YGM_EUNSUPPORTED 9 /* ygm_snapshot_v1 only: the update leaves pending structs or a pending delete set
-                              (missing dependencies), repeats or overlaps structs, or carries sub-documents --
-                              the caller keeps its yjs path for that document */
+#define YGM_EUNSUPPORTED 9 /* snapshot / step2 / contains only: the update repeats or overlaps structs or carries
+                              sub-documents (ygm_sync_step2_v1: or leaves pending structs / a pending delete set)
+                              -- the caller keeps its yjs path for that document */
 
 #define YGM_MAX_DEPTH 32
 
@@ -124,12 +124,15 @@ int ygm_sv_from_update_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *do
  * -- the bytes extension-database stores (packages/extension-database/src/Database.ts:55-60,
  * Y.encodeStateAsUpdate of the live document): YATA-integrated, deleted content garbage-collected,
  * adjacent structs merged (yjs Y@20500-32900 readUpdate / cleanupTransactions, Y@23300
- * encodeStateAsUpdate).  One update per document (e.g. the output of ygm_merge_v1).  Documents
- * outside the envelope carry YGM_EUNSUPPORTED. */
+ * encodeStateAsUpdate).  One update per document (e.g. the output of ygm_merge_v1).  An update whose
+ * document keeps pending structs / a pending delete set (lost or out-of-order updates) gives yjs's bytes
+ * too: mergeUpdates([state, pendingDs, pending structs]) (Y@23300), run by the merge kernels.  Documents
+ * outside the envelope (sub-documents, repeated / overlapping structs) carry YGM_EUNSUPPORTED. */
 int ygm_snapshot_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, uint32_t n_docs, ygm_result *out);
 /* Read-only SyncStep2: Y.snapshotContainsUpdate(Y.snapshot(doc), update) per document
  * (packages/server/src/MessageReceiver.ts:156-179; yjs 13.6 snapshotContainsUpdate).  states: each
- * document's doc-normalized state (ygm_snapshot_v1 output, whose delete set is the snapshot's);
+ * document's state (any update: its Y.snapshot view -- the store's integrated part, without pending structs or
+ * a pending delete set -- is taken by the snapshot kernels first; a ygm_snapshot_v1 output is its own view);
  * updates: the received update per document.  Document d's output is one byte, 1 = contained (the
  * server acks with SyncStatus true), 0 = new content (SyncStatus false). */
 int ygm_contains_v1(ygm_ctx *ctx, const uint8_t *states, const uint64_t *state_off, const uint8_t *updates,
@@ -139,8 +142,9 @@ int ygm_contains_v1(ygm_ctx *ctx, const uint8_t *states, const uint64_t *state_o
  * document loaded from stored bytes (extension-database Database.ts:44-50).  Computed as the doc-normalized
  * snapshot of `state` (ygm_snapshot_v1) followed by diffUpdate(snapshot, sv) in which every struct keeps its
  * parentSub bit (Item.write of an integrated item, yjs Y@80416).  states / state_off as ygm_snapshot_v1;
- * sv_arena / sv_off one encoded state vector per document.  A document outside the snapshot envelope carries
- * YGM_EUNSUPPORTED (the caller names it and keeps its yjs path). */
+ * sv_arena / sv_off one encoded state vector per document.  A document outside the snapshot envelope, or whose
+ * state leaves pending parts (encodeStateAsUpdate(doc, sv) diffs pending structs without the parentSub bit the
+ * integrated ones keep), carries YGM_EUNSUPPORTED (the caller names it and keeps its yjs path). */
 int ygm_sync_step2_v1(ygm_ctx *ctx, const uint8_t *states, const uint64_t *state_off, const uint8_t *sv_arena,
                       const uint64_t *sv_off, uint32_t n_docs, ygm_result *out);
 

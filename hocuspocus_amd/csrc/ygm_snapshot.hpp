@@ -24,9 +24,10 @@
 // readAndApplyDeleteSet keeps the ranges past the state.  encodeStateAsUpdate then returns
 // mergeUpdates([state, pendingDs, diffUpdate(pendingStructs.update)]) (Y@23300): the document's output is those three
 // updates (ST_PEND, the layout at pend_hdr) and the engine merges them with the merge kernels.
-// Envelope: an update that repeats a client block, overlaps structs, carries ContentDoc (sub-documents) or content
-// with non-minimal varuints in a verbatim field, or whose parent id names a non-type item, returns ST_UNSUP: the
-// caller keeps its yjs path for it.
+// Sub-documents (ContentDoc, one clock, never split) integrate like any other content; their options are written as
+// read when canonical (ContentDoc's constructor rebuilds them: read_struct's check), refused (ST_NONCANON) if not.
+// Envelope: an update that repeats a client block, overlaps structs, carries content with non-minimal varuints in a
+// verbatim field, or whose parent id names a non-type item, returns ST_UNSUP: the caller keeps its yjs path for it.
 // After one transaction on a fresh document every struct is a merge candidate, so the reference's
 // three merge passes (delete-set ranges, afterState, _mergeStructs) reduce to one right-to-left
 // pass per client: mergeability is preserved along a merged run, so maximal runs are unique.
@@ -248,7 +249,6 @@ struct Doc {
         x.ref = si.ref;
         if (x.kind == SK_ITEM) {
           if (si.nc) { fail(ST_NONCANON); return; }
-          if (x.ref == 9) { fail(ST_UNSUP); return; }   // sub-documents
           Cur h{in, si.start + 1, si.cstart, 0, 0};
           const uint8_t info = si.info;
           if (info & 0x80) { x.oc = (uint32_t)h.vu(); x.ok = (uint32_t)h.vu(); x.flags |= F_HO; }

@@ -45,8 +45,9 @@ extern "C" {
 #define YGM_ENOMEM 6
 #define YGM_EDEVICE 7      /* HIP error / device fault */
 #define YGM_EINVAL 8       /* bad call arguments */
-#define YGM_EUNSUPPORTED 9 /* snapshot / step2 / contains only: the update repeats or overlaps structs or carries
-                              sub-documents (ygm_sync_step2_v1: or leaves pending structs / a pending delete set)
+#define YGM_EUNSUPPORTED 9 /* snapshot / step2 / contains only: the update repeats a client block or overlaps
+                              structs (yjs's writers never do), or names a non-type item as a parent
+                              (ygm_sync_step2_v1: or leaves pending structs / a pending delete set)
                               -- the caller keeps its yjs path for that document */
 
 #define YGM_MAX_DEPTH 32
@@ -126,8 +127,9 @@ int ygm_sv_from_update_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *do
  * adjacent structs merged (yjs Y@20500-32900 readUpdate / cleanupTransactions, Y@23300
  * encodeStateAsUpdate).  One update per document (e.g. the output of ygm_merge_v1).  An update whose
  * document keeps pending structs / a pending delete set (lost or out-of-order updates) gives yjs's bytes
- * too: mergeUpdates([state, pendingDs, pending structs]) (Y@23300), run by the merge kernels.  Documents
- * outside the envelope (sub-documents, repeated / overlapping structs) carry YGM_EUNSUPPORTED. */
+ * too: mergeUpdates([state, pendingDs, pending structs]) (Y@23300), run by the merge kernels.  Sub-documents
+ * (ContentDoc) are integrated like any one-clock content.  Documents outside the envelope (repeated client
+ * blocks, overlapping structs) carry YGM_EUNSUPPORTED. */
 int ygm_snapshot_v1(ygm_ctx *ctx, const uint8_t *arena, const uint64_t *doc_off, uint32_t n_docs, ygm_result *out);
 /* Read-only SyncStep2: Y.snapshotContainsUpdate(Y.snapshot(doc), update) per document
  * (packages/server/src/MessageReceiver.ts:156-179; yjs 13.6 snapshotContainsUpdate).  states: each

@@ -334,7 +334,7 @@ def test_gpu_snapshot_lds_tier_equals_general(monkeypatch):
 def test_gpu_snapshot_envelope():
     """A gap and a missing origin leave pending structs: yjs 13.5.16 answers with the structs themselves (its bytes,
     computed by the bundle: node -e ... Y.encodeStateAsUpdate(applyUpdate(new Doc, u))); an empty update is malformed
-    (yjs throws); a sub-document is outside the envelope."""
+    (yjs throws)."""
     from hocuspocus_amd import Engine
     from hocuspocus_amd.engine import EMALFORMED
     with Engine(0, compat135=True) as e:
@@ -407,6 +407,56 @@ def test_pending_kernel_code_on_host(tmp_path, mode):
     res = [_resolve_pending(st, body, bool(mode)) for st, body in got]
     bad = [k for k in range(len(rows)) if res[k] != exp[k]]
     assert not bad, f"{len(bad)} documents differ, first {bad[:5]}"
+
+
+# sub-documents (ContentDoc: Y.Doc values in a map and an array, overwritten and deleted ones among them), complete and
+# with lost updates (tools/snap_fixture.py 160:61:120:subdoc 100:62:120:subpending)
+SFIX = os.path.join(ROOT, "tests", "golden", "snapshot_subdoc_v135.json.gz")
+
+
+def subdoc_fixtures():
+    d = json.load(gzip.open(SFIX, "rt"))
+    return [(bytes.fromhex(u), bytes.fromhex(e)) for u, e in d["rows"]]
+
+
+def test_subdoc_fixtures_present():
+    rows = subdoc_fixtures()
+    assert len(rows) == 260 and all(u and e for u, e in rows)
+
+
+@pytest.mark.skipif(not (NODE and BUNDLE), reason="node + the yjs bundle are needed to regenerate")
+def test_subdoc_fixtures_regenerate(tmp_path):
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "exp.bin")
+    subprocess.run([NODE, os.path.join(ROOT, "tools", "snap_corpus.js"), "20", "61", a, b, "120", "subdoc"], check=True, timeout=120)
+    rows = subdoc_fixtures()[:20]
+    assert read_in(a) == [u for u, _ in rows]
+    assert [e for _, e in read_res(b)] == [e for _, e in rows]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
+@pytest.mark.parametrize("mode", [1, 0])
+def test_subdoc_kernel_code_on_host(tmp_path, mode):
+    """Sub-documents through the kernel's code host-compiled: ContentDoc items integrate, split never (one clock), and
+    are garbage-collected to ContentDeleted when deleted; canonical options are written as read."""
+    from golden import ds_to_desc
+    exe = str(tmp_path / "snapdev")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", exe, os.path.join(ROOT, "tools", "snapdev", "snapdev.cpp")], check=True, timeout=300)
+    rows = subdoc_fixtures()
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
+    write_in(a, [u for u, _ in rows])
+    subprocess.run([exe, a, b, str(mode)], check=True, timeout=120)
+    exp = [(0, e) if mode else (0, bytes.fromhex(ds_to_desc(e.hex()))) for _, e in rows]
+    res = [_resolve_pending(st, body, bool(mode)) for st, body in read_res(b)]
+    bad = [k for k in range(len(rows)) if res[k] != exp[k]]
+    assert not bad, f"{len(bad)} documents differ, first {bad[:5]}"
+
+
+@pytest.mark.gpu
+def test_gpu_snapshot_subdocs_vs_yjs(eng135):
+    rows = subdoc_fixtures()
+    res = eng135.snapshot_batch([u for u, _ in rows])
+    bad = [k for k, ((_, e), r) in enumerate(zip(rows, res)) if r != (0, e)]
+    assert not bad, f"{len(bad)} documents differ from yjs, first {bad[:5]}: {res[bad[0]]}"
 
 
 @pytest.mark.gpu

@@ -8,7 +8,8 @@
 //   expected = Y.encodeStateAsUpdate(Y.applyUpdate(new Y.Doc(), u))  (what extension-database stores)
 // Writes `out.bin` (u32 n, then (u32 len, u) per session) and `exp.bin` (i32 status 0, u32 len, bytes),
 // the formats tools/snapdev and tests read.
-//   node tools/snap_corpus.js <n> <seed> <out.bin> <exp.bin> [maxOps] [text|pending|textpending]
+//   node tools/snap_corpus.js <n> <seed> <out.bin> <exp.bin> [maxOps] [text|pending|textpending|subdoc|subpending]
+// subdoc: the general sessions with sub-documents (Y.Doc values in a map and an array, some of them deleted)
 // pending: the same sessions with 1-3 of the log's updates lost (out-of-order delivery: later updates depend on the
 // missing ones) -- u merges what is left, so Y.applyUpdate leaves pending structs and / or a pending delete set
 const fs = require('fs')
@@ -69,7 +70,7 @@ function textSession (seed, maxOps, drop) {
   return [u, Y.encodeStateAsUpdate(fresh)]
 }
 
-function session (seed, maxOps, drop) {
+function session (seed, maxOps, drop, subdoc) {
   const R = rng(seed * 2654435761 + 12345)
   const ri = n => Math.floor(R() * n)
   const nPeers = 1 + ri(3)
@@ -89,7 +90,13 @@ function session (seed, maxOps, drop) {
     const d = peers[p]
     const k = ri(16)
     d.transact(() => {
-      if (k < 5) {
+      if (subdoc && R() < 0.15) {
+        // sub-documents (ContentDoc): set in a map (an overwrite deletes the previous one) or inserted in an array
+        const opts = [{}, { autoLoad: true }, { meta: { v: ri(9) } }, { gc: false }, { gc: false, autoLoad: true, meta: 'm' }][ri(5)]
+        const sd = new Y.Doc(Object.assign({ guid: 'sub-' + ri(1e9) }, opts))   // (a seeded guid: the vectors regenerate)
+        if (R() < 0.6) d.getMap('docs').set('d' + ri(3), sd)
+        else { const a = d.getArray('subs'); if (a.length && R() < 0.3) a.delete(ri(a.length), 1); else a.insert(ri(a.length + 1), [sd]) }
+      } else if (k < 5) {
         const t = d.getText('text')
         if (t.length > 0 && R() < 0.35) { const at = ri(t.length); t.delete(at, 1 + ri(Math.min(6, t.length - at))) }
         else t.insert(ri(t.length + 1), str(1 + ri(R() < 0.8 ? 3 : 12)), R() < 0.15 ? { bold: true } : undefined)
@@ -165,9 +172,10 @@ if (require.main === module) {
   const maxOps = parseInt(process.argv[6] || '60', 10)
   const mode = process.argv[7] || ''
   const gen = mode === 'text' || mode === 'textpending' ? textSession : session
-  const drop = mode === 'pending' || mode === 'textpending'
+  const drop = mode === 'pending' || mode === 'textpending' || mode === 'subpending'
+  const subdoc = mode === 'subdoc' || mode === 'subpending'
   const us = []; const ex = []
-  for (let i = 0; i < n; i++) { const [u, e] = gen(seed * 100003 + i, maxOps, drop); us.push(u); ex.push(e) }
+  for (let i = 0; i < n; i++) { const [u, e] = gen(seed * 100003 + i, maxOps, drop, subdoc); us.push(u); ex.push(e) }
   write(process.argv[4], us, false)
   const eb = [Buffer.from(new Uint32Array([ex.length]).buffer)]
   for (const b of ex) eb.push(Buffer.from(new Int32Array([0]).buffer), Buffer.from(new Uint32Array([b.length]).buffer), Buffer.from(b))

@@ -42,8 +42,14 @@ int ygm_k_launch_pend_plan(const uint32_t* list, uint32_t P, const uint8_t* ws, 
                            hipStream_t s);
 int ygm_k_launch_pend_copy(const uint32_t* list, uint32_t P, const uint8_t* ws, const uint64_t* out_off, const uint64_t* upd_off, uint8_t* dst,
                            hipStream_t s);
-int ygm_k_launch_pend_fix(const uint32_t* list, uint32_t P, const uint64_t* m_off, const uint64_t* m_len, const int32_t* m_st, uint64_t tail,
-                          uint64_t* out_off, uint64_t* out_len, int32_t* status, hipStream_t s);
+int ygm_k_launch_pend_fix(const uint32_t* list, uint32_t P, const uint64_t* m_off, const uint64_t* m_len, const int32_t* m_st,
+                          const int32_t* pst, uint64_t tail, uint64_t* out_off, uint64_t* out_len, int32_t* status, hipStream_t s);
+int ygm_k_launch_pend_split(const uint32_t* list, uint32_t P, const uint8_t* ws, const uint64_t* out_off, const uint8_t* sv,
+                            const uint64_t* sv_off, uint64_t* offs, uint8_t* da, uint8_t* db, uint8_t* dc, uint8_t* dsv, int pass,
+                            hipStream_t s);
+int ygm_k_launch_pend_join(uint32_t P, const uint8_t* ad, const uint64_t* a_off, const uint64_t* a_len, const int32_t* a_st, const uint8_t* bd,
+                           const uint64_t* offs, const uint8_t* cd, const uint64_t* c_off, const uint64_t* c_len, const int32_t* c_st,
+                           uint64_t* upd_off, uint32_t* doc_upd, int32_t* pst, uint8_t* dst, int pass, hipStream_t s);
 int ygm_k_launch_pack(const uint8_t* src, const uint64_t* off, const uint64_t* len, const int32_t* status, uint32_t n, uint64_t* bsum,
                       uint8_t* dst, uint64_t* poff, hipStream_t s);
 int ygm_k_launch_doc_lean(int mode, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* doc_off, const uint8_t* sv_arena,
@@ -185,7 +191,9 @@ struct ygm_ctx {
   DevBuf sv_tbl, sv_tn;                // diff: sorted state-vector tables (k_sv_table) and their entry counts
   DevBuf sn_cnt, sn_off, sn_bs, sn_ws, sn_claim, sn_pay;
   DevBuf sn_pend, pn_off, pn_du, pn_arena;   // snapshot: documents left pending, their three-update batch for the merge
-  ygm_ctx* pend_ctx = nullptr;               // ... merged on this child context (its own buffers and counters)  // snapshot: per-document counts, workspace offsets, scan scratch,
+  DevBuf pq_off, pq_a, pq_b, pq_c, pq_s, pq_st;   // step2 of pending documents: their parts and state vectors, statuses
+  ygm_ctx* pend_ctx = nullptr;               // ... merged on this child context (its own buffers and counters)
+  ygm_ctx* pend_dx[2] = {nullptr, nullptr};  // ... and the step2 diffs of their parts on these  // snapshot: per-document counts, workspace offsets, scan scratch,
   // [LDS-tier output slots | workspaces], LDS-tier claims, its payload / claimed counters
   // update V2: per-update V1 sizes -> offsets, transcoding statuses, scan scratch, the V1 arena, per-document column
   // lengths, the V2 outputs (packed), their offsets / lengths / statuses
@@ -279,10 +287,12 @@ void ygm_close(ygm_ctx* c) {
   for (DevBuf* b : {&c->arena, &c->offs, &c->docs, &c->sv_arena, &c->sv_offs, &c->out, &c->out_off, &c->out_len, &c->status,
                     &c->lb, &c->meta, &c->fb_list, &c->defer_list, &c->defer2_list, &c->defer_w_list, &c->route_list, &c->s_readers, &c->s_order, &c->s_tmp, &c->s_ubase, &c->s_ulen, &c->s_cnt,
                     &c->s_drec, &c->big_blk, &c->big_rec, &c->big_list, &c->big_scan, &c->big_up, &c->lens_off, &c->sv_tbl, &c->sv_tn, &c->sn_cnt, &c->sn_off, &c->sn_bs, &c->sn_ws, &c->sn_claim, &c->sn_pay,
-                    &c->sn_pend, &c->pn_off, &c->pn_du, &c->pn_arena, &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr, &c->v21_cl})
+                    &c->sn_pend, &c->pn_off, &c->pn_du, &c->pn_arena,
+                    &c->pq_off, &c->pq_a, &c->pq_b, &c->pq_c, &c->pq_s, &c->pq_st, &c->v2_len, &c->v2_st, &c->v2_bs, &c->v2_v1, &c->v2_L, &c->v2_out, &c->v2_off, &c->v2_olen, &c->v2_ost, &c->v2_fo, &c->v2_claim, &c->v2_pay, &c->v2_scr, &c->v21_cl})
     b->release();
   for (ygm_ctx* k : c->kid) if (k) ygm_close(k);
   if (c->pend_ctx) ygm_close(c->pend_ctx);
+  for (ygm_ctx* k : c->pend_dx) if (k) ygm_close(k);
   for (DevBuf* b : {&c->pk_data, &c->pk_off, &c->pk_bsum}) b->release();
   for (PinBuf* b : {&c->h_data, &c->h_off, &c->h_len, &c->h_status, &c->h_in}) b->release();
   for (hipEvent_t e : {c->e0, c->e1, c->e2, c->e3}) if (e) (void)hipEventDestroy(e);
@@ -602,29 +612,26 @@ static int run_doc_kernel(ygm_ctx* c, int mode, const uint8_t* d_arena, uint64_t
 // returns mergeUpdates of the three (Y@23300).  They are packed into one arena as three-update documents (k_pend_plan /
 // k_pend_copy) and merged by the merge kernels on the child context c->pend_ctx; the merged bytes are appended to the
 // snapshot's output region at `used` and the documents' offsets, lengths and statuses rewritten (k_pend_fix).
-static int snap_resolve_pending(ygm_ctx* c, hipStream_t s, uint32_t P, uint64_t used, uint64_t& data_bytes, unsigned long long& payload) {
-  if (!c->pn_off.ensure(8ull * (3ull * P + 1) + 16) || !c->pn_du.ensure(4ull * (P + 1) + 16)) return YGM_ENOMEM;
-  if (ygm_k_launch_pend_plan(c->sn_pend.as<uint32_t>(), P, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->pn_off.as<uint64_t>(),
-                             c->pn_du.as<uint32_t>(), s))
-    return YGM_EDEVICE;
-  uint64_t total = 0;
+// the pending documents' three-update batch (c->pn_arena / pn_off / pn_du, `total` bytes) merged on the child context
+// c->pend_ctx; the merged bytes appended to `dst` at `used` and the documents' places, lengths and statuses written
+// (pst: statuses decided before the merge, nullable)
+static uint64_t read_u64(ygm_ctx* c, hipStream_t s, const uint64_t* d_p, int& e) {
+  uint64_t v = 0;
   c->stats.host_syncs++;
-  HIPCHK(hipMemcpyAsync(c->h_meta, c->pn_off.as<uint64_t>() + 3ull * P, 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  memcpy(&total, c->h_meta, 8);
-  if (!c->pn_arena.ensure(total + 64)) return YGM_ENOMEM;
-  HIPCHK(hipMemsetAsync(c->pn_arena.as<uint8_t>() + total, 0, 64, s));   // (the merge kernels' tail padding)
-  if (ygm_k_launch_pend_copy(c->sn_pend.as<uint32_t>(), P, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->pn_off.as<uint64_t>(),
-                             c->pn_arena.as<uint8_t>(), s))
-    return YGM_EDEVICE;
+  e = hipMemcpyAsync(c->h_meta, d_p, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess ? YGM_EDEVICE : 0;
+  memcpy(&v, c->h_meta, 8);
+  return v;
+}
+static int pend_merge_place(ygm_ctx* c, hipStream_t s, uint32_t P, uint64_t total, const int32_t* pst, DevBuf& dst, uint64_t used,
+                            uint64_t& data_bytes, unsigned long long& payload) {
   if (!c->pend_ctx) { const int e = ygm_open(c->device, c->flags, &c->pend_ctx); if (e) return e; }
   int e = ygm_merge_v1_device_async(c->pend_ctx, c->pn_arena.as<uint8_t>(), total, c->pn_off.as<uint64_t>(), c->pn_du.as<uint32_t>(), 3 * P, P, s);
   ygm_device_result r;
   if (!e) e = ygm_merge_v1_device_finish(c->pend_ctx, &r);
   if (e) return e;
-  if (!c->sn_ws.ensure(used + r.data_bytes + 64, used, s)) return YGM_ENOMEM;
-  if (r.data_bytes) HIPCHK(hipMemcpyAsync(c->sn_ws.as<uint8_t>() + used, r.data, r.data_bytes, hipMemcpyDeviceToDevice, s));
-  if (ygm_k_launch_pend_fix(c->sn_pend.as<uint32_t>(), P, r.off, r.len, r.status, used, c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(),
+  if (!dst.ensure(used + r.data_bytes + 64, used, s)) return YGM_ENOMEM;
+  if (r.data_bytes) HIPCHK(hipMemcpyAsync(dst.as<uint8_t>() + used, r.data, r.data_bytes, hipMemcpyDeviceToDevice, s));
+  if (ygm_k_launch_pend_fix(c->sn_pend.as<uint32_t>(), P, r.off, r.len, r.status, pst, used, c->out_off.as<uint64_t>(), c->out_len.as<uint64_t>(),
                             c->status.as<int32_t>(), s))
     return YGM_EDEVICE;
   data_bytes = used + r.data_bytes;
@@ -632,10 +639,28 @@ static int snap_resolve_pending(ygm_ctx* c, hipStream_t s, uint32_t P, uint64_t 
   c->stats.docs_pending += P;
   return YGM_OK;
 }
+static int snap_resolve_pending(ygm_ctx* c, hipStream_t s, uint32_t P, uint64_t used, uint64_t& data_bytes, unsigned long long& payload) {
+  if (!c->pn_off.ensure(8ull * (3ull * P + 1) + 16) || !c->pn_du.ensure(4ull * (P + 1) + 16)) return YGM_ENOMEM;
+  if (ygm_k_launch_pend_plan(c->sn_pend.as<uint32_t>(), P, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->pn_off.as<uint64_t>(),
+                             c->pn_du.as<uint32_t>(), s))
+    return YGM_EDEVICE;
+  int e = 0;
+  const uint64_t total = read_u64(c, s, c->pn_off.as<uint64_t>() + 3ull * P, e);
+  if (e) return e;
+  if (!c->pn_arena.ensure(total + 64)) return YGM_ENOMEM;
+  HIPCHK(hipMemsetAsync(c->pn_arena.as<uint8_t>() + total, 0, 64, s));   // (the merge kernels' tail padding)
+  if (ygm_k_launch_pend_copy(c->sn_pend.as<uint32_t>(), P, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), c->pn_off.as<uint64_t>(),
+                             c->pn_arena.as<uint8_t>(), s))
+    return YGM_EDEVICE;
+  return pend_merge_place(c, s, P, total, nullptr, c->sn_ws, used, data_bytes, payload);
+}
 
-// the snapshot batch; xf: YGM_F_SNAP_NOPEND (step2) / YGM_F_SNAP_STATE (contains) for states that leave pending parts
+// the snapshot batch; xf: YGM_F_SNAP_STATE (contains) for states that leave pending parts
+// leave: when non-null, documents left pending are not resolved: their count goes there (list c->sn_pend, statuses
+// ST_PEND, their PendHdr layouts at out_off)
 static int snapshot_dev(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes, const uint64_t* d_doc_off, uint32_t n_docs,
-                        hipStream_t s, ygm_device_result* out, uint32_t xf) {
+                        hipStream_t s, ygm_device_result* out, uint32_t xf, uint32_t* leave = nullptr) {
+  if (leave) *leave = 0;
   const uint32_t fl = c->flags | xf;
   const uint32_t nb = (n_docs + 1 + 255) / 256;
   if (!c->sn_cnt.ensure(16ull * n_docs + 16) || !c->sn_off.ensure(8ull * n_docs + 16) || !c->sn_bs.ensure(8ull * nb + 16) ||
@@ -682,7 +707,8 @@ static int snapshot_dev(ygm_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes
       return YGM_EDEVICE;
     int e = read_meta(c, s, m, meta);
     if (e) return e;
-    if (m.fb_count && (e = snap_resolve_pending(c, s, m.fb_count, slot_total + total, total_out, m.payload))) return e;
+    if (m.fb_count && leave) *leave = m.fb_count;
+    else if (m.fb_count && (e = snap_resolve_pending(c, s, m.fb_count, slot_total + total, total_out, m.payload))) return e;
     HIPCHK(hipEventRecord(c->e1, s));
     HIPCHK(hipEventSynchronize(c->e1));
   } else {
@@ -782,9 +808,67 @@ int ygm_sv_from_update_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t ar
   return run_doc_kernel(c, 0, d_arena, arena_bytes, d_doc_off, nullptr, 0, nullptr, n_docs, stream, out);
 }
 
+// SyncStep2 of the documents the snapshot left pending (P of them, list c->sn_pend, PendHdr layouts in its output
+// region: split off before the main diff, finished after it): encodeStateAsUpdate(doc, sv) = mergeUpdates([writeStateAsUpdate(doc, sv), pendingDs, diffUpdate(pending
+// structs, sv)]) (Y@23300) -- the state part diffed keeping each struct's parentSub bit (an integrated item's write),
+// the pending structs by the plain diff (the lazy writer's), on two child contexts; the three merged on a third, and
+// appended to the step2 result (`out`, the diff kernels' output region) in the documents' places
+// split (before the main diff reuses the snapshot's out_off): parts and state vectors into c->pq_*; tot: their bytes
+static int step2_pending_split(ygm_ctx* c, hipStream_t s, uint32_t P, const uint8_t* d_sv_arena, const uint64_t* d_sv_off, uint64_t (&tot)[4]) {
+  const uint64_t np = (uint64_t)P + 1;
+  if (!c->pq_off.ensure(8ull * 4 * np + 16) || !c->pq_st.ensure(4ull * P + 16) || !c->pn_off.ensure(8ull * (3ull * P + 1) + 16) ||
+      !c->pn_du.ensure(4ull * np + 16))
+    return YGM_ENOMEM;
+  uint64_t* offs = c->pq_off.as<uint64_t>();
+  if (ygm_k_launch_pend_split(c->sn_pend.as<uint32_t>(), P, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), d_sv_arena, d_sv_off, offs,
+                              nullptr, nullptr, nullptr, nullptr, 0, s))
+    return YGM_EDEVICE;
+  c->stats.host_syncs++;
+  for (int k = 0; k < 4; k++) HIPCHK(hipMemcpyAsync((uint64_t*)c->h_meta + k, offs + (uint64_t)k * np + P, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  memcpy(tot, c->h_meta, sizeof tot);
+  DevBuf* part[4] = {&c->pq_a, &c->pq_b, &c->pq_c, &c->pq_s};
+  for (int k = 0; k < 4; k++) {
+    if (!part[k]->ensure(tot[k] + 64)) return YGM_ENOMEM;
+    HIPCHK(hipMemsetAsync(part[k]->as<uint8_t>() + tot[k], 0, 64, s));   // (readable tail padding for the kernels)
+  }
+  if (ygm_k_launch_pend_split(c->sn_pend.as<uint32_t>(), P, c->sn_ws.as<uint8_t>(), c->out_off.as<uint64_t>(), d_sv_arena, d_sv_off, offs,
+                              c->pq_a.as<uint8_t>(), c->pq_b.as<uint8_t>(), c->pq_c.as<uint8_t>(), c->pq_s.as<uint8_t>(), 1, s))
+    return YGM_EDEVICE;
+  return YGM_OK;
+}
+// finish (after the main diff): the two diffs, the join, the merge, the places in `out`
+static int step2_pending_finish(ygm_ctx* c, hipStream_t s, uint32_t P, const uint64_t (&tot)[4], ygm_device_result* out) {
+  const uint64_t np = (uint64_t)P + 1;
+  uint64_t* offs = c->pq_off.as<uint64_t>();
+  for (ygm_ctx*& k : c->pend_dx) if (!k) { const int e = ygm_open(c->device, c->flags, &k); if (e) return e; }
+  ygm_device_result ra, rc;
+  int e = run_doc_kernel(c->pend_dx[0], 1, c->pq_a.as<uint8_t>(), tot[0], offs, c->pq_s.as<uint8_t>(), tot[3], offs + 3 * np, P, s, &ra,
+                         YGM_F_KEEP_SUB);
+  if (!e) e = run_doc_kernel(c->pend_dx[1], 1, c->pq_c.as<uint8_t>(), tot[2], offs + 2 * np, c->pq_s.as<uint8_t>(), tot[3], offs + 3 * np, P,
+                             s, &rc, 0);
+  if (e) return e;
+  if (ygm_k_launch_pend_join(P, ra.data, ra.off, ra.len, ra.status, c->pq_b.as<uint8_t>(), offs, rc.data, rc.off, rc.len, rc.status,
+                             c->pn_off.as<uint64_t>(), c->pn_du.as<uint32_t>(), c->pq_st.as<int32_t>(), nullptr, 0, s))
+    return YGM_EDEVICE;
+  const uint64_t total = read_u64(c, s, c->pn_off.as<uint64_t>() + 3ull * P, e);
+  if (e) return e;
+  if (!c->pn_arena.ensure(total + 64)) return YGM_ENOMEM;
+  HIPCHK(hipMemsetAsync(c->pn_arena.as<uint8_t>() + total, 0, 64, s));
+  if (ygm_k_launch_pend_join(P, ra.data, ra.off, ra.len, ra.status, c->pq_b.as<uint8_t>(), offs, rc.data, rc.off, rc.len, rc.status,
+                             c->pn_off.as<uint64_t>(), c->pn_du.as<uint32_t>(), c->pq_st.as<int32_t>(), c->pn_arena.as<uint8_t>(), 1, s))
+    return YGM_EDEVICE;
+  uint64_t db = 0;
+  unsigned long long pay = out->payload_bytes;
+  if ((e = pend_merge_place(c, s, P, total, c->pq_st.as<int32_t>(), c->out, out->data_bytes, db, pay))) return e;
+  out->data = c->out.as<uint8_t>(); out->data_bytes = db; out->payload_bytes = pay;
+  return YGM_OK;
+}
+
 // SyncStep2 of stored documents (MessageReceiver.ts:137-138): the snapshot batch, its outputs packed into one arena
 // on the device (k_pack_*: offsets n + 1, the total at [n]), the diff kernels over it with F_KEEP_SUB, and the
-// snapshot's per-document refusals (EUNSUPPORTED, malformed states) carried into the result
+// snapshot's per-document refusals (EUNSUPPORTED, malformed states) carried into the result; states that leave
+// pending parts by step2_pending_split / _finish
 int ygm_sync_step2_v1_device(ygm_ctx* c, const uint8_t* d_states, uint64_t states_bytes, const uint64_t* d_state_off,
                              const uint8_t* d_sv_arena, const uint64_t* d_sv_off, uint32_t n_docs, void* stream,
                              ygm_device_result* out) {
@@ -794,9 +878,10 @@ int ygm_sync_step2_v1_device(ygm_ctx* c, const uint8_t* d_states, uint64_t state
   ygm_device_result r1;
   const bool dbg = getenv("YGM_DEBUG") != nullptr;
 #define S2CHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { if (dbg) fprintf(stderr, "ygm step2: %s: %s\n", #x, hipGetErrorString(_e)); return YGM_EDEVICE; } } while (0)
-  // (a state that leaves pending parts is EUNSUPPORTED here: encodeStateAsUpdate(doc, sv) diffs its pending structs
-  // without the parentSub bit the integrated ones keep -- the caller names it and keeps its own path)
-  int e = snapshot_dev(c, d_states, states_bytes, d_state_off, n_docs, s, &r1, YGM_F_SNAP_NOPEND);
+  uint32_t P = 0;   // documents the snapshot leaves pending (their parts split off now, answered after the diff)
+  uint64_t ptot[4] = {0, 0, 0, 0};
+  int e = snapshot_dev(c, d_states, states_bytes, d_state_off, n_docs, s, &r1, 0, &P);
+  if (!e && P) e = step2_pending_split(c, s, P, d_sv_arena, d_sv_off, ptot);
   if (dbg) fprintf(stderr, "ygm step2: snapshot rc %d payload %llu\n", e, (unsigned long long)r1.payload_bytes);
   if (e || (e = pack_snapshots(c, s, r1, n_docs))) return e;
   uint64_t sv_end = 0;
@@ -806,6 +891,7 @@ int ygm_sync_step2_v1_device(ygm_ctx* c, const uint8_t* d_states, uint64_t state
   if (dbg) fprintf(stderr, "ygm step2: diff rc %d\n", e);
   if (e) return e;
   if (n_docs && ygm_k_launch_v2_status(c->s2_st.as<int32_t>(), n_docs, out->status, out->len, s)) return YGM_EDEVICE;
+  if (P && (e = step2_pending_finish(c, s, P, ptot, out))) return e;
   S2CHK(hipStreamSynchronize(s));
   return YGM_OK;
 #undef S2CHK

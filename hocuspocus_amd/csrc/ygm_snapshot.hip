@@ -191,15 +191,107 @@ __global__ __launch_bounds__(256) void k_pend_copy(const uint32_t* __restrict__ 
   const uint64_t a = upd_off[3ull * j], n = upd_off[3ull * j + 3] - a;
   for (uint64_t i = threadIdx.x; i < n; i += 256) dst[a + i] = src[i];
 }
-// fix: the merged bytes were appended at `tail` of the output region: each document's place, length and status
+// fix: the merged bytes were appended at `tail` of the output region: each document's place, length and status (pst:
+// a status decided before the merge, which wins when non-zero)
 __global__ __launch_bounds__(256) void k_pend_fix(const uint32_t* __restrict__ list, uint32_t P, const uint64_t* __restrict__ m_off,
-                                                  const uint64_t* __restrict__ m_len, const int32_t* __restrict__ m_st, uint64_t tail,
-                                                  uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
+                                                  const uint64_t* __restrict__ m_len, const int32_t* __restrict__ m_st,
+                                                  const int32_t* __restrict__ pst, uint64_t tail, uint64_t* __restrict__ out_off,
+                                                  uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= P) return;
   const uint32_t d = list[j];
-  const int32_t st = m_st[j];
+  const int32_t st = pst && pst[j] ? pst[j] : m_st[j];
   out_off[d] = tail + m_off[j]; out_len[d] = st == ST_OK ? m_len[j] : 0u; status[d] = st;
+}
+
+// ---- SyncStep2 of pending documents: encodeStateAsUpdate(doc, sv) = mergeUpdates([writeStateAsUpdate(doc, sv),
+// pendingDs, diffUpdate(pending structs, sv)]) (Y@23300).  split: each document's three parts and its state vector
+// packed into four arenas (offsets k (P + 1) + j: k = state, pendingDs, pending structs, state vector), for the two
+// diffs; join: [diff(state), pendingDs, diff(pending structs)] packed as three-update documents for the merge
+YDEV uint32_t pend_len(const uint8_t* h, uint32_t k) {
+  return (uint32_t)h[4 * k] | ((uint32_t)h[4 * k + 1] << 8) | ((uint32_t)h[4 * k + 2] << 16) | ((uint32_t)h[4 * k + 3] << 24);
+}
+__global__ __launch_bounds__(1024) void k_pend_split_plan(const uint32_t* __restrict__ list, uint32_t P, const uint8_t* __restrict__ ws,
+                                                          const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ sv_off,
+                                                          uint64_t* __restrict__ offs) {
+  __shared__ uint64_t tmp[1024 / WAVE + 1];
+  __shared__ uint64_t carry[4];
+  if (threadIdx.x < 4) carry[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t j0 = 0; j0 < P; j0 += 1024) {
+    const uint32_t j = j0 + threadIdx.x;
+    uint64_t l[4] = {0, 0, 0, 0};
+    if (j < P) {
+      const uint32_t d = list[j];
+      const uint8_t* h = ws + out_off[d];
+      l[0] = pend_len(h, 0); l[1] = pend_len(h, 1); l[2] = pend_len(h, 2); l[3] = sv_off[d + 1] - sv_off[d];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint64_t tot;
+      const uint64_t pre = block_exscan<1024>(l[k], tmp, tot);
+      if (j < P) offs[(uint64_t)k * (P + 1) + j] = carry[k] + pre;
+      __syncthreads();
+      if (threadIdx.x == 0) carry[k] += tot;
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x < 4) offs[(uint64_t)threadIdx.x * (P + 1) + P] = carry[threadIdx.x];
+}
+__global__ __launch_bounds__(256) void k_pend_split_copy(const uint32_t* __restrict__ list, uint32_t P, const uint8_t* __restrict__ ws,
+                                                         const uint64_t* __restrict__ out_off, const uint8_t* __restrict__ sv,
+                                                         const uint64_t* __restrict__ sv_off, const uint64_t* __restrict__ offs,
+                                                         uint8_t* __restrict__ da, uint8_t* __restrict__ db, uint8_t* __restrict__ dc,
+                                                         uint8_t* __restrict__ dsv) {
+  const uint32_t j = blockIdx.x, d = list[j];
+  const uint8_t* src = ws + out_off[d] + sizeof(snap::PendHdr);
+  uint8_t* const dst[3] = {da, db, dc};
+#pragma unroll
+  for (uint32_t k = 0; k < 3; k++) {
+    const uint64_t a = offs[(uint64_t)k * (P + 1) + j], n = offs[(uint64_t)k * (P + 1) + j + 1] - a;
+    for (uint64_t i = threadIdx.x; i < n; i += 256) dst[k][a + i] = src[i];
+    src += n;
+  }
+  const uint64_t a = offs[3ull * (P + 1) + j], n = offs[3ull * (P + 1) + j + 1] - a, s0 = sv_off[d];
+  for (uint64_t i = threadIdx.x; i < n; i += 256) dsv[a + i] = sv[s0 + i];
+}
+__global__ __launch_bounds__(1024) void k_pend_join_plan(uint32_t P, const uint64_t* __restrict__ a_len, const int32_t* __restrict__ a_st,
+                                                         const uint64_t* __restrict__ offs, const uint64_t* __restrict__ c_len,
+                                                         const int32_t* __restrict__ c_st, uint64_t* __restrict__ upd_off,
+                                                         uint32_t* __restrict__ doc_upd, int32_t* __restrict__ pst) {
+  __shared__ uint64_t tmp[1024 / WAVE + 1];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t j0 = 0; j0 < P; j0 += 1024) {
+    const uint32_t j = j0 + threadIdx.x;
+    uint64_t l0 = 0, l1 = 0, l2 = 0;
+    if (j < P) {
+      l0 = a_st[j] == ST_OK ? a_len[j] : 0u;
+      l1 = offs[(P + 1) + j + 1] - offs[(P + 1) + j];
+      l2 = c_st[j] == ST_OK ? c_len[j] : 0u;
+      pst[j] = a_st[j] != ST_OK ? a_st[j] : c_st[j];
+    }
+    uint64_t tot;
+    const uint64_t pre = carry + block_exscan<1024>(l0 + l1 + l2, tmp, tot);
+    if (j < P) { upd_off[3ull * j] = pre; upd_off[3ull * j + 1] = pre + l0; upd_off[3ull * j + 2] = pre + l0 + l1; doc_upd[j] = 3u * j; }
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { upd_off[3ull * P] = carry; doc_upd[P] = 3u * P; }
+}
+__global__ __launch_bounds__(256) void k_pend_join_copy(uint32_t P, const uint8_t* __restrict__ ad, const uint64_t* __restrict__ a_off,
+                                                        const uint8_t* __restrict__ bd, const uint64_t* __restrict__ offs,
+                                                        const uint8_t* __restrict__ cd, const uint64_t* __restrict__ c_off,
+                                                        const uint64_t* __restrict__ upd_off, uint8_t* __restrict__ dst) {
+  const uint32_t j = blockIdx.x;
+  const uint8_t* const src[3] = {ad + a_off[j], bd + offs[(P + 1) + j], cd + c_off[j]};
+#pragma unroll
+  for (uint32_t k = 0; k < 3; k++) {
+    const uint64_t a = upd_off[3ull * j + k], n = upd_off[3ull * j + k + 1] - a;
+    for (uint64_t i = threadIdx.x; i < n; i += 256) dst[a + i] = src[k][i];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -379,10 +471,26 @@ int ygm_k_launch_pend_copy(const uint32_t* list, uint32_t P, const uint8_t* ws, 
   hipLaunchKernelGGL(k_pend_copy, dim3(P), dim3(256), 0, s, list, ws, out_off, upd_off, dst);
   return snap_rc(__func__);
 }
-int ygm_k_launch_pend_fix(const uint32_t* list, uint32_t P, const uint64_t* m_off, const uint64_t* m_len, const int32_t* m_st, uint64_t tail,
-                          uint64_t* out_off, uint64_t* out_len, int32_t* status, hipStream_t s) {
+int ygm_k_launch_pend_fix(const uint32_t* list, uint32_t P, const uint64_t* m_off, const uint64_t* m_len, const int32_t* m_st,
+                          const int32_t* pst, uint64_t tail, uint64_t* out_off, uint64_t* out_len, int32_t* status, hipStream_t s) {
   if (P == 0) return 0;
-  hipLaunchKernelGGL(k_pend_fix, dim3((P + 255) / 256), dim3(256), 0, s, list, P, m_off, m_len, m_st, tail, out_off, out_len, status);
+  hipLaunchKernelGGL(k_pend_fix, dim3((P + 255) / 256), dim3(256), 0, s, list, P, m_off, m_len, m_st, pst, tail, out_off, out_len, status);
+  return snap_rc(__func__);
+}
+int ygm_k_launch_pend_split(const uint32_t* list, uint32_t P, const uint8_t* ws, const uint64_t* out_off, const uint8_t* sv,
+                            const uint64_t* sv_off, uint64_t* offs, uint8_t* da, uint8_t* db, uint8_t* dc, uint8_t* dsv, int pass,
+                            hipStream_t s) {
+  if (P == 0) return 0;
+  if (pass == 0) hipLaunchKernelGGL(k_pend_split_plan, dim3(1), dim3(1024), 0, s, list, P, ws, out_off, sv_off, offs);
+  else hipLaunchKernelGGL(k_pend_split_copy, dim3(P), dim3(256), 0, s, list, P, ws, out_off, sv, sv_off, (const uint64_t*)offs, da, db, dc, dsv);
+  return snap_rc(__func__);
+}
+int ygm_k_launch_pend_join(uint32_t P, const uint8_t* ad, const uint64_t* a_off, const uint64_t* a_len, const int32_t* a_st, const uint8_t* bd,
+                           const uint64_t* offs, const uint8_t* cd, const uint64_t* c_off, const uint64_t* c_len, const int32_t* c_st,
+                           uint64_t* upd_off, uint32_t* doc_upd, int32_t* pst, uint8_t* dst, int pass, hipStream_t s) {
+  if (P == 0) return 0;
+  if (pass == 0) hipLaunchKernelGGL(k_pend_join_plan, dim3(1), dim3(1024), 0, s, P, a_len, a_st, offs, c_len, c_st, upd_off, doc_upd, pst);
+  else hipLaunchKernelGGL(k_pend_join_copy, dim3(P), dim3(256), 0, s, P, ad, a_off, bd, offs, cd, c_off, (const uint64_t*)upd_off, dst);
   return snap_rc(__func__);
 }
 

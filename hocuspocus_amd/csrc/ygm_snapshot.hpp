@@ -39,7 +39,6 @@ namespace snap {
 
 constexpr int ST_UNSUP = 9;   // YGM_EUNSUPPORTED
 constexpr int ST_PEND = 64;   // internal: the output is [state, pendingDs, pending structs] for the merge kernels
-constexpr uint32_t F_SNAP_NOPEND = 8u;   // YGM_F_SNAP_NOPEND: a pending document is ST_UNSUP
 constexpr uint32_t F_SNAP_STATE = 16u;   // YGM_F_SNAP_STATE: a pending document's output is its integrated state
 // a pending document's output: this header, then the three V1 updates back to back (an absent one as the empty update)
 struct PendHdr { uint32_t len[3]; uint32_t magic; };
@@ -797,7 +796,6 @@ struct Doc {
     o.vu(0);
   }
   YDEV uint32_t encode() {
-    if ((n_rest || n_pds) && (flags & F_SNAP_NOPEND)) { fail(ST_UNSUP); return 0; }
     if ((!n_rest && !n_pds) || (flags & F_SNAP_STATE)) {
       OutCap o{out, 0, cap_out};
       encode_state(o);

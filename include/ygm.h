@@ -47,7 +47,6 @@ extern "C" {
 #define YGM_EINVAL 8       /* bad call arguments */
 #define YGM_EUNSUPPORTED 9 /* snapshot / step2 / contains only: the update repeats a client block or overlaps
                               structs (yjs's writers never do), or names a non-type item as a parent
-                              (ygm_sync_step2_v1: or leaves pending structs / a pending delete set)
                               -- the caller keeps its yjs path for that document */
 
 #define YGM_MAX_DEPTH 32
@@ -56,8 +55,6 @@ extern "C" {
 #define YGM_F_COMPAT_135 1u   /* delete-set clients in first-seen order; lone surrogate -> error */
 #define YGM_F_FORCE_SEQ 2u    /* route every merge through the exact sequential kernel (testing) */
 #define YGM_F_KEEP_SUB 4u     /* internal to ygm_sync_step2_v1: diffs keep each struct's parentSub bit (0x20) */
-#define YGM_F_SNAP_NOPEND 8u  /* internal to ygm_sync_step2_v1: a state that leaves pending structs / delete set is
-                                 EUNSUPPORTED (encodeStateAsUpdate(doc, sv) diffs its pending part by other rules) */
 #define YGM_F_SNAP_STATE 16u  /* internal to ygm_contains_v1: such a state's snapshot is its integrated part alone
                                  (Y.snapshot(doc): the store's state vector and delete set) */
 
@@ -144,9 +141,10 @@ int ygm_contains_v1(ygm_ctx *ctx, const uint8_t *states, const uint64_t *state_o
  * document loaded from stored bytes (extension-database Database.ts:44-50).  Computed as the doc-normalized
  * snapshot of `state` (ygm_snapshot_v1) followed by diffUpdate(snapshot, sv) in which every struct keeps its
  * parentSub bit (Item.write of an integrated item, yjs Y@80416).  states / state_off as ygm_snapshot_v1;
- * sv_arena / sv_off one encoded state vector per document.  A document outside the snapshot envelope, or whose
- * state leaves pending parts (encodeStateAsUpdate(doc, sv) diffs pending structs without the parentSub bit the
- * integrated ones keep), carries YGM_EUNSUPPORTED (the caller names it and keeps its yjs path). */
+ * sv_arena / sv_off one encoded state vector per document.  A state that leaves pending structs / a pending delete
+ * set is answered as yjs does: mergeUpdates([writeStateAsUpdate(doc, sv), pendingDs, diffUpdate(pending structs,
+ * sv)]) (Y@23300; the pending structs diffed without the kept bit).  A document outside the snapshot envelope
+ * carries YGM_EUNSUPPORTED (the caller names it and keeps its yjs path). */
 int ygm_sync_step2_v1(ygm_ctx *ctx, const uint8_t *states, const uint64_t *state_off, const uint8_t *sv_arena,
                       const uint64_t *sv_off, uint32_t n_docs, ygm_result *out);
 

@@ -19,6 +19,15 @@ const Y = require(path.join(__dirname, '..', '..', '..', 'tools', 'yjs_bundle.js
 // a per-document status, as GpuEngine rejects a refused document (YgmError code)
 const refusal = fn => { try { return fn() } catch (e) { throw Object.assign(new Error(e.message), { code: 'EMALFORMED' }) } }
 
+// an update whose struct section names a client twice (yjs's writers never do: outside the snapshot envelope)
+function repeatsClient (u) {
+  const seen = new Set()
+  for (const [client] of Y.parseUpdateMeta(u).from) seen.add(client)
+  let pos = 0
+  const vu = () => { let v = 0; let m = 1; for (;;) { const b = u[pos++]; v += (b & 127) * m; if (b < 128) return v; m *= 128 } }
+  const nb = vu()
+  return nb > seen.size
+}
 class CpuDouble { // test double (never shipped): same API as GpuEngine
   constructor (device = 0) { this.calls = 0; this.device = device }
   async mergeUpdates (u) { this.calls++; return refusal(() => Y.mergeUpdates(u)) }
@@ -29,7 +38,8 @@ class CpuDouble { // test double (never shipped): same API as GpuEngine
     this.calls++
     return states.map((u, i) => {
       const d = new Y.Doc(); Y.applyUpdate(d, u)
-      if (d.store.pendingStructs || d.store.pendingDs) return Object.assign(new Error('EUNSUPPORTED'), { code: 'EUNSUPPORTED' })
+      // the snapshot kernel's envelope: a repeated client block is EUNSUPPORTED (ygm_snapshot.hpp)
+      if (repeatsClient(u)) return Object.assign(new Error('EUNSUPPORTED'), { code: 'EUNSUPPORTED' })
       return Y.encodeStateAsUpdate(d, svs[i])
     })
   }
@@ -620,24 +630,28 @@ test('sync responder answers a SyncStep1 batch', async (engine) => {
   })
 })
 
-// a state outside the snapshot envelope (a struct whose origin is missing: pending in yjs) is answered with
-// diffUpdate(state, sv) and named, never sent silently as if it were the reference's bytes
+// a state outside the snapshot envelope (a client block written twice: yjs keeps the second) is answered with
+// diffUpdate(state, sv) and named, never sent silently as if it were the reference's bytes; a state whose history
+// lost an update (pending structs in yjs) gets the reference's own reply
 test('sync responder names Step2 replies outside the snapshot envelope', async (engine) => {
   const src = new Y.Doc(); const ups = []
   src.on('update', u => ups.push(u))
   src.getText('t').insert(0, 'ab'); src.getText('t').insert(2, 'cd')
   const pending = ups[1]                                            // depends on the first update: pending alone
   const good = Y.mergeUpdates(ups)
-  const states = { pend: pending, good }
+  const twice = Uint8Array.from([2, 1, 5, 0, 4, 1, 1, 0x74, 1, 0x61, 1, 5, 1, 0x84, 5, 0, 1, 0x62, 0])   // client 5's block twice
+  const states = { pend: pending, good, twice }
   const r = new SyncResponder({ engine, getState: async n => states[n] })
-  const msgs = ['pend', 'good'].map(n => frame(n, MessageType.Sync, SyncStep.Step1, Uint8Array.from([0])))
+  const msgs = ['pend', 'good', 'twice'].map(n => frame(n, MessageType.Sync, SyncStep.Step1, Uint8Array.from([0])))
   const out = await r.answerMany(msgs)
-  assert.strictEqual(out[0].unnormalized, true)
-  assert.deepStrictEqual(r.unnormalized, ['pend'])
-  assert.strictEqual(Buffer.from(decodeSyncMessage(out[0][1]).payload).toString('hex'), Buffer.from(Y.diffUpdate(pending, Uint8Array.from([0]))).toString('hex'))
-  assert.ok(!out[1].unnormalized)
-  const loaded = new Y.Doc(); Y.applyUpdate(loaded, good)
-  assert.strictEqual(Buffer.from(decodeSyncMessage(out[1][1]).payload).toString('hex'), Buffer.from(Y.encodeStateAsUpdate(loaded, Uint8Array.from([0]))).toString('hex'))
+  for (const [k, state] of [[0, pending], [1, good]]) {
+    assert.ok(!out[k].unnormalized)
+    const loaded = new Y.Doc(); Y.applyUpdate(loaded, state)
+    assert.strictEqual(Buffer.from(decodeSyncMessage(out[k][1]).payload).toString('hex'), Buffer.from(Y.encodeStateAsUpdate(loaded, Uint8Array.from([0]))).toString('hex'))
+  }
+  assert.strictEqual(out[2].unnormalized, true)
+  assert.deepStrictEqual(r.unnormalized, ['twice'])
+  assert.strictEqual(Buffer.from(decodeSyncMessage(out[2][1]).payload).toString('hex'), Buffer.from(Y.diffUpdate(twice, Uint8Array.from([0]))).toString('hex'))
 })
 
 test('update V2 batches match yjs mergeUpdatesV2 / diffUpdateV2 / encodeStateVectorFromUpdateV2', async (engine) => {

@@ -565,19 +565,3 @@ def test_gpu_contains_pending_states_vs_yjs():
         with Engine(0, compat135=compat) as e:
             res = e.contains_batch([s for s, _, _ in rows], [u for _, u, _ in rows])
         assert res == [(0, x) for _, _, x in rows]
-
-
-@pytest.mark.gpu
-def test_gpu_step2_refuses_pending_states():
-    """SyncStep2 of a state that leaves pending parts stays EUNSUPPORTED (encodeStateAsUpdate(doc, sv) diffs the
-    pending structs without the parentSub bit the integrated ones keep); complete states beside them are answered."""
-    from hocuspocus_amd import Engine
-    from hocuspocus_amd.engine import EUNSUPPORTED
-    pend = [u for u, _ in pending_fixtures()[:40]]
-    full = [u for u, _ in fixtures()[:20]]
-    with Engine(0, compat135=True) as e:
-        snaps = e.snapshot_batch(pend)
-        res = e.sync_step2_batch(pend + full, [b"\x00"] * 60)
-    assert all(st == 0 for st, _ in snaps)
-    assert any(r[0] == EUNSUPPORTED for r in res[:40]) and all(r[0] in (0, EUNSUPPORTED) for r in res[:40])
-    assert all(r[0] == 0 for r in res[40:])

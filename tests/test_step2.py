@@ -118,3 +118,105 @@ def test_gpu_step2_default_mode_vs_oracle():
         if got != oracle.diff_update(snap, sv, keep_sub=True):
             bad.append(k)
     assert not bad, f"{len(bad)} differ, first {bad[:5]}"
+
+
+# ---------------------------------------------------------------------------------------- states with lost updates
+# tests/golden/step2_pending_v135.json.gz (node tools/step2_corpus.js OUT pending): the states of the pending and
+# sub-document snapshot corpora, pending ones kept, x four state vectors (empty, a cut, the store's own, the state's
+# own -- past the store's, inside the pending structs).  yjs's reply is mergeUpdates([writeStateAsUpdate(doc, sv),
+# pendingDs, diffUpdate(pending structs, sv)]) (Y@23300): the state part keeps each struct's parentSub bit, the
+# pending structs are diffed by the lazy writer's rules.
+PFIX = os.path.join(ROOT, "tests", "golden", "step2_pending_v135.json.gz")
+
+
+def pending_rows():
+    d = json.load(gzip.open(PFIX, "rt"))
+    return [(bytes.fromhex(u), bytes.fromhex(sv), None if e is None else bytes.fromhex(e)) for u, sv, e, _eq in d["rows"]]
+
+
+def test_step2_pending_fixtures_present():
+    r = pending_rows()
+    assert len(r) == 2320 and sum(1 for *_, e in r if e is None) == 22
+
+
+@pytest.mark.skipif(not (NODE and BUNDLE), reason="node + the yjs bundle (image) needed")
+def test_step2_pending_fixtures_regenerate(tmp_path):
+    out = str(tmp_path / "s2p.json.gz")
+    subprocess.run([NODE, os.path.join(ROOT, "tools", "step2_corpus.js"), out, "pending"], check=True, timeout=600, capture_output=True)
+    assert json.load(gzip.open(out, "rt"))["rows"] == json.load(gzip.open(PFIX, "rt"))["rows"]
+
+
+def _parts_reply(body, st, sv, compat135):
+    """The reply from the kernel code's output: a complete state's snapshot diffed keeping the bit; a pending one's
+    three parts (PendHdr) diffed (state: keeping the bit, pending structs: plain) and merged -- the engine's steps."""
+    import struct
+    if st == 0:
+        return oracle.diff_update(body, sv, compat135=compat135, keep_sub=True)
+    assert st == 64
+    ln = struct.unpack_from("<IIII", body, 0)
+    a, b, c = body[16:16 + ln[0]], body[16 + ln[0]:16 + ln[0] + ln[1]], body[16 + ln[0] + ln[1]:16 + ln[0] + ln[1] + ln[2]]
+    sa, da = oracle.diff_update(a, sv, compat135=compat135, keep_sub=True)
+    sc, dc = oracle.diff_update(c, sv, compat135=compat135)
+    if sa or sc:
+        return (sa or sc), None
+    return oracle.merge_updates([da, b, dc], compat135=compat135)
+
+
+def _kernel_outputs(tmp_path, states, mode):
+    from test_snapshot import write_in, read_res
+    exe = str(tmp_path / "snapdev")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-o", exe, os.path.join(ROOT, "tools", "snapdev", "snapdev.cpp")], check=True, timeout=300)
+    a, b = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
+    write_in(a, states)
+    subprocess.run([exe, a, b, str(mode)], check=True, timeout=120)
+    return read_res(b)
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
+def test_step2_pending_decomposition_on_host(tmp_path):
+    """The engine's decomposition, with the snapshot kernel's code host-compiled and the oracle's diff / merge, gives
+    yjs's reply on every row (13.5); where 13.5 throws (a cut surrogate pair) a part's diff refuses."""
+    r = pending_rows()
+    uniq = list(dict.fromkeys(u for u, *_ in r))
+    outs = dict(zip(uniq, _kernel_outputs(tmp_path, uniq, 1)))
+    assert sum(st == 64 for st, _ in outs.values()) >= 200
+    bad = []
+    for k, (u, sv, exp) in enumerate(r):
+        st, body = outs[u]
+        got = _parts_reply(body, st, sv, True)
+        if exp is None:
+            if got[0] != 4:
+                bad.append(k)
+        elif got != (0, exp):
+            bad.append(k)
+    assert not bad, f"{len(bad)} rows differ, first {bad[:5]}"
+
+
+@pytest.mark.gpu
+def test_gpu_step2_pending_vs_yjs(eng135):
+    """ygm_sync_step2_v1 on states with lost updates (the pending parts split off, diffed on child contexts, merged)
+    == yjs encodeStateAsUpdate(doc, sv), mixed with complete states."""
+    r = pending_rows() + [(u, sv, e) for u, sv, e, _ in rows()[:300]]
+    res = eng135.sync_step2_batch([u for u, *_ in r], [sv for _, sv, _ in r])
+    bad = []
+    for k, ((u, sv, exp), got) in enumerate(zip(r, res)):
+        if exp is None:
+            if got[0] != 4:
+                bad.append(k)
+        elif got != (0, exp):
+            bad.append(k)
+    assert not bad, f"{len(bad)} replies differ from yjs, first {bad[:5]}: {res[bad[0]]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
+def test_gpu_step2_pending_default_mode_vs_oracle(tmp_path):
+    """13.6 default mode: GPU replies vs the decomposition over the host-compiled kernel code and the oracle (default)."""
+    from hocuspocus_amd import Engine
+    r = pending_rows()[:1200]
+    uniq = list(dict.fromkeys(u for u, *_ in r))
+    outs = dict(zip(uniq, _kernel_outputs(tmp_path, uniq, 0)))
+    with Engine(0) as e:
+        res = e.sync_step2_batch([u for u, *_ in r], [sv for _, sv, _ in r])
+    bad = [k for k, ((u, sv, _), got) in enumerate(zip(r, res)) if got != _parts_reply(outs[u][1], outs[u][0], sv, False)]
+    assert not bad, f"{len(bad)} differ, first {bad[:5]}"

@@ -1075,6 +1075,14 @@ int ygm_convert_v2_to_v1_device(ygm_ctx* c, const uint8_t* d_arena, uint64_t are
 // only the packed outputs (not the per-document slots).  h2d_ms / d2h_ms are the copies' HIP-event
 // times (summed over chunks); the results live in the parent context's pinned buffers.
 static const uint64_t YGM_CHUNK_BYTES = 64ull << 20;
+// A batch of large [snapshot, ...log] documents runs the large-document tier once per chunk, each run as long as its
+// largest document: a third of the batch per chunk (at least 64 MB) keeps the copies overlapped and the tier's runs
+// few (tools/host_probe.py, profiles/r06_final/host_chunks.jsonl).  YGM_CHUNK_MB overrides (experiments).
+static uint64_t chunk_bytes(uint64_t in_bytes) {
+  const char* e = getenv("YGM_CHUNK_MB");
+  if (e && atoi(e) > 0) return (uint64_t)atoi(e) << 20;
+  return in_bytes / 3 > YGM_CHUNK_BYTES ? in_bytes / 3 : YGM_CHUNK_BYTES;
+}
 
 namespace {
 struct Chunk {   // documents [d0, d1): merge updates [u0, u1) / SV-diff documents
@@ -1156,7 +1164,8 @@ static int chunk_stage(ygm_ctx* k, const HostCall& H, Chunk& C) {
     for (uint64_t j = 0; j < n_sv; j++) rs[j] = H.sv_off[C.d0 + j] - s0;
     q += sb + 8 * n_sv;
   }
-  if (is_merge(H.mode)) {   // per-document update ranges, relative to the chunk
+  if (is_merge(H.mode)) {   // per-document update ranges, relative to the chunk (one walk over its updates: a binary
+                            // search per document measured 2-3x slower end to end, tools/host_probe.py)
     uint32_t* du = (uint32_t*)q;
     du[0] = 0;
     uint32_t u = C.u0;
@@ -1230,18 +1239,22 @@ static int host_call(ygm_ctx* c, const HostCall& H, ygm_result* out) {
   // chunks of whole documents
   std::vector<Chunk> ch;
   {
+    const uint64_t CB = chunk_bytes(n ? (is_merge(H.mode) ? H.off[H.n_upd] - H.off[0] : H.off[n] - H.off[0]) : 0);
     uint32_t d = 0, u = 0;
     while (d < n || ch.empty()) {
       Chunk C{};
       C.d0 = d; C.u0 = u;
       const uint64_t base = is_merge(H.mode) ? H.off[u] : H.off[d];
-      while (d < n) {
-        uint32_t ue = u;
-        if (is_merge(H.mode)) while (ue < H.n_upd && H.upd_doc[ue] == d) ue++;
-        const uint64_t end = is_merge(H.mode) ? H.off[ue] : H.off[d + 1];
-        if (d > C.d0 && end - base > YGM_CHUNK_BYTES) break;
-        d++; u = ue;
+      // the input end of documents [C.d0, x): binary searches over the ascending upd_doc / offsets (a walk over every
+      // update took milliseconds per call on batches of millions of updates)
+      auto first_upd = [&](uint32_t x) { return (uint32_t)(std::lower_bound(H.upd_doc, H.upd_doc + H.n_upd, x) - H.upd_doc); };
+      auto end_of = [&](uint32_t x) { return is_merge(H.mode) ? H.off[first_upd(x)] : H.off[x]; };
+      uint32_t lo = d + 1, hi = n;   // the last x in [d + 1, n] whose documents fit in CB (at least one document)
+      if (n > d && end_of(n) - base <= CB) lo = n;
+      else if (n > d) {
+        while (lo < hi) { const uint32_t mid = lo + (hi - lo + 1) / 2; if (end_of(mid) - base <= CB) lo = mid; else hi = mid - 1; }
       }
+      if (n > d) { d = lo; u = is_merge(H.mode) ? first_upd(d) : d; }
       C.d1 = d; C.u1 = u;
       ch.push_back(C);
       if (n == 0) break;

@@ -169,9 +169,25 @@ __global__ __launch_bounds__(V2_NT) void k_v12_write(const uint8_t* __restrict__
 // masks; the nine lanes of a document walk the same bytes (one decode stream, LDS reads broadcast) and each encodes
 // its own column -- a count pass, the layout from the nine lengths, a write pass that stores the column straight
 // into the document's slot (merge_slot of its V2 input bytes, as the V1 kernels place outputs: no scan, no
-// cross-document dependency).  The small tier stages documents of <= 3.5 KB (seven per wave, 63 lanes busy), a
+// cross-document dependency).  The small tier stages documents of <= 3.5 KB (four per wave, 36 lanes busy: seven
+// per wave, 63 lanes, needed 29 KB of LDS per wave and ran 5 % slower), a
 // second launch (D = 2, 7 KB) the larger ones.  claim[d] = 1 for a document done here; the general kernels take
 // the rest (their outputs after the slot region).
+// a lane's column from its scratch (16-byte aligned, CAP a multiple of 16) to its place in the slot: 16-byte loads,
+// each a whole piece of the column before its stores (a byte loop reloading the scratch after every store to the
+// slot -- which may alias it for the compiler -- waited on each load: ~1.5 ms per 10 000 documents)
+YDEV void v12f_copy_col(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, uint32_t n) {
+  typedef unsigned int cu32x4 __attribute__((ext_vector_type(4)));
+  uint32_t i = 0;
+  for (; i + 16u <= n; i += 16u) { const cu32x4 v = *(const cu32x4*)(s + i); __builtin_memcpy(d + i, &v, 16); }
+  if (i < n) {   // (i is a multiple of 16 below n <= CAP: the piece stays inside the lane's region)
+    const cu32x4 v = *(const cu32x4*)(s + i);
+    for (uint32_t k = 0; k < n - i; k++) {
+      const uint32_t w = k < 4u ? v.x : k < 8u ? v.y : k < 12u ? v.z : v.w;
+      d[i + k] = (uint8_t)(w >> (8u * (k & 3u)));
+    }
+  }
+}
 typedef __attribute__((address_space(3))) uint8_t FL8;
 typedef __attribute__((address_space(3))) uint64_t FL64;
 typedef unsigned int fu32x4 __attribute__((ext_vector_type(4)));
@@ -263,7 +279,7 @@ __global__ __launch_bounds__(64) void k_v12_fast(const uint8_t* __restrict__ v1,
         uint32_t mb = base[0];
 #pragma unroll
         for (int q = 1; q < (int)v2f::FC_N; q++) mb = col == (uint32_t)q ? base[q] : mb;
-        for (uint32_t i = 0; i < c.n; i++) o[mb + i] = cs[i];   // (the lane's own stores: program order)
+        v12f_copy_col(o + mb, cs, c.n);
       }
       if (col == 0u) {
         if (ok) {
@@ -287,7 +303,7 @@ static uint32_t v12f_grid() {
 }
 template <int D, int FIN>
 static size_t v12f_scratch() { return (size_t)v12f_grid<D, FIN>() * D * v2f::FC_N * (FIN + 64); }
-constexpr int V12F_D = 7, V12F_FS = 3584;   // small tier: seven documents of <= 3.5 KB per wave (29 KB of LDS)
+constexpr int V12F_D = 4, V12F_FS = 3584;   // small tier: four documents of <= 3.5 KB per wave (16 KB of LDS; one per wave: 30 % slower)
 
 __global__ __launch_bounds__(256) void k_v2_status(const int32_t* __restrict__ ust, uint32_t n, int32_t* __restrict__ status,
                                                   uint64_t* __restrict__ len) {

@@ -1687,6 +1687,12 @@ __global__ __launch_bounds__(1024) void k_big_pick(const uint8_t* __restrict__ a
 #ifndef YGM_SCAN_LDS
 #define YGM_SCAN_LDS 1
 #endif
+#ifndef YGM_SCAN_UTF
+#define YGM_SCAN_UTF 1   // a candidate string's verdict: 0 the UTF-8 decoder over the stage; 1 ASCII views first (see the scan)
+#endif
+#ifndef YGM_SCAN_PF
+#define YGM_SCAN_PF 1    // parent-form candidates whose parentInfo byte is past 1 are not parsed (see the scan's queue)
+#endif
 #ifndef YGM_SCAN_CLS
 #define YGM_SCAN_CLS 2   // candidate classes queued one after the other (1: position order)
 #endif
@@ -1729,7 +1735,13 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
         const uint32_t ib = i < w1 - w0 ? lb[i] : 1u;
         const bool txt = ib == 0u || ((ib & 0xC0u) && ((ib & 31u) == 1u || (ib & 31u) == 4u));
         const uint32_t k = NCLS == 1u ? 0u : txt ? 0u : (NCLS < 3u || (ib & 0xC0u)) ? 1u : 2u;   // (3: the rest split by origin)
-        const bool cand = i < w1 - w0 && big_cand(ib) && k == cls;   // (other positions are never read: nothing written)
+        bool cand = i < w1 - w0 && big_cand(ib) && k == cls;   // (other positions are never read: nothing written)
+#if YGM_SCAN_PF
+        // a parent-form Item (no origins) whose parentInfo byte is not 0 / 1 is refused by the validation wherever it
+        // stands, so it needs no end: its word is 0 (no parse -- the follow parses such a position from global memory
+        // should the chain meet it) and the queue keeps the candidates that can be structs write_struct emits
+        if (cand && ib != 0u && (ib & 0xC0u) == 0u && i + 1u < se - w0 && lb[i + 1u] > 1u) { cand = false; S.nv[P.pb + w0 + i] = 0u; }
+#endif
         const uint64_t m = __ballot(cand);
         if (cand) q[qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint16_t)i;
         qn += (uint32_t)__builtin_popcountll(m);
@@ -1748,7 +1760,14 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
 #endif
         uint32_t kind;
         uint64_t cv = 0;
+#if YGM_SCAN_SKIP1   // experiment: candidates of the other kinds not parsed (no end: the follow parses them from global memory)
+        const uint32_t ib0 = lb[i];
+        const bool txt0 = ib0 == 0u || ((ib0 & 0xC0u) && ((ib0 & 31u) == 1u || (ib0 & 31u) == 4u));
+        bool ok = txt0 && big_skip(c, kind, 8, &cv) && !c.err;
+        if (!txt0) c.err = ST_FALLBACK;
+#else
         bool ok = big_skip(c, kind, 8, &cv) && !c.err;
+#endif
         const uint8_t* vb = lb;   // (the string's bytes: the stage, or U0 after a redo)
         uint32_t cp = c.pos + w0;
         if (!ok && c.err == ST_MALFORMED && se < n0) {   // ran into the stage's end: the parse again from global memory
@@ -1763,8 +1782,24 @@ __global__ __launch_bounds__(256) void k_big_scan(const uint8_t* __restrict__ ar
             if (info == 0u || ((info & 0xC0u) && (ref == 1u || ref == 4u))) {
               // GC, or an Item with an origin and deleted / string content (text's structs): big_struct's verdict
               // from the skip parse itself (its varuints minimal, the string strict UTF-8, a non-zero length)
-              const int64_t len = c.nm ? -1 : ref == 4u ? gutf8_u16(vb + (cv >> 32), (uint32_t)cv) : (int64_t)cv;
-              v = big_v16((uint64_t)len, len > 0 && len < 0xFFFFFFFFll);
+              int64_t len = c.nm ? -1 : (int64_t)cv;
+              if (!c.nm && ref == 4u) {
+#if YGM_SCAN_UTF == 0 || !YGM_SCAN_LDS
+                len = gutf8_u16(vb + (cv >> 32), (uint32_t)cv);
+#else
+                // the string's bytes from the stage by 8-byte views: all ASCII (the common case, and a cheap no for most
+                // of the speculative parses) counts its bytes; otherwise the UTF-8 decoder (1) or no verdict (2: the
+                // merge kernel validates it if the chain meets it; 3: experiment, no verdict for any string)
+                const uint32_t s0 = (uint32_t)(cv >> 32), sl = (uint32_t)cv;
+                bool asc = vb == lb && YGM_SCAN_UTF != 3;
+                for (uint32_t k = 0; asc && k < sl; k += 8u) {
+                  const uint64_t w = c.w8(s0 + k), m = sl - k >= 8u ? ~0ull : (1ull << (8u * (sl - k))) - 1ull;
+                  asc = (w & m & 0x8080808080808080ull) == 0ull;
+                }
+                len = asc ? (int64_t)sl : YGM_SCAN_UTF == 1 ? gutf8_u16(vb + s0, sl) : -2;
+#endif
+              }
+              v = len == -2 ? 0u : big_v16((uint64_t)len, len > 0 && len < 0xFFFFFFFFll);
             } else {
               // the other kinds: big_struct in k_big_val (its registers would halve this kernel's waves), for a parse
               // whose end could start the next struct (most candidates are bytes inside other structs: their ends

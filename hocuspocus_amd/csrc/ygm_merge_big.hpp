@@ -21,6 +21,7 @@
 //   emit   lane 0 merges the block table with the sorted log pieces twice (sizes, then bytes);
 //          the wave copies each U0 block range with 16-byte loads / stores
 #pragma once
+#include <type_traits>
 #include "ygm_seqdoc.hpp"
 #include "ygm_merge_lean.hpp"
 
@@ -110,6 +111,13 @@ struct LCur {
     const __attribute__((address_space(3))) uint32_t* d = (const __attribute__((address_space(3))) uint32_t*)(p + q - sh);
     const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
     return ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32) | __builtin_amdgcn_alignbyte(d1, d0, sh);
+  }
+  YDEV void w16(uint32_t q, uint64_t& lo, uint64_t& hi) const {   // the 16 bytes at p + q
+    const uint32_t a = (uint32_t)(uintptr_t)(p + q), sh = a & 3u;
+    const __attribute__((address_space(3))) uint32_t* d = (const __attribute__((address_space(3))) uint32_t*)(p + q - sh);
+    const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
+    lo = ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32) | __builtin_amdgcn_alignbyte(d1, d0, sh);
+    hi = ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, sh) << 32) | __builtin_amdgcn_alignbyte(d3, d2, sh);
   }
   YDEV uint32_t u8() { if (pos >= end) { fail(ST_MALFORMED); return 0; } return raw(pos++); }
   YDEV uint64_t vu() {   // lib0 readVarUint (Cur::vu semantics)
@@ -295,6 +303,37 @@ YDEV_NI bool gany_skip(GCur& c, uint64_t n) {
   return false;
 }
 
+// The origin / right-origin ids after an info byte (npair id pairs: 2 or 4 varuints) skipped from one 16-byte view of
+// the stage and its terminator mask, instead of a dependent read per varuint: the cursor ends where the vu() calls
+// would leave it, with nm set the same way (a varuint's last byte zero past its first).  Returns false (cursor
+// untouched) when the ids do not end inside the view and the update or a varuint runs past 7 bytes: the vu() path.
+#ifndef YGM_SKIP_MASK
+#define YGM_SKIP_MASK 1
+#endif
+YDEV uint32_t top_bits8(uint64_t h) { return (uint32_t)((((h >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56); }
+YDEV uint64_t zero_bytes8(uint64_t x) {   // 0x80 in each zero byte of x, exactly (no borrow between bytes)
+  const uint64_t t = (x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full;
+  return ~(t | x | 0x7F7F7F7F7F7F7F7Full);
+}
+YDEV bool lcur_skip_ids(LCur& c, uint32_t npair) {
+  if (c.pos >= c.end) return false;
+  uint64_t lo, hi;
+  c.w16(c.pos, lo, hi);
+  const uint32_t T = top_bits8(~lo & 0x8080808080808080ull) | (top_bits8(~hi & 0x8080808080808080ull) << 8);
+  const uint32_t Z = top_bits8(zero_bytes8(lo)) | (top_bits8(zero_bytes8(hi)) << 8);
+  uint32_t t = T;
+  const uint32_t e1 = (uint32_t)__builtin_ctz(t | 0x80000000u); t &= t - 1u;
+  const uint32_t e2 = (uint32_t)__builtin_ctz(t | 0x80000000u); t &= t - 1u;
+  const uint32_t e3 = (uint32_t)__builtin_ctz(t | 0x80000000u); t &= t - 1u;
+  const uint32_t e4 = (uint32_t)__builtin_ctz(t | 0x80000000u);
+  const uint32_t e = npair == 2u ? e4 : e2;
+  const bool lens = e1 < 7u && e2 - e1 <= 7u && (npair != 2u || (e3 - e2 <= 7u && e4 - e3 <= 7u));
+  if (!(e < 16u && lens && c.pos + e < c.end)) return false;
+  if (Z & ~(T << 1) & ~1u & ((2u << e) - 1u)) c.nm = 1;
+  c.pos += e + 1u;
+  return true;
+}
+
 // Skip-only parse of one U0 struct (the sequential part of the walk): the bytes it spans and its
 // kind (0 GC, 1 Item); validation and lengths come later, in parallel (big_struct).  false: a
 // Skip, Any / Doc content or an unknown ref -- the document goes on to the general path.
@@ -306,8 +345,14 @@ YDEV bool big_skip(CUR& c, uint32_t& kind, uint64_t jcap = ~0ull, uint64_t* cv =
   if (c.err || info == 10u) return false;
   if ((info & 31u) == 0u) { kind = 0; const uint64_t n = c.vu(); if (cv) *cv = n; return !c.err; }
   uint32_t l;
-  if (info & 0x80u) { c.vu(); c.vu(); }
-  if (info & 0x40u) { c.vu(); c.vu(); }
+  bool skipped = false;
+#if YGM_SKIP_MASK
+  if constexpr (std::is_same<CUR, LCur>::value) skipped = (info & 0xC0u) == 0u || lcur_skip_ids(c, ((info >> 7) & 1u) + ((info >> 6) & 1u));
+#endif
+  if (!skipped) {
+    if (info & 0x80u) { c.vu(); c.vu(); }
+    if (info & 0x40u) { c.vu(); c.vu(); }
+  }
   if ((info & 0xC0u) == 0u) {
     const uint64_t pi = c.vu();
     if (pi == 1) c.buf(l); else { c.vu(); c.vu(); }

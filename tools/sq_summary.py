@@ -1,28 +1,17 @@
-"""Per-kernel SQ counter summary of a rocprofv3 --pmc run (measurement tooling): per-dispatch averages
-and derived ratios.  python tools/sq_summary.py <rocprof out dir>"""
-import collections
-import csv
-import glob
-import sys
+"""Per-kernel sums of a rocprofv3 --pmc counter_collection.csv, divided by SQ_WAVES (tooling).
 
-acc = collections.defaultdict(lambda: collections.defaultdict(float))
-disp = collections.defaultdict(set)
-for p in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(p)):
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        if k.startswith("__amd"):
-            continue
-        acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        disp[k].add(r["Dispatch_Id"])
-for k, d in acc.items():
-    n = len(disp[k])
-    a = {c: v / n for c, v in d.items()}
-    w = a.get("SQ_WAVES", 0) or 1
-    print(f"{k}: {n} dispatches")
-    for c in sorted(a):
-        print(f"  {c:24s} {a[c]:14.4g}   per wave {a[c] / w:12.4g}")
-    if "SQ_WAVE_CYCLES" in a:
-        wc = a["SQ_WAVE_CYCLES"]
-        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
-            if c in a:
-                print(f"  {c} / WAVE_CYCLES = {a[c] / wc:.3f}")
+    python tools/sq_summary.py <counter_collection.csv>"""
+import csv, sys, collections
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+cnt = collections.defaultdict(set); dur = collections.defaultdict(dict)
+for r in csv.DictReader(open(sys.argv[1])):
+    k = r["Kernel_Name"].split("(")[0].replace("ygm::", "")[:60]
+    agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+    cnt[k].add(r["Dispatch_Id"])
+    dur[k][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+for k, v in sorted(agg.items(), key=lambda x: -sum(dur[x[0]].values())):
+    t = sum(dur[k].values())
+    if t < 500: continue
+    w = v.get("SQ_WAVES", 0) or 1
+    s = " ".join(f"{c.replace('SQ_','')}={v[c]/w:.0f}" for c in sorted(v) if c != "SQ_WAVES")
+    print(f"{k:60s} n={len(cnt[k])} ms={t/1e3:.2f} waves={w:.0f} per-wave: {s}")

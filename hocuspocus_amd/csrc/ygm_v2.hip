@@ -169,8 +169,8 @@ __global__ __launch_bounds__(V2_NT) void k_v12_write(const uint8_t* __restrict__
 // masks; the nine lanes of a document walk the same bytes (one decode stream, LDS reads broadcast) and each encodes
 // its own column -- a count pass, the layout from the nine lengths, a write pass that stores the column straight
 // into the document's slot (merge_slot of its V2 input bytes, as the V1 kernels place outputs: no scan, no
-// cross-document dependency).  The small tier stages documents of <= 3.5 KB (four per wave, 36 lanes busy: seven
-// per wave, 63 lanes, needed 29 KB of LDS per wave and ran 5 % slower), a
+// cross-document dependency).  The small tier stages documents of <= 3.25 KB (five per wave, 45 lanes busy: the sizing
+// below), a
 // second launch (D = 2, 7 KB) the larger ones.  claim[d] = 1 for a document done here; the general kernels take
 // the rest (their outputs after the slot region).
 // a lane's column from its scratch (16-byte aligned, CAP a multiple of 16) to its place in the slot: 16-byte loads,
@@ -303,7 +303,10 @@ static uint32_t v12f_grid() {
 }
 template <int D, int FIN>
 static size_t v12f_scratch() { return (size_t)v12f_grid<D, FIN>() * D * v2f::FC_N * (FIN + 64); }
-constexpr int V12F_D = 4, V12F_FS = 3584;   // small tier: four documents of <= 3.5 KB per wave (16 KB of LDS; one per wave: 30 % slower)
+// small tier: five documents of <= 3.25 KB per wave (19.5 KB of LDS: eight waves per CU, 10 240 documents resident --
+// a batch of 10 000 merged C2 logs, <= 3 023 bytes each, in one round; four of <= 3.5 KB: 9 216 resident, two rounds,
+// 1.83 against 1.22 ms for the v2 block; one per wave: 30 % slower)
+constexpr int V12F_D = 5, V12F_FS = 3328;
 
 __global__ __launch_bounds__(256) void k_v2_status(const int32_t* __restrict__ ust, uint32_t n, int32_t* __restrict__ status,
                                                   uint64_t* __restrict__ len) {

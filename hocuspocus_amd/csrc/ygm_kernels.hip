@@ -3439,9 +3439,9 @@ int ygm_k_launch_doc(int mode, const uint8_t* arena, const uint64_t* doc_off, co
 
 // ======================================================================= host API: packed results
 // The device results leave each document's bytes in its own slot; the host API copies back only the
-// outputs, packed in document order: per-256-document sums, one scan of those sums, then each
-// workgroup places and copies its documents (a wave per document, 16-byte pieces, byte stores for the
-// last partial piece -- the neighbouring document's bytes are written by another wave).
+// outputs, packed in document order: per-256-document sums, one scan of those sums, each document's packed offset,
+// then the copy by 16 KB chunks of the packed output (16-byte pieces, byte stores for a segment's last partial piece:
+// the chunks' byte ranges are disjoint).
 __global__ __launch_bounds__(DOC_NT) void k_pack_sum(const uint64_t* __restrict__ len, const int32_t* __restrict__ status, uint32_t n,
                                                    uint64_t* __restrict__ bsum) {
   __shared__ uint64_t tmp[DOC_NT / WAVE + 1];
@@ -3468,27 +3468,50 @@ __global__ __launch_bounds__(1024) void k_pack_scan(uint64_t* __restrict__ bsum,
   }
   if (threadIdx.x == 0) bsum[nb] = carry;
 }
-__global__ __launch_bounds__(DOC_NT) void k_pack_copy(const uint8_t* __restrict__ src, const uint64_t* __restrict__ off,
-                                                    const uint64_t* __restrict__ len, const int32_t* __restrict__ status, uint32_t n,
-                                                    const uint64_t* __restrict__ bsum, uint8_t* __restrict__ dst,
-                                                    uint64_t* __restrict__ poff) {
+__global__ __launch_bounds__(DOC_NT) void k_pack_off(const uint64_t* __restrict__ len, const int32_t* __restrict__ status, uint32_t n,
+                                                   const uint64_t* __restrict__ bsum, uint64_t* __restrict__ poff) {
   __shared__ uint64_t tmp[DOC_NT / WAVE + 1];
-  __shared__ uint64_t s_at[DOC_NT], s_src[DOC_NT], s_len[DOC_NT];
-  const uint32_t t = threadIdx.x, d = blockIdx.x * DOC_NT + t;
+  const uint32_t d = blockIdx.x * DOC_NT + threadIdx.x;
   const uint64_t v = d < n && status[d] == ST_OK ? len[d] : 0ull;
   uint64_t tot;
   const uint64_t at = bsum[blockIdx.x] + block_exscan<DOC_NT>(v, tmp, tot);
   if (d < n) poff[d] = at;
-  s_at[t] = at; s_src[t] = d < n ? off[d] : 0ull; s_len[t] = v;
-  __syncthreads();
-  const uint32_t w = t / WAVE, l = t % WAVE;
-  for (uint32_t j = w; j < DOC_NT; j += DOC_NT / WAVE) {
-    const uint64_t L = s_len[j];
-    const uint8_t* a = src + s_src[j];
-    uint8_t* b = dst + s_at[j];
-    for (uint64_t c = 16ull * l; c < L; c += 16ull * WAVE) {
-      if (c + 16 <= L) { u32x4 x; __builtin_memcpy(&x, a + c, 16); __builtin_memcpy(b + c, &x, 16); }
-      else for (uint64_t k = c; k < L; k++) b[k] = a[k];
+}
+// the copy: a wave per 16 KB chunk of the packed output (persistent grid; the total from the scan), so that a document
+// of megabytes is copied by as many waves as it has chunks (a wave per document left one wave copying C3's 10 MB
+// document, and C5's 380 KB documents 64 to a wave: 10-20 ms).  The chunk's first document by a 64-way search of the
+// offsets (one load per lane and step), then the documents it spans, 16-byte pieces per lane.
+constexpr uint64_t PK_CH = 16384;
+__global__ __launch_bounds__(256) void k_pack_chunks(const uint8_t* __restrict__ src, const uint64_t* __restrict__ off, uint32_t n,
+                                                     const uint64_t* __restrict__ poff, const uint64_t* __restrict__ total_p,
+                                                     uint8_t* __restrict__ dst) {
+  const uint32_t l = threadIdx.x % WAVE;
+  const uint64_t total = *total_p, nch = (total + PK_CH - 1) / PK_CH;
+  const uint64_t W = (uint64_t)gridDim.x * (256 / WAVE);
+  for (uint64_t c = (uint64_t)blockIdx.x * (256 / WAVE) + threadIdx.x / WAVE; c < nch; c += W) {
+    const uint64_t s = c * PK_CH, e = s + PK_CH < total ? s + PK_CH : total;
+    // the last document d with poff[d] <= s (poff nondecreasing, poff[0] = 0)
+    uint32_t lo = 0, hi = n;
+    while (hi - lo > 1u) {
+      const uint32_t step = (hi - lo + WAVE - 1u) / WAVE, i = lo + l * step;
+      const bool le = i < hi && poff[i] <= s;
+      const uint64_t m = __ballot(le);   // (a prefix of the lanes; lane 0 holds: poff[lo] <= s)
+      const uint32_t k = 63u - (uint32_t)__builtin_clzll(m);
+      lo += k * step;
+      hi = lo + step < hi ? lo + step : hi;
+    }
+    for (uint32_t d = lo; d < n; d++) {
+      const uint64_t a = poff[d];
+      if (a >= e) break;
+      const uint64_t b = d + 1u < n ? poff[d + 1u] : total;
+      const uint64_t x0 = a > s ? a : s, x1 = b < e ? b : e;
+      const uint8_t* sp = src + off[d] + (x0 - a);
+      uint8_t* dp = dst + x0;
+      const uint64_t L = x1 > x0 ? x1 - x0 : 0ull;
+      for (uint64_t q = 16ull * l; q < L; q += 16ull * WAVE) {
+        if (q + 16 <= L) { u32x4 x; __builtin_memcpy(&x, sp + q, 16); __builtin_memcpy(dp + q, &x, 16); }
+        else for (uint64_t k = q; k < L; k++) dp[k] = sp[k];
+      }
     }
   }
 }
@@ -3498,7 +3521,9 @@ int ygm_k_launch_pack(const uint8_t* src, const uint64_t* off, const uint64_t* l
   const uint32_t nb = (n + DOC_NT - 1) / DOC_NT;
   hipLaunchKernelGGL(k_pack_sum, dim3(nb), dim3(DOC_NT), 0, s, len, status, n, bsum);
   hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(1024), 0, s, bsum, nb);
-  hipLaunchKernelGGL(k_pack_copy, dim3(nb), dim3(DOC_NT), 0, s, src, off, len, status, n, (const uint64_t*)bsum, dst, poff);
+  hipLaunchKernelGGL(k_pack_off, dim3(nb), dim3(DOC_NT), 0, s, len, status, n, (const uint64_t*)bsum, poff);
+  hipLaunchKernelGGL(k_pack_chunks, dim3(8u * device_cus()), dim3(256), 0, s, src, off, n, (const uint64_t*)poff,
+                     (const uint64_t*)(bsum + nb), dst);
   return launch_rc(__func__);
 }
 

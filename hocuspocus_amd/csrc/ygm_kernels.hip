@@ -857,11 +857,23 @@ __global__ __launch_bounds__(256) void k_route_big(const uint64_t* __restrict__ 
     const uint32_t u0 = in ? doc_upd[d] : 0u, u1 = in ? doc_upd[d + 1] : 0u, k = u1 - u0;
     // as merge_wave_doc: empty and one-update documents and the forced sequential mode stay with the wave kernel
     const bool cand = in && k >= 2u && !(flags & 2u);
+    // the largest update: a lane walks its document's offsets, or -- a document of more than 64 updates -- the wave
+    // does, 64 offsets at a time (a lane walking 100 000 updates held its wave for milliseconds)
+    const bool coop = cand && k > 64u;
     uint64_t mx = 0, prev = cand ? upd_off[u0] : 0ull;
-    for (uint32_t j = 1; j <= (cand ? k : 0u); j++) {
+    for (uint32_t j = 1; j <= (cand && !coop ? k : 0u); j++) {
       const uint64_t x = upd_off[u0 + j];
       mx = x - prev > mx ? x - prev : mx;
       prev = x;
+    }
+    for (uint64_t cm = __ballot(coop); cm; cm &= cm - 1ull) {   // (wave-uniform)
+      const int src = __builtin_ctzll(cm);
+      const uint32_t ua = (uint32_t)__shfl((int)u0, src), kk = (uint32_t)__shfl((int)k, src);
+      uint64_t m2 = 0;
+      for (uint32_t j = l; j < kk; j += WAVE) { const uint64_t n2 = upd_off[ua + j + 1] - upd_off[ua + j]; m2 = n2 > m2 ? n2 : m2; }
+#pragma unroll
+      for (int o = WAVE / 2; o > 0; o >>= 1) { const uint64_t t2 = __shfl_xor(m2, o, WAVE); m2 = t2 > m2 ? t2 : m2; }
+      if (l == (uint32_t)src) mx = m2;
     }
     const bool big = cand && mx >= (uint64_t)BIG_ROUTE_MIN;
     const uint64_t bm = __ballot(big), rm = __ballot(in && !big);

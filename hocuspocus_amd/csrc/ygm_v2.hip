@@ -305,7 +305,8 @@ template <int D, int FIN>
 static size_t v12f_scratch() { return (size_t)v12f_grid<D, FIN>() * D * v2f::FC_N * (FIN + 64); }
 // small tier: five documents of <= 3.25 KB per wave (19.5 KB of LDS: eight waves per CU, 10 240 documents resident --
 // a batch of 10 000 merged C2 logs, <= 3 023 bytes each, in one round; four of <= 3.5 KB: 9 216 resident, two rounds,
-// 1.83 against 1.22 ms for the v2 block; one per wave: 30 % slower)
+// 1.83 against 1.22 ms for the v2 block; six / seven of <= 3 KB per wave, also one round: 1.27 / 1.28 ms; one per
+// wave: 30 % slower)
 constexpr int V12F_D = 5, V12F_FS = 3328;
 
 __global__ __launch_bounds__(256) void k_v2_status(const int32_t* __restrict__ ust, uint32_t n, int32_t* __restrict__ status,
